@@ -1,0 +1,86 @@
+"""Shared test harness: drives any library exporting include/nakama_mm.h.
+
+Scenario runner for the known-answer fixtures (tests/golden/known_answer.json)
+and the seeded synthetic workloads of SURVEY.md 8(d) (tools/workloads.py).
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from nakama_amd import capi  # noqa: E402
+
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle_mm.so")
+PRODUCT_SO = os.path.join(ROOT, "nakama_amd", "libnakama_mm.so")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def build_oracle():
+    if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < max(
+            os.path.getmtime(os.path.join(ROOT, "oracle", f)) for f in ("mm_oracle.cpp", "go_compat.h")):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+
+
+_oracle_lib = None
+
+
+def oracle_lib():
+    global _oracle_lib
+    if _oracle_lib is None:
+        build_oracle()
+        _oracle_lib = capi.load_library(ORACLE_SO)
+    return _oracle_lib
+
+
+def load_known_answer():
+    with open(os.path.join(GOLDEN, "known_answer.json")) as f:
+        return json.load(f)
+
+
+def run_scenario(lib, sc, T0, step):
+    """Runs one fixture scenario; returns (process_results, errors_seen)."""
+    cfg = sc["config"]
+    mm = capi.Matchmaker(lib, max_tickets=cfg.get("max_tickets", 3), max_intervals=cfg.get("max_intervals", 2),
+                         rev_precision=cfg.get("rev_precision", False))
+    results = []
+    errors = []
+    i = 0
+    try:
+        for op in sc["ops"]:
+            if op["op"] == "add":
+                pres = [capi.Presence(p["user_id"], p["session_id"], p["username"], p["node"]) for p in op["presences"]]
+                err = None
+                try:
+                    mm.Add(pres, op["session_id"], op["party_id"], op["query"], op["min_count"], op["max_count"],
+                           op["count_multiple"], op["string_properties"], op["numeric_properties"],
+                           ticket=op["ticket"], created_at=T0 + step * i)
+                except capi.MatchmakerError as e:
+                    err = type(e).__name__
+                errors.append((op["ticket"], err, op.get("expect_error")))
+                i += 1
+            elif op["op"] == "remove_session":
+                mm.RemoveSession(op["session_id"], op["ticket"])
+            elif op["op"] == "process":
+                results.append(mm.Process())
+        extract = mm.Extract()
+    finally:
+        mm.close()
+    return results, errors, extract
+
+
+def matched_sessions(groups, sc):
+    """Session ids of matched entries (the test's matchesSeen keys)."""
+    sess = {}
+    for op in sc["ops"]:
+        if op["op"] == "add":
+            sess[op["ticket"]] = [p["session_id"] for p in op["presences"]]
+    out = set()
+    for g in groups:
+        for t, pi in g:
+            out.add(sess[t][pi])
+    return out

@@ -1,0 +1,79 @@
+"""Pins the CPU oracle against the reference's own known-answer tests.
+
+Every scenario in tests/golden/known_answer.json restates one test of
+server/matchmaker_test.go (cited in the fixture); the oracle must reproduce
+the test's assertions and the hand-derived pinned groups.  This is what makes
+the oracle trustworthy as the parity checker of the HIP path.
+"""
+import pytest
+
+import harness
+from nakama_amd import capi
+
+KA = harness.load_known_answer()
+
+
+@pytest.mark.parametrize("sc", KA["scenarios"], ids=[s["name"] for s in KA["scenarios"]])
+def test_known_answer(sc):
+    lib = harness.oracle_lib()
+    results, errors, _ = harness.run_scenario(lib, sc, KA["T0"], KA["created_step"])
+    for ticket, got, want in errors:
+        assert got == want, f"{sc['name']}: add {ticket} -> {got}, reference test expects {want}"
+    groups = [g for r in results for g in r]
+    a = sc["assert"]
+    sess = harness.matched_sessions(groups, sc)
+    if "matched_sessions_count" in a:
+        assert len(sess) == a["matched_sessions_count"], (sc["name"], groups)
+    for s in a.get("matched_sessions_include", []):
+        assert s in sess
+    if sc["pinned_groups"] is not None:
+        assert [[list(e) for e in g] for g in groups] == sc["pinned_groups"]
+
+
+@pytest.mark.parametrize("sc", [s for s in KA["scenarios"] if "expected_scores" in s],
+                         ids=[s["name"] for s in KA["scenarios"] if "expected_scores" in s])
+def test_hand_derived_scores(sc):
+    """scores derived from the vendored bluge source."""
+    lib = harness.oracle_lib()
+    mm = capi.Matchmaker(lib, max_intervals=5, rev_precision=True)
+    try:
+        i = 0
+        for op in sc["ops"]:
+            if op["op"] != "add":
+                continue
+            pres = [capi.Presence(p["user_id"], p["session_id"], p["username"], p["node"]) for p in op["presences"]]
+            mm.Add(pres, op["session_id"], op["party_id"], op["query"], op["min_count"], op["max_count"],
+                   op["count_multiple"], op["string_properties"], op["numeric_properties"], ticket=op["ticket"],
+                   created_at=KA["T0"] + KA["created_step"] * i)
+            i += 1
+        for t, want in sc["expected_scores"].items():
+            got = mm.debug_hits(t)
+            assert [[h, s] for h, s in got] == want
+    finally:
+        mm.close()
+
+
+def test_group_indexes_exact():
+    """TestGroupIndexes (server/matchmaker_test.go:1594-1621), exact."""
+    gi = KA["group_indexes"]
+    names = [x[0] for x in gi["indexes"]]
+    got = capi.group_indexes(harness.oracle_lib(), [x[1] for x in gi["indexes"]], [x[2] for x in gi["indexes"]],
+                             gi["required"])
+    got_named = [[[names[i] for i in idx], avg] for idx, avg in got]
+    assert got_named == [[list(g), avg] for g, avg in gi["expected"]]
+
+
+@pytest.mark.parametrize("q,status", KA["query_cases"], ids=[repr(q) for q, _ in KA["query_cases"]])
+def test_query_language(q, status):
+    lib = harness.oracle_lib()
+    mm = capi.Matchmaker(lib)
+    try:
+        pres = [capi.Presence("u", "s", "u", "n")]
+        try:
+            mm.Add(pres, "s", "", q, 2, 2, 1, {}, {}, ticket="t", created_at=1)
+            got = "ok"
+        except capi.ErrMatchmakerQueryInvalid:
+            got = "invalid"
+        assert got == status
+    finally:
+        mm.close()
