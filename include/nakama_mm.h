@@ -164,6 +164,9 @@ int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, dou
  * created_at); writes up to cap groups as member positions (into the input
  * arrays, in the reference's append order) and avgCreatedAt; returns the
  * number of groups.  group_members must hold 8*cap entries. */
+/* Query-string compile status only (no device work): MM_OK,
+ * MM_ERR_QUERY_INVALID or MM_ERR_UNSUPPORTED. */
+int mm_debug_compile(const char* query);
 int32_t mm_debug_group_indexes(const int32_t* counts, const int64_t* created_at, int32_t n, int32_t required,
                                int32_t* group_offsets, int32_t* group_members, int64_t* avg_created_at, int32_t cap);
 

@@ -1,0 +1,160 @@
+// nakama_amd/csrc/gocompat.h — Go-runtime semantics the matchmaker path depends on.
+//
+//  * bluge sortable numeric encoding (vendor/.../bluge/numeric/float.go:21-27)
+//  * strconv.ParseFloat accepted syntax (query_string_parser.go:198-260)
+//  * time.Parse for blugeParseDateTime's layouts (server/match_common.go:221-236)
+//    and the RFC3339 date-range endpoints (query_string_parser.go:163-169)
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+namespace nkm {
+
+inline int64_t sortable_i64(double f) {
+    int64_t i;
+    std::memcpy(&i, &f, sizeof i);
+    return i < 0 ? (i ^ INT64_MAX) : i;
+}
+
+// Go strconv.ParseFloat(s, 64): returns false on syntax error or overflow.
+inline bool go_parse_float(const std::string& s, double* out) {
+    size_t n = s.size(), i = 0;
+    if (n == 0) return false;
+    bool neg = false;
+    if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; i = 1; }
+    auto lower_eq = [&](size_t from, const char* w) {
+        size_t wl = std::strlen(w);
+        if (n - from != wl) return false;
+        for (size_t k = 0; k < wl; k++) {
+            char c = s[from + k];
+            if (c >= 'A' && c <= 'Z') c = char(c + 32);
+            if (c != w[k]) return false;
+        }
+        return true;
+    };
+    if (lower_eq(i, "inf") || lower_eq(i, "infinity")) { *out = neg ? -HUGE_VAL : HUGE_VAL; return true; }
+    if (i == 0 && lower_eq(0, "nan")) { *out = std::nan(""); return true; }
+    bool hex = (n - i >= 2) && s[i] == '0' && (s[i + 1] == 'x' || s[i + 1] == 'X');
+    std::string buf = hex ? "0x" : "";
+    size_t k = hex ? i + 2 : i;
+    int digits = 0, dots = 0;
+    bool exp_seen = false, exp_digit = false;
+    for (; k < n; k++) {
+        char c = s[k];
+        if (c == '_') { if (!hex) return false; continue; }
+        if (!exp_seen) {
+            bool isd = (c >= '0' && c <= '9') || (hex && ((c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F')));
+            if (isd) { digits++; buf += c; continue; }
+            if (c == '.') { if (++dots > 1) return false; buf += c; continue; }
+            bool ise = hex ? (c == 'p' || c == 'P') : (c == 'e' || c == 'E');
+            if (ise && digits > 0) {
+                exp_seen = true;
+                buf += c;
+                if (k + 1 < n && (s[k + 1] == '+' || s[k + 1] == '-')) buf += s[++k];
+                continue;
+            }
+            return false;
+        }
+        if (c < '0' || c > '9') return false;
+        exp_digit = true;
+        buf += c;
+    }
+    if (digits == 0) return false;
+    if (exp_seen && !exp_digit) return false;
+    if (hex && !exp_seen) return false;
+    char* end = nullptr;
+    double v = std::strtod(buf.c_str(), &end);
+    if (!end || *end) return false;
+    if (std::isinf(v)) return false;
+    *out = neg ? -v : v;
+    return true;
+}
+
+struct GoTime {
+    bool ok = false;
+    bool zero = false;       // time.Time.IsZero()
+    bool in_range = true;    // representable as UnixNano (isDatetimeCompatible)
+    int64_t unix_nano = 0;
+};
+
+inline int64_t civil_days(int64_t y, int m, int d) {  // days since 1970-01-01
+    y -= m <= 2;
+    int64_t era = (y >= 0 ? y : y - 399) / 400;
+    int64_t yoe = y - era * 400;
+    int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+    int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + doe - 719468;
+}
+
+// layout: 0 RFC3339Nano, 1 RFC3339, 2 "2006-01-02T15:04:05", 3 "2006-01-02 15:04:05", 4 "2006-01-02"
+inline GoTime go_parse_time(const std::string& v, int layout) {
+    GoTime t;
+    size_t p = 0, n = v.size();
+    auto dig = [&](size_t at) { return at < n && v[at] >= '0' && v[at] <= '9'; };
+    auto two = [&](int* o) {
+        if (!dig(p) || !dig(p + 1)) return false;
+        *o = (v[p] - '0') * 10 + (v[p + 1] - '0');
+        p += 2;
+        return true;
+    };
+    auto lit = [&](char c) { if (p < n && v[p] == c) { p++; return true; } return false; };
+    if (n < 4) return t;
+    int64_t year = 0;
+    for (int k = 0; k < 4; k++) { if (!dig(k)) return t; year = year * 10 + (v[k] - '0'); }
+    p = 4;
+    int mon, day, hh = 0, mm = 0, ss = 0;
+    int64_t ns = 0, off = 0;
+    if (!lit('-') || !two(&mon) || !lit('-') || !two(&day)) return t;
+    if (layout != 4) {
+        if (!lit(layout == 3 ? ' ' : 'T')) return t;
+        if (!dig(p)) return t;
+        hh = v[p++] - '0';
+        if (dig(p)) hh = hh * 10 + (v[p++] - '0');
+        if (!lit(':') || !two(&mm) || !lit(':') || !two(&ss)) return t;
+        if (p + 1 < n && (v[p] == '.' || v[p] == ',') && dig(p + 1)) {
+            p++;
+            int nd = 0;
+            while (dig(p)) { if (nd < 9) { ns = ns * 10 + (v[p] - '0'); nd++; } p++; }
+            while (nd++ < 9) ns *= 10;
+        }
+        if (layout <= 1) {
+            if (lit('Z')) {
+            } else {
+                if (p + 6 > n || (v[p] != '+' && v[p] != '-') || v[p + 3] != ':') return t;
+                int sign = v[p] == '-' ? -1 : 1;
+                p++;
+                int oh, om;
+                if (!two(&oh)) return t;
+                p++;
+                if (!two(&om)) return t;
+                if (oh > 24 || om > 60) return t;
+                off = sign * (oh * 3600 + om * 60);
+            }
+        }
+    }
+    if (p != n) return t;
+    if (mon < 1 || mon > 12) return t;
+    static const int dim[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    int maxd = dim[mon - 1] + (mon == 2 && ((year % 4 == 0 && year % 100 != 0) || year % 400 == 0));
+    if (day < 1 || day > maxd || hh > 23 || mm > 59 || ss > 59) return t;
+    __int128 secs = (__int128)civil_days(year, mon, day) * 86400 + hh * 3600 + mm * 60 + ss - off;
+    __int128 total = secs * 1000000000 + ns;
+    t.ok = true;
+    t.zero = (secs == (__int128)civil_days(1, 1, 1) * 86400) && ns == 0;
+    t.in_range = total >= (__int128)INT64_MIN && total <= (__int128)INT64_MAX;
+    t.unix_nano = (int64_t)(uint64_t)(unsigned __int128)total;
+    return t;
+}
+
+inline bool bluge_datetime(const std::string& v, int64_t* unix_nano) {
+    for (int layout = 0; layout < 5; layout++) {
+        GoTime t = go_parse_time(v, layout);
+        if (t.ok) { *unix_nano = t.unix_nano; return true; }
+    }
+    return false;
+}
+
+}  // namespace nkm

@@ -1,0 +1,113 @@
+// nakama_amd/csrc/mm_capi.cpp — extern "C" entry points of include/nakama_mm.h.
+// Every entry converts device failures into MM_ERR_DEVICE with a message in
+// mm_last_error; nothing here falls back to a CPU search.
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "mm_core.h"
+
+using nkm::Core;
+using nkm::DeviceError;
+
+namespace {
+thread_local std::string g_create_error;
+
+template <class F>
+int guarded(void* h, F&& f) {
+    if (!h) return MM_ERR_ARG;
+    Core* c = static_cast<Core*>(h);
+    try {
+        return f(*c);
+    } catch (const DeviceError& e) {
+        char buf[256];
+        std::snprintf(buf, sizeof buf, "HIP error %d (%s) at %s:%d", (int)e.err, hipGetErrorString(e.err), e.expr,
+                      e.line);
+        c->set_error(buf);
+        return MM_ERR_DEVICE;
+    } catch (const std::bad_alloc&) {
+        c->set_error("out of host memory");
+        return MM_ERR_INDEX;
+    }
+}
+std::string S(const char* p) { return p ? std::string(p) : std::string(); }
+}  // namespace
+
+extern "C" {
+
+int mm_abi_version(void) { return MM_ABI_VERSION; }
+const char* mm_backend_name(void) { return "hip-gfx950"; }
+
+void* mm_create(const mm_config* cfg) {
+    if (!cfg) return nullptr;
+    try {
+        return new Core(*cfg);
+    } catch (const DeviceError& e) {
+        g_create_error = std::string("mm_create: ") + hipGetErrorString(e.err);
+        return nullptr;
+    }
+}
+void mm_destroy(void* h) { delete static_cast<Core*>(h); }
+void mm_pause(void* h) { if (h) static_cast<Core*>(h)->pause(); }
+void mm_resume(void* h) { if (h) static_cast<Core*>(h)->resume(); }
+void mm_stop(void* h) { if (h) static_cast<Core*>(h)->stop(); }
+const char* mm_last_error(void* h) { return h ? static_cast<Core*>(h)->last_error() : g_create_error.c_str(); }
+
+int mm_add(void* h, const mm_ticket* t) {
+    if (!t) return MM_ERR_ARG;
+    return guarded(h, [&](Core& c) { return c.add(*t); });
+}
+int mm_insert(void* h, const mm_ticket* ts, int32_t n) {
+    if (n > 0 && !ts) return MM_ERR_ARG;
+    return guarded(h, [&](Core& c) { return c.insert(ts, n); });
+}
+int mm_extract(void* h, mm_extract_list* out) {
+    if (!out) return MM_ERR_ARG;
+    return guarded(h, [&](Core& c) { return c.extract(out); });
+}
+void mm_free_extract(void* h, mm_extract_list* out) {
+    if (h) static_cast<Core*>(h)->free_extract(out);
+}
+int mm_remove_session(void* h, const char* session_id, const char* ticket) {
+    return guarded(h, [&](Core& c) { return c.remove_session(S(session_id), S(ticket)); });
+}
+int mm_remove_session_all(void* h, const char* session_id) {
+    return guarded(h, [&](Core& c) { return c.remove_session_all(S(session_id)); });
+}
+int mm_remove_party(void* h, const char* party_id, const char* ticket) {
+    return guarded(h, [&](Core& c) { return c.remove_party(S(party_id), S(ticket)); });
+}
+int mm_remove_party_all(void* h, const char* party_id) {
+    return guarded(h, [&](Core& c) { return c.remove_party_all(S(party_id)); });
+}
+int mm_remove_all(void* h, const char* node) {
+    return guarded(h, [&](Core& c) { return c.remove_all(S(node)); });
+}
+int mm_remove(void* h, const char* const* tickets, int32_t n) {
+    if (n > 0 && !tickets) return MM_ERR_ARG;
+    return guarded(h, [&](Core& c) { return c.remove(tickets, n); });
+}
+int mm_process(void* h, mm_matched* out) {
+    if (!out) return MM_ERR_ARG;
+    return guarded(h, [&](Core& c) { return c.process(out); });
+}
+int mm_process_commit(void* h, const int32_t* group_offsets, const mm_entry_ref* entries, int32_t n_groups,
+                      mm_matched* out) {
+    if (!out || (n_groups > 0 && (!group_offsets || !entries))) return MM_ERR_ARG;
+    return guarded(h, [&](Core& c) { return c.process_commit(group_offsets, entries, n_groups, out); });
+}
+void mm_free_matched(void* h, mm_matched* out) {
+    if (h) static_cast<Core*>(h)->free_matched(out);
+}
+int32_t mm_ticket_count(void* h) { return h ? static_cast<Core*>(h)->ticket_count() : -1; }
+int32_t mm_active_count(void* h) { return h ? static_cast<Core*>(h)->active_count() : -1; }
+int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, double* scores_out, int32_t cap) {
+    int32_t r = -1;
+    int rc = guarded(h, [&](Core& c) {
+        r = c.debug_hits(S(ticket), tickets_out, scores_out, cap);
+        return MM_OK;
+    });
+    return rc == MM_OK ? r : rc;
+}
+
+}  // extern "C"

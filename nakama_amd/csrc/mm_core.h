@@ -1,0 +1,310 @@
+// nakama_amd/csrc/mm_core.h — host side of the MI355X matchmaker.
+//
+// `Core` mirrors LocalMatchmaker (server/matchmaker.go:185-212): the ticket
+// maps become a slot-indexed SoA store whose hot columns live in HBM
+// (mm_device.h), each ticket's query is compiled once at Add/Insert into a
+// clause list shared by every ticket with the same compiled signature, and
+// Process() runs the interval pass as batches of device searches followed by
+// an exact replay of processDefault's greedy grouping.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/nakama_mm.h"
+#include "mm_device.h"
+#include "qcompile.h"
+
+namespace nkm {
+
+hipError_t launch_search(const DStore& st, const DGroup* d_groups, int n_groups, DHit* d_out, uint8_t* d_rev,
+                         DGroupResult* d_res, hipStream_t stream);
+hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_t n, hipStream_t stream);
+hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, uint8_t* d_out, hipStream_t stream);
+int var_k_capacity();
+
+struct DeviceError {
+    hipError_t err;
+    const char* expr;
+    int line;
+};
+#define NKM_HIP(x)                                                        \
+    do {                                                                  \
+        hipError_t e__ = (x);                                             \
+        if (e__ != hipSuccess) throw ::nkm::DeviceError{e__, #x, __LINE__}; \
+    } while (0)
+
+// Growable device array.
+template <class T>
+struct DevArray {
+    T* p = nullptr;
+    size_t cap = 0;
+    void reserve(size_t n, bool keep = true);
+    void release();
+    ~DevArray() { release(); }
+};
+
+// Pinned host staging buffer.
+template <class T>
+struct PinnedArray {
+    T* p = nullptr;
+    size_t cap = 0;
+    void reserve(size_t n);
+    void release();
+    ~PinnedArray() { release(); }
+};
+
+// String dictionary (keyword values, query terms, party ids).
+struct Dict {
+    std::unordered_map<std::string, uint32_t> id;
+    std::vector<std::string> str;
+    uint32_t intern(const std::string& s) {
+        auto it = id.find(s);
+        if (it != id.end()) return it->second;
+        uint32_t v = (uint32_t)str.size();
+        id.emplace(s, v);
+        str.push_back(s);
+        return v;
+    }
+    int64_t find(const std::string& s) const {
+        auto it = id.find(s);
+        return it == id.end() ? -1 : (int64_t)it->second;
+    }
+    void clear() { id.clear(); str.clear(); }
+};
+
+struct Presence {
+    std::string user_id, session_id, username, node;
+};
+
+// Host-only per-ticket record kept for Extract and delivery.
+struct Cold {
+    std::string session_id, party_id, query, node;
+    std::vector<std::pair<std::string, std::string>> sprops;
+    std::vector<std::pair<std::string, double>> nprops;
+    std::vector<Presence> presences;
+};
+
+// One compiled signature: clauses + the searching ticket's filters.  Tickets
+// whose searches are identical share it (and share one device search).
+struct Sig {
+    uint32_t clause_off = 0;
+    uint16_t n_clauses = 0;
+    uint8_t qkind = 0;
+    bool var_score = false;
+    int32_t tmin = 0, tmax = 0;
+    uint32_t tparty = kNoParty;
+    int64_t ub_key = INT64_MAX;
+    std::vector<std::pair<uint16_t, uint32_t>> must_terms;  // candidate posting lists
+};
+
+// key id -> set of slots, optimised for the common one-slot case
+// (sessionTickets / partyTickets, matchmaker.go:201-204).
+struct SlotSets {
+    std::vector<uint32_t> first;
+    std::unordered_map<uint32_t, std::vector<uint32_t>> more;
+    void ensure(uint32_t key) { if (key >= first.size()) first.resize(key + 1, kNoSlot); }
+    size_t count(uint32_t key) const {
+        if (key >= first.size() || first[key] == kNoSlot) return 0;
+        auto it = more.find(key);
+        return 1 + (it == more.end() ? 0 : it->second.size());
+    }
+    void add(uint32_t key, uint32_t slot) {
+        ensure(key);
+        if (first[key] == kNoSlot) { first[key] = slot; return; }
+        more[key].push_back(slot);
+    }
+    void erase(uint32_t key, uint32_t slot) {
+        if (key >= first.size() || first[key] == kNoSlot) return;
+        auto it = more.find(key);
+        if (first[key] == slot) {
+            if (it == more.end()) { first[key] = kNoSlot; return; }
+            first[key] = it->second.back();
+            it->second.pop_back();
+        } else if (it != more.end()) {
+            auto& v = it->second;
+            for (size_t i = 0; i < v.size(); i++)
+                if (v[i] == slot) { v[i] = v.back(); v.pop_back(); break; }
+        } else {
+            return;
+        }
+        if (it != more.end() && it->second.empty()) more.erase(it);
+    }
+    std::vector<uint32_t> list(uint32_t key) const {
+        std::vector<uint32_t> v;
+        if (key >= first.size() || first[key] == kNoSlot) return v;
+        v.push_back(first[key]);
+        auto it = more.find(key);
+        if (it != more.end()) v.insert(v.end(), it->second.begin(), it->second.end());
+        return v;
+    }
+    void clear() { first.clear(); more.clear(); }
+};
+
+struct PostingRange {
+    uint32_t off = 0, len = 0, head = 0;  // head: first entry possibly alive
+};
+
+// Builtin document fields (MapMatchmakerIndex, matchmaker.go:1026-1040).
+enum BuiltinField : uint16_t { F_TICKET = 0, F_MIN = 1, F_MAX = 2, F_PARTY = 3, F_CREATED = 4, F_NBUILTIN = 5 };
+
+struct PassStats {
+    double eval_ms = 0;
+    int64_t pair_evals = 0;
+    int batches = 0;
+    int refetches = 0;
+};
+
+class Core {
+public:
+    explicit Core(const mm_config& cfg);
+    ~Core();
+
+    int add(const mm_ticket& t);
+    int insert(const mm_ticket* ts, int32_t n);
+    int extract(mm_extract_list* out);
+    void free_extract(mm_extract_list* out);
+    int remove_session(const std::string& sid, const std::string& ticket);
+    int remove_session_all(const std::string& sid);
+    int remove_party(const std::string& pid, const std::string& ticket);
+    int remove_party_all(const std::string& pid);
+    int remove_all(const std::string& node);
+    int remove(const char* const* tickets, int32_t n);
+    int process(mm_matched* out);
+    int process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t n_groups, mm_matched* out);
+    void free_matched(mm_matched* out);
+    int32_t ticket_count();
+    int32_t active_count();
+    int32_t debug_hits(const std::string& ticket, const char** tk, double* sc, int32_t cap);
+
+    void pause() { active_flag_ = false; }
+    void resume() { active_flag_ = true; }
+    void stop() { stopped_ = true; }
+    const char* last_error() const { return last_error_.c_str(); }
+    void set_error(const std::string& e) { last_error_ = e; }
+
+private:
+    friend struct Replay;
+    struct Ticket;
+
+    // ---- store ----
+    int add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_insert);
+    uint16_t field_of(const std::string& name);
+    uint32_t sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party);
+    void set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val);
+    void kill_slot(uint32_t slot, bool device_cleared = false);  // ticket leaves the index and the maps
+    void maybe_compact();
+    void compact();
+    bool live(uint32_t slot) const { return live_[slot] != 0; }
+    int64_t slot_of_ticket(const std::string& t) const;
+
+    // ---- device ----
+    void sync_device();     // uploads, index build, pending deletes
+    void build_index();     // scan order + posting lists
+    void ensure_field_on_device(uint16_t f);
+    DStore dstore() const;
+
+    // ---- pass ----
+    int process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& groups, std::vector<uint32_t>& expired,
+                        PassStats& st);
+    int process_custom(std::vector<std::vector<std::pair<uint32_t, int>>>& cands, std::vector<uint32_t>& expired,
+                       PassStats& st);
+    void finish_pass(const std::vector<uint32_t>& expired, std::vector<std::vector<std::pair<uint32_t, int>>>& groups);
+    void fill_matched(const std::vector<std::vector<std::pair<uint32_t, int>>>& groups, mm_matched* out, bool cands);
+    void choose_source(const Sig& s, DGroup& g);
+    void apply_selected_to_device(const std::vector<uint32_t>& slots);
+
+    std::mutex mu_;
+    mm_config cfg_;
+    std::string node_;
+    bool active_flag_ = true;
+    bool stopped_ = false;
+    std::string last_error_;
+    int device_ = 0;
+    hipStream_t stream_ = nullptr;
+    hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+
+public:
+    // ---- host SoA (per slot) ----  (public for the replay helpers)
+    Dict dict_;                       // keyword values / terms / parties
+    Dict sess_dict_;                  // presence session ids
+    Dict field_dict_;                 // field names -> field id
+    std::vector<std::string> ticket_;
+    std::vector<int64_t> created_;
+    std::vector<int64_t> ckey_;       // sortable key of float64(CreatedAt)
+    std::vector<int32_t> minc_, maxc_, cm_, count_, intervals_;
+    std::vector<uint32_t> party_;     // kNoParty for ""
+    std::vector<uint8_t> live_;       // in m.indexes (and in the bluge index)
+    std::vector<uint8_t> is_active_;  // in m.activeIndexes
+    std::vector<uint32_t> sig_;
+    std::vector<uint32_t> pres_off_;  // CSR over presences: [slot] -> first presence
+    std::vector<uint32_t> pres_sess_; // per presence: session dict id
+    std::vector<Cold> cold_;
+    std::vector<std::vector<int64_t>> fval_;
+    std::vector<std::vector<uint8_t>> fkind_;
+    std::unordered_map<std::string, uint32_t> slot_of_;  // may hold dead slots (checked with live_)
+    std::vector<uint32_t> active_list_;                  // pinned (CreatedAt, Ticket) order, may hold inactive
+    bool active_sorted_ = true;
+    SlotSets sess_slots_;             // session dict id -> slots (sessionTickets)
+    SlotSets party_slots_;            // party dict id -> slots (partyTickets)
+    uint32_t n_live_ = 0;
+
+    // ---- signatures / clauses ----
+    std::unordered_map<std::string, uint32_t> sig_index_;
+    std::vector<Sig> sigs_;
+    std::vector<DClause> clauses_;
+    std::vector<DQuery> squery_;      // per slot
+    std::vector<uint8_t> field_used_; // per field: referenced by some clause
+    std::vector<uint8_t> field_posting_; // per field: used as a MUST TERM source
+
+    // ---- index (scan order + postings), host mirror ----
+    std::vector<uint32_t> order_;
+    bool order_sorted_ = true;
+    bool index_dirty_ = true;
+    uint32_t order_head_ = 0;
+    std::unordered_map<uint64_t, PostingRange> postings_map_;
+    std::vector<uint32_t> postings_;
+    std::vector<uint32_t> pending_dead_;  // slots to clear on the device at next sync
+
+    // ---- device mirror ----
+    size_t dev_slots_ = 0;  // slots uploaded
+    size_t dev_cap_ = 0;
+    DevArray<uint8_t> d_alive_;
+    DevArray<int32_t> d_minc_, d_maxc_;
+    DevArray<uint32_t> d_party_;
+    DevArray<DQuery> d_squery_;
+    DevArray<DClause> d_clauses_;
+    size_t dev_clauses_ = 0;
+    std::vector<DevArray<int64_t>*> d_fval_;
+    std::vector<DevArray<uint8_t>*> d_fkind_;
+    std::vector<size_t> dev_field_slots_;
+    DevArray<int64_t*> d_fval_ptrs_;
+    DevArray<uint8_t*> d_fkind_ptrs_;
+    DevArray<uint32_t> d_order_, d_postings_;
+    DevArray<DGroup> d_groups_;
+    DevArray<DHit> d_out_;
+    DevArray<uint8_t> d_rev_;
+    DevArray<DGroupResult> d_res_;
+    DevArray<uint32_t> d_slots_tmp_;
+    DevArray<uint8_t> d_pair_out_;
+    PinnedArray<DGroup> h_groups_;
+    PinnedArray<DHit> h_out_;
+    PinnedArray<uint8_t> h_rev_;
+    PinnedArray<DGroupResult> h_res_;
+    PinnedArray<uint32_t> h_slots_tmp_;
+    PinnedArray<uint8_t> h_pair_out_;
+
+    // ---- open custom pass ----
+    bool custom_open_ = false;
+    std::vector<uint32_t> custom_expired_;
+
+    std::vector<std::string> debug_strings_;
+    DevArray<uint32_t> d_pm_;      // pair matrices (RevPrecision combos)
+    PinnedArray<uint32_t> h_pm_;
+};
+
+}  // namespace nkm

@@ -1,0 +1,85 @@
+// nakama_amd/csrc/mm_device.h — HBM layout of the ticket store and the work
+// descriptors of the query-eval kernels.  Shared by host code (.cpp) and the
+// HIP kernels (.hip); plain structs only.
+#pragma once
+#include <cstdint>
+
+namespace nkm {
+
+constexpr uint32_t kNoParty = 0xFFFFFFFFu;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+// Column value kinds (one byte per (field, slot)).
+enum : uint8_t { KIND_ABSENT = 0, KIND_KEYWORD = 1, KIND_NUMERIC = 2 };
+
+// One compiled clause (32 B).  lo/hi: sortable int64 bounds (RANGE) or the
+// numeric literal (NUMLIT, lo == hi); term: dictionary id of the keyword form.
+struct DClause {
+    int64_t lo;
+    int64_t hi;
+    double score;
+    uint32_t term;
+    uint16_t field;
+    uint8_t op;     // ClauseOp
+    uint8_t occur;  // Occur
+};
+static_assert(sizeof(DClause) == 32, "DClause is 32 bytes");
+
+// Query of one slot (its ParsedQuery), used by the reverse (RevPrecision) check.
+struct DQuery {
+    uint32_t clause_off;
+    uint16_t n_clauses;
+    uint8_t kind;       // QueryKind
+    uint8_t n_must_nz;  // 1 if the query has at least one MUST clause
+};
+
+// Read-only view of the device-resident SoA store passed to kernels.
+struct DStore {
+    const uint8_t* alive;       // [cap] 1 = in the index (not deleted / not selected)
+    const int32_t* minc;        // [cap] MinCount
+    const int32_t* maxc;        // [cap] MaxCount
+    const uint32_t* party;      // [cap] dictionary id of PartyId, kNoParty for ""
+    const DQuery* squery;       // [cap] per-slot parsed query descriptor
+    const DClause* clauses;     // clause table (all signatures)
+    const int64_t* const* fval; // [n_fields] -> [cap] keyword id or sortable int64
+    const uint8_t* const* fkind;// [n_fields] -> [cap] KIND_*
+    const uint32_t* order;      // scan order: slots sorted by (created key, slot)
+    const uint32_t* postings;   // concatenated posting lists (slots, scan order)
+};
+
+// One search (a group of rows sharing a compiled signature, or one row).
+struct DGroup {
+    uint32_t clause_off;
+    uint16_t n_clauses;
+    uint8_t qkind;
+    uint8_t var_score;     // 0: every hit scores the same (ordered compaction); 1: top-K by score
+    int32_t tmin, tmax;    // searching ticket's Min/MaxCount (count-range musts)
+    uint32_t tparty;       // kNoParty or dictionary id (party mustNot)
+    uint32_t rev_slot;     // kNoSlot, or the searching ticket for the per-hit reverse check
+    uint32_t src_kind;     // 0: order[], 1: postings[]
+    uint32_t src_off;
+    uint32_t src_len;
+    uint32_t k;            // max entries to emit
+    uint64_t out_off;      // first output entry
+    int64_t ub_key;        // sortable key of an upper bound of any score (early exit)
+    int64_t cur_key;       // pagination cursor: emit only entries after (cur_key, cur_idx)
+    uint32_t cur_idx;
+    uint32_t has_cursor;
+};
+
+// Per-group result.
+struct DGroupResult {
+    uint32_t count;     // entries written (<= k)
+    uint32_t complete;  // 1: no further hit exists after the written ones
+    uint32_t scanned;   // candidates examined
+    uint32_t matched;   // candidates that passed the predicate (after the cursor)
+};
+
+// One emitted hit.
+struct DHit {
+    uint32_t slot;
+    uint32_t idx;   // position in the group's source (tie-break / cursor)
+    int64_t key;    // sortable score key (tie-break / cursor); bit 0 of flags below
+};
+
+}  // namespace nkm

@@ -1,0 +1,282 @@
+// nakama_amd/csrc/mm_kernels.hip — CDNA4 (gfx950) kernels of the interval pass.
+//
+// search_kernel: one 256-thread workgroup (4 wave64) per search.  The search
+// streams its candidate source (a posting list of its most selective required
+// term, or the created-at scan order) in tiles of 256 candidates, one
+// candidate per lane: coalesced 4-B slot ids, then gathers of the SoA columns
+// the compiled query references (alive, Min/MaxCount, party, field columns).
+// Each lane evaluates the predicate/score bytecode (wave-uniform clause loop,
+// scalar loads) — the bluge search of matchmaker_process.go:65-103 restated as
+// a flat predicate.  Survivors are:
+//   * constant-score searches: compacted in source order with wave ballots +
+//     an LDS scan across the 4 waves (source order == the reference's
+//     (-score, created_at, doc) sort when every hit scores the same);
+//   * variable-score searches: merged into an LDS top-K list ordered by
+//     (score desc, source position asc) with a rank merge, with early exit once
+//     the K-th score reaches the query's score upper bound.
+// With RevPrecision the lane also evaluates the hit's own query against the
+// searching ticket's document (validateMatch, matchmaker.go:1042-1068).
+#include <hip/hip_runtime.h>
+
+#include "mm_device.h"
+#include "qcompile.h"
+
+namespace nkm {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kVarK = 512;  // LDS capacity of a variable-score top-K list
+
+__device__ __forceinline__ int64_t dsortable(double f) {
+    int64_t i = __double_as_longlong(f);
+    return i < 0 ? (i ^ 0x7fffffffffffffffLL) : i;
+}
+
+// Parsed-query evaluation on document `s` (bluge BooleanSearcher semantics,
+// search_boolean.go:174-244).  *sp receives the parsed query's score.
+__device__ __forceinline__ bool eval_parsed(const DStore& st, uint8_t qkind, const DClause* __restrict__ cl, int n,
+                                            uint32_t s, double* sp) {
+    if (qkind == QK_MATCHALL) { *sp = 1.0; return true; }
+    if (qkind == QK_MATCHNONE) return false;
+    double ms = 0.0, ss = 0.0;
+    bool has_must = false, has_should = false, any_should = false, fail = false;
+    for (int i = 0; i < n; i++) {
+        const DClause c = cl[i];
+        bool h = false;
+        if (c.op != OP_FALSE) {
+            const uint8_t kind = st.fkind[c.field][s];
+            const int64_t val = st.fval[c.field][s];
+            if (c.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)c.term;
+            else if (c.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= c.lo && val <= c.hi;
+            else h = (kind == KIND_KEYWORD && val == (int64_t)c.term) || (kind == KIND_NUMERIC && val == c.lo);
+        }
+        if (c.occur == OCC_MUST) { has_must = true; if (h) ms += c.score; else fail = true; }
+        else if (c.occur == OCC_SHOULD) { has_should = true; if (h) { ss += c.score; any_should = true; } }
+        else if (h) fail = true;
+    }
+    if (fail) return false;
+    if (!has_must && !has_should) { *sp = 1.0; return true; }  // only mustNots: MatchAll(1)
+    if (!has_must) { *sp = ss; return any_should; }
+    *sp = any_should ? ms + ss : ms;
+    return true;
+}
+
+struct Cand {
+    uint32_t slot;
+    uint32_t idx;
+    int64_t key;
+    uint8_t rev;
+    bool m;
+};
+
+__device__ __forceinline__ Cand eval_candidate(const DStore& st, const DGroup& g, const uint32_t* __restrict__ src,
+                                               uint32_t idx) {
+    Cand c{0, idx, 0, 1, false};
+    if (idx >= g.src_len) return c;
+    const uint32_t s = src[g.src_off + idx];
+    c.slot = s;
+    bool m = st.alive[s] != 0;
+    if (m) m = st.minc[s] >= g.tmin && st.maxc[s] <= g.tmax && (g.tparty == kNoParty || st.party[s] != g.tparty);
+    double sp = 0.0;
+    if (m) m = eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
+    if (m) {
+        // top-level BooleanQuery{must: parsed, min_count range, max_count range}
+        c.key = dsortable((sp + 1.0) + 1.0);
+        if (g.has_cursor) m = c.key < g.cur_key || (c.key == g.cur_key && idx > g.cur_idx);
+    }
+    if (m && g.rev_slot != kNoSlot) {
+        const DQuery q = st.squery[s];
+        double d;
+        c.rev = eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, g.rev_slot, &d) ? 1 : 0;
+    }
+    c.m = m;
+    return c;
+}
+
+__global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup* __restrict__ groups,
+                                                        DHit* __restrict__ out, uint8_t* __restrict__ out_rev,
+                                                        DGroupResult* __restrict__ res) {
+    __shared__ uint32_t wave_cnt[kWaves];
+    __shared__ int64_t wave_max[kWaves];
+    // variable-score list (double-buffered) + tile staging
+    __shared__ int64_t lkey[2][kVarK];
+    __shared__ uint32_t lidx[2][kVarK];
+    __shared__ uint32_t lslot[2][kVarK];
+    __shared__ uint8_t lrev[2][kVarK];
+    __shared__ int64_t tkey[kBlock];
+    __shared__ uint32_t tidx[kBlock];
+    __shared__ uint32_t tslot[kBlock];
+    __shared__ uint8_t trev[kBlock];
+
+    const DGroup g = groups[blockIdx.x];
+    const uint32_t* src = g.src_kind == 0 ? st.order : st.postings;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t K = g.k;
+
+    if (!g.var_score) {
+        // ---- ordered compaction -------------------------------------------------
+        uint32_t count = 0;
+        uint32_t base = 0;
+        bool stopped = false;
+        for (; base < g.src_len; base += kBlock) {
+            Cand c = eval_candidate(st, g, src, base + tid);
+            const uint64_t mask = __ballot(c.m);
+            if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(mask);
+            __syncthreads();
+            uint32_t off = 0, tot = 0;
+            for (int w = 0; w < kWaves; w++) {
+                const uint32_t v = wave_cnt[w];
+                off += (w < wave) ? v : 0;
+                tot += v;
+            }
+            if (c.m) {
+                const uint32_t pos = count + off + (uint32_t)__popcll(mask & lt_mask);
+                if (pos < K) {
+                    out[g.out_off + pos] = DHit{c.slot, c.idx, c.key};
+                    if (out_rev) out_rev[g.out_off + pos] = c.rev;
+                }
+            }
+            count += tot;
+            __syncthreads();
+            if (count > K) { stopped = true; base += kBlock; break; }
+        }
+        if (tid == 0) {
+            res[blockIdx.x] = DGroupResult{count < K ? count : K, stopped ? 0u : 1u,
+                                           base < g.src_len ? base : g.src_len, count};
+        }
+        return;
+    }
+
+    // ---- variable-score top-K ------------------------------------------------------
+    const uint32_t KK = K < (uint32_t)kVarK ? K : (uint32_t)kVarK;
+    uint32_t n = 0, total = 0;
+    int cur = 0;
+    bool early = false;
+    uint32_t base = 0;
+    for (; base < g.src_len; base += kBlock) {
+        Cand c = eval_candidate(st, g, src, base + tid);
+        const uint64_t pre = __ballot(c.m);
+        if (n == KK && c.m) c.m = c.key > lkey[cur][KK - 1];
+        const uint64_t mask = __ballot(c.m);
+        if (lane == 0) { wave_cnt[wave] = (uint32_t)__popcll(mask); wave_max[wave] = (int64_t)__popcll(pre); }
+        __syncthreads();
+        uint32_t off = 0, cnt = 0;
+        for (int w = 0; w < kWaves; w++) {
+            const uint32_t v = wave_cnt[w];
+            off += (w < wave) ? v : 0;
+            cnt += v;
+            total += (uint32_t)wave_max[w];
+        }
+        if (cnt == 0) { __syncthreads(); continue; }
+        if (c.m) {
+            const uint32_t p = off + (uint32_t)__popcll(mask & lt_mask);
+            tkey[p] = c.key; tidx[p] = c.idx; tslot[p] = c.slot; trev[p] = c.rev;
+        }
+        __syncthreads();
+        const int nxt = cur ^ 1;
+        if ((uint32_t)tid < cnt) {
+            const int64_t k = tkey[tid];
+            // rank among the old list: entries with key >= k (list is sorted desc)
+            uint32_t lo = 0, hi = n;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (lkey[cur][mid] >= k) lo = mid + 1; else hi = mid;
+            }
+            uint32_t r = lo;
+            for (uint32_t t = 0; t < cnt; t++) {
+                const int64_t kt = tkey[t];
+                r += (kt > k) || (kt == k && t < (uint32_t)tid);
+            }
+            if (r < KK) { lkey[nxt][r] = k; lidx[nxt][r] = tidx[tid]; lslot[nxt][r] = tslot[tid]; lrev[nxt][r] = trev[tid]; }
+        }
+        for (uint32_t i = tid; i < n; i += kBlock) {
+            const int64_t k = lkey[cur][i];
+            uint32_t r = i;
+            for (uint32_t t = 0; t < cnt; t++) r += tkey[t] > k;
+            if (r < KK) { lkey[nxt][r] = k; lidx[nxt][r] = lidx[cur][i]; lslot[nxt][r] = lslot[cur][i]; lrev[nxt][r] = lrev[cur][i]; }
+        }
+        n = (n + cnt < KK) ? n + cnt : KK;
+        cur = nxt;
+        __syncthreads();
+        if (n == KK && lkey[cur][KK - 1] >= g.ub_key) { early = true; base += kBlock; break; }
+    }
+    for (uint32_t i = tid; i < n; i += kBlock) {
+        out[g.out_off + i] = DHit{lslot[cur][i], lidx[cur][i], lkey[cur][i]};
+        if (out_rev) out_rev[g.out_off + i] = lrev[cur][i];
+    }
+    if (tid == 0) {
+        const bool complete = !early && total <= KK;
+        res[blockIdx.x] = DGroupResult{n, complete ? 1u : 0u, base < g.src_len ? base : g.src_len, total};
+    }
+}
+
+__global__ void clear_alive_kernel(uint8_t* __restrict__ alive, const uint32_t* __restrict__ slots, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) alive[slots[i]] = 0;
+}
+
+// validateMatch for explicit (from, to) pairs: does `to`'s document match
+// `from`'s parsed query?  (matchmaker.go:1042-1068)
+__global__ void pair_kernel(DStore st, const uint32_t* __restrict__ pairs, uint32_t n, uint8_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t from = pairs[2 * i], to = pairs[2 * i + 1];
+    const DQuery q = st.squery[from];
+    double d;
+    out[i] = (st.alive[to] && eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, to, &d)) ? 1 : 0;
+}
+
+// Pair matrices for RevPrecision combos (matchmaker_process.go:178-203): for
+// the first 32 entries a, b of each search's list, bit b of pm[g*32+a] is
+// "entry b's document matches entry a's parsed query".
+__global__ void pairmat_kernel(DStore st, const DGroup* __restrict__ groups, const DGroupResult* __restrict__ res,
+                               int n_groups, const DHit* __restrict__ out, uint32_t* __restrict__ pm) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int g = t >> 5, a = t & 31;
+    if (g >= n_groups) return;
+    const uint32_t n = res[g].count < 32u ? res[g].count : 32u;
+    uint32_t mask = 0;
+    if ((uint32_t)a < n) {
+        const uint64_t base = groups[g].out_off;
+        const uint32_t from = out[base + a].slot;
+        const DQuery q = st.squery[from];
+        for (uint32_t b = 0; b < n; b++) {
+            double d;
+            if (eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, out[base + b].slot, &d)) mask |= 1u << b;
+        }
+    }
+    pm[(uint64_t)g * 32 + a] = mask;
+}
+
+hipError_t launch_pairmat(const DStore& st, const DGroup* d_groups, const DGroupResult* d_res, int n_groups,
+                          const DHit* d_out, uint32_t* d_pm, hipStream_t stream) {
+    if (n_groups <= 0) return hipSuccess;
+    const int threads = n_groups * 32;
+    hipLaunchKernelGGL(pairmat_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, st, d_groups, d_res, n_groups,
+                       d_out, d_pm);
+    return hipGetLastError();
+}
+
+hipError_t launch_search(const DStore& st, const DGroup* d_groups, int n_groups, DHit* d_out, uint8_t* d_rev,
+                         DGroupResult* d_res, hipStream_t stream) {
+    if (n_groups <= 0) return hipSuccess;
+    hipLaunchKernelGGL(search_kernel, dim3(n_groups), dim3(kBlock), 0, stream, st, d_groups, d_out, d_rev, d_res);
+    return hipGetLastError();
+}
+
+hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(clear_alive_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_alive, d_slots, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, uint8_t* d_out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pair_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, st, d_pairs, n, d_out);
+    return hipGetLastError();
+}
+
+int var_k_capacity() { return kVarK; }
+
+}  // namespace nkm

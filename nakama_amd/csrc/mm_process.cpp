@@ -1,0 +1,853 @@
+// nakama_amd/csrc/mm_process.cpp — the interval pass.
+//
+// Process() (server/matchmaker.go:282-372) with processDefault
+// (server/matchmaker_process.go:27-334) restated as:
+//   1. batch the active tickets in the pinned (CreatedAt, Ticket) order;
+//   2. one device search per compiled signature present in the batch
+//      (mm_kernels.hip), returning hit lists already sorted the way bluge's
+//      TopN collector sorts them (-score, created_at, doc order);
+//   3. an exact host replay of the greedy grouping over those lists.
+// Tickets selected earlier in the batch are skipped in the lists (the
+// reference deletes them from the index before the next search, and deleting
+// never reorders the remaining hits).  When a list runs out before the row is
+// decided, the batch ends there and the next batch re-runs the search with the
+// device alive mask up to date; the first row of a batch may page further
+// through its list with a cursor, so every batch makes progress.
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+#include "gocompat.h"
+#include "mm_core.h"
+
+namespace nkm {
+
+hipError_t launch_pairmat(const DStore& st, const DGroup* d_groups, const DGroupResult* d_res, int n_groups,
+                          const DHit* d_out, uint32_t* d_pm, hipStream_t stream);
+constexpr int kPairP = 32;  // pair matrix covers the first 32 entries of a list
+
+constexpr size_t kMaxBatchRows = 1u << 16;
+constexpr uint64_t kOutCap = 1ull << 24;  // max hit entries per batch (16M x 16 B)
+
+struct CE {  // combo entry: (ticket slot, presence index, list position of its hit)
+    uint32_t slot;
+    uint32_t pi;
+    uint32_t lpos;
+};
+
+// groupIndexes (server/matchmaker.go:132-167), int64 wrapping arithmetic.
+struct IG { std::vector<uint32_t> idx; int64_t avg; };
+void group_indexes(const std::vector<uint32_t>& in, size_t from, int required, const std::vector<int32_t>& cnt,
+                   const std::vector<int64_t>& created, std::vector<IG>& out) {
+    if (from >= in.size() || required <= 0) return;
+    const uint32_t cur = in[from];
+    if (cnt[cur] > required) { group_indexes(in, from + 1, required, cnt, created, out); return; }
+    if (cnt[cur] == required) {
+        out.push_back(IG{{cur}, created[cur]});
+    } else {
+        std::vector<IG> fill;
+        group_indexes(in, from + 1, required - cnt[cur], cnt, created, fill);
+        for (auto& f : fill) {
+            const int64_t n = (int64_t)f.idx.size();
+            f.avg = (int64_t)((uint64_t)f.avg * (uint64_t)n + (uint64_t)created[cur]) / (n + 1);
+            f.idx.push_back(cur);
+            out.push_back(std::move(f));
+        }
+    }
+    group_indexes(in, from + 1, required, cnt, created, out);
+}
+
+// A batch group: one device search and its (possibly extended) hit list.
+struct BGroup {
+    uint32_t sig;
+    uint32_t nrows = 0;
+    uint32_t row_slot = kNoSlot;  // RevPrecision: the single searching row
+    DGroup d{};
+    const DHit* hits = nullptr;
+    const uint8_t* rev = nullptr;
+    const uint32_t* pm = nullptr;  // kPairP masks per entry (rev rows with combos)
+    uint32_t pm_n = 0;             // entries covered by pm
+    uint32_t n = 0;
+    bool complete = true;
+    uint32_t head = 0;
+    std::vector<DHit> ext;
+    std::vector<uint8_t> ext_rev;
+};
+
+struct Replay {
+    Core& c;
+    std::vector<uint8_t>& sel;
+    const bool rev;
+    const int max_intervals;
+    std::vector<std::vector<CE>> combos;
+    PassStats& stats;
+    DStore st;
+    hipStream_t stream;
+
+    Replay(Core& core, std::vector<uint8_t>& s, bool r, int mi, PassStats& ps, DStore ds, hipStream_t sm)
+        : c(core), sel(s), rev(r), max_intervals(mi), stats(ps), st(ds), stream(sm) {}
+
+    bool share_session(uint32_t a, uint32_t b) const {
+        for (uint32_t p = c.pres_off_[a]; p < c.pres_off_[a + 1]; p++)
+            for (uint32_t q = c.pres_off_[b]; q < c.pres_off_[b + 1]; q++)
+                if (c.pres_sess_[p] == c.pres_sess_[q]) return true;
+        return false;
+    }
+    bool has_session(uint32_t slot, uint32_t sess) const {
+        for (uint32_t q = c.pres_off_[slot]; q < c.pres_off_[slot + 1]; q++)
+            if (c.pres_sess_[q] == sess) return true;
+        return false;
+    }
+
+    // Fetches the next page of a group's list (cursor = its last entry).
+    void fetch_more(BGroup& g) {
+        stats.refetches++;
+        if (g.ext.empty() && g.n) {
+            g.ext.assign(g.hits, g.hits + g.n);
+            if (g.rev) g.ext_rev.assign(g.rev, g.rev + g.n);
+        }
+        DGroup d = g.d;
+        d.out_off = 0;
+        d.has_cursor = g.n ? 1 : 0;
+        if (g.n) {
+            d.cur_key = g.hits[g.n - 1].key;
+            d.cur_idx = g.hits[g.n - 1].idx;
+        }
+        d.k = d.var_score ? (uint32_t)var_k_capacity() : std::max<uint32_t>(4096, 2 * d.k);
+        c.h_groups_.reserve(1);
+        c.h_groups_.p[0] = d;
+        c.d_groups_.reserve(1, false);
+        c.d_out_.reserve(d.k, false);
+        c.d_rev_.reserve(d.k, false);
+        c.d_res_.reserve(1, false);
+        NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, sizeof(DGroup), hipMemcpyHostToDevice, stream));
+        NKM_HIP(launch_search(st, c.d_groups_.p, 1, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream));
+        c.h_res_.reserve(1);
+        NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
+        NKM_HIP(hipStreamSynchronize(stream));
+        const DGroupResult r = c.h_res_.p[0];
+        stats.pair_evals += r.scanned;
+        std::vector<DHit> page(r.count);
+        std::vector<uint8_t> prev(r.count);
+        if (r.count) {
+            NKM_HIP(hipMemcpy(page.data(), c.d_out_.p, r.count * sizeof(DHit), hipMemcpyDeviceToHost));
+            if (rev) NKM_HIP(hipMemcpy(prev.data(), c.d_rev_.p, r.count, hipMemcpyDeviceToHost));
+        }
+        g.ext.insert(g.ext.end(), page.begin(), page.end());
+        if (rev) g.ext_rev.insert(g.ext_rev.end(), prev.begin(), prev.end());
+        g.hits = g.ext.data();
+        g.rev = rev ? g.ext_rev.data() : nullptr;
+        g.n = (uint32_t)g.ext.size();
+        g.complete = r.complete != 0;
+        g.d.k = d.k;
+    }
+
+    // validateMatch(from's query, to) for two entries of the same list.
+    bool pair_ok(const BGroup& g, uint32_t from_pos, uint32_t to_pos) {
+        if (g.pm && from_pos < g.pm_n && to_pos < g.pm_n) return (g.pm[from_pos] >> to_pos) & 1u;
+        // slow path: evaluate the single pair on the device
+        uint32_t pr[2] = {g.hits[from_pos].slot, g.hits[to_pos].slot};
+        c.d_slots_tmp_.reserve(2, false);
+        c.d_pair_out_.reserve(1, false);
+        NKM_HIP(hipMemcpyAsync(c.d_slots_tmp_.p, pr, sizeof pr, hipMemcpyHostToDevice, stream));
+        NKM_HIP(launch_pairs(st, c.d_slots_tmp_.p, 1, c.d_pair_out_.p, stream));
+        uint8_t v = 0;
+        NKM_HIP(hipMemcpyAsync(&v, c.d_pair_out_.p, 1, hipMemcpyDeviceToHost, stream));
+        NKM_HIP(hipStreamSynchronize(stream));
+        return v != 0;
+    }
+
+    enum Status { MATCHED, NOMATCH, EXHAUSTED };
+
+    // Is there an unselected, non-self hit after position i?  (the
+    // hitCounter >= lastHitCounter test, matchmaker_process.go:130,233)
+    int more_hits_after(BGroup& g, uint32_t i, uint32_t T, bool can_fetch) {
+        for (uint32_t j = i + 1;; j++) {
+            if (j >= g.n) {
+                if (g.complete) return 0;
+                if (!can_fetch) return -1;
+                fetch_more(g);
+                if (j >= g.n) { if (g.complete) return 0; continue; }
+            }
+            const uint32_t s = g.hits[j].slot;
+            if (s != T && !sel[s]) return 1;
+        }
+    }
+
+    // processDefault's loop body for one active ticket T.
+    Status row(uint32_t T, BGroup& g, bool can_fetch, std::vector<std::pair<uint32_t, int>>& group_out) {
+        const bool last = c.intervals_[T] + 1 >= max_intervals || c.minc_[T] == c.maxc_[T];
+        const int tcount = c.count_[T], tmax = c.maxc_[T], tmin = c.minc_[T], tcm = c.cm_[T];
+        combos.clear();
+        while (g.head < g.n && sel[g.hits[g.head].slot]) g.head++;
+        for (uint32_t i = g.head;; i++) {
+            if (i >= g.n) {
+                if (g.complete) break;
+                if (!can_fetch) return EXHAUSTED;
+                fetch_more(g);
+                if (i >= g.n) { if (g.complete) break; i--; continue; }
+            }
+            const uint32_t H = g.hits[i].slot;
+            if (H == T || sel[H]) continue;
+            if (rev && !g.rev[i]) continue;                                              // :139-148
+            if (tmax < c.maxc_[H] && c.intervals_[H] <= max_intervals) continue;        // :150-153
+            if (share_session(T, H)) continue;                                            // :155-165
+            bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
+            int found = -1;
+            const int hcount = c.count_[H];
+            for (size_t ci = 0; ci < combos.size(); ci++) {
+                auto& combo = combos[ci];
+                if ((int)combo.size() + hcount + tcount <= tmax) {
+                    bool mconf = false;
+                    for (const CE& e : combo) {
+                        if (has_session(H, c.pres_sess_[c.pres_off_[e.slot] + e.pi])) { sconf = true; break; }
+                        if (rev) {
+                            if (!pair_ok(g, i, e.lpos)) { mconf = true; break; }
+                            if (c.live_[e.slot] && !pair_ok(g, e.lpos, i)) { mconf = true; break; }
+                        }
+                    }
+                    if (sconf || mconf) continue;
+                    for (int k = 0; k < hcount; k++) combo.push_back(CE{H, (uint32_t)k, i});
+                    found = (int)ci;
+                    break;
+                }
+            }
+            if (found < 0) {
+                combos.emplace_back();
+                for (int k = 0; k < hcount; k++) combos.back().push_back(CE{H, (uint32_t)k, i});
+                found = (int)combos.size() - 1;
+            }
+            std::vector<CE>& fc = combos[found];
+            int l = (int)fc.size() + tcount;
+            bool form = l == tmax;
+            if (!form && last && l >= tmin && l <= tmax) {
+                int more = more_hits_after(g, i, T, can_fetch);
+                if (more < 0) return EXHAUSTED;
+                form = more == 0;
+            }
+            if (!form) continue;
+            const int rem = l % tcm;
+            if (rem != 0) {                                                                // :234-280
+                std::vector<uint32_t> elig;
+                for (const CE& e : fc) {
+                    if (!c.live_[e.slot] || c.count_[e.slot] > rem) continue;
+                    if (std::find(elig.begin(), elig.end(), e.slot) == elig.end()) elig.push_back(e.slot);
+                }
+                std::vector<IG> groups;
+                group_indexes(elig, 0, rem, c.count_, c.created_, groups);
+                if (groups.empty()) continue;
+                std::stable_sort(groups.begin(), groups.end(), [](const IG& a, const IG& b) { return a.avg < b.avg; });
+                for (uint32_t gs : groups[0].idx) {
+                    for (int k = 0; k < (int)fc.size(); k++) {
+                        if (fc[k].slot == gs) {
+                            fc[k] = fc.back();
+                            fc.pop_back();
+                            k--;
+                        }
+                    }
+                }
+                l = (int)fc.size() + tcount;
+                if (l % tcm != 0) continue;
+            }
+            bool failed = false;                                                           // :287-296
+            for (const CE& e : fc) {
+                const uint32_t s = e.slot;
+                if (c.live_[s] && (c.minc_[s] > l || c.maxc_[s] < l || l % c.cm_[s] != 0)) { failed = true; break; }
+            }
+            if (failed) continue;
+            group_out.clear();
+            for (const CE& e : fc) group_out.push_back({e.slot, (int)e.pi});
+            for (int k = 0; k < tcount; k++) group_out.push_back({T, k});
+            return MATCHED;
+        }
+        return NOMATCH;
+    }
+};
+
+void Core::choose_source(const Sig& s, DGroup& g) {
+    g.src_kind = 0;
+    g.src_off = order_head_;
+    g.src_len = (uint32_t)order_.size() - order_head_;
+    bool have = false;
+    for (auto& mt : s.must_terms) {
+        auto it = postings_map_.find(((uint64_t)mt.first << 32) | mt.second);
+        uint32_t off = 0, len = 0;
+        if (it != postings_map_.end()) {
+            PostingRange& r = it->second;
+            while (r.head < r.len && !live_[postings_[r.off + r.head]]) r.head++;  // skip the dead prefix
+            off = r.off + r.head;
+            len = r.len - r.head;
+        }
+        if (!have || len < g.src_len) {
+            g.src_kind = 1;
+            g.src_off = off;
+            g.src_len = len;
+            have = true;
+        }
+    }
+}
+
+int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& out_groups,
+                          std::vector<uint32_t>& expired, PassStats& stats) {
+    const uint32_t N = (uint32_t)ticket_.size();
+    std::vector<uint8_t> sel(N, 0);
+    const bool rev = cfg_.rev_precision != 0;
+    const int maxI = cfg_.max_intervals;
+    std::vector<uint32_t> rows;
+    rows.reserve(active_list_.size());
+    for (uint32_t s : active_list_)
+        if (live_[s] && is_active_[s]) rows.push_back(s);
+
+    if (!active_flag_) {  // paused: intervals still advance (matchmaker_process.go:53-63)
+        for (uint32_t r : rows) {
+            intervals_[r]++;
+            if (intervals_[r] >= maxI || minc_[r] == maxc_[r]) expired.push_back(r);
+        }
+        return MM_OK;
+    }
+
+    const DStore st = dstore();
+    Replay rp(*this, sel, rev, maxI, stats, st, stream_);
+    std::vector<int32_t> sig_group(sigs_.size(), -1);
+    std::vector<BGroup> bg;
+    std::vector<uint32_t> brow, brow_group, newly;
+    std::vector<std::pair<uint32_t, int>> grp;
+    const uint32_t kvar = (uint32_t)var_k_capacity();
+    size_t pos = 0;
+    uint32_t retry_slot = kNoSlot;
+    while (order_head_ < order_.size() && !live_[order_[order_head_]]) order_head_++;
+
+    while (true) {
+        while (pos < rows.size() && sel[rows[pos]]) pos++;
+        if (pos >= rows.size()) break;
+        // ---- assemble the batch ----
+        for (auto& g : bg)
+            if (!rev) sig_group[g.sig] = -1;
+        bg.clear();
+        brow.clear();
+        brow_group.clear();
+        uint64_t total_k = 0;
+        size_t q = pos;
+        for (; q < rows.size() && brow.size() < kMaxBatchRows; q++) {
+            const uint32_t r = rows[q];
+            if (sel[r]) continue;
+            int32_t gi = rev ? -1 : sig_group[sig_[r]];
+            if (gi < 0) {
+                BGroup g;
+                g.sig = sig_[r];
+                const Sig& s = sigs_[g.sig];
+                g.d.clause_off = s.clause_off;
+                g.d.n_clauses = s.n_clauses;
+                g.d.qkind = s.qkind;
+                g.d.var_score = s.var_score ? 1 : 0;
+                g.d.tmin = s.tmin;
+                g.d.tmax = s.tmax;
+                g.d.tparty = s.tparty;
+                g.d.rev_slot = rev ? r : kNoSlot;
+                g.d.ub_key = s.ub_key;
+                g.d.has_cursor = 0;
+                choose_source(s, g.d);
+                g.d.k = 0;
+                g.row_slot = rev ? r : kNoSlot;
+                gi = (int32_t)bg.size();
+                bg.push_back(std::move(g));
+                if (!rev) sig_group[sig_[r]] = gi;
+            }
+            BGroup& g = bg[gi];
+            g.nrows++;
+            const uint64_t want = (uint64_t)g.nrows * (uint64_t)std::max(2, maxc_[r]) * 2 + 32;
+            uint32_t k = g.d.var_score ? (uint32_t)std::min<uint64_t>(kvar, want)
+                                       : (uint32_t)std::min<uint64_t>(std::max<uint32_t>(g.d.src_len, 1), want + 224);
+            if (r == retry_slot) k = g.d.var_score ? kvar : std::max<uint32_t>(g.d.src_len, 1);
+            total_k += (uint64_t)k - g.d.k;
+            g.d.k = std::max<uint32_t>(k, 1);
+            brow.push_back(r);
+            brow_group.push_back((uint32_t)gi);
+            if (total_k > kOutCap && brow.size() > 1) { q++; break; }
+        }
+        // ---- device search ----
+        const int ng = (int)bg.size();
+        uint64_t off = 0;
+        h_groups_.reserve(ng);
+        for (int i = 0; i < ng; i++) {
+            bg[i].d.out_off = off;
+            off += bg[i].d.k;
+            h_groups_.p[i] = bg[i].d;
+        }
+        d_groups_.reserve(ng, false);
+        d_res_.reserve(ng, false);
+        d_out_.reserve(std::max<uint64_t>(off, 1), false);
+        if (rev) d_rev_.reserve(std::max<uint64_t>(off, 1), false);
+        NKM_HIP(hipMemcpyAsync(d_groups_.p, h_groups_.p, ng * sizeof(DGroup), hipMemcpyHostToDevice, stream_));
+        NKM_HIP(hipEventRecord(ev0_, stream_));
+        NKM_HIP(launch_search(st, d_groups_.p, ng, d_out_.p, rev ? d_rev_.p : nullptr, d_res_.p, stream_));
+        NKM_HIP(hipEventRecord(ev1_, stream_));
+        bool need_pm = false;
+        if (rev) {
+            for (int i = 0; i < ng && !need_pm; i++) {
+                const uint32_t r = bg[i].row_slot;
+                need_pm = maxc_[r] - count_[r] >= 2;
+            }
+        }
+        if (need_pm) {
+            d_pm_.reserve((uint64_t)ng * kPairP, false);
+            NKM_HIP(launch_pairmat(st, d_groups_.p, d_res_.p, ng, d_out_.p, d_pm_.p, stream_));
+        }
+        h_res_.reserve(ng);
+        NKM_HIP(hipMemcpyAsync(h_res_.p, d_res_.p, ng * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream_));
+        h_out_.reserve(std::max<uint64_t>(off, 1));
+        NKM_HIP(hipMemcpyAsync(h_out_.p, d_out_.p, off * sizeof(DHit), hipMemcpyDeviceToHost, stream_));
+        if (rev) {
+            h_rev_.reserve(std::max<uint64_t>(off, 1));
+            NKM_HIP(hipMemcpyAsync(h_rev_.p, d_rev_.p, off, hipMemcpyDeviceToHost, stream_));
+        }
+        if (need_pm) {
+            h_pm_.reserve((uint64_t)ng * kPairP);
+            NKM_HIP(hipMemcpyAsync(h_pm_.p, d_pm_.p, (uint64_t)ng * kPairP * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   stream_));
+        }
+        NKM_HIP(hipStreamSynchronize(stream_));
+        float ms = 0.f;
+        NKM_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
+        stats.eval_ms += ms;
+        stats.batches++;
+        for (int i = 0; i < ng; i++) {
+            BGroup& g = bg[i];
+            const DGroupResult& r = h_res_.p[i];
+            g.hits = h_out_.p + g.d.out_off;
+            g.rev = rev ? h_rev_.p + g.d.out_off : nullptr;
+            g.pm = need_pm ? h_pm_.p + (uint64_t)i * kPairP : nullptr;
+            g.pm_n = need_pm ? std::min<uint32_t>(r.count, kPairP) : 0;
+            g.n = r.count;
+            g.complete = r.complete != 0;
+            g.head = 0;
+            stats.pair_evals += r.scanned;
+        }
+        // ---- replay ----
+        newly.clear();
+        size_t done = 0;
+        bool exhausted = false;
+        for (size_t bi = 0; bi < brow.size(); bi++) {
+            const uint32_t T = brow[bi];
+            if (sel[T]) { done = bi + 1; continue; }
+            auto status = rp.row(T, bg[brow_group[bi]], bi == 0, grp);
+            if (status == Replay::EXHAUSTED) {
+                exhausted = true;
+                retry_slot = T;
+                break;
+            }
+            intervals_[T]++;
+            if (intervals_[T] >= maxI || minc_[T] == maxc_[T]) expired.push_back(T);
+            if (status == Replay::MATCHED) {
+                for (auto& e : grp) {
+                    if (!sel[e.first]) {
+                        sel[e.first] = 1;
+                        newly.push_back(e.first);
+                    }
+                }
+                out_groups.push_back(grp);
+            }
+            done = bi + 1;
+        }
+        apply_selected_to_device(newly);
+        // advance past the rows this batch decided
+        if (exhausted) {
+            while (pos < rows.size() && rows[pos] != retry_slot) pos++;
+        } else {
+            pos = q;
+            retry_slot = kNoSlot;
+        }
+        (void)done;
+    }
+    return MM_OK;
+}
+
+// processCustom (matchmaker_process.go:336-612), up to the override call.
+int Core::process_custom(std::vector<std::vector<std::pair<uint32_t, int>>>& cands, std::vector<uint32_t>& expired,
+                         PassStats& stats) {
+    const bool rev = cfg_.rev_precision != 0;
+    const int maxI = cfg_.max_intervals;
+    std::vector<uint32_t> rows;
+    for (uint32_t s : active_list_)
+        if (live_[s] && is_active_[s]) rows.push_back(s);
+    for (uint32_t r : rows) intervals_[r]++;  // :347-350
+    for (uint32_t r : rows)
+        if (intervals_[r] >= maxI || minc_[r] == maxc_[r]) expired.push_back(r);
+    if (!active_flag_) return MM_OK;
+    const DStore st = dstore();
+    std::vector<uint8_t> sel(ticket_.size(), 0);  // processCustom never selects
+    Replay rp(*this, sel, rev, maxI, stats, st, stream_);
+    while (order_head_ < order_.size() && !live_[order_[order_head_]]) order_head_++;
+    const uint32_t kvar = (uint32_t)var_k_capacity();
+    // every row is independent: one search per row, in chunks
+    for (size_t base = 0; base < rows.size(); base += kMaxBatchRows / 4) {
+        const size_t end = std::min(rows.size(), base + kMaxBatchRows / 4);
+        std::vector<BGroup> bg(end - base);
+        uint64_t off = 0;
+        h_groups_.reserve(bg.size());
+        for (size_t i = 0; i < bg.size(); i++) {
+            const uint32_t r = rows[base + i];
+            BGroup& g = bg[i];
+            g.sig = sig_[r];
+            const Sig& s = sigs_[g.sig];
+            g.d.clause_off = s.clause_off;
+            g.d.n_clauses = s.n_clauses;
+            g.d.qkind = s.qkind;
+            g.d.var_score = s.var_score ? 1 : 0;
+            g.d.tmin = s.tmin;
+            g.d.tmax = s.tmax;
+            g.d.tparty = s.tparty;
+            g.d.rev_slot = rev ? r : kNoSlot;
+            g.d.ub_key = s.ub_key;
+            choose_source(s, g.d);
+            g.d.k = g.d.var_score ? kvar : std::min<uint32_t>(std::max<uint32_t>(g.d.src_len, 1), 128);
+            g.d.out_off = off;
+            off += g.d.k;
+            g.row_slot = r;
+            h_groups_.p[i] = g.d;
+        }
+        const int ng = (int)bg.size();
+        d_groups_.reserve(ng, false);
+        d_res_.reserve(ng, false);
+        d_out_.reserve(std::max<uint64_t>(off, 1), false);
+        d_rev_.reserve(std::max<uint64_t>(off, 1), false);
+        NKM_HIP(hipMemcpyAsync(d_groups_.p, h_groups_.p, ng * sizeof(DGroup), hipMemcpyHostToDevice, stream_));
+        NKM_HIP(hipEventRecord(ev0_, stream_));
+        NKM_HIP(launch_search(st, d_groups_.p, ng, d_out_.p, rev ? d_rev_.p : nullptr, d_res_.p, stream_));
+        NKM_HIP(hipEventRecord(ev1_, stream_));
+        h_res_.reserve(ng);
+        h_out_.reserve(std::max<uint64_t>(off, 1));
+        h_rev_.reserve(std::max<uint64_t>(off, 1));
+        NKM_HIP(hipMemcpyAsync(h_res_.p, d_res_.p, ng * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream_));
+        NKM_HIP(hipMemcpyAsync(h_out_.p, d_out_.p, off * sizeof(DHit), hipMemcpyDeviceToHost, stream_));
+        if (rev) NKM_HIP(hipMemcpyAsync(h_rev_.p, d_rev_.p, off, hipMemcpyDeviceToHost, stream_));
+        NKM_HIP(hipStreamSynchronize(stream_));
+        float ms = 0.f;
+        NKM_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
+        stats.eval_ms += ms;
+        stats.batches++;
+        for (size_t i = 0; i < bg.size(); i++) {
+            BGroup& g = bg[i];
+            const DGroupResult& res = h_res_.p[i];
+            g.hits = h_out_.p + g.d.out_off;
+            g.rev = rev ? h_rev_.p + g.d.out_off : nullptr;
+            g.n = res.count;
+            g.complete = res.complete != 0;
+            stats.pair_evals += res.scanned;
+        }
+        for (size_t i = 0; i < bg.size(); i++) {
+            BGroup& g = bg[i];
+            const uint32_t T = g.row_slot;
+            // all hits (paging through the list), filtered as :425-468
+            std::vector<uint32_t> hits, hpos;
+            uint32_t j = 0;
+            bool too_many = false;
+            for (;; j++) {
+                if (j >= g.n) {
+                    if (g.complete) break;
+                    rp.fetch_more(g);
+                    if (j >= g.n) break;
+                }
+                const uint32_t H = g.hits[j].slot;
+                if (H == T) continue;
+                if (rev && !g.rev[j]) continue;
+                if (maxc_[T] < maxc_[H] && intervals_[H] <= maxI) continue;
+                if (rp.share_session(T, H)) continue;
+                hits.push_back(H);
+                hpos.push_back(j);
+                if (hits.size() >= 63) { too_many = true; break; }
+            }
+            // combineIndexes: Go's `1 << length` is 0 / negative for length >= 63 -> no subsets
+            if (too_many) continue;
+            const size_t L = hits.size();
+            if (L > 40) continue;  // reference enumerates 2^L subsets (intractable); documented
+            const int cmin = minc_[T] - count_[T], cmax = maxc_[T] - count_[T];
+            // pairwise reverse checks among the hits (validateMatch both ways, incl. self)
+            std::vector<uint64_t> pm;
+            if (rev && L) {
+                std::vector<uint32_t> pr;
+                for (size_t a = 0; a < L; a++)
+                    for (size_t b = 0; b < L; b++) { pr.push_back(hits[a]); pr.push_back(hits[b]); }
+                d_slots_tmp_.reserve(pr.size(), false);
+                d_pair_out_.reserve(L * L, false);
+                NKM_HIP(hipMemcpyAsync(d_slots_tmp_.p, pr.data(), pr.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                       stream_));
+                NKM_HIP(launch_pairs(st, d_slots_tmp_.p, (uint32_t)(L * L), d_pair_out_.p, stream_));
+                std::vector<uint8_t> po(L * L);
+                NKM_HIP(hipMemcpyAsync(po.data(), d_pair_out_.p, L * L, hipMemcpyDeviceToHost, stream_));
+                NKM_HIP(hipStreamSynchronize(stream_));
+                pm.assign(L, 0);
+                for (size_t a = 0; a < L; a++)
+                    for (size_t b = 0; b < L; b++)
+                        if (po[a * L + b]) pm[a] |= 1ull << b;
+            }
+            const uint64_t limit = 1ull << L;
+            std::vector<uint32_t> combo;
+            for (uint64_t bits = 1; bits < limit; bits++) {
+                if (__builtin_popcountll(bits) > cmax) continue;
+                combo.clear();
+                int entry_count = 0;
+                bool over = false;
+                for (size_t el = 0; el < L; el++) {
+                    if ((bits >> el) & 1) {
+                        entry_count += count_[hits[el]];
+                        if (entry_count > cmax) { over = true; break; }
+                        combo.push_back((uint32_t)el);
+                    }
+                }
+                if (over || entry_count < cmin) continue;
+                const int hit_count = entry_count + count_[T];
+                if (hit_count > maxc_[T] || hit_count < minc_[T]) continue;
+                if (hit_count % cm_[T] != 0) continue;
+                bool reject = false;
+                for (uint32_t el : combo) {
+                    const uint32_t h = hits[el];
+                    if (hit_count > maxc_[h] || hit_count < minc_[h] || hit_count % cm_[h] != 0 ||
+                        (hit_count < maxc_[h] && intervals_[h] <= maxI)) { reject = true; break; }
+                }
+                if (reject) continue;
+                // session conflicts across the combo; mutual checks between its hits
+                bool conflict = false;
+                std::vector<uint32_t> sess_seen;
+                std::vector<uint32_t> pq;  // hits whose query is already in parsedQueries
+                for (uint32_t el : combo) {
+                    const uint32_t h = hits[el];
+                    for (uint32_t p = pres_off_[h]; p < pres_off_[h + 1] && !conflict; p++) {
+                        bool dup_in_ticket = false;
+                        for (uint32_t p2 = pres_off_[h]; p2 < p; p2++) dup_in_ticket |= pres_sess_[p2] == pres_sess_[p];
+                        if (dup_in_ticket) continue;  // SessionIDs is a set
+                        const uint32_t sid = pres_sess_[p];
+                        if (std::find(sess_seen.begin(), sess_seen.end(), sid) != sess_seen.end()) { conflict = true; break; }
+                        sess_seen.push_back(sid);
+                        if (rev) {
+                            for (uint32_t o : pq) {
+                                if (!((pm[el] >> o) & 1ull) || !((pm[o] >> el) & 1ull)) { conflict = true; break; }
+                            }
+                            if (conflict) break;
+                            if (std::find(pq.begin(), pq.end(), el) == pq.end()) pq.push_back(el);
+                        }
+                    }
+                    if (conflict) break;
+                }
+                if (conflict) continue;
+                std::vector<std::pair<uint32_t, int>> me;
+                for (uint32_t el : combo)
+                    for (int k = 0; k < count_[hits[el]]; k++) me.push_back({hits[el], k});
+                for (int k = 0; k < count_[T]; k++) me.push_back({T, k});
+                cands.push_back(std::move(me));
+            }
+        }
+    }
+    return MM_OK;
+}
+
+// Process() post-pass (matchmaker.go:320-372).
+void Core::finish_pass(const std::vector<uint32_t>& expired, std::vector<std::vector<std::pair<uint32_t, int>>>& groups) {
+    for (uint32_t s : expired) is_active_[s] = 0;
+    for (size_t i = 0; i < groups.size(); i++) {
+        bool incomplete = false;
+        for (auto& e : groups[i])
+            if (e.first == kNoSlot || !live_[e.first]) { incomplete = true; break; }
+        if (incomplete) {  // swap-remove (:337-341)
+            groups[i] = std::move(groups.back());
+            groups.pop_back();
+            i--;
+            continue;
+        }
+        for (auto& e : groups[i]) kill_slot(e.first, true);
+    }
+    size_t w = 0;
+    for (uint32_t s : active_list_)
+        if (live_[s] && is_active_[s]) active_list_[w++] = s;
+    active_list_.resize(w);
+}
+
+void Core::fill_matched(const std::vector<std::vector<std::pair<uint32_t, int>>>& groups, mm_matched* out,
+                        bool cands) {
+    size_t n = 0, bytes = 0;
+    for (auto& g : groups) {
+        n += g.size();
+        for (auto& e : g) bytes += (e.first < ticket_.size() ? ticket_[e.first].size() : 0) + 1;
+    }
+    auto* offs = new int32_t[groups.size() + 1];
+    auto* ents = new mm_entry_ref[n ? n : 1];
+    char* buf = new char[bytes ? bytes : 1];
+    size_t k = 0, b = 0;
+    offs[0] = 0;
+    for (size_t gi = 0; gi < groups.size(); gi++) {
+        for (auto& e : groups[gi]) {
+            const std::string& t = ticket_[e.first];
+            std::memcpy(buf + b, t.c_str(), t.size() + 1);
+            ents[k].ticket = buf + b;
+            ents[k].presence_index = e.second;
+            ents[k].reserved = 0;
+            b += t.size() + 1;
+            k++;
+        }
+        offs[gi + 1] = (int32_t)k;
+    }
+    out->n_groups = (int32_t)groups.size();
+    out->n_entries = (int32_t)k;
+    out->group_offsets = offs;
+    out->entries = ents;
+    out->is_candidates = cands ? 1 : 0;
+    out->reserved2 = (int64_t)(intptr_t)buf;
+}
+
+void Core::free_matched(mm_matched* out) {
+    if (!out) return;
+    delete[] out->group_offsets;
+    delete[] out->entries;
+    delete[] reinterpret_cast<char*>((intptr_t)out->reserved2);
+    std::memset(out, 0, sizeof(*out));
+}
+
+int Core::process(mm_matched* out) {
+    std::memset(out, 0, sizeof(*out));
+    const auto t0 = std::chrono::steady_clock::now();
+    std::lock_guard<std::mutex> lk(mu_);
+    if (custom_open_) return MM_ERR_STATE;
+    uint32_t n_active = 0;
+    for (uint32_t s : active_list_) n_active += live_[s] && is_active_[s];
+    std::vector<std::vector<std::pair<uint32_t, int>>> groups;
+    if (n_active == 0) {  // matchmaker.go:294-298
+        fill_matched(groups, out, false);
+        return MM_OK;
+    }
+    sync_device();
+    if (!active_sorted_) {
+        std::sort(active_list_.begin(), active_list_.end(), [&](uint32_t a, uint32_t b) {
+            if (created_[a] != created_[b]) return created_[a] < created_[b];
+            return ticket_[a] < ticket_[b];
+        });
+        active_sorted_ = true;
+    }
+    std::vector<uint32_t> expired;
+    PassStats stats;
+    if (cfg_.override_enabled) {
+        process_custom(groups, expired, stats);
+        out->n_expired = (int32_t)expired.size();
+        if (groups.empty()) {
+            std::vector<std::vector<std::pair<uint32_t, int>>> none;
+            finish_pass(expired, none);
+            fill_matched(none, out, false);
+        } else {
+            custom_open_ = true;
+            custom_expired_ = expired;
+            fill_matched(groups, out, true);
+        }
+    } else {
+        process_default(groups, expired, stats);
+        out->n_expired = (int32_t)expired.size();
+        finish_pass(expired, groups);
+        fill_matched(groups, out, false);
+    }
+    out->eval_ms = stats.eval_ms;
+    out->pair_evals = stats.pair_evals;
+    out->pass_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return MM_OK;
+}
+
+int Core::process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t n_groups, mm_matched* out) {
+    std::memset(out, 0, sizeof(*out));
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!custom_open_) return MM_ERR_STATE;
+    std::vector<std::vector<std::pair<uint32_t, int>>> groups;
+    for (int g = 0; g < n_groups; g++) {
+        std::vector<std::pair<uint32_t, int>> grp;
+        for (int k = offs[g]; k < offs[g + 1]; k++) {
+            int64_t s = slot_of_ticket(ents[k].ticket ? ents[k].ticket : "");
+            grp.push_back({s < 0 ? kNoSlot : (uint32_t)s, ents[k].presence_index});
+        }
+        groups.push_back(std::move(grp));
+    }
+    // processCustom never deletes from the index during the pass; matched
+    // tickets leave it here (their zombie documents would be filtered as
+    // "missing index" by later passes, matchmaker_process.go:432-437).
+    std::vector<uint32_t> exp = custom_expired_;
+    finish_pass(exp, groups);
+    custom_open_ = false;
+    custom_expired_.clear();
+    fill_matched(groups, out, false);
+    return MM_OK;
+}
+
+}  // namespace nkm
+
+extern "C" int32_t mm_debug_group_indexes(const int32_t* counts, const int64_t* created_at, int32_t n,
+                                          int32_t required, int32_t* group_offsets, int32_t* group_members,
+                                          int64_t* avg_created_at, int32_t cap) {
+    std::vector<int32_t> cnt(counts, counts + n);
+    std::vector<int64_t> cr(created_at, created_at + n);
+    std::vector<uint32_t> in(n);
+    for (int32_t i = 0; i < n; i++) in[i] = (uint32_t)i;
+    std::vector<nkm::IG> out;
+    nkm::group_indexes(in, 0, required, cnt, cr, out);
+    int32_t g = 0, k = 0;
+    group_offsets[0] = 0;
+    for (auto& gr : out) {
+        if (g >= cap) break;
+        for (uint32_t m : gr.idx)
+            if (k < 8 * cap) group_members[k++] = (int32_t)m;
+        avg_created_at[g] = gr.avg;
+        group_offsets[++g] = k;
+    }
+    return g;
+}
+
+extern "C" int mm_debug_compile(const char* query) {
+    nkm::CompiledQuery cq;
+    int rc = nkm::compile_query(query ? query : "", &cq);
+    return rc == nkm::CQ_OK ? MM_OK : rc == nkm::CQ_UNSUPPORTED ? MM_ERR_UNSUPPORTED : MM_ERR_QUERY_INVALID;
+}
+
+namespace nkm {
+
+int32_t Core::debug_hits(const std::string& ticket, const char** tk, double* sc, int32_t cap) {
+    std::lock_guard<std::mutex> lk(mu_);
+    int64_t T = slot_of_ticket(ticket);
+    if (T < 0) return -1;
+    sync_device();
+    const DStore st = dstore();
+    PassStats stats;
+    std::vector<uint8_t> sel(ticket_.size(), 0);
+    Replay rp(*this, sel, cfg_.rev_precision != 0, cfg_.max_intervals, stats, st, stream_);
+    BGroup g;
+    const Sig& s = sigs_[sig_[T]];
+    g.d.clause_off = s.clause_off;
+    g.d.n_clauses = s.n_clauses;
+    g.d.qkind = s.qkind;
+    g.d.var_score = s.var_score ? 1 : 0;
+    g.d.tmin = s.tmin;
+    g.d.tmax = s.tmax;
+    g.d.tparty = s.tparty;
+    g.d.rev_slot = kNoSlot;
+    g.d.ub_key = s.ub_key;
+    while (order_head_ < order_.size() && !live_[order_[order_head_]]) order_head_++;
+    choose_source(s, g.d);
+    g.d.k = 1;
+    g.n = 0;
+    g.complete = false;
+    while (!g.complete) rp.fetch_more(g);
+    debug_strings_.clear();
+    int32_t n = 0;
+    for (uint32_t i = 0; i < g.n; i++) {
+        if (g.hits[i].slot == (uint32_t)T) continue;
+        debug_strings_.push_back(ticket_[g.hits[i].slot]);
+    }
+    for (uint32_t i = 0; i < g.n; i++) {
+        if (g.hits[i].slot == (uint32_t)T) continue;
+        if (n < cap) {
+            if (tk) tk[n] = debug_strings_[n].c_str();
+            int64_t key = g.hits[i].key;
+            if (key < 0) key ^= INT64_MAX;
+            double d;
+            std::memcpy(&d, &key, 8);
+            if (sc) sc[n] = d;
+        }
+        n++;
+    }
+    return n;
+}
+
+}  // namespace nkm

@@ -1,0 +1,753 @@
+// nakama_amd/csrc/mm_store.cpp — ticket store: Add/Insert/Remove*/Extract,
+// compaction, and the HBM mirror (SoA columns, scan order, posting lists).
+//
+// Reference: server/matchmaker.go:443-1040 (mutators, MapMatchmakerIndex),
+// server/match_common.go:78-212 (document field mapping).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <unordered_set>
+
+#include "gocompat.h"
+#include "mm_core.h"
+
+namespace nkm {
+
+template <class T>
+void DevArray<T>::reserve(size_t n, bool keep) {
+    if (n <= cap) return;
+    size_t ncap = std::max<size_t>(n, cap ? cap + cap / 2 : 1024);
+    T* np = nullptr;
+    NKM_HIP(hipMalloc((void**)&np, ncap * sizeof(T)));
+    if (keep && p && cap) NKM_HIP(hipMemcpy(np, p, cap * sizeof(T), hipMemcpyDeviceToDevice));
+    if (p) (void)hipFree(p);
+    p = np;
+    cap = ncap;
+}
+template <class T>
+void DevArray<T>::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+}
+template <class T>
+void PinnedArray<T>::reserve(size_t n) {
+    if (n <= cap) return;
+    size_t ncap = std::max<size_t>(n, cap ? cap * 2 : 1024);
+    T* np = nullptr;
+    NKM_HIP(hipHostMalloc((void**)&np, ncap * sizeof(T), hipHostMallocDefault));
+    if (p) (void)hipHostFree(p);
+    p = np;
+    cap = ncap;
+}
+template <class T>
+void PinnedArray<T>::release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+}
+
+template struct DevArray<uint8_t>;
+template struct DevArray<int32_t>;
+template struct DevArray<uint32_t>;
+template struct DevArray<int64_t>;
+template struct DevArray<DQuery>;
+template struct DevArray<DClause>;
+template struct DevArray<DGroup>;
+template struct DevArray<DHit>;
+template struct DevArray<DGroupResult>;
+template struct DevArray<int64_t*>;
+template struct DevArray<uint8_t*>;
+template struct PinnedArray<DGroup>;
+template struct PinnedArray<DHit>;
+template struct PinnedArray<uint8_t>;
+template struct PinnedArray<DGroupResult>;
+template struct PinnedArray<uint32_t>;
+
+static const char* kBuiltinNames[F_NBUILTIN] = {"ticket", "min_count", "max_count", "party_id", "created_at"};
+
+Core::Core(const mm_config& cfg) : cfg_(cfg) {
+    node_ = cfg.node ? cfg.node : "";
+    cfg_.node = nullptr;
+    device_ = cfg.device;
+    int ndev = 0;
+    NKM_HIP(hipGetDeviceCount(&ndev));
+    if (ndev <= 0 || device_ < 0 || device_ >= ndev) throw DeviceError{hipErrorNoDevice, "device ordinal", __LINE__};
+    NKM_HIP(hipSetDevice(device_));
+    NKM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    NKM_HIP(hipEventCreate(&ev0_));
+    NKM_HIP(hipEventCreate(&ev1_));
+    for (int f = 0; f < F_NBUILTIN; f++) field_dict_.intern(kBuiltinNames[f]);
+    fval_.resize(F_NBUILTIN);
+    fkind_.resize(F_NBUILTIN);
+    field_used_.assign(F_NBUILTIN, 0);
+    field_posting_.assign(F_NBUILTIN, 0);
+    d_fval_.assign(F_NBUILTIN, nullptr);
+    d_fkind_.assign(F_NBUILTIN, nullptr);
+    dev_field_slots_.assign(F_NBUILTIN, 0);
+}
+
+Core::~Core() {
+    (void)hipSetDevice(device_);
+    for (auto* p : d_fval_) delete p;
+    for (auto* p : d_fkind_) delete p;
+    if (ev0_) (void)hipEventDestroy(ev0_);
+    if (ev1_) (void)hipEventDestroy(ev1_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+uint16_t Core::field_of(const std::string& name) {
+    int64_t f = field_dict_.find(name);
+    if (f >= 0) return (uint16_t)f;
+    if (field_dict_.str.size() >= 65535) throw DeviceError{hipErrorOutOfMemory, "too many fields", __LINE__};
+    uint16_t id = (uint16_t)field_dict_.intern(name);
+    fval_.emplace_back();
+    fkind_.emplace_back();
+    field_used_.push_back(0);
+    field_posting_.push_back(0);
+    d_fval_.push_back(nullptr);
+    d_fkind_.push_back(nullptr);
+    dev_field_slots_.push_back(0);
+    return id;
+}
+
+int64_t Core::slot_of_ticket(const std::string& t) const {
+    auto it = slot_of_.find(t);
+    if (it == slot_of_.end() || !live_[it->second]) return -1;
+    return it->second;
+}
+
+// Value of field f for slot s, computed from the host record (used to build a
+// dense column the first time a query references the field).
+static void field_value(const Core& c, uint16_t f, uint32_t s, const std::vector<std::pair<uint16_t, std::pair<uint8_t, int64_t>>>& props,
+                        uint8_t* kind, int64_t* val) {
+    (void)c;
+    *kind = KIND_ABSENT;
+    *val = 0;
+    for (auto& p : props)
+        if (p.first == f) { *kind = p.second.first; *val = p.second.second; }
+    (void)s;
+}
+
+// Builds the property part of the bluge document of a ticket
+// (blugeProcessProperty, match_common.go:148-212): string props become keyword
+// terms unless they parse as a datetime (then the raw UnixNano numeric term);
+// numeric props the sortable int64 of the float64; numeric wins on key clash
+// (matchmaker.go:460-466).
+static void doc_props(Core& c, const Cold& cold, std::vector<std::pair<uint16_t, std::pair<uint8_t, int64_t>>>& out,
+                      uint16_t (Core::*field_of_fn)(const std::string&)) {
+    out.clear();
+    std::unordered_map<std::string, std::pair<uint8_t, int64_t>> merged;
+    std::vector<std::string> keys;
+    for (auto& kv : cold.sprops) {
+        int64_t ns;
+        std::pair<uint8_t, int64_t> v;
+        if (bluge_datetime(kv.second, &ns)) v = {KIND_NUMERIC, ns};
+        else v = {KIND_KEYWORD, (int64_t)c.dict_.intern(kv.second)};
+        if (!merged.count(kv.first)) keys.push_back(kv.first);
+        merged[kv.first] = v;
+    }
+    for (auto& kv : cold.nprops) {
+        if (!merged.count(kv.first)) keys.push_back(kv.first);
+        merged[kv.first] = {KIND_NUMERIC, sortable_i64(kv.second)};
+    }
+    for (auto& k : keys) out.push_back({(c.*field_of_fn)("properties." + k), merged[k]});
+}
+
+void Core::set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val) {
+    fkind_[f][slot] = kind;
+    fval_[f][slot] = val;
+}
+
+// Assigns (or reuses) the compiled signature of a ticket's search.
+uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party) {
+    std::vector<DClause> dc;
+    dc.reserve(cq.clauses.size());
+    for (auto& c : cq.clauses) {
+        DClause d{};
+        d.op = c.op;
+        d.occur = c.occur;
+        d.lo = c.lo;
+        d.hi = c.hi;
+        d.score = c.score;
+        d.field = 0;
+        d.term = 0;
+        if (c.op != OP_FALSE) {
+            d.field = field_of(c.field);
+            if (c.op == OP_TERM || c.op == OP_NUMLIT) d.term = dict_.intern(c.term);
+        }
+        dc.push_back(d);
+    }
+    std::string key;
+    key.reserve(16 + dc.size() * sizeof(DClause));
+    key.push_back((char)cq.kind);
+    key.append((const char*)&mn, 4);
+    key.append((const char*)&mx, 4);
+    key.append((const char*)&party, 4);
+    if (!dc.empty()) key.append((const char*)dc.data(), dc.size() * sizeof(DClause));
+    auto it = sig_index_.find(key);
+    if (it != sig_index_.end()) return it->second;
+
+    Sig s;
+    s.clause_off = (uint32_t)clauses_.size();
+    s.n_clauses = (uint16_t)dc.size();
+    s.qkind = cq.kind;
+    s.tmin = mn;
+    s.tmax = mx;
+    s.tparty = party;
+    bool has_must = false, has_should = false, any_pos = false;
+    int n_should_live = 0;
+    double ms = 0.0, ss = 0.0, best_neg = -HUGE_VAL;
+    for (auto& d : dc) {
+        if (d.occur == OCC_MUST) {
+            has_must = true;
+            ms += d.score;
+            if (d.op == OP_TERM) s.must_terms.push_back({d.field, d.term});
+        } else if (d.occur == OCC_SHOULD) {
+            has_should = true;
+            if (d.op != OP_FALSE) {
+                n_should_live++;
+                if (d.score > 0) { ss += d.score; any_pos = true; }
+                else best_neg = std::max(best_neg, d.score);
+            }
+        }
+        if (d.op != OP_FALSE) {
+            field_used_[d.field] = 1;
+        }
+    }
+    for (auto& mt : s.must_terms) {
+        if (!field_posting_[mt.first]) { field_posting_[mt.first] = 1; index_dirty_ = true; }
+    }
+    s.var_score = cq.kind == QK_BOOL && !(n_should_live == 0 || (!has_must && n_should_live == 1));
+    double S;
+    if (cq.kind != QK_BOOL) S = 1.0;
+    else if (!has_must && !has_should) S = 1.0;
+    else if (!has_must) S = any_pos ? ss : best_neg;
+    else S = any_pos ? ms + ss : ms;
+    double ub = (S + 1.0) + 1.0;
+    s.ub_key = std::isfinite(ub) ? sortable_i64(ub) : INT64_MAX;
+    if (!std::isfinite(ms) || !std::isfinite(ss)) s.ub_key = INT64_MAX;
+    for (auto& d : dc) clauses_.push_back(d);
+    uint32_t id = (uint32_t)sigs_.size();
+    sigs_.push_back(std::move(s));
+    sig_index_.emplace(std::move(key), id);
+    // fields referenced for the first time get a dense host column now
+    for (size_t f = 0; f < field_used_.size(); f++) {
+        if (field_used_[f] && fval_[f].size() != ticket_.size()) {
+            fval_[f].assign(ticket_.size(), 0);
+            fkind_[f].assign(ticket_.size(), KIND_ABSENT);
+            for (uint32_t sl = 0; sl < ticket_.size(); sl++) {
+                if (f < F_NBUILTIN) {
+                    switch (f) {
+                    case F_TICKET: set_field((uint16_t)f, sl, KIND_KEYWORD, dict_.intern(ticket_[sl])); break;
+                    case F_MIN: set_field((uint16_t)f, sl, KIND_NUMERIC, sortable_i64((double)minc_[sl])); break;
+                    case F_MAX: set_field((uint16_t)f, sl, KIND_NUMERIC, sortable_i64((double)maxc_[sl])); break;
+                    case F_PARTY:
+                        set_field((uint16_t)f, sl, KIND_KEYWORD, dict_.intern(cold_[sl].party_id));
+                        break;
+                    case F_CREATED: set_field((uint16_t)f, sl, KIND_NUMERIC, ckey_[sl]); break;
+                    }
+                } else {
+                    std::vector<std::pair<uint16_t, std::pair<uint8_t, int64_t>>> props;
+                    doc_props(*this, cold_[sl], props, &Core::field_of);
+                    uint8_t k;
+                    int64_t v;
+                    field_value(*this, (uint16_t)f, sl, props, &k, &v);
+                    set_field((uint16_t)f, sl, k, v);
+                }
+            }
+            dev_field_slots_[f] = 0;
+        }
+    }
+    return id;
+}
+
+void Core::kill_slot(uint32_t s, bool device_cleared) {
+    if (!live_[s]) return;
+    live_[s] = 0;
+    is_active_[s] = 0;
+    n_live_--;
+    if (!device_cleared) pending_dead_.push_back(s);
+    uint32_t p0 = pres_off_[s], p1 = pres_off_[s + 1];
+    // sessionTickets bookkeeping (a ticket counts once per distinct session)
+    for (uint32_t p = p0; p < p1; p++) {
+        bool dup = false;
+        for (uint32_t q = p0; q < p; q++) dup |= pres_sess_[q] == pres_sess_[p];
+        if (!dup) sess_slots_.erase(pres_sess_[p], s);
+    }
+    if (party_[s] != kNoParty) party_slots_.erase(party_[s], s);
+}
+
+int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_insert) {
+    const std::string tk = t.ticket ? t.ticket : "";
+    int64_t existing = slot_of_ticket(tk);
+    if (existing >= 0) kill_slot((uint32_t)existing);  // same ticket id re-inserted: replace
+    const uint32_t s = (uint32_t)ticket_.size();
+    Cold cold;
+    cold.session_id = t.session_id ? t.session_id : "";
+    cold.party_id = t.party_id ? t.party_id : "";
+    cold.query = t.query ? t.query : "";
+    cold.node = from_insert ? (t.node ? t.node : "") : node_;
+    for (int i = 0; i < t.n_str_props; i++) cold.sprops.push_back({t.str_props[i].key, t.str_props[i].value});
+    for (int i = 0; i < t.n_num_props; i++) cold.nprops.push_back({t.num_props[i].key, t.num_props[i].value});
+    for (int i = 0; i < t.n_presences; i++) {
+        const mm_presence& p = t.presences[i];
+        cold.presences.push_back({p.user_id ? p.user_id : "", p.session_id ? p.session_id : "",
+                                  p.username ? p.username : "", p.node ? p.node : ""});
+    }
+    ticket_.push_back(tk);
+    created_.push_back(t.created_at);
+    ckey_.push_back(sortable_i64((double)t.created_at));
+    minc_.push_back(t.min_count);
+    maxc_.push_back(t.max_count);
+    cm_.push_back(t.count_multiple);
+    count_.push_back(t.n_presences);
+    intervals_.push_back(from_insert ? t.intervals : 0);
+    uint32_t party = cold.party_id.empty() ? kNoParty : dict_.intern(cold.party_id);
+    party_.push_back(party);
+    live_.push_back(1);
+    bool act = from_insert ? (t.intervals < cfg_.max_intervals) : true;
+    is_active_.push_back(act ? 1 : 0);
+    if (pres_off_.empty()) pres_off_.push_back(0);
+    for (auto& p : cold.presences) pres_sess_.push_back(sess_dict_.intern(p.session_id));
+    pres_off_.push_back((uint32_t)pres_sess_.size());
+    {
+        uint32_t p0 = pres_off_[s], p1 = pres_off_[s + 1];
+        for (uint32_t p = p0; p < p1; p++) {
+            bool dup = false;
+            for (uint32_t q = p0; q < p; q++) dup |= pres_sess_[q] == pres_sess_[p];
+            if (!dup) sess_slots_.add(pres_sess_[p], s);
+        }
+    }
+    if (party != kNoParty) party_slots_.add(party, s);
+    // dense columns of referenced fields
+    for (size_t f = 0; f < fval_.size(); f++) {
+        if (!fval_[f].empty() || field_used_[f]) {
+            fval_[f].push_back(0);
+            fkind_[f].push_back(KIND_ABSENT);
+        }
+    }
+    cold_.push_back(std::move(cold));
+    const Cold& c = cold_.back();
+    if (field_used_[F_TICKET]) set_field(F_TICKET, s, KIND_KEYWORD, dict_.intern(tk));
+    if (field_used_[F_MIN]) set_field(F_MIN, s, KIND_NUMERIC, sortable_i64((double)t.min_count));
+    if (field_used_[F_MAX]) set_field(F_MAX, s, KIND_NUMERIC, sortable_i64((double)t.max_count));
+    if (field_used_[F_PARTY]) set_field(F_PARTY, s, KIND_KEYWORD, dict_.intern(c.party_id));
+    if (field_used_[F_CREATED]) set_field(F_CREATED, s, KIND_NUMERIC, ckey_[s]);
+    std::vector<std::pair<uint16_t, std::pair<uint8_t, int64_t>>> props;
+    doc_props(*this, c, props, &Core::field_of);
+    for (auto& p : props) {
+        if (p.first < fval_.size() && fval_[p.first].size() == ticket_.size()) set_field(p.first, s, p.second.first, p.second.second);
+    }
+    sig_.push_back(0);
+    squery_.push_back(DQuery{});
+    uint32_t sg = sig_of(cq, t.min_count, t.max_count, party);  // may materialise new columns (incl. this slot)
+    sig_[s] = sg;
+    squery_[s] = DQuery{sigs_[sg].clause_off, sigs_[sg].n_clauses, sigs_[sg].qkind, 0};
+    slot_of_[tk] = s;
+    n_live_++;
+    if (act) {
+        if (!active_list_.empty()) {
+            uint32_t l = active_list_.back();
+            if (created_[l] > t.created_at || (created_[l] == t.created_at && ticket_[l] > tk)) active_sorted_ = false;
+        }
+        active_list_.push_back(s);
+    }
+    if (!order_.empty()) {
+        uint32_t l = order_.back();
+        if (ckey_[l] > ckey_[s]) order_sorted_ = false;
+    }
+    order_.push_back(s);
+    index_dirty_ = true;
+    return MM_OK;
+}
+
+static int status_of(int cq) { return cq == CQ_UNSUPPORTED ? MM_ERR_UNSUPPORTED : MM_ERR_QUERY_INVALID; }
+
+// Add (matchmaker.go:443-565).
+int Core::add(const mm_ticket& t) {
+    if (stopped_) return MM_ERR_NOT_AVAILABLE;
+    CompiledQuery cq;
+    int rc = compile_query(t.query ? t.query : "", &cq);
+    if (rc != CQ_OK) { last_error_ = "query"; return status_of(rc); }
+    {
+        std::unordered_set<std::string> seen;
+        for (int i = 0; i < t.n_presences; i++) {
+            std::string s = t.presences[i].session_id ? t.presences[i].session_id : "";
+            if (!seen.insert(s).second) return MM_ERR_DUPLICATE_SESSION;
+        }
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    if (custom_open_) return MM_ERR_STATE;
+    for (int i = 0; i < t.n_presences; i++) {
+        int64_t sid = sess_dict_.find(t.presences[i].session_id ? t.presences[i].session_id : "");
+        if (sid >= 0 && (int)sess_slots_.count((uint32_t)sid) >= cfg_.max_tickets) return MM_ERR_TOO_MANY_TICKETS;
+    }
+    std::string party = t.party_id ? t.party_id : "";
+    if (!party.empty()) {
+        int64_t pid = dict_.find(party);
+        if (pid >= 0 && (int)party_slots_.count((uint32_t)pid) >= cfg_.max_tickets) return MM_ERR_TOO_MANY_TICKETS;
+    }
+    maybe_compact();
+    return add_locked(t, cq, false);
+}
+
+// Insert (matchmaker.go:567-682): queries that fail to parse are skipped.
+int Core::insert(const mm_ticket* ts, int32_t n) {
+    if (stopped_ || n <= 0) return MM_OK;
+    std::vector<CompiledQuery> cqs((size_t)n);
+    std::vector<uint8_t> ok((size_t)n, 0);
+    for (int i = 0; i < n; i++) ok[i] = compile_query(ts[i].query ? ts[i].query : "", &cqs[i]) == CQ_OK;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (custom_open_) return MM_ERR_STATE;
+    maybe_compact();
+    for (int i = 0; i < n; i++)
+        if (ok[i]) add_locked(ts[i], cqs[i], true);
+    if (n >= 1024) sync_device();  // index the batch now (bluge indexes synchronously too)
+    return MM_OK;
+}
+
+int Core::extract(mm_extract_list* out) {
+    out->n = 0;
+    out->tickets = nullptr;
+    if (stopped_) return MM_OK;
+    std::lock_guard<std::mutex> lk(mu_);
+    std::vector<uint32_t> v;
+    for (uint32_t s = 0; s < ticket_.size(); s++)
+        if (live_[s] && cold_[s].node == node_) v.push_back(s);
+    auto* arr = new mm_ticket[v.empty() ? 1 : v.size()];
+    for (size_t i = 0; i < v.size(); i++) {
+        uint32_t s = v[i];
+        const Cold& c = cold_[s];
+        mm_ticket& t = arr[i];
+        t.ticket = ticket_[s].c_str();
+        t.session_id = c.session_id.c_str();
+        t.party_id = c.party_id.c_str();
+        t.query = c.query.c_str();
+        t.min_count = minc_[s];
+        t.max_count = maxc_[s];
+        t.count_multiple = cm_[s];
+        t.intervals = intervals_[s];
+        t.created_at = created_[s];
+        t.node = c.node.c_str();
+        auto* ps = new mm_presence[c.presences.empty() ? 1 : c.presences.size()];
+        for (size_t k = 0; k < c.presences.size(); k++)
+            ps[k] = {c.presences[k].user_id.c_str(), c.presences[k].session_id.c_str(),
+                     c.presences[k].username.c_str(), c.presences[k].node.c_str()};
+        t.presences = ps;
+        t.n_presences = (int32_t)c.presences.size();
+        auto* sp = new mm_str_prop[c.sprops.empty() ? 1 : c.sprops.size()];
+        for (size_t k = 0; k < c.sprops.size(); k++) sp[k] = {c.sprops[k].first.c_str(), c.sprops[k].second.c_str()};
+        t.str_props = sp;
+        t.n_str_props = (int32_t)c.sprops.size();
+        auto* np = new mm_num_prop[c.nprops.empty() ? 1 : c.nprops.size()];
+        for (size_t k = 0; k < c.nprops.size(); k++) np[k] = {c.nprops[k].first.c_str(), c.nprops[k].second};
+        t.num_props = np;
+        t.n_num_props = (int32_t)c.nprops.size();
+    }
+    out->n = (int32_t)v.size();
+    out->tickets = arr;
+    return MM_OK;
+}
+
+void Core::free_extract(mm_extract_list* out) {
+    if (!out || !out->tickets) return;
+    for (int i = 0; i < out->n; i++) {
+        delete[] out->tickets[i].presences;
+        delete[] out->tickets[i].str_props;
+        delete[] out->tickets[i].num_props;
+    }
+    delete[] out->tickets;
+    out->tickets = nullptr;
+    out->n = 0;
+}
+
+// RemoveSession (matchmaker.go:725-767)
+int Core::remove_session(const std::string& sid, const std::string& ticket) {
+    std::lock_guard<std::mutex> lk(mu_);
+    int64_t s = slot_of_ticket(ticket);
+    if (s < 0 || !cold_[s].party_id.empty() || cold_[s].session_id != sid) return MM_ERR_TICKET_NOT_FOUND;
+    kill_slot((uint32_t)s);
+    return MM_OK;
+}
+
+// RemoveSessionAll (matchmaker.go:769-828)
+int Core::remove_session_all(const std::string& sid) {
+    std::lock_guard<std::mutex> lk(mu_);
+    int64_t id = sess_dict_.find(sid);
+    if (id < 0) return MM_OK;
+    for (uint32_t s : sess_slots_.list((uint32_t)id)) kill_slot(s);
+    return MM_OK;
+}
+
+// RemoveParty (matchmaker.go:830-870)
+int Core::remove_party(const std::string& pid, const std::string& ticket) {
+    std::lock_guard<std::mutex> lk(mu_);
+    int64_t s = slot_of_ticket(ticket);
+    if (s < 0 || !cold_[s].session_id.empty() || cold_[s].party_id != pid) return MM_ERR_TICKET_NOT_FOUND;
+    kill_slot((uint32_t)s);
+    return MM_OK;
+}
+
+// RemovePartyAll (matchmaker.go:872-917)
+int Core::remove_party_all(const std::string& pid) {
+    std::lock_guard<std::mutex> lk(mu_);
+    int64_t id = dict_.find(pid);
+    if (id < 0 || pid.empty()) return MM_OK;
+    for (uint32_t s : party_slots_.list((uint32_t)id)) kill_slot(s);
+    return MM_OK;
+}
+
+// RemoveAll (matchmaker.go:919-970)
+int Core::remove_all(const std::string& node) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (uint32_t s = 0; s < ticket_.size(); s++)
+        if (live_[s] && cold_[s].node == node) kill_slot(s);
+    return MM_OK;
+}
+
+// Remove (matchmaker.go:972-1024)
+int Core::remove(const char* const* tickets, int32_t n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int i = 0; i < n; i++) {
+        int64_t s = slot_of_ticket(tickets[i] ? tickets[i] : "");
+        if (s >= 0) kill_slot((uint32_t)s);
+    }
+    return MM_OK;
+}
+
+int32_t Core::ticket_count() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return (int32_t)n_live_;
+}
+int32_t Core::active_count() {
+    std::lock_guard<std::mutex> lk(mu_);
+    int32_t n = 0;
+    for (uint32_t s : active_list_) n += is_active_[s] && live_[s];
+    return n;
+}
+
+void Core::maybe_compact() {
+    size_t n = ticket_.size();
+    if (n >= 65536 && n > 2 * (size_t)n_live_) compact();
+}
+
+// Drops dead slots and renumbers the store (preserves relative slot order, so
+// the scan order stays sorted and insertion-order tie-breaks are unchanged).
+void Core::compact() {
+    const size_t n = ticket_.size();
+    std::vector<uint32_t> remap(n, kNoSlot);
+    uint32_t m = 0;
+    for (uint32_t s = 0; s < n; s++)
+        if (live_[s]) remap[s] = m++;
+    auto keep = [&](auto& vec) {
+        size_t w = 0;
+        for (uint32_t s = 0; s < n; s++)
+            if (live_[s]) vec[w++] = std::move(vec[s]);
+        vec.resize(w);
+    };
+    // presences CSR and sessions (the session dictionary is rebuilt so it
+    // holds live sessions only)
+    std::vector<uint32_t> npoff{0};
+    std::vector<uint32_t> npsess;
+    Dict nsess;
+    for (uint32_t s = 0; s < n; s++) {
+        if (!live_[s]) continue;
+        for (uint32_t p = pres_off_[s]; p < pres_off_[s + 1]; p++)
+            npsess.push_back(nsess.intern(sess_dict_.str[pres_sess_[p]]));
+        npoff.push_back((uint32_t)npsess.size());
+    }
+    pres_off_ = std::move(npoff);
+    pres_sess_ = std::move(npsess);
+    sess_dict_ = std::move(nsess);
+    keep(ticket_); keep(created_); keep(ckey_); keep(minc_); keep(maxc_); keep(cm_); keep(count_);
+    keep(intervals_); keep(party_); keep(is_active_); keep(sig_); keep(cold_); keep(squery_);
+    for (size_t f = 0; f < fval_.size(); f++) {
+        if (fval_[f].size() == n) { keep(fval_[f]); keep(fkind_[f]); }
+    }
+    live_.assign(m, 1);
+    // maps
+    slot_of_.clear();
+    for (uint32_t s = 0; s < m; s++) slot_of_[ticket_[s]] = s;
+    sess_slots_.clear();
+    party_slots_.clear();
+    for (uint32_t s = 0; s < m; s++) {
+        uint32_t p0 = pres_off_[s], p1 = pres_off_[s + 1];
+        for (uint32_t p = p0; p < p1; p++) {
+            bool dup = false;
+            for (uint32_t q = p0; q < p; q++) dup |= pres_sess_[q] == pres_sess_[p];
+            if (!dup) sess_slots_.add(pres_sess_[p], s);
+        }
+        if (party_[s] != kNoParty) party_slots_.add(party_[s], s);
+    }
+    std::vector<uint32_t> nact;
+    for (uint32_t s : active_list_)
+        if (remap[s] != kNoSlot && is_active_[remap[s]]) nact.push_back(remap[s]);
+    active_list_ = std::move(nact);
+    std::vector<uint32_t> nord;
+    for (uint32_t s : order_)
+        if (remap[s] != kNoSlot) nord.push_back(remap[s]);
+    order_ = std::move(nord);
+    pending_dead_.clear();
+    index_dirty_ = true;
+    dev_slots_ = 0;
+    for (auto& d : dev_field_slots_) d = 0;
+    n_live_ = m;
+}
+
+// ---------------------------------------------------------------------------
+// HBM mirror
+// ---------------------------------------------------------------------------
+void Core::ensure_field_on_device(uint16_t f) {
+    if (!d_fval_[f]) {
+        d_fval_[f] = new DevArray<int64_t>();
+        d_fkind_[f] = new DevArray<uint8_t>();
+        dev_field_slots_[f] = 0;
+    }
+}
+
+void Core::build_index() {
+    const uint32_t n = (uint32_t)ticket_.size();
+    // scan order: slots sorted by (sortable float64(CreatedAt), slot)
+    if (!order_sorted_ || order_.size() != n) {
+        order_.resize(n);
+        for (uint32_t s = 0; s < n; s++) order_[s] = s;
+        std::stable_sort(order_.begin(), order_.end(), [&](uint32_t a, uint32_t b) { return ckey_[a] < ckey_[b]; });
+        order_sorted_ = true;
+    }
+    // posting lists for fields used as required-term sources
+    postings_map_.clear();
+    postings_.clear();
+    std::vector<uint16_t> pf;
+    for (size_t f = 0; f < field_posting_.size(); f++)
+        if (field_posting_[f]) pf.push_back((uint16_t)f);
+    if (!pf.empty()) {
+        for (uint32_t s : order_) {
+            if (!live_[s]) continue;
+            for (uint16_t f : pf) {
+                if (fkind_[f][s] != KIND_KEYWORD) continue;
+                uint64_t key = ((uint64_t)f << 32) | (uint64_t)(uint32_t)fval_[f][s];
+                postings_map_[key].len++;
+            }
+        }
+        uint32_t off = 0;
+        for (auto& kv : postings_map_) { kv.second.off = off; off += kv.second.len; kv.second.head = 0; }
+        postings_.resize(off);
+        for (auto& kv : postings_map_) kv.second.head = kv.second.off;
+        for (uint32_t s : order_) {
+            if (!live_[s]) continue;
+            for (uint16_t f : pf) {
+                if (fkind_[f][s] != KIND_KEYWORD) continue;
+                uint64_t key = ((uint64_t)f << 32) | (uint64_t)(uint32_t)fval_[f][s];
+                auto& r = postings_map_[key];
+                postings_[r.head++] = s;
+            }
+        }
+        for (auto& kv : postings_map_) kv.second.head = 0;
+    }
+    order_head_ = 0;
+    d_order_.reserve(std::max<size_t>(n, 1), false);
+    if (n) NKM_HIP(hipMemcpyAsync(d_order_.p, order_.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, stream_));
+    d_postings_.reserve(std::max<size_t>(postings_.size(), 1), false);
+    if (!postings_.empty())
+        NKM_HIP(hipMemcpyAsync(d_postings_.p, postings_.data(), postings_.size() * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, stream_));
+    index_dirty_ = false;
+}
+
+void Core::sync_device() {
+    NKM_HIP(hipSetDevice(device_));
+    const size_t n = ticket_.size();
+    const size_t need = std::max<size_t>(n, 1);
+    bool regrow = need > dev_cap_;
+    if (regrow) {
+        size_t cap = std::max(need, dev_cap_ + dev_cap_ / 2);
+        d_alive_.reserve(cap);
+        d_minc_.reserve(cap);
+        d_maxc_.reserve(cap);
+        d_party_.reserve(cap);
+        d_squery_.reserve(cap);
+        dev_cap_ = cap;
+    }
+    auto up = [&](auto* dst, const auto* src, size_t from, size_t to) {
+        if (to > from)
+            NKM_HIP(hipMemcpyAsync(dst + from, src + from, (to - from) * sizeof(*src), hipMemcpyHostToDevice, stream_));
+    };
+    if (dev_slots_ < n) {
+        up(d_alive_.p, live_.data(), dev_slots_, n);
+        up(d_minc_.p, minc_.data(), dev_slots_, n);
+        up(d_maxc_.p, maxc_.data(), dev_slots_, n);
+        up(d_party_.p, party_.data(), dev_slots_, n);
+        up(d_squery_.p, squery_.data(), dev_slots_, n);
+    }
+    // dead slots that were already on the device
+    if (!pending_dead_.empty()) {
+        std::vector<uint32_t> v;
+        for (uint32_t s : pending_dead_)
+            if (s < dev_slots_) v.push_back(s);
+        if (!v.empty()) apply_selected_to_device(v);
+        pending_dead_.clear();
+    }
+    dev_slots_ = n;
+    if (clauses_.size() > dev_clauses_ || !d_clauses_.p) {
+        d_clauses_.reserve(std::max<size_t>(clauses_.size(), 1));
+        up(d_clauses_.p, clauses_.data(), dev_clauses_, clauses_.size());
+        dev_clauses_ = clauses_.size();
+    }
+    bool ptrs_dirty = d_fval_ptrs_.cap < fval_.size();
+    for (size_t f = 0; f < fval_.size(); f++) {
+        if (!field_used_[f]) continue;
+        ensure_field_on_device((uint16_t)f);
+        if (d_fval_[f]->cap < need) {
+            d_fval_[f]->reserve(std::max(need, dev_cap_));
+            d_fkind_[f]->reserve(std::max(need, dev_cap_));
+            ptrs_dirty = true;
+        }
+        if (dev_field_slots_[f] < n) {
+            up(d_fval_[f]->p, fval_[f].data(), dev_field_slots_[f], n);
+            up(d_fkind_[f]->p, fkind_[f].data(), dev_field_slots_[f], n);
+            dev_field_slots_[f] = n;
+        }
+    }
+    if (ptrs_dirty || d_fval_ptrs_.cap < fval_.size() || true) {
+        std::vector<int64_t*> pv(std::max<size_t>(fval_.size(), 1), nullptr);
+        std::vector<uint8_t*> pk(std::max<size_t>(fval_.size(), 1), nullptr);
+        for (size_t f = 0; f < fval_.size(); f++) {
+            if (d_fval_[f]) { pv[f] = d_fval_[f]->p; pk[f] = d_fkind_[f]->p; }
+        }
+        d_fval_ptrs_.reserve(pv.size(), false);
+        d_fkind_ptrs_.reserve(pk.size(), false);
+        NKM_HIP(hipMemcpyAsync(d_fval_ptrs_.p, pv.data(), pv.size() * sizeof(int64_t*), hipMemcpyHostToDevice, stream_));
+        NKM_HIP(hipMemcpyAsync(d_fkind_ptrs_.p, pk.data(), pk.size() * sizeof(uint8_t*), hipMemcpyHostToDevice, stream_));
+    }
+    if (index_dirty_) build_index();
+    NKM_HIP(hipStreamSynchronize(stream_));
+}
+
+DStore Core::dstore() const {
+    DStore st;
+    st.alive = d_alive_.p;
+    st.minc = d_minc_.p;
+    st.maxc = d_maxc_.p;
+    st.party = d_party_.p;
+    st.squery = d_squery_.p;
+    st.clauses = d_clauses_.p;
+    st.fval = d_fval_ptrs_.p;
+    st.fkind = d_fkind_ptrs_.p;
+    st.order = d_order_.p;
+    st.postings = d_postings_.p;
+    return st;
+}
+
+void Core::apply_selected_to_device(const std::vector<uint32_t>& slots) {
+    if (slots.empty()) return;
+    h_slots_tmp_.reserve(slots.size());
+    std::memcpy(h_slots_tmp_.p, slots.data(), slots.size() * sizeof(uint32_t));
+    d_slots_tmp_.reserve(slots.size(), false);
+    NKM_HIP(hipMemcpyAsync(d_slots_tmp_.p, h_slots_tmp_.p, slots.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                           stream_));
+    NKM_HIP(launch_clear_alive(d_alive_.p, d_slots_tmp_.p, (uint32_t)slots.size(), stream_));
+    NKM_HIP(hipStreamSynchronize(stream_));
+}
+
+}  // namespace nkm

@@ -1,0 +1,69 @@
+"""Seeded synthetic ticket sets (tools/synth.cpp) for tests and bench.py.
+
+The generator returns native mm_ticket arrays that are passed unchanged to
+mm_insert of the HIP library or the CPU oracle, so both see identical inputs.
+Configs 1..5 follow BASELINE.json configs[0..4] / SURVEY.md 8(d); config 6 is
+a small mixed workload (parties, ranges, boosts, Min<Max, CountMultiple) for
+parity tests.
+"""
+import ctypes as C
+import os
+import subprocess
+
+from . import capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "tools", "libmm_synth.so")
+T0 = (1_700_000_000_000_000_000 // 1024) * 1024
+SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005, 6: 0x5EED0006}
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SO) or os.path.getmtime(SO) < os.path.getmtime(os.path.join(ROOT, "tools", "synth.cpp")):
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools")], check=True)
+        _lib = C.CDLL(SO)
+        _lib.synth_make.restype = C.c_void_p
+        _lib.synth_make.argtypes = [C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int64]
+        _lib.synth_tickets.restype = C.POINTER(capi.mm_ticket)
+        _lib.synth_tickets.argtypes = [C.c_void_p]
+        _lib.synth_count.restype = C.c_int64
+        _lib.synth_count.argtypes = [C.c_void_p]
+        _lib.synth_presences.restype = C.c_int64
+        _lib.synth_presences.argtypes = [C.c_void_p]
+        _lib.synth_free.argtypes = [C.c_void_p]
+    return _lib
+
+
+class TicketSet:
+    """Tickets [first, first+n) of a config; owns the native arrays."""
+
+    def __init__(self, config: int, n: int, first: int = 0, seed: int = None, t0: int = T0):
+        L = lib()
+        self.config = config
+        self.h = L.synth_make(config, SEEDS.get(config, 1) if seed is None else seed, first, n, t0)
+        self.n = L.synth_count(self.h)
+        self.presences = L.synth_presences(self.h)
+        self.tickets = L.synth_tickets(self.h)
+
+    def insert_into(self, mm: "capi.Matchmaker", chunk: int = 1 << 20):
+        for off in range(0, self.n, chunk):
+            cnt = min(chunk, self.n - off)
+            ptr = C.cast(C.addressof(self.tickets.contents) + off * C.sizeof(capi.mm_ticket), C.POINTER(capi.mm_ticket))
+            mm._check(mm.lib.mm_insert(mm.h, ptr, cnt))
+
+    def ticket_id(self, k: int) -> str:
+        return self.tickets[k].ticket.decode()
+
+    def close(self):
+        if self.h:
+            lib().synth_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

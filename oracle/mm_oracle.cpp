@@ -1311,6 +1311,11 @@ int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, dou
     return n;
 }
 
+int mm_debug_compile(const char* query) {
+    QP q;
+    return parse_query(query ? query : "", &q);
+}
+
 int32_t mm_debug_group_indexes(const int32_t* counts, const int64_t* created_at, int32_t n, int32_t required,
                                int32_t* group_offsets, int32_t* group_members, int64_t* avg_created_at, int32_t cap) {
     vector<IP> v;

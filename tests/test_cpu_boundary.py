@@ -1,0 +1,106 @@
+"""CPU-side checks of the drop-in boundary (no GPU needed).
+
+* the HIP library loads and exports every entry point include/nakama_mm.h
+  declares (and the oracle exports the same set);
+* the product's query compiler accepts/rejects exactly what the reference
+  parser does (the oracle's restatement of query_string, pinned by the
+  known-answer fixtures), over the fixture cases and a seeded fuzz corpus;
+* the product's groupIndexes restatement reproduces TestGroupIndexes exactly.
+"""
+import os
+import random
+import re
+
+import pytest
+
+import harness
+from nakama_amd import capi
+
+HEADER = os.path.join(harness.ROOT, "include", "nakama_mm.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mm_[a-z_]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def product():
+    import __graft_entry__  # noqa: F401
+    if not os.path.exists(harness.PRODUCT_SO):
+        __graft_entry__.build()
+    return capi.load_library(harness.PRODUCT_SO)
+
+
+def test_header_symbols_exported(product):
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(product, s), f"libnakama_mm.so does not export {s}"
+        assert hasattr(harness.oracle_lib(), s), f"oracle does not export {s}"
+    assert set(syms) == set(capi.EXPORTED_SYMBOLS)
+    assert product.mm_backend_name() == b"hip-gfx950"
+    assert product.mm_abi_version() == 1
+
+
+def test_library_is_gfx950(product):
+    # the shared object embeds a gfx950 code object (clang offload bundle)
+    blob = open(harness.PRODUCT_SO, "rb").read()
+    assert b"gfx950" in blob
+
+
+def _fuzz_corpus(n=3000, seed=7):
+    rnd = random.Random(seed)
+    atoms = ["properties.a", "properties.skill", "min_count", "party_id", "a", "5", "-", "+", ":", ">", "<", "=", ">=",
+             "<=", "^2", "^", "^0.5", "^x", "~", "~2", "\"x y\"", "\"2021-01-01T00:00:00Z\"", "\\:", "\\ ", "\\x",
+             "10", "-3.5", "1.2.3", "foo", "bar*", "/re/", " ", "  ", "\t", "é", "\xff"]
+    out = []
+    for _ in range(n):
+        k = rnd.randint(1, 7)
+        out.append("".join(rnd.choice(atoms) for _ in range(k)))
+    return out
+
+
+def test_compile_status_matches_oracle(product):
+    orc = harness.oracle_lib()
+    cases = [q for q, _ in harness.load_known_answer()["query_cases"]] + _fuzz_corpus()
+    bad = []
+    for q in cases:
+        b = q.encode("utf-8", "surrogateescape")
+        a, o = product.mm_debug_compile(b), orc.mm_debug_compile(b)
+        if a != o:
+            bad.append((q, a, o))
+    assert not bad, bad[:20]
+
+
+def test_group_indexes_product(product):
+    gi = harness.load_known_answer()["group_indexes"]
+    names = [x[0] for x in gi["indexes"]]
+    got = capi.group_indexes(product, [x[1] for x in gi["indexes"]], [x[2] for x in gi["indexes"]], gi["required"])
+    assert [[[names[i] for i in idx], avg] for idx, avg in got] == [[list(g), a] for g, a in gi["expected"]]
+
+
+def test_group_indexes_random_vs_oracle(product):
+    rnd = random.Random(11)
+    for _ in range(200):
+        n = rnd.randint(0, 9)
+        counts = [rnd.randint(1, 4) for _ in range(n)]
+        created = [rnd.randint(0, 1 << 62) for _ in range(n)]  # large values exercise int64 wrap
+        req = rnd.randint(0, 6)
+        assert capi.group_indexes(product, counts, created, req) == \
+            capi.group_indexes(harness.oracle_lib(), counts, created, req)
+
+
+def test_product_fails_loudly_without_device():
+    """No CPU fallback: creating a handle without a gfx950 device raises."""
+    import nakama_amd
+    try:
+        import torch  # noqa: F401
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("GPU present")
+    with pytest.raises(capi.ErrDevice):
+        nakama_amd.LocalMatchmaker()

@@ -1,0 +1,239 @@
+"""Parity of the HIP path with the CPU oracle (needs a gfx950 GPU).
+
+Bar: bit-exact matched groups (ticket, presence index, entry order, group
+order), identical post-pass state (remaining tickets, their Intervals, the
+active set), identical hit lists (order) and scores (exact for the dyadic
+boosts used here; the tolerance in the test is 1e-6 relative, as north_star
+states) — all through the C ABI of include/nakama_mm.h.
+"""
+import math
+import os
+
+import pytest
+
+import harness
+from nakama_amd import capi, synth
+
+pytestmark = pytest.mark.gpu
+
+KA = harness.load_known_answer()
+
+
+def product_lib():
+    import nakama_amd
+    return nakama_amd.load_library()
+
+
+def pair(cfg, **kw):
+    return (capi.Matchmaker(product_lib(), **cfg, **kw), capi.Matchmaker(harness.oracle_lib(), **cfg, **kw))
+
+
+@pytest.mark.parametrize("sc", KA["scenarios"], ids=[s["name"] for s in KA["scenarios"]])
+def test_known_answer_gpu(sc):
+    results, errors, extract = harness.run_scenario(product_lib(), sc, KA["T0"], KA["created_step"])
+    for ticket, got, want in errors:
+        assert got == want
+    groups = [g for r in results for g in r]
+    a = sc["assert"]
+    sess = harness.matched_sessions(groups, sc)
+    if "matched_sessions_count" in a:
+        assert len(sess) == a["matched_sessions_count"], (sc["name"], groups)
+    for s in a.get("matched_sessions_include", []):
+        assert s in sess
+    if sc["pinned_groups"] is not None:
+        assert [[list(e) for e in g] for g in groups] == sc["pinned_groups"]
+    # and the post-pass state equals the oracle's
+    o_results, _, o_extract = harness.run_scenario(harness.oracle_lib(), sc, KA["T0"], KA["created_step"])
+    assert results == o_results
+    assert [(t.ticket, t.intervals) for t in extract] == [(t.ticket, t.intervals) for t in o_extract]
+
+
+def state(mm):
+    return [(t.ticket, t.intervals) for t in mm.Extract()], mm.active_count()
+
+
+def run_passes(config, n, passes, cfg, override=None, extra=None):
+    ts = synth.TicketSet(config, n)
+    gpu, orc = (capi.Matchmaker(product_lib(), override=override, **cfg),
+                capi.Matchmaker(harness.oracle_lib(), override=override, **cfg))
+    try:
+        ts.insert_into(gpu)
+        ts.insert_into(orc)
+        for p in range(passes):
+            g = gpu.Process()
+            o = orc.Process()
+            assert g == o, f"config {config} pass {p}: groups differ (gpu {len(g)} vs oracle {len(o)})"
+            assert state(gpu) == state(orc)
+            if extra:
+                extra(p, gpu, orc)
+        return g
+    finally:
+        gpu.close()
+        orc.close()
+        ts.close()
+
+
+def test_c1_pool_query():
+    run_passes(1, 1200, 2, dict(max_intervals=2))
+
+
+def test_c2_skill_window_boosts():
+    run_passes(2, 1500, 2, dict(max_intervals=2))
+
+
+def test_c3_parties_5v5():
+    run_passes(3, 1500, 2, dict(max_intervals=2))
+
+
+def test_c4_many_pools():
+    run_passes(4, 1500, 1, dict(max_intervals=2))
+
+
+def test_c5_rev_precision_default_path():
+    run_passes(5, 800, 2, dict(max_intervals=2, rev_precision=True))
+
+
+def first_disjoint(cands):
+    """The deterministic override of SURVEY.md 8(d) C5: keep candidates, in
+    order, that do not overlap an already kept one."""
+    used, out = set(), []
+    for g in cands:
+        ts = {t for t, _ in g}
+        if ts & used:
+            continue
+        used |= ts
+        out.append(g)
+    return out
+
+
+def test_c5_override_candidates():
+    seen = {}
+
+    def rec(tag):
+        def f(c):
+            seen[tag] = [list(x) for x in c]
+            return first_disjoint(c)
+        return f
+
+    ts = synth.TicketSet(5, 400)
+    gpu = capi.Matchmaker(product_lib(), override=rec("g"), max_intervals=2, rev_precision=True)
+    orc = capi.Matchmaker(harness.oracle_lib(), override=rec("o"), max_intervals=2, rev_precision=True)
+    try:
+        ts.insert_into(gpu)
+        ts.insert_into(orc)
+        for _ in range(2):
+            seen.clear()
+            g, o = gpu.Process(), orc.Process()
+            assert seen.get("g") == seen.get("o"), "processCustom candidate lists differ"
+            assert g == o
+            assert state(gpu) == state(orc)
+    finally:
+        gpu.close()
+        orc.close()
+        ts.close()
+
+
+def test_mixed_parties_ranges_minmax():
+    run_passes(6, 1000, 3, dict(max_intervals=3))
+
+
+def test_mixed_rev_precision():
+    run_passes(6, 600, 3, dict(max_intervals=3, rev_precision=True))
+
+
+def test_paused_pass_bumps_intervals():
+    ts = synth.TicketSet(6, 200)
+    gpu, orc = pair(dict(max_intervals=3))
+    try:
+        ts.insert_into(gpu)
+        ts.insert_into(orc)
+        gpu.Pause()
+        orc.Pause()
+        assert gpu.Process() == orc.Process() == []
+        assert state(gpu) == state(orc)
+        gpu.Resume()
+        orc.Resume()
+        assert gpu.Process() == orc.Process()
+        assert state(gpu) == state(orc)
+    finally:
+        gpu.close()
+        orc.close()
+        ts.close()
+
+
+def test_interleaved_mutations():
+    """Insert / remove / add between passes (store maintenance + compaction)."""
+    gpu, orc = pair(dict(max_intervals=2, max_tickets=3))
+    sets = []
+    try:
+        for rnd in range(4):
+            ts = synth.TicketSet(6, 300, first=rnd * 300)
+            sets.append(ts)
+            ts.insert_into(gpu)
+            ts.insert_into(orc)
+            # remove a few tickets by id
+            victims = [ts.ticket_id(k) for k in range(0, 300, 37)]
+            gpu.Remove(victims)
+            orc.Remove(victims)
+            for k in range(1, 300, 53):
+                t = ts.tickets[k]
+                if t.n_presences == 1:
+                    sid = t.presences[0].session_id.decode()
+                    gpu.RemoveSessionAll(sid)
+                    orc.RemoveSessionAll(sid)
+            assert gpu.Process() == orc.Process()
+            assert state(gpu) == state(orc)
+            assert gpu.ticket_count() == orc.ticket_count()
+    finally:
+        gpu.close()
+        orc.close()
+        for s in sets:
+            s.close()
+
+
+@pytest.mark.parametrize("config", [1, 2, 3, 5, 6])
+def test_hit_lists_and_scores(config):
+    """Per-ticket search results: same hits, same order, scores within 1e-6."""
+    ts = synth.TicketSet(config, 500)
+    gpu, orc = pair(dict(max_intervals=2))
+    try:
+        ts.insert_into(gpu)
+        ts.insert_into(orc)
+        for k in range(0, 500, 41):
+            t = ts.ticket_id(k)
+            hg, ho = gpu.debug_hits(t), orc.debug_hits(t)
+            assert [h for h, _ in hg] == [h for h, _ in ho]
+            for (_, a), (_, b) in zip(hg, ho):
+                assert math.isclose(a, b, rel_tol=1e-6)
+    finally:
+        gpu.close()
+        orc.close()
+        ts.close()
+
+
+@pytest.mark.parametrize("n", [20_000])
+def test_large_pool_properties(n):
+    """Size-independent properties at a size the oracle cannot check directly:
+    every group has MaxCount presences, a multiple of CountMultiple, shares
+    the pool key, never repeats a ticket, and every matched ticket left the pool."""
+    ts = synth.TicketSet(3, n)
+    gpu = capi.Matchmaker(product_lib(), max_intervals=2)
+    props = {}
+    for k in range(n):
+        t = ts.tickets[k]
+        props[t.ticket.decode()] = tuple(t.str_props[j].value for j in range(t.n_str_props))
+    try:
+        ts.insert_into(gpu)
+        groups = gpu.Process()
+        seen = set()
+        for g in groups:
+            assert len(g) == 10
+            tickets = {t for t, _ in g}
+            assert len({props[t] for t in tickets}) == 1
+            assert not (tickets & seen)
+            seen |= tickets
+        assert gpu.ticket_count() == n - len(seen)
+        assert len(seen) > 0.9 * n
+    finally:
+        gpu.close()
+        ts.close()

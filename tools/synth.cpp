@@ -1,0 +1,209 @@
+// tools/synth.cpp — seeded synthetic ticket sets for the five BASELINE configs
+// (SURVEY.md 8(d)).  Bench/test tooling: produces mm_ticket arrays that are
+// handed unchanged to mm_insert of either the HIP library or the CPU oracle,
+// so both see byte-identical inputs.
+//
+//   CreatedAt = T0 + 1024*i (float64-exact, distinct), ticket id = UUID text
+//   from splitmix64(seed, i), one unique session per presence, Intervals = 0.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <deque>
+#include <vector>
+
+#include "../include/nakama_mm.h"
+
+namespace {
+
+uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+struct Rng {
+    uint64_t s;
+    uint64_t next() { s = splitmix64(s); return s; }
+    double uni() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+    double normal(double mu, double sd) {
+        double u1 = uni(), u2 = uni();
+        if (u1 < 1e-300) u1 = 1e-300;
+        return mu + sd * std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+    }
+};
+
+std::string uuid_of(uint64_t seed, uint64_t i) {
+    uint64_t a = splitmix64(seed * 0x100000001B3ull + i), b = splitmix64(a ^ 0xD6E8FEB86659FD93ull);
+    char buf[40];
+    std::snprintf(buf, sizeof buf, "%08x-%04x-4%03x-%04x-%012llx", (unsigned)(a >> 32), (unsigned)((a >> 16) & 0xffff),
+                  (unsigned)(a & 0xfff), (unsigned)(0x8000 | ((b >> 48) & 0x3fff)),
+                  (unsigned long long)(b & 0xffffffffffffull));
+    return buf;
+}
+
+struct Synth {
+    std::vector<mm_ticket> t;
+    std::vector<mm_presence> pres;
+    std::vector<mm_str_prop> sp;
+    std::vector<mm_num_prop> np;
+    std::deque<std::string> strs;  // owned strings (deque: stable addresses)
+    const char* keep(const std::string& s) {
+        strs.push_back(s);
+        return strs.back().c_str();
+    }
+};
+
+const char* kModes[8] = {"ranked", "casual", "arena", "coop", "draft", "blitz", "custom", "event"};
+const char* kRegions[8] = {"eu", "na", "sa", "ap", "me", "af", "oc", "cn"};
+
+}  // namespace
+
+extern "C" {
+
+// config: 1..5 as BASELINE.json configs[0..4].  Generates tickets [first, first+n).
+void* synth_make(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0) {
+    auto* S = new Synth();
+    S->t.resize((size_t)n);
+    S->pres.reserve((size_t)n * 5);
+    S->sp.reserve((size_t)n * 3);
+    S->np.reserve((size_t)n * 2);
+    struct Tmp { size_t p0, np, s0, ns, n0, nn; };
+    std::vector<Tmp> tmp((size_t)n);
+    for (int64_t k = 0; k < n; k++) {
+        const uint64_t i = (uint64_t)(first + k);
+        Rng r{splitmix64(seed ^ (i * 0x9E3779B97F4A7C15ull))};
+        mm_ticket& t = S->t[(size_t)k];
+        std::memset(&t, 0, sizeof t);
+        const std::string id = uuid_of(seed, i);
+        t.ticket = S->keep(id);
+        t.created_at = t0 + 1024 * (int64_t)i;
+        t.node = "node1";
+        t.count_multiple = 1;
+        int party = 1;
+        std::string query;
+        Tmp& tm = tmp[(size_t)k];
+        tm.s0 = S->sp.size();
+        tm.n0 = S->np.size();
+        switch (config) {
+        case 1: {
+            const char* mode = kModes[r.next() & 1];
+            const char* region = kRegions[r.next() & 3];
+            S->sp.push_back({"mode", mode});
+            S->sp.push_back({"region", region});
+            query = "+properties.mode:ranked +properties.region:eu";
+            t.min_count = t.max_count = 2;
+            break;
+        }
+        case 2: {
+            const char* region = kRegions[r.next() & 3];
+            const int s = (int)std::lround(r.normal(1500.0, 300.0));
+            S->sp.push_back({"region", region});
+            S->np.push_back({"skill", (double)s});
+            char q[256];
+            std::snprintf(q, sizeof q,
+                          "+properties.region:%s +properties.skill:>=%d +properties.skill:<=%d "
+                          "properties.skill:>=%d^2 properties.skill:<=%d^2",
+                          region, s - 200, s + 200, s - 50, s + 50);
+            query = q;
+            t.min_count = t.max_count = 2;
+            break;
+        }
+        case 3: {
+            const double u = r.uni();
+            party = u < 0.60 ? 1 : u < 0.80 ? 2 : u < 0.90 ? 3 : u < 0.95 ? 4 : 5;
+            const char* mode = kModes[r.next() & 1];
+            const char* region = kRegions[r.next() & 3];
+            S->sp.push_back({"mode", mode});
+            S->sp.push_back({"region", region});
+            query = std::string("+properties.mode:") + mode + " +properties.region:" + region;
+            t.min_count = t.max_count = 10;
+            t.count_multiple = 5;
+            break;
+        }
+        case 4: {
+            const char* mode = kModes[r.next() & 7];
+            const char* region = kRegions[r.next() & 7];
+            S->sp.push_back({"mode", mode});
+            S->sp.push_back({"region", region});
+            query = std::string("+properties.mode:") + mode + " +properties.region:" + region;
+            t.min_count = t.max_count = 2;
+            break;
+        }
+        case 5: {
+            const int s = (int)std::lround(r.normal(1500.0, 300.0));
+            char b[32];
+            std::snprintf(b, sizeof b, "b%lld", (long long)(i / 8));
+            S->sp.push_back({"bucket", S->keep(b)});
+            S->np.push_back({"skill", (double)s});
+            char q[160];
+            std::snprintf(q, sizeof q, "+properties.bucket:%s properties.skill:>=%d^2", b, s - 100);
+            query = q;
+            t.min_count = 2;
+            t.max_count = 4;
+            break;
+        }
+        default: {  // 6: small mixed workload for parity (parties, ranges, boosts, Min<Max)
+            const double u = r.uni();
+            party = u < 0.7 ? 1 : u < 0.9 ? 2 : 3;
+            const char* mode = kModes[r.next() & 1];
+            const int s = (int)(r.next() % 50);
+            S->sp.push_back({"mode", mode});
+            S->np.push_back({"skill", (double)s});
+            char q[200];
+            const int v = (int)(r.next() % 4);
+            if (v == 0) std::snprintf(q, sizeof q, "+properties.mode:%s", mode);
+            else if (v == 1) std::snprintf(q, sizeof q, "+properties.mode:%s properties.skill:>=%d^2", mode, s);
+            else if (v == 2) std::snprintf(q, sizeof q, "properties.skill:<=%d properties.mode:%s^3", s + 10, mode);
+            else std::snprintf(q, sizeof q, "+properties.skill:>=%d -properties.mode:nope", s - 20);
+            query = q;
+            const int shape = (int)(r.next() % 3);
+            if (shape == 0) { t.min_count = 2; t.max_count = 2; }
+            else if (shape == 1) { t.min_count = 2; t.max_count = 4; }
+            else { t.min_count = 4; t.max_count = 6; t.count_multiple = 2; }
+            break;
+        }
+        }
+        t.query = S->keep(query);
+        tm.p0 = S->pres.size();
+        for (int p = 0; p < party; p++) {
+            char u[48], s[48];
+            std::snprintf(u, sizeof u, "u%llu-%d", (unsigned long long)i, p);
+            std::snprintf(s, sizeof s, "s%llu-%d", (unsigned long long)i, p);
+            const char* us = S->keep(u);
+            S->pres.push_back({us, S->keep(s), us, "node1"});
+        }
+        tm.np = (size_t)party;
+        if (party > 1) {
+            char pid[48];
+            std::snprintf(pid, sizeof pid, "party-%llu", (unsigned long long)i);
+            t.party_id = S->keep(pid);
+            t.session_id = "";
+        } else {
+            t.party_id = "";
+            t.session_id = S->pres.back().session_id;
+        }
+        tm.ns = S->sp.size() - tm.s0;
+        tm.nn = S->np.size() - tm.n0;
+    }
+    for (int64_t k = 0; k < n; k++) {  // vectors are final now: wire the pointers
+        mm_ticket& t = S->t[(size_t)k];
+        const Tmp& tm = tmp[(size_t)k];
+        t.presences = S->pres.data() + tm.p0;
+        t.n_presences = (int32_t)tm.np;
+        t.str_props = S->sp.data() + tm.s0;
+        t.n_str_props = (int32_t)tm.ns;
+        t.num_props = S->np.data() + tm.n0;
+        t.n_num_props = (int32_t)tm.nn;
+    }
+    return S;
+}
+
+const mm_ticket* synth_tickets(void* h) { return static_cast<Synth*>(h)->t.data(); }
+int64_t synth_count(void* h) { return (int64_t)static_cast<Synth*>(h)->t.size(); }
+int64_t synth_presences(void* h) { return (int64_t)static_cast<Synth*>(h)->pres.size(); }
+void synth_free(void* h) { delete static_cast<Synth*>(h); }
+
+}  // extern "C"
