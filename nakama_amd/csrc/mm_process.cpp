@@ -167,7 +167,11 @@ struct Replay {
                 if (g.complete) return 0;
                 if (!can_fetch) return -1;
                 fetch_more(g);
-                if (j >= g.n) { if (g.complete) return 0; continue; }
+                if (j >= g.n) {
+                    if (g.complete) return 0;
+                    j--;  // nothing new yet: look at position j again
+                    continue;
+                }
             }
             const uint32_t s = g.hits[j].slot;
             if (s != T && !sel[s]) return 1;
