@@ -113,7 +113,10 @@ typedef struct mm_matched {
     double pass_ms;                 /* wall time of the pass inside the library */
     double eval_ms;                 /* device query-eval time (HIP events), 0 for the oracle */
     int64_t pair_evals;             /* (row, candidate) predicate evaluations issued */
-    int64_t reserved2;
+    int64_t reserved2;              /* library-private */
+    int64_t eval_bytes;             /* algorithmic bytes of the search launches (DESIGN.md roofline) */
+    int32_t eval_launches;          /* search kernel launches in the pass */
+    int32_t n_batches;              /* replay batches */
 } mm_matched;
 
 typedef struct mm_extract_list {

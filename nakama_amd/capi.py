@@ -111,7 +111,8 @@ class mm_matched(C.Structure):
     _fields_ = [("n_groups", C.c_int32), ("n_entries", C.c_int32), ("group_offsets", C.POINTER(C.c_int32)),
                 ("entries", C.POINTER(mm_entry_ref)), ("is_candidates", C.c_int32), ("n_expired", C.c_int32),
                 ("pass_ms", C.c_double), ("eval_ms", C.c_double), ("pair_evals", C.c_int64),
-                ("reserved2", C.c_int64)]
+                ("reserved2", C.c_int64), ("eval_bytes", C.c_int64), ("eval_launches", C.c_int32),
+                ("n_batches", C.c_int32)]
 
 
 class mm_extract_list(C.Structure):
@@ -205,6 +206,9 @@ class ProcessResult:
     pass_ms: float
     eval_ms: float
     pair_evals: int
+    eval_bytes: int = 0
+    eval_launches: int = 0
+    n_batches: int = 0
 
 
 class _TicketPack:
@@ -361,7 +365,7 @@ class Matchmaker:
         self._check(self.lib.mm_process(self.h, C.byref(out)))
         try:
             res = ProcessResult(self._groups(out), bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms,
-                                out.pair_evals)
+                                out.pair_evals, out.eval_bytes, out.eval_launches, out.n_batches)
         finally:
             self.lib.mm_free_matched(self.h, C.byref(out))
         return res

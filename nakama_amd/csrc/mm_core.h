@@ -99,6 +99,7 @@ struct Sig {
     int32_t tmin = 0, tmax = 0;
     uint32_t tparty = kNoParty;
     int64_t ub_key = INT64_MAX;
+    uint16_t n_fields = 0;  // distinct field columns the clauses read
     std::vector<std::pair<uint16_t, uint32_t>> must_terms;  // candidate posting lists
 };
 
@@ -155,9 +156,24 @@ enum BuiltinField : uint16_t { F_TICKET = 0, F_MIN = 1, F_MAX = 2, F_PARTY = 3, 
 struct PassStats {
     double eval_ms = 0;
     int64_t pair_evals = 0;
+    int64_t eval_bytes = 0;
+    int launches = 0;
     int batches = 0;
     int refetches = 0;
 };
+
+// Algorithmic HBM bytes of one search (DESIGN.md "Roofline"): every scanned
+// candidate reads its 4-B slot id and 1-B alive flag; candidates still in the
+// index also read Min/MaxCount (8 B), the party id when the searching ticket
+// has a party (4 B), and one 8-B value + 1-B kind per field column the query
+// references (plus the candidate's own query descriptor and clauses for the
+// RevPrecision reverse check); each emitted hit writes 16 B.
+inline int64_t search_bytes(const Sig& s, const DGroup& d, const DGroupResult& r) {
+    int64_t per_live = 8 + (d.tparty != kNoParty ? 4 : 0) + 9 * (int64_t)s.n_fields;
+    if (d.rev_slot != kNoSlot) per_live += 8 + 32 * (int64_t)s.n_clauses;
+    return (int64_t)r.scanned * 5 + (int64_t)r.live * per_live + (int64_t)r.count * 16 +
+           (int64_t)(sizeof(DGroup) + sizeof(DGroupResult));
+}
 
 class Core {
 public:

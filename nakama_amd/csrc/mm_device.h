@@ -73,6 +73,8 @@ struct DGroupResult {
     uint32_t complete;  // 1: no further hit exists after the written ones
     uint32_t scanned;   // candidates examined
     uint32_t matched;   // candidates that passed the predicate (after the cursor)
+    uint32_t live;      // scanned candidates still in the index (their columns were read)
+    uint32_t pad;
 };
 
 // One emitted hit.

@@ -67,15 +67,17 @@ struct Cand {
     int64_t key;
     uint8_t rev;
     bool m;
+    bool live;
 };
 
 __device__ __forceinline__ Cand eval_candidate(const DStore& st, const DGroup& g, const uint32_t* __restrict__ src,
                                                uint32_t idx) {
-    Cand c{0, idx, 0, 1, false};
+    Cand c{0, idx, 0, 1, false, false};
     if (idx >= g.src_len) return c;
     const uint32_t s = src[g.src_off + idx];
     c.slot = s;
     bool m = st.alive[s] != 0;
+    c.live = m;
     if (m) m = st.minc[s] >= g.tmin && st.maxc[s] <= g.tmax && (g.tparty == kNoParty || st.party[s] != g.tparty);
     double sp = 0.0;
     if (m) m = eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
@@ -113,6 +115,10 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint32_t K = g.k;
+    __shared__ uint32_t s_live;
+    uint32_t my_live = 0;
+    if (tid == 0) s_live = 0;
+    __syncthreads();
 
     if (!g.var_score) {
         // ---- ordered compaction -------------------------------------------------
@@ -121,6 +127,7 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
         bool stopped = false;
         for (; base < g.src_len; base += kBlock) {
             Cand c = eval_candidate(st, g, src, base + tid);
+            my_live += c.live;
             const uint64_t mask = __ballot(c.m);
             if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(mask);
             __syncthreads();
@@ -141,9 +148,11 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
             __syncthreads();
             if (count > K) { stopped = true; base += kBlock; break; }
         }
+        atomicAdd(&s_live, my_live);
+        __syncthreads();
         if (tid == 0) {
             res[blockIdx.x] = DGroupResult{count < K ? count : K, stopped ? 0u : 1u,
-                                           base < g.src_len ? base : g.src_len, count};
+                                           base < g.src_len ? base : g.src_len, count, s_live, 0u};
         }
         return;
     }
@@ -156,6 +165,7 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     uint32_t base = 0;
     for (; base < g.src_len; base += kBlock) {
         Cand c = eval_candidate(st, g, src, base + tid);
+        my_live += c.live;
         const uint64_t pre = __ballot(c.m);
         if (n == KK && c.m) c.m = c.key > lkey[cur][KK - 1];
         const uint64_t mask = __ballot(c.m);
@@ -205,9 +215,11 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
         out[g.out_off + i] = DHit{lslot[cur][i], lidx[cur][i], lkey[cur][i]};
         if (out_rev) out_rev[g.out_off + i] = lrev[cur][i];
     }
+    atomicAdd(&s_live, my_live);
+    __syncthreads();
     if (tid == 0) {
         const bool complete = !early && total <= KK;
-        res[blockIdx.x] = DGroupResult{n, complete ? 1u : 0u, base < g.src_len ? base : g.src_len, total};
+        res[blockIdx.x] = DGroupResult{n, complete ? 1u : 0u, base < g.src_len ? base : g.src_len, total, s_live, 0u};
     }
 }
 

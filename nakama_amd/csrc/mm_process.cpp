@@ -15,6 +15,8 @@
 // through its list with a cursor, so every batch makes progress.
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "gocompat.h"
@@ -26,7 +28,7 @@ hipError_t launch_pairmat(const DStore& st, const DGroup* d_groups, const DGroup
                           const DHit* d_out, uint32_t* d_pm, hipStream_t stream);
 constexpr int kPairP = 32;  // pair matrix covers the first 32 entries of a list
 
-constexpr size_t kMaxBatchRows = 1u << 16;
+constexpr size_t kMaxBatchRows = 1u << 20;
 constexpr uint64_t kOutCap = 1ull << 24;  // max hit entries per batch (16M x 16 B)
 
 struct CE {  // combo entry: (ticket slot, presence index, list position of its hit)
@@ -59,7 +61,7 @@ void group_indexes(const std::vector<uint32_t>& in, size_t from, int required, c
 
 // A batch group: one device search and its (possibly extended) hit list.
 struct BGroup {
-    uint32_t sig;
+    uint32_t sig = 0;
     uint32_t nrows = 0;
     uint32_t row_slot = kNoSlot;  // RevPrecision: the single searching row
     DGroup d{};
@@ -121,12 +123,19 @@ struct Replay {
         c.d_rev_.reserve(d.k, false);
         c.d_res_.reserve(1, false);
         NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, sizeof(DGroup), hipMemcpyHostToDevice, stream));
+        NKM_HIP(hipEventRecord(c.ev0_, stream));
         NKM_HIP(launch_search(st, c.d_groups_.p, 1, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream));
+        NKM_HIP(hipEventRecord(c.ev1_, stream));
         c.h_res_.reserve(1);
         NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
         NKM_HIP(hipStreamSynchronize(stream));
+        float ms = 0.f;
+        NKM_HIP(hipEventElapsedTime(&ms, c.ev0_, c.ev1_));
+        stats.eval_ms += ms;
         const DGroupResult r = c.h_res_.p[0];
         stats.pair_evals += r.scanned;
+        stats.eval_bytes += search_bytes(c.sigs_[g.sig], d, r);
+        stats.launches++;
         std::vector<DHit> page(r.count);
         std::vector<uint8_t> prev(r.count);
         if (r.count) {
@@ -140,6 +149,127 @@ struct Replay {
         g.n = (uint32_t)g.ext.size();
         g.complete = r.complete != 0;
         g.d.k = d.k;
+    }
+
+    // Runs one batch of searches.  Large constant-score searches are split
+    // into chunks of their source (one workgroup each, so a pool's full hit
+    // list is produced by many CUs); chunk outputs are stitched back in
+    // source order, which is the hit order when every hit scores the same.
+    std::vector<DHit> stitch;
+    std::vector<DGroup> lg;
+    std::vector<uint32_t> lg_group, lg_start;
+    static constexpr uint32_t kChunk = 4096;
+
+    void run_batch(std::vector<BGroup>& bg, bool need_pm) {
+        lg.clear();
+        lg_group.clear();
+        lg_start.clear();
+        for (uint32_t i = 0; i < bg.size(); i++) {
+            const DGroup& d = bg[i].d;
+            if (!d.var_score && !rev && d.src_len > kChunk && d.k > kChunk / 4) {
+                for (uint32_t s0 = 0; s0 < d.src_len; s0 += kChunk) {
+                    DGroup dc = d;
+                    dc.src_off = d.src_off + s0;
+                    dc.src_len = std::min(kChunk, d.src_len - s0);
+                    dc.k = std::max<uint32_t>(1, std::min(d.k, dc.src_len));
+                    lg.push_back(dc);
+                    lg_group.push_back(i);
+                    lg_start.push_back(s0);
+                }
+            } else {
+                lg.push_back(d);
+                lg_group.push_back(i);
+                lg_start.push_back(0);
+            }
+        }
+        const int ng = (int)lg.size();
+        uint64_t off = 0;
+        c.h_groups_.reserve(ng);
+        for (int i = 0; i < ng; i++) {
+            lg[i].out_off = off;
+            off += lg[i].k;
+            c.h_groups_.p[i] = lg[i];
+        }
+        c.d_groups_.reserve(ng, false);
+        c.d_res_.reserve(ng, false);
+        c.d_out_.reserve(std::max<uint64_t>(off, 1), false);
+        if (rev) c.d_rev_.reserve(std::max<uint64_t>(off, 1), false);
+        NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, ng * sizeof(DGroup), hipMemcpyHostToDevice, stream));
+        NKM_HIP(hipEventRecord(c.ev0_, stream));
+        NKM_HIP(launch_search(st, c.d_groups_.p, ng, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream));
+        NKM_HIP(hipEventRecord(c.ev1_, stream));
+        if (need_pm) {
+            c.d_pm_.reserve((uint64_t)ng * kPairP, false);
+            NKM_HIP(launch_pairmat(st, c.d_groups_.p, c.d_res_.p, ng, c.d_out_.p, c.d_pm_.p, stream));
+        }
+        c.h_res_.reserve(ng);
+        NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, ng * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
+        c.h_out_.reserve(std::max<uint64_t>(off, 1));
+        NKM_HIP(hipMemcpyAsync(c.h_out_.p, c.d_out_.p, off * sizeof(DHit), hipMemcpyDeviceToHost, stream));
+        if (rev) {
+            c.h_rev_.reserve(std::max<uint64_t>(off, 1));
+            NKM_HIP(hipMemcpyAsync(c.h_rev_.p, c.d_rev_.p, off, hipMemcpyDeviceToHost, stream));
+        }
+        if (need_pm) {
+            c.h_pm_.reserve((uint64_t)ng * kPairP);
+            NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, (uint64_t)ng * kPairP * sizeof(uint32_t),
+                                   hipMemcpyDeviceToHost, stream));
+        }
+        NKM_HIP(hipStreamSynchronize(stream));
+        float ms = 0.f;
+        NKM_HIP(hipEventElapsedTime(&ms, c.ev0_, c.ev1_));
+        stats.eval_ms += ms;
+        stats.batches++;
+        stats.launches++;
+        // stitch
+        uint64_t stitched = 0;
+        for (int i = 0; i < ng; i++)
+            if (lg_start[i] || (i + 1 < ng && lg_group[i + 1] == lg_group[i])) stitched += c.h_res_.p[i].count;
+        stitch.resize(stitched);
+        uint64_t so = 0;
+        for (int i = 0; i < ng;) {
+            const uint32_t gi = lg_group[i];
+            BGroup& g = bg[gi];
+            int j = i;
+            while (j < ng && lg_group[j] == gi) j++;
+            for (int t = i; t < j; t++) {
+                stats.pair_evals += c.h_res_.p[t].scanned;
+                stats.eval_bytes += search_bytes(c.sigs_[g.sig], lg[t], c.h_res_.p[t]);
+            }
+            g.head = 0;
+            if (j == i + 1) {  // single search
+                const DGroupResult& r = c.h_res_.p[i];
+                g.hits = c.h_out_.p + lg[i].out_off;
+                g.rev = rev ? c.h_rev_.p + lg[i].out_off : nullptr;
+                g.pm = need_pm ? c.h_pm_.p + (uint64_t)i * kPairP : nullptr;
+                g.pm_n = need_pm ? std::min<uint32_t>(r.count, kPairP) : 0;
+                g.n = r.count;
+                g.complete = r.complete != 0;
+            } else {
+                uint64_t n = 0;
+                bool complete = true;
+                DHit* dst = stitch.data() + so;
+                for (int t = i; t < j; t++) {
+                    const DGroupResult& r = c.h_res_.p[t];
+                    complete &= r.complete != 0;
+                    const DHit* src = c.h_out_.p + lg[t].out_off;
+                    for (uint32_t e = 0; e < r.count; e++) {
+                        dst[n] = src[e];
+                        dst[n].idx += lg_start[t];
+                        n++;
+                    }
+                }
+                so += n;
+                if (n > g.d.k) { n = g.d.k; complete = false; }
+                g.hits = dst;
+                g.rev = nullptr;
+                g.pm = nullptr;
+                g.pm_n = 0;
+                g.n = (uint32_t)n;
+                g.complete = complete;
+            }
+            i = j;
+        }
     }
 
     // validateMatch(from's query, to) for two entries of the same list.
@@ -174,8 +304,13 @@ struct Replay {
                 }
             }
             const uint32_t s = g.hits[j].slot;
-            if (s != T && !sel[s]) return 1;
+            if (s != T && !sel[s] && !same_party(T, s)) return 1;
         }
+    }
+
+    // the party mustNot of the search (matchmaker_process.go:80-85)
+    bool same_party(uint32_t T, uint32_t H) const {
+        return c.party_[T] != kNoParty && c.party_[H] == c.party_[T];
     }
 
     // processDefault's loop body for one active ticket T.
@@ -192,8 +327,8 @@ struct Replay {
                 if (i >= g.n) { if (g.complete) break; i--; continue; }
             }
             const uint32_t H = g.hits[i].slot;
-            if (H == T || sel[H]) continue;
-            if (rev && !g.rev[i]) continue;                                              // :139-148
+            if (H == T || sel[H] || same_party(T, H)) continue;
+            if (rev && !g.rev[i]) continue;                                            // :139-148
             if (tmax < c.maxc_[H] && c.intervals_[H] <= max_intervals) continue;        // :150-153
             if (share_session(T, H)) continue;                                            // :155-165
             bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
@@ -370,63 +505,14 @@ int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& ou
             if (total_k > kOutCap && brow.size() > 1) { q++; break; }
         }
         // ---- device search ----
-        const int ng = (int)bg.size();
-        uint64_t off = 0;
-        h_groups_.reserve(ng);
-        for (int i = 0; i < ng; i++) {
-            bg[i].d.out_off = off;
-            off += bg[i].d.k;
-            h_groups_.p[i] = bg[i].d;
-        }
-        d_groups_.reserve(ng, false);
-        d_res_.reserve(ng, false);
-        d_out_.reserve(std::max<uint64_t>(off, 1), false);
-        if (rev) d_rev_.reserve(std::max<uint64_t>(off, 1), false);
-        NKM_HIP(hipMemcpyAsync(d_groups_.p, h_groups_.p, ng * sizeof(DGroup), hipMemcpyHostToDevice, stream_));
-        NKM_HIP(hipEventRecord(ev0_, stream_));
-        NKM_HIP(launch_search(st, d_groups_.p, ng, d_out_.p, rev ? d_rev_.p : nullptr, d_res_.p, stream_));
-        NKM_HIP(hipEventRecord(ev1_, stream_));
         bool need_pm = false;
         if (rev) {
-            for (int i = 0; i < ng && !need_pm; i++) {
+            for (size_t i = 0; i < bg.size() && !need_pm; i++) {
                 const uint32_t r = bg[i].row_slot;
                 need_pm = maxc_[r] - count_[r] >= 2;
             }
         }
-        if (need_pm) {
-            d_pm_.reserve((uint64_t)ng * kPairP, false);
-            NKM_HIP(launch_pairmat(st, d_groups_.p, d_res_.p, ng, d_out_.p, d_pm_.p, stream_));
-        }
-        h_res_.reserve(ng);
-        NKM_HIP(hipMemcpyAsync(h_res_.p, d_res_.p, ng * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream_));
-        h_out_.reserve(std::max<uint64_t>(off, 1));
-        NKM_HIP(hipMemcpyAsync(h_out_.p, d_out_.p, off * sizeof(DHit), hipMemcpyDeviceToHost, stream_));
-        if (rev) {
-            h_rev_.reserve(std::max<uint64_t>(off, 1));
-            NKM_HIP(hipMemcpyAsync(h_rev_.p, d_rev_.p, off, hipMemcpyDeviceToHost, stream_));
-        }
-        if (need_pm) {
-            h_pm_.reserve((uint64_t)ng * kPairP);
-            NKM_HIP(hipMemcpyAsync(h_pm_.p, d_pm_.p, (uint64_t)ng * kPairP * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                   stream_));
-        }
-        NKM_HIP(hipStreamSynchronize(stream_));
-        float ms = 0.f;
-        NKM_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
-        stats.eval_ms += ms;
-        stats.batches++;
-        for (int i = 0; i < ng; i++) {
-            BGroup& g = bg[i];
-            const DGroupResult& r = h_res_.p[i];
-            g.hits = h_out_.p + g.d.out_off;
-            g.rev = rev ? h_rev_.p + g.d.out_off : nullptr;
-            g.pm = need_pm ? h_pm_.p + (uint64_t)i * kPairP : nullptr;
-            g.pm_n = need_pm ? std::min<uint32_t>(r.count, kPairP) : 0;
-            g.n = r.count;
-            g.complete = r.complete != 0;
-            g.head = 0;
-            stats.pair_evals += r.scanned;
-        }
+        rp.run_batch(bg, need_pm);
         // ---- replay ----
         newly.clear();
         size_t done = 0;
@@ -510,35 +596,8 @@ int Core::process_custom(std::vector<std::vector<std::pair<uint32_t, int>>>& can
             g.row_slot = r;
             h_groups_.p[i] = g.d;
         }
-        const int ng = (int)bg.size();
-        d_groups_.reserve(ng, false);
-        d_res_.reserve(ng, false);
-        d_out_.reserve(std::max<uint64_t>(off, 1), false);
-        d_rev_.reserve(std::max<uint64_t>(off, 1), false);
-        NKM_HIP(hipMemcpyAsync(d_groups_.p, h_groups_.p, ng * sizeof(DGroup), hipMemcpyHostToDevice, stream_));
-        NKM_HIP(hipEventRecord(ev0_, stream_));
-        NKM_HIP(launch_search(st, d_groups_.p, ng, d_out_.p, rev ? d_rev_.p : nullptr, d_res_.p, stream_));
-        NKM_HIP(hipEventRecord(ev1_, stream_));
-        h_res_.reserve(ng);
-        h_out_.reserve(std::max<uint64_t>(off, 1));
-        h_rev_.reserve(std::max<uint64_t>(off, 1));
-        NKM_HIP(hipMemcpyAsync(h_res_.p, d_res_.p, ng * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream_));
-        NKM_HIP(hipMemcpyAsync(h_out_.p, d_out_.p, off * sizeof(DHit), hipMemcpyDeviceToHost, stream_));
-        if (rev) NKM_HIP(hipMemcpyAsync(h_rev_.p, d_rev_.p, off, hipMemcpyDeviceToHost, stream_));
-        NKM_HIP(hipStreamSynchronize(stream_));
-        float ms = 0.f;
-        NKM_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
-        stats.eval_ms += ms;
-        stats.batches++;
-        for (size_t i = 0; i < bg.size(); i++) {
-            BGroup& g = bg[i];
-            const DGroupResult& res = h_res_.p[i];
-            g.hits = h_out_.p + g.d.out_off;
-            g.rev = rev ? h_rev_.p + g.d.out_off : nullptr;
-            g.n = res.count;
-            g.complete = res.complete != 0;
-            stats.pair_evals += res.scanned;
-        }
+        (void)off;
+        rp.run_batch(bg, rev);
         for (size_t i = 0; i < bg.size(); i++) {
             BGroup& g = bg[i];
             const uint32_t T = g.row_slot;
@@ -553,7 +612,7 @@ int Core::process_custom(std::vector<std::vector<std::pair<uint32_t, int>>>& can
                     if (j >= g.n) break;
                 }
                 const uint32_t H = g.hits[j].slot;
-                if (H == T) continue;
+                if (H == T || rp.same_party(T, H)) continue;
                 if (rev && !g.rev[j]) continue;
                 if (maxc_[T] < maxc_[H] && intervals_[H] <= maxI) continue;
                 if (rp.share_session(T, H)) continue;
@@ -568,7 +627,14 @@ int Core::process_custom(std::vector<std::vector<std::pair<uint32_t, int>>>& can
             const int cmin = minc_[T] - count_[T], cmax = maxc_[T] - count_[T];
             // pairwise reverse checks among the hits (validateMatch both ways, incl. self)
             std::vector<uint64_t> pm;
-            if (rev && L) {
+            bool covered = g.pm != nullptr;
+            for (size_t a = 0; a < L && covered; a++) covered = hpos[a] < g.pm_n;
+            if (rev && L && covered) {  // from the batch's pair matrices
+                pm.assign(L, 0);
+                for (size_t a = 0; a < L; a++)
+                    for (size_t b = 0; b < L; b++)
+                        if ((g.pm[hpos[a]] >> hpos[b]) & 1u) pm[a] |= 1ull << b;
+            } else if (rev && L) {
                 std::vector<uint32_t> pr;
                 for (size_t a = 0; a < L; a++)
                     for (size_t b = 0; b < L; b++) { pr.push_back(hits[a]); pr.push_back(hits[b]); }
@@ -741,13 +807,28 @@ int Core::process(mm_matched* out) {
             fill_matched(groups, out, true);
         }
     } else {
+        const auto t1 = std::chrono::steady_clock::now();
         process_default(groups, expired, stats);
+        const auto t2 = std::chrono::steady_clock::now();
         out->n_expired = (int32_t)expired.size();
         finish_pass(expired, groups);
+        const auto t3 = std::chrono::steady_clock::now();
         fill_matched(groups, out, false);
+        const auto t4 = std::chrono::steady_clock::now();
+        if (std::getenv("NKM_PROFILE")) {
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            std::fprintf(stderr,
+                         "[nkm] sync %.2f ms | pass %.2f ms (eval %.2f ms, %d batches, %d refetches, %d launches) | "
+                         "finish %.2f ms | fill %.2f ms | groups %zu\n",
+                         ms(t0, t1), ms(t1, t2), stats.eval_ms, stats.batches, stats.refetches, stats.launches,
+                         ms(t2, t3), ms(t3, t4), groups.size());
+        }
     }
     out->eval_ms = stats.eval_ms;
     out->pair_evals = stats.pair_evals;
+    out->eval_bytes = stats.eval_bytes;
+    out->eval_launches = stats.launches;
+    out->n_batches = stats.batches;
     out->pass_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MM_OK;
 }
@@ -817,6 +898,7 @@ int32_t Core::debug_hits(const std::string& ticket, const char** tk, double* sc,
     std::vector<uint8_t> sel(ticket_.size(), 0);
     Replay rp(*this, sel, cfg_.rev_precision != 0, cfg_.max_intervals, stats, st, stream_);
     BGroup g;
+    g.sig = sig_[T];
     const Sig& s = sigs_[sig_[T]];
     g.d.clause_off = s.clause_off;
     g.d.n_clauses = s.n_clauses;
@@ -835,12 +917,13 @@ int32_t Core::debug_hits(const std::string& ticket, const char** tk, double* sc,
     while (!g.complete) rp.fetch_more(g);
     debug_strings_.clear();
     int32_t n = 0;
+    auto skip = [&](uint32_t i) { return g.hits[i].slot == (uint32_t)T || rp.same_party((uint32_t)T, g.hits[i].slot); };
     for (uint32_t i = 0; i < g.n; i++) {
-        if (g.hits[i].slot == (uint32_t)T) continue;
+        if (skip(i)) continue;
         debug_strings_.push_back(ticket_[g.hits[i].slot]);
     }
     for (uint32_t i = 0; i < g.n; i++) {
-        if (g.hits[i].slot == (uint32_t)T) continue;
+        if (skip(i)) continue;
         if (n < cap) {
             if (tk) tk[n] = debug_strings_[n].c_str();
             int64_t key = g.hits[i].key;

@@ -227,6 +227,12 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
     double ub = (S + 1.0) + 1.0;
     s.ub_key = std::isfinite(ub) ? sortable_i64(ub) : INT64_MAX;
     if (!std::isfinite(ms) || !std::isfinite(ss)) s.ub_key = INT64_MAX;
+    {
+        std::vector<uint16_t> fs;
+        for (auto& d : dc)
+            if (d.op != OP_FALSE && std::find(fs.begin(), fs.end(), d.field) == fs.end()) fs.push_back(d.field);
+        s.n_fields = (uint16_t)fs.size();
+    }
     for (auto& d : dc) clauses_.push_back(d);
     uint32_t id = (uint32_t)sigs_.size();
     sigs_.push_back(std::move(s));
@@ -341,7 +347,11 @@ int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_inse
     }
     sig_.push_back(0);
     squery_.push_back(DQuery{});
-    uint32_t sg = sig_of(cq, t.min_count, t.max_count, party);  // may materialise new columns (incl. this slot)
+    // The party mustNot (matchmaker_process.go:80-85) only ever removes the
+    // searching ticket's own party (<= MaxTickets tickets), so it is applied
+    // while walking the hit list instead of in the shared search: party
+    // tickets then share their pool's search.
+    uint32_t sg = sig_of(cq, t.min_count, t.max_count, kNoParty);  // may materialise new columns (incl. this slot)
     sig_[s] = sg;
     squery_[s] = DQuery{sigs_[sg].clause_off, sigs_[sg].n_clauses, sigs_[sg].qkind, 0};
     slot_of_[tk] = s;
