@@ -129,24 +129,31 @@ def main():
     import nakama_amd
     from nakama_amd import synth
 
+    from nakama_amd import sharding
     mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local)
-    shard = 1_000_000_000  # ticket index range per (rank, step): disjoint ticket sets
+    # Pool sharding: each step draws a global set of world x tickets; every rank
+    # keeps the pools assign_pools gives it (weak scaling: ~tickets per rank).
+    npools = synth.N_POOLS.get(args.config, 0)
+    if world > 1 and npools < world:
+        raise SystemExit(f"config {args.config} has {npools} pools: cannot shard over {world} GPUs")
+    mask = None
+    if world > 1:
+        mine = sharding.assign_pools([1] * npools, world)[rank]
+        mask = sharding.pool_mask(mine)
+    per_step = world * args.tickets
     times, matched_all, presences_all = [], [], []
     eval_ms = eval_bytes = launches = 0
     batches = []
     for step in range(args.warmup + args.steps):
-        first = (rank * 1000 + step) * shard // 1000
-        ts = synth.TicketSet(args.config, args.tickets, first=first)
+        ts = synth.TicketSet(args.config, per_step, first=step * per_step, pool_mask=mask)
         ts.insert_into(mm)  # untimed: store maintenance + HBM upload
         barrier_sync(pg, local)
         t0 = time.perf_counter()
-        r = mm.process_raw()
+        _, n_groups, matched, pres, r = mm.process_timed()  # the C-ABI call; groups stay in C memory
         barrier_sync(pg, local)
         dt = time.perf_counter() - t0
         ts.close()
         dt_max = max_over_ranks(pg, local, dt)
-        matched = sum(len({t for t, _ in g}) for g in r.groups)
-        pres = sum(len(g) for g in r.groups)
         if step >= args.warmup:
             times.append(dt_max)
             matched_all.append(sum_over_ranks(pg, local, matched))

@@ -370,6 +370,32 @@ class Matchmaker:
             self.lib.mm_free_matched(self.h, C.byref(out))
         return res
 
+    def process_timed(self):
+        """One mm_process call timed at the C boundary (no Python conversion of
+        the groups inside the timed region).  Returns (seconds, n_groups,
+        matched tickets, matched presences, ProcessResult-without-groups)."""
+        import time
+        import numpy as np
+        out = mm_matched()
+        fn = self.lib.mm_process
+        t0 = time.perf_counter()
+        rc = fn(self.h, C.byref(out))
+        dt = time.perf_counter() - t0
+        self._check(rc)
+        try:
+            n = out.n_entries
+            if n:
+                raw = (C.c_char * (n * C.sizeof(mm_entry_ref))).from_address(C.addressof(out.entries.contents))
+                arr = np.frombuffer(raw, dtype=np.dtype([("p", "<u8"), ("pi", "<i4"), ("r", "<i4")]))
+                tickets = int(np.count_nonzero(arr["pi"] == 0))
+            else:
+                tickets = 0
+            res = ProcessResult([], bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms, out.pair_evals,
+                                out.eval_bytes, out.eval_launches, out.n_batches)
+            return dt, out.n_groups, tickets, n, res
+        finally:
+            self.lib.mm_free_matched(self.h, C.byref(out))
+
     def commit(self, groups: Sequence[Sequence[Tuple[str, int]]]) -> ProcessResult:
         offs = [0]
         ents = []

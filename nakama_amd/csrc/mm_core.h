@@ -9,6 +9,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <mutex>
 #include <string>
@@ -153,6 +154,14 @@ struct PostingRange {
 // Builtin document fields (MapMatchmakerIndex, matchmaker.go:1026-1040).
 enum BuiltinField : uint16_t { F_TICKET = 0, F_MIN = 1, F_MAX = 2, F_PARTY = 3, F_CREATED = 4, F_NBUILTIN = 5 };
 
+struct BGroup;  // a batch search and its hit list (mm_process.cpp)
+
+struct SrcChoice {  // the posting list a search streams, when it has one
+    bool has_term = false;
+    uint16_t field = 0;
+    uint32_t term = 0;
+};
+
 struct PassStats {
     double eval_ms = 0;
     int64_t pair_evals = 0;
@@ -160,6 +169,9 @@ struct PassStats {
     int launches = 0;
     int batches = 0;
     int refetches = 0;
+    double search_ms = 0;   // host wall time of batch searches incl. H2D/D2H and stitching
+    double replay_ms = 0;   // host wall time of the greedy replay
+    int parallel_batches = 0;
 };
 
 // Algorithmic HBM bytes of one search (DESIGN.md "Roofline"): every scanned
@@ -231,7 +243,11 @@ private:
                        PassStats& st);
     void finish_pass(const std::vector<uint32_t>& expired, std::vector<std::vector<std::pair<uint32_t, int>>>& groups);
     void fill_matched(const std::vector<std::vector<std::pair<uint32_t, int>>>& groups, mm_matched* out, bool cands);
-    void choose_source(const Sig& s, DGroup& g);
+    void choose_source(const Sig& s, DGroup& g, SrcChoice* ch = nullptr);
+    bool replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
+                         const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
+                         std::vector<std::vector<std::pair<uint32_t, int>>>& out_groups,
+                         std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats);
     void apply_selected_to_device(const std::vector<uint32_t>& slots);
 
     std::mutex mu_;
@@ -319,6 +335,11 @@ public:
     std::vector<uint32_t> custom_expired_;
 
     std::vector<std::string> debug_strings_;
+    // reusable output arena of mm_process (pages stay mapped across passes)
+    std::vector<char> out_chars_;
+    std::vector<mm_entry_ref> out_ents_;
+    std::vector<int32_t> out_offs_;
+    std::atomic<bool> out_in_use_{false};
     DevArray<uint32_t> d_pm_;      // pair matrices (RevPrecision combos)
     PinnedArray<uint32_t> h_pm_;
 };

@@ -14,10 +14,13 @@
 // device alive mask up to date; the first row of a batch may page further
 // through its list with a cursor, so every batch makes progress.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 
 #include "gocompat.h"
 #include "mm_core.h"
@@ -69,6 +72,9 @@ struct BGroup {
     const uint8_t* rev = nullptr;
     const uint32_t* pm = nullptr;  // kPairP masks per entry (rev rows with combos)
     uint32_t pm_n = 0;             // entries covered by pm
+    bool has_src_term = false;     // source = posting list of (src_field, src_term)
+    uint16_t src_field = 0;
+    uint32_t src_term = 0;
     uint32_t n = 0;
     bool complete = true;
     uint32_t head = 0;
@@ -81,7 +87,8 @@ struct Replay {
     std::vector<uint8_t>& sel;
     const bool rev;
     const int max_intervals;
-    std::vector<std::vector<CE>> combos;
+    std::vector<std::vector<CE>> combos;  // pool: the first ncomb are this row's entryCombos
+    size_t ncomb = 0;
     PassStats& stats;
     DStore st;
     hipStream_t stream;
@@ -317,7 +324,7 @@ struct Replay {
     Status row(uint32_t T, BGroup& g, bool can_fetch, std::vector<std::pair<uint32_t, int>>& group_out) {
         const bool last = c.intervals_[T] + 1 >= max_intervals || c.minc_[T] == c.maxc_[T];
         const int tcount = c.count_[T], tmax = c.maxc_[T], tmin = c.minc_[T], tcm = c.cm_[T];
-        combos.clear();
+        ncomb = 0;
         while (g.head < g.n && sel[g.hits[g.head].slot]) g.head++;
         for (uint32_t i = g.head;; i++) {
             if (i >= g.n) {
@@ -334,7 +341,7 @@ struct Replay {
             bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
             int found = -1;
             const int hcount = c.count_[H];
-            for (size_t ci = 0; ci < combos.size(); ci++) {
+            for (size_t ci = 0; ci < ncomb; ci++) {
                 auto& combo = combos[ci];
                 if ((int)combo.size() + hcount + tcount <= tmax) {
                     bool mconf = false;
@@ -352,9 +359,11 @@ struct Replay {
                 }
             }
             if (found < 0) {
-                combos.emplace_back();
-                for (int k = 0; k < hcount; k++) combos.back().push_back(CE{H, (uint32_t)k, i});
-                found = (int)combos.size() - 1;
+                if (ncomb == combos.size()) combos.emplace_back();
+                std::vector<CE>& nc = combos[ncomb];
+                nc.clear();
+                for (int k = 0; k < hcount; k++) nc.push_back(CE{H, (uint32_t)k, i});
+                found = (int)ncomb++;
             }
             std::vector<CE>& fc = combos[found];
             int l = (int)fc.size() + tcount;
@@ -403,11 +412,131 @@ struct Replay {
     }
 };
 
-void Core::choose_source(const Sig& s, DGroup& g) {
+// Pool-parallel replay.  When every search of the batch draws its hits from a
+// posting list of the same field with a distinct term, every searching ticket
+// carries its own search's term, and every list is complete, then each
+// search's rows only ever select tickets of its own posting list: the greedy
+// pass decomposes exactly into independent per-pool passes (processDefault's
+// sequential order is preserved within each pool, and no ticket is shared
+// across pools).  The pools run on host threads; results are merged back into
+// the pinned row order.  Returns false (nothing done) when the conditions fail.
+bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
+                           const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
+                           std::vector<std::vector<std::pair<uint32_t, int>>>& out_groups,
+                           std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats) {
+    const size_t nsearch = bg.size();
+    if (nsearch < 2) return false;
+    // pool key fields: fields every search requires a keyword term on
+    std::vector<uint16_t> keyf;
+    for (auto& mt : sigs_[bg[0].sig].must_terms) {
+        if (std::find(keyf.begin(), keyf.end(), mt.first) != keyf.end()) continue;
+        bool all = true;
+        for (size_t i = 1; i < nsearch && all; i++) {
+            bool has = false;
+            for (auto& m2 : sigs_[bg[i].sig].must_terms) has |= m2.first == mt.first;
+            all = has;
+        }
+        if (all) keyf.push_back(mt.first);
+    }
+    if (keyf.empty()) return false;
+    for (uint16_t f : keyf)
+        if (fkind_[f].size() != ticket_.size()) return false;
+    // pool key of each search (a search requiring two different terms on one
+    // field matches nothing; it gets a key of its own)
+    std::map<std::vector<uint32_t>, uint32_t> pool_of;
+    std::vector<uint32_t> search_pool(nsearch);
+    for (size_t i = 0; i < nsearch; i++) {
+        if (!bg[i].complete) return false;
+        std::vector<uint32_t> key(keyf.size(), UINT32_MAX);
+        for (size_t k = 0; k < keyf.size(); k++)
+            for (auto& mt : sigs_[bg[i].sig].must_terms)
+                if (mt.first == keyf[k]) {
+                    if (key[k] != UINT32_MAX && key[k] != mt.second) return false;
+                    key[k] = mt.second;
+                }
+        search_pool[i] = pool_of.emplace(std::move(key), (uint32_t)pool_of.size()).first->second;
+    }
+    const size_t ng = pool_of.size();
+    if (ng < 2) return false;
+    std::vector<std::vector<uint32_t>> pool_keys(ng);
+    for (auto& kv : pool_of) pool_keys[kv.second] = kv.first;
+    // every searching ticket must itself belong to its search's pool
+    for (size_t bi = 0; bi < brow.size(); bi++) {
+        const uint32_t r = brow[bi];
+        const auto& key = pool_keys[search_pool[brow_group[bi]]];
+        for (size_t k = 0; k < keyf.size(); k++)
+            if (fkind_[keyf[k]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[k]][r] != key[k]) return false;
+    }
+    // rows per pool, in batch order
+    std::vector<std::vector<uint32_t>> grows(ng);
+    for (size_t bi = 0; bi < brow.size(); bi++) grows[search_pool[brow_group[bi]]].push_back((uint32_t)bi);
+    struct Rec { uint32_t bi; uint8_t matched; uint8_t expired; uint32_t off, len; };
+    struct Out { std::vector<Rec> recs; std::vector<std::pair<uint32_t, int>> ents; };
+    std::vector<Out> outs(ng);
+    std::vector<uint32_t> order_g(ng);
+    for (size_t i = 0; i < ng; i++) order_g[i] = (uint32_t)i;
+    std::sort(order_g.begin(), order_g.end(), [&](uint32_t a, uint32_t b) { return grows[a].size() > grows[b].size(); });
+    std::atomic<size_t> next{0};
+    const DStore st = dstore();
+    const int maxI = cfg_.max_intervals;
+    auto worker = [&]() {
+        PassStats ls;
+        Replay rp(*this, sel, false, maxI, ls, st, stream_);
+        std::vector<std::pair<uint32_t, int>> grp;
+        for (;;) {
+            const size_t k = next.fetch_add(1);
+            if (k >= ng) break;
+            const uint32_t gi = order_g[k];
+            Out& o = outs[gi];
+            for (uint32_t bi : grows[gi]) {
+                const uint32_t T = brow[bi];
+                if (sel[T]) continue;
+                auto status = rp.row(T, bg[brow_group[bi]], false, grp);  // complete lists: never EXHAUSTED
+                intervals_[T]++;
+                Rec rec{bi, 0, (uint8_t)(intervals_[T] >= maxI || minc_[T] == maxc_[T]), 0, 0};
+                if (status == Replay::MATCHED) {
+                    rec.matched = 1;
+                    rec.off = (uint32_t)o.ents.size();
+                    rec.len = (uint32_t)grp.size();
+                    for (auto& e : grp) {
+                        sel[e.first] = 1;
+                        o.ents.push_back(e);
+                    }
+                }
+                o.recs.push_back(rec);
+            }
+        }
+    };
+    unsigned nt = std::min<unsigned>((unsigned)ng, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
+    // merge back into the pinned row order
+    std::vector<std::pair<uint32_t, uint32_t>> at(brow.size(), {UINT32_MAX, 0});  // bi -> (group, record)
+    for (uint32_t gi = 0; gi < ng; gi++)
+        for (uint32_t k = 0; k < outs[gi].recs.size(); k++) at[outs[gi].recs[k].bi] = {gi, k};
+    for (size_t bi = 0; bi < brow.size(); bi++) {
+        const uint32_t gi = at[bi].first, k = at[bi].second;
+        if (gi == UINT32_MAX) continue;
+        const Rec& rec = outs[gi].recs[k];
+        const uint32_t T = brow[rec.bi];
+        if (rec.expired) expired.push_back(T);
+        if (rec.matched) {
+            out_groups.emplace_back(outs[gi].ents.begin() + rec.off, outs[gi].ents.begin() + rec.off + rec.len);
+            for (auto& e : out_groups.back()) newly.push_back(e.first);
+        }
+    }
+    stats.refetches += 0;
+    return true;
+}
+
+void Core::choose_source(const Sig& s, DGroup& g, SrcChoice* ch) {
     g.src_kind = 0;
     g.src_off = order_head_;
     g.src_len = (uint32_t)order_.size() - order_head_;
     bool have = false;
+    if (ch) ch->has_term = false;
     for (auto& mt : s.must_terms) {
         auto it = postings_map_.find(((uint64_t)mt.first << 32) | mt.second);
         uint32_t off = 0, len = 0;
@@ -418,6 +547,7 @@ void Core::choose_source(const Sig& s, DGroup& g) {
             len = r.len - r.head;
         }
         if (!have || len < g.src_len) {
+            if (ch) { ch->has_term = true; ch->field = mt.first; ch->term = mt.second; }
             g.src_kind = 1;
             g.src_off = off;
             g.src_len = len;
@@ -485,7 +615,11 @@ int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& ou
                 g.d.rev_slot = rev ? r : kNoSlot;
                 g.d.ub_key = s.ub_key;
                 g.d.has_cursor = 0;
-                choose_source(s, g.d);
+                SrcChoice ch;
+                choose_source(s, g.d, &ch);
+                g.has_src_term = ch.has_term;
+                g.src_field = ch.field;
+                g.src_term = ch.term;
                 g.d.k = 0;
                 g.row_slot = rev ? r : kNoSlot;
                 gi = (int32_t)bg.size();
@@ -512,11 +646,22 @@ int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& ou
                 need_pm = maxc_[r] - count_[r] >= 2;
             }
         }
+        auto tb0 = std::chrono::steady_clock::now();
         rp.run_batch(bg, need_pm);
+        auto tb1 = std::chrono::steady_clock::now();
+        stats.search_ms += std::chrono::duration<double, std::milli>(tb1 - tb0).count();
         // ---- replay ----
         newly.clear();
         size_t done = 0;
         bool exhausted = false;
+        if (!rev && replay_parallel(bg, brow, brow_group, sel, out_groups, expired, newly, stats)) {
+            stats.parallel_batches++;
+            stats.replay_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb1).count();
+            apply_selected_to_device(newly);
+            pos = q;
+            retry_slot = kNoSlot;
+            continue;
+        }
         for (size_t bi = 0; bi < brow.size(); bi++) {
             const uint32_t T = brow[bi];
             if (sel[T]) { done = bi + 1; continue; }
@@ -539,6 +684,7 @@ int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& ou
             }
             done = bi + 1;
         }
+        stats.replay_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb1).count();
         apply_selected_to_device(newly);
         // advance past the rows this batch decided
         if (exhausted) {
@@ -739,19 +885,40 @@ void Core::fill_matched(const std::vector<std::vector<std::pair<uint32_t, int>>>
         n += g.size();
         for (auto& e : g) bytes += (e.first < ticket_.size() ? ticket_[e.first].size() : 0) + 1;
     }
-    auto* offs = new int32_t[groups.size() + 1];
-    auto* ents = new mm_entry_ref[n ? n : 1];
-    char* buf = new char[bytes ? bytes : 1];
+    // Reuse the handle's arena when no earlier result is outstanding (its pages
+    // stay mapped: no page-fault storm per pass); otherwise allocate.
+    bool arena = !out_in_use_.exchange(true);
+    int32_t* offs;
+    mm_entry_ref* ents;
+    char* buf;
+    if (arena) {
+        if (out_offs_.size() < groups.size() + 1) out_offs_.resize(groups.size() + 1);
+        if (out_ents_.size() < std::max<size_t>(n, 1)) out_ents_.resize(std::max<size_t>(n, 1));
+        if (out_chars_.size() < std::max<size_t>(bytes, 1)) out_chars_.resize(std::max<size_t>(bytes, 1));
+        offs = out_offs_.data();
+        ents = out_ents_.data();
+        buf = out_chars_.data();
+    } else {
+        offs = new int32_t[groups.size() + 1];
+        ents = new mm_entry_ref[n ? n : 1];
+        buf = new char[bytes ? bytes : 1];
+    }
     size_t k = 0, b = 0;
     offs[0] = 0;
     for (size_t gi = 0; gi < groups.size(); gi++) {
+        uint32_t prev = kNoSlot;
+        const char* prev_p = nullptr;
         for (auto& e : groups[gi]) {
-            const std::string& t = ticket_[e.first];
-            std::memcpy(buf + b, t.c_str(), t.size() + 1);
-            ents[k].ticket = buf + b;
+            if (e.first != prev) {  // a ticket's entries are adjacent: one string copy per ticket
+                const std::string& t = ticket_[e.first];
+                std::memcpy(buf + b, t.c_str(), t.size() + 1);
+                prev_p = buf + b;
+                prev = e.first;
+                b += t.size() + 1;
+            }
+            ents[k].ticket = prev_p;
             ents[k].presence_index = e.second;
             ents[k].reserved = 0;
-            b += t.size() + 1;
             k++;
         }
         offs[gi + 1] = (int32_t)k;
@@ -761,14 +928,18 @@ void Core::fill_matched(const std::vector<std::vector<std::pair<uint32_t, int>>>
     out->group_offsets = offs;
     out->entries = ents;
     out->is_candidates = cands ? 1 : 0;
-    out->reserved2 = (int64_t)(intptr_t)buf;
+    out->reserved2 = arena ? 1 : (int64_t)(intptr_t)buf;  // 1: the handle's arena
 }
 
 void Core::free_matched(mm_matched* out) {
     if (!out) return;
-    delete[] out->group_offsets;
-    delete[] out->entries;
-    delete[] reinterpret_cast<char*>((intptr_t)out->reserved2);
+    if (out->reserved2 == 1) {
+        out_in_use_.store(false);
+    } else if (out->reserved2 != 0 || out->group_offsets) {
+        delete[] out->group_offsets;
+        delete[] out->entries;
+        delete[] reinterpret_cast<char*>((intptr_t)out->reserved2);
+    }
     std::memset(out, 0, sizeof(*out));
 }
 
@@ -818,10 +989,12 @@ int Core::process(mm_matched* out) {
         if (std::getenv("NKM_PROFILE")) {
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
             std::fprintf(stderr,
-                         "[nkm] sync %.2f ms | pass %.2f ms (eval %.2f ms, %d batches, %d refetches, %d launches) | "
-                         "finish %.2f ms | fill %.2f ms | groups %zu\n",
-                         ms(t0, t1), ms(t1, t2), stats.eval_ms, stats.batches, stats.refetches, stats.launches,
-                         ms(t2, t3), ms(t3, t4), groups.size());
+                         "[nkm] sync %.2f ms | pass %.2f ms (search %.2f ms [kernel %.2f ms], replay %.2f ms, "
+                         "%d batches (%d parallel), %d refetches, %d launches) | finish %.2f ms | fill %.2f ms | "
+                         "groups %zu\n",
+                         ms(t0, t1), ms(t1, t2), stats.search_ms, stats.eval_ms, stats.replay_ms, stats.batches,
+                         stats.parallel_batches, stats.refetches, stats.launches, ms(t2, t3), ms(t3, t4),
+                         groups.size());
         }
     }
     out->eval_ms = stats.eval_ms;

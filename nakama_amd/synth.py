@@ -34,16 +34,33 @@ def lib():
         _lib.synth_presences.restype = C.c_int64
         _lib.synth_presences.argtypes = [C.c_void_p]
         _lib.synth_free.argtypes = [C.c_void_p]
+        _lib.synth_make_pools.restype = C.c_void_p
+        _lib.synth_make_pools.argtypes = [C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_uint64]
+        _lib.synth_pool_of.restype = C.c_int
+        _lib.synth_pool_of.argtypes = [C.c_int, C.c_uint64, C.c_uint64]
     return _lib
+
+
+N_POOLS = {3: 8, 4: 64}
+
+
+def pool_of(config: int, i: int, seed: int = None) -> int:
+    return lib().synth_pool_of(config, SEEDS.get(config, 1) if seed is None else seed, i)
 
 
 class TicketSet:
     """Tickets [first, first+n) of a config; owns the native arrays."""
 
-    def __init__(self, config: int, n: int, first: int = 0, seed: int = None, t0: int = T0):
+    def __init__(self, config: int, n: int, first: int = 0, seed: int = None, t0: int = T0, pool_mask: int = None):
+        """pool_mask: keep only tickets of these pools (bit p = pool p) out of
+        the n generated indices — a rank's shard of a pool-sharded set."""
         L = lib()
         self.config = config
-        self.h = L.synth_make(config, SEEDS.get(config, 1) if seed is None else seed, first, n, t0)
+        sd = SEEDS.get(config, 1) if seed is None else seed
+        if pool_mask is None:
+            self.h = L.synth_make(config, sd, first, n, t0)
+        else:
+            self.h = L.synth_make_pools(config, sd, first, n, t0, pool_mask)
         self.n = L.synth_count(self.h)
         self.presences = L.synth_presences(self.h)
         self.tickets = L.synth_tickets(self.h)

@@ -1,0 +1,100 @@
+"""Multi-rank (gloo, CPU) checks of the pool-sharded pass.
+
+Two ranks each take the pools `assign_pools` gives them, insert only their
+shard into a matchmaker (the CPU oracle here: the GPU path is the same C ABI),
+run one interval pass, and gather the groups to rank 0, which checks that the
+merged result is identical — groups, entry order and global group order — to a
+single pass over the whole ticket set.  This is the property the multi-GPU
+bench relies on.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, config, n, q):
+    import harness
+    from nakama_amd import capi, sharding, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        npools = synth.N_POOLS[config]
+        sizes = [0] * npools
+        for i in range(n):
+            sizes[synth.pool_of(config, i)] += 1
+        mine = sharding.assign_pools(sizes, world)[rank]
+        ts = synth.TicketSet(config, n, pool_mask=sharding.pool_mask(mine))
+        mm = capi.Matchmaker(harness.oracle_lib(), max_intervals=2)
+        ts.insert_into(mm)
+        groups = mm.Process()
+        created = {ts.ticket_id(k): ts.tickets[k].created_at for k in range(ts.n)}
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (groups, created, mine, ts.n))
+        if rank == 0:
+            q.put(gathered)
+        mm.close()
+        ts.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("config,n", [(3, 900), (4, 1200)])
+def test_pool_sharded_pass_equals_global_pass(config, n):
+    import harness
+    from nakama_amd import capi, sharding, synth
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, config, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    # shards are disjoint and cover the set
+    pools = [set(g[2]) for g in gathered]
+    assert not (pools[0] & pools[1])
+    assert sum(g[3] for g in gathered) == n
+    created = {}
+    for g in gathered:
+        created.update(g[1])
+    merged = sharding.merge_groups([g[0] for g in gathered], created)
+    # single global pass
+    ts = synth.TicketSet(config, n)
+    mm = capi.Matchmaker(harness.oracle_lib(), max_intervals=2)
+    try:
+        ts.insert_into(mm)
+        ref = mm.Process()
+    finally:
+        mm.close()
+        ts.close()
+    assert merged == ref
+
+
+def test_assign_pools_balanced_and_deterministic():
+    from nakama_amd import sharding
+    sizes = [125, 124, 130, 126, 119, 127, 125, 124]
+    a = sharding.assign_pools(sizes, 4)
+    assert sorted(p for b in a for p in b) == list(range(8))
+    loads = [sum(sizes[p] for p in b) for b in a]
+    assert max(loads) - min(loads) <= max(sizes)
+    assert a == sharding.assign_pools(sizes, 4)

@@ -63,9 +63,46 @@ const char* kRegions[8] = {"eu", "na", "sa", "ap", "me", "af", "oc", "cn"};
 
 extern "C" {
 
-// config: 1..5 as BASELINE.json configs[0..4].  Generates tickets [first, first+n).
+// Pool (mode x region partition) of ticket i for the pool-partitioned configs
+// (3: 2x4 = 8 pools, 4: 8x8 = 64 pools); -1 for the others.  Uses the same
+// draws as synth_make, so it agrees with the generated properties.
+int synth_pool_of(int config, uint64_t seed, uint64_t i) {
+    Rng r{splitmix64(seed ^ (i * 0x9E3779B97F4A7C15ull))};
+    if (config == 3) {
+        (void)r.uni();
+        const int mode = (int)(r.next() & 1), region = (int)(r.next() & 3);
+        return mode * 4 + region;
+    }
+    if (config == 4) {
+        const int mode = (int)(r.next() & 7), region = (int)(r.next() & 7);
+        return mode * 8 + region;
+    }
+    return -1;
+}
+
+void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0, uint64_t pool_mask);
+
+// config: 1..5 as BASELINE.json configs[0..4], 6 = mixed.  Generates tickets [first, first+n).
 void* synth_make(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0) {
+    return synth_make_impl(config, seed, first, n, t0, ~0ull);
+}
+
+// Same, keeping only tickets whose pool bit is set in pool_mask (pool-sharded
+// multi-GPU runs: each rank generates exactly its pools' tickets).
+void* synth_make_pools(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0, uint64_t pool_mask) {
+    return synth_make_impl(config, seed, first, n, t0, pool_mask);
+}
+
+void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, int64_t t0, uint64_t pool_mask) {
     auto* S = new Synth();
+    std::vector<uint64_t> idx;
+    idx.reserve((size_t)n_all);
+    for (int64_t k = 0; k < n_all; k++) {
+        const uint64_t i = (uint64_t)(first + k);
+        const int p = pool_mask == ~0ull ? -1 : synth_pool_of(config, seed, i);
+        if (p < 0 || ((pool_mask >> p) & 1)) idx.push_back(i);
+    }
+    const int64_t n = (int64_t)idx.size();
     S->t.resize((size_t)n);
     S->pres.reserve((size_t)n * 5);
     S->sp.reserve((size_t)n * 3);
@@ -73,7 +110,7 @@ void* synth_make(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0
     struct Tmp { size_t p0, np, s0, ns, n0, nn; };
     std::vector<Tmp> tmp((size_t)n);
     for (int64_t k = 0; k < n; k++) {
-        const uint64_t i = (uint64_t)(first + k);
+        const uint64_t i = idx[(size_t)k];
         Rng r{splitmix64(seed ^ (i * 0x9E3779B97F4A7C15ull))};
         mm_ticket& t = S->t[(size_t)k];
         std::memset(&t, 0, sizeof t);
