@@ -11,6 +11,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -156,6 +157,25 @@ enum BuiltinField : uint16_t { F_TICKET = 0, F_MIN = 1, F_MAX = 2, F_PARTY = 3, 
 
 struct BGroup;  // a batch search and its hit list (mm_process.cpp)
 
+// Matched (or candidate) groups of a pass as a flat CSR of (slot, presence
+// index) entries: group g = ents[off[g], off[g+1]).
+struct GroupList {
+    using Entry = std::pair<uint32_t, int>;
+    std::vector<uint32_t> off{0};
+    std::vector<Entry> ents;
+    size_t size() const { return off.size() - 1; }
+    bool empty() const { return off.size() == 1; }
+    template <class It>
+    void push(It b, It e) {
+        ents.insert(ents.end(), b, e);
+        off.push_back((uint32_t)ents.size());
+    }
+    void push(const std::vector<Entry>& g) { push(g.begin(), g.end()); }
+    const Entry* begin(size_t g) const { return ents.data() + off[g]; }
+    const Entry* end(size_t g) const { return ents.data() + off[g + 1]; }
+    size_t len(size_t g) const { return off[g + 1] - off[g]; }
+};
+
 struct SrcChoice {  // the posting list a search streams, when it has one
     bool has_term = false;
     uint16_t field = 0;
@@ -171,6 +191,8 @@ struct PassStats {
     int refetches = 0;
     double search_ms = 0;   // host wall time of batch searches incl. H2D/D2H and stitching
     double replay_ms = 0;   // host wall time of the greedy replay
+    double assemble_ms = 0; // batch assembly (rows -> searches)
+    double apply_ms = 0;    // pushing the batch's selections to the device alive mask
     int parallel_batches = 0;
 };
 
@@ -225,6 +247,7 @@ private:
     uint32_t sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party);
     void set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val);
     void kill_slot(uint32_t slot, bool device_cleared = false);  // ticket leaves the index and the maps
+    const char* arena_string(const std::string& s);
     void maybe_compact();
     void compact();
     bool live(uint32_t slot) const { return live_[slot] != 0; }
@@ -237,16 +260,16 @@ private:
     DStore dstore() const;
 
     // ---- pass ----
-    int process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& groups, std::vector<uint32_t>& expired,
+    int process_default(GroupList& groups, std::vector<uint32_t>& expired,
                         PassStats& st);
-    int process_custom(std::vector<std::vector<std::pair<uint32_t, int>>>& cands, std::vector<uint32_t>& expired,
+    int process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                        PassStats& st);
-    void finish_pass(const std::vector<uint32_t>& expired, std::vector<std::vector<std::pair<uint32_t, int>>>& groups);
-    void fill_matched(const std::vector<std::vector<std::pair<uint32_t, int>>>& groups, mm_matched* out, bool cands);
+    void finish_pass(const std::vector<uint32_t>& expired, GroupList& groups);
+    void fill_matched(const GroupList& groups, mm_matched* out, bool cands);
     void choose_source(const Sig& s, DGroup& g, SrcChoice* ch = nullptr);
     bool replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
                          const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
-                         std::vector<std::vector<std::pair<uint32_t, int>>>& out_groups,
+                         GroupList& out_groups,
                          std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats);
     void apply_selected_to_device(const std::vector<uint32_t>& slots);
 
@@ -263,9 +286,16 @@ private:
 public:
     // ---- host SoA (per slot) ----  (public for the replay helpers)
     Dict dict_;                       // keyword values / terms / parties
-    Dict sess_dict_;                  // presence session ids
+    Dict sess_dict_;                  // presence session ids (rebuilt at compaction)
+    Dict party_dict_;                 // party ids (rebuilt at compaction)
+    // per-pass scratch, kept across passes (no page faults on the hot path)
+    std::vector<uint8_t> sel_;
+    std::vector<uint32_t> rows_, brow_, brow_group_, newly_;
     Dict field_dict_;                 // field names -> field id
     std::vector<std::string> ticket_;
+    std::vector<const char*> tk_ptr_;               // per slot: NUL-terminated ticket id in tk_blocks_
+    std::vector<std::unique_ptr<char[]>> tk_blocks_;  // stable string arena (never moves)
+    size_t tk_block_used_ = 0;
     std::vector<int64_t> created_;
     std::vector<int64_t> ckey_;       // sortable key of float64(CreatedAt)
     std::vector<int32_t> minc_, maxc_, cm_, count_, intervals_;

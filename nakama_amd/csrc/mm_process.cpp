@@ -422,7 +422,7 @@ struct Replay {
 // the pinned row order.  Returns false (nothing done) when the conditions fail.
 bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
                            const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
-                           std::vector<std::vector<std::pair<uint32_t, int>>>& out_groups,
+                           GroupList& out_groups,
                            std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats) {
     const size_t nsearch = bg.size();
     if (nsearch < 2) return false;
@@ -523,8 +523,8 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
         const uint32_t T = brow[rec.bi];
         if (rec.expired) expired.push_back(T);
         if (rec.matched) {
-            out_groups.emplace_back(outs[gi].ents.begin() + rec.off, outs[gi].ents.begin() + rec.off + rec.len);
-            for (auto& e : out_groups.back()) newly.push_back(e.first);
+            out_groups.push(outs[gi].ents.begin() + rec.off, outs[gi].ents.begin() + rec.off + rec.len);
+            for (uint32_t k2 = rec.off; k2 < rec.off + rec.len; k2++) newly.push_back(outs[gi].ents[k2].first);
         }
     }
     stats.refetches += 0;
@@ -556,14 +556,15 @@ void Core::choose_source(const Sig& s, DGroup& g, SrcChoice* ch) {
     }
 }
 
-int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& out_groups,
+int Core::process_default(GroupList& out_groups,
                           std::vector<uint32_t>& expired, PassStats& stats) {
     const uint32_t N = (uint32_t)ticket_.size();
-    std::vector<uint8_t> sel(N, 0);
+    std::vector<uint8_t>& sel = sel_;
+    sel.assign(N, 0);
     const bool rev = cfg_.rev_precision != 0;
     const int maxI = cfg_.max_intervals;
-    std::vector<uint32_t> rows;
-    rows.reserve(active_list_.size());
+    std::vector<uint32_t>& rows = rows_;
+    rows.clear();
     for (uint32_t s : active_list_)
         if (live_[s] && is_active_[s]) rows.push_back(s);
 
@@ -579,7 +580,9 @@ int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& ou
     Replay rp(*this, sel, rev, maxI, stats, st, stream_);
     std::vector<int32_t> sig_group(sigs_.size(), -1);
     std::vector<BGroup> bg;
-    std::vector<uint32_t> brow, brow_group, newly;
+    std::vector<uint32_t>& brow = brow_;
+    std::vector<uint32_t>& brow_group = brow_group_;
+    std::vector<uint32_t>& newly = newly_;
     std::vector<std::pair<uint32_t, int>> grp;
     const uint32_t kvar = (uint32_t)var_k_capacity();
     size_t pos = 0;
@@ -590,6 +593,7 @@ int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& ou
         while (pos < rows.size() && sel[rows[pos]]) pos++;
         if (pos >= rows.size()) break;
         // ---- assemble the batch ----
+        const auto ta0 = std::chrono::steady_clock::now();
         for (auto& g : bg)
             if (!rev) sig_group[g.sig] = -1;
         bg.clear();
@@ -647,6 +651,7 @@ int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& ou
             }
         }
         auto tb0 = std::chrono::steady_clock::now();
+        stats.assemble_ms += std::chrono::duration<double, std::milli>(tb0 - ta0).count();
         rp.run_batch(bg, need_pm);
         auto tb1 = std::chrono::steady_clock::now();
         stats.search_ms += std::chrono::duration<double, std::milli>(tb1 - tb0).count();
@@ -656,8 +661,10 @@ int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& ou
         bool exhausted = false;
         if (!rev && replay_parallel(bg, brow, brow_group, sel, out_groups, expired, newly, stats)) {
             stats.parallel_batches++;
-            stats.replay_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb1).count();
+            const auto tr = std::chrono::steady_clock::now();
+            stats.replay_ms += std::chrono::duration<double, std::milli>(tr - tb1).count();
             apply_selected_to_device(newly);
+            stats.apply_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
             pos = q;
             retry_slot = kNoSlot;
             continue;
@@ -680,7 +687,7 @@ int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& ou
                         newly.push_back(e.first);
                     }
                 }
-                out_groups.push_back(grp);
+                out_groups.push(grp);
             }
             done = bi + 1;
         }
@@ -699,7 +706,7 @@ int Core::process_default(std::vector<std::vector<std::pair<uint32_t, int>>>& ou
 }
 
 // processCustom (matchmaker_process.go:336-612), up to the override call.
-int Core::process_custom(std::vector<std::vector<std::pair<uint32_t, int>>>& cands, std::vector<uint32_t>& expired,
+int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                          PassStats& stats) {
     const bool rev = cfg_.rev_precision != 0;
     const int maxI = cfg_.max_intervals;
@@ -850,7 +857,7 @@ int Core::process_custom(std::vector<std::vector<std::pair<uint32_t, int>>>& can
                 for (uint32_t el : combo)
                     for (int k = 0; k < count_[hits[el]]; k++) me.push_back({hits[el], k});
                 for (int k = 0; k < count_[T]; k++) me.push_back({T, k});
-                cands.push_back(std::move(me));
+                cands.push(me);
             }
         }
     }
@@ -858,19 +865,29 @@ int Core::process_custom(std::vector<std::vector<std::pair<uint32_t, int>>>& can
 }
 
 // Process() post-pass (matchmaker.go:320-372).
-void Core::finish_pass(const std::vector<uint32_t>& expired, std::vector<std::vector<std::pair<uint32_t, int>>>& groups) {
+void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups) {
     for (uint32_t s : expired) is_active_[s] = 0;
-    for (size_t i = 0; i < groups.size(); i++) {
+    // group order after the reference's swap-removes of incomplete groups
+    std::vector<uint32_t> order(groups.size());
+    for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
+    bool removed = false;
+    for (size_t i = 0; i < order.size(); i++) {
         bool incomplete = false;
-        for (auto& e : groups[i])
-            if (e.first == kNoSlot || !live_[e.first]) { incomplete = true; break; }
+        for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
+            if (e->first == kNoSlot || !live_[e->first]) { incomplete = true; break; }
         if (incomplete) {  // swap-remove (:337-341)
-            groups[i] = std::move(groups.back());
-            groups.pop_back();
+            order[i] = order.back();
+            order.pop_back();
+            removed = true;
             i--;
             continue;
         }
-        for (auto& e : groups[i]) kill_slot(e.first, true);
+        for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e) kill_slot(e->first, true);
+    }
+    if (removed) {
+        GroupList kept;
+        for (uint32_t g : order) kept.push(groups.begin(g), groups.end(g));
+        groups = std::move(kept);
     }
     size_t w = 0;
     for (uint32_t s : active_list_)
@@ -878,51 +895,51 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, std::vector<std::ve
     active_list_.resize(w);
 }
 
-void Core::fill_matched(const std::vector<std::vector<std::pair<uint32_t, int>>>& groups, mm_matched* out,
+void Core::fill_matched(const GroupList& groups, mm_matched* out,
                         bool cands) {
-    size_t n = 0, bytes = 0;
-    for (auto& g : groups) {
-        n += g.size();
-        for (auto& e : g) bytes += (e.first < ticket_.size() ? ticket_[e.first].size() : 0) + 1;
-    }
-    // Reuse the handle's arena when no earlier result is outstanding (its pages
-    // stay mapped: no page-fault storm per pass); otherwise allocate.
-    bool arena = !out_in_use_.exchange(true);
+    const size_t n = groups.ents.size();
+    // The handle's arena (reused: its pages stay mapped) points entries at the
+    // store's ticket-string arena, which does not move while the result is
+    // outstanding (compaction waits for mm_free_matched).  A second
+    // outstanding result gets private copies.
+    const bool arena = !out_in_use_.exchange(true);
     int32_t* offs;
     mm_entry_ref* ents;
-    char* buf;
+    char* buf = nullptr;
     if (arena) {
         if (out_offs_.size() < groups.size() + 1) out_offs_.resize(groups.size() + 1);
         if (out_ents_.size() < std::max<size_t>(n, 1)) out_ents_.resize(std::max<size_t>(n, 1));
-        if (out_chars_.size() < std::max<size_t>(bytes, 1)) out_chars_.resize(std::max<size_t>(bytes, 1));
         offs = out_offs_.data();
         ents = out_ents_.data();
-        buf = out_chars_.data();
     } else {
+        size_t bytes = 0;
+        for (auto& e : groups.ents) bytes += ticket_[e.first].size() + 1;
         offs = new int32_t[groups.size() + 1];
         ents = new mm_entry_ref[n ? n : 1];
         buf = new char[bytes ? bytes : 1];
     }
-    size_t k = 0, b = 0;
-    offs[0] = 0;
-    for (size_t gi = 0; gi < groups.size(); gi++) {
-        uint32_t prev = kNoSlot;
-        const char* prev_p = nullptr;
-        for (auto& e : groups[gi]) {
-            if (e.first != prev) {  // a ticket's entries are adjacent: one string copy per ticket
+    size_t b = 0;
+    for (size_t gi = 0; gi <= groups.size(); gi++) offs[gi] = (int32_t)groups.off[gi];
+    uint32_t prev = kNoSlot;
+    const char* prev_p = nullptr;
+    for (size_t k = 0; k < n; k++) {
+        const auto& e = groups.ents[k];
+        if (e.first != prev) {
+            if (arena) {
+                prev_p = tk_ptr_[e.first];
+            } else {
                 const std::string& t = ticket_[e.first];
                 std::memcpy(buf + b, t.c_str(), t.size() + 1);
                 prev_p = buf + b;
-                prev = e.first;
                 b += t.size() + 1;
             }
-            ents[k].ticket = prev_p;
-            ents[k].presence_index = e.second;
-            ents[k].reserved = 0;
-            k++;
+            prev = e.first;
         }
-        offs[gi + 1] = (int32_t)k;
+        ents[k].ticket = prev_p;
+        ents[k].presence_index = e.second;
+        ents[k].reserved = 0;
     }
+    const size_t k = n;
     out->n_groups = (int32_t)groups.size();
     out->n_entries = (int32_t)k;
     out->group_offsets = offs;
@@ -950,7 +967,7 @@ int Core::process(mm_matched* out) {
     if (custom_open_) return MM_ERR_STATE;
     uint32_t n_active = 0;
     for (uint32_t s : active_list_) n_active += live_[s] && is_active_[s];
-    std::vector<std::vector<std::pair<uint32_t, int>>> groups;
+    GroupList groups;
     if (n_active == 0) {  // matchmaker.go:294-298
         fill_matched(groups, out, false);
         return MM_OK;
@@ -969,7 +986,7 @@ int Core::process(mm_matched* out) {
         process_custom(groups, expired, stats);
         out->n_expired = (int32_t)expired.size();
         if (groups.empty()) {
-            std::vector<std::vector<std::pair<uint32_t, int>>> none;
+            GroupList none;
             finish_pass(expired, none);
             fill_matched(none, out, false);
         } else {
@@ -989,12 +1006,14 @@ int Core::process(mm_matched* out) {
         if (std::getenv("NKM_PROFILE")) {
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
             std::fprintf(stderr,
-                         "[nkm] sync %.2f ms | pass %.2f ms (search %.2f ms [kernel %.2f ms], replay %.2f ms, "
-                         "%d batches (%d parallel), %d refetches, %d launches) | finish %.2f ms | fill %.2f ms | "
-                         "groups %zu\n",
-                         ms(t0, t1), ms(t1, t2), stats.search_ms, stats.eval_ms, stats.replay_ms, stats.batches,
+                         "[nkm] sync %.2f ms | pass %.2f ms (assemble %.2f, search %.2f ms [kernel %.2f ms], replay %.2f "
+                         "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches) | finish %.2f ms | "
+                         "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu\n",
+                         ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms, stats.replay_ms,
+                         stats.apply_ms, stats.batches,
                          stats.parallel_batches, stats.refetches, stats.launches, ms(t2, t3), ms(t3, t4),
-                         groups.size());
+                         groups.size(), ticket_.size(), n_live_, active_list_.size(), sigs_.size(),
+                         dict_.str.size());
         }
     }
     out->eval_ms = stats.eval_ms;
@@ -1010,14 +1029,14 @@ int Core::process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t 
     std::memset(out, 0, sizeof(*out));
     std::lock_guard<std::mutex> lk(mu_);
     if (!custom_open_) return MM_ERR_STATE;
-    std::vector<std::vector<std::pair<uint32_t, int>>> groups;
+    GroupList groups;
     for (int g = 0; g < n_groups; g++) {
         std::vector<std::pair<uint32_t, int>> grp;
         for (int k = offs[g]; k < offs[g + 1]; k++) {
             int64_t s = slot_of_ticket(ents[k].ticket ? ents[k].ticket : "");
             grp.push_back({s < 0 ? kNoSlot : (uint32_t)s, ents[k].presence_index});
         }
-        groups.push_back(std::move(grp));
+        groups.push(grp);
     }
     // processCustom never deletes from the index during the pass; matched
     // tickets leave it here (their zombie documents would be filtered as

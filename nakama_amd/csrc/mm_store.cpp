@@ -154,6 +154,20 @@ static void doc_props(Core& c, const Cold& cold, std::vector<std::pair<uint16_t,
     for (auto& k : keys) out.push_back({(c.*field_of_fn)("properties." + k), merged[k]});
 }
 
+// Copies s into the ticket-string arena (1 MiB blocks that never move).
+const char* Core::arena_string(const std::string& s) {
+    constexpr size_t kBlock = 1 << 20;
+    const size_t need = s.size() + 1;
+    if (tk_blocks_.empty() || tk_block_used_ + need > kBlock) {
+        tk_blocks_.emplace_back(new char[std::max(kBlock, need)]);
+        tk_block_used_ = 0;
+    }
+    char* p = tk_blocks_.back().get() + tk_block_used_;
+    std::memcpy(p, s.c_str(), need);
+    tk_block_used_ += need;
+    return p;
+}
+
 void Core::set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val) {
     fkind_[f][slot] = kind;
     fval_[f][slot] = val;
@@ -302,6 +316,7 @@ int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_inse
                                   p.username ? p.username : "", p.node ? p.node : ""});
     }
     ticket_.push_back(tk);
+    tk_ptr_.push_back(arena_string(tk));
     created_.push_back(t.created_at);
     ckey_.push_back(sortable_i64((double)t.created_at));
     minc_.push_back(t.min_count);
@@ -309,7 +324,7 @@ int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_inse
     cm_.push_back(t.count_multiple);
     count_.push_back(t.n_presences);
     intervals_.push_back(from_insert ? t.intervals : 0);
-    uint32_t party = cold.party_id.empty() ? kNoParty : dict_.intern(cold.party_id);
+    uint32_t party = cold.party_id.empty() ? kNoParty : party_dict_.intern(cold.party_id);
     party_.push_back(party);
     live_.push_back(1);
     bool act = from_insert ? (t.intervals < cfg_.max_intervals) : true;
@@ -395,7 +410,7 @@ int Core::add(const mm_ticket& t) {
     }
     std::string party = t.party_id ? t.party_id : "";
     if (!party.empty()) {
-        int64_t pid = dict_.find(party);
+        int64_t pid = party_dict_.find(party);
         if (pid >= 0 && (int)party_slots_.count((uint32_t)pid) >= cfg_.max_tickets) return MM_ERR_TOO_MANY_TICKETS;
     }
     maybe_compact();
@@ -502,7 +517,7 @@ int Core::remove_party(const std::string& pid, const std::string& ticket) {
 // RemovePartyAll (matchmaker.go:872-917)
 int Core::remove_party_all(const std::string& pid) {
     std::lock_guard<std::mutex> lk(mu_);
-    int64_t id = dict_.find(pid);
+    int64_t id = party_dict_.find(pid);
     if (id < 0 || pid.empty()) return MM_OK;
     for (uint32_t s : party_slots_.list((uint32_t)id)) kill_slot(s);
     return MM_OK;
@@ -539,6 +554,8 @@ int32_t Core::active_count() {
 
 void Core::maybe_compact() {
     size_t n = ticket_.size();
+    // a process result still held by the caller points into the string arena
+    if (out_in_use_.load()) return;
     if (n >= 65536 && n > 2 * (size_t)n_live_) compact();
 }
 
@@ -576,6 +593,18 @@ void Core::compact() {
         if (fval_[f].size() == n) { keep(fval_[f]); keep(fkind_[f]); }
     }
     live_.assign(m, 1);
+    // party dictionary: live parties only
+    {
+        Dict np;
+        for (uint32_t s = 0; s < m; s++)
+            party_[s] = cold_[s].party_id.empty() ? kNoParty : np.intern(cold_[s].party_id);
+        party_dict_ = std::move(np);
+    }
+    // string arena: live ticket ids only
+    tk_blocks_.clear();
+    tk_block_used_ = 0;
+    tk_ptr_.resize(m);
+    for (uint32_t s = 0; s < m; s++) tk_ptr_[s] = arena_string(ticket_[s]);
     // maps
     slot_of_.clear();
     for (uint32_t s = 0; s < m; s++) slot_of_[ticket_[s]] = s;
