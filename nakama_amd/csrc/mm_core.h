@@ -10,10 +10,13 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -107,12 +110,93 @@ struct Sig {
 
 // key id -> set of slots, optimised for the common one-slot case
 // (sessionTickets / partyTickets, matchmaker.go:201-204).
+// Persistent host workers for the pass's data-parallel host phases (pool
+// replay, post-pass bookkeeping): run(n, fn) calls fn(0..n-1) over the
+// workers and the caller, and returns when all n tasks are done.
+class WorkPool {
+public:
+    explicit WorkPool(unsigned n_threads) {
+        for (unsigned i = 0; i + 1 < n_threads; i++) th_.emplace_back([this] { loop(); });
+    }
+    ~WorkPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    unsigned size() const { return (unsigned)th_.size() + 1; }
+    void run(size_t n, const std::function<void(size_t)>& fn) {
+        if (n == 0) return;
+        if (n == 1 || th_.empty()) {
+            for (size_t i = 0; i < n; i++) fn(i);
+            return;
+        }
+        // A job is shared with the workers: one that wakes late only sees an
+        // exhausted counter and never touches fn.
+        auto job = std::make_shared<Job>(&fn, n);
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = job;
+            gen_++;
+        }
+        cv_.notify_all();
+        work(*job);
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return job->done.load() == n; });
+        job_.reset();
+    }
+
+private:
+    struct Job {
+        Job(const std::function<void(size_t)>* f, size_t count) : fn(f), n(count) {}
+        const std::function<void(size_t)>* fn;
+        const size_t n;
+        std::atomic<size_t> next{0}, done{0};
+    };
+    void work(Job& j) {
+        size_t mine = 0;
+        for (;;) {
+            const size_t i = j.next.fetch_add(1);
+            if (i >= j.n) break;
+            (*j.fn)(i);
+            mine++;
+        }
+        if (mine && j.done.fetch_add(mine) + mine == j.n) {
+            std::lock_guard<std::mutex> lk(m_);
+            done_cv_.notify_all();
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            std::shared_ptr<Job> j;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+                j = job_;
+            }
+            if (j) work(*j);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    std::shared_ptr<Job> job_;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
+
 struct SlotSets {
     std::vector<uint32_t> first;
     std::unordered_map<uint32_t, std::vector<uint32_t>> more;
     void ensure(uint32_t key) { if (key >= first.size()) first.resize(key + 1, kNoSlot); }
     size_t count(uint32_t key) const {
         if (key >= first.size() || first[key] == kNoSlot) return 0;
+        if (more.empty()) return 1;
         auto it = more.find(key);
         return 1 + (it == more.end() ? 0 : it->second.size());
     }
@@ -123,6 +207,10 @@ struct SlotSets {
     }
     void erase(uint32_t key, uint32_t slot) {
         if (key >= first.size() || first[key] == kNoSlot) return;
+        if (more.empty()) {  // common case: every key holds one slot
+            if (first[key] == slot) first[key] = kNoSlot;
+            return;
+        }
         auto it = more.find(key);
         if (first[key] == slot) {
             if (it == more.end()) { first[key] = kNoSlot; return; }
@@ -171,6 +259,10 @@ struct GroupList {
         off.push_back((uint32_t)ents.size());
     }
     void push(const std::vector<Entry>& g) { push(g.begin(), g.end()); }
+    void reserve_more(size_t groups, size_t entries) {  // geometric, so repeated calls stay linear
+        if (off.capacity() < off.size() + groups) off.reserve(std::max(off.size() + groups, 2 * off.capacity()));
+        if (ents.capacity() < ents.size() + entries) ents.reserve(std::max(ents.size() + entries, 2 * ents.capacity()));
+    }
     const Entry* begin(size_t g) const { return ents.data() + off[g]; }
     const Entry* end(size_t g) const { return ents.data() + off[g + 1]; }
     size_t len(size_t g) const { return off[g + 1] - off[g]; }
@@ -194,6 +286,7 @@ struct PassStats {
     double assemble_ms = 0; // batch assembly (rows -> searches)
     double apply_ms = 0;    // pushing the batch's selections to the device alive mask
     int parallel_batches = 0;
+    double par_bucket_ms = 0, par_work_ms = 0, par_merge_ms = 0;  // parallel replay phases
 };
 
 // Algorithmic HBM bytes of one search (DESIGN.md "Roofline"): every scanned
@@ -264,7 +357,8 @@ private:
                         PassStats& st);
     int process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                        PassStats& st);
-    void finish_pass(const std::vector<uint32_t>& expired, GroupList& groups);
+    void finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, bool disjoint);
+    void finish_pass_serial(GroupList& groups);
     void fill_matched(const GroupList& groups, mm_matched* out, bool cands);
     void choose_source(const Sig& s, DGroup& g, SrcChoice* ch = nullptr);
     bool replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
@@ -282,6 +376,9 @@ private:
     int device_ = 0;
     hipStream_t stream_ = nullptr;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+    std::unique_ptr<WorkPool> workers_;  // created on the first large pass
+    WorkPool& workers();
+    size_t par_min(size_t auto_min) const { return par_mode_ == 2 ? 0 : auto_min; }
 
 public:
     // ---- host SoA (per slot) ----  (public for the replay helpers)
@@ -362,6 +459,10 @@ public:
 
     // ---- open custom pass ----
     bool custom_open_ = false;
+    // NKM_PARALLEL: "0" keeps every host phase serial, "force" takes the
+    // parallel paths at any size (tests), unset: parallel above the sizes
+    // where it pays.
+    int par_mode_ = 1;  // 0 off, 1 auto, 2 force
     std::vector<uint32_t> custom_expired_;
 
     std::vector<std::string> debug_strings_;

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <queue>
 
 #include "gocompat.h"
 #include "mm_core.h"
@@ -460,34 +461,62 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
     if (ng < 2) return false;
     std::vector<std::vector<uint32_t>> pool_keys(ng);
     for (auto& kv : pool_of) pool_keys[kv.second] = kv.first;
-    // every searching ticket must itself belong to its search's pool
-    for (size_t bi = 0; bi < brow.size(); bi++) {
-        const uint32_t r = brow[bi];
-        const auto& key = pool_keys[search_pool[brow_group[bi]]];
-        for (size_t k = 0; k < keyf.size(); k++)
-            if (fkind_[keyf[k]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[k]][r] != key[k]) return false;
-    }
-    // rows per pool, in batch order
+    // every searching ticket must itself belong to its search's pool; bucket
+    // the rows per pool in batch order (chunked over threads, concatenated in
+    // chunk order so each pool's list stays in batch order)
+    using clk = std::chrono::steady_clock;
+    auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto tp0 = clk::now();
+    WorkPool& wp = workers();
+    const unsigned nchunk = brow.size() >= par_min(65536) ? wp.size() : 1;
+    std::vector<std::vector<std::vector<uint32_t>>> cgrows(nchunk, std::vector<std::vector<uint32_t>>(ng));
+    std::vector<uint8_t> cbad(nchunk, 0);
+    auto bucket = [&](unsigned c) {
+        const size_t lo = brow.size() * c / nchunk, hi = brow.size() * (c + 1) / nchunk;
+        auto& gr = cgrows[c];
+        for (size_t bi = lo; bi < hi; bi++) {
+            const uint32_t r = brow[bi];
+            const uint32_t p = search_pool[brow_group[bi]];
+            const auto& key = pool_keys[p];
+            for (size_t k = 0; k < keyf.size(); k++)
+                if (fkind_[keyf[k]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[k]][r] != key[k]) {
+                    cbad[c] = 1;
+                    return;
+                }
+            gr[p].push_back((uint32_t)bi);
+        }
+    };
+    wp.run(nchunk, [&](size_t c) { bucket((unsigned)c); });
+    for (unsigned c = 0; c < nchunk; c++)
+        if (cbad[c]) return false;
     std::vector<std::vector<uint32_t>> grows(ng);
-    for (size_t bi = 0; bi < brow.size(); bi++) grows[search_pool[brow_group[bi]]].push_back((uint32_t)bi);
+    if (nchunk == 1) {
+        grows.swap(cgrows[0]);
+    } else {
+        for (size_t p = 0; p < ng; p++) {
+            size_t tot = 0;
+            for (unsigned c = 0; c < nchunk; c++) tot += cgrows[c][p].size();
+            grows[p].reserve(tot);
+            for (unsigned c = 0; c < nchunk; c++) grows[p].insert(grows[p].end(), cgrows[c][p].begin(), cgrows[c][p].end());
+        }
+    }
     struct Rec { uint32_t bi; uint8_t matched; uint8_t expired; uint32_t off, len; };
     struct Out { std::vector<Rec> recs; std::vector<std::pair<uint32_t, int>> ents; };
     std::vector<Out> outs(ng);
     std::vector<uint32_t> order_g(ng);
     for (size_t i = 0; i < ng; i++) order_g[i] = (uint32_t)i;
     std::sort(order_g.begin(), order_g.end(), [&](uint32_t a, uint32_t b) { return grows[a].size() > grows[b].size(); });
-    std::atomic<size_t> next{0};
     const DStore st = dstore();
     const int maxI = cfg_.max_intervals;
-    auto worker = [&]() {
+    const auto tp1 = clk::now();
+    auto worker = [&](size_t k) {
         PassStats ls;
         Replay rp(*this, sel, false, maxI, ls, st, stream_);
         std::vector<std::pair<uint32_t, int>> grp;
-        for (;;) {
-            const size_t k = next.fetch_add(1);
-            if (k >= ng) break;
+        {
             const uint32_t gi = order_g[k];
             Out& o = outs[gi];
+            o.recs.reserve(grows[gi].size() / 4 + 16);
             for (uint32_t bi : grows[gi]) {
                 const uint32_t T = brow[bi];
                 if (sel[T]) continue;
@@ -507,27 +536,35 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
             }
         }
     };
-    unsigned nt = std::min<unsigned>((unsigned)ng, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
-    std::vector<std::thread> th;
-    for (unsigned t = 1; t < nt; t++) th.emplace_back(worker);
-    worker();
-    for (auto& t : th) t.join();
-    // merge back into the pinned row order
-    std::vector<std::pair<uint32_t, uint32_t>> at(brow.size(), {UINT32_MAX, 0});  // bi -> (group, record)
-    for (uint32_t gi = 0; gi < ng; gi++)
-        for (uint32_t k = 0; k < outs[gi].recs.size(); k++) at[outs[gi].recs[k].bi] = {gi, k};
-    for (size_t bi = 0; bi < brow.size(); bi++) {
-        const uint32_t gi = at[bi].first, k = at[bi].second;
-        if (gi == UINT32_MAX) continue;
-        const Rec& rec = outs[gi].recs[k];
+    wp.run(ng, worker);
+    const auto tp2 = clk::now();
+    // k-way merge of the per-pool record streams (each ascending in batch
+    // index) back into the pinned row order
+    size_t nrec = 0, nent = 0;
+    for (auto& o : outs) nrec += o.recs.size(), nent += o.ents.size();
+    out_groups.reserve_more(nrec, nent);
+    std::vector<size_t> head(ng, 0);
+    using HE = std::pair<uint32_t, uint32_t>;  // (batch index, pool)
+    std::priority_queue<HE, std::vector<HE>, std::greater<HE>> heap;
+    for (uint32_t g = 0; g < ng; g++)
+        if (!outs[g].recs.empty()) heap.push({outs[g].recs[0].bi, g});
+    while (!heap.empty()) {
+        const uint32_t gi = heap.top().second;
+        heap.pop();
+        const Rec& rec = outs[gi].recs[head[gi]++];
+        if (head[gi] < outs[gi].recs.size()) heap.push({outs[gi].recs[head[gi]].bi, gi});
         const uint32_t T = brow[rec.bi];
         if (rec.expired) expired.push_back(T);
         if (rec.matched) {
-            out_groups.push(outs[gi].ents.begin() + rec.off, outs[gi].ents.begin() + rec.off + rec.len);
+            auto b = outs[gi].ents.begin() + rec.off;
+            out_groups.push(b, b + rec.len);
             for (uint32_t k2 = rec.off; k2 < rec.off + rec.len; k2++) newly.push_back(outs[gi].ents[k2].first);
         }
     }
-    stats.refetches += 0;
+    const auto tp3 = clk::now();
+    stats.par_bucket_ms += msd(tp0, tp1);
+    stats.par_work_ms += msd(tp1, tp2);
+    stats.par_merge_ms += msd(tp2, tp3);
     return true;
 }
 
@@ -659,7 +696,7 @@ int Core::process_default(GroupList& out_groups,
         newly.clear();
         size_t done = 0;
         bool exhausted = false;
-        if (!rev && replay_parallel(bg, brow, brow_group, sel, out_groups, expired, newly, stats)) {
+        if (!rev && par_mode_ && replay_parallel(bg, brow, brow_group, sel, out_groups, expired, newly, stats)) {
             stats.parallel_batches++;
             const auto tr = std::chrono::steady_clock::now();
             stats.replay_ms += std::chrono::duration<double, std::milli>(tr - tb1).count();
@@ -865,9 +902,74 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
 }
 
 // Process() post-pass (matchmaker.go:320-372).
-void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups) {
+// Post-pass bookkeeping (matchmaker.go:320-375).  `disjoint`: no ticket is in
+// two groups (the default pass's selection guarantees it; an override's
+// groups may overlap and then follow the reference's sequential order, where
+// a group meeting an already-retired ticket is dropped).
+void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, bool disjoint) {
     for (uint32_t s : expired) is_active_[s] = 0;
-    // group order after the reference's swap-removes of incomplete groups
+    const size_t ngr = groups.size();
+    if (!disjoint || !par_mode_ || ngr < par_min(16384)) {
+        finish_pass_serial(groups);
+    } else {
+        WorkPool& wp = workers();
+        const size_t nchunk = wp.size();
+        // a group is incomplete when one of its tickets left the index
+        std::vector<uint8_t> incomplete(ngr, 0);
+        wp.run(nchunk, [&](size_t c) {
+            for (size_t g = ngr * c / nchunk; g < ngr * (c + 1) / nchunk; g++)
+                for (const auto* e = groups.begin(g); e != groups.end(g); ++e)
+                    if (e->first == kNoSlot || !live_[e->first]) { incomplete[g] = 1; break; }
+        });
+        // group order after the reference's swap-removes (:337-341)
+        std::vector<uint32_t> order(ngr);
+        for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
+        bool removed = false;
+        for (size_t i = 0; i < order.size(); i++) {
+            if (incomplete[order[i]]) {
+                order[i] = order.back();
+                order.pop_back();
+                removed = true;
+                i--;
+            }
+        }
+        if (removed) {
+            GroupList kept;
+            for (uint32_t g : order) kept.push(groups.begin(g), groups.end(g));
+            groups = std::move(kept);
+        }
+        // Retire the matched tickets.  When no session or party holds more
+        // than one ticket, each slot's bookkeeping touches keys no other slot
+        // does, so chunks of whole groups retire in parallel.
+        if (sess_slots_.more.empty() && party_slots_.more.empty()) {
+            const size_t ng2 = groups.size();
+            std::vector<uint32_t> killed(nchunk, 0);
+            wp.run(nchunk, [&](size_t c) {
+                uint32_t k = 0;
+                const size_t e0 = groups.off[ng2 * c / nchunk], e1 = groups.off[ng2 * (c + 1) / nchunk];
+                for (size_t i = e0; i < e1; i++) {
+                    const uint32_t s = groups.ents[i].first;
+                    if (!live_[s]) continue;  // a ticket's presence entries repeat its slot
+                    live_[s] = 0;
+                    is_active_[s] = 0;
+                    k++;
+                    for (uint32_t p = pres_off_[s]; p < pres_off_[s + 1]; p++) sess_slots_.erase(pres_sess_[p], s);
+                    if (party_[s] != kNoParty) party_slots_.erase(party_[s], s);
+                }
+                killed[c] = k;
+            });
+            for (uint32_t k : killed) n_live_ -= k;
+        } else {
+            for (auto& e : groups.ents) kill_slot(e.first, true);
+        }
+    }
+    size_t w = 0;
+    for (uint32_t s : active_list_)
+        if (live_[s] && is_active_[s]) active_list_[w++] = s;
+    active_list_.resize(w);
+}
+
+void Core::finish_pass_serial(GroupList& groups) {
     std::vector<uint32_t> order(groups.size());
     for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
     bool removed = false;
@@ -889,10 +991,6 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups) 
         for (uint32_t g : order) kept.push(groups.begin(g), groups.end(g));
         groups = std::move(kept);
     }
-    size_t w = 0;
-    for (uint32_t s : active_list_)
-        if (live_[s] && is_active_[s]) active_list_[w++] = s;
-    active_list_.resize(w);
 }
 
 void Core::fill_matched(const GroupList& groups, mm_matched* out,
@@ -987,7 +1085,7 @@ int Core::process(mm_matched* out) {
         out->n_expired = (int32_t)expired.size();
         if (groups.empty()) {
             GroupList none;
-            finish_pass(expired, none);
+            finish_pass(expired, none, true);
             fill_matched(none, out, false);
         } else {
             custom_open_ = true;
@@ -999,7 +1097,7 @@ int Core::process(mm_matched* out) {
         process_default(groups, expired, stats);
         const auto t2 = std::chrono::steady_clock::now();
         out->n_expired = (int32_t)expired.size();
-        finish_pass(expired, groups);
+        finish_pass(expired, groups, true);
         const auto t3 = std::chrono::steady_clock::now();
         fill_matched(groups, out, false);
         const auto t4 = std::chrono::steady_clock::now();
@@ -1008,12 +1106,13 @@ int Core::process(mm_matched* out) {
             std::fprintf(stderr,
                          "[nkm] sync %.2f ms | pass %.2f ms (assemble %.2f, search %.2f ms [kernel %.2f ms], replay %.2f "
                          "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches) | finish %.2f ms | "
-                         "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu\n",
+                         "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu | par bucket %.2f work %.2f "
+                         "merge %.2f ms\n",
                          ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms, stats.replay_ms,
                          stats.apply_ms, stats.batches,
                          stats.parallel_batches, stats.refetches, stats.launches, ms(t2, t3), ms(t3, t4),
                          groups.size(), ticket_.size(), n_live_, active_list_.size(), sigs_.size(),
-                         dict_.str.size());
+                         dict_.str.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms);
         }
     }
     out->eval_ms = stats.eval_ms;
@@ -1042,7 +1141,7 @@ int Core::process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t 
     // tickets leave it here (their zombie documents would be filtered as
     // "missing index" by later passes, matchmaker_process.go:432-437).
     std::vector<uint32_t> exp = custom_expired_;
-    finish_pass(exp, groups);
+    finish_pass(exp, groups, false);
     custom_open_ = false;
     custom_expired_.clear();
     fill_matched(groups, out, false);

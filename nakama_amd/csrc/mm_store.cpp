@@ -5,7 +5,9 @@
 // server/match_common.go:78-212 (document field mapping).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <sched.h>
 #include <unordered_set>
 
 #include "gocompat.h"
@@ -77,6 +79,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     NKM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     NKM_HIP(hipEventCreate(&ev0_));
     NKM_HIP(hipEventCreate(&ev1_));
+    if (const char* e = std::getenv("NKM_PARALLEL")) par_mode_ = !std::strcmp(e, "0") ? 0 : !std::strcmp(e, "force") ? 2 : 1;
     for (int f = 0; f < F_NBUILTIN; f++) field_dict_.intern(kBuiltinNames[f]);
     fval_.resize(F_NBUILTIN);
     fkind_.resize(F_NBUILTIN);
@@ -87,7 +90,22 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     dev_field_slots_.assign(F_NBUILTIN, 0);
 }
 
+// Host worker count: NKM_THREADS, else the visible cores capped at 16 (the
+// per-GPU host share on an 8-GPU node).
+WorkPool& Core::workers() {
+    if (!workers_) {
+        unsigned n = std::thread::hardware_concurrency();
+        cpu_set_t cs;
+        if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = (unsigned)CPU_COUNT(&cs);
+        n = std::max(1u, std::min(16u, n));
+        if (const char* e = std::getenv("NKM_THREADS")) n = std::max(1, std::atoi(e));
+        workers_.reset(new WorkPool(n));
+    }
+    return *workers_;
+}
+
 Core::~Core() {
+    workers_.reset();
     (void)hipSetDevice(device_);
     for (auto* p : d_fval_) delete p;
     for (auto* p : d_fkind_) delete p;

@@ -81,11 +81,17 @@ def test_c2_skill_window_boosts():
     run_passes(2, 1500, 2, dict(max_intervals=2))
 
 
-def test_c3_parties_5v5():
+@pytest.mark.parametrize("par", ["0", "force"])
+def test_c3_parties_5v5(par, monkeypatch):
+    """NKM_PARALLEL=0: serial host replay/bookkeeping; force: the pool-parallel
+    replay and parallel post-pass at any size."""
+    monkeypatch.setenv("NKM_PARALLEL", par)
     run_passes(3, 1500, 2, dict(max_intervals=2))
 
 
-def test_c4_many_pools():
+@pytest.mark.parametrize("par", ["0", "force"])
+def test_c4_many_pools(par, monkeypatch):
+    monkeypatch.setenv("NKM_PARALLEL", par)
     run_passes(4, 1500, 1, dict(max_intervals=2))
 
 
@@ -237,3 +243,29 @@ def test_large_pool_properties(n):
     finally:
         gpu.close()
         ts.close()
+
+
+def _product_passes(config, n, passes, par, monkeypatch):
+    monkeypatch.setenv("NKM_PARALLEL", par)
+    ts = synth.TicketSet(config, n)
+    mm = capi.Matchmaker(product_lib(), max_intervals=2)
+    try:
+        ts.insert_into(mm)
+        out = []
+        for _ in range(passes):
+            out.append(mm.Process())
+            out.append(state(mm))
+        return out
+    finally:
+        mm.close()
+        ts.close()
+
+
+@pytest.mark.parametrize("config,n", [(3, 300_000), (4, 200_000)])
+def test_parallel_host_paths_equal_serial(config, n, monkeypatch):
+    """At sizes past the oracle's reach, the pool-parallel replay and the
+    parallel post-pass give exactly the serial path's groups and state (the
+    serial path is the one checked against the oracle above)."""
+    ser = _product_passes(config, n, 2, "0", monkeypatch)
+    par = _product_passes(config, n, 2, "1", monkeypatch)
+    assert par == ser
