@@ -190,6 +190,18 @@ private:
     bool quit_ = false;
 };
 
+// The fields the greedy replay reads for every hit it walks, packed in one
+// 32-B record per slot so that a hit costs one cache line instead of one per
+// column.  Immutable while the slot lives (rebuilt at compaction).
+struct HotRec {
+    uint32_t party;     // kNoParty for ""
+    uint32_t sess0;     // session of presence 0
+    uint32_t pres_off;  // first presence in pres_sess_
+    int32_t count, minc, maxc, cm;
+    uint32_t pad;
+};
+static_assert(sizeof(HotRec) == 32, "HotRec is half a cache line");
+
 struct SlotSets {
     std::vector<uint32_t> first;
     std::unordered_map<uint32_t, std::vector<uint32_t>> more;
@@ -259,6 +271,10 @@ struct GroupList {
         off.push_back((uint32_t)ents.size());
     }
     void push(const std::vector<Entry>& g) { push(g.begin(), g.end()); }
+    void clear() {
+        off.resize(1);
+        ents.clear();
+    }
     void reserve_more(size_t groups, size_t entries) {  // geometric, so repeated calls stay linear
         if (off.capacity() < off.size() + groups) off.reserve(std::max(off.size() + groups, 2 * off.capacity()));
         if (ents.capacity() < ents.size() + entries) ents.reserve(std::max(ents.size() + entries, 2 * ents.capacity()));
@@ -266,6 +282,18 @@ struct GroupList {
     const Entry* begin(size_t g) const { return ents.data() + off[g]; }
     const Entry* end(size_t g) const { return ents.data() + off[g + 1]; }
     size_t len(size_t g) const { return off[g + 1] - off[g]; }
+};
+
+// One pool's share of a parallel replay: a record per processed row, in row
+// order, and the matched groups' entries.
+struct PoolRec {
+    uint32_t bi;  // batch row
+    uint8_t matched, expired;
+    uint32_t off, len;  // into PoolOut::ents
+};
+struct PoolOut {
+    std::vector<PoolRec> recs;
+    std::vector<std::pair<uint32_t, int>> ents;
 };
 
 struct SrcChoice {  // the posting list a search streams, when it has one
@@ -287,6 +315,8 @@ struct PassStats {
     double apply_ms = 0;    // pushing the batch's selections to the device alive mask
     int parallel_batches = 0;
     double par_bucket_ms = 0, par_work_ms = 0, par_merge_ms = 0;  // parallel replay phases
+    double par_task_max_ms = 0;
+    uint64_t par_rows = 0, par_hits = 0;
 };
 
 // Algorithmic HBM bytes of one search (DESIGN.md "Roofline"): every scanned
@@ -388,6 +418,10 @@ public:
     // per-pass scratch, kept across passes (no page faults on the hot path)
     std::vector<uint8_t> sel_;
     std::vector<uint32_t> rows_, brow_, brow_group_, newly_;
+    std::vector<uint32_t> par_rec_, par_eoff_;  // parallel replay merge, per batch row
+    GroupList pass_groups_;
+    std::vector<uint32_t> expired_;
+    std::vector<PoolOut> pool_outs_;
     Dict field_dict_;                 // field names -> field id
     std::vector<std::string> ticket_;
     std::vector<const char*> tk_ptr_;               // per slot: NUL-terminated ticket id in tk_blocks_
@@ -400,6 +434,8 @@ public:
     std::vector<uint8_t> live_;       // in m.indexes (and in the bluge index)
     std::vector<uint8_t> is_active_;  // in m.activeIndexes
     std::vector<uint32_t> sig_;
+    std::vector<HotRec> hot_;         // per slot: the replay's packed fields
+    void set_hot(uint32_t s);
     std::vector<uint32_t> pres_off_;  // CSR over presences: [slot] -> first presence
     std::vector<uint32_t> pres_sess_; // per presence: session dict id
     std::vector<Cold> cold_;

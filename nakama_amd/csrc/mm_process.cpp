@@ -21,7 +21,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
-#include <queue>
 
 #include "gocompat.h"
 #include "mm_core.h"
@@ -35,10 +34,11 @@ constexpr int kPairP = 32;  // pair matrix covers the first 32 entries of a list
 constexpr size_t kMaxBatchRows = 1u << 20;
 constexpr uint64_t kOutCap = 1ull << 24;  // max hit entries per batch (16M x 16 B)
 
-struct CE {  // combo entry: (ticket slot, presence index, list position of its hit)
+struct CE {  // combo entry: (ticket slot, presence index, list position of its hit, session)
     uint32_t slot;
     uint32_t pi;
     uint32_t lpos;
+    uint32_t sess;
 };
 
 // groupIndexes (server/matchmaker.go:132-167), int64 wrapping arithmetic.
@@ -93,18 +93,23 @@ struct Replay {
     PassStats& stats;
     DStore st;
     hipStream_t stream;
+    uint64_t hits_seen = 0;  // profiling: hit-list entries the rows walked
+    static constexpr uint32_t kPrefetch = 8;
 
     Replay(Core& core, std::vector<uint8_t>& s, bool r, int mi, PassStats& ps, DStore ds, hipStream_t sm)
         : c(core), sel(s), rev(r), max_intervals(mi), stats(ps), st(ds), stream(sm) {}
 
-    bool share_session(uint32_t a, uint32_t b) const {
-        for (uint32_t p = c.pres_off_[a]; p < c.pres_off_[a + 1]; p++)
-            for (uint32_t q = c.pres_off_[b]; q < c.pres_off_[b + 1]; q++)
+    static bool share_session(const Core& c, const HotRec& a, const HotRec& b) {
+        if (a.count == 1 && b.count == 1) return a.sess0 == b.sess0;
+        for (uint32_t p = a.pres_off; p < a.pres_off + (uint32_t)a.count; p++)
+            for (uint32_t q = b.pres_off; q < b.pres_off + (uint32_t)b.count; q++)
                 if (c.pres_sess_[p] == c.pres_sess_[q]) return true;
         return false;
     }
-    bool has_session(uint32_t slot, uint32_t sess) const {
-        for (uint32_t q = c.pres_off_[slot]; q < c.pres_off_[slot + 1]; q++)
+    bool share_session(uint32_t a, uint32_t b) const { return share_session(c, c.hot_[a], c.hot_[b]); }
+    bool has_session(const HotRec& h, uint32_t sess) const {
+        if (h.count == 1) return h.sess0 == sess;
+        for (uint32_t q = h.pres_off; q < h.pres_off + (uint32_t)h.count; q++)
             if (c.pres_sess_[q] == sess) return true;
         return false;
     }
@@ -318,13 +323,15 @@ struct Replay {
 
     // the party mustNot of the search (matchmaker_process.go:80-85)
     bool same_party(uint32_t T, uint32_t H) const {
-        return c.party_[T] != kNoParty && c.party_[H] == c.party_[T];
+        return c.party_[T] != kNoParty && c.hot_[H].party == c.party_[T];
     }
 
     // processDefault's loop body for one active ticket T.
     Status row(uint32_t T, BGroup& g, bool can_fetch, std::vector<std::pair<uint32_t, int>>& group_out) {
-        const bool last = c.intervals_[T] + 1 >= max_intervals || c.minc_[T] == c.maxc_[T];
-        const int tcount = c.count_[T], tmax = c.maxc_[T], tmin = c.minc_[T], tcm = c.cm_[T];
+        const HotRec& ht = c.hot_[T];
+        const bool last = c.intervals_[T] + 1 >= max_intervals || ht.minc == ht.maxc;
+        const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
+        const uint32_t tparty = ht.party;
         ncomb = 0;
         while (g.head < g.n && sel[g.hits[g.head].slot]) g.head++;
         for (uint32_t i = g.head;; i++) {
@@ -334,27 +341,37 @@ struct Replay {
                 fetch_more(g);
                 if (i >= g.n) { if (g.complete) break; i--; continue; }
             }
+            if (i + kPrefetch < g.n) {  // the walk's next slots
+                const uint32_t P = g.hits[i + kPrefetch].slot;
+                __builtin_prefetch(&sel[P]);
+                __builtin_prefetch(&c.hot_[P]);
+            }
             const uint32_t H = g.hits[i].slot;
-            if (H == T || sel[H] || same_party(T, H)) continue;
+            hits_seen++;
+            if (H == T || sel[H]) continue;
+            const HotRec& hh = c.hot_[H];
+            if (tparty != kNoParty && hh.party == tparty) continue;                       // :80-85
             if (rev && !g.rev[i]) continue;                                            // :139-148
-            if (tmax < c.maxc_[H] && c.intervals_[H] <= max_intervals) continue;        // :150-153
-            if (share_session(T, H)) continue;                                            // :155-165
+            if (tmax < hh.maxc && c.intervals_[H] <= max_intervals) continue;           // :150-153
+            if (share_session(c, ht, hh)) continue;                                       // :155-165
             bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
             int found = -1;
-            const int hcount = c.count_[H];
+            const int hcount = hh.count;
+            const uint32_t hp = hh.pres_off;
             for (size_t ci = 0; ci < ncomb; ci++) {
                 auto& combo = combos[ci];
                 if ((int)combo.size() + hcount + tcount <= tmax) {
                     bool mconf = false;
                     for (const CE& e : combo) {
-                        if (has_session(H, c.pres_sess_[c.pres_off_[e.slot] + e.pi])) { sconf = true; break; }
+                        if (has_session(hh, e.sess)) { sconf = true; break; }
                         if (rev) {
                             if (!pair_ok(g, i, e.lpos)) { mconf = true; break; }
                             if (c.live_[e.slot] && !pair_ok(g, e.lpos, i)) { mconf = true; break; }
                         }
                     }
                     if (sconf || mconf) continue;
-                    for (int k = 0; k < hcount; k++) combo.push_back(CE{H, (uint32_t)k, i});
+                    for (int k = 0; k < hcount; k++)
+                        combo.push_back(CE{H, (uint32_t)k, i, hcount == 1 ? hh.sess0 : c.pres_sess_[hp + k]});
                     found = (int)ci;
                     break;
                 }
@@ -363,7 +380,7 @@ struct Replay {
                 if (ncomb == combos.size()) combos.emplace_back();
                 std::vector<CE>& nc = combos[ncomb];
                 nc.clear();
-                for (int k = 0; k < hcount; k++) nc.push_back(CE{H, (uint32_t)k, i});
+                for (int k = 0; k < hcount; k++) nc.push_back(CE{H, (uint32_t)k, i, hcount == 1 ? hh.sess0 : c.pres_sess_[hp + k]});
                 found = (int)ncomb++;
             }
             std::vector<CE>& fc = combos[found];
@@ -401,7 +418,8 @@ struct Replay {
             bool failed = false;                                                           // :287-296
             for (const CE& e : fc) {
                 const uint32_t s = e.slot;
-                if (c.live_[s] && (c.minc_[s] > l || c.maxc_[s] < l || l % c.cm_[s] != 0)) { failed = true; break; }
+                const HotRec& hs = c.hot_[s];
+                if (c.live_[s] && (hs.minc > l || hs.maxc < l || l % hs.cm != 0)) { failed = true; break; }
             }
             if (failed) continue;
             group_out.clear();
@@ -500,27 +518,50 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
             for (unsigned c = 0; c < nchunk; c++) grows[p].insert(grows[p].end(), cgrows[c][p].begin(), cgrows[c][p].end());
         }
     }
-    struct Rec { uint32_t bi; uint8_t matched; uint8_t expired; uint32_t off, len; };
-    struct Out { std::vector<Rec> recs; std::vector<std::pair<uint32_t, int>> ents; };
-    std::vector<Out> outs(ng);
+    using Rec = PoolRec;
+    if (pool_outs_.size() < ng) pool_outs_.resize(ng);  // kept across passes (capacity reused)
+    auto& outs = pool_outs_;
+    for (size_t i = 0; i < ng; i++) outs[i].recs.clear(), outs[i].ents.clear();
     std::vector<uint32_t> order_g(ng);
     for (size_t i = 0; i < ng; i++) order_g[i] = (uint32_t)i;
     std::sort(order_g.begin(), order_g.end(), [&](uint32_t a, uint32_t b) { return grows[a].size() > grows[b].size(); });
     const DStore st = dstore();
     const int maxI = cfg_.max_intervals;
     const auto tp1 = clk::now();
+    std::vector<double> task_ms(ng, 0.0);
+    std::vector<uint64_t> task_hits(ng, 0), task_rows(ng, 0);
+    // Each pool walks private copies of its searches and of the selection
+    // mask: pools touch disjoint tickets, and sharing the mask's cache lines
+    // (slots of different pools interleave) would ping-pong them between
+    // cores on every selection.
+    std::vector<uint32_t> local_idx(nsearch);
+    std::vector<std::vector<uint32_t>> pool_searches(ng);
+    for (size_t i = 0; i < nsearch; i++) {
+        local_idx[i] = (uint32_t)pool_searches[search_pool[i]].size();
+        pool_searches[search_pool[i]].push_back((uint32_t)i);
+    }
     auto worker = [&](size_t k) {
+        const auto tw0 = clk::now();
         PassStats ls;
-        Replay rp(*this, sel, false, maxI, ls, st, stream_);
+        const uint32_t gi = order_g[k];
+        // The worker thread's mask is all zero between tasks.  Starting from
+        // zero is exact: this batch's rows and hit lists hold no ticket an
+        // earlier batch selected (assembly skips them; the device alive mask
+        // dropped them before this batch's searches).
+        static thread_local std::vector<uint8_t> tl_sel;
+        if (tl_sel.size() < sel.size()) tl_sel.resize(sel.size(), 0);
+        std::vector<uint8_t>& psel = tl_sel;
+        std::vector<BGroup> mine;
+        mine.reserve(pool_searches[gi].size());
+        for (uint32_t i : pool_searches[gi]) mine.push_back(bg[i]);
+        Replay rp(*this, psel, false, maxI, ls, st, stream_);
         std::vector<std::pair<uint32_t, int>> grp;
         {
-            const uint32_t gi = order_g[k];
-            Out& o = outs[gi];
-            o.recs.reserve(grows[gi].size() / 4 + 16);
+            PoolOut& o = outs[gi];
             for (uint32_t bi : grows[gi]) {
                 const uint32_t T = brow[bi];
-                if (sel[T]) continue;
-                auto status = rp.row(T, bg[brow_group[bi]], false, grp);  // complete lists: never EXHAUSTED
+                if (psel[T]) continue;
+                auto status = rp.row(T, mine[local_idx[brow_group[bi]]], false, grp);  // complete lists: never EXHAUSTED
                 intervals_[T]++;
                 Rec rec{bi, 0, (uint8_t)(intervals_[T] >= maxI || minc_[T] == maxc_[T]), 0, 0};
                 if (status == Replay::MATCHED) {
@@ -528,43 +569,86 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
                     rec.off = (uint32_t)o.ents.size();
                     rec.len = (uint32_t)grp.size();
                     for (auto& e : grp) {
-                        sel[e.first] = 1;
+                        psel[e.first] = 1;
                         o.ents.push_back(e);
                     }
                 }
                 o.recs.push_back(rec);
             }
+            for (auto& e : o.ents) psel[e.first] = 0;
+            task_ms[k] = msd(tw0, clk::now());
+            task_hits[k] = rp.hits_seen;
+            task_rows[k] = o.recs.size();
         }
     };
     wp.run(ng, worker);
     const auto tp2 = clk::now();
-    // k-way merge of the per-pool record streams (each ascending in batch
-    // index) back into the pinned row order
-    size_t nrec = 0, nent = 0;
-    for (auto& o : outs) nrec += o.recs.size(), nent += o.ents.size();
-    out_groups.reserve_more(nrec, nent);
-    std::vector<size_t> head(ng, 0);
-    using HE = std::pair<uint32_t, uint32_t>;  // (batch index, pool)
-    std::priority_queue<HE, std::vector<HE>, std::greater<HE>> heap;
-    for (uint32_t g = 0; g < ng; g++)
-        if (!outs[g].recs.empty()) heap.push({outs[g].recs[0].bi, g});
-    while (!heap.empty()) {
-        const uint32_t gi = heap.top().second;
-        heap.pop();
-        const Rec& rec = outs[gi].recs[head[gi]++];
-        if (head[gi] < outs[gi].recs.size()) heap.push({outs[gi].recs[head[gi]].bi, gi});
-        const uint32_t T = brow[rec.bi];
-        if (rec.expired) expired.push_back(T);
-        if (rec.matched) {
-            auto b = outs[gi].ents.begin() + rec.off;
-            out_groups.push(b, b + rec.len);
-            for (uint32_t k2 = rec.off; k2 < rec.off + rec.len; k2++) newly.push_back(outs[gi].ents[k2].first);
+    // Merge back into the pinned row order without a serial walk: every
+    // processed row marks its batch index, a chunked prefix sum over the batch
+    // gives each matched row its group and entry offsets, and the pools
+    // scatter their groups there.  par_rec_[bi]: 0 = not processed, else
+    // 1 + (expired) + 2 * group length.
+    const size_t nb = brow.size();
+    if (par_rec_.size() < nb) par_rec_.resize(nb), par_eoff_.resize(nb);
+    const unsigned nch = nb >= par_min(65536) ? wp.size() : 1;
+    wp.run(nch, [&](size_t c) { std::memset(par_rec_.data() + nb * c / nch, 0, (nb * (c + 1) / nch - nb * c / nch) * 4); });
+    wp.run(ng, [&](size_t gi) {
+        for (const Rec& r : outs[gi].recs) par_rec_[r.bi] = 1u + r.expired + 2u * (r.matched ? r.len : 0u);
+    });
+    struct Cnt { size_t g = 0, e = 0, x = 0; };
+    std::vector<Cnt> cnt(nch + 1);
+    wp.run(nch, [&](size_t c) {
+        Cnt k;
+        for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++) {
+            const uint32_t v = par_rec_[bi];
+            if (!v) continue;
+            const uint32_t len = (v - 1) >> 1;
+            k.g += len != 0;
+            k.e += len;
+            k.x += (v - 1) & 1;
         }
-    }
+        cnt[c + 1] = k;
+    });
+    for (unsigned c = 0; c < nch; c++) cnt[c + 1].g += cnt[c].g, cnt[c + 1].e += cnt[c].e, cnt[c + 1].x += cnt[c].x;
+    const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
+    out_groups.off.resize(g0 + 1 + cnt[nch].g);
+    out_groups.ents.resize(e0 + cnt[nch].e);
+    expired.resize(x0 + cnt[nch].x);
+    newly.resize(n0 + cnt[nch].e);
+    wp.run(nch, [&](size_t c) {
+        size_t gk = g0 + cnt[c].g, ek = cnt[c].e, xk = x0 + cnt[c].x;
+        for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++) {
+            const uint32_t v = par_rec_[bi];
+            if (!v) continue;
+            if ((v - 1) & 1) expired[xk++] = brow[bi];
+            const uint32_t len = (v - 1) >> 1;
+            if (!len) continue;
+            par_eoff_[bi] = (uint32_t)ek;
+            ek += len;
+            out_groups.off[++gk] = (uint32_t)(e0 + ek);
+        }
+    });
+    wp.run(ng, [&](size_t gi) {
+        const PoolOut& o = outs[gi];
+        for (const Rec& r : o.recs) {
+            if (!r.matched) continue;
+            const size_t at = par_eoff_[r.bi];
+            std::copy(o.ents.begin() + r.off, o.ents.begin() + r.off + r.len, out_groups.ents.begin() + e0 + at);
+            for (uint32_t k = 0; k < r.len; k++) {
+                newly[n0 + at + k] = o.ents[r.off + k].first;
+                sel[o.ents[r.off + k].first] = 1;
+            }
+        }
+    });
     const auto tp3 = clk::now();
     stats.par_bucket_ms += msd(tp0, tp1);
     stats.par_work_ms += msd(tp1, tp2);
     stats.par_merge_ms += msd(tp2, tp3);
+    for (size_t k = 0; k < ng; k++) {
+        stats.par_task_max_ms = std::max(stats.par_task_max_ms, task_ms[k]);
+        stats.par_hits += task_hits[k];
+        stats.par_rows += task_rows[k];
+    }
     return true;
 }
 
@@ -636,48 +720,135 @@ int Core::process_default(GroupList& out_groups,
         bg.clear();
         brow.clear();
         brow_group.clear();
-        uint64_t total_k = 0;
         size_t q = pos;
-        for (; q < rows.size() && brow.size() < kMaxBatchRows; q++) {
-            const uint32_t r = rows[q];
-            if (sel[r]) continue;
-            int32_t gi = rev ? -1 : sig_group[sig_[r]];
-            if (gi < 0) {
-                BGroup g;
-                g.sig = sig_[r];
-                const Sig& s = sigs_[g.sig];
-                g.d.clause_off = s.clause_off;
-                g.d.n_clauses = s.n_clauses;
-                g.d.qkind = s.qkind;
-                g.d.var_score = s.var_score ? 1 : 0;
-                g.d.tmin = s.tmin;
-                g.d.tmax = s.tmax;
-                g.d.tparty = s.tparty;
-                g.d.rev_slot = rev ? r : kNoSlot;
-                g.d.ub_key = s.ub_key;
-                g.d.has_cursor = 0;
-                SrcChoice ch;
-                choose_source(s, g.d, &ch);
-                g.has_src_term = ch.has_term;
-                g.src_field = ch.field;
-                g.src_term = ch.term;
-                g.d.k = 0;
-                g.row_slot = rev ? r : kNoSlot;
-                gi = (int32_t)bg.size();
-                bg.push_back(std::move(g));
-                if (!rev) sig_group[sig_[r]] = gi;
+        auto new_group = [&](uint32_t sig, uint32_t r) {
+            BGroup g;
+            g.sig = sig;
+            const Sig& s = sigs_[g.sig];
+            g.d.clause_off = s.clause_off;
+            g.d.n_clauses = s.n_clauses;
+            g.d.qkind = s.qkind;
+            g.d.var_score = s.var_score ? 1 : 0;
+            g.d.tmin = s.tmin;
+            g.d.tmax = s.tmax;
+            g.d.tparty = s.tparty;
+            g.d.rev_slot = rev ? r : kNoSlot;
+            g.d.ub_key = s.ub_key;
+            g.d.has_cursor = 0;
+            SrcChoice ch;
+            choose_source(s, g.d, &ch);
+            g.has_src_term = ch.has_term;
+            g.src_field = ch.field;
+            g.src_term = ch.term;
+            g.d.k = 0;
+            g.row_slot = rev ? r : kNoSlot;
+            return g;
+        };
+        // a search's hit capacity after `nrows` rows, the last with MaxCount m
+        auto cap_k = [&](const BGroup& g, uint64_t nrows, int m) {
+            const uint64_t want = nrows * (uint64_t)std::max(2, m) * 2 + 32;
+            const uint32_t k = g.d.var_score ? (uint32_t)std::min<uint64_t>(kvar, want)
+                                             : (uint32_t)std::min<uint64_t>(std::max<uint32_t>(g.d.src_len, 1), want + 224);
+            return std::max<uint32_t>(k, 1);
+        };
+        // Parallel assembly (same batch as the serial loop below): chunks of
+        // the rows count their signatures, groups are numbered in first-
+        // appearance order, and each search's capacity is the serial loop's
+        // final value.  Taken only when the batch is all remaining rows, i.e.
+        // when even an upper bound of the serial loop's running capacity
+        // total stays within kOutCap (so it would not have cut the batch).
+        auto assemble_parallel = [&]() -> bool {
+            const size_t nr = rows.size() - pos, nsig = sigs_.size();
+            if (rev || retry_slot != kNoSlot || !par_mode_ || nr < par_min(65536) || nr > kMaxBatchRows || nsig > 4096)
+                return false;
+            WorkPool& wp = workers();
+            const unsigned nch = wp.size();
+            struct Chunk {
+                std::vector<uint32_t> first, cnt;
+                std::vector<int32_t> lastm, maxm;
+                size_t n = 0;
+            };
+            std::vector<Chunk> ch(nch);
+            wp.run(nch, [&](size_t c) {
+                Chunk& k = ch[c];
+                k.cnt.assign(nsig, 0);
+                k.lastm.assign(nsig, 0);
+                k.maxm.assign(nsig, 0);
+                for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
+                    const uint32_t r = rows[i];
+                    if (sel[r]) continue;
+                    const uint32_t sg = sig_[r];
+                    if (!k.cnt[sg]++) k.first.push_back(sg);
+                    const int32_t m = std::max(2, maxc_[r]);
+                    k.lastm[sg] = m;
+                    k.maxm[sg] = std::max(k.maxm[sg], m);
+                    k.n++;
+                }
+            });
+            uint64_t bound = 0;
+            for (unsigned c = 0; c < nch; c++)
+                for (uint32_t sg : ch[c].first)
+                    if (sig_group[sg] < 0) {
+                        sig_group[sg] = (int32_t)bg.size();
+                        bg.push_back(new_group(sg, kNoSlot));
+                    }
+            for (BGroup& g : bg) {
+                uint64_t nrows = 0;
+                int32_t lastm = 0, maxm = 0;
+                for (unsigned c = 0; c < nch; c++)
+                    if (ch[c].cnt[g.sig]) {
+                        nrows += ch[c].cnt[g.sig];
+                        lastm = ch[c].lastm[g.sig];
+                        maxm = std::max(maxm, ch[c].maxm[g.sig]);
+                    }
+                g.nrows = (uint32_t)nrows;
+                g.d.k = cap_k(g, nrows, lastm);
+                bound += cap_k(g, nrows, maxm);
             }
-            BGroup& g = bg[gi];
-            g.nrows++;
-            const uint64_t want = (uint64_t)g.nrows * (uint64_t)std::max(2, maxc_[r]) * 2 + 32;
-            uint32_t k = g.d.var_score ? (uint32_t)std::min<uint64_t>(kvar, want)
-                                       : (uint32_t)std::min<uint64_t>(std::max<uint32_t>(g.d.src_len, 1), want + 224);
-            if (r == retry_slot) k = g.d.var_score ? kvar : std::max<uint32_t>(g.d.src_len, 1);
-            total_k += (uint64_t)k - g.d.k;
-            g.d.k = std::max<uint32_t>(k, 1);
-            brow.push_back(r);
-            brow_group.push_back((uint32_t)gi);
-            if (total_k > kOutCap && brow.size() > 1) { q++; break; }
+            if (bound > kOutCap) {  // the serial loop may cut this batch: let it
+                for (auto& g : bg) sig_group[g.sig] = -1;
+                bg.clear();
+                return false;
+            }
+            std::vector<size_t> at(nch + 1, 0);
+            for (unsigned c = 0; c < nch; c++) at[c + 1] = at[c] + ch[c].n;
+            brow.resize(at[nch]);
+            brow_group.resize(at[nch]);
+            wp.run(nch, [&](size_t c) {
+                size_t o = at[c];
+                for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
+                    const uint32_t r = rows[i];
+                    if (sel[r]) continue;
+                    brow[o] = r;
+                    brow_group[o] = (uint32_t)sig_group[sig_[r]];
+                    o++;
+                }
+            });
+            return true;
+        };
+        if (!assemble_parallel()) {
+            uint64_t total_k = 0;
+            for (; q < rows.size() && brow.size() < kMaxBatchRows; q++) {
+                const uint32_t r = rows[q];
+                if (sel[r]) continue;
+                int32_t gi = rev ? -1 : sig_group[sig_[r]];
+                if (gi < 0) {
+                    gi = (int32_t)bg.size();
+                    bg.push_back(new_group(sig_[r], r));
+                    if (!rev) sig_group[sig_[r]] = gi;
+                }
+                BGroup& g = bg[gi];
+                g.nrows++;
+                uint32_t k = cap_k(g, g.nrows, maxc_[r]);
+                if (r == retry_slot) k = g.d.var_score ? kvar : std::max<uint32_t>(g.d.src_len, 1);
+                total_k += (uint64_t)k - g.d.k;
+                g.d.k = k;
+                brow.push_back(r);
+                brow_group.push_back((uint32_t)gi);
+                if (total_k > kOutCap && brow.size() > 1) { q++; break; }
+            }
+        } else {
+            q = rows.size();
         }
         // ---- device search ----
         bool need_pm = false;
@@ -1017,29 +1188,42 @@ void Core::fill_matched(const GroupList& groups, mm_matched* out,
         buf = new char[bytes ? bytes : 1];
     }
     size_t b = 0;
-    for (size_t gi = 0; gi <= groups.size(); gi++) offs[gi] = (int32_t)groups.off[gi];
-    uint32_t prev = kNoSlot;
-    const char* prev_p = nullptr;
-    for (size_t k = 0; k < n; k++) {
-        const auto& e = groups.ents[k];
-        if (e.first != prev) {
-            if (arena) {
-                prev_p = tk_ptr_[e.first];
-            } else {
-                const std::string& t = ticket_[e.first];
-                std::memcpy(buf + b, t.c_str(), t.size() + 1);
-                prev_p = buf + b;
-                b += t.size() + 1;
+    if (arena && par_mode_ && n >= par_min(65536)) {  // chunks of the result in parallel
+        WorkPool& wp = workers();
+        const size_t nch = wp.size(), ng = groups.size() + 1;
+        wp.run(nch, [&](size_t c) {
+            for (size_t gi = ng * c / nch; gi < ng * (c + 1) / nch; gi++) offs[gi] = (int32_t)groups.off[gi];
+            for (size_t k = n * c / nch; k < n * (c + 1) / nch; k++) {
+                const auto& e = groups.ents[k];
+                ents[k].ticket = tk_ptr_[e.first];
+                ents[k].presence_index = e.second;
+                ents[k].reserved = 0;
             }
-            prev = e.first;
+        });
+    } else {
+        for (size_t gi = 0; gi <= groups.size(); gi++) offs[gi] = (int32_t)groups.off[gi];
+        uint32_t prev = kNoSlot;
+        const char* prev_p = nullptr;
+        for (size_t k = 0; k < n; k++) {
+            const auto& e = groups.ents[k];
+            if (e.first != prev) {
+                if (arena) {
+                    prev_p = tk_ptr_[e.first];
+                } else {
+                    const std::string& t = ticket_[e.first];
+                    std::memcpy(buf + b, t.c_str(), t.size() + 1);
+                    prev_p = buf + b;
+                    b += t.size() + 1;
+                }
+                prev = e.first;
+            }
+            ents[k].ticket = prev_p;
+            ents[k].presence_index = e.second;
+            ents[k].reserved = 0;
         }
-        ents[k].ticket = prev_p;
-        ents[k].presence_index = e.second;
-        ents[k].reserved = 0;
     }
-    const size_t k = n;
     out->n_groups = (int32_t)groups.size();
-    out->n_entries = (int32_t)k;
+    out->n_entries = (int32_t)n;
     out->group_offsets = offs;
     out->entries = ents;
     out->is_candidates = cands ? 1 : 0;
@@ -1065,7 +1249,8 @@ int Core::process(mm_matched* out) {
     if (custom_open_) return MM_ERR_STATE;
     uint32_t n_active = 0;
     for (uint32_t s : active_list_) n_active += live_[s] && is_active_[s];
-    GroupList groups;
+    GroupList& groups = pass_groups_;  // kept across passes: no page faults on the hot path
+    groups.clear();
     if (n_active == 0) {  // matchmaker.go:294-298
         fill_matched(groups, out, false);
         return MM_OK;
@@ -1078,7 +1263,8 @@ int Core::process(mm_matched* out) {
         });
         active_sorted_ = true;
     }
-    std::vector<uint32_t> expired;
+    std::vector<uint32_t>& expired = expired_;
+    expired.clear();
     PassStats stats;
     if (cfg_.override_enabled) {
         process_custom(groups, expired, stats);
@@ -1107,12 +1293,13 @@ int Core::process(mm_matched* out) {
                          "[nkm] sync %.2f ms | pass %.2f ms (assemble %.2f, search %.2f ms [kernel %.2f ms], replay %.2f "
                          "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches) | finish %.2f ms | "
                          "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu | par bucket %.2f work %.2f "
-                         "merge %.2f ms\n",
+                         "merge %.2f ms (task max %.2f ms, rows %llu, hits %llu)\n",
                          ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms, stats.replay_ms,
                          stats.apply_ms, stats.batches,
                          stats.parallel_batches, stats.refetches, stats.launches, ms(t2, t3), ms(t3, t4),
                          groups.size(), ticket_.size(), n_live_, active_list_.size(), sigs_.size(),
-                         dict_.str.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms);
+                         dict_.str.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms,
+                         stats.par_task_max_ms, (unsigned long long)stats.par_rows, (unsigned long long)stats.par_hits);
         }
     }
     out->eval_ms = stats.eval_ms;

@@ -359,6 +359,8 @@ int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_inse
         }
     }
     if (party != kNoParty) party_slots_.add(party, s);
+    hot_.emplace_back();
+    set_hot(s);
     // dense columns of referenced fields
     for (size_t f = 0; f < fval_.size(); f++) {
         if (!fval_[f].empty() || field_used_[f]) {
@@ -570,6 +572,18 @@ int32_t Core::active_count() {
     return n;
 }
 
+void Core::set_hot(uint32_t s) {
+    HotRec& h = hot_[s];
+    h.party = party_[s];
+    h.pres_off = pres_off_[s];
+    h.sess0 = pres_off_[s + 1] > pres_off_[s] ? pres_sess_[pres_off_[s]] : kNoSlot;
+    h.count = count_[s];
+    h.minc = minc_[s];
+    h.maxc = maxc_[s];
+    h.cm = cm_[s];
+    h.pad = 0;
+}
+
 void Core::maybe_compact() {
     size_t n = ticket_.size();
     // a process result still held by the caller points into the string arena
@@ -618,6 +632,8 @@ void Core::compact() {
             party_[s] = cold_[s].party_id.empty() ? kNoParty : np.intern(cold_[s].party_id);
         party_dict_ = std::move(np);
     }
+    hot_.resize(m);
+    for (uint32_t s = 0; s < m; s++) set_hot(s);
     // string arena: live ticket ids only
     tk_blocks_.clear();
     tk_block_used_ = 0;
