@@ -115,9 +115,17 @@ struct Sig {
 // workers and the caller, and returns when all n tasks are done.
 class WorkPool {
 public:
-    explicit WorkPool(unsigned n_threads) {
-        for (unsigned i = 0; i + 1 < n_threads; i++) th_.emplace_back([this] { loop(); });
+    // cpus: optional placement for the workers (worker i -> cpus[i % size]).
+    explicit WorkPool(unsigned n_threads, const std::vector<int>& cpus = {}) {
+        for (unsigned i = 0; i + 1 < n_threads; i++) {
+            const int cpu = cpus.empty() ? -1 : cpus[i % cpus.size()];
+            th_.emplace_back([this, cpu] {
+                if (cpu >= 0) pin(cpu);
+                loop();
+            });
+        }
     }
+    static void pin(int cpu);
     ~WorkPool() {
         {
             std::lock_guard<std::mutex> lk(m_);
@@ -287,9 +295,10 @@ struct GroupList {
 // One pool's share of a parallel replay: a record per processed row, in row
 // order, and the matched groups' entries.
 struct PoolRec {
-    uint32_t bi;  // batch row
+    uint32_t bi;  // batch row (UINT32_MAX: the list's end sentinel)
     uint8_t matched, expired;
-    uint32_t off, len;  // into PoolOut::ents
+    uint32_t off, len;  // into PoolOut::ents (off: entries before this row)
+    uint32_t gcum, xcum;  // matched / expired rows before this one
 };
 struct PoolOut {
     std::vector<PoolRec> recs;
@@ -418,7 +427,6 @@ public:
     // per-pass scratch, kept across passes (no page faults on the hot path)
     std::vector<uint8_t> sel_;
     std::vector<uint32_t> rows_, brow_, brow_group_, newly_;
-    std::vector<uint32_t> par_rec_, par_eoff_;  // parallel replay merge, per batch row
     GroupList pass_groups_;
     std::vector<uint32_t> expired_;
     std::vector<PoolOut> pool_outs_;

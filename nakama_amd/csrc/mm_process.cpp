@@ -94,6 +94,9 @@ struct Replay {
     DStore st;
     hipStream_t stream;
     uint64_t hits_seen = 0;  // profiling: hit-list entries the rows walked
+    // pool-parallel replay: rows this worker processed earlier in the batch,
+    // whose Intervals increments are applied after the batch (1 = one pending)
+    const uint8_t* proc = nullptr;
     static constexpr uint32_t kPrefetch = 8;
 
     Replay(Core& core, std::vector<uint8_t>& s, bool r, int mi, PassStats& ps, DStore ds, hipStream_t sm)
@@ -352,7 +355,7 @@ struct Replay {
             const HotRec& hh = c.hot_[H];
             if (tparty != kNoParty && hh.party == tparty) continue;                       // :80-85
             if (rev && !g.rev[i]) continue;                                            // :139-148
-            if (tmax < hh.maxc && c.intervals_[H] <= max_intervals) continue;           // :150-153
+            if (tmax < hh.maxc && c.intervals_[H] + (proc ? proc[H] : 0) <= max_intervals) continue;  // :150-153
             if (share_session(c, ht, hh)) continue;                                       // :155-165
             bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
             int found = -1;
@@ -551,23 +554,32 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
         static thread_local std::vector<uint8_t> tl_sel;
         if (tl_sel.size() < sel.size()) tl_sel.resize(sel.size(), 0);
         std::vector<uint8_t>& psel = tl_sel;
+        static thread_local std::vector<uint8_t> tl_proc;  // rows processed in this task
+        if (tl_proc.size() < sel.size()) tl_proc.resize(sel.size(), 0);
         std::vector<BGroup> mine;
         mine.reserve(pool_searches[gi].size());
         for (uint32_t i : pool_searches[gi]) mine.push_back(bg[i]);
         Replay rp(*this, psel, false, maxI, ls, st, stream_);
+        // Intervals stay unwritten during the walk (slots of all pools share
+        // its cache lines): a row's increment is pending in tl_proc until the
+        // merge applies it.
+        rp.proc = tl_proc.data();
         std::vector<std::pair<uint32_t, int>> grp;
         {
             PoolOut& o = outs[gi];
+            uint32_t gcum = 0, xcum = 0;
             for (uint32_t bi : grows[gi]) {
                 const uint32_t T = brow[bi];
                 if (psel[T]) continue;
                 auto status = rp.row(T, mine[local_idx[brow_group[bi]]], false, grp);  // complete lists: never EXHAUSTED
-                intervals_[T]++;
-                Rec rec{bi, 0, (uint8_t)(intervals_[T] >= maxI || minc_[T] == maxc_[T]), 0, 0};
+                tl_proc[T] = 1;
+                Rec rec{bi, 0, (uint8_t)(intervals_[T] + 1 >= maxI || minc_[T] == maxc_[T]),
+                        (uint32_t)o.ents.size(), 0, gcum, xcum};
+                xcum += rec.expired;
                 if (status == Replay::MATCHED) {
                     rec.matched = 1;
-                    rec.off = (uint32_t)o.ents.size();
                     rec.len = (uint32_t)grp.size();
+                    gcum++;
                     for (auto& e : grp) {
                         psel[e.first] = 1;
                         o.ents.push_back(e);
@@ -576,68 +588,75 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
                 o.recs.push_back(rec);
             }
             for (auto& e : o.ents) psel[e.first] = 0;
+            for (const Rec& r : o.recs) tl_proc[brow[r.bi]] = 0;
+            o.recs.push_back(Rec{UINT32_MAX, 0, 0, (uint32_t)o.ents.size(), 0, gcum, xcum});  // sentinel
             task_ms[k] = msd(tw0, clk::now());
             task_hits[k] = rp.hits_seen;
-            task_rows[k] = o.recs.size();
+            task_rows[k] = o.recs.size() - 1;
         }
     };
     wp.run(ng, worker);
     const auto tp2 = clk::now();
-    // Merge back into the pinned row order without a serial walk: every
-    // processed row marks its batch index, a chunked prefix sum over the batch
-    // gives each matched row its group and entry offsets, and the pools
-    // scatter their groups there.  par_rec_[bi]: 0 = not processed, else
-    // 1 + (expired) + 2 * group length.
+    // Merge back into the pinned row order.  The batch's row range is cut
+    // into chunks; each pool's records (ascending in batch row, with running
+    // group / entry / expiry counts) are located in every chunk by binary
+    // search, so each chunk knows its output offsets up front and merges its
+    // share of the pools' records independently.  Applies the rows' pending
+    // Intervals increments on the way.
     const size_t nb = brow.size();
-    if (par_rec_.size() < nb) par_rec_.resize(nb), par_eoff_.resize(nb);
-    const unsigned nch = nb >= par_min(65536) ? wp.size() : 1;
-    wp.run(nch, [&](size_t c) { std::memset(par_rec_.data() + nb * c / nch, 0, (nb * (c + 1) / nch - nb * c / nch) * 4); });
-    wp.run(ng, [&](size_t gi) {
-        for (const Rec& r : outs[gi].recs) par_rec_[r.bi] = 1u + r.expired + 2u * (r.matched ? r.len : 0u);
-    });
+    const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
+    std::vector<uint32_t> cut((nch + 1) * ng);  // [c][pool]: first record with bi >= chunk start
+    for (size_t c = 0; c <= nch; c++) {
+        const uint32_t lo = (uint32_t)(nb * c / nch);
+        for (size_t gi = 0; gi < ng; gi++) {
+            const auto& r = outs[gi].recs;  // sentinel at the end (bi = UINT32_MAX)
+            cut[c * ng + gi] = c == nch ? (uint32_t)(r.size() - 1)
+                                        : (uint32_t)(std::lower_bound(r.begin(), r.end(), lo,
+                                                                      [](const Rec& x, uint32_t v) { return x.bi < v; }) -
+                                                     r.begin());
+        }
+    }
     struct Cnt { size_t g = 0, e = 0, x = 0; };
-    std::vector<Cnt> cnt(nch + 1);
-    wp.run(nch, [&](size_t c) {
+    std::vector<Cnt> at(nch + 1);
+    for (size_t c = 0; c < nch; c++) {
         Cnt k;
-        for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++) {
-            const uint32_t v = par_rec_[bi];
-            if (!v) continue;
-            const uint32_t len = (v - 1) >> 1;
-            k.g += len != 0;
-            k.e += len;
-            k.x += (v - 1) & 1;
+        for (size_t gi = 0; gi < ng; gi++) {
+            const Rec& a0 = outs[gi].recs[cut[c * ng + gi]];
+            const Rec& a1 = outs[gi].recs[cut[(c + 1) * ng + gi]];
+            k.g += a1.gcum - a0.gcum;
+            k.e += a1.off - a0.off;
+            k.x += a1.xcum - a0.xcum;
         }
-        cnt[c + 1] = k;
-    });
-    for (unsigned c = 0; c < nch; c++) cnt[c + 1].g += cnt[c].g, cnt[c + 1].e += cnt[c].e, cnt[c + 1].x += cnt[c].x;
+        at[c + 1] = {at[c].g + k.g, at[c].e + k.e, at[c].x + k.x};
+    }
     const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
-    out_groups.off.resize(g0 + 1 + cnt[nch].g);
-    out_groups.ents.resize(e0 + cnt[nch].e);
-    expired.resize(x0 + cnt[nch].x);
-    newly.resize(n0 + cnt[nch].e);
+    out_groups.off.resize(g0 + 1 + at[nch].g);
+    out_groups.ents.resize(e0 + at[nch].e);
+    expired.resize(x0 + at[nch].x);
+    newly.resize(n0 + at[nch].e);
     wp.run(nch, [&](size_t c) {
-        size_t gk = g0 + cnt[c].g, ek = cnt[c].e, xk = x0 + cnt[c].x;
-        for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++) {
-            const uint32_t v = par_rec_[bi];
-            if (!v) continue;
-            if ((v - 1) & 1) expired[xk++] = brow[bi];
-            const uint32_t len = (v - 1) >> 1;
-            if (!len) continue;
-            par_eoff_[bi] = (uint32_t)ek;
-            ek += len;
-            out_groups.off[++gk] = (uint32_t)(e0 + ek);
-        }
-    });
-    wp.run(ng, [&](size_t gi) {
-        const PoolOut& o = outs[gi];
-        for (const Rec& r : o.recs) {
+        std::vector<uint32_t> head(ng), end(ng);
+        for (size_t gi = 0; gi < ng; gi++) head[gi] = cut[c * ng + gi], end[gi] = cut[(c + 1) * ng + gi];
+        size_t gk = g0 + at[c].g, ek = e0 + at[c].e, xk = x0 + at[c].x;
+        for (;;) {
+            uint32_t best = UINT32_MAX, bg_ = 0;
+            for (uint32_t gi = 0; gi < ng; gi++)
+                if (head[gi] < end[gi] && outs[gi].recs[head[gi]].bi < best) best = outs[gi].recs[head[gi]].bi, bg_ = gi;
+            if (best == UINT32_MAX) break;
+            const PoolOut& o = outs[bg_];
+            const Rec& r = o.recs[head[bg_]++];
+            const uint32_t T = brow[r.bi];
+            intervals_[T]++;  // the row's pending Intervals increment
+            if (r.expired) expired[xk++] = T;
             if (!r.matched) continue;
-            const size_t at = par_eoff_[r.bi];
-            std::copy(o.ents.begin() + r.off, o.ents.begin() + r.off + r.len, out_groups.ents.begin() + e0 + at);
             for (uint32_t k = 0; k < r.len; k++) {
-                newly[n0 + at + k] = o.ents[r.off + k].first;
-                sel[o.ents[r.off + k].first] = 1;
+                const auto& e = o.ents[r.off + k];
+                out_groups.ents[ek + k] = e;
+                newly[n0 + (ek - e0) + k] = e.first;
+                sel[e.first] = 1;
             }
+            ek += r.len;
+            out_groups.off[++gk] = (uint32_t)ek;
         }
     });
     const auto tp3 = clk::now();
