@@ -31,6 +31,11 @@ hipError_t launch_search(const DStore& st, const DGroup* d_groups, int n_groups,
 hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_t n, hipStream_t stream);
 hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, uint8_t* d_out, hipStream_t stream);
 int var_k_capacity();
+hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, DHit* d_scratch, DGroupResult* d_cres,
+                       hipStream_t stream);
+hipError_t launch_stitch(const DChunkMap* d_map, const DGroup* d_chunks, int n_chunks, const DGroupResult* d_cres,
+                         const DHit* d_scratch, DHit* d_out, hipStream_t stream);
+int scan_chunk_len();
 
 struct DeviceError {
     hipError_t err;
@@ -490,6 +495,9 @@ public:
     DevArray<uint32_t> d_order_, d_postings_;
     DevArray<DGroup> d_groups_;
     DevArray<DHit> d_out_;
+    DevArray<DHit> d_scan_;          // scan_kernel chunk outputs (stitch_kernel input)
+    DevArray<DChunkMap> d_map_;
+    PinnedArray<DChunkMap> h_map_;
     DevArray<uint8_t> d_rev_;
     DevArray<DGroupResult> d_res_;
     DevArray<uint32_t> d_slots_tmp_;

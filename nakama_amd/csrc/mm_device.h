@@ -77,6 +77,15 @@ struct DGroupResult {
     uint32_t pad;
 };
 
+// Placement of one scan chunk (scan_kernel -> stitch_kernel).
+struct DChunkMap {
+    uint32_t first;    // index of the search's first chunk
+    uint32_t start;    // chunk's first source position within the search
+    uint32_t cap;      // the search's output capacity (k)
+    uint32_t pad;
+    uint64_t dst_off;  // the search's first output entry
+};
+
 // One emitted hit.
 struct DHit {
     uint32_t slot;

@@ -223,6 +223,151 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     }
 }
 
+// ---- constant-score scan (chunked) -----------------------------------------------
+// One 256-thread workgroup per chunk of kScanJ*256 source positions of a
+// constant-score search (every hit scores the same, so the hit order is the
+// source order).  Lane-major layout: position j*256+tid is the lane's j-th
+// candidate, so every column load is one coalesced (slot ids) or gathered
+// access per j, and all kScanJ loads of a column are in flight together —
+// one memory round trip per column instead of one per 256-candidate tile.
+// Survivors are compacted in source order (ballots + one LDS exchange) into
+// the chunk's scratch region; stitch_kernel places the chunks.
+constexpr int kScanJ = 8;
+constexpr int kScanChunk = kScanJ * kBlock;
+
+__global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* __restrict__ chunks,
+                                                      DHit* __restrict__ out, DGroupResult* __restrict__ res) {
+    __shared__ uint32_t wcnt[kScanJ][kWaves];
+    __shared__ uint32_t wlive[kWaves];
+    const DGroup g = chunks[blockIdx.x];
+    const uint32_t* __restrict__ src = (g.src_kind == 0 ? st.order : st.postings) + g.src_off;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t s[kScanJ];
+    bool m[kScanJ];
+#pragma unroll
+    for (int j = 0; j < kScanJ; j++) {
+        const uint32_t i = (uint32_t)(j * kBlock + tid);
+        s[j] = i < g.src_len ? src[i] : kNoSlot;
+    }
+#pragma unroll
+    for (int j = 0; j < kScanJ; j++) m[j] = s[j] != kNoSlot && st.alive[s[j]] != 0;
+    uint32_t live = 0;
+#pragma unroll
+    for (int j = 0; j < kScanJ; j++) live += m[j];
+#pragma unroll
+    for (int j = 0; j < kScanJ; j++)
+        if (m[j]) m[j] = st.minc[s[j]] >= g.tmin && st.maxc[s[j]] <= g.tmax;
+    if (g.tparty != kNoParty) {
+#pragma unroll
+        for (int j = 0; j < kScanJ; j++)
+            if (m[j]) m[j] = st.party[s[j]] != g.tparty;
+    }
+    // parsed query (eval_parsed, one clause at a time over the lane's candidates)
+    double ms[kScanJ], ss[kScanJ];
+    bool anys[kScanJ];
+#pragma unroll
+    for (int j = 0; j < kScanJ; j++) { ms[j] = 0.0; ss[j] = 0.0; anys[j] = false; }
+    bool has_must = false, has_should = false;
+    if (g.qkind == QK_MATCHNONE) {
+#pragma unroll
+        for (int j = 0; j < kScanJ; j++) m[j] = false;
+    } else if (g.qkind != QK_MATCHALL) {
+        const DClause* __restrict__ cl = st.clauses + g.clause_off;
+        for (int c = 0; c < g.n_clauses; c++) {
+            const DClause k = cl[c];
+            has_must |= k.occur == OCC_MUST;
+            has_should |= k.occur == OCC_SHOULD;
+            const int64_t* __restrict__ fv = st.fval[k.field];
+            const uint8_t* __restrict__ fk = st.fkind[k.field];
+#pragma unroll
+            for (int j = 0; j < kScanJ; j++) {
+                if (!m[j]) continue;
+                bool h = false;
+                if (k.op != OP_FALSE) {
+                    const uint8_t kind = fk[s[j]];
+                    const int64_t val = fv[s[j]];
+                    if (k.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)k.term;
+                    else if (k.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= k.lo && val <= k.hi;
+                    else h = (kind == KIND_KEYWORD && val == (int64_t)k.term) || (kind == KIND_NUMERIC && val == k.lo);
+                }
+                if (k.occur == OCC_MUST) { if (h) ms[j] += k.score; else m[j] = false; }
+                else if (k.occur == OCC_SHOULD) { if (h) { ss[j] += k.score; anys[j] = true; } }
+                else if (h) m[j] = false;
+            }
+        }
+    }
+    int64_t key[kScanJ];
+#pragma unroll
+    for (int j = 0; j < kScanJ; j++) {
+        double sp = 1.0;  // MatchAll, or only mustNots: MatchAll(1)
+        if (g.qkind != QK_MATCHALL && (has_must || has_should)) {
+            if (!has_must) { sp = ss[j]; m[j] = m[j] && anys[j]; }
+            else sp = anys[j] ? ms[j] + ss[j] : ms[j];
+        }
+        key[j] = dsortable((sp + 1.0) + 1.0);  // top-level {parsed, min_count, max_count} conjunction
+    }
+    // ordered compaction: position j*256+tid precedes (j, tid+1) and (j+1, *)
+    uint64_t mask[kScanJ];
+#pragma unroll
+    for (int j = 0; j < kScanJ; j++) {
+        mask[j] = __ballot(m[j]);
+        if (lane == 0) wcnt[j][wave] = (uint32_t)__popcll(mask[j]);
+    }
+    uint32_t wl = live;
+    for (int o = 32; o > 0; o >>= 1) wl += __shfl_xor(wl, o);
+    if (lane == 0) wlive[wave] = wl;
+    __syncthreads();
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < kScanJ; j++) {
+        uint32_t before = 0, tot = 0;
+        for (int w = 0; w < kWaves; w++) {
+            const uint32_t v = wcnt[j][w];
+            before += (w < wave) ? v : 0;
+            tot += v;
+        }
+        if (m[j]) {
+            const uint32_t pos = run + before + (uint32_t)__popcll(mask[j] & lt_mask);
+            out[g.out_off + pos] = DHit{s[j], (uint32_t)(j * kBlock + tid), key[j]};
+        }
+        run += tot;
+    }
+    if (tid == 0) {
+        uint32_t lv = 0;
+        for (int w = 0; w < kWaves; w++) lv += wlive[w];
+        res[blockIdx.x] = DGroupResult{run, 1u, g.src_len, run, lv, 0u};
+    }
+}
+
+// Places every chunk's compacted hits at its search's output: the chunk's
+// offset is the sum of the counts of the search's earlier chunks; entries
+// past the search's capacity are dropped (the host marks it incomplete).
+__global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restrict__ map, const DGroup* __restrict__ chunks,
+                                                        const DGroupResult* __restrict__ cres,
+                                                        const DHit* __restrict__ scratch, DHit* __restrict__ out) {
+    __shared__ uint32_t wsum[kWaves];
+    const uint32_t c = blockIdx.x;
+    const DChunkMap mp = map[c];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t part = 0;
+    for (uint32_t i = mp.first + tid; i < c; i += kBlock) part += cres[i].count;
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+    if (lane == 0) wsum[wave] = part;
+    __syncthreads();
+    uint32_t prefix = 0;
+    for (int w = 0; w < kWaves; w++) prefix += wsum[w];
+    const uint32_t n = cres[c].count;
+    const uint64_t so = chunks[c].out_off;
+    for (uint32_t e = tid; e < n; e += kBlock) {
+        const uint32_t pos = prefix + e;
+        if (pos >= mp.cap) break;
+        DHit h = scratch[so + e];
+        h.idx += mp.start;
+        out[mp.dst_off + pos] = h;
+    }
+}
+
 __global__ void clear_alive_kernel(uint8_t* __restrict__ alive, const uint32_t* __restrict__ slots, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) alive[slots[i]] = 0;
@@ -289,6 +434,21 @@ hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, u
     return hipGetLastError();
 }
 
+hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, DHit* d_scratch, DGroupResult* d_cres,
+                       hipStream_t stream) {
+    if (n_chunks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(scan_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, st, d_chunks, d_scratch, d_cres);
+    return hipGetLastError();
+}
+
+hipError_t launch_stitch(const DChunkMap* d_map, const DGroup* d_chunks, int n_chunks, const DGroupResult* d_cres,
+                         const DHit* d_scratch, DHit* d_out, hipStream_t stream) {
+    if (n_chunks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(stitch_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, d_map, d_chunks, d_cres, d_scratch, d_out);
+    return hipGetLastError();
+}
+
 int var_k_capacity() { return kVarK; }
+int scan_chunk_len() { return kScanChunk; }
 
 }  // namespace nkm

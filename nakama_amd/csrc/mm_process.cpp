@@ -168,67 +168,100 @@ struct Replay {
     }
 
     // Runs one batch of searches.  Large constant-score searches are split
-    // into chunks of their source (one workgroup each, so a pool's full hit
-    // list is produced by many CUs); chunk outputs are stitched back in
-    // source order, which is the hit order when every hit scores the same.
-    std::vector<DHit> stitch;
-    std::vector<DGroup> lg;
-    std::vector<uint32_t> lg_group, lg_start;
-    static constexpr uint32_t kChunk = 4096;
+    // into chunks of their source (scan_kernel, one workgroup per chunk, so a
+    // pool's full hit list is produced by many CUs); stitch_kernel places the
+    // chunk outputs back in source order on the device — the hit order when
+    // every hit scores the same.  Other searches run whole (search_kernel).
+    // d_groups_ / d_res_ hold [whole searches..., chunks...]; d_out_ holds
+    // [whole searches' outputs..., chunked searches' outputs...].
+    std::vector<DGroup> lg;                 // whole searches, then chunks
+    std::vector<uint32_t> lg_group;         // owning BGroup of each entry of lg
+    std::vector<DChunkMap> lmap;            // per chunk
+    std::vector<uint32_t> cg_list;          // chunked BGroups, in order
+    std::vector<uint64_t> cg_off;           // their output offsets in d_out_
+    std::vector<uint32_t> cg_first, cg_end; // their chunk ranges (indexes into lg)
 
     void run_batch(std::vector<BGroup>& bg, bool need_pm) {
+        const uint32_t kChunk = (uint32_t)scan_chunk_len();
         lg.clear();
         lg_group.clear();
-        lg_start.clear();
+        lmap.clear();
+        cg_list.clear();
+        cg_off.clear();
+        cg_first.clear();
+        cg_end.clear();
+        uint64_t off = 0;
         for (uint32_t i = 0; i < bg.size(); i++) {
             const DGroup& d = bg[i].d;
-            if (!d.var_score && !rev && d.src_len > kChunk && d.k > kChunk / 4) {
-                for (uint32_t s0 = 0; s0 < d.src_len; s0 += kChunk) {
-                    DGroup dc = d;
-                    dc.src_off = d.src_off + s0;
-                    dc.src_len = std::min(kChunk, d.src_len - s0);
-                    dc.k = std::max<uint32_t>(1, std::min(d.k, dc.src_len));
-                    lg.push_back(dc);
-                    lg_group.push_back(i);
-                    lg_start.push_back(s0);
-                }
-            } else {
-                lg.push_back(d);
-                lg_group.push_back(i);
-                lg_start.push_back(0);
+            if (!d.var_score && !rev && !d.has_cursor && d.src_len > kChunk && d.k > kChunk / 4) {
+                cg_list.push_back(i);
+                continue;
             }
+            DGroup w = d;
+            w.out_off = off;
+            off += w.k;
+            lg.push_back(w);
+            lg_group.push_back(i);
         }
-        const int ng = (int)lg.size();
-        uint64_t off = 0;
+        const int nwhole = (int)lg.size();
+        uint64_t scratch = 0;
+        for (uint32_t i : cg_list) {
+            const DGroup& d = bg[i].d;
+            const uint32_t first = (uint32_t)lg.size();
+            cg_first.push_back(first);
+            cg_off.push_back(off);
+            for (uint32_t s0 = 0; s0 < d.src_len; s0 += kChunk) {
+                DGroup dc = d;
+                dc.src_off = d.src_off + s0;
+                dc.src_len = std::min(kChunk, d.src_len - s0);
+                dc.k = dc.src_len;
+                dc.out_off = scratch;
+                scratch += dc.src_len;
+                lg.push_back(dc);
+                lg_group.push_back(i);
+                lmap.push_back(DChunkMap{first, s0, d.k, 0u, off});
+            }
+            cg_end.push_back((uint32_t)lg.size());
+            off += d.k;
+        }
+        const int ng = (int)lg.size(), nchunks = ng - nwhole;
         c.h_groups_.reserve(ng);
-        for (int i = 0; i < ng; i++) {
-            lg[i].out_off = off;
-            off += lg[i].k;
-            c.h_groups_.p[i] = lg[i];
-        }
+        std::memcpy(c.h_groups_.p, lg.data(), ng * sizeof(DGroup));
         c.d_groups_.reserve(ng, false);
         c.d_res_.reserve(ng, false);
         c.d_out_.reserve(std::max<uint64_t>(off, 1), false);
         if (rev) c.d_rev_.reserve(std::max<uint64_t>(off, 1), false);
+        if (nchunks) {
+            c.d_scan_.reserve(scratch, false);
+            c.h_map_.reserve(nchunks);
+            std::memcpy(c.h_map_.p, lmap.data(), nchunks * sizeof(DChunkMap));
+            c.d_map_.reserve(nchunks, false);
+            NKM_HIP(hipMemcpyAsync(c.d_map_.p, c.h_map_.p, nchunks * sizeof(DChunkMap), hipMemcpyHostToDevice, stream));
+        }
         NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, ng * sizeof(DGroup), hipMemcpyHostToDevice, stream));
         NKM_HIP(hipEventRecord(c.ev0_, stream));
-        NKM_HIP(launch_search(st, c.d_groups_.p, ng, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream));
+        NKM_HIP(launch_search(st, c.d_groups_.p, nwhole, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream));
+        NKM_HIP(launch_scan(st, c.d_groups_.p + nwhole, nchunks, c.d_scan_.p, c.d_res_.p + nwhole, stream));
         NKM_HIP(hipEventRecord(c.ev1_, stream));
+        NKM_HIP(launch_stitch(c.d_map_.p, c.d_groups_.p + nwhole, nchunks, c.d_res_.p + nwhole, c.d_scan_.p,
+                              c.d_out_.p, stream));
         if (need_pm) {
-            c.d_pm_.reserve((uint64_t)ng * kPairP, false);
-            NKM_HIP(launch_pairmat(st, c.d_groups_.p, c.d_res_.p, ng, c.d_out_.p, c.d_pm_.p, stream));
+            c.d_pm_.reserve((uint64_t)nwhole * kPairP, false);
+            NKM_HIP(launch_pairmat(st, c.d_groups_.p, c.d_res_.p, nwhole, c.d_out_.p, c.d_pm_.p, stream));
         }
         c.h_res_.reserve(ng);
         NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, ng * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
         c.h_out_.reserve(std::max<uint64_t>(off, 1));
-        NKM_HIP(hipMemcpyAsync(c.h_out_.p, c.d_out_.p, off * sizeof(DHit), hipMemcpyDeviceToHost, stream));
+        const uint64_t whole_off = nwhole ? lg[nwhole - 1].out_off + lg[nwhole - 1].k : 0;
+        if (whole_off)
+            NKM_HIP(hipMemcpyAsync(c.h_out_.p, c.d_out_.p, whole_off * sizeof(DHit), hipMemcpyDeviceToHost, stream));
         if (rev) {
             c.h_rev_.reserve(std::max<uint64_t>(off, 1));
             NKM_HIP(hipMemcpyAsync(c.h_rev_.p, c.d_rev_.p, off, hipMemcpyDeviceToHost, stream));
         }
         if (need_pm) {
-            c.h_pm_.reserve((uint64_t)ng * kPairP);
-            NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, (uint64_t)ng * kPairP * sizeof(uint32_t),
+            c.h_pm_.reserve((uint64_t)nwhole * kPairP);
+            NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, (uint64_t)nwhole * kPairP * sizeof(uint32_t),
                                    hipMemcpyDeviceToHost, stream));
         }
         NKM_HIP(hipStreamSynchronize(stream));
@@ -236,56 +269,41 @@ struct Replay {
         NKM_HIP(hipEventElapsedTime(&ms, c.ev0_, c.ev1_));
         stats.eval_ms += ms;
         stats.batches++;
-        stats.launches++;
-        // stitch
-        uint64_t stitched = 0;
-        for (int i = 0; i < ng; i++)
-            if (lg_start[i] || (i + 1 < ng && lg_group[i + 1] == lg_group[i])) stitched += c.h_res_.p[i].count;
-        stitch.resize(stitched);
-        uint64_t so = 0;
-        for (int i = 0; i < ng;) {
-            const uint32_t gi = lg_group[i];
-            BGroup& g = bg[gi];
-            int j = i;
-            while (j < ng && lg_group[j] == gi) j++;
-            for (int t = i; t < j; t++) {
-                stats.pair_evals += c.h_res_.p[t].scanned;
-                stats.eval_bytes += search_bytes(c.sigs_[g.sig], lg[t], c.h_res_.p[t]);
-            }
-            g.head = 0;
-            if (j == i + 1) {  // single search
-                const DGroupResult& r = c.h_res_.p[i];
-                g.hits = c.h_out_.p + lg[i].out_off;
-                g.rev = rev ? c.h_rev_.p + lg[i].out_off : nullptr;
-                g.pm = need_pm ? c.h_pm_.p + (uint64_t)i * kPairP : nullptr;
-                g.pm_n = need_pm ? std::min<uint32_t>(r.count, kPairP) : 0;
-                g.n = r.count;
-                g.complete = r.complete != 0;
-            } else {
-                uint64_t n = 0;
-                bool complete = true;
-                DHit* dst = stitch.data() + so;
-                for (int t = i; t < j; t++) {
-                    const DGroupResult& r = c.h_res_.p[t];
-                    complete &= r.complete != 0;
-                    const DHit* src = c.h_out_.p + lg[t].out_off;
-                    for (uint32_t e = 0; e < r.count; e++) {
-                        dst[n] = src[e];
-                        dst[n].idx += lg_start[t];
-                        n++;
-                    }
-                }
-                so += n;
-                if (n > g.d.k) { n = g.d.k; complete = false; }
-                g.hits = dst;
-                g.rev = nullptr;
-                g.pm = nullptr;
-                g.pm_n = 0;
-                g.n = (uint32_t)n;
-                g.complete = complete;
-            }
-            i = j;
+        stats.launches += (nwhole > 0) + (nchunks > 0);
+        for (int t = 0; t < ng; t++) {
+            stats.pair_evals += c.h_res_.p[t].scanned;
+            stats.eval_bytes += search_bytes(c.sigs_[bg[lg_group[t]].sig], lg[t], c.h_res_.p[t]);
         }
+        for (int i = 0; i < nwhole; i++) {
+            BGroup& g = bg[lg_group[i]];
+            const DGroupResult& r = c.h_res_.p[i];
+            g.head = 0;
+            g.hits = c.h_out_.p + lg[i].out_off;
+            g.rev = rev ? c.h_rev_.p + lg[i].out_off : nullptr;
+            g.pm = need_pm ? c.h_pm_.p + (uint64_t)i * kPairP : nullptr;
+            g.pm_n = need_pm ? std::min<uint32_t>(r.count, kPairP) : 0;
+            g.n = r.count;
+            g.complete = r.complete != 0;
+        }
+        // chunked searches: exact hit counts are known now; copy just those
+        for (size_t k = 0; k < cg_list.size(); k++) {
+            BGroup& g = bg[cg_list[k]];
+            uint64_t n = 0;
+            for (uint32_t t = cg_first[k]; t < cg_end[k]; t++) n += c.h_res_.p[t].count;
+            bool complete = true;
+            if (n > g.d.k) { n = g.d.k; complete = false; }
+            if (n)
+                NKM_HIP(hipMemcpyAsync(c.h_out_.p + cg_off[k], c.d_out_.p + cg_off[k], n * sizeof(DHit),
+                                       hipMemcpyDeviceToHost, stream));
+            g.head = 0;
+            g.hits = c.h_out_.p + cg_off[k];
+            g.rev = nullptr;
+            g.pm = nullptr;
+            g.pm_n = 0;
+            g.n = (uint32_t)n;
+            g.complete = complete;
+        }
+        if (!cg_list.empty()) NKM_HIP(hipStreamSynchronize(stream));
     }
 
     // validateMatch(from's query, to) for two entries of the same list.

@@ -59,6 +59,8 @@ template struct DevArray<DQuery>;
 template struct DevArray<DClause>;
 template struct DevArray<DGroup>;
 template struct DevArray<DHit>;
+template struct DevArray<DChunkMap>;
+template struct PinnedArray<DChunkMap>;
 template struct DevArray<DGroupResult>;
 template struct DevArray<int64_t*>;
 template struct DevArray<uint8_t*>;
