@@ -69,10 +69,10 @@ def dist_setup(args):
 
 
 def barrier_sync(pg, local):
+    import torch
     if pg is not None:
-        import torch
         pg.barrier()
-        torch.cuda.synchronize(local)
+    torch.cuda.synchronize(local)
 
 
 def max_over_ranks(pg, local, x):
@@ -149,9 +149,10 @@ def main():
         ts.insert_into(mm)  # untimed: store maintenance + HBM upload
         barrier_sync(pg, local)
         t0 = time.perf_counter()
-        _, n_groups, matched, pres, r = mm.process_timed()  # the C-ABI call; groups stay in C memory
+        out = mm.process_call()  # the C-ABI call: one whole Process() pass
         barrier_sync(pg, local)
         dt = time.perf_counter() - t0
+        n_groups, matched, pres, r = mm.process_summary(out)  # untimed: counts the groups, frees them
         ts.close()
         dt_max = max_over_ranks(pg, local, dt)
         if step >= args.warmup:

@@ -370,18 +370,18 @@ class Matchmaker:
             self.lib.mm_free_matched(self.h, C.byref(out))
         return res
 
-    def process_timed(self):
-        """One mm_process call timed at the C boundary (no Python conversion of
-        the groups inside the timed region).  Returns (seconds, n_groups,
-        matched tickets, matched presences, ProcessResult-without-groups)."""
-        import time
-        import numpy as np
+    def process_call(self):
+        """One mm_process call, nothing else: returns the library-owned result
+        (pass it to process_summary, which frees it).  bench.py times exactly
+        this call."""
         out = mm_matched()
-        fn = self.lib.mm_process
-        t0 = time.perf_counter()
-        rc = fn(self.h, C.byref(out))
-        dt = time.perf_counter() - t0
-        self._check(rc)
+        self._check(self.lib.mm_process(self.h, C.byref(out)))
+        return out
+
+    def process_summary(self, out):
+        """(n_groups, matched tickets, matched presences, ProcessResult without
+        the groups) of a process_call result; frees it."""
+        import numpy as np
         try:
             n = out.n_entries
             if n:
@@ -392,9 +392,19 @@ class Matchmaker:
                 tickets = 0
             res = ProcessResult([], bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms, out.pair_evals,
                                 out.eval_bytes, out.eval_launches, out.n_batches)
-            return dt, out.n_groups, tickets, n, res
+            return out.n_groups, tickets, n, res
         finally:
             self.lib.mm_free_matched(self.h, C.byref(out))
+
+    def process_timed(self):
+        """One mm_process call timed at the C boundary (no Python conversion of
+        the groups inside the timed region).  Returns (seconds, n_groups,
+        matched tickets, matched presences, ProcessResult-without-groups)."""
+        import time
+        t0 = time.perf_counter()
+        out = self.process_call()
+        dt = time.perf_counter() - t0
+        return (dt,) + self.process_summary(out)
 
     def commit(self, groups: Sequence[Sequence[Tuple[str, int]]]) -> ProcessResult:
         offs = [0]

@@ -23,6 +23,7 @@
 #include "../../include/nakama_mm.h"
 #include "mm_device.h"
 #include "qcompile.h"
+#include "replay_core.h"
 
 namespace nkm {
 
@@ -206,14 +207,6 @@ private:
 // The fields the greedy replay reads for every hit it walks, packed in one
 // 32-B record per slot so that a hit costs one cache line instead of one per
 // column.  Immutable while the slot lives (rebuilt at compaction).
-struct HotRec {
-    uint32_t party;     // kNoParty for ""
-    uint32_t sess0;     // session of presence 0
-    uint32_t pres_off;  // first presence in pres_sess_
-    int32_t count, minc, maxc, cm;
-    uint32_t pad;
-};
-static_assert(sizeof(HotRec) == 32, "HotRec is half a cache line");
 
 struct SlotSets {
     std::vector<uint32_t> first;
@@ -268,7 +261,6 @@ struct PostingRange {
 // Builtin document fields (MapMatchmakerIndex, matchmaker.go:1026-1040).
 enum BuiltinField : uint16_t { F_TICKET = 0, F_MIN = 1, F_MAX = 2, F_PARTY = 3, F_CREATED = 4, F_NBUILTIN = 5 };
 
-struct BGroup;  // a batch search and its hit list (mm_process.cpp)
 
 // Matched (or candidate) groups of a pass as a flat CSR of (slot, presence
 // index) entries: group g = ents[off[g], off[g+1]).
@@ -295,19 +287,6 @@ struct GroupList {
     const Entry* begin(size_t g) const { return ents.data() + off[g]; }
     const Entry* end(size_t g) const { return ents.data() + off[g + 1]; }
     size_t len(size_t g) const { return off[g + 1] - off[g]; }
-};
-
-// One pool's share of a parallel replay: a record per processed row, in row
-// order, and the matched groups' entries.
-struct PoolRec {
-    uint32_t bi;  // batch row (UINT32_MAX: the list's end sentinel)
-    uint8_t matched, expired;
-    uint32_t off, len;  // into PoolOut::ents (off: entries before this row)
-    uint32_t gcum, xcum;  // matched / expired rows before this one
-};
-struct PoolOut {
-    std::vector<PoolRec> recs;
-    std::vector<std::pair<uint32_t, int>> ents;
 };
 
 struct SrcChoice {  // the posting list a search streams, when it has one

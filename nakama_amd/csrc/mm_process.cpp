@@ -29,96 +29,25 @@ namespace nkm {
 
 hipError_t launch_pairmat(const DStore& st, const DGroup* d_groups, const DGroupResult* d_res, int n_groups,
                           const DHit* d_out, uint32_t* d_pm, hipStream_t stream);
-constexpr int kPairP = 32;  // pair matrix covers the first 32 entries of a list
 
 constexpr size_t kMaxBatchRows = 1u << 20;
 constexpr uint64_t kOutCap = 1ull << 24;  // max hit entries per batch (16M x 16 B)
 
-struct CE {  // combo entry: (ticket slot, presence index, list position of its hit, session)
-    uint32_t slot;
-    uint32_t pi;
-    uint32_t lpos;
-    uint32_t sess;
-};
-
-// groupIndexes (server/matchmaker.go:132-167), int64 wrapping arithmetic.
-struct IG { std::vector<uint32_t> idx; int64_t avg; };
-void group_indexes(const std::vector<uint32_t>& in, size_t from, int required, const std::vector<int32_t>& cnt,
-                   const std::vector<int64_t>& created, std::vector<IG>& out) {
-    if (from >= in.size() || required <= 0) return;
-    const uint32_t cur = in[from];
-    if (cnt[cur] > required) { group_indexes(in, from + 1, required, cnt, created, out); return; }
-    if (cnt[cur] == required) {
-        out.push_back(IG{{cur}, created[cur]});
-    } else {
-        std::vector<IG> fill;
-        group_indexes(in, from + 1, required - cnt[cur], cnt, created, fill);
-        for (auto& f : fill) {
-            const int64_t n = (int64_t)f.idx.size();
-            f.avg = (int64_t)((uint64_t)f.avg * (uint64_t)n + (uint64_t)created[cur]) / (n + 1);
-            f.idx.push_back(cur);
-            out.push_back(std::move(f));
-        }
-    }
-    group_indexes(in, from + 1, required, cnt, created, out);
-}
-
-// A batch group: one device search and its (possibly extended) hit list.
-struct BGroup {
-    uint32_t sig = 0;
-    uint32_t nrows = 0;
-    uint32_t row_slot = kNoSlot;  // RevPrecision: the single searching row
-    DGroup d{};
-    const DHit* hits = nullptr;
-    const uint8_t* rev = nullptr;
-    const uint32_t* pm = nullptr;  // kPairP masks per entry (rev rows with combos)
-    uint32_t pm_n = 0;             // entries covered by pm
-    bool has_src_term = false;     // source = posting list of (src_field, src_term)
-    uint16_t src_field = 0;
-    uint32_t src_term = 0;
-    uint32_t n = 0;
-    bool complete = true;
-    uint32_t head = 0;
-    std::vector<DHit> ext;
-    std::vector<uint8_t> ext_rev;
-};
-
-struct Replay {
+struct Replay : ReplayCore {
     Core& c;
-    std::vector<uint8_t>& sel;
-    const bool rev;
-    const int max_intervals;
-    std::vector<std::vector<CE>> combos;  // pool: the first ncomb are this row's entryCombos
-    size_t ncomb = 0;
     PassStats& stats;
     DStore st;
     hipStream_t stream;
-    uint64_t hits_seen = 0;  // profiling: hit-list entries the rows walked
-    // pool-parallel replay: rows this worker processed earlier in the batch,
-    // whose Intervals increments are applied after the batch (1 = one pending)
-    const uint8_t* proc = nullptr;
-    static constexpr uint32_t kPrefetch = 8;
 
+    static ReplayView view(const Core& core) {
+        return ReplayView{core.hot_.data(), core.pres_sess_.data(), core.party_.data(), core.intervals_.data(),
+                          core.live_.data(), core.count_.data(), core.created_.data()};
+    }
     Replay(Core& core, std::vector<uint8_t>& s, bool r, int mi, PassStats& ps, DStore ds, hipStream_t sm)
-        : c(core), sel(s), rev(r), max_intervals(mi), stats(ps), st(ds), stream(sm) {}
-
-    static bool share_session(const Core& c, const HotRec& a, const HotRec& b) {
-        if (a.count == 1 && b.count == 1) return a.sess0 == b.sess0;
-        for (uint32_t p = a.pres_off; p < a.pres_off + (uint32_t)a.count; p++)
-            for (uint32_t q = b.pres_off; q < b.pres_off + (uint32_t)b.count; q++)
-                if (c.pres_sess_[p] == c.pres_sess_[q]) return true;
-        return false;
-    }
-    bool share_session(uint32_t a, uint32_t b) const { return share_session(c, c.hot_[a], c.hot_[b]); }
-    bool has_session(const HotRec& h, uint32_t sess) const {
-        if (h.count == 1) return h.sess0 == sess;
-        for (uint32_t q = h.pres_off; q < h.pres_off + (uint32_t)h.count; q++)
-            if (c.pres_sess_[q] == sess) return true;
-        return false;
-    }
+        : ReplayCore(view(core), s, r, mi), c(core), stats(ps), st(ds), stream(sm) {}
 
     // Fetches the next page of a group's list (cursor = its last entry).
-    void fetch_more(BGroup& g) {
+    void fetch_more(BGroup& g) override {
         stats.refetches++;
         if (g.ext.empty() && g.n) {
             g.ext.assign(g.hits, g.hits + g.n);
@@ -306,149 +235,17 @@ struct Replay {
         if (!cg_list.empty()) NKM_HIP(hipStreamSynchronize(stream));
     }
 
-    // validateMatch(from's query, to) for two entries of the same list.
-    bool pair_ok(const BGroup& g, uint32_t from_pos, uint32_t to_pos) {
-        if (g.pm && from_pos < g.pm_n && to_pos < g.pm_n) return (g.pm[from_pos] >> to_pos) & 1u;
+    bool pair_slow(const BGroup& g, uint32_t from_pos, uint32_t to_pos) override {
         // slow path: evaluate the single pair on the device
         uint32_t pr[2] = {g.hits[from_pos].slot, g.hits[to_pos].slot};
         c.d_slots_tmp_.reserve(2, false);
         c.d_pair_out_.reserve(1, false);
         NKM_HIP(hipMemcpyAsync(c.d_slots_tmp_.p, pr, sizeof pr, hipMemcpyHostToDevice, stream));
         NKM_HIP(launch_pairs(st, c.d_slots_tmp_.p, 1, c.d_pair_out_.p, stream));
-        uint8_t v = 0;
-        NKM_HIP(hipMemcpyAsync(&v, c.d_pair_out_.p, 1, hipMemcpyDeviceToHost, stream));
+        uint8_t ok = 0;
+        NKM_HIP(hipMemcpyAsync(&ok, c.d_pair_out_.p, 1, hipMemcpyDeviceToHost, stream));
         NKM_HIP(hipStreamSynchronize(stream));
-        return v != 0;
-    }
-
-    enum Status { MATCHED, NOMATCH, EXHAUSTED };
-
-    // Is there an unselected, non-self hit after position i?  (the
-    // hitCounter >= lastHitCounter test, matchmaker_process.go:130,233)
-    int more_hits_after(BGroup& g, uint32_t i, uint32_t T, bool can_fetch) {
-        for (uint32_t j = i + 1;; j++) {
-            if (j >= g.n) {
-                if (g.complete) return 0;
-                if (!can_fetch) return -1;
-                fetch_more(g);
-                if (j >= g.n) {
-                    if (g.complete) return 0;
-                    j--;  // nothing new yet: look at position j again
-                    continue;
-                }
-            }
-            const uint32_t s = g.hits[j].slot;
-            if (s != T && !sel[s] && !same_party(T, s)) return 1;
-        }
-    }
-
-    // the party mustNot of the search (matchmaker_process.go:80-85)
-    bool same_party(uint32_t T, uint32_t H) const {
-        return c.party_[T] != kNoParty && c.hot_[H].party == c.party_[T];
-    }
-
-    // processDefault's loop body for one active ticket T.
-    Status row(uint32_t T, BGroup& g, bool can_fetch, std::vector<std::pair<uint32_t, int>>& group_out) {
-        const HotRec& ht = c.hot_[T];
-        const bool last = c.intervals_[T] + 1 >= max_intervals || ht.minc == ht.maxc;
-        const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
-        const uint32_t tparty = ht.party;
-        ncomb = 0;
-        while (g.head < g.n && sel[g.hits[g.head].slot]) g.head++;
-        for (uint32_t i = g.head;; i++) {
-            if (i >= g.n) {
-                if (g.complete) break;
-                if (!can_fetch) return EXHAUSTED;
-                fetch_more(g);
-                if (i >= g.n) { if (g.complete) break; i--; continue; }
-            }
-            if (i + kPrefetch < g.n) {  // the walk's next slots
-                const uint32_t P = g.hits[i + kPrefetch].slot;
-                __builtin_prefetch(&sel[P]);
-                __builtin_prefetch(&c.hot_[P]);
-            }
-            const uint32_t H = g.hits[i].slot;
-            hits_seen++;
-            if (H == T || sel[H]) continue;
-            const HotRec& hh = c.hot_[H];
-            if (tparty != kNoParty && hh.party == tparty) continue;                       // :80-85
-            if (rev && !g.rev[i]) continue;                                            // :139-148
-            if (tmax < hh.maxc && c.intervals_[H] + (proc ? proc[H] : 0) <= max_intervals) continue;  // :150-153
-            if (share_session(c, ht, hh)) continue;                                       // :155-165
-            bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
-            int found = -1;
-            const int hcount = hh.count;
-            const uint32_t hp = hh.pres_off;
-            for (size_t ci = 0; ci < ncomb; ci++) {
-                auto& combo = combos[ci];
-                if ((int)combo.size() + hcount + tcount <= tmax) {
-                    bool mconf = false;
-                    for (const CE& e : combo) {
-                        if (has_session(hh, e.sess)) { sconf = true; break; }
-                        if (rev) {
-                            if (!pair_ok(g, i, e.lpos)) { mconf = true; break; }
-                            if (c.live_[e.slot] && !pair_ok(g, e.lpos, i)) { mconf = true; break; }
-                        }
-                    }
-                    if (sconf || mconf) continue;
-                    for (int k = 0; k < hcount; k++)
-                        combo.push_back(CE{H, (uint32_t)k, i, hcount == 1 ? hh.sess0 : c.pres_sess_[hp + k]});
-                    found = (int)ci;
-                    break;
-                }
-            }
-            if (found < 0) {
-                if (ncomb == combos.size()) combos.emplace_back();
-                std::vector<CE>& nc = combos[ncomb];
-                nc.clear();
-                for (int k = 0; k < hcount; k++) nc.push_back(CE{H, (uint32_t)k, i, hcount == 1 ? hh.sess0 : c.pres_sess_[hp + k]});
-                found = (int)ncomb++;
-            }
-            std::vector<CE>& fc = combos[found];
-            int l = (int)fc.size() + tcount;
-            bool form = l == tmax;
-            if (!form && last && l >= tmin && l <= tmax) {
-                int more = more_hits_after(g, i, T, can_fetch);
-                if (more < 0) return EXHAUSTED;
-                form = more == 0;
-            }
-            if (!form) continue;
-            const int rem = l % tcm;
-            if (rem != 0) {                                                                // :234-280
-                std::vector<uint32_t> elig;
-                for (const CE& e : fc) {
-                    if (!c.live_[e.slot] || c.count_[e.slot] > rem) continue;
-                    if (std::find(elig.begin(), elig.end(), e.slot) == elig.end()) elig.push_back(e.slot);
-                }
-                std::vector<IG> groups;
-                group_indexes(elig, 0, rem, c.count_, c.created_, groups);
-                if (groups.empty()) continue;
-                std::stable_sort(groups.begin(), groups.end(), [](const IG& a, const IG& b) { return a.avg < b.avg; });
-                for (uint32_t gs : groups[0].idx) {
-                    for (int k = 0; k < (int)fc.size(); k++) {
-                        if (fc[k].slot == gs) {
-                            fc[k] = fc.back();
-                            fc.pop_back();
-                            k--;
-                        }
-                    }
-                }
-                l = (int)fc.size() + tcount;
-                if (l % tcm != 0) continue;
-            }
-            bool failed = false;                                                           // :287-296
-            for (const CE& e : fc) {
-                const uint32_t s = e.slot;
-                const HotRec& hs = c.hot_[s];
-                if (c.live_[s] && (hs.minc > l || hs.maxc < l || l % hs.cm != 0)) { failed = true; break; }
-            }
-            if (failed) continue;
-            group_out.clear();
-            for (const CE& e : fc) group_out.push_back({e.slot, (int)e.pi});
-            for (int k = 0; k < tcount; k++) group_out.push_back({T, k});
-            return MATCHED;
-        }
-        return NOMATCH;
+        return ok != 0;
     }
 };
 
@@ -581,33 +378,11 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
         // Intervals stay unwritten during the walk (slots of all pools share
         // its cache lines): a row's increment is pending in tl_proc until the
         // merge applies it.
-        rp.proc = tl_proc.data();
-        std::vector<std::pair<uint32_t, int>> grp;
         {
             PoolOut& o = outs[gi];
-            uint32_t gcum = 0, xcum = 0;
-            for (uint32_t bi : grows[gi]) {
-                const uint32_t T = brow[bi];
-                if (psel[T]) continue;
-                auto status = rp.row(T, mine[local_idx[brow_group[bi]]], false, grp);  // complete lists: never EXHAUSTED
-                tl_proc[T] = 1;
-                Rec rec{bi, 0, (uint8_t)(intervals_[T] + 1 >= maxI || minc_[T] == maxc_[T]),
-                        (uint32_t)o.ents.size(), 0, gcum, xcum};
-                xcum += rec.expired;
-                if (status == Replay::MATCHED) {
-                    rec.matched = 1;
-                    rec.len = (uint32_t)grp.size();
-                    gcum++;
-                    for (auto& e : grp) {
-                        psel[e.first] = 1;
-                        o.ents.push_back(e);
-                    }
-                }
-                o.recs.push_back(rec);
-            }
-            for (auto& e : o.ents) psel[e.first] = 0;
-            for (const Rec& r : o.recs) tl_proc[brow[r.bi]] = 0;
-            o.recs.push_back(Rec{UINT32_MAX, 0, 0, (uint32_t)o.ents.size(), 0, gcum, xcum});  // sentinel
+            replay_pool(rp, grows[gi], brow.data(),
+                        [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; }, psel,
+                        tl_proc.data(), minc_.data(), maxc_.data(), o);
             task_ms[k] = msd(tw0, clk::now());
             task_hits[k] = rp.hits_seen;
             task_rows[k] = o.recs.size() - 1;
@@ -1382,7 +1157,7 @@ extern "C" int32_t mm_debug_group_indexes(const int32_t* counts, const int64_t* 
     std::vector<uint32_t> in(n);
     for (int32_t i = 0; i < n; i++) in[i] = (uint32_t)i;
     std::vector<nkm::IG> out;
-    nkm::group_indexes(in, 0, required, cnt, cr, out);
+    nkm::group_indexes(in, 0, required, cnt.data(), cr.data(), out);
     int32_t g = 0, k = 0;
     group_offsets[0] = 0;
     for (auto& gr : out) {

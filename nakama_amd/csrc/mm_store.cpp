@@ -181,14 +181,16 @@ static std::vector<int> worker_cpus(unsigned want) {
     return out;
 }
 
-// Host worker count: NKM_THREADS, else the visible cores capped at 16 (the
-// per-GPU host share on an 8-GPU node).
+// Host worker count: NKM_THREADS, else the visible cores capped at 8.  The
+// per-GPU host share on an 8-GPU node is 16 CPUs, but measured on MI355X
+// boxes (profiles/r01_threads_*) 8 workers beat 16 on every pass phase: the
+// replay has one task per pool, and the extra workers only add contention.
 WorkPool& Core::workers() {
     if (!workers_) {
         unsigned n = std::thread::hardware_concurrency();
         cpu_set_t cs;
         if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = (unsigned)CPU_COUNT(&cs);
-        n = std::max(1u, std::min(16u, n));
+        n = std::max(1u, std::min(8u, n));
         if (const char* e = std::getenv("NKM_THREADS")) n = std::max(1, std::atoi(e));
         workers_.reset(new WorkPool(n, worker_cpus(n - 1)));
     }
@@ -672,7 +674,8 @@ void Core::set_hot(uint32_t s) {
     h.minc = minc_[s];
     h.maxc = maxc_[s];
     h.cm = cm_[s];
-    h.pad = 0;
+    h.smask = 0;
+    for (uint32_t p = pres_off_[s]; p < pres_off_[s + 1]; p++) h.smask |= 1u << (pres_sess_[p] & 31);
 }
 
 void Core::maybe_compact() {

@@ -1,0 +1,324 @@
+// nakama_amd/csrc/replay_core.h — the exact greedy replay of processDefault's
+// loop body (server/matchmaker_process.go:105-330) over a hit list that the
+// device searches produced.  Pure host code over plain per-slot arrays (no HIP
+// calls): paging a truncated list and single RevPrecision pair checks are
+// hooks the device-backed subclass (mm_process.cpp) implements.  Kept free of
+// the store so the replay can be timed and tested on its own
+// (tools/replay_bench.cpp).
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+#include "mm_device.h"
+
+namespace nkm {
+
+// Per-slot fields the replay reads, packed (one 32-B record per ticket).
+struct HotRec {
+    uint32_t party;     // kNoParty for ""
+    uint32_t sess0;     // session of presence 0
+    uint32_t pres_off;  // first presence in pres_sess
+    int32_t count, minc, maxc, cm;
+    uint32_t smask;     // OR of 1 << (session id & 31) over the presences: disjoint masks share no session
+};
+static_assert(sizeof(HotRec) == 32, "HotRec is half a cache line");
+
+struct CE {  // combo entry: (ticket slot, presence index, list position of its hit, session)
+    uint32_t slot;
+    uint32_t pi;
+    uint32_t lpos;
+    uint32_t sess;
+};
+
+// groupIndexes (server/matchmaker.go:132-167), int64 wrapping arithmetic.
+struct IG { std::vector<uint32_t> idx; int64_t avg; };
+inline void group_indexes(const std::vector<uint32_t>& in, size_t from, int required, const int32_t* cnt,
+                          const int64_t* created, std::vector<IG>& out) {
+    if (from >= in.size() || required <= 0) return;
+    const uint32_t cur = in[from];
+    if (cnt[cur] > required) { group_indexes(in, from + 1, required, cnt, created, out); return; }
+    if (cnt[cur] == required) {
+        out.push_back(IG{{cur}, created[cur]});
+    } else {
+        std::vector<IG> fill;
+        group_indexes(in, from + 1, required - cnt[cur], cnt, created, fill);
+        for (auto& f : fill) {
+            const int64_t n = (int64_t)f.idx.size();
+            f.avg = (int64_t)((uint64_t)f.avg * (uint64_t)n + (uint64_t)created[cur]) / (n + 1);
+            f.idx.push_back(cur);
+            out.push_back(std::move(f));
+        }
+    }
+    group_indexes(in, from + 1, required, cnt, created, out);
+}
+
+// A batch search and its (possibly extended) hit list.
+struct BGroup {
+    uint32_t sig = 0;
+    uint32_t nrows = 0;
+    uint32_t row_slot = kNoSlot;  // RevPrecision: the single searching row
+    DGroup d{};
+    const DHit* hits = nullptr;
+    const uint8_t* rev = nullptr;
+    const uint32_t* pm = nullptr;  // kPairP masks per entry (rev rows with combos)
+    uint32_t pm_n = 0;             // entries covered by pm
+    bool has_src_term = false;     // source = posting list of (src_field, src_term)
+    uint16_t src_field = 0;
+    uint32_t src_term = 0;
+    uint32_t n = 0;
+    bool complete = true;
+    uint32_t head = 0;
+    std::vector<DHit> ext;
+    std::vector<uint8_t> ext_rev;
+};
+
+// Read-only per-slot views of the store that the replay consults.
+struct ReplayView {
+    const HotRec* hot;
+    const uint32_t* pres_sess;  // per presence: session dictionary id
+    const uint32_t* party;      // per slot: party dictionary id (kNoParty for "")
+    const int32_t* intervals;
+    const uint8_t* live;        // in m.indexes
+    const int32_t* count;
+    const int64_t* created;
+};
+
+struct ReplayCore {
+    ReplayView v;
+    std::vector<uint8_t>& sel;
+    const bool rev;
+    const int max_intervals;
+    std::vector<std::vector<CE>> combos;  // pool: the first ncomb are this row's entryCombos
+    std::vector<uint32_t> cmask;          // per combo: OR of its entries' session masks (a superset)
+    size_t ncomb = 0;
+    uint64_t hits_seen = 0;  // profiling: hit-list entries the rows walked
+    // pool-parallel replay: rows this worker processed earlier in the batch,
+    // whose Intervals increments are applied after the batch (1 = one pending)
+    const uint8_t* proc = nullptr;
+    static constexpr uint32_t kPrefetch = 8;
+    static constexpr uint32_t kPairP = 32;  // pair matrices cover the first 32 entries of a list
+
+    ReplayCore(const ReplayView& view, std::vector<uint8_t>& s, bool r, int mi)
+        : v(view), sel(s), rev(r), max_intervals(mi) {}
+    virtual ~ReplayCore() = default;
+
+    // Next page of a truncated list (device search with a cursor).
+    virtual void fetch_more(BGroup& g) = 0;
+    // validateMatch for a pair outside the list's pair matrix.
+    virtual bool pair_slow(const BGroup& g, uint32_t from_pos, uint32_t to_pos) = 0;
+
+    bool share_session(const HotRec& a, const HotRec& b) const {
+        if (a.count == 1 && b.count == 1) return a.sess0 == b.sess0;
+        for (uint32_t p = a.pres_off; p < a.pres_off + (uint32_t)a.count; p++)
+            for (uint32_t q = b.pres_off; q < b.pres_off + (uint32_t)b.count; q++)
+                if (v.pres_sess[p] == v.pres_sess[q]) return true;
+        return false;
+    }
+    bool share_session(uint32_t a, uint32_t b) const { return share_session(v.hot[a], v.hot[b]); }
+    bool has_session(const HotRec& h, uint32_t sess) const {
+        if (h.count == 1) return h.sess0 == sess;
+        for (uint32_t q = h.pres_off; q < h.pres_off + (uint32_t)h.count; q++)
+            if (v.pres_sess[q] == sess) return true;
+        return false;
+    }
+    // the party mustNot of the search (matchmaker_process.go:80-85)
+    bool same_party(uint32_t T, uint32_t H) const {
+        return v.party[T] != kNoParty && v.hot[H].party == v.party[T];
+    }
+
+    // validateMatch(from's query, to) for two entries of the same list.
+    bool pair_ok(const BGroup& g, uint32_t from_pos, uint32_t to_pos) {
+        if (g.pm && from_pos < g.pm_n && to_pos < g.pm_n) return (g.pm[from_pos] >> to_pos) & 1u;
+        return pair_slow(g, from_pos, to_pos);
+    }
+
+    enum Status { MATCHED, NOMATCH, EXHAUSTED };
+
+    // Is there an unselected, non-self hit after position i?  (the
+    // hitCounter >= lastHitCounter test, matchmaker_process.go:130,233)
+    int more_hits_after(BGroup& g, uint32_t i, uint32_t T, bool can_fetch) {
+        for (uint32_t j = i + 1;; j++) {
+            if (j >= g.n) {
+                if (g.complete) return 0;
+                if (!can_fetch) return -1;
+                fetch_more(g);
+                if (j >= g.n) {
+                    if (g.complete) return 0;
+                    j--;  // nothing new yet: look at position j again
+                    continue;
+                }
+            }
+            const uint32_t s = g.hits[j].slot;
+            if (s != T && !sel[s] && !same_party(T, s)) return 1;
+        }
+    }
+
+    // processDefault's loop body for one active ticket T.
+    Status row(uint32_t T, BGroup& g, bool can_fetch, std::vector<std::pair<uint32_t, int>>& group_out) {
+        const HotRec& ht = v.hot[T];
+        const bool last = v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc;
+        const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
+        const uint32_t tparty = ht.party;
+        ncomb = 0;
+        while (g.head < g.n && sel[g.hits[g.head].slot]) g.head++;
+        for (uint32_t i = g.head;; i++) {
+            if (i >= g.n) {
+                if (g.complete) break;
+                if (!can_fetch) return EXHAUSTED;
+                fetch_more(g);
+                if (i >= g.n) { if (g.complete) break; i--; continue; }
+            }
+            if (i + kPrefetch < g.n) {  // the walk's next slots
+                const uint32_t P = g.hits[i + kPrefetch].slot;
+                __builtin_prefetch(&sel[P]);
+                __builtin_prefetch(&v.hot[P]);
+            }
+            const uint32_t H = g.hits[i].slot;
+            hits_seen++;
+            if (H == T || sel[H]) continue;
+            const HotRec& hh = v.hot[H];
+            if (tparty != kNoParty && hh.party == tparty) continue;                       // :80-85
+            if (rev && !g.rev[i]) continue;                                            // :139-148
+            if (tmax < hh.maxc && v.intervals[H] + (proc ? proc[H] : 0) <= max_intervals) continue;  // :150-153
+            if ((ht.smask & hh.smask) && share_session(ht, hh)) continue;                 // :155-165
+            bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
+            int found = -1;
+            const int hcount = hh.count;
+            const uint32_t hp = hh.pres_off;
+            for (size_t ci = 0; ci < ncomb; ci++) {
+                auto& combo = combos[ci];
+                if ((int)combo.size() + hcount + tcount <= tmax) {
+                    bool mconf = false;
+                    const bool may_share = (cmask[ci] & hh.smask) != 0;
+                    if (may_share || rev) for (const CE& e : combo) {
+                        if (may_share && has_session(hh, e.sess)) { sconf = true; break; }
+                        if (rev) {
+                            if (!pair_ok(g, i, e.lpos)) { mconf = true; break; }
+                            if (v.live[e.slot] && !pair_ok(g, e.lpos, i)) { mconf = true; break; }
+                        }
+                    }
+                    if (sconf || mconf) continue;
+                    for (int k = 0; k < hcount; k++)
+                        combo.push_back(CE{H, (uint32_t)k, i, hcount == 1 ? hh.sess0 : v.pres_sess[hp + k]});
+                    cmask[ci] |= hh.smask;
+                    found = (int)ci;
+                    break;
+                }
+            }
+            if (found < 0) {
+                if (ncomb == combos.size()) {
+                    combos.emplace_back();
+                    cmask.push_back(0);
+                }
+                std::vector<CE>& nc = combos[ncomb];
+                nc.clear();
+                for (int k = 0; k < hcount; k++) nc.push_back(CE{H, (uint32_t)k, i, hcount == 1 ? hh.sess0 : v.pres_sess[hp + k]});
+                cmask[ncomb] = hh.smask;
+                found = (int)ncomb++;
+            }
+            std::vector<CE>& fc = combos[found];
+            int l = (int)fc.size() + tcount;
+            bool form = l == tmax;
+            if (!form && last && l >= tmin && l <= tmax) {
+                int more = more_hits_after(g, i, T, can_fetch);
+                if (more < 0) return EXHAUSTED;
+                form = more == 0;
+            }
+            if (!form) continue;
+            const int rem = l % tcm;
+            if (rem != 0) {                                                                // :234-280
+                std::vector<uint32_t> elig;
+                for (const CE& e : fc) {
+                    if (!v.live[e.slot] || v.count[e.slot] > rem) continue;
+                    if (std::find(elig.begin(), elig.end(), e.slot) == elig.end()) elig.push_back(e.slot);
+                }
+                std::vector<IG> groups;
+                group_indexes(elig, 0, rem, v.count, v.created, groups);
+                if (groups.empty()) continue;
+                std::stable_sort(groups.begin(), groups.end(), [](const IG& a, const IG& b) { return a.avg < b.avg; });
+                for (uint32_t gs : groups[0].idx) {
+                    for (int k = 0; k < (int)fc.size(); k++) {
+                        if (fc[k].slot == gs) {
+                            fc[k] = fc.back();
+                            fc.pop_back();
+                            k--;
+                        }
+                    }
+                }
+                l = (int)fc.size() + tcount;
+                if (l % tcm != 0) continue;
+            }
+            bool failed = false;                                                           // :287-296
+            int32_t last_cm = 0;  // l % cm for the previous entry's cm (entries mostly share one)
+            bool last_ok = true;
+            for (const CE& e : fc) {
+                const uint32_t s = e.slot;
+                const HotRec& hs = v.hot[s];
+                if (!v.live[s]) continue;
+                if (hs.minc > l || hs.maxc < l) { failed = true; break; }
+                if (hs.cm != last_cm) { last_cm = hs.cm; last_ok = l % hs.cm == 0; }
+                if (!last_ok) { failed = true; break; }
+            }
+            if (failed) continue;
+            group_out.clear();
+            for (const CE& e : fc) group_out.push_back({e.slot, (int)e.pi});
+            for (int k = 0; k < tcount; k++) group_out.push_back({T, k});
+            return MATCHED;
+        }
+        return NOMATCH;
+    }
+};
+
+// One pool's share of a parallel replay: a record per processed row, in row
+// order, and the matched groups' entries.
+struct PoolRec {
+    uint32_t bi;  // batch row (UINT32_MAX: the list's end sentinel)
+    uint8_t matched, expired;
+    uint32_t off, len;  // into PoolOut::ents (off: entries before this row)
+    uint32_t gcum, xcum;  // matched / expired rows before this one
+};
+// Over-aligned: the workers of a parallel replay fill different pools'
+// outputs at once, and vector headers sharing a cache line would bounce
+// between their cores on every push_back.
+struct alignas(128) PoolOut {
+    std::vector<PoolRec> recs;
+    std::vector<std::pair<uint32_t, int>> ents;
+};
+
+// Replays one pool's rows (batch rows `bis`, ascending; slot brow[bi]) over
+// complete hit lists: group_of(bi) gives the row's search.  `psel` and `proc`
+// start all zero and are restored to zero on return (the caller's thread
+// keeps them across tasks).  Appends the records + a sentinel to `o`.
+template <class GroupOf>
+void replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uint32_t* brow, GroupOf group_of,
+                 std::vector<uint8_t>& psel, uint8_t* proc, const int32_t* minc, const int32_t* maxc, PoolOut& o) {
+    std::vector<std::pair<uint32_t, int>> grp;
+    uint32_t gcum = 0, xcum = 0;
+    rp.proc = proc;
+    for (uint32_t bi : bis) {
+        const uint32_t T = brow[bi];
+        if (psel[T]) continue;
+        auto status = rp.row(T, group_of(bi), false, grp);  // complete lists: never EXHAUSTED
+        proc[T] = 1;
+        PoolRec rec{bi, 0, (uint8_t)(rp.v.intervals[T] + 1 >= rp.max_intervals || minc[T] == maxc[T]),
+                    (uint32_t)o.ents.size(), 0, gcum, xcum};
+        xcum += rec.expired;
+        if (status == ReplayCore::MATCHED) {
+            rec.matched = 1;
+            rec.len = (uint32_t)grp.size();
+            gcum++;
+            for (auto& e : grp) {
+                psel[e.first] = 1;
+                o.ents.push_back(e);
+            }
+        }
+        o.recs.push_back(rec);
+    }
+    for (auto& e : o.ents) psel[e.first] = 0;
+    for (const PoolRec& r : o.recs) proc[brow[r.bi]] = 0;
+    o.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)o.ents.size(), 0, gcum, xcum});  // sentinel
+}
+
+}  // namespace nkm
