@@ -59,10 +59,13 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pg = None
+    # torch's HIP runtime comes up before the library's (loading the library
+    # first leaves torch with "No HIP GPUs are available")
+    import torch
+    torch.cuda.set_device(local)
+    torch.cuda.synchronize(local)
     if world > 1:
-        import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         pg = dist
     return world, rank, local, pg

@@ -376,13 +376,23 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
         for (uint32_t i : pool_searches[gi]) mine.push_back(bg[i]);
         Replay rp(*this, psel, false, maxI, ls, st, stream_);
         // Intervals stay unwritten during the walk (slots of all pools share
-        // its cache lines): a row's increment is pending in tl_proc until the
-        // merge applies it.
+        // its cache lines): a row's increment is pending in tl_proc (generic
+        // walk) or in the dense walk's per-position flags until the merge
+        // applies it.
         {
             PoolOut& o = outs[gi];
-            replay_pool(rp, grows[gi], brow.data(),
-                        [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; }, psel,
-                        tl_proc.data(), minc_.data(), maxc_.data(), o);
+            if (mine.size() == 1) {  // one search: walk dense per-position copies of the pool
+                static thread_local DenseReplay tl_dense;
+                static thread_local std::vector<uint32_t> tl_pos;
+                if (tl_pos.size() < sel.size()) tl_pos.resize(sel.size(), kNoSlot);
+                tl_dense.hits_seen = 0;
+                tl_dense.run(Replay::view(*this), maxI, mine[0], grows[gi], brow.data(), tl_pos, o);
+                rp.hits_seen = tl_dense.hits_seen;
+            } else {
+                replay_pool(rp, grows[gi], brow.data(),
+                            [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; }, psel,
+                            tl_proc.data(), minc_.data(), maxc_.data(), o);
+            }
             task_ms[k] = msd(tw0, clk::now());
             task_hits[k] = rp.hits_seen;
             task_rows[k] = o.recs.size() - 1;

@@ -6,12 +6,14 @@
 // time per replay of the pool and a checksum of the groups so that variants
 // of the replay can be compared for speed and identical output.
 //
-//   make -C tools replay_bench && tools/replay_bench [tickets] [reps]
+//   make -C tools replay_bench && tools/replay_bench [tickets] [reps] [threads]   (RB_POOLS=n pools, RB_DENSE=1)
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <thread>
 #include <signal.h>
 #include <sys/time.h>
 #include <ucontext.h>
@@ -44,7 +46,9 @@ static uint64_t splitmix(uint64_t& s) {
 int main(int argc, char** argv) {
     const uint32_t N = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 1000000;
     const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
-    const int npools = 8;
+    const int nthreads = argc > 3 ? std::atoi(argv[3]) : 0;  // >0: replay every pool, one thread per pool
+    const bool dense = std::getenv("RB_DENSE") && *std::getenv("RB_DENSE");   // DenseReplay instead of replay_pool
+    const int npools = std::getenv("RB_POOLS") ? std::atoi(std::getenv("RB_POOLS")) : 8;
     uint64_t rng = 0x5EED0003ull;
     std::vector<HotRec> hot(N);
     std::vector<uint32_t> party(N), pres_sess;
@@ -81,8 +85,54 @@ int main(int argc, char** argv) {
             brow.push_back(i);
         }
     ReplayView v{hot.data(), pres_sess.data(), party.data(), intervals.data(), live.data(), count.data(), created.data()};
+    if (nthreads > 0) {
+        // every pool at once, `nthreads` threads taking pools from a counter
+        std::vector<std::vector<DHit>> ph(npools);
+        std::vector<std::vector<uint32_t>> pbrow(npools), pbis(npools);
+        for (uint32_t i = 0; i < N; i++) {
+            const uint32_t p = pool[i];
+            ph[p].push_back(DHit{i, (uint32_t)ph[p].size(), 0});
+            pbis[p].push_back((uint32_t)pbrow[p].size());
+            pbrow[p].push_back(i);
+        }
+        for (int r = 0; r < reps; r++) {
+            std::atomic<int> next{0};
+            std::vector<double> task(npools);
+            const auto t0 = std::chrono::steady_clock::now();
+            std::vector<std::thread> th;
+            for (int t = 0; t < nthreads; t++)
+                th.emplace_back([&] {
+                    std::vector<uint8_t> ps(N, 0), pr(N, 0);
+                    std::vector<uint32_t> pos_of(N, kNoSlot);
+                    DenseReplay dr;
+                    PoolOut po;
+                    for (int p; (p = next.fetch_add(1)) < npools;) {
+                        const auto a = std::chrono::steady_clock::now();
+                        BGroup g;
+                        g.hits = ph[p].data();
+                        g.n = (uint32_t)ph[p].size();
+                        NoDevice rp(v, ps, false, 2);
+                        po.recs.clear();
+                        po.ents.clear();
+                        if (dense) dr.run(v, 2, g, pbis[p], pbrow[p].data(), pos_of, po);
+                        else replay_pool(rp, pbis[p], pbrow[p].data(), [&](uint32_t) -> BGroup& { return g; }, ps,
+                                         pr.data(), minc.data(), maxc.data(), po);
+                        task[p] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+                    }
+                });
+            for (auto& t : th) t.join();
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            double mx = 0, sm = 0;
+            for (double x : task) mx = std::max(mx, x), sm += x;
+            std::printf("%d pools on %d threads: wall %.3f ms | task max %.3f mean %.3f ms\n", npools, nthreads, ms, mx,
+                        sm / npools);
+        }
+        return 0;
+    }
     std::vector<uint8_t> psel(N, 0), proc(N, 0);
     PoolOut o;  // reused across reps, as the library keeps its pool outputs
+    std::vector<uint32_t> pos_of(N, kNoSlot);
+    DenseReplay dr;
     const bool prof = std::getenv("RB_PROF") != nullptr;
     if (prof) {
         struct sigaction sa {};
@@ -104,8 +154,9 @@ int main(int argc, char** argv) {
         o.recs.clear();
         o.ents.clear();
         const auto t0 = std::chrono::steady_clock::now();
-        replay_pool(rp, bis, brow.data(), [&](uint32_t) -> BGroup& { return g; }, psel, proc.data(), minc.data(),
-                    maxc.data(), o);
+        if (dense) dr.run(v, 2, g, bis, brow.data(), pos_of, o);
+        else replay_pool(rp, bis, brow.data(), [&](uint32_t) -> BGroup& { return g; }, psel, proc.data(), minc.data(),
+                         maxc.data(), o);
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         best = std::min(best, ms);
         total += ms;
@@ -114,7 +165,7 @@ int main(int argc, char** argv) {
         for (auto& rc : o.recs) sum = (sum ^ (rc.bi * 7ull + rc.matched)) * 1099511628211ull;
         groups = o.recs.back().gcum;
         rows = o.recs.size() - 1;
-        hits_seen = rp.hits_seen;
+        hits_seen = dense ? dr.hits_seen / (r + 1) : rp.hits_seen;
     }
     if (prof) {
         itimerval off{};
