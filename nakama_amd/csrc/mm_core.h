@@ -414,6 +414,9 @@ public:
     GroupList pass_groups_;
     std::vector<uint32_t> expired_;
     std::vector<PoolOut> pool_outs_;
+    std::vector<DensePool> dense_pools_;  // dense replay per pool (kept: capacity reused)
+    std::vector<DenseRun> dense_runs_;
+    std::vector<uint32_t> pos_of_;        // slot -> list position during a dense replay, else kNoSlot
     Dict field_dict_;                 // field names -> field id
     std::vector<std::string> ticket_;
     std::vector<const char*> tk_ptr_;               // per slot: NUL-terminated ticket id in tk_blocks_
@@ -494,6 +497,8 @@ public:
     // parallel paths at any size (tests), unset: parallel above the sizes
     // where it pays.
     int par_mode_ = 1;  // 0 off, 1 auto, 2 force
+    // NKM_DENSE=0: single-search pools take the generic walk too (A/B, tests)
+    bool dense_mode_ = true;
     std::vector<uint32_t> custom_expired_;
 
     std::vector<std::string> debug_strings_;

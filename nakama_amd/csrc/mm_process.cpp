@@ -358,47 +358,68 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
         local_idx[i] = (uint32_t)pool_searches[search_pool[i]].size();
         pool_searches[search_pool[i]].push_back((uint32_t)i);
     }
+    // Pools with one search walk dense per-position copies of their list
+    // (DensePool/DenseRun); the copies are gathered first, in chunks across
+    // the workers.  Other pools take the generic walk over the store.
+    if (dense_pools_.size() < ng) dense_pools_.resize(ng);
+    if (dense_runs_.size() < ng) dense_runs_.resize(ng);
+    if (pos_of_.size() < ticket_.size()) pos_of_.resize(ticket_.size(), kNoSlot);
+    const ReplayView rv = Replay::view(*this);
+    std::vector<std::pair<uint32_t, uint32_t>> chunks;  // (pool, chunk) of the dense gathers
+    constexpr uint32_t kGatherChunk = 16384;
+    std::vector<uint8_t> dense(ng, 0);
+    for (size_t gi = 0; gi < ng; gi++) {
+        if (pool_searches[gi].size() != 1 || !dense_mode_) continue;
+        dense[gi] = 1;
+        DensePool& P = dense_pools_[gi];
+        P.reset(bg[pool_searches[gi][0]], grows[gi], brow.data());
+        for (uint32_t c = 0; c * kGatherChunk < P.n; c++) chunks.push_back({(uint32_t)gi, c});
+    }
+    wp.run(chunks.size(), [&](size_t t) {
+        DensePool& P = dense_pools_[chunks[t].first];
+        const uint32_t lo = chunks[t].second * kGatherChunk;
+        P.gather(rv, lo, std::min(P.n, lo + kGatherChunk), pos_of_.data());
+    });
     auto worker = [&](size_t k) {
         const auto tw0 = clk::now();
-        PassStats ls;
         const uint32_t gi = order_g[k];
-        // The worker thread's mask is all zero between tasks.  Starting from
-        // zero is exact: this batch's rows and hit lists hold no ticket an
-        // earlier batch selected (assembly skips them; the device alive mask
-        // dropped them before this batch's searches).
-        static thread_local std::vector<uint8_t> tl_sel;
-        if (tl_sel.size() < sel.size()) tl_sel.resize(sel.size(), 0);
-        std::vector<uint8_t>& psel = tl_sel;
-        static thread_local std::vector<uint8_t> tl_proc;  // rows processed in this task
-        if (tl_proc.size() < sel.size()) tl_proc.resize(sel.size(), 0);
-        std::vector<BGroup> mine;
-        mine.reserve(pool_searches[gi].size());
-        for (uint32_t i : pool_searches[gi]) mine.push_back(bg[i]);
-        Replay rp(*this, psel, false, maxI, ls, st, stream_);
-        // Intervals stay unwritten during the walk (slots of all pools share
-        // its cache lines): a row's increment is pending in tl_proc (generic
-        // walk) or in the dense walk's per-position flags until the merge
-        // applies it.
-        {
-            PoolOut& o = outs[gi];
-            if (mine.size() == 1) {  // one search: walk dense per-position copies of the pool
-                static thread_local DenseReplay tl_dense;
-                static thread_local std::vector<uint32_t> tl_pos;
-                if (tl_pos.size() < sel.size()) tl_pos.resize(sel.size(), kNoSlot);
-                tl_dense.hits_seen = 0;
-                tl_dense.run(Replay::view(*this), maxI, mine[0], grows[gi], brow.data(), tl_pos, o);
-                rp.hits_seen = tl_dense.hits_seen;
-            } else {
-                replay_pool(rp, grows[gi], brow.data(),
-                            [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; }, psel,
-                            tl_proc.data(), minc_.data(), maxc_.data(), o);
-            }
-            task_ms[k] = msd(tw0, clk::now());
+        PoolOut& o = outs[gi];
+        if (dense[gi]) {
+            DenseRun& run = dense_runs_[gi];
+            run.reset(dense_pools_[gi].n);
+            run.walk(dense_pools_[gi], rv, maxI, pos_of_.data(), 0, dense_pools_[gi].nrows);
+            run.finish(o);
+            task_hits[k] = run.hits_seen;
+        } else {
+            // The worker thread's masks are all zero between tasks.  Starting
+            // from zero is exact: this batch's rows and hit lists hold no
+            // ticket an earlier batch selected (assembly skips them; the
+            // device alive mask dropped them before this batch's searches).
+            // Intervals stay unwritten during the walk (slots of all pools
+            // share its cache lines): a row's increment is pending in tl_proc
+            // until the merge applies it.
+            static thread_local std::vector<uint8_t> tl_sel, tl_proc;
+            if (tl_sel.size() < sel.size()) tl_sel.resize(sel.size(), 0);
+            if (tl_proc.size() < sel.size()) tl_proc.resize(sel.size(), 0);
+            PassStats ls;
+            std::vector<BGroup> mine;
+            mine.reserve(pool_searches[gi].size());
+            for (uint32_t i : pool_searches[gi]) mine.push_back(bg[i]);
+            Replay rp(*this, tl_sel, false, maxI, ls, st, stream_);
+            replay_pool(rp, grows[gi], brow.data(),
+                        [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; }, tl_sel,
+                        tl_proc.data(), minc_.data(), maxc_.data(), o);
             task_hits[k] = rp.hits_seen;
-            task_rows[k] = o.recs.size() - 1;
         }
+        task_ms[k] = msd(tw0, clk::now());
+        task_rows[k] = o.recs.size() - 1;
     };
     wp.run(ng, worker);
+    wp.run(chunks.size(), [&](size_t t) {
+        const DensePool& P = dense_pools_[chunks[t].first];
+        const uint32_t lo = chunks[t].second * kGatherChunk;
+        P.clear_pos(lo, std::min(P.n, lo + kGatherChunk), pos_of_.data());
+    });
     const auto tp2 = clk::now();
     // Merge back into the pinned row order.  The batch's row range is cut
     // into chunks; each pool's records (ascending in batch row, with running

@@ -83,6 +83,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     NKM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     NKM_HIP(hipEventCreate(&ev0_));
     NKM_HIP(hipEventCreate(&ev1_));
+    if (const char* e = std::getenv("NKM_DENSE")) dense_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_PARALLEL")) par_mode_ = !std::strcmp(e, "0") ? 0 : !std::strcmp(e, "force") ? 2 : 1;
     for (int f = 0; f < F_NBUILTIN; f++) field_dict_.intern(kBuiltinNames[f]);
     fval_.resize(F_NBUILTIN);
@@ -181,16 +182,16 @@ static std::vector<int> worker_cpus(unsigned want) {
     return out;
 }
 
-// Host worker count: NKM_THREADS, else the visible cores capped at 8.  The
-// per-GPU host share on an 8-GPU node is 16 CPUs, but measured on MI355X
-// boxes (profiles/r01_threads_*) 8 workers beat 16 on every pass phase: the
-// replay has one task per pool, and the extra workers only add contention.
+// Host worker count: NKM_THREADS, else the visible cores capped at 16 (the
+// per-GPU host share on an 8-GPU node).  Same-box A/B runs on MI355X boxes
+// (profiles/r01_ab_threads.txt) put 8 and 16 workers within the boxes'
+// run-to-run noise on C3 (8 pools); 16 keeps pools > 8 (C4) parallel.
 WorkPool& Core::workers() {
     if (!workers_) {
         unsigned n = std::thread::hardware_concurrency();
         cpu_set_t cs;
         if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = (unsigned)CPU_COUNT(&cs);
-        n = std::max(1u, std::min(8u, n));
+        n = std::max(1u, std::min(16u, n));
         if (const char* e = std::getenv("NKM_THREADS")) n = std::max(1, std::atoi(e));
         workers_.reset(new WorkPool(n, worker_cpus(n - 1)));
     }

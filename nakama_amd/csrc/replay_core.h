@@ -321,204 +321,244 @@ void replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uint32_
     o.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)o.ents.size(), 0, gcum, xcum});  // sentinel
 }
 
-// Dense replay of a pool with a single complete search (no RevPrecision):
-// the same loop body as ReplayCore::row, but every per-ticket field the walk
-// reads is first gathered into arrays indexed by list position (records,
-// sessions, selection and processed flags), so the walk streams contiguous
-// memory instead of chasing slots through the store.  Output is identical to
-// replay_pool over the same list (tests/test_gpu_parity.py checks the
+// ---- dense pool replay (a pool with one complete search, no RevPrecision) ----
+//
+// The same loop body as ReplayCore::row, but every per-ticket field the walk
+// reads is first gathered into arrays indexed by list position (in parallel
+// chunks), so the walk streams contiguous memory instead of chasing slots
+// through the store.  Output is identical to replay_pool over the same list
+// (tools/replay_bench.cpp checks it; tests/test_gpu_parity.py checks the
 // parallel paths against the serial one).
-struct DenseReplay {
-    struct LRec {
-        int32_t count, minc, maxc, cm;
-        uint32_t party, sess0, pres_off, intervals, smask;
-    };
-    std::vector<LRec> rec;
-    std::vector<uint32_t> slot, pres;
-    std::vector<uint8_t> lsel, lproc;
-    std::vector<std::vector<CE>> combos;
-    std::vector<uint32_t> cmask;
-    std::vector<std::pair<uint32_t, int>> grp;
-    uint64_t hits_seen = 0;
+//
+// (A pool's walk is not cut into speculative segments: tried, with an exact
+// state-difference repair, but on C3 pools the speculative and true runs stay
+// one group boundary apart indefinitely — the greedy packing locks onto its
+// phase — so the repair degenerated to the serial walk.)
 
-    // pos_of: per-slot scratch, all kNoSlot on entry and on return.
-    template <class Rows>
-    void run(const ReplayView& v, int max_intervals, const BGroup& g, const Rows& bis, const uint32_t* brow,
-             std::vector<uint32_t>& pos_of, PoolOut& o) {
-        const uint32_t n = g.n;
-        rec.resize(n);
-        slot.resize(n);
-        lsel.assign(n, 0);
-        lproc.assign(n, 0);
-        pres.clear();
-        for (uint32_t k = 0; k < n; k++) {
-            const uint32_t s = g.hits[k].slot;
-            if (k + 16 < n) {
-                const uint32_t p = g.hits[k + 16].slot;
+struct DenseRec {
+    int32_t count, minc, maxc, cm;
+    uint32_t party, sess0, pres_off, intervals, smask;
+};
+
+// One pool's per-position copies (filled by gather, in parallel chunks).
+struct DensePool {
+    const DHit* hits = nullptr;
+    uint32_t n = 0;
+    const uint32_t* bis = nullptr;  // the pool's batch rows, ascending
+    uint32_t nrows = 0;
+    const uint32_t* brow = nullptr;  // batch row -> slot
+    std::vector<DenseRec> rec;
+    std::vector<uint32_t> slot;
+
+    void reset(const BGroup& g, const std::vector<uint32_t>& rows, const uint32_t* batch_slots) {
+        hits = g.hits;
+        n = g.n;
+        bis = rows.data();
+        nrows = (uint32_t)rows.size();
+        brow = batch_slots;
+        if (rec.size() < n) rec.resize(n);
+        if (slot.size() < n) slot.resize(n);
+    }
+    // positions [lo, hi): records, slots, and pos_of[slot] = position
+    void gather(const ReplayView& v, uint32_t lo, uint32_t hi, uint32_t* pos_of) {
+        for (uint32_t k = lo; k < hi; k++) {
+            const uint32_t s = hits[k].slot;
+            if (k + 16 < hi) {
+                const uint32_t p = hits[k + 16].slot;
                 __builtin_prefetch(&v.hot[p]);
                 __builtin_prefetch(&v.intervals[p]);
                 __builtin_prefetch(&pos_of[p], 1);
             }
             const HotRec& h = v.hot[s];
-            LRec& r = rec[k];
-            r.count = h.count;
-            r.minc = h.minc;
-            r.maxc = h.maxc;
-            r.cm = h.cm;
-            r.party = h.party;
-            r.sess0 = h.sess0;
-            r.smask = h.smask;
-            r.intervals = (uint32_t)v.intervals[s];
-            r.pres_off = (uint32_t)pres.size();
-            if (h.count > 1)
-                for (int q = 0; q < h.count; q++) pres.push_back(v.pres_sess[h.pres_off + q]);
+            rec[k] = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party, h.sess0, h.pres_off,
+                              (uint32_t)v.intervals[s], h.smask};
             slot[k] = s;
             pos_of[s] = k;
         }
-        uint32_t head = 0, gcum = 0, xcum = 0;
+    }
+    void clear_pos(uint32_t lo, uint32_t hi, uint32_t* pos_of) const {
+        for (uint32_t k = lo; k < hi; k++) pos_of[slot[k]] = kNoSlot;
+    }
+};
+
+// The state and output of one walk over a range of a pool's rows.
+struct DenseRun {
+    std::vector<uint8_t> sel, proc;  // by position
+    uint32_t head = 0;               // positions before head are all selected
+    // output: one record per processed row, and the matched groups' entries
+    std::vector<PoolRec> recs;
+    std::vector<std::pair<uint32_t, int>> ents;
+    uint64_t hits_seen = 0;
+    // scratch
+    std::vector<std::vector<CE>> combos;
+    std::vector<uint32_t> cmask;
+    std::vector<std::pair<uint32_t, int>> grp;
+
+    void reset(uint32_t n) {
+        sel.assign(n, 0);
+        proc.assign(n, 0);
+        head = 0;
+        recs.clear();
+        ents.clear();
+        hits_seen = 0;
+    }
+
+    // processDefault's loop body for row index j (ReplayCore::row over the
+    // dense copies).  Returns false when the row's ticket is already selected.
+    bool step(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of, uint32_t j) {
+        const uint32_t n = P.n;
+        const uint32_t bi = P.bis[j];
+        const uint32_t T = P.brow[bi];
+        const uint32_t kT = pos_of[T];
+        if (kT != kNoSlot && sel[kT]) return false;
+        DenseRec rt;
+        const uint32_t* tpres = v.pres_sess;
+        if (kT != kNoSlot) {
+            rt = P.rec[kT];
+        } else {
+            const HotRec& h = v.hot[T];
+            rt = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party, h.sess0, h.pres_off, (uint32_t)v.intervals[T], h.smask};
+        }
+        const bool last = (int)rt.intervals + 1 >= max_intervals || rt.minc == rt.maxc;
+        const int tcount = rt.count, tmax = rt.maxc, tmin = rt.minc, tcm = rt.cm;
+        const uint32_t tparty = rt.party;
+        auto t_has = [&](uint32_t sess) {
+            if (tcount == 1) return rt.sess0 == sess;
+            for (int q = 0; q < tcount; q++)
+                if (tpres[rt.pres_off + q] == sess) return true;
+            return false;
+        };
+        auto h_has = [&](const DenseRec& h, uint32_t sess) {
+            if (h.count == 1) return h.sess0 == sess;
+            for (int q = 0; q < h.count; q++)
+                if (v.pres_sess[h.pres_off + q] == sess) return true;
+            return false;
+        };
         size_t ncomb = 0;
-        for (uint32_t bi : bis) {
-            const uint32_t T = brow[bi];
-            const uint32_t kT = pos_of[T];
-            if (kT != kNoSlot && lsel[kT]) continue;
-            // the row's own record: from the list when it is on it, else the store
-            LRec rt;
-            const uint32_t* tpres;
-            if (kT != kNoSlot) {
-                rt = rec[kT];
-                tpres = pres.data();
-            } else {
-                const HotRec& h = v.hot[T];
-                rt = LRec{h.count, h.minc, h.maxc, h.cm, h.party, h.sess0, h.pres_off, (uint32_t)v.intervals[T], h.smask};
-                tpres = v.pres_sess;
+        while (head < n && sel[head]) head++;
+        bool matched = false;
+        for (uint32_t i = head; i < n; i++) {
+            hits_seen++;
+            if (i == kT || sel[i]) continue;
+            const DenseRec& hh = P.rec[i];
+            if (tparty != kNoParty && hh.party == tparty) continue;                      // :80-85
+            if (tmax < hh.maxc && (int)hh.intervals + proc[i] <= max_intervals) continue;  // :150-153
+            if (rt.smask & hh.smask) {                                                   // :155-165
+                bool shared = false;
+                if (hh.count == 1) shared = t_has(hh.sess0);
+                else
+                    for (int q = 0; q < hh.count && !shared; q++) shared = t_has(v.pres_sess[hh.pres_off + q]);
+                if (shared) continue;
             }
-            const bool last = (int)rt.intervals + 1 >= max_intervals || rt.minc == rt.maxc;
-            const int tcount = rt.count, tmax = rt.maxc, tmin = rt.minc, tcm = rt.cm;
-            const uint32_t tparty = rt.party;
-            auto t_has = [&](uint32_t sess) {
-                if (tcount == 1) return rt.sess0 == sess;
-                for (int q = 0; q < tcount; q++)
-                    if (tpres[rt.pres_off + q] == sess) return true;
-                return false;
-            };
-            auto h_has = [&](const LRec& h, uint32_t sess) {
-                if (h.count == 1) return h.sess0 == sess;
-                for (int q = 0; q < h.count; q++)
-                    if (pres[h.pres_off + q] == sess) return true;
-                return false;
-            };
-            ncomb = 0;
-            while (head < n && lsel[head]) head++;
-            bool matched = false;
-            for (uint32_t i = head; i < n; i++) {
-                hits_seen++;
-                if (i == kT || lsel[i]) continue;
-                const LRec& hh = rec[i];
-                if (tparty != kNoParty && hh.party == tparty) continue;                      // :80-85
-                if (tmax < hh.maxc && (int)hh.intervals + lproc[i] <= max_intervals) continue;  // :150-153
-                if (rt.smask & hh.smask) {                                                   // :155-165
-                    bool shared = false;
-                    if (hh.count == 1) shared = t_has(hh.sess0);
-                    else
-                        for (int q = 0; q < hh.count && !shared; q++) shared = t_has(pres[hh.pres_off + q]);
-                    if (shared) continue;
-                }
-                bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
-                int found = -1;
-                const int hcount = hh.count;
-                for (size_t ci = 0; ci < ncomb; ci++) {
-                    auto& combo = combos[ci];
-                    if ((int)combo.size() + hcount + tcount <= tmax) {
-                        if (cmask[ci] & hh.smask)
-                            for (const CE& e : combo)
-                                if (h_has(hh, e.sess)) { sconf = true; break; }
-                        if (sconf) continue;
-                        for (int k = 0; k < hcount; k++)
-                            combo.push_back(CE{slot[i], (uint32_t)k, i, hcount == 1 ? hh.sess0 : pres[hh.pres_off + k]});
-                        cmask[ci] |= hh.smask;
-                        found = (int)ci;
-                        break;
-                    }
-                }
-                if (found < 0) {
-                    if (ncomb == combos.size()) {
-                        combos.emplace_back();
-                        cmask.push_back(0);
-                    }
-                    std::vector<CE>& nc = combos[ncomb];
-                    nc.clear();
+            bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
+            int found = -1;
+            const int hcount = hh.count;
+            for (size_t ci = 0; ci < ncomb; ci++) {
+                auto& combo = combos[ci];
+                if ((int)combo.size() + hcount + tcount <= tmax) {
+                    if (cmask[ci] & hh.smask)
+                        for (const CE& e : combo)
+                            if (h_has(hh, e.sess)) { sconf = true; break; }
+                    if (sconf) continue;
                     for (int k = 0; k < hcount; k++)
-                        nc.push_back(CE{slot[i], (uint32_t)k, i, hcount == 1 ? hh.sess0 : pres[hh.pres_off + k]});
-                    cmask[ncomb] = hh.smask;
-                    found = (int)ncomb++;
+                        combo.push_back(CE{P.slot[i], (uint32_t)k, i, hcount == 1 ? hh.sess0 : v.pres_sess[hh.pres_off + k]});
+                    cmask[ci] |= hh.smask;
+                    found = (int)ci;
+                    break;
                 }
-                std::vector<CE>& fc = combos[found];
-                int l = (int)fc.size() + tcount;
-                bool form = l == tmax;
-                if (!form && last && l >= tmin && l <= tmax) {
-                    bool more = false;  // an unselected, non-self, non-party hit after i (:130, :233)
-                    for (uint32_t j = i + 1; j < n && !more; j++)
-                        more = j != kT && !lsel[j] && !(tparty != kNoParty && rec[j].party == tparty);
-                    form = !more;
+            }
+            if (found < 0) {
+                if (ncomb == combos.size()) {
+                    combos.emplace_back();
+                    cmask.push_back(0);
                 }
-                if (!form) continue;
-                const int rem = l % tcm;
-                if (rem != 0) {                                                              // :234-280
-                    std::vector<uint32_t> elig;
-                    for (const CE& e : fc) {
-                        if (!v.live[e.slot] || v.count[e.slot] > rem) continue;
-                        if (std::find(elig.begin(), elig.end(), e.slot) == elig.end()) elig.push_back(e.slot);
-                    }
-                    std::vector<IG> groups;
-                    group_indexes(elig, 0, rem, v.count, v.created, groups);
-                    if (groups.empty()) continue;
-                    std::stable_sort(groups.begin(), groups.end(), [](const IG& a, const IG& b) { return a.avg < b.avg; });
-                    for (uint32_t gs : groups[0].idx) {
-                        for (int k = 0; k < (int)fc.size(); k++) {
-                            if (fc[k].slot == gs) {
-                                fc[k] = fc.back();
-                                fc.pop_back();
-                                k--;
-                            }
+                std::vector<CE>& nc = combos[ncomb];
+                nc.clear();
+                for (int k = 0; k < hcount; k++)
+                    nc.push_back(CE{P.slot[i], (uint32_t)k, i, hcount == 1 ? hh.sess0 : v.pres_sess[hh.pres_off + k]});
+                cmask[ncomb] = hh.smask;
+                found = (int)ncomb++;
+            }
+            std::vector<CE>& fc = combos[found];
+            int l = (int)fc.size() + tcount;
+            bool form = l == tmax;
+            if (!form && last && l >= tmin && l <= tmax) {
+                bool more = false;  // an unselected, non-self, non-party hit after i (:130, :233)
+                for (uint32_t q = i + 1; q < n && !more; q++)
+                    more = q != kT && !sel[q] && !(tparty != kNoParty && P.rec[q].party == tparty);
+                form = !more;
+            }
+            if (!form) continue;
+            const int rem = l % tcm;
+            if (rem != 0) {                                                              // :234-280
+                std::vector<uint32_t> elig;
+                for (const CE& e : fc) {
+                    if (!v.live[e.slot] || v.count[e.slot] > rem) continue;
+                    if (std::find(elig.begin(), elig.end(), e.slot) == elig.end()) elig.push_back(e.slot);
+                }
+                std::vector<IG> groups;
+                group_indexes(elig, 0, rem, v.count, v.created, groups);
+                if (groups.empty()) continue;
+                std::stable_sort(groups.begin(), groups.end(), [](const IG& a, const IG& b) { return a.avg < b.avg; });
+                for (uint32_t gs : groups[0].idx) {
+                    for (int k = 0; k < (int)fc.size(); k++) {
+                        if (fc[k].slot == gs) {
+                            fc[k] = fc.back();
+                            fc.pop_back();
+                            k--;
                         }
                     }
-                    l = (int)fc.size() + tcount;
-                    if (l % tcm != 0) continue;
                 }
-                bool failed = false;                                                         // :287-296
-                int32_t last_cm = 0;
-                bool last_ok = true;
-                for (const CE& e : fc) {
-                    if (!v.live[e.slot]) continue;
-                    const LRec& hs = rec[e.lpos];
-                    if (hs.minc > l || hs.maxc < l) { failed = true; break; }
-                    if (hs.cm != last_cm) { last_cm = hs.cm; last_ok = l % hs.cm == 0; }
-                    if (!last_ok) { failed = true; break; }
-                }
-                if (failed) continue;
-                grp.clear();
-                for (const CE& e : fc) {
-                    grp.push_back({e.slot, (int)e.pi});
-                    lsel[e.lpos] = 1;
-                }
-                for (int k = 0; k < tcount; k++) grp.push_back({T, k});
-                if (kT != kNoSlot) lsel[kT] = 1;
-                matched = true;
-                break;
+                l = (int)fc.size() + tcount;
+                if (l % tcm != 0) continue;
             }
-            if (kT != kNoSlot) lproc[kT] = 1;
-            PoolRec r{bi, 0, (uint8_t)last, (uint32_t)o.ents.size(), 0, gcum, xcum};
-            xcum += r.expired;
-            if (matched) {
-                r.matched = 1;
-                r.len = (uint32_t)grp.size();
-                gcum++;
-                o.ents.insert(o.ents.end(), grp.begin(), grp.end());
+            bool failed = false;                                                         // :287-296
+            int32_t last_cm = 0;
+            bool last_ok = true;
+            for (const CE& e : fc) {
+                if (!v.live[e.slot]) continue;
+                const DenseRec& hs = P.rec[e.lpos];
+                if (hs.minc > l || hs.maxc < l) { failed = true; break; }
+                if (hs.cm != last_cm) { last_cm = hs.cm; last_ok = l % hs.cm == 0; }
+                if (!last_ok) { failed = true; break; }
             }
-            o.recs.push_back(r);
+            if (failed) continue;
+            grp.clear();
+            for (const CE& e : fc) {
+                grp.push_back({e.slot, (int)e.pi});
+                sel[e.lpos] = 1;
+            }
+            for (int k = 0; k < tcount; k++) grp.push_back({T, k});
+            if (kT != kNoSlot) sel[kT] = 1;
+            matched = true;
+            break;
         }
-        for (uint32_t k = 0; k < n; k++) pos_of[slot[k]] = kNoSlot;
-        o.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)o.ents.size(), 0, gcum, xcum});  // sentinel
+        if (kT != kNoSlot) proc[kT] = 1;
+        recs.push_back(PoolRec{bi, (uint8_t)matched, (uint8_t)last, (uint32_t)ents.size(),
+                               matched ? (uint32_t)grp.size() : 0u, 0, 0});
+        if (matched) ents.insert(ents.end(), grp.begin(), grp.end());
+        return true;
+    }
+
+    void walk(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of, uint32_t j0,
+              uint32_t j1) {
+        for (uint32_t j = j0; j < j1; j++) step(P, v, max_intervals, pos_of, j);
+    }
+
+    // Hands the records to a PoolOut (running offsets/counts, sentinel).
+    void finish(PoolOut& o) {
+        uint32_t g = 0, x = 0, off = 0;
+        for (PoolRec& r : recs) {
+            r.off = off;
+            r.gcum = g;
+            r.xcum = x;
+            off += r.len;
+            g += r.matched;
+            x += r.expired;
+        }
+        recs.push_back(PoolRec{UINT32_MAX, 0, 0, off, 0, g, x});
+        o.recs.swap(recs);
+        o.ents.swap(ents);
     }
 };
 

@@ -1,21 +1,31 @@
-// tools/replay_bench.cpp — times the host greedy replay (replay_core.h) alone,
-// on a C3-shaped pool: one pool's tickets interleaved with 7 others in slot
-// order (as the store holds them), party sizes {1:60%,2:20%,3:10%,4:5%,5:5%},
-// one session per presence, Min=Max=10, CountMultiple=5, a complete
-// constant-score hit list = the pool's tickets in created order.  Prints the
-// time per replay of the pool and a checksum of the groups so that variants
-// of the replay can be compared for speed and identical output.
+// tools/replay_bench.cpp — times the host greedy replay (replay_core.h) alone
+// and checks that its variants agree, on synthetic pools shaped like the
+// bench configs: NPOOLS pools interleaved in slot order (as the store holds
+// them), one session per presence, one complete constant-score hit list per
+// pool = the pool's tickets in created order.
 //
-//   make -C tools replay_bench && tools/replay_bench [tickets] [reps] [threads]   (RB_POOLS=n pools, RB_DENSE=1)
+//   RB_MODE=c3     party sizes {1:60%,2:20%,3:10%,4:5%,5:5%}, Min=Max=10, CM=5 (default)
+//   RB_MODE=solo2  solo tickets, Min=Max=2 (1v1)
+//   RB_MODE=mixed  parties, Min 4..10 / Max 10, CM 1 or 2, Intervals 0..2
+//                  (exercises the last-interval rule and the CountMultiple trim)
+//
+//   tools/replay_bench [tickets] [reps] [threads]
+//     threads = 0: pool 0 only, single thread: generic replay_pool vs the
+//                  dense walk (checksums must match; exit status 1 if not)
+//     threads > 0: every pool, dense: gathers in chunks, then one walk per
+//                  pool, on `threads` threads
+//   RB_POOLS=n (default 8), RB_PROF=1 (SIGPROF sampler -> /tmp/rb_prof.txt)
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
-#include <thread>
 #include <signal.h>
+#include <string>
 #include <sys/time.h>
+#include <thread>
 #include <ucontext.h>
 
 #include "../nakama_amd/csrc/replay_core.h"
@@ -28,8 +38,6 @@ struct NoDevice : ReplayCore {
     bool pair_slow(const BGroup&, uint32_t, uint32_t) override { std::abort(); }
 };
 
-// RB_PROF=1: a SIGPROF sampler of the instruction pointer (no profiler in the
-// image); addresses go to llvm-symbolizer.
 static uint64_t g_samples[1 << 16];
 static volatile size_t g_ns = 0;
 static void on_prof(int, siginfo_t*, void* ctx) {
@@ -43,23 +51,45 @@ static uint64_t splitmix(uint64_t& s) {
     return z ^ (z >> 31);
 }
 
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static uint64_t checksum(const PoolOut& o) {
+    uint64_t sum = 1469598103934665603ull;
+    for (auto& e : o.ents) sum = (sum ^ (e.first * 131ull + (uint64_t)e.second)) * 1099511628211ull;
+    for (auto& rc : o.recs)
+        sum = (sum ^ (rc.bi * 7ull + rc.matched * 3ull + rc.expired + rc.len * 11ull + rc.off * 13ull + rc.gcum * 17ull +
+                      rc.xcum * 19ull)) * 1099511628211ull;
+    return sum;
+}
+
 int main(int argc, char** argv) {
     const uint32_t N = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 1000000;
     const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
-    const int nthreads = argc > 3 ? std::atoi(argv[3]) : 0;  // >0: replay every pool, one thread per pool
-    const bool dense = std::getenv("RB_DENSE") && *std::getenv("RB_DENSE");   // DenseReplay instead of replay_pool
+    const int nthreads = argc > 3 ? std::atoi(argv[3]) : 0;
     const int npools = std::getenv("RB_POOLS") ? std::atoi(std::getenv("RB_POOLS")) : 8;
+    const std::string mode = std::getenv("RB_MODE") ? std::getenv("RB_MODE") : "c3";
+    const int maxI = 2;
     uint64_t rng = 0x5EED0003ull;
     std::vector<HotRec> hot(N);
     std::vector<uint32_t> party(N), pres_sess;
-    std::vector<int32_t> intervals(N, 0), count(N), minc(N, 10), maxc(N, 10);
+    std::vector<int32_t> intervals(N, 0), count(N), minc(N), maxc(N);
     std::vector<uint8_t> live(N, 1);
     std::vector<int64_t> created(N);
     std::vector<uint32_t> pool(N);
     uint32_t next_party = 0, next_sess = 0;
     for (uint32_t i = 0; i < N; i++) {
         const double u = (splitmix(rng) >> 11) * 0x1.0p-53;
-        const int ps = u < 0.60 ? 1 : u < 0.80 ? 2 : u < 0.90 ? 3 : u < 0.95 ? 4 : 5;
+        int ps = u < 0.60 ? 1 : u < 0.80 ? 2 : u < 0.90 ? 3 : u < 0.95 ? 4 : 5;
+        int mn = 10, mx = 10, cm = 5;
+        if (mode == "solo2") ps = 1, mn = mx = 2, cm = 1;
+        if (mode == "mixed") {
+            mn = 4 + (int)(splitmix(rng) % 7);
+            mx = 10;
+            cm = splitmix(rng) % 3 == 0 ? 2 : 1;
+            intervals[i] = (int)(splitmix(rng) % 3);
+        }
         pool[i] = (uint32_t)(splitmix(rng) % npools);
         party[i] = ps > 1 ? next_party++ : kNoParty;
         HotRec& h = hot[i];
@@ -68,116 +98,129 @@ int main(int argc, char** argv) {
         for (int p = 0; p < ps; p++) pres_sess.push_back(next_sess++);
         h.sess0 = pres_sess[h.pres_off];
         h.count = count[i] = ps;
-        h.minc = 10;
-        h.maxc = 10;
-        h.cm = 5;
+        h.minc = minc[i] = mn;
+        h.maxc = maxc[i] = mx;
+        h.cm = cm;
         h.smask = 0;
         for (int p = 0; p < ps; p++) h.smask |= 1u << (pres_sess[h.pres_off + p] & 31);
         created[i] = 1700000000000000000ll + 1024ll * i;
     }
-    // pool 0's hit list and rows
-    std::vector<DHit> hits;
-    std::vector<uint32_t> brow, bis;
-    for (uint32_t i = 0; i < N; i++)
-        if (pool[i] == 0) {
-            hits.push_back(DHit{i, (uint32_t)hits.size(), 0});
-            bis.push_back((uint32_t)brow.size());
-            brow.push_back(i);
-        }
+    std::vector<std::vector<DHit>> ph(npools);
+    std::vector<std::vector<uint32_t>> pbis(npools);
+    std::vector<uint32_t> brow(N);  // batch row i = slot i
+    for (uint32_t i = 0; i < N; i++) {
+        brow[i] = i;
+        ph[pool[i]].push_back(DHit{i, (uint32_t)ph[pool[i]].size(), 0});
+        pbis[pool[i]].push_back(i);
+    }
     ReplayView v{hot.data(), pres_sess.data(), party.data(), intervals.data(), live.data(), count.data(), created.data()};
-    if (nthreads > 0) {
-        // every pool at once, `nthreads` threads taking pools from a counter
-        std::vector<std::vector<DHit>> ph(npools);
-        std::vector<std::vector<uint32_t>> pbrow(npools), pbis(npools);
-        for (uint32_t i = 0; i < N; i++) {
-            const uint32_t p = pool[i];
-            ph[p].push_back(DHit{i, (uint32_t)ph[p].size(), 0});
-            pbis[p].push_back((uint32_t)pbrow[p].size());
-            pbrow[p].push_back(i);
+    std::vector<uint32_t> pos_of(N, kNoSlot);
+
+    if (nthreads == 0) {
+        // pool 0: generic vs dense, same output required
+        std::vector<uint8_t> psel(N, 0), proc(N, 0);
+        PoolOut og, od;
+        DensePool P;
+        DenseRun run;
+        BGroup g;
+        g.hits = ph[0].data();
+        g.n = (uint32_t)ph[0].size();
+        double bg = 1e30, bd = 1e30;
+        uint64_t hg = 0;
+        const bool prof = std::getenv("RB_PROF") != nullptr;
+        if (prof) {
+            struct sigaction sa {};
+            sa.sa_sigaction = on_prof;
+            sa.sa_flags = SA_SIGINFO | SA_RESTART;
+            sigaction(SIGPROF, &sa, nullptr);
+            itimerval it{{0, 200}, {0, 200}};
+            setitimer(ITIMER_PROF, &it, nullptr);
         }
         for (int r = 0; r < reps; r++) {
-            std::atomic<int> next{0};
-            std::vector<double> task(npools);
-            const auto t0 = std::chrono::steady_clock::now();
-            std::vector<std::thread> th;
-            for (int t = 0; t < nthreads; t++)
-                th.emplace_back([&] {
-                    std::vector<uint8_t> ps(N, 0), pr(N, 0);
-                    std::vector<uint32_t> pos_of(N, kNoSlot);
-                    DenseReplay dr;
-                    PoolOut po;
-                    for (int p; (p = next.fetch_add(1)) < npools;) {
-                        const auto a = std::chrono::steady_clock::now();
-                        BGroup g;
-                        g.hits = ph[p].data();
-                        g.n = (uint32_t)ph[p].size();
-                        NoDevice rp(v, ps, false, 2);
-                        po.recs.clear();
-                        po.ents.clear();
-                        if (dense) dr.run(v, 2, g, pbis[p], pbrow[p].data(), pos_of, po);
-                        else replay_pool(rp, pbis[p], pbrow[p].data(), [&](uint32_t) -> BGroup& { return g; }, ps,
-                                         pr.data(), minc.data(), maxc.data(), po);
-                        task[p] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
-                    }
-                });
-            for (auto& t : th) t.join();
-            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-            double mx = 0, sm = 0;
-            for (double x : task) mx = std::max(mx, x), sm += x;
-            std::printf("%d pools on %d threads: wall %.3f ms | task max %.3f mean %.3f ms\n", npools, nthreads, ms, mx,
-                        sm / npools);
+            og.recs.clear();
+            og.ents.clear();
+            g.head = 0;
+            NoDevice rp(v, psel, false, maxI);
+            double t0 = now_ms();
+            replay_pool(rp, pbis[0], brow.data(), [&](uint32_t) -> BGroup& { return g; }, psel, proc.data(), minc.data(),
+                        maxc.data(), og);
+            bg = std::min(bg, now_ms() - t0);
+            hg = rp.hits_seen;
+            t0 = now_ms();
+            P.reset(g, pbis[0], brow.data());
+            P.gather(v, 0, P.n, pos_of.data());
+            run.reset(P.n);
+            run.walk(P, v, maxI, pos_of.data(), 0, P.nrows);
+            run.finish(od);
+            P.clear_pos(0, P.n, pos_of.data());
+            bd = std::min(bd, now_ms() - t0);
         }
-        return 0;
+        if (prof) {
+            itimerval off{};
+            setitimer(ITIMER_PROF, &off, nullptr);
+            std::map<uint64_t, size_t> h;
+            for (size_t i = 0; i < g_ns; i++) h[g_samples[i]]++;
+            FILE* f = std::fopen("/tmp/rb_prof.txt", "w");
+            for (auto& kv : h) std::fprintf(f, "%zu 0x%llx\n", kv.second, (unsigned long long)kv.first);
+            std::fclose(f);
+        }
+        const uint64_t cg = checksum(og), cd = checksum(od);
+        std::printf("[%s] pool of %u tickets: %zu rows, %u groups, %llu hits | generic %.3f ms | dense %.3f ms | "
+                    "checksums %016llx %016llx %s\n",
+                    mode.c_str(), g.n, og.recs.size() - 1, og.recs.back().gcum, (unsigned long long)hg, bg, bd,
+                    (unsigned long long)cg, (unsigned long long)cd, cg == cd ? "MATCH" : "MISMATCH");
+        return cg == cd ? 0 : 1;
     }
-    std::vector<uint8_t> psel(N, 0), proc(N, 0);
-    PoolOut o;  // reused across reps, as the library keeps its pool outputs
-    std::vector<uint32_t> pos_of(N, kNoSlot);
-    DenseReplay dr;
-    const bool prof = std::getenv("RB_PROF") != nullptr;
-    if (prof) {
-        struct sigaction sa {};
-        sa.sa_sigaction = on_prof;
-        sa.sa_flags = SA_SIGINFO | SA_RESTART;
-        sigaction(SIGPROF, &sa, nullptr);
-        itimerval it{{0, 200}, {0, 200}};
-        setitimer(ITIMER_PROF, &it, nullptr);
+
+    // every pool, dense: gathers in chunks, then one walk per pool, on `nthreads` threads
+    std::vector<DensePool> P(npools);
+    std::vector<DenseRun> runs(npools);
+    std::vector<PoolOut> outs(npools);
+    std::vector<BGroup> gs(npools);
+    for (int p = 0; p < npools; p++) {
+        gs[p].hits = ph[p].data();
+        gs[p].n = (uint32_t)ph[p].size();
     }
-    double best = 1e30, total = 0;
-    uint64_t sum = 0;
-    size_t groups = 0, rows = 0, hits_seen = 0;
+    auto par = [&](size_t n, const std::function<void(size_t)>& f) {
+        std::atomic<size_t> next{0};
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthreads; t++)
+            th.emplace_back([&] {
+                for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+            });
+        for (auto& t : th) t.join();
+    };
+    constexpr uint32_t kChunk = 16384;
     for (int r = 0; r < reps; r++) {
-        BGroup g;
-        g.hits = hits.data();
-        g.n = (uint32_t)hits.size();
-        g.complete = true;
-        NoDevice rp(v, psel, false, 2);
-        o.recs.clear();
-        o.ents.clear();
-        const auto t0 = std::chrono::steady_clock::now();
-        if (dense) dr.run(v, 2, g, bis, brow.data(), pos_of, o);
-        else replay_pool(rp, bis, brow.data(), [&](uint32_t) -> BGroup& { return g; }, psel, proc.data(), minc.data(),
-                         maxc.data(), o);
-        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        best = std::min(best, ms);
-        total += ms;
-        sum = 1469598103934665603ull;
-        for (auto& e : o.ents) sum = (sum ^ (e.first * 131ull + (uint64_t)e.second)) * 1099511628211ull;
-        for (auto& rc : o.recs) sum = (sum ^ (rc.bi * 7ull + rc.matched)) * 1099511628211ull;
-        groups = o.recs.back().gcum;
-        rows = o.recs.size() - 1;
-        hits_seen = dense ? dr.hits_seen / (r + 1) : rp.hits_seen;
+        const double t0 = now_ms();
+        std::vector<std::pair<int, uint32_t>> chunks;
+        for (int p = 0; p < npools; p++) {
+            P[p].reset(gs[p], pbis[p], brow.data());
+            for (uint32_t c = 0; c * kChunk < P[p].n; c++) chunks.push_back({p, c});
+        }
+        par(chunks.size(), [&](size_t t) {
+            DensePool& q = P[chunks[t].first];
+            const uint32_t lo = chunks[t].second * kChunk;
+            q.gather(v, lo, std::min(q.n, lo + kChunk), pos_of.data());
+        });
+        const double t1 = now_ms();
+        std::vector<double> task(npools);
+        par(npools, [&](size_t p) {
+            const double a = now_ms();
+            runs[p].reset(P[p].n);
+            runs[p].walk(P[p], v, maxI, pos_of.data(), 0, P[p].nrows);
+            runs[p].finish(outs[p]);
+            task[p] = now_ms() - a;
+        });
+        const double t2 = now_ms();
+        par(npools, [&](size_t p) { P[p].clear_pos(0, P[p].n, pos_of.data()); });
+        uint64_t sum = 0;
+        for (auto& o : outs) sum ^= checksum(o);
+        double mx = 0, mean = 0;
+        for (double x : task) mx = std::max(mx, x), mean += x / npools;
+        std::printf("[%s] %d pools on %d threads: wall %.3f ms (gather %.3f, walks %.3f: task max %.3f mean %.3f) | "
+                    "xor-checksum %016llx\n",
+                    mode.c_str(), npools, nthreads, now_ms() - t0, t1 - t0, t2 - t1, mx, mean, (unsigned long long)sum);
     }
-    if (prof) {
-        itimerval off{};
-        setitimer(ITIMER_PROF, &off, nullptr);
-        std::map<uint64_t, size_t> h;
-        for (size_t i = 0; i < g_ns; i++) h[g_samples[i]]++;
-        FILE* f = std::fopen("/tmp/rb_prof.txt", "w");
-        for (auto& kv : h) std::fprintf(f, "%zu 0x%llx\n", kv.second, (unsigned long long)kv.first);
-        std::fclose(f);
-    }
-    std::printf("pool of %zu tickets: %zu rows, %zu groups, %zu hits walked | best %.3f ms, mean %.3f ms "
-                "(%.1f ns/row) | checksum %016llx\n",
-                hits.size(), rows, groups, hits_seen, best, total / reps, best * 1e6 / rows, (unsigned long long)sum);
     return 0;
 }
