@@ -16,8 +16,9 @@ collective — so scaling is weak; the timed region of each step is bracketed
 by a barrier + device synchronize and the per-step time is the max over ranks.
 value = all ranks' matched tickets / sum of per-step max times.
 
-Also reported: roofline of the dominant kernel (search_kernel: algorithmic
-bytes per launch / HIP-event launch time, vs 8 TB/s HBM), and the CPU
+Also reported: roofline of the dominant query-eval kernel of the pass (the
+one with the most algorithmic bytes: mscan_kernel on C3; its algorithmic
+bytes per launch / its HIP-event launch time, vs 8 TB/s HBM), and the CPU
 baseline (the oracle restatement of the reference algorithm, single core,
 bounded prefix sample — see DESIGN.md).
 """
@@ -32,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+KERNELS = {0: "search_kernel", 1: "scan_kernel", 2: "mscan_kernel"}  # mm_matched.eval_kernel
 WORKLOADS = {
     1: "C1: 10k solo 1v1, '+properties.mode:ranked +properties.region:eu'",
     2: "C2: skill-window range queries with ^boost, 1v1",
@@ -146,7 +148,7 @@ def main():
     per_step = world * args.tickets
     times, matched_all, presences_all = [], [], []
     eval_ms = eval_bytes = launches = 0
-    batches = []
+    batches, kernels = [], set()
     for step in range(args.warmup + args.steps):
         ts = synth.TicketSet(args.config, per_step, first=step * per_step, pool_mask=mask)
         ts.insert_into(mm)  # untimed: store maintenance + HBM upload
@@ -166,6 +168,7 @@ def main():
             eval_bytes += r.eval_bytes
             launches += r.eval_launches
             batches.append(r.n_batches)
+            kernels.add(KERNELS.get(r.eval_kernel, str(r.eval_kernel)))
         # drain what is left so the next step starts from a fresh 1M set
         mm.Remove([t.ticket for t in mm.Extract()]) if mm.ticket_count() else None
     total_t = sum(times)
@@ -198,7 +201,7 @@ def main():
                    "matched_per_step": sum(matched_all) / args.steps, "batches_per_pass": batches},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "search_kernel", "launches": launches, "avg_launch_ms": avg_launch_ms,
+                     "kernel": "+".join(sorted(kernels)), "launches": launches, "avg_launch_ms": avg_launch_ms,
                      "bytes_per_launch": eval_bytes / max(1, launches)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 1
+#define MM_ABI_VERSION 2
 
 /* Status codes. */
 #define MM_OK 0
@@ -117,6 +117,8 @@ typedef struct mm_matched {
     int64_t eval_bytes;             /* algorithmic bytes of the search launches (DESIGN.md roofline) */
     int32_t eval_launches;          /* search kernel launches in the pass */
     int32_t n_batches;              /* replay batches */
+    int32_t eval_kernel;            /* query-eval kernel with the most bytes: 0 search, 1 scan, 2 mscan (ABI 2) */
+    int32_t reserved3;
 } mm_matched;
 
 typedef struct mm_extract_list {

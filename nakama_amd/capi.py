@@ -112,7 +112,7 @@ class mm_matched(C.Structure):
                 ("entries", C.POINTER(mm_entry_ref)), ("is_candidates", C.c_int32), ("n_expired", C.c_int32),
                 ("pass_ms", C.c_double), ("eval_ms", C.c_double), ("pair_evals", C.c_int64),
                 ("reserved2", C.c_int64), ("eval_bytes", C.c_int64), ("eval_launches", C.c_int32),
-                ("n_batches", C.c_int32)]
+                ("n_batches", C.c_int32), ("eval_kernel", C.c_int32), ("reserved3", C.c_int32)]
 
 
 class mm_extract_list(C.Structure):
@@ -209,6 +209,7 @@ class ProcessResult:
     eval_bytes: int = 0
     eval_launches: int = 0
     n_batches: int = 0
+    eval_kernel: int = 0  # 0 search_kernel, 1 scan_kernel, 2 mscan_kernel
 
 
 class _TicketPack:
@@ -365,7 +366,7 @@ class Matchmaker:
         self._check(self.lib.mm_process(self.h, C.byref(out)))
         try:
             res = ProcessResult(self._groups(out), bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms,
-                                out.pair_evals, out.eval_bytes, out.eval_launches, out.n_batches)
+                                out.pair_evals, out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel)
         finally:
             self.lib.mm_free_matched(self.h, C.byref(out))
         return res
@@ -391,7 +392,7 @@ class Matchmaker:
             else:
                 tickets = 0
             res = ProcessResult([], bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms, out.pair_evals,
-                                out.eval_bytes, out.eval_launches, out.n_batches)
+                                out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel)
             return out.n_groups, tickets, n, res
         finally:
             self.lib.mm_free_matched(self.h, C.byref(out))

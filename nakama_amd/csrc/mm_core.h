@@ -34,9 +34,15 @@ hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, u
 int var_k_capacity();
 hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, DHit* d_scratch, DGroupResult* d_cres,
                        hipStream_t stream);
-hipError_t launch_stitch(const DChunkMap* d_map, const DGroup* d_chunks, int n_chunks, const DGroupResult* d_cres,
-                         const DHit* d_scratch, DHit* d_out, hipStream_t stream);
+hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResult* d_cres, const DHit* d_scratch,
+                         DHit* d_out, hipStream_t stream);
 int scan_chunk_len();
+hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, DHit* d_scratch,
+                        DGroupResult* d_cres, hipStream_t stream);
+int mscan_chunk_len();
+int mscan_max_sigs();
+int mscan_max_fields();
+int mscan_max_clauses();
 
 struct DeviceError {
     hipError_t err;
@@ -296,10 +302,19 @@ struct SrcChoice {  // the posting list a search streams, when it has one
 };
 
 struct PassStats {
-    double eval_ms = 0;
+    // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel
+    double k_ms[3] = {0, 0, 0};      // HIP-event time of the launches
+    int64_t k_bytes[3] = {0, 0, 0};  // algorithmic bytes
+    int k_launches[3] = {0, 0, 0};
     int64_t pair_evals = 0;
-    int64_t eval_bytes = 0;
-    int launches = 0;
+    double eval_ms() const { return k_ms[0] + k_ms[1] + k_ms[2]; }
+    int launches() const { return k_launches[0] + k_launches[1] + k_launches[2]; }
+    int dominant() const {  // the kernel with the most algorithmic bytes
+        int d = 0;
+        for (int k = 1; k < 3; k++)
+            if (k_bytes[k] > k_bytes[d]) d = k;
+        return d;
+    }
     int batches = 0;
     int refetches = 0;
     double search_ms = 0;   // host wall time of batch searches incl. H2D/D2H and stitching
@@ -398,7 +413,7 @@ private:
     std::string last_error_;
     int device_ = 0;
     hipStream_t stream_ = nullptr;
-    hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+    hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};  // around search / scan / mscan launches
     std::unique_ptr<WorkPool> workers_;  // created on the first large pass
     WorkPool& workers();
     size_t par_min(size_t auto_min) const { return par_mode_ == 2 ? 0 : auto_min; }
@@ -480,6 +495,10 @@ public:
     DevArray<DHit> d_scan_;          // scan_kernel chunk outputs (stitch_kernel input)
     DevArray<DChunkMap> d_map_;
     PinnedArray<DChunkMap> h_map_;
+    DevArray<DClause> d_mcl_;        // mscan_kernel's clause copies
+    PinnedArray<DClause> h_mcl_;
+    DevArray<DMSig> d_msig_;         // mscan_kernel's signatures
+    PinnedArray<DMSig> h_msig_;
     DevArray<uint8_t> d_rev_;
     DevArray<DGroupResult> d_res_;
     DevArray<uint32_t> d_slots_tmp_;
@@ -499,6 +518,12 @@ public:
     int par_mode_ = 1;  // 0 off, 1 auto, 2 force
     // NKM_DENSE=0: single-search pools take the generic walk too (A/B, tests)
     bool dense_mode_ = true;
+    // NKM_KERNEL: which query-eval kernel takes a batch's constant-score
+    // searches (tests run every path against the oracle at small sizes):
+    // "auto" (by size and coverage), "search" (search_kernel only),
+    // "scan" (scan_kernel at any size), "mscan" (mscan_kernel whenever eligible)
+    enum KernelMode { KM_AUTO = 0, KM_SEARCH = 1, KM_SCAN = 2, KM_MSCAN = 3 };
+    int kernel_mode_ = KM_AUTO;
     std::vector<uint32_t> custom_expired_;
 
     std::vector<std::string> debug_strings_;

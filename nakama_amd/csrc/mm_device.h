@@ -77,13 +77,43 @@ struct DGroupResult {
     uint32_t pad;
 };
 
+// A multi-signature scan (mscan_kernel): the scan-order range, the fields the
+// signatures' clauses read (clause.field indexes this list in the rewritten
+// clause copies), and the (signature x chunk) output grid.
+struct DMScan {
+    uint32_t src_off, src_len;  // range of order[]
+    uint32_t n_sigs, n_chunks;
+    uint32_t n_fields;
+    uint32_t n_clauses;         // of all the signatures (staged in LDS)
+    uint16_t field[4];
+};
+
+// One signature of a multi-signature scan.  term_only: every clause is a
+// MUST keyword TERM, so the match is "field f == req[f] for every f in
+// req_mask" and every hit scores `key` (precomputed on the host exactly as
+// the device would sum the clause scores); otherwise the clauses at
+// clause_off are evaluated.
+struct DMSig {
+    int64_t req[4];
+    int64_t key;
+    int32_t tmin, tmax;
+    uint32_t clause_off;
+    uint16_t n_clauses;
+    uint8_t qkind;
+    uint8_t term_only;
+    uint8_t req_mask;
+    uint8_t pad[7];
+};
+static_assert(sizeof(DMSig) == 64, "DMSig is 64 bytes");
+
 // Placement of one scan chunk (scan_kernel -> stitch_kernel).
 struct DChunkMap {
-    uint32_t first;    // index of the search's first chunk
+    uint32_t first;    // result index of the search's first chunk
     uint32_t start;    // chunk's first source position within the search
     uint32_t cap;      // the search's output capacity (k)
     uint32_t pad;
     uint64_t dst_off;  // the search's first output entry
+    uint64_t so;       // the chunk's compacted hits in the scratch buffer
 };
 
 // One emitted hit.

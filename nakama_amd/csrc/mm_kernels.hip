@@ -340,10 +340,196 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* _
     }
 }
 
+// ---- multi-signature scan over the scan order ---------------------------------------
+// When a batch's constant-score searches together cover most of the store
+// (C3: 8 pool signatures, each a quarter of the store through its region
+// posting list), gathering every signature's candidates through posting
+// lists re-reads the same column lines once per signature.  mscan_kernel
+// instead streams the scan order (created-at order: near-contiguous slots)
+// once, loads each candidate's columns once into registers, and evaluates
+// every signature of the batch on them — a (signatures x candidates) tile per
+// workgroup.  Each signature's survivors are compacted in scan order (= its
+// hit order when all its hits score the same) into the (signature, chunk)
+// scratch region; stitch_kernel places them.
+constexpr int kMJ = 4;                    // candidates per lane
+constexpr int kMChunk = kMJ * kBlock;     // candidates per workgroup
+constexpr int kMaxMSig = 16;
+constexpr int kMaxMField = 4;
+
+constexpr int kMaxMClause = 64;          // clauses of all the batch's mscan signatures
+
+__global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, const DMSig* __restrict__ sigs,
+                                                       const DClause* __restrict__ mcl, DHit* __restrict__ out,
+                                                       DGroupResult* __restrict__ res) {
+    // the batch's signatures and clauses, staged once per workgroup
+    __shared__ DMSig lsig[kMaxMSig];
+    __shared__ DClause lcl[kMaxMClause];
+    __shared__ uint32_t wcnt[kMaxMSig][kMJ][kWaves];
+    __shared__ int64_t lkey[kMaxMSig];
+    __shared__ uint32_t wlive[kWaves];
+    const uint32_t c = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t nq = ms.n_sigs;
+    {
+        const uint32_t* gs = reinterpret_cast<const uint32_t*>(sigs);
+        uint32_t* gd = reinterpret_cast<uint32_t*>(lsig);
+        for (uint32_t i = tid; i < nq * (sizeof(DMSig) / 4); i += kBlock) gd[i] = gs[i];
+        const uint32_t* cs = reinterpret_cast<const uint32_t*>(mcl);
+        uint32_t* cd = reinterpret_cast<uint32_t*>(lcl);
+        for (uint32_t i = tid; i < ms.n_clauses * (sizeof(DClause) / 4); i += kBlock) cd[i] = cs[i];
+    }
+    const uint32_t base = c * (uint32_t)kMChunk;
+    const uint32_t len = ms.src_len - base < (uint32_t)kMChunk ? ms.src_len - base : (uint32_t)kMChunk;
+    const uint32_t* __restrict__ src = st.order + ms.src_off + base;
+    uint32_t s[kMJ];
+    bool a[kMJ];
+    int32_t mn[kMJ], mx[kMJ];
+    uint8_t kk[kMaxMField][kMJ];
+    int64_t vv[kMaxMField][kMJ];
+#pragma unroll
+    for (int j = 0; j < kMJ; j++) {
+        const uint32_t i = (uint32_t)(j * kBlock + tid);
+        s[j] = i < len ? src[i] : kNoSlot;
+    }
+#pragma unroll
+    for (int j = 0; j < kMJ; j++) a[j] = s[j] != kNoSlot && st.alive[s[j]] != 0;
+#pragma unroll
+    for (int j = 0; j < kMJ; j++) {
+        mn[j] = a[j] ? st.minc[s[j]] : 0;
+        mx[j] = a[j] ? st.maxc[s[j]] : 0;
+    }
+#pragma unroll
+    for (int f = 0; f < kMaxMField; f++) {
+        if (f < (int)ms.n_fields) {
+            const uint8_t* __restrict__ fk = st.fkind[ms.field[f]];
+            const int64_t* __restrict__ fv = st.fval[ms.field[f]];
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) {
+                kk[f][j] = a[j] ? fk[s[j]] : (uint8_t)KIND_ABSENT;
+                vv[f][j] = a[j] ? fv[s[j]] : 0;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) { kk[f][j] = KIND_ABSENT; vv[f][j] = 0; }
+        }
+    }
+    uint32_t live = 0;
+#pragma unroll
+    for (int j = 0; j < kMJ; j++) live += a[j];
+    for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o);
+    if (lane == 0) wlive[wave] = live;
+    __syncthreads();  // lsig / lcl staged
+    // phase 1: every signature on the lane's candidates -> bit (q * kMJ + j)
+    uint64_t bits = 0;
+    for (uint32_t q = 0; q < nq; q++) {
+        const DMSig& g = lsig[q];
+        bool m[kMJ];
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) m[j] = a[j] && mn[j] >= g.tmin && mx[j] <= g.tmax;
+        if (g.term_only) {
+            // a pool signature: equality on the required keyword fields
+#pragma unroll
+            for (int f = 0; f < kMaxMField; f++) {
+                if (!((g.req_mask >> f) & 1u)) continue;
+                const int64_t want = g.req[f];
+#pragma unroll
+                for (int j = 0; j < kMJ; j++) m[j] = m[j] && kk[f][j] == KIND_KEYWORD && vv[f][j] == want;
+            }
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) {
+                any |= m[j];
+                bits |= (uint64_t)m[j] << (q * kMJ + j);
+                const uint64_t mask = __ballot(m[j]);
+                if (lane == 0) wcnt[q][j][wave] = (uint32_t)__popcll(mask);
+            }
+            if (any) lkey[q] = g.key;
+            continue;
+        }
+        double msc[kMJ], ssc[kMJ];
+        bool anys[kMJ];
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) {
+            msc[j] = 0.0;
+            ssc[j] = 0.0;
+            anys[j] = false;
+        }
+        bool has_must = false, has_should = false;
+        if (g.qkind == QK_MATCHNONE) {
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) m[j] = false;
+        } else if (g.qkind != QK_MATCHALL) {
+            for (int ci = 0; ci < g.n_clauses; ci++) {
+                const DClause k = lcl[g.clause_off + ci];  // field = index into ms.field
+                has_must |= k.occur == OCC_MUST;
+                has_should |= k.occur == OCC_SHOULD;
+#pragma unroll
+                for (int j = 0; j < kMJ; j++) {
+                    uint8_t kind = KIND_ABSENT;
+                    int64_t val = 0;
+#pragma unroll
+                    for (int f = 0; f < kMaxMField; f++)
+                        if (k.field == f) { kind = kk[f][j]; val = vv[f][j]; }
+                    bool h = false;
+                    if (k.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)k.term;
+                    else if (k.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= k.lo && val <= k.hi;
+                    else if (k.op != OP_FALSE)
+                        h = (kind == KIND_KEYWORD && val == (int64_t)k.term) || (kind == KIND_NUMERIC && val == k.lo);
+                    if (k.occur == OCC_MUST) { if (h) msc[j] += k.score; else m[j] = false; }
+                    else if (k.occur == OCC_SHOULD) { if (h) { ssc[j] += k.score; anys[j] = true; } }
+                    else if (h) m[j] = false;
+                }
+            }
+        }
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) {
+            double sp = 1.0;
+            if (g.qkind != QK_MATCHALL && (has_must || has_should)) {
+                if (!has_must) { sp = ssc[j]; m[j] = m[j] && anys[j]; }
+                else sp = anys[j] ? msc[j] + ssc[j] : msc[j];
+            }
+            // a constant-score signature: every hit has the same key
+            if (m[j] && !any) { lkey[q] = dsortable((sp + 1.0) + 1.0); any = true; }
+            bits |= (uint64_t)m[j] << (q * kMJ + j);
+            const uint64_t mask = __ballot(m[j]);
+            if (lane == 0) wcnt[q][j][wave] = (uint32_t)__popcll(mask);
+        }
+    }
+    __syncthreads();
+    // phase 2: ordered compaction of every signature into its (signature, chunk) cell
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t q = 0; q < nq; q++) {
+        const uint64_t so = ((uint64_t)q * ms.n_chunks + c) * (uint64_t)kMChunk;
+        const int64_t key = lkey[q];
+        uint32_t run = 0;
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) {
+            const bool m = (bits >> (q * kMJ + j)) & 1u;
+            const uint64_t mask = __ballot(m);
+            uint32_t before = 0, tot = 0;
+            for (int w = 0; w < kWaves; w++) {
+                const uint32_t v = wcnt[q][j][w];
+                before += (w < wave) ? v : 0;
+                tot += v;
+            }
+            if (m) out[so + run + before + (uint32_t)__popcll(mask & lt_mask)] = DHit{s[j], (uint32_t)(j * kBlock + tid), key};
+            run += tot;
+        }
+        if (tid == 0) {
+            uint32_t lv = 0;
+            for (int w = 0; w < kWaves; w++) lv += wlive[w];
+            // the chunk's columns are read once for all signatures: its
+            // scanned/live bytes are accounted to signature 0 only
+            res[(uint64_t)q * ms.n_chunks + c] = DGroupResult{run, 1u, q == 0 ? len : 0u, run, q == 0 ? lv : 0u, 0u};
+        }
+    }
+}
+
 // Places every chunk's compacted hits at its search's output: the chunk's
 // offset is the sum of the counts of the search's earlier chunks; entries
 // past the search's capacity are dropped (the host marks it incomplete).
-__global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restrict__ map, const DGroup* __restrict__ chunks,
+__global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restrict__ map,
                                                         const DGroupResult* __restrict__ cres,
                                                         const DHit* __restrict__ scratch, DHit* __restrict__ out) {
     __shared__ uint32_t wsum[kWaves];
@@ -358,7 +544,7 @@ __global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restr
     uint32_t prefix = 0;
     for (int w = 0; w < kWaves; w++) prefix += wsum[w];
     const uint32_t n = cres[c].count;
-    const uint64_t so = chunks[c].out_off;
+    const uint64_t so = mp.so;
     for (uint32_t e = tid; e < n; e += kBlock) {
         const uint32_t pos = prefix + e;
         if (pos >= mp.cap) break;
@@ -441,12 +627,26 @@ hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, D
     return hipGetLastError();
 }
 
-hipError_t launch_stitch(const DChunkMap* d_map, const DGroup* d_chunks, int n_chunks, const DGroupResult* d_cres,
-                         const DHit* d_scratch, DHit* d_out, hipStream_t stream) {
+hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResult* d_cres, const DHit* d_scratch,
+                         DHit* d_out, hipStream_t stream) {
     if (n_chunks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(stitch_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, d_map, d_chunks, d_cres, d_scratch, d_out);
+    hipLaunchKernelGGL(stitch_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, d_map, d_cres, d_scratch, d_out);
     return hipGetLastError();
 }
+
+hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, DHit* d_scratch,
+                        DGroupResult* d_cres, hipStream_t stream) {
+    if (ms.n_chunks == 0 || ms.n_sigs == 0) return hipSuccess;
+    if (ms.n_sigs > (uint32_t)kMaxMSig || ms.n_fields > (uint32_t)kMaxMField || ms.n_clauses > (uint32_t)kMaxMClause)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(mscan_kernel, dim3(ms.n_chunks), dim3(kBlock), 0, stream, st, ms, d_sigs, d_mcl, d_scratch, d_cres);
+    return hipGetLastError();
+}
+
+int mscan_chunk_len() { return kMChunk; }
+int mscan_max_sigs() { return kMaxMSig; }
+int mscan_max_fields() { return kMaxMField; }
+int mscan_max_clauses() { return kMaxMClause; }
 
 int var_k_capacity() { return kVarK; }
 int scan_chunk_len() { return kScanChunk; }

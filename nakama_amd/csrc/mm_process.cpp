@@ -68,19 +68,19 @@ struct Replay : ReplayCore {
         c.d_rev_.reserve(d.k, false);
         c.d_res_.reserve(1, false);
         NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, sizeof(DGroup), hipMemcpyHostToDevice, stream));
-        NKM_HIP(hipEventRecord(c.ev0_, stream));
+        NKM_HIP(hipEventRecord(c.ev_[0], stream));
         NKM_HIP(launch_search(st, c.d_groups_.p, 1, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream));
-        NKM_HIP(hipEventRecord(c.ev1_, stream));
+        NKM_HIP(hipEventRecord(c.ev_[1], stream));
         c.h_res_.reserve(1);
         NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
         NKM_HIP(hipStreamSynchronize(stream));
         float ms = 0.f;
-        NKM_HIP(hipEventElapsedTime(&ms, c.ev0_, c.ev1_));
-        stats.eval_ms += ms;
+        NKM_HIP(hipEventElapsedTime(&ms, c.ev_[0], c.ev_[1]));
+        stats.k_ms[0] += ms;
         const DGroupResult r = c.h_res_.p[0];
         stats.pair_evals += r.scanned;
-        stats.eval_bytes += search_bytes(c.sigs_[g.sig], d, r);
-        stats.launches++;
+        stats.k_bytes[0] += search_bytes(c.sigs_[g.sig], d, r);
+        stats.k_launches[0]++;
         std::vector<DHit> page(r.count);
         std::vector<uint8_t> prev(r.count);
         if (r.count) {
@@ -96,19 +96,115 @@ struct Replay : ReplayCore {
         g.d.k = d.k;
     }
 
-    // Runs one batch of searches.  Large constant-score searches are split
-    // into chunks of their source (scan_kernel, one workgroup per chunk, so a
-    // pool's full hit list is produced by many CUs); stitch_kernel places the
-    // chunk outputs back in source order on the device — the hit order when
-    // every hit scores the same.  Other searches run whole (search_kernel).
-    // d_groups_ / d_res_ hold [whole searches..., chunks...]; d_out_ holds
-    // [whole searches' outputs..., chunked searches' outputs...].
+    // Runs one batch of searches, each on one of three kernels:
+    //  * mscan_kernel: the batch's large constant-score searches, when they
+    //    together cover at least half of the scan order and read <= 4 fields:
+    //    one pass over the scan order evaluates all of them (DMScan);
+    //  * scan_kernel: other large constant-score searches, split into chunks
+    //    of their posting list (one workgroup per chunk);
+    //  * search_kernel: everything else, one workgroup per search (top-K for
+    //    variable scores, RevPrecision, cursors).
+    // stitch_kernel places the chunk outputs of the first two back in source
+    // order on the device — the hit order when every hit scores the same.
+    // d_groups_ holds [whole searches, chunks, mscan signatures]; d_res_ holds
+    // [whole searches, chunks, mscan (signature x chunk) cells]; d_out_ holds
+    // every search's output region.
     std::vector<DGroup> lg;                 // whole searches, then chunks
     std::vector<uint32_t> lg_group;         // owning BGroup of each entry of lg
-    std::vector<DChunkMap> lmap;            // per chunk
-    std::vector<uint32_t> cg_list;          // chunked BGroups, in order
+    std::vector<DChunkMap> lmap;            // per chunk, then per mscan cell
+    std::vector<uint32_t> cg_list;          // chunked / mscan BGroups, in order
     std::vector<uint64_t> cg_off;           // their output offsets in d_out_
-    std::vector<uint32_t> cg_first, cg_end; // their chunk ranges (indexes into lg)
+    std::vector<uint32_t> cg_first, cg_end; // their result cells (indexes into d_res_ after the whole searches)
+    std::vector<uint32_t> m_list;           // BGroups on mscan_kernel
+    std::vector<DClause> mcl;               // their clauses, field = index into DMScan::field
+    std::vector<DMSig> msig;
+
+    // The mscan descriptor of one search; a term-only signature gets its
+    // required values per scanned field and its hit key, summed exactly as
+    // the device sums clause scores (clause order, from 0.0; then +1 +1 for
+    // the min/max count musts).
+    DMSig make_msig(const DGroup& d, uint32_t clause_off) const {
+        DMSig m{};
+        m.tmin = d.tmin;
+        m.tmax = d.tmax;
+        m.clause_off = clause_off;
+        m.n_clauses = d.n_clauses;
+        m.qkind = d.qkind;
+        bool term_only = d.qkind == QK_BOOL && d.n_clauses > 0;
+        double ms = 0.0;
+        for (uint32_t k = 0; k < d.n_clauses && term_only; k++) {
+            const DClause& cl = mcl[clause_off + k];
+            if (cl.op != OP_TERM || cl.occur != OCC_MUST) { term_only = false; break; }
+            const int64_t want = (int64_t)cl.term;
+            if ((m.req_mask >> cl.field) & 1u) {
+                if (m.req[cl.field] != want) m.qkind = QK_MATCHNONE;  // two different terms on one field
+            } else {
+                m.req_mask |= (uint8_t)(1u << cl.field);
+                m.req[cl.field] = want;
+            }
+            ms += cl.score;
+        }
+        if (!term_only) {
+            m.qkind = d.qkind;
+            m.req_mask = 0;
+            for (auto& r : m.req) r = 0;
+            return m;
+        }
+        m.term_only = m.qkind == QK_MATCHNONE ? 0 : 1;
+        m.key = sortable_i64((ms + 1.0) + 1.0);
+        return m;
+    }
+
+    // Picks the searches for mscan_kernel (see above); fills m_list / mcl / ms.
+    bool plan_mscan(const std::vector<BGroup>& bg, uint32_t chunk, DMScan& ms) {
+        m_list.clear();
+        mcl.clear();
+        const int km = c.kernel_mode_;
+        if (rev || km == Core::KM_SEARCH || km == Core::KM_SCAN || c.order_head_ >= c.order_.size()) return false;
+        const bool any_size = km == Core::KM_MSCAN;
+        const uint64_t order_len = c.order_.size() - c.order_head_;
+        uint64_t covered = 0;
+        std::vector<uint16_t> fields;
+        for (uint32_t i = 0; i < bg.size(); i++) {
+            const DGroup& d = bg[i].d;
+            if (d.var_score || d.has_cursor || d.tparty != kNoParty) continue;
+            if (!any_size && (d.src_len <= chunk || d.k <= chunk / 4)) continue;
+            const Sig& sg = c.sigs_[bg[i].sig];
+            for (uint32_t k = 0; k < sg.n_clauses; k++) {
+                const DClause& cl = c.clauses_[sg.clause_off + k];
+                if (cl.op != OP_FALSE && std::find(fields.begin(), fields.end(), cl.field) == fields.end())
+                    fields.push_back(cl.field);
+            }
+            m_list.push_back(i);
+            covered += d.src_len;
+        }
+        size_t nclauses = 0;
+        for (uint32_t i : m_list) nclauses += c.sigs_[bg[i].sig].n_clauses;
+        if (m_list.empty() || m_list.size() > (size_t)mscan_max_sigs() || fields.size() > (size_t)mscan_max_fields() ||
+            nclauses > (size_t)mscan_max_clauses() || (!any_size && 2 * covered < order_len)) {
+            m_list.clear();
+            return false;
+        }
+        ms = DMScan{};
+        ms.src_off = c.order_head_;
+        ms.src_len = (uint32_t)order_len;
+        ms.n_sigs = (uint32_t)m_list.size();
+        const uint32_t mchunk = (uint32_t)mscan_chunk_len();
+        ms.n_chunks = (ms.src_len + mchunk - 1) / mchunk;
+        ms.n_fields = (uint32_t)fields.size();
+        ms.n_clauses = (uint32_t)nclauses;
+        for (size_t f = 0; f < fields.size(); f++) ms.field[f] = fields[f];
+        for (uint32_t i : m_list) {
+            const Sig& sg = c.sigs_[bg[i].sig];
+            for (uint32_t k = 0; k < sg.n_clauses; k++) {
+                DClause cl = c.clauses_[sg.clause_off + k];
+                cl.field = cl.op == OP_FALSE ? 0
+                                             : (uint16_t)(std::find(fields.begin(), fields.end(), cl.field) - fields.begin());
+                mcl.push_back(cl);
+            }
+        }
+        return true;
+    }
 
     void run_batch(std::vector<BGroup>& bg, bool need_pm) {
         const uint32_t kChunk = (uint32_t)scan_chunk_len();
@@ -119,11 +215,25 @@ struct Replay : ReplayCore {
         cg_off.clear();
         cg_first.clear();
         cg_end.clear();
+        DMScan ms{};
+        const bool use_m = plan_mscan(bg, kChunk, ms);
+        std::vector<uint8_t> on_m(bg.size(), 0);
+        for (uint32_t i : m_list) {
+            on_m[i] = 1;
+            // an mscan list is never cut: its hit positions are scan-order
+            // positions, which a cursor page over the search's own source
+            // (fetch_more) could not continue from
+            bg[i].d.k = std::max(bg[i].d.k, bg[i].d.src_len);
+        }
         uint64_t off = 0;
+        std::vector<uint32_t> chunked;
         for (uint32_t i = 0; i < bg.size(); i++) {
+            if (on_m[i]) continue;
             const DGroup& d = bg[i].d;
-            if (!d.var_score && !rev && !d.has_cursor && d.src_len > kChunk && d.k > kChunk / 4) {
-                cg_list.push_back(i);
+            const bool big = d.src_len > kChunk && d.k > kChunk / 4;
+            if (!d.var_score && !rev && !d.has_cursor && d.src_len > 0 &&
+                (c.kernel_mode_ == Core::KM_SCAN || (c.kernel_mode_ != Core::KM_SEARCH && big))) {
+                chunked.push_back(i);
                 continue;
             }
             DGroup w = d;
@@ -134,10 +244,10 @@ struct Replay : ReplayCore {
         }
         const int nwhole = (int)lg.size();
         uint64_t scratch = 0;
-        for (uint32_t i : cg_list) {
+        for (uint32_t i : chunked) {
             const DGroup& d = bg[i].d;
-            const uint32_t first = (uint32_t)lg.size();
-            cg_first.push_back(first);
+            cg_list.push_back(i);
+            cg_first.push_back((uint32_t)(lg.size() - nwhole));
             cg_off.push_back(off);
             for (uint32_t s0 = 0; s0 < d.src_len; s0 += kChunk) {
                 DGroup dc = d;
@@ -146,40 +256,79 @@ struct Replay : ReplayCore {
                 dc.k = dc.src_len;
                 dc.out_off = scratch;
                 scratch += dc.src_len;
+                lmap.push_back(DChunkMap{cg_first.back(), s0, d.k, 0u, off, dc.out_off});
                 lg.push_back(dc);
                 lg_group.push_back(i);
-                lmap.push_back(DChunkMap{first, s0, d.k, 0u, off});
             }
-            cg_end.push_back((uint32_t)lg.size());
+            cg_end.push_back((uint32_t)(lg.size() - nwhole));
             off += d.k;
         }
-        const int ng = (int)lg.size(), nchunks = ng - nwhole;
+        const int nchunks = (int)lg.size() - nwhole;
+        // mscan: signatures (DMSig, clause_off indexing mcl), result cells after the chunks
+        const uint32_t mchunk = (uint32_t)mscan_chunk_len();
+        const uint64_t mscratch = scratch;
+        uint32_t mcl_off = 0;
+        msig.clear();
+        for (uint32_t q = 0; q < m_list.size(); q++) {
+            const uint32_t i = m_list[q];
+            const DGroup& d = bg[i].d;
+            msig.push_back(make_msig(d, mcl_off));
+            mcl_off += d.n_clauses;
+            cg_list.push_back(i);
+            const uint32_t first = (uint32_t)nchunks + q * ms.n_chunks;
+            cg_first.push_back(first);
+            cg_end.push_back(first + ms.n_chunks);
+            cg_off.push_back(off);
+            for (uint32_t ch = 0; ch < ms.n_chunks; ch++)
+                lmap.push_back(DChunkMap{first, ch * mchunk, d.k, 0u, off,
+                                         mscratch + ((uint64_t)q * ms.n_chunks + ch) * mchunk});
+            off += d.k;
+        }
+        const uint32_t ncells = use_m ? ms.n_sigs * ms.n_chunks : 0;
+        if (use_m) scratch += (uint64_t)ncells * mchunk;
+        const int ng = (int)lg.size();
+        const uint32_t nres = (uint32_t)(nwhole + nchunks) + ncells, nmap = (uint32_t)lmap.size();
         c.h_groups_.reserve(ng);
         std::memcpy(c.h_groups_.p, lg.data(), ng * sizeof(DGroup));
         c.d_groups_.reserve(ng, false);
-        c.d_res_.reserve(ng, false);
+        c.d_res_.reserve(std::max<uint32_t>(nres, 1), false);
         c.d_out_.reserve(std::max<uint64_t>(off, 1), false);
         if (rev) c.d_rev_.reserve(std::max<uint64_t>(off, 1), false);
-        if (nchunks) {
+        if (nmap) {
             c.d_scan_.reserve(scratch, false);
-            c.h_map_.reserve(nchunks);
-            std::memcpy(c.h_map_.p, lmap.data(), nchunks * sizeof(DChunkMap));
-            c.d_map_.reserve(nchunks, false);
-            NKM_HIP(hipMemcpyAsync(c.d_map_.p, c.h_map_.p, nchunks * sizeof(DChunkMap), hipMemcpyHostToDevice, stream));
+            c.h_map_.reserve(nmap);
+            std::memcpy(c.h_map_.p, lmap.data(), nmap * sizeof(DChunkMap));
+            c.d_map_.reserve(nmap, false);
+            NKM_HIP(hipMemcpyAsync(c.d_map_.p, c.h_map_.p, nmap * sizeof(DChunkMap), hipMemcpyHostToDevice, stream));
+        }
+        if (use_m) {
+            c.h_msig_.reserve(msig.size());
+            std::memcpy(c.h_msig_.p, msig.data(), msig.size() * sizeof(DMSig));
+            c.d_msig_.reserve(msig.size(), false);
+            NKM_HIP(hipMemcpyAsync(c.d_msig_.p, c.h_msig_.p, msig.size() * sizeof(DMSig), hipMemcpyHostToDevice, stream));
+            c.h_mcl_.reserve(std::max<size_t>(mcl.size(), 1));
+            std::memcpy(c.h_mcl_.p, mcl.data(), mcl.size() * sizeof(DClause));
+            c.d_mcl_.reserve(std::max<size_t>(mcl.size(), 1), false);
+            NKM_HIP(hipMemcpyAsync(c.d_mcl_.p, c.h_mcl_.p, mcl.size() * sizeof(DClause), hipMemcpyHostToDevice, stream));
         }
         NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, ng * sizeof(DGroup), hipMemcpyHostToDevice, stream));
-        NKM_HIP(hipEventRecord(c.ev0_, stream));
+        // one event pair per eval kernel (per-kernel roofline in bench.py)
+        NKM_HIP(hipEventRecord(c.ev_[0], stream));
         NKM_HIP(launch_search(st, c.d_groups_.p, nwhole, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream));
+        NKM_HIP(hipEventRecord(c.ev_[1], stream));
         NKM_HIP(launch_scan(st, c.d_groups_.p + nwhole, nchunks, c.d_scan_.p, c.d_res_.p + nwhole, stream));
-        NKM_HIP(hipEventRecord(c.ev1_, stream));
-        NKM_HIP(launch_stitch(c.d_map_.p, c.d_groups_.p + nwhole, nchunks, c.d_res_.p + nwhole, c.d_scan_.p,
-                              c.d_out_.p, stream));
+        NKM_HIP(hipEventRecord(c.ev_[2], stream));
+        if (use_m)
+            NKM_HIP(launch_mscan(st, ms, c.d_msig_.p, c.d_mcl_.p, c.d_scan_.p + mscratch,
+                                 c.d_res_.p + nwhole + nchunks, stream));
+        NKM_HIP(hipEventRecord(c.ev_[3], stream));
+        NKM_HIP(launch_stitch(c.d_map_.p, (int)nmap, c.d_res_.p + nwhole, c.d_scan_.p, c.d_out_.p, stream));
         if (need_pm) {
             c.d_pm_.reserve((uint64_t)nwhole * kPairP, false);
             NKM_HIP(launch_pairmat(st, c.d_groups_.p, c.d_res_.p, nwhole, c.d_out_.p, c.d_pm_.p, stream));
         }
-        c.h_res_.reserve(ng);
-        NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, ng * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
+        c.h_res_.reserve(std::max<uint32_t>(nres, 1));
+        NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, nres * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
         c.h_out_.reserve(std::max<uint64_t>(off, 1));
         const uint64_t whole_off = nwhole ? lg[nwhole - 1].out_off + lg[nwhole - 1].k : 0;
         if (whole_off)
@@ -194,14 +343,28 @@ struct Replay : ReplayCore {
                                    hipMemcpyDeviceToHost, stream));
         }
         NKM_HIP(hipStreamSynchronize(stream));
-        float ms = 0.f;
-        NKM_HIP(hipEventElapsedTime(&ms, c.ev0_, c.ev1_));
-        stats.eval_ms += ms;
+        const bool ran[3] = {nwhole > 0, nchunks > 0, use_m};
+        for (int kk = 0; kk < 3; kk++) {
+            if (!ran[kk]) continue;
+            float ms_k = 0.f;
+            NKM_HIP(hipEventElapsedTime(&ms_k, c.ev_[kk], c.ev_[kk + 1]));
+            stats.k_ms[kk] += ms_k;
+            stats.k_launches[kk]++;
+        }
         stats.batches++;
-        stats.launches += (nwhole > 0) + (nchunks > 0);
-        for (int t = 0; t < ng; t++) {
+        for (int t = 0; t < nwhole + nchunks; t++) {
             stats.pair_evals += c.h_res_.p[t].scanned;
-            stats.eval_bytes += search_bytes(c.sigs_[bg[lg_group[t]].sig], lg[t], c.h_res_.p[t]);
+            stats.k_bytes[t < nwhole ? 0 : 1] += search_bytes(c.sigs_[bg[lg_group[t]].sig], lg[t], c.h_res_.p[t]);
+        }
+        if (use_m) {
+            // columns read once per candidate for all signatures; hits written per signature
+            const int64_t per_live = 8 + 9 * (int64_t)ms.n_fields;
+            const DGroupResult* mr = c.h_res_.p + nwhole + nchunks;
+            for (uint32_t t = 0; t < ncells; t++) {
+                stats.k_bytes[2] += (int64_t)mr[t].scanned * 5 + (int64_t)mr[t].live * per_live + (int64_t)mr[t].count * 16;
+                stats.pair_evals += (int64_t)mr[t].scanned * ms.n_sigs;
+            }
+            stats.k_bytes[2] += (int64_t)(ms.n_sigs * sizeof(DMSig) + mcl.size() * sizeof(DClause));
         }
         for (int i = 0; i < nwhole; i++) {
             BGroup& g = bg[lg_group[i]];
@@ -214,11 +377,11 @@ struct Replay : ReplayCore {
             g.n = r.count;
             g.complete = r.complete != 0;
         }
-        // chunked searches: exact hit counts are known now; copy just those
+        // chunked / mscan searches: exact hit counts are known now; copy just those
         for (size_t k = 0; k < cg_list.size(); k++) {
             BGroup& g = bg[cg_list[k]];
             uint64_t n = 0;
-            for (uint32_t t = cg_first[k]; t < cg_end[k]; t++) n += c.h_res_.p[t].count;
+            for (uint32_t t = cg_first[k]; t < cg_end[k]; t++) n += c.h_res_.p[nwhole + t].count;
             bool complete = true;
             if (n > g.d.k) { n = g.d.k; complete = false; }
             if (n)
@@ -1137,18 +1300,20 @@ int Core::process(mm_matched* out) {
                          "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches) | finish %.2f ms | "
                          "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu | par bucket %.2f work %.2f "
                          "merge %.2f ms (task max %.2f ms, rows %llu, hits %llu)\n",
-                         ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms, stats.replay_ms,
+                         ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms(), stats.replay_ms,
                          stats.apply_ms, stats.batches,
-                         stats.parallel_batches, stats.refetches, stats.launches, ms(t2, t3), ms(t3, t4),
+                         stats.parallel_batches, stats.refetches, stats.launches(), ms(t2, t3), ms(t3, t4),
                          groups.size(), ticket_.size(), n_live_, active_list_.size(), sigs_.size(),
                          dict_.str.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms,
                          stats.par_task_max_ms, (unsigned long long)stats.par_rows, (unsigned long long)stats.par_hits);
         }
     }
-    out->eval_ms = stats.eval_ms;
+    const int dk = stats.dominant();  // bench.py's roofline kernel
+    out->eval_kernel = dk;
+    out->eval_ms = stats.k_ms[dk];
     out->pair_evals = stats.pair_evals;
-    out->eval_bytes = stats.eval_bytes;
-    out->eval_launches = stats.launches;
+    out->eval_bytes = stats.k_bytes[dk];
+    out->eval_launches = stats.k_launches[dk];
     out->n_batches = stats.batches;
     out->pass_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MM_OK;

@@ -61,6 +61,9 @@ template struct DevArray<DGroup>;
 template struct DevArray<DHit>;
 template struct DevArray<DChunkMap>;
 template struct PinnedArray<DChunkMap>;
+template struct PinnedArray<DClause>;
+template struct PinnedArray<DMSig>;
+template struct DevArray<DMSig>;
 template struct DevArray<DGroupResult>;
 template struct DevArray<int64_t*>;
 template struct DevArray<uint8_t*>;
@@ -81,9 +84,11 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (ndev <= 0 || device_ < 0 || device_ >= ndev) throw DeviceError{hipErrorNoDevice, "device ordinal", __LINE__};
     NKM_HIP(hipSetDevice(device_));
     NKM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    NKM_HIP(hipEventCreate(&ev0_));
-    NKM_HIP(hipEventCreate(&ev1_));
+    for (auto& e : ev_) NKM_HIP(hipEventCreate(&e));
     if (const char* e = std::getenv("NKM_DENSE")) dense_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_KERNEL"))
+        kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN
+                     : !std::strcmp(e, "mscan") ? KM_MSCAN : KM_AUTO;
     if (const char* e = std::getenv("NKM_PARALLEL")) par_mode_ = !std::strcmp(e, "0") ? 0 : !std::strcmp(e, "force") ? 2 : 1;
     for (int f = 0; f < F_NBUILTIN; f++) field_dict_.intern(kBuiltinNames[f]);
     fval_.resize(F_NBUILTIN);
@@ -203,8 +208,8 @@ Core::~Core() {
     (void)hipSetDevice(device_);
     for (auto* p : d_fval_) delete p;
     for (auto* p : d_fkind_) delete p;
-    if (ev0_) (void)hipEventDestroy(ev0_);
-    if (ev1_) (void)hipEventDestroy(ev1_);
+    for (auto& e : ev_)
+        if (e) (void)hipEventDestroy(e);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 

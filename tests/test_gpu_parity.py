@@ -73,7 +73,15 @@ def run_passes(config, n, passes, cfg, override=None, extra=None):
         ts.close()
 
 
-def test_c1_pool_query():
+# NKM_KERNEL routes a batch's constant-score searches to one query-eval
+# kernel at any size (auto picks by size/coverage, which the small oracle
+# workloads here never reach): every kernel is checked against the oracle.
+KERNELS = ["search", "scan", "mscan"]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_c1_pool_query(kernel, monkeypatch):
+    monkeypatch.setenv("NKM_KERNEL", kernel)
     run_passes(1, 1200, 2, dict(max_intervals=2))
 
 
@@ -81,17 +89,26 @@ def test_c2_skill_window_boosts():
     run_passes(2, 1500, 2, dict(max_intervals=2))
 
 
-@pytest.mark.parametrize("par", ["0", "force"])
-def test_c3_parties_5v5(par, monkeypatch):
+HOST_KERNEL = [("0", "1", "search"), ("force", "1", "scan"), ("force", "1", "mscan"), ("force", "0", "mscan"),
+               ("0", "1", "mscan")]
+
+
+@pytest.mark.parametrize("par,dense,kernel", HOST_KERNEL)
+def test_c3_parties_5v5(par, dense, kernel, monkeypatch):
     """NKM_PARALLEL=0: serial host replay/bookkeeping; force: the pool-parallel
-    replay and parallel post-pass at any size."""
+    replay and parallel post-pass at any size; NKM_DENSE: dense or generic
+    pool walk; NKM_KERNEL: the query-eval kernel."""
     monkeypatch.setenv("NKM_PARALLEL", par)
+    monkeypatch.setenv("NKM_DENSE", dense)
+    monkeypatch.setenv("NKM_KERNEL", kernel)
     run_passes(3, 1500, 2, dict(max_intervals=2))
 
 
-@pytest.mark.parametrize("par", ["0", "force"])
-def test_c4_many_pools(par, monkeypatch):
+@pytest.mark.parametrize("par,dense,kernel", HOST_KERNEL)
+def test_c4_many_pools(par, dense, kernel, monkeypatch):
     monkeypatch.setenv("NKM_PARALLEL", par)
+    monkeypatch.setenv("NKM_DENSE", dense)
+    monkeypatch.setenv("NKM_KERNEL", kernel)
     run_passes(4, 1500, 1, dict(max_intervals=2))
 
 
@@ -139,7 +156,11 @@ def test_c5_override_candidates():
         ts.close()
 
 
-def test_mixed_parties_ranges_minmax():
+@pytest.mark.parametrize("par,dense,kernel", HOST_KERNEL)
+def test_mixed_parties_ranges_minmax(par, dense, kernel, monkeypatch):
+    monkeypatch.setenv("NKM_PARALLEL", par)
+    monkeypatch.setenv("NKM_DENSE", dense)
+    monkeypatch.setenv("NKM_KERNEL", kernel)
     run_passes(6, 1000, 3, dict(max_intervals=3))
 
 
@@ -245,8 +266,10 @@ def test_large_pool_properties(n):
         ts.close()
 
 
-def _product_passes(config, n, passes, par, monkeypatch):
+def _product_passes(config, n, passes, par, monkeypatch, dense="1", kernel="auto"):
     monkeypatch.setenv("NKM_PARALLEL", par)
+    monkeypatch.setenv("NKM_DENSE", dense)
+    monkeypatch.setenv("NKM_KERNEL", kernel)
     ts = synth.TicketSet(config, n)
     mm = capi.Matchmaker(product_lib(), max_intervals=2)
     try:
@@ -266,6 +289,8 @@ def test_parallel_host_paths_equal_serial(config, n, monkeypatch):
     """At sizes past the oracle's reach, the pool-parallel replay and the
     parallel post-pass give exactly the serial path's groups and state (the
     serial path is the one checked against the oracle above)."""
-    ser = _product_passes(config, n, 2, "0", monkeypatch)
+    ser = _product_passes(config, n, 2, "0", monkeypatch, kernel="scan")
     par = _product_passes(config, n, 2, "1", monkeypatch)
     assert par == ser
+    gen = _product_passes(config, n, 2, "1", monkeypatch, dense="0", kernel="mscan")
+    assert gen == ser
