@@ -64,11 +64,20 @@ def dist_setup(args):
     # torch's HIP runtime comes up before the library's (loading the library
     # first leaves torch with "No HIP GPUs are available")
     import torch
+    # NKM_BENCH_BACKEND=gloo rehearses the multi-rank path on a one-GPU box
+    # (ranks share device 0; collectives on the host); the driver's runs use
+    # "nccl" (RCCL) with one GPU per rank.
+    backend = os.environ.get("NKM_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     torch.cuda.synchronize(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         pg = dist
     return world, rank, local, pg
 
@@ -80,11 +89,15 @@ def barrier_sync(pg, local):
     torch.cuda.synchronize(local)
 
 
+def _red_device(pg, local):
+    return f"cuda:{local}" if pg.get_backend() == "nccl" else "cpu"
+
+
 def max_over_ranks(pg, local, x):
     if pg is None:
         return x
     import torch
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([x], dtype=torch.float64, device=_red_device(pg, local))
     pg.all_reduce(t, op=pg.ReduceOp.MAX)
     return float(t.item())
 
@@ -93,7 +106,7 @@ def sum_over_ranks(pg, local, x):
     if pg is None:
         return x
     import torch
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([x], dtype=torch.float64, device=_red_device(pg, local))
     pg.all_reduce(t, op=pg.ReduceOp.SUM)
     return float(t.item())
 
@@ -134,23 +147,19 @@ def main():
     import nakama_amd
     from nakama_amd import synth
 
-    from nakama_amd import sharding
     mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local)
-    # Pool sharding: each step draws a global set of world x tickets; every rank
-    # keeps the pools assign_pools gives it (weak scaling: ~tickets per rank).
-    npools = synth.N_POOLS.get(args.config, 0)
-    if world > 1 and npools < world:
-        raise SystemExit(f"config {args.config} has {npools} pools: cannot shard over {world} GPUs")
-    mask = None
-    if world > 1:
-        mine = sharding.assign_pools([1] * npools, world)[rank]
-        mask = sharding.pool_mask(mine)
-    per_step = world * args.tickets
+    # Pool sharding (weak scaling): the N-GPU workload is N disjoint instances
+    # of the config's pool set (region values suffixed per instance, so C3's
+    # 8 pools become 8N), and GPU r owns instance r whole — every GPU runs
+    # exactly the single-GPU workload, no ticket can match across GPUs, and
+    # the pass needs no data-path collective.
     times, matched_all, presences_all = [], [], []
     eval_ms = eval_bytes = launches = 0
     batches, kernels = [], set()
     for step in range(args.warmup + args.steps):
-        ts = synth.TicketSet(args.config, per_step, first=step * per_step, pool_mask=mask)
+        first = (step * world + rank) * args.tickets
+        ts = (synth.TicketSet(args.config, args.tickets, first=first, shard=rank) if world > 1
+              else synth.TicketSet(args.config, args.tickets, first=first))
         ts.insert_into(mm)  # untimed: store maintenance + HBM upload
         barrier_sync(pg, local)
         t0 = time.perf_counter()
@@ -197,7 +206,7 @@ def main():
         "dtype": "int64/f64",
         "data": "synthetic",
         "config": {"workload": WORKLOADS.get(args.config, str(args.config)), "tickets_per_gpu": args.tickets,
-                   "max_intervals": 2, "parallelism": f"pool-sharded x{world}",
+                   "max_intervals": 2, "parallelism": f"pool-sharded x{world}: {world} disjoint pool sets, one per GPU",
                    "matched_per_step": sum(matched_all) / args.steps, "batches_per_pass": batches},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

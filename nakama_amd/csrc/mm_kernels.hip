@@ -358,13 +358,15 @@ constexpr int kMaxMField = 4;
 
 constexpr int kMaxMClause = 64;          // clauses of all the batch's mscan signatures
 
+template <int NF>  // fields the signatures read (registers per candidate scale with it)
 __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, const DMSig* __restrict__ sigs,
                                                        const DClause* __restrict__ mcl, DHit* __restrict__ out,
                                                        DGroupResult* __restrict__ res) {
     // the batch's signatures and clauses, staged once per workgroup
     __shared__ DMSig lsig[kMaxMSig];
     __shared__ DClause lcl[kMaxMClause];
-    __shared__ uint32_t wcnt[kMaxMSig][kMJ][kWaves];
+    __shared__ uint32_t wcnt[kMaxMSig][kMJ][kWaves];  // phase 1: counts; then exclusive prefixes
+    __shared__ uint32_t qtot[kMaxMSig];
     __shared__ int64_t lkey[kMaxMSig];
     __shared__ uint32_t wlive[kWaves];
     const uint32_t c = blockIdx.x;
@@ -384,33 +386,32 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     uint32_t s[kMJ];
     bool a[kMJ];
     int32_t mn[kMJ], mx[kMJ];
-    uint8_t kk[kMaxMField][kMJ];
-    int64_t vv[kMaxMField][kMJ];
+    uint8_t kk[NF][kMJ];
+    int64_t vv[NF][kMJ];
 #pragma unroll
     for (int j = 0; j < kMJ; j++) {
         const uint32_t i = (uint32_t)(j * kBlock + tid);
         s[j] = i < len ? src[i] : kNoSlot;
     }
-#pragma unroll
-    for (int j = 0; j < kMJ; j++) a[j] = s[j] != kNoSlot && st.alive[s[j]] != 0;
+    // every column load depends only on the slot id, so they are all in
+    // flight together (one round trip); dead slots are masked afterwards
 #pragma unroll
     for (int j = 0; j < kMJ; j++) {
-        mn[j] = a[j] ? st.minc[s[j]] : 0;
-        mx[j] = a[j] ? st.maxc[s[j]] : 0;
+        const bool v = s[j] != kNoSlot;
+        a[j] = v && st.alive[s[j]] != 0;
+        mn[j] = v ? st.minc[s[j]] : 0;
+        mx[j] = v ? st.maxc[s[j]] : 0;
     }
 #pragma unroll
-    for (int f = 0; f < kMaxMField; f++) {
-        if (f < (int)ms.n_fields) {
-            const uint8_t* __restrict__ fk = st.fkind[ms.field[f]];
-            const int64_t* __restrict__ fv = st.fval[ms.field[f]];
+    for (int f = 0; f < NF; f++) {
+        const bool have = f < (int)ms.n_fields;  // NF = 1 also serves signature sets that read no field
+        const uint8_t* __restrict__ fk = have ? st.fkind[ms.field[f]] : nullptr;
+        const int64_t* __restrict__ fv = have ? st.fval[ms.field[f]] : nullptr;
 #pragma unroll
-            for (int j = 0; j < kMJ; j++) {
-                kk[f][j] = a[j] ? fk[s[j]] : (uint8_t)KIND_ABSENT;
-                vv[f][j] = a[j] ? fv[s[j]] : 0;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < kMJ; j++) { kk[f][j] = KIND_ABSENT; vv[f][j] = 0; }
+        for (int j = 0; j < kMJ; j++) {
+            const bool v = have && s[j] != kNoSlot;
+            kk[f][j] = v ? fk[s[j]] : (uint8_t)KIND_ABSENT;
+            vv[f][j] = v ? fv[s[j]] : 0;
         }
     }
     uint32_t live = 0;
@@ -420,7 +421,7 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     if (lane == 0) wlive[wave] = live;
     __syncthreads();  // lsig / lcl staged
     // phase 1: every signature on the lane's candidates -> bit (q * kMJ + j)
-    uint64_t bits = 0;
+    uint32_t bits[kMaxMSig / 8] = {0, 0};  // bit (q % 8) * kMJ + j of word q / 8: candidate j matches q
     for (uint32_t q = 0; q < nq; q++) {
         const DMSig& g = lsig[q];
         bool m[kMJ];
@@ -429,7 +430,7 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
         if (g.term_only) {
             // a pool signature: equality on the required keyword fields
 #pragma unroll
-            for (int f = 0; f < kMaxMField; f++) {
+            for (int f = 0; f < NF; f++) {
                 if (!((g.req_mask >> f) & 1u)) continue;
                 const int64_t want = g.req[f];
 #pragma unroll
@@ -439,7 +440,7 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
 #pragma unroll
             for (int j = 0; j < kMJ; j++) {
                 any |= m[j];
-                bits |= (uint64_t)m[j] << (q * kMJ + j);
+                bits[q >> 3] |= (uint32_t)m[j] << ((q & 7) * kMJ + j);
                 const uint64_t mask = __ballot(m[j]);
                 if (lane == 0) wcnt[q][j][wave] = (uint32_t)__popcll(mask);
             }
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
                     uint8_t kind = KIND_ABSENT;
                     int64_t val = 0;
 #pragma unroll
-                    for (int f = 0; f < kMaxMField; f++)
+                    for (int f = 0; f < NF; f++)
                         if (k.field == f) { kind = kk[f][j]; val = vv[f][j]; }
                     bool h = false;
                     if (k.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)k.term;
@@ -491,38 +492,45 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
             }
             // a constant-score signature: every hit has the same key
             if (m[j] && !any) { lkey[q] = dsortable((sp + 1.0) + 1.0); any = true; }
-            bits |= (uint64_t)m[j] << (q * kMJ + j);
+            bits[q >> 3] |= (uint32_t)m[j] << ((q & 7) * kMJ + j);
             const uint64_t mask = __ballot(m[j]);
             if (lane == 0) wcnt[q][j][wave] = (uint32_t)__popcll(mask);
         }
     }
     __syncthreads();
+    // exclusive prefix of every signature's counts in (j, wave) order — the
+    // candidate order j * 256 + tid — one thread per signature
+    if ((uint32_t)tid < nq) {
+        uint32_t run = 0;
+        for (int j = 0; j < kMJ; j++)
+            for (int w = 0; w < kWaves; w++) {
+                const uint32_t v = wcnt[tid][j][w];
+                wcnt[tid][j][w] = run;
+                run += v;
+            }
+        qtot[tid] = run;
+    }
+    __syncthreads();
     // phase 2: ordered compaction of every signature into its (signature, chunk) cell
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (uint32_t q = 0; q < nq; q++) {
         const uint64_t so = ((uint64_t)q * ms.n_chunks + c) * (uint64_t)kMChunk;
         const int64_t key = lkey[q];
-        uint32_t run = 0;
+        const uint32_t word = bits[q >> 3] >> ((q & 7) * kMJ);
 #pragma unroll
         for (int j = 0; j < kMJ; j++) {
-            const bool m = (bits >> (q * kMJ + j)) & 1u;
+            const bool m = (word >> j) & 1u;
             const uint64_t mask = __ballot(m);
-            uint32_t before = 0, tot = 0;
-            for (int w = 0; w < kWaves; w++) {
-                const uint32_t v = wcnt[q][j][w];
-                before += (w < wave) ? v : 0;
-                tot += v;
-            }
-            if (m) out[so + run + before + (uint32_t)__popcll(mask & lt_mask)] = DHit{s[j], (uint32_t)(j * kBlock + tid), key};
-            run += tot;
+            if (m) out[so + wcnt[q][j][wave] + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] =
+                DHit{s[j], (uint32_t)(j * kBlock + tid), key};
         }
-        if (tid == 0) {
-            uint32_t lv = 0;
-            for (int w = 0; w < kWaves; w++) lv += wlive[w];
-            // the chunk's columns are read once for all signatures: its
-            // scanned/live bytes are accounted to signature 0 only
-            res[(uint64_t)q * ms.n_chunks + c] = DGroupResult{run, 1u, q == 0 ? len : 0u, run, q == 0 ? lv : 0u, 0u};
-        }
+    }
+    if ((uint32_t)tid < nq) {
+        uint32_t lv = 0;
+        for (int w = 0; w < kWaves; w++) lv += wlive[w];
+        // the chunk's columns are read once for all signatures: its
+        // scanned/live bytes are accounted to signature 0 only
+        const uint32_t n = qtot[tid];
+        res[(uint64_t)tid * ms.n_chunks + c] = DGroupResult{n, 1u, tid == 0 ? len : 0u, n, tid == 0 ? lv : 0u, 0u};
     }
 }
 
@@ -639,7 +647,13 @@ hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs,
     if (ms.n_chunks == 0 || ms.n_sigs == 0) return hipSuccess;
     if (ms.n_sigs > (uint32_t)kMaxMSig || ms.n_fields > (uint32_t)kMaxMField || ms.n_clauses > (uint32_t)kMaxMClause)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(mscan_kernel, dim3(ms.n_chunks), dim3(kBlock), 0, stream, st, ms, d_sigs, d_mcl, d_scratch, d_cres);
+    switch (ms.n_fields) {
+        case 0:
+        case 1: hipLaunchKernelGGL(mscan_kernel<1>, dim3(ms.n_chunks), dim3(kBlock), 0, stream, st, ms, d_sigs, d_mcl, d_scratch, d_cres); break;
+        case 2: hipLaunchKernelGGL(mscan_kernel<2>, dim3(ms.n_chunks), dim3(kBlock), 0, stream, st, ms, d_sigs, d_mcl, d_scratch, d_cres); break;
+        case 3: hipLaunchKernelGGL(mscan_kernel<3>, dim3(ms.n_chunks), dim3(kBlock), 0, stream, st, ms, d_sigs, d_mcl, d_scratch, d_cres); break;
+        default: hipLaunchKernelGGL(mscan_kernel<4>, dim3(ms.n_chunks), dim3(kBlock), 0, stream, st, ms, d_sigs, d_mcl, d_scratch, d_cres); break;
+    }
     return hipGetLastError();
 }
 

@@ -36,6 +36,8 @@ def lib():
         _lib.synth_free.argtypes = [C.c_void_p]
         _lib.synth_make_pools.restype = C.c_void_p
         _lib.synth_make_pools.argtypes = [C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_uint64]
+        _lib.synth_make_shard.restype = C.c_void_p
+        _lib.synth_make_shard.argtypes = [C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int]
         _lib.synth_pool_of.restype = C.c_int
         _lib.synth_pool_of.argtypes = [C.c_int, C.c_uint64, C.c_uint64]
     return _lib
@@ -51,13 +53,18 @@ def pool_of(config: int, i: int, seed: int = None) -> int:
 class TicketSet:
     """Tickets [first, first+n) of a config; owns the native arrays."""
 
-    def __init__(self, config: int, n: int, first: int = 0, seed: int = None, t0: int = T0, pool_mask: int = None):
+    def __init__(self, config: int, n: int, first: int = 0, seed: int = None, t0: int = T0, pool_mask: int = None,
+                 shard: int = None):
         """pool_mask: keep only tickets of these pools (bit p = pool p) out of
-        the n generated indices — a rank's shard of a pool-sharded set."""
+        the n generated indices — a rank's shard of a pool-sharded set.
+        shard: region values suffixed "-g<shard>" (configs 1-4): a disjoint
+        copy of the config's pools (the N-GPU weak-scaling workload)."""
         L = lib()
         self.config = config
         sd = SEEDS.get(config, 1) if seed is None else seed
-        if pool_mask is None:
+        if shard is not None:
+            self.h = L.synth_make_shard(config, sd, first, n, t0, shard)
+        elif pool_mask is None:
             self.h = L.synth_make(config, sd, first, n, t0)
         else:
             self.h = L.synth_make_pools(config, sd, first, n, t0, pool_mask)

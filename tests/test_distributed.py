@@ -98,3 +98,64 @@ def test_assign_pools_balanced_and_deterministic():
     loads = [sum(sizes[p] for p in b) for b in a]
     assert max(loads) - min(loads) <= max(sizes)
     assert a == sharding.assign_pools(sizes, 4)
+
+
+def _shard_worker(rank, world, port, config, n, q):
+    """bench.py's multi-GPU workload: rank r owns shard instance r whole."""
+    import harness
+    from nakama_amd import capi, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ts = synth.TicketSet(config, n, first=rank * n, shard=rank)
+        mm = capi.Matchmaker(harness.oracle_lib(), max_intervals=2)
+        ts.insert_into(mm)
+        groups = mm.Process()
+        created = {ts.ticket_id(k): ts.tickets[k].created_at for k in range(ts.n)}
+        matched = sum(len({t for t, _ in g}) for g in groups)
+        tot = [None] * world
+        dist.all_gather_object(tot, (groups, created, matched))
+        if rank == 0:
+            q.put(tot)
+        mm.close()
+        ts.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("config,n", [(3, 700), (4, 800)])
+def test_shard_instances_equal_one_global_pass(config, n):
+    """N ranks each running one disjoint instance of the config (bench.py's
+    weak-scaling workload) produce exactly the groups of a single pass over
+    all N instances together: the instances share no pool, so no group can
+    span GPUs and no collective is needed in the data path."""
+    import harness
+    from nakama_amd import capi, sharding, synth
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, config, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    created = {}
+    for g in gathered:
+        created.update(g[1])
+    merged = sharding.merge_groups([g[0] for g in gathered], created)
+    mm = capi.Matchmaker(harness.oracle_lib(), max_intervals=2)
+    sets = [synth.TicketSet(config, n, first=r * n, shard=r) for r in range(world)]
+    try:
+        for ts in sets:
+            ts.insert_into(mm)
+        ref = mm.Process()
+    finally:
+        mm.close()
+        for ts in sets:
+            ts.close()
+    assert merged == ref
+    assert sum(g[2] for g in gathered) == sum(len({t for t, _ in g}) for g in ref) > 0

@@ -80,20 +80,32 @@ int synth_pool_of(int config, uint64_t seed, uint64_t i) {
     return -1;
 }
 
-void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0, uint64_t pool_mask);
+void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0, uint64_t pool_mask, int shard);
 
 // config: 1..5 as BASELINE.json configs[0..4], 6 = mixed.  Generates tickets [first, first+n).
 void* synth_make(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0) {
-    return synth_make_impl(config, seed, first, n, t0, ~0ull);
+    return synth_make_impl(config, seed, first, n, t0, ~0ull, -1);
+}
+
+// Same, with every region value suffixed "-g<shard>" (configs 1-4): shard s is
+// a disjoint copy of the config's pool set (8 pools of C3 become 8 new ones),
+// so N shards are the weak-scaling workload of an N-GPU pool-sharded run in
+// which every GPU owns exactly one config instance.
+void* synth_make_shard(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0, int shard) {
+    return synth_make_impl(config, seed, first, n, t0, ~0ull, shard);
 }
 
 // Same, keeping only tickets whose pool bit is set in pool_mask (pool-sharded
 // multi-GPU runs: each rank generates exactly its pools' tickets).
 void* synth_make_pools(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0, uint64_t pool_mask) {
-    return synth_make_impl(config, seed, first, n, t0, pool_mask);
+    return synth_make_impl(config, seed, first, n, t0, pool_mask, -1);
 }
 
-void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, int64_t t0, uint64_t pool_mask) {
+void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, int64_t t0, uint64_t pool_mask, int shard) {
+    char sfx[16] = "";
+    if (shard >= 0) std::snprintf(sfx, sizeof sfx, "-g%d", shard);
+    std::vector<const char*> shard_regions(8);  // region values of this shard
+    for (int k = 0; k < 8; k++) shard_regions[k] = kRegions[k];
     auto* S = new Synth();
     std::vector<uint64_t> idx;
     idx.reserve((size_t)n_all);
@@ -103,6 +115,8 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
         if (p < 0 || ((pool_mask >> p) & 1)) idx.push_back(i);
     }
     const int64_t n = (int64_t)idx.size();
+    if (shard >= 0)
+        for (int k = 0; k < 8; k++) shard_regions[k] = S->keep(std::string(kRegions[k]) + sfx);
     S->t.resize((size_t)n);
     S->pres.reserve((size_t)n * 5);
     S->sp.reserve((size_t)n * 3);
@@ -127,15 +141,15 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
         switch (config) {
         case 1: {
             const char* mode = kModes[r.next() & 1];
-            const char* region = kRegions[r.next() & 3];
+            const char* region = shard_regions[r.next() & 3];
             S->sp.push_back({"mode", mode});
             S->sp.push_back({"region", region});
-            query = "+properties.mode:ranked +properties.region:eu";
+            query = std::string("+properties.mode:ranked +properties.region:eu") + sfx;
             t.min_count = t.max_count = 2;
             break;
         }
         case 2: {
-            const char* region = kRegions[r.next() & 3];
+            const char* region = shard_regions[r.next() & 3];
             const int s = (int)std::lround(r.normal(1500.0, 300.0));
             S->sp.push_back({"region", region});
             S->np.push_back({"skill", (double)s});
@@ -152,7 +166,7 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             const double u = r.uni();
             party = u < 0.60 ? 1 : u < 0.80 ? 2 : u < 0.90 ? 3 : u < 0.95 ? 4 : 5;
             const char* mode = kModes[r.next() & 1];
-            const char* region = kRegions[r.next() & 3];
+            const char* region = shard_regions[r.next() & 3];
             S->sp.push_back({"mode", mode});
             S->sp.push_back({"region", region});
             query = std::string("+properties.mode:") + mode + " +properties.region:" + region;
@@ -162,7 +176,7 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
         }
         case 4: {
             const char* mode = kModes[r.next() & 7];
-            const char* region = kRegions[r.next() & 7];
+            const char* region = shard_regions[r.next() & 7];
             S->sp.push_back({"mode", mode});
             S->sp.push_back({"region", region});
             query = std::string("+properties.mode:") + mode + " +properties.region:" + region;
