@@ -28,17 +28,19 @@
 namespace nkm {
 
 hipError_t launch_search(const DStore& st, const DGroup* d_groups, int n_groups, DHit* d_out, uint8_t* d_rev,
-                         DGroupResult* d_res, hipStream_t stream);
+                         DGroupResult* d_res, hipStream_t stream, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_t n, hipStream_t stream);
 hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, uint8_t* d_out, hipStream_t stream);
 int var_k_capacity();
 hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, DHit* d_scratch, DGroupResult* d_cres,
-                       hipStream_t stream);
+                       hipStream_t stream, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResult* d_cres, const DHit* d_scratch,
                          DHit* d_out, hipStream_t stream);
 int scan_chunk_len();
+// gen: some signature is not term-only (the clause-loop instantiation)
 hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, DHit* d_scratch,
-                        DGroupResult* d_cres, hipStream_t stream);
+                        DGroupResult* d_cres, bool gen, hipStream_t stream, hipEvent_t ev0 = nullptr,
+                        hipEvent_t ev1 = nullptr);
 int mscan_chunk_len();
 int mscan_max_sigs();
 int mscan_max_fields();
@@ -413,10 +415,11 @@ private:
     std::string last_error_;
     int device_ = 0;
     hipStream_t stream_ = nullptr;
-    hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};  // around search / scan / mscan launches
+    hipEvent_t ev_[7] = {};  // start/stop of the search / scan / mscan dispatches; a marker before stitch_kernel
     std::unique_ptr<WorkPool> workers_;  // created on the first large pass
     WorkPool& workers();
     size_t par_min(size_t auto_min) const { return par_mode_ == 2 ? 0 : auto_min; }
+    bool big_list(const std::vector<uint32_t>& v) const { return par_mode_ != 0 && v.size() >= par_min(65536); }
 
 public:
     // ---- host SoA (per slot) ----  (public for the replay helpers)
@@ -425,7 +428,7 @@ public:
     Dict party_dict_;                 // party ids (rebuilt at compaction)
     // per-pass scratch, kept across passes (no page faults on the hot path)
     std::vector<uint8_t> sel_;
-    std::vector<uint32_t> rows_, brow_, brow_group_, newly_;
+    std::vector<uint32_t> rows_, brow_, brow_group_, newly_, list_tmp_;
     GroupList pass_groups_;
     std::vector<uint32_t> expired_;
     std::vector<PoolOut> pool_outs_;
@@ -518,6 +521,9 @@ public:
     int par_mode_ = 1;  // 0 off, 1 auto, 2 force
     // NKM_DENSE=0: single-search pools take the generic walk too (A/B, tests)
     bool dense_mode_ = true;
+    // NKM_FAST=0: every row takes the exact loop body, also when no two live
+    // tickets share a session (the fast walk, replay_core.h) (A/B, tests)
+    bool fast_mode_ = true;
     // NKM_KERNEL: which query-eval kernel takes a batch's constant-score
     // searches (tests run every path against the oracle at small sizes):
     // "auto" (by size and coverage), "search" (search_kernel only),

@@ -84,7 +84,7 @@ struct DMScan {
     uint32_t src_off, src_len;  // range of order[]
     uint32_t n_sigs, n_chunks;
     uint32_t n_fields;
-    uint32_t n_clauses;         // of all the signatures (staged in LDS)
+    uint32_t n_clauses;         // of all the signatures
     uint16_t field[4];
 };
 
@@ -106,7 +106,7 @@ struct DMSig {
 };
 static_assert(sizeof(DMSig) == 64, "DMSig is 64 bytes");
 
-// Placement of one scan chunk (scan_kernel -> stitch_kernel).
+// Placement of one scan chunk (scan_kernel / mscan_kernel -> stitch_kernel).
 struct DChunkMap {
     uint32_t first;    // result index of the search's first chunk
     uint32_t start;    // chunk's first source position within the search

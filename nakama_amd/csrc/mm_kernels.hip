@@ -17,6 +17,7 @@
 // With RevPrecision the lane also evaluates the hit's own query against the
 // searching ticket's document (validateMatch, matchmaker.go:1042-1068).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "mm_device.h"
 #include "qcompile.h"
@@ -348,41 +349,45 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* _
 // instead streams the scan order (created-at order: near-contiguous slots)
 // once, loads each candidate's columns once into registers, and evaluates
 // every signature of the batch on them — a (signatures x candidates) tile per
-// workgroup.  Each signature's survivors are compacted in scan order (= its
-// hit order when all its hits score the same) into the (signature, chunk)
-// scratch region; stitch_kernel places them.
+// workgroup, the signatures read wave-uniformly through the scalar cache.
+// Each signature's survivors are compacted in scan order (= its hit order
+// when all its hits score the same) into the (signature, chunk) scratch cell;
+// stitch_kernel places the cells.  (A single-pass variant that ranked its
+// chunks by a look-back over the earlier chunks' published counts ran 46 us
+// against this kernel's + stitch's on C3 1M: every chunk of the one-round
+// grid waited on the slowest earlier one; DESIGN.md.)
 constexpr int kMJ = 4;                    // candidates per lane
 constexpr int kMChunk = kMJ * kBlock;     // candidates per workgroup
 constexpr int kMaxMSig = 16;
 constexpr int kMaxMField = 4;
+constexpr int kMaxMClause = 64;           // clauses of all the batch's mscan signatures
+static_assert(kMaxMSig * kMJ == 64, "one match bit per (signature, candidate) in a 64-bit word");
+constexpr uint64_t kSigStride = 0x1111111111111111ull;  // bit q * kMJ of every signature q
 
-constexpr int kMaxMClause = 64;          // clauses of all the batch's mscan signatures
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
 
-template <int NF>  // fields the signatures read (registers per candidate scale with it)
+// NF: fields the signatures read (registers per candidate scale with it);
+// GEN: some signature is not term-only (the clause loop is compiled in).
+template <int NF, bool GEN>
 __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, const DMSig* __restrict__ sigs,
                                                        const DClause* __restrict__ mcl, DHit* __restrict__ out,
                                                        DGroupResult* __restrict__ res) {
-    // the batch's signatures and clauses, staged once per workgroup
-    __shared__ DMSig lsig[kMaxMSig];
-    __shared__ DClause lcl[kMaxMClause];
-    __shared__ uint32_t wcnt[kMaxMSig][kMJ][kWaves];  // phase 1: counts; then exclusive prefixes
+    __shared__ uint32_t wcnt[kMaxMSig][kMJ][kWaves];   // hits per (signature, j, wave); then exclusive prefixes
+    __shared__ uint64_t wmask[kMaxMSig][kMJ][kWaves];  // their ballots
     __shared__ uint32_t qtot[kMaxMSig];
     __shared__ int64_t lkey[kMaxMSig];
     __shared__ uint32_t wlive[kWaves];
     const uint32_t c = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t nq = ms.n_sigs;
-    {
-        const uint32_t* gs = reinterpret_cast<const uint32_t*>(sigs);
-        uint32_t* gd = reinterpret_cast<uint32_t*>(lsig);
-        for (uint32_t i = tid; i < nq * (sizeof(DMSig) / 4); i += kBlock) gd[i] = gs[i];
-        const uint32_t* cs = reinterpret_cast<const uint32_t*>(mcl);
-        uint32_t* cd = reinterpret_cast<uint32_t*>(lcl);
-        for (uint32_t i = tid; i < ms.n_clauses * (sizeof(DClause) / 4); i += kBlock) cd[i] = cs[i];
-    }
     const uint32_t base = c * (uint32_t)kMChunk;
     const uint32_t len = ms.src_len - base < (uint32_t)kMChunk ? ms.src_len - base : (uint32_t)kMChunk;
     const uint32_t* __restrict__ src = st.order + ms.src_off + base;
+    // a term-only signature's hits all carry its precomputed key; the others
+    // write theirs in phase 1 (disjoint signatures: no race)
+    if ((uint32_t)tid < nq && sigs[tid].term_only) lkey[tid] = sigs[tid].key;
     uint32_t s[kMJ];
     bool a[kMJ];
     int32_t mn[kMJ], mx[kMJ];
@@ -419,82 +424,88 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     for (int j = 0; j < kMJ; j++) live += a[j];
     for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o);
     if (lane == 0) wlive[wave] = live;
-    __syncthreads();  // lsig / lcl staged
-    // phase 1: every signature on the lane's candidates -> bit (q * kMJ + j)
-    uint32_t bits[kMaxMSig / 8] = {0, 0};  // bit (q % 8) * kMJ + j of word q / 8: candidate j matches q
+    // a candidate's keyword value per field, or a value no term id takes
+    int64_t kw[NF][kMJ];
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) kw[f][j] = kk[f][j] == KIND_KEYWORD ? vv[f][j] : INT64_MIN;
+    // phase 1: every signature on the lane's candidates -> bit q * kMJ + j
+    uint64_t bits = 0;
     for (uint32_t q = 0; q < nq; q++) {
-        const DMSig& g = lsig[q];
+        const DMSig& g = sigs[q];
         bool m[kMJ];
 #pragma unroll
         for (int j = 0; j < kMJ; j++) m[j] = a[j] && mn[j] >= g.tmin && mx[j] <= g.tmax;
-        if (g.term_only) {
+        if (!GEN || g.term_only) {
             // a pool signature: equality on the required keyword fields
 #pragma unroll
             for (int f = 0; f < NF; f++) {
                 if (!((g.req_mask >> f) & 1u)) continue;
                 const int64_t want = g.req[f];
 #pragma unroll
-                for (int j = 0; j < kMJ; j++) m[j] = m[j] && kk[f][j] == KIND_KEYWORD && vv[f][j] == want;
+                for (int j = 0; j < kMJ; j++) m[j] = m[j] && kw[f][j] == want;
+            }
+        } else if constexpr (GEN) {
+            double msc[kMJ], ssc[kMJ];
+            bool anys[kMJ];
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) {
+                msc[j] = 0.0;
+                ssc[j] = 0.0;
+                anys[j] = false;
+            }
+            bool has_must = false, has_should = false;
+            if (g.qkind == QK_MATCHNONE) {
+#pragma unroll
+                for (int j = 0; j < kMJ; j++) m[j] = false;
+            } else if (g.qkind != QK_MATCHALL) {
+                for (int ci = 0; ci < g.n_clauses; ci++) {
+                    const DClause k = mcl[g.clause_off + ci];  // field = index into ms.field
+                    has_must |= k.occur == OCC_MUST;
+                    has_should |= k.occur == OCC_SHOULD;
+#pragma unroll
+                    for (int j = 0; j < kMJ; j++) {
+                        uint8_t kind = KIND_ABSENT;
+                        int64_t val = 0;
+#pragma unroll
+                        for (int f = 0; f < NF; f++)
+                            if (k.field == f) { kind = kk[f][j]; val = vv[f][j]; }
+                        bool h = false;
+                        if (k.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)k.term;
+                        else if (k.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= k.lo && val <= k.hi;
+                        else if (k.op != OP_FALSE)
+                            h = (kind == KIND_KEYWORD && val == (int64_t)k.term) || (kind == KIND_NUMERIC && val == k.lo);
+                        if (k.occur == OCC_MUST) { if (h) msc[j] += k.score; else m[j] = false; }
+                        else if (k.occur == OCC_SHOULD) { if (h) { ssc[j] += k.score; anys[j] = true; } }
+                        else if (h) m[j] = false;
+                    }
+                }
             }
             bool any = false;
 #pragma unroll
             for (int j = 0; j < kMJ; j++) {
-                any |= m[j];
-                bits[q >> 3] |= (uint32_t)m[j] << ((q & 7) * kMJ + j);
-                const uint64_t mask = __ballot(m[j]);
-                if (lane == 0) wcnt[q][j][wave] = (uint32_t)__popcll(mask);
-            }
-            if (any) lkey[q] = g.key;
-            continue;
-        }
-        double msc[kMJ], ssc[kMJ];
-        bool anys[kMJ];
-#pragma unroll
-        for (int j = 0; j < kMJ; j++) {
-            msc[j] = 0.0;
-            ssc[j] = 0.0;
-            anys[j] = false;
-        }
-        bool has_must = false, has_should = false;
-        if (g.qkind == QK_MATCHNONE) {
-#pragma unroll
-            for (int j = 0; j < kMJ; j++) m[j] = false;
-        } else if (g.qkind != QK_MATCHALL) {
-            for (int ci = 0; ci < g.n_clauses; ci++) {
-                const DClause k = lcl[g.clause_off + ci];  // field = index into ms.field
-                has_must |= k.occur == OCC_MUST;
-                has_should |= k.occur == OCC_SHOULD;
-#pragma unroll
-                for (int j = 0; j < kMJ; j++) {
-                    uint8_t kind = KIND_ABSENT;
-                    int64_t val = 0;
-#pragma unroll
-                    for (int f = 0; f < NF; f++)
-                        if (k.field == f) { kind = kk[f][j]; val = vv[f][j]; }
-                    bool h = false;
-                    if (k.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)k.term;
-                    else if (k.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= k.lo && val <= k.hi;
-                    else if (k.op != OP_FALSE)
-                        h = (kind == KIND_KEYWORD && val == (int64_t)k.term) || (kind == KIND_NUMERIC && val == k.lo);
-                    if (k.occur == OCC_MUST) { if (h) msc[j] += k.score; else m[j] = false; }
-                    else if (k.occur == OCC_SHOULD) { if (h) { ssc[j] += k.score; anys[j] = true; } }
-                    else if (h) m[j] = false;
+                double sp = 1.0;
+                if (g.qkind != QK_MATCHALL && (has_must || has_should)) {
+                    if (!has_must) { sp = ssc[j]; m[j] = m[j] && anys[j]; }
+                    else sp = anys[j] ? msc[j] + ssc[j] : msc[j];
                 }
+                // a constant-score signature: every hit has the same key
+                if (m[j] && !any) { lkey[q] = dsortable((sp + 1.0) + 1.0); any = true; }
             }
         }
-        bool any = false;
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) bits |= (uint64_t)m[j] << (q * kMJ + j);
+    }
+    // per (signature, j, wave): the ballot and its count
+    for (uint32_t q = 0; q < nq; q++) {
 #pragma unroll
         for (int j = 0; j < kMJ; j++) {
-            double sp = 1.0;
-            if (g.qkind != QK_MATCHALL && (has_must || has_should)) {
-                if (!has_must) { sp = ssc[j]; m[j] = m[j] && anys[j]; }
-                else sp = anys[j] ? msc[j] + ssc[j] : msc[j];
+            const uint64_t mask = __ballot((int)((bits >> (q * kMJ + j)) & 1ull));
+            if (lane == 0) {
+                wmask[q][j][wave] = mask;
+                wcnt[q][j][wave] = (uint32_t)__popcll(mask);
             }
-            // a constant-score signature: every hit has the same key
-            if (m[j] && !any) { lkey[q] = dsortable((sp + 1.0) + 1.0); any = true; }
-            bits[q >> 3] |= (uint32_t)m[j] << ((q & 7) * kMJ + j);
-            const uint64_t mask = __ballot(m[j]);
-            if (lane == 0) wcnt[q][j][wave] = (uint32_t)__popcll(mask);
         }
     }
     __syncthreads();
@@ -511,24 +522,38 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
         qtot[tid] = run;
     }
     __syncthreads();
-    // phase 2: ordered compaction of every signature into its (signature, chunk) cell
-    for (uint32_t q = 0; q < nq; q++) {
-        const uint64_t so = ((uint64_t)q * ms.n_chunks + c) * (uint64_t)kMChunk;
-        const int64_t key = lkey[q];
-        const uint32_t word = bits[q >> 3] >> ((q & 7) * kMJ);
+    // phase 2: ordered compaction into the (signature, chunk) cells.  A
+    // candidate matching one signature (every candidate of a pool batch)
+    // stores once; a wave holding a candidate that matches several
+    // signatures takes the per-signature loop.
+    const uint64_t cell0 = (uint64_t)c * kMChunk, cstride = (uint64_t)ms.n_chunks * kMChunk;
+    bool multi = false;
+#pragma unroll
+    for (int j = 0; j < kMJ; j++) multi |= __popcll((bits >> j) & kSigStride) > 1;
+    if (!__any(multi)) {
 #pragma unroll
         for (int j = 0; j < kMJ; j++) {
-            const bool m = (word >> j) & 1u;
-            const uint64_t mask = __ballot(m);
-            if (m) out[so + wcnt[q][j][wave] + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] =
-                DHit{s[j], (uint32_t)(j * kBlock + tid), key};
+            const uint64_t t = (bits >> j) & kSigStride;
+            if (!t) continue;
+            const uint32_t q = (uint32_t)__builtin_ctzll(t) / kMJ;
+            const uint32_t pos = wcnt[q][j][wave] + lanes_below(wmask[q][j][wave]);
+            out[q * cstride + cell0 + pos] = DHit{s[j], (uint32_t)(j * kBlock + tid), lkey[q]};
+        }
+    } else {
+        for (uint32_t q = 0; q < nq; q++) {
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) {
+                if (!((bits >> (q * kMJ + j)) & 1ull)) continue;
+                const uint32_t pos = wcnt[q][j][wave] + lanes_below(wmask[q][j][wave]);
+                out[q * cstride + cell0 + pos] = DHit{s[j], (uint32_t)(j * kBlock + tid), lkey[q]};
+            }
         }
     }
     if ((uint32_t)tid < nq) {
         uint32_t lv = 0;
         for (int w = 0; w < kWaves; w++) lv += wlive[w];
         // the chunk's columns are read once for all signatures: its
-        // scanned/live bytes are accounted to signature 0 only
+        // scanned/live counts are accounted to signature 0 only
         const uint32_t n = qtot[tid];
         res[(uint64_t)tid * ms.n_chunks + c] = DGroupResult{n, 1u, tid == 0 ? len : 0u, n, tid == 0 ? lv : 0u, 0u};
     }
@@ -609,10 +634,14 @@ hipError_t launch_pairmat(const DStore& st, const DGroup* d_groups, const DGroup
     return hipGetLastError();
 }
 
+// The eval kernels' launches carry an optional start/stop event pair: the
+// events take the dispatch's own timestamps (what rocprofv3 reports as the
+// kernel's duration), not the host-side enqueue around it.
 hipError_t launch_search(const DStore& st, const DGroup* d_groups, int n_groups, DHit* d_out, uint8_t* d_rev,
-                         DGroupResult* d_res, hipStream_t stream) {
+                         DGroupResult* d_res, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
     if (n_groups <= 0) return hipSuccess;
-    hipLaunchKernelGGL(search_kernel, dim3(n_groups), dim3(kBlock), 0, stream, st, d_groups, d_out, d_rev, d_res);
+    hipExtLaunchKernelGGL(search_kernel, dim3(n_groups), dim3(kBlock), 0, stream, ev0, ev1, 0, st, d_groups, d_out, d_rev,
+                          d_res);
     return hipGetLastError();
 }
 
@@ -629,9 +658,10 @@ hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, u
 }
 
 hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, DHit* d_scratch, DGroupResult* d_cres,
-                       hipStream_t stream) {
+                       hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
     if (n_chunks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(scan_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, st, d_chunks, d_scratch, d_cres);
+    hipExtLaunchKernelGGL(scan_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, ev0, ev1, 0, st, d_chunks, d_scratch,
+                          d_cres);
     return hipGetLastError();
 }
 
@@ -642,18 +672,28 @@ hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResul
     return hipGetLastError();
 }
 
-hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, DHit* d_scratch,
-                        DGroupResult* d_cres, hipStream_t stream) {
+hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, DHit* d_out,
+                        DGroupResult* d_cres, bool gen, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
     if (ms.n_chunks == 0 || ms.n_sigs == 0) return hipSuccess;
     if (ms.n_sigs > (uint32_t)kMaxMSig || ms.n_fields > (uint32_t)kMaxMField || ms.n_clauses > (uint32_t)kMaxMClause)
         return hipErrorInvalidValue;
-    switch (ms.n_fields) {
-        case 0:
-        case 1: hipLaunchKernelGGL(mscan_kernel<1>, dim3(ms.n_chunks), dim3(kBlock), 0, stream, st, ms, d_sigs, d_mcl, d_scratch, d_cres); break;
-        case 2: hipLaunchKernelGGL(mscan_kernel<2>, dim3(ms.n_chunks), dim3(kBlock), 0, stream, st, ms, d_sigs, d_mcl, d_scratch, d_cres); break;
-        case 3: hipLaunchKernelGGL(mscan_kernel<3>, dim3(ms.n_chunks), dim3(kBlock), 0, stream, st, ms, d_sigs, d_mcl, d_scratch, d_cres); break;
-        default: hipLaunchKernelGGL(mscan_kernel<4>, dim3(ms.n_chunks), dim3(kBlock), 0, stream, st, ms, d_sigs, d_mcl, d_scratch, d_cres); break;
+    const dim3 grid(ms.n_chunks), block(kBlock);
+    const int nf = ms.n_fields < 1 ? 1 : (int)ms.n_fields;
+    const int sel = (nf - 1) * 2 + (gen ? 1 : 0);
+#define NKM_MSCAN(NF, G)                                                                                       \
+    hipExtLaunchKernelGGL(mscan_kernel<NF, G>, grid, block, 0, stream, ev0, ev1, 0, st, ms, d_sigs, d_mcl, d_out, \
+                          d_cres)
+    switch (sel) {
+        case 0: NKM_MSCAN(1, false); break;
+        case 1: NKM_MSCAN(1, true); break;
+        case 2: NKM_MSCAN(2, false); break;
+        case 3: NKM_MSCAN(2, true); break;
+        case 4: NKM_MSCAN(3, false); break;
+        case 5: NKM_MSCAN(3, true); break;
+        case 6: NKM_MSCAN(4, false); break;
+        default: NKM_MSCAN(4, true); break;
     }
+#undef NKM_MSCAN
     return hipGetLastError();
 }
 

@@ -31,6 +31,33 @@ hipError_t launch_pairmat(const DStore& st, const DGroup* d_groups, const DGroup
                           const DHit* d_out, uint32_t* d_pm, hipStream_t stream);
 
 constexpr size_t kMaxBatchRows = 1u << 20;
+
+// Order-preserving filter of a slot list: on the workers in chunks (counts,
+// then every chunk writes at its offset), or serially when wp is null.
+template <class Keep>
+static void filter_slots(WorkPool* wp, const std::vector<uint32_t>& in, std::vector<uint32_t>& out, Keep keep) {
+    const size_t n = in.size();
+    if (!wp || wp->size() < 2) {
+        out.clear();
+        for (uint32_t s : in)
+            if (keep(s)) out.push_back(s);
+        return;
+    }
+    const size_t nch = wp->size();
+    std::vector<size_t> at(nch + 1, 0);
+    wp->run(nch, [&](size_t c) {
+        size_t k = 0;
+        for (size_t i = n * c / nch; i < n * (c + 1) / nch; i++) k += keep(in[i]) ? 1 : 0;
+        at[c + 1] = k;
+    });
+    for (size_t c = 0; c < nch; c++) at[c + 1] += at[c];
+    out.resize(at[nch]);
+    wp->run(nch, [&](size_t c) {
+        size_t o = at[c];
+        for (size_t i = n * c / nch; i < n * (c + 1) / nch; i++)
+            if (keep(in[i])) out[o++] = in[i];
+    });
+}
 constexpr uint64_t kOutCap = 1ull << 24;  // max hit entries per batch (16M x 16 B)
 
 struct Replay : ReplayCore {
@@ -41,10 +68,12 @@ struct Replay : ReplayCore {
 
     static ReplayView view(const Core& core) {
         return ReplayView{core.hot_.data(), core.pres_sess_.data(), core.party_.data(), core.intervals_.data(),
-                          core.live_.data(), core.count_.data(), core.created_.data()};
+                          core.live_.data(), core.count_.data(), core.created_.data(), core.sess_slots_.more.empty()};
     }
     Replay(Core& core, std::vector<uint8_t>& s, bool r, int mi, PassStats& ps, DStore ds, hipStream_t sm)
-        : ReplayCore(view(core), s, r, mi), c(core), stats(ps), st(ds), stream(sm) {}
+        : ReplayCore(view(core), s, r, mi), c(core), stats(ps), st(ds), stream(sm) {
+        fast = core.fast_mode_;
+    }
 
     // Fetches the next page of a group's list (cursor = its last entry).
     void fetch_more(BGroup& g) override {
@@ -68,9 +97,8 @@ struct Replay : ReplayCore {
         c.d_rev_.reserve(d.k, false);
         c.d_res_.reserve(1, false);
         NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, sizeof(DGroup), hipMemcpyHostToDevice, stream));
-        NKM_HIP(hipEventRecord(c.ev_[0], stream));
-        NKM_HIP(launch_search(st, c.d_groups_.p, 1, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream));
-        NKM_HIP(hipEventRecord(c.ev_[1], stream));
+        NKM_HIP(launch_search(st, c.d_groups_.p, 1, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream,
+                              c.ev_[0], c.ev_[1]));
         c.h_res_.reserve(1);
         NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
         NKM_HIP(hipStreamSynchronize(stream));
@@ -106,9 +134,9 @@ struct Replay : ReplayCore {
     //    variable scores, RevPrecision, cursors).
     // stitch_kernel places the chunk outputs of the first two back in source
     // order on the device — the hit order when every hit scores the same.
-    // d_groups_ holds [whole searches, chunks, mscan signatures]; d_res_ holds
-    // [whole searches, chunks, mscan (signature x chunk) cells]; d_out_ holds
-    // every search's output region.
+    // d_groups_ holds [whole searches, chunks]; d_res_ holds [whole searches,
+    // chunks, mscan (signature x chunk) cells]; d_out_ holds every search's
+    // output region.
     std::vector<DGroup> lg;                 // whole searches, then chunks
     std::vector<uint32_t> lg_group;         // owning BGroup of each entry of lg
     std::vector<DChunkMap> lmap;            // per chunk, then per mscan cell
@@ -312,16 +340,19 @@ struct Replay : ReplayCore {
             NKM_HIP(hipMemcpyAsync(c.d_mcl_.p, c.h_mcl_.p, mcl.size() * sizeof(DClause), hipMemcpyHostToDevice, stream));
         }
         NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, ng * sizeof(DGroup), hipMemcpyHostToDevice, stream));
-        // one event pair per eval kernel (per-kernel roofline in bench.py)
-        NKM_HIP(hipEventRecord(c.ev_[0], stream));
-        NKM_HIP(launch_search(st, c.d_groups_.p, nwhole, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream));
-        NKM_HIP(hipEventRecord(c.ev_[1], stream));
-        NKM_HIP(launch_scan(st, c.d_groups_.p + nwhole, nchunks, c.d_scan_.p, c.d_res_.p + nwhole, stream));
-        NKM_HIP(hipEventRecord(c.ev_[2], stream));
+        // per eval kernel, the start/stop events of its dispatch (per-kernel roofline in bench.py)
+        NKM_HIP(launch_search(st, c.d_groups_.p, nwhole, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream,
+                              c.ev_[0], c.ev_[1]));
+        NKM_HIP(launch_scan(st, c.d_groups_.p + nwhole, nchunks, c.d_scan_.p, c.d_res_.p + nwhole, stream, c.ev_[2],
+                            c.ev_[3]));
         if (use_m)
-            NKM_HIP(launch_mscan(st, ms, c.d_msig_.p, c.d_mcl_.p, c.d_scan_.p + mscratch,
-                                 c.d_res_.p + nwhole + nchunks, stream));
-        NKM_HIP(hipEventRecord(c.ev_[3], stream));
+            NKM_HIP(launch_mscan(st, ms, c.d_msig_.p, c.d_mcl_.p, c.d_scan_.p + mscratch, c.d_res_.p + nwhole + nchunks,
+                                 std::any_of(msig.begin(), msig.end(), [](const DMSig& m) { return !m.term_only; }),
+                                 stream, c.ev_[4], c.ev_[5]));
+        // a marker between the eval kernels and stitch_kernel: without it the
+        // runtime may complete mscan_kernel's dispatch together with the next
+        // one, and its stop event then reads the stitch's end
+        NKM_HIP(hipEventRecord(c.ev_[6], stream));
         NKM_HIP(launch_stitch(c.d_map_.p, (int)nmap, c.d_res_.p + nwhole, c.d_scan_.p, c.d_out_.p, stream));
         if (need_pm) {
             c.d_pm_.reserve((uint64_t)nwhole * kPairP, false);
@@ -347,7 +378,7 @@ struct Replay : ReplayCore {
         for (int kk = 0; kk < 3; kk++) {
             if (!ran[kk]) continue;
             float ms_k = 0.f;
-            NKM_HIP(hipEventElapsedTime(&ms_k, c.ev_[kk], c.ev_[kk + 1]));
+            NKM_HIP(hipEventElapsedTime(&ms_k, c.ev_[2 * kk], c.ev_[2 * kk + 1]));
             stats.k_ms[kk] += ms_k;
             stats.k_launches[kk]++;
         }
@@ -550,6 +581,7 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
         if (dense[gi]) {
             DenseRun& run = dense_runs_[gi];
             run.reset(dense_pools_[gi].n);
+            run.fast = fast_mode_;
             run.walk(dense_pools_[gi], rv, maxI, pos_of_.data(), 0, dense_pools_[gi].nrows);
             run.finish(o);
             task_hits[k] = run.hits_seen;
@@ -691,9 +723,8 @@ int Core::process_default(GroupList& out_groups,
     const bool rev = cfg_.rev_precision != 0;
     const int maxI = cfg_.max_intervals;
     std::vector<uint32_t>& rows = rows_;
-    rows.clear();
-    for (uint32_t s : active_list_)
-        if (live_[s] && is_active_[s]) rows.push_back(s);
+    filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, rows,
+                 [&](uint32_t s) { return live_[s] && is_active_[s]; });
 
     if (!active_flag_) {  // paused: intervals still advance (matchmaker_process.go:53-63)
         for (uint32_t r : rows) {
@@ -886,7 +917,7 @@ int Core::process_default(GroupList& out_groups,
         for (size_t bi = 0; bi < brow.size(); bi++) {
             const uint32_t T = brow[bi];
             if (sel[T]) { done = bi + 1; continue; }
-            auto status = rp.row(T, bg[brow_group[bi]], bi == 0, grp);
+            auto status = rp.decide(T, bg[brow_group[bi]], bi == 0, grp);
             if (status == Replay::EXHAUSTED) {
                 exhausted = true;
                 retry_slot = T;
@@ -1140,10 +1171,9 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
             for (auto& e : groups.ents) kill_slot(e.first, true);
         }
     }
-    size_t w = 0;
-    for (uint32_t s : active_list_)
-        if (live_[s] && is_active_[s]) active_list_[w++] = s;
-    active_list_.resize(w);
+    filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, list_tmp_,
+                 [&](uint32_t s) { return live_[s] && is_active_[s]; });
+    active_list_.swap(list_tmp_);
 }
 
 void Core::finish_pass_serial(GroupList& groups) {
@@ -1253,11 +1283,12 @@ int Core::process(mm_matched* out) {
     const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lk(mu_);
     if (custom_open_) return MM_ERR_STATE;
-    uint32_t n_active = 0;
-    for (uint32_t s : active_list_) n_active += live_[s] && is_active_[s];
+    bool any_active = false;
+    for (uint32_t s : active_list_)
+        if (live_[s] && is_active_[s]) { any_active = true; break; }
     GroupList& groups = pass_groups_;  // kept across passes: no page faults on the hot path
     groups.clear();
-    if (n_active == 0) {  // matchmaker.go:294-298
+    if (!any_active) {  // matchmaker.go:294-298
         fill_matched(groups, out, false);
         return MM_OK;
     }

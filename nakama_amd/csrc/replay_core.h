@@ -83,6 +83,19 @@ struct ReplayView {
     const uint8_t* live;        // in m.indexes
     const int32_t* count;
     const int64_t* created;
+    // no two live tickets share a session (sessionTickets holds one ticket
+    // per session): every session check of the loop body is false
+    bool sessions_exclusive = false;
+};
+
+// Combos of the fast walks: member tickets (slots, or list positions in the
+// dense walk) and entry counts only — what the loop body needs when no
+// session check can fire.  A row that outgrows them takes the exact path.
+constexpr int kFastComb = 32, kFastMem = 32;
+struct FastCombos {
+    int32_t size[kFastComb];            // entries
+    uint32_t nmem[kFastComb];
+    uint32_t mem[kFastComb][kFastMem];  // members, in the order they joined
 };
 
 struct ReplayCore {
@@ -99,6 +112,9 @@ struct ReplayCore {
     const uint8_t* proc = nullptr;
     static constexpr uint32_t kPrefetch = 8;
     static constexpr uint32_t kPairP = 32;  // pair matrices cover the first 32 entries of a list
+    // fast_row() for rows it covers (NKM_FAST=0: row() only)
+    bool fast = true;
+    FastCombos fcb;
 
     ReplayCore(const ReplayView& view, std::vector<uint8_t>& s, bool r, int mi)
         : v(view), sel(s), rev(r), max_intervals(mi) {}
@@ -134,7 +150,86 @@ struct ReplayCore {
         return pair_slow(g, from_pos, to_pos);
     }
 
-    enum Status { MATCHED, NOMATCH, EXHAUSTED };
+    enum Status { MATCHED, NOMATCH, EXHAUSTED, BAIL };
+
+    // processDefault's loop body for T: fast_row() when it applies (and does
+    // not bail), else row().
+    Status decide(uint32_t T, BGroup& g, bool can_fetch, std::vector<std::pair<uint32_t, int>>& group_out) {
+        if (fast && !rev && v.sessions_exclusive && g.complete) {
+            const Status s = fast_row(T, g, group_out);
+            if (s != BAIL) return s;
+        }
+        return row(T, g, can_fetch, group_out);
+    }
+
+    // row() when no two live tickets share a session, without RevPrecision,
+    // over a complete list: every session check is false, so a combo is its
+    // member slots and entry count.  Returns BAIL, having changed nothing but
+    // the list head, when the row reaches the CountMultiple trim
+    // (matchmaker_process.go:234-280) or outgrows the fixed combos.
+    Status fast_row(uint32_t T, BGroup& g, std::vector<std::pair<uint32_t, int>>& group_out) {
+        const HotRec& ht = v.hot[T];
+        const bool last = v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc;
+        const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
+        const int room = tmax - tcount;  // entries a combo may hold
+        const uint32_t tparty = ht.party;
+        int ncomb = 0;
+        while (g.head < g.n && sel[g.hits[g.head].slot]) g.head++;
+        for (uint32_t i = g.head; i < g.n; i++) {
+            if (i + kPrefetch < g.n) {
+                const uint32_t P = g.hits[i + kPrefetch].slot;
+                __builtin_prefetch(&sel[P]);
+                __builtin_prefetch(&v.hot[P]);
+            }
+            const uint32_t H = g.hits[i].slot;
+            hits_seen++;
+            if (H == T || sel[H]) continue;
+            const HotRec& hh = v.hot[H];
+            if (tparty != kNoParty && hh.party == tparty) continue;                                  // :80-85
+            if (tmax < hh.maxc && v.intervals[H] + (proc ? proc[H] : 0) <= max_intervals) continue;  // :150-153
+            const int hc = hh.count;
+            int f = 0;  // first fit (:167-226)
+            while (f < ncomb && fcb.size[f] + hc > room) f++;
+            if (f == ncomb) {
+                if (f == kFastComb) return BAIL;
+                fcb.size[f] = 0;
+                fcb.nmem[f] = 0;
+                ncomb++;
+            } else if (fcb.nmem[f] == (uint32_t)kFastMem) {
+                return BAIL;
+            }
+            fcb.size[f] += hc;
+            fcb.mem[f][fcb.nmem[f]++] = H;
+            const int l = fcb.size[f] + tcount;
+            bool form = l == tmax;  // :233
+            if (!form && last && l >= tmin && l <= tmax) {
+                bool more = false;
+                for (uint32_t q = i + 1; q < g.n && !more; q++) {
+                    const uint32_t s = g.hits[q].slot;
+                    more = s != T && !sel[s] && !same_party(T, s);
+                }
+                form = !more;
+            }
+            if (!form) continue;
+            if (l % tcm != 0) return BAIL;
+            bool failed = false;  // :287-296
+            for (uint32_t k = 0; k < fcb.nmem[f] && !failed; k++) {
+                const uint32_t s = fcb.mem[f][k];
+                if (!v.live[s]) continue;
+                const HotRec& hs = v.hot[s];
+                failed = hs.minc > l || hs.maxc < l || l % hs.cm != 0;
+            }
+            if (failed) continue;
+            group_out.clear();
+            for (uint32_t k = 0; k < fcb.nmem[f]; k++) {
+                const uint32_t s = fcb.mem[f][k];
+                for (int e = 0; e < v.hot[s].count; e++) group_out.push_back({s, e});
+            }
+            for (int e = 0; e < tcount; e++) group_out.push_back({T, e});
+            return MATCHED;
+        }
+        return NOMATCH;
+    }
 
     // Is there an unselected, non-self hit after position i?  (the
     // hitCounter >= lastHitCounter test, matchmaker_process.go:130,233)
@@ -182,7 +277,7 @@ struct ReplayCore {
             if (tparty != kNoParty && hh.party == tparty) continue;                       // :80-85
             if (rev && !g.rev[i]) continue;                                            // :139-148
             if (tmax < hh.maxc && v.intervals[H] + (proc ? proc[H] : 0) <= max_intervals) continue;  // :150-153
-            if ((ht.smask & hh.smask) && share_session(ht, hh)) continue;                 // :155-165
+            if (!v.sessions_exclusive && (ht.smask & hh.smask) && share_session(ht, hh)) continue;  // :155-165
             bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
             int found = -1;
             const int hcount = hh.count;
@@ -191,7 +286,7 @@ struct ReplayCore {
                 auto& combo = combos[ci];
                 if ((int)combo.size() + hcount + tcount <= tmax) {
                     bool mconf = false;
-                    const bool may_share = (cmask[ci] & hh.smask) != 0;
+                    const bool may_share = !v.sessions_exclusive && (cmask[ci] & hh.smask) != 0;
                     if (may_share || rev) for (const CE& e : combo) {
                         if (may_share && has_session(hh, e.sess)) { sconf = true; break; }
                         if (rev) {
@@ -300,7 +395,7 @@ void replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uint32_
     for (uint32_t bi : bis) {
         const uint32_t T = brow[bi];
         if (psel[T]) continue;
-        auto status = rp.row(T, group_of(bi), false, grp);  // complete lists: never EXHAUSTED
+        auto status = rp.decide(T, group_of(bi), false, grp);  // complete lists: never EXHAUSTED
         proc[T] = 1;
         PoolRec rec{bi, 0, (uint8_t)(rp.v.intervals[T] + 1 >= rp.max_intervals || minc[T] == maxc[T]),
                     (uint32_t)o.ents.size(), 0, gcum, xcum};
@@ -393,6 +488,8 @@ struct DenseRun {
     std::vector<std::vector<CE>> combos;
     std::vector<uint32_t> cmask;
     std::vector<std::pair<uint32_t, int>> grp;
+    FastCombos fcb;
+    bool fast = true;  // fast_step() for the rows it covers (NKM_FAST=0: step() only)
 
     void reset(uint32_t n) {
         sel.assign(n, 0);
@@ -443,7 +540,7 @@ struct DenseRun {
             const DenseRec& hh = P.rec[i];
             if (tparty != kNoParty && hh.party == tparty) continue;                      // :80-85
             if (tmax < hh.maxc && (int)hh.intervals + proc[i] <= max_intervals) continue;  // :150-153
-            if (rt.smask & hh.smask) {                                                   // :155-165
+            if (!v.sessions_exclusive && (rt.smask & hh.smask)) {                        // :155-165
                 bool shared = false;
                 if (hh.count == 1) shared = t_has(hh.sess0);
                 else
@@ -456,7 +553,7 @@ struct DenseRun {
             for (size_t ci = 0; ci < ncomb; ci++) {
                 auto& combo = combos[ci];
                 if ((int)combo.size() + hcount + tcount <= tmax) {
-                    if (cmask[ci] & hh.smask)
+                    if (!v.sessions_exclusive && (cmask[ci] & hh.smask))
                         for (const CE& e : combo)
                             if (h_has(hh, e.sess)) { sconf = true; break; }
                     if (sconf) continue;
@@ -540,9 +637,91 @@ struct DenseRun {
         return true;
     }
 
+    // step() when no two live tickets share a session: combos are member
+    // positions + entry counts.  Returns 0 (row already selected), 1 (done),
+    // or 2 when the row reaches the CountMultiple trim or outgrows the fixed
+    // combos — nothing changed but the head; step() then decides the row.
+    int fast_step(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of, uint32_t j) {
+        const uint32_t n = P.n;
+        const uint32_t bi = P.bis[j];
+        const uint32_t T = P.brow[bi];
+        const uint32_t kT = pos_of[T];
+        if (kT != kNoSlot && sel[kT]) return 0;
+        int32_t tcount, tmin, tmax, tcm;
+        uint32_t tparty, tivl;
+        if (kT != kNoSlot) {
+            const DenseRec& r = P.rec[kT];
+            tcount = r.count; tmin = r.minc; tmax = r.maxc; tcm = r.cm; tparty = r.party; tivl = r.intervals;
+        } else {
+            const HotRec& h = v.hot[T];
+            tcount = h.count; tmin = h.minc; tmax = h.maxc; tcm = h.cm; tparty = h.party;
+            tivl = (uint32_t)v.intervals[T];
+        }
+        const bool last = (int)tivl + 1 >= max_intervals || tmin == tmax;
+        const int room = tmax - tcount;
+        int ncomb = 0, fi = -1;
+        while (head < n && sel[head]) head++;
+        for (uint32_t i = head; i < n; i++) {
+            hits_seen++;
+            if (i == kT || sel[i]) continue;
+            const DenseRec& hh = P.rec[i];
+            if (tparty != kNoParty && hh.party == tparty) continue;                      // :80-85
+            if (tmax < hh.maxc && (int)hh.intervals + proc[i] <= max_intervals) continue;  // :150-153
+            const int hc = hh.count;
+            int f = 0;  // first fit (:167-226)
+            while (f < ncomb && fcb.size[f] + hc > room) f++;
+            if (f == ncomb) {
+                if (f == kFastComb) return 2;
+                fcb.size[f] = 0;
+                fcb.nmem[f] = 0;
+                ncomb++;
+            } else if (fcb.nmem[f] == (uint32_t)kFastMem) {
+                return 2;
+            }
+            fcb.size[f] += hc;
+            fcb.mem[f][fcb.nmem[f]++] = i;
+            const int l = fcb.size[f] + tcount;
+            bool form = l == tmax;  // :233
+            if (!form && last && l >= tmin && l <= tmax) {
+                bool more = false;
+                for (uint32_t q = i + 1; q < n && !more; q++)
+                    more = q != kT && !sel[q] && !(tparty != kNoParty && P.rec[q].party == tparty);
+                form = !more;
+            }
+            if (!form) continue;
+            if (l % tcm != 0) return 2;  // the CountMultiple trim: step()
+            bool failed = false;         // :287-296
+            for (uint32_t k = 0; k < fcb.nmem[f] && !failed; k++) {
+                const uint32_t m = fcb.mem[f][k];
+                if (!v.live[P.slot[m]]) continue;
+                const DenseRec& hs = P.rec[m];
+                failed = hs.minc > l || hs.maxc < l || l % hs.cm != 0;
+            }
+            if (failed) continue;
+            fi = f;
+            break;
+        }
+        const uint32_t off = (uint32_t)ents.size();
+        if (fi >= 0) {
+            for (uint32_t k = 0; k < fcb.nmem[fi]; k++) {
+                const uint32_t m = fcb.mem[fi][k];
+                const uint32_t s = P.slot[m];
+                for (int e = 0; e < P.rec[m].count; e++) ents.push_back({s, e});
+                sel[m] = 1;
+            }
+            for (int e = 0; e < tcount; e++) ents.push_back({T, e});
+            if (kT != kNoSlot) sel[kT] = 1;
+        }
+        if (kT != kNoSlot) proc[kT] = 1;
+        recs.push_back(PoolRec{bi, (uint8_t)(fi >= 0), (uint8_t)last, off, (uint32_t)ents.size() - off, 0, 0});
+        return 1;
+    }
+
     void walk(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of, uint32_t j0,
               uint32_t j1) {
-        for (uint32_t j = j0; j < j1; j++) step(P, v, max_intervals, pos_of, j);
+        const bool f = fast && v.sessions_exclusive;
+        for (uint32_t j = j0; j < j1; j++)
+            if (!f || fast_step(P, v, max_intervals, pos_of, j) == 2) step(P, v, max_intervals, pos_of, j);
     }
 
     // Hands the records to a PoolOut (running offsets/counts, sentinel).

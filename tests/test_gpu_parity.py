@@ -112,6 +112,17 @@ def test_c4_many_pools(par, dense, kernel, monkeypatch):
     run_passes(4, 1500, 1, dict(max_intervals=2))
 
 
+@pytest.mark.parametrize("config,n,passes,mi", [(3, 1500, 2, 2), (6, 1000, 3, 3), (4, 1500, 1, 2)])
+@pytest.mark.parametrize("par", ["0", "force"])
+def test_exact_walk_without_fast_path(config, n, passes, mi, par, monkeypatch):
+    """NKM_FAST=0: every row takes the exact loop body even though no two
+    tickets share a session (the default takes the fast walks there); both
+    serial and pool-parallel replays against the oracle."""
+    monkeypatch.setenv("NKM_FAST", "0")
+    monkeypatch.setenv("NKM_PARALLEL", par)
+    run_passes(config, n, passes, dict(max_intervals=mi))
+
+
 def test_c5_rev_precision_default_path():
     run_passes(5, 800, 2, dict(max_intervals=2, rev_precision=True))
 
@@ -266,10 +277,11 @@ def test_large_pool_properties(n):
         ts.close()
 
 
-def _product_passes(config, n, passes, par, monkeypatch, dense="1", kernel="auto"):
+def _product_passes(config, n, passes, par, monkeypatch, dense="1", kernel="auto", fast="1"):
     monkeypatch.setenv("NKM_PARALLEL", par)
     monkeypatch.setenv("NKM_DENSE", dense)
     monkeypatch.setenv("NKM_KERNEL", kernel)
+    monkeypatch.setenv("NKM_FAST", fast)
     ts = synth.TicketSet(config, n)
     mm = capi.Matchmaker(product_lib(), max_intervals=2)
     try:
@@ -287,10 +299,14 @@ def _product_passes(config, n, passes, par, monkeypatch, dense="1", kernel="auto
 @pytest.mark.parametrize("config,n", [(3, 300_000), (4, 200_000)])
 def test_parallel_host_paths_equal_serial(config, n, monkeypatch):
     """At sizes past the oracle's reach, the pool-parallel replay and the
-    parallel post-pass give exactly the serial path's groups and state (the
-    serial path is the one checked against the oracle above)."""
-    ser = _product_passes(config, n, 2, "0", monkeypatch, kernel="scan")
+    parallel post-pass, with the fast (exclusive-session) walks, give exactly
+    the serial exact path's groups and state (the serial path is the one
+    checked against the oracle above); mscan_kernel's look-back runs over ~300
+    chunks here."""
+    ser = _product_passes(config, n, 2, "0", monkeypatch, kernel="scan", fast="0")
     par = _product_passes(config, n, 2, "1", monkeypatch)
     assert par == ser
     gen = _product_passes(config, n, 2, "1", monkeypatch, dense="0", kernel="mscan")
     assert gen == ser
+    exact = _product_passes(config, n, 2, "1", monkeypatch, fast="0")
+    assert exact == ser

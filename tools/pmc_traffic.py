@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--calib-fetch")
     ap.add_argument("--calib-write")
-    ap.add_argument("--kernel", default="search_kernel")
+    ap.add_argument("--kernel", default="mscan_kernel")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 

@@ -14,7 +14,9 @@
 //                  dense walk (checksums must match; exit status 1 if not)
 //     threads > 0: every pool, dense: gathers in chunks, then one walk per
 //                  pool, on `threads` threads
-//   RB_POOLS=n (default 8), RB_PROF=1 (SIGPROF sampler -> /tmp/rb_prof.txt)
+//   RB_POOLS=n (default 8), RB_PROF=1 (SIGPROF sampler -> /tmp/rb_prof.txt),
+//   RB_FAST=0 (threads > 0: exact walk only; sessions here are exclusive, so
+//   the fast walks apply by default)
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -113,20 +115,23 @@ int main(int argc, char** argv) {
         ph[pool[i]].push_back(DHit{i, (uint32_t)ph[pool[i]].size(), 0});
         pbis[pool[i]].push_back(i);
     }
-    ReplayView v{hot.data(), pres_sess.data(), party.data(), intervals.data(), live.data(), count.data(), created.data()};
+    ReplayView v{hot.data(), pres_sess.data(), party.data(), intervals.data(), live.data(), count.data(), created.data(),
+                 true};  // one session per presence: sessions are exclusive
+    const bool fast = !std::getenv("RB_FAST") || std::atoi(std::getenv("RB_FAST")) != 0;
     std::vector<uint32_t> pos_of(N, kNoSlot);
 
     if (nthreads == 0) {
-        // pool 0: generic vs dense, same output required
+        // pool 0: the generic and dense walks, each exact (row()/step()) and
+        // fast (exclusive sessions): all four must give the same output
         std::vector<uint8_t> psel(N, 0), proc(N, 0);
-        PoolOut og, od;
+        PoolOut out[4];
+        const char* name[4] = {"generic", "generic-fast", "dense", "dense-fast"};
+        double best[4] = {1e30, 1e30, 1e30, 1e30};
         DensePool P;
         DenseRun run;
         BGroup g;
         g.hits = ph[0].data();
         g.n = (uint32_t)ph[0].size();
-        double bg = 1e30, bd = 1e30;
-        uint64_t hg = 0;
         const bool prof = std::getenv("RB_PROF") != nullptr;
         if (prof) {
             struct sigaction sa {};
@@ -137,23 +142,28 @@ int main(int argc, char** argv) {
             setitimer(ITIMER_PROF, &it, nullptr);
         }
         for (int r = 0; r < reps; r++) {
-            og.recs.clear();
-            og.ents.clear();
-            g.head = 0;
-            NoDevice rp(v, psel, false, maxI);
-            double t0 = now_ms();
-            replay_pool(rp, pbis[0], brow.data(), [&](uint32_t) -> BGroup& { return g; }, psel, proc.data(), minc.data(),
-                        maxc.data(), og);
-            bg = std::min(bg, now_ms() - t0);
-            hg = rp.hits_seen;
-            t0 = now_ms();
-            P.reset(g, pbis[0], brow.data());
-            P.gather(v, 0, P.n, pos_of.data());
-            run.reset(P.n);
-            run.walk(P, v, maxI, pos_of.data(), 0, P.nrows);
-            run.finish(od);
-            P.clear_pos(0, P.n, pos_of.data());
-            bd = std::min(bd, now_ms() - t0);
+            for (int k = 0; k < 2; k++) {
+                out[k].recs.clear();
+                out[k].ents.clear();
+                g.head = 0;
+                NoDevice rp(v, psel, false, maxI);
+                rp.fast = k == 1;
+                const double t0 = now_ms();
+                replay_pool(rp, pbis[0], brow.data(), [&](uint32_t) -> BGroup& { return g; }, psel, proc.data(),
+                            minc.data(), maxc.data(), out[k]);
+                best[k] = std::min(best[k], now_ms() - t0);
+            }
+            for (int k = 2; k < 4; k++) {
+                const double t0 = now_ms();
+                P.reset(g, pbis[0], brow.data());
+                P.gather(v, 0, P.n, pos_of.data());
+                run.fast = k == 3;
+                run.reset(P.n);
+                run.walk(P, v, maxI, pos_of.data(), 0, P.nrows);
+                run.finish(out[k]);
+                P.clear_pos(0, P.n, pos_of.data());
+                best[k] = std::min(best[k], now_ms() - t0);
+            }
         }
         if (prof) {
             itimerval off{};
@@ -164,12 +174,14 @@ int main(int argc, char** argv) {
             for (auto& kv : h) std::fprintf(f, "%zu 0x%llx\n", kv.second, (unsigned long long)kv.first);
             std::fclose(f);
         }
-        const uint64_t cg = checksum(og), cd = checksum(od);
-        std::printf("[%s] pool of %u tickets: %zu rows, %u groups, %llu hits | generic %.3f ms | dense %.3f ms | "
-                    "checksums %016llx %016llx %s\n",
-                    mode.c_str(), g.n, og.recs.size() - 1, og.recs.back().gcum, (unsigned long long)hg, bg, bd,
-                    (unsigned long long)cg, (unsigned long long)cd, cg == cd ? "MATCH" : "MISMATCH");
-        return cg == cd ? 0 : 1;
+        bool same = true;
+        const uint64_t c0 = checksum(out[0]);
+        for (int k = 1; k < 4; k++) same &= checksum(out[k]) == c0;
+        std::printf("[%s] pool of %u tickets: %zu rows, %u groups |", mode.c_str(), g.n, out[0].recs.size() - 1,
+                    out[0].recs.back().gcum);
+        for (int k = 0; k < 4; k++) std::printf(" %s %.3f ms", name[k], best[k]);
+        std::printf(" | checksum %016llx %s\n", (unsigned long long)c0, same ? "MATCH" : "MISMATCH");
+        return same ? 0 : 1;
     }
 
     // every pool, dense: gathers in chunks, then one walk per pool, on `nthreads` threads
@@ -208,6 +220,7 @@ int main(int argc, char** argv) {
         par(npools, [&](size_t p) {
             const double a = now_ms();
             runs[p].reset(P[p].n);
+            runs[p].fast = fast;
             runs[p].walk(P[p], v, maxI, pos_of.data(), 0, P[p].nrows);
             runs[p].finish(outs[p]);
             task[p] = now_ms() - a;
