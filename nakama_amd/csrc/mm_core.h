@@ -34,14 +34,16 @@ hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, u
 int var_k_capacity();
 hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, DHit* d_scratch, DGroupResult* d_cres,
                        hipStream_t stream, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResult* d_cres, const DHit* d_scratch,
-                         DHit* d_out, hipStream_t stream);
+// cell_scan_kernel (ranks of every chunk in its search, one workgroup per
+// search: d_ranges = [first cell, end cell) pairs) then stitch_kernel.
+hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResult* d_cres, const uint32_t* d_ranges,
+                         int n_searches, uint32_t* d_offs, const DHit* d_scratch, DHit* d_out, hipStream_t stream);
 int scan_chunk_len();
 // gen: some signature is not term-only (the clause-loop instantiation)
 hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, DHit* d_scratch,
                         DGroupResult* d_cres, bool gen, hipStream_t stream, hipEvent_t ev0 = nullptr,
                         hipEvent_t ev1 = nullptr);
-int mscan_chunk_len();
+int mscan_chunk_len(uint32_t n_sigs);
 int mscan_max_sigs();
 int mscan_max_fields();
 int mscan_max_clauses();
@@ -497,6 +499,8 @@ public:
     DevArray<DHit> d_out_;
     DevArray<DHit> d_scan_;          // scan_kernel chunk outputs (stitch_kernel input)
     DevArray<DChunkMap> d_map_;
+    DevArray<uint32_t> d_cranges_, d_coffs_;  // per chunked search: its cell range; per cell: its rank
+    PinnedArray<uint32_t> h_cranges_;
     PinnedArray<DChunkMap> h_map_;
     DevArray<DClause> d_mcl_;        // mscan_kernel's clause copies
     PinnedArray<DClause> h_mcl_;

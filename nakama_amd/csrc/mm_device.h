@@ -86,6 +86,8 @@ struct DMScan {
     uint32_t n_fields;
     uint32_t n_clauses;         // of all the signatures
     uint16_t field[4];
+    uint32_t chunk;             // candidates per chunk (workgroup): 4 or 8 per lane
+    uint32_t pad;
 };
 
 // One signature of a multi-signature scan.  term_only: every clause is a

@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <cstdlib>
+
 #include "mm_device.h"
 #include "qcompile.h"
 
@@ -356,13 +358,14 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* _
 // chunks by a look-back over the earlier chunks' published counts ran 46 us
 // against this kernel's + stitch's on C3 1M: every chunk of the one-round
 // grid waited on the slowest earlier one; DESIGN.md.)
-constexpr int kMJ = 4;                    // candidates per lane
-constexpr int kMChunk = kMJ * kBlock;     // candidates per workgroup
+// MJ candidates per lane (a chunk = MJ * 256 candidates per workgroup; the
+// 64-bit match word holds 64 / MJ signatures).
 constexpr int kMaxMSig = 16;
 constexpr int kMaxMField = 4;
 constexpr int kMaxMClause = 64;           // clauses of all the batch's mscan signatures
-static_assert(kMaxMSig * kMJ == 64, "one match bit per (signature, candidate) in a 64-bit word");
-constexpr uint64_t kSigStride = 0x1111111111111111ull;  // bit q * kMJ of every signature q
+__host__ __device__ constexpr uint64_t sig_stride(int mj) {  // bit q * mj of every signature q
+    return mj == 8 ? 0x0101010101010101ull : mj == 4 ? 0x1111111111111111ull : 0x5555555555555555ull;
+}
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -370,12 +373,16 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 
 // NF: fields the signatures read (registers per candidate scale with it);
 // GEN: some signature is not term-only (the clause loop is compiled in).
-template <int NF, bool GEN>
+template <int NF, bool GEN, int kMJ>
 __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, const DMSig* __restrict__ sigs,
                                                        const DClause* __restrict__ mcl, DHit* __restrict__ out,
                                                        DGroupResult* __restrict__ res) {
-    __shared__ uint32_t wcnt[kMaxMSig][kMJ][kWaves];   // hits per (signature, j, wave); then exclusive prefixes
-    __shared__ uint64_t wmask[kMaxMSig][kMJ][kWaves];  // their ballots
+    static_assert(kMJ == 2 || kMJ == 4 || kMJ == 8, "2, 4 or 8 candidates per lane");
+    constexpr int kMChunk = kMJ * kBlock;
+    constexpr int kNSig = 64 / kMJ < kMaxMSig ? 64 / kMJ : kMaxMSig;  // signatures the 64-bit match word holds
+    constexpr uint64_t kSigStride = sig_stride(kMJ);
+    __shared__ uint32_t wcnt[kNSig][kMJ][kWaves];   // hits per (signature, j, wave); then exclusive prefixes
+    __shared__ uint64_t wmask[kNSig][kMJ][kWaves];  // their ballots
     __shared__ uint32_t qtot[kMaxMSig];
     __shared__ int64_t lkey[kMaxMSig];
     __shared__ uint32_t wlive[kWaves];
@@ -559,23 +566,45 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     }
 }
 
-// Places every chunk's compacted hits at its search's output: the chunk's
-// offset is the sum of the counts of the search's earlier chunks; entries
-// past the search's capacity are dropped (the host marks it incomplete).
+// Places every chunk's compacted hits at its search's output, at the chunk's
+// rank from cell_scan_kernel; entries past the search's capacity are dropped
+// (the host marks it incomplete).
+// Exclusive prefix of the chunk counts of each chunked / mscan search (one
+// workgroup per search, cell range [ranges[2b], ranges[2b+1])): the rank of
+// every chunk's first hit in its search, for stitch_kernel.
+__global__ __launch_bounds__(kBlock) void cell_scan_kernel(const uint32_t* __restrict__ ranges,
+                                                           const DGroupResult* __restrict__ cres,
+                                                           uint32_t* __restrict__ offs) {
+    __shared__ uint32_t wsum[kWaves];
+    const uint32_t b = ranges[2 * blockIdx.x], n = ranges[2 * blockIdx.x + 1] - b;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t per = (n + kBlock - 1) / kBlock;  // each thread: a contiguous run of cells
+    const uint32_t lo = b + min(n, per * (uint32_t)tid), hi = b + min(n, per * (uint32_t)(tid + 1));
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < hi; i++) sum += cres[i].count;
+    uint32_t incl = sum;  // inclusive scan of the threads' sums: within waves, then across them
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (int w = 0; w < wave; w++) run += wsum[w];
+    for (uint32_t i = lo; i < hi; i++) {
+        offs[i] = run;
+        run += cres[i].count;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restrict__ map,
                                                         const DGroupResult* __restrict__ cres,
+                                                        const uint32_t* __restrict__ offs,
                                                         const DHit* __restrict__ scratch, DHit* __restrict__ out) {
-    __shared__ uint32_t wsum[kWaves];
     const uint32_t c = blockIdx.x;
     const DChunkMap mp = map[c];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t part = 0;
-    for (uint32_t i = mp.first + tid; i < c; i += kBlock) part += cres[i].count;
-    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-    if (lane == 0) wsum[wave] = part;
-    __syncthreads();
-    uint32_t prefix = 0;
-    for (int w = 0; w < kWaves; w++) prefix += wsum[w];
+    const int tid = threadIdx.x;
+    const uint32_t prefix = offs[c];
     const uint32_t n = cres[c].count;
     const uint64_t so = mp.so;
     for (uint32_t e = tid; e < n; e += kBlock) {
@@ -665,10 +694,11 @@ hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, D
     return hipGetLastError();
 }
 
-hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResult* d_cres, const DHit* d_scratch,
-                         DHit* d_out, hipStream_t stream) {
+hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResult* d_cres, const uint32_t* d_ranges,
+                         int n_searches, uint32_t* d_offs, const DHit* d_scratch, DHit* d_out, hipStream_t stream) {
     if (n_chunks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(stitch_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, d_map, d_cres, d_scratch, d_out);
+    hipLaunchKernelGGL(cell_scan_kernel, dim3(n_searches), dim3(kBlock), 0, stream, d_ranges, d_cres, d_offs);
+    hipLaunchKernelGGL(stitch_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, d_map, d_cres, d_offs, d_scratch, d_out);
     return hipGetLastError();
 }
 
@@ -680,9 +710,20 @@ hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs,
     const dim3 grid(ms.n_chunks), block(kBlock);
     const int nf = ms.n_fields < 1 ? 1 : (int)ms.n_fields;
     const int sel = (nf - 1) * 2 + (gen ? 1 : 0);
-#define NKM_MSCAN(NF, G)                                                                                       \
-    hipExtLaunchKernelGGL(mscan_kernel<NF, G>, grid, block, 0, stream, ev0, ev1, 0, st, ms, d_sigs, d_mcl, d_out, \
+    const uint32_t mj = ms.chunk / kBlock;
+    if (ms.chunk % kBlock || (mj != 2 && mj != 4 && mj != 8) || (mj == 8 && ms.n_sigs > 8)) return hipErrorInvalidValue;
+#define NKM_MSCAN_J(NF, G, J)                                                                                 \
+    hipExtLaunchKernelGGL(mscan_kernel<NF, G, J>, grid, block, 0, stream, ev0, ev1, 0, st, ms, d_sigs, d_mcl, d_out, \
                           d_cres)
+#define NKM_MSCAN(NF, G)                 \
+    do {                                 \
+        if (mj == 8)                     \
+            NKM_MSCAN_J(NF, G, 8);       \
+        else if (mj == 4)                \
+            NKM_MSCAN_J(NF, G, 4);       \
+        else                             \
+            NKM_MSCAN_J(NF, G, 2);       \
+    } while (0)
     switch (sel) {
         case 0: NKM_MSCAN(1, false); break;
         case 1: NKM_MSCAN(1, true); break;
@@ -694,10 +735,17 @@ hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs,
         default: NKM_MSCAN(4, true); break;
     }
 #undef NKM_MSCAN
+#undef NKM_MSCAN_J
     return hipGetLastError();
 }
 
-int mscan_chunk_len() { return kMChunk; }
+// Candidates per lane: NKM_MSCAN_J (2, 4 or 8; 8 needs <= 8 signatures), default 2
+// (C3 1M: 21.7 us at 2, 24.6 at 4, 35.2 at 8 — more, shorter waves hide more latency).
+int mscan_chunk_len(uint32_t n_sigs) {
+    static const int env = std::getenv("NKM_MSCAN_J") ? std::atoi(std::getenv("NKM_MSCAN_J")) : 0;
+    const int j = env == 2 || env == 4 || (env == 8 && n_sigs <= 8) ? env : 2;
+    return j * kBlock;
+}
 int mscan_max_sigs() { return kMaxMSig; }
 int mscan_max_fields() { return kMaxMField; }
 int mscan_max_clauses() { return kMaxMClause; }

@@ -217,7 +217,8 @@ struct Replay : ReplayCore {
         ms.src_off = c.order_head_;
         ms.src_len = (uint32_t)order_len;
         ms.n_sigs = (uint32_t)m_list.size();
-        const uint32_t mchunk = (uint32_t)mscan_chunk_len();
+        const uint32_t mchunk = (uint32_t)mscan_chunk_len(ms.n_sigs);
+        ms.chunk = mchunk;
         ms.n_chunks = (ms.src_len + mchunk - 1) / mchunk;
         ms.n_fields = (uint32_t)fields.size();
         ms.n_clauses = (uint32_t)nclauses;
@@ -293,7 +294,7 @@ struct Replay : ReplayCore {
         }
         const int nchunks = (int)lg.size() - nwhole;
         // mscan: signatures (DMSig, clause_off indexing mcl), result cells after the chunks
-        const uint32_t mchunk = (uint32_t)mscan_chunk_len();
+        const uint32_t mchunk = ms.chunk;
         const uint64_t mscratch = scratch;
         uint32_t mcl_off = 0;
         msig.clear();
@@ -353,7 +354,19 @@ struct Replay : ReplayCore {
         // runtime may complete mscan_kernel's dispatch together with the next
         // one, and its stop event then reads the stitch's end
         NKM_HIP(hipEventRecord(c.ev_[6], stream));
-        NKM_HIP(launch_stitch(c.d_map_.p, (int)nmap, c.d_res_.p + nwhole, c.d_scan_.p, c.d_out_.p, stream));
+        if (nmap) {
+            const size_t ns = cg_list.size();
+            c.h_cranges_.reserve(2 * ns);
+            for (size_t k = 0; k < ns; k++) {
+                c.h_cranges_.p[2 * k] = cg_first[k];
+                c.h_cranges_.p[2 * k + 1] = cg_end[k];
+            }
+            c.d_cranges_.reserve(2 * ns, false);
+            c.d_coffs_.reserve(nmap, false);
+            NKM_HIP(hipMemcpyAsync(c.d_cranges_.p, c.h_cranges_.p, 2 * ns * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+            NKM_HIP(launch_stitch(c.d_map_.p, (int)nmap, c.d_res_.p + nwhole, c.d_cranges_.p, (int)ns, c.d_coffs_.p,
+                                  c.d_scan_.p, c.d_out_.p, stream));
+        }
         if (need_pm) {
             c.d_pm_.reserve((uint64_t)nwhole * kPairP, false);
             NKM_HIP(launch_pairmat(st, c.d_groups_.p, c.d_res_.p, nwhole, c.d_out_.p, c.d_pm_.p, stream));
