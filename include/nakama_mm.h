@@ -172,6 +172,14 @@ int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, dou
 /* Query-string compile status only (no device work): MM_OK,
  * MM_ERR_QUERY_INVALID or MM_ERR_UNSUPPORTED. */
 int mm_debug_compile(const char* query);
+/* Term matching of one multi-term clause, as bluge's dictionary enumeration
+ * decides it (no device work): kind 1 = RegexpQuery pattern (after the leading
+ * '^' trim, bluge/query.go:1264), 3 = WildcardQuery text (query.go:1475-1485),
+ * 2 = FuzzyQuery term with `fuzziness` (search_fuzzy.go:43-143).  Returns 1 and
+ * the per-term boost in *boost when `term` is accepted, 0 when not, -1 when
+ * every search with the pattern fails (Go/vellum parse error, fuzziness outside
+ * [0, 2]), -2 for a construct not lowered (MM_ERR_UNSUPPORTED at Add). */
+int mm_debug_term_match(int32_t kind, const char* pattern, int32_t fuzziness, const char* term, double* boost);
 int32_t mm_debug_group_indexes(const int32_t* counts, const int64_t* created_at, int32_t n, int32_t required,
                                int32_t* group_offsets, int32_t* group_members, int64_t* avg_created_at, int32_t cap);
 

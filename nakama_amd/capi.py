@@ -124,7 +124,7 @@ EXPORTED_SYMBOLS = (
     "mm_backend_name", "mm_add", "mm_insert", "mm_extract", "mm_free_extract", "mm_remove_session",
     "mm_remove_session_all", "mm_remove_party", "mm_remove_party_all", "mm_remove_all", "mm_remove",
     "mm_process", "mm_process_commit", "mm_free_matched", "mm_ticket_count", "mm_active_count",
-    "mm_debug_hits", "mm_debug_compile", "mm_debug_group_indexes",
+    "mm_debug_hits", "mm_debug_compile", "mm_debug_term_match", "mm_debug_group_indexes",
 )
 
 
@@ -160,6 +160,7 @@ def load_library(path: str) -> C.CDLL:
         "mm_active_count": (C.c_int32, [vp]),
         "mm_debug_hits": (C.c_int32, [vp, C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int32]),
         "mm_debug_compile": (C.c_int, [C.c_char_p]),
+        "mm_debug_term_match": (C.c_int, [C.c_int32, C.c_char_p, C.c_int32, C.c_char_p, C.POINTER(C.c_double)]),
         "mm_debug_group_indexes": (C.c_int32, [C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_int32, C.c_int32,
                                                C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int64),
                                                C.c_int32]),

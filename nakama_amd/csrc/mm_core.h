@@ -23,6 +23,7 @@
 #include "../../include/nakama_mm.h"
 #include "mm_device.h"
 #include "qcompile.h"
+#include "termmatch.h"
 #include "replay_core.h"
 
 namespace nkm {
@@ -380,6 +381,8 @@ private:
     int add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_insert);
     uint16_t field_of(const std::string& name);
     uint32_t sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party);
+    uint32_t termset_of(const HostClause& c);  // interned regexp/wildcard/fuzzy matcher
+    void refresh_termsets();                   // extends accepted sets over new dictionary terms, uploads
     void set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val);
     void kill_slot(uint32_t slot, bool device_cleared = false);  // ticket leaves the index and the maps
     const char* arena_string(const std::string& s);
@@ -488,6 +491,20 @@ public:
     DevArray<uint32_t> d_party_;
     DevArray<DQuery> d_squery_;
     DevArray<DClause> d_clauses_;
+    // multi-term matchers (OP_TERMSET): accepted dictionary ids (ascending) and
+    // each one's score contribution; device copy = desc (off, len) + ids + scores
+    struct TermSet {
+        TermMatcher m;
+        double b = 1.0;         // query boost of the clause
+        uint32_t done = 0;      // dictionary ids [0, done) already tested
+        std::vector<uint32_t> ids;
+        std::vector<double> sc;
+    };
+    std::vector<TermSet> tsets_;
+    std::unordered_map<std::string, uint32_t> tset_index_;
+    bool tsets_dirty_ = false;
+    DevArray<uint32_t> d_tset_desc_, d_tset_ids_;
+    DevArray<double> d_tset_sc_;
     size_t dev_clauses_ = 0;
     std::vector<DevArray<int64_t>*> d_fval_;
     std::vector<DevArray<uint8_t>*> d_fkind_;

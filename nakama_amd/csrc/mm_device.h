@@ -13,7 +13,8 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 enum : uint8_t { KIND_ABSENT = 0, KIND_KEYWORD = 1, KIND_NUMERIC = 2 };
 
 // One compiled clause (32 B).  lo/hi: sortable int64 bounds (RANGE) or the
-// numeric literal (NUMLIT, lo == hi); term: dictionary id of the keyword form.
+// numeric literal (NUMLIT, lo == hi); term: dictionary id of the keyword form
+// (TERMSET: the matcher's set index).
 struct DClause {
     int64_t lo;
     int64_t hi;
@@ -45,6 +46,9 @@ struct DStore {
     const uint8_t* const* fkind;// [n_fields] -> [cap] KIND_*
     const uint32_t* order;      // scan order: slots sorted by (created key, slot)
     const uint32_t* postings;   // concatenated posting lists (slots, scan order)
+    const uint32_t* tset_desc;  // [2 * n_sets] (offset, length) of each OP_TERMSET matcher's set
+    const uint32_t* tset_ids;   // accepted keyword dictionary ids, ascending per set
+    const double* tset_sc;      // the clause's score contribution for each accepted id
 };
 
 // One search (a group of rows sharing a compiled signature, or one row).

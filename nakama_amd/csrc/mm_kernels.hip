@@ -35,6 +35,22 @@ __device__ __forceinline__ int64_t dsortable(double f) {
     return i < 0 ? (i ^ 0x7fffffffffffffffLL) : i;
 }
 
+// OP_TERMSET: is keyword id `val` in the matcher's accepted set?  Binary search
+// of the set's ascending ids; *sc = the clause's score for that term.
+__device__ __forceinline__ bool termset_hit(const DStore& st, uint32_t set, int64_t val, double* sc) {
+    const uint32_t off = st.tset_desc[2 * set];
+    uint32_t lo = 0, hi = st.tset_desc[2 * set + 1];
+    const uint32_t v = (uint32_t)val;
+    const uint32_t* __restrict__ ids = st.tset_ids + off;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ids[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < st.tset_desc[2 * set + 1] && ids[lo] == v) { *sc = st.tset_sc[off + lo]; return true; }
+    return false;
+}
+
 // Parsed-query evaluation on document `s` (bluge BooleanSearcher semantics,
 // search_boolean.go:174-244).  *sp receives the parsed query's score.
 __device__ __forceinline__ bool eval_parsed(const DStore& st, uint8_t qkind, const DClause* __restrict__ cl, int n,
@@ -46,15 +62,17 @@ __device__ __forceinline__ bool eval_parsed(const DStore& st, uint8_t qkind, con
     for (int i = 0; i < n; i++) {
         const DClause c = cl[i];
         bool h = false;
+        double sc = c.score;
         if (c.op != OP_FALSE) {
             const uint8_t kind = st.fkind[c.field][s];
             const int64_t val = st.fval[c.field][s];
             if (c.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)c.term;
             else if (c.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= c.lo && val <= c.hi;
+            else if (c.op == OP_TERMSET) h = kind == KIND_KEYWORD && termset_hit(st, c.term, val, &sc);
             else h = (kind == KIND_KEYWORD && val == (int64_t)c.term) || (kind == KIND_NUMERIC && val == c.lo);
         }
-        if (c.occur == OCC_MUST) { has_must = true; if (h) ms += c.score; else fail = true; }
-        else if (c.occur == OCC_SHOULD) { has_should = true; if (h) { ss += c.score; any_should = true; } }
+        if (c.occur == OCC_MUST) { has_must = true; if (h) ms += sc; else fail = true; }
+        else if (c.occur == OCC_SHOULD) { has_should = true; if (h) { ss += sc; any_should = true; } }
         else if (h) fail = true;
     }
     if (fail) return false;
@@ -286,15 +304,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* _
             for (int j = 0; j < kScanJ; j++) {
                 if (!m[j]) continue;
                 bool h = false;
+                double sc = k.score;
                 if (k.op != OP_FALSE) {
                     const uint8_t kind = fk[s[j]];
                     const int64_t val = fv[s[j]];
                     if (k.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)k.term;
                     else if (k.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= k.lo && val <= k.hi;
+                    else if (k.op == OP_TERMSET) h = kind == KIND_KEYWORD && termset_hit(st, k.term, val, &sc);
                     else h = (kind == KIND_KEYWORD && val == (int64_t)k.term) || (kind == KIND_NUMERIC && val == k.lo);
                 }
-                if (k.occur == OCC_MUST) { if (h) ms[j] += k.score; else m[j] = false; }
-                else if (k.occur == OCC_SHOULD) { if (h) { ss[j] += k.score; anys[j] = true; } }
+                if (k.occur == OCC_MUST) { if (h) ms[j] += sc; else m[j] = false; }
+                else if (k.occur == OCC_SHOULD) { if (h) { ss[j] += sc; anys[j] = true; } }
                 else if (h) m[j] = false;
             }
         }
@@ -479,12 +499,14 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
                         for (int f = 0; f < NF; f++)
                             if (k.field == f) { kind = kk[f][j]; val = vv[f][j]; }
                         bool h = false;
+                        double sc = k.score;
                         if (k.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)k.term;
                         else if (k.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= k.lo && val <= k.hi;
+                        else if (k.op == OP_TERMSET) h = kind == KIND_KEYWORD && termset_hit(st, k.term, val, &sc);
                         else if (k.op != OP_FALSE)
                             h = (kind == KIND_KEYWORD && val == (int64_t)k.term) || (kind == KIND_NUMERIC && val == k.lo);
-                        if (k.occur == OCC_MUST) { if (h) msc[j] += k.score; else m[j] = false; }
-                        else if (k.occur == OCC_SHOULD) { if (h) { ssc[j] += k.score; anys[j] = true; } }
+                        if (k.occur == OCC_MUST) { if (h) msc[j] += sc; else m[j] = false; }
+                        else if (k.occur == OCC_SHOULD) { if (h) { ssc[j] += sc; anys[j] = true; } }
                         else if (h) m[j] = false;
                     }
                 }

@@ -1410,6 +1410,24 @@ extern "C" int32_t mm_debug_group_indexes(const int32_t* counts, const int64_t* 
     return g;
 }
 
+extern "C" int mm_debug_term_match(int32_t kind, const char* pattern, int32_t fuzziness, const char* term,
+                                   double* boost) {
+    nkm::TermMatcher m;
+    *boost = 0.0;
+    if (kind == 2) {
+        if (fuzziness < 0 || fuzziness > 2) return -1;
+        m.kind = nkm::TermMatcher::K_FUZZY;
+        m.pattern = pattern;
+        m.fuzziness = fuzziness;
+    } else {
+        m.kind = nkm::TermMatcher::K_REGEXP;
+        m.pattern = kind == 3 ? nkm::wildcard_to_regexp(pattern) : std::string(pattern);
+        nkm::MtStatus st = m.re.compile(m.pattern);
+        if (st != nkm::MT_OK) return st == nkm::MT_UNSUPPORTED ? -2 : -1;
+    }
+    return m.accept(term, boost) ? 1 : 0;
+}
+
 extern "C" int mm_debug_compile(const char* query) {
     nkm::CompiledQuery cq;
     int rc = nkm::compile_query(query ? query : "", &cq);

@@ -291,6 +291,68 @@ void Core::set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val) {
     fval_[f][slot] = val;
 }
 
+// Interns a regexp/wildcard/fuzzy matcher (kind, pattern, fuzziness, boost).
+uint32_t Core::termset_of(const HostClause& c) {
+    std::string key;
+    key.push_back((char)c.mt_kind);
+    key.push_back((char)c.fuzziness);
+    key.append((const char*)&c.score, sizeof(double));
+    key += c.term;
+    auto it = tset_index_.find(key);
+    if (it != tset_index_.end()) return it->second;
+    TermSet ts;
+    ts.m.kind = (TermMatcher::Kind)c.mt_kind;
+    ts.m.pattern = c.term;
+    ts.m.fuzziness = c.fuzziness;
+    if (ts.m.kind == TermMatcher::K_REGEXP) ts.m.re.compile(c.term);  // validated by compile_query
+    ts.b = c.score;
+    const uint32_t id = (uint32_t)tsets_.size();
+    tsets_.push_back(std::move(ts));
+    tset_index_.emplace(std::move(key), id);
+    tsets_dirty_ = true;
+    return id;
+}
+
+// bluge enumerates the field dictionary through the matcher's automaton at
+// every search (search_regexp.go:27-56, search_fuzzy.go:79-113); the keyword
+// dictionary here only grows, so each set is extended over the ids interned
+// since the last pass.  Ids of strings that are not values of the clause's
+// field are harmless: the kernels test the candidate's own value id.
+void Core::refresh_termsets() {
+    if (tsets_.empty()) return;
+    const uint32_t nd = (uint32_t)dict_.str.size();
+    for (auto& ts : tsets_) {
+        for (uint32_t id = ts.done; id < nd; id++) {
+            double tb;
+            if (!ts.m.accept(dict_.str[id], &tb)) continue;
+            ts.ids.push_back(id);
+            // RegexpQuery(b): b.  Fuzzy MatchQuery(b): (0 + b*tb) * b (composite.go:37-43)
+            ts.sc.push_back(ts.m.kind == TermMatcher::K_FUZZY ? (0.0 + ts.b * tb) * ts.b : ts.b);
+            tsets_dirty_ = true;
+        }
+        ts.done = nd;
+    }
+    if (!tsets_dirty_) return;
+    std::vector<uint32_t> desc, ids;
+    std::vector<double> sc;
+    for (auto& ts : tsets_) {
+        desc.push_back((uint32_t)ids.size());
+        desc.push_back((uint32_t)ts.ids.size());
+        ids.insert(ids.end(), ts.ids.begin(), ts.ids.end());
+        sc.insert(sc.end(), ts.sc.begin(), ts.sc.end());
+    }
+    d_tset_desc_.reserve(desc.size(), false);
+    d_tset_ids_.reserve(std::max<size_t>(ids.size(), 1), false);
+    d_tset_sc_.reserve(std::max<size_t>(sc.size(), 1), false);
+    NKM_HIP(hipMemcpyAsync(d_tset_desc_.p, desc.data(), desc.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream_));
+    if (!ids.empty()) {
+        NKM_HIP(hipMemcpyAsync(d_tset_ids_.p, ids.data(), ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream_));
+        NKM_HIP(hipMemcpyAsync(d_tset_sc_.p, sc.data(), sc.size() * sizeof(double), hipMemcpyHostToDevice, stream_));
+    }
+    NKM_HIP(hipStreamSynchronize(stream_));  // the staging vectors die here
+    tsets_dirty_ = false;
+}
+
 // Assigns (or reuses) the compiled signature of a ticket's search.
 uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party) {
     std::vector<DClause> dc;
@@ -307,9 +369,14 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
         if (c.op != OP_FALSE) {
             d.field = field_of(c.field);
             if (c.op == OP_TERM || c.op == OP_NUMLIT) d.term = dict_.intern(c.term);
+            else if (c.op == OP_TERMSET) d.term = termset_of(c);
         }
         dc.push_back(d);
     }
+    // a fuzzy clause scores per accepted term: variable-score search, no score bound
+    bool fuzzy = false;
+    for (auto& c : cq.clauses)
+        if (c.op == OP_TERMSET && c.mt_kind == TermMatcher::K_FUZZY && c.occur != OCC_MUSTNOT) fuzzy = true;
     std::string key;
     key.reserve(16 + dc.size() * sizeof(DClause));
     key.push_back((char)cq.kind);
@@ -359,6 +426,10 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
     double ub = (S + 1.0) + 1.0;
     s.ub_key = std::isfinite(ub) ? sortable_i64(ub) : INT64_MAX;
     if (!std::isfinite(ms) || !std::isfinite(ss)) s.ub_key = INT64_MAX;
+    if (fuzzy) {
+        s.var_score = true;
+        s.ub_key = INT64_MAX;
+    }
     {
         std::vector<uint16_t> fs;
         for (auto& d : dc)
@@ -895,6 +966,7 @@ void Core::sync_device() {
         NKM_HIP(hipMemcpyAsync(d_fkind_ptrs_.p, pk.data(), pk.size() * sizeof(uint8_t*), hipMemcpyHostToDevice, stream_));
     }
     if (index_dirty_) build_index();
+    refresh_termsets();
     NKM_HIP(hipStreamSynchronize(stream_));
 }
 
@@ -910,6 +982,9 @@ DStore Core::dstore() const {
     st.fkind = d_fkind_ptrs_.p;
     st.order = d_order_.p;
     st.postings = d_postings_.p;
+    st.tset_desc = d_tset_desc_.p;
+    st.tset_ids = d_tset_ids_.p;
+    st.tset_sc = d_tset_sc_.p;
     return st;
 }
 

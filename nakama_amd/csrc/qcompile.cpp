@@ -8,6 +8,7 @@
 // yacc table resolves to the longer production, which is also what the
 // matcher tries first).
 #include "qcompile.h"
+#include "termmatch.h"
 
 #include <cmath>
 
@@ -172,8 +173,14 @@ private:
 
     struct Base {
         HostClause c;
-        enum { B_MATCH, B_NUMLIT, B_RANGE, B_DATE, B_PHRASE } kind;
+        enum { B_MATCH, B_NUMLIT, B_RANGE, B_DATE, B_PHRASE, B_REGEXP, B_FUZZY } kind;
     };
+    bool search_error_ = false;
+    Base multi_term(const std::string& field, const std::string& pattern, uint8_t kind, int fuzz);
+    Base fuzzy_token(const std::string& field, const std::string& s, const std::string& fz);
+public:
+    bool search_error() const { return search_error_; }
+private:
     Base base();
     Base string_token(const std::string& field, const std::string& s);
     Base number_token(const std::string& field, const std::string& s);
@@ -189,14 +196,59 @@ std::string Compiler::signed_number() {  // posOrNegNumber
 
 Compiler::Base Compiler::string_token(const std::string& field, const std::string& s) {
     // queryStringStringToken (query_string_parser.go:171-183)
-    if (s.size() >= 2 && s.front() == '/' && s.back() == '/') throw Fail{CQ_UNSUPPORTED};  // RegexpQuery
-    if (s.find_first_of("*?") != std::string::npos) throw Fail{CQ_UNSUPPORTED};          // WildcardQuery
+    if (s.size() >= 2 && s.front() == '/' && s.back() == '/') {
+        // RegexpQuery: one leading '^' trimmed (bluge/query.go:1264-1265)
+        std::string re = s.substr(1, s.size() - 2);
+        if (!re.empty() && re[0] == '^') re.erase(0, 1);
+        return multi_term(field, re, TermMatcher::K_REGEXP, 0);
+    }
+    if (s.find_first_of("*?") != std::string::npos)  // WildcardQuery (query.go:1475-1485)
+        return multi_term(field, wildcard_to_regexp(s), TermMatcher::K_REGEXP, 0);
     Base b;
     b.kind = Base::B_MATCH;
     b.c.op = field.empty() ? OP_FALSE : OP_TERM;  // "" -> _all, never indexed
     b.c.field = field;
     b.c.term = s;
     return b;
+}
+
+Compiler::Base Compiler::multi_term(const std::string& field, const std::string& pattern, uint8_t kind, int fuzz) {
+    Base b;
+    b.kind = kind == TermMatcher::K_FUZZY ? Base::B_FUZZY : Base::B_REGEXP;
+    b.c.op = field.empty() ? OP_FALSE : OP_TERMSET;
+    b.c.field = field;
+    b.c.term = pattern;
+    b.c.mt_kind = kind;
+    b.c.fuzziness = fuzz;
+    if (kind == TermMatcher::K_REGEXP) {
+        GoRegexp re;
+        MtStatus st = re.compile(pattern);
+        if (st == MT_UNSUPPORTED) throw Fail{CQ_UNSUPPORTED};
+        if (st == MT_SEARCH_ERROR) search_error_ = true;
+    }
+    return b;
+}
+
+// queryStringStringTokenFuzzy (query_string_parser.go:185-196): MatchQuery with
+// fuzziness int(ParseFloat(fz)); fuzziness 0 is a plain MatchQuery, outside
+// [0, MaxFuzziness=2] the FuzzySearcher fails (search_fuzzy.go:47-53).
+Compiler::Base Compiler::fuzzy_token(const std::string& field, const std::string& s, const std::string& fz) {
+    double v;
+    if (!go_parse_float(fz, &v)) bad();
+    if (std::isnan(v) || v <= -1.0 || v >= 3.0) {
+        search_error_ = true;
+        return multi_term(field, s, TermMatcher::K_FUZZY, 0);
+    }
+    const int f = (int)v;  // Go int(): truncation toward zero
+    if (f == 0) {
+        Base b;
+        b.kind = Base::B_MATCH;
+        b.c.op = field.empty() ? OP_FALSE : OP_TERM;
+        b.c.field = field;
+        b.c.term = s;
+        return b;
+    }
+    return multi_term(field, s, TermMatcher::K_FUZZY, f);
 }
 
 Compiler::Base Compiler::number_token(const std::string& field, const std::string& s) {
@@ -255,13 +307,13 @@ Compiler::Base Compiler::base() {
     if (at() == TK_PHRASE) { i_++; Base b; b.kind = Base::B_PHRASE; b.c.op = OP_FALSE; return b; }
     if (at() != TK_STR) bad();
     std::string first = t_[i_++].s;
-    if (at() == TK_TILDE) throw Fail{CQ_UNSUPPORTED};  // fuzzy
+    if (at() == TK_TILDE) { std::string fz = t_[i_++].s; return fuzzy_token("", first, fz); }
     if (at() != TK_COLON) return string_token("", first);
     i_++;
     switch (at()) {
     case TK_STR: {
         std::string v = t_[i_++].s;
-        if (at() == TK_TILDE) throw Fail{CQ_UNSUPPORTED};  // fuzzy
+        if (at() == TK_TILDE) { std::string fz = t_[i_++].s; return fuzzy_token(first, v, fz); }
         return string_token(first, v);
     }
     case TK_NUM:
@@ -310,6 +362,11 @@ void Compiler::run() {
         case Base::B_RANGE: b.c.score = boosted ? boost : 1.0; break;
         case Base::B_DATE: b.c.score = 1.0; break;
         case Base::B_PHRASE: b.c.score = 0.0; break;
+        // RegexpQuery(b): term searchers ConstantScorer(b), one term per doc -> b.
+        // Fuzzy MatchQuery(b): Bool{should:[Fuzzy(b)], boost b}, term boost
+        // b*tb -> (0 + b*tb) * b; the set stores the per-term value, score = b.
+        case Base::B_REGEXP:
+        case Base::B_FUZZY: b.c.score = boosted ? boost : 1.0; break;
         }
         b.c.occur = occ;
         out_->clauses.push_back(b.c);
@@ -328,6 +385,10 @@ int compile_query(const std::string& q, CompiledQuery* out) {
     try {
         Compiler c(toks, out);
         c.run();
+        if (c.search_error()) {  // every search with this query fails
+            out->clauses.clear();
+            out->kind = QK_MATCHNONE;
+        }
     } catch (const Fail& f) {
         out->clauses.clear();
         return f.code;

@@ -19,6 +19,7 @@ enum ClauseOp : uint8_t {
     OP_RANGE = 1,   // numeric/datetime term value in [lo, hi]            (Numeric/DateRangeQuery)
     OP_NUMLIT = 2,  // keyword == term  OR  numeric term value == lo      (queryStringNumberToken)
     OP_FALSE = 3,   // never matches (phrase on untokenised fields, unfielded `_all` clauses)
+    OP_TERMSET = 4, // keyword value in the accepted-term set of a regexp/wildcard/fuzzy matcher (termmatch.h)
 };
 enum Occur : uint8_t { OCC_MUST = 0, OCC_SHOULD = 1, OCC_MUSTNOT = 2 };
 
@@ -28,7 +29,9 @@ struct HostClause {
     std::string field;  // full field name, e.g. "properties.region", "min_count"
     std::string term;   // TERM / NUMLIT keyword form
     int64_t lo = 0, hi = 0;
-    double score = 1.0; // contribution when matched
+    double score = 1.0; // contribution when matched (TERMSET: the query boost b)
+    uint8_t mt_kind = 0; // TERMSET: TermMatcher::Kind; `term` holds the regexp / fuzzy term
+    int fuzziness = 0;
 };
 
 enum QueryKind : uint8_t { QK_BOOL = 0, QK_MATCHALL = 1, QK_MATCHNONE = 2 };
@@ -41,8 +44,13 @@ struct CompiledQuery {
 enum CompileStatus { CQ_OK = 0, CQ_INVALID = -1, CQ_UNSUPPORTED = -8 };
 
 // Compiles `q`; CQ_INVALID mirrors ErrMatchmakerQueryInvalid (parse or Validate
-// failure, server/matchmaker.go:449-457).  Regexp, wildcard and fuzzy clauses
-// return CQ_UNSUPPORTED (not yet lowered).
+// failure, server/matchmaker.go:449-457).  A regexp that Go's parser (or
+// vellum's compiler) rejects, or a fuzziness outside [0, 2], is accepted at Add
+// (RegexpQuery.Validate returns nil, query.go:1271-1273) but fails every search:
+// such a query compiles to QK_MATCHNONE, the outcome of processDefault's
+// `continue` on a search error (matchmaker_process.go:97-101).  Regexp constructs
+// not lowered here (Unicode classes, flag groups, POSIX classes) return
+// CQ_UNSUPPORTED.
 int compile_query(const std::string& q, CompiledQuery* out);
 
 }  // namespace nkm

@@ -1,0 +1,526 @@
+// nakama_amd/csrc/termmatch.cpp — regexp / wildcard / fuzzy term matchers
+// (see termmatch.h).  The regexp parser follows Go 1.20 regexp/syntax
+// (parse.go: Parse with Perl = ClassNL|OneLine|PerlX|UnicodeGroups) for the
+// constructs vellum compiles; the matcher is a Pike VM over runes.
+#include "termmatch.h"
+
+#include <algorithm>
+#include <cctype>
+#include <cstdlib>
+#include <cstring>
+
+namespace nkm {
+
+namespace {
+
+constexpr uint32_t kMaxRune = 0x10FFFF;
+constexpr uint32_t kBadRune = 0xFFFFFFFFu;
+constexpr size_t kMaxProg = 1u << 18;  // stands in for vellum's DFA size limit (regexp.DefaultLimit)
+
+using Ranges = std::vector<std::pair<uint32_t, uint32_t>>;
+
+// Decodes one rune; invalid sequences (incl. surrogates, overlongs) give kBadRune
+// and consume one byte (Go's utf8.DecodeRuneInString width-1 error).
+uint32_t decode(const std::string& s, size_t& i) {
+    const unsigned char c = (unsigned char)s[i];
+    if (c < 0x80) { i++; return c; }
+    int n = c >= 0xF0 && c <= 0xF4 ? 4 : c >= 0xE0 ? 3 : c >= 0xC2 && c < 0xE0 ? 2 : 0;
+    if (n == 0 || i + n > s.size()) { i++; return kBadRune; }
+    uint32_t r = n == 2 ? (c & 0x1F) : n == 3 ? (c & 0x0F) : (c & 0x07);
+    for (int k = 1; k < n; k++) {
+        const unsigned char d = (unsigned char)s[i + k];
+        if ((d & 0xC0) != 0x80) { i++; return kBadRune; }
+        r = (r << 6) | (d & 0x3F);
+    }
+    if ((n == 3 && r < 0x800) || (n == 4 && (r < 0x10000 || r > kMaxRune)) || (r >= 0xD800 && r <= 0xDFFF)) {
+        i++;
+        return kBadRune;
+    }
+    i += n;
+    return r;
+}
+
+void normalize(Ranges& r) {
+    std::sort(r.begin(), r.end());
+    Ranges o;
+    for (auto& p : r) {
+        if (!o.empty() && p.first <= o.back().second + 1) o.back().second = std::max(o.back().second, p.second);
+        else o.push_back(p);
+    }
+    r.swap(o);
+}
+
+Ranges negate(Ranges r) {
+    normalize(r);
+    Ranges o;
+    uint32_t next = 0;
+    for (auto& p : r) {
+        if (p.first > next) o.push_back({next, p.first - 1});
+        next = p.second + 1;
+    }
+    if (next <= kMaxRune) o.push_back({next, kMaxRune});
+    return o;
+}
+
+// Perl classes \d \s \w (regexp/syntax perl_groups.go), ASCII only.
+bool perl_class(char c, Ranges* out) {
+    Ranges r;
+    switch (c | 0x20) {
+    case 'd': r = {{'0', '9'}}; break;
+    case 's': r = {{'\t', '\n'}, {'\f', '\r'}, {' ', ' '}}; break;
+    case 'w': r = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}; break;
+    default: return false;
+    }
+    if (c >= 'A' && c <= 'Z') r = negate(r);
+    out->insert(out->end(), r.begin(), r.end());
+    return true;
+}
+
+struct Stop { MtStatus st; };
+
+struct Node {
+    enum T : uint8_t { CLASS, CAT, ALT, STAR, PLUS, QUEST, REPEAT, EMPTY } t;
+    Ranges cls;
+    std::vector<int> sub;
+    int mn = 0, mx = 0;
+};
+
+int hexval(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+}
+
+}  // namespace
+
+struct RxCompiler {
+    const std::string& s;
+    size_t i = 0;
+    int depth = 0;
+    std::vector<Node> nodes;
+    explicit RxCompiler(const std::string& p) : s(p) {}
+
+    [[noreturn]] static void err() { throw Stop{MT_SEARCH_ERROR}; }
+    [[noreturn]] static void unsupported() { throw Stop{MT_UNSUPPORTED}; }
+    bool end() const { return i >= s.size(); }
+    char peek(size_t k = 0) const { return i + k < s.size() ? s[i + k] : '\0'; }
+    int add(Node n) { nodes.push_back(std::move(n)); return (int)nodes.size() - 1; }
+    int lit(uint32_t lo, uint32_t hi) { Node n; n.t = Node::CLASS; n.cls = {{lo, hi}}; return add(std::move(n)); }
+
+    uint32_t rune() {
+        uint32_t r = decode(s, i);
+        if (r == kBadRune) err();  // ErrInvalidUTF8
+        return r;
+    }
+
+    // parseEscape (parse.go): the character after a backslash (i at the backslash).
+    uint32_t escape_char() {
+        i++;
+        if (end()) err();  // ErrTrailingBackslash
+        const char c = s[i];
+        if (c >= '1' && c <= '7') {
+            if (!(peek(1) >= '0' && peek(1) <= '7')) err();  // backreference
+        }
+        if (c >= '0' && c <= '7') {
+            uint32_t r = c - '0';
+            i++;
+            for (int k = 1; k < 3 && !end() && s[i] >= '0' && s[i] <= '7'; k++) r = r * 8 + (s[i++] - '0');
+            return r;
+        }
+        if (c == 'x') {
+            i++;
+            if (end()) err();
+            if (s[i] == '{') {
+                i++;
+                uint32_t r = 0;
+                int nd = 0;
+                while (!end() && hexval(s[i]) >= 0) {
+                    r = r * 16 + hexval(s[i++]);
+                    if (r > kMaxRune) err();
+                    nd++;
+                }
+                if (end() || s[i] != '}' || nd == 0) err();
+                i++;
+                return r;
+            }
+            if (i + 1 >= s.size() || hexval(s[i]) < 0 || hexval(s[i + 1]) < 0) err();
+            uint32_t r = hexval(s[i]) * 16 + hexval(s[i + 1]);
+            i += 2;
+            return r;
+        }
+        static const char kCtl[] = "a\af\fn\nr\rt\tv\v";
+        for (int k = 0; kCtl[k]; k += 2)
+            if (c == kCtl[k]) { i++; return (uint32_t)(unsigned char)kCtl[k + 1]; }
+        if ((unsigned char)c < 0x80 && !std::isalnum((unsigned char)c)) { i++; return (uint32_t)c; }
+        err();  // ErrInvalidEscape
+    }
+
+    int char_class() {  // parseClass, i at '['
+        i++;
+        Ranges r;
+        bool neg = false;
+        if (peek() == '^') { neg = true; i++; }
+        bool first = true;
+        while (first || peek() != ']') {
+            if (end()) err();  // ErrMissingBracket
+            first = false;
+            if (peek() == '[' && peek(1) == ':' && s.find(":]", i + 2) != std::string::npos) unsupported();  // POSIX
+            if (peek() == '\\' && (peek(1) == 'p' || peek(1) == 'P')) unsupported();                     // \pN
+            if (peek() == '\\' && perl_class(peek(1), &r)) { i += 2; continue; }
+            uint32_t lo = peek() == '\\' ? escape_char() : rune();
+            uint32_t hi = lo;
+            if (peek() == '-' && i + 1 < s.size() && s[i + 1] != ']') {
+                i++;
+                hi = peek() == '\\' ? escape_char() : rune();
+                if (hi < lo) err();  // ErrInvalidCharRange
+            }
+            r.push_back({lo, hi});
+        }
+        i++;  // ']'
+        if (neg) r = negate(r);  // ClassNL: a negated class may match '\n'
+        else normalize(r);
+        Node n;
+        n.t = Node::CLASS;
+        n.cls = std::move(r);
+        return add(std::move(n));
+    }
+
+    // {n}, {n,}, {n,m}; false (literal '{') when it does not parse (parseRepeat).
+    bool repeat_bounds(int* mn, int* mx) {
+        size_t j = i + 1;
+        auto num = [&](int* v) {
+            size_t st = j;
+            long x = 0;
+            while (j < s.size() && s[j] >= '0' && s[j] <= '9') {
+                x = x * 10 + (s[j] - '0');
+                if (x > 100000) x = 100000;
+                j++;
+            }
+            if (j == st || (s[st] == '0' && j - st > 1)) return false;
+            *v = (int)x;
+            return true;
+        };
+        if (!num(mn)) return false;
+        if (j < s.size() && s[j] == ',') {
+            j++;
+            if (j < s.size() && s[j] == '}') *mx = -1;
+            else if (!num(mx)) return false;
+        } else {
+            *mx = *mn;
+        }
+        if (j >= s.size() || s[j] != '}') return false;
+        i = j + 1;
+        return true;
+    }
+
+    int concat() {
+        std::vector<int> items;
+        bool last_repeat = false;
+        while (!end() && peek() != '|' && peek() != ')') {
+            const char c = peek();
+            int mn = 0, mx = 0;
+            Node::T rt = Node::EMPTY;
+            if (c == '*') { rt = Node::STAR; i++; }
+            else if (c == '+') { rt = Node::PLUS; i++; }
+            else if (c == '?') { rt = Node::QUEST; i++; }
+            else if (c == '{' && repeat_bounds(&mn, &mx)) {
+                rt = Node::REPEAT;
+                if (mn > 1000 || mx > 1000 || (mx >= 0 && mx < mn)) err();  // ErrInvalidRepeatSize
+            }
+            if (rt != Node::EMPTY) {
+                if (items.empty()) err();  // ErrMissingRepeatArgument
+                if (last_repeat) err();    // ErrInvalidRepeatOp (a**)
+                bool lazy = false;
+                if (peek() == '?') { lazy = true; i++; }
+                Node n;
+                n.t = rt;
+                n.sub = {items.back()};
+                n.mn = mn;
+                n.mx = mx;
+                items.back() = add(std::move(n));
+                last_repeat = true;
+                if (lazy) err();  // vellum ErrNoLazy
+                continue;
+            }
+            last_repeat = false;
+            items.push_back(atom());
+        }
+        if (items.empty()) { Node n; n.t = Node::EMPTY; return add(std::move(n)); }
+        if (items.size() == 1) return items[0];
+        Node n;
+        n.t = Node::CAT;
+        n.sub = std::move(items);
+        return add(std::move(n));
+    }
+
+    int alternate() {
+        std::vector<int> br{concat()};
+        while (peek() == '|' && !end()) { i++; br.push_back(concat()); }
+        if (br.size() == 1) return br[0];
+        Node n;
+        n.t = Node::ALT;
+        n.sub = std::move(br);
+        return add(std::move(n));
+    }
+
+    int atom() {
+        const char c = peek();
+        switch (c) {
+        case '(': {
+            i++;
+            if (peek() == '?') {
+                if (peek(1) == ':') i += 2;
+                else if (peek(1) == 'P' && peek(2) == '<') {
+                    size_t close = s.find('>', i + 3);
+                    if (close == std::string::npos || close == i + 3) err();  // ErrInvalidNamedCapture
+                    for (size_t k = i + 3; k < close; k++)
+                        if (!(std::isalnum((unsigned char)s[k]) || s[k] == '_')) err();
+                    i = close + 1;
+                } else {
+                    unsupported();  // flag groups (?i) (?s:...) ...
+                }
+            }
+            if (++depth > 1000) err();  // ErrNestingDepth
+            int r = alternate();
+            depth--;
+            if (peek() != ')' || end()) err();  // ErrMissingParen
+            i++;
+            return r;
+        }
+        case '.': { i++; Node n; n.t = Node::CLASS; n.cls = {{0, 9}, {11, kMaxRune}}; return add(std::move(n)); }
+        case '^':
+        case '$': err();  // OpBeginText/OpEndText: vellum ErrNoEmpty
+        case '[': return char_class();
+        case '\\': {
+            const char e = peek(1);
+            if (e == 'A' || e == 'z' || e == 'b' || e == 'B') err();  // anchors / word boundaries (vellum)
+            if (e == 'p' || e == 'P') unsupported();
+            if (e == 'Q') {  // \Q...\E literal text
+                i += 2;
+                std::vector<int> items;
+                while (!end() && !(peek() == '\\' && peek(1) == 'E')) {
+                    uint32_t r = rune();
+                    items.push_back(lit(r, r));
+                }
+                if (!end()) i += 2;
+                Node n;
+                if (items.empty()) { n.t = Node::EMPTY; return add(std::move(n)); }
+                n.t = Node::CAT;
+                n.sub = std::move(items);
+                return add(std::move(n));
+            }
+            Ranges r;
+            if (perl_class(e, &r)) {
+                i += 2;
+                normalize(r);
+                Node n;
+                n.t = Node::CLASS;
+                n.cls = std::move(r);
+                return add(std::move(n));
+            }
+            uint32_t ch = escape_char();
+            return lit(ch, ch);
+        }
+        default: {
+            uint32_t r = rune();
+            return lit(r, r);
+        }
+        }
+    }
+
+    // Thompson construction into the Pike-VM program.
+    GoRegexp* g = nullptr;
+    void emit(int n) {
+        auto& P = g->prog_;
+        if (P.size() > kMaxProg) err();
+        const Node& nd = nodes[n];
+        switch (nd.t) {
+        case Node::EMPTY: break;
+        case Node::CLASS:
+            g->classes_.push_back(nd.cls);
+            P.push_back({GoRegexp::I_CLASS, (uint32_t)g->classes_.size() - 1, 0});
+            break;
+        case Node::CAT:
+            for (int x : nd.sub) emit(x);
+            break;
+        case Node::ALT: {
+            std::vector<size_t> jumps;
+            for (size_t k = 0; k + 1 < nd.sub.size(); k++) {
+                size_t sp = P.size();
+                P.push_back({GoRegexp::I_SPLIT, 0, 0});
+                P[sp].x = (uint32_t)P.size();
+                emit(nd.sub[k]);
+                jumps.push_back(P.size());
+                P.push_back({GoRegexp::I_JMP, 0, 0});
+                P[sp].y = (uint32_t)P.size();
+            }
+            emit(nd.sub.back());
+            for (size_t j : jumps) P[j].x = (uint32_t)P.size();
+            break;
+        }
+        case Node::STAR: star(nd.sub[0]); break;
+        case Node::PLUS: {
+            size_t l1 = P.size();
+            emit(nd.sub[0]);
+            P.push_back({GoRegexp::I_SPLIT, (uint32_t)l1, (uint32_t)P.size() + 1});
+            break;
+        }
+        case Node::QUEST: quest(nd.sub[0]); break;
+        case Node::REPEAT:
+            for (int k = 0; k < nd.mn; k++) emit(nd.sub[0]);
+            if (nd.mx < 0) star(nd.sub[0]);
+            else {
+                // x{n,m}: (x(x(...)?)?)? nested, m-n deep
+                std::vector<size_t> splits;
+                for (int k = nd.mn; k < nd.mx; k++) {
+                    splits.push_back(P.size());
+                    P.push_back({GoRegexp::I_SPLIT, (uint32_t)P.size() + 1, 0});
+                    emit(nd.sub[0]);
+                    if (P.size() > kMaxProg) err();
+                }
+                for (size_t sp : splits) P[sp].y = (uint32_t)P.size();
+            }
+            break;
+        }
+    }
+    void star(int sub) {
+        auto& P = g->prog_;
+        size_t l1 = P.size();
+        P.push_back({GoRegexp::I_SPLIT, (uint32_t)l1 + 1, 0});
+        emit(sub);
+        P.push_back({GoRegexp::I_JMP, (uint32_t)l1, 0});
+        P[l1].y = (uint32_t)P.size();
+    }
+    void quest(int sub) {
+        auto& P = g->prog_;
+        size_t sp = P.size();
+        P.push_back({GoRegexp::I_SPLIT, (uint32_t)sp + 1, 0});
+        emit(sub);
+        P[sp].y = (uint32_t)P.size();
+    }
+};
+
+MtStatus GoRegexp::compile(const std::string& pattern) {
+    prog_.clear();
+    classes_.clear();
+    RxCompiler c(pattern);
+    c.g = this;
+    try {
+        int root = c.alternate();
+        if (!c.end()) RxCompiler::err();  // unmatched ')' (ErrUnexpectedParen)
+        c.emit(root);
+        prog_.push_back({I_MATCH, 0, 0});
+    } catch (const Stop& s) {
+        prog_.clear();
+        return s.st;
+    }
+    return MT_OK;
+}
+
+bool GoRegexp::full_match(const std::string& term) const {
+    if (prog_.empty()) return false;
+    const size_t n = prog_.size();
+    std::vector<uint32_t> cur, nxt, stack;
+    std::vector<uint32_t> mark(n, 0);
+    uint32_t gen = 1;
+    auto add = [&](std::vector<uint32_t>& list, uint32_t pc0) {
+        stack.clear();
+        stack.push_back(pc0);
+        while (!stack.empty()) {
+            uint32_t pc = stack.back();
+            stack.pop_back();
+            if (mark[pc] == gen) continue;
+            mark[pc] = gen;
+            const Inst& in = prog_[pc];
+            if (in.op == I_JMP) stack.push_back(in.x);
+            else if (in.op == I_SPLIT) { stack.push_back(in.y); stack.push_back(in.x); }
+            else list.push_back(pc);
+        }
+    };
+    add(cur, 0);
+    size_t i = 0;
+    while (i < term.size()) {
+        if (cur.empty()) return false;
+        const uint32_t r = decode(term, i);
+        gen++;
+        nxt.clear();
+        for (uint32_t pc : cur) {
+            const Inst& in = prog_[pc];
+            if (in.op != I_CLASS || r == kBadRune) continue;
+            const auto& cls = classes_[in.x];
+            auto it = std::upper_bound(cls.begin(), cls.end(), std::make_pair(r, kBadRune));
+            if (it != cls.begin() && std::prev(it)->second >= r) add(nxt, pc + 1);
+        }
+        cur.swap(nxt);
+    }
+    for (uint32_t pc : cur)
+        if (prog_[pc].op == I_MATCH) return true;
+    return false;
+}
+
+namespace {
+// Runes as Go's range loop yields them (invalid bytes -> U+FFFD each).
+std::vector<uint32_t> runes_of(const std::string& s) {
+    std::vector<uint32_t> v;
+    size_t i = 0;
+    while (i < s.size()) {
+        uint32_t r = decode(s, i);
+        v.push_back(r == kBadRune ? 0xFFFD : r);
+    }
+    return v;
+}
+}  // namespace
+
+int osa_distance_runes(const std::string& a, const std::string& b, int max) {
+    const std::vector<uint32_t> x = runes_of(a), y = runes_of(b);
+    const int n = (int)x.size(), m = (int)y.size();
+    if (std::abs(n - m) > max) return max + 1;
+    std::vector<int> p2(m + 1), p1(m + 1), c(m + 1);
+    for (int j = 0; j <= m; j++) p1[j] = j;
+    for (int i = 1; i <= n; i++) {
+        c[0] = i;
+        int row_min = c[0];
+        for (int j = 1; j <= m; j++) {
+            int v = std::min({p1[j] + 1, c[j - 1] + 1, p1[j - 1] + (x[i - 1] == y[j - 1] ? 0 : 1)});
+            if (i > 1 && j > 1 && x[i - 1] == y[j - 2] && x[i - 2] == y[j - 1]) v = std::min(v, p2[j - 2] + 1);
+            c[j] = v;
+            row_min = std::min(row_min, v);
+        }
+        if (row_min > max) return max + 1;
+        p2.swap(p1);
+        p1.swap(c);
+    }
+    return std::min(p1[m], max + 1);
+}
+
+bool TermMatcher::accept(const std::string& term, double* boost) const {
+    *boost = 1.0;
+    if (kind == K_REGEXP) return re.full_match(term);
+    int d = osa_distance_runes(pattern, term, fuzziness);
+    if (d > fuzziness) return false;
+    if (term != pattern) {  // boostFromDistance (search_fuzzy.go:115-126)
+        const double ml = (double)std::min(runes_of(pattern).size(), runes_of(term).size());
+        *boost = 1.0 - ((double)d / ml);
+    }
+    return true;
+}
+
+std::string wildcard_to_regexp(const std::string& w) {
+    std::string o;
+    for (char c : w) {
+        switch (c) {
+        case '+': case '(': case ')': case '^': case '$': case '.':
+        case '{': case '}': case '[': case ']': case '|': case '\\':
+            o += '\\';
+            o += c;
+            break;
+        case '*': o += ".*"; break;
+        case '?': o += '.'; break;
+        default: o += c;
+        }
+    }
+    return o;
+}
+
+}  // namespace nkm

@@ -1,0 +1,376 @@
+// oracle/go_regexp.h — TEST INFRASTRUCTURE ONLY (part of the CPU oracle; never
+// linked into the product).  Restates, for the oracle's per-document query
+// evaluation, the term matching of bluge's multi-term queries:
+//   * RegexpQuery / WildcardQuery (vendor/.../bluge/query.go:1254-1273,
+//     1455-1485; search/searcher/search_regexp.go:27-100): the pattern is parsed
+//     by Go regexp/syntax with syntax.Perl flags and compiled by
+//     vellum/regexp/compile.go:56-200, which rejects anchors, word boundaries and
+//     lazy repetitions; a term matches when the WHOLE term is in the language;
+//   * FuzzyQuery (search_fuzzy.go:43-143): terms within restricted
+//     Damerau-Levenshtein distance <= fuzziness (vellum levenshtein automaton built
+//     with transpositions), per-term boost 1 - d / min(rune lengths).
+// Parsing is a direct recursive restatement of the grammar; matching computes
+// the set of end positions reachable from each start position over the term's
+// runes (no automaton), an independent method from the product's Pike VM.
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+namespace oracle_re {
+
+enum Status { OK = 0, SEARCH_ERROR = 1, UNSUPPORTED = 2 };
+
+// UTF-8 -> runes; invalid bytes -> -1 (a rune no class contains).
+inline std::vector<int32_t> runes(const std::string& s, bool bad_as_fffd) {
+    std::vector<int32_t> out;
+    size_t i = 0;
+    while (i < s.size()) {
+        unsigned char c = s[i];
+        int n = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+        int32_t r = -1;
+        if (n == 1) r = c;
+        else if (n > 1 && i + n <= s.size()) {
+            r = c & (0x7F >> n);
+            for (int k = 1; k < n; k++) {
+                unsigned char d = s[i + k];
+                if ((d >> 6) != 2) { r = -1; break; }
+                r = (r << 6) | (d & 0x3F);
+            }
+            static const int32_t kMin[5] = {0, 0, 0x80, 0x800, 0x10000};
+            if (r >= 0 && (r < kMin[n] || r > 0x10FFFF || (r >= 0xD800 && r < 0xE000))) r = -1;
+        }
+        if (r < 0) { i++; out.push_back(bad_as_fffd ? 0xFFFD : -1); }
+        else { i += n; out.push_back(r); }
+    }
+    return out;
+}
+
+struct Re {
+    enum K { SET, SEQ, OR, REP } k = SEQ;
+    std::vector<std::pair<int32_t, int32_t>> set;  // SET: rune ranges
+    bool neg = false;
+    std::vector<std::shared_ptr<Re>> kids;
+    int lo = 0, hi = 0;  // REP: hi < 0 = unbounded
+    bool has(int32_t r) const {
+        if (r < 0) return false;
+        bool in = false;
+        for (auto& p : set) in = in || (r >= p.first && r <= p.second);
+        return in != neg;
+    }
+};
+using RP = std::shared_ptr<Re>;
+
+struct Parse {
+    std::vector<int32_t> p;  // pattern runes
+    size_t i = 0;
+    int nest = 0;
+    struct Fail { Status s; };
+    [[noreturn]] void fail() { throw Fail{SEARCH_ERROR}; }
+    [[noreturn]] void unsup() { throw Fail{UNSUPPORTED}; }
+    bool at_end() const { return i >= p.size(); }
+    int32_t cur(size_t k = 0) const { return i + k < p.size() ? p[i + k] : -2; }
+
+    static RP single(int32_t a, int32_t b) { auto r = std::make_shared<Re>(); r->k = Re::SET; r->set = {{a, b}}; return r; }
+    static bool alnum(int32_t c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+    static bool odig(int32_t c) { return c >= '0' && c <= '7'; }
+    static int hexd(int32_t c) {
+        return c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+    }
+    // \d \s \w and negations as (ranges, negated)
+    bool perl(int32_t c, std::vector<std::pair<int32_t, int32_t>>* rs, bool* neg) {
+        int32_t l = c | 0x20;
+        if (l == 'd') *rs = {{'0', '9'}};
+        else if (l == 's') *rs = {{9, 10}, {12, 13}, {32, 32}};
+        else if (l == 'w') *rs = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}};
+        else return false;
+        *neg = c != l;
+        return true;
+    }
+    int32_t esc() {  // after the backslash
+        if (at_end()) fail();
+        int32_t c = p[i++];
+        if (c >= '1' && c <= '7' && !odig(cur())) fail();
+        if (odig(c)) {
+            int32_t v = c - '0';
+            for (int k = 0; k < 2 && odig(cur()); k++) v = v * 8 + (p[i++] - '0');
+            return v;
+        }
+        if (c == 'x') {
+            if (cur() == '{') {
+                i++;
+                int64_t v = 0;
+                size_t st = i;
+                while (hexd(cur()) >= 0) { v = v * 16 + hexd(p[i++]); if (v > 0x10FFFF) fail(); }
+                if (i == st || cur() != '}') fail();
+                i++;
+                return (int32_t)v;
+            }
+            if (hexd(cur()) < 0 || hexd(cur(1)) < 0) fail();
+            int32_t v = hexd(p[i]) * 16 + hexd(p[i + 1]);
+            i += 2;
+            return v;
+        }
+        switch (c) {
+        case 'a': return 7;
+        case 'f': return 12;
+        case 'n': return 10;
+        case 'r': return 13;
+        case 't': return 9;
+        case 'v': return 11;
+        }
+        if (c < 0x80 && !alnum(c)) return c;
+        fail();
+    }
+    RP klass() {  // after '['
+        auto r = std::make_shared<Re>();
+        r->k = Re::SET;
+        if (cur() == '^') { r->neg = true; i++; }
+        bool first = true;
+        std::vector<std::pair<int32_t, int32_t>> negs;  // negated perl classes inside
+        while (first || cur() != ']') {
+            if (at_end()) fail();
+            first = false;
+            if (cur() == '[' && cur(1) == ':') {
+                for (size_t j = i + 2; j + 1 < p.size(); j++)
+                    if (p[j] == ':' && p[j + 1] == ']') unsup();
+            }
+            if (cur() == '\\' && (cur(1) == 'p' || cur(1) == 'P')) unsup();
+            std::vector<std::pair<int32_t, int32_t>> rs;
+            bool ng;
+            if (cur() == '\\' && perl(cur(1), &rs, &ng)) {
+                i += 2;
+                if (!ng) r->set.insert(r->set.end(), rs.begin(), rs.end());
+                else {  // complement of rs within [0, 0x10FFFF]
+                    int32_t nx = 0;
+                    for (auto& q : rs) { if (q.first > nx) r->set.push_back({nx, q.first - 1}); nx = q.second + 1; }
+                    r->set.push_back({nx, 0x10FFFF});
+                }
+                continue;
+            }
+            int32_t a;
+            if (cur() == '\\') { i++; a = esc(); }
+            else { if (cur() < 0) fail(); a = p[i++]; }
+            int32_t b = a;
+            if (cur() == '-' && i + 1 < p.size() && p[i + 1] != ']') {
+                i++;
+                if (cur() == '\\') { i++; b = esc(); }
+                else { if (cur() < 0) fail(); b = p[i++]; }
+                if (b < a) fail();
+            }
+            r->set.push_back({a, b});
+        }
+        i++;
+        return r;
+    }
+    bool bounds(int* lo, int* hi) {  // at '{'
+        size_t j = i + 1;
+        auto num = [&](int* v) {
+            size_t s = j;
+            long x = 0;
+            while (j < p.size() && p[j] >= '0' && p[j] <= '9') { x = std::min(100000L, x * 10 + (p[j] - '0')); j++; }
+            if (j == s || (j - s > 1 && p[s] == '0')) return false;
+            *v = (int)x;
+            return true;
+        };
+        if (!num(lo)) return false;
+        *hi = *lo;
+        if (j < p.size() && p[j] == ',') {
+            j++;
+            if (j < p.size() && p[j] == '}') *hi = -1;
+            else if (!num(hi)) return false;
+        }
+        if (j >= p.size() || p[j] != '}') return false;
+        i = j + 1;
+        return true;
+    }
+    RP atom() {
+        int32_t c = cur();
+        if (c == -1) fail();  // invalid UTF-8 in the pattern
+        if (c == '(') {
+            i++;
+            if (cur() == '?') {
+                if (cur(1) == ':') i += 2;
+                else if (cur(1) == 'P' && cur(2) == '<') {
+                    i += 3;
+                    size_t s = i;
+                    while (i < p.size() && p[i] != '>') {
+                        if (!(alnum(p[i]) || p[i] == '_')) fail();
+                        i++;
+                    }
+                    if (at_end() || i == s) fail();
+                    i++;
+                } else unsup();
+            }
+            if (++nest > 1000) fail();
+            RP r = alt();
+            nest--;
+            if (cur() != ')') fail();
+            i++;
+            return r;
+        }
+        if (c == '^' || c == '$') fail();
+        if (c == '.') { i++; auto r = single(10, 10); r->neg = true; return r; }
+        if (c == '[') { i++; return klass(); }
+        if (c == '\\') {
+            int32_t e = cur(1);
+            if (e == 'A' || e == 'z' || e == 'b' || e == 'B') fail();
+            if (e == 'p' || e == 'P') unsup();
+            if (e == 'Q') {
+                i += 2;
+                auto seq = std::make_shared<Re>();
+                seq->k = Re::SEQ;
+                while (!at_end() && !(cur() == '\\' && cur(1) == 'E')) {
+                    if (cur() < 0) fail();
+                    seq->kids.push_back(single(p[i], p[i]));
+                    i++;
+                }
+                if (!at_end()) i += 2;
+                return seq;
+            }
+            std::vector<std::pair<int32_t, int32_t>> rs;
+            bool ng;
+            if (perl(e, &rs, &ng)) {
+                i += 2;
+                auto r = std::make_shared<Re>();
+                r->k = Re::SET;
+                r->set = rs;
+                r->neg = ng;
+                return r;
+            }
+            i++;
+            int32_t v = esc();
+            return single(v, v);
+        }
+        i++;
+        return single(c, c);
+    }
+    RP seq() {
+        auto s = std::make_shared<Re>();
+        s->k = Re::SEQ;
+        bool after_rep = false;
+        while (!at_end() && cur() != '|' && cur() != ')') {
+            int32_t c = cur();
+            int lo = -9, hi = -9;
+            if (c == '*') { lo = 0; hi = -1; i++; }
+            else if (c == '+') { lo = 1; hi = -1; i++; }
+            else if (c == '?') { lo = 0; hi = 1; i++; }
+            else if (c == '{' && bounds(&lo, &hi)) {
+                if (lo > 1000 || hi > 1000 || (hi >= 0 && hi < lo)) fail();
+            }
+            if (lo != -9) {
+                if (s->kids.empty() || after_rep) fail();
+                bool lazy = cur() == '?';
+                if (lazy) i++;
+                auto r = std::make_shared<Re>();
+                r->k = Re::REP;
+                r->lo = lo;
+                r->hi = hi;
+                r->kids = {s->kids.back()};
+                s->kids.back() = r;
+                after_rep = true;
+                if (lazy) fail();
+                continue;
+            }
+            after_rep = false;
+            s->kids.push_back(atom());
+        }
+        return s;
+    }
+    RP alt() {
+        auto o = std::make_shared<Re>();
+        o->k = Re::OR;
+        o->kids.push_back(seq());
+        while (cur() == '|') { i++; o->kids.push_back(seq()); }
+        return o;
+    }
+};
+
+// End positions of `r` matched from each position in `from` over runes `t`.
+inline std::set<size_t> step(const Re& r, const std::vector<int32_t>& t, const std::set<size_t>& from) {
+    std::set<size_t> out;
+    switch (r.k) {
+    case Re::SET:
+        for (size_t s : from)
+            if (s < t.size() && r.has(t[s])) out.insert(s + 1);
+        return out;
+    case Re::SEQ: {
+        std::set<size_t> cur = from;
+        for (auto& k : r.kids) cur = step(*k, t, cur);
+        return cur;
+    }
+    case Re::OR:
+        for (auto& k : r.kids) {
+            auto e = step(*k, t, from);
+            out.insert(e.begin(), e.end());
+        }
+        return out;
+    case Re::REP: {
+        std::set<size_t> cur = from;
+        for (int n = 0; n < r.lo; n++) cur = step(*r.kids[0], t, cur);
+        out = cur;
+        if (r.hi < 0) {  // closure
+            std::set<size_t> frontier = cur;
+            while (!frontier.empty()) {
+                auto e = step(*r.kids[0], t, frontier);
+                frontier.clear();
+                for (size_t x : e)
+                    if (out.insert(x).second) frontier.insert(x);
+            }
+        } else {
+            for (int n = r.lo; n < r.hi && !cur.empty(); n++) {
+                cur = step(*r.kids[0], t, cur);
+                out.insert(cur.begin(), cur.end());
+            }
+        }
+        return out;
+    }
+    }
+    return out;
+}
+
+struct Regexp {
+    RP root;
+    Status compile(const std::string& pattern) {
+        Parse ps;
+        ps.p = runes(pattern, false);
+        try {
+            root = ps.alt();
+            if (!ps.at_end()) ps.fail();
+        } catch (const Parse::Fail& f) {
+            root.reset();
+            return f.s;
+        }
+        return OK;
+    }
+    bool matches(const std::string& term) const {
+        if (!root) return false;
+        auto t = runes(term, false);
+        auto e = step(*root, t, {0});
+        return e.count(t.size()) > 0;
+    }
+};
+
+// Optimal-string-alignment distance over runes (full table, no cutoff).
+inline int osa(const std::string& a, const std::string& b) {
+    auto x = runes(a, true), y = runes(b, true);
+    const size_t n = x.size(), m = y.size();
+    std::vector<std::vector<int>> d(n + 1, std::vector<int>(m + 1));
+    for (size_t i = 0; i <= n; i++) d[i][0] = (int)i;
+    for (size_t j = 0; j <= m; j++) d[0][j] = (int)j;
+    for (size_t i = 1; i <= n; i++)
+        for (size_t j = 1; j <= m; j++) {
+            int v = std::min(d[i - 1][j] + 1, d[i][j - 1] + 1);
+            v = std::min(v, d[i - 1][j - 1] + (x[i - 1] == y[j - 1] ? 0 : 1));
+            if (i > 1 && j > 1 && x[i - 1] == y[j - 2] && x[i - 2] == y[j - 1]) v = std::min(v, d[i - 2][j - 2] + 1);
+            d[i][j] = v;
+        }
+    return d[n][m];
+}
+
+inline size_t rune_count(const std::string& s) { return runes(s, true).size(); }
+
+}  // namespace oracle_re

@@ -25,6 +25,7 @@
 
 #include "../include/nakama_mm.h"
 #include "go_compat.h"
+#include "go_regexp.h"
 
 #include <algorithm>
 #include <chrono>
@@ -50,7 +51,7 @@ namespace oracle {
 struct Query;
 using QP = std::shared_ptr<Query>;
 
-enum QKind { Q_BOOL, Q_TERM, Q_RANGE, Q_MATCHALL, Q_MATCHNONE, Q_PHRASE, Q_UNSUPPORTED };
+enum QKind { Q_BOOL, Q_TERM, Q_RANGE, Q_MATCHALL, Q_MATCHNONE, Q_PHRASE, Q_UNSUPPORTED, Q_REGEXP, Q_FUZZY };
 
 struct Query {
     QKind kind = Q_MATCHNONE;
@@ -65,6 +66,9 @@ struct Query {
     int64_t lo = 0, hi = 0;      // NumericRangeSearcher bounds after ±1 adjustment (search_numeric_range.go:26-52)
     double const_score = 1.0;    // ConstantScorer value of the range's term searchers
     bool is_date = false;        // DateRangeQuery: ConstantScorer(1) whatever the boost
+    // RegexpQuery / WildcardQuery (term = pattern) and FuzzyQuery (term, fuzziness)
+    std::shared_ptr<oracle_re::Regexp> re;
+    int fuzziness = 0;
 };
 
 static double boost_value(const Query& q) { return q.has_boost ? q.boost : 1.0; }
@@ -92,6 +96,24 @@ static EvalRes eval(const Query& q, const Doc& d) {
         auto it = d.find(q.field);
         if (it != d.end() && it->second.kind == 1 && it->second.kw == q.term) return {true, boost_value(q)};
         return {false, 0.0};
+    }
+    case Q_REGEXP: {  // multi-term disjunction of TermSearchers(boost), one term per keyword doc
+        auto it = d.find(q.field);
+        if (it != d.end() && it->second.kind == 1 && q.re->matches(it->second.kw)) return {true, boost_value(q)};
+        return {false, 0.0};
+    }
+    case Q_FUZZY: {   // FuzzySearcher: TermSearcher(boost * boostFromDistance) (search_fuzzy.go:99-126)
+        auto it = d.find(q.field);
+        if (it == d.end() || it->second.kind != 1) return {false, 0.0};
+        const string& t = it->second.kw;
+        int dist = oracle_re::osa(q.term, t);
+        if (dist > q.fuzziness) return {false, 0.0};
+        double tb = 1.0;
+        if (t != q.term) {
+            double ml = (double)std::min(oracle_re::rune_count(q.term), oracle_re::rune_count(t));
+            tb = 1.0 - ((double)dist / ml);
+        }
+        return {true, boost_value(q) * tb};
     }
     case Q_RANGE: {   // NumericRangeSearcher: disjoint prefix-coded terms, one hit per doc
         auto it = d.find(q.field);
@@ -380,7 +402,7 @@ struct Parser {
         if (t0 == T_PHRASE) { take(); auto q = std::make_shared<Query>(); q->kind = Q_PHRASE; return q; }
         if (t0 != T_STRING) throw ParseError{};
         string s1 = take().s;
-        if (peek() == T_TILDE) { take(); throw Unsupported{}; }   // fuzzy
+        if (peek() == T_TILDE) return fuzzy_token("", s1, take().s);
         if (peek() != T_COLON) {  // unfielded string -> _all
             return string_token("", s1);
         }
@@ -388,7 +410,7 @@ struct Parser {
         Tok t2 = peek();
         if (t2 == T_STRING) {
             string s3 = take().s;
-            if (peek() == T_TILDE) { take(); throw Unsupported{}; }  // fuzzy
+            if (peek() == T_TILDE) return fuzzy_token(s1, s3, take().s);
             return string_token(s1, s3);
         }
         if (t2 == T_NUMBER || t2 == T_MINUS) {
@@ -410,10 +432,49 @@ struct Parser {
         }
         throw ParseError{};
     }
-    QP string_token(const string& field, const string& s) {  // queryStringStringToken
-        if (s.size() >= 2 && s.front() == '/' && s.back() == '/') throw Unsupported{};  // regexp
-        if (s.find_first_of("*?") != string::npos) throw Unsupported{};               // wildcard
+    bool search_error = false;  // accepted by the parser, fails at search time
+    QP regexp(const string& field, const string& pattern) {
+        auto q = std::make_shared<Query>();
+        q->kind = Q_REGEXP;
+        q->field = field.empty() ? "_all" : field;
+        q->term = pattern;
+        q->re = std::make_shared<oracle_re::Regexp>();
+        oracle_re::Status st = q->re->compile(pattern);
+        if (st == oracle_re::UNSUPPORTED) throw Unsupported{};
+        if (st == oracle_re::SEARCH_ERROR) search_error = true;
+        return q;
+    }
+    QP string_token(const string& field, const string& s) {  // queryStringStringToken (query_string_parser.go:171-183)
+        if (s.size() >= 2 && s.front() == '/' && s.back() == '/') {
+            string re = s.substr(1, s.size() - 2);
+            if (re.rfind("^", 0) == 0) re = re.substr(1);  // strings.TrimPrefix(regexp, "^") (query.go:1264-1265)
+            return regexp(field, re);
+        }
+        if (s.find_first_of("*?") != string::npos) {     // WildcardQuery: wildcardRegexpReplacer (query.go:1455-1485)
+            string re;
+            for (char c : s) {
+                if (string("+()^$.{}[]|\\").find(c) != string::npos) { re += '\\'; re += c; }
+                else if (c == '*') re += ".*";
+                else if (c == '?') re += ".";
+                else re += c;
+            }
+            return regexp(field, re);
+        }
         return make_match(field, s);
+    }
+    // queryStringStringTokenFuzzy (query_string_parser.go:185-196): MatchQuery
+    // with fuzziness int(ParseFloat(fz)) -> Bool{should:[Fuzzy]} (query.go:966-975)
+    QP fuzzy_token(const string& field, const string& s, const string& fz) {
+        double v;
+        if (!gocompat::parse_float(fz, &v)) throw ParseError{};
+        long f;
+        if (std::isnan(v) || v >= 3.0 || v <= -1.0) { search_error = true; f = 3; }  // > MaxFuzziness or negative
+        else f = (long)v;
+        QP m = make_match(field, s);
+        if (f == 0) return m;
+        m->should[0]->kind = Q_FUZZY;
+        m->should[0]->fuzziness = (int)f;
+        return m;
     }
     QP parse() {
         top = std::make_shared<Query>();
@@ -428,7 +489,8 @@ struct Parser {
                 double b;
                 if (!gocompat::parse_float(take().s, &b)) throw ParseError{};
                 // queryStringSetBoost (query_string_parser.go:262-280)
-                if (q->kind == Q_BOOL && q->min_should == 1 && q->should.size() == 1 && q->should[0]->kind == Q_TERM &&
+                if (q->kind == Q_BOOL && q->min_should == 1 && q->should.size() == 1 &&
+                    (q->should[0]->kind == Q_TERM || q->should[0]->kind == Q_FUZZY) &&
                     q->must.empty() && q->mustnot.empty()) {
                     set_match_boost(q, b);               // MatchQuery
                 } else if (q->kind == Q_RANGE) {
@@ -468,6 +530,10 @@ static int parse_query(const string& query, QP* out) {
         Parser ps;
         ps.toks = lex(query);
         QP q = ps.parse();
+        if (ps.search_error) {  // every search fails: processDefault `continue`s (matchmaker_process.go:97-101)
+            q = std::make_shared<Query>();
+            q->kind = Q_MATCHNONE;
+        }
         *out = q;
         return 0;
     } catch (const Unsupported&) {
@@ -1309,6 +1375,36 @@ int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, dou
         n++;
     }
     return n;
+}
+
+int mm_debug_term_match(int32_t kind, const char* pattern, int32_t fuzziness, const char* term, double* boost) {
+    *boost = 0.0;
+    string t = term;
+    if (kind == 2) {
+        if (fuzziness < 0 || fuzziness > 2) return -1;
+        int d = oracle_re::osa(pattern, t);
+        if (d > fuzziness) return 0;
+        *boost = 1.0;
+        if (t != pattern)
+            *boost = 1.0 - (double)d / (double)std::min(oracle_re::rune_count(pattern), oracle_re::rune_count(t));
+        return 1;
+    }
+    string re = pattern;
+    if (kind == 3) {  // the query parser's wildcard lowering, via a one-clause query
+        re.clear();
+        for (char c : string(pattern)) {
+            if (string("+()^$.{}[]|\\").find(c) != string::npos) { re += '\\'; re += c; }
+            else if (c == '*') re += ".*";
+            else if (c == '?') re += ".";
+            else re += c;
+        }
+    }
+    oracle_re::Regexp rx;
+    oracle_re::Status st = rx.compile(re);
+    if (st != oracle_re::OK) return st == oracle_re::UNSUPPORTED ? -2 : -1;
+    if (!rx.matches(t)) return 0;
+    *boost = 1.0;
+    return 1;
 }
 
 int mm_debug_compile(const char* query) {

@@ -73,6 +73,36 @@ def run_scenario(lib, sc, T0, step):
     return results, errors, extract
 
 
+def search_case_hit(lib, case, T0):
+    """One single-document search of a `search_cases` fixture: the document is a
+    ticket with Query "*" (Min=Max=2) and the case's string properties; the query
+    runs as the search of a second ticket (no properties).  Returns whether the
+    document is among the hits and the hit list."""
+    mm = capi.Matchmaker(lib, max_intervals=5)
+    try:
+        mm.Add([capi.Presence("u1", "sid1", "u1", "n")], "sid1", "", "*", 2, 2, 1, case["doc"], {},
+               ticket="ticket1", created_at=T0)
+        mm.Add([capi.Presence("u2", "sid2", "u2", "n")], "sid2", "", case["query"], 2, 2, 1, {}, {},
+               ticket="searcher", created_at=T0 + 1024)
+        hits = mm.debug_hits("searcher")
+    finally:
+        mm.close()
+    return "ticket1" in [h for h, _ in hits], hits
+
+
+def term_match(lib, kind, pattern, fuzziness, term):
+    """mm_debug_term_match -> [matched, boost] or "search_error" / "unsupported"."""
+    import ctypes
+    b = ctypes.c_double(0.0)
+    rc = lib.mm_debug_term_match(kind, pattern.encode("utf-8", "surrogateescape"), fuzziness,
+                                 term.encode("utf-8", "surrogateescape"), ctypes.byref(b))
+    if rc == -1:
+        return "search_error"
+    if rc == -2:
+        return "unsupported"
+    return [rc, b.value if rc == 1 else 0]
+
+
 def matched_sessions(groups, sc):
     """Session ids of matched entries (the test's matchesSeen keys)."""
     sess = {}

@@ -54,7 +54,8 @@ def _fuzz_corpus(n=3000, seed=7):
     rnd = random.Random(seed)
     atoms = ["properties.a", "properties.skill", "min_count", "party_id", "a", "5", "-", "+", ":", ">", "<", "=", ">=",
              "<=", "^2", "^", "^0.5", "^x", "~", "~2", "\"x y\"", "\"2021-01-01T00:00:00Z\"", "\\:", "\\ ", "\\x",
-             "10", "-3.5", "1.2.3", "foo", "bar*", "/re/", " ", "  ", "\t", "é", "\xff"]
+             "10", "-3.5", "1.2.3", "foo", "bar*", "/re/", " ", "  ", "\t", "é", "\xff", "/(/", "/a|b/", "/[a-/",
+             "/\\pL/", "/(?i)a/", "/x{2}/", "~1.5", "~-1", "~3", "ba?r", "/\\w+/", "/a$/"]
     out = []
     for _ in range(n):
         k = rnd.randint(1, 7)
@@ -104,3 +105,69 @@ def test_product_fails_loudly_without_device():
         pytest.skip("GPU present")
     with pytest.raises(capi.ErrDevice):
         nakama_amd.LocalMatchmaker()
+
+
+def test_term_cases_product(product):
+    """The product's matchers reproduce the fixture term cases (CPU only)."""
+    for kind, pattern, fz, term, want in harness.load_known_answer()["term_cases"]:
+        got = harness.term_match(product, kind, pattern, fz, term)
+        if isinstance(want, list):
+            assert got[0] == want[0] and got[1] == want[1] or abs(got[1] - want[1]) <= 1e-15, (pattern, term, got)
+        else:
+            assert got == want, (pattern, term, got)
+
+
+def _rand_regex(rnd, depth=0):
+    atoms = ["a", "b", "c", ".", "[ab]", "[^a]", "[a-c]", "\\d", "\\w", "\\s", "\\.", "x", "é", "-", "_", "{", "}"]
+    parts = []
+    for _ in range(rnd.randint(0, 4)):
+        r = rnd.random()
+        if r < 0.15 and depth < 3:
+            a = "(" + _rand_regex(rnd, depth + 1) + ")"
+        elif r < 0.2 and depth < 3:
+            a = "(?:" + _rand_regex(rnd, depth + 1) + "|" + _rand_regex(rnd, depth + 1) + ")"
+        else:
+            a = rnd.choice(atoms)
+        q = rnd.random()
+        if q < 0.15: a += "*"
+        elif q < 0.25: a += "+"
+        elif q < 0.32: a += "?"
+        elif q < 0.38: a += rnd.choice(["{2}", "{1,2}", "{0,}", "{3,1}", "{,2}", "*?", "**"])
+        parts.append(a)
+    s = "".join(parts)
+    if rnd.random() < 0.1:
+        s += rnd.choice(["|", "(", ")", "[", "\\", "$", "^"])
+    return s
+
+
+def test_regexp_differential_vs_oracle(product):
+    """Product Pike VM vs the oracle's end-position-set matcher on random
+    patterns and terms: same parse status, same acceptance."""
+    rnd = random.Random(5)
+    orc = harness.oracle_lib()
+    alphabet = ["a", "b", "c", "x", ".", "1", "_", " ", "\n", "é", "-"]
+    bad = []
+    for _ in range(1500):
+        pat = _rand_regex(rnd)
+        for _ in range(6):
+            term = "".join(rnd.choice(alphabet) for _ in range(rnd.randint(0, 6)))
+            a = harness.term_match(product, 1, pat, 0, term)
+            o = harness.term_match(orc, 1, pat, 0, term)
+            if a != o:
+                bad.append((pat, term, a, o))
+    assert not bad, bad[:10]
+
+
+def test_fuzzy_differential_vs_oracle(product):
+    rnd = random.Random(9)
+    orc = harness.oracle_lib()
+    alphabet = ["a", "b", "c", "é"]
+    bad = []
+    for _ in range(3000):
+        p = "".join(rnd.choice(alphabet) for _ in range(rnd.randint(1, 6)))
+        t = "".join(rnd.choice(alphabet) for _ in range(rnd.randint(0, 7)))
+        fz = rnd.randint(1, 2)
+        a, o = harness.term_match(product, 2, p, fz, t), harness.term_match(orc, 2, p, fz, t)
+        if a != o:
+            bad.append((p, t, fz, a, o))
+    assert not bad, bad[:10]

@@ -310,3 +310,62 @@ def test_parallel_host_paths_equal_serial(config, n, monkeypatch):
     assert gen == ser
     exact = _product_passes(config, n, 2, "1", monkeypatch, fast="0")
     assert exact == ser
+
+
+# ---- regexp / wildcard / fuzzy clauses (OP_TERMSET) ----
+
+@pytest.mark.parametrize("case", KA["search_cases"], ids=[c["name"] for c in KA["search_cases"]])
+def test_regexp_search_cases_gpu(case):
+    """TestMatchmakerPropertyRegexSubmatch{,Multiple} through the device search."""
+    hit, hits = harness.search_case_hit(product_lib(), case, KA["T0"])
+    assert hit == case["hit"], (case["name"], hits)
+    assert hits == harness.search_case_hit(harness.oracle_lib(), case, KA["T0"])[1]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_multi_term_passes(kernel, monkeypatch):
+    """Config 7: blocked-list regexps, alternations, wildcards, fuzzy (variable
+    scores), a pattern that fails every search; every query-eval kernel."""
+    monkeypatch.setenv("NKM_KERNEL", kernel)
+    run_passes(7, 1200, 3, dict(max_intervals=3))
+
+
+def test_multi_term_rev_precision():
+    run_passes(7, 600, 2, dict(max_intervals=2, rev_precision=True))
+
+
+def test_multi_term_hit_lists():
+    ts = synth.TicketSet(7, 600)
+    gpu, orc = pair(dict(max_intervals=2))
+    try:
+        ts.insert_into(gpu)
+        ts.insert_into(orc)
+        for k in range(0, 600, 7):
+            t = ts.ticket_id(k)
+            hg, ho = gpu.debug_hits(t), orc.debug_hits(t)
+            assert [h for h, _ in hg] == [h for h, _ in ho]
+            for (_, a), (_, b) in zip(hg, ho):
+                assert math.isclose(a, b, rel_tol=1e-6)
+    finally:
+        gpu.close()
+        orc.close()
+        ts.close()
+
+
+def test_multi_term_sets_grow_between_passes():
+    """Terms interned after a pattern was first evaluated join its set."""
+    gpu, orc = pair(dict(max_intervals=3))
+    sets = []
+    try:
+        for rnd in range(3):
+            ts = synth.TicketSet(7, 250, first=rnd * 250)
+            sets.append(ts)
+            ts.insert_into(gpu)
+            ts.insert_into(orc)
+            assert gpu.Process() == orc.Process()
+            assert state(gpu) == state(orc)
+    finally:
+        gpu.close()
+        orc.close()
+        for s in sets:
+            s.close()

@@ -77,3 +77,21 @@ def test_query_language(q, status):
         assert got == status
     finally:
         mm.close()
+
+
+@pytest.mark.parametrize("case", KA["search_cases"], ids=[c["name"] for c in KA["search_cases"]])
+def test_regexp_search_cases(case):
+    """TestMatchmakerPropertyRegexSubmatch{,Multiple} (server/matchmaker_test.go:162-378)."""
+    hit, hits = harness.search_case_hit(harness.oracle_lib(), case, KA["T0"])
+    assert hit == case["hit"], (case["name"], hits)
+
+
+@pytest.mark.parametrize("case", KA["term_cases"], ids=[f"{c[0]}:{c[1]!r}~{c[2]}:{c[3]!r}" for c in KA["term_cases"]])
+def test_term_cases(case):
+    """Regexp / wildcard / fuzzy term acceptance and per-term boosts (derived cases)."""
+    kind, pattern, fz, term, want = case
+    got = harness.term_match(harness.oracle_lib(), kind, pattern, fz, term)
+    if isinstance(want, list):
+        assert got[0] == want[0] and got[1] == pytest.approx(want[1], rel=1e-15), got
+    else:
+        assert got == want

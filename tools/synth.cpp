@@ -82,7 +82,7 @@ int synth_pool_of(int config, uint64_t seed, uint64_t i) {
 
 void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0, uint64_t pool_mask, int shard);
 
-// config: 1..5 as BASELINE.json configs[0..4], 6 = mixed.  Generates tickets [first, first+n).
+// config: 1..5 as BASELINE.json configs[0..4], 6 = mixed, 7 = regexp/wildcard/fuzzy.  Generates tickets [first, first+n).
 void* synth_make(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0) {
     return synth_make_impl(config, seed, first, n, t0, ~0ull, -1);
 }
@@ -194,6 +194,39 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             query = q;
             t.min_count = 2;
             t.max_count = 4;
+            break;
+        }
+        case 7: {  // multi-term clauses: regexp / wildcard / fuzzy (blocked-list pattern of
+                   // TestMatchmakerPropertyRegexSubmatch, server/matchmaker_test.go:162-286)
+            static const char* kMaps[8] = {"map1", "map2", "map3", "map4", "map5", "map6", "some_map", "other_map"};
+            party = r.uni() < 0.8 ? 1 : 2;
+            const char* mode = kModes[r.next() & 1];
+            const char* map = kMaps[r.next() & 7];
+            char id[24], tag[24], blocked[64];
+            std::snprintf(id, sizeof id, "u%llu", (unsigned long long)(i % 200));
+            std::snprintf(tag, sizeof tag, "p%d", (int)(r.next() % 40));
+            std::snprintf(blocked, sizeof blocked, "u%d u%d", (int)(r.next() % 200), (int)(r.next() % 200));
+            S->sp.push_back({"mode", mode});
+            S->sp.push_back({"map", map});
+            S->sp.push_back({"id", S->keep(id)});
+            S->sp.push_back({"tag", S->keep(tag)});
+            S->sp.push_back({"blocked", S->keep(blocked)});
+            char q[200];
+            switch ((int)(r.next() % 8)) {
+            case 0: std::snprintf(q, sizeof q, "+properties.mode:%s -properties.blocked:/.*%s([^0-9].*)?/", mode, id); break;
+            case 1: std::snprintf(q, sizeof q, "+properties.mode:%s +properties.map:/(map[1-3]|some_map)/", mode); break;
+            case 2: std::snprintf(q, sizeof q, "+properties.mode:%s properties.map:ma*1^2", mode); break;
+            case 3: std::snprintf(q, sizeof q, "+properties.mode:%s properties.map:mapp2~1", mode); break;
+            case 4: std::snprintf(q, sizeof q, "+properties.map:map~2 -properties.tag:/p[0-9]/"); break;
+            case 5: std::snprintf(q, sizeof q, "+properties.mode:%s +properties.tag:p?", mode); break;
+            case 6: std::snprintf(q, sizeof q, "+properties.mode:%s -properties.map:/(/", mode); break;
+            default:
+                std::snprintf(q, sizeof q, "+properties.mode:%s properties.map:/\\w+_map/^4 properties.tag:p1*", mode);
+            }
+            query = q;
+            const int shape = (int)(r.next() % 2);
+            t.min_count = 2;
+            t.max_count = shape == 0 ? 2 : 4;
             break;
         }
         default: {  // 6: small mixed workload for parity (parties, ranges, boosts, Min<Max)
