@@ -213,7 +213,7 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             S->sp.push_back({"blocked", S->keep(blocked)});
             char q[200];
             switch ((int)(r.next() % 8)) {
-            case 0: std::snprintf(q, sizeof q, "+properties.mode:%s -properties.blocked:/.*%s([^0-9].*)?/", mode, id); break;
+            case 0: std::snprintf(q, sizeof q, "+properties.mode:%s -properties.blocked:/.*%s([\\^0-9].*)?/", mode, id); break;
             case 1: std::snprintf(q, sizeof q, "+properties.mode:%s +properties.map:/(map[1-3]|some_map)/", mode); break;
             case 2: std::snprintf(q, sizeof q, "+properties.mode:%s properties.map:ma*1^2", mode); break;
             case 3: std::snprintf(q, sizeof q, "+properties.mode:%s properties.map:mapp2~1", mode); break;
