@@ -39,7 +39,8 @@ WORKLOADS = {
     2: "C2: skill-window range queries with ^boost, 1v1",
     3: "C3: 1M tickets/GPU, 5v5 (Min=Max=10, CountMultiple=5), party tickets, 8 pools",
     4: "C4: solo 1v1 over 64 mode x region pools",
-    5: "C5: RevPrecision, buckets of 8, Min=2 Max=4",
+    5: "C5: RevPrecision, buckets of 8, Min=2 Max=4 (processDefault; no override registered)",
+    7: "C7: regexp / wildcard / fuzzy clauses (blocked lists, alternations, fuzzy map names)",
 }
 
 
@@ -147,7 +148,7 @@ def main():
     import nakama_amd
     from nakama_amd import synth
 
-    mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local)
+    mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config == 5)
     # Pool sharding (weak scaling): the N-GPU workload is N disjoint instances
     # of the config's pool set (region values suffixed per instance, so C3's
     # 8 pools become 8N), and GPU r owns instance r whole — every GPU runs
