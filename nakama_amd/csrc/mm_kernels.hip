@@ -28,7 +28,7 @@ namespace nkm {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kVarK = 512;  // LDS capacity of a variable-score top-K list
+constexpr int kVarK = 512;  // LDS capacity of a variable-score top-K list (search_kernel<kVarK>)
 
 __device__ __forceinline__ int64_t dsortable(double f) {
     int64_t i = __double_as_longlong(f);
@@ -116,22 +116,30 @@ __device__ __forceinline__ Cand eval_candidate(const DStore& st, const DGroup& g
     return c;
 }
 
+// VK = 0: the instantiation for constant-score searches (no top-K list in
+// LDS); VK = kVarK: variable-score searches.  Both are launched over the same
+// group array and each returns at once on the other kind's groups, so the
+// constant-score searches keep a small LDS footprint (full occupancy).
+template <int VK>
 __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup* __restrict__ groups,
                                                         DHit* __restrict__ out, uint8_t* __restrict__ out_rev,
                                                         DGroupResult* __restrict__ res) {
+    constexpr int LV = VK > 0 ? VK : 1;
     __shared__ uint32_t wave_cnt[kWaves];
     __shared__ int64_t wave_max[kWaves];
     // variable-score list (double-buffered) + tile staging
-    __shared__ int64_t lkey[2][kVarK];
-    __shared__ uint32_t lidx[2][kVarK];
-    __shared__ uint32_t lslot[2][kVarK];
-    __shared__ uint8_t lrev[2][kVarK];
+    __shared__ int64_t lkey[2][LV];
+    __shared__ uint32_t lidx[2][LV];
+    __shared__ uint32_t lslot[2][LV];
+    __shared__ uint8_t lrev[2][LV];
     __shared__ int64_t tkey[kBlock];
+    __shared__ int64_t tsk[kBlock];  // the tile's keys in rank order (descending)
     __shared__ uint32_t tidx[kBlock];
     __shared__ uint32_t tslot[kBlock];
     __shared__ uint8_t trev[kBlock];
 
     const DGroup g = groups[blockIdx.x];
+    if ((g.var_score != 0) != (VK > 0)) return;  // the other instantiation's search (block-uniform)
     const uint32_t* src = g.src_kind == 0 ? st.order : st.postings;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -179,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     }
 
     // ---- variable-score top-K ------------------------------------------------------
-    const uint32_t KK = K < (uint32_t)kVarK ? K : (uint32_t)kVarK;
+    const uint32_t KK = K < (uint32_t)VK ? K : (uint32_t)VK;
     uint32_t n = 0, total = 0;
     int cur = 0;
     bool early = false;
@@ -214,17 +222,26 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
                 const uint32_t mid = (lo + hi) >> 1;
                 if (lkey[cur][mid] >= k) lo = mid + 1; else hi = mid;
             }
-            uint32_t r = lo;
+            // rank within the tile (ties: earlier source position first)
+            uint32_t rt = 0;
             for (uint32_t t = 0; t < cnt; t++) {
                 const int64_t kt = tkey[t];
-                r += (kt > k) || (kt == k && t < (uint32_t)tid);
+                rt += (kt > k) || (kt == k && t < (uint32_t)tid);
             }
+            tsk[rt] = k;
+            const uint32_t r = lo + rt;
             if (r < KK) { lkey[nxt][r] = k; lidx[nxt][r] = tidx[tid]; lslot[nxt][r] = tslot[tid]; lrev[nxt][r] = trev[tid]; }
         }
+        __syncthreads();
         for (uint32_t i = tid; i < n; i += kBlock) {
             const int64_t k = lkey[cur][i];
-            uint32_t r = i;
-            for (uint32_t t = 0; t < cnt; t++) r += tkey[t] > k;
+            // tile keys strictly above k: binary search of the rank-ordered tile
+            uint32_t lo = 0, hi = cnt;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (tsk[mid] > k) lo = mid + 1; else hi = mid;
+            }
+            const uint32_t r = i + lo;
             if (r < KK) { lkey[nxt][r] = k; lidx[nxt][r] = lidx[cur][i]; lslot[nxt][r] = lslot[cur][i]; lrev[nxt][r] = lrev[cur][i]; }
         }
         n = (n + cnt < KK) ? n + cnt : KK;
@@ -689,10 +706,16 @@ hipError_t launch_pairmat(const DStore& st, const DGroup* d_groups, const DGroup
 // events take the dispatch's own timestamps (what rocprofv3 reports as the
 // kernel's duration), not the host-side enqueue around it.
 hipError_t launch_search(const DStore& st, const DGroup* d_groups, int n_groups, DHit* d_out, uint8_t* d_rev,
-                         DGroupResult* d_res, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
-    if (n_groups <= 0) return hipSuccess;
-    hipExtLaunchKernelGGL(search_kernel, dim3(n_groups), dim3(kBlock), 0, stream, ev0, ev1, 0, st, d_groups, d_out, d_rev,
-                          d_res);
+                         DGroupResult* d_res, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1, int kinds) {
+    if (n_groups <= 0 || !(kinds & 3)) return hipSuccess;
+    // bit 0: some search is constant-score, bit 1: some is variable-score; the
+    // event pair spans both dispatches
+    if (kinds & 1)
+        hipExtLaunchKernelGGL(search_kernel<0>, dim3(n_groups), dim3(kBlock), 0, stream, ev0, (kinds & 2) ? nullptr : ev1,
+                              0, st, d_groups, d_out, d_rev, d_res);
+    if (kinds & 2)
+        hipExtLaunchKernelGGL(search_kernel<kVarK>, dim3(n_groups), dim3(kBlock), 0, stream, (kinds & 1) ? nullptr : ev0,
+                              ev1, 0, st, d_groups, d_out, d_rev, d_res);
     return hipGetLastError();
 }
 

@@ -98,7 +98,7 @@ struct Replay : ReplayCore {
         c.d_res_.reserve(1, false);
         NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, sizeof(DGroup), hipMemcpyHostToDevice, stream));
         NKM_HIP(launch_search(st, c.d_groups_.p, 1, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream,
-                              c.ev_[0], c.ev_[1]));
+                              c.ev_[0], c.ev_[1], d.var_score ? 2 : 1));
         c.h_res_.reserve(1);
         NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
         NKM_HIP(hipStreamSynchronize(stream));
@@ -342,8 +342,10 @@ struct Replay : ReplayCore {
         }
         NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, ng * sizeof(DGroup), hipMemcpyHostToDevice, stream));
         // per eval kernel, the start/stop events of its dispatch (per-kernel roofline in bench.py)
+        int kinds = 0;
+        for (size_t i = 0; i < nwhole; i++) kinds |= c.h_groups_.p[i].var_score ? 2 : 1;
         NKM_HIP(launch_search(st, c.d_groups_.p, nwhole, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream,
-                              c.ev_[0], c.ev_[1]));
+                              c.ev_[0], c.ev_[1], kinds));
         NKM_HIP(launch_scan(st, c.d_groups_.p + nwhole, nchunks, c.d_scan_.p, c.d_res_.p + nwhole, stream, c.ev_[2],
                             c.ev_[3]));
         if (use_m)
@@ -797,7 +799,7 @@ int Core::process_default(GroupList& out_groups,
         // a search's hit capacity after `nrows` rows, the last with MaxCount m
         auto cap_k = [&](const BGroup& g, uint64_t nrows, int m) {
             const uint64_t want = nrows * (uint64_t)std::max(2, m) * 2 + 32;
-            const uint32_t k = g.d.var_score ? (uint32_t)std::min<uint64_t>(kvar, want)
+            const uint32_t k = g.d.var_score ? (uint32_t)std::min<uint64_t>(std::min<uint32_t>(kvar, std::max<uint32_t>(g.d.src_len, 1)), want)
                                              : (uint32_t)std::min<uint64_t>(std::max<uint32_t>(g.d.src_len, 1), want + 224);
             return std::max<uint32_t>(k, 1);
         };
@@ -1001,7 +1003,8 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
             g.d.rev_slot = rev ? r : kNoSlot;
             g.d.ub_key = s.ub_key;
             choose_source(s, g.d);
-            g.d.k = g.d.var_score ? kvar : std::min<uint32_t>(std::max<uint32_t>(g.d.src_len, 1), 128);
+            g.d.k = g.d.var_score ? std::min<uint32_t>(kvar, std::max<uint32_t>(g.d.src_len, 1))
+                                   : std::min<uint32_t>(std::max<uint32_t>(g.d.src_len, 1), 128);
             g.d.out_off = off;
             off += g.d.k;
             g.row_slot = r;
