@@ -477,6 +477,7 @@ public:
 
     // ---- index (scan order + postings), host mirror ----
     std::vector<uint32_t> order_;
+    bool page_mode_ = true;  // NKM_PAGE=0: only a batch's first row pages a truncated list
     bool order_sorted_ = true;
     bool index_dirty_ = true;
     uint32_t order_head_ = 0;

@@ -932,7 +932,15 @@ int Core::process_default(GroupList& out_groups,
         for (size_t bi = 0; bi < brow.size(); bi++) {
             const uint32_t T = brow[bi];
             if (sel[T]) { done = bi + 1; continue; }
-            auto status = rp.decide(T, bg[brow_group[bi]], bi == 0, grp);
+            // a row past the end of its truncated list pages it with a cursor (the
+            // batch's first row, and with page_mode_ any row of a constant-score
+            // search, whose page holds >= 4096 hits; variable-score rows instead
+            // end the batch and the searches re-run, since their 512-entry pages
+            // would be fetched one synchronous launch at a time).  A page may
+            // hold tickets selected earlier in this batch, which the walk skips,
+            // so the list stays exact.
+            BGroup& bgr = bg[brow_group[bi]];
+            auto status = rp.decide(T, bgr, bi == 0 || (page_mode_ && !bgr.d.var_score), grp);
             if (status == Replay::EXHAUSTED) {
                 exhausted = true;
                 retry_slot = T;

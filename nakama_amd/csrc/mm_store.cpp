@@ -87,6 +87,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     for (auto& e : ev_) NKM_HIP(hipEventCreate(&e));
     if (const char* e = std::getenv("NKM_DENSE")) dense_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FAST")) fast_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_PAGE")) page_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_KERNEL"))
         kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN
                      : !std::strcmp(e, "mscan") ? KM_MSCAN : KM_AUTO;

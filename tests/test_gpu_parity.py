@@ -175,7 +175,9 @@ def test_mixed_parties_ranges_minmax(par, dense, kernel, monkeypatch):
     run_passes(6, 1000, 3, dict(max_intervals=3))
 
 
-def test_mixed_rev_precision():
+@pytest.mark.parametrize("page", ["1", "0"])
+def test_mixed_rev_precision(page, monkeypatch):
+    monkeypatch.setenv("NKM_PAGE", page)
     run_passes(6, 600, 3, dict(max_intervals=3, rev_precision=True))
 
 
@@ -322,11 +324,13 @@ def test_regexp_search_cases_gpu(case):
     assert hits == harness.search_case_hit(harness.oracle_lib(), case, KA["T0"])[1]
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
-def test_multi_term_passes(kernel, monkeypatch):
+@pytest.mark.parametrize("kernel,page", [("search", "1"), ("scan", "1"), ("mscan", "1"), ("search", "0")])
+def test_multi_term_passes(kernel, page, monkeypatch):
     """Config 7: blocked-list regexps, alternations, wildcards, fuzzy (variable
-    scores), a pattern that fails every search; every query-eval kernel."""
+    scores), a pattern that fails every search; every query-eval kernel;
+    truncated lists paged by any row (NKM_PAGE=1) or by batch restarts."""
     monkeypatch.setenv("NKM_KERNEL", kernel)
+    monkeypatch.setenv("NKM_PAGE", page)
     run_passes(7, 1200, 3, dict(max_intervals=3))
 
 
