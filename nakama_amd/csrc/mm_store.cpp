@@ -15,6 +15,9 @@
 #include "gocompat.h"
 #include "mm_core.h"
 
+#include <chrono>
+#include <cstdio>
+
 namespace nkm {
 
 template <class T>
@@ -612,15 +615,36 @@ int Core::add(const mm_ticket& t) {
 // Insert (matchmaker.go:567-682): queries that fail to parse are skipped.
 int Core::insert(const mm_ticket* ts, int32_t n) {
     if (stopped_ || n <= 0) return MM_OK;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     std::vector<CompiledQuery> cqs((size_t)n);
     std::vector<uint8_t> ok((size_t)n, 0);
-    for (int i = 0; i < n; i++) ok[i] = compile_query(ts[i].query ? ts[i].query : "", &cqs[i]) == CQ_OK;
-    std::lock_guard<std::mutex> lk(mu_);
+    std::lock_guard<std::mutex> lk(mu_);  // also serialises use of the worker pool
     if (custom_open_) return MM_ERR_STATE;
+    // query compiles are independent: spread large batches over the host workers
+    auto compile_range = [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; i++) ok[i] = compile_query(ts[i].query ? ts[i].query : "", &cqs[i]) == CQ_OK;
+    };
+    static const bool par_compile = !std::getenv("NKM_PAR_COMPILE") || std::strcmp(std::getenv("NKM_PAR_COMPILE"), "0") != 0;
+    if (par_compile && par_mode_ && (size_t)n >= par_min(16384)) {
+        WorkPool& wp = workers();
+        const size_t nch = (size_t)wp.size() * 4;
+        wp.run(nch, [&](size_t c) { compile_range((size_t)n * c / nch, (size_t)n * (c + 1) / nch); });
+    } else {
+        compile_range(0, (size_t)n);
+    }
+    const auto t1 = clk::now();
     maybe_compact();
+    const auto t2 = clk::now();
     for (int i = 0; i < n; i++)
         if (ok[i]) add_locked(ts[i], cqs[i], true);
+    const auto t3 = clk::now();
     if (n >= 1024) sync_device();  // index the batch now (bluge indexes synchronously too)
+    if (std::getenv("NKM_PROFILE") && n >= 1024) {
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "[nkm] insert %d: compile %.1f ms | compact %.1f ms | add %.1f ms | sync/index/upload %.1f ms\n", n,
+                     ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, clk::now()));
+    }
     return MM_OK;
 }
 
