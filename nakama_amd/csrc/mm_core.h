@@ -477,6 +477,7 @@ public:
 
     // ---- index (scan order + postings), host mirror ----
     std::vector<uint32_t> order_;
+    bool full_var_mode_ = true;  // NKM_FULLVAR=0: variable-score searches always use the LDS top-K
     bool page_mode_ = true;  // NKM_PAGE=0: only a batch's first row pages a truncated list
     bool order_sorted_ = true;
     bool index_dirty_ = true;
@@ -526,6 +527,8 @@ public:
     DevArray<DMSig> d_msig_;         // mscan_kernel's signatures
     PinnedArray<DMSig> h_msig_;
     DevArray<uint8_t> d_rev_;
+    PinnedArray<DHit> h_page_;       // fetch_more's page (pinned: one round trip)
+    PinnedArray<uint8_t> h_page_rev_;
     DevArray<DGroupResult> d_res_;
     DevArray<uint32_t> d_slots_tmp_;
     DevArray<uint8_t> d_pair_out_;

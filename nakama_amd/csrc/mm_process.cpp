@@ -59,6 +59,7 @@ static void filter_slots(WorkPool* wp, const std::vector<uint32_t>& in, std::vec
     });
 }
 constexpr uint64_t kOutCap = 1ull << 24;  // max hit entries per batch (16M x 16 B)
+constexpr uint32_t kFullVarMax = 16384;   // max source of a full-list variable-score search
 
 struct Replay : ReplayCore {
     Core& c;
@@ -101,6 +102,13 @@ struct Replay : ReplayCore {
                               c.ev_[0], c.ev_[1], d.var_score ? 2 : 1));
         c.h_res_.reserve(1);
         NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
+        // the whole page capacity comes back in the same round trip (pinned)
+        c.h_page_.reserve(d.k);
+        NKM_HIP(hipMemcpyAsync(c.h_page_.p, c.d_out_.p, (size_t)d.k * sizeof(DHit), hipMemcpyDeviceToHost, stream));
+        if (rev) {
+            c.h_page_rev_.reserve(d.k);
+            NKM_HIP(hipMemcpyAsync(c.h_page_rev_.p, c.d_rev_.p, d.k, hipMemcpyDeviceToHost, stream));
+        }
         NKM_HIP(hipStreamSynchronize(stream));
         float ms = 0.f;
         NKM_HIP(hipEventElapsedTime(&ms, c.ev_[0], c.ev_[1]));
@@ -109,14 +117,8 @@ struct Replay : ReplayCore {
         stats.pair_evals += r.scanned;
         stats.k_bytes[0] += search_bytes(c.sigs_[g.sig], d, r);
         stats.k_launches[0]++;
-        std::vector<DHit> page(r.count);
-        std::vector<uint8_t> prev(r.count);
-        if (r.count) {
-            NKM_HIP(hipMemcpy(page.data(), c.d_out_.p, r.count * sizeof(DHit), hipMemcpyDeviceToHost));
-            if (rev) NKM_HIP(hipMemcpy(prev.data(), c.d_rev_.p, r.count, hipMemcpyDeviceToHost));
-        }
-        g.ext.insert(g.ext.end(), page.begin(), page.end());
-        if (rev) g.ext_rev.insert(g.ext_rev.end(), prev.begin(), prev.end());
+        g.ext.insert(g.ext.end(), c.h_page_.p, c.h_page_.p + r.count);
+        if (rev) g.ext_rev.insert(g.ext_rev.end(), c.h_page_rev_.p, c.h_page_rev_.p + r.count);
         g.hits = g.ext.data();
         g.rev = rev ? g.ext_rev.data() : nullptr;
         g.n = (uint32_t)g.ext.size();
@@ -256,6 +258,7 @@ struct Replay : ReplayCore {
         }
         uint64_t off = 0;
         std::vector<uint32_t> chunked;
+        std::vector<uint32_t> full_var;
         for (uint32_t i = 0; i < bg.size(); i++) {
             if (on_m[i]) continue;
             const DGroup& d = bg[i].d;
@@ -266,6 +269,17 @@ struct Replay : ReplayCore {
                 continue;
             }
             DGroup w = d;
+            // A variable-score search whose rows need more than the LDS top-K
+            // (k was capped at kVarK) over a small source runs as a full list:
+            // the constant-score path emits every hit with its own score key
+            // in source order, and the host sorts it stably by key (source
+            // order breaks ties, as the top-K does), so the list is complete.
+            if (d.var_score && !rev && !d.has_cursor && d.k >= (uint32_t)var_k_capacity() && d.src_len > d.k &&
+                d.src_len <= kFullVarMax && c.full_var_mode_) {
+                w.var_score = 0;
+                w.k = d.src_len;
+                full_var.push_back((uint32_t)lg.size());
+            }
             w.out_off = off;
             off += w.k;
             lg.push_back(w);
@@ -411,6 +425,10 @@ struct Replay : ReplayCore {
                 stats.pair_evals += (int64_t)mr[t].scanned * ms.n_sigs;
             }
             stats.k_bytes[2] += (int64_t)(ms.n_sigs * sizeof(DMSig) + mcl.size() * sizeof(DClause));
+        }
+        for (uint32_t i : full_var) {
+            DHit* h = c.h_out_.p + lg[i].out_off;
+            std::stable_sort(h, h + c.h_res_.p[i].count, [](const DHit& a, const DHit& b) { return a.key > b.key; });
         }
         for (int i = 0; i < nwhole; i++) {
             BGroup& g = bg[lg_group[i]];

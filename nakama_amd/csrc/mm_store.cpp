@@ -90,6 +90,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     for (auto& e : ev_) NKM_HIP(hipEventCreate(&e));
     if (const char* e = std::getenv("NKM_DENSE")) dense_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FAST")) fast_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_FULLVAR")) full_var_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_PAGE")) page_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_KERNEL"))
         kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN
@@ -625,7 +626,10 @@ int Core::insert(const mm_ticket* ts, int32_t n) {
     auto compile_range = [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; i++) ok[i] = compile_query(ts[i].query ? ts[i].query : "", &cqs[i]) == CQ_OK;
     };
-    static const bool par_compile = !std::getenv("NKM_PAR_COMPILE") || std::strcmp(std::getenv("NKM_PAR_COMPILE"), "0") != 0;
+    // opt-in (NKM_PAR_COMPILE=1): 10x faster compiles, but the pass's row
+    // bucketing on the same workers then ran 2.2 ms instead of 0.85 ms
+    // (profiles/r01_ab_par_compile.txt), and the pass is the headline
+    static const bool par_compile = std::getenv("NKM_PAR_COMPILE") && std::strcmp(std::getenv("NKM_PAR_COMPILE"), "0") != 0;
     if (par_compile && par_mode_ && (size_t)n >= par_min(16384)) {
         WorkPool& wp = workers();
         const size_t nch = (size_t)wp.size() * 4;

@@ -324,13 +324,15 @@ def test_regexp_search_cases_gpu(case):
     assert hits == harness.search_case_hit(harness.oracle_lib(), case, KA["T0"])[1]
 
 
-@pytest.mark.parametrize("kernel,page", [("search", "1"), ("scan", "1"), ("mscan", "1"), ("search", "0")])
-def test_multi_term_passes(kernel, page, monkeypatch):
+@pytest.mark.parametrize("kernel,page,fullvar", [("search", "1", "1"), ("scan", "1", "1"), ("mscan", "1", "1"),
+                                                 ("search", "0", "1"), ("search", "1", "0")])
+def test_multi_term_passes(kernel, page, fullvar, monkeypatch):
     """Config 7: blocked-list regexps, alternations, wildcards, fuzzy (variable
     scores), a pattern that fails every search; every query-eval kernel;
     truncated lists paged by any row (NKM_PAGE=1) or by batch restarts."""
     monkeypatch.setenv("NKM_KERNEL", kernel)
     monkeypatch.setenv("NKM_PAGE", page)
+    monkeypatch.setenv("NKM_FULLVAR", fullvar)
     run_passes(7, 1200, 3, dict(max_intervals=3))
 
 
