@@ -118,7 +118,7 @@ typedef struct mm_matched {
     int32_t eval_launches;          /* search kernel launches in the pass */
     int32_t n_batches;              /* replay batches */
     int32_t eval_kernel;            /* query-eval kernel with the most bytes: 0 search, 1 scan, 2 mscan (ABI 2) */
-    int32_t reserved3;
+    int32_t full_lists;             /* variable-score searches run as full lists (host-sorted), 0 for the oracle */
 } mm_matched;
 
 typedef struct mm_extract_list {

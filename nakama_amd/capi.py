@@ -112,7 +112,7 @@ class mm_matched(C.Structure):
                 ("entries", C.POINTER(mm_entry_ref)), ("is_candidates", C.c_int32), ("n_expired", C.c_int32),
                 ("pass_ms", C.c_double), ("eval_ms", C.c_double), ("pair_evals", C.c_int64),
                 ("reserved2", C.c_int64), ("eval_bytes", C.c_int64), ("eval_launches", C.c_int32),
-                ("n_batches", C.c_int32), ("eval_kernel", C.c_int32), ("reserved3", C.c_int32)]
+                ("n_batches", C.c_int32), ("eval_kernel", C.c_int32), ("full_lists", C.c_int32)]
 
 
 class mm_extract_list(C.Structure):
@@ -211,6 +211,7 @@ class ProcessResult:
     eval_launches: int = 0
     n_batches: int = 0
     eval_kernel: int = 0  # 0 search_kernel, 1 scan_kernel, 2 mscan_kernel
+    full_lists: int = 0   # variable-score searches run as host-sorted full lists
 
 
 class _TicketPack:
@@ -367,7 +368,8 @@ class Matchmaker:
         self._check(self.lib.mm_process(self.h, C.byref(out)))
         try:
             res = ProcessResult(self._groups(out), bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms,
-                                out.pair_evals, out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel)
+                                out.pair_evals, out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel,
+                                out.full_lists)
         finally:
             self.lib.mm_free_matched(self.h, C.byref(out))
         return res
@@ -393,7 +395,7 @@ class Matchmaker:
             else:
                 tickets = 0
             res = ProcessResult([], bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms, out.pair_evals,
-                                out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel)
+                                out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel, out.full_lists)
             return out.n_groups, tickets, n, res
         finally:
             self.lib.mm_free_matched(self.h, C.byref(out))

@@ -28,6 +28,12 @@ int guarded(void* h, F&& f) {
     } catch (const std::bad_alloc&) {
         c->set_error("out of host memory");
         return MM_ERR_INDEX;
+    } catch (const std::exception& e) {  // nothing may unwind into the cgo caller
+        c->set_error(std::string("internal error: ") + e.what());
+        return MM_ERR_INDEX;
+    } catch (...) {
+        c->set_error("internal error");
+        return MM_ERR_INDEX;
     }
 }
 std::string S(const char* p) { return p ? std::string(p) : std::string(); }
@@ -45,9 +51,20 @@ void* mm_create(const mm_config* cfg) {
     } catch (const DeviceError& e) {
         g_create_error = std::string("mm_create: ") + hipGetErrorString(e.err);
         return nullptr;
+    } catch (const std::exception& e) {
+        g_create_error = std::string("mm_create: ") + e.what();
+        return nullptr;
+    } catch (...) {
+        g_create_error = "mm_create: internal error";
+        return nullptr;
     }
 }
-void mm_destroy(void* h) { delete static_cast<Core*>(h); }
+void mm_destroy(void* h) {
+    try {
+        delete static_cast<Core*>(h);
+    } catch (...) {
+    }
+}
 void mm_pause(void* h) { if (h) static_cast<Core*>(h)->pause(); }
 void mm_resume(void* h) { if (h) static_cast<Core*>(h)->resume(); }
 void mm_stop(void* h) { if (h) static_cast<Core*>(h)->stop(); }
@@ -66,7 +83,7 @@ int mm_extract(void* h, mm_extract_list* out) {
     return guarded(h, [&](Core& c) { return c.extract(out); });
 }
 void mm_free_extract(void* h, mm_extract_list* out) {
-    if (h) static_cast<Core*>(h)->free_extract(out);
+    (void)guarded(h, [&](Core& c) { c.free_extract(out); return MM_OK; });
 }
 int mm_remove_session(void* h, const char* session_id, const char* ticket) {
     return guarded(h, [&](Core& c) { return c.remove_session(S(session_id), S(ticket)); });
@@ -97,10 +114,18 @@ int mm_process_commit(void* h, const int32_t* group_offsets, const mm_entry_ref*
     return guarded(h, [&](Core& c) { return c.process_commit(group_offsets, entries, n_groups, out); });
 }
 void mm_free_matched(void* h, mm_matched* out) {
-    if (h) static_cast<Core*>(h)->free_matched(out);
+    (void)guarded(h, [&](Core& c) { c.free_matched(out); return MM_OK; });
 }
-int32_t mm_ticket_count(void* h) { return h ? static_cast<Core*>(h)->ticket_count() : -1; }
-int32_t mm_active_count(void* h) { return h ? static_cast<Core*>(h)->active_count() : -1; }
+int32_t mm_ticket_count(void* h) {
+    int32_t n = -1;
+    (void)guarded(h, [&](Core& c) { n = c.ticket_count(); return MM_OK; });
+    return n;
+}
+int32_t mm_active_count(void* h) {
+    int32_t n = -1;
+    (void)guarded(h, [&](Core& c) { n = c.active_count(); return MM_OK; });
+    return n;
+}
 int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, double* scores_out, int32_t cap) {
     int32_t r = -1;
     int rc = guarded(h, [&](Core& c) {

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
@@ -307,7 +308,26 @@ struct SrcChoice {  // the posting list a search streams, when it has one
     uint32_t term = 0;
 };
 
+// RevThreshold (matchmaker.go:244-248, matchmaker_process.go:31-46): with
+// RevPrecision and RevThreshold > 0, an active pass starts a timer of
+// IntervalSec * RevThreshold seconds; the rows examined after it fired skip
+// every reverse (validateMatch) check.  Pin: the timer counts as fired at the
+// first row examined once the duration has elapsed (a zero duration fires at
+// the first row; Go's channel select may see it a little later).
+struct RevTimer {
+    bool armed = false, fired = false;
+    double limit_ms = 0;
+    std::chrono::steady_clock::time_point t0;
+    RevTimer(bool arm, double seconds) : armed(arm), limit_ms(seconds * 1e3), t0(std::chrono::steady_clock::now()) {}
+    bool check() {
+        if (armed && !fired)
+            fired = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() >= limit_ms;
+        return fired;
+    }
+};
+
 struct PassStats {
+    int full_lists = 0;  // variable-score searches run as full lists (host-sorted)
     // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel
     double k_ms[3] = {0, 0, 0};      // HIP-event time of the launches
     int64_t k_bytes[3] = {0, 0, 0};  // algorithmic bytes

@@ -90,7 +90,9 @@ struct Replay : ReplayCore {
             d.cur_key = g.hits[g.n - 1].key;
             d.cur_idx = g.hits[g.n - 1].idx;
         }
-        d.k = d.var_score ? (uint32_t)var_k_capacity() : std::max<uint32_t>(4096, 2 * d.k);
+        // constant-score pages double, but never past the rest of the source
+        d.k = d.var_score ? (uint32_t)var_k_capacity()
+                          : std::min<uint32_t>(std::max<uint32_t>(4096, 2 * d.k), std::max<uint32_t>(d.src_len, 1));
         c.h_groups_.reserve(1);
         c.h_groups_.p[0] = d;
         c.d_groups_.reserve(1, false);
@@ -102,14 +104,25 @@ struct Replay : ReplayCore {
                               c.ev_[0], c.ev_[1], d.var_score ? 2 : 1));
         c.h_res_.reserve(1);
         NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
-        // the whole page capacity comes back in the same round trip (pinned)
+        // up to kPage1 entries come back in the same round trip (pinned); a
+        // larger page copies the rest once its count is known
+        constexpr uint32_t kPage1 = 4096;
+        const uint32_t first = std::min(d.k, kPage1);
         c.h_page_.reserve(d.k);
-        NKM_HIP(hipMemcpyAsync(c.h_page_.p, c.d_out_.p, (size_t)d.k * sizeof(DHit), hipMemcpyDeviceToHost, stream));
+        NKM_HIP(hipMemcpyAsync(c.h_page_.p, c.d_out_.p, (size_t)first * sizeof(DHit), hipMemcpyDeviceToHost, stream));
         if (rev) {
             c.h_page_rev_.reserve(d.k);
-            NKM_HIP(hipMemcpyAsync(c.h_page_rev_.p, c.d_rev_.p, d.k, hipMemcpyDeviceToHost, stream));
+            NKM_HIP(hipMemcpyAsync(c.h_page_rev_.p, c.d_rev_.p, first, hipMemcpyDeviceToHost, stream));
         }
         NKM_HIP(hipStreamSynchronize(stream));
+        if (c.h_res_.p[0].count > first) {
+            const uint32_t rest = c.h_res_.p[0].count - first;
+            NKM_HIP(hipMemcpyAsync(c.h_page_.p + first, c.d_out_.p + first, (size_t)rest * sizeof(DHit),
+                                   hipMemcpyDeviceToHost, stream));
+            if (rev)
+                NKM_HIP(hipMemcpyAsync(c.h_page_rev_.p + first, c.d_rev_.p + first, rest, hipMemcpyDeviceToHost, stream));
+            NKM_HIP(hipStreamSynchronize(stream));
+        }
         float ms = 0.f;
         NKM_HIP(hipEventElapsedTime(&ms, c.ev_[0], c.ev_[1]));
         stats.k_ms[0] += ms;
@@ -259,6 +272,10 @@ struct Replay : ReplayCore {
         uint64_t off = 0;
         std::vector<uint32_t> chunked;
         std::vector<uint32_t> full_var;
+        // output entries the batch reserves: full-list promotions (below) may
+        // only use what batch assembly left of kOutCap
+        uint64_t budget = 0;
+        for (const BGroup& g : bg) budget += g.d.k;
         for (uint32_t i = 0; i < bg.size(); i++) {
             if (on_m[i]) continue;
             const DGroup& d = bg[i].d;
@@ -275,10 +292,12 @@ struct Replay : ReplayCore {
             // in source order, and the host sorts it stably by key (source
             // order breaks ties, as the top-K does), so the list is complete.
             if (d.var_score && !rev && !d.has_cursor && d.k >= (uint32_t)var_k_capacity() && d.src_len > d.k &&
-                d.src_len <= kFullVarMax && c.full_var_mode_) {
+                d.src_len <= kFullVarMax && c.full_var_mode_ && budget + (d.src_len - d.k) <= kOutCap) {
+                budget += d.src_len - d.k;
                 w.var_score = 0;
                 w.k = d.src_len;
                 full_var.push_back((uint32_t)lg.size());
+                stats.full_lists++;
             }
             w.out_off = off;
             off += w.k;
@@ -753,7 +772,9 @@ int Core::process_default(GroupList& out_groups,
     const uint32_t N = (uint32_t)ticket_.size();
     std::vector<uint8_t>& sel = sel_;
     sel.assign(N, 0);
-    const bool rev = cfg_.rev_precision != 0;
+    bool rev = cfg_.rev_precision != 0;
+    RevTimer timer(rev && active_flag_ && cfg_.rev_threshold > 0,
+                   (double)cfg_.interval_sec * (double)cfg_.rev_threshold);
     const int maxI = cfg_.max_intervals;
     std::vector<uint32_t>& rows = rows_;
     filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, rows,
@@ -783,6 +804,8 @@ int Core::process_default(GroupList& out_groups,
     while (true) {
         while (pos < rows.size() && sel[rows[pos]]) pos++;
         if (pos >= rows.size()) break;
+        // the RevThreshold timer fired: the remaining rows search as without RevPrecision
+        if (rev && timer.check()) rev = rp.rev = false;
         // ---- assemble the batch ----
         const auto ta0 = std::chrono::steady_clock::now();
         for (auto& g : bg)
@@ -958,6 +981,7 @@ int Core::process_default(GroupList& out_groups,
             // hold tickets selected earlier in this batch, which the walk skips,
             // so the list stays exact.
             BGroup& bgr = bg[brow_group[bi]];
+            if (rp.rev && timer.check()) rp.rev = false;  // later rows of this batch skip the reverse checks
             auto status = rp.decide(T, bgr, bi == 0 || (page_mode_ && !bgr.d.var_score), grp);
             if (status == Replay::EXHAUSTED) {
                 exhausted = true;
@@ -994,8 +1018,10 @@ int Core::process_default(GroupList& out_groups,
 // processCustom (matchmaker_process.go:336-612), up to the override call.
 int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                          PassStats& stats) {
-    const bool rev = cfg_.rev_precision != 0;
+    const bool rev_cfg = cfg_.rev_precision != 0;
     const int maxI = cfg_.max_intervals;
+    RevTimer timer(rev_cfg && active_flag_ && cfg_.rev_threshold > 0,
+                   (double)cfg_.interval_sec * (double)cfg_.rev_threshold);  // :340-346
     std::vector<uint32_t> rows;
     for (uint32_t s : active_list_)
         if (live_[s] && is_active_[s]) rows.push_back(s);
@@ -1003,6 +1029,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
     for (uint32_t r : rows)
         if (intervals_[r] >= maxI || minc_[r] == maxc_[r]) expired.push_back(r);
     if (!active_flag_) return MM_OK;
+    bool rev = rev_cfg;
     const DStore st = dstore();
     std::vector<uint8_t> sel(ticket_.size(), 0);  // processCustom never selects
     Replay rp(*this, sel, rev, maxI, stats, st, stream_);
@@ -1011,6 +1038,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
     // every row is independent: one search per row, in chunks
     for (size_t base = 0; base < rows.size(); base += kMaxBatchRows / 4) {
         const size_t end = std::min(rows.size(), base + kMaxBatchRows / 4);
+        if (rev && timer.check()) rev = rp.rev = false;
         std::vector<BGroup> bg(end - base);
         uint64_t off = 0;
         h_groups_.reserve(bg.size());
@@ -1041,6 +1069,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
         for (size_t i = 0; i < bg.size(); i++) {
             BGroup& g = bg[i];
             const uint32_t T = g.row_slot;
+            if (rev && timer.check()) rev = rp.rev = false;  // :353-358
             // all hits (paging through the list), filtered as :425-468
             std::vector<uint32_t> hits, hpos;
             uint32_t j = 0;
@@ -1063,8 +1092,8 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
             // combineIndexes: Go's `1 << length` is 0 / negative for length >= 63 -> no subsets
             if (too_many) continue;
             const size_t L = hits.size();
-            if (L > 40) continue;  // reference enumerates 2^L subsets (intractable); documented
             const int cmin = minc_[T] - count_[T], cmax = maxc_[T] - count_[T];
+            if (L == 0 || cmax <= 0) continue;  // every subset holds >= 1 ticket > max: none emitted
             // pairwise reverse checks among the hits (validateMatch both ways, incl. self)
             std::vector<uint64_t> pm;
             bool covered = g.pm != nullptr;
@@ -1093,8 +1122,9 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
             }
             const uint64_t limit = 1ull << L;
             std::vector<uint32_t> combo;
-            for (uint64_t bits = 1; bits < limit; bits++) {
-                if (__builtin_popcountll(bits) > cmax) continue;
+            // combineIndexes' ascending bitmask loop (:586-610), visiting only
+            // the masks its `count > max` test lets through (next_mask_le)
+            for (uint64_t bits = next_mask_le(1, cmax); bits < limit; bits = next_mask_le(bits + 1, cmax)) {
                 combo.clear();
                 int entry_count = 0;
                 bool over = false;
@@ -1388,6 +1418,7 @@ int Core::process(mm_matched* out) {
     out->eval_bytes = stats.k_bytes[dk];
     out->eval_launches = stats.k_launches[dk];
     out->n_batches = stats.batches;
+    out->full_lists = stats.full_lists;
     out->pass_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MM_OK;
 }
@@ -1440,7 +1471,7 @@ extern "C" int32_t mm_debug_group_indexes(const int32_t* counts, const int64_t* 
 }
 
 extern "C" int mm_debug_term_match(int32_t kind, const char* pattern, int32_t fuzziness, const char* term,
-                                   double* boost) {
+                                   double* boost) try {
     nkm::TermMatcher m;
     *boost = 0.0;
     if (kind == 2) {
@@ -1455,12 +1486,18 @@ extern "C" int mm_debug_term_match(int32_t kind, const char* pattern, int32_t fu
         if (st != nkm::MT_OK) return st == nkm::MT_UNSUPPORTED ? -2 : -1;
     }
     return m.accept(term, boost) ? 1 : 0;
+} catch (...) {
+    return -1;
 }
 
 extern "C" int mm_debug_compile(const char* query) {
-    nkm::CompiledQuery cq;
-    int rc = nkm::compile_query(query ? query : "", &cq);
-    return rc == nkm::CQ_OK ? MM_OK : rc == nkm::CQ_UNSUPPORTED ? MM_ERR_UNSUPPORTED : MM_ERR_QUERY_INVALID;
+    try {
+        nkm::CompiledQuery cq;
+        int rc = nkm::compile_query(query ? query : "", &cq);
+        return rc == nkm::CQ_OK ? MM_OK : rc == nkm::CQ_UNSUPPORTED ? MM_ERR_UNSUPPORTED : MM_ERR_QUERY_INVALID;
+    } catch (...) {
+        return MM_ERR_INDEX;
+    }
 }
 
 namespace nkm {

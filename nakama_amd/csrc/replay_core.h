@@ -54,6 +54,17 @@ inline void group_indexes(const std::vector<uint32_t>& in, size_t from, int requ
     group_indexes(in, from + 1, required, cnt, created, out);
 }
 
+// The smallest mask >= x with at most c bits set (c >= 1).  Every value
+// skipped lies in (x, x + lowbit(x)) for an x with more than c bits, i.e. it
+// holds x's bits plus lower ones: combineIndexes (matchmaker_process.go:
+// 586-590) `continue`s on all of them, so walking the masks this way visits
+// exactly the subsets its ascending loop emits, in the same order, without
+// the 2^n iterations.
+inline uint64_t next_mask_le(uint64_t x, int c) {
+    while (__builtin_popcountll(x) > c) x += x & (~x + 1);
+    return x;
+}
+
 // A batch search and its (possibly extended) hit list.
 struct BGroup {
     uint32_t sig = 0;
@@ -101,7 +112,9 @@ struct FastCombos {
 struct ReplayCore {
     ReplayView v;
     std::vector<uint8_t>& sel;
-    const bool rev;
+    // RevPrecision reverse checks; cleared for the rest of the pass once the
+    // RevThreshold timer fires (matchmaker_process.go:40-46,139,178)
+    bool rev;
     const int max_intervals;
     std::vector<std::vector<CE>> combos;  // pool: the first ncomb are this row's entryCombos
     std::vector<uint32_t> cmask;          // per combo: OR of its entries' session masks (a superset)

@@ -692,6 +692,22 @@ static vector<IGroup> group_indexes(const vector<IP>& indexes, size_t from, int 
     return results;
 }
 
+// m.revThresholdFn (matchmaker.go:244-248): a timer of IntervalSec*RevThreshold
+// seconds, created at the start of an active pass when RevPrecision is on and
+// RevThreshold > 0.  Pin: it counts as fired from the first row examined after
+// the duration elapsed (zero duration: from the first row).
+struct RevThresholdTimer {
+    bool armed;
+    double limit_s;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit RevThresholdTimer(const Matchmaker& m)
+        : armed(m.active && m.cfg.rev_precision && m.cfg.rev_threshold > 0),
+          limit_s((double)m.cfg.interval_sec * (double)m.cfg.rev_threshold) {}
+    bool fired() const {
+        return armed && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >= limit_s;
+    }
+};
+
 static vector<IP> active_order(Matchmaker& m) {  // pin: (CreatedAt, Ticket)
     vector<IP> v;
     v.reserve(m.active_indexes.size());
@@ -708,9 +724,13 @@ static void process_default(Matchmaker& m, const vector<IP>& order,
                             const std::unordered_map<string, IP>& indexes_copy,
                             vector<vector<Entry>>& matched, vector<string>& expired, int64_t* pair_evals) {
     std::unordered_set<string> selected;
-    const bool rev = m.cfg.rev_precision != 0;
     const int max_intervals = m.cfg.max_intervals;
+    // RevThreshold timer (matchmaker.go:244-248, matchmaker_process.go:31-46)
+    RevThresholdTimer timer(m);
+    bool threshold = false;
     for (const IP& ai : order) {
+        if (!threshold && timer.fired()) threshold = true;
+        const bool rev = m.cfg.rev_precision != 0 && !threshold;  // :139, :178
         const string& ticket = ai->ticket;
         if (selected.count(ticket)) continue;
         ai->intervals++;
@@ -831,10 +851,13 @@ static void process_default(Matchmaker& m, const vector<IP>& order,
 static void process_custom(Matchmaker& m, const vector<IP>& order,
                            const std::unordered_map<string, IP>& indexes_copy,
                            vector<vector<Entry>>& candidates, vector<string>& expired, int64_t* pair_evals) {
-    const bool rev = m.cfg.rev_precision != 0;
     const int max_intervals = m.cfg.max_intervals;
+    RevThresholdTimer timer(m);  // :340-346
+    bool threshold = false;
     for (const IP& ix : order) ix->intervals++;
     for (const IP& ix : order) {
+        if (!threshold && timer.fired()) threshold = true;  // :353-358
+        const bool rev = m.cfg.rev_precision != 0 && !threshold;  // :439, :519
         const string& ticket = ix->ticket;
         bool last_interval = ix->intervals >= max_intervals || ix->min_count == ix->max_count;
         if (last_interval) expired.push_back(ticket);
@@ -858,12 +881,18 @@ static void process_custom(Matchmaker& m, const vector<IP>& order,
         // combineIndexes (:578-612): Go `1 << length` is 0 / negative for length >= 63
         size_t length = hit_indexes.size();
         if (length >= 63) continue;
-        if (length > 40) continue;  // reference enumerates 2^length subsets; intractable (documented)
         int cmin = ix->min_count - ix->count, cmax = ix->max_count - ix->count;
+        if (cmax <= 0) continue;  // `count > max` rejects every mask
         uint64_t limit = 1ULL << length;
         for (uint64_t bits = 1; bits < limit; bits++) {
             int cnt = __builtin_popcountll(bits);
-            if (cnt > cmax) continue;
+            if (cnt > cmax) {
+                // `continue` (:590) up to the next mask that can pass: below
+                // bits + lowbit(bits) every mask holds all of bits' set bits
+                // plus more, so it fails the same test (keeps n <= 62 tractable)
+                bits += (bits & (~bits + 1)) - 1;
+                continue;
+            }
             vector<IP> combo;
             int entry_count = 0;
             bool over = false;

@@ -52,24 +52,44 @@ def state(mm):
     return [(t.ticket, t.intervals) for t in mm.Extract()], mm.active_count()
 
 
-def run_passes(config, n, passes, cfg, override=None, extra=None):
+# Oracle runs are memoised per workload: the kernel / host-path variants of a
+# config compare the product against one oracle run (C1 10k is ~16 s of oracle).
+_ORACLE_RUNS = {}
+
+
+def _oracle_passes(config, n, passes, cfg):
+    key = (config, n, passes, tuple(sorted(cfg.items())))
+    if key not in _ORACLE_RUNS:
+        ts = synth.TicketSet(config, n)
+        orc = capi.Matchmaker(harness.oracle_lib(), **cfg)
+        try:
+            ts.insert_into(orc)
+            _ORACLE_RUNS[key] = [(orc.Process(), state(orc)) for _ in range(passes)]
+        finally:
+            orc.close()
+            ts.close()
+    return _ORACLE_RUNS[key]
+
+
+def run_passes(config, n, passes, cfg, extra=None):
+    """Product passes against the (memoised) oracle's; returns the product's
+    ProcessResults (groups + pass statistics)."""
+    want = _oracle_passes(config, n, passes, cfg)
     ts = synth.TicketSet(config, n)
-    gpu, orc = (capi.Matchmaker(product_lib(), override=override, **cfg),
-                capi.Matchmaker(harness.oracle_lib(), override=override, **cfg))
+    gpu = capi.Matchmaker(product_lib(), **cfg)
+    out = []
     try:
         ts.insert_into(gpu)
-        ts.insert_into(orc)
         for p in range(passes):
-            g = gpu.Process()
-            o = orc.Process()
-            assert g == o, f"config {config} pass {p}: groups differ (gpu {len(g)} vs oracle {len(o)})"
-            assert state(gpu) == state(orc)
+            r = gpu.process_raw()
+            assert r.groups == want[p][0], f"config {config} pass {p}: groups differ (gpu {len(r.groups)} vs oracle {len(want[p][0])})"
+            assert state(gpu) == want[p][1]
             if extra:
-                extra(p, gpu, orc)
-        return g
+                extra(p, gpu)
+            out.append(r)
+        return out
     finally:
         gpu.close()
-        orc.close()
         ts.close()
 
 
@@ -80,13 +100,75 @@ KERNELS = ["search", "scan", "mscan"]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_c1_pool_query(kernel, monkeypatch):
+@pytest.mark.parametrize("n", [1200, 10_000])
+def test_c1_pool_query(kernel, n, monkeypatch):
+    """C1 at its stated 10k (BASELINE configs[0]) on every query-eval kernel."""
     monkeypatch.setenv("NKM_KERNEL", kernel)
-    run_passes(1, 1200, 2, dict(max_intervals=2))
+    run_passes(1, n, 2, dict(max_intervals=2))
 
 
 def test_c2_skill_window_boosts():
     run_passes(2, 1500, 2, dict(max_intervals=2))
+
+
+@pytest.mark.parametrize("fullvar", ["1", "0"])
+def test_c2_region_lists_past_topk(fullvar, monkeypatch):
+    """C2's shape at 10k: region posting lists of ~2,500 (past the 512-entry
+    LDS top-K), ~1,000 skill-window signatures, so search_kernel<512>'s
+    truncation, early exit at the score bound and batch restarts all run;
+    NKM_FULLVAR=1 also sends re-searched rows through full lists."""
+    monkeypatch.setenv("NKM_FULLVAR", fullvar)
+    rs = run_passes(2, 10_000, 2, dict(max_intervals=2))
+    assert sum(r.n_batches for r in rs) > 2  # truncated lists restarted batches
+    full = sum(r.full_lists for r in rs)
+    assert (full > 0) if fullvar == "1" else (full == 0)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("config", [3, 4])
+def test_c3_c4_at_6k(config, kernel, monkeypatch):
+    """C3 (parties, 5v5) and C4 (64 pools) at 6,000 tickets on every kernel."""
+    monkeypatch.setenv("NKM_KERNEL", kernel)
+    run_passes(config, 6000, 2, dict(max_intervals=2))
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_datetime_props_and_date_ranges(kernel, monkeypatch):
+    """Config 8: string properties in each layout blugeParseDateTime accepts
+    (indexed as raw-UnixNano numeric terms, match_common.go:161-170,221-236)
+    mixed with strings none parses (keywords), queried with RFC3339 date-range
+    clauses (query_string_parser.go:234-250; ConstantScorer(1))."""
+    monkeypatch.setenv("NKM_KERNEL", kernel)
+    run_passes(8, 3000, 3, dict(max_intervals=3))
+
+
+def test_datetime_hit_lists():
+    ts = synth.TicketSet(8, 600)
+    gpu, orc = pair(dict(max_intervals=2))
+    try:
+        ts.insert_into(gpu)
+        ts.insert_into(orc)
+        for k in range(0, 600, 13):
+            t = ts.ticket_id(k)
+            hg, ho = gpu.debug_hits(t), orc.debug_hits(t)
+            assert [h for h, _ in hg] == [h for h, _ in ho]
+            for (_, a), (_, b) in zip(hg, ho):
+                assert math.isclose(a, b, rel_tol=1e-6)
+    finally:
+        gpu.close()
+        orc.close()
+        ts.close()
+
+
+@pytest.mark.parametrize("config,n,mi", [(5, 800, 2), (6, 600, 3)])
+def test_rev_threshold_fired(config, n, mi):
+    """RevThreshold (matchmaker.go:244-248): IntervalSec * RevThreshold = 0 s,
+    so the timer has fired at the first row and every reverse check is skipped
+    (matchmaker_process.go:40-46,139,178) — the pass equals the one without
+    RevPrecision."""
+    cfg = dict(max_intervals=mi, rev_precision=True, interval_sec=0, rev_threshold=1)
+    run_passes(config, n, 2, cfg)
+    assert _oracle_passes(config, n, 2, cfg) == _oracle_passes(config, n, 2, dict(max_intervals=mi))
 
 
 HOST_KERNEL = [("0", "1", "search"), ("force", "1", "scan"), ("force", "1", "mscan"), ("force", "0", "mscan"),
@@ -140,7 +222,10 @@ def first_disjoint(cands):
     return out
 
 
-def test_c5_override_candidates():
+@pytest.mark.parametrize("n", [400, 5000])
+def test_c5_override_candidates(n):
+    """processCustom candidates (RevPrecision, buckets of 8) handed to the
+    deterministic first-disjoint override of SURVEY 8(d) C5, then committed."""
     seen = {}
 
     def rec(tag):
@@ -149,7 +234,7 @@ def test_c5_override_candidates():
             return first_disjoint(c)
         return f
 
-    ts = synth.TicketSet(5, 400)
+    ts = synth.TicketSet(5, n)
     gpu = capi.Matchmaker(product_lib(), override=rec("g"), max_intervals=2, rev_precision=True)
     orc = capi.Matchmaker(harness.oracle_lib(), override=rec("o"), max_intervals=2, rev_precision=True)
     try:
@@ -333,7 +418,12 @@ def test_multi_term_passes(kernel, page, fullvar, monkeypatch):
     monkeypatch.setenv("NKM_KERNEL", kernel)
     monkeypatch.setenv("NKM_PAGE", page)
     monkeypatch.setenv("NKM_FULLVAR", fullvar)
-    run_passes(7, 1200, 3, dict(max_intervals=3))
+    rs = run_passes(7, 1200, 3, dict(max_intervals=3))
+    full = sum(r.full_lists for r in rs)
+    if fullvar == "0":
+        assert full == 0
+    elif kernel == "search":
+        assert full > 0  # the full-list branch ran
 
 
 def test_multi_term_rev_precision():
@@ -375,3 +465,27 @@ def test_multi_term_sets_grow_between_passes():
         orc.close()
         for s in sets:
             s.close()
+
+
+def _custom_many_hits(lib, n_tickets):
+    """n_tickets tickets with query "*", Min=2 Max=3: every row has
+    n_tickets-1 filtered hits (> 40, < 63), so combineIndexes' ascending mask
+    loop (matchmaker_process.go:578-612) emits every 2-subset (hitCount 3;
+    1-subsets reach hitCount 2 < MaxCount and are rejected, :496)."""
+    seen = []
+    mm = capi.Matchmaker(lib, override=lambda c: (seen.append([list(g) for g in c]), [])[1], max_intervals=5)
+    try:
+        for i in range(n_tickets):
+            mm.Add([capi.Presence(f"u{i}", f"s{i}", f"u{i}", "n")], f"s{i}", "", "*", 2, 3, 1, {"k": "v"}, {},
+                   ticket=f"t{i:03d}", created_at=synth.T0 + 1024 * i)
+        mm.Process()
+        return seen[0] if seen else []
+    finally:
+        mm.close()
+
+
+def test_custom_rows_past_40_hits():
+    n = 51
+    cands = _custom_many_hits(product_lib(), n)
+    assert len(cands) == n * (n - 1) * (n - 2) // 2
+    assert cands == _custom_many_hits(harness.oracle_lib(), n)

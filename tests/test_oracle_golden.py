@@ -95,3 +95,40 @@ def test_term_cases(case):
         assert got[0] == want[0] and got[1] == pytest.approx(want[1], rel=1e-15), got
     else:
         assert got == want
+
+
+def test_oracle_rev_threshold_fired_equals_no_rev():
+    """RevThreshold timer of 0 s (IntervalSec * RevThreshold): every reverse
+    check is skipped from the first row (matchmaker_process.go:40-46,139,178)."""
+    from nakama_amd import synth
+    outs = []
+    for cfg in (dict(rev_precision=True, interval_sec=0, rev_threshold=1), dict(rev_precision=False),
+                dict(rev_precision=True, interval_sec=15, rev_threshold=1)):
+        ts = synth.TicketSet(6, 300)
+        mm = capi.Matchmaker(harness.oracle_lib(), max_intervals=3, **cfg)
+        try:
+            ts.insert_into(mm)
+            outs.append([mm.Process() for _ in range(2)])
+        finally:
+            mm.close()
+            ts.close()
+    assert outs[0] == outs[1]
+    assert outs[2] != outs[1]  # the reverse checks do change config 6's groups
+
+
+def test_oracle_custom_enumeration_past_40_hits():
+    """combineIndexes over 50 hits: the ascending mask loop visits only masks
+    with <= max bits (the others `continue`), so it finishes; every 2-subset."""
+    n, seen = 51, []
+    mm = capi.Matchmaker(harness.oracle_lib(), override=lambda c: (seen.append(c), [])[1], max_intervals=5)
+    try:
+        for i in range(n):
+            mm.Add([capi.Presence(f"u{i}", f"s{i}", f"u{i}", "n")], f"s{i}", "", "*", 2, 3, 1, {}, {},
+                   ticket=f"t{i:03d}", created_at=1_700_000_000_000_000_000 + 1024 * i)
+        mm.Process()
+    finally:
+        mm.close()
+    cands = seen[0]
+    assert len(cands) == n * (n - 1) * (n - 2) // 2
+    # candidates of row 0 come first, in ascending mask order over its hit list
+    assert [t for t, _ in cands[0]] == ["t001", "t002", "t000"]

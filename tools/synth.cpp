@@ -229,6 +229,46 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             t.max_count = shape == 0 ? 2 : 4;
             break;
         }
+        case 8: {  // datetime-typed string properties (blugeProcessProperty, match_common.go:161-170,221-236)
+                   // and RFC3339 date-range clauses (query_string_parser.go:234-250)
+            party = r.uni() < 0.85 ? 1 : 2;
+            const char* mode = kModes[r.next() & 1];
+            const int day = (int)(r.next() % 60), hh = (int)(r.next() % 24), mi = (int)(r.next() % 60),
+                      ss = (int)(r.next() % 60);
+            const int mon = 1 + day / 28, dd = 1 + day % 28;
+            char since[64];
+            switch ((int)(r.next() % 6)) {  // the five layouts bluge tries, and a string none parses
+            case 0: std::snprintf(since, sizeof since, "2024-%02d-%02dT%02d:%02d:%02dZ", mon, dd, hh, mi, ss); break;
+            case 1:
+                std::snprintf(since, sizeof since, "2024-%02d-%02dT%02d:%02d:%02d.%09d+02:00", mon, dd, hh, mi, ss,
+                              (int)(r.next() % 1000000000));
+                break;
+            case 2: std::snprintf(since, sizeof since, "2024-%02d-%02dT%02d:%02d:%02d", mon, dd, hh, mi, ss); break;
+            case 3: std::snprintf(since, sizeof since, "2024-%02d-%02d %02d:%02d:%02d", mon, dd, hh, mi, ss); break;
+            case 4: std::snprintf(since, sizeof since, "2024-%02d-%02d", mon, dd); break;
+            default: std::snprintf(since, sizeof since, "2024-%02d-%02dX%02d", mon, dd, hh); break;  // keyword
+            }
+            S->sp.push_back({"mode", mode});
+            S->sp.push_back({"since", S->keep(since)});
+            const int d0 = (int)(r.next() % 50), d1 = d0 + 3 + (int)(r.next() % 20);
+            char lo[40], hi[40];
+            std::snprintf(lo, sizeof lo, "2024-%02d-%02dT00:00:00Z", 1 + d0 / 28, 1 + d0 % 28);
+            std::snprintf(hi, sizeof hi, "2024-%02d-%02dT12:00:00+01:00", 1 + (d1 % 56) / 28, 1 + d1 % 28);
+            char q[256];
+            switch ((int)(r.next() % 4)) {
+            case 0: std::snprintf(q, sizeof q, "+properties.mode:%s +properties.since:>=\"%s\"", mode, lo); break;
+            case 1:
+                std::snprintf(q, sizeof q, "+properties.mode:%s properties.since:>\"%s\"^2 properties.since:<=\"%s\"",
+                              mode, lo, hi);
+                break;
+            case 2: std::snprintf(q, sizeof q, "+properties.mode:%s -properties.since:<\"%s\"", mode, lo); break;
+            default: std::snprintf(q, sizeof q, "+properties.since:>=\"%s\" +properties.since:<=\"%s\"", lo, hi);
+            }
+            query = q;
+            t.min_count = 2;
+            t.max_count = (r.next() % 2) ? 2 : 3;
+            break;
+        }
         default: {  // 6: small mixed workload for parity (parties, ranges, boosts, Min<Max)
             const double u = r.uni();
             party = u < 0.7 ? 1 : u < 0.9 ? 2 : 3;
