@@ -20,7 +20,13 @@
  *  - Outputs (mm_matched, mm_extract_list) are library-owned and released
  *    with the matching mm_free_* call.
  *  - A handle is internally synchronised: mutators and mm_process may be
- *    called from different threads (server/matchmaker.go:186 mutex).
+ *    called from different threads (server/matchmaker.go:186 mutex).  Like
+ *    LocalMatchmaker.Process, mm_process holds the handle's lock only to take
+ *    its snapshot and to finish (matchmaker.go:290-343): a mutator called while
+ *    a pass runs returns its status at once (validated against the store plus
+ *    the mutations already queued) and is applied when the pass ends, before
+ *    the completeness re-check, so a group that lost a ticket is dropped.
+ *    mm_extract and mm_debug_hits wait for a running pass to end.
  *
  * The CPU oracle under oracle/ exports the same symbols from its own shared
  * object so that one test harness can drive both (tests only).
@@ -35,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 2
+#define MM_ABI_VERSION 3
 
 /* Status codes. */
 #define MM_OK 0
@@ -126,6 +132,12 @@ typedef struct mm_extract_list {
     const mm_ticket* tickets;
 } mm_extract_list;
 
+/* A library-owned list of strings (ticket ids), freed with mm_free_str_list. */
+typedef struct mm_str_list {
+    int32_t n;
+    const char* const* items;
+} mm_str_list;
+
 /* ---- lifecycle (NewLocalMatchmaker / Pause / Resume / Stop) ---- */
 void* mm_create(const mm_config* cfg);                 /* matchmaker.go:214 */
 void  mm_destroy(void* h);
@@ -158,7 +170,18 @@ int  mm_process_commit(void* h, const int32_t* group_offsets, const mm_entry_ref
                        int32_t n_groups, mm_matched* out);
 void mm_free_matched(void* h, mm_matched* out);
 
+/* Tickets that left the matchmaker (Remove*, a re-inserted ticket id, or
+ * matched and retired by a pass) since the previous call; the first call
+ * starts the recording.  The Go shim drops its delivery entries with them
+ * (ABI 3). */
+int  mm_drain_removed(void* h, mm_str_list* out);
+void mm_free_str_list(void* h, mm_str_list* out);
+
 /* ---- introspection used by tests and the bench ---- */
+/* Test hook: fn(ctx) is called once per pass, on the pass's thread, after the
+ * device searches and the replay and before the post-pass finish, with the
+ * handle unlocked (mutators called from it are queued as concurrent ones). */
+void mm_debug_set_pass_hook(void* h, void (*fn)(void*), void* ctx);
 int32_t mm_ticket_count(void* h);
 int32_t mm_active_count(void* h);
 /* Hit list of one active ticket as processDefault's search would return it

@@ -119,12 +119,20 @@ class mm_extract_list(C.Structure):
     _fields_ = [("n", C.c_int32), ("tickets", C.POINTER(mm_ticket))]
 
 
+class mm_str_list(C.Structure):
+    _fields_ = [("n", C.c_int32), ("items", C.POINTER(C.c_char_p))]
+
+
+PASS_HOOK = C.CFUNCTYPE(None, C.c_void_p)
+
+
 EXPORTED_SYMBOLS = (
     "mm_create", "mm_destroy", "mm_pause", "mm_resume", "mm_stop", "mm_last_error", "mm_abi_version",
     "mm_backend_name", "mm_add", "mm_insert", "mm_extract", "mm_free_extract", "mm_remove_session",
     "mm_remove_session_all", "mm_remove_party", "mm_remove_party_all", "mm_remove_all", "mm_remove",
     "mm_process", "mm_process_commit", "mm_free_matched", "mm_ticket_count", "mm_active_count",
     "mm_debug_hits", "mm_debug_compile", "mm_debug_term_match", "mm_debug_group_indexes",
+    "mm_drain_removed", "mm_free_str_list", "mm_debug_set_pass_hook",
 )
 
 
@@ -160,6 +168,9 @@ def load_library(path: str) -> C.CDLL:
         "mm_active_count": (C.c_int32, [vp]),
         "mm_debug_hits": (C.c_int32, [vp, C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int32]),
         "mm_debug_compile": (C.c_int, [C.c_char_p]),
+        "mm_drain_removed": (C.c_int, [vp, C.POINTER(mm_str_list)]),
+        "mm_free_str_list": (None, [vp, C.POINTER(mm_str_list)]),
+        "mm_debug_set_pass_hook": (None, [vp, PASS_HOOK, vp]),
         "mm_debug_term_match": (C.c_int, [C.c_int32, C.c_char_p, C.c_int32, C.c_char_p, C.POINTER(C.c_double)]),
         "mm_debug_group_indexes": (C.c_int32, [C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_int32, C.c_int32,
                                                C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int64),
@@ -442,6 +453,24 @@ class Matchmaker:
         if r.groups and self._matched_fn is not None:
             self._matched_fn(r.groups)
         return r.groups
+
+    def drain_removed(self) -> List[str]:
+        """Tickets that left the matchmaker since the previous call (the first
+        call starts the recording): what the Go shim drops from its delivery
+        entries (include/nakama_mm.h, ABI 3)."""
+        out = mm_str_list()
+        self._check(self.lib.mm_drain_removed(self.h, C.byref(out)))
+        try:
+            return [out.items[i].decode("utf-8") for i in range(out.n)]
+        finally:
+            self.lib.mm_free_str_list(self.h, C.byref(out))
+
+    def set_pass_hook(self, fn):
+        """Test hook: fn() runs once per pass between the searches/replay and
+        the post-pass finish, with the handle unlocked (mutators called from it
+        are queued as concurrent ones).  None removes it."""
+        self._hook = PASS_HOOK(lambda _ctx: fn()) if fn is not None else None
+        self.lib.mm_debug_set_pass_hook(self.h, self._hook if fn is not None else PASS_HOOK(), None)
 
     # introspection
     def ticket_count(self) -> int:

@@ -126,6 +126,16 @@ int32_t mm_active_count(void* h) {
     (void)guarded(h, [&](Core& c) { n = c.active_count(); return MM_OK; });
     return n;
 }
+int mm_drain_removed(void* h, mm_str_list* out) {
+    if (!out) return MM_ERR_ARG;
+    return guarded(h, [&](Core& c) { return c.drain_removed(out); });
+}
+void mm_free_str_list(void* h, mm_str_list* out) {
+    (void)guarded(h, [&](Core& c) { c.free_str_list(out); return MM_OK; });
+}
+void mm_debug_set_pass_hook(void* h, void (*fn)(void*), void* ctx) {
+    (void)guarded(h, [&](Core& c) { c.set_pass_hook(fn, ctx); return MM_OK; });
+}
 int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, double* scores_out, int32_t cap) {
     int32_t r = -1;
     int rc = guarded(h, [&](Core& c) {

@@ -32,7 +32,8 @@ namespace nkm {
 hipError_t launch_search(const DStore& st, const DGroup* d_groups, int n_groups, DHit* d_out, uint8_t* d_rev,
                          DGroupResult* d_res, hipStream_t stream, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
                          int kinds = 3);
-hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_t n, hipStream_t stream);
+hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_t n, hipStream_t stream,
+                              uint8_t value = 0);
 hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, uint8_t* d_out, hipStream_t stream);
 int var_k_capacity();
 hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, DHit* d_scratch, DGroupResult* d_cres,
@@ -393,10 +394,81 @@ public:
     void stop() { stopped_ = true; }
     const char* last_error() const { return last_error_.c_str(); }
     void set_error(const std::string& e) { last_error_ = e; }
+    void set_pass_hook(void (*fn)(void*), void* ctx) {
+        std::lock_guard<std::mutex> lk(mu_);
+        pass_hook_ = fn;
+        pass_hook_ctx_ = ctx;
+    }
+    int drain_removed(mm_str_list* out);
+    void free_str_list(mm_str_list* out);
 
 private:
     friend struct Replay;
     struct Ticket;
+
+    // ---- mutations that arrive while a pass runs ----
+    // Process() holds the store lock only to take its snapshot and to finish;
+    // a mutator called in between validates against the store plus the
+    // mutations already queued (the "effective" state), returns its status,
+    // and queues itself; the queue is applied in arrival order when the pass
+    // ends, before its completeness re-check (matchmaker.go:309-343), so a
+    // group that lost a ticket is dropped exactly as the reference drops it.
+    struct OwnedTicket {  // an mm_ticket's strings, owned (callers' memory is not retained)
+        std::string ticket, session_id, party_id, query, node;
+        int32_t min_count = 0, max_count = 0, count_multiple = 1, intervals = 0;
+        int64_t created_at = 0;
+        std::vector<Presence> presences;
+        std::vector<std::pair<std::string, std::string>> sprops;
+        std::vector<std::pair<std::string, double>> nprops;
+        explicit OwnedTicket(const mm_ticket& t);
+        struct View {  // an mm_ticket over this record (valid while it lives)
+            mm_ticket t{};
+            std::vector<mm_presence> p;
+            std::vector<mm_str_prop> s;
+            std::vector<mm_num_prop> n;
+        };
+        void view(View& v) const;
+    };
+    enum PendKind { P_ADD, P_INSERT, P_REMOVE_SESSION, P_REMOVE_SESSION_ALL, P_REMOVE_PARTY, P_REMOVE_PARTY_ALL,
+                    P_REMOVE_ALL, P_REMOVE };
+    struct PendingOp {
+        PendKind kind;
+        std::vector<OwnedTicket> tickets;  // P_ADD / P_INSERT
+        std::vector<CompiledQuery> cqs;
+        std::vector<uint8_t> ok;
+        std::string a, b;                  // session / party / node, ticket
+        std::vector<std::string> ids;      // P_REMOVE
+    };
+    struct PendTk {  // a ticket's effective state while a pass runs
+        bool alive = false;
+        std::string session_id, party_id, node;
+        std::vector<std::string> sessions;  // distinct, presence order
+    };
+    bool pass_running_ = false;
+    std::vector<PendingOp> pending_;
+    std::unordered_map<std::string, PendTk> pend_tk_;
+    std::unordered_map<std::string, int> pend_sess_, pend_party_;  // ticket-count deltas
+    PendTk* eff_ticket(const std::string& id);
+    void eff_remove(PendTk& t);
+    void eff_add(const OwnedTicket& t);
+    int eff_sess_count(const std::string& sid);
+    int eff_party_count(const std::string& pid);
+    void apply_pending();  // under mu_, at the end of a pass
+    void (*pass_hook_)(void*) = nullptr;  // tests: called once per pass, between the searches and the finish
+    void* pass_hook_ctx_ = nullptr;
+    // tickets that left the matchmaker since the last drain (Remove*, replaced
+    // ids, matched): the Go shim drops its delivery entries with them
+    bool track_removed_ = false;
+    std::vector<std::string> removed_ids_;
+    std::unordered_map<const char* const*, std::vector<std::string>*> str_lists_;  // outstanding drains
+    std::mutex process_mu_;  // one pass at a time (the ticker); lock order process_mu_ -> mu_
+    int remove_session_locked(const std::string& sid, const std::string& ticket);
+    int remove_session_all_locked(const std::string& sid);
+    int remove_party_locked(const std::string& pid, const std::string& ticket);
+    int remove_party_all_locked(const std::string& pid);
+    int remove_all_locked(const std::string& node);
+    int remove_locked(const std::vector<std::string>& ids);
+    void restore_alive_on_device(const std::vector<uint32_t>& slots);
 
     // ---- store ----
     int add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_insert);
@@ -405,7 +477,7 @@ private:
     uint32_t termset_of(const HostClause& c);  // interned regexp/wildcard/fuzzy matcher
     void refresh_termsets();                   // extends accepted sets over new dictionary terms, uploads
     void set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val);
-    void kill_slot(uint32_t slot, bool device_cleared = false);  // ticket leaves the index and the maps
+    void kill_slot(uint32_t slot, bool device_cleared = false, bool replaced = false);  // ticket leaves the index and the maps
     const char* arena_string(const std::string& s);
     void maybe_compact();
     void compact();

@@ -655,9 +655,12 @@ __global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restr
     }
 }
 
-__global__ void clear_alive_kernel(uint8_t* __restrict__ alive, const uint32_t* __restrict__ slots, uint32_t n) {
+// Sets the device alive flag of the listed slots (0: selected / removed; 1:
+// restored, for the members of a group the post-pass re-check dropped).
+__global__ void clear_alive_kernel(uint8_t* __restrict__ alive, const uint32_t* __restrict__ slots, uint32_t n,
+                                   uint8_t value) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) alive[slots[i]] = 0;
+    if (i < n) alive[slots[i]] = value;
 }
 
 // validateMatch for explicit (from, to) pairs: does `to`'s document match
@@ -719,9 +722,10 @@ hipError_t launch_search(const DStore& st, const DGroup* d_groups, int n_groups,
     return hipGetLastError();
 }
 
-hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_t n, hipStream_t stream) {
+hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_t n, hipStream_t stream,
+                              uint8_t value) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(clear_alive_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_alive, d_slots, n);
+    hipLaunchKernelGGL(clear_alive_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_alive, d_slots, n, value);
     return hipGetLastError();
 }
 

@@ -1205,8 +1205,11 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
         std::vector<uint32_t> order(ngr);
         for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
         bool removed = false;
+        std::vector<uint32_t> restore;
         for (size_t i = 0; i < order.size(); i++) {
             if (incomplete[order[i]]) {
+                for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
+                    if (e->first != kNoSlot && live_[e->first]) restore.push_back(e->first);
                 order[i] = order.back();
                 order.pop_back();
                 removed = true;
@@ -1217,6 +1220,7 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
             GroupList kept;
             for (uint32_t g : order) kept.push(groups.begin(g), groups.end(g));
             groups = std::move(kept);
+            restore_alive_on_device(restore);
         }
         // Retire the matched tickets.  When no session or party holds more
         // than one ticket, each slot's bookkeeping touches keys no other slot
@@ -1224,12 +1228,14 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
         if (sess_slots_.more.empty() && party_slots_.more.empty()) {
             const size_t ng2 = groups.size();
             std::vector<uint32_t> killed(nchunk, 0);
+            std::vector<std::vector<std::string>> gone(track_removed_ ? nchunk : 0);
             wp.run(nchunk, [&](size_t c) {
                 uint32_t k = 0;
                 const size_t e0 = groups.off[ng2 * c / nchunk], e1 = groups.off[ng2 * (c + 1) / nchunk];
                 for (size_t i = e0; i < e1; i++) {
                     const uint32_t s = groups.ents[i].first;
                     if (!live_[s]) continue;  // a ticket's presence entries repeat its slot
+                    if (track_removed_) gone[c].push_back(ticket_[s]);
                     live_[s] = 0;
                     is_active_[s] = 0;
                     k++;
@@ -1239,6 +1245,7 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
                 killed[c] = k;
             });
             for (uint32_t k : killed) n_live_ -= k;
+            for (auto& v : gone) removed_ids_.insert(removed_ids_.end(), v.begin(), v.end());
         } else {
             for (auto& e : groups.ents) kill_slot(e.first, true);
         }
@@ -1252,11 +1259,14 @@ void Core::finish_pass_serial(GroupList& groups) {
     std::vector<uint32_t> order(groups.size());
     for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
     bool removed = false;
+    std::vector<uint32_t> restore;  // live members of dropped groups
     for (size_t i = 0; i < order.size(); i++) {
         bool incomplete = false;
         for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
             if (e->first == kNoSlot || !live_[e->first]) { incomplete = true; break; }
         if (incomplete) {  // swap-remove (:337-341)
+            for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
+                if (e->first != kNoSlot && live_[e->first]) restore.push_back(e->first);
             order[i] = order.back();
             order.pop_back();
             removed = true;
@@ -1270,6 +1280,11 @@ void Core::finish_pass_serial(GroupList& groups) {
         for (uint32_t g : order) kept.push(groups.begin(g), groups.end(g));
         groups = std::move(kept);
     }
+    // a member retired by a later group of this pass stays retired
+    std::vector<uint32_t> still;
+    for (uint32_t s : restore)
+        if (live_[s]) still.push_back(s);
+    restore_alive_on_device(still);
 }
 
 void Core::fill_matched(const GroupList& groups, mm_matched* out,
@@ -1353,7 +1368,8 @@ void Core::free_matched(mm_matched* out) {
 int Core::process(mm_matched* out) {
     std::memset(out, 0, sizeof(*out));
     const auto t0 = std::chrono::steady_clock::now();
-    std::lock_guard<std::mutex> lk(mu_);
+    std::unique_lock<std::mutex> pl(process_mu_);
+    std::unique_lock<std::mutex> lk(mu_);
     if (custom_open_) return MM_ERR_STATE;
     bool any_active = false;
     for (uint32_t s : active_list_)
@@ -1375,14 +1391,26 @@ int Core::process(mm_matched* out) {
     std::vector<uint32_t>& expired = expired_;
     expired.clear();
     PassStats stats;
+    // the snapshot is taken: mutators queue until the pass ends (matchmaker.go:309)
+    pass_running_ = true;
+    lk.unlock();
+    auto hook = [&] {
+        if (pass_hook_) pass_hook_(pass_hook_ctx_);
+    };
     if (cfg_.override_enabled) {
         process_custom(groups, expired, stats);
+        hook();
+        lk.lock();
         out->n_expired = (int32_t)expired.size();
         if (groups.empty()) {
+            apply_pending();
             GroupList none;
             finish_pass(expired, none, true);
+            pass_running_ = false;
             fill_matched(none, out, false);
         } else {
+            // the pass stays open (mutators keep queueing) until
+            // mm_process_commit hands back the override's choice
             custom_open_ = true;
             custom_expired_ = expired;
             fill_matched(groups, out, true);
@@ -1390,9 +1418,13 @@ int Core::process(mm_matched* out) {
     } else {
         const auto t1 = std::chrono::steady_clock::now();
         process_default(groups, expired, stats);
+        hook();
         const auto t2 = std::chrono::steady_clock::now();
+        lk.lock();  // matchmaker.go:320
         out->n_expired = (int32_t)expired.size();
+        apply_pending();
         finish_pass(expired, groups, true);
+        pass_running_ = false;
         const auto t3 = std::chrono::steady_clock::now();
         fill_matched(groups, out, false);
         const auto t4 = std::chrono::steady_clock::now();
@@ -1425,8 +1457,12 @@ int Core::process(mm_matched* out) {
 
 int Core::process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t n_groups, mm_matched* out) {
     std::memset(out, 0, sizeof(*out));
+    std::lock_guard<std::mutex> pl(process_mu_);
     std::lock_guard<std::mutex> lk(mu_);
     if (!custom_open_) return MM_ERR_STATE;
+    // the mutations queued while the pass was open come first: a chosen
+    // group that lost a ticket is then dropped by the re-check (:326-341)
+    apply_pending();
     GroupList groups;
     for (int g = 0; g < n_groups; g++) {
         std::vector<std::pair<uint32_t, int>> grp;
@@ -1442,6 +1478,7 @@ int Core::process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t 
     std::vector<uint32_t> exp = custom_expired_;
     finish_pass(exp, groups, false);
     custom_open_ = false;
+    pass_running_ = false;
     custom_expired_.clear();
     fill_matched(groups, out, false);
     return MM_OK;
@@ -1503,6 +1540,7 @@ extern "C" int mm_debug_compile(const char* query) {
 namespace nkm {
 
 int32_t Core::debug_hits(const std::string& ticket, const char** tk, double* sc, int32_t cap) {
+    std::lock_guard<std::mutex> pl(process_mu_);  // the pass owns the stream and the device buffers
     std::lock_guard<std::mutex> lk(mu_);
     int64_t T = slot_of_ticket(ticket);
     if (T < 0) return -1;

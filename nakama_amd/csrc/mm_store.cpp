@@ -476,8 +476,9 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
     return id;
 }
 
-void Core::kill_slot(uint32_t s, bool device_cleared) {
+void Core::kill_slot(uint32_t s, bool device_cleared, bool replaced) {
     if (!live_[s]) return;
+    if (track_removed_ && !replaced) removed_ids_.push_back(ticket_[s]);  // a replaced id lives on
     live_[s] = 0;
     is_active_[s] = 0;
     n_live_--;
@@ -495,7 +496,7 @@ void Core::kill_slot(uint32_t s, bool device_cleared) {
 int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_insert) {
     const std::string tk = t.ticket ? t.ticket : "";
     int64_t existing = slot_of_ticket(tk);
-    if (existing >= 0) kill_slot((uint32_t)existing);  // same ticket id re-inserted: replace
+    if (existing >= 0) kill_slot((uint32_t)existing, false, true);  // same ticket id re-inserted: replace
     const uint32_t s = (uint32_t)ticket_.size();
     Cold cold;
     cold.session_id = t.session_id ? t.session_id : "";
@@ -599,18 +600,171 @@ int Core::add(const mm_ticket& t) {
         }
     }
     std::lock_guard<std::mutex> lk(mu_);
-    if (custom_open_) return MM_ERR_STATE;
-    for (int i = 0; i < t.n_presences; i++) {
-        int64_t sid = sess_dict_.find(t.presences[i].session_id ? t.presences[i].session_id : "");
-        if (sid >= 0 && (int)sess_slots_.count((uint32_t)sid) >= cfg_.max_tickets) return MM_ERR_TOO_MANY_TICKETS;
-    }
+    // MaxTickets per session / party (matchmaker.go:505-520), against the
+    // effective state while a pass runs
+    for (int i = 0; i < t.n_presences; i++)
+        if (eff_sess_count(t.presences[i].session_id ? t.presences[i].session_id : "") >= cfg_.max_tickets)
+            return MM_ERR_TOO_MANY_TICKETS;
     std::string party = t.party_id ? t.party_id : "";
-    if (!party.empty()) {
-        int64_t pid = party_dict_.find(party);
-        if (pid >= 0 && (int)party_slots_.count((uint32_t)pid) >= cfg_.max_tickets) return MM_ERR_TOO_MANY_TICKETS;
+    if (!party.empty() && eff_party_count(party) >= cfg_.max_tickets) return MM_ERR_TOO_MANY_TICKETS;
+    if (pass_running_) {
+        PendingOp op{P_ADD};
+        op.tickets.emplace_back(t);
+        op.cqs.push_back(std::move(cq));
+        op.ok.push_back(1);
+        eff_add(op.tickets.back());
+        pending_.push_back(std::move(op));
+        return MM_OK;
     }
     maybe_compact();
     return add_locked(t, cq, false);
+}
+
+// ---- the effective state while a pass runs (see mm_core.h) ----
+Core::OwnedTicket::OwnedTicket(const mm_ticket& t) {
+    auto S = [](const char* p) { return p ? std::string(p) : std::string(); };
+    ticket = S(t.ticket);
+    session_id = S(t.session_id);
+    party_id = S(t.party_id);
+    query = S(t.query);
+    node = S(t.node);
+    min_count = t.min_count;
+    max_count = t.max_count;
+    count_multiple = t.count_multiple;
+    intervals = t.intervals;
+    created_at = t.created_at;
+    for (int i = 0; i < t.n_presences; i++)
+        presences.push_back({S(t.presences[i].user_id), S(t.presences[i].session_id), S(t.presences[i].username),
+                             S(t.presences[i].node)});
+    for (int i = 0; i < t.n_str_props; i++) sprops.push_back({S(t.str_props[i].key), S(t.str_props[i].value)});
+    for (int i = 0; i < t.n_num_props; i++) nprops.push_back({S(t.num_props[i].key), t.num_props[i].value});
+}
+
+void Core::OwnedTicket::view(View& v) const {
+    v.p.clear();
+    v.s.clear();
+    v.n.clear();
+    for (auto& p : presences)
+        v.p.push_back({p.user_id.c_str(), p.session_id.c_str(), p.username.c_str(), p.node.c_str()});
+    for (auto& kv : sprops) v.s.push_back({kv.first.c_str(), kv.second.c_str()});
+    for (auto& kv : nprops) v.n.push_back({kv.first.c_str(), kv.second});
+    v.t = mm_ticket{ticket.c_str(), session_id.c_str(), party_id.c_str(), query.c_str(), min_count, max_count,
+                    count_multiple, intervals, created_at, node.c_str(), v.p.data(), (int32_t)v.p.size(),
+                    v.s.data(), (int32_t)v.s.size(), v.n.data(), (int32_t)v.n.size()};
+}
+
+Core::PendTk* Core::eff_ticket(const std::string& id) {
+    auto it = pend_tk_.find(id);
+    if (it != pend_tk_.end()) return &it->second;
+    const int64_t s = slot_of_ticket(id);
+    if (s < 0) return nullptr;
+    PendTk t;
+    t.alive = true;
+    const Cold& c = cold_[s];
+    t.session_id = c.session_id;
+    t.party_id = c.party_id;
+    t.node = c.node;
+    for (auto& p : c.presences)
+        if (std::find(t.sessions.begin(), t.sessions.end(), p.session_id) == t.sessions.end())
+            t.sessions.push_back(p.session_id);
+    return &pend_tk_.emplace(id, std::move(t)).first->second;
+}
+
+void Core::eff_remove(PendTk& t) {
+    if (!t.alive) return;
+    t.alive = false;
+    for (auto& s : t.sessions) pend_sess_[s]--;
+    if (!t.party_id.empty()) pend_party_[t.party_id]--;
+}
+
+void Core::eff_add(const OwnedTicket& ot) {
+    if (PendTk* old = eff_ticket(ot.ticket)) eff_remove(*old);  // same id: replaced
+    PendTk t;
+    t.alive = true;
+    t.session_id = ot.session_id;
+    t.party_id = ot.party_id;
+    t.node = ot.node;
+    for (auto& p : ot.presences)
+        if (std::find(t.sessions.begin(), t.sessions.end(), p.session_id) == t.sessions.end())
+            t.sessions.push_back(p.session_id);
+    for (auto& s : t.sessions) pend_sess_[s]++;
+    if (!t.party_id.empty()) pend_party_[t.party_id]++;
+    pend_tk_[ot.ticket] = std::move(t);
+}
+
+int Core::eff_sess_count(const std::string& sid) {
+    const int64_t id = sess_dict_.find(sid);
+    int n = id >= 0 ? (int)sess_slots_.count((uint32_t)id) : 0;
+    if (pass_running_) {
+        auto it = pend_sess_.find(sid);
+        if (it != pend_sess_.end()) n += it->second;
+    }
+    return n;
+}
+
+int Core::eff_party_count(const std::string& pid) {
+    const int64_t id = party_dict_.find(pid);
+    int n = id >= 0 ? (int)party_slots_.count((uint32_t)id) : 0;
+    if (pass_running_) {
+        auto it = pend_party_.find(pid);
+        if (it != pend_party_.end()) n += it->second;
+    }
+    return n;
+}
+
+// The queued mutations, in arrival order, against the store as the pass
+// found it (their statuses were decided against that same state).
+void Core::apply_pending() {
+    for (PendingOp& op : pending_) {
+        switch (op.kind) {
+        case P_ADD:
+        case P_INSERT: {
+            OwnedTicket::View v;
+            for (size_t i = 0; i < op.tickets.size(); i++) {
+                if (!op.ok[i]) continue;
+                op.tickets[i].view(v);
+                add_locked(v.t, op.cqs[i], op.kind == P_INSERT);
+            }
+            break;
+        }
+        case P_REMOVE_SESSION: remove_session_locked(op.a, op.b); break;
+        case P_REMOVE_SESSION_ALL: remove_session_all_locked(op.a); break;
+        case P_REMOVE_PARTY: remove_party_locked(op.a, op.b); break;
+        case P_REMOVE_PARTY_ALL: remove_party_all_locked(op.a); break;
+        case P_REMOVE_ALL: remove_all_locked(op.a); break;
+        case P_REMOVE: remove_locked(op.ids); break;
+        }
+    }
+    pending_.clear();
+    pend_tk_.clear();
+    pend_sess_.clear();
+    pend_party_.clear();
+}
+
+int Core::drain_removed(mm_str_list* out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    track_removed_ = true;
+    auto* v = new std::vector<std::string>(std::move(removed_ids_));
+    removed_ids_.clear();
+    auto* ptrs = new const char*[v->empty() ? 1 : v->size()];
+    for (size_t i = 0; i < v->size(); i++) ptrs[i] = (*v)[i].c_str();
+    out->n = (int32_t)v->size();
+    out->items = ptrs;
+    str_lists_[ptrs] = v;
+    return MM_OK;
+}
+
+void Core::free_str_list(mm_str_list* out) {
+    if (!out || !out->items) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = str_lists_.find(out->items);
+    if (it != str_lists_.end()) {
+        delete it->second;
+        str_lists_.erase(it);
+    }
+    delete[] out->items;
+    out->items = nullptr;
+    out->n = 0;
 }
 
 // Insert (matchmaker.go:567-682): queries that fail to parse are skipped.
@@ -621,7 +775,18 @@ int Core::insert(const mm_ticket* ts, int32_t n) {
     std::vector<CompiledQuery> cqs((size_t)n);
     std::vector<uint8_t> ok((size_t)n, 0);
     std::lock_guard<std::mutex> lk(mu_);  // also serialises use of the worker pool
-    if (custom_open_) return MM_ERR_STATE;
+    if (pass_running_) {  // queued (the pass owns the workers)
+        PendingOp op{P_INSERT};
+        op.tickets.reserve((size_t)n);
+        for (int i = 0; i < n; i++) {
+            op.tickets.emplace_back(ts[i]);
+            op.ok.push_back(compile_query(ts[i].query ? ts[i].query : "", &cqs[i]) == CQ_OK);
+            if (op.ok.back()) eff_add(op.tickets.back());
+        }
+        op.cqs = std::move(cqs);
+        pending_.push_back(std::move(op));
+        return MM_OK;
+    }
     // query compiles are independent: spread large batches over the host workers
     auto compile_range = [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; i++) ok[i] = compile_query(ts[i].query ? ts[i].query : "", &cqs[i]) == CQ_OK;
@@ -656,6 +821,7 @@ int Core::extract(mm_extract_list* out) {
     out->n = 0;
     out->tickets = nullptr;
     if (stopped_) return MM_OK;
+    std::lock_guard<std::mutex> pl(process_mu_);  // a running pass writes Intervals
     std::lock_guard<std::mutex> lk(mu_);
     std::vector<uint32_t> v;
     for (uint32_t s = 0; s < ticket_.size(); s++)
@@ -710,6 +876,14 @@ void Core::free_extract(mm_extract_list* out) {
 // RemoveSession (matchmaker.go:725-767)
 int Core::remove_session(const std::string& sid, const std::string& ticket) {
     std::lock_guard<std::mutex> lk(mu_);
+    if (!pass_running_) return remove_session_locked(sid, ticket);
+    PendTk* t = eff_ticket(ticket);
+    if (!t || !t->alive || !t->party_id.empty() || t->session_id != sid) return MM_ERR_TICKET_NOT_FOUND;
+    eff_remove(*t);
+    pending_.push_back(PendingOp{P_REMOVE_SESSION, {}, {}, {}, sid, ticket, {}});
+    return MM_OK;
+}
+int Core::remove_session_locked(const std::string& sid, const std::string& ticket) {
     int64_t s = slot_of_ticket(ticket);
     if (s < 0 || !cold_[s].party_id.empty() || cold_[s].session_id != sid) return MM_ERR_TICKET_NOT_FOUND;
     kill_slot((uint32_t)s);
@@ -719,6 +893,18 @@ int Core::remove_session(const std::string& sid, const std::string& ticket) {
 // RemoveSessionAll (matchmaker.go:769-828)
 int Core::remove_session_all(const std::string& sid) {
     std::lock_guard<std::mutex> lk(mu_);
+    if (!pass_running_) return remove_session_all_locked(sid);
+    const int64_t id = sess_dict_.find(sid);
+    if (id >= 0)
+        for (uint32_t s : sess_slots_.list((uint32_t)id))
+            if (PendTk* t = eff_ticket(ticket_[s])) eff_remove(*t);
+    for (auto& kv : pend_tk_)
+        if (kv.second.alive && std::find(kv.second.sessions.begin(), kv.second.sessions.end(), sid) != kv.second.sessions.end())
+            eff_remove(kv.second);
+    pending_.push_back(PendingOp{P_REMOVE_SESSION_ALL, {}, {}, {}, sid, {}, {}});
+    return MM_OK;
+}
+int Core::remove_session_all_locked(const std::string& sid) {
     int64_t id = sess_dict_.find(sid);
     if (id < 0) return MM_OK;
     for (uint32_t s : sess_slots_.list((uint32_t)id)) kill_slot(s);
@@ -728,6 +914,14 @@ int Core::remove_session_all(const std::string& sid) {
 // RemoveParty (matchmaker.go:830-870)
 int Core::remove_party(const std::string& pid, const std::string& ticket) {
     std::lock_guard<std::mutex> lk(mu_);
+    if (!pass_running_) return remove_party_locked(pid, ticket);
+    PendTk* t = eff_ticket(ticket);
+    if (!t || !t->alive || !t->session_id.empty() || t->party_id != pid) return MM_ERR_TICKET_NOT_FOUND;
+    eff_remove(*t);
+    pending_.push_back(PendingOp{P_REMOVE_PARTY, {}, {}, {}, pid, ticket, {}});
+    return MM_OK;
+}
+int Core::remove_party_locked(const std::string& pid, const std::string& ticket) {
     int64_t s = slot_of_ticket(ticket);
     if (s < 0 || !cold_[s].session_id.empty() || cold_[s].party_id != pid) return MM_ERR_TICKET_NOT_FOUND;
     kill_slot((uint32_t)s);
@@ -737,6 +931,18 @@ int Core::remove_party(const std::string& pid, const std::string& ticket) {
 // RemovePartyAll (matchmaker.go:872-917)
 int Core::remove_party_all(const std::string& pid) {
     std::lock_guard<std::mutex> lk(mu_);
+    if (!pass_running_) return remove_party_all_locked(pid);
+    if (pid.empty()) return MM_OK;
+    const int64_t id = party_dict_.find(pid);
+    if (id >= 0)
+        for (uint32_t s : party_slots_.list((uint32_t)id))
+            if (PendTk* t = eff_ticket(ticket_[s])) eff_remove(*t);
+    for (auto& kv : pend_tk_)
+        if (kv.second.alive && kv.second.party_id == pid) eff_remove(kv.second);
+    pending_.push_back(PendingOp{P_REMOVE_PARTY_ALL, {}, {}, {}, pid, {}, {}});
+    return MM_OK;
+}
+int Core::remove_party_all_locked(const std::string& pid) {
     int64_t id = party_dict_.find(pid);
     if (id < 0 || pid.empty()) return MM_OK;
     for (uint32_t s : party_slots_.list((uint32_t)id)) kill_slot(s);
@@ -746,6 +952,16 @@ int Core::remove_party_all(const std::string& pid) {
 // RemoveAll (matchmaker.go:919-970)
 int Core::remove_all(const std::string& node) {
     std::lock_guard<std::mutex> lk(mu_);
+    if (!pass_running_) return remove_all_locked(node);
+    for (uint32_t s = 0; s < ticket_.size(); s++)
+        if (live_[s] && cold_[s].node == node)
+            if (PendTk* t = eff_ticket(ticket_[s])) eff_remove(*t);
+    for (auto& kv : pend_tk_)
+        if (kv.second.alive && kv.second.node == node) eff_remove(kv.second);
+    pending_.push_back(PendingOp{P_REMOVE_ALL, {}, {}, {}, node, {}, {}});
+    return MM_OK;
+}
+int Core::remove_all_locked(const std::string& node) {
     for (uint32_t s = 0; s < ticket_.size(); s++)
         if (live_[s] && cold_[s].node == node) kill_slot(s);
     return MM_OK;
@@ -753,9 +969,19 @@ int Core::remove_all(const std::string& node) {
 
 // Remove (matchmaker.go:972-1024)
 int Core::remove(const char* const* tickets, int32_t n) {
+    std::vector<std::string> ids;
+    ids.reserve((size_t)std::max(n, 0));
+    for (int i = 0; i < n; i++) ids.emplace_back(tickets[i] ? tickets[i] : "");
     std::lock_guard<std::mutex> lk(mu_);
-    for (int i = 0; i < n; i++) {
-        int64_t s = slot_of_ticket(tickets[i] ? tickets[i] : "");
+    if (!pass_running_) return remove_locked(ids);
+    for (auto& id : ids)
+        if (PendTk* t = eff_ticket(id)) eff_remove(*t);
+    pending_.push_back(PendingOp{P_REMOVE, {}, {}, {}, {}, {}, std::move(ids)});
+    return MM_OK;
+}
+int Core::remove_locked(const std::vector<std::string>& ids) {
+    for (auto& id : ids) {
+        int64_t s = slot_of_ticket(id);
         if (s >= 0) kill_slot((uint32_t)s);
     }
     return MM_OK;
@@ -1015,6 +1241,19 @@ DStore Core::dstore() const {
     st.tset_ids = d_tset_ids_.p;
     st.tset_sc = d_tset_sc_.p;
     return st;
+}
+
+// Members of a group the post-pass re-check dropped stay in the index, but
+// the pass had cleared their device alive flags when it selected them.
+void Core::restore_alive_on_device(const std::vector<uint32_t>& slots) {
+    if (slots.empty()) return;
+    h_slots_tmp_.reserve(slots.size());
+    std::memcpy(h_slots_tmp_.p, slots.data(), slots.size() * sizeof(uint32_t));
+    d_slots_tmp_.reserve(slots.size(), false);
+    NKM_HIP(hipMemcpyAsync(d_slots_tmp_.p, h_slots_tmp_.p, slots.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                           stream_));
+    NKM_HIP(launch_clear_alive(d_alive_.p, d_slots_tmp_.p, (uint32_t)slots.size(), stream_, 1));
+    NKM_HIP(hipStreamSynchronize(stream_));
 }
 
 void Core::apply_selected_to_device(const std::vector<uint32_t>& slots) {

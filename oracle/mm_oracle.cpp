@@ -585,6 +585,13 @@ struct Matchmaker {
     // open processCustom pass
     bool custom_open = false;
     vector<string> custom_expired;
+    // drained removals (mm_drain_removed): ids that left m.indexes
+    bool track_removed = false;
+    vector<string> removed;
+    void note_removed(const string& t) { if (track_removed) removed.push_back(t); }
+    // test hook: between processDefault/processCustom and the post-pass lock
+    void (*pass_hook)(void*) = nullptr;
+    void* pass_hook_ctx = nullptr;
     // output storage
     vector<string> out_strings;
     // debug hit strings / extract keep-alive
@@ -962,6 +969,7 @@ static void finish_pass(Matchmaker& m, const vector<string>& expired, vector<vec
         }
         for (auto& e : matched[i]) {
             const string t = e.idx->ticket;
+            if (m.indexes.count(t)) m.note_removed(t);
             m.indexes.erase(t);
             m.active_indexes.erase(t);
             m.rev_cache.erase(t);
@@ -1201,6 +1209,7 @@ int mm_remove_session(void* h, const char* session_id, const char* ticket) {  //
     if (it == m.indexes.end() || !it->second->party_id.empty() || it->second->session_id != session_id)
         return MM_ERR_TICKET_NOT_FOUND;
     IP ix = it->second;
+    m.note_removed(ix->ticket);
     m.indexes.erase(it);
     for (auto& p : ix->entries) erase_session_ticket(m, p.session_id, ix->ticket);
     if (!ix->party_id.empty()) erase_party_ticket(m, ix->party_id, ix->ticket);
@@ -1222,6 +1231,7 @@ int mm_remove_session_all(void* h, const char* session_id) {  // :769-828
         auto it = m.indexes.find(t);
         if (it == m.indexes.end()) continue;
         IP ix = it->second;
+        m.note_removed(t);
         m.indexes.erase(it);
         m.active_indexes.erase(t);
         m.rev_cache.erase(t);
@@ -1241,6 +1251,7 @@ int mm_remove_party(void* h, const char* party_id, const char* ticket) {  // :83
     if (it == m.indexes.end() || !it->second->session_id.empty() || it->second->party_id != party_id)
         return MM_ERR_TICKET_NOT_FOUND;
     IP ix = it->second;
+    m.note_removed(ix->ticket);
     m.indexes.erase(it);
     for (auto& p : ix->entries) erase_session_ticket(m, p.session_id, ix->ticket);
     erase_party_ticket(m, party_id, ix->ticket);
@@ -1262,6 +1273,7 @@ int mm_remove_party_all(void* h, const char* party_id) {  // :872-917
         auto it = m.indexes.find(t);
         if (it == m.indexes.end()) continue;
         IP ix = it->second;
+        m.note_removed(t);
         m.indexes.erase(it);
         m.active_indexes.erase(t);
         m.rev_cache.erase(t);
@@ -1272,6 +1284,7 @@ int mm_remove_party_all(void* h, const char* party_id) {  // :872-917
 
 static void remove_tickets(Matchmaker& m, const vector<IP>& v) {
     for (auto& ix : v) {
+        m.note_removed(ix->ticket);
         bluge_delete(m, ix->ticket);
         m.indexes.erase(ix->ticket);
         m.active_indexes.erase(ix->ticket);
@@ -1311,16 +1324,19 @@ int mm_process(void* h, mm_matched* out) {
     auto& m = *static_cast<Matchmaker*>(h);
     std::memset(out, 0, sizeof(*out));
     auto t0 = std::chrono::steady_clock::now();
-    std::lock_guard<std::mutex> lk(m.mu);
+    std::unique_lock<std::mutex> lk(m.mu);
     if (m.custom_open) return MM_ERR_STATE;
     if (m.active_indexes.empty()) { fill_matched(m, {}, out, false); return MM_OK; }
-    std::unordered_map<string, IP> indexes_copy = m.indexes;
+    std::unordered_map<string, IP> indexes_copy = m.indexes;  // snapshot (matchmaker.go:300-307)
     vector<IP> order = active_order(m);
     vector<vector<Entry>> matched;
     vector<string> expired;
     int64_t pe = 0;
+    lk.unlock();  // the pass runs unlocked (:309); mutators apply to the live maps meanwhile
     if (m.cfg.override_enabled) {
         process_custom(m, order, indexes_copy, matched, expired, &pe);
+        if (m.pass_hook) m.pass_hook(m.pass_hook_ctx);
+        lk.lock();
         out->n_expired = (int32_t)expired.size();
         if (matched.empty()) {
             // no candidates: the override is not called (:568-570)
@@ -1334,6 +1350,8 @@ int mm_process(void* h, mm_matched* out) {
         }
     } else {
         process_default(m, order, indexes_copy, matched, expired, &pe);
+        if (m.pass_hook) m.pass_hook(m.pass_hook_ctx);
+        lk.lock();  // :320
         out->n_expired = (int32_t)expired.size();
         finish_pass(m, expired, matched);
         fill_matched(m, matched, out, false);
@@ -1434,6 +1452,36 @@ int mm_debug_term_match(int32_t kind, const char* pattern, int32_t fuzziness, co
     if (!rx.matches(t)) return 0;
     *boost = 1.0;
     return 1;
+}
+
+int mm_drain_removed(void* h, mm_str_list* out) {
+    auto& m = *static_cast<Matchmaker*>(h);
+    std::lock_guard<std::mutex> lk(m.mu);
+    m.track_removed = true;
+    auto* v = new vector<string>(std::move(m.removed));
+    m.removed.clear();
+    auto* ptrs = new const char*[v->size() + 1];
+    for (size_t i = 0; i < v->size(); i++) ptrs[i] = (*v)[i].c_str();
+    ptrs[v->size()] = reinterpret_cast<const char*>(v);  // owner, after the last item
+    out->n = (int32_t)v->size();
+    out->items = ptrs;
+    return MM_OK;
+}
+
+void mm_free_str_list(void* h, mm_str_list* out) {
+    (void)h;
+    if (!out || !out->items) return;
+    delete reinterpret_cast<const vector<string>*>(out->items[out->n]);
+    delete[] out->items;
+    out->items = nullptr;
+    out->n = 0;
+}
+
+void mm_debug_set_pass_hook(void* h, void (*fn)(void*), void* ctx) {
+    auto& m = *static_cast<Matchmaker*>(h);
+    std::lock_guard<std::mutex> lk(m.mu);
+    m.pass_hook = fn;
+    m.pass_hook_ctx = ctx;
 }
 
 int mm_debug_compile(const char* query) {
