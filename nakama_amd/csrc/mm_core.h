@@ -468,7 +468,6 @@ private:
     int remove_party_all_locked(const std::string& pid);
     int remove_all_locked(const std::string& node);
     int remove_locked(const std::vector<std::string>& ids);
-    void restore_alive_on_device(const std::vector<uint32_t>& slots);
 
     // ---- store ----
     int add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_insert);
@@ -496,7 +495,9 @@ private:
     int process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                        PassStats& st);
     void finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, bool disjoint);
-    void finish_pass_serial(GroupList& groups);
+    // selected: the groups' tickets were deleted from the search index during
+    // the pass (processDefault), so members of a dropped group leave it
+    void finish_pass_serial(GroupList& groups, bool selected);
     void fill_matched(const GroupList& groups, mm_matched* out, bool cands);
     void choose_source(const Sig& s, DGroup& g, SrcChoice* ch = nullptr);
     bool replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
@@ -542,7 +543,11 @@ public:
     std::vector<int64_t> ckey_;       // sortable key of float64(CreatedAt)
     std::vector<int32_t> minc_, maxc_, cm_, count_, intervals_;
     std::vector<uint32_t> party_;     // kNoParty for ""
-    std::vector<uint8_t> live_;       // in m.indexes (and in the bluge index)
+    std::vector<uint8_t> live_;       // in m.indexes
+    // in the search index: 0 for the members of a group the post-pass re-check
+    // dropped (processDefault had deleted them from bluge when it selected
+    // them; they stay in m.indexes and can search, but are never found)
+    std::vector<uint8_t> indexed_;
     std::vector<uint8_t> is_active_;  // in m.activeIndexes
     std::vector<uint32_t> sig_;
     std::vector<HotRec> hot_;         // per slot: the replay's packed fields

@@ -1082,6 +1082,9 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                 }
                 const uint32_t H = g.hits[j].slot;
                 if (H == T || rp.same_party(T, H)) continue;
+                // a ticket an earlier processCustom pass retired is still in
+                // the search index, but not in indexesCopy: "missing index" (:432-437)
+                if (!live_[H]) continue;
                 if (rev && !g.rev[j]) continue;
                 if (maxc_[T] < maxc_[H] && intervals_[H] <= maxI) continue;
                 if (rp.share_session(T, H)) continue;
@@ -1190,7 +1193,7 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
     for (uint32_t s : expired) is_active_[s] = 0;
     const size_t ngr = groups.size();
     if (!disjoint || !par_mode_ || ngr < par_min(16384)) {
-        finish_pass_serial(groups);
+        finish_pass_serial(groups, disjoint);
     } else {
         WorkPool& wp = workers();
         const size_t nchunk = wp.size();
@@ -1205,11 +1208,13 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
         std::vector<uint32_t> order(ngr);
         for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
         bool removed = false;
-        std::vector<uint32_t> restore;
         for (size_t i = 0; i < order.size(); i++) {
             if (incomplete[order[i]]) {
+                // its members were deleted from the search index when the pass
+                // selected them (matchmaker_process.go:306-321) and stay out of
+                // it: they remain in m.indexes and may still search
                 for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
-                    if (e->first != kNoSlot && live_[e->first]) restore.push_back(e->first);
+                    if (e->first != kNoSlot && live_[e->first]) indexed_[e->first] = 0;
                 order[i] = order.back();
                 order.pop_back();
                 removed = true;
@@ -1220,7 +1225,6 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
             GroupList kept;
             for (uint32_t g : order) kept.push(groups.begin(g), groups.end(g));
             groups = std::move(kept);
-            restore_alive_on_device(restore);
         }
         // Retire the matched tickets.  When no session or party holds more
         // than one ticket, each slot's bookkeeping touches keys no other slot
@@ -1255,18 +1259,20 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
     active_list_.swap(list_tmp_);
 }
 
-void Core::finish_pass_serial(GroupList& groups) {
+void Core::finish_pass_serial(GroupList& groups, bool selected) {
     std::vector<uint32_t> order(groups.size());
     for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
     bool removed = false;
-    std::vector<uint32_t> restore;  // live members of dropped groups
     for (size_t i = 0; i < order.size(); i++) {
         bool incomplete = false;
         for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
             if (e->first == kNoSlot || !live_[e->first]) { incomplete = true; break; }
         if (incomplete) {  // swap-remove (:337-341)
-            for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
-                if (e->first != kNoSlot && live_[e->first]) restore.push_back(e->first);
+            // processDefault deleted the members from the search index when it
+            // selected them (matchmaker_process.go:306-321): they stay out of it
+            if (selected)
+                for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
+                    if (e->first != kNoSlot && live_[e->first]) indexed_[e->first] = 0;
             order[i] = order.back();
             order.pop_back();
             removed = true;
@@ -1280,11 +1286,6 @@ void Core::finish_pass_serial(GroupList& groups) {
         for (uint32_t g : order) kept.push(groups.begin(g), groups.end(g));
         groups = std::move(kept);
     }
-    // a member retired by a later group of this pass stays retired
-    std::vector<uint32_t> still;
-    for (uint32_t s : restore)
-        if (live_[s]) still.push_back(s);
-    restore_alive_on_device(still);
 }
 
 void Core::fill_matched(const GroupList& groups, mm_matched* out,

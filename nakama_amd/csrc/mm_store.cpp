@@ -522,6 +522,7 @@ int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_inse
     uint32_t party = cold.party_id.empty() ? kNoParty : party_dict_.intern(cold.party_id);
     party_.push_back(party);
     live_.push_back(1);
+    indexed_.push_back(1);
     bool act = from_insert ? (t.intervals < cfg_.max_intervals) : true;
     is_active_.push_back(act ? 1 : 0);
     if (pres_off_.empty()) pres_off_.push_back(0);
@@ -1047,7 +1048,7 @@ void Core::compact() {
     pres_sess_ = std::move(npsess);
     sess_dict_ = std::move(nsess);
     keep(ticket_); keep(created_); keep(ckey_); keep(minc_); keep(maxc_); keep(cm_); keep(count_);
-    keep(intervals_); keep(party_); keep(is_active_); keep(sig_); keep(cold_); keep(squery_);
+    keep(intervals_); keep(party_); keep(is_active_); keep(sig_); keep(cold_); keep(squery_); keep(indexed_);
     for (size_t f = 0; f < fval_.size(); f++) {
         if (fval_[f].size() == n) { keep(fval_[f]); keep(fkind_[f]); }
     }
@@ -1174,7 +1175,12 @@ void Core::sync_device() {
             NKM_HIP(hipMemcpyAsync(dst + from, src + from, (to - from) * sizeof(*src), hipMemcpyHostToDevice, stream_));
     };
     if (dev_slots_ < n) {
-        up(d_alive_.p, live_.data(), dev_slots_, n);
+        // device alive = in the search index: in m.indexes and not a dropped
+        // group's member (indexed_)
+        std::vector<uint8_t> alive(n - dev_slots_);
+        for (size_t s = dev_slots_; s < n; s++) alive[s - dev_slots_] = live_[s] & indexed_[s];
+        NKM_HIP(hipMemcpyAsync(d_alive_.p + dev_slots_, alive.data(), alive.size(), hipMemcpyHostToDevice, stream_));
+        NKM_HIP(hipStreamSynchronize(stream_));  // the staging vector dies here
         up(d_minc_.p, minc_.data(), dev_slots_, n);
         up(d_maxc_.p, maxc_.data(), dev_slots_, n);
         up(d_party_.p, party_.data(), dev_slots_, n);
@@ -1241,19 +1247,6 @@ DStore Core::dstore() const {
     st.tset_ids = d_tset_ids_.p;
     st.tset_sc = d_tset_sc_.p;
     return st;
-}
-
-// Members of a group the post-pass re-check dropped stay in the index, but
-// the pass had cleared their device alive flags when it selected them.
-void Core::restore_alive_on_device(const std::vector<uint32_t>& slots) {
-    if (slots.empty()) return;
-    h_slots_tmp_.reserve(slots.size());
-    std::memcpy(h_slots_tmp_.p, slots.data(), slots.size() * sizeof(uint32_t));
-    d_slots_tmp_.reserve(slots.size(), false);
-    NKM_HIP(hipMemcpyAsync(d_slots_tmp_.p, h_slots_tmp_.p, slots.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                           stream_));
-    NKM_HIP(launch_clear_alive(d_alive_.p, d_slots_tmp_.p, (uint32_t)slots.size(), stream_, 1));
-    NKM_HIP(hipStreamSynchronize(stream_));
 }
 
 void Core::apply_selected_to_device(const std::vector<uint32_t>& slots) {
