@@ -4,26 +4,35 @@ active tickets (BASELINE.json metric), one interval pass per step.
 
 Workload (BASELINE.json configs[2]): 1,000,000 synthetic
 tickets per GPU, party sizes {1:60%,2:20%,3:10%,4:5%,5:5%} (~1.75M presences),
-8 pools (mode x region), query = own pool, MinCount=MaxCount=10,
-CountMultiple=5, MaxIntervals=2.  A step = insert a fresh ticket set (untimed:
-the tickets are resident in HBM before the timed region starts), then ONE
-timed LocalMatchmaker.Process() through the C ABI — device searches, the
-greedy replay and all post-pass bookkeeping.
+8 pools (mode x region) per GPU, query = own pool, MinCount=MaxCount=10,
+CountMultiple=5, MaxIntervals=2.  A step = insert a fresh ticket set
+(untimed: the tickets are resident in HBM before the timed region starts),
+then ONE timed Process() through the C ABI — device searches, the greedy
+replay and all post-pass bookkeeping.
 
-Multi-GPU (torchrun, one process per GPU): every rank owns a disjoint ticket
-set (its own pools) — the pass partitions by pool with no data-path
-collective — so scaling is weak; the timed region of each step is bracketed
-by a barrier + device synchronize and the per-step time is the max over ranks.
-value = all ranks' matched tickets / sum of per-step max times.
+Multi-GPU (torchrun, one process per GPU, RCCL): ONE ticket set of N x 1M
+tickets over 8N pools (C3's pools times N, every pool spread over the whole
+index range) goes through the product's multi-GPU front
+(nakama_amd/cluster.py): each rank ingests a 1M slice, the front routes every
+ticket to its pool's rank (routing keys + one all-to-all of packed records,
+untimed like the single-GPU insert), and the timed step is the cluster-wide
+Process(): every rank's pass plus the merge of the ranks' group lists into the
+reference's group order (an all-gather of 8 B per group, merged on rank 0).
+Scaling is weak for C3 (1M per GPU); --config 4 (4M tickets over 64 pools in
+total) and --config 5 (1M in total) split one fixed set (strong).  Each step is
+bracketed by a barrier + device synchronize; its time is the max over ranks;
+value = all ranks' matched tickets / sum of the per-step max times.
 
 Also reported: roofline of the dominant query-eval kernel of the pass (the
-one with the most algorithmic bytes: mscan_kernel on C3; its algorithmic
-bytes per launch / its HIP-event launch time, vs 8 TB/s HBM), and the CPU
-baseline (the oracle restatement of the reference algorithm, single core,
-bounded prefix sample — see DESIGN.md).
+one with the most algorithmic bytes: mscan_kernel on C3; algorithmic bytes per
+launch / its HIP-event launch time, vs 8 TB/s HBM) with the PMC traffic of the
+same kernel from the committed rocprofv3 pass, and the CPU baseline (the
+oracle restatement of the reference algorithm: a timed prefix of the 1M pass,
+extrapolated to the whole pass as BASELINE.md prescribes — see cpu_baseline).
 """
 import argparse
 import json
+import math
 import os
 import statistics
 import sys
@@ -37,11 +46,16 @@ KERNELS = {0: "search_kernel", 1: "scan_kernel", 2: "mscan_kernel"}  # mm_matche
 WORKLOADS = {
     1: "C1: 10k solo 1v1, '+properties.mode:ranked +properties.region:eu'",
     2: "C2: skill-window range queries with ^boost, 1v1",
-    3: "C3: 1M tickets/GPU, 5v5 (Min=Max=10, CountMultiple=5), party tickets, 8 pools",
-    4: "C4: solo 1v1 over 64 mode x region pools",
-    5: "C5: RevPrecision, buckets of 8, Min=2 Max=4 (processDefault; no override registered)",
+    3: "C3: 1M tickets/GPU, 5v5 (Min=Max=10, CountMultiple=5), party tickets, 8 pools/GPU",
+    4: "C4: solo 1v1, 4M tickets over 64 mode x region pools (in total)",
+    5: "C5: RevPrecision, buckets of 8, Min=2 Max=4 (processDefault; no override registered), 1M in total",
     7: "C7: regexp / wildcard / fuzzy clauses (blocked lists, alternations, fuzzy map names)",
 }
+# the query fields a pool is keyed on (the cluster front's routing)
+POOL_FIELDS = {1: ("properties.mode", "properties.region"), 3: ("properties.mode", "properties.region"),
+               4: ("properties.mode", "properties.region"), 5: ("properties.bucket",)}
+DEFAULT_TICKETS = {4: 4_000_000}  # C4 is quoted on 4M in total; the others on 1M (per GPU for C3)
+STRONG = (4, 5)                   # configs whose ticket count is the whole job's
 
 
 def parse():
@@ -50,11 +64,15 @@ def parse():
     ap.add_argument("--steps", type=int, default=11)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=3)
-    ap.add_argument("--tickets", type=int, default=1_000_000, help="tickets per GPU per step")
+    ap.add_argument("--tickets", type=int, default=None,
+                    help="tickets per GPU per step (C3), or in total (C4, C5); default 1M (C4: 4M)")
     ap.add_argument("--cpu-rows", type=int, default=24, help="active rows in the CPU-baseline prefix sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
-    return ap.parse_args()
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_traffic.json"))
+    a = ap.parse_args()
+    if a.tickets is None:
+        a.tickets = DEFAULT_TICKETS.get(a.config, 1_000_000)
+    return a
 
 
 def dist_setup(args):
@@ -80,7 +98,7 @@ def dist_setup(args):
         else:
             dist.init_process_group(backend)
         pg = dist
-    return world, rank, local, pg
+    return world, rank, local, pg, backend
 
 
 def barrier_sync(pg, local):
@@ -103,101 +121,164 @@ def max_over_ranks(pg, local, x):
     return float(t.item())
 
 
-def sum_over_ranks(pg, local, x):
-    if pg is None:
-        return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64, device=_red_device(pg, local))
-    pg.all_reduce(t, op=pg.ReduceOp.SUM)
-    return float(t.item())
+def host_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return model, os.cpu_count(), usable
 
 
-def cpu_baseline(args):
-    """The oracle (oracle/mm_oracle.cpp: per-row full scan + full sort, the
-    reference's algorithm class) on one host core: the full 1M-ticket index
-    of the same workload, with only the first --cpu-rows tickets active (the
-    rest inserted with Intervals = MaxIntervals, i.e. searchable but not
-    searching).  Matched tickets / pass wall time."""
+def cpu_baseline(args, n_pools, searches, matched):
+    """The reference Go/bluge path cannot run here (no Go toolchain; SURVEY
+    §8(c)), so the baseline is the oracle restatement (oracle/mm_oracle.cpp:
+    the reference's per-row search + full sort + greedy walk), timed on this
+    host as BASELINE.md prescribes for C3: a prefix of the 1M-ticket pass (the
+    first --cpu-rows rows active, every row a full search of the 1M index),
+    extrapolated to the whole pass with the sum of c * P * log2 P over its
+    searches, P = the searching ticket's remaining pool (pools shrink linearly
+    as the pass consumes them; the search and group counts are the measured
+    pass's, identical to the reference's).  All-cores figure: pools are
+    independent, so per-pool passes run in parallel, ideally balanced over
+    min(pools, cores).  Both figures are EXTRAPOLATED, labelled so."""
     from nakama_amd import capi, synth
     lib = capi.load_library(os.path.join(ROOT, "oracle", "liboracle_mm.so"))
     ts = synth.TicketSet(args.config, args.tickets, first=0)
     for k in range(args.cpu_rows, ts.n):
         ts.tickets[k].intervals = 2
-    mm = capi.Matchmaker(lib, max_intervals=2)
+    mm = capi.Matchmaker(lib, max_intervals=2, rev_precision=args.config == 5)
     try:
         ts.insert_into(mm)
         t0 = time.perf_counter()
         r = mm.process_raw()
         dt = time.perf_counter() - t0
-        matched = sum(len({t for t, _ in g}) for g in r.groups)
+        pre_matched = sum(len({t for t, _ in g}) for g in r.groups)
     finally:
         mm.close()
         ts.close()
-    return {"value": matched / dt if dt > 0 else 0.0, "unit": "tickets/s", "cores": 1, "kind": "port",
-            "sample": f"oracle pass over the full {args.tickets}-ticket config-{args.config} index with the first "
-                      f"{args.cpu_rows} tickets active: {matched} tickets matched in {dt:.2f} s "
-                      f"({dt / max(1, args.cpu_rows) * 1e3:.0f} ms per searching ticket)",
-            "pass_s": dt, "matched": matched}
+    p0 = args.tickets / n_pools
+    c = (dt / args.cpu_rows) / (p0 * math.log2(p0))
+    per_pool_s, per_pool_m = searches / n_pools, matched / n_pools
+    steps = max(1, int(round(per_pool_s)))
+    total = 0.0
+    for k in range(steps):  # one pool's searches, pool shrinking linearly
+        p = max(2.0, p0 - per_pool_m * k / steps)
+        total += c * p * math.log2(p)
+    total *= per_pool_s / steps * n_pools
+    model, ncpu, usable = host_info()
+    par = min(n_pools, usable)
+    return {"value": matched / total, "unit": "tickets/s", "cores": 1, "kind": "port",
+            "sample": (f"EXTRAPOLATED: oracle prefix of the {args.tickets}-ticket config-{args.config} pass "
+                       f"({args.cpu_rows} searches over the full index, {dt:.2f} s, {pre_matched} tickets matched) "
+                       f"scaled by sum(c*P*log2 P) over the pass's {searches} searches in {n_pools} shrinking "
+                       f"pools -> {total:.0f} s for {matched} matched tickets on one core"),
+            "all_cores": {"value": matched / (total / par), "cores": par,
+                          "note": f"per-pool passes in parallel, ideal balance over min({n_pools} pools, "
+                                  f"{usable} usable cores)"},
+            "host": {"cpu_model": model, "nproc": ncpu, "usable_cores": usable},
+            "prefix_s": dt, "extrapolated_pass_s": total}
+
+
+def make_set(args, world, rank, step):
+    from nakama_amd import synth
+    strong = args.config in STRONG
+    total = args.tickets if strong else args.tickets * world
+    lo = step * total + total * rank // world
+    n = total * (rank + 1) // world - total * rank // world
+    if world == 1:
+        return synth.TicketSet(args.config, n, first=lo)
+    groups = world if args.config in (1, 2, 3) else None  # weak scaling: C3's pools times N
+    return synth.TicketSet(args.config, n, first=lo, pool_groups=groups)
 
 
 def main():
     args = parse()
-    world, rank, local, pg = dist_setup(args)
+    world, rank, local, pg, backend = dist_setup(args)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     import nakama_amd
-    from nakama_amd import synth
+    import torch
 
     mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config == 5)
-    # Pool sharding (weak scaling): the N-GPU workload is N disjoint instances
-    # of the config's pool set (region values suffixed per instance, so C3's
-    # 8 pools become 8N), and GPU r owns instance r whole — every GPU runs
-    # exactly the single-GPU workload, no ticket can match across GPUs, and
-    # the pass needs no data-path collective (DESIGN.md §7).
-    times, matched_all, presences_all, ins_times = [], [], [], []
+    cm = None
+    if world > 1:
+        from nakama_amd import cluster
+        cm = cluster.ClusterMatchmaker(mm, pg, POOL_FIELDS[args.config],
+                                       comm_device=torch.device("cuda", local) if backend == "nccl" else None)
+    times, matched_all, presences_all, ins_times, searched = [], [], [], [], []
     eval_ms = eval_bytes = launches = 0
-    batches, kernels = [], set()
+    batches, kernels, unroutable = [], set(), 0
     for step in range(args.warmup + args.steps):
-        first = (step * world + rank) * args.tickets
-        ts = (synth.TicketSet(args.config, args.tickets, first=first, shard=rank) if world > 1
-              else synth.TicketSet(args.config, args.tickets, first=first))
+        ts = make_set(args, world, rank, step)
         t_ins = time.perf_counter()
-        ts.insert_into(mm)  # untimed: one Insert() C-ABI call (store maintenance, index build, H2D upload)
+        if cm is None:
+            ts.insert_into(mm)  # untimed: one Insert() C-ABI call (store maintenance, index build, H2D upload)
+        else:
+            unroutable += len(cm.Insert(ts.ptr(), ts.n))  # untimed: route by pool, all-to-all, Insert()
         ins_dt = time.perf_counter() - t_ins
         barrier_sync(pg, local)
         t0 = time.perf_counter()
-        out = mm.process_call()  # the C-ABI call: one whole Process() pass
+        if cm is None:
+            out = mm.process_call()  # the C-ABI call: one whole Process() pass
+        else:
+            cp = cm.Process()        # every rank's pass + the merge into the reference's group order
         barrier_sync(pg, local)
         dt = time.perf_counter() - t0
-        n_groups, matched, pres, r = mm.process_summary(out)  # untimed: counts the groups, frees them
+        if cm is None:
+            n_groups, matched, pres, r = mm.process_summary(out)  # untimed: counts the groups, frees them
+            st = {"eval_ms": r.eval_ms, "eval_bytes": r.eval_bytes, "eval_launches": r.eval_launches,
+                  "n_batches": r.n_batches, "eval_kernel": r.eval_kernel}
+        else:
+            n_groups, matched, pres = cp.n_groups, cp.matched_tickets, cp.matched_presences
+            st = cp.local_stats
         ts.close()
         dt_max = max_over_ranks(pg, local, dt)
         if step >= args.warmup:
             times.append(dt_max)
             ins_times.append(max_over_ranks(pg, local, ins_dt))
-            matched_all.append(sum_over_ranks(pg, local, matched))
-            presences_all.append(sum_over_ranks(pg, local, pres))
-            eval_ms += r.eval_ms
-            eval_bytes += r.eval_bytes
-            launches += r.eval_launches
-            batches.append(r.n_batches)
-            kernels.add(KERNELS.get(r.eval_kernel, str(r.eval_kernel)))
-        # drain what is left so the next step starts from a fresh 1M set
+            matched_all.append(matched)
+            presences_all.append(pres)
+            # searches the pass ran: rows that were not yet selected when reached
+            searched.append(n_groups + mm.ticket_count())  # C3: every leftover searched too
+            eval_ms += st["eval_ms"]
+            eval_bytes += st["eval_bytes"]
+            launches += st["eval_launches"]
+            batches.append(st["n_batches"])
+            kernels.add(KERNELS.get(st["eval_kernel"], str(st["eval_kernel"])))
+        # drain what is left so the next step starts from a fresh set
         mm.Remove([t.ticket for t in mm.Extract()]) if mm.ticket_count() else None
     total_t = sum(times)
     value = sum(matched_all) / total_t
     achieved = (eval_bytes / 1e9) / (eval_ms / 1e3) if eval_ms > 0 else 0.0
     avg_launch_ms = eval_ms / max(1, launches)
-    # HBM bytes per launch from the PMC passes (tools/pmc_traffic.py), when
-    # they were taken on this kernel
-    traffic = None
+    # HBM bytes per launch from the PMC passes of the committed rocprofv3 run
+    # (tools/pmc_traffic.py) — not measured in this process, labelled so
+    traffic, traffic_src = None, None
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
             if tr.get("kernel") in kernels:
-                traffic = tr.get("bytes_per_launch")
+                traffic, traffic_src = tr.get("bytes_per_launch"), os.path.relpath(args.traffic, ROOT)
         except Exception:
             traffic = None
+    strong = args.config in STRONG
+    if world == 1:
+        par = "single GPU"
+    elif strong:
+        par = (f"pool-sharded x{world} through the cluster front: one set of {args.tickets} tickets, each rank "
+               f"ingests 1/{world} and the front routes tickets to their pool's rank")
+    else:
+        par = (f"pool-sharded x{world} through the cluster front: one set of {world}x{args.tickets} tickets over "
+               f"{world}x the config's pools, each rank ingests {args.tickets} and the front routes tickets to "
+               f"their pool's rank")
     out = {
         "metric": "tickets matched/sec + Process() interval p50 latency at 1M active tickets",
         "value": value,
@@ -213,21 +294,22 @@ def main():
         "insert_ms": 1e3 * statistics.median(ins_times),
         "with_insert_tickets_per_s": sum(matched_all) / (total_t + sum(ins_times)),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "int64/f64",
         "data": "synthetic",
-        "config": {"workload": WORKLOADS.get(args.config, str(args.config)), "tickets_per_gpu": args.tickets,
-                   "max_intervals": 2, "parallelism": f"pool-sharded x{world}: {world} disjoint pool sets, one per GPU",
-                   "matched_per_step": sum(matched_all) / args.steps, "batches_per_pass": batches},
+        "config": {"workload": WORKLOADS.get(args.config, str(args.config)),
+                   ("tickets_total" if strong else "tickets_per_gpu"): args.tickets,
+                   "max_intervals": 2, "parallelism": par, "unroutable": unroutable,
+                   "matched_per_step": sum(matched_all) / args.steps, "batches_per_pass_rank0": batches},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "+".join(sorted(kernels)), "launches": launches, "avg_launch_ms": avg_launch_ms,
-                     "bytes_per_launch": eval_bytes / max(1, launches)},
+                     "bytes_per_launch": eval_bytes / max(1, launches), "rank": 0},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(args)
-        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 3:
+        cb = cpu_baseline(args, 8, int(statistics.median(searched)), int(statistics.median(matched_all)))
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "all_cores", "host")}
     else:
         out["cpu_baseline"] = None
     mm.close()

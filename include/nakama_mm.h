@@ -125,6 +125,8 @@ typedef struct mm_matched {
     int32_t n_batches;              /* replay batches */
     int32_t eval_kernel;            /* query-eval kernel with the most bytes: 0 search, 1 scan, 2 mscan (ABI 2) */
     int32_t full_lists;             /* variable-score searches run as full lists (host-sorted), 0 for the oracle */
+    const int64_t* group_created;   /* n_groups: CreatedAt of each group's last entry (its searching ticket) — the
+                                       key a pool-sharded cluster merges rank results by (ABI 3) */
 } mm_matched;
 
 typedef struct mm_extract_list {

@@ -112,7 +112,8 @@ class mm_matched(C.Structure):
                 ("entries", C.POINTER(mm_entry_ref)), ("is_candidates", C.c_int32), ("n_expired", C.c_int32),
                 ("pass_ms", C.c_double), ("eval_ms", C.c_double), ("pair_evals", C.c_int64),
                 ("reserved2", C.c_int64), ("eval_bytes", C.c_int64), ("eval_launches", C.c_int32),
-                ("n_batches", C.c_int32), ("eval_kernel", C.c_int32), ("full_lists", C.c_int32)]
+                ("n_batches", C.c_int32), ("eval_kernel", C.c_int32), ("full_lists", C.c_int32),
+                ("group_created", C.POINTER(C.c_int64))]
 
 
 class mm_extract_list(C.Structure):

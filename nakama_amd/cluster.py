@@ -1,0 +1,336 @@
+"""One `server.Matchmaker` over the GPUs of a node: the pool-sharded front.
+
+The reference runs a single LocalMatchmaker per node; every Add/Insert/
+Remove* reaches it and one Process() pass covers every ticket
+(server/matchmaker.go:169-183, constructed at main.go:160).  Here one process
+per GPU holds a rank-local handle (libnakama_mm, `mm_config.device`) and
+`ClusterMatchmaker` keeps the single-instance contract over all of them.
+
+Routing (include/nakama_cluster.h).  A ticket belongs to the pool named by
+the keyword values its query requires on the configured pool fields, which
+must also be its own property values (`mm_route_keys`).  Searches of a pool
+only hit that pool's documents and only that pool's searches hit them, so the
+reference's pass over all tickets is the interleaving of independent per-pool
+passes (matchmaker_process.go:38-330: selection, Intervals and hit lists
+never cross a pool).  Whole pools are placed on ranks by a directory that
+every rank updates identically (online longest-processing-time: a new pool
+goes to the least-loaded rank), and tickets move to their owner with one
+all-to-all of packed records (RCCL over xGMI when the group is "nccl").
+
+Process.  Every rank runs its own pass — no data-path collective — and the
+reference's group order is recovered by merging the ranks' group lists on
+the searching ticket's (CreatedAt, Ticket) (`mm_merge_groups`; the keys come
+back in `mm_matched.group_created`): one all-gather of 8 B per group.  A
+group's tickets all live on one rank, which owns its delivery; rank 0 holds
+the global order (`ClusterPass.order`) and `gather_groups()` materialises the
+merged list for callers that need it whole (tests).
+
+Every method is a collective: all ranks call it, in the same order.  Tickets
+that are not partitionable on the pool fields (a query that does not pin a
+pool field to the ticket's own value) are returned to the caller by Insert
+and not inserted — a deployment with cross-pool queries uses the
+row-sharded mode instead.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PRODUCT_SO = os.path.join(ROOT, "nakama_amd", "libnakama_mm.so")
+
+_router = None
+
+
+def router_lib(path: str = PRODUCT_SO) -> C.CDLL:
+    """The routing entry points of include/nakama_cluster.h (host-only: they
+    load and run without a GPU)."""
+    global _router
+    if _router is None:
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        lib = C.CDLL(path, mode=C.RTLD_LOCAL)
+        lib.mm_route_keys.restype = C.c_int32
+        lib.mm_route_keys.argtypes = [C.POINTER(capi.mm_ticket), C.c_int32, C.POINTER(C.c_char_p), C.c_int32,
+                                      C.POINTER(C.c_uint64)]
+        lib.mm_pack_tickets.restype = C.c_int64
+        lib.mm_pack_tickets.argtypes = [C.POINTER(capi.mm_ticket), C.POINTER(C.c_int32), C.c_int32, C.c_void_p,
+                                        C.c_int64]
+        lib.mm_unpack_tickets.restype = C.c_void_p
+        lib.mm_unpack_tickets.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_int32),
+                                          C.POINTER(C.POINTER(capi.mm_ticket))]
+        lib.mm_free_unpacked.argtypes = [C.c_void_p]
+        lib.mm_merge_groups.restype = C.c_int32
+        lib.mm_merge_groups.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        _router = lib
+    return _router
+
+
+CLUSTER_SYMBOLS = ("mm_route_keys", "mm_pack_tickets", "mm_unpack_tickets", "mm_free_unpacked", "mm_merge_groups")
+
+
+def route_keys(tickets, n: int, pool_fields: Sequence[str]) -> np.ndarray:
+    """uint64 pool key per ticket (0: not partitionable on pool_fields)."""
+    L = router_lib()
+    keys = np.zeros(max(n, 1), dtype=np.uint64)
+    fs = (C.c_char_p * len(pool_fields))(*[f.encode() for f in pool_fields])
+    if n:
+        L.mm_route_keys(tickets, n, fs, len(pool_fields), keys.ctypes.data_as(C.POINTER(C.c_uint64)))
+    return keys[:n]
+
+
+def pack(tickets, idx: np.ndarray) -> np.ndarray:
+    L = router_lib()
+    idx = np.ascontiguousarray(idx, dtype=np.int32)
+    ip = idx.ctypes.data_as(C.POINTER(C.c_int32))
+    need = L.mm_pack_tickets(tickets, ip, len(idx), None, 0)
+    buf = np.empty(need, dtype=np.uint8)
+    got = L.mm_pack_tickets(tickets, ip, len(idx), buf.ctypes.data, need)
+    assert got == need
+    return buf
+
+
+class Unpacked:
+    """Tickets decoded from packed records (owned by the library until close)."""
+
+    def __init__(self, buf: np.ndarray):
+        L = router_lib()
+        self.n = C.c_int32(0)
+        self.tickets = C.POINTER(capi.mm_ticket)()
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        self.h = L.mm_unpack_tickets(buf.ctypes.data if len(buf) else None, len(buf), C.byref(self.n),
+                                     C.byref(self.tickets))
+        if not self.h:
+            raise ValueError("malformed ticket records")
+
+    def close(self):
+        if self.h:
+            router_lib().mm_free_unpacked(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class ClusterPass:
+    """One cluster-wide Process(): every rank's local result plus the global
+    group order (rank 0)."""
+    n_groups: int = 0              # all ranks
+    matched_tickets: int = 0       # all ranks
+    matched_presences: int = 0     # all ranks
+    local: Optional[capi.ProcessResult] = None   # this rank's groups (when kept)
+    order: Optional[np.ndarray] = None           # rank 0: (rank, local index) per global position
+    local_stats: Dict[str, float] = field(default_factory=dict)
+
+
+class ClusterMatchmaker:
+    """server.Matchmaker across the ranks of a torch.distributed group.
+
+    local: this rank's handle (capi.Matchmaker over libnakama_mm on this
+    rank's GPU, or any library with the same ABI); dist: torch.distributed
+    (initialised); pool_fields: the query fields a pool is keyed on, e.g.
+    ("properties.mode", "properties.region")."""
+
+    def __init__(self, local: capi.Matchmaker, dist, pool_fields: Sequence[str], *, comm_device=None):
+        self.local = local
+        self.dist = dist
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.pool_fields = list(pool_fields)
+        self.comm_device = comm_device  # torch.device for "nccl" tensors, None for host (gloo)
+        self.directory: Dict[int, int] = {}
+        self.load = [0] * self.world
+        self.owner_of: Dict[str, int] = {}  # rank 0, global override scope: ticket -> rank
+
+    # ---- collectives over tensors ----
+    def _t(self, arr: np.ndarray):
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(arr))
+        return t.to(self.comm_device) if self.comm_device is not None else t
+
+    def _host(self, t) -> np.ndarray:
+        return t.cpu().numpy() if self.comm_device is not None else t.numpy()
+
+    def _all_gather_var(self, arr: np.ndarray) -> Tuple[np.ndarray, List[int]]:
+        """Concatenation of every rank's 1-D array (ranks in order), and the counts."""
+        import torch
+        n = np.array([len(arr)], dtype=np.int64)
+        sizes = [self._t(np.zeros(1, dtype=np.int64)) for _ in range(self.world)]
+        self.dist.all_gather(sizes, self._t(n))
+        counts = [int(self._host(s)[0]) for s in sizes]
+        m = max(counts) if counts else 0
+        pad = np.zeros(max(m, 1), dtype=arr.dtype)
+        pad[:len(arr)] = arr
+        outs = [self._t(np.zeros(max(m, 1), dtype=arr.dtype)) for _ in range(self.world)]
+        self.dist.all_gather(outs, self._t(pad))
+        parts = [self._host(o)[:c] for o, c in zip(outs, counts)]
+        return (np.concatenate(parts) if parts else np.zeros(0, dtype=arr.dtype)), counts
+
+    def _all_to_all_bytes(self, send: np.ndarray, splits: List[int]) -> np.ndarray:
+        import torch
+        sizes_in = self._t(np.array(splits, dtype=np.int64))
+        sizes_out = self._t(np.zeros(self.world, dtype=np.int64))
+        self.dist.all_to_all_single(sizes_out, sizes_in)
+        out_splits = [int(x) for x in self._host(sizes_out)]
+        recv = self._t(np.zeros(max(sum(out_splits), 1), dtype=np.uint8))
+        self.dist.all_to_all_single(recv[:sum(out_splits)] if sum(out_splits) else recv[:0],
+                                    self._t(send) if len(send) else self._t(np.zeros(0, dtype=np.uint8)),
+                                    output_split_sizes=out_splits, input_split_sizes=splits)
+        return self._host(recv)[:sum(out_splits)]
+
+    # ---- routing ----
+    def _place_new_pools(self, keys: np.ndarray):
+        """Directory update, identical on every rank: the pools no rank had
+        seen, largest first, each to the least-loaded rank."""
+        ks = keys[keys != 0]
+        uniq, cnt = np.unique(ks, return_counts=True)
+        new = np.array([int(k) not in self.directory for k in uniq], dtype=bool) if len(uniq) else np.zeros(0, bool)
+        gathered = [None] * self.world
+        self.dist.all_gather_object(gathered, (uniq[new].tolist(), cnt[new].tolist()))
+        tot: Dict[int, int] = {}
+        for ks_r, cs_r in gathered:
+            for k, c in zip(ks_r, cs_r):
+                tot[int(k)] = tot.get(int(k), 0) + int(c)
+        for k in sorted(tot, key=lambda k: (-tot[k], k)):
+            r = min(range(self.world), key=lambda q: (self.load[q], q))
+            self.directory[k] = r
+            self.load[r] += tot[k]
+
+    def owners(self, keys: np.ndarray) -> np.ndarray:
+        """Owning rank of each pool key (-1: not partitionable / unknown)."""
+        own = np.full(len(keys), -1, dtype=np.int32)
+        if not self.directory or not len(keys):
+            return own
+        dk = np.fromiter(self.directory.keys(), dtype=np.uint64, count=len(self.directory))
+        dr = np.fromiter(self.directory.values(), dtype=np.int32, count=len(self.directory))
+        o = np.argsort(dk)
+        dk, dr = dk[o], dr[o]
+        pos = np.clip(np.searchsorted(dk, keys), 0, len(dk) - 1)
+        hit = (dk[pos] == keys) & (keys != 0)
+        own[hit] = dr[pos[hit]]
+        return own
+
+    def Insert(self, tickets, n: int) -> np.ndarray:
+        """Insert (matchmaker.go:567-682) of this rank's ingest batch (an
+        mm_ticket array): each ticket goes to its pool's rank.  Returns the
+        indexes of the tickets that are not partitionable (not inserted)."""
+        keys = route_keys(tickets, n, self.pool_fields)
+        self._place_new_pools(keys)
+        own = self.owners(keys)
+        order = np.argsort(own, kind="stable")
+        bounds = np.searchsorted(own[order], np.arange(self.world + 1), side="left")  # the -1s sort first
+        parts, splits = [], []
+        for r in range(self.world):
+            idx = order[bounds[r]:bounds[r + 1]]
+            buf = pack(tickets, idx) if len(idx) else np.zeros(0, dtype=np.uint8)
+            parts.append(buf)
+            splits.append(len(buf))
+        send = np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8)
+        recv = self._all_to_all_bytes(send, splits)
+        u = Unpacked(recv)
+        try:
+            if u.n.value:
+                self.local._check(self.local.lib.mm_insert(self.local.h, u.tickets, u.n.value))
+        finally:
+            u.close()
+        return np.nonzero(own < 0)[0]
+
+    # ---- the pass ----
+    def Process(self, keep_groups: bool = False) -> ClusterPass:
+        """One interval pass on every rank, and the reference's group order
+        over all of them (on rank 0).  keep_groups: also convert this rank's
+        groups to Python (tests, delivery)."""
+        out = self.local.process_call()
+        try:
+            ng = out.n_groups
+            keys = np.ctypeslib.as_array(out.group_created, (ng,)).copy() if ng else np.zeros(0, dtype=np.int64)
+            if keep_groups:
+                res = capi.ProcessResult(capi.Matchmaker._groups(out), bool(out.is_candidates), out.n_expired,
+                                         out.pass_ms, out.eval_ms, out.pair_evals, out.eval_bytes, out.eval_launches,
+                                         out.n_batches, out.eval_kernel, out.full_lists)
+                tie_ids = [g[-1][0] for g in res.groups]
+            else:
+                res, tie_ids = None, None
+            _, tickets, pres, stats = self.local.process_summary(out)
+            out = None
+        finally:
+            if out is not None:
+                self.local.lib.mm_free_matched(self.local.h, C.byref(out))
+        cp = ClusterPass(local=res)
+        cp.local_stats = {"pass_ms": stats.pass_ms, "eval_ms": stats.eval_ms, "eval_bytes": stats.eval_bytes,
+                          "eval_launches": stats.eval_launches, "n_batches": stats.n_batches,
+                          "eval_kernel": stats.eval_kernel}
+        allk, counts = self._all_gather_var(keys)
+        tot = self._t(np.array([ng, tickets, pres], dtype=np.int64))
+        self.dist.all_reduce(tot)
+        cp.n_groups, cp.matched_tickets, cp.matched_presences = (int(x) for x in self._host(tot))
+        ties = 0
+        if self.rank == 0:
+            cnt = np.array(counts, dtype=np.int32)
+            orank = np.zeros(max(len(allk), 1), dtype=np.int32)
+            oidx = np.zeros(max(len(allk), 1), dtype=np.int32)
+            ties = router_lib().mm_merge_groups(np.ascontiguousarray(allk).ctypes.data, cnt.ctypes.data, self.world,
+                                                orank.ctypes.data, oidx.ctypes.data)
+            cp.order = np.stack([orank[:len(allk)], oidx[:len(allk)]], axis=1)
+        flag = self._t(np.array([ties], dtype=np.int32))
+        self.dist.broadcast(flag, 0)
+        if int(self._host(flag)[0]):
+            self._order_ties(cp, allk, counts, tie_ids)
+        return cp
+
+    def _order_ties(self, cp: ClusterPass, allk: np.ndarray, counts: List[int], tie_ids):
+        """Equal CreatedAt on two ranks: those groups are ordered by their
+        searching ticket's id, the second key of the pinned active order."""
+        if tie_ids is None:
+            raise RuntimeError("equal CreatedAt across ranks: call Process(keep_groups=True) to order by ticket id")
+        gathered = [None] * self.world
+        self.dist.all_gather_object(gathered, tie_ids)
+        if self.rank != 0:
+            return
+        off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        o = cp.order
+        pos = sorted(range(len(o)), key=lambda p: (int(allk[off[o[p][0]] + o[p][1]]), gathered[o[p][0]][o[p][1]]))
+        cp.order = o[pos]
+
+    def gather_groups(self, cp: ClusterPass) -> Optional[List[List[Tuple[str, int]]]]:
+        """Rank 0: the merged group list in the reference's order (needs
+        Process(keep_groups=True) on every rank)."""
+        gathered = [None] * self.world
+        self.dist.all_gather_object(gathered, cp.local.groups if cp.local is not None else None)
+        if self.rank != 0:
+            return None
+        return [gathered[int(r)][int(i)] for r, i in cp.order]
+
+    # ---- mutators and state (routed or broadcast) ----
+    def ticket_count(self) -> int:
+        t = self._t(np.array([self.local.ticket_count()], dtype=np.int64))
+        self.dist.all_reduce(t)
+        return int(self._host(t)[0])
+
+    def active_count(self) -> int:
+        t = self._t(np.array([self.local.active_count()], dtype=np.int64))
+        self.dist.all_reduce(t)
+        return int(self._host(t)[0])
+
+    def Extract(self) -> Optional[List[capi.Ticket]]:
+        """Extract (matchmaker.go:684-723) of every rank, sorted by ticket (rank 0)."""
+        gathered = [None] * self.world
+        self.dist.all_gather_object(gathered, self.local.Extract())
+        if self.rank != 0:
+            return None
+        return sorted((t for ts in gathered for t in ts), key=lambda t: t.ticket)
+
+    def Remove(self, tickets: Sequence[str]):
+        """Remove (matchmaker.go:972-1024): ids may live on any rank; every
+        rank removes the ones it holds (the others are no-ops there)."""
+        self.local.Remove(list(tickets))

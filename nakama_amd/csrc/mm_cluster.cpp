@@ -1,0 +1,268 @@
+// nakama_amd/csrc/mm_cluster.cpp — routing keys and the ticket wire format of
+// the pool-sharded multi-GPU front (include/nakama_cluster.h, cluster.py).
+//
+// A pool is the set of tickets whose queries require the same keyword values
+// on the pool fields and whose own properties carry those values.  Searches
+// of pool P only hit documents with P's values, and only P's searches hit P's
+// documents, so processDefault / processCustom over all tickets is the
+// interleaving of independent per-pool passes (matchmaker_process.go:38-330:
+// selection, Intervals and the hit lists never cross a pool); the front
+// places whole pools on ranks.
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../../include/nakama_cluster.h"
+#include "gocompat.h"
+#include "qcompile.h"
+
+namespace {
+
+using nkm::CompiledQuery;
+
+uint64_t fnv1a(const std::string& s, uint64_t h) {
+    for (unsigned char c : s) {
+        h ^= c;
+        h *= 0x100000001B3ull;
+    }
+    return h;
+}
+
+// The document value of string property `key` as bluge indexes it
+// (blugeProcessProperty, match_common.go:148-212; numeric props win on a
+// key clash, matchmaker.go:460-466): true with the keyword when it is one.
+bool keyword_prop(const mm_ticket& t, const std::string& key, std::string* out) {
+    for (int i = 0; i < t.n_num_props; i++)
+        if (t.num_props[i].key && key == t.num_props[i].key) return false;
+    bool found = false;
+    for (int i = 0; i < t.n_str_props; i++) {
+        if (!t.str_props[i].key || key != t.str_props[i].key) continue;
+        *out = t.str_props[i].value ? t.str_props[i].value : "";
+        found = true;  // the last one wins, as the map build does
+    }
+    if (!found) return false;
+    int64_t ns;
+    return !nkm::bluge_datetime(*out, &ns);
+}
+
+uint64_t route_key(const mm_ticket& t, const std::vector<std::string>& fields) {
+    CompiledQuery cq;
+    if (nkm::compile_query(t.query ? t.query : "", &cq) != nkm::CQ_OK || cq.kind != nkm::QK_BOOL) return 0;
+    uint64_t h = 0xCBF29CE484222325ull;
+    for (const std::string& f : fields) {
+        static const std::string kProps = "properties.";
+        if (f.compare(0, kProps.size(), kProps) != 0) return 0;
+        std::string value;
+        if (!keyword_prop(t, f.substr(kProps.size()), &value)) return 0;
+        bool pinned = false;
+        for (const auto& c : cq.clauses) {
+            if (c.occur != nkm::OCC_MUST || c.field != f) continue;
+            if (c.op != nkm::OP_TERM && c.op != nkm::OP_NUMLIT) continue;
+            if (c.term != value) return 0;  // requires another pool's value
+            pinned = true;
+        }
+        if (!pinned) return 0;  // the search is not confined to one value of f
+        h = fnv1a(value, h);
+        h = fnv1a(std::string(1, '\0'), h);
+    }
+    return h | 1;  // 0 means "not partitionable"
+}
+
+// ---- wire format: per ticket a u32 record length, then fixed fields, then
+// NUL-terminated strings (so an unpacked ticket points into the buffer copy)
+struct Writer {
+    uint8_t* p;
+    int64_t cap, n = 0;
+    void raw(const void* v, size_t k) {
+        if (p && n + (int64_t)k <= cap) std::memcpy(p + n, v, k);
+        n += (int64_t)k;
+    }
+    template <class T>
+    void put(T v) { raw(&v, sizeof v); }
+    void str(const char* s) {
+        const uint32_t len = s ? (uint32_t)std::strlen(s) : 0;
+        put(len);
+        raw(s ? s : "", len);
+        put<char>('\0');
+    }
+};
+
+struct Unpacked {
+    std::vector<uint8_t> buf;
+    std::vector<mm_ticket> t;
+    std::vector<mm_presence> pres;
+    std::vector<mm_str_prop> sp;
+    std::vector<mm_num_prop> np;
+};
+
+struct Reader {
+    const uint8_t* p;
+    int64_t len, at = 0;
+    bool ok = true;
+    template <class T>
+    T get() {
+        T v{};
+        if (at + (int64_t)sizeof v > len) { ok = false; return v; }
+        std::memcpy(&v, p + at, sizeof v);
+        at += sizeof v;
+        return v;
+    }
+    const char* str() {
+        const uint32_t n = get<uint32_t>();
+        if (!ok || at + (int64_t)n + 1 > len || p[at + n] != 0) { ok = false; return ""; }
+        const char* s = (const char*)p + at;
+        at += n + 1;
+        return s;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int32_t mm_route_keys(const mm_ticket* ts, int32_t n, const char* const* pool_fields, int32_t n_fields,
+                      uint64_t* keys_out) {
+    if (n <= 0 || !ts || !keys_out || n_fields <= 0 || !pool_fields) return 0;
+    std::vector<std::string> fields;
+    for (int i = 0; i < n_fields; i++) fields.emplace_back(pool_fields[i] ? pool_fields[i] : "");
+    int32_t ok = 0;
+    for (int32_t i = 0; i < n; i++) {
+        try {
+            keys_out[i] = route_key(ts[i], fields);
+        } catch (...) {
+            keys_out[i] = 0;
+        }
+        ok += keys_out[i] != 0;
+    }
+    return ok;
+}
+
+int64_t mm_pack_tickets(const mm_ticket* ts, const int32_t* idx, int32_t n, uint8_t* buf, int64_t cap) {
+    Writer w{buf, cap};
+    for (int32_t k = 0; k < n; k++) {
+        const mm_ticket& t = ts[idx ? idx[k] : k];
+        const int64_t start = w.n;
+        w.put<uint32_t>(0);  // record length, patched below
+        w.put(t.min_count);
+        w.put(t.max_count);
+        w.put(t.count_multiple);
+        w.put(t.intervals);
+        w.put(t.created_at);
+        w.put(t.n_presences);
+        w.put(t.n_str_props);
+        w.put(t.n_num_props);
+        w.str(t.ticket);
+        w.str(t.session_id);
+        w.str(t.party_id);
+        w.str(t.query);
+        w.str(t.node);
+        for (int i = 0; i < t.n_presences; i++) {
+            w.str(t.presences[i].user_id);
+            w.str(t.presences[i].session_id);
+            w.str(t.presences[i].username);
+            w.str(t.presences[i].node);
+        }
+        for (int i = 0; i < t.n_str_props; i++) {
+            w.str(t.str_props[i].key);
+            w.str(t.str_props[i].value);
+        }
+        for (int i = 0; i < t.n_num_props; i++) {
+            w.str(t.num_props[i].key);
+            w.put(t.num_props[i].value);
+        }
+        const uint32_t rec = (uint32_t)(w.n - start);
+        if (buf && w.n <= cap) std::memcpy(buf + start, &rec, sizeof rec);
+    }
+    return w.n;
+}
+
+void* mm_unpack_tickets(const uint8_t* buf, int64_t len, int32_t* n_out, const mm_ticket** tickets_out) {
+    if ((!buf && len > 0) || len < 0 || !n_out || !tickets_out) return nullptr;
+    auto* u = new Unpacked();
+    u->buf.assign(buf, buf + len);
+    Reader r{u->buf.data(), len};
+    struct Tmp { size_t p0, s0, n0; };
+    std::vector<Tmp> tmp;
+    while (r.ok && r.at < len) {
+        const int64_t start = r.at;
+        const uint32_t rec = r.get<uint32_t>();
+        mm_ticket t{};
+        t.min_count = r.get<int32_t>();
+        t.max_count = r.get<int32_t>();
+        t.count_multiple = r.get<int32_t>();
+        t.intervals = r.get<int32_t>();
+        t.created_at = r.get<int64_t>();
+        t.n_presences = r.get<int32_t>();
+        t.n_str_props = r.get<int32_t>();
+        t.n_num_props = r.get<int32_t>();
+        t.ticket = r.str();
+        t.session_id = r.str();
+        t.party_id = r.str();
+        t.query = r.str();
+        t.node = r.str();
+        if (t.n_presences < 0 || t.n_str_props < 0 || t.n_num_props < 0) r.ok = false;
+        Tmp tm{u->pres.size(), u->sp.size(), u->np.size()};
+        for (int i = 0; i < t.n_presences && r.ok; i++) {
+            mm_presence p;
+            p.user_id = r.str();
+            p.session_id = r.str();
+            p.username = r.str();
+            p.node = r.str();
+            u->pres.push_back(p);
+        }
+        for (int i = 0; i < t.n_str_props && r.ok; i++) {
+            mm_str_prop p;
+            p.key = r.str();
+            p.value = r.str();
+            u->sp.push_back(p);
+        }
+        for (int i = 0; i < t.n_num_props && r.ok; i++) {
+            mm_num_prop p;
+            p.key = r.str();
+            p.value = r.get<double>();
+            u->np.push_back(p);
+        }
+        if (r.at - start != (int64_t)rec) r.ok = false;
+        u->t.push_back(t);
+        tmp.push_back(tm);
+    }
+    if (!r.ok) {
+        delete u;
+        return nullptr;
+    }
+    for (size_t k = 0; k < u->t.size(); k++) {  // the vectors are final: wire the pointers
+        u->t[k].presences = u->pres.data() + tmp[k].p0;
+        u->t[k].str_props = u->sp.data() + tmp[k].s0;
+        u->t[k].num_props = u->np.data() + tmp[k].n0;
+    }
+    *n_out = (int32_t)u->t.size();
+    *tickets_out = u->t.data();
+    return u;
+}
+
+void mm_free_unpacked(void* set) { delete static_cast<Unpacked*>(set); }
+
+int32_t mm_merge_groups(const int64_t* keys, const int32_t* counts, int32_t world, int32_t* out_rank,
+                        int32_t* out_idx) {
+    // heads of the ranks' key runs; a linear k-way merge (world <= 64)
+    std::vector<int64_t> off((size_t)world + 1, 0);
+    for (int32_t r = 0; r < world; r++) off[r + 1] = off[r] + counts[r];
+    std::vector<int64_t> head(off.begin(), off.end() - 1);
+    int32_t ties = 0;
+    for (int64_t k = 0; k < off[world]; k++) {
+        int32_t best = -1;
+        for (int32_t r = 0; r < world; r++) {
+            if (head[r] >= off[r + 1]) continue;
+            if (best < 0 || keys[head[r]] < keys[head[best]]) best = r;
+            else if (keys[head[r]] == keys[head[best]]) ties = 1;  // equal CreatedAt on two ranks
+        }
+        out_rank[k] = best;
+        out_idx[k] = (int32_t)(head[best] - off[best]);
+        head[best]++;
+    }
+    return ties;
+}
+
+}  // extern "C"

@@ -660,6 +660,7 @@ public:
     std::vector<char> out_chars_;
     std::vector<mm_entry_ref> out_ents_;
     std::vector<int32_t> out_offs_;
+    std::vector<int64_t> out_created_;
     std::atomic<bool> out_in_use_{false};
     DevArray<uint32_t> d_pm_;      // pair matrices (RevPrecision combos)
     PinnedArray<uint32_t> h_pm_;

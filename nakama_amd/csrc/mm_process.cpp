@@ -1346,6 +1346,18 @@ void Core::fill_matched(const GroupList& groups, mm_matched* out,
             ents[k].reserved = 0;
         }
     }
+    int64_t* gc;
+    if (arena) {
+        if (out_created_.size() < std::max<size_t>(groups.size(), 1)) out_created_.resize(std::max<size_t>(groups.size(), 1));
+        gc = out_created_.data();
+    } else {
+        gc = new int64_t[groups.size() ? groups.size() : 1];
+    }
+    for (size_t g = 0; g < groups.size(); g++) {
+        const uint32_t last = groups.len(g) ? groups.end(g)[-1].first : kNoSlot;
+        gc[g] = last == kNoSlot ? 0 : created_[last];
+    }
+    out->group_created = gc;
     out->n_groups = (int32_t)groups.size();
     out->n_entries = (int32_t)n;
     out->group_offsets = offs;
@@ -1361,6 +1373,7 @@ void Core::free_matched(mm_matched* out) {
     } else if (out->reserved2 != 0 || out->group_offsets) {
         delete[] out->group_offsets;
         delete[] out->entries;
+        delete[] out->group_created;
         delete[] reinterpret_cast<char*>((intptr_t)out->reserved2);
     }
     std::memset(out, 0, sizeof(*out));

@@ -40,6 +40,8 @@ def lib():
         _lib.synth_make_shard.argtypes = [C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int]
         _lib.synth_pool_of.restype = C.c_int
         _lib.synth_pool_of.argtypes = [C.c_int, C.c_uint64, C.c_uint64]
+        _lib.synth_make_scaled.restype = C.c_void_p
+        _lib.synth_make_scaled.argtypes = [C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int]
     return _lib
 
 
@@ -54,15 +56,20 @@ class TicketSet:
     """Tickets [first, first+n) of a config; owns the native arrays."""
 
     def __init__(self, config: int, n: int, first: int = 0, seed: int = None, t0: int = T0, pool_mask: int = None,
-                 shard: int = None):
+                 shard: int = None, pool_groups: int = None):
         """pool_mask: keep only tickets of these pools (bit p = pool p) out of
         the n generated indices — a rank's shard of a pool-sharded set.
         shard: region values suffixed "-g<shard>" (configs 1-4): a disjoint
-        copy of the config's pools (the N-GPU weak-scaling workload)."""
+        copy of the config's pools.  pool_groups: ONE set whose regions carry
+        "-g<h>", h drawn per ticket in [0, pool_groups) (configs 1-4): the
+        config's pools times pool_groups, spread over every index range — the
+        N-GPU weak-scaling workload the cluster front routes."""
         L = lib()
         self.config = config
         sd = SEEDS.get(config, 1) if seed is None else seed
-        if shard is not None:
+        if pool_groups:
+            self.h = L.synth_make_scaled(config, sd, first, n, t0, pool_groups)
+        elif shard is not None:
             self.h = L.synth_make_shard(config, sd, first, n, t0, shard)
         elif pool_mask is None:
             self.h = L.synth_make(config, sd, first, n, t0)
@@ -77,6 +84,10 @@ class TicketSet:
             cnt = min(chunk, self.n - off)
             ptr = C.cast(C.addressof(self.tickets.contents) + off * C.sizeof(capi.mm_ticket), C.POINTER(capi.mm_ticket))
             mm._check(mm.lib.mm_insert(mm.h, ptr, cnt))
+
+    def ptr(self, off: int = 0):
+        """mm_ticket* to ticket `off` of the native array."""
+        return C.cast(C.addressof(self.tickets.contents) + off * C.sizeof(capi.mm_ticket), C.POINTER(capi.mm_ticket))
 
     def ticket_id(self, k: int) -> str:
         return self.tickets[k].ticket.decode()

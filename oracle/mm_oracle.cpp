@@ -1009,6 +1009,9 @@ static void fill_matched(Matchmaker& m, const vector<vector<Entry>>& groups, mm_
         offs[gi + 1] = (int32_t)k;
     }
     for (size_t i = 0; i < k; i++) ents[i].ticket = (*strs)[i].c_str();
+    auto* gc = new int64_t[groups.size() + 1];
+    for (size_t gi = 0; gi < groups.size(); gi++) gc[gi] = groups[gi].empty() ? 0 : groups[gi].back().idx->created_at;
+    out->group_created = gc;
     out->n_groups = (int32_t)groups.size();
     out->n_entries = (int32_t)k;
     out->group_offsets = offs;
@@ -1396,6 +1399,7 @@ void mm_free_matched(void* h, mm_matched* out) {
     if (!out) return;
     delete[] out->group_offsets;
     delete[] out->entries;
+    delete[] out->group_created;
     delete reinterpret_cast<vector<string>*>((intptr_t)out->reserved2);
     std::memset(out, 0, sizeof(*out));
 }

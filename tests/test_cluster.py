@@ -1,0 +1,208 @@
+"""The pool-sharded front (nakama_amd/cluster.py) over world-size-2 gloo.
+
+Each rank ingests a slice of ONE ticket set; `ClusterMatchmaker.Insert`
+routes every ticket to its pool's rank (mm_route_keys + an all-to-all of
+packed records), each rank runs its own pass, and the merged group list
+(`mm_merge_groups` over the ranks' group_created keys) must equal — group for
+group, entry for entry, in order — one pass of a single matchmaker over the
+whole set, and so must the post-pass state.  The rank-local matchmaker here is
+the CPU oracle (same C ABI as the HIP library; the `gpu`-marked test below
+runs the HIP library on both ranks, sharing device 0 of the one-GPU box);
+routing always runs the product's host code.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+POOL_FIELDS = {3: ("properties.mode", "properties.region"), 4: ("properties.mode", "properties.region"),
+               5: ("properties.bucket",), 1: ("properties.mode", "properties.region")}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _make(config, n, world, rank, groups):
+    from nakama_amd import synth
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    return synth.TicketSet(config, hi - lo, first=lo, pool_groups=groups)
+
+
+def cluster_worker(rank, world, port, config, n, groups, passes, cfg, use_product, q):
+    import harness
+    from nakama_amd import capi, cluster
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if use_product:
+            import nakama_amd
+            lib = nakama_amd.load_library()
+        else:
+            lib = harness.oracle_lib()
+        mm = capi.Matchmaker(lib, **cfg)
+        cm = cluster.ClusterMatchmaker(mm, dist, POOL_FIELDS[config])
+        ts = _make(config, n, world, rank, groups)
+        bad = cm.Insert(ts.ptr(), ts.n)
+        bad_ids = [ts.ticket_id(int(k)) for k in bad]
+        out = []
+        for _ in range(passes):
+            cp = cm.Process(keep_groups=True)
+            merged = cm.gather_groups(cp)
+            state = cm.Extract()
+            active = cm.active_count()
+            out.append((merged, None if state is None else [(t.ticket, t.intervals) for t in state], active,
+                        cp.n_groups, cp.matched_tickets))
+        allbad = [None] * world
+        dist.all_gather_object(allbad, bad_ids)
+        loads = [sum(1 for r in cm.directory.values() if r == k) for k in range(world)]
+        if rank == 0:
+            q.put((out, sorted(b for bs in allbad for b in bs), loads))
+        mm.close()
+        ts.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def run_cluster(config, n, groups, passes, cfg, world=2, use_product=False):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=cluster_worker, args=(r, world, port, config, n, groups, passes, cfg, use_product, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return res
+
+
+def single_pass(config, n, groups, passes, cfg, exclude=()):
+    import harness
+    from nakama_amd import capi, synth
+    ts = synth.TicketSet(config, n, pool_groups=groups)
+    mm = capi.Matchmaker(harness.oracle_lib(), **cfg)
+    ex = set(exclude)
+    try:
+        keep = [k for k in range(ts.n) if ts.ticket_id(k) not in ex]
+        if len(keep) == ts.n:
+            ts.insert_into(mm)
+        else:
+            for k in keep:
+                mm._check(mm.lib.mm_insert(mm.h, ts.ptr(k), 1))
+        out = []
+        for _ in range(passes):
+            g = mm.Process()
+            out.append((g, [(t.ticket, t.intervals) for t in mm.Extract()], mm.active_count()))
+        return out
+    finally:
+        mm.close()
+        ts.close()
+
+
+@pytest.mark.parametrize("config,n,groups,passes", [(3, 1600, 2, 2), (4, 1200, 0, 1), (5, 640, 0, 2)])
+def test_cluster_pass_equals_single_pass(config, n, groups, passes):
+    cfg = dict(max_intervals=2, rev_precision=config == 5)
+    out, bad, loads = run_cluster(config, n, groups, passes, cfg)
+    assert bad == []
+    assert min(loads) > 0  # both ranks own pools
+    want = single_pass(config, n, groups, passes, cfg)
+    for (merged, state, active, ng, matched), (g, st, act) in zip(out, want):
+        assert merged == g
+        assert ng == len(g) and matched == len({t for grp in g for t, _ in grp})
+        assert state == st and active == act
+
+
+def test_cluster_rejects_cross_pool_tickets():
+    """C1's tickets all search (ranked, eu): a casual or non-eu ticket's search
+    leaves its own pool, so it is not partitionable on (mode, region) and the
+    front returns it instead of inserting it; the rest match exactly as a
+    single matchmaker over them."""
+    cfg = dict(max_intervals=2)
+    out, bad, _ = run_cluster(1, 800, 0, 1, cfg)
+    assert 0 < len(bad) < 800
+    want = single_pass(1, 800, 0, 1, cfg, exclude=bad)
+    assert out[0][0] == want[0][0]
+    assert out[0][1] == want[0][1]
+
+
+def test_route_keys_and_pack_roundtrip():
+    from nakama_amd import cluster, synth
+    ts = synth.TicketSet(3, 500, pool_groups=3)
+    try:
+        keys = cluster.route_keys(ts.ptr(), ts.n, ("properties.mode", "properties.region"))
+        assert (keys != 0).all()
+        pools = {}
+        for k in range(ts.n):
+            t = ts.tickets[k]
+            props = tuple(t.str_props[j].value for j in range(t.n_str_props))
+            pools.setdefault(props, set()).add(int(keys[k]))
+        assert len(pools) == 2 * 4 * 3 and all(len(v) == 1 for v in pools.values())
+        assert len({next(iter(v)) for v in pools.values()}) == len(pools)
+        # a query field the ticket's own property does not match -> 0
+        assert (cluster.route_keys(ts.ptr(), ts.n, ("properties.mode", "properties.nope")) == 0).all()
+        idx = np.arange(0, ts.n, 3)
+        buf = cluster.pack(ts.ptr(), idx)
+        u = cluster.Unpacked(buf)
+        try:
+            assert u.n.value == len(idx)
+            for j, k in enumerate(idx):
+                a, b = u.tickets[j], ts.tickets[int(k)]
+                assert (a.ticket, a.query, a.created_at, a.n_presences, a.min_count) == \
+                       (b.ticket, b.query, b.created_at, b.n_presences, b.min_count)
+                assert [a.presences[i].session_id for i in range(a.n_presences)] == \
+                       [b.presences[i].session_id for i in range(b.n_presences)]
+                assert [(a.str_props[i].key, a.str_props[i].value) for i in range(a.n_str_props)] == \
+                       [(b.str_props[i].key, b.str_props[i].value) for i in range(b.n_str_props)]
+        finally:
+            u.close()
+        with pytest.raises(ValueError):
+            cluster.Unpacked(buf[:-3])
+    finally:
+        ts.close()
+
+
+def test_merge_groups_order():
+    from nakama_amd import cluster
+    import ctypes as C
+    keys = np.array([1, 5, 9, 2, 3, 10, 4], dtype=np.int64)
+    counts = np.array([3, 3, 1], dtype=np.int32)
+    r = np.zeros(7, dtype=np.int32)
+    i = np.zeros(7, dtype=np.int32)
+    ties = cluster.router_lib().mm_merge_groups(keys.ctypes.data, counts.ctypes.data, 3, r.ctypes.data, i.ctypes.data)
+    assert ties == 0
+    assert list(zip(r.tolist(), i.tolist())) == [(0, 0), (1, 0), (1, 1), (2, 0), (0, 1), (0, 2), (1, 2)]
+    keys2 = np.array([1, 3, 3], dtype=np.int64)
+    counts2 = np.array([2, 1], dtype=np.int32)
+    assert cluster.router_lib().mm_merge_groups(keys2.ctypes.data, counts2.ctypes.data, 2, r.ctypes.data,
+                                                i.ctypes.data) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,n,groups,passes", [(3, 3000, 2, 2), (4, 2400, 0, 1), (5, 1200, 0, 2)])
+def test_cluster_gpu_pass_equals_single_oracle_pass(config, n, groups, passes):
+    """Two ranks (gloo, sharing device 0 on the one-GPU box) each run the HIP
+    library on the pools the front routed to them; the merged groups and the
+    post-pass state equal one oracle pass over the whole set."""
+    cfg = dict(max_intervals=2, rev_precision=config == 5)
+    out, bad, loads = run_cluster(config, n, groups, passes, cfg, use_product=True)
+    assert bad == [] and min(loads) > 0
+    want = single_pass(config, n, groups, passes, cfg)
+    for (merged, state, active, ng, matched), (g, st, act) in zip(out, want):
+        assert merged == g
+        assert state == st and active == act

@@ -33,6 +33,16 @@ def product():
     return capi.load_library(harness.PRODUCT_SO)
 
 
+def test_cluster_header_symbols_exported(product):
+    """include/nakama_cluster.h: the multi-GPU front's host entry points."""
+    from nakama_amd import cluster
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(harness.ROOT, "include", "nakama_cluster.h")).read(), flags=re.S)
+    syms = sorted(set(re.findall(r"\b(mm_[a-z_]+)\s*\(", txt)))
+    assert set(syms) == set(cluster.CLUSTER_SYMBOLS)
+    for s in syms:
+        assert hasattr(product, s), f"libnakama_mm.so does not export {s}"
+
+
 def test_header_symbols_exported(product):
     syms = declared_symbols()
     assert len(syms) >= 25

@@ -5,6 +5,7 @@
 //
 //   CreatedAt = T0 + 1024*i (float64-exact, distinct), ticket id = UUID text
 //   from splitmix64(seed, i), one unique session per presence, Intervals = 0.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -80,7 +81,22 @@ int synth_pool_of(int config, uint64_t seed, uint64_t i) {
     return -1;
 }
 
-void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0, uint64_t pool_mask, int shard);
+void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0, uint64_t pool_mask, int shard,
+                      int pool_groups = 0);
+
+// The pool group of ticket i in a scaled set (synth_make_scaled).
+int synth_group_of(uint64_t seed, uint64_t i, int pool_groups) {
+    return pool_groups > 0 ? (int)(splitmix64(seed ^ 0xA5A5A5A5ull ^ (i * 0xD1B54A32D192ED03ull)) % (uint64_t)pool_groups) : 0;
+}
+
+// The N-GPU weak-scaling set of configs 1-4 as ONE ticket set: every region
+// value carries "-g<h>" with h = synth_group_of(i) in [0, pool_groups), so C3's
+// 8 pools become 8 * pool_groups pools of the same size, spread over the whole
+// index range (any rank's ingest slice holds tickets of every pool; the
+// cluster front routes them).
+void* synth_make_scaled(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0, int pool_groups) {
+    return synth_make_impl(config, seed, first, n, t0, ~0ull, -1, pool_groups);
+}
 
 // config: 1..5 as BASELINE.json configs[0..4], 6 = mixed, 7 = regexp/wildcard/fuzzy.  Generates tickets [first, first+n).
 void* synth_make(int config, uint64_t seed, int64_t first, int64_t n, int64_t t0) {
@@ -101,12 +117,17 @@ void* synth_make_pools(int config, uint64_t seed, int64_t first, int64_t n, int6
     return synth_make_impl(config, seed, first, n, t0, pool_mask, -1);
 }
 
-void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, int64_t t0, uint64_t pool_mask, int shard) {
+void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, int64_t t0, uint64_t pool_mask, int shard,
+                      int pool_groups) {
     char sfx[16] = "";
     if (shard >= 0) std::snprintf(sfx, sizeof sfx, "-g%d", shard);
     std::vector<const char*> shard_regions(8);  // region values of this shard
     for (int k = 0; k < 8; k++) shard_regions[k] = kRegions[k];
     auto* S = new Synth();
+    // scaled sets: region values per pool group
+    std::vector<std::vector<const char*>> grp_regions(std::max(pool_groups, 0), std::vector<const char*>(8));
+    for (int g = 0; g < pool_groups; g++)
+        for (int k = 0; k < 8; k++) grp_regions[g][k] = S->keep(std::string(kRegions[k]) + "-g" + std::to_string(g));
     std::vector<uint64_t> idx;
     idx.reserve((size_t)n_all);
     for (int64_t k = 0; k < n_all; k++) {
@@ -138,18 +159,21 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
         Tmp& tm = tmp[(size_t)k];
         tm.s0 = S->sp.size();
         tm.n0 = S->np.size();
+        const std::vector<const char*>& shard_regions_i =
+            pool_groups > 0 ? grp_regions[synth_group_of(seed, i, pool_groups)] : shard_regions;
         switch (config) {
         case 1: {
             const char* mode = kModes[r.next() & 1];
-            const char* region = shard_regions[r.next() & 3];
+            const char* region = shard_regions_i[r.next() & 3];
             S->sp.push_back({"mode", mode});
             S->sp.push_back({"region", region});
-            query = std::string("+properties.mode:ranked +properties.region:eu") + sfx;
+            query = std::string("+properties.mode:ranked +properties.region:") +
+                    (pool_groups > 0 ? std::string(shard_regions_i[0]) : std::string("eu") + sfx);
             t.min_count = t.max_count = 2;
             break;
         }
         case 2: {
-            const char* region = shard_regions[r.next() & 3];
+            const char* region = shard_regions_i[r.next() & 3];
             const int s = (int)std::lround(r.normal(1500.0, 300.0));
             S->sp.push_back({"region", region});
             S->np.push_back({"skill", (double)s});
@@ -166,7 +190,7 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             const double u = r.uni();
             party = u < 0.60 ? 1 : u < 0.80 ? 2 : u < 0.90 ? 3 : u < 0.95 ? 4 : 5;
             const char* mode = kModes[r.next() & 1];
-            const char* region = shard_regions[r.next() & 3];
+            const char* region = shard_regions_i[r.next() & 3];
             S->sp.push_back({"mode", mode});
             S->sp.push_back({"region", region});
             query = std::string("+properties.mode:") + mode + " +properties.region:" + region;
@@ -176,7 +200,7 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
         }
         case 4: {
             const char* mode = kModes[r.next() & 7];
-            const char* region = shard_regions[r.next() & 7];
+            const char* region = shard_regions_i[r.next() & 7];
             S->sp.push_back({"mode", mode});
             S->sp.push_back({"region", region});
             query = std::string("+properties.mode:") + mode + " +properties.region:" + region;
