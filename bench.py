@@ -216,6 +216,7 @@ def main():
     times, matched_all, presences_all, ins_times, searched = [], [], [], [], []
     eval_ms = eval_bytes = launches = 0
     batches, kernels, unroutable = [], set(), 0
+    breakdown = {"local_call_ms": [], "summary_ms": [], "merge_ms": []}  # rank 0's cluster-pass phases
     for step in range(args.warmup + args.steps):
         ts = make_set(args, world, rank, step)
         t_ins = time.perf_counter()
@@ -239,6 +240,9 @@ def main():
         else:
             n_groups, matched, pres = cp.n_groups, cp.matched_tickets, cp.matched_presences
             st = cp.local_stats
+            if step >= args.warmup:
+                for k in breakdown:
+                    breakdown[k].append(st[k])
         ts.close()
         dt_max = max_over_ranks(pg, local, dt)
         if step >= args.warmup:
@@ -301,7 +305,9 @@ def main():
         "config": {"workload": WORKLOADS.get(args.config, str(args.config)),
                    ("tickets_total" if strong else "tickets_per_gpu"): args.tickets,
                    "max_intervals": 2, "parallelism": par, "unroutable": unroutable,
-                   "matched_per_step": sum(matched_all) / args.steps, "batches_per_pass_rank0": batches},
+                   "matched_per_step": sum(matched_all) / args.steps, "batches_per_pass_rank0": batches,
+                   "cluster_phases_ms_rank0": ({k: statistics.median(v) for k, v in breakdown.items()}
+                                               if cm is not None else None)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "+".join(sorted(kernels)), "launches": launches, "avg_launch_ms": avg_launch_ms,

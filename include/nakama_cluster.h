@@ -51,12 +51,11 @@ void mm_free_unpacked(void* set);
  * appends a group when its searching ticket (the group's last entry) is
  * processed, in the pinned (CreatedAt, Ticket) order, so the global list is
  * the merge of the ranks' lists by their mm_matched.group_created keys.
- * keys = the ranks' key arrays concatenated (each ascending), counts[r] = rank
- * r's group count; writes the (rank, local index) of every global position.
- * Returns 1 when equal keys met on different ranks (the caller orders those
- * by ticket id), else 0. */
-int32_t mm_merge_groups(const int64_t* keys, const int32_t* counts, int32_t world, int32_t* out_rank,
-                        int32_t* out_idx);
+ * keys = every rank's key array concatenated (each ascending), counts[r] =
+ * rank r's group count; writes the global position of each of `rank`'s
+ * groups (linear in the keys).  Returns 1 when one of them has the same key
+ * as a group of another rank (the caller orders those by ticket id), else 0. */
+int32_t mm_merge_positions(const int64_t* keys, const int32_t* counts, int32_t world, int32_t rank, int64_t* pos_out);
 
 #ifdef __cplusplus
 }

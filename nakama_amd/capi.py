@@ -394,21 +394,26 @@ class Matchmaker:
         self._check(self.lib.mm_process(self.h, C.byref(out)))
         return out
 
-    def process_summary(self, out):
+    @staticmethod
+    def summary_counts(out):
         """(n_groups, matched tickets, matched presences, ProcessResult without
-        the groups) of a process_call result; frees it."""
+        the groups) of a process_call result (not freed)."""
         import numpy as np
+        n = out.n_entries
+        if n:
+            raw = (C.c_char * (n * C.sizeof(mm_entry_ref))).from_address(C.addressof(out.entries.contents))
+            arr = np.frombuffer(raw, dtype=np.dtype([("p", "<u8"), ("pi", "<i4"), ("r", "<i4")]))
+            tickets = int(np.count_nonzero(arr["pi"] == 0))
+        else:
+            tickets = 0
+        res = ProcessResult([], bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms, out.pair_evals,
+                            out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel, out.full_lists)
+        return out.n_groups, tickets, n, res
+
+    def process_summary(self, out):
+        """summary_counts of a process_call result; frees it."""
         try:
-            n = out.n_entries
-            if n:
-                raw = (C.c_char * (n * C.sizeof(mm_entry_ref))).from_address(C.addressof(out.entries.contents))
-                arr = np.frombuffer(raw, dtype=np.dtype([("p", "<u8"), ("pi", "<i4"), ("r", "<i4")]))
-                tickets = int(np.count_nonzero(arr["pi"] == 0))
-            else:
-                tickets = 0
-            res = ProcessResult([], bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms, out.pair_evals,
-                                out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel, out.full_lists)
-            return out.n_groups, tickets, n, res
+            return self.summary_counts(out)
         finally:
             self.lib.mm_free_matched(self.h, C.byref(out))
 

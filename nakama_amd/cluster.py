@@ -19,11 +19,12 @@ all-to-all of packed records (RCCL over xGMI when the group is "nccl").
 
 Process.  Every rank runs its own pass — no data-path collective — and the
 reference's group order is recovered by merging the ranks' group lists on
-the searching ticket's (CreatedAt, Ticket) (`mm_merge_groups`; the keys come
-back in `mm_matched.group_created`): one all-gather of 8 B per group.  A
-group's tickets all live on one rank, which owns its delivery; rank 0 holds
-the global order (`ClusterPass.order`) and `gather_groups()` materialises the
-merged list for callers that need it whole (tests).
+the searching ticket's (CreatedAt, Ticket) (`mm_merge_positions`; the keys
+come back in `mm_matched.group_created`): one all-gather of 8 B per group,
+after which every rank knows the global position of each of its groups
+(`ClusterPass.positions`, a linear merge on each rank).  A group's tickets all
+live on one rank, which owns its delivery; `gather_groups()` materialises the
+merged list on rank 0 for callers that need it whole (tests).
 
 Every method is a collective: all ranks call it, in the same order.  Tickets
 that are not partitionable on the pool fields (a query that does not pin a
@@ -66,13 +67,14 @@ def router_lib(path: str = PRODUCT_SO) -> C.CDLL:
         lib.mm_unpack_tickets.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_int32),
                                           C.POINTER(C.POINTER(capi.mm_ticket))]
         lib.mm_free_unpacked.argtypes = [C.c_void_p]
-        lib.mm_merge_groups.restype = C.c_int32
-        lib.mm_merge_groups.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        lib.mm_merge_positions.restype = C.c_int32
+        lib.mm_merge_positions.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
         _router = lib
     return _router
 
 
-CLUSTER_SYMBOLS = ("mm_route_keys", "mm_pack_tickets", "mm_unpack_tickets", "mm_free_unpacked", "mm_merge_groups")
+CLUSTER_SYMBOLS = ("mm_route_keys", "mm_pack_tickets", "mm_unpack_tickets", "mm_free_unpacked",
+                   "mm_merge_positions")
 
 
 def route_keys(tickets, n: int, pool_fields: Sequence[str]) -> np.ndarray:
@@ -129,7 +131,7 @@ class ClusterPass:
     matched_tickets: int = 0       # all ranks
     matched_presences: int = 0     # all ranks
     local: Optional[capi.ProcessResult] = None   # this rank's groups (when kept)
-    order: Optional[np.ndarray] = None           # rank 0: (rank, local index) per global position
+    positions: Optional[np.ndarray] = None       # global position of each of this rank's groups
     local_stats: Dict[str, float] = field(default_factory=dict)
 
 
@@ -247,69 +249,81 @@ class ClusterMatchmaker:
 
     # ---- the pass ----
     def Process(self, keep_groups: bool = False) -> ClusterPass:
-        """One interval pass on every rank, and the reference's group order
-        over all of them (on rank 0).  keep_groups: also convert this rank's
+        """One interval pass on every rank, and the global position of every
+        group in the reference's order.  keep_groups: also convert this rank's
         groups to Python (tests, delivery)."""
+        import time
+        t0 = time.perf_counter()
         out = self.local.process_call()
+        t1 = time.perf_counter()
         try:
             ng = out.n_groups
             keys = np.ctypeslib.as_array(out.group_created, (ng,)).copy() if ng else np.zeros(0, dtype=np.int64)
+            res = None
             if keep_groups:
                 res = capi.ProcessResult(capi.Matchmaker._groups(out), bool(out.is_candidates), out.n_expired,
                                          out.pass_ms, out.eval_ms, out.pair_evals, out.eval_bytes, out.eval_launches,
                                          out.n_batches, out.eval_kernel, out.full_lists)
-                tie_ids = [g[-1][0] for g in res.groups]
-            else:
-                res, tie_ids = None, None
-            _, tickets, pres, stats = self.local.process_summary(out)
-            out = None
+            _, tickets, pres, stats = self.local.summary_counts(out)
+            t2 = time.perf_counter()
+            cp = ClusterPass(local=res)
+            # one all-gather of (groups, matched tickets, presences): sizes + totals
+            hdr = [self._t(np.zeros(3, dtype=np.int64)) for _ in range(self.world)]
+            self.dist.all_gather(hdr, self._t(np.array([ng, tickets, pres], dtype=np.int64)))
+            hdr = np.stack([self._host(h) for h in hdr])
+            counts = hdr[:, 0].astype(np.int32)
+            cp.n_groups, cp.matched_tickets, cp.matched_presences = (int(x) for x in hdr.sum(axis=0))
+            # one all-gather of the keys (padded to the largest rank's count)
+            m = max(int(counts.max()), 1)
+            pad = np.zeros(m, dtype=np.int64)
+            pad[:ng] = keys
+            outs = [self._t(np.zeros(m, dtype=np.int64)) for _ in range(self.world)]
+            self.dist.all_gather(outs, self._t(pad))
+            allk = np.concatenate([self._host(o)[:c] for o, c in zip(outs, counts)])
+            pos = np.zeros(max(ng, 1), dtype=np.int64)
+            ties = router_lib().mm_merge_positions(allk.ctypes.data, counts.ctypes.data, self.world, self.rank,
+                                                   pos.ctypes.data)
+            cp.positions = pos[:ng]
+            flag = self._t(np.array([ties], dtype=np.int32))
+            self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX)
+            if int(self._host(flag)[0]):  # rare: the searching tickets' ids order the tied groups
+                offs = out.group_offsets
+                tie_ids = [out.entries[offs[g + 1] - 1].ticket.decode() for g in range(ng)]
+                self._order_ties(cp, allk, counts, tie_ids)
         finally:
-            if out is not None:
-                self.local.lib.mm_free_matched(self.local.h, C.byref(out))
-        cp = ClusterPass(local=res)
+            self.local.lib.mm_free_matched(self.local.h, C.byref(out))
+        t3 = time.perf_counter()
         cp.local_stats = {"pass_ms": stats.pass_ms, "eval_ms": stats.eval_ms, "eval_bytes": stats.eval_bytes,
                           "eval_launches": stats.eval_launches, "n_batches": stats.n_batches,
-                          "eval_kernel": stats.eval_kernel}
-        allk, counts = self._all_gather_var(keys)
-        tot = self._t(np.array([ng, tickets, pres], dtype=np.int64))
-        self.dist.all_reduce(tot)
-        cp.n_groups, cp.matched_tickets, cp.matched_presences = (int(x) for x in self._host(tot))
-        ties = 0
-        if self.rank == 0:
-            cnt = np.array(counts, dtype=np.int32)
-            orank = np.zeros(max(len(allk), 1), dtype=np.int32)
-            oidx = np.zeros(max(len(allk), 1), dtype=np.int32)
-            ties = router_lib().mm_merge_groups(np.ascontiguousarray(allk).ctypes.data, cnt.ctypes.data, self.world,
-                                                orank.ctypes.data, oidx.ctypes.data)
-            cp.order = np.stack([orank[:len(allk)], oidx[:len(allk)]], axis=1)
-        flag = self._t(np.array([ties], dtype=np.int32))
-        self.dist.broadcast(flag, 0)
-        if int(self._host(flag)[0]):
-            self._order_ties(cp, allk, counts, tie_ids)
+                          "eval_kernel": stats.eval_kernel, "local_call_ms": 1e3 * (t1 - t0),
+                          "summary_ms": 1e3 * (t2 - t1), "merge_ms": 1e3 * (t3 - t2)}
         return cp
 
-    def _order_ties(self, cp: ClusterPass, allk: np.ndarray, counts: List[int], tie_ids):
+    def _order_ties(self, cp: ClusterPass, allk: np.ndarray, counts: np.ndarray, tie_ids):
         """Equal CreatedAt on two ranks: those groups are ordered by their
         searching ticket's id, the second key of the pinned active order."""
-        if tie_ids is None:
-            raise RuntimeError("equal CreatedAt across ranks: call Process(keep_groups=True) to order by ticket id")
         gathered = [None] * self.world
         self.dist.all_gather_object(gathered, tie_ids)
-        if self.rank != 0:
-            return
         off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
-        o = cp.order
-        pos = sorted(range(len(o)), key=lambda p: (int(allk[off[o[p][0]] + o[p][1]]), gathered[o[p][0]][o[p][1]]))
-        cp.order = o[pos]
+        allpos = sorted(((int(allk[off[r] + i]), gathered[r][i], r, i) for r in range(self.world)
+                         for i in range(int(counts[r]))))
+        for p, (_, _, r, i) in enumerate(allpos):
+            if r == self.rank:
+                cp.positions[i] = p
 
     def gather_groups(self, cp: ClusterPass) -> Optional[List[List[Tuple[str, int]]]]:
         """Rank 0: the merged group list in the reference's order (needs
         Process(keep_groups=True) on every rank)."""
         gathered = [None] * self.world
-        self.dist.all_gather_object(gathered, cp.local.groups if cp.local is not None else None)
+        self.dist.all_gather_object(gathered, (cp.local.groups if cp.local is not None else None,
+                                               cp.positions.tolist()))
         if self.rank != 0:
             return None
-        return [gathered[int(r)][int(i)] for r, i in cp.order]
+        merged = [None] * cp.n_groups
+        for groups, pos in gathered:
+            for g, p in zip(groups, pos):
+                merged[p] = g
+        return merged
 
     # ---- mutators and state (routed or broadcast) ----
     def ticket_count(self) -> int:

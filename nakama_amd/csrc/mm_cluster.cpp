@@ -244,23 +244,25 @@ void* mm_unpack_tickets(const uint8_t* buf, int64_t len, int32_t* n_out, const m
 
 void mm_free_unpacked(void* set) { delete static_cast<Unpacked*>(set); }
 
-int32_t mm_merge_groups(const int64_t* keys, const int32_t* counts, int32_t world, int32_t* out_rank,
-                        int32_t* out_idx) {
-    // heads of the ranks' key runs; a linear k-way merge (world <= 64)
+int32_t mm_merge_positions(const int64_t* keys, const int32_t* counts, int32_t world, int32_t rank, int64_t* pos_out) {
+    // my group i lands after my i earlier groups and after every other rank's
+    // groups with a smaller key: one linear two-pointer walk per other rank
     std::vector<int64_t> off((size_t)world + 1, 0);
     for (int32_t r = 0; r < world; r++) off[r + 1] = off[r] + counts[r];
-    std::vector<int64_t> head(off.begin(), off.end() - 1);
+    const int64_t* mine = keys + off[rank];
+    const int64_t n = counts[rank];
+    for (int64_t i = 0; i < n; i++) pos_out[i] = i;
     int32_t ties = 0;
-    for (int64_t k = 0; k < off[world]; k++) {
-        int32_t best = -1;
-        for (int32_t r = 0; r < world; r++) {
-            if (head[r] >= off[r + 1]) continue;
-            if (best < 0 || keys[head[r]] < keys[head[best]]) best = r;
-            else if (keys[head[r]] == keys[head[best]]) ties = 1;  // equal CreatedAt on two ranks
+    for (int32_t q = 0; q < world; q++) {
+        if (q == rank) continue;
+        const int64_t* other = keys + off[q];
+        const int64_t m = counts[q];
+        int64_t j = 0;
+        for (int64_t i = 0; i < n; i++) {
+            while (j < m && other[j] < mine[i]) j++;
+            if (j < m && other[j] == mine[i]) ties = 1;  // equal CreatedAt on two ranks
+            pos_out[i] += j;
         }
-        out_rank[k] = best;
-        out_idx[k] = (int32_t)(head[best] - off[best]);
-        head[best]++;
     }
     return ties;
 }

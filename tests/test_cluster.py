@@ -3,7 +3,7 @@
 Each rank ingests a slice of ONE ticket set; `ClusterMatchmaker.Insert`
 routes every ticket to its pool's rank (mm_route_keys + an all-to-all of
 packed records), each rank runs its own pass, and the merged group list
-(`mm_merge_groups` over the ranks' group_created keys) must equal — group for
+(`mm_merge_positions` over the ranks' group_created keys) must equal — group for
 group, entry for entry, in order — one pass of a single matchmaker over the
 whole set, and so must the post-pass state.  The rank-local matchmaker here is
 the CPU oracle (same C ABI as the HIP library; the `gpu`-marked test below
@@ -35,13 +35,17 @@ def _free_port():
     return p
 
 
-def _make(config, n, world, rank, groups):
+def _make(config, n, world, rank, groups, ties=False):
     from nakama_amd import synth
     lo, hi = n * rank // world, n * (rank + 1) // world
-    return synth.TicketSet(config, hi - lo, first=lo, pool_groups=groups)
+    ts = synth.TicketSet(config, hi - lo, first=lo, pool_groups=groups)
+    if ties:  # tickets 2j and 2j+1 share a CreatedAt: ordered by ticket id
+        for k in range(ts.n):
+            ts.tickets[k].created_at -= 1024 * ((lo + k) % 2)
+    return ts
 
 
-def cluster_worker(rank, world, port, config, n, groups, passes, cfg, use_product, q):
+def cluster_worker(rank, world, port, config, n, groups, passes, cfg, use_product, q, ties=False):
     import harness
     from nakama_amd import capi, cluster
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -55,7 +59,7 @@ def cluster_worker(rank, world, port, config, n, groups, passes, cfg, use_produc
             lib = harness.oracle_lib()
         mm = capi.Matchmaker(lib, **cfg)
         cm = cluster.ClusterMatchmaker(mm, dist, POOL_FIELDS[config])
-        ts = _make(config, n, world, rank, groups)
+        ts = _make(config, n, world, rank, groups, ties)
         bad = cm.Insert(ts.ptr(), ts.n)
         bad_ids = [ts.ticket_id(int(k)) for k in bad]
         out = []
@@ -77,11 +81,12 @@ def cluster_worker(rank, world, port, config, n, groups, passes, cfg, use_produc
         dist.destroy_process_group()
 
 
-def run_cluster(config, n, groups, passes, cfg, world=2, use_product=False):
+def run_cluster(config, n, groups, passes, cfg, world=2, use_product=False, ties=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=cluster_worker, args=(r, world, port, config, n, groups, passes, cfg, use_product, q))
+    procs = [ctx.Process(target=cluster_worker,
+                         args=(r, world, port, config, n, groups, passes, cfg, use_product, q, ties))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -92,10 +97,13 @@ def run_cluster(config, n, groups, passes, cfg, world=2, use_product=False):
     return res
 
 
-def single_pass(config, n, groups, passes, cfg, exclude=()):
+def single_pass(config, n, groups, passes, cfg, exclude=(), ties=False):
     import harness
     from nakama_amd import capi, synth
     ts = synth.TicketSet(config, n, pool_groups=groups)
+    if ties:
+        for k in range(ts.n):
+            ts.tickets[k].created_at -= 1024 * (k % 2)
     mm = capi.Matchmaker(harness.oracle_lib(), **cfg)
     ex = set(exclude)
     try:
@@ -141,6 +149,16 @@ def test_cluster_rejects_cross_pool_tickets():
     assert out[0][1] == want[0][1]
 
 
+def test_cluster_orders_equal_created_at_by_ticket():
+    """Groups whose searching tickets share a CreatedAt on two ranks follow
+    the pinned (CreatedAt, Ticket) order."""
+    cfg = dict(max_intervals=2)
+    out, bad, _ = run_cluster(4, 1200, 0, 1, cfg, world=3, ties=True)
+    want = single_pass(4, 1200, 0, 1, cfg, ties=True)
+    assert out[0][0] == want[0][0]
+    assert out[0][1] == want[0][1]
+
+
 def test_route_keys_and_pack_roundtrip():
     from nakama_amd import cluster, synth
     ts = synth.TicketSet(3, 500, pool_groups=3)
@@ -177,20 +195,20 @@ def test_route_keys_and_pack_roundtrip():
         ts.close()
 
 
-def test_merge_groups_order():
+def test_merge_positions():
     from nakama_amd import cluster
-    import ctypes as C
     keys = np.array([1, 5, 9, 2, 3, 10, 4], dtype=np.int64)
     counts = np.array([3, 3, 1], dtype=np.int32)
-    r = np.zeros(7, dtype=np.int32)
-    i = np.zeros(7, dtype=np.int32)
-    ties = cluster.router_lib().mm_merge_groups(keys.ctypes.data, counts.ctypes.data, 3, r.ctypes.data, i.ctypes.data)
-    assert ties == 0
-    assert list(zip(r.tolist(), i.tolist())) == [(0, 0), (1, 0), (1, 1), (2, 0), (0, 1), (0, 2), (1, 2)]
+    want = {0: [0, 4, 5], 1: [1, 2, 6], 2: [3]}
+    for r in range(3):
+        pos = np.zeros(3, dtype=np.int64)
+        ties = cluster.router_lib().mm_merge_positions(keys.ctypes.data, counts.ctypes.data, 3, r, pos.ctypes.data)
+        assert ties == 0
+        assert pos[:counts[r]].tolist() == want[r]
     keys2 = np.array([1, 3, 3], dtype=np.int64)
     counts2 = np.array([2, 1], dtype=np.int32)
-    assert cluster.router_lib().mm_merge_groups(keys2.ctypes.data, counts2.ctypes.data, 2, r.ctypes.data,
-                                                i.ctypes.data) == 1
+    pos = np.zeros(2, dtype=np.int64)
+    assert cluster.router_lib().mm_merge_positions(keys2.ctypes.data, counts2.ctypes.data, 2, 0, pos.ctypes.data) == 1
 
 
 @pytest.mark.gpu
