@@ -500,7 +500,16 @@ private:
     void finish_pass_serial(GroupList& groups, bool selected);
     void fill_matched(const GroupList& groups, mm_matched* out, bool cands);
     void choose_source(const Sig& s, DGroup& g, SrcChoice* ch = nullptr);
-    bool replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
+    struct ParPlan {  // a batch's pools (plan_parallel), bucketed while its searches run
+        bool ok = false;
+        size_t ng = 0;
+        std::vector<uint32_t> search_pool;           // per search
+        std::vector<std::vector<uint32_t>> grows;    // per pool: its batch rows, ascending
+    };
+    ParPlan par_plan_;
+    bool plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
+                       const std::vector<uint32_t>& brow_group, ParPlan& P, PassStats& stats);
+    bool replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
                          const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                          GroupList& out_groups,
                          std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats);
@@ -515,6 +524,8 @@ private:
     int device_ = 0;
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[7] = {};  // start/stop of the search / scan / mscan dispatches; a marker before stitch_kernel
+    hipEvent_t apply_ev_ = nullptr;  // after the last asynchronous alive-flag update (h_slots_tmp_ reuse)
+    bool apply_pending_ = false;
     std::unique_ptr<WorkPool> workers_;  // created on the first large pass
     WorkPool& workers();
     size_t par_min(size_t auto_min) const { return par_mode_ == 2 ? 0 : auto_min; }

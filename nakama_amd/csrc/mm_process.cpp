@@ -250,7 +250,9 @@ struct Replay : ReplayCore {
         return true;
     }
 
-    void run_batch(std::vector<BGroup>& bg, bool need_pm) {
+    // overlap: host work run while the batch's kernels and copies are in
+    // flight (the pool bucketing of the rows, which needs no hit list)
+    void run_batch(std::vector<BGroup>& bg, bool need_pm, const std::function<void()>& overlap = nullptr) {
         const uint32_t kChunk = (uint32_t)scan_chunk_len();
         lg.clear();
         lg_group.clear();
@@ -421,6 +423,7 @@ struct Replay : ReplayCore {
             NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, (uint64_t)nwhole * kPairP * sizeof(uint32_t),
                                    hipMemcpyDeviceToHost, stream));
         }
+        if (overlap) overlap();
         NKM_HIP(hipStreamSynchronize(stream));
         const bool ran[3] = {nwhole > 0, nchunks > 0, use_m};
         for (int kk = 0; kk < 3; kk++) {
@@ -503,10 +506,12 @@ struct Replay : ReplayCore {
 // sequential order is preserved within each pool, and no ticket is shared
 // across pools).  The pools run on host threads; results are merged back into
 // the pinned row order.  Returns false (nothing done) when the conditions fail.
-bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
-                           const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
-                           GroupList& out_groups,
-                           std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats) {
+// The part of the pool-parallel replay that needs no hit list — the pool
+// keys and the rows bucketed per pool — run while the batch's searches are
+// on the device.  Returns false when the batch does not partition into pools.
+bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
+                         const std::vector<uint32_t>& brow_group, ParPlan& P, PassStats& stats) {
+    P.ok = false;
     const size_t nsearch = bg.size();
     if (nsearch < 2) return false;
     // pool key fields: fields every search requires a keyword term on
@@ -527,9 +532,9 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
     // pool key of each search (a search requiring two different terms on one
     // field matches nothing; it gets a key of its own)
     std::map<std::vector<uint32_t>, uint32_t> pool_of;
-    std::vector<uint32_t> search_pool(nsearch);
+    std::vector<uint32_t>& search_pool = P.search_pool;
+    search_pool.assign(nsearch, 0);
     for (size_t i = 0; i < nsearch; i++) {
-        if (!bg[i].complete) return false;
         std::vector<uint32_t> key(keyf.size(), UINT32_MAX);
         for (size_t k = 0; k < keyf.size(); k++)
             for (auto& mt : sigs_[bg[i].sig].must_terms)
@@ -541,6 +546,7 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
     }
     const size_t ng = pool_of.size();
     if (ng < 2) return false;
+    P.ng = ng;
     std::vector<std::vector<uint32_t>> pool_keys(ng);
     for (auto& kv : pool_of) pool_keys[kv.second] = kv.first;
     // every searching ticket must itself belong to its search's pool; bucket
@@ -571,7 +577,8 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
     wp.run(nchunk, [&](size_t c) { bucket((unsigned)c); });
     for (unsigned c = 0; c < nchunk; c++)
         if (cbad[c]) return false;
-    std::vector<std::vector<uint32_t>> grows(ng);
+    std::vector<std::vector<uint32_t>>& grows = P.grows;
+    grows.assign(ng, {});
     if (nchunk == 1) {
         grows.swap(cgrows[0]);
     } else {
@@ -582,6 +589,26 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
             for (unsigned c = 0; c < nchunk; c++) grows[p].insert(grows[p].end(), cgrows[c][p].begin(), cgrows[c][p].end());
         }
     }
+    stats.par_bucket_ms += msd(tp0, clk::now());
+    P.ok = true;
+    return true;
+}
+
+// Pool-parallel replay over the bucketed rows (plan_parallel); false when a
+// pool's list came back truncated (the serial replay then decides the batch).
+bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
+                           const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
+                           GroupList& out_groups,
+                           std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats) {
+    if (!P.ok) return false;
+    for (const BGroup& g : bg)
+        if (!g.complete) return false;
+    using clk = std::chrono::steady_clock;
+    auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const size_t nsearch = bg.size(), ng = P.ng;
+    const std::vector<uint32_t>& search_pool = P.search_pool;
+    const std::vector<std::vector<uint32_t>>& grows = P.grows;
+    WorkPool& wp = workers();
     using Rec = PoolRec;
     if (pool_outs_.size() < ng) pool_outs_.resize(ng);  // kept across passes (capacity reused)
     auto& outs = pool_outs_;
@@ -731,7 +758,6 @@ bool Core::replay_parallel(std::vector<BGroup>& bg, const std::vector<uint32_t>&
         }
     });
     const auto tp3 = clk::now();
-    stats.par_bucket_ms += msd(tp0, tp1);
     stats.par_work_ms += msd(tp1, tp2);
     stats.par_merge_ms += msd(tp2, tp3);
     for (size_t k = 0; k < ng; k++) {
@@ -953,14 +979,18 @@ int Core::process_default(GroupList& out_groups,
         }
         auto tb0 = std::chrono::steady_clock::now();
         stats.assemble_ms += std::chrono::duration<double, std::milli>(tb0 - ta0).count();
-        rp.run_batch(bg, need_pm);
+        ParPlan& plan = par_plan_;
+        plan.ok = false;
+        rp.run_batch(bg, need_pm, [&] {  // pools bucketed while the searches run
+            if (!rev && par_mode_) plan_parallel(bg, brow, brow_group, plan, stats);
+        });
         auto tb1 = std::chrono::steady_clock::now();
         stats.search_ms += std::chrono::duration<double, std::milli>(tb1 - tb0).count();
         // ---- replay ----
         newly.clear();
         size_t done = 0;
         bool exhausted = false;
-        if (!rev && par_mode_ && replay_parallel(bg, brow, brow_group, sel, out_groups, expired, newly, stats)) {
+        if (!rev && par_mode_ && replay_parallel(plan, bg, brow, brow_group, sel, out_groups, expired, newly, stats)) {
             stats.parallel_batches++;
             const auto tr = std::chrono::steady_clock::now();
             stats.replay_ms += std::chrono::duration<double, std::milli>(tr - tb1).count();

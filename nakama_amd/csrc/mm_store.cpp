@@ -88,6 +88,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     NKM_HIP(hipSetDevice(device_));
     NKM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     for (auto& e : ev_) NKM_HIP(hipEventCreate(&e));
+    NKM_HIP(hipEventCreateWithFlags(&apply_ev_, hipEventDisableTiming));
     if (const char* e = std::getenv("NKM_DENSE")) dense_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FAST")) fast_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FULLVAR")) full_var_mode_ = std::strcmp(e, "0") != 0;
@@ -202,6 +203,8 @@ WorkPool& Core::workers() {
         unsigned n = std::thread::hardware_concurrency();
         cpu_set_t cs;
         if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = (unsigned)CPU_COUNT(&cs);
+        // one process per GPU: the node's cores are shared by the local ranks
+        if (const char* lw = std::getenv("LOCAL_WORLD_SIZE")) n /= std::max(1, std::atoi(lw));
         n = std::max(1u, std::min(16u, n));
         if (const char* e = std::getenv("NKM_THREADS")) n = std::max(1, std::atoi(e));
         workers_.reset(new WorkPool(n, worker_cpus(n - 1)));
@@ -216,6 +219,7 @@ Core::~Core() {
     for (auto* p : d_fkind_) delete p;
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
+    if (apply_ev_) (void)hipEventDestroy(apply_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -1249,15 +1253,23 @@ DStore Core::dstore() const {
     return st;
 }
 
+// Clears the device alive flags of the given slots.  Asynchronous: the copy
+// and kernel are ordered before the next search on the library's stream; the
+// pinned staging buffer is reused only after the previous copy completed.
 void Core::apply_selected_to_device(const std::vector<uint32_t>& slots) {
     if (slots.empty()) return;
+    if (apply_pending_) {
+        NKM_HIP(hipEventSynchronize(apply_ev_));
+        apply_pending_ = false;
+    }
     h_slots_tmp_.reserve(slots.size());
     std::memcpy(h_slots_tmp_.p, slots.data(), slots.size() * sizeof(uint32_t));
     d_slots_tmp_.reserve(slots.size(), false);
     NKM_HIP(hipMemcpyAsync(d_slots_tmp_.p, h_slots_tmp_.p, slots.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
                            stream_));
     NKM_HIP(launch_clear_alive(d_alive_.p, d_slots_tmp_.p, (uint32_t)slots.size(), stream_));
-    NKM_HIP(hipStreamSynchronize(stream_));
+    NKM_HIP(hipEventRecord(apply_ev_, stream_));
+    apply_pending_ = true;
 }
 
 }  // namespace nkm
