@@ -57,6 +57,32 @@ void mm_free_unpacked(void* set);
  * as a group of another rank (the caller orders those by ticket id), else 0. */
 int32_t mm_merge_positions(const int64_t* keys, const int32_t* counts, int32_t world, int32_t rank, int64_t* pos_out);
 
+/* ---- Row-sharded mode --------------------------------------------------
+ * For queries that cross pools (or a pool larger than one GPU) the pool
+ * split above does not hold.  Then every rank keeps the whole ticket set (the
+ * caller replicates Insert/Remove*) and runs the same pass, but each batch's
+ * searches are cut into `world` contiguous blocks balanced by source length:
+ * rank r evaluates block r only, and the blocks' results — per-search result
+ * records, hit lists (16 B per hit), RevPrecision flags and pair matrices —
+ * are exchanged in place, after which every rank replays the same lists into
+ * the same groups (processDefault's single ordered replay, replicated).  The
+ * RevThreshold timer is read at batch boundaries and OR-ed over the ranks, so
+ * the replicas never diverge.  Only mm_process's batch searches are split;
+ * a row's extra pages (a truncated list) are searched by every rank alike. */
+
+/* Host transport: fn(ctx, buf, offsets) must fill buf[offsets[q],
+ * offsets[q+1]) with rank q's segment for every q != rank (an in-place
+ * all-gather-v over host memory, e.g. gloo); offsets has world + 1 entries (bytes).
+ * Returns 0 on success. */
+typedef int (*mm_allgather_fn)(void* ctx, void* buf, const int64_t* offsets);
+int mm_shard_rows(void* h, int32_t world, int32_t rank, mm_allgather_fn fn, void* ctx);
+
+/* Device transport: the exchange runs as RCCL broadcasts over xGMI on the
+ * library's stream, between device buffers.  Rank 0 calls mm_rccl_unique_id
+ * (128 bytes) and every rank passes the same id to mm_shard_rows_rccl. */
+int mm_rccl_unique_id(uint8_t* out, int32_t cap);
+int mm_shard_rows_rccl(void* h, int32_t world, int32_t rank, const uint8_t* uid, int32_t len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,7 +74,7 @@ def router_lib(path: str = PRODUCT_SO) -> C.CDLL:
 
 
 CLUSTER_SYMBOLS = ("mm_route_keys", "mm_pack_tickets", "mm_unpack_tickets", "mm_free_unpacked",
-                   "mm_merge_positions")
+                   "mm_merge_positions", "mm_shard_rows", "mm_rccl_unique_id", "mm_shard_rows_rccl")
 
 
 def route_keys(tickets, n: int, pool_fields: Sequence[str]) -> np.ndarray:
@@ -348,3 +348,101 @@ class ClusterMatchmaker:
         """Remove (matchmaker.go:972-1024): ids may live on any rank; every
         rank removes the ones it holds (the others are no-ops there)."""
         self.local.Remove(list(tickets))
+
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64))
+
+
+class RowShardedMatchmaker:
+    """The row-sharded mode (include/nakama_cluster.h): for queries that cross
+    pools, every rank holds the whole ticket set and runs the same pass; each
+    batch's searches are split into one block per rank and the blocks'
+    results are exchanged in place before the (replicated) ordered replay, so
+    every rank forms the reference's groups.  transport "rccl": the exchange
+    runs inside the library as RCCL broadcasts between device buffers (xGMI);
+    "host": through a gloo all-gather of host buffers (the one-GPU rehearsal:
+    RCCL cannot put two ranks on one device); None: replicas only, no split.
+    Every method is a collective."""
+
+    def __init__(self, local: capi.Matchmaker, dist, transport: Optional[str] = "rccl"):
+        self.local = local
+        self.dist = dist
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.transport = transport
+        lib = router_lib()
+        lib.mm_shard_rows.restype = C.c_int
+        lib.mm_shard_rows.argtypes = [C.c_void_p, C.c_int32, C.c_int32, ALLGATHER_FN, C.c_void_p]
+        lib.mm_shard_rows_rccl.restype = C.c_int
+        lib.mm_shard_rows_rccl.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32]
+        lib.mm_rccl_unique_id.restype = C.c_int
+        lib.mm_rccl_unique_id.argtypes = [C.c_void_p, C.c_int32]
+        self.gather_bytes = 0  # exchanged by this rank's host all-gathers (host transport)
+        if transport == "rccl":
+            uid = (C.c_uint8 * 128)()
+            if self.rank == 0 and lib.mm_rccl_unique_id(uid, 128) != 0:
+                raise capi.ErrDevice("ncclGetUniqueId failed")
+            box = [bytes(uid) if self.rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            buf = (C.c_uint8 * 128).from_buffer_copy(box[0])
+            local._check(lib.mm_shard_rows_rccl(local.h, self.world, self.rank, buf, 128))
+        elif transport == "host":
+            self._fn = ALLGATHER_FN(self._allgather)
+            local._check(lib.mm_shard_rows(local.h, self.world, self.rank, self._fn, None))
+        # transport None: replicas only — every rank runs the whole pass itself
+        # (the CPU tests of the replication plumbing, over the oracle)
+
+    def _allgather(self, _ctx, buf, offsets) -> int:
+        """mm_allgather_fn over gloo: fill every other rank's segment of buf."""
+        import torch
+        try:
+            off = [offsets[i] for i in range(self.world + 1)]
+            sizes = [off[q + 1] - off[q] for q in range(self.world)]
+            m = max(max(sizes), 1)
+            mine = np.zeros(m, dtype=np.uint8)
+            n = sizes[self.rank]
+            if n:
+                C.memmove(mine.ctypes.data, buf + off[self.rank], n)
+            outs = [torch.zeros(m, dtype=torch.uint8) for _ in range(self.world)]
+            self.dist.all_gather(outs, torch.from_numpy(mine))
+            for q in range(self.world):
+                if q != self.rank and sizes[q]:
+                    C.memmove(buf + off[q], outs[q].numpy().ctypes.data, sizes[q])
+            self.gather_bytes += sum(sizes)
+            return 0
+        except Exception:
+            return 1
+
+    def Insert(self, tickets, n: int):
+        """Insert of this rank's ingest batch, replicated: every rank inserts
+        every rank's tickets, in rank order (identical stores)."""
+        import torch
+        buf = pack(tickets, np.arange(n, dtype=np.int32)) if n else np.zeros(0, dtype=np.uint8)
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world)]
+        self.dist.all_gather(sizes, torch.tensor([len(buf)], dtype=torch.int64))
+        sizes = [int(s.item()) for s in sizes]
+        m = max(max(sizes), 1)
+        pad = np.zeros(m, dtype=np.uint8)
+        pad[:len(buf)] = buf
+        outs = [torch.zeros(m, dtype=torch.uint8) for _ in range(self.world)]
+        self.dist.all_gather(outs, torch.from_numpy(pad))
+        for q in range(self.world):
+            u = Unpacked(outs[q].numpy()[:sizes[q]])
+            try:
+                if u.n.value:
+                    self.local._check(self.local.lib.mm_insert(self.local.h, u.tickets, u.n.value))
+            finally:
+                u.close()
+
+    def Remove(self, tickets: Sequence[str]):
+        gathered = [None] * self.world
+        self.dist.all_gather_object(gathered, list(tickets))
+        self.local.Remove([t for ts in gathered for t in ts])
+
+    def Process(self) -> capi.ProcessResult:
+        """The pass, searches split over the ranks; every rank returns the
+        same groups (the reference's, in its order)."""
+        return self.local.process_raw()
+
+    def Extract(self):
+        return self.local.Extract()

@@ -136,6 +136,12 @@ void mm_free_str_list(void* h, mm_str_list* out) {
 void mm_debug_set_pass_hook(void* h, void (*fn)(void*), void* ctx) {
     (void)guarded(h, [&](Core& c) { c.set_pass_hook(fn, ctx); return MM_OK; });
 }
+int mm_shard_rows(void* h, int32_t world, int32_t rank, mm_allgather_fn fn, void* ctx) {
+    return guarded(h, [&](Core& c) { return c.set_row_shard(world, rank, fn, ctx); });
+}
+int mm_shard_rows_rccl(void* h, int32_t world, int32_t rank, const uint8_t* uid, int32_t len) {
+    return guarded(h, [&](Core& c) { return c.set_row_shard_rccl(world, rank, uid, len); });
+}
 int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, double* scores_out, int32_t cap) {
     int32_t r = -1;
     int rc = guarded(h, [&](Core& c) {

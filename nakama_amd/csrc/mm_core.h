@@ -21,6 +21,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "../../include/nakama_cluster.h"
 #include "../../include/nakama_mm.h"
 #include "mm_device.h"
 #include "qcompile.h"
@@ -646,6 +647,23 @@ public:
     PinnedArray<DGroupResult> h_res_;
     PinnedArray<uint32_t> h_slots_tmp_;
     PinnedArray<uint8_t> h_pair_out_;
+
+    // ---- row-sharded mode (include/nakama_cluster.h) ----
+    int shard_world_ = 1, shard_rank_ = 0;
+    mm_allgather_fn shard_fn_ = nullptr;  // host transport
+    void* shard_ctx_ = nullptr;
+    void* nccl_comm_ = nullptr;           // device transport: an ncclComm_t (RCCL over xGMI)
+    // a transport is set (also at world 1: the exchange path runs, trivially)
+    bool row_shard() const { return shard_fn_ != nullptr || nccl_comm_ != nullptr; }
+    int set_row_shard(int world, int rank, mm_allgather_fn fn, void* ctx);
+    int set_row_shard_rccl(int world, int rank, const uint8_t* uid, int len);
+    // In-place all-gather-v of the byte ranges [off[q], off[q+1]) of a buffer:
+    // a device buffer over RCCL (enqueued on the stream), or a host buffer
+    // through the caller's function.
+    void shard_gather_device(void* dbuf, const std::vector<int64_t>& off);
+    void shard_gather_host(void* hbuf, const std::vector<int64_t>& off);
+    bool shard_any(bool v);  // OR over the ranks
+    void shard_release();
 
     // ---- open custom pass ----
     bool custom_open_ = false;

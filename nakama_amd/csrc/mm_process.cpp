@@ -203,7 +203,8 @@ struct Replay : ReplayCore {
         m_list.clear();
         mcl.clear();
         const int km = c.kernel_mode_;
-        if (rev || km == Core::KM_SEARCH || km == Core::KM_SCAN || c.order_head_ >= c.order_.size()) return false;
+        if (rev || km == Core::KM_SEARCH || km == Core::KM_SCAN || c.order_head_ >= c.order_.size() || c.row_shard())
+            return false;
         const bool any_size = km == Core::KM_MSCAN;
         const uint64_t order_len = c.order_.size() - c.order_head_;
         uint64_t covered = 0;
@@ -282,7 +283,7 @@ struct Replay : ReplayCore {
             if (on_m[i]) continue;
             const DGroup& d = bg[i].d;
             const bool big = d.src_len > kChunk && d.k > kChunk / 4;
-            if (!d.var_score && !rev && !d.has_cursor && d.src_len > 0 &&
+            if (!d.var_score && !rev && !d.has_cursor && d.src_len > 0 && !c.row_shard() &&
                 (c.kernel_mode_ == Core::KM_SCAN || (c.kernel_mode_ != Core::KM_SEARCH && big))) {
                 chunked.push_back(i);
                 continue;
@@ -376,11 +377,30 @@ struct Replay : ReplayCore {
             NKM_HIP(hipMemcpyAsync(c.d_mcl_.p, c.h_mcl_.p, mcl.size() * sizeof(DClause), hipMemcpyHostToDevice, stream));
         }
         NKM_HIP(hipMemcpyAsync(c.d_groups_.p, c.h_groups_.p, ng * sizeof(DGroup), hipMemcpyHostToDevice, stream));
+        // row-sharded: this rank evaluates the block [b0, b1) of the whole
+        // searches, cut at the world's quantiles of their source lengths
+        int b0 = 0, b1 = nwhole;
+        std::vector<int> blk;
+        if (c.row_shard()) {
+            const int W = c.shard_world_;
+            uint64_t tot = 0;
+            for (int i = 0; i < nwhole; i++) tot += lg[i].src_len + 64;
+            blk.assign(W + 1, nwhole);
+            blk[0] = 0;
+            uint64_t run = 0;
+            int q = 1;
+            for (int i = 0; i < nwhole && q < W; i++) {
+                run += lg[i].src_len + 64;
+                while (q < W && run * W >= tot * (uint64_t)q) blk[q++] = i + 1;
+            }
+            b0 = blk[c.shard_rank_];
+            b1 = blk[c.shard_rank_ + 1];
+        }
         // per eval kernel, the start/stop events of its dispatch (per-kernel roofline in bench.py)
         int kinds = 0;
-        for (size_t i = 0; i < nwhole; i++) kinds |= c.h_groups_.p[i].var_score ? 2 : 1;
-        NKM_HIP(launch_search(st, c.d_groups_.p, nwhole, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p, stream,
-                              c.ev_[0], c.ev_[1], kinds));
+        for (int i = b0; i < b1; i++) kinds |= c.h_groups_.p[i].var_score ? 2 : 1;
+        NKM_HIP(launch_search(st, c.d_groups_.p + b0, b1 - b0, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p + b0,
+                              stream, c.ev_[0], c.ev_[1], kinds));
         NKM_HIP(launch_scan(st, c.d_groups_.p + nwhole, nchunks, c.d_scan_.p, c.d_res_.p + nwhole, stream, c.ev_[2],
                             c.ev_[3]));
         if (use_m)
@@ -406,26 +426,63 @@ struct Replay : ReplayCore {
         }
         if (need_pm) {
             c.d_pm_.reserve((uint64_t)nwhole * kPairP, false);
-            NKM_HIP(launch_pairmat(st, c.d_groups_.p, c.d_res_.p, nwhole, c.d_out_.p, c.d_pm_.p, stream));
+            NKM_HIP(launch_pairmat(st, c.d_groups_.p + b0, c.d_res_.p + b0, b1 - b0, c.d_out_.p, c.d_pm_.p + (uint64_t)b0 * kPairP,
+                                   stream));
         }
         c.h_res_.reserve(std::max<uint32_t>(nres, 1));
-        NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, nres * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
         c.h_out_.reserve(std::max<uint64_t>(off, 1));
+        if (rev) c.h_rev_.reserve(std::max<uint64_t>(off, 1));
+        if (need_pm) c.h_pm_.reserve((uint64_t)nwhole * kPairP);
         const uint64_t whole_off = nwhole ? lg[nwhole - 1].out_off + lg[nwhole - 1].k : 0;
-        if (whole_off)
-            NKM_HIP(hipMemcpyAsync(c.h_out_.p, c.d_out_.p, whole_off * sizeof(DHit), hipMemcpyDeviceToHost, stream));
-        if (rev) {
-            c.h_rev_.reserve(std::max<uint64_t>(off, 1));
-            NKM_HIP(hipMemcpyAsync(c.h_rev_.p, c.d_rev_.p, off, hipMemcpyDeviceToHost, stream));
+        // the blocks' byte ranges in each exchanged buffer: result records,
+        // hit lists, RevPrecision flags, pair matrices
+        std::vector<int64_t> o_res, o_out, o_rev, o_pm;
+        if (c.row_shard()) {
+            for (int q = 0; q <= c.shard_world_; q++) {
+                const int b = blk[q];
+                const uint64_t oo = b < nwhole ? lg[b].out_off : whole_off;
+                o_res.push_back((int64_t)b * (int64_t)sizeof(DGroupResult));
+                o_out.push_back((int64_t)(oo * sizeof(DHit)));
+                o_rev.push_back((int64_t)oo);
+                o_pm.push_back((int64_t)b * kPairP * (int64_t)sizeof(uint32_t));
+            }
         }
-        if (need_pm) {
-            c.h_pm_.reserve((uint64_t)nwhole * kPairP);
-            NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, (uint64_t)nwhole * kPairP * sizeof(uint32_t),
-                                   hipMemcpyDeviceToHost, stream));
+        const bool host_x = c.row_shard() && !c.nccl_comm_;
+        if (c.row_shard() && c.nccl_comm_) {  // every block to every rank, in place, over xGMI
+            c.shard_gather_device(c.d_res_.p, o_res);
+            c.shard_gather_device(c.d_out_.p, o_out);
+            if (rev) c.shard_gather_device(c.d_rev_.p, o_rev);
+            if (need_pm) c.shard_gather_device(c.d_pm_.p, o_pm);
+        }
+        if (host_x) {  // this rank's block to the host; the others' arrive through the host all-gather
+            auto d2h = [&](void* h, const void* d, const std::vector<int64_t>& o) {
+                const int64_t n = o[c.shard_rank_ + 1] - o[c.shard_rank_];
+                if (n > 0)
+                    NKM_HIP(hipMemcpyAsync((char*)h + o[c.shard_rank_], (const char*)d + o[c.shard_rank_], (size_t)n,
+                                           hipMemcpyDeviceToHost, stream));
+            };
+            d2h(c.h_res_.p, c.d_res_.p, o_res);
+            d2h(c.h_out_.p, c.d_out_.p, o_out);
+            if (rev) d2h(c.h_rev_.p, c.d_rev_.p, o_rev);
+            if (need_pm) d2h(c.h_pm_.p, c.d_pm_.p, o_pm);
+        } else {
+            NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, nres * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
+            if (whole_off)
+                NKM_HIP(hipMemcpyAsync(c.h_out_.p, c.d_out_.p, whole_off * sizeof(DHit), hipMemcpyDeviceToHost, stream));
+            if (rev) NKM_HIP(hipMemcpyAsync(c.h_rev_.p, c.d_rev_.p, off, hipMemcpyDeviceToHost, stream));
+            if (need_pm)
+                NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, (uint64_t)nwhole * kPairP * sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, stream));
         }
         if (overlap) overlap();
         NKM_HIP(hipStreamSynchronize(stream));
-        const bool ran[3] = {nwhole > 0, nchunks > 0, use_m};
+        if (host_x) {
+            c.shard_gather_host(c.h_res_.p, o_res);
+            c.shard_gather_host(c.h_out_.p, o_out);
+            if (rev) c.shard_gather_host(c.h_rev_.p, o_rev);
+            if (need_pm) c.shard_gather_host(c.h_pm_.p, o_pm);
+        }
+        const bool ran[3] = {b1 > b0, nchunks > 0, use_m};
         for (int kk = 0; kk < 3; kk++) {
             if (!ran[kk]) continue;
             float ms_k = 0.f;
@@ -435,6 +492,7 @@ struct Replay : ReplayCore {
         }
         stats.batches++;
         for (int t = 0; t < nwhole + nchunks; t++) {
+            if (t < b0 || (t >= b1 && t < nwhole)) continue;  // another rank's block
             stats.pair_evals += c.h_res_.p[t].scanned;
             stats.k_bytes[t < nwhole ? 0 : 1] += search_bytes(c.sigs_[bg[lg_group[t]].sig], lg[t], c.h_res_.p[t]);
         }
@@ -830,8 +888,9 @@ int Core::process_default(GroupList& out_groups,
     while (true) {
         while (pos < rows.size() && sel[rows[pos]]) pos++;
         if (pos >= rows.size()) break;
-        // the RevThreshold timer fired: the remaining rows search as without RevPrecision
-        if (rev && timer.check()) rev = rp.rev = false;
+        // the RevThreshold timer fired: the remaining rows search as without
+        // RevPrecision (row-sharded: decided at batch starts, OR-ed over the ranks)
+        if (rev && (row_shard() ? shard_any(timer.check()) : timer.check())) rev = rp.rev = false;
         // ---- assemble the batch ----
         const auto ta0 = std::chrono::steady_clock::now();
         for (auto& g : bg)
@@ -1011,7 +1070,7 @@ int Core::process_default(GroupList& out_groups,
             // hold tickets selected earlier in this batch, which the walk skips,
             // so the list stays exact.
             BGroup& bgr = bg[brow_group[bi]];
-            if (rp.rev && timer.check()) rp.rev = false;  // later rows of this batch skip the reverse checks
+            if (rp.rev && !row_shard() && timer.check()) rp.rev = false;  // later rows skip the reverse checks
             auto status = rp.decide(T, bgr, bi == 0 || (page_mode_ && !bgr.d.var_score), grp);
             if (status == Replay::EXHAUSTED) {
                 exhausted = true;
@@ -1068,7 +1127,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
     // every row is independent: one search per row, in chunks
     for (size_t base = 0; base < rows.size(); base += kMaxBatchRows / 4) {
         const size_t end = std::min(rows.size(), base + kMaxBatchRows / 4);
-        if (rev && timer.check()) rev = rp.rev = false;
+        if (rev && (row_shard() ? shard_any(timer.check()) : timer.check())) rev = rp.rev = false;
         std::vector<BGroup> bg(end - base);
         uint64_t off = 0;
         h_groups_.reserve(bg.size());
@@ -1099,7 +1158,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
         for (size_t i = 0; i < bg.size(); i++) {
             BGroup& g = bg[i];
             const uint32_t T = g.row_slot;
-            if (rev && timer.check()) rev = rp.rev = false;  // :353-358
+            if (rev && !row_shard() && timer.check()) rev = rp.rev = false;  // :353-358
             // all hits (paging through the list), filtered as :425-468
             std::vector<uint32_t> hits, hpos;
             uint32_t j = 0;

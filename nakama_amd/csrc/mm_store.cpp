@@ -214,6 +214,7 @@ WorkPool& Core::workers() {
 
 Core::~Core() {
     workers_.reset();
+    shard_release();
     (void)hipSetDevice(device_);
     for (auto* p : d_fval_) delete p;
     for (auto* p : d_fkind_) delete p;

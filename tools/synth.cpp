@@ -253,6 +253,21 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             t.max_count = shape == 0 ? 2 : 4;
             break;
         }
+        case 9: {  // C2's skill windows without the region must: every search crosses the
+                   // region pools (the row-sharded mode's workload, include/nakama_cluster.h)
+            const char* region = shard_regions_i[r.next() & 3];
+            const int s = (int)std::lround(r.normal(1500.0, 300.0));
+            S->sp.push_back({"region", region});
+            S->np.push_back({"skill", (double)s});
+            char q[256];
+            std::snprintf(q, sizeof q,
+                          "+properties.skill:>=%d +properties.skill:<=%d properties.skill:>=%d^2 "
+                          "properties.skill:<=%d^2 properties.region:%s",
+                          s - 200, s + 200, s - 50, s + 50, region);
+            query = q;
+            t.min_count = t.max_count = 2;
+            break;
+        }
         case 8: {  // datetime-typed string properties (blugeProcessProperty, match_common.go:161-170,221-236)
                    // and RFC3339 date-range clauses (query_string_parser.go:234-250)
             party = r.uni() < 0.85 ? 1 : 2;
