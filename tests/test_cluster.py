@@ -35,6 +35,24 @@ def _free_port():
     return p
 
 
+def _wait(q, procs, timeout=600):
+    """The rank-0 result, failing fast (instead of waiting out the timeout)
+    when a rank died."""
+    import queue
+    import time
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            return q.get(timeout=2)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead:
+                for p in procs:
+                    p.kill()
+                raise AssertionError(f"a rank exited with {dead}")
+    raise AssertionError("no result")
+
+
 def _make(config, n, world, rank, groups, ties=False):
     from nakama_amd import synth
     lo, hi = n * rank // world, n * (rank + 1) // world
@@ -90,7 +108,7 @@ def run_cluster(config, n, groups, passes, cfg, world=2, use_product=False, ties
              for r in range(world)]
     for p in procs:
         p.start()
-    res = q.get(timeout=600)
+    res = _wait(q, procs)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-from test_cluster import _free_port  # noqa: E402
+from test_cluster import _free_port, _wait  # noqa: E402
 
 
 def row_worker(rank, world, port, config, n, passes, cfg, transport, use_product, q, backend="gloo"):
@@ -69,7 +69,7 @@ def run_rows(config, n, passes, cfg, transport, use_product, world=2, backend="g
              for r in range(world)]
     for p in procs:
         p.start()
-    res = q.get(timeout=600)
+    res = _wait(q, procs)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
