@@ -117,7 +117,7 @@ def test_row_sharded_rccl_transport_world1():
     """The RCCL path (grouped in-place ncclBroadcast on the library's stream)
     at world 1 — the exchange runs, trivially — equal to the oracle."""
     cfg = dict(max_intervals=2)
-    allout = run_rows(9, 2000, 2, cfg, "rccl", True, world=1, backend="nccl")
+    allout = run_rows(9, 2000, 2, cfg, "rccl", True, world=1)
     want = oracle_passes(9, 2000, 2, cfg)
     out, _ = allout[0]
     assert [(g, s, a) for g, s, a, _ in out] == want

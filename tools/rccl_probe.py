@@ -12,7 +12,9 @@ os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29541")
 torch.cuda.set_device(0)
 print("init pg", flush=True)
-dist.init_process_group(os.environ.get("PROBE_BACKEND", "gloo"), rank=0, world_size=1)
+world = int(os.environ.get("WORLD_SIZE", "1"))
+rank = int(os.environ.get("RANK", "0"))
+dist.init_process_group(os.environ.get("PROBE_BACKEND", "gloo"), rank=rank, world_size=world)
 import nakama_amd  # noqa: E402
 from nakama_amd import capi, cluster, synth  # noqa: E402
 
@@ -20,7 +22,7 @@ mm = nakama_amd.LocalMatchmaker(max_intervals=2)
 print("row shard init", flush=True)
 rm = cluster.RowShardedMatchmaker(mm, dist, transport="rccl")
 print("insert", flush=True)
-ts = synth.TicketSet(9, 2000)
+ts = synth.TicketSet(9, 2000 // world, first=rank * (2000 // world))
 rm.Insert(ts.ptr(), ts.n)
 print("process", flush=True)
 t0 = time.time()
