@@ -33,6 +33,10 @@ namespace nkm {
 hipError_t launch_search(const DStore& st, const DGroup* d_groups, int n_groups, DHit* d_out, uint8_t* d_rev,
                          DGroupResult* d_res, hipStream_t stream, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
                          int kinds = 3);
+hipError_t launch_rsmall(const DStore& st, const DGroup* d_groups, const uint32_t* d_rows, uint32_t n_rows, DHit* d_out,
+                         uint8_t* d_rev, uint32_t* d_pm, DGroupResult* d_res, hipStream_t stream, hipEvent_t ev0,
+                         hipEvent_t ev1);
+int small_src_max();
 hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_t n, hipStream_t stream,
                               uint8_t value = 0);
 hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, uint8_t* d_out, hipStream_t stream);
@@ -331,15 +335,16 @@ struct RevTimer {
 struct PassStats {
     int full_lists = 0;  // variable-score searches run as full lists (host-sorted)
     // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel
-    double k_ms[3] = {0, 0, 0};      // HIP-event time of the launches
-    int64_t k_bytes[3] = {0, 0, 0};  // algorithmic bytes
-    int k_launches[3] = {0, 0, 0};
+    // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel
+    double k_ms[4] = {0, 0, 0, 0};      // HIP-event time of the launches
+    int64_t k_bytes[4] = {0, 0, 0, 0};  // algorithmic bytes
+    int k_launches[4] = {0, 0, 0, 0};
     int64_t pair_evals = 0;
-    double eval_ms() const { return k_ms[0] + k_ms[1] + k_ms[2]; }
-    int launches() const { return k_launches[0] + k_launches[1] + k_launches[2]; }
+    double eval_ms() const { return k_ms[0] + k_ms[1] + k_ms[2] + k_ms[3]; }
+    int launches() const { return k_launches[0] + k_launches[1] + k_launches[2] + k_launches[3]; }
     int dominant() const {  // the kernel with the most algorithmic bytes
         int d = 0;
-        for (int k = 1; k < 3; k++)
+        for (int k = 1; k < 4; k++)
             if (k_bytes[k] > k_bytes[d]) d = k;
         return d;
     }
@@ -462,6 +467,7 @@ private:
     bool track_removed_ = false;
     std::vector<std::string> removed_ids_;
     std::unordered_map<const char* const*, std::vector<std::string>*> str_lists_;  // outstanding drains
+    std::mutex pair_mu_;     // Replay::pair_slow from pool workers
     std::mutex process_mu_;  // one pass at a time (the ticker); lock order process_mu_ -> mu_
     int remove_session_locked(const std::string& sid, const std::string& ticket);
     int remove_session_all_locked(const std::string& sid);
@@ -501,6 +507,7 @@ private:
     void finish_pass_serial(GroupList& groups, bool selected);
     void fill_matched(const GroupList& groups, mm_matched* out, bool cands);
     void choose_source(const Sig& s, DGroup& g, SrcChoice* ch = nullptr);
+    void source_of(const Sig& s, DGroup& g, SrcChoice* ch = nullptr) const;
     struct ParPlan {  // a batch's pools (plan_parallel), bucketed while its searches run
         bool ok = false;
         size_t ng = 0;
@@ -513,7 +520,8 @@ private:
     bool replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
                          const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                          GroupList& out_groups,
-                         std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats);
+                         std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats,
+                         bool rev = false);
     void apply_selected_to_device(const std::vector<uint32_t>& slots);
 
     std::mutex mu_;
@@ -524,7 +532,8 @@ private:
     std::string last_error_;
     int device_ = 0;
     hipStream_t stream_ = nullptr;
-    hipEvent_t ev_[7] = {};  // start/stop of the search / scan / mscan dispatches; a marker before stitch_kernel
+    hipEvent_t ev_[9] = {};  // start/stop of the search / scan / mscan dispatches, a marker before stitch_kernel,
+                             // start/stop of the rsmall dispatch
     hipEvent_t apply_ev_ = nullptr;  // after the last asynchronous alive-flag update (h_slots_tmp_ reuse)
     bool apply_pending_ = false;
     std::unique_ptr<WorkPool> workers_;  // created on the first large pass
@@ -636,6 +645,8 @@ public:
     DevArray<DMSig> d_msig_;         // mscan_kernel's signatures
     PinnedArray<DMSig> h_msig_;
     DevArray<uint8_t> d_rev_;
+    DevArray<uint32_t> d_small_;     // rsmall_kernel's rows (indexes of the batch's whole searches)
+    PinnedArray<uint32_t> h_small_;
     PinnedArray<DHit> h_page_;       // fetch_more's page (pinned: one round trip)
     PinnedArray<uint8_t> h_page_rev_;
     DevArray<DGroupResult> d_res_;

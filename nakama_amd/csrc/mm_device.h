@@ -64,12 +64,15 @@ struct DGroup {
     uint32_t src_off;
     uint32_t src_len;
     uint32_t k;            // max entries to emit
+    uint32_t path;         // 0: search_kernel; 1: rsmall_kernel (a short source, one wave per row)
     uint64_t out_off;      // first output entry
     int64_t ub_key;        // sortable key of an upper bound of any score (early exit)
     int64_t cur_key;       // pagination cursor: emit only entries after (cur_key, cur_idx)
     uint32_t cur_idx;
     uint32_t has_cursor;
 };
+
+static_assert(sizeof(DGroup) == 80, "DGroup layout");
 
 // Per-group result.
 struct DGroupResult {

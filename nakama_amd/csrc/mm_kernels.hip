@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     __shared__ uint8_t trev[kBlock];
 
     const DGroup g = groups[blockIdx.x];
-    if ((g.var_score != 0) != (VK > 0)) return;  // the other instantiation's search (block-uniform)
+    if ((g.var_score != 0) != (VK > 0) || g.path != 0) return;  // another instantiation's / kernel's search
     const uint32_t* src = g.src_kind == 0 ? st.order : st.postings;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -675,26 +675,113 @@ __global__ void pair_kernel(DStore st, const uint32_t* __restrict__ pairs, uint3
 }
 
 // Pair matrices for RevPrecision combos (matchmaker_process.go:178-203): for
-// the first 32 entries a, b of each search's list, bit b of pm[g*32+a] is
-// "entry b's document matches entry a's parsed query".
+// the first 32 entries a, b of each search's list, bit b of pm[out_off + a]
+// is "entry b's document matches entry a's parsed query" (one word per list
+// entry, beside the entry).  rsmall_kernel writes its searches' own.
 __global__ void pairmat_kernel(DStore st, const DGroup* __restrict__ groups, const DGroupResult* __restrict__ res,
                                int n_groups, const DHit* __restrict__ out, uint32_t* __restrict__ pm) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int g = t >> 5, a = t & 31;
-    if (g >= n_groups) return;
+    if (g >= n_groups || groups[g].path != 0) return;
     const uint32_t n = res[g].count < 32u ? res[g].count : 32u;
+    if ((uint32_t)a >= n) return;
     uint32_t mask = 0;
-    if ((uint32_t)a < n) {
-        const uint64_t base = groups[g].out_off;
-        const uint32_t from = out[base + a].slot;
-        const DQuery q = st.squery[from];
-        for (uint32_t b = 0; b < n; b++) {
+    const uint64_t base = groups[g].out_off;
+    const uint32_t from = out[base + a].slot;
+    const DQuery q = st.squery[from];
+    for (uint32_t b = 0; b < n; b++) {
+        double d;
+        if (eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, out[base + b].slot, &d)) mask |= 1u << b;
+    }
+    pm[base + a] = mask;
+}
+
+// ---- RevPrecision rows over short sources ---------------------------------------
+// With RevPrecision every row is its own search (the reverse check depends on
+// the row), and with bucketed queries (C5: buckets of 8) a row's source is a
+// few entries: search_kernel would spend a 256-lane workgroup per row.  Here
+// one wave takes one row (4 rows per workgroup): lane j evaluates source entry
+// j (the predicate, its score key, and the reverse check Q_H(T)), the wave
+// ranks its matches by (score key desc, source position asc) with shuffles —
+// the hit order of search_kernel's top-K — and writes the whole list, its
+// reverse flags and (pm != null) the pair matrix of its first 32 entries.
+constexpr int kSmallSrc = 64;
+
+__global__ __launch_bounds__(kBlock) void rsmall_kernel(DStore st, const DGroup* __restrict__ groups,
+                                                        const uint32_t* __restrict__ rows, uint32_t n_rows,
+                                                        DHit* __restrict__ out, uint8_t* __restrict__ out_rev,
+                                                        uint32_t* __restrict__ pm, DGroupResult* __restrict__ res) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t r = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (r >= n_rows) return;  // wave-uniform
+    const uint32_t gi = rows[r];
+    const DGroup g = groups[gi];
+    const uint32_t* src = (g.src_kind == 0 ? st.order : st.postings) + g.src_off;
+    const uint32_t j = (uint32_t)lane;
+    bool m = false, live = false;
+    uint32_t s = kNoSlot;
+    int64_t key = 0;
+    uint8_t rv = 1;
+    if (j < g.src_len) {
+        s = src[j];
+        live = st.alive[s] != 0;
+        m = live && st.minc[s] >= g.tmin && st.maxc[s] <= g.tmax && (g.tparty == kNoParty || st.party[s] != g.tparty);
+        double sp = 0.0;
+        if (m) m = eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
+        if (m) {
+            key = dsortable((sp + 1.0) + 1.0);
+            const DQuery q = st.squery[s];
             double d;
-            if (eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, out[base + b].slot, &d)) mask |= 1u << b;
+            rv = eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, g.rev_slot, &d) ? 1 : 0;
         }
     }
-    pm[(uint64_t)g * 32 + a] = mask;
+    const uint64_t mask = __ballot(m);
+    // rank among the matches: higher keys first, then earlier source positions
+    uint32_t rank = 0;
+    for (uint64_t rest = mask; rest; rest &= rest - 1) {
+        const int i = __builtin_ctzll(rest);
+        const int64_t ki = __shfl(key, i);
+        rank += (ki > key) || (ki == key && (uint32_t)i < j);
+    }
+    if (m) {
+        out[g.out_off + rank] = DHit{s, j, key};
+        if (out_rev) out_rev[g.out_off + rank] = rv;
+    }
+    const uint32_t cnt = (uint32_t)__popcll(mask);
+    if (pm) {
+        // entry `rank` (a < 32): bit b = entry b's document matches this entry's query
+        uint32_t pmask = 0;
+        const DQuery q = m ? st.squery[s] : DQuery{};
+        for (uint64_t rest = mask; rest; rest &= rest - 1) {
+            const int i = __builtin_ctzll(rest);
+            const uint32_t si = (uint32_t)__shfl((int)s, i);
+            const int64_t ki = __shfl(key, i);
+            uint32_t ri = 0;  // entry i's rank
+            for (uint64_t rr = mask; rr; rr &= rr - 1) {
+                const int t = __builtin_ctzll(rr);
+                const int64_t kt = __shfl(key, t);
+                ri += (kt > ki) || (kt == ki && t < i);
+            }
+            if (m && rank < 32 && ri < 32) {
+                double d;
+                if (eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, si, &d)) pmask |= 1u << ri;
+            }
+        }
+        if (m && rank < 32) pm[g.out_off + rank] = pmask;
+    }
+    const uint32_t nlive = (uint32_t)__popcll(__ballot(live));
+    if (lane == 0) res[gi] = DGroupResult{cnt, 1u, g.src_len, cnt, nlive, 0u};
 }
+
+hipError_t launch_rsmall(const DStore& st, const DGroup* d_groups, const uint32_t* d_rows, uint32_t n_rows, DHit* d_out,
+                         uint8_t* d_rev, uint32_t* d_pm, DGroupResult* d_res, hipStream_t stream, hipEvent_t ev0,
+                         hipEvent_t ev1) {
+    if (n_rows == 0) return hipSuccess;
+    hipExtLaunchKernelGGL(rsmall_kernel, dim3((n_rows + kWaves - 1) / kWaves), dim3(kBlock), 0, stream, ev0, ev1, 0, st,
+                          d_groups, d_rows, n_rows, d_out, d_rev, d_pm, d_res);
+    return hipGetLastError();
+}
+int small_src_max() { return kSmallSrc; }
 
 hipError_t launch_pairmat(const DStore& st, const DGroup* d_groups, const DGroupResult* d_res, int n_groups,
                           const DHit* d_out, uint32_t* d_pm, hipStream_t stream) {

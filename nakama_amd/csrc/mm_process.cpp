@@ -161,6 +161,7 @@ struct Replay : ReplayCore {
     std::vector<uint32_t> m_list;           // BGroups on mscan_kernel
     std::vector<DClause> mcl;               // their clauses, field = index into DMScan::field
     std::vector<DMSig> msig;
+    std::vector<uint32_t> small_rows;       // rsmall_kernel's searches (indexes into lg)
 
     // The mscan descriptor of one search; a term-only signature gets its
     // required values per scanned field and its hit key, summed exactly as
@@ -289,12 +290,19 @@ struct Replay : ReplayCore {
                 continue;
             }
             DGroup w = d;
+            w.path = 0;
+            // a RevPrecision row over a short source: rsmall_kernel, whole list
+            if (d.rev_slot != kNoSlot && rev && !d.has_cursor && d.src_len > 0 &&
+                d.src_len <= (uint32_t)small_src_max()) {
+                w.path = 1;
+                w.k = d.src_len;
+            }
             // A variable-score search whose rows need more than the LDS top-K
             // (k was capped at kVarK) over a small source runs as a full list:
             // the constant-score path emits every hit with its own score key
             // in source order, and the host sorts it stably by key (source
             // order breaks ties, as the top-K does), so the list is complete.
-            if (d.var_score && !rev && !d.has_cursor && d.k >= (uint32_t)var_k_capacity() && d.src_len > d.k &&
+            if (w.path == 0 && d.var_score && !rev && !d.has_cursor && d.k >= (uint32_t)var_k_capacity() && d.src_len > d.k &&
                 d.src_len <= kFullVarMax && c.full_var_mode_ && budget + (d.src_len - d.k) <= kOutCap) {
                 budget += d.src_len - d.k;
                 w.var_score = 0;
@@ -399,8 +407,25 @@ struct Replay : ReplayCore {
         // per eval kernel, the start/stop events of its dispatch (per-kernel roofline in bench.py)
         int kinds = 0;
         for (int i = b0; i < b1; i++) kinds |= c.h_groups_.p[i].var_score ? 2 : 1;
+        // rsmall_kernel's rows of this rank's block
+        std::vector<uint32_t>& small = small_rows;
+        small.clear();
+        for (int i = b0; i < b1; i++)
+            if (c.h_groups_.p[i].path == 1) small.push_back((uint32_t)i);
+        if (small.size() == (size_t)(b1 - b0)) kinds = 0;  // no search_kernel work
         NKM_HIP(launch_search(st, c.d_groups_.p + b0, b1 - b0, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p + b0,
                               stream, c.ev_[0], c.ev_[1], kinds));
+        if (need_pm) c.d_pm_.reserve(std::max<uint64_t>(off, 1), false);  // one word per list entry
+        if (!small.empty()) {
+            c.h_small_.reserve(small.size());
+            std::memcpy(c.h_small_.p, small.data(), small.size() * sizeof(uint32_t));
+            c.d_small_.reserve(small.size(), false);
+            NKM_HIP(hipMemcpyAsync(c.d_small_.p, c.h_small_.p, small.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                   stream));
+            NKM_HIP(launch_rsmall(st, c.d_groups_.p, c.d_small_.p, (uint32_t)small.size(), c.d_out_.p,
+                                  rev ? c.d_rev_.p : nullptr, need_pm ? c.d_pm_.p : nullptr, c.d_res_.p, stream,
+                                  c.ev_[7], c.ev_[8]));
+        }
         NKM_HIP(launch_scan(st, c.d_groups_.p + nwhole, nchunks, c.d_scan_.p, c.d_res_.p + nwhole, stream, c.ev_[2],
                             c.ev_[3]));
         if (use_m)
@@ -424,15 +449,12 @@ struct Replay : ReplayCore {
             NKM_HIP(launch_stitch(c.d_map_.p, (int)nmap, c.d_res_.p + nwhole, c.d_cranges_.p, (int)ns, c.d_coffs_.p,
                                   c.d_scan_.p, c.d_out_.p, stream));
         }
-        if (need_pm) {
-            c.d_pm_.reserve((uint64_t)nwhole * kPairP, false);
-            NKM_HIP(launch_pairmat(st, c.d_groups_.p + b0, c.d_res_.p + b0, b1 - b0, c.d_out_.p, c.d_pm_.p + (uint64_t)b0 * kPairP,
-                                   stream));
-        }
+        if (need_pm && kinds)
+            NKM_HIP(launch_pairmat(st, c.d_groups_.p + b0, c.d_res_.p + b0, b1 - b0, c.d_out_.p, c.d_pm_.p, stream));
         c.h_res_.reserve(std::max<uint32_t>(nres, 1));
         c.h_out_.reserve(std::max<uint64_t>(off, 1));
         if (rev) c.h_rev_.reserve(std::max<uint64_t>(off, 1));
-        if (need_pm) c.h_pm_.reserve((uint64_t)nwhole * kPairP);
+        if (need_pm) c.h_pm_.reserve(std::max<uint64_t>(off, 1));
         const uint64_t whole_off = nwhole ? lg[nwhole - 1].out_off + lg[nwhole - 1].k : 0;
         // the blocks' byte ranges in each exchanged buffer: result records,
         // hit lists, RevPrecision flags, pair matrices
@@ -444,7 +466,7 @@ struct Replay : ReplayCore {
                 o_res.push_back((int64_t)b * (int64_t)sizeof(DGroupResult));
                 o_out.push_back((int64_t)(oo * sizeof(DHit)));
                 o_rev.push_back((int64_t)oo);
-                o_pm.push_back((int64_t)b * kPairP * (int64_t)sizeof(uint32_t));
+                o_pm.push_back((int64_t)(oo * sizeof(uint32_t)));
             }
         }
         const bool host_x = c.row_shard() && !c.nccl_comm_;
@@ -470,9 +492,8 @@ struct Replay : ReplayCore {
             if (whole_off)
                 NKM_HIP(hipMemcpyAsync(c.h_out_.p, c.d_out_.p, whole_off * sizeof(DHit), hipMemcpyDeviceToHost, stream));
             if (rev) NKM_HIP(hipMemcpyAsync(c.h_rev_.p, c.d_rev_.p, off, hipMemcpyDeviceToHost, stream));
-            if (need_pm)
-                NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, (uint64_t)nwhole * kPairP * sizeof(uint32_t),
-                                       hipMemcpyDeviceToHost, stream));
+            if (need_pm && whole_off)
+                NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, whole_off * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         }
         if (overlap) overlap();
         NKM_HIP(hipStreamSynchronize(stream));
@@ -482,11 +503,12 @@ struct Replay : ReplayCore {
             if (rev) c.shard_gather_host(c.h_rev_.p, o_rev);
             if (need_pm) c.shard_gather_host(c.h_pm_.p, o_pm);
         }
-        const bool ran[3] = {b1 > b0, nchunks > 0, use_m};
-        for (int kk = 0; kk < 3; kk++) {
+        const bool ran[4] = {kinds != 0, nchunks > 0, use_m, !small.empty()};
+        static const int ev0[4] = {0, 2, 4, 7};
+        for (int kk = 0; kk < 4; kk++) {
             if (!ran[kk]) continue;
             float ms_k = 0.f;
-            NKM_HIP(hipEventElapsedTime(&ms_k, c.ev_[2 * kk], c.ev_[2 * kk + 1]));
+            NKM_HIP(hipEventElapsedTime(&ms_k, c.ev_[ev0[kk]], c.ev_[ev0[kk] + 1]));
             stats.k_ms[kk] += ms_k;
             stats.k_launches[kk]++;
         }
@@ -494,7 +516,8 @@ struct Replay : ReplayCore {
         for (int t = 0; t < nwhole + nchunks; t++) {
             if (t < b0 || (t >= b1 && t < nwhole)) continue;  // another rank's block
             stats.pair_evals += c.h_res_.p[t].scanned;
-            stats.k_bytes[t < nwhole ? 0 : 1] += search_bytes(c.sigs_[bg[lg_group[t]].sig], lg[t], c.h_res_.p[t]);
+            const int kk = t >= nwhole ? 1 : lg[t].path == 1 ? 3 : 0;
+            stats.k_bytes[kk] += search_bytes(c.sigs_[bg[lg_group[t]].sig], lg[t], c.h_res_.p[t]);
         }
         if (use_m) {
             // columns read once per candidate for all signatures; hits written per signature
@@ -516,7 +539,7 @@ struct Replay : ReplayCore {
             g.head = 0;
             g.hits = c.h_out_.p + lg[i].out_off;
             g.rev = rev ? c.h_rev_.p + lg[i].out_off : nullptr;
-            g.pm = need_pm ? c.h_pm_.p + (uint64_t)i * kPairP : nullptr;
+            g.pm = need_pm ? c.h_pm_.p + lg[i].out_off : nullptr;
             g.pm_n = need_pm ? std::min<uint32_t>(r.count, kPairP) : 0;
             g.n = r.count;
             g.complete = r.complete != 0;
@@ -543,7 +566,9 @@ struct Replay : ReplayCore {
     }
 
     bool pair_slow(const BGroup& g, uint32_t from_pos, uint32_t to_pos) override {
-        // slow path: evaluate the single pair on the device
+        // slow path: evaluate the single pair on the device (pool workers of a
+        // RevPrecision parallel replay share the stream and the buffers)
+        std::lock_guard<std::mutex> lk(c.pair_mu_);
         uint32_t pr[2] = {g.hits[from_pos].slot, g.hits[to_pos].slot};
         c.d_slots_tmp_.reserve(2, false);
         c.d_pair_out_.reserve(1, false);
@@ -657,7 +682,7 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
 bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
                            const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                            GroupList& out_groups,
-                           std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats) {
+                           std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats, bool rev) {
     if (!P.ok) return false;
     for (const BGroup& g : bg)
         if (!g.complete) return false;
@@ -700,7 +725,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
     constexpr uint32_t kGatherChunk = 16384;
     std::vector<uint8_t> dense(ng, 0);
     for (size_t gi = 0; gi < ng; gi++) {
-        if (pool_searches[gi].size() != 1 || !dense_mode_) continue;
+        if (pool_searches[gi].size() != 1 || !dense_mode_ || rev) continue;  // the dense walk has no reverse checks
         dense[gi] = 1;
         DensePool& P = dense_pools_[gi];
         P.reset(bg[pool_searches[gi][0]], grows[gi], brow.data());
@@ -737,7 +762,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
             std::vector<BGroup> mine;
             mine.reserve(pool_searches[gi].size());
             for (uint32_t i : pool_searches[gi]) mine.push_back(bg[i]);
-            Replay rp(*this, tl_sel, false, maxI, ls, st, stream_);
+            Replay rp(*this, tl_sel, rev, maxI, ls, st, stream_);
             replay_pool(rp, grows[gi], brow.data(),
                         [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; }, tl_sel,
                         tl_proc.data(), minc_.data(), maxc_.data(), o);
@@ -824,6 +849,31 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
         stats.par_rows += task_rows[k];
     }
     return true;
+}
+
+// choose_source without advancing the posting lists' dead-prefix heads (safe
+// on the host workers): the same list, possibly starting at dead entries.
+void Core::source_of(const Sig& s, DGroup& g, SrcChoice* ch) const {
+    g.src_kind = 0;
+    g.src_off = order_head_;
+    g.src_len = (uint32_t)order_.size() - order_head_;
+    bool have = false;
+    if (ch) ch->has_term = false;
+    for (auto& mt : s.must_terms) {
+        auto it = postings_map_.find(((uint64_t)mt.first << 32) | mt.second);
+        uint32_t off = 0, len = 0;
+        if (it != postings_map_.end()) {
+            off = it->second.off + it->second.head;
+            len = it->second.len - it->second.head;
+        }
+        if (!have || len < g.src_len) {
+            if (ch) { ch->has_term = true; ch->field = mt.first; ch->term = mt.second; }
+            g.src_kind = 1;
+            g.src_off = off;
+            g.src_len = len;
+            have = true;
+        }
+    }
 }
 
 void Core::choose_source(const Sig& s, DGroup& g, SrcChoice* ch) {
@@ -1004,7 +1054,64 @@ int Core::process_default(GroupList& out_groups,
             });
             return true;
         };
-        if (!assemble_parallel()) {
+        // RevPrecision: one search per row; large batches build them on the
+        // workers (sources from a non-mutating lookup of the posting ranges)
+        auto assemble_parallel_rev = [&]() -> bool {
+            const size_t nr = rows.size() - pos;
+            if (!rev || retry_slot != kNoSlot || !par_mode_ || nr < par_min(65536) || nr > kMaxBatchRows) return false;
+            WorkPool& wp = workers();
+            const unsigned nch = wp.size() * 4;
+            std::vector<std::vector<BGroup>> cg(nch);
+            std::vector<std::vector<uint32_t>> crow(nch);
+            std::vector<uint64_t> ck(nch, 0);
+            wp.run(nch, [&](size_t c) {
+                for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
+                    const uint32_t r = rows[i];
+                    if (sel[r]) continue;
+                    BGroup g;
+                    g.sig = sig_[r];
+                    const Sig& sg = sigs_[g.sig];
+                    g.d.clause_off = sg.clause_off;
+                    g.d.n_clauses = sg.n_clauses;
+                    g.d.qkind = sg.qkind;
+                    g.d.var_score = sg.var_score ? 1 : 0;
+                    g.d.tmin = sg.tmin;
+                    g.d.tmax = sg.tmax;
+                    g.d.tparty = sg.tparty;
+                    g.d.rev_slot = r;
+                    g.d.ub_key = sg.ub_key;
+                    SrcChoice ch;
+                    source_of(sg, g.d, &ch);
+                    g.has_src_term = ch.has_term;
+                    g.src_field = ch.field;
+                    g.src_term = ch.term;
+                    g.row_slot = r;
+                    g.nrows = 1;
+                    g.d.k = cap_k(g, 1, maxc_[r]);
+                    ck[c] += g.d.k;
+                    cg[c].push_back(std::move(g));
+                    crow[c].push_back(r);
+                }
+            });
+            uint64_t tot = 0;
+            size_t n = 0;
+            for (unsigned c = 0; c < nch; c++) tot += ck[c], n += cg[c].size();
+            if (tot > kOutCap) return false;  // the serial loop cuts the batch
+            bg.reserve(n);
+            brow.resize(n);
+            brow_group.resize(n);
+            for (unsigned c = 0; c < nch; c++) {
+                for (size_t k = 0; k < cg[c].size(); k++) {
+                    brow[bg.size()] = crow[c][k];
+                    brow_group[bg.size()] = (uint32_t)bg.size();
+                    bg.push_back(std::move(cg[c][k]));
+                }
+            }
+            return true;
+        };
+        if (assemble_parallel_rev()) {
+            q = rows.size();
+        } else if (!assemble_parallel()) {
             uint64_t total_k = 0;
             for (; q < rows.size() && brow.size() < kMaxBatchRows; q++) {
                 const uint32_t r = rows[q];
@@ -1040,8 +1147,10 @@ int Core::process_default(GroupList& out_groups,
         stats.assemble_ms += std::chrono::duration<double, std::milli>(tb0 - ta0).count();
         ParPlan& plan = par_plan_;
         plan.ok = false;
+        // a RevThreshold timer that may still fire is read per row: serial replay
+        const bool timer_live = rev && timer.armed && !timer.fired;
         rp.run_batch(bg, need_pm, [&] {  // pools bucketed while the searches run
-            if (!rev && par_mode_) plan_parallel(bg, brow, brow_group, plan, stats);
+            if (par_mode_ && !timer_live) plan_parallel(bg, brow, brow_group, plan, stats);
         });
         auto tb1 = std::chrono::steady_clock::now();
         stats.search_ms += std::chrono::duration<double, std::milli>(tb1 - tb0).count();
@@ -1049,7 +1158,7 @@ int Core::process_default(GroupList& out_groups,
         newly.clear();
         size_t done = 0;
         bool exhausted = false;
-        if (!rev && par_mode_ && replay_parallel(plan, bg, brow, brow_group, sel, out_groups, expired, newly, stats)) {
+        if (par_mode_ && replay_parallel(plan, bg, brow, brow_group, sel, out_groups, expired, newly, stats, rev)) {
             stats.parallel_batches++;
             const auto tr = std::chrono::steady_clock::now();
             stats.replay_ms += std::chrono::duration<double, std::milli>(tr - tb1).count();

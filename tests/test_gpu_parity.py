@@ -205,7 +205,11 @@ def test_exact_walk_without_fast_path(config, n, passes, mi, par, monkeypatch):
     run_passes(config, n, passes, dict(max_intervals=mi))
 
 
-def test_c5_rev_precision_default_path():
+@pytest.mark.parametrize("par", ["0", "1", "force"])
+def test_c5_rev_precision_default_path(par, monkeypatch):
+    """NKM_PARALLEL=force: the RevPrecision rows' pool-parallel replay and
+    parallel batch assembly at any size (rsmall_kernel's lists either way)."""
+    monkeypatch.setenv("NKM_PARALLEL", par)
     run_passes(5, 800, 2, dict(max_intervals=2, rev_precision=True))
 
 
@@ -260,9 +264,10 @@ def test_mixed_parties_ranges_minmax(par, dense, kernel, monkeypatch):
     run_passes(6, 1000, 3, dict(max_intervals=3))
 
 
-@pytest.mark.parametrize("page", ["1", "0"])
-def test_mixed_rev_precision(page, monkeypatch):
+@pytest.mark.parametrize("page,par", [("1", "1"), ("0", "1"), ("1", "force")])
+def test_mixed_rev_precision(page, par, monkeypatch):
     monkeypatch.setenv("NKM_PAGE", page)
+    monkeypatch.setenv("NKM_PARALLEL", par)
     run_passes(6, 600, 3, dict(max_intervals=3, rev_precision=True))
 
 
