@@ -42,7 +42,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-KERNELS = {0: "search_kernel", 1: "scan_kernel", 2: "mscan_kernel"}  # mm_matched.eval_kernel
+KERNELS = {0: "search_kernel", 1: "scan_kernel", 2: "mscan_kernel", 3: "rsmall_kernel"}  # mm_matched.eval_kernel
 WORKLOADS = {
     1: "C1: 10k solo 1v1, '+properties.mode:ranked +properties.region:eu'",
     2: "C2: skill-window range queries with ^boost, 1v1",
@@ -154,7 +154,7 @@ def cpu_baseline(args, n_pools, searches, matched):
     ts = synth.TicketSet(args.config, args.tickets, first=0)
     for k in range(args.cpu_rows, ts.n):
         ts.tickets[k].intervals = 2
-    mm = capi.Matchmaker(lib, max_intervals=2, rev_precision=args.config == 5)
+    mm = capi.Matchmaker(lib, max_intervals=2, rev_precision=args.config == 5, rev_threshold=0)
     try:
         ts.insert_into(mm)
         t0 = time.perf_counter()
@@ -207,7 +207,8 @@ def main():
     import nakama_amd
     import torch
 
-    mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config == 5)
+    # SURVEY 8(d) harness pins: MaxIntervals=2, RevThreshold=0 (no wall-clock cutoff)
+    mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config == 5, rev_threshold=0)
     cm = None
     if world > 1:
         from nakama_amd import cluster

@@ -511,9 +511,17 @@ private:
     struct ParPlan {  // a batch's pools (plan_parallel), bucketed while its searches run
         bool ok = false;
         size_t ng = 0;
-        std::vector<uint32_t> search_pool;           // per search
-        std::vector<std::vector<uint32_t>> grows;    // per pool: its batch rows, ascending
+        std::vector<uint32_t> search_pool;  // per search
+        std::vector<uint32_t> pool_off;     // CSR: pool p's batch rows are pool_rows[pool_off[p], pool_off[p+1])
+        std::vector<uint32_t> pool_rows;    // ascending per pool
     };
+    struct RowRec {  // a batch row's outcome in a parallel replay (indexed by batch row)
+        uint32_t ent, len, task;  // its group's entries: task_ents_[task][ent, ent + len)
+        uint8_t matched, expired, processed, pad;
+    };
+    std::vector<RowRec> row_recs_;
+    std::vector<std::vector<std::pair<uint32_t, int>>> task_ents_;
+    std::vector<uint32_t> pool_remap_;  // dictionary id -> pool (one-field pool keys)
     ParPlan par_plan_;
     bool plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
                        const std::vector<uint32_t>& brow_group, ParPlan& P, PassStats& stats);
@@ -551,9 +559,7 @@ public:
     std::vector<uint32_t> rows_, brow_, brow_group_, newly_, list_tmp_;
     GroupList pass_groups_;
     std::vector<uint32_t> expired_;
-    std::vector<PoolOut> pool_outs_;
     std::vector<DensePool> dense_pools_;  // dense replay per pool (kept: capacity reused)
-    std::vector<DenseRun> dense_runs_;
     std::vector<uint32_t> pos_of_;        // slot -> list position during a dense replay, else kNoSlot
     Dict field_dict_;                 // field names -> field id
     std::vector<std::string> ticket_;

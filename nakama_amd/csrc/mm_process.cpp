@@ -30,7 +30,7 @@ namespace nkm {
 hipError_t launch_pairmat(const DStore& st, const DGroup* d_groups, const DGroupResult* d_res, int n_groups,
                           const DHit* d_out, uint32_t* d_pm, hipStream_t stream);
 
-constexpr size_t kMaxBatchRows = 1u << 20;
+constexpr size_t kMaxBatchRows = 1u << 22;  // a batch may hold C4's 4M rows
 
 // Order-preserving filter of a slot list: on the workers in chunks (counts,
 // then every chunk writes at its offset), or serially when wp is null.
@@ -597,6 +597,9 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
     P.ok = false;
     const size_t nsearch = bg.size();
     if (nsearch < 2) return false;
+    using clk = std::chrono::steady_clock;
+    auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto tp0 = clk::now();
     // pool key fields: fields every search requires a keyword term on
     std::vector<uint16_t> keyf;
     for (auto& mt : sigs_[bg[0].sig].must_terms) {
@@ -612,66 +615,88 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
     if (keyf.empty()) return false;
     for (uint16_t f : keyf)
         if (fkind_[f].size() != ticket_.size()) return false;
-    // pool key of each search (a search requiring two different terms on one
-    // field matches nothing; it gets a key of its own)
-    std::map<std::vector<uint32_t>, uint32_t> pool_of;
+    // pool key of each search; a search requiring two different terms on one
+    // field matches nothing (the batch then takes the serial replay).  One key
+    // field (C5's buckets: ~10^5 pools): pools numbered through a dictionary-id
+    // table; more fields (mode x region: few pools): an ordered map.
     std::vector<uint32_t>& search_pool = P.search_pool;
     search_pool.assign(nsearch, 0);
-    for (size_t i = 0; i < nsearch; i++) {
-        std::vector<uint32_t> key(keyf.size(), UINT32_MAX);
+    std::vector<std::vector<uint32_t>> pool_keys;
+    auto key_of = [&](size_t i, std::vector<uint32_t>& key) {
+        key.assign(keyf.size(), UINT32_MAX);
         for (size_t k = 0; k < keyf.size(); k++)
             for (auto& mt : sigs_[bg[i].sig].must_terms)
                 if (mt.first == keyf[k]) {
                     if (key[k] != UINT32_MAX && key[k] != mt.second) return false;
                     key[k] = mt.second;
                 }
-        search_pool[i] = pool_of.emplace(std::move(key), (uint32_t)pool_of.size()).first->second;
+        return true;
+    };
+    std::vector<uint32_t> key;
+    if (keyf.size() == 1) {
+        std::vector<uint32_t>& remap = pool_remap_;
+        remap.assign(dict_.str.size(), UINT32_MAX);
+        for (size_t i = 0; i < nsearch; i++) {
+            if (!key_of(i, key)) return false;
+            uint32_t& p = remap[key[0]];
+            if (p == UINT32_MAX) {
+                p = (uint32_t)pool_keys.size();
+                pool_keys.push_back(key);
+            }
+            search_pool[i] = p;
+        }
+    } else {
+        std::map<std::vector<uint32_t>, uint32_t> pool_of;
+        for (size_t i = 0; i < nsearch; i++) {
+            if (!key_of(i, key)) return false;
+            auto it = pool_of.emplace(key, (uint32_t)pool_of.size());
+            if (it.second) pool_keys.push_back(key);
+            search_pool[i] = it.first->second;
+        }
     }
-    const size_t ng = pool_of.size();
+    const size_t ng = pool_keys.size();
     if (ng < 2) return false;
     P.ng = ng;
-    std::vector<std::vector<uint32_t>> pool_keys(ng);
-    for (auto& kv : pool_of) pool_keys[kv.second] = kv.first;
-    // every searching ticket must itself belong to its search's pool; bucket
-    // the rows per pool in batch order (chunked over threads, concatenated in
-    // chunk order so each pool's list stays in batch order)
-    using clk = std::chrono::steady_clock;
-    auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    const auto tp0 = clk::now();
+    // every searching ticket must itself belong to its search's pool; the
+    // rows are bucketed per pool in batch order (CSR: per-chunk counts, then
+    // every chunk scatters at its offsets)
     WorkPool& wp = workers();
-    const unsigned nchunk = brow.size() >= par_min(65536) ? wp.size() : 1;
-    std::vector<std::vector<std::vector<uint32_t>>> cgrows(nchunk, std::vector<std::vector<uint32_t>>(ng));
+    const size_t nb = brow.size();
+    const unsigned nchunk = nb >= par_min(65536) ? wp.size() : 1;
+    std::vector<uint32_t> cnt((size_t)nchunk * ng, 0);
     std::vector<uint8_t> cbad(nchunk, 0);
-    auto bucket = [&](unsigned c) {
-        const size_t lo = brow.size() * c / nchunk, hi = brow.size() * (c + 1) / nchunk;
-        auto& gr = cgrows[c];
-        for (size_t bi = lo; bi < hi; bi++) {
+    wp.run(nchunk, [&](size_t c) {
+        uint32_t* k = cnt.data() + c * ng;
+        for (size_t bi = nb * c / nchunk; bi < nb * (c + 1) / nchunk; bi++) {
             const uint32_t r = brow[bi];
             const uint32_t p = search_pool[brow_group[bi]];
-            const auto& key = pool_keys[p];
-            for (size_t k = 0; k < keyf.size(); k++)
-                if (fkind_[keyf[k]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[k]][r] != key[k]) {
+            const auto& pk = pool_keys[p];
+            for (size_t f = 0; f < keyf.size(); f++)
+                if (fkind_[keyf[f]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[f]][r] != pk[f]) {
                     cbad[c] = 1;
                     return;
                 }
-            gr[p].push_back((uint32_t)bi);
+            k[p]++;
         }
-    };
-    wp.run(nchunk, [&](size_t c) { bucket((unsigned)c); });
+    });
     for (unsigned c = 0; c < nchunk; c++)
         if (cbad[c]) return false;
-    std::vector<std::vector<uint32_t>>& grows = P.grows;
-    grows.assign(ng, {});
-    if (nchunk == 1) {
-        grows.swap(cgrows[0]);
-    } else {
-        for (size_t p = 0; p < ng; p++) {
-            size_t tot = 0;
-            for (unsigned c = 0; c < nchunk; c++) tot += cgrows[c][p].size();
-            grows[p].reserve(tot);
-            for (unsigned c = 0; c < nchunk; c++) grows[p].insert(grows[p].end(), cgrows[c][p].begin(), cgrows[c][p].end());
+    P.pool_off.assign(ng + 1, 0);
+    for (size_t p = 0; p < ng; p++) {  // cnt becomes each (chunk, pool)'s first position
+        uint32_t run = P.pool_off[p];
+        for (unsigned c = 0; c < nchunk; c++) {
+            const uint32_t v = cnt[c * ng + p];
+            cnt[c * ng + p] = run;
+            run += v;
         }
+        P.pool_off[p + 1] = run;
     }
+    P.pool_rows.resize(nb);
+    wp.run(nchunk, [&](size_t c) {
+        uint32_t* at = cnt.data() + c * ng;
+        for (size_t bi = nb * c / nchunk; bi < nb * (c + 1) / nchunk; bi++)
+            P.pool_rows[at[search_pool[brow_group[bi]]]++] = (uint32_t)bi;
+    });
     stats.par_bucket_ms += msd(tp0, clk::now());
     P.ok = true;
     return true;
@@ -679,6 +704,11 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
 
 // Pool-parallel replay over the bucketed rows (plan_parallel); false when a
 // pool's list came back truncated (the serial replay then decides the batch).
+// Pools are walked on the host workers (largest first, small ones bundled
+// into tasks); every processed row leaves a record at its batch position, and
+// one pass over the batch in row order assembles the groups, the expired list
+// and the Intervals increments — processDefault's sequential order, because
+// no pool ever selects another pool's ticket.
 bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
                            const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                            GroupList& out_groups,
@@ -688,153 +718,162 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
         if (!g.complete) return false;
     using clk = std::chrono::steady_clock;
     auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    const size_t nsearch = bg.size(), ng = P.ng;
+    const auto tp1 = clk::now();
+    const size_t nsearch = bg.size(), ng = P.ng, nb = brow.size();
     const std::vector<uint32_t>& search_pool = P.search_pool;
-    const std::vector<std::vector<uint32_t>>& grows = P.grows;
     WorkPool& wp = workers();
-    using Rec = PoolRec;
-    if (pool_outs_.size() < ng) pool_outs_.resize(ng);  // kept across passes (capacity reused)
-    auto& outs = pool_outs_;
-    for (size_t i = 0; i < ng; i++) outs[i].recs.clear(), outs[i].ents.clear();
-    std::vector<uint32_t> order_g(ng);
-    for (size_t i = 0; i < ng; i++) order_g[i] = (uint32_t)i;
-    std::sort(order_g.begin(), order_g.end(), [&](uint32_t a, uint32_t b) { return grows[a].size() > grows[b].size(); });
     const DStore st = dstore();
     const int maxI = cfg_.max_intervals;
-    const auto tp1 = clk::now();
-    std::vector<double> task_ms(ng, 0.0);
-    std::vector<uint64_t> task_hits(ng, 0), task_rows(ng, 0);
-    // Each pool walks private copies of its searches and of the selection
-    // mask: pools touch disjoint tickets, and sharing the mask's cache lines
-    // (slots of different pools interleave) would ping-pong them between
-    // cores on every selection.
-    std::vector<uint32_t> local_idx(nsearch);
-    std::vector<std::vector<uint32_t>> pool_searches(ng);
-    for (size_t i = 0; i < nsearch; i++) {
-        local_idx[i] = (uint32_t)pool_searches[search_pool[i]].size();
-        pool_searches[search_pool[i]].push_back((uint32_t)i);
+    // each pool's searches (CSR) and each search's index among them
+    std::vector<uint32_t> soff(ng + 1, 0), sidx(nsearch), local_idx(nsearch);
+    for (size_t i = 0; i < nsearch; i++) soff[search_pool[i] + 1]++;
+    for (size_t p = 0; p < ng; p++) soff[p + 1] += soff[p];
+    {
+        std::vector<uint32_t> at(soff.begin(), soff.end() - 1);
+        for (size_t i = 0; i < nsearch; i++) {
+            const uint32_t p = search_pool[i];
+            local_idx[i] = at[p] - soff[p];
+            sidx[at[p]++] = (uint32_t)i;
+        }
     }
-    // Pools with one search walk dense per-position copies of their list
-    // (DensePool/DenseRun); the copies are gathered first, in chunks across
-    // the workers.  Other pools take the generic walk over the store.
+    auto prows = [&](size_t p) { return P.pool_off[p + 1] - P.pool_off[p]; };
+    // tasks: pools by size (largest first), the small ones bundled
+    std::vector<uint32_t> order_g(ng);
+    for (size_t i = 0; i < ng; i++) order_g[i] = (uint32_t)i;
+    std::sort(order_g.begin(), order_g.end(), [&](uint32_t a, uint32_t b) { return prows(a) > prows(b); });
+    const size_t per_task = std::max<size_t>(1, nb / ((size_t)wp.size() * 8));
+    std::vector<uint32_t> task_off{0};
+    for (size_t k = 0, acc = 0; k < ng; k++) {
+        acc += prows(order_g[k]);
+        if (acc >= per_task || k + 1 == ng) {
+            task_off.push_back((uint32_t)(k + 1));
+            acc = 0;
+        }
+    }
+    const size_t ntask = task_off.size() - 1;
+    if (task_ents_.size() < ntask) task_ents_.resize(ntask);
+    if (row_recs_.size() < nb) row_recs_.resize(nb);
+    RowRec* rr = row_recs_.data();
+    wp.run(wp.size(), [&](size_t c) {  // rows no pool processes (selected before they were reached) stay zero
+        std::memset((void*)(rr + nb * c / wp.size()), 0, (nb * (c + 1) / wp.size() - nb * c / wp.size()) * sizeof(RowRec));
+    });
+    // Pools with one search (no RevPrecision) walk dense per-position copies
+    // of their list (DensePool/DenseRun), gathered first in chunks across the
+    // workers; the others take the generic walk over the store.
     if (dense_pools_.size() < ng) dense_pools_.resize(ng);
-    if (dense_runs_.size() < ng) dense_runs_.resize(ng);
     if (pos_of_.size() < ticket_.size()) pos_of_.resize(ticket_.size(), kNoSlot);
     const ReplayView rv = Replay::view(*this);
     std::vector<std::pair<uint32_t, uint32_t>> chunks;  // (pool, chunk) of the dense gathers
     constexpr uint32_t kGatherChunk = 16384;
     std::vector<uint8_t> dense(ng, 0);
     for (size_t gi = 0; gi < ng; gi++) {
-        if (pool_searches[gi].size() != 1 || !dense_mode_ || rev) continue;  // the dense walk has no reverse checks
+        if (soff[gi + 1] - soff[gi] != 1 || !dense_mode_ || rev) continue;  // the dense walk has no reverse checks
         dense[gi] = 1;
-        DensePool& P = dense_pools_[gi];
-        P.reset(bg[pool_searches[gi][0]], grows[gi], brow.data());
-        for (uint32_t c = 0; c * kGatherChunk < P.n; c++) chunks.push_back({(uint32_t)gi, c});
+        DensePool& D = dense_pools_[gi];
+        D.reset(bg[sidx[soff[gi]]], P.pool_rows.data() + P.pool_off[gi], (uint32_t)prows(gi), brow.data());
+        for (uint32_t c = 0; c * kGatherChunk < D.n; c++) chunks.push_back({(uint32_t)gi, c});
     }
     wp.run(chunks.size(), [&](size_t t) {
-        DensePool& P = dense_pools_[chunks[t].first];
+        DensePool& D = dense_pools_[chunks[t].first];
         const uint32_t lo = chunks[t].second * kGatherChunk;
-        P.gather(rv, lo, std::min(P.n, lo + kGatherChunk), pos_of_.data());
+        D.gather(rv, lo, std::min(D.n, lo + kGatherChunk), pos_of_.data());
     });
-    auto worker = [&](size_t k) {
-        const auto tw0 = clk::now();
-        const uint32_t gi = order_g[k];
-        PoolOut& o = outs[gi];
-        if (dense[gi]) {
-            DenseRun& run = dense_runs_[gi];
-            run.reset(dense_pools_[gi].n);
-            run.fast = fast_mode_;
-            run.walk(dense_pools_[gi], rv, maxI, pos_of_.data(), 0, dense_pools_[gi].nrows);
-            run.finish(o);
-            task_hits[k] = run.hits_seen;
-        } else {
-            // The worker thread's masks are all zero between tasks.  Starting
-            // from zero is exact: this batch's rows and hit lists hold no
-            // ticket an earlier batch selected (assembly skips them; the
-            // device alive mask dropped them before this batch's searches).
-            // Intervals stay unwritten during the walk (slots of all pools
-            // share its cache lines): a row's increment is pending in tl_proc
-            // until the merge applies it.
-            static thread_local std::vector<uint8_t> tl_sel, tl_proc;
-            if (tl_sel.size() < sel.size()) tl_sel.resize(sel.size(), 0);
-            if (tl_proc.size() < sel.size()) tl_proc.resize(sel.size(), 0);
-            PassStats ls;
-            std::vector<BGroup> mine;
-            mine.reserve(pool_searches[gi].size());
-            for (uint32_t i : pool_searches[gi]) mine.push_back(bg[i]);
-            Replay rp(*this, tl_sel, rev, maxI, ls, st, stream_);
-            replay_pool(rp, grows[gi], brow.data(),
-                        [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; }, tl_sel,
-                        tl_proc.data(), minc_.data(), maxc_.data(), o);
-            task_hits[k] = rp.hits_seen;
+    std::vector<double> task_ms(ntask, 0.0);
+    std::vector<uint64_t> task_hits(ntask, 0);
+    auto to_rows = [&](const PoolOut& o, uint32_t task, std::vector<std::pair<uint32_t, int>>& ents) {
+        const uint32_t base = (uint32_t)ents.size();
+        ents.insert(ents.end(), o.ents.begin(), o.ents.end());
+        for (size_t k = 0; k + 1 < o.recs.size(); k++) {  // the last record is the sentinel
+            const PoolRec& r = o.recs[k];
+            rr[r.bi] = RowRec{base + r.off, r.len, task, r.matched, r.expired, 1, 0};
         }
-        task_ms[k] = msd(tw0, clk::now());
-        task_rows[k] = o.recs.size() - 1;
     };
-    wp.run(ng, worker);
+    auto worker = [&](size_t t) {
+        const auto tw0 = clk::now();
+        auto& ents = task_ents_[t];
+        ents.clear();
+        static thread_local PoolOut o;
+        static thread_local DenseRun run;
+        // The worker thread's masks are all zero between pools.  Starting
+        // from zero is exact: this batch's rows and hit lists hold no ticket
+        // an earlier batch selected (assembly skips them; the device alive
+        // mask dropped them before this batch's searches).  Intervals stay
+        // unwritten during the walk (slots of all pools share its cache
+        // lines): a row's increment is pending in tl_proc until the merge.
+        static thread_local std::vector<uint8_t> tl_sel, tl_proc;
+        if (tl_sel.size() < sel.size()) tl_sel.resize(sel.size(), 0);
+        if (tl_proc.size() < sel.size()) tl_proc.resize(sel.size(), 0);
+        PassStats ls;
+        Replay rp(*this, tl_sel, rev, maxI, ls, st, stream_);
+        std::vector<BGroup> mine;
+        std::vector<uint32_t> rows_of;
+        for (uint32_t k = task_off[t]; k < task_off[t + 1]; k++) {
+            const uint32_t gi = order_g[k];
+            o.recs.clear();
+            o.ents.clear();
+            if (dense[gi]) {
+                run.reset(dense_pools_[gi].n);
+                run.fast = fast_mode_;
+                run.walk(dense_pools_[gi], rv, maxI, pos_of_.data(), 0, dense_pools_[gi].nrows);
+                run.finish(o);
+                task_hits[t] += run.hits_seen;
+            } else {
+                mine.clear();
+                for (uint32_t j = soff[gi]; j < soff[gi + 1]; j++) mine.push_back(bg[sidx[j]]);
+                rows_of.assign(P.pool_rows.begin() + P.pool_off[gi], P.pool_rows.begin() + P.pool_off[gi + 1]);
+                rp.hits_seen = 0;
+                replay_pool(rp, rows_of, brow.data(),
+                            [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; }, tl_sel,
+                            tl_proc.data(), minc_.data(), maxc_.data(), o);
+                task_hits[t] += rp.hits_seen;
+            }
+            to_rows(o, (uint32_t)t, ents);
+        }
+        task_ms[t] = msd(tw0, clk::now());
+    };
+    wp.run(ntask, worker);
     wp.run(chunks.size(), [&](size_t t) {
-        const DensePool& P = dense_pools_[chunks[t].first];
+        const DensePool& D = dense_pools_[chunks[t].first];
         const uint32_t lo = chunks[t].second * kGatherChunk;
-        P.clear_pos(lo, std::min(P.n, lo + kGatherChunk), pos_of_.data());
+        D.clear_pos(lo, std::min(D.n, lo + kGatherChunk), pos_of_.data());
     });
     const auto tp2 = clk::now();
-    // Merge back into the pinned row order.  The batch's row range is cut
-    // into chunks; each pool's records (ascending in batch row, with running
-    // group / entry / expiry counts) are located in every chunk by binary
-    // search, so each chunk knows its output offsets up front and merges its
-    // share of the pools' records independently.  Applies the rows' pending
-    // Intervals increments on the way.
-    const size_t nb = brow.size();
+    // Back into the pinned row order: per chunk of the batch, its groups /
+    // entries / expired counts, then every chunk fills its share at its
+    // offsets and applies its rows' pending Intervals increments.
     const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
-    std::vector<uint32_t> cut((nch + 1) * ng);  // [c][pool]: first record with bi >= chunk start
-    for (size_t c = 0; c <= nch; c++) {
-        const uint32_t lo = (uint32_t)(nb * c / nch);
-        for (size_t gi = 0; gi < ng; gi++) {
-            const auto& r = outs[gi].recs;  // sentinel at the end (bi = UINT32_MAX)
-            cut[c * ng + gi] = c == nch ? (uint32_t)(r.size() - 1)
-                                        : (uint32_t)(std::lower_bound(r.begin(), r.end(), lo,
-                                                                      [](const Rec& x, uint32_t v) { return x.bi < v; }) -
-                                                     r.begin());
-        }
-    }
     struct Cnt { size_t g = 0, e = 0, x = 0; };
     std::vector<Cnt> at(nch + 1);
-    for (size_t c = 0; c < nch; c++) {
+    wp.run(nch, [&](size_t c) {
         Cnt k;
-        for (size_t gi = 0; gi < ng; gi++) {
-            const Rec& a0 = outs[gi].recs[cut[c * ng + gi]];
-            const Rec& a1 = outs[gi].recs[cut[(c + 1) * ng + gi]];
-            k.g += a1.gcum - a0.gcum;
-            k.e += a1.off - a0.off;
-            k.x += a1.xcum - a0.xcum;
+        for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++) {
+            const RowRec& r = rr[bi];
+            if (!r.processed) continue;
+            k.x += r.expired;
+            if (r.matched) k.g++, k.e += r.len;
         }
-        at[c + 1] = {at[c].g + k.g, at[c].e + k.e, at[c].x + k.x};
-    }
+        at[c + 1] = k;
+    });
+    for (size_t c = 0; c < nch; c++) at[c + 1] = {at[c].g + at[c + 1].g, at[c].e + at[c + 1].e, at[c].x + at[c + 1].x};
     const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
     out_groups.off.resize(g0 + 1 + at[nch].g);
     out_groups.ents.resize(e0 + at[nch].e);
     expired.resize(x0 + at[nch].x);
     newly.resize(n0 + at[nch].e);
     wp.run(nch, [&](size_t c) {
-        std::vector<uint32_t> head(ng), end(ng);
-        for (size_t gi = 0; gi < ng; gi++) head[gi] = cut[c * ng + gi], end[gi] = cut[(c + 1) * ng + gi];
         size_t gk = g0 + at[c].g, ek = e0 + at[c].e, xk = x0 + at[c].x;
-        for (;;) {
-            uint32_t best = UINT32_MAX, bg_ = 0;
-            for (uint32_t gi = 0; gi < ng; gi++)
-                if (head[gi] < end[gi] && outs[gi].recs[head[gi]].bi < best) best = outs[gi].recs[head[gi]].bi, bg_ = gi;
-            if (best == UINT32_MAX) break;
-            const PoolOut& o = outs[bg_];
-            const Rec& r = o.recs[head[bg_]++];
-            const uint32_t T = brow[r.bi];
+        for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++) {
+            const RowRec& r = rr[bi];
+            if (!r.processed) continue;
+            const uint32_t T = brow[bi];
             intervals_[T]++;  // the row's pending Intervals increment
             if (r.expired) expired[xk++] = T;
             if (!r.matched) continue;
+            const auto* src = task_ents_[r.task].data() + r.ent;
             for (uint32_t k = 0; k < r.len; k++) {
-                const auto& e = o.ents[r.off + k];
-                out_groups.ents[ek + k] = e;
-                newly[n0 + (ek - e0) + k] = e.first;
-                sel[e.first] = 1;
+                out_groups.ents[ek + k] = src[k];
+                newly[n0 + (ek - e0) + k] = src[k].first;
+                sel[src[k].first] = 1;
             }
             ek += r.len;
             out_groups.off[++gk] = (uint32_t)ek;
@@ -843,11 +882,11 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
     const auto tp3 = clk::now();
     stats.par_work_ms += msd(tp1, tp2);
     stats.par_merge_ms += msd(tp2, tp3);
-    for (size_t k = 0; k < ng; k++) {
+    for (size_t k = 0; k < ntask; k++) {
         stats.par_task_max_ms = std::max(stats.par_task_max_ms, task_ms[k]);
         stats.par_hits += task_hits[k];
-        stats.par_rows += task_rows[k];
     }
+    stats.par_rows += nb;
     return true;
 }
 

@@ -458,11 +458,11 @@ struct DensePool {
     std::vector<DenseRec> rec;
     std::vector<uint32_t> slot;
 
-    void reset(const BGroup& g, const std::vector<uint32_t>& rows, const uint32_t* batch_slots) {
+    void reset(const BGroup& g, const uint32_t* rows, uint32_t n_rows, const uint32_t* batch_slots) {
         hits = g.hits;
         n = g.n;
-        bis = rows.data();
-        nrows = (uint32_t)rows.size();
+        bis = rows;
+        nrows = n_rows;
         brow = batch_slots;
         if (rec.size() < n) rec.resize(n);
         if (slot.size() < n) slot.resize(n);

@@ -155,7 +155,7 @@ int main(int argc, char** argv) {
             }
             for (int k = 2; k < 4; k++) {
                 const double t0 = now_ms();
-                P.reset(g, pbis[0], brow.data());
+                P.reset(g, pbis[0].data(), (uint32_t)pbis[0].size(), brow.data());
                 P.gather(v, 0, P.n, pos_of.data());
                 run.fast = k == 3;
                 run.reset(P.n);
@@ -207,7 +207,7 @@ int main(int argc, char** argv) {
         const double t0 = now_ms();
         std::vector<std::pair<int, uint32_t>> chunks;
         for (int p = 0; p < npools; p++) {
-            P[p].reset(gs[p], pbis[p], brow.data());
+            P[p].reset(gs[p], pbis[p].data(), (uint32_t)pbis[p].size(), brow.data());
             for (uint32_t c = 0; c * kChunk < P[p].n; c++) chunks.push_back({p, c});
         }
         par(chunks.size(), [&](size_t t) {
