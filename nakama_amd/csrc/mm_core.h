@@ -366,9 +366,9 @@ struct PassStats {
 // has a party (4 B), and one 8-B value + 1-B kind per field column the query
 // references (plus the candidate's own query descriptor and clauses for the
 // RevPrecision reverse check); each emitted hit writes 16 B.
-inline int64_t search_bytes(const Sig& s, const DGroup& d, const DGroupResult& r) {
-    int64_t per_live = 8 + (d.tparty != kNoParty ? 4 : 0) + 9 * (int64_t)s.n_fields;
-    if (d.rev_slot != kNoSlot) per_live += 8 + 32 * (int64_t)s.n_clauses;
+inline int64_t search_bytes(uint16_t n_fields, const DGroup& d, const DGroupResult& r) {
+    int64_t per_live = 8 + (d.tparty != kNoParty ? 4 : 0) + 9 * (int64_t)n_fields;
+    if (d.rev_slot != kNoSlot) per_live += 8 + 32 * (int64_t)d.n_clauses;
     return (int64_t)r.scanned * 5 + (int64_t)r.live * per_live + (int64_t)r.count * 16 +
            (int64_t)(sizeof(DGroup) + sizeof(DGroupResult));
 }

@@ -14,6 +14,7 @@
 // device alive mask up to date; the first row of a batch may page further
 // through its list with a cursor, so every batch makes progress.
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -128,7 +129,7 @@ struct Replay : ReplayCore {
         stats.k_ms[0] += ms;
         const DGroupResult r = c.h_res_.p[0];
         stats.pair_evals += r.scanned;
-        stats.k_bytes[0] += search_bytes(c.sigs_[g.sig], d, r);
+        stats.k_bytes[0] += search_bytes(c.sigs_[g.sig].n_fields, d, r);
         stats.k_launches[0]++;
         g.ext.insert(g.ext.end(), c.h_page_.p, c.h_page_.p + r.count);
         if (rev) g.ext_rev.insert(g.ext_rev.end(), c.h_page_rev_.p, c.h_page_rev_.p + r.count);
@@ -513,11 +514,26 @@ struct Replay : ReplayCore {
             stats.k_launches[kk]++;
         }
         stats.batches++;
-        for (int t = 0; t < nwhole + nchunks; t++) {
-            if (t < b0 || (t >= b1 && t < nwhole)) continue;  // another rank's block
-            stats.pair_evals += c.h_res_.p[t].scanned;
-            const int kk = t >= nwhole ? 1 : lg[t].path == 1 ? 3 : 0;
-            stats.k_bytes[kk] += search_bytes(c.sigs_[bg[lg_group[t]].sig], lg[t], c.h_res_.p[t]);
+        {
+            // per-search accounting (on the workers for large batches)
+            const size_t ns = (size_t)(nwhole + nchunks);
+            const size_t nch = ns >= 65536 && c.par_mode_ ? c.workers().size() : 1;
+            std::vector<std::array<int64_t, 5>> acc(nch, std::array<int64_t, 5>{0, 0, 0, 0, 0});
+            auto count = [&](size_t ch) {
+                auto& a = acc[ch];
+                for (size_t t = ns * ch / nch; t < ns * (ch + 1) / nch; t++) {
+                    if ((int)t < b0 || ((int)t >= b1 && (int)t < nwhole)) continue;  // another rank's block
+                    a[4] += c.h_res_.p[t].scanned;
+                    const int kk = (int)t >= nwhole ? 1 : lg[t].path == 1 ? 3 : 0;
+                    a[kk] += search_bytes(bg[lg_group[t]].n_fields, lg[t], c.h_res_.p[t]);
+                }
+            };
+            if (nch > 1) c.workers().run(nch, count);
+            else count(0);
+            for (auto& a : acc) {
+                for (int kk = 0; kk < 4; kk++) stats.k_bytes[kk] += a[kk];
+                stats.pair_evals += a[4];
+            }
         }
         if (use_m) {
             // columns read once per candidate for all signatures; hits written per signature
@@ -533,16 +549,24 @@ struct Replay : ReplayCore {
             DHit* h = c.h_out_.p + lg[i].out_off;
             std::stable_sort(h, h + c.h_res_.p[i].count, [](const DHit& a, const DHit& b) { return a.key > b.key; });
         }
-        for (int i = 0; i < nwhole; i++) {
-            BGroup& g = bg[lg_group[i]];
-            const DGroupResult& r = c.h_res_.p[i];
-            g.head = 0;
-            g.hits = c.h_out_.p + lg[i].out_off;
-            g.rev = rev ? c.h_rev_.p + lg[i].out_off : nullptr;
-            g.pm = need_pm ? c.h_pm_.p + lg[i].out_off : nullptr;
-            g.pm_n = need_pm ? std::min<uint32_t>(r.count, kPairP) : 0;
-            g.n = r.count;
-            g.complete = r.complete != 0;
+        auto wire = [&](size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; i++) {
+                BGroup& g = bg[lg_group[i]];
+                const DGroupResult& r = c.h_res_.p[i];
+                g.head = 0;
+                g.hits = c.h_out_.p + lg[i].out_off;
+                g.rev = rev ? c.h_rev_.p + lg[i].out_off : nullptr;
+                g.pm = need_pm ? c.h_pm_.p + lg[i].out_off : nullptr;
+                g.pm_n = need_pm ? std::min<uint32_t>(r.count, kPairP) : 0;
+                g.n = r.count;
+                g.complete = r.complete != 0;
+            }
+        };
+        if (nwhole >= 65536 && c.par_mode_) {
+            const size_t nch = c.workers().size();
+            c.workers().run(nch, [&](size_t ch) { wire((size_t)nwhole * ch / nch, (size_t)nwhole * (ch + 1) / nch); });
+        } else {
+            wire(0, (size_t)nwhole);
         }
         // chunked / mscan searches: exact hit counts are known now; copy just those
         for (size_t k = 0; k < cg_list.size(); k++) {
@@ -600,25 +624,40 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
     using clk = std::chrono::steady_clock;
     auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     const auto tp0 = clk::now();
-    // pool key fields: fields every search requires a keyword term on
+    WorkPool& wp = workers();
+    const bool par = nsearch >= par_min(65536) && par_mode_;
+    const unsigned nsch = par ? wp.size() * 2 : 1;
+    // pool key fields: fields every search requires a keyword term on (the
+    // candidates are the first search's; each chunk of searches checks them)
+    std::vector<uint16_t> cand;
+    for (auto& mt : sigs_[bg[0].sig].must_terms)
+        if (std::find(cand.begin(), cand.end(), mt.first) == cand.end()) cand.push_back(mt.first);
+    std::vector<std::vector<uint8_t>> has(nsch, std::vector<uint8_t>(cand.size(), 1));
+    auto verify = [&](size_t ch) {
+        for (size_t i = nsearch * ch / nsch; i < nsearch * (ch + 1) / nsch; i++)
+            for (size_t k = 0; k < cand.size(); k++) {
+                if (!has[ch][k]) continue;
+                bool h = false;
+                for (auto& m2 : sigs_[bg[i].sig].must_terms) h |= m2.first == cand[k];
+                if (!h) has[ch][k] = 0;
+            }
+    };
+    if (nsch > 1) wp.run(nsch, verify);
+    else verify(0);
     std::vector<uint16_t> keyf;
-    for (auto& mt : sigs_[bg[0].sig].must_terms) {
-        if (std::find(keyf.begin(), keyf.end(), mt.first) != keyf.end()) continue;
+    for (size_t k = 0; k < cand.size(); k++) {
         bool all = true;
-        for (size_t i = 1; i < nsearch && all; i++) {
-            bool has = false;
-            for (auto& m2 : sigs_[bg[i].sig].must_terms) has |= m2.first == mt.first;
-            all = has;
-        }
-        if (all) keyf.push_back(mt.first);
+        for (unsigned ch = 0; ch < nsch; ch++) all = all && has[ch][k];
+        if (all) keyf.push_back(cand[k]);
     }
     if (keyf.empty()) return false;
     for (uint16_t f : keyf)
         if (fkind_[f].size() != ticket_.size()) return false;
     // pool key of each search; a search requiring two different terms on one
     // field matches nothing (the batch then takes the serial replay).  One key
-    // field (C5's buckets: ~10^5 pools): pools numbered through a dictionary-id
-    // table; more fields (mode x region: few pools): an ordered map.
+    // field (C5's buckets: ~10^5 pools): keys extracted on the workers and
+    // pools numbered through a dictionary-id table; more fields (mode x
+    // region: few pools): an ordered map.
     std::vector<uint32_t>& search_pool = P.search_pool;
     search_pool.assign(nsearch, 0);
     std::vector<std::vector<uint32_t>> pool_keys;
@@ -634,16 +673,28 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
     };
     std::vector<uint32_t> key;
     if (keyf.size() == 1) {
+        std::vector<uint32_t>& k1 = search_pool;  // the key term first, renumbered in place below
+        std::vector<uint8_t> bad(nsch, 0);
+        auto extract = [&](size_t ch) {
+            std::vector<uint32_t> kk;
+            for (size_t i = nsearch * ch / nsch; i < nsearch * (ch + 1) / nsch; i++) {
+                if (!key_of(i, kk)) { bad[ch] = 1; return; }
+                k1[i] = kk[0];
+            }
+        };
+        if (nsch > 1) wp.run(nsch, extract);
+        else extract(0);
+        for (uint8_t b : bad)
+            if (b) return false;
         std::vector<uint32_t>& remap = pool_remap_;
         remap.assign(dict_.str.size(), UINT32_MAX);
         for (size_t i = 0; i < nsearch; i++) {
-            if (!key_of(i, key)) return false;
-            uint32_t& p = remap[key[0]];
+            uint32_t& p = remap[k1[i]];
             if (p == UINT32_MAX) {
                 p = (uint32_t)pool_keys.size();
-                pool_keys.push_back(key);
+                pool_keys.push_back({k1[i]});
             }
-            search_pool[i] = p;
+            k1[i] = p;
         }
     } else {
         std::map<std::vector<uint32_t>, uint32_t> pool_of;
@@ -659,14 +710,13 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
     P.ng = ng;
     // every searching ticket must itself belong to its search's pool; the
     // rows are bucketed per pool in batch order (CSR: per-chunk counts, then
-    // every chunk scatters at its offsets)
-    WorkPool& wp = workers();
+    // every chunk scatters at its offsets; counters stay thread-private)
     const size_t nb = brow.size();
     const unsigned nchunk = nb >= par_min(65536) ? wp.size() : 1;
     std::vector<uint32_t> cnt((size_t)nchunk * ng, 0);
     std::vector<uint8_t> cbad(nchunk, 0);
     wp.run(nchunk, [&](size_t c) {
-        uint32_t* k = cnt.data() + c * ng;
+        std::vector<uint32_t> k(ng, 0);
         for (size_t bi = nb * c / nchunk; bi < nb * (c + 1) / nchunk; bi++) {
             const uint32_t r = brow[bi];
             const uint32_t p = search_pool[brow_group[bi]];
@@ -678,6 +728,7 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
                 }
             k[p]++;
         }
+        std::copy(k.begin(), k.end(), cnt.begin() + c * ng);
     });
     for (unsigned c = 0; c < nchunk; c++)
         if (cbad[c]) return false;
@@ -693,7 +744,7 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
     }
     P.pool_rows.resize(nb);
     wp.run(nchunk, [&](size_t c) {
-        uint32_t* at = cnt.data() + c * ng;
+        std::vector<uint32_t> at(cnt.begin() + c * ng, cnt.begin() + (c + 1) * ng);
         for (size_t bi = nb * c / nchunk; bi < nb * (c + 1) / nchunk; bi++)
             P.pool_rows[at[search_pool[brow_group[bi]]]++] = (uint32_t)bi;
     });
@@ -815,8 +866,14 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
                 run.reset(dense_pools_[gi].n);
                 run.fast = fast_mode_;
                 run.walk(dense_pools_[gi], rv, maxI, pos_of_.data(), 0, dense_pools_[gi].nrows);
-                run.finish(o);
                 task_hits[t] += run.hits_seen;
+                // the walk's records straight to the rows (entries offsets are run.ents')
+                const uint32_t base = (uint32_t)ents.size();
+                if (ents.empty()) ents.swap(run.ents);
+                else ents.insert(ents.end(), run.ents.begin(), run.ents.end());
+                for (const PoolRec& r : run.recs)
+                    rr[r.bi] = RowRec{base + r.off, r.len, (uint32_t)t, r.matched, r.expired, 1, 0};
+                continue;
             } else {
                 mine.clear();
                 for (uint32_t j = soff[gi]; j < soff[gi + 1]; j++) mine.push_back(bg[sidx[j]]);
@@ -992,6 +1049,7 @@ int Core::process_default(GroupList& out_groups,
             BGroup g;
             g.sig = sig;
             const Sig& s = sigs_[g.sig];
+            g.n_fields = s.n_fields;
             g.d.clause_off = s.clause_off;
             g.d.n_clauses = s.n_clauses;
             g.d.qkind = s.qkind;
@@ -1110,6 +1168,7 @@ int Core::process_default(GroupList& out_groups,
                     BGroup g;
                     g.sig = sig_[r];
                     const Sig& sg = sigs_[g.sig];
+                    g.n_fields = sg.n_fields;
                     g.d.clause_off = sg.clause_off;
                     g.d.n_clauses = sg.n_clauses;
                     g.d.qkind = sg.qkind;
@@ -1284,6 +1343,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
             BGroup& g = bg[i];
             g.sig = sig_[r];
             const Sig& s = sigs_[g.sig];
+            g.n_fields = s.n_fields;
             g.d.clause_off = s.clause_off;
             g.d.n_clauses = s.n_clauses;
             g.d.qkind = s.qkind;
@@ -1803,6 +1863,7 @@ int32_t Core::debug_hits(const std::string& ticket, const char** tk, double* sc,
     BGroup g;
     g.sig = sig_[T];
     const Sig& s = sigs_[sig_[T]];
+    g.n_fields = s.n_fields;
     g.d.clause_off = s.clause_off;
     g.d.n_clauses = s.n_clauses;
     g.d.qkind = s.qkind;

@@ -68,6 +68,7 @@ inline uint64_t next_mask_le(uint64_t x, int c) {
 // A batch search and its (possibly extended) hit list.
 struct BGroup {
     uint32_t sig = 0;
+    uint16_t n_fields = 0;        // field columns the signature reads (roofline bytes)
     uint32_t nrows = 0;
     uint32_t row_slot = kNoSlot;  // RevPrecision: the single searching row
     DGroup d{};
