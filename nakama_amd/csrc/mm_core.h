@@ -560,6 +560,11 @@ public:
     GroupList pass_groups_;
     std::vector<uint32_t> expired_;
     std::vector<DensePool> dense_pools_;  // dense replay per pool (kept: capacity reused)
+    std::vector<PoolOut> pool_outs_;      // few-pool replays: each pool's records
+    void merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
+                     GroupList& out_groups, std::vector<uint32_t>& expired, std::vector<uint32_t>& newly);
+    void merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
+                    GroupList& out_groups, std::vector<uint32_t>& expired, std::vector<uint32_t>& newly);
     std::vector<uint32_t> pos_of_;        // slot -> list position during a dense replay, else kNoSlot
     Dict field_dict_;                 // field names -> field id
     std::vector<std::string> ticket_;

@@ -802,12 +802,20 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
         }
     }
     const size_t ntask = task_off.size() - 1;
+    // Few pools (C3's 8, C4's 64): each pool keeps its records in its own
+    // array and the merge interleaves them (their rows interleave finely in
+    // batch order, so per-row stores from several walks would share cache
+    // lines).  Many pools (C5's buckets: each a short run of the batch):
+    // records go straight to their batch rows.
+    const bool few = ng <= 64;
     if (task_ents_.size() < ntask) task_ents_.resize(ntask);
-    if (row_recs_.size() < nb) row_recs_.resize(nb);
-    RowRec* rr = row_recs_.data();
-    wp.run(wp.size(), [&](size_t c) {  // rows no pool processes (selected before they were reached) stay zero
-        std::memset((void*)(rr + nb * c / wp.size()), 0, (nb * (c + 1) / wp.size() - nb * c / wp.size()) * sizeof(RowRec));
-    });
+    if (few && pool_outs_.size() < ng) pool_outs_.resize(ng);
+    if (!few && row_recs_.size() < nb) row_recs_.resize(nb);
+    RowRec* rr = few ? nullptr : row_recs_.data();
+    if (!few)
+        wp.run(wp.size(), [&](size_t c) {  // rows no pool processes (selected before they were reached) stay zero
+            std::memset((void*)(rr + nb * c / wp.size()), 0, (nb * (c + 1) / wp.size() - nb * c / wp.size()) * sizeof(RowRec));
+        });
     // Pools with one search (no RevPrecision) walk dense per-position copies
     // of their list (DensePool/DenseRun), gathered first in chunks across the
     // workers; the others take the generic walk over the store.
@@ -860,13 +868,18 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
         std::vector<uint32_t> rows_of;
         for (uint32_t k = task_off[t]; k < task_off[t + 1]; k++) {
             const uint32_t gi = order_g[k];
-            o.recs.clear();
-            o.ents.clear();
+            PoolOut& po = few ? pool_outs_[gi] : o;
+            po.recs.clear();
+            po.ents.clear();
             if (dense[gi]) {
                 run.reset(dense_pools_[gi].n);
                 run.fast = fast_mode_;
                 run.walk(dense_pools_[gi], rv, maxI, pos_of_.data(), 0, dense_pools_[gi].nrows);
                 task_hits[t] += run.hits_seen;
+                if (few) {
+                    run.finish(po);
+                    continue;
+                }
                 // the walk's records straight to the rows (entries offsets are run.ents')
                 const uint32_t base = (uint32_t)ents.size();
                 if (ents.empty()) ents.swap(run.ents);
@@ -881,10 +894,10 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
                 rp.hits_seen = 0;
                 replay_pool(rp, rows_of, brow.data(),
                             [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; }, tl_sel,
-                            tl_proc.data(), minc_.data(), maxc_.data(), o);
+                            tl_proc.data(), minc_.data(), maxc_.data(), po);
                 task_hits[t] += rp.hits_seen;
             }
-            to_rows(o, (uint32_t)t, ents);
+            if (!few) to_rows(o, (uint32_t)t, ents);
         }
         task_ms[t] = msd(tw0, clk::now());
     };
@@ -895,11 +908,29 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
         D.clear_pos(lo, std::min(D.n, lo + kGatherChunk), pos_of_.data());
     });
     const auto tp2 = clk::now();
+    const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
+    if (few) merge_pools(ng, nch, brow, sel, out_groups, expired, newly);
+    else merge_rows(nb, nch, brow, sel, out_groups, expired, newly);
+    const auto tp3 = clk::now();
+    stats.par_work_ms += msd(tp1, tp2);
+    stats.par_merge_ms += msd(tp2, tp3);
+    for (size_t k = 0; k < ntask; k++) {
+        stats.par_task_max_ms = std::max(stats.par_task_max_ms, task_ms[k]);
+        stats.par_hits += task_hits[k];
+    }
+    stats.par_rows += nb;
+    return true;
+}
+
+// Merge of per-row records (many pools) back into the pinned row order.
+void Core::merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
+                      GroupList& out_groups, std::vector<uint32_t>& expired, std::vector<uint32_t>& newly) {
+    WorkPool& wp = workers();
+    const RowRec* rr = row_recs_.data();
+    struct Cnt { size_t g = 0, e = 0, x = 0; };
     // Back into the pinned row order: per chunk of the batch, its groups /
     // entries / expired counts, then every chunk fills its share at its
     // offsets and applies its rows' pending Intervals increments.
-    const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
-    struct Cnt { size_t g = 0, e = 0, x = 0; };
     std::vector<Cnt> at(nch + 1);
     wp.run(nch, [&](size_t c) {
         Cnt k;
@@ -936,15 +967,74 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
             out_groups.off[++gk] = (uint32_t)ek;
         }
     });
-    const auto tp3 = clk::now();
-    stats.par_work_ms += msd(tp1, tp2);
-    stats.par_merge_ms += msd(tp2, tp3);
-    for (size_t k = 0; k < ntask; k++) {
-        stats.par_task_max_ms = std::max(stats.par_task_max_ms, task_ms[k]);
-        stats.par_hits += task_hits[k];
+}
+
+// Merge of few pools' record arrays back into the pinned row order.  The
+// batch's row range is cut into chunks; each pool's records (ascending in
+// batch row, with running group / entry / expiry counts) are located in every
+// chunk by binary search, so each chunk knows its output offsets up front and
+// merges its share of the pools' records independently.  Applies the rows'
+// pending Intervals increments on the way.
+void Core::merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
+                       GroupList& out_groups, std::vector<uint32_t>& expired, std::vector<uint32_t>& newly) {
+    using Rec = PoolRec;
+    auto& outs = pool_outs_;
+    WorkPool& wp = workers();
+    const size_t nb = brow.size();
+    std::vector<uint32_t> cut((nch + 1) * ng);  // [c][pool]: first record with bi >= chunk start
+    for (size_t c = 0; c <= nch; c++) {
+        const uint32_t lo = (uint32_t)(nb * c / nch);
+        for (size_t gi = 0; gi < ng; gi++) {
+            const auto& r = outs[gi].recs;  // sentinel at the end (bi = UINT32_MAX)
+            cut[c * ng + gi] = c == nch ? (uint32_t)(r.size() - 1)
+                                        : (uint32_t)(std::lower_bound(r.begin(), r.end(), lo,
+                                                                      [](const Rec& x, uint32_t v) { return x.bi < v; }) -
+                                                     r.begin());
+        }
     }
-    stats.par_rows += nb;
-    return true;
+    struct Cnt { size_t g = 0, e = 0, x = 0; };
+    std::vector<Cnt> at(nch + 1);
+    for (size_t c = 0; c < nch; c++) {
+        Cnt k;
+        for (size_t gi = 0; gi < ng; gi++) {
+            const Rec& a0 = outs[gi].recs[cut[c * ng + gi]];
+            const Rec& a1 = outs[gi].recs[cut[(c + 1) * ng + gi]];
+            k.g += a1.gcum - a0.gcum;
+            k.e += a1.off - a0.off;
+            k.x += a1.xcum - a0.xcum;
+        }
+        at[c + 1] = {at[c].g + k.g, at[c].e + k.e, at[c].x + k.x};
+    }
+    const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
+    out_groups.off.resize(g0 + 1 + at[nch].g);
+    out_groups.ents.resize(e0 + at[nch].e);
+    expired.resize(x0 + at[nch].x);
+    newly.resize(n0 + at[nch].e);
+    wp.run(nch, [&](size_t c) {
+        std::vector<uint32_t> head(ng), end(ng);
+        for (size_t gi = 0; gi < ng; gi++) head[gi] = cut[c * ng + gi], end[gi] = cut[(c + 1) * ng + gi];
+        size_t gk = g0 + at[c].g, ek = e0 + at[c].e, xk = x0 + at[c].x;
+        for (;;) {
+            uint32_t best = UINT32_MAX, bg_ = 0;
+            for (uint32_t gi = 0; gi < ng; gi++)
+                if (head[gi] < end[gi] && outs[gi].recs[head[gi]].bi < best) best = outs[gi].recs[head[gi]].bi, bg_ = gi;
+            if (best == UINT32_MAX) break;
+            const PoolOut& o = outs[bg_];
+            const Rec& r = o.recs[head[bg_]++];
+            const uint32_t T = brow[r.bi];
+            intervals_[T]++;  // the row's pending Intervals increment
+            if (r.expired) expired[xk++] = T;
+            if (!r.matched) continue;
+            for (uint32_t k = 0; k < r.len; k++) {
+                const auto& e = o.ents[r.off + k];
+                out_groups.ents[ek + k] = e;
+                newly[n0 + (ek - e0) + k] = e.first;
+                sel[e.first] = 1;
+            }
+            ek += r.len;
+            out_groups.off[++gk] = (uint32_t)ek;
+        }
+    });
 }
 
 // choose_source without advancing the posting lists' dead-prefix heads (safe
