@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <string_view>
 
 namespace nkm {
 
@@ -90,7 +91,7 @@ inline int64_t civil_days(int64_t y, int m, int d) {  // days since 1970-01-01
 }
 
 // layout: 0 RFC3339Nano, 1 RFC3339, 2 "2006-01-02T15:04:05", 3 "2006-01-02 15:04:05", 4 "2006-01-02"
-inline GoTime go_parse_time(const std::string& v, int layout) {
+inline GoTime go_parse_time(std::string_view v, int layout) {
     GoTime t;
     size_t p = 0, n = v.size();
     auto dig = [&](size_t at) { return at < n && v[at] >= '0' && v[at] <= '9'; };
@@ -149,7 +150,7 @@ inline GoTime go_parse_time(const std::string& v, int layout) {
     return t;
 }
 
-inline bool bluge_datetime(const std::string& v, int64_t* unix_nano) {
+inline bool bluge_datetime(std::string_view v, int64_t* unix_nano) {
     for (int layout = 0; layout < 5; layout++) {
         GoTime t = go_parse_time(v, layout);
         if (t.ok) { *unix_nano = t.unix_nano; return true; }

@@ -27,6 +27,7 @@
 #include "qcompile.h"
 #include "termmatch.h"
 #include "replay_core.h"
+#include "strstore.h"
 
 namespace nkm {
 
@@ -88,35 +89,17 @@ struct PinnedArray {
     ~PinnedArray() { release(); }
 };
 
-// String dictionary (keyword values, query terms, party ids).
-struct Dict {
-    std::unordered_map<std::string, uint32_t> id;
-    std::vector<std::string> str;
-    uint32_t intern(const std::string& s) {
-        auto it = id.find(s);
-        if (it != id.end()) return it->second;
-        uint32_t v = (uint32_t)str.size();
-        id.emplace(s, v);
-        str.push_back(s);
-        return v;
-    }
-    int64_t find(const std::string& s) const {
-        auto it = id.find(s);
-        return it == id.end() ? -1 : (int64_t)it->second;
-    }
-    void clear() { id.clear(); str.clear(); }
-};
+// Resizes with 25% headroom once the capacity is exceeded: a pass's arrays
+// settle at the first pass's size plus a margin instead of reallocating (and
+// page-faulting a fresh copy) on a later pass a few percent larger.
+template <class V>
+inline void grow_to(V& v, size_t n) {
+    if (n > v.capacity()) v.reserve(n + n / 4);
+    v.resize(n);
+}
 
 struct Presence {
     std::string user_id, session_id, username, node;
-};
-
-// Host-only per-ticket record kept for Extract and delivery.
-struct Cold {
-    std::string session_id, party_id, query, node;
-    std::vector<std::pair<std::string, std::string>> sprops;
-    std::vector<std::pair<std::string, double>> nprops;
-    std::vector<Presence> presences;
 };
 
 // One compiled signature: clauses + the searching ticket's filters.  Tickets
@@ -477,18 +460,29 @@ private:
     int remove_locked(const std::vector<std::string>& ids);
 
     // ---- store ----
-    int add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_insert);
+    int add_locked(const mm_ticket& t, uint32_t sig, bool from_insert);
+    // Signature of a ticket's search, through a cache keyed by (query text,
+    // MinCount, MaxCount): a repeated query skips the compile.  -1 - status
+    // when the query does not compile.
+    int64_t sig_cached(const mm_ticket& t);
+    Dict qtext_;                    // cached query texts
+    std::vector<int32_t> qstatus_;  // per cached text: compile_query's status
+    struct QSig { uint32_t q; int32_t mn, mx; uint32_t sig; };
+    std::vector<QSig> qsig_;
+    HashIndex qsig_idx_;
+    Dict prop_key_;                 // property name -> field ("properties." + name)
+    std::vector<uint16_t> prop_field_;
+    uint16_t prop_field(std::string_view key);
     uint16_t field_of(const std::string& name);
     uint32_t sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party);
     uint32_t termset_of(const HostClause& c);  // interned regexp/wildcard/fuzzy matcher
     void refresh_termsets();                   // extends accepted sets over new dictionary terms, uploads
     void set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val);
     void kill_slot(uint32_t slot, bool device_cleared = false, bool replaced = false);  // ticket leaves the index and the maps
-    const char* arena_string(const std::string& s);
     void maybe_compact();
     void compact();
     bool live(uint32_t slot) const { return live_[slot] != 0; }
-    int64_t slot_of_ticket(const std::string& t) const;
+    int64_t slot_of_ticket(std::string_view t) const;
 
     // ---- device ----
     void sync_device();     // uploads, index build, pending deletes
@@ -550,6 +544,8 @@ private:
     bool big_list(const std::vector<uint32_t>& v) const { return par_mode_ != 0 && v.size() >= par_min(65536); }
 
 public:
+    using Props = std::vector<std::pair<uint16_t, std::pair<uint8_t, int64_t>>>;  // (field, (kind, value))
+    void doc_props(const ColdView& v, Props& out);
     // ---- host SoA (per slot) ----  (public for the replay helpers)
     Dict dict_;                       // keyword values / terms / parties
     Dict sess_dict_;                  // presence session ids (rebuilt at compaction)
@@ -567,10 +563,11 @@ public:
                     GroupList& out_groups, std::vector<uint32_t>& expired, std::vector<uint32_t>& newly);
     std::vector<uint32_t> pos_of_;        // slot -> list position during a dense replay, else kNoSlot
     Dict field_dict_;                 // field names -> field id
-    std::vector<std::string> ticket_;
-    std::vector<const char*> tk_ptr_;               // per slot: NUL-terminated ticket id in tk_blocks_
-    std::vector<std::unique_ptr<char[]>> tk_blocks_;  // stable string arena (never moves)
-    size_t tk_block_used_ = 0;
+    std::vector<const char*> tk_ptr_;  // per slot: NUL-terminated ticket id in tk_arena_
+    std::vector<uint32_t> tk_len_;
+    StrArena tk_arena_;                // ticket ids (blocks never move: results point here)
+    std::string_view tk(uint32_t s) const { return {tk_ptr_[s], tk_len_[s]}; }
+    size_t nslots() const { return tk_ptr_.size(); }
     std::vector<int64_t> created_;
     std::vector<int64_t> ckey_;       // sortable key of float64(CreatedAt)
     std::vector<int32_t> minc_, maxc_, cm_, count_, intervals_;
@@ -586,10 +583,12 @@ public:
     void set_hot(uint32_t s);
     std::vector<uint32_t> pres_off_;  // CSR over presences: [slot] -> first presence
     std::vector<uint32_t> pres_sess_; // per presence: session dict id
-    std::vector<Cold> cold_;
+    ColdStore cold_;                  // per slot: session, party, query, presences, properties
+    std::vector<uint32_t> tnode_;     // per slot: node_dict_ id
+    Dict node_dict_;
     std::vector<std::vector<int64_t>> fval_;
     std::vector<std::vector<uint8_t>> fkind_;
-    std::unordered_map<std::string, uint32_t> slot_of_;  // may hold dead slots (checked with live_)
+    HashIndex slot_of_;               // ticket id -> latest slot (may be dead: checked with live_)
     std::vector<uint32_t> active_list_;                  // pinned (CreatedAt, Ticket) order, may hold inactive
     bool active_sorted_ = true;
     SlotSets sess_slots_;             // session dict id -> slots (sessionTickets)

@@ -652,7 +652,7 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
     }
     if (keyf.empty()) return false;
     for (uint16_t f : keyf)
-        if (fkind_[f].size() != ticket_.size()) return false;
+        if (fkind_[f].size() != nslots()) return false;
     // pool key of each search; a search requiring two different terms on one
     // field matches nothing (the batch then takes the serial replay).  One key
     // field (C5's buckets: ~10^5 pools): keys extracted on the workers and
@@ -687,7 +687,7 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
         for (uint8_t b : bad)
             if (b) return false;
         std::vector<uint32_t>& remap = pool_remap_;
-        remap.assign(dict_.str.size(), UINT32_MAX);
+        remap.assign(dict_.size(), UINT32_MAX);
         for (size_t i = 0; i < nsearch; i++) {
             uint32_t& p = remap[k1[i]];
             if (p == UINT32_MAX) {
@@ -810,7 +810,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
     const bool few = ng <= 64;
     if (task_ents_.size() < ntask) task_ents_.resize(ntask);
     if (few && pool_outs_.size() < ng) pool_outs_.resize(ng);
-    if (!few && row_recs_.size() < nb) row_recs_.resize(nb);
+    if (!few && row_recs_.size() < nb) grow_to(row_recs_, nb);
     RowRec* rr = few ? nullptr : row_recs_.data();
     if (!few)
         wp.run(wp.size(), [&](size_t c) {  // rows no pool processes (selected before they were reached) stay zero
@@ -820,7 +820,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
     // of their list (DensePool/DenseRun), gathered first in chunks across the
     // workers; the others take the generic walk over the store.
     if (dense_pools_.size() < ng) dense_pools_.resize(ng);
-    if (pos_of_.size() < ticket_.size()) pos_of_.resize(ticket_.size(), kNoSlot);
+    if (pos_of_.size() < nslots()) pos_of_.resize(nslots(), kNoSlot);
     const ReplayView rv = Replay::view(*this);
     std::vector<std::pair<uint32_t, uint32_t>> chunks;  // (pool, chunk) of the dense gathers
     constexpr uint32_t kGatherChunk = 16384;
@@ -944,10 +944,10 @@ void Core::merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, 
     });
     for (size_t c = 0; c < nch; c++) at[c + 1] = {at[c].g + at[c + 1].g, at[c].e + at[c + 1].e, at[c].x + at[c + 1].x};
     const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
-    out_groups.off.resize(g0 + 1 + at[nch].g);
-    out_groups.ents.resize(e0 + at[nch].e);
-    expired.resize(x0 + at[nch].x);
-    newly.resize(n0 + at[nch].e);
+    grow_to(out_groups.off, g0 + 1 + at[nch].g);
+    grow_to(out_groups.ents, e0 + at[nch].e);
+    grow_to(expired, x0 + at[nch].x);
+    grow_to(newly, n0 + at[nch].e);
     wp.run(nch, [&](size_t c) {
         size_t gk = g0 + at[c].g, ek = e0 + at[c].e, xk = x0 + at[c].x;
         for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++) {
@@ -1006,10 +1006,10 @@ void Core::merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow,
         at[c + 1] = {at[c].g + k.g, at[c].e + k.e, at[c].x + k.x};
     }
     const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
-    out_groups.off.resize(g0 + 1 + at[nch].g);
-    out_groups.ents.resize(e0 + at[nch].e);
-    expired.resize(x0 + at[nch].x);
-    newly.resize(n0 + at[nch].e);
+    grow_to(out_groups.off, g0 + 1 + at[nch].g);
+    grow_to(out_groups.ents, e0 + at[nch].e);
+    grow_to(expired, x0 + at[nch].x);
+    grow_to(newly, n0 + at[nch].e);
     wp.run(nch, [&](size_t c) {
         std::vector<uint32_t> head(ng), end(ng);
         for (size_t gi = 0; gi < ng; gi++) head[gi] = cut[c * ng + gi], end[gi] = cut[(c + 1) * ng + gi];
@@ -1089,7 +1089,7 @@ void Core::choose_source(const Sig& s, DGroup& g, SrcChoice* ch) {
 
 int Core::process_default(GroupList& out_groups,
                           std::vector<uint32_t>& expired, PassStats& stats) {
-    const uint32_t N = (uint32_t)ticket_.size();
+    const uint32_t N = (uint32_t)nslots();
     std::vector<uint8_t>& sel = sel_;
     sel.assign(N, 0);
     bool rev = cfg_.rev_precision != 0;
@@ -1227,8 +1227,8 @@ int Core::process_default(GroupList& out_groups,
             }
             std::vector<size_t> at(nch + 1, 0);
             for (unsigned c = 0; c < nch; c++) at[c + 1] = at[c] + ch[c].n;
-            brow.resize(at[nch]);
-            brow_group.resize(at[nch]);
+            grow_to(brow, at[nch]);
+            grow_to(brow_group, at[nch]);
             wp.run(nch, [&](size_t c) {
                 size_t o = at[c];
                 for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
@@ -1286,8 +1286,8 @@ int Core::process_default(GroupList& out_groups,
             for (unsigned c = 0; c < nch; c++) tot += ck[c], n += cg[c].size();
             if (tot > kOutCap) return false;  // the serial loop cuts the batch
             bg.reserve(n);
-            brow.resize(n);
-            brow_group.resize(n);
+            grow_to(brow, n);
+            grow_to(brow_group, n);
             for (unsigned c = 0; c < nch; c++) {
                 for (size_t k = 0; k < cg[c].size(); k++) {
                     brow[bg.size()] = crow[c][k];
@@ -1417,7 +1417,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
     if (!active_flag_) return MM_OK;
     bool rev = rev_cfg;
     const DStore st = dstore();
-    std::vector<uint8_t> sel(ticket_.size(), 0);  // processCustom never selects
+    std::vector<uint8_t> sel(nslots(), 0);  // processCustom never selects
     Replay rp(*this, sel, rev, maxI, stats, st, stream_);
     while (order_head_ < order_.size() && !live_[order_[order_head_]]) order_head_++;
     const uint32_t kvar = (uint32_t)var_k_capacity();
@@ -1626,7 +1626,7 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
                 for (size_t i = e0; i < e1; i++) {
                     const uint32_t s = groups.ents[i].first;
                     if (!live_[s]) continue;  // a ticket's presence entries repeat its slot
-                    if (track_removed_) gone[c].push_back(ticket_[s]);
+                    if (track_removed_) gone[c].emplace_back(tk(s));
                     live_[s] = 0;
                     is_active_[s] = 0;
                     k++;
@@ -1687,23 +1687,37 @@ void Core::fill_matched(const GroupList& groups, mm_matched* out,
     mm_entry_ref* ents;
     char* buf = nullptr;
     if (arena) {
-        if (out_offs_.size() < groups.size() + 1) out_offs_.resize(groups.size() + 1);
-        if (out_ents_.size() < std::max<size_t>(n, 1)) out_ents_.resize(std::max<size_t>(n, 1));
+        if (out_offs_.size() < groups.size() + 1) grow_to(out_offs_, groups.size() + 1);
+        if (out_ents_.size() < std::max<size_t>(n, 1)) grow_to(out_ents_, std::max<size_t>(n, 1));
         offs = out_offs_.data();
         ents = out_ents_.data();
     } else {
         size_t bytes = 0;
-        for (auto& e : groups.ents) bytes += ticket_[e.first].size() + 1;
+        for (auto& e : groups.ents) bytes += tk_len_[e.first] + 1;
         offs = new int32_t[groups.size() + 1];
         ents = new mm_entry_ref[n ? n : 1];
         buf = new char[bytes ? bytes : 1];
     }
+    int64_t* gc;  // per group: its last entry's CreatedAt (the cluster merge's key)
+    if (arena) {
+        if (out_created_.size() < std::max<size_t>(groups.size(), 1)) grow_to(out_created_, std::max<size_t>(groups.size(), 1));
+        gc = out_created_.data();
+    } else {
+        gc = new int64_t[groups.size() ? groups.size() : 1];
+    }
+    auto created_of = [&](size_t g) {
+        const uint32_t last = groups.len(g) ? groups.end(g)[-1].first : kNoSlot;
+        gc[g] = last == kNoSlot ? 0 : created_[last];
+    };
     size_t b = 0;
     if (arena && par_mode_ && n >= par_min(65536)) {  // chunks of the result in parallel
         WorkPool& wp = workers();
         const size_t nch = wp.size(), ng = groups.size() + 1;
         wp.run(nch, [&](size_t c) {
-            for (size_t gi = ng * c / nch; gi < ng * (c + 1) / nch; gi++) offs[gi] = (int32_t)groups.off[gi];
+            for (size_t gi = ng * c / nch; gi < ng * (c + 1) / nch; gi++) {
+                offs[gi] = (int32_t)groups.off[gi];
+                if (gi < ng - 1) created_of(gi);
+            }
             for (size_t k = n * c / nch; k < n * (c + 1) / nch; k++) {
                 const auto& e = groups.ents[k];
                 ents[k].ticket = tk_ptr_[e.first];
@@ -1713,6 +1727,7 @@ void Core::fill_matched(const GroupList& groups, mm_matched* out,
         });
     } else {
         for (size_t gi = 0; gi <= groups.size(); gi++) offs[gi] = (int32_t)groups.off[gi];
+        for (size_t g = 0; g < groups.size(); g++) created_of(g);
         uint32_t prev = kNoSlot;
         const char* prev_p = nullptr;
         for (size_t k = 0; k < n; k++) {
@@ -1721,10 +1736,9 @@ void Core::fill_matched(const GroupList& groups, mm_matched* out,
                 if (arena) {
                     prev_p = tk_ptr_[e.first];
                 } else {
-                    const std::string& t = ticket_[e.first];
-                    std::memcpy(buf + b, t.c_str(), t.size() + 1);
+                    std::memcpy(buf + b, tk_ptr_[e.first], tk_len_[e.first] + 1);
                     prev_p = buf + b;
-                    b += t.size() + 1;
+                    b += tk_len_[e.first] + 1;
                 }
                 prev = e.first;
             }
@@ -1732,17 +1746,6 @@ void Core::fill_matched(const GroupList& groups, mm_matched* out,
             ents[k].presence_index = e.second;
             ents[k].reserved = 0;
         }
-    }
-    int64_t* gc;
-    if (arena) {
-        if (out_created_.size() < std::max<size_t>(groups.size(), 1)) out_created_.resize(std::max<size_t>(groups.size(), 1));
-        gc = out_created_.data();
-    } else {
-        gc = new int64_t[groups.size() ? groups.size() : 1];
-    }
-    for (size_t g = 0; g < groups.size(); g++) {
-        const uint32_t last = groups.len(g) ? groups.end(g)[-1].first : kNoSlot;
-        gc[g] = last == kNoSlot ? 0 : created_[last];
     }
     out->group_created = gc;
     out->n_groups = (int32_t)groups.size();
@@ -1785,7 +1788,7 @@ int Core::process(mm_matched* out) {
     if (!active_sorted_) {
         std::sort(active_list_.begin(), active_list_.end(), [&](uint32_t a, uint32_t b) {
             if (created_[a] != created_[b]) return created_[a] < created_[b];
-            return ticket_[a] < ticket_[b];
+            return tk(a) < tk(b);
         });
         active_sorted_ = true;
     }
@@ -1839,8 +1842,8 @@ int Core::process(mm_matched* out) {
                          ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms(), stats.replay_ms,
                          stats.apply_ms, stats.batches,
                          stats.parallel_batches, stats.refetches, stats.launches(), ms(t2, t3), ms(t3, t4),
-                         groups.size(), ticket_.size(), n_live_, active_list_.size(), sigs_.size(),
-                         dict_.str.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms,
+                         groups.size(), nslots(), n_live_, active_list_.size(), sigs_.size(),
+                         dict_.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms,
                          stats.par_task_max_ms, (unsigned long long)stats.par_rows, (unsigned long long)stats.par_hits);
         }
     }
@@ -1948,7 +1951,7 @@ int32_t Core::debug_hits(const std::string& ticket, const char** tk, double* sc,
     sync_device();
     const DStore st = dstore();
     PassStats stats;
-    std::vector<uint8_t> sel(ticket_.size(), 0);
+    std::vector<uint8_t> sel(nslots(), 0);
     Replay rp(*this, sel, cfg_.rev_precision != 0, cfg_.max_intervals, stats, st, stream_);
     BGroup g;
     g.sig = sig_[T];
@@ -1974,7 +1977,7 @@ int32_t Core::debug_hits(const std::string& ticket, const char** tk, double* sc,
     auto skip = [&](uint32_t i) { return g.hits[i].slot == (uint32_t)T || rp.same_party((uint32_t)T, g.hits[i].slot); };
     for (uint32_t i = 0; i < g.n; i++) {
         if (skip(i)) continue;
-        debug_strings_.push_back(ticket_[g.hits[i].slot]);
+        debug_strings_.emplace_back(this->tk(g.hits[i].slot));
     }
     for (uint32_t i = 0; i < g.n; i++) {
         if (skip(i)) continue;

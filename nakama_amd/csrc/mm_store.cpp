@@ -227,7 +227,7 @@ Core::~Core() {
 uint16_t Core::field_of(const std::string& name) {
     int64_t f = field_dict_.find(name);
     if (f >= 0) return (uint16_t)f;
-    if (field_dict_.str.size() >= 65535) throw DeviceError{hipErrorOutOfMemory, "too many fields", __LINE__};
+    if (field_dict_.size() >= 65535) throw DeviceError{hipErrorOutOfMemory, "too many fields", __LINE__};
     uint16_t id = (uint16_t)field_dict_.intern(name);
     fval_.emplace_back();
     fkind_.emplace_back();
@@ -239,61 +239,54 @@ uint16_t Core::field_of(const std::string& name) {
     return id;
 }
 
-int64_t Core::slot_of_ticket(const std::string& t) const {
-    auto it = slot_of_.find(t);
-    if (it == slot_of_.end() || !live_[it->second]) return -1;
-    return it->second;
+int64_t Core::slot_of_ticket(std::string_view t) const {
+    const int64_t s = slot_of_.find(str_hash(t), [&](uint32_t v) { return tk(v) == t; });
+    if (s < 0 || !live_[s]) return -1;
+    return s;
 }
 
-// Value of field f for slot s, computed from the host record (used to build a
-// dense column the first time a query references the field).
-static void field_value(const Core& c, uint16_t f, uint32_t s, const std::vector<std::pair<uint16_t, std::pair<uint8_t, int64_t>>>& props,
-                        uint8_t* kind, int64_t* val) {
-    (void)c;
+// Value of field f in a ticket's document properties (doc_props).
+static void field_value(uint16_t f, const Core::Props& props, uint8_t* kind, int64_t* val) {
     *kind = KIND_ABSENT;
     *val = 0;
     for (auto& p : props)
         if (p.first == f) { *kind = p.second.first; *val = p.second.second; }
-    (void)s;
+}
+
+// Field of a property name ("properties." + name, interned on first sight).
+uint16_t Core::prop_field(std::string_view key) {
+    const int64_t i = prop_key_.find(key);
+    if (i >= 0) return prop_field_[i];
+    std::string name = "properties.";
+    name.append(key);
+    const uint16_t f = field_of(name);
+    prop_key_.intern(key);
+    prop_field_.push_back(f);
+    return f;
 }
 
 // Builds the property part of the bluge document of a ticket
 // (blugeProcessProperty, match_common.go:148-212): string props become keyword
 // terms unless they parse as a datetime (then the raw UnixNano numeric term);
 // numeric props the sortable int64 of the float64; numeric wins on key clash
-// (matchmaker.go:460-466).
-static void doc_props(Core& c, const Cold& cold, std::vector<std::pair<uint16_t, std::pair<uint8_t, int64_t>>>& out,
-                      uint16_t (Core::*field_of_fn)(const std::string&)) {
+// (matchmaker.go:460-466).  Fields in first-seen order, the last value wins.
+void Core::doc_props(const ColdView& v, Props& out) {
     out.clear();
-    std::unordered_map<std::string, std::pair<uint8_t, int64_t>> merged;
-    std::vector<std::string> keys;
-    for (auto& kv : cold.sprops) {
-        int64_t ns;
-        std::pair<uint8_t, int64_t> v;
-        if (bluge_datetime(kv.second, &ns)) v = {KIND_NUMERIC, ns};
-        else v = {KIND_KEYWORD, (int64_t)c.dict_.intern(kv.second)};
-        if (!merged.count(kv.first)) keys.push_back(kv.first);
-        merged[kv.first] = v;
-    }
-    for (auto& kv : cold.nprops) {
-        if (!merged.count(kv.first)) keys.push_back(kv.first);
-        merged[kv.first] = {KIND_NUMERIC, sortable_i64(kv.second)};
-    }
-    for (auto& k : keys) out.push_back({(c.*field_of_fn)("properties." + k), merged[k]});
-}
-
-// Copies s into the ticket-string arena (1 MiB blocks that never move).
-const char* Core::arena_string(const std::string& s) {
-    constexpr size_t kBlock = 1 << 20;
-    const size_t need = s.size() + 1;
-    if (tk_blocks_.empty() || tk_block_used_ + need > kBlock) {
-        tk_blocks_.emplace_back(new char[std::max(kBlock, need)]);
-        tk_block_used_ = 0;
-    }
-    char* p = tk_blocks_.back().get() + tk_block_used_;
-    std::memcpy(p, s.c_str(), need);
-    tk_block_used_ += need;
-    return p;
+    auto put = [&](uint16_t f, uint8_t kind, int64_t val) {
+        for (auto& p : out)
+            if (p.first == f) {
+                p.second = {kind, val};
+                return;
+            }
+        out.push_back({f, {kind, val}});
+    };
+    v.each_prop(
+        [&](std::string_view k, std::string_view val) {
+            int64_t ns;
+            if (bluge_datetime(val, &ns)) put(prop_field(k), KIND_NUMERIC, ns);
+            else put(prop_field(k), KIND_KEYWORD, (int64_t)dict_.intern(val));
+        },
+        [&](std::string_view k, double d) { put(prop_field(k), KIND_NUMERIC, sortable_i64(d)); });
 }
 
 void Core::set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val) {
@@ -330,11 +323,11 @@ uint32_t Core::termset_of(const HostClause& c) {
 // field are harmless: the kernels test the candidate's own value id.
 void Core::refresh_termsets() {
     if (tsets_.empty()) return;
-    const uint32_t nd = (uint32_t)dict_.str.size();
+    const uint32_t nd = (uint32_t)dict_.size();
     for (auto& ts : tsets_) {
         for (uint32_t id = ts.done; id < nd; id++) {
             double tb;
-            if (!ts.m.accept(dict_.str[id], &tb)) continue;
+            if (!ts.m.accept(std::string(dict_.str(id)), &tb)) continue;
             ts.ids.push_back(id);
             // RegexpQuery(b): b.  Fuzzy MatchQuery(b): (0 + b*tb) * b (composite.go:37-43)
             ts.sc.push_back(ts.m.kind == TermMatcher::K_FUZZY ? (0.0 + ts.b * tb) * ts.b : ts.b);
@@ -451,27 +444,28 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
     sigs_.push_back(std::move(s));
     sig_index_.emplace(std::move(key), id);
     // fields referenced for the first time get a dense host column now
+    const size_t n = nslots();
     for (size_t f = 0; f < field_used_.size(); f++) {
-        if (field_used_[f] && fval_[f].size() != ticket_.size()) {
-            fval_[f].assign(ticket_.size(), 0);
-            fkind_[f].assign(ticket_.size(), KIND_ABSENT);
-            for (uint32_t sl = 0; sl < ticket_.size(); sl++) {
+        if (field_used_[f] && fval_[f].size() != n) {
+            fval_[f].assign(n, 0);
+            fkind_[f].assign(n, KIND_ABSENT);
+            Props props;
+            for (uint32_t sl = 0; sl < n; sl++) {
                 if (f < F_NBUILTIN) {
                     switch (f) {
-                    case F_TICKET: set_field((uint16_t)f, sl, KIND_KEYWORD, dict_.intern(ticket_[sl])); break;
+                    case F_TICKET: set_field((uint16_t)f, sl, KIND_KEYWORD, dict_.intern(tk(sl))); break;
                     case F_MIN: set_field((uint16_t)f, sl, KIND_NUMERIC, sortable_i64((double)minc_[sl])); break;
                     case F_MAX: set_field((uint16_t)f, sl, KIND_NUMERIC, sortable_i64((double)maxc_[sl])); break;
                     case F_PARTY:
-                        set_field((uint16_t)f, sl, KIND_KEYWORD, dict_.intern(cold_[sl].party_id));
+                        set_field((uint16_t)f, sl, KIND_KEYWORD, dict_.intern(cold_.view(sl).party_id));
                         break;
                     case F_CREATED: set_field((uint16_t)f, sl, KIND_NUMERIC, ckey_[sl]); break;
                     }
                 } else {
-                    std::vector<std::pair<uint16_t, std::pair<uint8_t, int64_t>>> props;
-                    doc_props(*this, cold_[sl], props, &Core::field_of);
+                    doc_props(cold_.view(sl), props);
                     uint8_t k;
                     int64_t v;
-                    field_value(*this, (uint16_t)f, sl, props, &k, &v);
+                    field_value((uint16_t)f, props, &k, &v);
                     set_field((uint16_t)f, sl, k, v);
                 }
             }
@@ -483,7 +477,7 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
 
 void Core::kill_slot(uint32_t s, bool device_cleared, bool replaced) {
     if (!live_[s]) return;
-    if (track_removed_ && !replaced) removed_ids_.push_back(ticket_[s]);  // a replaced id lives on
+    if (track_removed_ && !replaced) removed_ids_.emplace_back(tk(s));  // a replaced id lives on
     live_[s] = 0;
     is_active_[s] = 0;
     n_live_--;
@@ -498,25 +492,40 @@ void Core::kill_slot(uint32_t s, bool device_cleared, bool replaced) {
     if (party_[s] != kNoParty) party_slots_.erase(party_[s], s);
 }
 
-int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_insert) {
-    const std::string tk = t.ticket ? t.ticket : "";
-    int64_t existing = slot_of_ticket(tk);
-    if (existing >= 0) kill_slot((uint32_t)existing, false, true);  // same ticket id re-inserted: replace
-    const uint32_t s = (uint32_t)ticket_.size();
-    Cold cold;
-    cold.session_id = t.session_id ? t.session_id : "";
-    cold.party_id = t.party_id ? t.party_id : "";
-    cold.query = t.query ? t.query : "";
-    cold.node = from_insert ? (t.node ? t.node : "") : node_;
-    for (int i = 0; i < t.n_str_props; i++) cold.sprops.push_back({t.str_props[i].key, t.str_props[i].value});
-    for (int i = 0; i < t.n_num_props; i++) cold.nprops.push_back({t.num_props[i].key, t.num_props[i].value});
-    for (int i = 0; i < t.n_presences; i++) {
-        const mm_presence& p = t.presences[i];
-        cold.presences.push_back({p.user_id ? p.user_id : "", p.session_id ? p.session_id : "",
-                                  p.username ? p.username : "", p.node ? p.node : ""});
+int Core::add_locked(const mm_ticket& t, uint32_t sg, bool from_insert) {
+    auto S = [](const char* p) { return p ? std::string_view(p) : std::string_view(); };
+    const std::string_view tkv = S(t.ticket);
+    const uint64_t th = str_hash(tkv);
+    const int64_t existing = slot_of_.find(th, [&](uint32_t v) { return tk(v) == tkv; });
+    if (existing >= 0 && live_[existing]) kill_slot((uint32_t)existing, false, true);  // same id re-inserted: replace
+    const uint32_t s = (uint32_t)nslots();
+    tk_ptr_.push_back(tk_arena_.put(tkv));
+    tk_len_.push_back((uint32_t)tkv.size());
+    {
+        ColdStore::Writer w = cold_.begin();
+        w.u32((uint32_t)std::max(t.n_presences, 0));
+        w.u32((uint32_t)std::max(t.n_str_props, 0));
+        w.u32((uint32_t)std::max(t.n_num_props, 0));
+        w.str(t.session_id);
+        w.str(t.party_id);
+        w.str(t.query);
+        for (int i = 0; i < t.n_presences; i++) {
+            const mm_presence& p = t.presences[i];
+            w.str(p.user_id);
+            w.str(p.session_id);
+            w.str(p.username);
+            w.str(p.node);
+        }
+        for (int i = 0; i < t.n_str_props; i++) {
+            w.str(t.str_props[i].key);
+            w.str(t.str_props[i].value);
+        }
+        for (int i = 0; i < t.n_num_props; i++) {
+            w.str(t.num_props[i].key);
+            w.f64(t.num_props[i].value);
+        }
     }
-    ticket_.push_back(tk);
-    tk_ptr_.push_back(arena_string(tk));
+    tnode_.push_back(node_dict_.intern(from_insert ? S(t.node) : std::string_view(node_)));
     created_.push_back(t.created_at);
     ckey_.push_back(sortable_i64((double)t.created_at));
     minc_.push_back(t.min_count);
@@ -524,14 +533,15 @@ int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_inse
     cm_.push_back(t.count_multiple);
     count_.push_back(t.n_presences);
     intervals_.push_back(from_insert ? t.intervals : 0);
-    uint32_t party = cold.party_id.empty() ? kNoParty : party_dict_.intern(cold.party_id);
+    const std::string_view pid = S(t.party_id);
+    const uint32_t party = pid.empty() ? kNoParty : party_dict_.intern(pid);
     party_.push_back(party);
     live_.push_back(1);
     indexed_.push_back(1);
     bool act = from_insert ? (t.intervals < cfg_.max_intervals) : true;
     is_active_.push_back(act ? 1 : 0);
     if (pres_off_.empty()) pres_off_.push_back(0);
-    for (auto& p : cold.presences) pres_sess_.push_back(sess_dict_.intern(p.session_id));
+    for (int i = 0; i < t.n_presences; i++) pres_sess_.push_back(sess_dict_.intern(S(t.presences[i].session_id)));
     pres_off_.push_back((uint32_t)pres_sess_.size());
     {
         uint32_t p0 = pres_off_[s], p1 = pres_off_[s + 1];
@@ -551,33 +561,30 @@ int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_inse
             fkind_[f].push_back(KIND_ABSENT);
         }
     }
-    cold_.push_back(std::move(cold));
-    const Cold& c = cold_.back();
-    if (field_used_[F_TICKET]) set_field(F_TICKET, s, KIND_KEYWORD, dict_.intern(tk));
+    if (field_used_[F_TICKET]) set_field(F_TICKET, s, KIND_KEYWORD, dict_.intern(tkv));
     if (field_used_[F_MIN]) set_field(F_MIN, s, KIND_NUMERIC, sortable_i64((double)t.min_count));
     if (field_used_[F_MAX]) set_field(F_MAX, s, KIND_NUMERIC, sortable_i64((double)t.max_count));
-    if (field_used_[F_PARTY]) set_field(F_PARTY, s, KIND_KEYWORD, dict_.intern(c.party_id));
+    if (field_used_[F_PARTY]) set_field(F_PARTY, s, KIND_KEYWORD, dict_.intern(pid));
     if (field_used_[F_CREATED]) set_field(F_CREATED, s, KIND_NUMERIC, ckey_[s]);
-    std::vector<std::pair<uint16_t, std::pair<uint8_t, int64_t>>> props;
-    doc_props(*this, c, props, &Core::field_of);
-    for (auto& p : props) {
-        if (p.first < fval_.size() && fval_[p.first].size() == ticket_.size()) set_field(p.first, s, p.second.first, p.second.second);
+    {
+        static thread_local Props props;
+        doc_props(cold_.view(s), props);
+        for (auto& p : props)
+            if (p.first < fval_.size() && fval_[p.first].size() == nslots()) set_field(p.first, s, p.second.first, p.second.second);
     }
-    sig_.push_back(0);
-    squery_.push_back(DQuery{});
     // The party mustNot (matchmaker_process.go:80-85) only ever removes the
     // searching ticket's own party (<= MaxTickets tickets), so it is applied
     // while walking the hit list instead of in the shared search: party
-    // tickets then share their pool's search.
-    uint32_t sg = sig_of(cq, t.min_count, t.max_count, kNoParty);  // may materialise new columns (incl. this slot)
-    sig_[s] = sg;
-    squery_[s] = DQuery{sigs_[sg].clause_off, sigs_[sg].n_clauses, sigs_[sg].qkind, 0};
-    slot_of_[tk] = s;
+    // tickets then share their pool's search (sig: the caller's sig_of with
+    // kNoParty).
+    sig_.push_back(sg);
+    squery_.push_back(DQuery{sigs_[sg].clause_off, sigs_[sg].n_clauses, sigs_[sg].qkind, 0});
+    slot_of_.put(th, s, [&](uint32_t v) { return tk(v) == tkv; });
     n_live_++;
     if (act) {
         if (!active_list_.empty()) {
             uint32_t l = active_list_.back();
-            if (created_[l] > t.created_at || (created_[l] == t.created_at && ticket_[l] > tk)) active_sorted_ = false;
+            if (created_[l] > t.created_at || (created_[l] == t.created_at && tk(l) > tkv)) active_sorted_ = false;
         }
         active_list_.push_back(s);
     }
@@ -588,6 +595,41 @@ int Core::add_locked(const mm_ticket& t, const CompiledQuery& cq, bool from_inse
     order_.push_back(s);
     index_dirty_ = true;
     return MM_OK;
+}
+
+// sig_of through the (query text, MinCount, MaxCount) cache.  The cache is
+// dropped when it reaches 64k texts (a workload of unique queries gains
+// nothing from it and must not grow it without bound).
+int64_t Core::sig_cached(const mm_ticket& t) {
+    const std::string_view q = t.query ? std::string_view(t.query) : std::string_view();
+    if (qtext_.size() >= (1u << 16)) {
+        qtext_.clear();
+        qstatus_.clear();
+        qsig_.clear();
+        qsig_idx_.clear();
+    }
+    int64_t qi = qtext_.find(q);
+    CompiledQuery cq;
+    bool compiled = false;
+    if (qi < 0) {
+        const int rc = compile_query(std::string(q), &cq);
+        compiled = true;
+        qi = qtext_.intern(q);
+        qstatus_.push_back(rc);
+    }
+    if (qstatus_[qi] != CQ_OK) return -1 - qstatus_[qi];
+    uint64_t h = (uint64_t)qi * 0x9E3779B97F4A7C15ull;
+    h = (h ^ (uint32_t)t.min_count) * 0xBF58476D1CE4E5B9ull;
+    h = (h ^ (uint32_t)t.max_count) * 0x94D049BB133111EBull;
+    h ^= h >> 31;
+    auto eq = [&](uint32_t i) { return qsig_[i].q == qi && qsig_[i].mn == t.min_count && qsig_[i].mx == t.max_count; };
+    const int64_t e = qsig_idx_.find(h, eq);
+    if (e >= 0) return qsig_[e].sig;
+    if (!compiled) compile_query(std::string(q), &cq);
+    const uint32_t sg = sig_of(cq, t.min_count, t.max_count, kNoParty);  // may materialise new columns
+    qsig_idx_.put_new(h, (uint32_t)qsig_.size());
+    qsig_.push_back(QSig{(uint32_t)qi, t.min_count, t.max_count, sg});
+    return sg;
 }
 
 static int status_of(int cq) { return cq == CQ_UNSUPPORTED ? MM_ERR_UNSUPPORTED : MM_ERR_QUERY_INVALID; }
@@ -623,7 +665,7 @@ int Core::add(const mm_ticket& t) {
         return MM_OK;
     }
     maybe_compact();
-    return add_locked(t, cq, false);
+    return add_locked(t, sig_of(cq, t.min_count, t.max_count, kNoParty), false);
 }
 
 // ---- the effective state while a pass runs (see mm_core.h) ----
@@ -666,13 +708,13 @@ Core::PendTk* Core::eff_ticket(const std::string& id) {
     if (s < 0) return nullptr;
     PendTk t;
     t.alive = true;
-    const Cold& c = cold_[s];
-    t.session_id = c.session_id;
-    t.party_id = c.party_id;
-    t.node = c.node;
-    for (auto& p : c.presences)
-        if (std::find(t.sessions.begin(), t.sessions.end(), p.session_id) == t.sessions.end())
-            t.sessions.push_back(p.session_id);
+    const ColdView c = cold_.view((uint32_t)s);
+    t.session_id = std::string(c.session_id);
+    t.party_id = std::string(c.party_id);
+    t.node = std::string(node_dict_.str(tnode_[s]));
+    c.each_presence([&](std::string_view, std::string_view sid, std::string_view, std::string_view) {
+        if (std::find(t.sessions.begin(), t.sessions.end(), sid) == t.sessions.end()) t.sessions.emplace_back(sid);
+    });
     return &pend_tk_.emplace(id, std::move(t)).first->second;
 }
 
@@ -729,7 +771,7 @@ void Core::apply_pending() {
             for (size_t i = 0; i < op.tickets.size(); i++) {
                 if (!op.ok[i]) continue;
                 op.tickets[i].view(v);
-                add_locked(v.t, op.cqs[i], op.kind == P_INSERT);
+                add_locked(v.t, sig_of(op.cqs[i], v.t.min_count, v.t.max_count, kNoParty), op.kind == P_INSERT);
             }
             break;
         }
@@ -777,48 +819,34 @@ void Core::free_str_list(mm_str_list* out) {
 int Core::insert(const mm_ticket* ts, int32_t n) {
     if (stopped_ || n <= 0) return MM_OK;
     using clk = std::chrono::steady_clock;
-    const auto t0 = clk::now();
-    std::vector<CompiledQuery> cqs((size_t)n);
-    std::vector<uint8_t> ok((size_t)n, 0);
     std::lock_guard<std::mutex> lk(mu_);  // also serialises use of the worker pool
     if (pass_running_) {  // queued (the pass owns the workers)
         PendingOp op{P_INSERT};
         op.tickets.reserve((size_t)n);
+        op.cqs.resize((size_t)n);
         for (int i = 0; i < n; i++) {
             op.tickets.emplace_back(ts[i]);
-            op.ok.push_back(compile_query(ts[i].query ? ts[i].query : "", &cqs[i]) == CQ_OK);
+            op.ok.push_back(compile_query(ts[i].query ? ts[i].query : "", &op.cqs[i]) == CQ_OK);
             if (op.ok.back()) eff_add(op.tickets.back());
         }
-        op.cqs = std::move(cqs);
         pending_.push_back(std::move(op));
         return MM_OK;
     }
-    // query compiles are independent: spread large batches over the host workers
-    auto compile_range = [&](size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; i++) ok[i] = compile_query(ts[i].query ? ts[i].query : "", &cqs[i]) == CQ_OK;
-    };
-    // opt-in (NKM_PAR_COMPILE=1): 10x faster compiles, but the pass's row
-    // bucketing on the same workers then ran 2.2 ms instead of 0.85 ms
-    // (profiles/r01_ab_par_compile.txt), and the pass is the headline
-    static const bool par_compile = std::getenv("NKM_PAR_COMPILE") && std::strcmp(std::getenv("NKM_PAR_COMPILE"), "0") != 0;
-    if (par_compile && par_mode_ && (size_t)n >= par_min(16384)) {
-        WorkPool& wp = workers();
-        const size_t nch = (size_t)wp.size() * 4;
-        wp.run(nch, [&](size_t c) { compile_range((size_t)n * c / nch, (size_t)n * (c + 1) / nch); });
-    } else {
-        compile_range(0, (size_t)n);
-    }
+    // Repeated queries (a pool's tickets share theirs) skip the compile
+    // through the signature cache; the rest compile here, under the lock.
     const auto t1 = clk::now();
     maybe_compact();
     const auto t2 = clk::now();
-    for (int i = 0; i < n; i++)
-        if (ok[i]) add_locked(ts[i], cqs[i], true);
+    for (int i = 0; i < n; i++) {
+        const int64_t sg = sig_cached(ts[i]);
+        if (sg >= 0) add_locked(ts[i], (uint32_t)sg, true);
+    }
     const auto t3 = clk::now();
     if (n >= 1024) sync_device();  // index the batch now (bluge indexes synchronously too)
     if (std::getenv("NKM_PROFILE") && n >= 1024) {
         auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "[nkm] insert %d: compile %.1f ms | compact %.1f ms | add %.1f ms | sync/index/upload %.1f ms\n", n,
-                     ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, clk::now()));
+        std::fprintf(stderr, "[nkm] insert %d: compact %.1f ms | add (incl. compiles) %.1f ms | sync/index/upload %.1f ms\n", n,
+                     ms(t1, t2), ms(t2, t3), ms(t3, clk::now()));
     }
     return MM_OK;
 }
@@ -830,51 +858,75 @@ int Core::extract(mm_extract_list* out) {
     std::lock_guard<std::mutex> pl(process_mu_);  // a running pass writes Intervals
     std::lock_guard<std::mutex> lk(mu_);
     std::vector<uint32_t> v;
-    for (uint32_t s = 0; s < ticket_.size(); s++)
-        if (live_[s] && cold_[s].node == node_) v.push_back(s);
-    auto* arr = new mm_ticket[v.empty() ? 1 : v.size()];
+    const int64_t me = node_dict_.find(node_);
+    for (uint32_t s = 0; s < nslots(); s++)
+        if (live_[s] && (int64_t)tnode_[s] == me) v.push_back(s);
+    // One block owned by the result: the ticket array, the presence and
+    // property arrays, then copies of the tickets' records and strings (the
+    // store may compact or grow before the caller frees the result).
+    size_t np = 0, nsp = 0, nnp = 0, bytes = 0;
+    for (uint32_t s : v) {
+        const ColdView c = cold_.view(s);
+        np += c.n_pres;
+        nsp += c.n_sp;
+        nnp += c.n_np;
+        bytes += cold_.record_bytes(s) + tk_len_[s] + 1 + node_dict_.str(tnode_[s]).size() + 1;
+    }
+    static_assert(sizeof(mm_ticket) % 8 == 0 && sizeof(mm_presence) % 8 == 0 && sizeof(mm_str_prop) % 8 == 0 &&
+                      sizeof(mm_num_prop) % 8 == 0,
+                  "extract block layout");
+    const size_t head = v.size() * sizeof(mm_ticket) + np * sizeof(mm_presence) + nsp * sizeof(mm_str_prop) +
+                        nnp * sizeof(mm_num_prop);
+    char* blob = new char[head + bytes + 1];
+    mm_ticket* T = reinterpret_cast<mm_ticket*>(blob);
+    mm_presence* P = reinterpret_cast<mm_presence*>(T + v.size());
+    mm_str_prop* SP = reinterpret_cast<mm_str_prop*>(P + np);
+    mm_num_prop* NP = reinterpret_cast<mm_num_prop*>(SP + nsp);
+    char* str = reinterpret_cast<char*>(NP + nnp);
+    auto copy = [&](std::string_view x) {
+        char* at = str;
+        if (!x.empty()) std::memcpy(at, x.data(), x.size());
+        at[x.size()] = 0;
+        str += x.size() + 1;
+        return (const char*)at;
+    };
     for (size_t i = 0; i < v.size(); i++) {
-        uint32_t s = v[i];
-        const Cold& c = cold_[s];
-        mm_ticket& t = arr[i];
-        t.ticket = ticket_[s].c_str();
-        t.session_id = c.session_id.c_str();
-        t.party_id = c.party_id.c_str();
-        t.query = c.query.c_str();
+        const uint32_t s = v[i];
+        const size_t rb = cold_.record_bytes(s);
+        std::memcpy(str, cold_.bytes.data() + cold_.off[s], rb);
+        const ColdView c = ColdStore::parse(str);  // strings in the record are NUL-terminated
+        str += rb;
+        mm_ticket& t = T[i];
+        t.ticket = copy(tk(s));
+        t.session_id = c.session_id.data();
+        t.party_id = c.party_id.data();
+        t.query = c.query.data();
         t.min_count = minc_[s];
         t.max_count = maxc_[s];
         t.count_multiple = cm_[s];
         t.intervals = intervals_[s];
         t.created_at = created_[s];
-        t.node = c.node.c_str();
-        auto* ps = new mm_presence[c.presences.empty() ? 1 : c.presences.size()];
-        for (size_t k = 0; k < c.presences.size(); k++)
-            ps[k] = {c.presences[k].user_id.c_str(), c.presences[k].session_id.c_str(),
-                     c.presences[k].username.c_str(), c.presences[k].node.c_str()};
-        t.presences = ps;
-        t.n_presences = (int32_t)c.presences.size();
-        auto* sp = new mm_str_prop[c.sprops.empty() ? 1 : c.sprops.size()];
-        for (size_t k = 0; k < c.sprops.size(); k++) sp[k] = {c.sprops[k].first.c_str(), c.sprops[k].second.c_str()};
-        t.str_props = sp;
-        t.n_str_props = (int32_t)c.sprops.size();
-        auto* np = new mm_num_prop[c.nprops.empty() ? 1 : c.nprops.size()];
-        for (size_t k = 0; k < c.nprops.size(); k++) np[k] = {c.nprops[k].first.c_str(), c.nprops[k].second};
-        t.num_props = np;
-        t.n_num_props = (int32_t)c.nprops.size();
+        t.node = copy(node_dict_.str(tnode_[s]));
+        t.presences = P;
+        t.n_presences = (int32_t)c.n_pres;
+        c.each_presence([&](std::string_view u, std::string_view se, std::string_view un, std::string_view nd) {
+            *P++ = mm_presence{u.data(), se.data(), un.data(), nd.data()};
+        });
+        t.str_props = SP;
+        t.n_str_props = (int32_t)c.n_sp;
+        t.num_props = NP;
+        t.n_num_props = (int32_t)c.n_np;
+        c.each_prop([&](std::string_view k, std::string_view val) { *SP++ = mm_str_prop{k.data(), val.data()}; },
+                    [&](std::string_view k, double d) { *NP++ = mm_num_prop{k.data(), d}; });
     }
     out->n = (int32_t)v.size();
-    out->tickets = arr;
+    out->tickets = T;
     return MM_OK;
 }
 
 void Core::free_extract(mm_extract_list* out) {
     if (!out || !out->tickets) return;
-    for (int i = 0; i < out->n; i++) {
-        delete[] out->tickets[i].presences;
-        delete[] out->tickets[i].str_props;
-        delete[] out->tickets[i].num_props;
-    }
-    delete[] out->tickets;
+    delete[] reinterpret_cast<const char*>(out->tickets);
     out->tickets = nullptr;
     out->n = 0;
 }
@@ -891,7 +943,9 @@ int Core::remove_session(const std::string& sid, const std::string& ticket) {
 }
 int Core::remove_session_locked(const std::string& sid, const std::string& ticket) {
     int64_t s = slot_of_ticket(ticket);
-    if (s < 0 || !cold_[s].party_id.empty() || cold_[s].session_id != sid) return MM_ERR_TICKET_NOT_FOUND;
+    if (s < 0) return MM_ERR_TICKET_NOT_FOUND;
+    const ColdView c = cold_.view((uint32_t)s);
+    if (!c.party_id.empty() || c.session_id != sid) return MM_ERR_TICKET_NOT_FOUND;
     kill_slot((uint32_t)s);
     return MM_OK;
 }
@@ -903,7 +957,7 @@ int Core::remove_session_all(const std::string& sid) {
     const int64_t id = sess_dict_.find(sid);
     if (id >= 0)
         for (uint32_t s : sess_slots_.list((uint32_t)id))
-            if (PendTk* t = eff_ticket(ticket_[s])) eff_remove(*t);
+            if (PendTk* t = eff_ticket(std::string(tk(s)))) eff_remove(*t);
     for (auto& kv : pend_tk_)
         if (kv.second.alive && std::find(kv.second.sessions.begin(), kv.second.sessions.end(), sid) != kv.second.sessions.end())
             eff_remove(kv.second);
@@ -929,7 +983,9 @@ int Core::remove_party(const std::string& pid, const std::string& ticket) {
 }
 int Core::remove_party_locked(const std::string& pid, const std::string& ticket) {
     int64_t s = slot_of_ticket(ticket);
-    if (s < 0 || !cold_[s].session_id.empty() || cold_[s].party_id != pid) return MM_ERR_TICKET_NOT_FOUND;
+    if (s < 0) return MM_ERR_TICKET_NOT_FOUND;
+    const ColdView c = cold_.view((uint32_t)s);
+    if (!c.session_id.empty() || c.party_id != pid) return MM_ERR_TICKET_NOT_FOUND;
     kill_slot((uint32_t)s);
     return MM_OK;
 }
@@ -942,7 +998,7 @@ int Core::remove_party_all(const std::string& pid) {
     const int64_t id = party_dict_.find(pid);
     if (id >= 0)
         for (uint32_t s : party_slots_.list((uint32_t)id))
-            if (PendTk* t = eff_ticket(ticket_[s])) eff_remove(*t);
+            if (PendTk* t = eff_ticket(std::string(tk(s)))) eff_remove(*t);
     for (auto& kv : pend_tk_)
         if (kv.second.alive && kv.second.party_id == pid) eff_remove(kv.second);
     pending_.push_back(PendingOp{P_REMOVE_PARTY_ALL, {}, {}, {}, pid, {}, {}});
@@ -959,17 +1015,19 @@ int Core::remove_party_all_locked(const std::string& pid) {
 int Core::remove_all(const std::string& node) {
     std::lock_guard<std::mutex> lk(mu_);
     if (!pass_running_) return remove_all_locked(node);
-    for (uint32_t s = 0; s < ticket_.size(); s++)
-        if (live_[s] && cold_[s].node == node)
-            if (PendTk* t = eff_ticket(ticket_[s])) eff_remove(*t);
+    const int64_t nid = node_dict_.find(node);
+    for (uint32_t s = 0; s < nslots(); s++)
+        if (live_[s] && (int64_t)tnode_[s] == nid)
+            if (PendTk* t = eff_ticket(std::string(tk(s)))) eff_remove(*t);
     for (auto& kv : pend_tk_)
         if (kv.second.alive && kv.second.node == node) eff_remove(kv.second);
     pending_.push_back(PendingOp{P_REMOVE_ALL, {}, {}, {}, node, {}, {}});
     return MM_OK;
 }
 int Core::remove_all_locked(const std::string& node) {
-    for (uint32_t s = 0; s < ticket_.size(); s++)
-        if (live_[s] && cold_[s].node == node) kill_slot(s);
+    const int64_t nid = node_dict_.find(node);
+    for (uint32_t s = 0; s < nslots(); s++)
+        if (live_[s] && (int64_t)tnode_[s] == nid) kill_slot(s);
     return MM_OK;
 }
 
@@ -1018,7 +1076,7 @@ void Core::set_hot(uint32_t s) {
 }
 
 void Core::maybe_compact() {
-    size_t n = ticket_.size();
+    size_t n = nslots();
     // a process result still held by the caller points into the string arena
     if (out_in_use_.load()) return;
     if (n >= 65536 && n > 2 * (size_t)n_live_) compact();
@@ -1026,8 +1084,11 @@ void Core::maybe_compact() {
 
 // Drops dead slots and renumbers the store (preserves relative slot order, so
 // the scan order stays sorted and insertion-order tie-breaks are unchanged).
+// The work is proportional to the slot count for the fixed-size columns and
+// to the live tickets for strings and dictionaries (a store whose tickets all
+// matched drops its arenas as a few blocks).
 void Core::compact() {
-    const size_t n = ticket_.size();
+    const size_t n = nslots();
     std::vector<uint32_t> remap(n, kNoSlot);
     uint32_t m = 0;
     for (uint32_t s = 0; s < n; s++)
@@ -1046,35 +1107,39 @@ void Core::compact() {
     for (uint32_t s = 0; s < n; s++) {
         if (!live_[s]) continue;
         for (uint32_t p = pres_off_[s]; p < pres_off_[s + 1]; p++)
-            npsess.push_back(nsess.intern(sess_dict_.str[pres_sess_[p]]));
+            npsess.push_back(nsess.intern(sess_dict_.str(pres_sess_[p])));
         npoff.push_back((uint32_t)npsess.size());
     }
     pres_off_ = std::move(npoff);
     pres_sess_ = std::move(npsess);
     sess_dict_ = std::move(nsess);
-    keep(ticket_); keep(created_); keep(ckey_); keep(minc_); keep(maxc_); keep(cm_); keep(count_);
-    keep(intervals_); keep(party_); keep(is_active_); keep(sig_); keep(cold_); keep(squery_); keep(indexed_);
+    // party dictionary: live parties only
+    {
+        Dict np;
+        for (uint32_t s = 0; s < n; s++)
+            if (live_[s] && party_[s] != kNoParty) party_[s] = np.intern(party_dict_.str(party_[s]));
+        party_dict_ = std::move(np);
+    }
+    // ticket-id arena: live ids only
+    {
+        StrArena na;
+        for (uint32_t s = 0; s < n; s++)
+            if (live_[s]) tk_ptr_[s] = na.put(tk(s));
+        tk_arena_ = std::move(na);
+    }
+    cold_.compact(live_);
+    keep(tk_ptr_); keep(tk_len_); keep(tnode_); keep(created_); keep(ckey_); keep(minc_); keep(maxc_); keep(cm_);
+    keep(count_); keep(intervals_); keep(party_); keep(is_active_); keep(sig_); keep(squery_); keep(indexed_);
     for (size_t f = 0; f < fval_.size(); f++) {
         if (fval_[f].size() == n) { keep(fval_[f]); keep(fkind_[f]); }
     }
     live_.assign(m, 1);
-    // party dictionary: live parties only
-    {
-        Dict np;
-        for (uint32_t s = 0; s < m; s++)
-            party_[s] = cold_[s].party_id.empty() ? kNoParty : np.intern(cold_[s].party_id);
-        party_dict_ = std::move(np);
-    }
     hot_.resize(m);
     for (uint32_t s = 0; s < m; s++) set_hot(s);
-    // string arena: live ticket ids only
-    tk_blocks_.clear();
-    tk_block_used_ = 0;
-    tk_ptr_.resize(m);
-    for (uint32_t s = 0; s < m; s++) tk_ptr_[s] = arena_string(ticket_[s]);
     // maps
     slot_of_.clear();
-    for (uint32_t s = 0; s < m; s++) slot_of_[ticket_[s]] = s;
+    slot_of_.reserve(m);
+    for (uint32_t s = 0; s < m; s++) slot_of_.put_new(str_hash(tk(s)), s);
     sess_slots_.clear();
     party_slots_.clear();
     for (uint32_t s = 0; s < m; s++) {
@@ -1113,7 +1178,7 @@ void Core::ensure_field_on_device(uint16_t f) {
 }
 
 void Core::build_index() {
-    const uint32_t n = (uint32_t)ticket_.size();
+    const uint32_t n = (uint32_t)nslots();
     // scan order: slots sorted by (sortable float64(CreatedAt), slot)
     if (!order_sorted_ || order_.size() != n) {
         order_.resize(n);
@@ -1163,7 +1228,7 @@ void Core::build_index() {
 
 void Core::sync_device() {
     NKM_HIP(hipSetDevice(device_));
-    const size_t n = ticket_.size();
+    const size_t n = nslots();
     const size_t need = std::max<size_t>(n, 1);
     bool regrow = need > dev_cap_;
     if (regrow) {

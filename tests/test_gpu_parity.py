@@ -49,7 +49,9 @@ def test_known_answer_gpu(sc):
 
 
 def state(mm):
-    return [(t.ticket, t.intervals) for t in mm.Extract()], mm.active_count()
+    """Post-pass store state: every extracted field of every ticket (sessions,
+    party, query, node, presences, properties, intervals) + the active count."""
+    return mm.Extract(), mm.active_count()
 
 
 # Oracle runs are memoised per workload: the kernel / host-path variants of a
@@ -319,6 +321,46 @@ def test_interleaved_mutations():
         orc.close()
         for s in sets:
             s.close()
+
+
+def test_store_compaction_extract_and_replace():
+    """Store maintenance at a size that compacts (>= 65,536 slots, over half
+    dead): bulk Insert, mass Remove, the compaction on the next Insert, ids
+    re-inserted within and across batches (replace), RemoveAll by node, and
+    the full Extract / pass results against the oracle after each step."""
+    gpu, orc = pair(dict(max_intervals=3, max_tickets=3))
+    big = synth.TicketSet(3, 70_000)
+    small = synth.TicketSet(6, 400, first=70_000)
+    try:
+        big.insert_into(gpu)
+        big.insert_into(orc)
+        assert gpu.ticket_count() == orc.ticket_count() == 70_000
+        keep = set(range(0, 70_000, 151))
+        victims = [big.ticket_id(k) for k in range(70_000) if k not in keep]
+        gpu.Remove(victims)
+        orc.Remove(victims)
+        small.insert_into(gpu)  # compacts: 70,400 slots, ~860 live
+        small.insert_into(orc)
+        assert state(gpu) == state(orc)
+        assert gpu.Process() == orc.Process()
+        assert state(gpu) == state(orc)
+        small.insert_into(gpu)  # every id again: replaced in place of the old slots
+        small.insert_into(orc)
+        assert gpu.ticket_count() == orc.ticket_count()
+        assert state(gpu) == state(orc)
+        assert gpu.Process() == orc.Process()
+        assert state(gpu) == state(orc)
+        nodes = sorted({t.node for t in gpu.Extract()})
+        if nodes:
+            gpu.RemoveAll(nodes[0])
+            orc.RemoveAll(nodes[0])
+        assert state(gpu) == state(orc)
+        assert gpu.Process() == orc.Process()
+    finally:
+        gpu.close()
+        orc.close()
+        big.close()
+        small.close()
 
 
 @pytest.mark.parametrize("config", [1, 2, 3, 5, 6])
