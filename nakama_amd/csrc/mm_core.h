@@ -607,6 +607,14 @@ public:
     std::vector<uint32_t> order_;
     bool full_var_mode_ = true;  // NKM_FULLVAR=0: variable-score searches always use the LDS top-K
     bool page_mode_ = true;  // NKM_PAGE=0: only a batch's first row pages a truncated list
+    // Batch window after a variable-score list ran out (NKM_WIN=0: off): the
+    // next batch takes twice the rows the last one decided (at least
+    // win_min_), not every remaining row, since its lists go stale at about
+    // the same depth; a batch that runs to its end doubles the window.
+    bool win_mode_ = true;
+    bool full_src_mode_ = true;  // NKM_FULLSRC=0: constant-score searches keep their row-count capacity
+    size_t win_min_ = 2048;   // NKM_WIN_MIN
+    uint32_t vark_min_ = 64;  // NKM_VARK_MIN: floor of a variable-score search's hit capacity
     bool order_sorted_ = true;
     bool index_dirty_ = true;
     uint32_t order_head_ = 0;

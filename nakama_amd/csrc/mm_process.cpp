@@ -311,6 +311,15 @@ struct Replay : ReplayCore {
                 full_var.push_back((uint32_t)lg.size());
                 stats.full_lists++;
             }
+            // A constant-score search over a source the batch can afford in
+            // full (a quarter of kOutCap for all promotions) returns its whole
+            // list: rows that walk far (a row that matches nothing walks all
+            // of it) then never page it one synchronous launch at a time.
+            if (w.path == 0 && !d.var_score && !rev && !d.has_cursor && d.k < d.src_len && c.full_src_mode_ &&
+                budget + (d.src_len - d.k) <= kOutCap / 4) {
+                budget += d.src_len - d.k;
+                w.k = d.src_len;
+            }
             w.out_off = off;
             off += w.k;
             lg.push_back(w);
@@ -1119,6 +1128,10 @@ int Core::process_default(GroupList& out_groups,
     const uint32_t kvar = (uint32_t)var_k_capacity();
     size_t pos = 0;
     uint32_t retry_slot = kNoSlot;
+    size_t win = SIZE_MAX;  // rows per batch (win_mode_)
+    // floor of a variable-score search's capacity: doubles (up to the top-K
+    // capacity) each time a batch ends on a list that ran out
+    uint32_t vfloor = vark_min_;
     while (order_head_ < order_.size() && !live_[order_[order_head_]]) order_head_++;
 
     while (true) {
@@ -1162,7 +1175,8 @@ int Core::process_default(GroupList& out_groups,
         // a search's hit capacity after `nrows` rows, the last with MaxCount m
         auto cap_k = [&](const BGroup& g, uint64_t nrows, int m) {
             const uint64_t want = nrows * (uint64_t)std::max(2, m) * 2 + 32;
-            const uint32_t k = g.d.var_score ? (uint32_t)std::min<uint64_t>(std::min<uint32_t>(kvar, std::max<uint32_t>(g.d.src_len, 1)), want)
+            const uint32_t k = g.d.var_score ? (uint32_t)std::min<uint64_t>(std::min<uint32_t>(kvar, std::max<uint32_t>(g.d.src_len, 1)),
+                                                                         std::max<uint64_t>(want, vfloor))
                                              : (uint32_t)std::min<uint64_t>(std::max<uint32_t>(g.d.src_len, 1), want + 224);
             return std::max<uint32_t>(k, 1);
         };
@@ -1174,7 +1188,8 @@ int Core::process_default(GroupList& out_groups,
         // total stays within kOutCap (so it would not have cut the batch).
         auto assemble_parallel = [&]() -> bool {
             const size_t nr = rows.size() - pos, nsig = sigs_.size();
-            if (rev || retry_slot != kNoSlot || !par_mode_ || nr < par_min(65536) || nr > kMaxBatchRows || nsig > 4096)
+            if (rev || retry_slot != kNoSlot || !par_mode_ || nr < par_min(65536) || nr > kMaxBatchRows || nsig > 4096 ||
+                nr > win)
                 return false;
             WorkPool& wp = workers();
             const unsigned nch = wp.size();
@@ -1245,7 +1260,8 @@ int Core::process_default(GroupList& out_groups,
         // workers (sources from a non-mutating lookup of the posting ranges)
         auto assemble_parallel_rev = [&]() -> bool {
             const size_t nr = rows.size() - pos;
-            if (!rev || retry_slot != kNoSlot || !par_mode_ || nr < par_min(65536) || nr > kMaxBatchRows) return false;
+            if (!rev || retry_slot != kNoSlot || !par_mode_ || nr < par_min(65536) || nr > kMaxBatchRows || nr > win)
+                return false;
             WorkPool& wp = workers();
             const unsigned nch = wp.size() * 4;
             std::vector<std::vector<BGroup>> cg(nch);
@@ -1301,7 +1317,7 @@ int Core::process_default(GroupList& out_groups,
             q = rows.size();
         } else if (!assemble_parallel()) {
             uint64_t total_k = 0;
-            for (; q < rows.size() && brow.size() < kMaxBatchRows; q++) {
+            for (; q < rows.size() && brow.size() < kMaxBatchRows && brow.size() < win; q++) {
                 const uint32_t r = rows[q];
                 if (sel[r]) continue;
                 int32_t gi = rev ? -1 : sig_group[sig_[r]];
@@ -1354,6 +1370,7 @@ int Core::process_default(GroupList& out_groups,
             stats.apply_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
             pos = q;
             retry_slot = kNoSlot;
+            if (win != SIZE_MAX) win *= 2;
             continue;
         }
         for (size_t bi = 0; bi < brow.size(); bi++) {
@@ -1392,11 +1409,13 @@ int Core::process_default(GroupList& out_groups,
         // advance past the rows this batch decided
         if (exhausted) {
             while (pos < rows.size() && rows[pos] != retry_slot) pos++;
+            if (win_mode_) win = std::max(win_min_, 2 * done);
+            vfloor = std::min<uint32_t>(kvar, 2 * vfloor);
         } else {
             pos = q;
             retry_slot = kNoSlot;
+            if (win != SIZE_MAX) win = win > SIZE_MAX / 2 ? SIZE_MAX : 2 * win;
         }
-        (void)done;
     }
     return MM_OK;
 }

@@ -93,6 +93,10 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_FAST")) fast_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FULLVAR")) full_var_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_PAGE")) page_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_WIN")) win_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_FULLSRC")) full_src_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_WIN_MIN")) win_min_ = (size_t)std::max(1L, std::atol(e));
+    if (const char* e = std::getenv("NKM_VARK_MIN")) vark_min_ = (uint32_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("NKM_KERNEL"))
         kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN
                      : !std::strcmp(e, "mscan") ? KM_MSCAN : KM_AUTO;

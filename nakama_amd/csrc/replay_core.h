@@ -120,6 +120,12 @@ struct ReplayCore {
     std::vector<std::vector<CE>> combos;  // pool: the first ncomb are this row's entryCombos
     std::vector<uint32_t> cmask;          // per combo: OR of its entries' session masks (a superset)
     size_t ncomb = 0;
+    // this row's combos that can still take an entry (size + T's count < MaxCount),
+    // in index order.  A combo changes only when a hit joins it, which needs
+    // room, so one that is full stays full: dropping it from the first-fit scan
+    // is exact, and a row whose hits can never share a combo (T's party fills
+    // MaxCount) scans nothing instead of every earlier hit's combo.
+    std::vector<uint32_t> open;
     uint64_t hits_seen = 0;  // profiling: hit-list entries the rows walked
     // pool-parallel replay: rows this worker processed earlier in the batch,
     // whose Intervals increments are applied after the batch (1 = one pending)
@@ -271,6 +277,7 @@ struct ReplayCore {
         const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
         const uint32_t tparty = ht.party;
         ncomb = 0;
+        open.clear();
         while (g.head < g.n && sel[g.hits[g.head].slot]) g.head++;
         for (uint32_t i = g.head;; i++) {
             if (i >= g.n) {
@@ -296,8 +303,12 @@ struct ReplayCore {
             int found = -1;
             const int hcount = hh.count;
             const uint32_t hp = hh.pres_off;
-            for (size_t ci = 0; ci < ncomb; ci++) {
+            size_t w = 0, r = 0;  // first fit over the open combos, dropping full ones on the way
+            for (; r < open.size(); r++) {
+                const uint32_t ci = open[r];
                 auto& combo = combos[ci];
+                if ((int)combo.size() + tcount >= tmax) continue;  // full for good
+                open[w++] = ci;
                 if ((int)combo.size() + hcount + tcount <= tmax) {
                     bool mconf = false;
                     const bool may_share = !v.sessions_exclusive && (cmask[ci] & hh.smask) != 0;
@@ -313,9 +324,12 @@ struct ReplayCore {
                         combo.push_back(CE{H, (uint32_t)k, i, hcount == 1 ? hh.sess0 : v.pres_sess[hp + k]});
                     cmask[ci] |= hh.smask;
                     found = (int)ci;
+                    r++;
                     break;
                 }
             }
+            for (; r < open.size(); r++) open[w++] = open[r];
+            open.resize(w);
             if (found < 0) {
                 if (ncomb == combos.size()) {
                     combos.emplace_back();
@@ -326,6 +340,7 @@ struct ReplayCore {
                 for (int k = 0; k < hcount; k++) nc.push_back(CE{H, (uint32_t)k, i, hcount == 1 ? hh.sess0 : v.pres_sess[hp + k]});
                 cmask[ncomb] = hh.smask;
                 found = (int)ncomb++;
+                if (hcount + tcount < tmax) open.push_back((uint32_t)found);
             }
             std::vector<CE>& fc = combos[found];
             int l = (int)fc.size() + tcount;
@@ -357,6 +372,9 @@ struct ReplayCore {
                     }
                 }
                 l = (int)fc.size() + tcount;
+                // a combo created full may have room again: back into the scan, in index order
+                if (l < tmax && std::find(open.begin(), open.end(), (uint32_t)found) == open.end())
+                    open.insert(std::lower_bound(open.begin(), open.end(), (uint32_t)found), (uint32_t)found);
                 if (l % tcm != 0) continue;
             }
             bool failed = false;                                                           // :287-296
@@ -501,6 +519,7 @@ struct DenseRun {
     // scratch
     std::vector<std::vector<CE>> combos;
     std::vector<uint32_t> cmask;
+    std::vector<uint32_t> open;  // combos with room (ReplayCore::open)
     std::vector<std::pair<uint32_t, int>> grp;
     FastCombos fcb;
     bool fast = true;  // fast_step() for the rows it covers (NKM_FAST=0: step() only)
@@ -546,6 +565,7 @@ struct DenseRun {
             return false;
         };
         size_t ncomb = 0;
+        open.clear();  // combos with room (see ReplayCore::open)
         while (head < n && sel[head]) head++;
         bool matched = false;
         for (uint32_t i = head; i < n; i++) {
@@ -564,8 +584,12 @@ struct DenseRun {
             bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
             int found = -1;
             const int hcount = hh.count;
-            for (size_t ci = 0; ci < ncomb; ci++) {
+            size_t w = 0, r = 0;
+            for (; r < open.size(); r++) {
+                const uint32_t ci = open[r];
                 auto& combo = combos[ci];
+                if ((int)combo.size() + tcount >= tmax) continue;  // full for good
+                open[w++] = ci;
                 if ((int)combo.size() + hcount + tcount <= tmax) {
                     if (!v.sessions_exclusive && (cmask[ci] & hh.smask))
                         for (const CE& e : combo)
@@ -575,9 +599,12 @@ struct DenseRun {
                         combo.push_back(CE{P.slot[i], (uint32_t)k, i, hcount == 1 ? hh.sess0 : v.pres_sess[hh.pres_off + k]});
                     cmask[ci] |= hh.smask;
                     found = (int)ci;
+                    r++;
                     break;
                 }
             }
+            for (; r < open.size(); r++) open[w++] = open[r];
+            open.resize(w);
             if (found < 0) {
                 if (ncomb == combos.size()) {
                     combos.emplace_back();
@@ -589,6 +616,7 @@ struct DenseRun {
                     nc.push_back(CE{P.slot[i], (uint32_t)k, i, hcount == 1 ? hh.sess0 : v.pres_sess[hh.pres_off + k]});
                 cmask[ncomb] = hh.smask;
                 found = (int)ncomb++;
+                if (hcount + tcount < tmax) open.push_back((uint32_t)found);
             }
             std::vector<CE>& fc = combos[found];
             int l = (int)fc.size() + tcount;
@@ -621,6 +649,8 @@ struct DenseRun {
                     }
                 }
                 l = (int)fc.size() + tcount;
+                if (l < tmax && std::find(open.begin(), open.end(), (uint32_t)found) == open.end())
+                    open.insert(std::lower_bound(open.begin(), open.end(), (uint32_t)found), (uint32_t)found);
                 if (l % tcm != 0) continue;
             }
             bool failed = false;                                                         // :287-296
