@@ -48,7 +48,7 @@ WORKLOADS = {
     2: "C2: skill-window range queries with ^boost, 1v1",
     3: "C3: 1M tickets/GPU, 5v5 (Min=Max=10, CountMultiple=5), party tickets, 8 pools/GPU",
     4: "C4: solo 1v1, 4M tickets over 64 mode x region pools (in total)",
-    5: "C5: RevPrecision, buckets of 8, Min=2 Max=4 (processDefault; no override registered), 1M in total",
+    5: "C5: RevPrecision, buckets of 8, Min=2 Max=4, 1M in total",
     7: "C7: regexp / wildcard / fuzzy clauses (blocked lists, alternations, fuzzy map names)",
 }
 # the query fields a pool is keyed on (the cluster front's routing)
@@ -68,6 +68,9 @@ def parse():
                     help="tickets per GPU per step (C3), or in total (C4, C5); default 1M (C4: 4M)")
     ap.add_argument("--cpu-rows", type=int, default=24, help="active rows in the CPU-baseline prefix sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--override", action="store_true",
+                    help="register a MatchmakerOverride (processCustom path): the timed step is the candidate pass, "
+                         "a native first-disjoint override and mm_process_commit (single GPU)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_traffic.json"))
     a = ap.parse_args()
     if a.tickets is None:
@@ -208,7 +211,11 @@ def main():
     import torch
 
     # SURVEY 8(d) harness pins: MaxIntervals=2, RevThreshold=0 (no wall-clock cutoff)
-    mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config == 5, rev_threshold=0)
+    if args.override and world > 1:
+        raise SystemExit("--override runs on one GPU (the cluster front merges processDefault groups)")
+    from nakama_amd import synth
+    mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config == 5, rev_threshold=0,
+                                    override=(lambda groups: groups) if args.override else None)
     cm = None
     if world > 1:
         from nakama_amd import cluster
@@ -230,6 +237,8 @@ def main():
         t0 = time.perf_counter()
         if cm is None:
             out = mm.process_call()  # the C-ABI call: one whole Process() pass
+            if args.override and out.is_candidates:  # processCustom: override + commit, in the timed step
+                out = synth.override_commit(mm, out)
         else:
             cp = cm.Process()        # every rank's pass + the merge into the reference's group order
         barrier_sync(pg, local)
@@ -303,7 +312,10 @@ def main():
         "vs_baseline": None,
         "dtype": "int64/f64",
         "data": "synthetic",
-        "config": {"workload": WORKLOADS.get(args.config, str(args.config)),
+        "config": {"workload": WORKLOADS.get(args.config, str(args.config)) +
+                               (" + MatchmakerOverride (processCustom candidates, native first-disjoint override, "
+                                "mm_process_commit)" if args.override else
+                                " (processDefault: no override registered)" if args.config == 5 else ""),
                    ("tickets_total" if strong else "tickets_per_gpu"): args.tickets,
                    "max_intervals": 2, "parallelism": par, "unroutable": unroutable,
                    "matched_per_step": sum(matched_all) / args.steps, "batches_per_pass_rank0": batches,

@@ -1445,45 +1445,73 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
         const size_t end = std::min(rows.size(), base + kMaxBatchRows / 4);
         if (rev && (row_shard() ? shard_any(timer.check()) : timer.check())) rev = rp.rev = false;
         std::vector<BGroup> bg(end - base);
-        uint64_t off = 0;
-        h_groups_.reserve(bg.size());
-        for (size_t i = 0; i < bg.size(); i++) {
-            const uint32_t r = rows[base + i];
-            BGroup& g = bg[i];
-            g.sig = sig_[r];
-            const Sig& s = sigs_[g.sig];
-            g.n_fields = s.n_fields;
-            g.d.clause_off = s.clause_off;
-            g.d.n_clauses = s.n_clauses;
-            g.d.qkind = s.qkind;
-            g.d.var_score = s.var_score ? 1 : 0;
-            g.d.tmin = s.tmin;
-            g.d.tmax = s.tmax;
-            g.d.tparty = s.tparty;
-            g.d.rev_slot = rev ? r : kNoSlot;
-            g.d.ub_key = s.ub_key;
-            choose_source(s, g.d);
-            g.d.k = g.d.var_score ? std::min<uint32_t>(kvar, std::max<uint32_t>(g.d.src_len, 1))
-                                   : std::min<uint32_t>(std::max<uint32_t>(g.d.src_len, 1), 128);
-            g.d.out_off = off;
-            off += g.d.k;
-            g.row_slot = r;
-            h_groups_.p[i] = g.d;
+        // the rows' searches (built on the workers for large chunks: the
+        // sources from the non-mutating posting lookup)
+        auto build = [&](size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; i++) {
+                const uint32_t r = rows[base + i];
+                BGroup& g = bg[i];
+                g.sig = sig_[r];
+                const Sig& s = sigs_[g.sig];
+                g.n_fields = s.n_fields;
+                g.d.clause_off = s.clause_off;
+                g.d.n_clauses = s.n_clauses;
+                g.d.qkind = s.qkind;
+                g.d.var_score = s.var_score ? 1 : 0;
+                g.d.tmin = s.tmin;
+                g.d.tmax = s.tmax;
+                g.d.tparty = s.tparty;
+                g.d.rev_slot = rev ? r : kNoSlot;
+                g.d.ub_key = s.ub_key;
+                source_of(s, g.d);
+                g.d.k = g.d.var_score ? std::min<uint32_t>(kvar, std::max<uint32_t>(g.d.src_len, 1))
+                                       : std::min<uint32_t>(std::max<uint32_t>(g.d.src_len, 1), 128);
+                g.row_slot = r;
+            }
+        };
+        const bool par = par_mode_ && bg.size() >= par_min(4096);
+        const auto tc0 = std::chrono::steady_clock::now();
+        if (par) {
+            WorkPool& wp = workers();
+            const size_t nch = (size_t)wp.size() * 4;
+            wp.run(nch, [&](size_t c) { build(bg.size() * c / nch, bg.size() * (c + 1) / nch); });
+        } else {
+            build(0, bg.size());
         }
-        (void)off;
+        const auto tc1 = std::chrono::steady_clock::now();
         rp.run_batch(bg, rev);
-        for (size_t i = 0; i < bg.size(); i++) {
+        const auto tc2 = std::chrono::steady_clock::now();
+        stats.assemble_ms += std::chrono::duration<double, std::milli>(tc1 - tc0).count();
+        stats.search_ms += std::chrono::duration<double, std::milli>(tc2 - tc1).count();
+        // Every row is independent (processCustom selects nothing): chunks of
+        // rows run on the workers into their own candidate lists, appended in
+        // row order — unless a RevThreshold timer that may still fire is read
+        // per row.  Device round trips (pages past a truncated list, pair
+        // checks past the pair matrix) take turns on the stream.
+        std::mutex dev_mu;
+        struct Scratch {
+            std::vector<uint32_t> hits, hpos, combo, sess_seen, pq, pr;
+            std::vector<uint64_t> pm;
+            std::vector<uint8_t> po;
+            std::vector<std::pair<uint32_t, int>> me;
+        };
+        auto do_row = [&](size_t i, GroupList& out, Scratch& sc, bool row_rev) {
             BGroup& g = bg[i];
             const uint32_t T = g.row_slot;
-            if (rev && !row_shard() && timer.check()) rev = rp.rev = false;  // :353-358
             // all hits (paging through the list), filtered as :425-468
-            std::vector<uint32_t> hits, hpos;
+            std::vector<uint32_t>& hits = sc.hits;
+            std::vector<uint32_t>& hpos = sc.hpos;
+            hits.clear();
+            hpos.clear();
             uint32_t j = 0;
             bool too_many = false;
             for (;; j++) {
                 if (j >= g.n) {
                     if (g.complete) break;
-                    rp.fetch_more(g);
+                    {
+                        std::lock_guard<std::mutex> lk(dev_mu);
+                        rp.fetch_more(g);
+                    }
                     if (j >= g.n) break;
                 }
                 const uint32_t H = g.hits[j].slot;
@@ -1491,7 +1519,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                 // a ticket an earlier processCustom pass retired is still in
                 // the search index, but not in indexesCopy: "missing index" (:432-437)
                 if (!live_[H]) continue;
-                if (rev && !g.rev[j]) continue;
+                if (row_rev && !g.rev[j]) continue;
                 if (maxc_[T] < maxc_[H] && intervals_[H] <= maxI) continue;
                 if (rp.share_session(T, H)) continue;
                 hits.push_back(H);
@@ -1499,38 +1527,43 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                 if (hits.size() >= 63) { too_many = true; break; }
             }
             // combineIndexes: Go's `1 << length` is 0 / negative for length >= 63 -> no subsets
-            if (too_many) continue;
+            if (too_many) return;
             const size_t L = hits.size();
             const int cmin = minc_[T] - count_[T], cmax = maxc_[T] - count_[T];
-            if (L == 0 || cmax <= 0) continue;  // every subset holds >= 1 ticket > max: none emitted
+            if (L == 0 || cmax <= 0) return;  // every subset holds >= 1 ticket > max: none emitted
             // pairwise reverse checks among the hits (validateMatch both ways, incl. self)
-            std::vector<uint64_t> pm;
+            std::vector<uint64_t>& pm = sc.pm;
+            pm.clear();
             bool covered = g.pm != nullptr;
             for (size_t a = 0; a < L && covered; a++) covered = hpos[a] < g.pm_n;
-            if (rev && L && covered) {  // from the batch's pair matrices
+            if (row_rev && covered) {  // from the batch's pair matrices
                 pm.assign(L, 0);
                 for (size_t a = 0; a < L; a++)
                     for (size_t b = 0; b < L; b++)
                         if ((g.pm[hpos[a]] >> hpos[b]) & 1u) pm[a] |= 1ull << b;
-            } else if (rev && L) {
-                std::vector<uint32_t> pr;
+            } else if (row_rev) {
+                std::vector<uint32_t>& pr = sc.pr;
+                pr.clear();
                 for (size_t a = 0; a < L; a++)
                     for (size_t b = 0; b < L; b++) { pr.push_back(hits[a]); pr.push_back(hits[b]); }
-                d_slots_tmp_.reserve(pr.size(), false);
-                d_pair_out_.reserve(L * L, false);
-                NKM_HIP(hipMemcpyAsync(d_slots_tmp_.p, pr.data(), pr.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                                       stream_));
-                NKM_HIP(launch_pairs(st, d_slots_tmp_.p, (uint32_t)(L * L), d_pair_out_.p, stream_));
-                std::vector<uint8_t> po(L * L);
-                NKM_HIP(hipMemcpyAsync(po.data(), d_pair_out_.p, L * L, hipMemcpyDeviceToHost, stream_));
-                NKM_HIP(hipStreamSynchronize(stream_));
+                sc.po.assign(L * L, 0);
+                {
+                    std::lock_guard<std::mutex> lk(dev_mu);
+                    d_slots_tmp_.reserve(pr.size(), false);
+                    d_pair_out_.reserve(L * L, false);
+                    NKM_HIP(hipMemcpyAsync(d_slots_tmp_.p, pr.data(), pr.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                           stream_));
+                    NKM_HIP(launch_pairs(st, d_slots_tmp_.p, (uint32_t)(L * L), d_pair_out_.p, stream_));
+                    NKM_HIP(hipMemcpyAsync(sc.po.data(), d_pair_out_.p, L * L, hipMemcpyDeviceToHost, stream_));
+                    NKM_HIP(hipStreamSynchronize(stream_));
+                }
                 pm.assign(L, 0);
                 for (size_t a = 0; a < L; a++)
                     for (size_t b = 0; b < L; b++)
-                        if (po[a * L + b]) pm[a] |= 1ull << b;
+                        if (sc.po[a * L + b]) pm[a] |= 1ull << b;
             }
             const uint64_t limit = 1ull << L;
-            std::vector<uint32_t> combo;
+            std::vector<uint32_t>& combo = sc.combo;
             // combineIndexes' ascending bitmask loop (:586-610), visiting only
             // the masks its `count > max` test lets through (next_mask_le)
             for (uint64_t bits = next_mask_le(1, cmax); bits < limit; bits = next_mask_le(bits + 1, cmax)) {
@@ -1557,8 +1590,10 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                 if (reject) continue;
                 // session conflicts across the combo; mutual checks between its hits
                 bool conflict = false;
-                std::vector<uint32_t> sess_seen;
-                std::vector<uint32_t> pq;  // hits whose query is already in parsedQueries
+                std::vector<uint32_t>& sess_seen = sc.sess_seen;
+                std::vector<uint32_t>& pq = sc.pq;  // hits whose query is already in parsedQueries
+                sess_seen.clear();
+                pq.clear();
                 for (uint32_t el : combo) {
                     const uint32_t h = hits[el];
                     for (uint32_t p = pres_off_[h]; p < pres_off_[h + 1] && !conflict; p++) {
@@ -1568,7 +1603,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                         const uint32_t sid = pres_sess_[p];
                         if (std::find(sess_seen.begin(), sess_seen.end(), sid) != sess_seen.end()) { conflict = true; break; }
                         sess_seen.push_back(sid);
-                        if (rev) {
+                        if (row_rev) {
                             for (uint32_t o : pq) {
                                 if (!((pm[el] >> o) & 1ull) || !((pm[o] >> el) & 1ull)) { conflict = true; break; }
                             }
@@ -1579,13 +1614,39 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                     if (conflict) break;
                 }
                 if (conflict) continue;
-                std::vector<std::pair<uint32_t, int>> me;
+                std::vector<std::pair<uint32_t, int>>& me = sc.me;
+                me.clear();
                 for (uint32_t el : combo)
                     for (int k = 0; k < count_[hits[el]]; k++) me.push_back({hits[el], k});
                 for (int k = 0; k < count_[T]; k++) me.push_back({T, k});
-                cands.push(me);
+                out.push(me);
+            }
+        };
+        const bool timer_live = rev && !row_shard() && timer.armed && !timer.fired;
+        if (par && !timer_live) {
+            WorkPool& wp = workers();
+            const size_t nch = (size_t)wp.size() * 4;
+            std::vector<GroupList> outs(nch);
+            wp.run(nch, [&](size_t c) {
+                Scratch sc;
+                for (size_t i = bg.size() * c / nch; i < bg.size() * (c + 1) / nch; i++) do_row(i, outs[c], sc, rev);
+            });
+            size_t ng = 0, ne = 0;
+            for (auto& o : outs) ng += o.size(), ne += o.ents.size();
+            cands.reserve_more(ng, ne);
+            for (auto& o : outs) {
+                const uint32_t e0 = (uint32_t)cands.ents.size();
+                cands.ents.insert(cands.ents.end(), o.ents.begin(), o.ents.end());
+                for (size_t g = 1; g < o.off.size(); g++) cands.off.push_back(e0 + o.off[g]);
+            }
+        } else {
+            Scratch sc;
+            for (size_t i = 0; i < bg.size(); i++) {
+                if (rev && !row_shard() && timer.check()) rev = rp.rev = false;  // :353-358
+                do_row(i, cands, sc, rev);
             }
         }
+        stats.replay_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc2).count();
     }
     return MM_OK;
 }
@@ -1821,8 +1882,10 @@ int Core::process(mm_matched* out) {
         if (pass_hook_) pass_hook_(pass_hook_ctx_);
     };
     if (cfg_.override_enabled) {
+        const auto t1 = std::chrono::steady_clock::now();
         process_custom(groups, expired, stats);
         hook();
+        const auto t2 = std::chrono::steady_clock::now();
         lk.lock();
         out->n_expired = (int32_t)expired.size();
         if (groups.empty()) {
@@ -1837,6 +1900,14 @@ int Core::process(mm_matched* out) {
             custom_open_ = true;
             custom_expired_ = expired;
             fill_matched(groups, out, true);
+        }
+        if (std::getenv("NKM_PROFILE")) {
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            std::fprintf(stderr,
+                         "[nkm] custom: sync %.2f ms | pass %.2f ms (build %.2f, search %.2f ms [kernel %.2f ms], "
+                         "combos %.2f ms, %d refetches) | candidates %zu (%zu entries) | fill %.2f ms\n",
+                         ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms(), stats.replay_ms,
+                         stats.refetches, groups.size(), groups.ents.size(), ms(t2, std::chrono::steady_clock::now()));
         }
     } else {
         const auto t1 = std::chrono::steady_clock::now();
@@ -1880,6 +1951,7 @@ int Core::process(mm_matched* out) {
 
 int Core::process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t n_groups, mm_matched* out) {
     std::memset(out, 0, sizeof(*out));
+    const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> pl(process_mu_);
     std::lock_guard<std::mutex> lk(mu_);
     if (!custom_open_) return MM_ERR_STATE;
@@ -1898,12 +1970,19 @@ int Core::process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t 
     // processCustom never deletes from the index during the pass; matched
     // tickets leave it here (their zombie documents would be filtered as
     // "missing index" by later passes, matchmaker_process.go:432-437).
+    const auto t1 = std::chrono::steady_clock::now();
     std::vector<uint32_t> exp = custom_expired_;
     finish_pass(exp, groups, false);
     custom_open_ = false;
     pass_running_ = false;
     custom_expired_.clear();
+    const auto t2 = std::chrono::steady_clock::now();
     fill_matched(groups, out, false);
+    if (std::getenv("NKM_PROFILE")) {
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "[nkm] commit: %d groups | lookup %.2f ms | finish %.2f ms | fill %.2f ms\n", n_groups,
+                     ms(t0, t1), ms(t1, t2), ms(t2, std::chrono::steady_clock::now()));
+    }
     return MM_OK;
 }
 

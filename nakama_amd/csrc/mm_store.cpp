@@ -360,6 +360,19 @@ void Core::refresh_termsets() {
     tsets_dirty_ = false;
 }
 
+// Identity of a signature: query kind, the searching ticket's filters and the
+// compiled clauses (field / term ids, bounds, boosts).
+static std::string sig_key(uint8_t kind, int32_t mn, int32_t mx, uint32_t party, const DClause* dc, size_t n) {
+    std::string key;
+    key.reserve(16 + n * sizeof(DClause));
+    key.push_back((char)kind);
+    key.append((const char*)&mn, 4);
+    key.append((const char*)&mx, 4);
+    key.append((const char*)&party, 4);
+    if (n) key.append((const char*)dc, n * sizeof(DClause));
+    return key;
+}
+
 // Assigns (or reuses) the compiled signature of a ticket's search.
 uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party) {
     std::vector<DClause> dc;
@@ -384,13 +397,7 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
     bool fuzzy = false;
     for (auto& c : cq.clauses)
         if (c.op == OP_TERMSET && c.mt_kind == TermMatcher::K_FUZZY && c.occur != OCC_MUSTNOT) fuzzy = true;
-    std::string key;
-    key.reserve(16 + dc.size() * sizeof(DClause));
-    key.push_back((char)cq.kind);
-    key.append((const char*)&mn, 4);
-    key.append((const char*)&mx, 4);
-    key.append((const char*)&party, 4);
-    if (!dc.empty()) key.append((const char*)dc.data(), dc.size() * sizeof(DClause));
+    std::string key = sig_key(cq.kind, mn, mx, party, dc.data(), dc.size());
     auto it = sig_index_.find(key);
     if (it != sig_index_.end()) return it->second;
 
@@ -1154,6 +1161,40 @@ void Core::compact() {
             if (!dup) sess_slots_.add(pres_sess_[p], s);
         }
         if (party_[s] != kNoParty) party_slots_.add(party_[s], s);
+    }
+    // signatures and clauses: the live tickets' only (a workload of unique
+    // queries would grow them without bound); renumbered in slot order
+    {
+        std::vector<uint32_t> smap(sigs_.size(), UINT32_MAX);
+        std::vector<Sig> ns;
+        std::vector<DClause> nc;
+        for (uint32_t s = 0; s < m; s++) {
+            uint32_t& g = sig_[s];
+            if (smap[g] == UINT32_MAX) {
+                smap[g] = (uint32_t)ns.size();
+                Sig x = sigs_[g];
+                const uint32_t off = (uint32_t)nc.size();
+                nc.insert(nc.end(), clauses_.begin() + x.clause_off, clauses_.begin() + x.clause_off + x.n_clauses);
+                x.clause_off = off;
+                ns.push_back(std::move(x));
+            }
+            g = smap[g];
+            squery_[s].clause_off = ns[g].clause_off;
+        }
+        std::unordered_map<std::string, uint32_t> nidx;
+        nidx.reserve(ns.size());
+        for (uint32_t g = 0; g < ns.size(); g++)
+            nidx.emplace(sig_key(ns[g].qkind, ns[g].tmin, ns[g].tmax, ns[g].tparty, nc.data() + ns[g].clause_off,
+                                 ns[g].n_clauses),
+                         g);
+        sigs_.swap(ns);
+        clauses_.swap(nc);
+        sig_index_.swap(nidx);
+        dev_clauses_ = 0;
+        qtext_.clear();  // the (query, counts) -> signature cache holds old ids
+        qstatus_.clear();
+        qsig_.clear();
+        qsig_idx_.clear();
     }
     std::vector<uint32_t> nact;
     for (uint32_t s : active_list_)

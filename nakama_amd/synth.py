@@ -42,6 +42,9 @@ def lib():
         _lib.synth_pool_of.argtypes = [C.c_int, C.c_uint64, C.c_uint64]
         _lib.synth_make_scaled.restype = C.c_void_p
         _lib.synth_make_scaled.argtypes = [C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int]
+        _lib.synth_override_first_disjoint.restype = C.c_int32
+        _lib.synth_override_first_disjoint.argtypes = [C.POINTER(C.c_int32), C.POINTER(capi.mm_entry_ref), C.c_int32,
+                                                       C.POINTER(C.c_int32), C.POINTER(capi.mm_entry_ref)]
     return _lib
 
 
@@ -102,3 +105,21 @@ class TicketSet:
             self.close()
         except Exception:
             pass
+
+
+def override_commit(mm: "capi.Matchmaker", out) -> "capi.mm_matched":
+    """The bench's override step on a candidate result `out` (freed here): the
+    native first-disjoint override (tools/synth.cpp) picks groups, and
+    mm_process_commit hands them back.  Returns the commit's result (free it
+    with the library's mm_free_matched)."""
+    n = out.n_groups
+    ne = out.n_entries
+    offs = (C.c_int32 * (n + 1))()
+    ents = (capi.mm_entry_ref * max(1, ne))()
+    kept = lib().synth_override_first_disjoint(out.group_offsets, out.entries, n, offs, ents)
+    res = capi.mm_matched()
+    try:  # the kept entries point into the candidate result: it goes back after the commit
+        mm._check(mm.lib.mm_process_commit(mm.h, offs, ents, kept, C.byref(res)))
+    finally:
+        mm.lib.mm_free_matched(mm.h, C.byref(out))
+    return res

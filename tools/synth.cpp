@@ -11,7 +11,9 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <string_view>
 #include <deque>
+#include <unordered_set>
 #include <vector>
 
 #include "../include/nakama_mm.h"
@@ -368,5 +370,30 @@ const mm_ticket* synth_tickets(void* h) { return static_cast<Synth*>(h)->t.data(
 int64_t synth_count(void* h) { return (int64_t)static_cast<Synth*>(h)->t.size(); }
 int64_t synth_presences(void* h) { return (int64_t)static_cast<Synth*>(h)->pres.size(); }
 void synth_free(void* h) { delete static_cast<Synth*>(h); }
+
+// The bench's MatchmakerOverride (a RuntimeMatchmakerOverrideFunction,
+// server/runtime.go:212, stands in for user code): keeps every candidate group
+// none of whose tickets an earlier kept group holds, in candidate order.
+// Tickets are told apart by their ids' text.  Writes the kept groups'
+// offsets (n_kept + 1) and entries into the caller's arrays (sized like the
+// candidates'); returns the number of kept groups.
+int32_t synth_override_first_disjoint(const int32_t* offs, const mm_entry_ref* ents, int32_t n_groups,
+                                      int32_t* out_offs, mm_entry_ref* out_ents) {
+    std::unordered_set<std::string_view> taken;
+    taken.reserve((size_t)(n_groups > 0 ? offs[n_groups] : 0));
+    int32_t kept = 0, e = 0;
+    out_offs[0] = 0;
+    for (int32_t g = 0; g < n_groups; g++) {
+        bool free = true;
+        for (int32_t k = offs[g]; k < offs[g + 1] && free; k++) free = !taken.count(ents[k].ticket);
+        if (!free) continue;
+        for (int32_t k = offs[g]; k < offs[g + 1]; k++) {
+            taken.insert(ents[k].ticket);
+            out_ents[e++] = ents[k];
+        }
+        out_offs[++kept] = e;
+    }
+    return kept;
+}
 
 }  // extern "C"
