@@ -50,7 +50,7 @@ hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResul
                          int n_searches, uint32_t* d_offs, const DHit* d_scratch, DHit* d_out, hipStream_t stream);
 int scan_chunk_len();
 // gen: some signature is not term-only (the clause-loop instantiation)
-hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, DHit* d_scratch,
+hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, uint32_t* d_scratch,
                         DGroupResult* d_cres, bool gen, hipStream_t stream, hipEvent_t ev0 = nullptr,
                         hipEvent_t ev1 = nullptr);
 int mscan_chunk_len(uint32_t n_sigs);

@@ -120,7 +120,7 @@ struct DChunkMap {
     uint32_t first;    // result index of the search's first chunk
     uint32_t start;    // chunk's first source position within the search
     uint32_t cap;      // the search's output capacity (k)
-    uint32_t pad;
+    uint32_t u32;      // 1: the cell and the output hold 4-B slot ids (mscan), `so` / dst in slot words
     uint64_t dst_off;  // the search's first output entry
     uint64_t so;       // the chunk's compacted hits in the scratch buffer
 };

@@ -412,7 +412,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 // GEN: some signature is not term-only (the clause loop is compiled in).
 template <int NF, bool GEN, int kMJ>
 __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, const DMSig* __restrict__ sigs,
-                                                       const DClause* __restrict__ mcl, DHit* __restrict__ out,
+                                                       const DClause* __restrict__ mcl, uint32_t* __restrict__ out,
                                                        DGroupResult* __restrict__ res) {
     static_assert(kMJ == 2 || kMJ == 4 || kMJ == 8, "2, 4 or 8 candidates per lane");
     constexpr int kMChunk = kMJ * kBlock;
@@ -421,7 +421,6 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     __shared__ uint32_t wcnt[kNSig][kMJ][kWaves];   // hits per (signature, j, wave); then exclusive prefixes
     __shared__ uint64_t wmask[kNSig][kMJ][kWaves];  // their ballots
     __shared__ uint32_t qtot[kMaxMSig];
-    __shared__ int64_t lkey[kMaxMSig];
     __shared__ uint32_t wlive[kWaves];
     const uint32_t c = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -429,9 +428,8 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     const uint32_t base = c * (uint32_t)kMChunk;
     const uint32_t len = ms.src_len - base < (uint32_t)kMChunk ? ms.src_len - base : (uint32_t)kMChunk;
     const uint32_t* __restrict__ src = st.order + ms.src_off + base;
-    // a term-only signature's hits all carry its precomputed key; the others
-    // write theirs in phase 1 (disjoint signatures: no race)
-    if ((uint32_t)tid < nq && sigs[tid].term_only) lkey[tid] = sigs[tid].key;
+    // hits are 4-B slot ids: an mscan search is constant-score and never cut,
+    // so its list needs neither score keys nor source positions
     uint32_t s[kMJ];
     bool a[kMJ];
     int32_t mn[kMJ], mx[kMJ];
@@ -528,17 +526,11 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
                     }
                 }
             }
-            bool any = false;
 #pragma unroll
-            for (int j = 0; j < kMJ; j++) {
-                double sp = 1.0;
-                if (g.qkind != QK_MATCHALL && (has_must || has_should)) {
-                    if (!has_must) { sp = ssc[j]; m[j] = m[j] && anys[j]; }
-                    else sp = anys[j] ? msc[j] + ssc[j] : msc[j];
-                }
-                // a constant-score signature: every hit has the same key
-                if (m[j] && !any) { lkey[q] = dsortable((sp + 1.0) + 1.0); any = true; }
-            }
+            for (int j = 0; j < kMJ; j++)  // a query of SHOULD clauses only: one of them must hit
+                if (g.qkind != QK_MATCHALL && !has_must && has_should) m[j] = m[j] && anys[j];
+            (void)msc;
+            (void)ssc;
         }
 #pragma unroll
         for (int j = 0; j < kMJ; j++) bits |= (uint64_t)m[j] << (q * kMJ + j);
@@ -583,7 +575,7 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
             if (!t) continue;
             const uint32_t q = (uint32_t)__builtin_ctzll(t) / kMJ;
             const uint32_t pos = wcnt[q][j][wave] + lanes_below(wmask[q][j][wave]);
-            out[q * cstride + cell0 + pos] = DHit{s[j], (uint32_t)(j * kBlock + tid), lkey[q]};
+            out[q * cstride + cell0 + pos] = s[j];
         }
     } else {
         for (uint32_t q = 0; q < nq; q++) {
@@ -591,7 +583,7 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
             for (int j = 0; j < kMJ; j++) {
                 if (!((bits >> (q * kMJ + j)) & 1ull)) continue;
                 const uint32_t pos = wcnt[q][j][wave] + lanes_below(wmask[q][j][wave]);
-                out[q * cstride + cell0 + pos] = DHit{s[j], (uint32_t)(j * kBlock + tid), lkey[q]};
+                out[q * cstride + cell0 + pos] = s[j];
             }
         }
     }
@@ -646,6 +638,14 @@ __global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restr
     const uint32_t prefix = offs[c];
     const uint32_t n = cres[c].count;
     const uint64_t so = mp.so;
+    if (mp.u32) {  // an mscan cell: 4-B slot ids, offsets in slot words
+        const uint32_t* __restrict__ s32 = reinterpret_cast<const uint32_t*>(scratch);
+        uint32_t* __restrict__ o32 = reinterpret_cast<uint32_t*>(out);
+        const uint32_t lim = mp.cap > prefix ? mp.cap - prefix : 0u;
+        const uint32_t m = n < lim ? n : lim;
+        for (uint32_t e = tid; e < m; e += kBlock) o32[4 * mp.dst_off + prefix + e] = s32[so + e];
+        return;
+    }
     for (uint32_t e = tid; e < n; e += kBlock) {
         const uint32_t pos = prefix + e;
         if (pos >= mp.cap) break;
@@ -838,7 +838,7 @@ hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResul
     return hipGetLastError();
 }
 
-hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, DHit* d_out,
+hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, uint32_t* d_out,
                         DGroupResult* d_cres, bool gen, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
     if (ms.n_chunks == 0 || ms.n_sigs == 0) return hipSuccess;
     if (ms.n_sigs > (uint32_t)kMaxMSig || ms.n_fields > (uint32_t)kMaxMField || ms.n_clauses > (uint32_t)kMaxMClause)

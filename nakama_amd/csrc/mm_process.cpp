@@ -80,6 +80,8 @@ struct Replay : ReplayCore {
     // Fetches the next page of a group's list (cursor = its last entry).
     void fetch_more(BGroup& g) override {
         stats.refetches++;
+        if (!g.hits && g.n)  // a slot list (mscan) is complete by construction: nothing to page
+            throw DeviceError{hipErrorUnknown, "page of a slot list", __LINE__};
         if (g.ext.empty() && g.n) {
             g.ext.assign(g.hits, g.hits + g.n);
             if (g.rev) g.ext_rev.assign(g.rev, g.rev + g.n);
@@ -133,7 +135,7 @@ struct Replay : ReplayCore {
         stats.k_launches[0]++;
         g.ext.insert(g.ext.end(), c.h_page_.p, c.h_page_.p + r.count);
         if (rev) g.ext_rev.insert(g.ext_rev.end(), c.h_page_rev_.p, c.h_page_rev_.p + r.count);
-        g.hits = g.ext.data();
+        g.set_hits(g.ext.data());
         g.rev = rev ? g.ext_rev.data() : nullptr;
         g.n = (uint32_t)g.ext.size();
         g.complete = r.complete != 0;
@@ -362,13 +364,14 @@ struct Replay : ReplayCore {
             cg_first.push_back(first);
             cg_end.push_back(first + ms.n_chunks);
             cg_off.push_back(off);
+            // u32 cells and output: `so` in slot words from the scratch base
             for (uint32_t ch = 0; ch < ms.n_chunks; ch++)
-                lmap.push_back(DChunkMap{first, ch * mchunk, d.k, 0u, off,
-                                         mscratch + ((uint64_t)q * ms.n_chunks + ch) * mchunk});
+                lmap.push_back(DChunkMap{first, ch * mchunk, d.k, 1u, off,
+                                         4 * mscratch + ((uint64_t)q * ms.n_chunks + ch) * mchunk});
             off += d.k;
         }
         const uint32_t ncells = use_m ? ms.n_sigs * ms.n_chunks : 0;
-        if (use_m) scratch += (uint64_t)ncells * mchunk;
+        if (use_m) scratch += ((uint64_t)ncells * mchunk + 3) / 4;  // 4-B slots in 16-B DHit units
         const int ng = (int)lg.size();
         const uint32_t nres = (uint32_t)(nwhole + nchunks) + ncells, nmap = (uint32_t)lmap.size();
         c.h_groups_.reserve(ng);
@@ -439,7 +442,8 @@ struct Replay : ReplayCore {
         NKM_HIP(launch_scan(st, c.d_groups_.p + nwhole, nchunks, c.d_scan_.p, c.d_res_.p + nwhole, stream, c.ev_[2],
                             c.ev_[3]));
         if (use_m)
-            NKM_HIP(launch_mscan(st, ms, c.d_msig_.p, c.d_mcl_.p, c.d_scan_.p + mscratch, c.d_res_.p + nwhole + nchunks,
+            NKM_HIP(launch_mscan(st, ms, c.d_msig_.p, c.d_mcl_.p, reinterpret_cast<uint32_t*>(c.d_scan_.p + mscratch),
+                                 c.d_res_.p + nwhole + nchunks,
                                  std::any_of(msig.begin(), msig.end(), [](const DMSig& m) { return !m.term_only; }),
                                  stream, c.ev_[4], c.ev_[5]));
         // a marker between the eval kernels and stitch_kernel: without it the
@@ -549,7 +553,7 @@ struct Replay : ReplayCore {
             const int64_t per_live = 8 + 9 * (int64_t)ms.n_fields;
             const DGroupResult* mr = c.h_res_.p + nwhole + nchunks;
             for (uint32_t t = 0; t < ncells; t++) {
-                stats.k_bytes[2] += (int64_t)mr[t].scanned * 5 + (int64_t)mr[t].live * per_live + (int64_t)mr[t].count * 16;
+                stats.k_bytes[2] += (int64_t)mr[t].scanned * 5 + (int64_t)mr[t].live * per_live + (int64_t)mr[t].count * 4;
                 stats.pair_evals += (int64_t)mr[t].scanned * ms.n_sigs;
             }
             stats.k_bytes[2] += (int64_t)(ms.n_sigs * sizeof(DMSig) + mcl.size() * sizeof(DClause));
@@ -563,7 +567,7 @@ struct Replay : ReplayCore {
                 BGroup& g = bg[lg_group[i]];
                 const DGroupResult& r = c.h_res_.p[i];
                 g.head = 0;
-                g.hits = c.h_out_.p + lg[i].out_off;
+                g.set_hits(c.h_out_.p + lg[i].out_off);
                 g.rev = rev ? c.h_rev_.p + lg[i].out_off : nullptr;
                 g.pm = need_pm ? c.h_pm_.p + lg[i].out_off : nullptr;
                 g.pm_n = need_pm ? std::min<uint32_t>(r.count, kPairP) : 0;
@@ -577,18 +581,24 @@ struct Replay : ReplayCore {
         } else {
             wire(0, (size_t)nwhole);
         }
-        // chunked / mscan searches: exact hit counts are known now; copy just those
+        // chunked / mscan searches: exact hit counts are known now; copy just
+        // those (an mscan list: 4-B slot ids, in the first quarter of its region)
+        const size_t n_scan_cg = cg_list.size() - (use_m ? m_list.size() : 0);
         for (size_t k = 0; k < cg_list.size(); k++) {
             BGroup& g = bg[cg_list[k]];
+            const bool slots = k >= n_scan_cg;
             uint64_t n = 0;
             for (uint32_t t = cg_first[k]; t < cg_end[k]; t++) n += c.h_res_.p[nwhole + t].count;
             bool complete = true;
             if (n > g.d.k) { n = g.d.k; complete = false; }
+            if (slots && !complete)  // mscan lists are sized to their whole source (plan above)
+                throw DeviceError{hipErrorUnknown, "mscan list cut", __LINE__};
             if (n)
-                NKM_HIP(hipMemcpyAsync(c.h_out_.p + cg_off[k], c.d_out_.p + cg_off[k], n * sizeof(DHit),
+                NKM_HIP(hipMemcpyAsync(c.h_out_.p + cg_off[k], c.d_out_.p + cg_off[k], n * (slots ? 4 : sizeof(DHit)),
                                        hipMemcpyDeviceToHost, stream));
             g.head = 0;
-            g.hits = c.h_out_.p + cg_off[k];
+            if (slots) g.set_slots(reinterpret_cast<const uint32_t*>(c.h_out_.p + cg_off[k]));
+            else g.set_hits(c.h_out_.p + cg_off[k]);
             g.rev = nullptr;
             g.pm = nullptr;
             g.pm_n = 0;
@@ -602,7 +612,7 @@ struct Replay : ReplayCore {
         // slow path: evaluate the single pair on the device (pool workers of a
         // RevPrecision parallel replay share the stream and the buffers)
         std::lock_guard<std::mutex> lk(c.pair_mu_);
-        uint32_t pr[2] = {g.hits[from_pos].slot, g.hits[to_pos].slot};
+        uint32_t pr[2] = {g.slot(from_pos), g.slot(to_pos)};
         c.d_slots_tmp_.reserve(2, false);
         c.d_pair_out_.reserve(1, false);
         NKM_HIP(hipMemcpyAsync(c.d_slots_tmp_.p, pr, sizeof pr, hipMemcpyHostToDevice, stream));
@@ -1514,7 +1524,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                     }
                     if (j >= g.n) break;
                 }
-                const uint32_t H = g.hits[j].slot;
+                const uint32_t H = g.slot(j);
                 if (H == T || rp.same_party(T, H)) continue;
                 // a ticket an earlier processCustom pass retired is still in
                 // the search index, but not in indexesCopy: "missing index" (:432-437)
@@ -2072,10 +2082,10 @@ int32_t Core::debug_hits(const std::string& ticket, const char** tk, double* sc,
     while (!g.complete) rp.fetch_more(g);
     debug_strings_.clear();
     int32_t n = 0;
-    auto skip = [&](uint32_t i) { return g.hits[i].slot == (uint32_t)T || rp.same_party((uint32_t)T, g.hits[i].slot); };
+    auto skip = [&](uint32_t i) { return g.slot(i) == (uint32_t)T || rp.same_party((uint32_t)T, g.slot(i)); };
     for (uint32_t i = 0; i < g.n; i++) {
         if (skip(i)) continue;
-        debug_strings_.emplace_back(this->tk(g.hits[i].slot));
+        debug_strings_.emplace_back(this->tk(g.slot(i)));
     }
     for (uint32_t i = 0; i < g.n; i++) {
         if (skip(i)) continue;

@@ -72,7 +72,24 @@ struct BGroup {
     uint32_t nrows = 0;
     uint32_t row_slot = kNoSlot;  // RevPrecision: the single searching row
     DGroup d{};
+    // The hit list: `hits` (16-B DHit, slot + source position + score key) or,
+    // for mscan lists (never cut, so no cursor needs their keys), 4-B slot
+    // ids only.  slot(i) reads either: sp/ss = the first slot and the stride
+    // in u32 words (4 over a DHit array, 1 over a slot list).
     const DHit* hits = nullptr;
+    const uint32_t* sp = nullptr;
+    uint32_t ss = 4;
+    uint32_t slot(uint32_t i) const { return sp[(size_t)i * ss]; }
+    void set_hits(const DHit* h) {
+        hits = h;
+        sp = h ? &h->slot : nullptr;
+        ss = 4;
+    }
+    void set_slots(const uint32_t* s) {
+        hits = nullptr;
+        sp = s;
+        ss = 1;
+    }
     const uint8_t* rev = nullptr;
     const uint32_t* pm = nullptr;  // kPairP masks per entry (rev rows with combos)
     uint32_t pm_n = 0;             // entries covered by pm
@@ -194,14 +211,14 @@ struct ReplayCore {
         const int room = tmax - tcount;  // entries a combo may hold
         const uint32_t tparty = ht.party;
         int ncomb = 0;
-        while (g.head < g.n && sel[g.hits[g.head].slot]) g.head++;
+        while (g.head < g.n && sel[g.slot(g.head)]) g.head++;
         for (uint32_t i = g.head; i < g.n; i++) {
             if (i + kPrefetch < g.n) {
-                const uint32_t P = g.hits[i + kPrefetch].slot;
+                const uint32_t P = g.slot(i + kPrefetch);
                 __builtin_prefetch(&sel[P]);
                 __builtin_prefetch(&v.hot[P]);
             }
-            const uint32_t H = g.hits[i].slot;
+            const uint32_t H = g.slot(i);
             hits_seen++;
             if (H == T || sel[H]) continue;
             const HotRec& hh = v.hot[H];
@@ -225,7 +242,7 @@ struct ReplayCore {
             if (!form && last && l >= tmin && l <= tmax) {
                 bool more = false;
                 for (uint32_t q = i + 1; q < g.n && !more; q++) {
-                    const uint32_t s = g.hits[q].slot;
+                    const uint32_t s = g.slot(q);
                     more = s != T && !sel[s] && !same_party(T, s);
                 }
                 form = !more;
@@ -265,7 +282,7 @@ struct ReplayCore {
                     continue;
                 }
             }
-            const uint32_t s = g.hits[j].slot;
+            const uint32_t s = g.slot(j);
             if (s != T && !sel[s] && !same_party(T, s)) return 1;
         }
     }
@@ -278,7 +295,7 @@ struct ReplayCore {
         const uint32_t tparty = ht.party;
         ncomb = 0;
         open.clear();
-        while (g.head < g.n && sel[g.hits[g.head].slot]) g.head++;
+        while (g.head < g.n && sel[g.slot(g.head)]) g.head++;
         for (uint32_t i = g.head;; i++) {
             if (i >= g.n) {
                 if (g.complete) break;
@@ -287,11 +304,11 @@ struct ReplayCore {
                 if (i >= g.n) { if (g.complete) break; i--; continue; }
             }
             if (i + kPrefetch < g.n) {  // the walk's next slots
-                const uint32_t P = g.hits[i + kPrefetch].slot;
+                const uint32_t P = g.slot(i + kPrefetch);
                 __builtin_prefetch(&sel[P]);
                 __builtin_prefetch(&v.hot[P]);
             }
-            const uint32_t H = g.hits[i].slot;
+            const uint32_t H = g.slot(i);
             hits_seen++;
             if (H == T || sel[H]) continue;
             const HotRec& hh = v.hot[H];
@@ -469,7 +486,8 @@ struct DenseRec {
 
 // One pool's per-position copies (filled by gather, in parallel chunks).
 struct DensePool {
-    const DHit* hits = nullptr;
+    const uint32_t* sp = nullptr;  // the list's slots (BGroup::slot)
+    uint32_t ss = 4;
     uint32_t n = 0;
     const uint32_t* bis = nullptr;  // the pool's batch rows, ascending
     uint32_t nrows = 0;
@@ -478,7 +496,8 @@ struct DensePool {
     std::vector<uint32_t> slot;
 
     void reset(const BGroup& g, const uint32_t* rows, uint32_t n_rows, const uint32_t* batch_slots) {
-        hits = g.hits;
+        sp = g.sp;
+        ss = g.ss;
         n = g.n;
         bis = rows;
         nrows = n_rows;
@@ -489,9 +508,9 @@ struct DensePool {
     // positions [lo, hi): records, slots, and pos_of[slot] = position
     void gather(const ReplayView& v, uint32_t lo, uint32_t hi, uint32_t* pos_of) {
         for (uint32_t k = lo; k < hi; k++) {
-            const uint32_t s = hits[k].slot;
+            const uint32_t s = sp[(size_t)k * ss];
             if (k + 16 < hi) {
-                const uint32_t p = hits[k + 16].slot;
+                const uint32_t p = sp[(size_t)(k + 16) * ss];
                 __builtin_prefetch(&v.hot[p]);
                 __builtin_prefetch(&v.intervals[p]);
                 __builtin_prefetch(&pos_of[p], 1);
