@@ -992,8 +992,9 @@ void Core::merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, 
 // batch's row range is cut into chunks; each pool's records (ascending in
 // batch row, with running group / entry / expiry counts) are located in every
 // chunk by binary search, so each chunk knows its output offsets up front and
-// merges its share of the pools' records independently.  Applies the rows'
-// pending Intervals increments on the way.
+// merges its share of the pools' records independently (through a
+// chunk-local row map).  Applies the rows' pending Intervals increments on
+// the way.
 void Core::merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
                        GroupList& out_groups, std::vector<uint32_t>& expired, std::vector<uint32_t>& newly) {
     using Rec = PoolRec;
@@ -1030,16 +1031,23 @@ void Core::merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow,
     grow_to(expired, x0 + at[nch].x);
     grow_to(newly, n0 + at[nch].e);
     wp.run(nch, [&](size_t c) {
-        std::vector<uint32_t> head(ng), end(ng);
-        for (size_t gi = 0; gi < ng; gi++) head[gi] = cut[c * ng + gi], end[gi] = cut[(c + 1) * ng + gi];
+        // the chunk's records placed by batch row (a chunk-local map written by
+        // this worker alone), then swept in row order: linear in the chunk for
+        // any number of pools
+        const uint32_t lo = (uint32_t)(nb * c / nch), hi = (uint32_t)(nb * (c + 1) / nch);
+        static thread_local std::vector<uint64_t> at_row;  // (pool << 32 | record) + 1; 0: no record
+        at_row.assign(hi - lo, 0);
+        for (size_t gi = 0; gi < ng; gi++) {
+            const auto& recs = outs[gi].recs;
+            for (uint32_t k = cut[c * ng + gi]; k < cut[(c + 1) * ng + gi]; k++)
+                at_row[recs[k].bi - lo] = (((uint64_t)gi << 32) | k) + 1;
+        }
         size_t gk = g0 + at[c].g, ek = e0 + at[c].e, xk = x0 + at[c].x;
-        for (;;) {
-            uint32_t best = UINT32_MAX, bg_ = 0;
-            for (uint32_t gi = 0; gi < ng; gi++)
-                if (head[gi] < end[gi] && outs[gi].recs[head[gi]].bi < best) best = outs[gi].recs[head[gi]].bi, bg_ = gi;
-            if (best == UINT32_MAX) break;
-            const PoolOut& o = outs[bg_];
-            const Rec& r = o.recs[head[bg_]++];
+        for (uint32_t i = 0; i < hi - lo; i++) {
+            if (!at_row[i]) continue;
+            const uint64_t v = at_row[i] - 1;
+            const PoolOut& o = outs[v >> 32];
+            const Rec& r = o.recs[(uint32_t)v];
             const uint32_t T = brow[r.bi];
             intervals_[T]++;  // the row's pending Intervals increment
             if (r.expired) expired[xk++] = T;
