@@ -94,12 +94,19 @@ struct Cand {
 __device__ __forceinline__ Cand eval_candidate(const DStore& st, const DGroup& g, const uint32_t* __restrict__ src,
                                                uint32_t idx) {
     Cand c{0, idx, 0, 1, false, false};
-    if (idx >= g.src_len) return c;
-    const uint32_t s = src[g.src_off + idx];
+    if (g.src_len == 0) return c;
+    // unconditional loads (a clamped position past the end, masked below):
+    // the slot id, then alive / Min / Max / party in one round trip
+    const bool valid = idx < g.src_len;
+    const uint32_t s = src[g.src_off + (valid ? idx : g.src_len - 1)];
+    const uint8_t al = st.alive[s];
+    const int32_t mn = st.minc[s], mx = st.maxc[s];
+    const uint32_t pt = g.tparty != kNoParty ? st.party[s] : 0u;
+    if (!valid) return c;
     c.slot = s;
-    bool m = st.alive[s] != 0;
+    bool m = al != 0;
     c.live = m;
-    if (m) m = st.minc[s] >= g.tmin && st.maxc[s] <= g.tmax && (g.tparty == kNoParty || st.party[s] != g.tparty);
+    m = m && mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
     double sp = 0.0;
     if (m) m = eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
     if (m) {
@@ -408,7 +415,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// NF: fields the signatures read (registers per candidate scale with it);
+// NF: fields the signatures read, 0-4 (registers per candidate scale with it);
 // GEN: some signature is not term-only (the clause loop is compiled in).
 template <int NF, bool GEN, int kMJ>
 __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, const DMSig* __restrict__ sigs,
@@ -429,37 +436,51 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     const uint32_t len = ms.src_len - base < (uint32_t)kMChunk ? ms.src_len - base : (uint32_t)kMChunk;
     const uint32_t* __restrict__ src = st.order + ms.src_off + base;
     // hits are 4-B slot ids: an mscan search is constant-score and never cut,
-    // so its list needs neither score keys nor source positions
-    uint32_t s[kMJ];
-    bool a[kMJ];
-    int32_t mn[kMJ], mx[kMJ];
-    uint8_t kk[NF][kMJ];
-    int64_t vv[NF][kMJ];
+    // so its list needs neither score keys nor source positions.
+    // Every load below is unconditional — the chunk's tail lanes read a
+    // clamped position / slot and are masked afterwards — so the compiler
+    // issues each round's loads back to back before one wait: the slot ids,
+    // then all columns of all kMJ candidates (one HBM round trip each) instead
+    // of a branch and a wait around every load.  The field columns' base
+    // pointers are scalar loads issued ahead of the slot ids.
+    constexpr int NFA = NF > 0 ? NF : 1;  // array extent (NF = 0: signature sets that read no field)
+    const uint8_t* __restrict__ fkp[NFA];
+    const int64_t* __restrict__ fvp[NFA];
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+        fkp[f] = st.fkind[ms.field[f]];
+        fvp[f] = st.fval[ms.field[f]];
+    }
+    uint32_t s[kMJ], sl[kMJ];
 #pragma unroll
     for (int j = 0; j < kMJ; j++) {
         const uint32_t i = (uint32_t)(j * kBlock + tid);
-        s[j] = i < len ? src[i] : kNoSlot;
+        sl[j] = src[i < len ? i : len - 1];
+        s[j] = i < len ? sl[j] : kNoSlot;
     }
-    // every column load depends only on the slot id, so they are all in
-    // flight together (one round trip); dead slots are masked afterwards
+    uint8_t al[kMJ];
+    int32_t mn[kMJ], mx[kMJ];
+    uint8_t kk[NFA][kMJ];
+    int64_t vv[NFA][kMJ];
+#pragma unroll
+    for (int j = 0; j < kMJ; j++) {
+        al[j] = st.alive[sl[j]];
+        mn[j] = st.minc[sl[j]];
+        mx[j] = st.maxc[sl[j]];
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            kk[f][j] = fkp[f][sl[j]];
+            vv[f][j] = fvp[f][sl[j]];
+        }
+    }
+    bool a[kMJ];
 #pragma unroll
     for (int j = 0; j < kMJ; j++) {
         const bool v = s[j] != kNoSlot;
-        a[j] = v && st.alive[s[j]] != 0;
-        mn[j] = v ? st.minc[s[j]] : 0;
-        mx[j] = v ? st.maxc[s[j]] : 0;
-    }
+        a[j] = v && al[j] != 0;
 #pragma unroll
-    for (int f = 0; f < NF; f++) {
-        const bool have = f < (int)ms.n_fields;  // NF = 1 also serves signature sets that read no field
-        const uint8_t* __restrict__ fk = have ? st.fkind[ms.field[f]] : nullptr;
-        const int64_t* __restrict__ fv = have ? st.fval[ms.field[f]] : nullptr;
-#pragma unroll
-        for (int j = 0; j < kMJ; j++) {
-            const bool v = have && s[j] != kNoSlot;
-            kk[f][j] = v ? fk[s[j]] : (uint8_t)KIND_ABSENT;
-            vv[f][j] = v ? fv[s[j]] : 0;
-        }
+        for (int f = 0; f < NF; f++)
+            if (!v) kk[f][j] = (uint8_t)KIND_ABSENT;
     }
     uint32_t live = 0;
 #pragma unroll
@@ -467,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o);
     if (lane == 0) wlive[wave] = live;
     // a candidate's keyword value per field, or a value no term id takes
-    int64_t kw[NF][kMJ];
+    int64_t kw[NFA][kMJ];
 #pragma unroll
     for (int f = 0; f < NF; f++)
 #pragma unroll
@@ -844,8 +865,7 @@ hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs,
     if (ms.n_sigs > (uint32_t)kMaxMSig || ms.n_fields > (uint32_t)kMaxMField || ms.n_clauses > (uint32_t)kMaxMClause)
         return hipErrorInvalidValue;
     const dim3 grid(ms.n_chunks), block(kBlock);
-    const int nf = ms.n_fields < 1 ? 1 : (int)ms.n_fields;
-    const int sel = (nf - 1) * 2 + (gen ? 1 : 0);
+    const int sel = (int)ms.n_fields * 2 + (gen ? 1 : 0);
     const uint32_t mj = ms.chunk / kBlock;
     if (ms.chunk % kBlock || (mj != 2 && mj != 4 && mj != 8) || (mj == 8 && ms.n_sigs > 8)) return hipErrorInvalidValue;
 #define NKM_MSCAN_J(NF, G, J)                                                                                 \
@@ -861,13 +881,15 @@ hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs,
             NKM_MSCAN_J(NF, G, 2);       \
     } while (0)
     switch (sel) {
-        case 0: NKM_MSCAN(1, false); break;
-        case 1: NKM_MSCAN(1, true); break;
-        case 2: NKM_MSCAN(2, false); break;
-        case 3: NKM_MSCAN(2, true); break;
-        case 4: NKM_MSCAN(3, false); break;
-        case 5: NKM_MSCAN(3, true); break;
-        case 6: NKM_MSCAN(4, false); break;
+        case 0: NKM_MSCAN(0, false); break;
+        case 1: NKM_MSCAN(0, true); break;
+        case 2: NKM_MSCAN(1, false); break;
+        case 3: NKM_MSCAN(1, true); break;
+        case 4: NKM_MSCAN(2, false); break;
+        case 5: NKM_MSCAN(2, true); break;
+        case 6: NKM_MSCAN(3, false); break;
+        case 7: NKM_MSCAN(3, true); break;
+        case 8: NKM_MSCAN(4, false); break;
         default: NKM_MSCAN(4, true); break;
     }
 #undef NKM_MSCAN
