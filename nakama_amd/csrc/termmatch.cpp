@@ -3,6 +3,7 @@
 // (parse.go: Parse with Perl = ClassNL|OneLine|PerlX|UnicodeGroups) for the
 // constructs vellum compiles; the matcher is a Pike VM over runes.
 #include "termmatch.h"
+#include "unicode_tables.h"
 
 #include <algorithm>
 #include <cctype>
@@ -62,8 +63,35 @@ Ranges negate(Ranges r) {
     return o;
 }
 
+// Adds the simple case-folding orbit of every rune in r (Go's
+// appendFoldedRange; vellum expands a FoldCase literal to the same orbit
+// through unicode.SimpleFold).
+void fold(Ranges& r) {
+    Ranges add;
+    const uint32_t* fr = uni::kFoldRune;
+    const uint32_t* fe = fr + uni::kFoldCount;
+    for (auto& p : r) {
+        for (const uint32_t* q = std::lower_bound(fr, fe, p.first); q < fe && *q <= p.second; q++) {
+            const int o = uni::kFoldOrbit[q - fr];
+            for (int k = uni::kOrbitStart[o]; k < uni::kOrbitStart[o + 1]; k++)
+                add.push_back({uni::kOrbitRunes[k], uni::kOrbitRunes[k]});
+        }
+    }
+    r.insert(r.end(), add.begin(), add.end());
+    normalize(r);
+}
+
+// appendGroup (parse.go): a named group's ranges, folded under (?i), then
+// negated for the negative form (ClassNL: may match '\n').
+void append_group(Ranges g, bool neg, bool fold_case, Ranges* out) {
+    normalize(g);
+    if (fold_case) fold(g);
+    if (neg) g = negate(g);
+    out->insert(out->end(), g.begin(), g.end());
+}
+
 // Perl classes \d \s \w (regexp/syntax perl_groups.go), ASCII only.
-bool perl_class(char c, Ranges* out) {
+bool perl_class(char c, bool fold_case, Ranges* out) {
     Ranges r;
     switch (c | 0x20) {
     case 'd': r = {{'0', '9'}}; break;
@@ -71,9 +99,31 @@ bool perl_class(char c, Ranges* out) {
     case 'w': r = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}; break;
     default: return false;
     }
-    if (c >= 'A' && c <= 'Z') r = negate(r);
-    out->insert(out->end(), r.begin(), r.end());
+    append_group(std::move(r), c >= 'A' && c <= 'Z', fold_case, out);
     return true;
+}
+
+// POSIX classes [:name:] (perl_groups.go posixGroup).
+bool posix_class(const std::string& name, Ranges* r) {
+    static const struct { const char* n; std::vector<std::pair<uint32_t, uint32_t>> r; } kTab[] = {
+        {"alnum", {{'0', '9'}, {'A', 'Z'}, {'a', 'z'}}},
+        {"alpha", {{'A', 'Z'}, {'a', 'z'}}},
+        {"ascii", {{0, 0x7F}}},
+        {"blank", {{'\t', '\t'}, {' ', ' '}}},
+        {"cntrl", {{0, 0x1F}, {0x7F, 0x7F}}},
+        {"digit", {{'0', '9'}}},
+        {"graph", {{'!', '~'}}},
+        {"lower", {{'a', 'z'}}},
+        {"print", {{' ', '~'}}},
+        {"punct", {{'!', '/'}, {':', '@'}, {'[', '`'}, {'{', '~'}}},
+        {"space", {{'\t', '\r'}, {' ', ' '}}},
+        {"upper", {{'A', 'Z'}}},
+        {"word", {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}},
+        {"xdigit", {{'0', '9'}, {'A', 'F'}, {'a', 'f'}}},
+    };
+    for (auto& e : kTab)
+        if (name == e.n) { *r = e.r; return true; }
+    return false;
 }
 
 struct Stop { MtStatus st; };
@@ -99,6 +149,9 @@ struct RxCompiler {
     size_t i = 0;
     int depth = 0;
     std::vector<Node> nodes;
+    // Perl flags in effect (parsePerlFlags): (?i) FoldCase, (?s) DotNL; a
+    // group restores its opener's flags when it closes
+    bool fold_case = false, dot_nl = false;
     explicit RxCompiler(const std::string& p) : s(p) {}
 
     [[noreturn]] static void err() { throw Stop{MT_SEARCH_ERROR}; }
@@ -106,7 +159,43 @@ struct RxCompiler {
     bool end() const { return i >= s.size(); }
     char peek(size_t k = 0) const { return i + k < s.size() ? s[i + k] : '\0'; }
     int add(Node n) { nodes.push_back(std::move(n)); return (int)nodes.size() - 1; }
-    int lit(uint32_t lo, uint32_t hi) { Node n; n.t = Node::CLASS; n.cls = {{lo, hi}}; return add(std::move(n)); }
+    int lit(uint32_t lo, uint32_t hi) {
+        Node n;
+        n.t = Node::CLASS;
+        n.cls = {{lo, hi}};
+        if (fold_case) fold(n.cls);
+        return add(std::move(n));
+    }
+
+    // \pN, \p{Name}, \p{^Name}, \PN (parseUnicodeClass), i at the backslash.
+    // Names: Go's general categories and Any; a script name (\p{Greek}) is
+    // not lowered (MM_ERR_UNSUPPORTED), nor is any other unknown name.
+    void unicode_class(Ranges* out) {
+        bool neg = s[i + 1] == 'P';
+        i += 2;
+        std::string name;
+        if (end()) err();
+        if (s[i] == '{') {
+            const size_t close = s.find('}', i);
+            if (close == std::string::npos) err();  // ErrInvalidCharRange
+            name = s.substr(i + 1, close - i - 1);
+            i = close + 1;
+        } else {
+            const size_t st = i;
+            (void)rune();
+            name = s.substr(st, i - st);
+        }
+        if (!name.empty() && name[0] == '^') { neg = !neg; name.erase(0, 1); }
+        Ranges t;
+        if (name == "Any") {
+            t = {{0, kMaxRune}};
+        } else if (const uni::Category* c = uni::category(name.data(), name.size())) {
+            for (int k = 0; k < c->n; k++) t.push_back({c->r[k].lo, c->r[k].hi});
+        } else {
+            unsupported();
+        }
+        append_group(std::move(t), neg, fold_case, out);
+    }
 
     uint32_t rune() {
         uint32_t r = decode(s, i);
@@ -165,9 +254,21 @@ struct RxCompiler {
         while (first || peek() != ']') {
             if (end()) err();  // ErrMissingBracket
             first = false;
-            if (peek() == '[' && peek(1) == ':' && s.find(":]", i + 2) != std::string::npos) unsupported();  // POSIX
-            if (peek() == '\\' && (peek(1) == 'p' || peek(1) == 'P')) unsupported();                     // \pN
-            if (peek() == '\\' && perl_class(peek(1), &r)) { i += 2; continue; }
+            if (peek() == '[' && peek(1) == ':') {  // [:name:] / [:^name:] (parseNamedClass)
+                const size_t close = s.find(":]", i + 2);
+                if (close != std::string::npos) {
+                    std::string name = s.substr(i + 2, close - i - 2);
+                    const bool pneg = !name.empty() && name[0] == '^';
+                    if (pneg) name.erase(0, 1);
+                    Ranges g;
+                    if (!posix_class(name, &g)) err();  // ErrInvalidCharRange
+                    append_group(std::move(g), pneg, fold_case, &r);
+                    i = close + 2;
+                    continue;
+                }
+            }
+            if (peek() == '\\' && (peek(1) == 'p' || peek(1) == 'P')) { unicode_class(&r); continue; }
+            if (peek() == '\\' && perl_class(peek(1), fold_case, &r)) { i += 2; continue; }
             uint32_t lo = peek() == '\\' ? escape_char() : rune();
             uint32_t hi = lo;
             if (peek() == '-' && i + 1 < s.size() && s[i + 1] != ']') {
@@ -175,7 +276,9 @@ struct RxCompiler {
                 hi = peek() == '\\' ? escape_char() : rune();
                 if (hi < lo) err();  // ErrInvalidCharRange
             }
-            r.push_back({lo, hi});
+            Ranges one{{lo, hi}};
+            if (fold_case) fold(one);
+            r.insert(r.end(), one.begin(), one.end());
         }
         i++;  // ']'
         if (neg) r = negate(r);  // ClassNL: a negated class may match '\n'
@@ -244,7 +347,8 @@ struct RxCompiler {
                 continue;
             }
             last_repeat = false;
-            items.push_back(atom());
+            const int a = atom();
+            if (a >= 0) items.push_back(a);  // -1: a (?flags) item, which adds no node
         }
         if (items.empty()) { Node n; n.t = Node::EMPTY; return add(std::move(n)); }
         if (items.size() == 1) return items[0];
@@ -269,16 +373,40 @@ struct RxCompiler {
         switch (c) {
         case '(': {
             i++;
+            const bool saved_fold = fold_case, saved_dot = dot_nl;
             if (peek() == '?') {
-                if (peek(1) == ':') i += 2;
-                else if (peek(1) == 'P' && peek(2) == '<') {
+                if (peek(1) == 'P' && peek(2) == '<') {
                     size_t close = s.find('>', i + 3);
                     if (close == std::string::npos || close == i + 3) err();  // ErrInvalidNamedCapture
                     for (size_t k = i + 3; k < close; k++)
                         if (!(std::isalnum((unsigned char)s[k]) || s[k] == '_')) err();
                     i = close + 1;
                 } else {
-                    unsupported();  // flag groups (?i) (?s:...) ...
+                    // (?flags) / (?flags:re) / (?flags-flags...) (parsePerlFlags)
+                    i++;
+                    bool fc = fold_case, dn = dot_nl, neg = false, saw = false;
+                    for (;;) {
+                        if (end()) err();  // ErrInvalidPerlOp / missing paren
+                        const char c = s[i++];
+                        if (c == 'i') { fc = !neg; saw = true; }
+                        else if (c == 's') { dn = !neg; saw = true; }
+                        else if (c == 'm') { saw = true; }  // OneLine: only ^ $ (rejected by vellum anyway)
+                        else if (c == 'U') { unsupported(); }  // NonGreedy: every later node lazy
+                        else if (c == '-') { if (neg) err(); neg = true; saw = false; }
+                        else if (c == ':' || c == ')') {
+                            if (neg && !saw) err();
+                            if (c == ')') {  // flags for the rest of the enclosing group: no node
+                                fold_case = fc;
+                                dot_nl = dn;
+                                return -1;
+                            }
+                            fold_case = fc;
+                            dot_nl = dn;
+                            break;
+                        } else {
+                            err();  // ErrInvalidPerlOp
+                        }
+                    }
                 }
             }
             if (++depth > 1000) err();  // ErrNestingDepth
@@ -286,16 +414,32 @@ struct RxCompiler {
             depth--;
             if (peek() != ')' || end()) err();  // ErrMissingParen
             i++;
+            fold_case = saved_fold;
+            dot_nl = saved_dot;
             return r;
         }
-        case '.': { i++; Node n; n.t = Node::CLASS; n.cls = {{0, 9}, {11, kMaxRune}}; return add(std::move(n)); }
+        case '.': {
+            i++;
+            Node n;
+            n.t = Node::CLASS;
+            n.cls = dot_nl ? Ranges{{0, kMaxRune}} : Ranges{{0, 9}, {11, kMaxRune}};
+            return add(std::move(n));
+        }
         case '^':
         case '$': err();  // OpBeginText/OpEndText: vellum ErrNoEmpty
         case '[': return char_class();
         case '\\': {
             const char e = peek(1);
             if (e == 'A' || e == 'z' || e == 'b' || e == 'B') err();  // anchors / word boundaries (vellum)
-            if (e == 'p' || e == 'P') unsupported();
+            if (e == 'p' || e == 'P') {
+                Ranges r;
+                unicode_class(&r);
+                normalize(r);
+                Node n;
+                n.t = Node::CLASS;
+                n.cls = std::move(r);
+                return add(std::move(n));
+            }
             if (e == 'Q') {  // \Q...\E literal text
                 i += 2;
                 std::vector<int> items;
@@ -311,7 +455,7 @@ struct RxCompiler {
                 return add(std::move(n));
             }
             Ranges r;
-            if (perl_class(e, &r)) {
+            if (perl_class(e, fold_case, &r)) {
                 i += 2;
                 normalize(r);
                 Node n;

@@ -20,6 +20,8 @@
 #include <string>
 #include <vector>
 
+#include "../nakama_amd/csrc/unicode_tables.h"  // data only: Unicode 13 categories and fold orbits
+
 namespace oracle_re {
 
 enum Status { OK = 0, SEARCH_ERROR = 1, UNSUPPORTED = 2 };
@@ -64,10 +66,44 @@ struct Re {
 };
 using RP = std::shared_ptr<Re>;
 
+using RangeV = std::vector<std::pair<int32_t, int32_t>>;
+
+// (?i): every orbit of the simple case folding that meets the set joins it
+// whole (unicode.SimpleFold orbits, as vellum expands FoldCase literals and Go's
+// parser folds classes).
+inline void fold_in(RangeV& rs) {
+    const int n_orbits = (int)(sizeof(uni::kOrbitStart) / sizeof(uni::kOrbitStart[0])) - 1;
+    RangeV add;
+    for (int o = 0; o < n_orbits; o++) {
+        bool meets = false;
+        for (int k = uni::kOrbitStart[o]; k < uni::kOrbitStart[o + 1] && !meets; k++)
+            for (auto& q : rs)
+                if ((int32_t)uni::kOrbitRunes[k] >= q.first && (int32_t)uni::kOrbitRunes[k] <= q.second) { meets = true; break; }
+        if (meets)
+            for (int k = uni::kOrbitStart[o]; k < uni::kOrbitStart[o + 1]; k++)
+                add.push_back({(int32_t)uni::kOrbitRunes[k], (int32_t)uni::kOrbitRunes[k]});
+    }
+    rs.insert(rs.end(), add.begin(), add.end());
+}
+
+// complement within [0, 0x10FFFF]
+inline RangeV complement(RangeV rs) {
+    std::sort(rs.begin(), rs.end());
+    RangeV out;
+    int32_t nx = 0;
+    for (auto& q : rs) {
+        if (q.first > nx) out.push_back({nx, q.first - 1});
+        nx = std::max(nx, q.second + 1);
+    }
+    if (nx <= 0x10FFFF) out.push_back({nx, 0x10FFFF});
+    return out;
+}
+
 struct Parse {
     std::vector<int32_t> p;  // pattern runes
     size_t i = 0;
     int nest = 0;
+    bool fc = false, dn = false;  // (?i) FoldCase, (?s) DotNL in effect
     struct Fail { Status s; };
     [[noreturn]] void fail() { throw Fail{SEARCH_ERROR}; }
     [[noreturn]] void unsup() { throw Fail{UNSUPPORTED}; }
@@ -75,6 +111,67 @@ struct Parse {
     int32_t cur(size_t k = 0) const { return i + k < p.size() ? p[i + k] : -2; }
 
     static RP single(int32_t a, int32_t b) { auto r = std::make_shared<Re>(); r->k = Re::SET; r->set = {{a, b}}; return r; }
+    RP literal(int32_t a) {  // a pattern rune (folded under (?i))
+        RP r = single(a, a);
+        if (fc) fold_in(r->set);
+        return r;
+    }
+    // a named group's runes (perl / POSIX / Unicode class), folded under (?i),
+    // complemented for the negative form
+    RangeV group(RangeV g, bool negative) const {
+        if (fc) fold_in(g);
+        return negative ? complement(g) : g;
+    }
+    static bool posix(const std::vector<int32_t>& name, RangeV* out) {
+        std::string n;
+        for (int32_t c : name) { if (c < 0 || c > 0x7e) return false; n.push_back((char)c); }
+        if (n == "alnum") *out = {{'0', '9'}, {'A', 'Z'}, {'a', 'z'}};
+        else if (n == "alpha") *out = {{'A', 'Z'}, {'a', 'z'}};
+        else if (n == "ascii") *out = {{0, 127}};
+        else if (n == "blank") *out = {{9, 9}, {32, 32}};
+        else if (n == "cntrl") *out = {{0, 31}, {127, 127}};
+        else if (n == "digit") *out = {{'0', '9'}};
+        else if (n == "graph") *out = {{33, 126}};
+        else if (n == "lower") *out = {{'a', 'z'}};
+        else if (n == "print") *out = {{32, 126}};
+        else if (n == "punct") *out = {{33, 47}, {58, 64}, {91, 96}, {123, 126}};
+        else if (n == "space") *out = {{9, 13}, {32, 32}};
+        else if (n == "upper") *out = {{'A', 'Z'}};
+        else if (n == "word") *out = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}};
+        else if (n == "xdigit") *out = {{'0', '9'}, {'A', 'F'}, {'a', 'f'}};
+        else return false;
+        return true;
+    }
+    // at the backslash of \p / \P: the class's runes (scripts and unknown names: unsupported)
+    RangeV uclass() {
+        bool negative = cur(1) == 'P';
+        i += 2;
+        std::vector<int32_t> name;
+        if (cur() == '{') {
+            size_t j = i + 1;
+            while (j < p.size() && p[j] != '}') j++;
+            if (j >= p.size()) fail();
+            name.assign(p.begin() + i + 1, p.begin() + j);
+            i = j + 1;
+        } else {
+            if (at_end()) fail();
+            if (cur() < 0) fail();
+            name.push_back(p[i++]);
+        }
+        if (!name.empty() && name[0] == '^') { negative = !negative; name.erase(name.begin()); }
+        std::string n;
+        for (int32_t c : name) { if (c < 0 || c > 0x7e) unsup(); n.push_back((char)c); }
+        RangeV g;
+        if (n == "Any") g = {{0, 0x10FFFF}};
+        else {
+            const uni::Category* cat = nullptr;
+            for (const uni::Category& c : uni::kCategories)
+                if (n == c.name) cat = &c;
+            if (!cat) unsup();
+            for (int k = 0; k < cat->n; k++) g.push_back({(int32_t)cat->r[k].lo, (int32_t)cat->r[k].hi});
+        }
+        return group(g, negative);
+    }
     static bool alnum(int32_t c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
     static bool odig(int32_t c) { return c >= '0' && c <= '7'; }
     static int hexd(int32_t c) {
@@ -134,21 +231,32 @@ struct Parse {
         while (first || cur() != ']') {
             if (at_end()) fail();
             first = false;
-            if (cur() == '[' && cur(1) == ':') {
-                for (size_t j = i + 2; j + 1 < p.size(); j++)
-                    if (p[j] == ':' && p[j + 1] == ']') unsup();
+            if (cur() == '[' && cur(1) == ':') {  // [:name:] / [:^name:] when a ":]" follows
+                size_t j = i + 2;
+                while (j + 1 < p.size() && !(p[j] == ':' && p[j + 1] == ']')) j++;
+                if (j + 1 < p.size()) {
+                    std::vector<int32_t> name(p.begin() + i + 2, p.begin() + j);
+                    bool negative = !name.empty() && name[0] == '^';
+                    if (negative) name.erase(name.begin());
+                    RangeV g;
+                    if (!posix(name, &g)) fail();
+                    RangeV gg = group(g, negative);
+                    r->set.insert(r->set.end(), gg.begin(), gg.end());
+                    i = j + 2;
+                    continue;
+                }
             }
-            if (cur() == '\\' && (cur(1) == 'p' || cur(1) == 'P')) unsup();
+            if (cur() == '\\' && (cur(1) == 'p' || cur(1) == 'P')) {
+                RangeV gg = uclass();
+                r->set.insert(r->set.end(), gg.begin(), gg.end());
+                continue;
+            }
             std::vector<std::pair<int32_t, int32_t>> rs;
             bool ng;
             if (cur() == '\\' && perl(cur(1), &rs, &ng)) {
                 i += 2;
-                if (!ng) r->set.insert(r->set.end(), rs.begin(), rs.end());
-                else {  // complement of rs within [0, 0x10FFFF]
-                    int32_t nx = 0;
-                    for (auto& q : rs) { if (q.first > nx) r->set.push_back({nx, q.first - 1}); nx = q.second + 1; }
-                    r->set.push_back({nx, 0x10FFFF});
-                }
+                RangeV gg = group(rs, ng);
+                r->set.insert(r->set.end(), gg.begin(), gg.end());
                 continue;
             }
             int32_t a;
@@ -161,7 +269,9 @@ struct Parse {
                 else { if (cur() < 0) fail(); b = p[i++]; }
                 if (b < a) fail();
             }
-            r->set.push_back({a, b});
+            RangeV one{{a, b}};
+            if (fc) fold_in(one);
+            r->set.insert(r->set.end(), one.begin(), one.end());
         }
         i++;
         return r;
@@ -192,9 +302,9 @@ struct Parse {
         if (c == -1) fail();  // invalid UTF-8 in the pattern
         if (c == '(') {
             i++;
+            const bool fc0 = fc, dn0 = dn;
             if (cur() == '?') {
-                if (cur(1) == ':') i += 2;
-                else if (cur(1) == 'P' && cur(2) == '<') {
+                if (cur(1) == 'P' && cur(2) == '<') {
                     i += 3;
                     size_t s = i;
                     while (i < p.size() && p[i] != '>') {
@@ -203,29 +313,64 @@ struct Parse {
                     }
                     if (at_end() || i == s) fail();
                     i++;
-                } else unsup();
+                } else {
+                    // flags: [imsU]* ( '-' [imsU]+ )? then ':' (a group) or ')' (the rest of this group)
+                    i++;
+                    bool on = true, any_after_minus = false, minus = false;
+                    bool nfc = fc, ndn = dn;
+                    while (true) {
+                        int32_t f = cur();
+                        if (f < 0 && at_end()) fail();
+                        i++;
+                        if (f == 'i') { nfc = on; any_after_minus = true; }
+                        else if (f == 's') { ndn = on; any_after_minus = true; }
+                        else if (f == 'm') { any_after_minus = true; }
+                        else if (f == 'U') unsup();
+                        else if (f == '-' && !minus) { minus = true; on = false; any_after_minus = false; }
+                        else if (f == ':' || f == ')') {
+                            if (minus && !any_after_minus) fail();
+                            fc = nfc;
+                            dn = ndn;
+                            if (f == ')') return nullptr;  // no node: the flags hold to the group's end
+                            break;
+                        } else fail();
+                    }
+                }
             }
             if (++nest > 1000) fail();
             RP r = alt();
             nest--;
             if (cur() != ')') fail();
             i++;
+            fc = fc0;
+            dn = dn0;
             return r;
         }
         if (c == '^' || c == '$') fail();
-        if (c == '.') { i++; auto r = single(10, 10); r->neg = true; return r; }
+        if (c == '.') {
+            i++;
+            auto r = single(10, 10);
+            if (dn) r->set.clear();  // (?s): any rune
+            r->neg = true;
+            return r;
+        }
         if (c == '[') { i++; return klass(); }
         if (c == '\\') {
             int32_t e = cur(1);
             if (e == 'A' || e == 'z' || e == 'b' || e == 'B') fail();
-            if (e == 'p' || e == 'P') unsup();
+            if (e == 'p' || e == 'P') {
+                auto r = std::make_shared<Re>();
+                r->k = Re::SET;
+                r->set = uclass();
+                return r;
+            }
             if (e == 'Q') {
                 i += 2;
                 auto seq = std::make_shared<Re>();
                 seq->k = Re::SEQ;
                 while (!at_end() && !(cur() == '\\' && cur(1) == 'E')) {
                     if (cur() < 0) fail();
-                    seq->kids.push_back(single(p[i], p[i]));
+                    seq->kids.push_back(literal(p[i]));
                     i++;
                 }
                 if (!at_end()) i += 2;
@@ -237,16 +382,15 @@ struct Parse {
                 i += 2;
                 auto r = std::make_shared<Re>();
                 r->k = Re::SET;
-                r->set = rs;
-                r->neg = ng;
+                r->set = group(rs, ng);
                 return r;
             }
             i++;
             int32_t v = esc();
-            return single(v, v);
+            return literal(v);
         }
         i++;
-        return single(c, c);
+        return literal(c);
     }
     RP seq() {
         auto s = std::make_shared<Re>();
@@ -276,7 +420,7 @@ struct Parse {
                 continue;
             }
             after_rep = false;
-            s->kids.push_back(atom());
+            if (RP a = atom()) s->kids.push_back(a);  // null: a (?flags) item
         }
         return s;
     }

@@ -127,8 +127,49 @@ def test_term_cases_product(product):
             assert got == want, (pattern, term, got)
 
 
+# Go 1.20 regexp/syntax semantics of flags, POSIX and Unicode classes and case
+# folding (parse.go parsePerlFlags / parseNamedClass / parseUnicodeClass,
+# appendFoldedRange; unicode.SimpleFold orbits, Unicode 13.0), derived by hand:
+# (pattern, term, expected) with expected True/False (whole-term match),
+# "search_error" or "unsupported".
+GO_REGEXP_CASES = [
+    ("(?i)k", "k", True), ("(?i)k", "K", True), ("(?i)k", "\u212a", True), ("(?i)k", "x", False),
+    ("k", "K", False), ("(?i)ß", "\u1e9e", True), ("(?i)σ+", "Σσς", True), ("(?i)[a-c]+", "AbC", True),
+    ("(?i)\\w", "\u212a", True), ("(?i)\\w", "\u017f", True), ("\\w", "\u212a", False), ("(?i)\\W", "\u212a", False),
+    ("(?i)[^k]", "\u212a", False), ("(?i)é", "É", True), ("(?i)i", "\u0130", False), ("(?i)i", "\u0131", False),
+    ("(?s).", "\n", True), (".", "\n", False), ("a(?i)b", "aB", True), ("a(?i)b", "AB", False),
+    ("(?i:a)b", "Ab", True), ("(?i:a)b", "AB", False), ("(?i)a|b", "B", True), ("((?i)a)b", "AB", False),
+    ("(?i-s:a.)", "A\n", False), ("(?s-i:A.)", "A\n", True), ("(?)a", "a", True), ("(?m)a", "a", True),
+    ("[[:alpha:]]+", "abcXYZ", True), ("[[:alpha:]]+", "ab1", False), ("[[:^digit:]]", "a", True),
+    ("[[:^digit:]]", "5", False), ("(?i)[[:upper:]]", "q", True), ("[[:upper:]]", "q", False),
+    ("[[:word:][:punct:]]+", "a_!", True), ("[[:foo:]]", "a", "search_error"), ("[[:alpha:]", "a", "search_error"),
+    ("\\pL+", "héllo", True), ("\\pL+", "Ωμέγα", True), ("\\pL+", "h3", False), ("\\p{Lu}\\p{Ll}+", "Hello", True),
+    ("\\p{Lu}\\p{Ll}+", "hello", False), ("\\PL", "3", True), ("\\p{^L}", "3", True), ("\\P{^L}", "x", True),
+    ("\\pN", "\u0663", True), ("\\p{Nd}", "\u2167", False), ("\\p{Nl}", "\u2167", True), ("[\\pL\\d]+", "a1b2", True),
+    ("\\p{Any}+", "a\n", True), ("(?i)\\p{Lu}", "a", True), ("\\p{Lu}", "a", False),
+    ("\\p{Greek}", "α", "unsupported"), ("(?U)a", "a", "unsupported"), ("(?i-)a", "a", "search_error"),
+    ("(?x)a", "a", "search_error"), ("(?P=n)", "a", "search_error"), ("\\p{", "a", "search_error"),
+]
+
+
+def test_go_regexp_flag_and_class_cases(product):
+    """Flags (?i) (?s) (?m), POSIX [:classes:], Unicode \\p classes and case
+    folding: hand-derived Go semantics, product and oracle alike."""
+    orc = harness.oracle_lib()
+    for pat, term, want in GO_REGEXP_CASES:
+        for lib in (product, orc):
+            got = harness.term_match(lib, 1, pat, 0, term)
+            if isinstance(want, bool):
+                assert isinstance(got, list) and bool(got[0]) == want, (pat, term, got, want)
+            else:
+                assert got == want, (pat, term, got, want)
+
+
 def _rand_regex(rnd, depth=0):
-    atoms = ["a", "b", "c", ".", "[ab]", "[^a]", "[a-c]", "\\d", "\\w", "\\s", "\\.", "x", "é", "-", "_", "{", "}"]
+    atoms = ["a", "b", "c", ".", "[ab]", "[^a]", "[a-c]", "\\d", "\\w", "\\s", "\\.", "x", "é", "-", "_", "{", "}",
+             "(?i)", "(?s)", "(?-i)", "K", "k", "\u212a", "s", "ſ", "É", "σ", "Σ", "[[:alpha:]]", "[[:^lower:]]",
+             "[[:punct:][:digit:]]", "\\pL", "\\PL", "\\p{Lu}", "\\p{^Ll}", "[\\pN_]", "\\W", "[^\\w]", "(?i:k)",
+             "(?s:.)"]
     parts = []
     for _ in range(rnd.randint(0, 4)):
         r = rnd.random()
@@ -155,7 +196,8 @@ def test_regexp_differential_vs_oracle(product):
     patterns and terms: same parse status, same acceptance."""
     rnd = random.Random(5)
     orc = harness.oracle_lib()
-    alphabet = ["a", "b", "c", "x", ".", "1", "_", " ", "\n", "é", "-"]
+    alphabet = ["a", "b", "c", "x", ".", "1", "_", " ", "\n", "é", "-", "A", "K", "k", "\u212a", "ſ", "S", "É", "σ",
+                "ς", "Σ", "!", "٣"]
     bad = []
     for _ in range(1500):
         pat = _rand_regex(rnd)
