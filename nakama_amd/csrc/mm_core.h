@@ -555,6 +555,9 @@ public:
     std::vector<uint32_t> rows_, brow_, brow_group_, newly_, list_tmp_;
     GroupList pass_groups_;
     std::vector<uint32_t> expired_;
+    std::vector<BGroup> bg_;              // a pass's batch searches (kept: capacity reused)
+    std::vector<DGroup> lg_;              // their device descriptors (Replay::lg)
+    std::vector<uint32_t> lg_group_;
     std::vector<DensePool> dense_pools_;  // dense replay per pool (kept: capacity reused)
     std::vector<PoolOut> pool_outs_;      // few-pool replays: each pool's records
     void merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,

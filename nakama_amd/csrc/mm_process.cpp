@@ -73,7 +73,8 @@ struct Replay : ReplayCore {
                           core.live_.data(), core.count_.data(), core.created_.data(), core.sess_slots_.more.empty()};
     }
     Replay(Core& core, std::vector<uint8_t>& s, bool r, int mi, PassStats& ps, DStore ds, hipStream_t sm)
-        : ReplayCore(view(core), s, r, mi), c(core), stats(ps), st(ds), stream(sm) {
+        : ReplayCore(view(core), s, r, mi), c(core), stats(ps), st(ds), stream(sm), lg(core.lg_),
+          lg_group(core.lg_group_) {
         fast = core.fast_mode_;
     }
 
@@ -155,8 +156,8 @@ struct Replay : ReplayCore {
     // d_groups_ holds [whole searches, chunks]; d_res_ holds [whole searches,
     // chunks, mscan (signature x chunk) cells]; d_out_ holds every search's
     // output region.
-    std::vector<DGroup> lg;                 // whole searches, then chunks
-    std::vector<uint32_t> lg_group;         // owning BGroup of each entry of lg
+    std::vector<DGroup>& lg;                // whole searches, then chunks (Core::lg_: capacity kept)
+    std::vector<uint32_t>& lg_group;        // owning BGroup of each entry of lg
     std::vector<DChunkMap> lmap;            // per chunk, then per mscan cell
     std::vector<uint32_t> cg_list;          // chunked / mscan BGroups, in order
     std::vector<uint64_t> cg_off;           // their output offsets in d_out_
@@ -283,7 +284,43 @@ struct Replay : ReplayCore {
         // only use what batch assembly left of kOutCap
         uint64_t budget = 0;
         for (const BGroup& g : bg) budget += g.d.k;
-        for (uint32_t i = 0; i < bg.size(); i++) {
+        // A large RevPrecision batch (every search whole: no chunks, full
+        // lists or promotions) builds its descriptors on the workers.
+        const bool par_lg = rev && c.par_mode_ && m_list.empty() && bg.size() >= c.par_min(65536);
+        if (par_lg) {
+            WorkPool& wp = c.workers();
+            const size_t nb = bg.size(), nch = (size_t)wp.size() * 4;
+            grow_to(lg, nb);
+            grow_to(lg_group, nb);
+            std::vector<uint64_t> at(nch + 1, 0);
+            const uint32_t small_max = (uint32_t)small_src_max();
+            wp.run(nch, [&](size_t ch) {
+                uint64_t k = 0;
+                for (size_t i = nb * ch / nch; i < nb * (ch + 1) / nch; i++) {
+                    const DGroup& d = bg[i].d;
+                    DGroup& w = lg[i];
+                    w = d;
+                    w.path = 0;
+                    if (d.rev_slot != kNoSlot && !d.has_cursor && d.src_len > 0 && d.src_len <= small_max) {
+                        w.path = 1;
+                        w.k = d.src_len;
+                    }
+                    k += w.k;
+                    lg_group[i] = (uint32_t)i;
+                }
+                at[ch + 1] = k;
+            });
+            for (size_t ch = 0; ch < nch; ch++) at[ch + 1] += at[ch];
+            wp.run(nch, [&](size_t ch) {
+                uint64_t o = at[ch];
+                for (size_t i = nb * ch / nch; i < nb * (ch + 1) / nch; i++) {
+                    lg[i].out_off = o;
+                    o += lg[i].k;
+                }
+            });
+            off = at[nch];
+        }
+        for (uint32_t i = 0; i < bg.size() && !par_lg; i++) {
             if (on_m[i]) continue;
             const DGroup& d = bg[i].d;
             const bool big = d.src_len > kChunk && d.k > kChunk / 4;
@@ -375,7 +412,15 @@ struct Replay : ReplayCore {
         const int ng = (int)lg.size();
         const uint32_t nres = (uint32_t)(nwhole + nchunks) + ncells, nmap = (uint32_t)lmap.size();
         c.h_groups_.reserve(ng);
-        std::memcpy(c.h_groups_.p, lg.data(), ng * sizeof(DGroup));
+        if (ng >= 65536 && c.par_mode_) {  // 80 B per search: large batches copy on the workers
+            const size_t nch = c.workers().size();
+            c.workers().run(nch, [&](size_t ch) {
+                const size_t lo = (size_t)ng * ch / nch, hi = (size_t)ng * (ch + 1) / nch;
+                std::memcpy(c.h_groups_.p + lo, lg.data() + lo, (hi - lo) * sizeof(DGroup));
+            });
+        } else {
+            std::memcpy(c.h_groups_.p, lg.data(), ng * sizeof(DGroup));
+        }
         c.d_groups_.reserve(ng, false);
         c.d_res_.reserve(std::max<uint32_t>(nres, 1), false);
         c.d_out_.reserve(std::max<uint64_t>(off, 1), false);
@@ -1138,7 +1183,8 @@ int Core::process_default(GroupList& out_groups,
     const DStore st = dstore();
     Replay rp(*this, sel, rev, maxI, stats, st, stream_);
     std::vector<int32_t> sig_group(sigs_.size(), -1);
-    std::vector<BGroup> bg;
+    std::vector<BGroup>& bg = bg_;  // kept across passes: no page faults on the hot path
+    bg.clear();
     std::vector<uint32_t>& brow = brow_;
     std::vector<uint32_t>& brow_group = brow_group_;
     std::vector<uint32_t>& newly = newly_;
@@ -1162,7 +1208,9 @@ int Core::process_default(GroupList& out_groups,
         const auto ta0 = std::chrono::steady_clock::now();
         for (auto& g : bg)
             if (!rev) sig_group[g.sig] = -1;
-        bg.clear();
+        // RevPrecision batches refill the array in place on the workers
+        // (assemble_parallel_rev clears it whenever it declines)
+        if (!(rev && par_mode_)) bg.clear();
         brow.clear();
         brow_group.clear();
         size_t q = pos;
@@ -1278,18 +1326,32 @@ int Core::process_default(GroupList& out_groups,
         // workers (sources from a non-mutating lookup of the posting ranges)
         auto assemble_parallel_rev = [&]() -> bool {
             const size_t nr = rows.size() - pos;
-            if (!rev || retry_slot != kNoSlot || !par_mode_ || nr < par_min(65536) || nr > kMaxBatchRows || nr > win)
+            if (!rev || retry_slot != kNoSlot || !par_mode_ || nr < par_min(65536) || nr > kMaxBatchRows || nr > win) {
+                bg.clear();
                 return false;
+            }
             WorkPool& wp = workers();
             const unsigned nch = wp.size() * 4;
-            std::vector<std::vector<BGroup>> cg(nch);
-            std::vector<std::vector<uint32_t>> crow(nch);
-            std::vector<uint64_t> ck(nch, 0);
+            // count, then every chunk builds its rows' searches in place
+            std::vector<size_t> at(nch + 1, 0);
             wp.run(nch, [&](size_t c) {
+                size_t k = 0;
+                for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) k += !sel[rows[i]];
+                at[c + 1] = k;
+            });
+            for (unsigned c = 0; c < nch; c++) at[c + 1] += at[c];
+            const size_t n = at[nch];
+            std::vector<uint64_t> ck(nch, 0);
+            bg.resize(n);  // constructs only past the array's previous size
+            grow_to(brow, n);
+            grow_to(brow_group, n);
+            wp.run(nch, [&](size_t c) {
+                size_t o = at[c];
                 for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
                     const uint32_t r = rows[i];
                     if (sel[r]) continue;
-                    BGroup g;
+                    BGroup& g = bg[o];
+                    g.reset();
                     g.sig = sig_[r];
                     const Sig& sg = sigs_[g.sig];
                     g.n_fields = sg.n_fields;
@@ -1311,23 +1373,18 @@ int Core::process_default(GroupList& out_groups,
                     g.nrows = 1;
                     g.d.k = cap_k(g, 1, maxc_[r]);
                     ck[c] += g.d.k;
-                    cg[c].push_back(std::move(g));
-                    crow[c].push_back(r);
+                    brow[o] = r;
+                    brow_group[o] = (uint32_t)o;
+                    o++;
                 }
             });
             uint64_t tot = 0;
-            size_t n = 0;
-            for (unsigned c = 0; c < nch; c++) tot += ck[c], n += cg[c].size();
-            if (tot > kOutCap) return false;  // the serial loop cuts the batch
-            bg.reserve(n);
-            grow_to(brow, n);
-            grow_to(brow_group, n);
-            for (unsigned c = 0; c < nch; c++) {
-                for (size_t k = 0; k < cg[c].size(); k++) {
-                    brow[bg.size()] = crow[c][k];
-                    brow_group[bg.size()] = (uint32_t)bg.size();
-                    bg.push_back(std::move(cg[c][k]));
-                }
+            for (unsigned c = 0; c < nch; c++) tot += ck[c];
+            if (tot > kOutCap) {  // the serial loop cuts the batch
+                bg.clear();
+                brow.clear();
+                brow_group.clear();
+                return false;
             }
             return true;
         };

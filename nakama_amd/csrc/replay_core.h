@@ -101,6 +101,29 @@ struct BGroup {
     uint32_t head = 0;
     std::vector<DHit> ext;
     std::vector<uint8_t> ext_rev;
+    // back to a default-constructed search, keeping the vectors' capacity
+    // (a reused batch array is refilled in place by the host workers)
+    void reset() {
+        sig = 0;
+        n_fields = 0;
+        nrows = 0;
+        row_slot = kNoSlot;
+        d = DGroup{};
+        hits = nullptr;
+        sp = nullptr;
+        ss = 4;
+        rev = nullptr;
+        pm = nullptr;
+        pm_n = 0;
+        has_src_term = false;
+        src_field = 0;
+        src_term = 0;
+        n = 0;
+        complete = true;
+        head = 0;
+        ext.clear();
+        ext_rev.clear();
+    }
 };
 
 // Read-only per-slot views of the store that the replay consults.
