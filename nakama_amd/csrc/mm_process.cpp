@@ -463,13 +463,41 @@ struct Replay : ReplayCore {
             b1 = blk[c.shard_rank_ + 1];
         }
         // per eval kernel, the start/stop events of its dispatch (per-kernel roofline in bench.py)
+        // (read from lg: the pinned copy may be write-combined)
         int kinds = 0;
-        for (int i = b0; i < b1; i++) kinds |= c.h_groups_.p[i].var_score ? 2 : 1;
         // rsmall_kernel's rows of this rank's block
         std::vector<uint32_t>& small = small_rows;
         small.clear();
-        for (int i = b0; i < b1; i++)
-            if (c.h_groups_.p[i].path == 1) small.push_back((uint32_t)i);
+        if (b1 - b0 >= 65536 && c.par_mode_) {
+            WorkPool& wp = c.workers();
+            const size_t nblk = (size_t)(b1 - b0), nch = (size_t)wp.size() * 4;
+            std::vector<int> ck(nch, 0);
+            std::vector<size_t> at(nch + 1, 0);
+            wp.run(nch, [&](size_t ch) {
+                int k = 0;
+                size_t m = 0;
+                for (size_t i = b0 + nblk * ch / nch; i < b0 + nblk * (ch + 1) / nch; i++) {
+                    k |= lg[i].var_score ? 2 : 1;
+                    m += lg[i].path == 1;
+                }
+                ck[ch] = k;
+                at[ch + 1] = m;
+            });
+            for (size_t ch = 0; ch < nch; ch++) {
+                kinds |= ck[ch];
+                at[ch + 1] += at[ch];
+            }
+            small.resize(at[nch]);
+            wp.run(nch, [&](size_t ch) {
+                size_t o = at[ch];
+                for (size_t i = b0 + nblk * ch / nch; i < b0 + nblk * (ch + 1) / nch; i++)
+                    if (lg[i].path == 1) small[o++] = (uint32_t)i;
+            });
+        } else {
+            for (int i = b0; i < b1; i++) kinds |= lg[i].var_score ? 2 : 1;
+            for (int i = b0; i < b1; i++)
+                if (lg[i].path == 1) small.push_back((uint32_t)i);
+        }
         if (small.size() == (size_t)(b1 - b0)) kinds = 0;  // no search_kernel work
         NKM_HIP(launch_search(st, c.d_groups_.p + b0, b1 - b0, c.d_out_.p, rev ? c.d_rev_.p : nullptr, c.d_res_.p + b0,
                               stream, c.ev_[0], c.ev_[1], kinds));
