@@ -615,7 +615,8 @@ public:
     // win_min_), not every remaining row, since its lists go stale at about
     // the same depth; a batch that runs to its end doubles the window.
     bool win_mode_ = true;
-    bool full_src_mode_ = true;  // NKM_FULLSRC=0: constant-score searches keep their row-count capacity
+    bool full_src_mode_ = true;
+    bool batch_profile_ = false;  // NKM_PROFILE=2: one stderr line per serial batch  // NKM_FULLSRC=0: constant-score searches keep their row-count capacity
     size_t win_min_ = 2048;   // NKM_WIN_MIN
     uint32_t vark_min_ = 64;  // NKM_VARK_MIN: floor of a variable-score search's hit capacity
     bool order_sorted_ = true;

@@ -1507,8 +1507,15 @@ int Core::process_default(GroupList& out_groups,
             }
             done = bi + 1;
         }
-        stats.replay_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb1).count();
+        const auto tb2 = std::chrono::steady_clock::now();
+        stats.replay_ms += std::chrono::duration<double, std::milli>(tb2 - tb1).count();
         apply_selected_to_device(newly);
+        if (batch_profile_)
+            std::fprintf(stderr, "[nkm]   batch %d: rows %zu searches %zu decided %zu%s | assemble %.2f search %.2f replay %.2f ms\n",
+                         stats.batches, brow.size(), bg.size(), done, exhausted ? " (list ran out)" : "",
+                         std::chrono::duration<double, std::milli>(tb0 - ta0).count(),
+                         std::chrono::duration<double, std::milli>(tb1 - tb0).count(),
+                         std::chrono::duration<double, std::milli>(tb2 - tb1).count());
         // advance past the rows this batch decided
         if (exhausted) {
             while (pos < rows.size() && rows[pos] != retry_slot) pos++;
