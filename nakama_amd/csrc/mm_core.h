@@ -523,7 +523,8 @@ private:
                          const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                          GroupList& out_groups,
                          std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats,
-                         bool rev = false);
+                         bool rev, uint32_t* min_stop);
+    std::vector<uint8_t> dec_;  // per pass: rows a parallel replay decided ahead of the pass's row pointer
     void apply_selected_to_device(const std::vector<uint32_t>& slots);
 
     std::mutex mu_;
@@ -616,7 +617,8 @@ public:
     // the same depth; a batch that runs to its end doubles the window.
     bool win_mode_ = true;
     bool full_src_mode_ = true;
-    bool batch_profile_ = false;  // NKM_PROFILE=2: one stderr line per serial batch  // NKM_FULLSRC=0: constant-score searches keep their row-count capacity
+    bool batch_profile_ = false;  // NKM_PROFILE=2: one stderr line per serial batch
+    bool partial_mode_ = true;    // NKM_PARTIAL=0: a batch with a truncated list replays serially  // NKM_FULLSRC=0: constant-score searches keep their row-count capacity
     size_t win_min_ = 2048;   // NKM_WIN_MIN
     uint32_t vark_min_ = 64;  // NKM_VARK_MIN: floor of a variable-score search's hit capacity
     bool order_sorted_ = true;

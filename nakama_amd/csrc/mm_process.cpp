@@ -855,10 +855,17 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
 bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
                            const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                            GroupList& out_groups,
-                           std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats, bool rev) {
+                           std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats, bool rev,
+                           uint32_t* min_stop) {
+    *min_stop = UINT32_MAX;
     if (!P.ok) return false;
-    for (const BGroup& g : bg)
-        if (!g.complete) return false;
+    // Truncated lists are allowed: a pool whose row runs past the end of its
+    // list stops there (the row's search re-runs in the next batch), the other
+    // pools carry on; every row a pool processed is decided (pools never share
+    // a ticket), and the pass puts the groups back in row order at its end.
+    bool all_complete = true;
+    for (const BGroup& g : bg) all_complete = all_complete && g.complete;
+    if (!all_complete && !partial_mode_) return false;
     using clk = std::chrono::steady_clock;
     auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     const auto tp1 = clk::now();
@@ -919,6 +926,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
     std::vector<uint8_t> dense(ng, 0);
     for (size_t gi = 0; gi < ng; gi++) {
         if (soff[gi + 1] - soff[gi] != 1 || !dense_mode_ || rev) continue;  // the dense walk has no reverse checks
+        if (!bg[sidx[soff[gi]]].complete) continue;                        // nor pages
         dense[gi] = 1;
         DensePool& D = dense_pools_[gi];
         D.reset(bg[sidx[soff[gi]]], P.pool_rows.data() + P.pool_off[gi], (uint32_t)prows(gi), brow.data());
@@ -931,6 +939,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
     });
     std::vector<double> task_ms(ntask, 0.0);
     std::vector<uint64_t> task_hits(ntask, 0);
+    std::vector<uint32_t> pool_stop(ng, UINT32_MAX);  // per pool: the batch row its list ran out at
     auto to_rows = [&](const PoolOut& o, uint32_t task, std::vector<std::pair<uint32_t, int>>& ents) {
         const uint32_t base = (uint32_t)ents.size();
         ents.insert(ents.end(), o.ents.begin(), o.ents.end());
@@ -984,9 +993,9 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
                 for (uint32_t j = soff[gi]; j < soff[gi + 1]; j++) mine.push_back(bg[sidx[j]]);
                 rows_of.assign(P.pool_rows.begin() + P.pool_off[gi], P.pool_rows.begin() + P.pool_off[gi + 1]);
                 rp.hits_seen = 0;
-                replay_pool(rp, rows_of, brow.data(),
-                            [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; }, tl_sel,
-                            tl_proc.data(), minc_.data(), maxc_.data(), po);
+                pool_stop[gi] = replay_pool(rp, rows_of, brow.data(),
+                                            [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; },
+                                            tl_sel, tl_proc.data(), minc_.data(), maxc_.data(), po);
                 task_hits[t] += rp.hits_seen;
             }
             if (!few) to_rows(o, (uint32_t)t, ents);
@@ -1000,6 +1009,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
         D.clear_pos(lo, std::min(D.n, lo + kGatherChunk), pos_of_.data());
     });
     const auto tp2 = clk::now();
+    for (uint32_t v : pool_stop) *min_stop = std::min(*min_stop, v);
     const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
     if (few) merge_pools(ng, nch, brow, sel, out_groups, expired, newly);
     else merge_rows(nb, nch, brow, sel, out_groups, expired, newly);
@@ -1047,6 +1057,7 @@ void Core::merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, 
             if (!r.processed) continue;
             const uint32_t T = brow[bi];
             intervals_[T]++;  // the row's pending Intervals increment
+            dec_[T] = 1;      // decided: a later batch of the pass skips it
             if (r.expired) expired[xk++] = T;
             if (!r.matched) continue;
             const auto* src = task_ents_[r.task].data() + r.ent;
@@ -1123,6 +1134,7 @@ void Core::merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow,
             const Rec& r = o.recs[(uint32_t)v];
             const uint32_t T = brow[r.bi];
             intervals_[T]++;  // the row's pending Intervals increment
+            dec_[T] = 1;      // decided: a later batch of the pass skips it
             if (r.expired) expired[xk++] = T;
             if (!r.matched) continue;
             for (uint32_t k = 0; k < r.len; k++) {
@@ -1192,6 +1204,9 @@ int Core::process_default(GroupList& out_groups,
     const uint32_t N = (uint32_t)nslots();
     std::vector<uint8_t>& sel = sel_;
     sel.assign(N, 0);
+    std::vector<uint8_t>& dec = dec_;  // rows decided ahead of `pos` by a partial parallel replay
+    dec.assign(N, 0);
+    bool out_of_order = false;         // groups appended out of row order (sorted at the end)
     bool rev = cfg_.rev_precision != 0;
     RevTimer timer(rev && active_flag_ && cfg_.rev_threshold > 0,
                    (double)cfg_.interval_sec * (double)cfg_.rev_threshold);
@@ -1227,7 +1242,7 @@ int Core::process_default(GroupList& out_groups,
     while (order_head_ < order_.size() && !live_[order_[order_head_]]) order_head_++;
 
     while (true) {
-        while (pos < rows.size() && sel[rows[pos]]) pos++;
+        while (pos < rows.size() && (sel[rows[pos]] | dec[rows[pos]])) pos++;
         if (pos >= rows.size()) break;
         // the RevThreshold timer fired: the remaining rows search as without
         // RevPrecision (row-sharded: decided at batch starts, OR-ed over the ranks)
@@ -1300,7 +1315,7 @@ int Core::process_default(GroupList& out_groups,
                 k.maxm.assign(nsig, 0);
                 for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
                     const uint32_t r = rows[i];
-                    if (sel[r]) continue;
+                    if (sel[r] | dec[r]) continue;
                     const uint32_t sg = sig_[r];
                     if (!k.cnt[sg]++) k.first.push_back(sg);
                     const int32_t m = std::max(2, maxc_[r]);
@@ -1342,7 +1357,7 @@ int Core::process_default(GroupList& out_groups,
                 size_t o = at[c];
                 for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
                     const uint32_t r = rows[i];
-                    if (sel[r]) continue;
+                    if (sel[r] | dec[r]) continue;
                     brow[o] = r;
                     brow_group[o] = (uint32_t)sig_group[sig_[r]];
                     o++;
@@ -1364,7 +1379,7 @@ int Core::process_default(GroupList& out_groups,
             std::vector<size_t> at(nch + 1, 0);
             wp.run(nch, [&](size_t c) {
                 size_t k = 0;
-                for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) k += !sel[rows[i]];
+                for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) k += !(sel[rows[i]] | dec[rows[i]]);
                 at[c + 1] = k;
             });
             for (unsigned c = 0; c < nch; c++) at[c + 1] += at[c];
@@ -1377,7 +1392,7 @@ int Core::process_default(GroupList& out_groups,
                 size_t o = at[c];
                 for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
                     const uint32_t r = rows[i];
-                    if (sel[r]) continue;
+                    if (sel[r] | dec[r]) continue;
                     BGroup& g = bg[o];
                     g.reset();
                     g.sig = sig_[r];
@@ -1422,7 +1437,7 @@ int Core::process_default(GroupList& out_groups,
             uint64_t total_k = 0;
             for (; q < rows.size() && brow.size() < kMaxBatchRows && brow.size() < win; q++) {
                 const uint32_t r = rows[q];
-                if (sel[r]) continue;
+                if (sel[r] | dec[r]) continue;
                 int32_t gi = rev ? -1 : sig_group[sig_[r]];
                 if (gi < 0) {
                     gi = (int32_t)bg.size();
@@ -1465,15 +1480,32 @@ int Core::process_default(GroupList& out_groups,
         newly.clear();
         size_t done = 0;
         bool exhausted = false;
-        if (par_mode_ && replay_parallel(plan, bg, brow, brow_group, sel, out_groups, expired, newly, stats, rev)) {
+        uint32_t stop_bi = UINT32_MAX;
+        if (par_mode_ && replay_parallel(plan, bg, brow, brow_group, sel, out_groups, expired, newly, stats, rev,
+                                         &stop_bi)) {
             stats.parallel_batches++;
             const auto tr = std::chrono::steady_clock::now();
             stats.replay_ms += std::chrono::duration<double, std::milli>(tr - tb1).count();
             apply_selected_to_device(newly);
             stats.apply_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
-            pos = q;
-            retry_slot = kNoSlot;
-            if (win != SIZE_MAX) win *= 2;
+            if (batch_profile_)
+                std::fprintf(stderr, "[nkm]   batch %d (parallel): rows %zu searches %zu%s | search %.2f replay %.2f ms\n",
+                             stats.batches, brow.size(), bg.size(), stop_bi != UINT32_MAX ? " (a list ran out)" : "",
+                             std::chrono::duration<double, std::milli>(tb1 - tb0).count(),
+                             std::chrono::duration<double, std::milli>(tr - tb1).count());
+            if (stop_bi == UINT32_MAX) {
+                pos = q;
+                retry_slot = kNoSlot;
+                if (win != SIZE_MAX) win = win > SIZE_MAX / 2 ? SIZE_MAX : 2 * win;
+            } else {
+                // pools past their stop are decided (dec); the row whose list ran
+                // out re-searches first, the window sized like the serial path's
+                out_of_order = true;
+                retry_slot = brow[stop_bi];
+                while (pos < rows.size() && (sel[rows[pos]] | dec[rows[pos]])) pos++;
+                if (win_mode_) win = std::max(win_min_, 2 * (size_t)stop_bi);
+                vfloor = std::min<uint32_t>(kvar, 2 * vfloor);
+            }
             continue;
         }
         for (size_t bi = 0; bi < brow.size(); bi++) {
@@ -1526,6 +1558,24 @@ int Core::process_default(GroupList& out_groups,
             retry_slot = kNoSlot;
             if (win != SIZE_MAX) win = win > SIZE_MAX / 2 ? SIZE_MAX : 2 * win;
         }
+    }
+    if (out_of_order) {
+        // back into the pinned row order: a group's searching ticket (its last
+        // entry) is the row that formed it
+        std::vector<uint32_t>& rowpos = list_tmp_;
+        grow_to(rowpos, N);
+        for (uint32_t k = 0; k < rows.size(); k++) rowpos[rows[k]] = k;
+        const size_t ng = out_groups.size();
+        std::vector<uint32_t> ord(ng);
+        for (uint32_t g = 0; g < ng; g++) ord[g] = g;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+            return rowpos[out_groups.end(a)[-1].first] < rowpos[out_groups.end(b)[-1].first];
+        });
+        GroupList sorted;
+        sorted.reserve_more(ng, out_groups.ents.size());
+        for (uint32_t g : ord) sorted.push(out_groups.begin(g), out_groups.end(g));
+        std::swap(out_groups.off, sorted.off);
+        std::swap(out_groups.ents, sorted.ents);
     }
     return MM_OK;
 }

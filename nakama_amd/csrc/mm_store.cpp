@@ -96,6 +96,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_WIN")) win_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FULLSRC")) full_src_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_PROFILE")) batch_profile_ = std::strcmp(e, "2") == 0;
+    if (const char* e = std::getenv("NKM_PARTIAL")) partial_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_WIN_MIN")) win_min_ = (size_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("NKM_VARK_MIN")) vark_min_ = (uint32_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("NKM_KERNEL"))

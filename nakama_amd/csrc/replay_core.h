@@ -454,20 +454,26 @@ struct alignas(128) PoolOut {
     std::vector<std::pair<uint32_t, int>> ents;
 };
 
-// Replays one pool's rows (batch rows `bis`, ascending; slot brow[bi]) over
-// complete hit lists: group_of(bi) gives the row's search.  `psel` and `proc`
-// start all zero and are restored to zero on return (the caller's thread
-// keeps them across tasks).  Appends the records + a sentinel to `o`.
+// Replays one pool's rows (batch rows `bis`, ascending; slot brow[bi]):
+// group_of(bi) gives the row's search.  `psel` and `proc` start all zero and
+// are restored to zero on return (the caller's thread keeps them across
+// tasks).  Appends the records + a sentinel to `o`.  A row whose truncated
+// list runs out (EXHAUSTED: its search must re-run after the batch) stops the
+// pool there: returns its batch row, else UINT32_MAX.
 template <class GroupOf>
-void replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uint32_t* brow, GroupOf group_of,
-                 std::vector<uint8_t>& psel, uint8_t* proc, const int32_t* minc, const int32_t* maxc, PoolOut& o) {
+uint32_t replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uint32_t* brow, GroupOf group_of,
+                     std::vector<uint8_t>& psel, uint8_t* proc, const int32_t* minc, const int32_t* maxc, PoolOut& o) {
     std::vector<std::pair<uint32_t, int>> grp;
-    uint32_t gcum = 0, xcum = 0;
+    uint32_t gcum = 0, xcum = 0, stop = UINT32_MAX;
     rp.proc = proc;
     for (uint32_t bi : bis) {
         const uint32_t T = brow[bi];
         if (psel[T]) continue;
-        auto status = rp.decide(T, group_of(bi), false, grp);  // complete lists: never EXHAUSTED
+        auto status = rp.decide(T, group_of(bi), false, grp);
+        if (status == ReplayCore::EXHAUSTED) {
+            stop = bi;
+            break;
+        }
         proc[T] = 1;
         PoolRec rec{bi, 0, (uint8_t)(rp.v.intervals[T] + 1 >= rp.max_intervals || minc[T] == maxc[T]),
                     (uint32_t)o.ents.size(), 0, gcum, xcum};
@@ -486,6 +492,7 @@ void replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uint32_
     for (auto& e : o.ents) psel[e.first] = 0;
     for (const PoolRec& r : o.recs) proc[brow[r.bi]] = 0;
     o.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)o.ents.size(), 0, gcum, xcum});  // sentinel
+    return stop;
 }
 
 // ---- dense pool replay (a pool with one complete search, no RevPrecision) ----

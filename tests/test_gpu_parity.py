@@ -126,6 +126,19 @@ def test_c2_region_lists_past_topk(fullvar, monkeypatch):
     assert (full > 0) if fullvar == "1" else (full == 0)
 
 
+@pytest.mark.parametrize("partial", ["1", "0"])
+def test_c2_partial_parallel_replay(partial, monkeypatch):
+    """Truncated variable-score lists under the pool-parallel replay (forced
+    at 10k): a pool whose row runs past its list stops there and re-searches,
+    the other pools carry on, and the pass restores the reference's group
+    order; NKM_PARTIAL=0 replays such batches serially."""
+    monkeypatch.setenv("NKM_PARALLEL", "force")
+    monkeypatch.setenv("NKM_FULLVAR", "0")
+    monkeypatch.setenv("NKM_PARTIAL", partial)
+    rs = run_passes(2, 10_000, 2, dict(max_intervals=2))
+    assert sum(r.n_batches for r in rs) > 2  # truncated lists restarted batches
+
+
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("config", [3, 4])
 def test_c3_c4_at_6k(config, kernel, monkeypatch):
