@@ -1207,6 +1207,7 @@ int Core::process_default(GroupList& out_groups,
     std::vector<uint8_t>& dec = dec_;  // rows decided ahead of `pos` by a partial parallel replay
     dec.assign(N, 0);
     bool out_of_order = false;         // groups appended out of row order (sorted at the end)
+    std::vector<uint32_t>& rowpos = list_tmp_;  // slot -> pinned position (set when out_of_order)
     bool rev = cfg_.rev_precision != 0;
     RevTimer timer(rev && active_flag_ && cfg_.rev_threshold > 0,
                    (double)cfg_.interval_sec * (double)cfg_.rev_threshold);
@@ -1500,9 +1501,17 @@ int Core::process_default(GroupList& out_groups,
             } else {
                 // pools past their stop are decided (dec); the row whose list ran
                 // out re-searches first, the window sized like the serial path's
+                if (!out_of_order) {  // the pinned positions, for the final reorder
+                    grow_to(rowpos, N);
+                    for (uint32_t k = 0; k < rows.size(); k++) rowpos[rows[k]] = k;
+                }
                 out_of_order = true;
                 retry_slot = brow[stop_bi];
-                while (pos < rows.size() && (sel[rows[pos]] | dec[rows[pos]])) pos++;
+                // the rest of the pass skips decided and selected rows for good
+                size_t w = pos;
+                for (size_t k = pos; k < rows.size(); k++)
+                    if (!(sel[rows[k]] | dec[rows[k]])) rows[w++] = rows[k];
+                rows.resize(w);
                 if (win_mode_) win = std::max(win_min_, 2 * (size_t)stop_bi);
                 vfloor = std::min<uint32_t>(kvar, 2 * vfloor);
             }
@@ -1562,9 +1571,6 @@ int Core::process_default(GroupList& out_groups,
     if (out_of_order) {
         // back into the pinned row order: a group's searching ticket (its last
         // entry) is the row that formed it
-        std::vector<uint32_t>& rowpos = list_tmp_;
-        grow_to(rowpos, N);
-        for (uint32_t k = 0; k < rows.size(); k++) rowpos[rows[k]] = k;
         const size_t ng = out_groups.size();
         std::vector<uint32_t> ord(ng);
         for (uint32_t g = 0; g < ng; g++) ord[g] = g;
