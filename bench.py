@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--override", action="store_true",
                     help="register a MatchmakerOverride (processCustom path): the timed step is the candidate pass, "
-                         "a native first-disjoint override and mm_process_commit (single GPU)")
+                         "a native first-disjoint override and mm_process_commit (per rank under the cluster front)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_traffic.json"))
     a = ap.parse_args()
     if a.tickets is None:
@@ -211,8 +211,6 @@ def main():
     import torch
 
     # SURVEY 8(d) harness pins: MaxIntervals=2, RevThreshold=0 (no wall-clock cutoff)
-    if args.override and world > 1:
-        raise SystemExit("--override runs on one GPU (the cluster front merges processDefault groups)")
     from nakama_amd import synth
     mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config == 5, rev_threshold=0,
                                     override=(lambda groups: groups) if args.override else None)
@@ -220,7 +218,8 @@ def main():
     if world > 1:
         from nakama_amd import cluster
         cm = cluster.ClusterMatchmaker(mm, pg, POOL_FIELDS[args.config],
-                                       comm_device=torch.device("cuda", local) if backend == "nccl" else None)
+                                       comm_device=torch.device("cuda", local) if backend == "nccl" else None,
+                                       override_commit=synth.override_commit if args.override else None)
     times, matched_all, presences_all, ins_times, searched = [], [], [], [], []
     eval_ms = eval_bytes = launches = 0
     batches, kernels, unroutable = [], set(), 0

@@ -427,6 +427,23 @@ class Matchmaker:
         dt = time.perf_counter() - t0
         return (dt,) + self.process_summary(out)
 
+    def commit_call(self, groups: Sequence[Sequence[Tuple[str, int]]]):
+        """mm_process_commit of (ticket, presence index) groups; returns the
+        library-owned result (free it with the library's mm_free_matched)."""
+        offs = [0]
+        ents = []
+        for g in groups:
+            ents.extend(g)
+            offs.append(len(ents))
+        off_arr = (C.c_int32 * len(offs))(*offs)
+        keep = [_b(t) for t, _ in ents]
+        ent_arr = (mm_entry_ref * max(1, len(ents)))()
+        for i, (t, pi) in enumerate(ents):
+            ent_arr[i] = mm_entry_ref(keep[i], pi, 0)
+        out = mm_matched()
+        self._check(self.lib.mm_process_commit(self.h, off_arr, ent_arr, len(groups), C.byref(out)))
+        return out
+
     def commit(self, groups: Sequence[Sequence[Tuple[str, int]]]) -> ProcessResult:
         offs = [0]
         ents = []

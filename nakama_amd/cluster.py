@@ -143,7 +143,16 @@ class ClusterMatchmaker:
     (initialised); pool_fields: the query fields a pool is keyed on, e.g.
     ("properties.mode", "properties.region")."""
 
-    def __init__(self, local: capi.Matchmaker, dist, pool_fields: Sequence[str], *, comm_device=None):
+    def __init__(self, local: capi.Matchmaker, dist, pool_fields: Sequence[str], *, comm_device=None,
+                 override_commit=None):
+        """override_commit(local, candidates) -> committed result: with a
+        MatchmakerOverride registered, the rank's hand-off of its processCustom
+        candidates (frees them; returns mm_process_commit's library-owned
+        result); default: local.override over the candidates as Python
+        groups, then mm_process_commit.  The override runs per rank on that
+        rank's candidates — exact for overrides that decide each pool on its
+        own (a candidate group never spans pools), such as first-disjoint."""
+        self.override_commit = override_commit
         self.local = local
         self.dist = dist
         self.rank = dist.get_rank()
@@ -255,6 +264,8 @@ class ClusterMatchmaker:
         import time
         t0 = time.perf_counter()
         out = self.local.process_call()
+        if out.is_candidates:  # processCustom: this rank's override hand-off
+            out = self._override(out)
         t1 = time.perf_counter()
         try:
             ng = out.n_groups
@@ -298,6 +309,16 @@ class ClusterMatchmaker:
                           "eval_kernel": stats.eval_kernel, "local_call_ms": 1e3 * (t1 - t0),
                           "summary_ms": 1e3 * (t2 - t1), "merge_ms": 1e3 * (t3 - t2)}
         return cp
+
+    def _override(self, out):
+        if self.override_commit is not None:
+            return self.override_commit(self.local, out)
+        try:
+            cands = capi.Matchmaker._groups(out)
+        finally:
+            self.local.lib.mm_free_matched(self.local.h, C.byref(out))
+        chosen = self.local.override(cands) if self.local.override is not None else []
+        return self.local.commit_call(chosen)
 
     def _order_ties(self, cp: ClusterPass, allk: np.ndarray, counts: np.ndarray, tie_ids):
         """Equal CreatedAt on two ranks: those groups are ordered by their

@@ -27,6 +27,18 @@ POOL_FIELDS = {3: ("properties.mode", "properties.region"), 4: ("properties.mode
                5: ("properties.bucket",), 1: ("properties.mode", "properties.region")}
 
 
+def first_disjoint(groups):
+    """A MatchmakerOverride that decides each pool on its own: keep every
+    candidate none of whose tickets an earlier kept one holds."""
+    taken, kept = set(), []
+    for g in groups:
+        ts = {t for t, _ in g}
+        if not ts & taken:
+            taken |= ts
+            kept.append(g)
+    return kept
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -75,8 +87,13 @@ def cluster_worker(rank, world, port, config, n, groups, passes, cfg, use_produc
             lib = nakama_amd.load_library()
         else:
             lib = harness.oracle_lib()
+        cfg = dict(cfg)
+        native = cfg.pop("native_override", False)
         mm = capi.Matchmaker(lib, **cfg)
-        cm = cluster.ClusterMatchmaker(mm, dist, POOL_FIELDS[config])
+        if native:
+            from nakama_amd import synth
+        cm = cluster.ClusterMatchmaker(mm, dist, POOL_FIELDS[config],
+                                       override_commit=synth.override_commit if native else None)
         ts = _make(config, n, world, rank, groups, ties)
         bad = cm.Insert(ts.ptr(), ts.n)
         bad_ids = [ts.ticket_id(int(k)) for k in bad]
@@ -151,6 +168,23 @@ def test_cluster_pass_equals_single_pass(config, n, groups, passes):
     for (merged, state, active, ng, matched), (g, st, act) in zip(out, want):
         assert merged == g
         assert ng == len(g) and matched == len({t for grp in g for t, _ in grp})
+        assert state == st and active == act
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_cluster_override_equals_single_override(native):
+    """C5 with a MatchmakerOverride: each rank hands its processCustom
+    candidates to the override and commits; the merged groups and the
+    post-pass state equal one matchmaker's pass with the same override.
+    native: the bench's hand-off (tools/synth.cpp first-disjoint over the raw
+    candidate result, then mm_process_commit) instead of the Python one."""
+    cfg = dict(max_intervals=2, rev_precision=True, rev_threshold=0, override=first_disjoint)
+    out, bad, loads = run_cluster(5, 640, 0, 2, dict(cfg, native_override=native))
+    assert bad == [] and min(loads) > 0
+    want = single_pass(5, 640, 0, 2, cfg)
+    assert sum(len(g) for g, _, _ in want) > 0
+    for (merged, state, active, ng, matched), (g, st, act) in zip(out, want):
+        assert merged == g
         assert state == st and active == act
 
 
