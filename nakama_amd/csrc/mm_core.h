@@ -41,6 +41,11 @@ int small_src_max();
 hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_t n, hipStream_t stream,
                               uint8_t value = 0);
 hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, uint8_t* d_out, hipStream_t stream);
+// enum_kernel: d_base == nullptr -> the count pass (2 words per item into
+// d_cnt); else the write pass (entries as word pairs, group ends + e0).
+hipError_t launch_enum(const DEnumRow* d_rows, const DEnumHit* d_hits, const DEnumItem* d_items, uint32_t n_items,
+                       uint32_t* d_cnt, const uint64_t* d_base, uint32_t e0, uint32_t* d_ents, uint32_t* d_off,
+                       hipStream_t stream);
 int var_k_capacity();
 hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, DHit* d_scratch, DGroupResult* d_cres,
                        hipStream_t stream, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
@@ -618,7 +623,8 @@ public:
     bool win_mode_ = true;
     bool full_src_mode_ = true;
     bool batch_profile_ = false;  // NKM_PROFILE=2: one stderr line per serial batch
-    bool partial_mode_ = true;    // NKM_PARTIAL=0: a batch with a truncated list replays serially  // NKM_FULLSRC=0: constant-score searches keep their row-count capacity
+    bool partial_mode_ = true;    // NKM_PARTIAL=0: a batch with a truncated list replays serially
+    bool dev_enum_mode_ = true;   // NKM_DEVENUM=0: processCustom enumerates its subsets on the host
     size_t win_min_ = 2048;   // NKM_WIN_MIN
     uint32_t vark_min_ = 64;  // NKM_VARK_MIN: floor of a variable-score search's hit capacity
     bool order_sorted_ = true;
@@ -728,6 +734,18 @@ public:
     std::atomic<bool> out_in_use_{false};
     DevArray<uint32_t> d_pm_;      // pair matrices (RevPrecision combos)
     PinnedArray<uint32_t> h_pm_;
+    // processCustom's device enumeration (enum_kernel): rows, hits, work items,
+    // per-item counts and scanned bases, the candidates' entries and group ends
+    DevArray<DEnumRow> d_erows_;
+    DevArray<DEnumHit> d_ehits_;
+    DevArray<DEnumItem> d_eitems_;
+    DevArray<uint32_t> d_ecnt_, d_eents_, d_eoff_;
+    DevArray<uint64_t> d_ebase_;
+    PinnedArray<DEnumRow> h_erows_;
+    PinnedArray<DEnumHit> h_ehits_;
+    PinnedArray<DEnumItem> h_eitems_;
+    PinnedArray<uint32_t> h_ecnt_;
+    PinnedArray<uint64_t> h_ebase_;
 };
 
 }  // namespace nkm

@@ -4,6 +4,14 @@
 #pragma once
 #include <cstdint>
 
+// Helpers below compile for both sides in the kernels' translation unit and
+// as plain host functions elsewhere.
+#if defined(__HIPCC__)
+#define NKM_HD __host__ __device__
+#else
+#define NKM_HD
+#endif
+
 namespace nkm {
 
 constexpr uint32_t kNoParty = 0xFFFFFFFFu;
@@ -131,5 +139,70 @@ struct DHit {
     uint32_t idx;   // position in the group's source (tie-break / cursor)
     int64_t key;    // sortable score key (tie-break / cursor); bit 0 of flags below
 };
+
+// ---- processCustom's combineIndexes on the device (enum_kernel) -------------
+// combineIndexes (matchmaker_process.go:578-612) walks the bitmasks of a row's
+// L filtered hits in ascending order; every mask with more than
+// Max - Count bits is rejected by its first test (each hit holds >= 1 entry),
+// so the masks that reach the remaining tests are exactly those with at most
+// c = min(Max - Count, L) bits, in ascending order.  Rank r of that sequence
+// (mask 0 = rank 0) is found by unrank_mask; a work item takes kEnumSpan
+// consecutive ranks of one row.
+
+// One searching row (T) of the pass.
+struct DEnumRow {
+    uint32_t hit_off;  // its first DEnumHit
+    uint32_t T;        // its slot
+    int32_t L;         // filtered hits (1..62)
+    int32_t tcount;    // T's entries
+    int32_t cmin, cmax;  // entries the hits may add: [Min - Count, Max - Count]
+    int32_t tmin, tmax, tcm;
+    int32_t pad;
+};
+static_assert(sizeof(DEnumRow) == 40, "DEnumRow is 40 bytes");
+
+// One filtered hit of a row, with what the member checks read (:487-498).
+struct DEnumHit {
+    uint64_t pm;   // bit b: validateMatch holds both ways with hit b (all ones without RevPrecision)
+    uint32_t slot;
+    int32_t count, minc, maxc, cm;
+    uint8_t wait;     // Intervals <= MaxIntervals (the member waits for a fuller group)
+    uint8_t self_ok;  // a hit with >= 2 sessions meets itself in parsedQueries (:509-546): its own query must match it
+    uint8_t pad[2];
+};
+static_assert(sizeof(DEnumHit) == 32, "DEnumHit is 32 bytes");
+
+struct DEnumItem {
+    uint64_t rank;  // first rank (>= 1: the empty mask is never a candidate)
+    uint32_t row;
+    uint32_t n;     // ranks [rank, rank + n), n <= kEnumSpan
+};
+
+constexpr uint32_t kEnumSpan = 256;  // masks per work item
+
+// Number of L-bit masks with at most c bits set: sum_{k <= min(c, L)} C(L, k)
+// (L <= 62: every partial product fits 64 bits).
+NKM_HD inline uint64_t masks_le(int L, int c) {
+    uint64_t s = 0, b = 1;
+    for (int k = 0; k <= c && k <= L; k++) {
+        s += b;
+        b = b * (uint64_t)(L - k) / (uint64_t)(k + 1);
+    }
+    return s;
+}
+
+// The mask of rank r among the L-bit masks with at most c bits, ascending.
+NKM_HD inline uint64_t unrank_mask(uint64_t r, int L, int c) {
+    uint64_t m = 0;
+    for (int p = L - 1; p >= 0 && r > 0; p--) {
+        const uint64_t below = masks_le(p, c);  // those with bit p clear (the bits above fixed)
+        if (r >= below) {
+            m |= 1ull << p;
+            r -= below;
+            c--;
+        }
+    }
+    return m;
+}
 
 }  // namespace nkm

@@ -676,6 +676,82 @@ __global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restr
     }
 }
 
+// processCustom's candidate enumeration (combineIndexes, matchmaker_process.go:
+// 578-612, and the checks :470-546 applied to each subset), one thread per work
+// item (a run of kEnumSpan masks of one row, mm_device.h).  COUNT: the item's
+// candidate and entry counts -> cnt[2 item], cnt[2 item + 1].  Otherwise the
+// item's candidates at the bases the host scanned from those counts: entries
+// as (slot, presence index) word pairs — the hits in ascending bit order, each
+// with all its presences, then T's — and every group's end offset (+ e0).
+// Sessions are exclusive on this path (no two live tickets share one), so the
+// pairwise session test (:509-519) never rejects; the mutual validateMatch
+// test is a mask test: every member's pm covers the other members.
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock) void enum_kernel(const DEnumRow* __restrict__ rows,
+                                                      const DEnumHit* __restrict__ hits,
+                                                      const DEnumItem* __restrict__ items, uint32_t n_items,
+                                                      uint32_t* __restrict__ cnt, const uint64_t* __restrict__ base,
+                                                      uint32_t e0, uint32_t* __restrict__ ents,
+                                                      uint32_t* __restrict__ off) {
+    const uint32_t it = blockIdx.x * kBlock + threadIdx.x;
+    if (it >= n_items) return;
+    const DEnumItem item = items[it];
+    const DEnumRow row = rows[item.row];
+    const DEnumHit* __restrict__ h = hits + row.hit_off;
+    const int c = row.cmax < row.L ? row.cmax : row.L;
+    uint64_t m = unrank_mask(item.rank, row.L, c);
+    uint32_t ng = 0, ne = 0;
+    uint64_t gk = 0, ek = 0;
+    if (!COUNT) {
+        gk = base[2 * (size_t)it];
+        ek = base[2 * (size_t)it + 1];
+    }
+    for (uint32_t s = 0; s < item.n; s++) {
+        if (s) {  // the next mask with at most c bits
+            m++;
+            while (__popcll(m) > c) m += m & (~m + 1);
+        }
+        int entries = 0;  // :593-600
+        bool over = false;
+        for (uint64_t b = m; b; b &= b - 1) {
+            entries += h[__builtin_ctzll(b)].count;
+            if (entries > row.cmax) { over = true; break; }
+        }
+        if (over || entries < row.cmin) continue;
+        const int hc = entries + row.tcount;  // :470-486
+        if (hc > row.tmax || hc < row.tmin || hc % row.tcm != 0) continue;
+        bool ok = true;
+        for (uint64_t b = m; b && ok; b &= b - 1) {  // :487-498, :520-546
+            const int el = __builtin_ctzll(b);
+            const DEnumHit& e = h[el];
+            ok = !(hc > e.maxc || hc < e.minc || hc % e.cm != 0 || (hc < e.maxc && e.wait)) && e.self_ok &&
+                 ((e.pm | (1ull << el)) & m) == m;
+        }
+        if (!ok) continue;
+        if (COUNT) {
+            ng++;
+            ne += (uint32_t)hc;
+            continue;
+        }
+        for (uint64_t b = m; b; b &= b - 1) {
+            const DEnumHit& e = h[__builtin_ctzll(b)];
+            for (int k = 0; k < e.count; k++, ek++) {
+                ents[2 * ek] = e.slot;
+                ents[2 * ek + 1] = (uint32_t)k;
+            }
+        }
+        for (int k = 0; k < row.tcount; k++, ek++) {
+            ents[2 * ek] = row.T;
+            ents[2 * ek + 1] = (uint32_t)k;
+        }
+        off[gk++] = e0 + (uint32_t)ek;
+    }
+    if (COUNT) {
+        cnt[2 * (size_t)it] = ng;
+        cnt[2 * (size_t)it + 1] = ne;
+    }
+}
+
 // Sets the device alive flag of the listed slots (0: selected / removed; 1:
 // restored, for the members of a group the post-pass re-check dropped).
 __global__ void clear_alive_kernel(uint8_t* __restrict__ alive, const uint32_t* __restrict__ slots, uint32_t n,
@@ -834,6 +910,20 @@ hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_
                               uint8_t value) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(clear_alive_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_alive, d_slots, n, value);
+    return hipGetLastError();
+}
+
+hipError_t launch_enum(const DEnumRow* d_rows, const DEnumHit* d_hits, const DEnumItem* d_items, uint32_t n_items,
+                       uint32_t* d_cnt, const uint64_t* d_base, uint32_t e0, uint32_t* d_ents, uint32_t* d_off,
+                       hipStream_t stream) {
+    if (n_items == 0) return hipSuccess;
+    const dim3 grid((n_items + kBlock - 1) / kBlock);
+    if (d_base == nullptr)
+        hipLaunchKernelGGL(enum_kernel<true>, grid, dim3(kBlock), 0, stream, d_rows, d_hits, d_items, n_items, d_cnt,
+                           nullptr, 0u, nullptr, nullptr);
+    else
+        hipLaunchKernelGGL(enum_kernel<false>, grid, dim3(kBlock), 0, stream, d_rows, d_hits, d_items, n_items, nullptr,
+                           d_base, e0, d_ents, d_off);
     return hipGetLastError();
 }
 

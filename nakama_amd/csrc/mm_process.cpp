@@ -1661,7 +1661,9 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
             std::vector<uint8_t> po;
             std::vector<std::pair<uint32_t, int>> me;
         };
-        auto do_row = [&](size_t i, GroupList& out, Scratch& sc, bool row_rev) {
+        // The row's filtered hits (:425-468) and, with RevPrecision, their
+        // pairwise validateMatch masks; false: the row yields no candidates.
+        auto filter_row = [&](size_t i, Scratch& sc, bool row_rev, int& cmin, int& cmax) -> bool {
             BGroup& g = bg[i];
             const uint32_t T = g.row_slot;
             // all hits (paging through the list), filtered as :425-468
@@ -1693,10 +1695,11 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                 if (hits.size() >= 63) { too_many = true; break; }
             }
             // combineIndexes: Go's `1 << length` is 0 / negative for length >= 63 -> no subsets
-            if (too_many) return;
+            if (too_many) return false;
             const size_t L = hits.size();
-            const int cmin = minc_[T] - count_[T], cmax = maxc_[T] - count_[T];
-            if (L == 0 || cmax <= 0) return;  // every subset holds >= 1 ticket > max: none emitted
+            cmin = minc_[T] - count_[T];
+            cmax = maxc_[T] - count_[T];
+            if (L == 0 || cmax <= 0) return false;  // every subset holds >= 1 ticket > max: none emitted
             // pairwise reverse checks among the hits (validateMatch both ways, incl. self)
             std::vector<uint64_t>& pm = sc.pm;
             pm.clear();
@@ -1728,6 +1731,15 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                     for (size_t b = 0; b < L; b++)
                         if (sc.po[a * L + b]) pm[a] |= 1ull << b;
             }
+            return true;
+        };
+        auto do_row = [&](size_t i, GroupList& out, Scratch& sc, bool row_rev) {
+            int cmin, cmax;
+            if (!filter_row(i, sc, row_rev, cmin, cmax)) return;
+            const uint32_t T = bg[i].row_slot;
+            const std::vector<uint32_t>& hits = sc.hits;
+            const std::vector<uint64_t>& pm = sc.pm;
+            const size_t L = hits.size();
             const uint64_t limit = 1ull << L;
             std::vector<uint32_t>& combo = sc.combo;
             // combineIndexes' ascending bitmask loop (:586-610), visiting only
@@ -1789,7 +1801,131 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
             }
         };
         const bool timer_live = rev && !row_shard() && timer.armed && !timer.fired;
-        if (par && !timer_live) {
+        if (dev_enum_mode_ && !timer_live && Replay::view(*this).sessions_exclusive) {
+            // Device enumeration (enum_kernel): the rows' filtered hits are
+            // gathered on the workers and every row's masks are cut into work
+            // items; a count pass, the host's scan of the counts, and a write
+            // pass straight into the candidate list (row order, masks
+            // ascending, as the host loop below appends them).
+            struct EnumChunk {
+                std::vector<DEnumRow> rows;
+                std::vector<DEnumHit> hits;
+                std::vector<DEnumItem> items;
+            };
+            WorkPool& wp = workers();
+            const size_t nch = par ? (size_t)wp.size() * 4 : 1;
+            std::vector<EnumChunk> ec(nch);
+            std::vector<uint8_t> huge(nch, 0);
+            auto gather = [&](size_t c) {
+                Scratch sc;
+                EnumChunk& E = ec[c];
+                for (size_t i = bg.size() * c / nch; i < bg.size() * (c + 1) / nch; i++) {
+                    int cmin, cmax;
+                    if (!filter_row(i, sc, rev, cmin, cmax)) continue;
+                    const uint32_t T = bg[i].row_slot;
+                    const int L = (int)sc.hits.size();
+                    const uint64_t V = masks_le(L, std::min(cmax, L));  // ranks 1 .. V-1 (rank 0: the empty mask)
+                    if ((V - 1) / kEnumSpan >= (1ull << 26)) {
+                        huge[c] = 1;
+                        return;
+                    }
+                    const uint32_t r = (uint32_t)E.rows.size();
+                    E.rows.push_back(DEnumRow{(uint32_t)E.hits.size(), T, L, (int32_t)count_[T], cmin, cmax,
+                                              (int32_t)minc_[T], (int32_t)maxc_[T], (int32_t)cm_[T], 0});
+                    for (int el = 0; el < L; el++) {
+                        const uint32_t h = sc.hits[el];
+                        DEnumHit d{};
+                        d.pm = rev ? sc.pm[el] : ~0ull;
+                        d.slot = h;
+                        d.count = (int32_t)count_[h];
+                        d.minc = (int32_t)minc_[h];
+                        d.maxc = (int32_t)maxc_[h];
+                        d.cm = (int32_t)cm_[h];
+                        d.wait = intervals_[h] <= maxI;
+                        bool multi = false;  // two distinct sessions (SessionIDs is a set)
+                        for (uint32_t p = pres_off_[h] + 1; p < pres_off_[h + 1] && !multi; p++)
+                            multi = pres_sess_[p] != pres_sess_[pres_off_[h]];
+                        d.self_ok = !rev || !multi || ((sc.pm[el] >> el) & 1ull);
+                        E.hits.push_back(d);
+                    }
+                    for (uint64_t r0 = 1; r0 < V; r0 += kEnumSpan)
+                        E.items.push_back(DEnumItem{r0, r, (uint32_t)std::min<uint64_t>(kEnumSpan, V - r0)});
+                }
+            };
+            if (nch > 1) wp.run(nch, gather);
+            else gather(0);
+            for (uint8_t x : huge)
+                if (x) throw std::length_error("processCustom: a row's subsets exceed the enumeration limit");
+            std::vector<size_t> rb(nch + 1, 0), hb(nch + 1, 0), ib(nch + 1, 0);
+            for (size_t c = 0; c < nch; c++) {
+                rb[c + 1] = rb[c] + ec[c].rows.size();
+                hb[c + 1] = hb[c] + ec[c].hits.size();
+                ib[c + 1] = ib[c] + ec[c].items.size();
+            }
+            const size_t nrow = rb[nch], nhit = hb[nch], nitem = ib[nch];
+            if (nhit >= UINT32_MAX || nitem >= UINT32_MAX)
+                throw std::length_error("processCustom: too many enumeration items");
+            if (nitem) {
+                h_erows_.reserve(nrow);
+                h_ehits_.reserve(nhit);
+                h_eitems_.reserve(nitem);
+                auto pack = [&](size_t c) {
+                    const EnumChunk& E = ec[c];
+                    for (size_t k = 0; k < E.rows.size(); k++) {
+                        DEnumRow r = E.rows[k];
+                        r.hit_off += (uint32_t)hb[c];
+                        h_erows_.p[rb[c] + k] = r;
+                    }
+                    if (!E.hits.empty()) std::memcpy(h_ehits_.p + hb[c], E.hits.data(), E.hits.size() * sizeof(DEnumHit));
+                    for (size_t k = 0; k < E.items.size(); k++) {
+                        DEnumItem it = E.items[k];
+                        it.row += (uint32_t)rb[c];
+                        h_eitems_.p[ib[c] + k] = it;
+                    }
+                };
+                if (nch > 1) wp.run(nch, pack);
+                else pack(0);
+                d_erows_.reserve(nrow, false);
+                d_ehits_.reserve(nhit, false);
+                d_eitems_.reserve(nitem, false);
+                d_ecnt_.reserve(2 * nitem, false);
+                h_ecnt_.reserve(2 * nitem);
+                NKM_HIP(hipMemcpyAsync(d_erows_.p, h_erows_.p, nrow * sizeof(DEnumRow), hipMemcpyHostToDevice, stream_));
+                NKM_HIP(hipMemcpyAsync(d_ehits_.p, h_ehits_.p, nhit * sizeof(DEnumHit), hipMemcpyHostToDevice, stream_));
+                NKM_HIP(hipMemcpyAsync(d_eitems_.p, h_eitems_.p, nitem * sizeof(DEnumItem), hipMemcpyHostToDevice, stream_));
+                NKM_HIP(launch_enum(d_erows_.p, d_ehits_.p, d_eitems_.p, (uint32_t)nitem, d_ecnt_.p, nullptr, 0, nullptr,
+                                    nullptr, stream_));
+                NKM_HIP(hipMemcpyAsync(h_ecnt_.p, d_ecnt_.p, 2 * nitem * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+                NKM_HIP(hipStreamSynchronize(stream_));
+                h_ebase_.reserve(2 * nitem);  // exclusive scan: every item's first group and entry
+                uint64_t G = 0, E = 0;
+                for (size_t k = 0; k < nitem; k++) {
+                    h_ebase_.p[2 * k] = G;
+                    h_ebase_.p[2 * k + 1] = E;
+                    G += h_ecnt_.p[2 * k];
+                    E += h_ecnt_.p[2 * k + 1];
+                }
+                const size_t g0 = cands.size(), e0 = cands.ents.size();
+                if (e0 + E >= UINT32_MAX) throw std::length_error("processCustom: more than 2^32 candidate entries");
+                if (G) {
+                    static_assert(sizeof(GroupList::Entry) == 8, "(slot, presence index) word pairs");
+                    d_ebase_.reserve(2 * nitem, false);
+                    d_eents_.reserve(2 * E, false);
+                    d_eoff_.reserve(G, false);
+                    NKM_HIP(hipMemcpyAsync(d_ebase_.p, h_ebase_.p, 2 * nitem * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                           stream_));
+                    NKM_HIP(launch_enum(d_erows_.p, d_ehits_.p, d_eitems_.p, (uint32_t)nitem, nullptr, d_ebase_.p,
+                                        (uint32_t)e0, d_eents_.p, d_eoff_.p, stream_));
+                    grow_to(cands.ents, e0 + E);
+                    grow_to(cands.off, g0 + 1 + G);
+                    NKM_HIP(hipMemcpyAsync(cands.ents.data() + e0, d_eents_.p, E * sizeof(GroupList::Entry),
+                                           hipMemcpyDeviceToHost, stream_));
+                    NKM_HIP(hipMemcpyAsync(cands.off.data() + g0 + 1, d_eoff_.p, G * sizeof(uint32_t),
+                                           hipMemcpyDeviceToHost, stream_));
+                    NKM_HIP(hipStreamSynchronize(stream_));
+                }
+            }
+        } else if (par && !timer_live) {
             WorkPool& wp = workers();
             const size_t nch = (size_t)wp.size() * 4;
             std::vector<GroupList> outs(nch);
@@ -2124,14 +2260,29 @@ int Core::process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t 
     // the mutations queued while the pass was open come first: a chosen
     // group that lost a ticket is then dropped by the re-check (:326-341)
     apply_pending();
+    // the chosen groups' entries back to slots (a ticket no longer known
+    // becomes kNoSlot: its group fails the re-check), on the workers
+    for (int g = 0; g < n_groups; g++)
+        if (offs[g + 1] < offs[g]) return MM_ERR_ARG;
     GroupList groups;
-    for (int g = 0; g < n_groups; g++) {
-        std::vector<std::pair<uint32_t, int>> grp;
-        for (int k = offs[g]; k < offs[g + 1]; k++) {
-            int64_t s = slot_of_ticket(ents[k].ticket ? ents[k].ticket : "");
-            grp.push_back({s < 0 ? kNoSlot : (uint32_t)s, ents[k].presence_index});
+    const int32_t o0 = n_groups > 0 ? offs[0] : 0;
+    const size_t ne = n_groups > 0 ? (size_t)(offs[n_groups] - o0) : 0;
+    groups.off.resize((size_t)n_groups + 1);
+    for (int g = 0; g <= n_groups; g++) groups.off[g] = (uint32_t)(n_groups > 0 ? offs[g] - o0 : 0);
+    groups.ents.resize(ne);
+    auto look = [&](size_t lo, size_t hi) {
+        for (size_t k = lo; k < hi; k++) {
+            const mm_entry_ref& e = ents[o0 + k];
+            const int64_t s = slot_of_ticket(e.ticket ? e.ticket : "");
+            groups.ents[k] = {s < 0 ? kNoSlot : (uint32_t)s, e.presence_index};
         }
-        groups.push(grp);
+    };
+    if (par_mode_ && ne >= par_min(65536)) {
+        WorkPool& wp = workers();
+        const size_t nch = (size_t)wp.size() * 4;
+        wp.run(nch, [&](size_t c) { look(ne * c / nch, ne * (c + 1) / nch); });
+    } else {
+        look(0, ne);
     }
     // processCustom never deletes from the index during the pass; matched
     // tickets leave it here (their zombie documents would be filtered as

@@ -75,6 +75,14 @@ template struct PinnedArray<DHit>;
 template struct PinnedArray<uint8_t>;
 template struct PinnedArray<DGroupResult>;
 template struct PinnedArray<uint32_t>;
+template struct DevArray<uint64_t>;
+template struct DevArray<DEnumRow>;
+template struct DevArray<DEnumHit>;
+template struct DevArray<DEnumItem>;
+template struct PinnedArray<uint64_t>;
+template struct PinnedArray<DEnumRow>;
+template struct PinnedArray<DEnumHit>;
+template struct PinnedArray<DEnumItem>;
 
 static const char* kBuiltinNames[F_NBUILTIN] = {"ticket", "min_count", "max_count", "party_id", "created_at"};
 
@@ -97,6 +105,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_FULLSRC")) full_src_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_PROFILE")) batch_profile_ = std::strcmp(e, "2") == 0;
     if (const char* e = std::getenv("NKM_PARTIAL")) partial_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_DEVENUM")) dev_enum_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_WIN_MIN")) win_min_ = (size_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("NKM_VARK_MIN")) vark_min_ = (uint32_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("NKM_KERNEL"))

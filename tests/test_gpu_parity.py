@@ -241,10 +241,15 @@ def first_disjoint(cands):
     return out
 
 
-@pytest.mark.parametrize("n", [400, 5000])
-def test_c5_override_candidates(n):
-    """processCustom candidates (RevPrecision, buckets of 8) handed to the
-    deterministic first-disjoint override of SURVEY 8(d) C5, then committed."""
+@pytest.mark.parametrize("config,n,devenum", [(5, 400, "1"), (5, 5000, "1"), (5, 5000, "0"), (6, 100, "1"),
+                                               (6, 100, "0"), (7, 300, "1")])
+def test_c5_override_candidates(config, n, devenum, monkeypatch):
+    """processCustom candidates (RevPrecision; C5's buckets of 8, config 6's
+    parties, count ranges and CountMultiple — 81k candidates per pass at 100
+    tickets — and config 7's multi-term queries) handed to the deterministic
+    first-disjoint override of SURVEY 8(d) C5, then committed.  NKM_DEVENUM:
+    the subsets enumerated by enum_kernel (1) or on the host (0)."""
+    monkeypatch.setenv("NKM_DEVENUM", devenum)
     seen = {}
 
     def rec(tag):
@@ -253,7 +258,7 @@ def test_c5_override_candidates(n):
             return first_disjoint(c)
         return f
 
-    ts = synth.TicketSet(5, n)
+    ts = synth.TicketSet(config, n)
     gpu = capi.Matchmaker(product_lib(), override=rec("g"), max_intervals=2, rev_precision=True)
     orc = capi.Matchmaker(harness.oracle_lib(), override=rec("o"), max_intervals=2, rev_precision=True)
     try:
@@ -544,7 +549,9 @@ def _custom_many_hits(lib, n_tickets):
         mm.close()
 
 
-def test_custom_rows_past_40_hits():
+@pytest.mark.parametrize("devenum", ["1", "0"])
+def test_custom_rows_past_40_hits(devenum, monkeypatch):
+    monkeypatch.setenv("NKM_DEVENUM", devenum)
     n = 51
     cands = _custom_many_hits(product_lib(), n)
     assert len(cands) == n * (n - 1) * (n - 2) // 2

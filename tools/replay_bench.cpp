@@ -130,7 +130,7 @@ int main(int argc, char** argv) {
         DensePool P;
         DenseRun run;
         BGroup g;
-        g.hits = ph[0].data();
+        g.set_hits(ph[0].data());
         g.n = (uint32_t)ph[0].size();
         const bool prof = std::getenv("RB_PROF") != nullptr;
         if (prof) {
@@ -190,7 +190,7 @@ int main(int argc, char** argv) {
     std::vector<PoolOut> outs(npools);
     std::vector<BGroup> gs(npools);
     for (int p = 0; p < npools; p++) {
-        gs[p].hits = ph[p].data();
+        gs[p].set_hits(ph[p].data());
         gs[p].n = (uint32_t)ph[p].size();
     }
     auto par = [&](size_t n, const std::function<void(size_t)>& f) {

@@ -379,16 +379,64 @@ void synth_free(void* h) { delete static_cast<Synth*>(h); }
 // candidates'); returns the number of kept groups.
 int32_t synth_override_first_disjoint(const int32_t* offs, const mm_entry_ref* ents, int32_t n_groups,
                                       int32_t* out_offs, mm_entry_ref* out_ents) {
-    std::unordered_set<std::string_view> taken;
-    taken.reserve((size_t)(n_groups > 0 ? offs[n_groups] : 0));
+    // The taken ticket ids: an open-addressing set of their texts (every
+    // library's entries compare by text; the product's share one pointer per
+    // ticket, the oracle's are copies), grown at half load.
+    struct Key {
+        const char* p;
+        uint32_t n;
+        uint32_t tag;
+    };
+    std::vector<Key> tab(1u << 16, Key{nullptr, 0, 0});
+    size_t used = 0;
+    auto hash = [](const char* p, size_t n) {
+        uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+        size_t i = 0;
+        for (; i + 8 <= n; i += 8) {
+            uint64_t w;
+            std::memcpy(&w, p + i, 8);
+            h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+            h ^= h >> 31;
+        }
+        if (i < n) {
+            uint64_t w = 0;
+            std::memcpy(&w, p + i, n - i);
+            h = (h ^ w) * 0x94D049BB133111EBull;
+        }
+        return h ^ (h >> 29);
+    };
+    auto find = [&](const char* p, size_t n, uint64_t h) -> Key* {  // the key's slot, or the empty one it goes in
+        const size_t mask = tab.size() - 1;
+        for (size_t i = h & mask;; i = (i + 1) & mask) {
+            Key& k = tab[i];
+            if (!k.p || (k.tag == (uint32_t)(h >> 32) && k.n == n && (k.p == p || !std::memcmp(k.p, p, n)))) return &k;
+        }
+    };
+    auto insert = [&](const char* p, size_t n, uint64_t h) {
+        Key* k = find(p, n, h);
+        if (k->p) return;
+        *k = Key{p, (uint32_t)n, (uint32_t)(h >> 32)};
+        if (2 * ++used > tab.size()) {
+            std::vector<Key> old(tab.size() * 2, Key{nullptr, 0, 0});
+            old.swap(tab);
+            for (const Key& o : old)
+                if (o.p) *find(o.p, o.n, hash(o.p, o.n)) = o;
+        }
+    };
     int32_t kept = 0, e = 0;
     out_offs[0] = 0;
     for (int32_t g = 0; g < n_groups; g++) {
         bool free = true;
-        for (int32_t k = offs[g]; k < offs[g + 1] && free; k++) free = !taken.count(ents[k].ticket);
+        for (int32_t k = offs[g]; k < offs[g + 1] && free; k++) {
+            const char* t = ents[k].ticket;
+            const size_t n = std::strlen(t);
+            free = find(t, n, hash(t, n))->p == nullptr;
+        }
         if (!free) continue;
         for (int32_t k = offs[g]; k < offs[g + 1]; k++) {
-            taken.insert(ents[k].ticket);
+            const char* t = ents[k].ticket;
+            const size_t n = std::strlen(t);
+            insert(t, n, hash(t, n));
             out_ents[e++] = ents[k];
         }
         out_offs[++kept] = e;
