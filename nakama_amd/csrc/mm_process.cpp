@@ -1610,13 +1610,15 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
     for (size_t base = 0; base < rows.size(); base += kMaxBatchRows / 4) {
         const size_t end = std::min(rows.size(), base + kMaxBatchRows / 4);
         if (rev && (row_shard() ? shard_any(timer.check()) : timer.check())) rev = rp.rev = false;
-        std::vector<BGroup> bg(end - base);
+        std::vector<BGroup>& bg = bg_;  // kept across passes (refilled in place: no allocation per row)
+        bg.resize(end - base);
         // the rows' searches (built on the workers for large chunks: the
         // sources from the non-mutating posting lookup)
         auto build = [&](size_t lo, size_t hi) {
             for (size_t i = lo; i < hi; i++) {
                 const uint32_t r = rows[base + i];
                 BGroup& g = bg[i];
+                g.reset();
                 g.sig = sig_[r];
                 const Sig& s = sigs_[g.sig];
                 g.n_fields = s.n_fields;

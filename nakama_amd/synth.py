@@ -112,10 +112,16 @@ def override_commit(mm: "capi.Matchmaker", out) -> "capi.mm_matched":
     native first-disjoint override (tools/synth.cpp) picks groups, and
     mm_process_commit hands them back.  Returns the commit's result (free it
     with the library's mm_free_matched)."""
+    import numpy as np
     n = out.n_groups
     ne = out.n_entries
-    offs = (C.c_int32 * (n + 1))()
-    ents = (capi.mm_entry_ref * max(1, ne))()
+    # output room for every candidate, left uninitialised (numpy.empty: only
+    # the pages the kept groups are written to get touched; a ctypes array
+    # would zero-fill gigabytes)
+    offs_buf = np.empty(n + 1, dtype=np.int32)
+    ents_buf = np.empty(max(1, ne) * C.sizeof(capi.mm_entry_ref), dtype=np.uint8)
+    offs = offs_buf.ctypes.data_as(C.POINTER(C.c_int32))
+    ents = ents_buf.ctypes.data_as(C.POINTER(capi.mm_entry_ref))
     kept = lib().synth_override_first_disjoint(out.group_offsets, out.entries, n, offs, ents)
     res = capi.mm_matched()
     try:  # the kept entries point into the candidate result: it goes back after the commit

@@ -423,20 +423,43 @@ int32_t synth_override_first_disjoint(const int32_t* offs, const mm_entry_ref* e
                 if (o.p) *find(o.p, o.n, hash(o.p, o.n)) = o;
         }
     };
+    // The pointers of taken entries, checked first: a library whose entries
+    // share one pointer per ticket answers most lookups without hashing text.
+    std::vector<const char*> ptab(1u << 16, nullptr);
+    size_t pused = 0;
+    auto pslot = [&](const char* p) -> const char** {
+        const size_t mask = ptab.size() - 1;
+        uint64_t h = (uint64_t)(uintptr_t)p * 0x9E3779B97F4A7C15ull;
+        for (size_t i = (h >> 20) & mask;; i = (i + 1) & mask)
+            if (!ptab[i] || ptab[i] == p) return &ptab[i];
+    };
+    auto pinsert = [&](const char* p) {
+        const char** q = pslot(p);
+        if (*q) return;
+        *q = p;
+        if (2 * ++pused > ptab.size()) {
+            std::vector<const char*> old(ptab.size() * 2, nullptr);
+            old.swap(ptab);
+            for (const char* o : old)
+                if (o) *pslot(o) = o;
+        }
+    };
+    auto taken = [&](const char* t) {
+        if (*pslot(t)) return true;
+        const size_t n = std::strlen(t);
+        return find(t, n, hash(t, n))->p != nullptr;
+    };
     int32_t kept = 0, e = 0;
     out_offs[0] = 0;
     for (int32_t g = 0; g < n_groups; g++) {
         bool free = true;
-        for (int32_t k = offs[g]; k < offs[g + 1] && free; k++) {
-            const char* t = ents[k].ticket;
-            const size_t n = std::strlen(t);
-            free = find(t, n, hash(t, n))->p == nullptr;
-        }
+        for (int32_t k = offs[g]; k < offs[g + 1] && free; k++) free = !taken(ents[k].ticket);
         if (!free) continue;
         for (int32_t k = offs[g]; k < offs[g + 1]; k++) {
             const char* t = ents[k].ticket;
             const size_t n = std::strlen(t);
             insert(t, n, hash(t, n));
+            pinsert(t);
             out_ents[e++] = ents[k];
         }
         out_offs[++kept] = e;
