@@ -82,6 +82,89 @@ __device__ __forceinline__ bool eval_parsed(const DStore& st, uint8_t qkind, con
     return true;
 }
 
+// The distinct field columns one search's clauses read (wave-uniform, found
+// once per search).  With at most kEvalF of them, a candidate's columns are
+// loaded in the same round trip as its alive / Min / Max / party words and the
+// clause loop selects from registers (eval_loaded); eval_parsed's per-clause
+// load inside the data-dependent loop cost one dependent memory round trip per
+// clause (C2's five clauses: five).  n < 0: more fields, per-clause loads.
+constexpr int kEvalF = 4;
+struct EvalFields {
+    int n;
+    uint16_t f[kEvalF];
+    const uint8_t* kp[kEvalF];
+    const int64_t* vp[kEvalF];
+};
+
+__device__ __forceinline__ EvalFields eval_fields(const DStore& st, uint8_t qkind, const DClause* __restrict__ cl,
+                                                  int n) {
+    EvalFields e{};
+    if (qkind == QK_MATCHALL || qkind == QK_MATCHNONE) return e;
+    for (int i = 0; i < n; i++) {
+        const DClause c = cl[i];
+        if (c.op == OP_FALSE) continue;
+        bool seen = false;
+#pragma unroll
+        for (int k = 0; k < kEvalF; k++) seen |= k < e.n && e.f[k] == c.field;
+        if (seen) continue;
+        if (e.n == kEvalF) { e.n = -1; return e; }
+#pragma unroll
+        for (int k = 0; k < kEvalF; k++)
+            if (k == e.n) e.f[k] = c.field;
+        e.n++;
+    }
+#pragma unroll
+    for (int k = 0; k < kEvalF; k++)
+        if (k < e.n) { e.kp[k] = st.fkind[e.f[k]]; e.vp[k] = st.fval[e.f[k]]; }
+    return e;
+}
+
+// A candidate's columns for eval_loaded (ef.n >= 0).
+struct Loaded {
+    uint8_t kind[kEvalF];
+    int64_t val[kEvalF];
+};
+
+__device__ __forceinline__ void load_fields(const EvalFields& ef, uint32_t s, Loaded& L) {
+#pragma unroll
+    for (int k = 0; k < kEvalF; k++)
+        if (k < ef.n) { L.kind[k] = ef.kp[k][s]; L.val[k] = ef.vp[k][s]; }
+}
+
+// eval_parsed over preloaded columns (same semantics, bluge BooleanSearcher,
+// search_boolean.go:174-244).
+__device__ __forceinline__ bool eval_loaded(const DStore& st, uint8_t qkind, const DClause* __restrict__ cl, int n,
+                                            const EvalFields& ef, const Loaded& L, double* sp) {
+    if (qkind == QK_MATCHALL) { *sp = 1.0; return true; }
+    if (qkind == QK_MATCHNONE) return false;
+    double ms = 0.0, ss = 0.0;
+    bool has_must = false, has_should = false, any_should = false, fail = false;
+    for (int i = 0; i < n; i++) {
+        const DClause c = cl[i];
+        bool h = false;
+        double sc = c.score;
+        if (c.op != OP_FALSE) {
+            uint8_t kind = KIND_ABSENT;
+            int64_t val = 0;
+#pragma unroll
+            for (int k = 0; k < kEvalF; k++)
+                if (k < ef.n && ef.f[k] == c.field) { kind = L.kind[k]; val = L.val[k]; }
+            if (c.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)c.term;
+            else if (c.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= c.lo && val <= c.hi;
+            else if (c.op == OP_TERMSET) h = kind == KIND_KEYWORD && termset_hit(st, c.term, val, &sc);
+            else h = (kind == KIND_KEYWORD && val == (int64_t)c.term) || (kind == KIND_NUMERIC && val == c.lo);
+        }
+        if (c.occur == OCC_MUST) { has_must = true; if (h) ms += sc; else fail = true; }
+        else if (c.occur == OCC_SHOULD) { has_should = true; if (h) { ss += sc; any_should = true; } }
+        else if (h) fail = true;
+    }
+    if (fail) return false;
+    if (!has_must && !has_should) { *sp = 1.0; return true; }  // only mustNots: MatchAll(1)
+    if (!has_must) { *sp = ss; return any_should; }
+    *sp = any_should ? ms + ss : ms;
+    return true;
+}
+
 struct Cand {
     uint32_t slot;
     uint32_t idx;
@@ -91,24 +174,34 @@ struct Cand {
     bool live;
 };
 
-__device__ __forceinline__ Cand eval_candidate(const DStore& st, const DGroup& g, const uint32_t* __restrict__ src,
+// The slot id of source position idx (clamped past the end: masked later).
+__device__ __forceinline__ uint32_t cand_slot(const DGroup& g, const uint32_t* __restrict__ src, uint32_t idx) {
+    return src[g.src_off + (idx < g.src_len ? idx : g.src_len - 1)];
+}
+
+// s: cand_slot(g, src, idx), loaded ahead (the search loops prefetch the next
+// tile's slot ids while they rank the current one).
+__device__ __forceinline__ Cand eval_candidate(const DStore& st, const DGroup& g, const EvalFields& ef, uint32_t s,
                                                uint32_t idx) {
     Cand c{0, idx, 0, 1, false, false};
     if (g.src_len == 0) return c;
     // unconditional loads (a clamped position past the end, masked below):
-    // the slot id, then alive / Min / Max / party in one round trip
+    // alive / Min / Max / party and the query's columns in one round trip
     const bool valid = idx < g.src_len;
-    const uint32_t s = src[g.src_off + (valid ? idx : g.src_len - 1)];
     const uint8_t al = st.alive[s];
     const int32_t mn = st.minc[s], mx = st.maxc[s];
     const uint32_t pt = g.tparty != kNoParty ? st.party[s] : 0u;
+    Loaded L;
+    if (ef.n > 0) load_fields(ef, s, L);
     if (!valid) return c;
     c.slot = s;
     bool m = al != 0;
     c.live = m;
     m = m && mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
     double sp = 0.0;
-    if (m) m = eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
+    if (m)
+        m = ef.n >= 0 ? eval_loaded(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, ef, L, &sp)
+                      : eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
     if (m) {
         // top-level BooleanQuery{must: parsed, min_count range, max_count range}
         c.key = dsortable((sp + 1.0) + 1.0);
@@ -155,6 +248,9 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     uint32_t my_live = 0;
     if (tid == 0) s_live = 0;
     __syncthreads();
+    const EvalFields ef = eval_fields(st, g.qkind, st.clauses + g.clause_off, g.n_clauses);
+    // the next tile's slot ids are loaded while the current tile is ranked
+    uint32_t s_next = g.src_len ? cand_slot(g, src, tid) : 0u;
 
     if (!g.var_score) {
         // ---- ordered compaction -------------------------------------------------
@@ -162,7 +258,9 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
         uint32_t base = 0;
         bool stopped = false;
         for (; base < g.src_len; base += kBlock) {
-            Cand c = eval_candidate(st, g, src, base + tid);
+            const uint32_t s_cur = s_next;
+            if (base + kBlock < g.src_len) s_next = cand_slot(g, src, base + kBlock + tid);
+            Cand c = eval_candidate(st, g, ef, s_cur, base + tid);
             my_live += c.live;
             const uint64_t mask = __ballot(c.m);
             if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(mask);
@@ -200,7 +298,9 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     bool early = false;
     uint32_t base = 0;
     for (; base < g.src_len; base += kBlock) {
-        Cand c = eval_candidate(st, g, src, base + tid);
+        const uint32_t s_cur = s_next;
+        if (base + kBlock < g.src_len) s_next = cand_slot(g, src, base + kBlock + tid);
+        Cand c = eval_candidate(st, g, ef, s_cur, base + tid);
         my_live += c.live;
         const uint64_t pre = __ballot(c.m);
         if (n == KK && c.m) c.m = c.key > lkey[cur][KK - 1];
@@ -287,26 +387,49 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* _
     const DGroup g = chunks[blockIdx.x];
     const uint32_t* __restrict__ src = (g.src_kind == 0 ? st.order : st.postings) + g.src_off;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t s[kScanJ];
+    // Every load is unconditional (tail lanes read a clamped position and are
+    // masked after): the slot ids, then alive / Min / Max / party and — when
+    // the query reads at most two fields (C1, C4: mode x region) — its
+    // columns, all in one round trip, instead of a dependent load per filter
+    // stage and per clause.
+    const EvalFields ef = eval_fields(st, g.qkind, st.clauses + g.clause_off, g.n_clauses);
+    const bool pre = ef.n >= 1 && ef.n <= 2;
+    const uint32_t last = g.src_len ? g.src_len - 1 : 0;
+    uint32_t s[kScanJ], sl[kScanJ];
     bool m[kScanJ];
 #pragma unroll
     for (int j = 0; j < kScanJ; j++) {
         const uint32_t i = (uint32_t)(j * kBlock + tid);
-        s[j] = i < g.src_len ? src[i] : kNoSlot;
+        sl[j] = g.src_len ? src[i < g.src_len ? i : last] : 0u;
+        s[j] = i < g.src_len ? sl[j] : kNoSlot;
+    }
+    uint8_t al[kScanJ], fk0[kScanJ], fk1[kScanJ];
+    int32_t mn[kScanJ], mx[kScanJ];
+    uint32_t pt[kScanJ];
+    int64_t fv0[kScanJ], fv1[kScanJ];
+#pragma unroll
+    for (int j = 0; j < kScanJ; j++) {
+        al[j] = st.alive[sl[j]];
+        mn[j] = st.minc[sl[j]];
+        mx[j] = st.maxc[sl[j]];
+        pt[j] = g.tparty != kNoParty ? st.party[sl[j]] : 0u;
+        if (pre) {
+            fk0[j] = ef.kp[0][sl[j]];
+            fv0[j] = ef.vp[0][sl[j]];
+            if (ef.n == 2) {
+                fk1[j] = ef.kp[1][sl[j]];
+                fv1[j] = ef.vp[1][sl[j]];
+            }
+        }
     }
 #pragma unroll
-    for (int j = 0; j < kScanJ; j++) m[j] = s[j] != kNoSlot && st.alive[s[j]] != 0;
+    for (int j = 0; j < kScanJ; j++) m[j] = s[j] != kNoSlot && al[j] != 0;
     uint32_t live = 0;
 #pragma unroll
     for (int j = 0; j < kScanJ; j++) live += m[j];
 #pragma unroll
     for (int j = 0; j < kScanJ; j++)
-        if (m[j]) m[j] = st.minc[s[j]] >= g.tmin && st.maxc[s[j]] <= g.tmax;
-    if (g.tparty != kNoParty) {
-#pragma unroll
-        for (int j = 0; j < kScanJ; j++)
-            if (m[j]) m[j] = st.party[s[j]] != g.tparty;
-    }
+        m[j] = m[j] && mn[j] >= g.tmin && mx[j] <= g.tmax && (g.tparty == kNoParty || pt[j] != g.tparty);
     // parsed query (eval_parsed, one clause at a time over the lane's candidates)
     double ms[kScanJ], ss[kScanJ];
     bool anys[kScanJ];
@@ -324,14 +447,18 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* _
             has_should |= k.occur == OCC_SHOULD;
             const int64_t* __restrict__ fv = st.fval[k.field];
             const uint8_t* __restrict__ fk = st.fkind[k.field];
+            const int sel = pre ? (k.field == ef.f[0] ? 0 : 1) : -1;
 #pragma unroll
             for (int j = 0; j < kScanJ; j++) {
                 if (!m[j]) continue;
                 bool h = false;
                 double sc = k.score;
                 if (k.op != OP_FALSE) {
-                    const uint8_t kind = fk[s[j]];
-                    const int64_t val = fv[s[j]];
+                    uint8_t kind;
+                    int64_t val;
+                    if (sel == 0) { kind = fk0[j]; val = fv0[j]; }
+                    else if (sel == 1) { kind = fk1[j]; val = fv1[j]; }
+                    else { kind = fk[s[j]]; val = fv[s[j]]; }
                     if (k.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)k.term;
                     else if (k.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= k.lo && val <= k.hi;
                     else if (k.op == OP_TERMSET) h = kind == KIND_KEYWORD && termset_hit(st, k.term, val, &sc);
@@ -819,15 +946,25 @@ __global__ __launch_bounds__(kBlock) void rsmall_kernel(DStore st, const DGroup*
     uint32_t s = kNoSlot;
     int64_t key = 0;
     uint8_t rv = 1;
+    const EvalFields ef = eval_fields(st, g.qkind, st.clauses + g.clause_off, g.n_clauses);
     if (j < g.src_len) {
         s = src[j];
-        live = st.alive[s] != 0;
-        m = live && st.minc[s] >= g.tmin && st.maxc[s] <= g.tmax && (g.tparty == kNoParty || st.party[s] != g.tparty);
+        // one round trip for every column the row's predicate reads, and the
+        // hit's own query descriptor for the reverse check
+        const uint8_t al = st.alive[s];
+        const int32_t mn = st.minc[s], mx = st.maxc[s];
+        const uint32_t pt = st.party[s];
+        const DQuery q = st.squery[s];
+        Loaded L;
+        if (ef.n > 0) load_fields(ef, s, L);
+        live = al != 0;
+        m = live && mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
         double sp = 0.0;
-        if (m) m = eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
+        if (m)
+            m = ef.n >= 0 ? eval_loaded(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, ef, L, &sp)
+                          : eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
         if (m) {
             key = dsortable((sp + 1.0) + 1.0);
-            const DQuery q = st.squery[s];
             double d;
             rv = eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, g.rev_slot, &d) ? 1 : 0;
         }

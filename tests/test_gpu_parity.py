@@ -175,6 +175,36 @@ def test_datetime_hit_lists():
         ts.close()
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_wide_queries(kernel, monkeypatch):
+    """Config 10: queries over 1-6 distinct keyword / numeric fields with every
+    occur: the kernels' preloaded-column evaluation (search/rsmall <= 4 fields,
+    scan <= 2) and its per-clause fallback beyond, on every kernel."""
+    monkeypatch.setenv("NKM_KERNEL", kernel)
+    run_passes(10, 3000, 3, dict(max_intervals=3))
+
+
+def test_wide_queries_rev_precision_and_hit_lists():
+    """Config 10 with RevPrecision (rsmall / search reverse checks), and its
+    hit lists and scores row by row."""
+    run_passes(10, 1500, 2, dict(max_intervals=2, rev_precision=True, rev_threshold=0))
+    ts = synth.TicketSet(10, 800)
+    gpu, orc = pair(dict(max_intervals=2))
+    try:
+        ts.insert_into(gpu)
+        ts.insert_into(orc)
+        for k in range(0, 800, 7):
+            t = ts.ticket_id(k)
+            hg, ho = gpu.debug_hits(t), orc.debug_hits(t)
+            assert [h for h, _ in hg] == [h for h, _ in ho]
+            for (_, a), (_, b) in zip(hg, ho):
+                assert math.isclose(a, b, rel_tol=1e-6)
+    finally:
+        gpu.close()
+        orc.close()
+        ts.close()
+
+
 @pytest.mark.parametrize("config,n,mi", [(5, 800, 2), (6, 600, 3)])
 def test_rev_threshold_fired(config, n, mi):
     """RevThreshold (matchmaker.go:244-248): IntervalSec * RevThreshold = 0 s,

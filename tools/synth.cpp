@@ -270,6 +270,36 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             t.min_count = t.max_count = 2;
             break;
         }
+        case 10: {  // wide queries: 1-6 distinct fields per query (keyword and numeric), every occur,
+                    // so the kernels' preloaded-column paths (<= 2 / <= 4 fields) and their
+                    // per-clause fallbacks all run
+            static const char* kf[3] = {"k0", "k1", "k2"};
+            static const char* nf[3] = {"n0", "n1", "n2"};
+            static const char* kv[3] = {"a", "b", "c"};
+            for (int f = 0; f < 3; f++)
+                if (r.next() % 8) S->sp.push_back({kf[f], kv[r.next() % 3]});
+            for (int f = 0; f < 3; f++)
+                if (r.next() % 8) S->np.push_back({nf[f], (double)(r.next() % 20)});
+            const int nfield = 1 + (int)(r.next() % 6);
+            std::string q;
+            bool any_pos = false;
+            for (int c = 0; c < nfield; c++) {
+                const int f = c % 3;
+                const int occ = (int)(r.next() % 4);  // 0,1: must, 2: should (^2), 3: mustNot
+                const char* pre = occ <= 1 ? "+" : occ == 3 ? "-" : "";
+                char cl[96];
+                if (c < 3) std::snprintf(cl, sizeof cl, "%sproperties.%s:%s", pre, kf[f], kv[r.next() % 3]);
+                else std::snprintf(cl, sizeof cl, "%sproperties.%s:>=%d", pre, nf[f], (int)(r.next() % 12));
+                if (occ == 2) std::strcat(cl, "^2");
+                any_pos |= occ != 3;
+                q += (q.empty() ? "" : " ") + std::string(cl);
+            }
+            if (!any_pos) q += " properties.n0:<=15";
+            query = q;
+            t.min_count = 2;
+            t.max_count = (r.next() % 2) ? 2 : 3;
+            break;
+        }
         case 8: {  // datetime-typed string properties (blugeProcessProperty, match_common.go:161-170,221-236)
                    // and RFC3339 date-range clauses (query_string_parser.go:234-250)
             party = r.uni() < 0.85 ? 1 : 2;
