@@ -51,6 +51,8 @@ hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, D
                        hipStream_t stream, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // cell_scan_kernel (ranks of every chunk in its search, one workgroup per
 // search: d_ranges = [first cell, end cell) pairs) then stitch_kernel.
+hipError_t launch_pack_slots(const DHit* d_out, uint64_t n, uint32_t* d_slots, const DGroup* d_groups,
+                             const DGroupResult* d_res, int n_whole, DHit* d_last, hipStream_t stream);
 hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResult* d_cres, const uint32_t* d_ranges,
                          int n_searches, uint32_t* d_offs, const DHit* d_scratch, DHit* d_out, hipStream_t stream);
 int scan_chunk_len();
@@ -615,6 +617,7 @@ public:
     // ---- index (scan order + postings), host mirror ----
     std::vector<uint32_t> order_;
     bool full_var_mode_ = true;  // NKM_FULLVAR=0: variable-score searches always use the LDS top-K
+    bool slot_lists_mode_ = true;  // NKM_SLOTLISTS=0: hit lists come back as 16-B DHits, not 4-B slot ids
     bool page_mode_ = true;  // NKM_PAGE=0: only a batch's first row pages a truncated list
     // Batch window after a variable-score list ran out (NKM_WIN=0: off): the
     // next batch takes twice the rows the last one decided (at least
@@ -684,6 +687,10 @@ public:
     DevArray<uint8_t> d_pair_out_;
     PinnedArray<DGroup> h_groups_;
     PinnedArray<DHit> h_out_;
+    DevArray<uint32_t> d_slots_;     // hit lists packed to slot ids (pack_slots_kernel)
+    PinnedArray<uint32_t> h_slots_;
+    DevArray<DHit> d_last_;          // each whole search's last entry (its cursor)
+    PinnedArray<DHit> h_last_;
     PinnedArray<uint8_t> h_rev_;
     PinnedArray<DGroupResult> h_res_;
     PinnedArray<uint32_t> h_slots_tmp_;

@@ -185,19 +185,21 @@ __device__ __forceinline__ Cand eval_candidate(const DStore& st, const DGroup& g
                                                uint32_t idx) {
     Cand c{0, idx, 0, 1, false, false};
     if (g.src_len == 0) return c;
-    // unconditional loads (a clamped position past the end, masked below):
-    // alive / Min / Max / party and the query's columns in one round trip
+    // The alive byte first (a posting-list candidate is a gather: every
+    // column costs a cache line, and late in a pass most candidates are
+    // dead), then Min / Max / party and the query's columns of a live
+    // candidate together in one more round trip.
     const bool valid = idx < g.src_len;
     const uint8_t al = st.alive[s];
+    if (!valid) return c;
+    c.slot = s;
+    c.live = al != 0;
+    if (!c.live) return c;
     const int32_t mn = st.minc[s], mx = st.maxc[s];
     const uint32_t pt = g.tparty != kNoParty ? st.party[s] : 0u;
     Loaded L;
     if (ef.n > 0) load_fields(ef, s, L);
-    if (!valid) return c;
-    c.slot = s;
-    bool m = al != 0;
-    c.live = m;
-    m = m && mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
+    bool m = mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
     double sp = 0.0;
     if (m)
         m = ef.n >= 0 ? eval_loaded(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, ef, L, &sp)
@@ -387,49 +389,43 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* _
     const DGroup g = chunks[blockIdx.x];
     const uint32_t* __restrict__ src = (g.src_kind == 0 ? st.order : st.postings) + g.src_off;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // Every load is unconditional (tail lanes read a clamped position and are
-    // masked after): the slot ids, then alive / Min / Max / party and — when
-    // the query reads at most two fields (C1, C4: mode x region) — its
-    // columns, all in one round trip, instead of a dependent load per filter
-    // stage and per clause.
+    // The slot ids, then the alive bytes (a posting list's candidates are
+    // gathers: every column costs a cache line, and dead candidates read no
+    // more), then Min / Max / party and — when the query reads at most two
+    // fields (C1, C4: mode x region) — its columns for the live candidates,
+    // all in one round trip, instead of a dependent load per filter stage and
+    // per clause.
     const EvalFields ef = eval_fields(st, g.qkind, st.clauses + g.clause_off, g.n_clauses);
     const bool pre = ef.n >= 1 && ef.n <= 2;
-    const uint32_t last = g.src_len ? g.src_len - 1 : 0;
-    uint32_t s[kScanJ], sl[kScanJ];
+    uint32_t s[kScanJ];
     bool m[kScanJ];
 #pragma unroll
     for (int j = 0; j < kScanJ; j++) {
         const uint32_t i = (uint32_t)(j * kBlock + tid);
-        sl[j] = g.src_len ? src[i < g.src_len ? i : last] : 0u;
-        s[j] = i < g.src_len ? sl[j] : kNoSlot;
-    }
-    uint8_t al[kScanJ], fk0[kScanJ], fk1[kScanJ];
-    int32_t mn[kScanJ], mx[kScanJ];
-    uint32_t pt[kScanJ];
-    int64_t fv0[kScanJ], fv1[kScanJ];
-#pragma unroll
-    for (int j = 0; j < kScanJ; j++) {
-        al[j] = st.alive[sl[j]];
-        mn[j] = st.minc[sl[j]];
-        mx[j] = st.maxc[sl[j]];
-        pt[j] = g.tparty != kNoParty ? st.party[sl[j]] : 0u;
-        if (pre) {
-            fk0[j] = ef.kp[0][sl[j]];
-            fv0[j] = ef.vp[0][sl[j]];
-            if (ef.n == 2) {
-                fk1[j] = ef.kp[1][sl[j]];
-                fv1[j] = ef.vp[1][sl[j]];
-            }
-        }
+        s[j] = i < g.src_len ? src[i] : kNoSlot;
     }
 #pragma unroll
-    for (int j = 0; j < kScanJ; j++) m[j] = s[j] != kNoSlot && al[j] != 0;
+    for (int j = 0; j < kScanJ; j++) m[j] = s[j] != kNoSlot && st.alive[s[j]] != 0;
     uint32_t live = 0;
 #pragma unroll
     for (int j = 0; j < kScanJ; j++) live += m[j];
+    uint8_t fk0[kScanJ], fk1[kScanJ];
+    int64_t fv0[kScanJ], fv1[kScanJ];
 #pragma unroll
-    for (int j = 0; j < kScanJ; j++)
-        m[j] = m[j] && mn[j] >= g.tmin && mx[j] <= g.tmax && (g.tparty == kNoParty || pt[j] != g.tparty);
+    for (int j = 0; j < kScanJ; j++) {
+        if (!m[j]) continue;
+        const int32_t mn = st.minc[s[j]], mx = st.maxc[s[j]];
+        const uint32_t pt = g.tparty != kNoParty ? st.party[s[j]] : 0u;
+        if (pre) {
+            fk0[j] = ef.kp[0][s[j]];
+            fv0[j] = ef.vp[0][s[j]];
+            if (ef.n == 2) {
+                fk1[j] = ef.kp[1][s[j]];
+                fv1[j] = ef.vp[1][s[j]];
+            }
+        }
+        m[j] = mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
+    }
     // parsed query (eval_parsed, one clause at a time over the lane's candidates)
     double ms[kScanJ], ss[kScanJ];
     bool anys[kScanJ];
@@ -803,6 +799,26 @@ __global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restr
     }
 }
 
+// Hit lists for the host as 4-B slot ids: the replay walks slots only, so the
+// D2H of a batch's lists moves a quarter of the 16-B DHit bytes (C2's
+// top-512 lists: 55 MB -> 14 MB per batch).  Entries [0, n) of the DHit
+// output (unwritten capacity included: contiguous, one copy), and each whole
+// search's last written entry (its pagination cursor: key and source position).
+__global__ __launch_bounds__(kBlock) void pack_slots_kernel(const DHit* __restrict__ out, uint64_t n,
+                                                            uint32_t* __restrict__ slots) {
+    for (uint64_t e = blockIdx.x * (uint64_t)kBlock + threadIdx.x; e < n; e += (uint64_t)gridDim.x * kBlock)
+        slots[e] = out[e].slot;
+}
+
+__global__ __launch_bounds__(kBlock) void last_hits_kernel(const DGroup* __restrict__ groups,
+                                                           const DGroupResult* __restrict__ res, int n,
+                                                           const DHit* __restrict__ out, DHit* __restrict__ last) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = res[i].count;
+    last[i] = c ? out[groups[i].out_off + c - 1] : DHit{kNoSlot, 0u, 0};
+}
+
 // processCustom's candidate enumeration (combineIndexes, matchmaker_process.go:
 // 578-612, and the checks :470-546 applied to each subset), one thread per work
 // item (a run of kEnumSpan masks of one row, mm_device.h).  COUNT: the item's
@@ -949,22 +965,25 @@ __global__ __launch_bounds__(kBlock) void rsmall_kernel(DStore st, const DGroup*
     const EvalFields ef = eval_fields(st, g.qkind, st.clauses + g.clause_off, g.n_clauses);
     if (j < g.src_len) {
         s = src[j];
-        // one round trip for every column the row's predicate reads, and the
-        // hit's own query descriptor for the reverse check
-        const uint8_t al = st.alive[s];
-        const int32_t mn = st.minc[s], mx = st.maxc[s];
-        const uint32_t pt = st.party[s];
-        const DQuery q = st.squery[s];
-        Loaded L;
-        if (ef.n > 0) load_fields(ef, s, L);
-        live = al != 0;
-        m = live && mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
-        double sp = 0.0;
-        if (m)
-            m = ef.n >= 0 ? eval_loaded(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, ef, L, &sp)
-                          : eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
+        // the alive byte, then one round trip for every column a live
+        // candidate's predicate reads and its own query descriptor (the
+        // reverse check)
+        live = st.alive[s] != 0;
+        DQuery q{};
+        if (live) {
+            const int32_t mn = st.minc[s], mx = st.maxc[s];
+            const uint32_t pt = st.party[s];
+            q = st.squery[s];
+            Loaded L;
+            if (ef.n > 0) load_fields(ef, s, L);
+            m = mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
+            double sp = 0.0;
+            if (m)
+                m = ef.n >= 0 ? eval_loaded(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, ef, L, &sp)
+                              : eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
+            if (m) key = dsortable((sp + 1.0) + 1.0);
+        }
         if (m) {
-            key = dsortable((sp + 1.0) + 1.0);
             double d;
             rv = eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, g.rev_slot, &d) ? 1 : 0;
         }
@@ -1075,6 +1094,19 @@ hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, D
     if (n_chunks <= 0) return hipSuccess;
     hipExtLaunchKernelGGL(scan_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, ev0, ev1, 0, st, d_chunks, d_scratch,
                           d_cres);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_slots(const DHit* d_out, uint64_t n, uint32_t* d_slots, const DGroup* d_groups,
+                             const DGroupResult* d_res, int n_whole, DHit* d_last, hipStream_t stream) {
+    if (n) {
+        const uint64_t blocks = (n + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(pack_slots_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(kBlock), 0, stream,
+                           d_out, n, d_slots);
+    }
+    if (n_whole > 0)
+        hipLaunchKernelGGL(last_hits_kernel, dim3((n_whole + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, d_groups,
+                           d_res, n_whole, d_out, d_last);
     return hipGetLastError();
 }
 

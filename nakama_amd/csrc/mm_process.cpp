@@ -81,9 +81,16 @@ struct Replay : ReplayCore {
     // Fetches the next page of a group's list (cursor = its last entry).
     void fetch_more(BGroup& g) override {
         stats.refetches++;
-        if (!g.hits && g.n)  // a slot list (mscan) is complete by construction: nothing to page
-            throw DeviceError{hipErrorUnknown, "page of a slot list", __LINE__};
-        if (g.ext.empty() && g.n) {
+        // a slot list (run_batch's packed lists): its cursor is g.last
+        const bool slot_list = !g.hits && g.sp;
+        if (slot_list && g.n && g.last.slot == kNoSlot)  // an mscan list: complete by construction
+            throw DeviceError{hipErrorUnknown, "page of a slot list without a cursor", __LINE__};
+        if (slot_list) {
+            if (g.ext_slots.empty() && g.n) {
+                g.ext_slots.assign(g.sp, g.sp + g.n);
+                if (g.rev) g.ext_rev.assign(g.rev, g.rev + g.n);
+            }
+        } else if (g.ext.empty() && g.n) {
             g.ext.assign(g.hits, g.hits + g.n);
             if (g.rev) g.ext_rev.assign(g.rev, g.rev + g.n);
         }
@@ -91,8 +98,9 @@ struct Replay : ReplayCore {
         d.out_off = 0;
         d.has_cursor = g.n ? 1 : 0;
         if (g.n) {
-            d.cur_key = g.hits[g.n - 1].key;
-            d.cur_idx = g.hits[g.n - 1].idx;
+            const DHit& lh = slot_list ? g.last : g.hits[g.n - 1];
+            d.cur_key = lh.key;
+            d.cur_idx = lh.idx;
         }
         // constant-score pages double, but never past the rest of the source
         d.k = d.var_score ? (uint32_t)var_k_capacity()
@@ -134,11 +142,18 @@ struct Replay : ReplayCore {
         stats.pair_evals += r.scanned;
         stats.k_bytes[0] += search_bytes(c.sigs_[g.sig].n_fields, d, r);
         stats.k_launches[0]++;
-        g.ext.insert(g.ext.end(), c.h_page_.p, c.h_page_.p + r.count);
         if (rev) g.ext_rev.insert(g.ext_rev.end(), c.h_page_rev_.p, c.h_page_rev_.p + r.count);
-        g.set_hits(g.ext.data());
         g.rev = rev ? g.ext_rev.data() : nullptr;
-        g.n = (uint32_t)g.ext.size();
+        if (slot_list) {
+            for (uint32_t k = 0; k < r.count; k++) g.ext_slots.push_back(c.h_page_.p[k].slot);
+            if (r.count) g.last = c.h_page_.p[r.count - 1];
+            g.set_slots(g.ext_slots.data());
+            g.n = (uint32_t)g.ext_slots.size();
+        } else {
+            g.ext.insert(g.ext.end(), c.h_page_.p, c.h_page_.p + r.count);
+            g.set_hits(g.ext.data());
+            g.n = (uint32_t)g.ext.size();
+        }
         g.complete = r.complete != 0;
         g.d.k = d.k;
     }
@@ -386,6 +401,12 @@ struct Replay : ReplayCore {
             off += d.k;
         }
         const int nchunks = (int)lg.size() - nwhole;
+        // The lists of whole and chunked searches come back to the host as
+        // 4-B slot ids plus each list's last DHit (its cursor) — unless the
+        // host needs every key (full-list searches are sorted by key here) or
+        // the lists are exchanged between ranks as DHits (row-sharded).
+        const uint64_t scan_end = off;
+        const bool slots_only = c.slot_lists_mode_ && full_var.empty() && !c.row_shard() && scan_end > 0;
         // mscan: signatures (DMSig, clause_off indexing mcl), result cells after the chunks
         const uint32_t mchunk = ms.chunk;
         const uint64_t mscratch = scratch;
@@ -538,6 +559,14 @@ struct Replay : ReplayCore {
         }
         if (need_pm && kinds)
             NKM_HIP(launch_pairmat(st, c.d_groups_.p + b0, c.d_res_.p + b0, b1 - b0, c.d_out_.p, c.d_pm_.p, stream));
+        if (slots_only) {
+            c.d_slots_.reserve(scan_end, false);
+            c.h_slots_.reserve(scan_end);
+            c.d_last_.reserve(std::max(nwhole, 1), false);
+            c.h_last_.reserve((size_t)nwhole + cg_list.size() + 1);
+            NKM_HIP(launch_pack_slots(c.d_out_.p, scan_end, c.d_slots_.p, c.d_groups_.p, c.d_res_.p, nwhole, c.d_last_.p,
+                                      stream));
+        }
         c.h_res_.reserve(std::max<uint32_t>(nres, 1));
         c.h_out_.reserve(std::max<uint64_t>(off, 1));
         if (rev) c.h_rev_.reserve(std::max<uint64_t>(off, 1));
@@ -576,8 +605,14 @@ struct Replay : ReplayCore {
             if (need_pm) d2h(c.h_pm_.p, c.d_pm_.p, o_pm);
         } else {
             NKM_HIP(hipMemcpyAsync(c.h_res_.p, c.d_res_.p, nres * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
-            if (whole_off)
+            if (whole_off && slots_only) {
+                NKM_HIP(hipMemcpyAsync(c.h_slots_.p, c.d_slots_.p, whole_off * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                       stream));
+                NKM_HIP(hipMemcpyAsync(c.h_last_.p, c.d_last_.p, (size_t)nwhole * sizeof(DHit), hipMemcpyDeviceToHost,
+                                       stream));
+            } else if (whole_off) {
                 NKM_HIP(hipMemcpyAsync(c.h_out_.p, c.d_out_.p, whole_off * sizeof(DHit), hipMemcpyDeviceToHost, stream));
+            }
             if (rev) NKM_HIP(hipMemcpyAsync(c.h_rev_.p, c.d_rev_.p, off, hipMemcpyDeviceToHost, stream));
             if (need_pm && whole_off)
                 NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, whole_off * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -640,7 +675,12 @@ struct Replay : ReplayCore {
                 BGroup& g = bg[lg_group[i]];
                 const DGroupResult& r = c.h_res_.p[i];
                 g.head = 0;
-                g.set_hits(c.h_out_.p + lg[i].out_off);
+                if (slots_only) {
+                    g.set_slots(c.h_slots_.p + lg[i].out_off);
+                    g.last = c.h_last_.p[i];
+                } else {
+                    g.set_hits(c.h_out_.p + lg[i].out_off);
+                }
                 g.rev = rev ? c.h_rev_.p + lg[i].out_off : nullptr;
                 g.pm = need_pm ? c.h_pm_.p + lg[i].out_off : nullptr;
                 g.pm_n = need_pm ? std::min<uint32_t>(r.count, kPairP) : 0;
@@ -666,11 +706,20 @@ struct Replay : ReplayCore {
             if (n > g.d.k) { n = g.d.k; complete = false; }
             if (slots && !complete)  // mscan lists are sized to their whole source (plan above)
                 throw DeviceError{hipErrorUnknown, "mscan list cut", __LINE__};
-            if (n)
+            const bool packed = !slots && slots_only;  // a chunked list: slot ids + its last DHit
+            if (n && packed) {
+                NKM_HIP(hipMemcpyAsync(c.h_slots_.p + cg_off[k], c.d_slots_.p + cg_off[k], n * sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, stream));
+                NKM_HIP(hipMemcpyAsync(c.h_last_.p + nwhole + k, c.d_out_.p + cg_off[k] + n - 1, sizeof(DHit),
+                                       hipMemcpyDeviceToHost, stream));
+            } else if (n) {
                 NKM_HIP(hipMemcpyAsync(c.h_out_.p + cg_off[k], c.d_out_.p + cg_off[k], n * (slots ? 4 : sizeof(DHit)),
                                        hipMemcpyDeviceToHost, stream));
+            }
             g.head = 0;
+            g.last = DHit{kNoSlot, 0, 0};
             if (slots) g.set_slots(reinterpret_cast<const uint32_t*>(c.h_out_.p + cg_off[k]));
+            else if (packed) g.set_slots(c.h_slots_.p + cg_off[k]);
             else g.set_hits(c.h_out_.p + cg_off[k]);
             g.rev = nullptr;
             g.pm = nullptr;
@@ -679,6 +728,11 @@ struct Replay : ReplayCore {
             g.complete = complete;
         }
         if (!cg_list.empty()) NKM_HIP(hipStreamSynchronize(stream));
+        if (slots_only)  // the chunked lists' cursors (copied above)
+            for (size_t k = 0; k < n_scan_cg; k++) {
+                BGroup& g = bg[cg_list[k]];
+                g.last = g.n ? c.h_last_.p[nwhole + k] : DHit{kNoSlot, 0, 0};
+            }
     }
 
     bool pair_slow(const BGroup& g, uint32_t from_pos, uint32_t to_pos) override {

@@ -90,6 +90,9 @@ struct BGroup {
         sp = s;
         ss = 1;
     }
+    // a slot list's last entry (its pagination cursor: score key and source
+    // position), kept beside it because the list itself holds slots only
+    DHit last{kNoSlot, 0, 0};
     const uint8_t* rev = nullptr;
     const uint32_t* pm = nullptr;  // kPairP masks per entry (rev rows with combos)
     uint32_t pm_n = 0;             // entries covered by pm
@@ -100,6 +103,7 @@ struct BGroup {
     bool complete = true;
     uint32_t head = 0;
     std::vector<DHit> ext;
+    std::vector<uint32_t> ext_slots;  // a paged slot list
     std::vector<uint8_t> ext_rev;
     // back to a default-constructed search, keeping the vectors' capacity
     // (a reused batch array is refilled in place by the host workers)
@@ -122,7 +126,9 @@ struct BGroup {
         complete = true;
         head = 0;
         ext.clear();
+        ext_slots.clear();
         ext_rev.clear();
+        last = DHit{kNoSlot, 0, 0};
     }
 };
 
