@@ -82,89 +82,6 @@ __device__ __forceinline__ bool eval_parsed(const DStore& st, uint8_t qkind, con
     return true;
 }
 
-// The distinct field columns one search's clauses read (wave-uniform, found
-// once per search).  With at most kEvalF of them, a candidate's columns are
-// loaded in the same round trip as its alive / Min / Max / party words and the
-// clause loop selects from registers (eval_loaded); eval_parsed's per-clause
-// load inside the data-dependent loop cost one dependent memory round trip per
-// clause (C2's five clauses: five).  n < 0: more fields, per-clause loads.
-constexpr int kEvalF = 4;
-struct EvalFields {
-    int n;
-    uint16_t f[kEvalF];
-    const uint8_t* kp[kEvalF];
-    const int64_t* vp[kEvalF];
-};
-
-__device__ __forceinline__ EvalFields eval_fields(const DStore& st, uint8_t qkind, const DClause* __restrict__ cl,
-                                                  int n) {
-    EvalFields e{};
-    if (qkind == QK_MATCHALL || qkind == QK_MATCHNONE) return e;
-    for (int i = 0; i < n; i++) {
-        const DClause c = cl[i];
-        if (c.op == OP_FALSE) continue;
-        bool seen = false;
-#pragma unroll
-        for (int k = 0; k < kEvalF; k++) seen |= k < e.n && e.f[k] == c.field;
-        if (seen) continue;
-        if (e.n == kEvalF) { e.n = -1; return e; }
-#pragma unroll
-        for (int k = 0; k < kEvalF; k++)
-            if (k == e.n) e.f[k] = c.field;
-        e.n++;
-    }
-#pragma unroll
-    for (int k = 0; k < kEvalF; k++)
-        if (k < e.n) { e.kp[k] = st.fkind[e.f[k]]; e.vp[k] = st.fval[e.f[k]]; }
-    return e;
-}
-
-// A candidate's columns for eval_loaded (ef.n >= 0).
-struct Loaded {
-    uint8_t kind[kEvalF];
-    int64_t val[kEvalF];
-};
-
-__device__ __forceinline__ void load_fields(const EvalFields& ef, uint32_t s, Loaded& L) {
-#pragma unroll
-    for (int k = 0; k < kEvalF; k++)
-        if (k < ef.n) { L.kind[k] = ef.kp[k][s]; L.val[k] = ef.vp[k][s]; }
-}
-
-// eval_parsed over preloaded columns (same semantics, bluge BooleanSearcher,
-// search_boolean.go:174-244).
-__device__ __forceinline__ bool eval_loaded(const DStore& st, uint8_t qkind, const DClause* __restrict__ cl, int n,
-                                            const EvalFields& ef, const Loaded& L, double* sp) {
-    if (qkind == QK_MATCHALL) { *sp = 1.0; return true; }
-    if (qkind == QK_MATCHNONE) return false;
-    double ms = 0.0, ss = 0.0;
-    bool has_must = false, has_should = false, any_should = false, fail = false;
-    for (int i = 0; i < n; i++) {
-        const DClause c = cl[i];
-        bool h = false;
-        double sc = c.score;
-        if (c.op != OP_FALSE) {
-            uint8_t kind = KIND_ABSENT;
-            int64_t val = 0;
-#pragma unroll
-            for (int k = 0; k < kEvalF; k++)
-                if (k < ef.n && ef.f[k] == c.field) { kind = L.kind[k]; val = L.val[k]; }
-            if (c.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)c.term;
-            else if (c.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= c.lo && val <= c.hi;
-            else if (c.op == OP_TERMSET) h = kind == KIND_KEYWORD && termset_hit(st, c.term, val, &sc);
-            else h = (kind == KIND_KEYWORD && val == (int64_t)c.term) || (kind == KIND_NUMERIC && val == c.lo);
-        }
-        if (c.occur == OCC_MUST) { has_must = true; if (h) ms += sc; else fail = true; }
-        else if (c.occur == OCC_SHOULD) { has_should = true; if (h) { ss += sc; any_should = true; } }
-        else if (h) fail = true;
-    }
-    if (fail) return false;
-    if (!has_must && !has_should) { *sp = 1.0; return true; }  // only mustNots: MatchAll(1)
-    if (!has_must) { *sp = ss; return any_should; }
-    *sp = any_should ? ms + ss : ms;
-    return true;
-}
-
 struct Cand {
     uint32_t slot;
     uint32_t idx;
@@ -174,36 +91,24 @@ struct Cand {
     bool live;
 };
 
-// The slot id of source position idx (clamped past the end: masked later).
-__device__ __forceinline__ uint32_t cand_slot(const DGroup& g, const uint32_t* __restrict__ src, uint32_t idx) {
-    return src[g.src_off + (idx < g.src_len ? idx : g.src_len - 1)];
-}
-
-// s: cand_slot(g, src, idx), loaded ahead (the search loops prefetch the next
-// tile's slot ids while they rank the current one).
-__device__ __forceinline__ Cand eval_candidate(const DStore& st, const DGroup& g, const EvalFields& ef, uint32_t s,
+__device__ __forceinline__ Cand eval_candidate(const DStore& st, const DGroup& g, const uint32_t* __restrict__ src,
                                                uint32_t idx) {
     Cand c{0, idx, 0, 1, false, false};
     if (g.src_len == 0) return c;
-    // The alive byte first (a posting-list candidate is a gather: every
-    // column costs a cache line, and late in a pass most candidates are
-    // dead), then Min / Max / party and the query's columns of a live
-    // candidate together in one more round trip.
+    // unconditional loads (a clamped position past the end, masked below):
+    // the slot id, then alive / Min / Max / party in one round trip
     const bool valid = idx < g.src_len;
+    const uint32_t s = src[g.src_off + (valid ? idx : g.src_len - 1)];
     const uint8_t al = st.alive[s];
-    if (!valid) return c;
-    c.slot = s;
-    c.live = al != 0;
-    if (!c.live) return c;
     const int32_t mn = st.minc[s], mx = st.maxc[s];
     const uint32_t pt = g.tparty != kNoParty ? st.party[s] : 0u;
-    Loaded L;
-    if (ef.n > 0) load_fields(ef, s, L);
-    bool m = mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
+    if (!valid) return c;
+    c.slot = s;
+    bool m = al != 0;
+    c.live = m;
+    m = m && mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
     double sp = 0.0;
-    if (m)
-        m = ef.n >= 0 ? eval_loaded(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, ef, L, &sp)
-                      : eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
+    if (m) m = eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
     if (m) {
         // top-level BooleanQuery{must: parsed, min_count range, max_count range}
         c.key = dsortable((sp + 1.0) + 1.0);
@@ -250,9 +155,6 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     uint32_t my_live = 0;
     if (tid == 0) s_live = 0;
     __syncthreads();
-    const EvalFields ef = eval_fields(st, g.qkind, st.clauses + g.clause_off, g.n_clauses);
-    // the next tile's slot ids are loaded while the current tile is ranked
-    uint32_t s_next = g.src_len ? cand_slot(g, src, tid) : 0u;
 
     if (!g.var_score) {
         // ---- ordered compaction -------------------------------------------------
@@ -260,9 +162,7 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
         uint32_t base = 0;
         bool stopped = false;
         for (; base < g.src_len; base += kBlock) {
-            const uint32_t s_cur = s_next;
-            if (base + kBlock < g.src_len) s_next = cand_slot(g, src, base + kBlock + tid);
-            Cand c = eval_candidate(st, g, ef, s_cur, base + tid);
+            Cand c = eval_candidate(st, g, src, base + tid);
             my_live += c.live;
             const uint64_t mask = __ballot(c.m);
             if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(mask);
@@ -300,9 +200,7 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     bool early = false;
     uint32_t base = 0;
     for (; base < g.src_len; base += kBlock) {
-        const uint32_t s_cur = s_next;
-        if (base + kBlock < g.src_len) s_next = cand_slot(g, src, base + kBlock + tid);
-        Cand c = eval_candidate(st, g, ef, s_cur, base + tid);
+        Cand c = eval_candidate(st, g, src, base + tid);
         my_live += c.live;
         const uint64_t pre = __ballot(c.m);
         if (n == KK && c.m) c.m = c.key > lkey[cur][KK - 1];
@@ -389,14 +287,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* _
     const DGroup g = chunks[blockIdx.x];
     const uint32_t* __restrict__ src = (g.src_kind == 0 ? st.order : st.postings) + g.src_off;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // The slot ids, then the alive bytes (a posting list's candidates are
-    // gathers: every column costs a cache line, and dead candidates read no
-    // more), then Min / Max / party and — when the query reads at most two
-    // fields (C1, C4: mode x region) — its columns for the live candidates,
-    // all in one round trip, instead of a dependent load per filter stage and
-    // per clause.
-    const EvalFields ef = eval_fields(st, g.qkind, st.clauses + g.clause_off, g.n_clauses);
-    const bool pre = ef.n >= 1 && ef.n <= 2;
     uint32_t s[kScanJ];
     bool m[kScanJ];
 #pragma unroll
@@ -409,22 +299,13 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* _
     uint32_t live = 0;
 #pragma unroll
     for (int j = 0; j < kScanJ; j++) live += m[j];
-    uint8_t fk0[kScanJ], fk1[kScanJ];
-    int64_t fv0[kScanJ], fv1[kScanJ];
 #pragma unroll
-    for (int j = 0; j < kScanJ; j++) {
-        if (!m[j]) continue;
-        const int32_t mn = st.minc[s[j]], mx = st.maxc[s[j]];
-        const uint32_t pt = g.tparty != kNoParty ? st.party[s[j]] : 0u;
-        if (pre) {
-            fk0[j] = ef.kp[0][s[j]];
-            fv0[j] = ef.vp[0][s[j]];
-            if (ef.n == 2) {
-                fk1[j] = ef.kp[1][s[j]];
-                fv1[j] = ef.vp[1][s[j]];
-            }
-        }
-        m[j] = mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
+    for (int j = 0; j < kScanJ; j++)
+        if (m[j]) m[j] = st.minc[s[j]] >= g.tmin && st.maxc[s[j]] <= g.tmax;
+    if (g.tparty != kNoParty) {
+#pragma unroll
+        for (int j = 0; j < kScanJ; j++)
+            if (m[j]) m[j] = st.party[s[j]] != g.tparty;
     }
     // parsed query (eval_parsed, one clause at a time over the lane's candidates)
     double ms[kScanJ], ss[kScanJ];
@@ -443,18 +324,14 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const DGroup* _
             has_should |= k.occur == OCC_SHOULD;
             const int64_t* __restrict__ fv = st.fval[k.field];
             const uint8_t* __restrict__ fk = st.fkind[k.field];
-            const int sel = pre ? (k.field == ef.f[0] ? 0 : 1) : -1;
 #pragma unroll
             for (int j = 0; j < kScanJ; j++) {
                 if (!m[j]) continue;
                 bool h = false;
                 double sc = k.score;
                 if (k.op != OP_FALSE) {
-                    uint8_t kind;
-                    int64_t val;
-                    if (sel == 0) { kind = fk0[j]; val = fv0[j]; }
-                    else if (sel == 1) { kind = fk1[j]; val = fv1[j]; }
-                    else { kind = fk[s[j]]; val = fv[s[j]]; }
+                    const uint8_t kind = fk[s[j]];
+                    const int64_t val = fv[s[j]];
                     if (k.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)k.term;
                     else if (k.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= k.lo && val <= k.hi;
                     else if (k.op == OP_TERMSET) h = kind == KIND_KEYWORD && termset_hit(st, k.term, val, &sc);
@@ -962,28 +839,15 @@ __global__ __launch_bounds__(kBlock) void rsmall_kernel(DStore st, const DGroup*
     uint32_t s = kNoSlot;
     int64_t key = 0;
     uint8_t rv = 1;
-    const EvalFields ef = eval_fields(st, g.qkind, st.clauses + g.clause_off, g.n_clauses);
     if (j < g.src_len) {
         s = src[j];
-        // the alive byte, then one round trip for every column a live
-        // candidate's predicate reads and its own query descriptor (the
-        // reverse check)
         live = st.alive[s] != 0;
-        DQuery q{};
-        if (live) {
-            const int32_t mn = st.minc[s], mx = st.maxc[s];
-            const uint32_t pt = st.party[s];
-            q = st.squery[s];
-            Loaded L;
-            if (ef.n > 0) load_fields(ef, s, L);
-            m = mn >= g.tmin && mx <= g.tmax && (g.tparty == kNoParty || pt != g.tparty);
-            double sp = 0.0;
-            if (m)
-                m = ef.n >= 0 ? eval_loaded(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, ef, L, &sp)
-                              : eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
-            if (m) key = dsortable((sp + 1.0) + 1.0);
-        }
+        m = live && st.minc[s] >= g.tmin && st.maxc[s] <= g.tmax && (g.tparty == kNoParty || st.party[s] != g.tparty);
+        double sp = 0.0;
+        if (m) m = eval_parsed(st, g.qkind, st.clauses + g.clause_off, g.n_clauses, s, &sp);
         if (m) {
+            key = dsortable((sp + 1.0) + 1.0);
+            const DQuery q = st.squery[s];
             double d;
             rv = eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, g.rev_slot, &d) ? 1 : 0;
         }

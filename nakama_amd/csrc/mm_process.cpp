@@ -405,8 +405,10 @@ struct Replay : ReplayCore {
         // 4-B slot ids plus each list's last DHit (its cursor) — unless the
         // host needs every key (full-list searches are sorted by key here) or
         // the lists are exchanged between ranks as DHits (row-sharded).
+        // RevPrecision batches keep DHits: C5's 8-entry rsmall lists measured
+        // 5-10 % slower per pass with the pack (profiles/r02c_ab_configs.txt).
         const uint64_t scan_end = off;
-        const bool slots_only = c.slot_lists_mode_ && full_var.empty() && !c.row_shard() && scan_end > 0;
+        const bool slots_only = c.slot_lists_mode_ && full_var.empty() && !c.row_shard() && !rev && scan_end > 0;
         // mscan: signatures (DMSig, clause_off indexing mcl), result cells after the chunks
         const uint32_t mchunk = ms.chunk;
         const uint64_t mscratch = scratch;
@@ -975,21 +977,37 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
     if (dense_pools_.size() < ng) dense_pools_.resize(ng);
     if (pos_of_.size() < nslots()) pos_of_.resize(nslots(), kNoSlot);
     const ReplayView rv = Replay::view(*this);
-    std::vector<std::pair<uint32_t, uint32_t>> chunks;  // (pool, chunk) of the dense gathers
-    constexpr uint32_t kGatherChunk = 16384;
+    // The gathers run in tasks that each take the same fraction of EVERY
+    // dense pool's list: the pools interleave in scan order, so task t's
+    // pieces all read one slot region and the store lines it touches (2
+    // HotRecs, 16 Intervals / pos_of words per line) are shared by the pools'
+    // pieces while they sit in the core's cache — per-pool tasks read each
+    // line once per pool (C4: 64 pools, every read a miss).
+    constexpr uint32_t kGatherTask = 16384;  // list positions per task, over all pools
     std::vector<uint8_t> dense(ng, 0);
+    std::vector<uint32_t> dense_ids;
+    uint64_t dense_total = 0;
     for (size_t gi = 0; gi < ng; gi++) {
         if (soff[gi + 1] - soff[gi] != 1 || !dense_mode_ || rev) continue;  // the dense walk has no reverse checks
         if (!bg[sidx[soff[gi]]].complete) continue;                        // nor pages
         dense[gi] = 1;
         DensePool& D = dense_pools_[gi];
         D.reset(bg[sidx[soff[gi]]], P.pool_rows.data() + P.pool_off[gi], (uint32_t)prows(gi), brow.data());
-        for (uint32_t c = 0; c * kGatherChunk < D.n; c++) chunks.push_back({(uint32_t)gi, c});
+        dense_ids.push_back((uint32_t)gi);
+        dense_total += D.n;
     }
-    wp.run(chunks.size(), [&](size_t t) {
-        DensePool& D = dense_pools_[chunks[t].first];
-        const uint32_t lo = chunks[t].second * kGatherChunk;
-        D.gather(rv, lo, std::min(D.n, lo + kGatherChunk), pos_of_.data());
+    const size_t ntask_g = (size_t)((dense_total + kGatherTask - 1) / kGatherTask);
+    auto piece = [&](const DensePool& D, size_t t, uint32_t& lo, uint32_t& hi) {
+        lo = (uint32_t)((uint64_t)D.n * t / ntask_g);
+        hi = (uint32_t)((uint64_t)D.n * (t + 1) / ntask_g);
+    };
+    wp.run(ntask_g, [&](size_t t) {
+        for (uint32_t gi : dense_ids) {
+            DensePool& D = dense_pools_[gi];
+            uint32_t lo, hi;
+            piece(D, t, lo, hi);
+            D.gather(rv, lo, hi, pos_of_.data());
+        }
     });
     std::vector<double> task_ms(ntask, 0.0);
     std::vector<uint64_t> task_hits(ntask, 0);
@@ -1057,10 +1075,13 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
         task_ms[t] = msd(tw0, clk::now());
     };
     wp.run(ntask, worker);
-    wp.run(chunks.size(), [&](size_t t) {
-        const DensePool& D = dense_pools_[chunks[t].first];
-        const uint32_t lo = chunks[t].second * kGatherChunk;
-        D.clear_pos(lo, std::min(D.n, lo + kGatherChunk), pos_of_.data());
+    wp.run(ntask_g, [&](size_t t) {
+        for (uint32_t gi : dense_ids) {
+            const DensePool& D = dense_pools_[gi];
+            uint32_t lo, hi;
+            piece(D, t, lo, hi);
+            D.clear_pos(lo, hi, pos_of_.data());
+        }
     });
     const auto tp2 = clk::now();
     for (uint32_t v : pool_stop) *min_stop = std::min(*min_stop, v);
