@@ -18,6 +18,8 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
+#include <utility>
 #include <unordered_map>
 #include <vector>
 
@@ -273,10 +275,47 @@ enum BuiltinField : uint16_t { F_TICKET = 0, F_MIN = 1, F_MAX = 2, F_PARTY = 3, 
 
 // Matched (or candidate) groups of a pass as a flat CSR of (slot, presence
 // index) entries: group g = ents[off[g], off[g+1]).
+// std::allocator whose value-less construct() default-initialises, so
+// resize() of trivially constructible elements leaves them unwritten: the
+// pass's output arrays are filled in full by the parallel merges, and
+// std::vector's value-initialisation was a serial zero-fill of the whole
+// output ahead of them (C3: 21 MB per pass).
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInitAlloc<U>;
+    };
+    DefaultInitAlloc() = default;
+    template <class U>
+    DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using UVec = std::vector<T, DefaultInitAlloc<T>>;
+
+// One group entry: (ticket slot, presence index).  Trivially default
+// constructible (see DefaultInitAlloc); converts from the replay's pairs.
+struct GroupEntry {
+    uint32_t first;
+    int second;
+    GroupEntry() = default;
+    constexpr GroupEntry(uint32_t a, int b) : first(a), second(b) {}
+    GroupEntry(const std::pair<uint32_t, int>& p) : first(p.first), second(p.second) {}
+};
+static_assert(std::is_trivially_default_constructible<GroupEntry>::value, "GroupEntry: no zero-fill on resize");
+
 struct GroupList {
-    using Entry = std::pair<uint32_t, int>;
-    std::vector<uint32_t> off{0};
-    std::vector<Entry> ents;
+    using Entry = GroupEntry;
+    UVec<uint32_t> off{0};
+    UVec<Entry> ents;
     size_t size() const { return off.size() - 1; }
     bool empty() const { return off.size() == 1; }
     template <class It>
@@ -284,7 +323,7 @@ struct GroupList {
         ents.insert(ents.end(), b, e);
         off.push_back((uint32_t)ents.size());
     }
-    void push(const std::vector<Entry>& g) { push(g.begin(), g.end()); }
+    void push(const std::vector<std::pair<uint32_t, int>>& g) { push(g.begin(), g.end()); }
     void clear() {
         off.resize(1);
         ents.clear();
@@ -529,10 +568,10 @@ private:
     bool replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
                          const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                          GroupList& out_groups,
-                         std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats,
+                         std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats,
                          bool rev, uint32_t* min_stop);
     std::vector<uint8_t> dec_;  // per pass: rows a parallel replay decided ahead of the pass's row pointer
-    void apply_selected_to_device(const std::vector<uint32_t>& slots);
+    void apply_selected_to_device(const uint32_t* slots, size_t n);
 
     std::mutex mu_;
     mm_config cfg_;
@@ -560,7 +599,8 @@ public:
     Dict party_dict_;                 // party ids (rebuilt at compaction)
     // per-pass scratch, kept across passes (no page faults on the hot path)
     std::vector<uint8_t> sel_;
-    std::vector<uint32_t> rows_, brow_, brow_group_, newly_, list_tmp_;
+    std::vector<uint32_t> rows_, brow_, brow_group_, list_tmp_;
+    UVec<uint32_t> newly_;  // slots selected by the batch (filled in full by the merges)
     GroupList pass_groups_;
     std::vector<uint32_t> expired_;
     std::vector<BGroup> bg_;              // a pass's batch searches (kept: capacity reused)
@@ -569,9 +609,9 @@ public:
     std::vector<DensePool> dense_pools_;  // dense replay per pool (kept: capacity reused)
     std::vector<PoolOut> pool_outs_;      // few-pool replays: each pool's records
     void merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
-                     GroupList& out_groups, std::vector<uint32_t>& expired, std::vector<uint32_t>& newly);
+                     GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly);
     void merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
-                    GroupList& out_groups, std::vector<uint32_t>& expired, std::vector<uint32_t>& newly);
+                    GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly);
     std::vector<uint32_t> pos_of_;        // slot -> list position during a dense replay, else kNoSlot
     Dict field_dict_;                 // field names -> field id
     std::vector<const char*> tk_ptr_;  // per slot: NUL-terminated ticket id in tk_arena_

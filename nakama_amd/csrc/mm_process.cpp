@@ -911,7 +911,7 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
 bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
                            const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                            GroupList& out_groups,
-                           std::vector<uint32_t>& expired, std::vector<uint32_t>& newly, PassStats& stats, bool rev,
+                           std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
                            uint32_t* min_stop) {
     *min_stop = UINT32_MAX;
     if (!P.ok) return false;
@@ -1101,7 +1101,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
 
 // Merge of per-row records (many pools) back into the pinned row order.
 void Core::merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
-                      GroupList& out_groups, std::vector<uint32_t>& expired, std::vector<uint32_t>& newly) {
+                      GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly) {
     WorkPool& wp = workers();
     const RowRec* rr = row_recs_.data();
     struct Cnt { size_t g = 0, e = 0, x = 0; };
@@ -1155,7 +1155,7 @@ void Core::merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, 
 // chunk-local row map).  Applies the rows' pending Intervals increments on
 // the way.
 void Core::merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
-                       GroupList& out_groups, std::vector<uint32_t>& expired, std::vector<uint32_t>& newly) {
+                       GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly) {
     using Rec = PoolRec;
     auto& outs = pool_outs_;
     WorkPool& wp = workers();
@@ -1306,7 +1306,7 @@ int Core::process_default(GroupList& out_groups,
     bg.clear();
     std::vector<uint32_t>& brow = brow_;
     std::vector<uint32_t>& brow_group = brow_group_;
-    std::vector<uint32_t>& newly = newly_;
+    UVec<uint32_t>& newly = newly_;
     std::vector<std::pair<uint32_t, int>> grp;
     const uint32_t kvar = (uint32_t)var_k_capacity();
     size_t pos = 0;
@@ -1562,7 +1562,7 @@ int Core::process_default(GroupList& out_groups,
             stats.parallel_batches++;
             const auto tr = std::chrono::steady_clock::now();
             stats.replay_ms += std::chrono::duration<double, std::milli>(tr - tb1).count();
-            apply_selected_to_device(newly);
+            apply_selected_to_device(newly.data(), newly.size());
             stats.apply_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
             if (batch_profile_)
                 std::fprintf(stderr, "[nkm]   batch %d (parallel): rows %zu searches %zu%s | search %.2f replay %.2f ms\n",
@@ -1625,7 +1625,7 @@ int Core::process_default(GroupList& out_groups,
         }
         const auto tb2 = std::chrono::steady_clock::now();
         stats.replay_ms += std::chrono::duration<double, std::milli>(tb2 - tb1).count();
-        apply_selected_to_device(newly);
+        apply_selected_to_device(newly.data(), newly.size());
         if (batch_profile_)
             std::fprintf(stderr, "[nkm]   batch %d: rows %zu searches %zu decided %zu%s | assemble %.2f search %.2f replay %.2f ms\n",
                          stats.batches, brow.size(), bg.size(), done, exhausted ? " (list ran out)" : "",

@@ -1318,7 +1318,7 @@ void Core::sync_device() {
         std::vector<uint32_t> v;
         for (uint32_t s : pending_dead_)
             if (s < dev_slots_) v.push_back(s);
-        if (!v.empty()) apply_selected_to_device(v);
+        if (!v.empty()) apply_selected_to_device(v.data(), v.size());
         pending_dead_.clear();
     }
     dev_slots_ = n;
@@ -1379,18 +1379,18 @@ DStore Core::dstore() const {
 // Clears the device alive flags of the given slots.  Asynchronous: the copy
 // and kernel are ordered before the next search on the library's stream; the
 // pinned staging buffer is reused only after the previous copy completed.
-void Core::apply_selected_to_device(const std::vector<uint32_t>& slots) {
-    if (slots.empty()) return;
+void Core::apply_selected_to_device(const uint32_t* slots, size_t n_slots) {
+    if (!n_slots) return;
     if (apply_pending_) {
         NKM_HIP(hipEventSynchronize(apply_ev_));
         apply_pending_ = false;
     }
-    h_slots_tmp_.reserve(slots.size());
-    std::memcpy(h_slots_tmp_.p, slots.data(), slots.size() * sizeof(uint32_t));
-    d_slots_tmp_.reserve(slots.size(), false);
-    NKM_HIP(hipMemcpyAsync(d_slots_tmp_.p, h_slots_tmp_.p, slots.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+    h_slots_tmp_.reserve(n_slots);
+    std::memcpy(h_slots_tmp_.p, slots, n_slots * sizeof(uint32_t));
+    d_slots_tmp_.reserve(n_slots, false);
+    NKM_HIP(hipMemcpyAsync(d_slots_tmp_.p, h_slots_tmp_.p, n_slots * sizeof(uint32_t), hipMemcpyHostToDevice,
                            stream_));
-    NKM_HIP(launch_clear_alive(d_alive_.p, d_slots_tmp_.p, (uint32_t)slots.size(), stream_));
+    NKM_HIP(launch_clear_alive(d_alive_.p, d_slots_tmp_.p, (uint32_t)n_slots, stream_));
     NKM_HIP(hipEventRecord(apply_ev_, stream_));
     apply_pending_ = true;
 }
