@@ -563,10 +563,10 @@ private:
     std::vector<std::vector<std::pair<uint32_t, int>>> task_ents_;
     std::vector<uint32_t> pool_remap_;  // dictionary id -> pool (one-field pool keys)
     ParPlan par_plan_;
-    bool plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
-                       const std::vector<uint32_t>& brow_group, ParPlan& P, PassStats& stats);
-    bool replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
-                         const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
+    bool plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
+                       const UVec<uint32_t>& brow_group, ParPlan& P, PassStats& stats);
+    bool replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
+                         const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                          GroupList& out_groups,
                          std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats,
                          bool rev, uint32_t* min_stop);
@@ -599,7 +599,8 @@ public:
     Dict party_dict_;                 // party ids (rebuilt at compaction)
     // per-pass scratch, kept across passes (no page faults on the hot path)
     std::vector<uint8_t> sel_;
-    std::vector<uint32_t> rows_, brow_, brow_group_, list_tmp_;
+    std::vector<uint32_t> rows_, list_tmp_;
+    UVec<uint32_t> brow_, brow_group_;  // the batch's rows and their searches (filled in full)
     UVec<uint32_t> newly_;  // slots selected by the batch (filled in full by the merges)
     GroupList pass_groups_;
     std::vector<uint32_t> expired_;
@@ -608,9 +609,9 @@ public:
     std::vector<uint32_t> lg_group_;
     std::vector<DensePool> dense_pools_;  // dense replay per pool (kept: capacity reused)
     std::vector<PoolOut> pool_outs_;      // few-pool replays: each pool's records
-    void merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
+    void merge_pools(size_t ng, size_t nch, const UVec<uint32_t>& brow, std::vector<uint8_t>& sel,
                      GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly);
-    void merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
+    void merge_rows(size_t nb, size_t nch, const UVec<uint32_t>& brow, std::vector<uint8_t>& sel,
                     GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly);
     std::vector<uint32_t> pos_of_;        // slot -> list position during a dense replay, else kNoSlot
     Dict field_dict_;                 // field names -> field id

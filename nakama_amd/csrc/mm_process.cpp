@@ -764,8 +764,8 @@ struct Replay : ReplayCore {
 // The part of the pool-parallel replay that needs no hit list — the pool
 // keys and the rows bucketed per pool — run while the batch's searches are
 // on the device.  Returns false when the batch does not partition into pools.
-bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
-                         const std::vector<uint32_t>& brow_group, ParPlan& P, PassStats& stats) {
+bool Core::plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
+                         const UVec<uint32_t>& brow_group, ParPlan& P, PassStats& stats) {
     P.ok = false;
     const size_t nsearch = bg.size();
     if (nsearch < 2) return false;
@@ -908,8 +908,8 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const std::vector<uint32
 // one pass over the batch in row order assembles the groups, the expired list
 // and the Intervals increments — processDefault's sequential order, because
 // no pool ever selects another pool's ticket.
-bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std::vector<uint32_t>& brow,
-                           const std::vector<uint32_t>& brow_group, std::vector<uint8_t>& sel,
+bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
+                           const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                            GroupList& out_groups,
                            std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
                            uint32_t* min_stop) {
@@ -931,14 +931,13 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
     const DStore st = dstore();
     const int maxI = cfg_.max_intervals;
     // each pool's searches (CSR) and each search's index among them
-    std::vector<uint32_t> soff(ng + 1, 0), sidx(nsearch), local_idx(nsearch);
+    std::vector<uint32_t> soff(ng + 1, 0), sidx(nsearch);
     for (size_t i = 0; i < nsearch; i++) soff[search_pool[i] + 1]++;
     for (size_t p = 0; p < ng; p++) soff[p + 1] += soff[p];
     {
         std::vector<uint32_t> at(soff.begin(), soff.end() - 1);
         for (size_t i = 0; i < nsearch; i++) {
             const uint32_t p = search_pool[i];
-            local_idx[i] = at[p] - soff[p];
             sidx[at[p]++] = (uint32_t)i;
         }
     }
@@ -1037,7 +1036,6 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
         if (tl_proc.size() < sel.size()) tl_proc.resize(sel.size(), 0);
         PassStats ls;
         Replay rp(*this, tl_sel, rev, maxI, ls, st, stream_);
-        std::vector<BGroup> mine;
         std::vector<uint32_t> rows_of;
         for (uint32_t k = task_off[t]; k < task_off[t + 1]; k++) {
             const uint32_t gi = order_g[k];
@@ -1061,12 +1059,10 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
                     rr[r.bi] = RowRec{base + r.off, r.len, (uint32_t)t, r.matched, r.expired, 1, 0};
                 continue;
             } else {
-                mine.clear();
-                for (uint32_t j = soff[gi]; j < soff[gi + 1]; j++) mine.push_back(bg[sidx[j]]);
                 rows_of.assign(P.pool_rows.begin() + P.pool_off[gi], P.pool_rows.begin() + P.pool_off[gi + 1]);
                 rp.hits_seen = 0;
                 pool_stop[gi] = replay_pool(rp, rows_of, brow.data(),
-                                            [&](uint32_t bi) -> BGroup& { return mine[local_idx[brow_group[bi]]]; },
+                                            [&](uint32_t bi) -> BGroup& { return bg[brow_group[bi]]; },
                                             tl_sel, tl_proc.data(), minc_.data(), maxc_.data(), po);
                 task_hits[t] += rp.hits_seen;
             }
@@ -1100,7 +1096,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const std:
 }
 
 // Merge of per-row records (many pools) back into the pinned row order.
-void Core::merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
+void Core::merge_rows(size_t nb, size_t nch, const UVec<uint32_t>& brow, std::vector<uint8_t>& sel,
                       GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly) {
     WorkPool& wp = workers();
     const RowRec* rr = row_recs_.data();
@@ -1154,7 +1150,7 @@ void Core::merge_rows(size_t nb, size_t nch, const std::vector<uint32_t>& brow, 
 // merges its share of the pools' records independently (through a
 // chunk-local row map).  Applies the rows' pending Intervals increments on
 // the way.
-void Core::merge_pools(size_t ng, size_t nch, const std::vector<uint32_t>& brow, std::vector<uint8_t>& sel,
+void Core::merge_pools(size_t ng, size_t nch, const UVec<uint32_t>& brow, std::vector<uint8_t>& sel,
                        GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly) {
     using Rec = PoolRec;
     auto& outs = pool_outs_;
@@ -1304,8 +1300,8 @@ int Core::process_default(GroupList& out_groups,
     std::vector<int32_t> sig_group(sigs_.size(), -1);
     std::vector<BGroup>& bg = bg_;  // kept across passes: no page faults on the hot path
     bg.clear();
-    std::vector<uint32_t>& brow = brow_;
-    std::vector<uint32_t>& brow_group = brow_group_;
+    UVec<uint32_t>& brow = brow_;
+    UVec<uint32_t>& brow_group = brow_group_;
     UVec<uint32_t>& newly = newly_;
     std::vector<std::pair<uint32_t, int>> grp;
     const uint32_t kvar = (uint32_t)var_k_capacity();
