@@ -12,7 +12,7 @@ IFS=';' read -ra SETS <<< "$LIST"
 for a in "${SETS[@]}"; do
   for t in ${AB_TREES:-ab_old . ab_old .}; do
     echo "== $t $a" >> gpurun_out/abc.err
-    (cd $t && NKM_PROFILE=1 timeout -k 10 300 python bench.py $a --steps 3 --warmup 1 --no-cpu-baseline | sed "s/^{/{\"tree\": \"$t\", \"args\": \"$a\", /") >> gpurun_out/abc.jsonl 2>> gpurun_out/abc.err || exit 1
+    (cd $t && NKM_PROFILE=1 timeout -k 10 300 python bench.py $a --steps ${ABSTEPS:-8} --warmup 2 --no-cpu-baseline | sed "s/^{/{\"tree\": \"$t\", \"args\": \"$a\", /") >> gpurun_out/abc.jsonl 2>> gpurun_out/abc.err || exit 1
   done
 done
 echo EXIT $?
