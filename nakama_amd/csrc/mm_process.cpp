@@ -81,15 +81,17 @@ struct Replay : ReplayCore {
     // Fetches the next page of a group's list (cursor = its last entry).
     void fetch_more(BGroup& g) override {
         stats.refetches++;
-        // a slot list (run_batch's packed lists): its cursor is g.last
-        const bool slot_list = !g.hits && g.sp;
-        if (slot_list && g.n && g.last.slot == kNoSlot)  // an mscan list: complete by construction
-            throw DeviceError{hipErrorUnknown, "page of a slot list without a cursor", __LINE__};
-        if (slot_list) {
-            if (g.ext_slots.empty() && g.n) {
-                g.ext_slots.assign(g.sp, g.sp + g.n);
-                if (g.rev) g.ext_rev.assign(g.rev, g.rev + g.n);
-            }
+        // A slot list (run_batch's packed lists) becomes a DHit list: its
+        // entries' slots, and as the last entry the cursor the batch kept
+        // (Core::h_last_) — the only entry whose key and position are read.
+        if (!g.hits && g.sp && g.n) {
+            if (g.last_i == UINT32_MAX)  // an mscan list: complete by construction
+                throw DeviceError{hipErrorUnknown, "page of a slot list without a cursor", __LINE__};
+            g.ext.resize(g.n);
+            for (uint32_t k = 0; k < g.n; k++) g.ext[k] = DHit{g.sp[k], 0u, 0};
+            g.ext[g.n - 1] = c.h_last_.p[g.last_i];
+            if (g.rev) g.ext_rev.assign(g.rev, g.rev + g.n);
+            g.set_hits(g.ext.data());
         } else if (g.ext.empty() && g.n) {
             g.ext.assign(g.hits, g.hits + g.n);
             if (g.rev) g.ext_rev.assign(g.rev, g.rev + g.n);
@@ -98,9 +100,8 @@ struct Replay : ReplayCore {
         d.out_off = 0;
         d.has_cursor = g.n ? 1 : 0;
         if (g.n) {
-            const DHit& lh = slot_list ? g.last : g.hits[g.n - 1];
-            d.cur_key = lh.key;
-            d.cur_idx = lh.idx;
+            d.cur_key = g.hits[g.n - 1].key;
+            d.cur_idx = g.hits[g.n - 1].idx;
         }
         // constant-score pages double, but never past the rest of the source
         d.k = d.var_score ? (uint32_t)var_k_capacity()
@@ -142,18 +143,11 @@ struct Replay : ReplayCore {
         stats.pair_evals += r.scanned;
         stats.k_bytes[0] += search_bytes(c.sigs_[g.sig].n_fields, d, r);
         stats.k_launches[0]++;
+        g.ext.insert(g.ext.end(), c.h_page_.p, c.h_page_.p + r.count);
         if (rev) g.ext_rev.insert(g.ext_rev.end(), c.h_page_rev_.p, c.h_page_rev_.p + r.count);
+        g.set_hits(g.ext.data());
         g.rev = rev ? g.ext_rev.data() : nullptr;
-        if (slot_list) {
-            for (uint32_t k = 0; k < r.count; k++) g.ext_slots.push_back(c.h_page_.p[k].slot);
-            if (r.count) g.last = c.h_page_.p[r.count - 1];
-            g.set_slots(g.ext_slots.data());
-            g.n = (uint32_t)g.ext_slots.size();
-        } else {
-            g.ext.insert(g.ext.end(), c.h_page_.p, c.h_page_.p + r.count);
-            g.set_hits(g.ext.data());
-            g.n = (uint32_t)g.ext.size();
-        }
+        g.n = (uint32_t)g.ext.size();
         g.complete = r.complete != 0;
         g.d.k = d.k;
     }
@@ -679,7 +673,7 @@ struct Replay : ReplayCore {
                 g.head = 0;
                 if (slots_only) {
                     g.set_slots(c.h_slots_.p + lg[i].out_off);
-                    g.last = c.h_last_.p[i];
+                    g.last_i = (uint32_t)i;
                 } else {
                     g.set_hits(c.h_out_.p + lg[i].out_off);
                 }
@@ -719,7 +713,7 @@ struct Replay : ReplayCore {
                                        hipMemcpyDeviceToHost, stream));
             }
             g.head = 0;
-            g.last = DHit{kNoSlot, 0, 0};
+            g.last_i = packed ? (uint32_t)(nwhole + k) : UINT32_MAX;
             if (slots) g.set_slots(reinterpret_cast<const uint32_t*>(c.h_out_.p + cg_off[k]));
             else if (packed) g.set_slots(c.h_slots_.p + cg_off[k]);
             else g.set_hits(c.h_out_.p + cg_off[k]);
@@ -730,11 +724,6 @@ struct Replay : ReplayCore {
             g.complete = complete;
         }
         if (!cg_list.empty()) NKM_HIP(hipStreamSynchronize(stream));
-        if (slots_only)  // the chunked lists' cursors (copied above)
-            for (size_t k = 0; k < n_scan_cg; k++) {
-                BGroup& g = bg[cg_list[k]];
-                g.last = g.n ? c.h_last_.p[nwhole + k] : DHit{kNoSlot, 0, 0};
-            }
     }
 
     bool pair_slow(const BGroup& g, uint32_t from_pos, uint32_t to_pos) override {

@@ -79,6 +79,10 @@ struct BGroup {
     const DHit* hits = nullptr;
     const uint32_t* sp = nullptr;
     uint32_t ss = 4;
+    // a slot list's last entry (its pagination cursor: score key and source
+    // position) is kept by the batch beside the lists (Core::h_last_): its
+    // index there, or UINT32_MAX (an mscan list: complete, never paged)
+    uint32_t last_i = UINT32_MAX;
     uint32_t slot(uint32_t i) const { return sp[(size_t)i * ss]; }
     void set_hits(const DHit* h) {
         hits = h;
@@ -90,9 +94,6 @@ struct BGroup {
         sp = s;
         ss = 1;
     }
-    // a slot list's last entry (its pagination cursor: score key and source
-    // position), kept beside it because the list itself holds slots only
-    DHit last{kNoSlot, 0, 0};
     const uint8_t* rev = nullptr;
     const uint32_t* pm = nullptr;  // kPairP masks per entry (rev rows with combos)
     uint32_t pm_n = 0;             // entries covered by pm
@@ -103,7 +104,6 @@ struct BGroup {
     bool complete = true;
     uint32_t head = 0;
     std::vector<DHit> ext;
-    std::vector<uint32_t> ext_slots;  // a paged slot list
     std::vector<uint8_t> ext_rev;
     // back to a default-constructed search, keeping the vectors' capacity
     // (a reused batch array is refilled in place by the host workers)
@@ -116,6 +116,7 @@ struct BGroup {
         hits = nullptr;
         sp = nullptr;
         ss = 4;
+        last_i = UINT32_MAX;
         rev = nullptr;
         pm = nullptr;
         pm_n = 0;
@@ -126,9 +127,8 @@ struct BGroup {
         complete = true;
         head = 0;
         ext.clear();
-        ext_slots.clear();
         ext_rev.clear();
-        last = DHit{kNoSlot, 0, 0};
+        last_i = UINT32_MAX;
     }
 };
 
