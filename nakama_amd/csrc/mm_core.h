@@ -762,6 +762,7 @@ public:
     int par_mode_ = 1;  // 0 off, 1 auto, 2 force
     // NKM_DENSE=0: single-search pools take the generic walk too (A/B, tests)
     bool dense_mode_ = true;
+    bool pipe_mode_ = true;  // NKM_PIPE=0: the pool walks' merge runs after all walks, not beside them
     // NKM_FAST=0: every row takes the exact loop body, also when no two live
     // tickets share a session (the fast walk, replay_core.h) (A/B, tests)
     bool fast_mode_ = true;

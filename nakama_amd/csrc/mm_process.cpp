@@ -989,14 +989,106 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         lo = (uint32_t)((uint64_t)D.n * t / ntask_g);
         hi = (uint32_t)((uint64_t)D.n * (t + 1) / ntask_g);
     };
+    // Pipelined merge: with few pools, all dense, the merge runs in the same
+    // job as the walks — tasks [0, ntask) walk, the next nch tasks merge one
+    // chunk of batch rows each as soon as every walk has passed the chunk's
+    // end (tasks are claimed in index order, so every walk is running before
+    // any merge waits).  C3's 8 walks would otherwise leave 8 of 16 workers
+    // idle while the merge waits for the slowest walk.
+    const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
+    const bool pipe = few && pipe_mode_ && !dense_ids.empty() && dense_ids.size() == ng && nch > 1;
+    // each pool's entry bound (every ticket of its list and rows joins at
+    // most one group): the walk reserves it so readers never see a move
+    std::vector<uint64_t> esum(pipe ? ntask_g * ng : 0, 0);
     wp.run(ntask_g, [&](size_t t) {
         for (uint32_t gi : dense_ids) {
             DensePool& D = dense_pools_[gi];
             uint32_t lo, hi;
             piece(D, t, lo, hi);
             D.gather(rv, lo, hi, pos_of_.data());
+            if (!pipe) continue;
+            uint64_t e = 0;
+            for (uint32_t k = lo; k < hi; k++) e += (uint64_t)D.rec[k].count;
+            const uint32_t r0 = (uint32_t)((uint64_t)D.nrows * t / ntask_g), r1 = (uint32_t)((uint64_t)D.nrows * (t + 1) / ntask_g);
+            for (uint32_t j = r0; j < r1; j++) e += (uint64_t)rv.hot[brow[D.bis[j]]].count;
+            esum[t * ng + gi] = e;
         }
     });
+    struct alignas(128) Prog {
+        std::atomic<uint64_t> st{0};  // (records published << 32) | rows done
+        const PoolRec* recs = nullptr;
+        const std::pair<uint32_t, int>* ents = nullptr;
+    };
+    std::unique_ptr<Prog[]> prog(pipe ? new Prog[ng] : nullptr);
+    std::vector<uint64_t> ebound(pipe ? ng : 0, 0);
+    uint64_t ebound_all = 0;
+    for (size_t t = 0; pipe && t < ntask_g; t++)
+        for (size_t gi = 0; gi < ng; gi++) ebound[gi] += esum[t * ng + gi];
+    for (uint64_t e : ebound) ebound_all += e;
+    const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
+    if (pipe) {  // bounds now (no zero-fill: default-initialising vectors), the totals after the job
+        grow_to(out_groups.off, g0 + 1 + nb);
+        grow_to(out_groups.ents, e0 + ebound_all);
+        grow_to(expired, x0 + nb);
+        grow_to(newly, n0 + ebound_all);
+    }
+    // one chunk of the pipelined merge (merge_pools' chunk body, offsets
+    // from the pools' running counts instead of a global prefix)
+    auto merge_chunk = [&](size_t c) {
+        const uint32_t lo = (uint32_t)(nb * c / nch), hi = (uint32_t)(nb * (c + 1) / nch);
+        size_t gk = g0, ek = e0, xk = x0;
+        static thread_local std::vector<uint64_t> span;  // per pool: records [a, b) of the chunk
+        span.assign(ng, 0);
+        for (size_t gi = 0; gi < ng; gi++) {
+            const DensePool& D = dense_pools_[gi];
+            const uint32_t need = (uint32_t)(std::lower_bound(D.bis, D.bis + D.nrows, hi) - D.bis);
+            if (!need) continue;
+            uint64_t v;
+            while (((v = prog[gi].st.load(std::memory_order_acquire)) & 0xffffffffu) < need) std::this_thread::yield();
+            const uint32_t nrec = (uint32_t)(v >> 32);
+            const PoolRec* R = prog[gi].recs;
+            auto by_bi = [](const PoolRec& x, uint32_t b) { return x.bi < b; };
+            const uint32_t a = (uint32_t)(std::lower_bound(R, R + nrec, lo, by_bi) - R);
+            const uint32_t b = (uint32_t)(std::lower_bound(R + a, R + nrec, hi, by_bi) - R);
+            if (a < nrec) {
+                gk += R[a].gcum;
+                ek += R[a].off;
+                xk += R[a].xcum;
+            } else if (nrec) {
+                const PoolRec& l = R[nrec - 1];
+                gk += l.gcum + l.matched;
+                ek += l.off + l.len;
+                xk += l.xcum + l.expired;
+            }
+            span[gi] = ((uint64_t)b << 32) | a;
+        }
+        static thread_local std::vector<uint64_t> at_row;  // (pool << 32 | record) + 1; 0: no record
+        at_row.assign(hi - lo, 0);
+        for (size_t gi = 0; gi < ng; gi++) {
+            const PoolRec* R = prog[gi].recs;
+            for (uint32_t k = (uint32_t)span[gi]; k < (uint32_t)(span[gi] >> 32); k++)
+                at_row[R[k].bi - lo] = (((uint64_t)gi << 32) | k) + 1;
+        }
+        for (uint32_t i = 0; i < hi - lo; i++) {
+            if (!at_row[i]) continue;
+            const uint64_t v = at_row[i] - 1;
+            const Prog& pr = prog[v >> 32];
+            const PoolRec& r = pr.recs[(uint32_t)v];
+            const uint32_t T = brow[r.bi];
+            intervals_[T]++;  // the row's pending Intervals increment
+            dec_[T] = 1;      // decided: a later batch of the pass skips it
+            if (r.expired) expired[xk++] = T;
+            if (!r.matched) continue;
+            for (uint32_t k = 0; k < r.len; k++) {
+                const auto& e = pr.ents[r.off + k];
+                out_groups.ents[ek + k] = e;
+                newly[n0 + (ek - e0) + k] = e.first;
+                sel[e.first] = 1;
+            }
+            ek += r.len;
+            out_groups.off[++gk] = (uint32_t)ek;
+        }
+    };
     std::vector<double> task_ms(ntask, 0.0);
     std::vector<uint64_t> task_hits(ntask, 0);
     std::vector<uint32_t> pool_stop(ng, UINT32_MAX);  // per pool: the batch row its list ran out at
@@ -1031,6 +1123,25 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             PoolOut& po = few ? pool_outs_[gi] : o;
             po.recs.clear();
             po.ents.clear();
+            if (dense[gi] && pipe) {
+                const DensePool& D = dense_pools_[gi];
+                run.reset(D.n);
+                run.fast = fast_mode_;
+                run.recs.reserve((size_t)D.nrows + 1);
+                run.ents.reserve(ebound[gi]);
+                prog[gi].recs = run.recs.data();
+                prog[gi].ents = run.ents.data();
+                run.walk_published(D, rv, maxI, pos_of_.data(), &prog[gi].st);
+                if (run.ents.data() != prog[gi].ents || run.recs.data() != prog[gi].recs)
+                    std::abort();  // the bound above was wrong: readers hold the old buffers
+                task_hits[t] += run.hits_seen;
+                // the sentinel (its capacity was reserved), then the buffers to
+                // the pool's PoolOut (a header swap: the readers' pointers stay)
+                run.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)run.ents.size(), 0, run.g_run, run.x_run});
+                po.recs.swap(run.recs);
+                po.ents.swap(run.ents);
+                continue;
+            }
             if (dense[gi]) {
                 run.reset(dense_pools_[gi].n);
                 run.fast = fast_mode_;
@@ -1059,7 +1170,25 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         }
         task_ms[t] = msd(tw0, clk::now());
     };
-    wp.run(ntask, worker);
+    if (pipe) {
+        wp.run(ntask + nch, [&](size_t t) {
+            if (t < ntask) worker(t);
+            else merge_chunk(t - ntask);
+        });
+        size_t G = 0, E = 0, X = 0;  // totals: the pools' sentinels
+        for (size_t gi = 0; gi < ng; gi++) {
+            const PoolRec& sr = pool_outs_[gi].recs.back();
+            G += sr.gcum;
+            E += sr.off;
+            X += sr.xcum;
+        }
+        out_groups.off.resize(g0 + 1 + G);
+        out_groups.ents.resize(e0 + E);
+        expired.resize(x0 + X);
+        newly.resize(n0 + E);
+    } else {
+        wp.run(ntask, worker);
+    }
     wp.run(ntask_g, [&](size_t t) {
         for (uint32_t gi : dense_ids) {
             const DensePool& D = dense_pools_[gi];
@@ -1070,9 +1199,12 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     });
     const auto tp2 = clk::now();
     for (uint32_t v : pool_stop) *min_stop = std::min(*min_stop, v);
-    const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
-    if (few) merge_pools(ng, nch, brow, sel, out_groups, expired, newly);
-    else merge_rows(nb, nch, brow, sel, out_groups, expired, newly);
+    if (pipe) {
+    } else if (few) {
+        merge_pools(ng, nch, brow, sel, out_groups, expired, newly);
+    } else {
+        merge_rows(nb, nch, brow, sel, out_groups, expired, newly);
+    }
     const auto tp3 = clk::now();
     stats.par_work_ms += msd(tp1, tp2);
     stats.par_merge_ms += msd(tp2, tp3);

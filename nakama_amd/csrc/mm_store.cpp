@@ -98,6 +98,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     for (auto& e : ev_) NKM_HIP(hipEventCreate(&e));
     NKM_HIP(hipEventCreateWithFlags(&apply_ev_, hipEventDisableTiming));
     if (const char* e = std::getenv("NKM_DENSE")) dense_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_PIPE")) pipe_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FAST")) fast_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FULLVAR")) full_var_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_SLOTLISTS")) slot_lists_mode_ = std::strcmp(e, "0") != 0;

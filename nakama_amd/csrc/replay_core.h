@@ -7,6 +7,7 @@
 // (tools/replay_bench.cpp).
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <utility>
 #include <vector>
@@ -571,6 +572,7 @@ struct DenseRun {
     std::vector<PoolRec> recs;
     std::vector<std::pair<uint32_t, int>> ents;
     uint64_t hits_seen = 0;
+    uint32_t g_run = 0, x_run = 0;  // matched / expired records so far (PoolRec::gcum / xcum)
     // scratch
     std::vector<std::vector<CE>> combos;
     std::vector<uint32_t> cmask;
@@ -586,6 +588,7 @@ struct DenseRun {
         recs.clear();
         ents.clear();
         hits_seen = 0;
+        g_run = x_run = 0;
     }
 
     // processDefault's loop body for row index j (ReplayCore::row over the
@@ -731,7 +734,9 @@ struct DenseRun {
         }
         if (kT != kNoSlot) proc[kT] = 1;
         recs.push_back(PoolRec{bi, (uint8_t)matched, (uint8_t)last, (uint32_t)ents.size(),
-                               matched ? (uint32_t)grp.size() : 0u, 0, 0});
+                               matched ? (uint32_t)grp.size() : 0u, g_run, x_run});
+        g_run += matched;
+        x_run += last;
         if (matched) ents.insert(ents.end(), grp.begin(), grp.end());
         return true;
     }
@@ -812,7 +817,9 @@ struct DenseRun {
             if (kT != kNoSlot) sel[kT] = 1;
         }
         if (kT != kNoSlot) proc[kT] = 1;
-        recs.push_back(PoolRec{bi, (uint8_t)(fi >= 0), (uint8_t)last, off, (uint32_t)ents.size() - off, 0, 0});
+        recs.push_back(PoolRec{bi, (uint8_t)(fi >= 0), (uint8_t)last, off, (uint32_t)ents.size() - off, g_run, x_run});
+        g_run += fi >= 0;
+        x_run += last;
         return 1;
     }
 
@@ -821,6 +828,21 @@ struct DenseRun {
         const bool f = fast && v.sessions_exclusive;
         for (uint32_t j = j0; j < j1; j++)
             if (!f || fast_step(P, v, max_intervals, pos_of, j) == 2) step(P, v, max_intervals, pos_of, j);
+    }
+
+    // walk() over all rows that publishes its progress every kPublish rows
+    // for readers on other threads (the pipelined merge): one release store
+    // of (records pushed so far << 32 | rows done).  The caller reserved recs
+    // and ents so that neither reallocates under the readers.
+    void walk_published(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of,
+                        std::atomic<uint64_t>* progress) {
+        constexpr uint32_t kPublish = 512;
+        const bool f = fast && v.sessions_exclusive;
+        for (uint32_t j = 0; j < P.nrows; j++) {
+            if (!f || fast_step(P, v, max_intervals, pos_of, j) == 2) step(P, v, max_intervals, pos_of, j);
+            if ((j + 1) % kPublish == 0 || j + 1 == P.nrows)
+                progress->store(((uint64_t)recs.size() << 32) | (j + 1), std::memory_order_release);
+        }
     }
 
     // Hands the records to a PoolOut (running offsets/counts, sentinel).

@@ -231,6 +231,17 @@ def test_c3_parties_5v5(par, dense, kernel, monkeypatch):
     run_passes(3, 1500, 2, dict(max_intervals=2))
 
 
+@pytest.mark.parametrize("config,n,passes", [(3, 1500, 2), (4, 1500, 1), (1, 4000, 2)])
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_pipelined_merge(config, n, passes, pipe, monkeypatch):
+    """Forced pool-parallel replay with the merge beside the pool walks
+    (NKM_PIPE=1: each chunk of rows merged once every walk has passed it) and
+    after them (0), against the oracle."""
+    monkeypatch.setenv("NKM_PARALLEL", "force")
+    monkeypatch.setenv("NKM_PIPE", pipe)
+    run_passes(config, n, passes, dict(max_intervals=2))
+
+
 @pytest.mark.parametrize("par,dense,kernel", HOST_KERNEL)
 def test_c4_many_pools(par, dense, kernel, monkeypatch):
     monkeypatch.setenv("NKM_PARALLEL", par)
@@ -492,6 +503,10 @@ def test_parallel_host_paths_equal_serial(config, n, monkeypatch):
     assert gen == ser
     exact = _product_passes(config, n, 2, "1", monkeypatch, fast="0")
     assert exact == ser
+    monkeypatch.setenv("NKM_PIPE", "0")  # the merge after all pool walks instead of beside them
+    nopipe = _product_passes(config, n, 2, "1", monkeypatch)
+    monkeypatch.delenv("NKM_PIPE")
+    assert nopipe == ser
 
 
 # ---- regexp / wildcard / fuzzy clauses (OP_TERMSET) ----
