@@ -659,6 +659,7 @@ public:
     std::vector<uint32_t> order_;
     bool full_var_mode_ = true;  // NKM_FULLVAR=0: variable-score searches always use the LDS top-K
     bool slot_lists_mode_ = true;  // NKM_SLOTLISTS=0: hit lists come back as 16-B DHits, not 4-B slot ids
+    bool slot_lists_rev_ = false;  // NKM_SLOTLISTS=2: RevPrecision batches' lists as slot ids too
     bool page_mode_ = true;  // NKM_PAGE=0: only a batch's first row pages a truncated list
     // Batch window after a variable-score list ran out (NKM_WIN=0: off): the
     // next batch takes twice the rows the last one decided (at least

@@ -399,10 +399,10 @@ struct Replay : ReplayCore {
         // 4-B slot ids plus each list's last DHit (its cursor) — unless the
         // host needs every key (full-list searches are sorted by key here) or
         // the lists are exchanged between ranks as DHits (row-sharded).
-        // RevPrecision batches keep DHits: C5's 8-entry rsmall lists measured
-        // 5-10 % slower per pass with the pack (profiles/r02c_ab_configs.txt).
+        // NKM_SLOTLISTS=2 packs RevPrecision batches too (A/B).
         const uint64_t scan_end = off;
-        const bool slots_only = c.slot_lists_mode_ && full_var.empty() && !c.row_shard() && !rev && scan_end > 0;
+        const bool slots_only = c.slot_lists_mode_ && full_var.empty() && !c.row_shard() &&
+                                (!rev || c.slot_lists_rev_) && scan_end > 0;
         // mscan: signatures (DMSig, clause_off indexing mcl), result cells after the chunks
         const uint32_t mchunk = ms.chunk;
         const uint64_t mscratch = scratch;

@@ -101,7 +101,10 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_PIPE")) pipe_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FAST")) fast_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FULLVAR")) full_var_mode_ = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("NKM_SLOTLISTS")) slot_lists_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_SLOTLISTS")) {
+        slot_lists_mode_ = std::strcmp(e, "0") != 0;
+        slot_lists_rev_ = std::strcmp(e, "2") == 0;
+    }
     if (const char* e = std::getenv("NKM_PAGE")) page_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_WIN")) win_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FULLSRC")) full_src_mode_ = std::strcmp(e, "0") != 0;
