@@ -126,6 +126,19 @@ def test_c2_region_lists_past_topk(fullvar, monkeypatch):
     assert (full > 0) if fullvar == "1" else (full == 0)
 
 
+@pytest.mark.parametrize("mode", ["0", "2"])
+@pytest.mark.parametrize("config,n,cfg", [(2, 10_000, dict(max_intervals=2)), (4, 3000, dict(max_intervals=2)),
+                                          (5, 2000, dict(max_intervals=2, rev_precision=True, rev_threshold=0)),
+                                          (7, 3000, dict(max_intervals=2))])
+def test_hit_list_transfer_modes(config, n, cfg, mode, monkeypatch):
+    """Hit lists back to the host as 16-B DHits (NKM_SLOTLISTS=0) and as slot
+    ids for RevPrecision batches too (2; the default packs the others only),
+    with the kernel forced to the chunked scan so chunked lists page."""
+    monkeypatch.setenv("NKM_SLOTLISTS", mode)
+    monkeypatch.setenv("NKM_KERNEL", "scan")
+    run_passes(config, n, 2, cfg)
+
+
 @pytest.mark.parametrize("partial", ["1", "0"])
 def test_c2_partial_parallel_replay(partial, monkeypatch):
     """Truncated variable-score lists under the pool-parallel replay (forced
