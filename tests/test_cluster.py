@@ -263,6 +263,31 @@ def test_merge_positions():
     assert cluster.router_lib().mm_merge_positions(keys2.ctypes.data, counts2.ctypes.data, 2, 0, pos.ctypes.data) == 1
 
 
+@pytest.mark.parametrize("world,n,tie", [(8, 180_000, False), (4, 400_000, True)])
+def test_merge_positions_large(world, n, tie):
+    """The threaded walk (past 2^20 steps) against a sort of all keys: every
+    rank's positions are its keys' ranks in the merged order."""
+    from nakama_amd import cluster
+    rng = np.random.default_rng(world)
+    allk = rng.choice(np.arange(40 * world * n, dtype=np.int64), size=world * n, replace=False)
+    if tie:
+        allk[1] = allk[n + 5]  # one equal CreatedAt on two ranks
+    parts = [np.sort(allk[r * n:(r + 1) * n]) for r in range(world)]
+    keys = np.concatenate(parts)
+    counts = np.full(world, n, dtype=np.int32)
+    order = np.argsort(keys, kind="stable")
+    rank_of = np.empty(len(keys), dtype=np.int64)
+    rank_of[order] = np.arange(len(keys))
+    for r in range(world):
+        pos = np.zeros(n, dtype=np.int64)
+        ties = cluster.router_lib().mm_merge_positions(keys.ctypes.data, counts.ctypes.data, world, r, pos.ctypes.data)
+        if tie:
+            assert ties == (1 if r < 2 else 0)  # ranks 0 and 1 hold the equal keys
+        else:
+            assert ties == 0
+            assert (pos == rank_of[r * n:(r + 1) * n]).all()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("config,n,groups,passes", [(3, 3000, 2, 2), (4, 2400, 0, 1), (5, 1200, 0, 2)])
 def test_cluster_gpu_pass_equals_single_oracle_pass(config, n, groups, passes):
