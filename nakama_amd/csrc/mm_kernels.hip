@@ -444,12 +444,17 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     // of a branch and a wait around every load.  The field columns' base
     // pointers are scalar loads issued ahead of the slot ids.
     constexpr int NFA = NF > 0 ? NF : 1;  // array extent (NF = 0: signature sets that read no field)
-    const uint8_t* __restrict__ fkp[NFA];
-    const int64_t* __restrict__ fvp[NFA];
+    // The column base pointers come from a pointer table: marked global so
+    // the loads are global_load (a flat load also counts in lgkmcnt, so every
+    // later LDS / scalar wait would wait for the columns too).
+    typedef const __attribute__((address_space(1))) uint8_t gu8;
+    typedef const __attribute__((address_space(1))) int64_t gi64;
+    gu8* fkp[NFA];
+    gi64* fvp[NFA];
 #pragma unroll
     for (int f = 0; f < NF; f++) {
-        fkp[f] = st.fkind[ms.field[f]];
-        fvp[f] = st.fval[ms.field[f]];
+        fkp[f] = (gu8*)st.fkind[ms.field[f]];
+        fvp[f] = (gi64*)st.fval[ms.field[f]];
     }
     uint32_t s[kMJ], sl[kMJ];
 #pragma unroll
@@ -457,6 +462,21 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
         const uint32_t i = (uint32_t)(j * kBlock + tid);
         sl[j] = src[i < len ? i : len - 1];
         s[j] = i < len ? sl[j] : kNoSlot;
+    }
+    // The signatures' filter fields into LDS, one thread per signature, while
+    // the column loads are in flight: the signature loop then reads LDS
+    // instead of a scalar load per field and a vector load per byte field
+    // (term_only, req_mask) with a full memory wait in every iteration.
+    __shared__ int64_t sq_req[kMaxMSig][NFA];
+    __shared__ int32_t sq_tmin[kMaxMSig], sq_tmax[kMaxMSig];
+    __shared__ uint32_t sq_flags[kMaxMSig];  // term_only | req_mask << 8
+    if ((uint32_t)tid < nq) {
+        const DMSig g = sigs[tid];
+#pragma unroll
+        for (int f = 0; f < NF; f++) sq_req[tid][f] = g.req[f];
+        sq_tmin[tid] = g.tmin;
+        sq_tmax[tid] = g.tmax;
+        sq_flags[tid] = (uint32_t)g.term_only | ((uint32_t)g.req_mask << 8);
     }
     uint8_t al[kMJ];
     int32_t mn[kMJ], mx[kMJ];
@@ -493,23 +513,49 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     for (int f = 0; f < NF; f++)
 #pragma unroll
         for (int j = 0; j < kMJ; j++) kw[f][j] = kk[f][j] == KIND_KEYWORD ? vv[f][j] : INT64_MIN;
+    __syncthreads();  // the signature fields are in LDS
     // phase 1: every signature on the lane's candidates -> bit q * kMJ + j
     uint64_t bits = 0;
-    for (uint32_t q = 0; q < nq; q++) {
-        const DMSig& g = sigs[q];
+    if constexpr (!GEN) {
+        // pool signatures only: equality on the required keyword fields.
+        // Unrolled over the signature capacity, so every signature's LDS
+        // fields are read up front and the bit positions are constants.
+#pragma unroll
+        for (int q = 0; q < kNSig; q++) {
+            if ((uint32_t)q >= nq) continue;
+            const uint32_t flags = sq_flags[q];
+            const int32_t tmin = sq_tmin[q], tmax = sq_tmax[q];
+            bool m[kMJ];
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) m[j] = a[j] & (mn[j] >= tmin) & (mx[j] <= tmax);
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                const int64_t want = sq_req[q][f];
+                const bool need = (flags >> (8 + f)) & 1u;
+#pragma unroll
+                for (int j = 0; j < kMJ; j++) m[j] = m[j] & (!need | (kw[f][j] == want));
+            }
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) bits |= (uint64_t)m[j] << (q * kMJ + j);
+        }
+    }
+    for (uint32_t q = 0; GEN && q < nq; q++) {
+        const uint32_t flags = sq_flags[q];
+        const int32_t tmin = sq_tmin[q], tmax = sq_tmax[q];
         bool m[kMJ];
 #pragma unroll
-        for (int j = 0; j < kMJ; j++) m[j] = a[j] && mn[j] >= g.tmin && mx[j] <= g.tmax;
-        if (!GEN || g.term_only) {
+        for (int j = 0; j < kMJ; j++) m[j] = a[j] && mn[j] >= tmin && mx[j] <= tmax;
+        if (!GEN || (flags & 0xffu)) {
             // a pool signature: equality on the required keyword fields
 #pragma unroll
             for (int f = 0; f < NF; f++) {
-                if (!((g.req_mask >> f) & 1u)) continue;
-                const int64_t want = g.req[f];
+                if (!((flags >> (8 + f)) & 1u)) continue;
+                const int64_t want = sq_req[q][f];
 #pragma unroll
                 for (int j = 0; j < kMJ; j++) m[j] = m[j] && kw[f][j] == want;
             }
         } else if constexpr (GEN) {
+            const DMSig& g = sigs[q];
             double msc[kMJ], ssc[kMJ];
             bool anys[kMJ];
 #pragma unroll
@@ -557,7 +603,9 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
         for (int j = 0; j < kMJ; j++) bits |= (uint64_t)m[j] << (q * kMJ + j);
     }
     // per (signature, j, wave): the ballot and its count
-    for (uint32_t q = 0; q < nq; q++) {
+#pragma unroll
+    for (int q = 0; q < kNSig; q++) {
+        if ((uint32_t)q >= nq) continue;
 #pragma unroll
         for (int j = 0; j < kMJ; j++) {
             const uint64_t mask = __ballot((int)((bits >> (q * kMJ + j)) & 1ull));
