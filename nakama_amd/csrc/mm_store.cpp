@@ -1390,7 +1390,16 @@ void Core::apply_selected_to_device(const uint32_t* slots, size_t n_slots) {
         apply_pending_ = false;
     }
     h_slots_tmp_.reserve(n_slots);
-    std::memcpy(h_slots_tmp_.p, slots, n_slots * sizeof(uint32_t));
+    if (n_slots >= (1u << 20) && par_mode_) {  // a whole pass's selection (C3: 7 MB) copies on the workers
+        WorkPool& wp = workers();
+        const size_t nch = wp.size();
+        wp.run(nch, [&](size_t c) {
+            const size_t lo = n_slots * c / nch, hi = n_slots * (c + 1) / nch;
+            std::memcpy(h_slots_tmp_.p + lo, slots + lo, (hi - lo) * sizeof(uint32_t));
+        });
+    } else {
+        std::memcpy(h_slots_tmp_.p, slots, n_slots * sizeof(uint32_t));
+    }
     d_slots_tmp_.reserve(n_slots, false);
     NKM_HIP(hipMemcpyAsync(d_slots_tmp_.p, h_slots_tmp_.p, n_slots * sizeof(uint32_t), hipMemcpyHostToDevice,
                            stream_));
