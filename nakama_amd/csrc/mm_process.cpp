@@ -2153,6 +2153,10 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
 // groups may overlap and then follow the reference's sequential order, where
 // a group meeting an already-retired ticket is dropped).
 void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, bool disjoint) {
+    using fclk = std::chrono::steady_clock;
+    const auto f0 = fclk::now();
+    auto f_ms = [](fclk::time_point a, fclk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fclk::time_point f1 = f0, f2 = f0;
     for (uint32_t s : expired) is_active_[s] = 0;
     const size_t ngr = groups.size();
     if (!disjoint || !par_mode_ || ngr < par_min(16384)) {
@@ -2189,6 +2193,7 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
             for (uint32_t g : order) kept.push(groups.begin(g), groups.end(g));
             groups = std::move(kept);
         }
+        f1 = fclk::now();
         // Retire the matched tickets.  When no session or party holds more
         // than one ticket, each slot's bookkeeping touches keys no other slot
         // does, so chunks of whole groups retire in parallel.
@@ -2216,10 +2221,14 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
         } else {
             for (auto& e : groups.ents) kill_slot(e.first, true);
         }
+        f2 = fclk::now();
     }
     filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, list_tmp_,
                  [&](uint32_t s) { return live_[s] && is_active_[s]; });
     active_list_.swap(list_tmp_);
+    if (batch_profile_)
+        std::fprintf(stderr, "[nkm]   finish: expired %zu, checks/order %.2f, retire %.2f, active filter %.2f ms\n",
+                     expired.size(), f_ms(f0, f1), f_ms(f1, f2), f_ms(f2 > f0 ? f2 : f0, fclk::now()));
 }
 
 void Core::finish_pass_serial(GroupList& groups, bool selected) {
