@@ -700,10 +700,14 @@ __global__ __launch_bounds__(kBlock) void cell_scan_kernel(const uint32_t* __res
 __global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restrict__ map,
                                                         const DGroupResult* __restrict__ cres,
                                                         const uint32_t* __restrict__ offs,
-                                                        const DHit* __restrict__ scratch, DHit* __restrict__ out) {
-    const uint32_t c = blockIdx.x;
+                                                        const DHit* __restrict__ scratch, DHit* __restrict__ out,
+                                                        uint32_t n_cells) {
+    // one wave per cell (C3: 16k cells of ~64 slot ids — a workgroup each
+    // spent more on dispatch than on the copy)
+    const uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (c >= n_cells) return;  // wave-uniform
     const DChunkMap mp = map[c];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x & 63;
     const uint32_t prefix = offs[c];
     const uint32_t n = cres[c].count;
     const uint64_t so = mp.so;
@@ -712,10 +716,10 @@ __global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restr
         uint32_t* __restrict__ o32 = reinterpret_cast<uint32_t*>(out);
         const uint32_t lim = mp.cap > prefix ? mp.cap - prefix : 0u;
         const uint32_t m = n < lim ? n : lim;
-        for (uint32_t e = tid; e < m; e += kBlock) o32[4 * mp.dst_off + prefix + e] = s32[so + e];
+        for (uint32_t e = tid; e < m; e += 64) o32[4 * mp.dst_off + prefix + e] = s32[so + e];
         return;
     }
-    for (uint32_t e = tid; e < n; e += kBlock) {
+    for (uint32_t e = tid; e < n; e += 64) {
         const uint32_t pos = prefix + e;
         if (pos >= mp.cap) break;
         DHit h = scratch[so + e];
@@ -1026,7 +1030,8 @@ hipError_t launch_stitch(const DChunkMap* d_map, int n_chunks, const DGroupResul
                          int n_searches, uint32_t* d_offs, const DHit* d_scratch, DHit* d_out, hipStream_t stream) {
     if (n_chunks <= 0) return hipSuccess;
     hipLaunchKernelGGL(cell_scan_kernel, dim3(n_searches), dim3(kBlock), 0, stream, d_ranges, d_cres, d_offs);
-    hipLaunchKernelGGL(stitch_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, d_map, d_cres, d_offs, d_scratch, d_out);
+    hipLaunchKernelGGL(stitch_kernel, dim3((n_chunks + kWaves - 1) / kWaves), dim3(kBlock), 0, stream, d_map, d_cres, d_offs,
+                       d_scratch, d_out, (uint32_t)n_chunks);
     return hipGetLastError();
 }
 
