@@ -681,16 +681,34 @@ __global__ __launch_bounds__(kBlock) void cell_scan_kernel(const uint32_t* __res
     const uint32_t per = (n + kBlock - 1) / kBlock;  // each thread: a contiguous run of cells
     const uint32_t lo = b + min(n, per * (uint32_t)tid), hi = b + min(n, per * (uint32_t)(tid + 1));
     uint32_t sum = 0;
-    for (uint32_t i = lo; i < hi; i++) sum += cres[i].count;
+    constexpr int kUnroll = 8;  // C3: 2048 cells per search -> 8 per thread, loaded in one round trip
+    const bool unrolled = per <= (uint32_t)kUnroll;
+    uint32_t v[kUnroll];
+    if (unrolled) {
+#pragma unroll
+        for (int k = 0; k < kUnroll; k++) v[k] = lo + k < hi ? cres[lo + k].count : 0u;
+#pragma unroll
+        for (int k = 0; k < kUnroll; k++) sum += v[k];
+    } else {
+        for (uint32_t i = lo; i < hi; i++) sum += cres[i].count;
+    }
     uint32_t incl = sum;  // inclusive scan of the threads' sums: within waves, then across them
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
+        const uint32_t u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
     }
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
     uint32_t run = incl - sum;
     for (int w = 0; w < wave; w++) run += wsum[w];
+    if (unrolled) {
+#pragma unroll
+        for (int k = 0; k < kUnroll; k++) {
+            if (lo + k < hi) offs[lo + k] = run;
+            run += v[k];
+        }
+        return;
+    }
     for (uint32_t i = lo; i < hi; i++) {
         offs[i] = run;
         run += cres[i].count;
