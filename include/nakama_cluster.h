@@ -83,6 +83,90 @@ int mm_shard_rows(void* h, int32_t world, int32_t rank, mm_allgather_fn fn, void
 int mm_rccl_unique_id(uint8_t* out, int32_t cap);
 int mm_shard_rows_rccl(void* h, int32_t world, int32_t rank, const uint8_t* uid, int32_t len);
 
+/* ---- One handle over several GPUs, in one process ---------------------
+ * The reference constructs ONE matchmaker per server process (main.go:160)
+ * behind server.Matchmaker (server/matchmaker.go:169-183).  mm_create_multi
+ * returns a handle that every entry point of nakama_mm.h accepts, exactly as
+ * a single-device handle, and that drives one sub-handle per listed device
+ * from host threads (no Python, no torch): a Go server gets a node's GPUs
+ * through one cgo Matchmaker.
+ *
+ * MM_MULTI_POOLS — pools kept whole.  Add/Insert route each ticket by its
+ *   pool key (mm_route_keys over pool_fields) to the sub-handle that owns the
+ *   pool (a new pool goes to the least-loaded sub-handle, largest first within
+ *   a batch); Process runs every sub-handle's pass concurrently and merges
+ *   the group lists into the reference's order by the searching ticket's
+ *   (CreatedAt, Ticket) — the group's last entry (matchmaker_process.go:
+ *   299-301, mm_matched.group_created).  With an override registered the
+ *   merged processCustom candidate list goes to the caller in the same order
+ *   and mm_process_commit re-checks the chosen groups in the reference's
+ *   post-pass order (matchmaker.go:326-343, swap-remove included) before
+ *   handing each sub-handle its part.  MaxTickets per session / party
+ *   (matchmaker.go:508-521) is checked against the tickets of all
+ *   sub-handles.  A ticket whose query does not pin every pool field to its
+ *   own property value is refused by Add with MM_ERR_UNSUPPORTED (Insert
+ *   inserts the others and returns MM_ERR_UNSUPPORTED); such workloads use
+ *   MM_MULTI_ROWS.
+ * MM_MULTI_ROWS — any query.  Every sub-handle holds every ticket (mutators
+ *   are replicated); each pass's batch searches are split into one block per
+ *   sub-handle and exchanged before the replicated ordered replay (the
+ *   row-sharded mode above): over RCCL between distinct devices
+ *   (transport MM_MULTI_RCCL, ncclCommInitRank per sub-handle thread), or
+ *   through host memory (MM_MULTI_HOST: sub-handles may share a device).
+ *
+ * api: the entry points of the library the sub-handles come from; NULL =
+ * this library (HIP sub-handles, cfg->device replaced by devices[i]).  The
+ * tests pass the CPU oracle's entry points (MM_MULTI_POOLS only).  Returns
+ * NULL on failure (mm_last_error(NULL) says why). */
+typedef struct mm_sub_api {
+    void* (*create)(const mm_config*);
+    void (*destroy)(void*);
+    void (*pause)(void*);
+    void (*resume)(void*);
+    void (*stop)(void*);
+    const char* (*last_error)(void*);
+    int (*add)(void*, const mm_ticket*);
+    int (*insert)(void*, const mm_ticket*, int32_t);
+    int (*extract)(void*, mm_extract_list*);
+    void (*free_extract)(void*, mm_extract_list*);
+    int (*remove_session)(void*, const char*, const char*);
+    int (*remove_session_all)(void*, const char*);
+    int (*remove_party)(void*, const char*, const char*);
+    int (*remove_party_all)(void*, const char*);
+    int (*remove_all)(void*, const char*);
+    int (*remove)(void*, const char* const*, int32_t);
+    int (*process)(void*, mm_matched*);
+    int (*process_commit)(void*, const int32_t*, const mm_entry_ref*, int32_t, mm_matched*);
+    void (*free_matched)(void*, mm_matched*);
+    int32_t (*ticket_count)(void*);
+    int32_t (*active_count)(void*);
+    int (*drain_removed)(void*, mm_str_list*);
+    void (*free_str_list)(void*, mm_str_list*);
+    int32_t (*debug_hits)(void*, const char*, const char**, double*, int32_t);
+    void (*debug_set_pass_hook)(void*, void (*)(void*), void*);
+} mm_sub_api;
+
+#define MM_MULTI_POOLS 0
+#define MM_MULTI_ROWS 1
+#define MM_MULTI_AUTO 0 /* transport: RCCL when the devices are distinct, else host */
+#define MM_MULTI_HOST 1
+#define MM_MULTI_RCCL 2
+
+typedef struct mm_multi_config {
+    const int32_t* devices;          /* one sub-handle per entry (HIP ordinals; repeats share a device) */
+    int32_t n_devices;
+    int32_t mode;                    /* MM_MULTI_POOLS / MM_MULTI_ROWS */
+    const char* const* pool_fields;  /* MM_MULTI_POOLS: query fields a pool is keyed on, e.g. "properties.region" */
+    int32_t n_pool_fields;
+    int32_t transport;               /* MM_MULTI_ROWS: MM_MULTI_AUTO / _HOST / _RCCL */
+    const mm_sub_api* api;           /* NULL: this library */
+} mm_multi_config;
+
+void* mm_create_multi(const mm_config* cfg, const mm_multi_config* mc);
+/* Number of sub-handles of a multi handle (0 for a single-device handle);
+ * with sub >= 0, that sub-handle's ticket count. */
+int32_t mm_multi_info(void* h, int32_t sub);
+
 #ifdef __cplusplus
 }
 #endif

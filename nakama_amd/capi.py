@@ -126,6 +126,37 @@ class mm_str_list(C.Structure):
 
 PASS_HOOK = C.CFUNCTYPE(None, C.c_void_p)
 
+# mm_sub_api (include/nakama_cluster.h): the entry points a multi handle
+# drives its sub-handles through, in declaration order -> exported symbol
+SUB_API = (("create", "mm_create"), ("destroy", "mm_destroy"), ("pause", "mm_pause"), ("resume", "mm_resume"),
+           ("stop", "mm_stop"), ("last_error", "mm_last_error"), ("add", "mm_add"), ("insert", "mm_insert"),
+           ("extract", "mm_extract"), ("free_extract", "mm_free_extract"), ("remove_session", "mm_remove_session"),
+           ("remove_session_all", "mm_remove_session_all"), ("remove_party", "mm_remove_party"),
+           ("remove_party_all", "mm_remove_party_all"), ("remove_all", "mm_remove_all"), ("remove", "mm_remove"),
+           ("process", "mm_process"), ("process_commit", "mm_process_commit"), ("free_matched", "mm_free_matched"),
+           ("ticket_count", "mm_ticket_count"), ("active_count", "mm_active_count"),
+           ("drain_removed", "mm_drain_removed"), ("free_str_list", "mm_free_str_list"),
+           ("debug_hits", "mm_debug_hits"), ("debug_set_pass_hook", "mm_debug_set_pass_hook"))
+
+
+class mm_sub_api(C.Structure):
+    _fields_ = [(f, C.c_void_p) for f, _ in SUB_API]
+
+
+def sub_api(lib: C.CDLL) -> mm_sub_api:
+    """The mm_sub_api table of a library exporting nakama_mm.h (e.g. the oracle)."""
+    return mm_sub_api(*[C.cast(getattr(lib, sym), C.c_void_p) for _, sym in SUB_API])
+
+
+MM_MULTI_POOLS, MM_MULTI_ROWS = 0, 1
+MM_MULTI_AUTO, MM_MULTI_HOST, MM_MULTI_RCCL = 0, 1, 2
+
+
+class mm_multi_config(C.Structure):
+    _fields_ = [("devices", C.POINTER(C.c_int32)), ("n_devices", C.c_int32), ("mode", C.c_int32),
+                ("pool_fields", C.POINTER(C.c_char_p)), ("n_pool_fields", C.c_int32), ("transport", C.c_int32),
+                ("api", C.POINTER(mm_sub_api))]
+
 
 EXPORTED_SYMBOLS = (
     "mm_create", "mm_destroy", "mm_pause", "mm_resume", "mm_stop", "mm_last_error", "mm_abi_version",
@@ -177,6 +208,9 @@ def load_library(path: str) -> C.CDLL:
                                                C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int64),
                                                C.c_int32]),
     }
+    if hasattr(lib, "mm_create_multi"):  # the product: one handle over several devices (nakama_cluster.h)
+        sig["mm_create_multi"] = (vp, [C.POINTER(mm_config), C.POINTER(mm_multi_config)])
+        sig["mm_multi_info"] = (C.c_int32, [vp, C.c_int32])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
@@ -261,14 +295,30 @@ class Matchmaker:
 
     def __init__(self, lib: C.CDLL, *, max_tickets: int = 3, interval_sec: int = 15, max_intervals: int = 2,
                  rev_precision: bool = False, rev_threshold: int = 1, override=None, device: int = 0,
-                 node: str = "node1"):
+                 node: str = "node1", multi: Optional[dict] = None):
+        """multi: one handle over several sub-handles (mm_create_multi,
+        include/nakama_cluster.h): dict(devices=[...], mode=MM_MULTI_POOLS |
+        MM_MULTI_ROWS, pool_fields=[...], transport=MM_MULTI_AUTO, sub_lib=None
+        (this library) or another library exporting nakama_mm.h)."""
         self.lib = lib
         self._node_b = _b(node)
         cfg = mm_config(max_tickets, interval_sec, max_intervals, int(bool(rev_precision)), rev_threshold,
                         int(override is not None), device, self._node_b)
-        self.h = lib.mm_create(C.byref(cfg))
+        if multi is None:
+            self.h = lib.mm_create(C.byref(cfg))
+        else:
+            devs = list(multi.get("devices", [device]))
+            fields = [f.encode() for f in multi.get("pool_fields", ())]
+            self._multi_keep = [(C.c_int32 * len(devs))(*devs), (C.c_char_p * max(1, len(fields)))(*fields)]
+            api = None
+            if multi.get("sub_lib") is not None:
+                self._multi_keep.append(sub_api(multi["sub_lib"]))
+                api = C.pointer(self._multi_keep[-1])
+            mc = mm_multi_config(self._multi_keep[0], len(devs), multi.get("mode", MM_MULTI_POOLS),
+                                 self._multi_keep[1], len(fields), multi.get("transport", MM_MULTI_AUTO), api)
+            self.h = lib.mm_create_multi(C.byref(cfg), C.byref(mc))
         if not self.h:
-            raise ErrDevice("mm_create failed")
+            raise ErrDevice((lib.mm_last_error(None) or b"mm_create failed").decode("utf-8", "replace"))
         self.override = override
         self._matched_fn = None
         self.node = node

@@ -74,7 +74,8 @@ def router_lib(path: str = PRODUCT_SO) -> C.CDLL:
 
 
 CLUSTER_SYMBOLS = ("mm_route_keys", "mm_pack_tickets", "mm_unpack_tickets", "mm_free_unpacked",
-                   "mm_merge_positions", "mm_shard_rows", "mm_rccl_unique_id", "mm_shard_rows_rccl")
+                   "mm_merge_positions", "mm_shard_rows", "mm_rccl_unique_id", "mm_shard_rows_rccl",
+                   "mm_create_multi", "mm_multi_info")
 
 
 def route_keys(tickets, n: int, pool_fields: Sequence[str]) -> np.ndarray:

@@ -9,6 +9,7 @@
 
 using nkm::Core;
 using nkm::DeviceError;
+using nkm::Handle;
 
 namespace {
 thread_local std::string g_create_error;
@@ -16,7 +17,7 @@ thread_local std::string g_create_error;
 template <class F>
 int guarded(void* h, F&& f) {
     if (!h) return MM_ERR_ARG;
-    Core* c = static_cast<Core*>(h);
+    Handle* c = static_cast<Handle*>(h);
     try {
         return f(*c);
     } catch (const DeviceError& e) {
@@ -39,6 +40,8 @@ int guarded(void* h, F&& f) {
 std::string S(const char* p) { return p ? std::string(p) : std::string(); }
 }  // namespace
 
+void nkm::set_create_error(const std::string& e) { g_create_error = e; }
+
 extern "C" {
 
 int mm_abi_version(void) { return MM_ABI_VERSION; }
@@ -47,7 +50,7 @@ const char* mm_backend_name(void) { return "hip-gfx950"; }
 void* mm_create(const mm_config* cfg) {
     if (!cfg) return nullptr;
     try {
-        return new Core(*cfg);
+        return static_cast<Handle*>(new Core(*cfg));
     } catch (const DeviceError& e) {
         g_create_error = std::string("mm_create: ") + hipGetErrorString(e.err);
         return nullptr;
@@ -61,90 +64,90 @@ void* mm_create(const mm_config* cfg) {
 }
 void mm_destroy(void* h) {
     try {
-        delete static_cast<Core*>(h);
+        delete static_cast<Handle*>(h);
     } catch (...) {
     }
 }
-void mm_pause(void* h) { if (h) static_cast<Core*>(h)->pause(); }
-void mm_resume(void* h) { if (h) static_cast<Core*>(h)->resume(); }
-void mm_stop(void* h) { if (h) static_cast<Core*>(h)->stop(); }
-const char* mm_last_error(void* h) { return h ? static_cast<Core*>(h)->last_error() : g_create_error.c_str(); }
+void mm_pause(void* h) { if (h) static_cast<Handle*>(h)->pause(); }
+void mm_resume(void* h) { if (h) static_cast<Handle*>(h)->resume(); }
+void mm_stop(void* h) { if (h) static_cast<Handle*>(h)->stop(); }
+const char* mm_last_error(void* h) { return h ? static_cast<Handle*>(h)->last_error() : g_create_error.c_str(); }
 
 int mm_add(void* h, const mm_ticket* t) {
     if (!t) return MM_ERR_ARG;
-    return guarded(h, [&](Core& c) { return c.add(*t); });
+    return guarded(h, [&](Handle& c) { return c.add(*t); });
 }
 int mm_insert(void* h, const mm_ticket* ts, int32_t n) {
     if (n > 0 && !ts) return MM_ERR_ARG;
-    return guarded(h, [&](Core& c) { return c.insert(ts, n); });
+    return guarded(h, [&](Handle& c) { return c.insert(ts, n); });
 }
 int mm_extract(void* h, mm_extract_list* out) {
     if (!out) return MM_ERR_ARG;
-    return guarded(h, [&](Core& c) { return c.extract(out); });
+    return guarded(h, [&](Handle& c) { return c.extract(out); });
 }
 void mm_free_extract(void* h, mm_extract_list* out) {
-    (void)guarded(h, [&](Core& c) { c.free_extract(out); return MM_OK; });
+    (void)guarded(h, [&](Handle& c) { c.free_extract(out); return MM_OK; });
 }
 int mm_remove_session(void* h, const char* session_id, const char* ticket) {
-    return guarded(h, [&](Core& c) { return c.remove_session(S(session_id), S(ticket)); });
+    return guarded(h, [&](Handle& c) { return c.remove_session(S(session_id), S(ticket)); });
 }
 int mm_remove_session_all(void* h, const char* session_id) {
-    return guarded(h, [&](Core& c) { return c.remove_session_all(S(session_id)); });
+    return guarded(h, [&](Handle& c) { return c.remove_session_all(S(session_id)); });
 }
 int mm_remove_party(void* h, const char* party_id, const char* ticket) {
-    return guarded(h, [&](Core& c) { return c.remove_party(S(party_id), S(ticket)); });
+    return guarded(h, [&](Handle& c) { return c.remove_party(S(party_id), S(ticket)); });
 }
 int mm_remove_party_all(void* h, const char* party_id) {
-    return guarded(h, [&](Core& c) { return c.remove_party_all(S(party_id)); });
+    return guarded(h, [&](Handle& c) { return c.remove_party_all(S(party_id)); });
 }
 int mm_remove_all(void* h, const char* node) {
-    return guarded(h, [&](Core& c) { return c.remove_all(S(node)); });
+    return guarded(h, [&](Handle& c) { return c.remove_all(S(node)); });
 }
 int mm_remove(void* h, const char* const* tickets, int32_t n) {
     if (n > 0 && !tickets) return MM_ERR_ARG;
-    return guarded(h, [&](Core& c) { return c.remove(tickets, n); });
+    return guarded(h, [&](Handle& c) { return c.remove(tickets, n); });
 }
 int mm_process(void* h, mm_matched* out) {
     if (!out) return MM_ERR_ARG;
-    return guarded(h, [&](Core& c) { return c.process(out); });
+    return guarded(h, [&](Handle& c) { return c.process(out); });
 }
 int mm_process_commit(void* h, const int32_t* group_offsets, const mm_entry_ref* entries, int32_t n_groups,
                       mm_matched* out) {
     if (!out || (n_groups > 0 && (!group_offsets || !entries))) return MM_ERR_ARG;
-    return guarded(h, [&](Core& c) { return c.process_commit(group_offsets, entries, n_groups, out); });
+    return guarded(h, [&](Handle& c) { return c.process_commit(group_offsets, entries, n_groups, out); });
 }
 void mm_free_matched(void* h, mm_matched* out) {
-    (void)guarded(h, [&](Core& c) { c.free_matched(out); return MM_OK; });
+    (void)guarded(h, [&](Handle& c) { c.free_matched(out); return MM_OK; });
 }
 int32_t mm_ticket_count(void* h) {
     int32_t n = -1;
-    (void)guarded(h, [&](Core& c) { n = c.ticket_count(); return MM_OK; });
+    (void)guarded(h, [&](Handle& c) { n = c.ticket_count(); return MM_OK; });
     return n;
 }
 int32_t mm_active_count(void* h) {
     int32_t n = -1;
-    (void)guarded(h, [&](Core& c) { n = c.active_count(); return MM_OK; });
+    (void)guarded(h, [&](Handle& c) { n = c.active_count(); return MM_OK; });
     return n;
 }
 int mm_drain_removed(void* h, mm_str_list* out) {
     if (!out) return MM_ERR_ARG;
-    return guarded(h, [&](Core& c) { return c.drain_removed(out); });
+    return guarded(h, [&](Handle& c) { return c.drain_removed(out); });
 }
 void mm_free_str_list(void* h, mm_str_list* out) {
-    (void)guarded(h, [&](Core& c) { c.free_str_list(out); return MM_OK; });
+    (void)guarded(h, [&](Handle& c) { c.free_str_list(out); return MM_OK; });
 }
 void mm_debug_set_pass_hook(void* h, void (*fn)(void*), void* ctx) {
-    (void)guarded(h, [&](Core& c) { c.set_pass_hook(fn, ctx); return MM_OK; });
+    (void)guarded(h, [&](Handle& c) { c.set_pass_hook(fn, ctx); return MM_OK; });
 }
 int mm_shard_rows(void* h, int32_t world, int32_t rank, mm_allgather_fn fn, void* ctx) {
-    return guarded(h, [&](Core& c) { return c.set_row_shard(world, rank, fn, ctx); });
+    return guarded(h, [&](Handle& c) { return c.set_row_shard(world, rank, fn, ctx); });
 }
 int mm_shard_rows_rccl(void* h, int32_t world, int32_t rank, const uint8_t* uid, int32_t len) {
-    return guarded(h, [&](Core& c) { return c.set_row_shard_rccl(world, rank, uid, len); });
+    return guarded(h, [&](Handle& c) { return c.set_row_shard_rccl(world, rank, uid, len); });
 }
 int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, double* scores_out, int32_t cap) {
     int32_t r = -1;
-    int rc = guarded(h, [&](Core& c) {
+    int rc = guarded(h, [&](Handle& c) {
         r = c.debug_hits(S(ticket), tickets_out, scores_out, cap);
         return MM_OK;
     });

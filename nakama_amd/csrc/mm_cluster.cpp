@@ -18,6 +18,7 @@
 
 #include "../../include/nakama_cluster.h"
 #include "gocompat.h"
+#include "mm_handle.h"
 #include "qcompile.h"
 
 namespace {
@@ -49,28 +50,6 @@ bool keyword_prop(const mm_ticket& t, const std::string& key, std::string* out) 
     return !nkm::bluge_datetime(*out, &ns);
 }
 
-uint64_t route_key(const mm_ticket& t, const std::vector<std::string>& fields) {
-    CompiledQuery cq;
-    if (nkm::compile_query(t.query ? t.query : "", &cq) != nkm::CQ_OK || cq.kind != nkm::QK_BOOL) return 0;
-    uint64_t h = 0xCBF29CE484222325ull;
-    for (const std::string& f : fields) {
-        static const std::string kProps = "properties.";
-        if (f.compare(0, kProps.size(), kProps) != 0) return 0;
-        std::string value;
-        if (!keyword_prop(t, f.substr(kProps.size()), &value)) return 0;
-        bool pinned = false;
-        for (const auto& c : cq.clauses) {
-            if (c.occur != nkm::OCC_MUST || c.field != f) continue;
-            if (c.op != nkm::OP_TERM && c.op != nkm::OP_NUMLIT) continue;
-            if (c.term != value) return 0;  // requires another pool's value
-            pinned = true;
-        }
-        if (!pinned) return 0;  // the search is not confined to one value of f
-        h = fnv1a(value, h);
-        h = fnv1a(std::string(1, '\0'), h);
-    }
-    return h | 1;  // 0 means "not partitionable"
-}
 
 // ---- wire format: per ticket a u32 record length, then fixed fields, then
 // NUL-terminated strings (so an unpacked ticket points into the buffer copy)
@@ -122,6 +101,38 @@ struct Reader {
 
 }  // namespace
 
+namespace nkm {
+
+uint64_t route_key(const mm_ticket& t, const std::vector<std::string>& fields) {
+    CompiledQuery cq;
+    if (nkm::compile_query(t.query ? t.query : "", &cq) != nkm::CQ_OK) return 0;
+    return route_key(t, fields, cq);
+}
+
+uint64_t route_key(const mm_ticket& t, const std::vector<std::string>& fields, const CompiledQuery& cq) {
+    if (cq.kind != nkm::QK_BOOL) return 0;
+    uint64_t h = 0xCBF29CE484222325ull;
+    for (const std::string& f : fields) {
+        static const std::string kProps = "properties.";
+        if (f.compare(0, kProps.size(), kProps) != 0) return 0;
+        std::string value;
+        if (!keyword_prop(t, f.substr(kProps.size()), &value)) return 0;
+        bool pinned = false;
+        for (const auto& c : cq.clauses) {
+            if (c.occur != nkm::OCC_MUST || c.field != f) continue;
+            if (c.op != nkm::OP_TERM && c.op != nkm::OP_NUMLIT) continue;
+            if (c.term != value) return 0;  // requires another pool's value
+            pinned = true;
+        }
+        if (!pinned) return 0;  // the search is not confined to one value of f
+        h = fnv1a(value, h);
+        h = fnv1a(std::string(1, '\0'), h);
+    }
+    return h | 1;  // 0 means "not partitionable"
+}
+
+}  // namespace nkm
+
 extern "C" {
 
 int32_t mm_route_keys(const mm_ticket* ts, int32_t n, const char* const* pool_fields, int32_t n_fields,
@@ -132,7 +143,7 @@ int32_t mm_route_keys(const mm_ticket* ts, int32_t n, const char* const* pool_fi
     int32_t ok = 0;
     for (int32_t i = 0; i < n; i++) {
         try {
-            keys_out[i] = route_key(ts[i], fields);
+            keys_out[i] = nkm::route_key(ts[i], fields);
         } catch (...) {
             keys_out[i] = 0;
         }

@@ -26,6 +26,7 @@
 #include "../../include/nakama_cluster.h"
 #include "../../include/nakama_mm.h"
 #include "mm_device.h"
+#include "mm_handle.h"
 #include "qcompile.h"
 #include "termmatch.h"
 #include "replay_core.h"
@@ -402,40 +403,46 @@ inline int64_t search_bytes(uint16_t n_fields, const DGroup& d, const DGroupResu
            (int64_t)(sizeof(DGroup) + sizeof(DGroupResult));
 }
 
-class Core {
+// Set by the multi-device front (mm_multi.cpp) around the creation of its
+// sub-handles: the number of Cores that share this process's host cores.
+extern thread_local unsigned g_create_share;
+
+class Core : public Handle {
 public:
     explicit Core(const mm_config& cfg);
-    ~Core();
+    ~Core() override;
 
-    int add(const mm_ticket& t);
-    int insert(const mm_ticket* ts, int32_t n);
-    int extract(mm_extract_list* out);
-    void free_extract(mm_extract_list* out);
-    int remove_session(const std::string& sid, const std::string& ticket);
-    int remove_session_all(const std::string& sid);
-    int remove_party(const std::string& pid, const std::string& ticket);
-    int remove_party_all(const std::string& pid);
-    int remove_all(const std::string& node);
-    int remove(const char* const* tickets, int32_t n);
-    int process(mm_matched* out);
-    int process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t n_groups, mm_matched* out);
-    void free_matched(mm_matched* out);
-    int32_t ticket_count();
-    int32_t active_count();
-    int32_t debug_hits(const std::string& ticket, const char** tk, double* sc, int32_t cap);
+    int add(const mm_ticket& t) override;
+    int insert(const mm_ticket* ts, int32_t n) override;
+    int extract(mm_extract_list* out) override;
+    void free_extract(mm_extract_list* out) override;
+    int remove_session(const std::string& sid, const std::string& ticket) override;
+    int remove_session_all(const std::string& sid) override;
+    int remove_party(const std::string& pid, const std::string& ticket) override;
+    int remove_party_all(const std::string& pid) override;
+    int remove_all(const std::string& node) override;
+    int remove(const char* const* tickets, int32_t n) override;
+    int process(mm_matched* out) override;
+    int process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t n_groups, mm_matched* out) override;
+    void free_matched(mm_matched* out) override;
+    int32_t ticket_count() override;
+    int32_t active_count() override;
+    int32_t debug_hits(const std::string& ticket, const char** tk, double* sc, int32_t cap) override;
 
-    void pause() { active_flag_ = false; }
-    void resume() { active_flag_ = true; }
-    void stop() { stopped_ = true; }
-    const char* last_error() const { return last_error_.c_str(); }
-    void set_error(const std::string& e) { last_error_ = e; }
-    void set_pass_hook(void (*fn)(void*), void* ctx) {
+    void pause() override { active_flag_ = false; }
+    void resume() override { active_flag_ = true; }
+    void stop() override { stopped_ = true; }
+    const char* last_error() const override { return last_error_.c_str(); }
+    void set_error(const std::string& e) override { last_error_ = e; }
+    void set_pass_hook(void (*fn)(void*), void* ctx) override {
         std::lock_guard<std::mutex> lk(mu_);
         pass_hook_ = fn;
         pass_hook_ctx_ = ctx;
     }
-    int drain_removed(mm_str_list* out);
-    void free_str_list(mm_str_list* out);
+    int drain_removed(mm_str_list* out) override;
+    void free_str_list(mm_str_list* out) override;
+    int set_row_shard(int world, int rank, mm_allgather_fn fn, void* ctx) override;
+    int set_row_shard_rccl(int world, int rank, const uint8_t* uid, int len) override;
 
 private:
     friend struct Replay;
@@ -586,6 +593,7 @@ private:
     hipEvent_t apply_ev_ = nullptr;  // after the last asynchronous alive-flag update (h_slots_tmp_ reuse)
     bool apply_pending_ = false;
     std::unique_ptr<WorkPool> workers_;  // created on the first large pass
+    unsigned host_share_ = 1;            // Cores sharing the host cores (multi handle)
     WorkPool& workers();
     size_t par_min(size_t auto_min) const { return par_mode_ == 2 ? 0 : auto_min; }
     bool big_list(const std::vector<uint32_t>& v) const { return par_mode_ != 0 && v.size() >= par_min(65536); }
@@ -745,8 +753,6 @@ public:
     void* nccl_comm_ = nullptr;           // device transport: an ncclComm_t (RCCL over xGMI)
     // a transport is set (also at world 1: the exchange path runs, trivially)
     bool row_shard() const { return shard_fn_ != nullptr || nccl_comm_ != nullptr; }
-    int set_row_shard(int world, int rank, mm_allgather_fn fn, void* ctx);
-    int set_row_shard_rccl(int world, int rank, const uint8_t* uid, int len);
     // In-place all-gather-v of the byte ranges [off[q], off[q+1]) of a buffer:
     // a device buffer over RCCL (enqueued on the stream), or a host buffer
     // through the caller's function.

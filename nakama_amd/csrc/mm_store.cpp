@@ -90,6 +90,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     node_ = cfg.node ? cfg.node : "";
     cfg_.node = nullptr;
     device_ = cfg.device;
+    host_share_ = g_create_share;
     int ndev = 0;
     NKM_HIP(hipGetDeviceCount(&ndev));
     if (ndev <= 0 || device_ < 0 || device_ >= ndev) throw DeviceError{hipErrorNoDevice, "device ordinal", __LINE__};
@@ -225,6 +226,7 @@ WorkPool& Core::workers() {
         if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = (unsigned)CPU_COUNT(&cs);
         // one process per GPU: the node's cores are shared by the local ranks
         if (const char* lw = std::getenv("LOCAL_WORLD_SIZE")) n /= std::max(1, std::atoi(lw));
+        n /= std::max(1u, host_share_);  // sub-handles of one multi handle (mm_multi.cpp) split them too
         n = std::max(1u, std::min(16u, n));
         if (const char* e = std::getenv("NKM_THREADS")) n = std::max(1, std::atoi(e));
         workers_.reset(new WorkPool(n, worker_cpus(n - 1)));

@@ -15,7 +15,7 @@ from . import capi
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "tools", "libmm_synth.so")
 T0 = (1_700_000_000_000_000_000 // 1024) * 1024
-SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005, 6: 0x5EED0006, 8: 0x5EED0008, 9: 0x5EED0009}
+SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005, 6: 0x5EED0006, 8: 0x5EED0008, 9: 0x5EED0009, 12: 0x5EED0006}
 _lib = None
 
 
@@ -45,7 +45,58 @@ def lib():
         _lib.synth_override_first_disjoint.restype = C.c_int32
         _lib.synth_override_first_disjoint.argtypes = [C.POINTER(C.c_int32), C.POINTER(capi.mm_entry_ref), C.c_int32,
                                                        C.POINTER(C.c_int32), C.POINTER(capi.mm_entry_ref)]
+        _lib.synth_sha_new.restype = C.c_void_p
+        _lib.synth_sha_new.argtypes = []
+        _lib.synth_sha_bytes.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+        _lib.synth_sha_groups.restype = C.c_int64
+        _lib.synth_sha_groups.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(capi.mm_entry_ref), C.c_int32]
+        _lib.synth_sha_extract.argtypes = [C.c_void_p, C.POINTER(capi.mm_ticket), C.c_int32]
+        _lib.synth_sha_final.argtypes = [C.c_void_p, C.c_char_p]
     return _lib
+
+
+class Digest:
+    """Streaming SHA-256 over the canonical text of group lists / post-pass
+    states (tools/synth.cpp): groups as "<ticket>:<presence index>," per entry
+    and "\\n" per group; a state as "<ticket>:<intervals>\\n" per remaining
+    ticket in ascending id order.  hashlib over the same bytes agrees."""
+
+    def __init__(self):
+        self.h = lib().synth_sha_new()
+
+    def groups_raw(self, out) -> int:
+        """Adds an mm_matched's groups (native: no Python per entry)."""
+        if out.n_groups == 0:
+            return 0
+        return lib().synth_sha_groups(self.h, out.group_offsets, out.entries, out.n_groups)
+
+    def groups(self, groups) -> None:
+        """Adds Python groups [[(ticket, pi), ...], ...]."""
+        self.raw(groups_text(groups))
+
+    def raw(self, b: bytes) -> None:
+        lib().synth_sha_bytes(self.h, b, len(b))
+
+    def extract_raw(self, mm: "capi.Matchmaker") -> int:
+        """Adds mm's post-pass state (mm_extract through the C ABI); returns
+        the remaining ticket count."""
+        out = capi.mm_extract_list()
+        mm._check(mm.lib.mm_extract(mm.h, C.byref(out)))
+        try:
+            lib().synth_sha_extract(self.h, out.tickets, out.n)
+            return out.n
+        finally:
+            mm.lib.mm_free_extract(mm.h, C.byref(out))
+
+    def hexdigest(self) -> str:
+        buf = C.create_string_buffer(32)
+        lib().synth_sha_final(self.h, buf)
+        self.h = None
+        return buf.raw.hex()
+
+
+def groups_text(groups) -> bytes:
+    return b"".join(b"".join(t.encode() + b":%d," % pi for t, pi in g) + b"\n" for g in groups)
 
 
 N_POOLS = {3: 8, 4: 64}

@@ -103,6 +103,34 @@ def term_match(lib, kind, pattern, fuzziness, term):
     return [rc, b.value if rc == 1 else 0]
 
 
+CUSTOM_POOLS = {"a": 64, "b": 65, "c": 63, "d": 5}  # filtered hits per row: 63, 64, 62, 4
+
+
+def custom_pool_candidates(lib, pools=CUSTOM_POOLS):
+    """processCustom over interleaved pools of solo tickets, query
+    "+properties.k:<own pool>", Min=2 Max=3: a row of a pool of n tickets has
+    n-1 filtered hits.  combineIndexes loops `combinationBits < (1 << length)`
+    over Go ints (server/matchmaker_process.go:588), so a row with 63 hits
+    (1 << 63 is negative) or 64 (1 << 64 is 0) yields no candidate, while a
+    row with 62 yields every 2-subset (1-subsets reach hitCount 2 < MaxCount
+    with Intervals <= MaxIntervals and are rejected, :496).  Returns (the
+    candidate list the override received, ticket -> pool)."""
+    order = [(p, k) for p, n in pools.items() for k in range(n)]
+    order.sort(key=lambda pk: ((pk[1] * 7919 + ord(pk[0]) * 104729) % 1009, pk[0], pk[1]))  # interleave the pools
+    seen, pool_of = [], {}
+    mm = capi.Matchmaker(lib, override=lambda c: (seen.append([list(g) for g in c]), [])[1], max_intervals=5)
+    try:
+        for i, (p, k) in enumerate(order):
+            t = f"t-{p}-{k:03d}"
+            pool_of[t] = p
+            mm.Add([capi.Presence(f"u{i}", f"s{i}", f"u{i}", "n")], f"s{i}", "", f"+properties.k:{p}", 2, 3, 1,
+                   {"k": p}, {}, ticket=t, created_at=1_700_000_000_000_000_000 + 1024 * i)
+        mm.Process()
+    finally:
+        mm.close()
+    return (seen[0] if seen else []), pool_of
+
+
 def matched_sessions(groups, sc):
     """Session ids of matched entries (the test's matchesSeen keys)."""
     sess = {}

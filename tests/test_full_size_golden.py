@@ -1,0 +1,94 @@
+"""The product's full-size passes against the oracle's (needs a gfx950 GPU).
+
+tests/golden/full_<name>.json holds, for one Process() over the bench-sized
+synthetic set of a BASELINE config (C2 100k, C3 1M, C4 4M, C5 1M with
+RevPrecision, C5 1M + MatchmakerOverride), the SHA-256 of the oracle's ordered
+groups (and processCustom candidate list) and of its post-pass state,
+produced offline by tools/make_full_golden.py (per-pool / per-bucket-chunk
+oracle runs recombined exactly; see its docstring).  Here the HIP library runs
+the same pass on the whole set through the C ABI — crossing every size
+threshold the small parity tests do not reach (batch and hit budgets, mscan's
+thousands of chunks, the pipelined merge over 125k-row pools) — and its
+digests must be equal: bit-exact groups, entry order, group order, candidate
+order, and the remaining tickets' intervals.
+"""
+import ctypes as C
+import json
+import os
+
+import pytest
+
+import harness
+from nakama_amd import capi, synth
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ["c2", "c3", "c4", "c5", "c5o"]
+
+
+def _golden(name):
+    path = os.path.join(harness.GOLDEN, f"full_{name}.json")
+    if not os.path.exists(path):
+        pytest.skip(f"{path} not generated (tools/make_full_golden.py {name})")
+    with open(path) as f:
+        return json.load(f)
+
+
+def _product_pass(g):
+    import nakama_amd
+    lib = nakama_amd.load_library()
+    kw = dict(g["matchmaker"])
+    ts = synth.TicketSet(g["config"], g["tickets"])
+    mm = capi.Matchmaker(lib, override=(lambda c: c) if g["override"] else None, **kw)
+    got = {}
+    try:
+        ts.insert_into(mm)
+        out = mm.process_call()
+        if g["override"]:
+            assert out.is_candidates
+            cd = synth.Digest()
+            got["candidates"] = out.n_groups
+            got["candidate_entries"] = cd.groups_raw(out)
+            got["candidates_sha256"] = cd.hexdigest()
+            out = synth.override_commit(mm, out)
+        try:
+            gd = synth.Digest()
+            got["groups"] = out.n_groups
+            got["entries"] = gd.groups_raw(out)
+            got["groups_sha256"] = gd.hexdigest()
+            got["matched_tickets"] = mm.summary_counts(out)[1]
+            got["eval_kernel"] = out.eval_kernel
+        finally:
+            lib.mm_free_matched(mm.h, C.byref(out))
+        sd = synth.Digest()
+        got["remaining"] = sd.extract_raw(mm)
+        got["state_sha256"] = sd.hexdigest()
+        got["active"] = mm.active_count()
+        return got
+    finally:
+        mm.close()
+        ts.close()
+
+
+def _check(name):
+    g = _golden(name)
+    got = _product_pass(g)
+    keys = ["groups", "entries", "matched_tickets", "remaining", "active", "groups_sha256", "state_sha256"]
+    if g["override"]:
+        keys += ["candidates", "candidate_entries", "candidates_sha256"]
+    assert {k: got[k] for k in keys} == {k: g[k] for k in keys}, name
+    return got
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_full_size_pass_equals_oracle(name):
+    _check(name)
+
+
+@pytest.mark.parametrize("env", [{"NKM_PIPE": "0"}, {"NKM_FAST": "0"}, {"NKM_DENSE": "0"}, {"NKM_KERNEL": "scan"}],
+                         ids=["nopipe", "exact-walk", "generic-walk", "scan-kernel"])
+def test_full_size_c3_host_paths(env, monkeypatch):
+    """C3 at 1M through the other host replay paths and the chunked scan."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    _check("c3")

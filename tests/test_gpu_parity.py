@@ -608,6 +608,21 @@ def _custom_many_hits(lib, n_tickets):
 
 
 @pytest.mark.parametrize("devenum", ["1", "0"])
+def test_custom_zero_candidates_at_63_hits(devenum, monkeypatch):
+    """Rows with 63 / 64 filtered hits hand over no candidate (Go's `1 <<
+    length` overflow, matchmaker_process.go:588) while rows of 62 and 4 hits
+    in the same pass hand over theirs; the device (enum_kernel) and host
+    enumerations both equal the oracle's list."""
+    from math import comb
+    monkeypatch.setenv("NKM_DEVENUM", devenum)
+    got, pool_of = harness.custom_pool_candidates(product_lib())
+    want, _ = harness.custom_pool_candidates(harness.oracle_lib())
+    assert len(got) == 63 * comb(62, 2) + 5 * comb(4, 2)
+    assert not any(pool_of[g[-1][0]] in ("a", "b") for g in got)
+    assert got == want
+
+
+@pytest.mark.parametrize("devenum", ["1", "0"])
 def test_custom_rows_past_40_hits(devenum, monkeypatch):
     monkeypatch.setenv("NKM_DEVENUM", devenum)
     n = 51

@@ -116,6 +116,26 @@ def test_oracle_rev_threshold_fired_equals_no_rev():
     assert outs[2] != outs[1]  # the reverse checks do change config 6's groups
 
 
+def test_oracle_custom_zero_candidates_at_63_hits():
+    """combineIndexes' int shift (matchmaker_process.go:588): rows with 63 or
+    64 filtered hits hand over no candidate; rows with 62 and 4 hits in the
+    same pass hand over every 2-subset, in row order then ascending mask."""
+    from math import comb
+    cands, pool_of = harness.custom_pool_candidates(harness.oracle_lib())
+    roots = {}
+    for g in cands:
+        roots.setdefault(g[-1][0], []).append(g)
+    by_pool = {}
+    for t, gs in roots.items():
+        by_pool.setdefault(pool_of[t], []).append(len(gs))
+    assert "a" not in by_pool and "b" not in by_pool  # 63 / 64 hits: zero candidates
+    assert sorted(by_pool["c"]) == [comb(62, 2)] * 63
+    assert sorted(by_pool["d"]) == [comb(4, 2)] * 5
+    assert len(cands) == 63 * comb(62, 2) + 5 * comb(4, 2)
+    # every candidate stays inside its root's pool
+    assert all(len({pool_of[t] for t, _ in g}) == 1 for g in cands)
+
+
 def test_oracle_custom_enumeration_past_40_hits():
     """combineIndexes over 50 hits: the ascending mask loop visits only masks
     with <= max bits (the others `continue`), so it finishes; every 2-subset."""

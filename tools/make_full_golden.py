@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Full-size oracle digests of the BASELINE configs' passes (test fixtures).
+
+Writes tests/golden/full_<name>.json: the SHA-256 of the ordered matched
+groups (tickets, presence indexes, entry and group order), of the post-pass
+state ((ticket, intervals) of every remaining ticket) and the counts, for one
+Process() over a fresh synthetic set at the size bench.py and BASELINE.json
+quote — produced by the CPU oracle (oracle/liboracle_mm.so, the restatement of
+server/matchmaker_process.go:27-334 / :336-612), so that
+tests/test_full_size_golden.py can hold the HIP product's full-size pass to
+it on the GPU.  Text formats: nakama_amd/synth.py Digest.
+
+The oracle scans every document per search (O(N^2) per pass), so a 1M pass
+is split into independent sub-passes and the results recombined exactly:
+  * pool configs (C2's 4 region pools, C3's 8 mode x region pools, C4's 64):
+    every query requires its own ticket's pool values (synth.cpp), so no
+    search ever finds a ticket of another pool and processDefault's greedy
+    walk is the interleaving of per-pool walks (the property the cluster
+    tests check, tests/test_cluster.py).  Each pool runs in its own process;
+    the group lists are merged by their searching ticket — a group's last
+    entry (matchmaker_process.go:299-301) — in the pinned (CreatedAt, Ticket)
+    order;
+  * C5 (buckets of 8 consecutive tickets): chunks of 1000 consecutive
+    tickets (125 whole buckets) run in index order, which is also CreatedAt
+    order, so the chunks' lists concatenate.  With --override the chunk's
+    processCustom candidate list is digested too, and the native
+    first-disjoint override (tools/synth.cpp) picks the groups per chunk —
+    candidates of different buckets never share a ticket, so the choice
+    equals the whole list's.
+
+Usage: python tools/make_full_golden.py c3 [c2 c4 c5 c5o] [--jobs 8]
+Runs in this container (CPU only); C3 ~12 min on 8 cores, C4 ~1 h.
+"""
+import argparse
+import ctypes as C
+import hashlib
+import heapq
+import json
+import os
+import sys
+import time
+from concurrent.futures import ProcessPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from nakama_amd import capi, synth  # noqa: E402
+
+ORACLE = os.path.join(ROOT, "oracle", "liboracle_mm.so")
+OUT = os.path.join(ROOT, "tests", "golden")
+
+# name -> (config, tickets, pools or None, Matchmaker kwargs, override)
+SPECS = {
+    "c2": (2, 100_000, 4, dict(max_intervals=2), False),
+    "c3": (3, 1_000_000, 8, dict(max_intervals=2), False),
+    "c4": (4, 4_000_000, 64, dict(max_intervals=2), False),
+    "c5": (5, 1_000_000, None, dict(max_intervals=2, rev_precision=True, rev_threshold=0), False),
+    "c5o": (5, 1_000_000, None, dict(max_intervals=2, rev_precision=True, rev_threshold=0), True),
+}
+C5_CHUNK = 1000
+
+
+def _state_lines(mm):
+    return [(t.ticket, t.intervals) for t in mm.Extract()]
+
+
+def pool_part(args):
+    """One pool's pass: its groups with their searching-ticket keys, its
+    remaining (ticket, intervals) and active count."""
+    config, n, pool, kw = args
+    lib = capi.load_library(ORACLE)
+    ts = synth.TicketSet(config, n, pool_mask=1 << pool)
+    created = {ts.ticket_id(k): ts.tickets[k].created_at for k in range(ts.n)}
+    mm = capi.Matchmaker(lib, **kw)
+    try:
+        ts.insert_into(mm)
+        t0 = time.time()
+        r = mm.process_raw()
+        dt = time.time() - t0
+        keyed = [((created[g[-1][0]], g[-1][0]), g) for g in r.groups]
+        return pool, ts.n, keyed, _state_lines(mm), mm.active_count(), dt
+    finally:
+        mm.close()
+        ts.close()
+
+
+def run_pools(name, jobs):
+    config, n, pools, kw, _ = SPECS[name]
+    t0 = time.time()
+    with ProcessPoolExecutor(max_workers=jobs) as ex:
+        parts = list(ex.map(pool_part, [(config, n, p, kw) for p in range(pools)]))
+    total = sum(p[1] for p in parts)
+    assert total == n, (total, n)
+    merged = list(heapq.merge(*[p[2] for p in parts], key=lambda kg: kg[0]))
+    groups = [g for _, g in merged]
+    state = sorted(x for p in parts for x in p[3])
+    active = sum(p[4] for p in parts)
+    gh = hashlib.sha256(synth.groups_text(groups)).hexdigest()
+    sh = hashlib.sha256(b"".join(t.encode() + b":%d\n" % iv for t, iv in state)).hexdigest()
+    return {
+        "groups": len(groups), "entries": sum(len(g) for g in groups),
+        "matched_tickets": sum(len({t for t, _ in g}) for g in groups),
+        "groups_sha256": gh, "remaining": len(state), "active": active, "state_sha256": sh,
+        "split": f"{pools} pools, one oracle process each, groups merged by searching ticket (CreatedAt, Ticket)",
+        "oracle_pool_pass_s": [round(p[5], 1) for p in sorted(parts)], "wall_s": round(time.time() - t0, 1),
+    }
+
+
+def run_c5(name):
+    config, n, _, kw, override = SPECS[name]
+    lib = capi.load_library(ORACLE)
+    t0 = time.time()
+    gd, cd = synth.Digest(), synth.Digest()
+    n_groups = n_entries = n_cands = n_cand_entries = matched = active = 0
+    state = []
+    for first in range(0, n, C5_CHUNK):
+        ts = synth.TicketSet(config, min(C5_CHUNK, n - first), first=first)
+        mm = capi.Matchmaker(lib, override=(lambda c: c) if override else None, **kw)
+        try:
+            ts.insert_into(mm)
+            out = mm.process_call()
+            if override:
+                assert out.is_candidates
+                n_cands += out.n_groups
+                n_cand_entries += cd.groups_raw(out)
+                out = synth.override_commit(mm, out)  # frees the candidates
+            try:
+                n_groups += out.n_groups
+                n_entries += gd.groups_raw(out)
+                _, tk, _, _ = mm.summary_counts(out)
+                matched += tk
+            finally:
+                mm.lib.mm_free_matched(mm.h, C.byref(out))
+            state += _state_lines(mm)
+            active += mm.active_count()
+        finally:
+            mm.close()
+            ts.close()
+    state.sort()
+    sh = hashlib.sha256(b"".join(t.encode() + b":%d\n" % iv for t, iv in state)).hexdigest()
+    res = {"groups": n_groups, "entries": n_entries, "matched_tickets": matched, "groups_sha256": gd.hexdigest(),
+           "remaining": len(state), "active": active, "state_sha256": sh,
+           "split": f"chunks of {C5_CHUNK} consecutive tickets (whole buckets of 8) in index order, concatenated",
+           "wall_s": round(time.time() - t0, 1)}
+    if override:
+        res["candidates"] = n_cands
+        res["candidate_entries"] = n_cand_entries
+        res["candidates_sha256"] = cd.hexdigest()
+        res["override"] = "first-disjoint (tools/synth.cpp synth_override_first_disjoint)"
+    else:
+        cd.hexdigest()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("names", nargs="+", choices=sorted(SPECS))
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    a = ap.parse_args()
+    for name in a.names:
+        config, n, pools, kw, override = SPECS[name]
+        res = run_pools(name, a.jobs) if pools else run_c5(name)
+        doc = {"name": name, "config": config, "tickets": n, "passes": 1, "matchmaker": kw, "override": override,
+               "seed": synth.SEEDS[config], "T0": synth.T0,
+               "generator": "tools/make_full_golden.py over oracle/liboracle_mm.so", **res}
+        path = os.path.join(OUT, f"full_{name}.json")
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1)
+            f.write("\n")
+        print(json.dumps(doc), flush=True)
+
+
+if __name__ == "__main__":
+    main()

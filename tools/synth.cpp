@@ -67,10 +67,12 @@ const char* kRegions[8] = {"eu", "na", "sa", "ap", "me", "af", "oc", "cn"};
 extern "C" {
 
 // Pool (mode x region partition) of ticket i for the pool-partitioned configs
-// (3: 2x4 = 8 pools, 4: 8x8 = 64 pools); -1 for the others.  Uses the same
-// draws as synth_make, so it agrees with the generated properties.
+// (2: its 4 region pools, 3: 2x4 = 8 pools, 4: 8x8 = 64 pools); -1 for the
+// others.  Uses the same draws as synth_make, so it agrees with the generated
+// properties.
 int synth_pool_of(int config, uint64_t seed, uint64_t i) {
     Rng r{splitmix64(seed ^ (i * 0x9E3779B97F4A7C15ull))};
+    if (config == 2) return (int)(r.next() & 3);
     if (config == 3) {
         (void)r.uni();
         const int mode = (int)(r.next() & 1), region = (int)(r.next() & 3);
@@ -353,7 +355,9 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             else if (v == 1) std::snprintf(q, sizeof q, "+properties.mode:%s properties.skill:>=%d^2", mode, s);
             else if (v == 2) std::snprintf(q, sizeof q, "properties.skill:<=%d properties.mode:%s^3", s + 10, mode);
             else std::snprintf(q, sizeof q, "+properties.skill:>=%d -properties.mode:nope", s - 20);
-            query = q;
+            // 12: the same workload with every query pinned to its own mode
+            // (pools by mode: the multi-GPU fronts' Min<Max / CountMultiple case)
+            query = config == 12 ? std::string("+properties.mode:") + mode + " " + q : std::string(q);
             const int shape = (int)(r.next() % 3);
             if (shape == 0) { t.min_count = 2; t.max_count = 2; }
             else if (shape == 1) { t.min_count = 2; t.max_count = 4; }
@@ -495,6 +499,104 @@ int32_t synth_override_first_disjoint(const int32_t* offs, const mm_entry_ref* e
         out_offs[++kept] = e;
     }
     return kept;
+}
+
+// ---- digests of pass results (tests/golden/full_*.json, tools/make_full_golden.py) ----
+// SHA-256 (FIPS 180-4) over a canonical text of a group list or a post-pass
+// state, streamed so that 100M-entry candidate lists need no buffer:
+//   groups: per group, per entry "<ticket>:<presence index>," then "\n";
+//   state:  per remaining ticket in ascending id order "<ticket>:<intervals>\n".
+// Python's hashlib over the same bytes gives the same digest
+// (tools/make_full_golden.py merges pool lists in Python that way).
+struct Sha256 {
+    uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                     0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    uint8_t buf[64];
+    size_t nbuf = 0;
+    uint64_t total = 0;
+    static uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+    void block(const uint8_t* p) {
+        static const uint32_t K[64] = {
+            0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+            0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+            0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+            0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+            0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+            0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+            0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+            0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+        uint32_t w[64];
+        for (int i = 0; i < 16; i++)
+            w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+        for (int i = 16; i < 64; i++) {
+            const uint32_t s0 = rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3);
+            const uint32_t s1 = rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10);
+            w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+        }
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+        for (int i = 0; i < 64; i++) {
+            const uint32_t t1 = hh + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) + K[i] + w[i];
+            const uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+            hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+    }
+    void update(const void* data, size_t n) {
+        const uint8_t* p = static_cast<const uint8_t*>(data);
+        total += n;
+        while (n) {
+            const size_t k = std::min(n, 64 - nbuf);
+            std::memcpy(buf + nbuf, p, k);
+            nbuf += k; p += k; n -= k;
+            if (nbuf == 64) { block(buf); nbuf = 0; }
+        }
+    }
+    void final(uint8_t out[32]) {
+        const uint64_t bits = total * 8;
+        const uint8_t one = 0x80, zero = 0;
+        update(&one, 1);
+        while (nbuf != 56) update(&zero, 1);
+        uint8_t len[8];
+        for (int i = 0; i < 8; i++) len[i] = (uint8_t)(bits >> (56 - 8 * i));
+        update(len, 8);
+        for (int i = 0; i < 8; i++)
+            for (int k = 0; k < 4; k++) out[4 * i + k] = (uint8_t)(h[i] >> (24 - 8 * k));
+    }
+};
+
+void* synth_sha_new() { return new Sha256(); }
+void synth_sha_bytes(void* s, const uint8_t* p, int64_t n) { static_cast<Sha256*>(s)->update(p, (size_t)n); }
+// Appends groups [0, n_groups) of a CSR group list; returns the entry count.
+int64_t synth_sha_groups(void* s, const int32_t* offs, const mm_entry_ref* ents, int32_t n_groups) {
+    Sha256& h = *static_cast<Sha256*>(s);
+    char num[16];
+    for (int32_t g = 0; g < n_groups; g++) {
+        for (int32_t k = offs[g]; k < offs[g + 1]; k++) {
+            h.update(ents[k].ticket, std::strlen(ents[k].ticket));
+            const int m = std::snprintf(num, sizeof num, ":%d,", ents[k].presence_index);
+            h.update(num, (size_t)m);
+        }
+        h.update("\n", 1);
+    }
+    return n_groups ? offs[n_groups] - offs[0] : 0;
+}
+// Appends a post-pass state: the extract list's (ticket, intervals) in
+// ascending ticket order.
+void synth_sha_extract(void* s, const mm_ticket* ts, int32_t n) {
+    Sha256& h = *static_cast<Sha256*>(s);
+    std::vector<int32_t> ord((size_t)n);
+    for (int32_t i = 0; i < n; i++) ord[(size_t)i] = i;
+    std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return std::strcmp(ts[a].ticket, ts[b].ticket) < 0; });
+    char num[24];
+    for (int32_t i : ord) {
+        h.update(ts[i].ticket, std::strlen(ts[i].ticket));
+        const int m = std::snprintf(num, sizeof num, ":%d\n", ts[i].intervals);
+        h.update(num, (size_t)m);
+    }
+}
+void synth_sha_final(void* s, uint8_t* out32) {
+    static_cast<Sha256*>(s)->final(out32);
+    delete static_cast<Sha256*>(s);
 }
 
 }  // extern "C"
