@@ -146,7 +146,7 @@ def run_c5(name):
         res["candidates"] = n_cands
         res["candidate_entries"] = n_cand_entries
         res["candidates_sha256"] = cd.hexdigest()
-        res["override"] = "first-disjoint (tools/synth.cpp synth_override_first_disjoint)"
+        res["override_fn"] = "first-disjoint (tools/synth.cpp synth_override_first_disjoint)"
     else:
         cd.hexdigest()
     return res
