@@ -126,8 +126,6 @@ struct Sig {
     std::vector<std::pair<uint16_t, uint32_t>> must_terms;  // candidate posting lists
 };
 
-// key id -> set of slots, optimised for the common one-slot case
-// (sessionTickets / partyTickets, matchmaker.go:201-204).
 // Persistent host workers for the pass's data-parallel host phases (pool
 // replay, post-pass bookkeeping): run(n, fn) calls fn(0..n-1) over the
 // workers and the caller, and returns when all n tasks are done.
@@ -216,23 +214,27 @@ private:
     bool quit_ = false;
 };
 
-// The fields the greedy replay reads for every hit it walks, packed in one
-// 32-B record per slot so that a hit costs one cache line instead of one per
-// column.  Immutable while the slot lives (rebuilt at compaction).
-
+// key id -> set of slots, optimised for the common one-slot case
+// (sessionTickets / partyTickets, matchmaker.go:201-204).  `first` may hold a
+// dead slot (a ticket a pass retired without touching this map: slots are
+// never reused before compaction rebuilds it), which counts as absent; `more`
+// holds live slots only (erase keeps it exact).
 struct SlotSets {
     std::vector<uint32_t> first;
     std::unordered_map<uint32_t, std::vector<uint32_t>> more;
+    const std::vector<uint8_t>* live = nullptr;  // the store's live_ (set by Core)
+    bool alive(uint32_t s) const { return s != kNoSlot && (*live)[s]; }
     void ensure(uint32_t key) { if (key >= first.size()) first.resize(key + 1, kNoSlot); }
     size_t count(uint32_t key) const {
-        if (key >= first.size() || first[key] == kNoSlot) return 0;
-        if (more.empty()) return 1;
+        if (key >= first.size()) return 0;
+        const size_t n = alive(first[key]) ? 1 : 0;
+        if (more.empty()) return n;
         auto it = more.find(key);
-        return 1 + (it == more.end() ? 0 : it->second.size());
+        return n + (it == more.end() ? 0 : it->second.size());
     }
     void add(uint32_t key, uint32_t slot) {
         ensure(key);
-        if (first[key] == kNoSlot) { first[key] = slot; return; }
+        if (!alive(first[key])) { first[key] = slot; return; }
         more[key].push_back(slot);
     }
     void erase(uint32_t key, uint32_t slot) {
@@ -242,10 +244,18 @@ struct SlotSets {
             return;
         }
         auto it = more.find(key);
-        if (first[key] == slot) {
-            if (it == more.end()) { first[key] = kNoSlot; return; }
-            first[key] = it->second.back();
-            it->second.pop_back();
+        if (first[key] == slot || !alive(first[key])) {
+            if (first[key] != slot && it != more.end()) {  // a stale first: the slot may sit in more
+                auto& v = it->second;
+                for (size_t i = 0; i < v.size(); i++)
+                    if (v[i] == slot) { v[i] = v.back(); v.pop_back(); break; }
+            }
+            if (it == more.end() || it->second.empty()) {
+                first[key] = kNoSlot;
+            } else {
+                first[key] = it->second.back();
+                it->second.pop_back();
+            }
         } else if (it != more.end()) {
             auto& v = it->second;
             for (size_t i = 0; i < v.size(); i++)
@@ -257,8 +267,8 @@ struct SlotSets {
     }
     std::vector<uint32_t> list(uint32_t key) const {
         std::vector<uint32_t> v;
-        if (key >= first.size() || first[key] == kNoSlot) return v;
-        v.push_back(first[key]);
+        if (key >= first.size()) return v;
+        if (alive(first[key])) v.push_back(first[key]);
         auto it = more.find(key);
         if (it != more.end()) v.insert(v.end(), it->second.begin(), it->second.end());
         return v;
@@ -387,6 +397,11 @@ struct PassStats {
     int parallel_batches = 0;
     double par_bucket_ms = 0, par_work_ms = 0, par_merge_ms = 0;  // parallel replay phases
     double par_task_max_ms = 0;
+    // finer split (NKM_PROFILE): run_batch's host prep + launches, the
+    // overlapped host work, the wait for the device, result accounting and
+    // wiring, the hit-list copies; replay_parallel's gathers and the walk job
+    double rb_prep_ms = 0, rb_overlap_ms = 0, rb_wait_ms = 0, rb_post_ms = 0, rb_lists_ms = 0;
+    double par_gather_ms = 0, par_job_ms = 0, par_clear_ms = 0;
     uint64_t par_rows = 0, par_hits = 0;
 };
 
@@ -579,6 +594,13 @@ private:
                          bool rev, uint32_t* min_stop);
     std::vector<uint8_t> dec_;  // per pass: rows a parallel replay decided ahead of the pass's row pointer
     void apply_selected_to_device(const uint32_t* slots, size_t n);
+    // A batch's selections reach the device alive mask before the next
+    // device search (the next batch, a page, a pair check, the next pass's
+    // sync_device): deferred here, flushed by flush_apply (a compaction
+    // renumbers the slots and drops them: its re-upload carries the flags).
+    UVec<uint32_t> apply_defer_;
+    void defer_apply(UVec<uint32_t>& newly);
+    void flush_apply();
 
     std::mutex mu_;
     mm_config cfg_;

@@ -268,6 +268,10 @@ struct Replay : ReplayCore {
     // overlap: host work run while the batch's kernels and copies are in
     // flight (the pool bucketing of the rows, which needs no hit list)
     void run_batch(std::vector<BGroup>& bg, bool need_pm, const std::function<void()>& overlap = nullptr) {
+        using rclk = std::chrono::steady_clock;
+        auto rms = [](rclk::time_point a, rclk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        const auto r0 = rclk::now();
+        c.flush_apply();  // the previous batch's selections, before this batch's searches
         const uint32_t kChunk = (uint32_t)scan_chunk_len();
         lg.clear();
         lg_group.clear();
@@ -613,8 +617,14 @@ struct Replay : ReplayCore {
             if (need_pm && whole_off)
                 NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, whole_off * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         }
+        const auto r1 = rclk::now();
         if (overlap) overlap();
+        const auto r2 = rclk::now();
         NKM_HIP(hipStreamSynchronize(stream));
+        const auto r3 = rclk::now();
+        stats.rb_prep_ms += rms(r0, r1);
+        stats.rb_overlap_ms += rms(r1, r2);
+        stats.rb_wait_ms += rms(r2, r3);
         if (host_x) {
             c.shard_gather_host(c.h_res_.p, o_res);
             c.shard_gather_host(c.h_out_.p, o_out);
@@ -690,6 +700,8 @@ struct Replay : ReplayCore {
         } else {
             wire(0, (size_t)nwhole);
         }
+        const auto r4 = rclk::now();
+        stats.rb_post_ms += rms(r3, r4);
         // chunked / mscan searches: exact hit counts are known now; copy just
         // those (an mscan list: 4-B slot ids, in the first quarter of its region)
         const size_t n_scan_cg = cg_list.size() - (use_m ? m_list.size() : 0);
@@ -724,6 +736,7 @@ struct Replay : ReplayCore {
             g.complete = complete;
         }
         if (!cg_list.empty()) NKM_HIP(hipStreamSynchronize(stream));
+        stats.rb_lists_ms += rms(r4, rclk::now());
     }
 
     bool pair_slow(const BGroup& g, uint32_t from_pos, uint32_t to_pos) override {
@@ -1000,6 +1013,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     // each pool's entry bound (every ticket of its list and rows joins at
     // most one group): the walk reserves it so readers never see a move
     std::vector<uint64_t> esum(pipe ? ntask_g * ng : 0, 0);
+    const auto tg0 = clk::now();
     wp.run(ntask_g, [&](size_t t) {
         for (uint32_t gi : dense_ids) {
             DensePool& D = dense_pools_[gi];
@@ -1170,6 +1184,8 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         }
         task_ms[t] = msd(tw0, clk::now());
     };
+    const auto tg1 = clk::now();
+    stats.par_gather_ms += msd(tg0, tg1);
     if (pipe) {
         wp.run(ntask + nch, [&](size_t t) {
             if (t < ntask) worker(t);
@@ -1189,6 +1205,8 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     } else {
         wp.run(ntask, worker);
     }
+    const auto tg2 = clk::now();
+    stats.par_job_ms += msd(tg1, tg2);
     wp.run(ntask_g, [&](size_t t) {
         for (uint32_t gi : dense_ids) {
             const DensePool& D = dense_pools_[gi];
@@ -1198,6 +1216,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         }
     });
     const auto tp2 = clk::now();
+    stats.par_clear_ms += msd(tg2, tp2);
     for (uint32_t v : pool_stop) *min_stop = std::min(*min_stop, v);
     if (pipe) {
     } else if (few) {
@@ -1679,7 +1698,7 @@ int Core::process_default(GroupList& out_groups,
             stats.parallel_batches++;
             const auto tr = std::chrono::steady_clock::now();
             stats.replay_ms += std::chrono::duration<double, std::milli>(tr - tb1).count();
-            apply_selected_to_device(newly.data(), newly.size());
+            defer_apply(newly);
             stats.apply_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
             if (batch_profile_)
                 std::fprintf(stderr, "[nkm]   batch %d (parallel): rows %zu searches %zu%s | search %.2f replay %.2f ms\n",
@@ -1742,7 +1761,7 @@ int Core::process_default(GroupList& out_groups,
         }
         const auto tb2 = std::chrono::steady_clock::now();
         stats.replay_ms += std::chrono::duration<double, std::milli>(tb2 - tb1).count();
-        apply_selected_to_device(newly.data(), newly.size());
+        defer_apply(newly);
         if (batch_profile_)
             std::fprintf(stderr, "[nkm]   batch %d: rows %zu searches %zu decided %zu%s | assemble %.2f search %.2f replay %.2f ms\n",
                          stats.batches, brow.size(), bg.size(), done, exhausted ? " (list ran out)" : "",
@@ -2195,8 +2214,9 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
         }
         f1 = fclk::now();
         // Retire the matched tickets.  When no session or party holds more
-        // than one ticket, each slot's bookkeeping touches keys no other slot
-        // does, so chunks of whole groups retire in parallel.
+        // than one ticket, a retired slot left in sessionTickets /
+        // partyTickets counts as absent (SlotSets reads live_), so retiring is
+        // clearing the flags, in parallel chunks of whole groups.
         if (sess_slots_.more.empty() && party_slots_.more.empty()) {
             const size_t ng2 = groups.size();
             std::vector<uint32_t> killed(nchunk, 0);
@@ -2211,8 +2231,6 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
                     live_[s] = 0;
                     is_active_[s] = 0;
                     k++;
-                    for (uint32_t p = pres_off_[s]; p < pres_off_[s + 1]; p++) sess_slots_.erase(pres_sess_[p], s);
-                    if (party_[s] != kNoParty) party_slots_.erase(party_[s], s);
                 }
                 killed[c] = k;
             });
@@ -2433,13 +2451,16 @@ int Core::process(mm_matched* out) {
                          "[nkm] sync %.2f ms | pass %.2f ms (assemble %.2f, search %.2f ms [kernel %.2f ms], replay %.2f "
                          "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches) | finish %.2f ms | "
                          "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu | par bucket %.2f work %.2f "
-                         "merge %.2f ms (task max %.2f ms, rows %llu, hits %llu)\n",
+                         "merge %.2f ms (task max %.2f ms, rows %llu, hits %llu) | batch: prep %.2f overlap %.2f wait %.2f "
+                         "post %.2f lists %.2f | replay: gather %.2f job %.2f clear %.2f\n",
                          ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms(), stats.replay_ms,
                          stats.apply_ms, stats.batches,
                          stats.parallel_batches, stats.refetches, stats.launches(), ms(t2, t3), ms(t3, t4),
                          groups.size(), nslots(), n_live_, active_list_.size(), sigs_.size(),
                          dict_.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms,
-                         stats.par_task_max_ms, (unsigned long long)stats.par_rows, (unsigned long long)stats.par_hits);
+                         stats.par_task_max_ms, (unsigned long long)stats.par_rows, (unsigned long long)stats.par_hits,
+                         stats.rb_prep_ms, stats.rb_overlap_ms, stats.rb_wait_ms, stats.rb_post_ms, stats.rb_lists_ms,
+                         stats.par_gather_ms, stats.par_job_ms, stats.par_clear_ms);
         }
     }
     const int dk = stats.dominant();  // bench.py's roofline kernel

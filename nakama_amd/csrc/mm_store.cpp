@@ -91,6 +91,8 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     cfg_.node = nullptr;
     device_ = cfg.device;
     host_share_ = g_create_share;
+    sess_slots_.live = &live_;
+    party_slots_.live = &live_;
     int ndev = 0;
     NKM_HIP(hipGetDeviceCount(&ndev));
     if (ndev <= 0 || device_ < 0 || device_ >= ndev) throw DeviceError{hipErrorNoDevice, "device ordinal", __LINE__};
@@ -1223,6 +1225,7 @@ void Core::compact() {
         if (remap[s] != kNoSlot) nord.push_back(remap[s]);
     order_ = std::move(nord);
     pending_dead_.clear();
+    apply_defer_.clear();  // old slot numbers; the re-upload below carries the flags
     index_dirty_ = true;
     dev_slots_ = 0;
     for (auto& d : dev_field_slots_) d = 0;
@@ -1319,6 +1322,7 @@ void Core::sync_device() {
         up(d_party_.p, party_.data(), dev_slots_, n);
         up(d_squery_.p, squery_.data(), dev_slots_, n);
     }
+    flush_apply();  // the last pass's selections (slots below dev_slots_)
     // dead slots that were already on the device
     if (!pending_dead_.empty()) {
         std::vector<uint32_t> v;
@@ -1380,6 +1384,19 @@ DStore Core::dstore() const {
     st.tset_ids = d_tset_ids_.p;
     st.tset_sc = d_tset_sc_.p;
     return st;
+}
+
+void Core::defer_apply(UVec<uint32_t>& newly) {
+    if (newly.empty()) return;
+    flush_apply();
+    apply_defer_.swap(newly);  // newly keeps the other buffer's capacity
+    newly.clear();
+}
+
+void Core::flush_apply() {
+    if (apply_defer_.empty()) return;
+    apply_selected_to_device(apply_defer_.data(), apply_defer_.size());
+    apply_defer_.clear();
 }
 
 // Clears the device alive flags of the given slots.  Asynchronous: the copy

@@ -152,6 +152,11 @@ struct RxCompiler {
     // Perl flags in effect (parsePerlFlags): (?i) FoldCase, (?s) DotNL; a
     // group restores its opener's flags when it closes
     bool fold_case = false, dot_nl = false;
+    // (?U) NonGreedy: regexp/syntax stamps it on every node parsed while it
+    // holds (literals, classes, captures), and vellum rejects any node that
+    // carries it (compile.go:57-59, ErrNoLazy) — under (?U) every atom is a
+    // search error; flag groups and empty groups parse to no node.
+    bool non_greedy = false;
     explicit RxCompiler(const std::string& p) : s(p) {}
 
     [[noreturn]] static void err() { throw Stop{MT_SEARCH_ERROR}; }
@@ -168,8 +173,8 @@ struct RxCompiler {
     }
 
     // \pN, \p{Name}, \p{^Name}, \PN (parseUnicodeClass), i at the backslash.
-    // Names: Go's general categories and Any; a script name (\p{Greek}) is
-    // not lowered (MM_ERR_UNSUPPORTED), nor is any other unknown name.
+    // Names: Any, Go's general categories, then its scripts (\p{Greek},
+    // unicodeTable's order); any other name is ErrInvalidCharRange.
     void unicode_class(Ranges* out) {
         bool neg = s[i + 1] == 'P';
         i += 2;
@@ -192,7 +197,7 @@ struct RxCompiler {
         } else if (const uni::Category* c = uni::category(name.data(), name.size())) {
             for (int k = 0; k < c->n; k++) t.push_back({c->r[k].lo, c->r[k].hi});
         } else {
-            unsupported();
+            err();
         }
         append_group(std::move(t), neg, fold_case, out);
     }
@@ -336,6 +341,7 @@ struct RxCompiler {
                 if (last_repeat) err();    // ErrInvalidRepeatOp (a**)
                 bool lazy = false;
                 if (peek() == '?') { lazy = true; i++; }
+                lazy = lazy != non_greedy;  // `x*?` under (?U) is greedy again (flags ^= NonGreedy)
                 Node n;
                 n.t = rt;
                 n.sub = {items.back()};
@@ -347,6 +353,7 @@ struct RxCompiler {
                 continue;
             }
             last_repeat = false;
+            if (non_greedy && c != '(') err();  // an atom carrying NonGreedy
             const int a = atom();
             if (a >= 0) items.push_back(a);  // -1: a (?flags) item, which adds no node
         }
@@ -373,9 +380,11 @@ struct RxCompiler {
         switch (c) {
         case '(': {
             i++;
-            const bool saved_fold = fold_case, saved_dot = dot_nl;
+            const bool saved_fold = fold_case, saved_dot = dot_nl, saved_ng = non_greedy;
+            if (peek() != '?' && non_greedy) err();  // a capture under (?U)
             if (peek() == '?') {
                 if (peek(1) == 'P' && peek(2) == '<') {
+                    if (non_greedy) err();
                     size_t close = s.find('>', i + 3);
                     if (close == std::string::npos || close == i + 3) err();  // ErrInvalidNamedCapture
                     for (size_t k = i + 3; k < close; k++)
@@ -384,24 +393,26 @@ struct RxCompiler {
                 } else {
                     // (?flags) / (?flags:re) / (?flags-flags...) (parsePerlFlags)
                     i++;
-                    bool fc = fold_case, dn = dot_nl, neg = false, saw = false;
+                    bool fc = fold_case, dn = dot_nl, ng = non_greedy, neg = false, saw = false;
                     for (;;) {
                         if (end()) err();  // ErrInvalidPerlOp / missing paren
                         const char c = s[i++];
                         if (c == 'i') { fc = !neg; saw = true; }
                         else if (c == 's') { dn = !neg; saw = true; }
                         else if (c == 'm') { saw = true; }  // OneLine: only ^ $ (rejected by vellum anyway)
-                        else if (c == 'U') { unsupported(); }  // NonGreedy: every later node lazy
+                        else if (c == 'U') { ng = !neg; saw = true; }  // NonGreedy
                         else if (c == '-') { if (neg) err(); neg = true; saw = false; }
                         else if (c == ':' || c == ')') {
                             if (neg && !saw) err();
                             if (c == ')') {  // flags for the rest of the enclosing group: no node
                                 fold_case = fc;
                                 dot_nl = dn;
+                                non_greedy = ng;
                                 return -1;
                             }
                             fold_case = fc;
                             dot_nl = dn;
+                            non_greedy = ng;
                             break;
                         } else {
                             err();  // ErrInvalidPerlOp
@@ -416,6 +427,7 @@ struct RxCompiler {
             i++;
             fold_case = saved_fold;
             dot_nl = saved_dot;
+            non_greedy = saved_ng;
             return r;
         }
         case '.': {

@@ -20,7 +20,7 @@
 #include <string>
 #include <vector>
 
-#include "../nakama_amd/csrc/unicode_tables.h"  // data only: Unicode 13 categories and fold orbits
+#include "unicode_ref.h"  // data only, the oracle's own layout: Unicode 13 category / script runs, SimpleFold
 
 namespace oracle_re {
 
@@ -68,22 +68,59 @@ using RP = std::shared_ptr<Re>;
 
 using RangeV = std::vector<std::pair<int32_t, int32_t>>;
 
-// (?i): every orbit of the simple case folding that meets the set joins it
-// whole (unicode.SimpleFold orbits, as vellum expands FoldCase literals and Go's
-// parser folds classes).
+// unicode.SimpleFold (the next rune of r's orbit; r itself when alone)
+inline int32_t simple_fold(int32_t r) {
+    int lo = 0, hi = uref::kNFold;
+    while (lo < hi) {
+        const int mid = (lo + hi) / 2;
+        if ((int32_t)uref::kSimpleFold[mid].r < r) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < uref::kNFold && (int32_t)uref::kSimpleFold[lo].r == r ? (int32_t)uref::kSimpleFold[lo].next : r;
+}
+
+// (?i): every rune of the set brings its whole SimpleFold orbit (vellum
+// expands FoldCase literals through unicode.SimpleFold; Go's parser folds
+// classes the same way).
 inline void fold_in(RangeV& rs) {
-    const int n_orbits = (int)(sizeof(uni::kOrbitStart) / sizeof(uni::kOrbitStart[0])) - 1;
     RangeV add;
-    for (int o = 0; o < n_orbits; o++) {
-        bool meets = false;
-        for (int k = uni::kOrbitStart[o]; k < uni::kOrbitStart[o + 1] && !meets; k++)
-            for (auto& q : rs)
-                if ((int32_t)uni::kOrbitRunes[k] >= q.first && (int32_t)uni::kOrbitRunes[k] <= q.second) { meets = true; break; }
-        if (meets)
-            for (int k = uni::kOrbitStart[o]; k < uni::kOrbitStart[o + 1]; k++)
-                add.push_back({(int32_t)uni::kOrbitRunes[k], (int32_t)uni::kOrbitRunes[k]});
+    for (int k = 0; k < uref::kNFold; k++) {
+        const int32_t r = (int32_t)uref::kSimpleFold[k].r;
+        bool in = false;
+        for (auto& q : rs) in = in || (r >= q.first && r <= q.second);
+        if (!in) continue;
+        for (int32_t x = simple_fold(r); x != r; x = simple_fold(x)) add.push_back({x, x});
     }
     rs.insert(rs.end(), add.begin(), add.end());
+}
+
+// The runes of a Go class name: unicode.Categories (two-letter categories
+// without Cn, and the one-letter unions, C without Cn), then unicode.Scripts
+// (regexp/syntax unicodeTable); false for any other name.
+inline bool named_class(const std::string& n, RangeV* out) {
+    int want_cat = -1, want_script = -1;
+    bool union_of = false;
+    if (n.size() == 2 && n != "Cn") {
+        for (int k = 0; k < uref::kNCat; k++)
+            if (n == uref::kCatName[k]) want_cat = k;
+    } else if (n.size() == 1 && std::string("CLMNPSZ").find(n[0]) != std::string::npos) {
+        union_of = true;
+    }
+    if (want_cat < 0 && !union_of)
+        for (int k = 1; k < uref::kNScript; k++)
+            if (n == uref::kScriptName[k]) want_script = k;
+    if (want_cat < 0 && !union_of && want_script < 0) return false;
+    out->clear();
+    for (int k = 0; k < uref::kNRuns; k++) {
+        const uref::Run& r = uref::kRuns[k];
+        const char* cn = uref::kCatName[r.cat];
+        const bool in = union_of ? (cn[0] == n[0] && std::string(cn) != "Cn")
+                                 : want_cat >= 0 ? (int)r.cat == want_cat : (int)r.script == want_script;
+        if (!in) continue;
+        if (!out->empty() && out->back().second + 1 == (int32_t)r.lo) out->back().second = (int32_t)r.hi;
+        else out->push_back({(int32_t)r.lo, (int32_t)r.hi});
+    }
+    return true;
 }
 
 // complement within [0, 0x10FFFF]
@@ -103,7 +140,12 @@ struct Parse {
     std::vector<int32_t> p;  // pattern runes
     size_t i = 0;
     int nest = 0;
-    bool fc = false, dn = false;  // (?i) FoldCase, (?s) DotNL in effect
+    // (?i) FoldCase, (?s) DotNL, (?U) NonGreedy in effect.  NonGreedy is
+    // stamped on every node parsed while it holds (regexp/syntax copies the
+    // flags into each literal, class and capture), and vellum rejects any
+    // node carrying it (compile.go:57-59, ErrNoLazy): under (?U) every atom
+    // is a search error; empty groups and flag groups parse to no node.
+    bool fc = false, dn = false, ug = false;
     struct Fail { Status s; };
     [[noreturn]] void fail() { throw Fail{SEARCH_ERROR}; }
     [[noreturn]] void unsup() { throw Fail{UNSUPPORTED}; }
@@ -142,7 +184,8 @@ struct Parse {
         else return false;
         return true;
     }
-    // at the backslash of \p / \P: the class's runes (scripts and unknown names: unsupported)
+    // at the backslash of \p / \P: the class's runes (an unknown name is
+    // ErrInvalidCharRange: a search error)
     RangeV uclass() {
         bool negative = cur(1) == 'P';
         i += 2;
@@ -160,16 +203,10 @@ struct Parse {
         }
         if (!name.empty() && name[0] == '^') { negative = !negative; name.erase(name.begin()); }
         std::string n;
-        for (int32_t c : name) { if (c < 0 || c > 0x7e) unsup(); n.push_back((char)c); }
+        for (int32_t c : name) { if (c < 0 || c > 0x7e) fail(); n.push_back((char)c); }
         RangeV g;
         if (n == "Any") g = {{0, 0x10FFFF}};
-        else {
-            const uni::Category* cat = nullptr;
-            for (const uni::Category& c : uni::kCategories)
-                if (n == c.name) cat = &c;
-            if (!cat) unsup();
-            for (int k = 0; k < cat->n; k++) g.push_back({(int32_t)cat->r[k].lo, (int32_t)cat->r[k].hi});
-        }
+        else if (!named_class(n, &g)) fail();
         return group(g, negative);
     }
     static bool alnum(int32_t c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
@@ -302,9 +339,11 @@ struct Parse {
         if (c == -1) fail();  // invalid UTF-8 in the pattern
         if (c == '(') {
             i++;
-            const bool fc0 = fc, dn0 = dn;
+            const bool fc0 = fc, dn0 = dn, ug0 = ug;
+            if (cur() != '?' && ug) fail();  // a capture under (?U)
             if (cur() == '?') {
                 if (cur(1) == 'P' && cur(2) == '<') {
+                    if (ug) fail();
                     i += 3;
                     size_t s = i;
                     while (i < p.size() && p[i] != '>') {
@@ -317,7 +356,7 @@ struct Parse {
                     // flags: [imsU]* ( '-' [imsU]+ )? then ':' (a group) or ')' (the rest of this group)
                     i++;
                     bool on = true, any_after_minus = false, minus = false;
-                    bool nfc = fc, ndn = dn;
+                    bool nfc = fc, ndn = dn, nug = ug;
                     while (true) {
                         int32_t f = cur();
                         if (f < 0 && at_end()) fail();
@@ -325,12 +364,13 @@ struct Parse {
                         if (f == 'i') { nfc = on; any_after_minus = true; }
                         else if (f == 's') { ndn = on; any_after_minus = true; }
                         else if (f == 'm') { any_after_minus = true; }
-                        else if (f == 'U') unsup();
+                        else if (f == 'U') { nug = on; any_after_minus = true; }
                         else if (f == '-' && !minus) { minus = true; on = false; any_after_minus = false; }
                         else if (f == ':' || f == ')') {
                             if (minus && !any_after_minus) fail();
                             fc = nfc;
                             dn = ndn;
+                            ug = nug;
                             if (f == ')') return nullptr;  // no node: the flags hold to the group's end
                             break;
                         } else fail();
@@ -344,8 +384,10 @@ struct Parse {
             i++;
             fc = fc0;
             dn = dn0;
+            ug = ug0;
             return r;
         }
+        if (ug) fail();  // any other atom under (?U) carries NonGreedy
         if (c == '^' || c == '$') fail();
         if (c == '.') {
             i++;
@@ -409,6 +451,7 @@ struct Parse {
                 if (s->kids.empty() || after_rep) fail();
                 bool lazy = cur() == '?';
                 if (lazy) i++;
+                lazy = lazy != ug;  // `x*?` under (?U) is greedy again (flags ^= NonGreedy)
                 auto r = std::make_shared<Re>();
                 r->k = Re::REP;
                 r->lo = lo;

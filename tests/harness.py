@@ -22,7 +22,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def build_oracle():
     if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < max(
-            os.path.getmtime(os.path.join(ROOT, "oracle", f)) for f in ("mm_oracle.cpp", "go_compat.h")):
+            os.path.getmtime(os.path.join(ROOT, "oracle", f)) for f in ("mm_oracle.cpp", "go_compat.h", "go_regexp.h", "unicode_ref.h")):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
 
 

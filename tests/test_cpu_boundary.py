@@ -147,7 +147,18 @@ GO_REGEXP_CASES = [
     ("\\p{Lu}\\p{Ll}+", "hello", False), ("\\PL", "3", True), ("\\p{^L}", "3", True), ("\\P{^L}", "x", True),
     ("\\pN", "\u0663", True), ("\\p{Nd}", "\u2167", False), ("\\p{Nl}", "\u2167", True), ("[\\pL\\d]+", "a1b2", True),
     ("\\p{Any}+", "a\n", True), ("(?i)\\p{Lu}", "a", True), ("\\p{Lu}", "a", False),
-    ("\\p{Greek}", "α", "unsupported"), ("(?U)a", "a", "unsupported"), ("(?i-)a", "a", "search_error"),
+    ("(?i-)a", "a", "search_error"),
+    # Go's unicode.Scripts after its Categories (unicodeTable); FoldScript under (?i)
+    ("\\p{Greek}", "α", True), ("\\p{Greek}", "a", False), ("\\p{Greek}+", "Ωμέγα", True),
+    ("\\p{Greek}", "\u00b5", False), ("(?i)\\p{Greek}", "\u00b5", True), ("\\P{Greek}", "\u00b5", True),
+    ("\\p{Latin}+", "héllo", True), ("\\p{Han}", "中", True), ("\\p{Cyrillic}\\p{Latin}", "жa", True),
+    ("\\p{Common}", "1", True), ("\\p{Inherited}", "\u0301", True), ("[\\p{Greek}\\p{Latin}]+", "aβc", True),
+    ("\\p{greek}", "α", "search_error"), ("\\p{Foo}", "a", "search_error"), ("\\p{Cn}", "a", "search_error"),
+    ("\\p{Cypro_Minoan}", "a", "search_error"),  # a Unicode 14 script: not in Go 1.20
+    # (?U): NonGreedy stamped on every later node; vellum rejects each (ErrNoLazy)
+    ("(?U)a", "a", "search_error"), ("(?U)", "", True), ("a(?U)", "a", True), ("(?U:)a", "a", True),
+    ("(?U)(?-U)a", "a", True), ("(?U:a)", "a", "search_error"), ("(?U)()", "", "search_error"),
+    ("(?U:(?-U:a+))", "aa", True), ("a*?", "a", "search_error"),
     ("(?x)a", "a", "search_error"), ("(?P=n)", "a", "search_error"), ("\\p{", "a", "search_error"),
 ]
 
@@ -169,7 +180,7 @@ def _rand_regex(rnd, depth=0):
     atoms = ["a", "b", "c", ".", "[ab]", "[^a]", "[a-c]", "\\d", "\\w", "\\s", "\\.", "x", "é", "-", "_", "{", "}",
              "(?i)", "(?s)", "(?-i)", "K", "k", "\u212a", "s", "ſ", "É", "σ", "Σ", "[[:alpha:]]", "[[:^lower:]]",
              "[[:punct:][:digit:]]", "\\pL", "\\PL", "\\p{Lu}", "\\p{^Ll}", "[\\pN_]", "\\W", "[^\\w]", "(?i:k)",
-             "(?s:.)"]
+             "(?s:.)", "\\p{Greek}", "\\P{Latin}", "[\\p{Greek}x]", "(?U)", "(?-U)", "(?U:)", "α", "Ω"]
     parts = []
     for _ in range(rnd.randint(0, 4)):
         r = rnd.random()
@@ -197,7 +208,7 @@ def test_regexp_differential_vs_oracle(product):
     rnd = random.Random(5)
     orc = harness.oracle_lib()
     alphabet = ["a", "b", "c", "x", ".", "1", "_", " ", "\n", "é", "-", "A", "K", "k", "\u212a", "ſ", "S", "É", "σ",
-                "ς", "Σ", "!", "٣"]
+                "ς", "Σ", "!", "٣", "α", "Ω", "\u00b5", "ж"]
     bad = []
     for _ in range(1500):
         pat = _rand_regex(rnd)
