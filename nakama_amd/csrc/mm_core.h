@@ -568,6 +568,7 @@ private:
     // the pass (processDefault), so members of a dropped group leave it
     void finish_pass_serial(GroupList& groups, bool selected);
     void fill_matched(const GroupList& groups, mm_matched* out, bool cands);
+    bool finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& groups, mm_matched* out);
     void choose_source(const Sig& s, DGroup& g, SrcChoice* ch = nullptr);
     void source_of(const Sig& s, DGroup& g, SrcChoice* ch = nullptr) const;
     struct ParPlan {  // a batch's pools (plan_parallel), bucketed while its searches run
@@ -576,6 +577,7 @@ private:
         std::vector<uint32_t> search_pool;  // per search
         std::vector<uint32_t> pool_off;     // CSR: pool p's batch rows are pool_rows[pool_off[p], pool_off[p+1])
         std::vector<uint32_t> pool_rows;    // ascending per pool
+        std::vector<uint8_t> self_rows;     // per pool: every row carries its own search's terms
     };
     struct RowRec {  // a batch row's outcome in a parallel replay (indexed by batch row)
         uint32_t ent, len, task;  // its group's entries: task_ents_[task][ent, ent + len)
@@ -661,6 +663,14 @@ public:
     std::vector<uint8_t> indexed_;
     std::vector<uint8_t> is_active_;  // in m.activeIndexes
     std::vector<uint32_t> sig_;
+    // per slot: the ticket carries every keyword its own query requires (its
+    // signature's MUST terms), so it lies in its own pool (plan_parallel)
+    std::vector<uint8_t> self_match_;
+    // slots in CreatedAt order with strictly increasing created_ and ckey_
+    // (tickets inserted in time order): scan order, slot order and the pinned
+    // active order agree
+    bool monotone_ = true;
+    uint8_t self_match_of(uint32_t s) const;
     std::vector<HotRec> hot_;         // per slot: the replay's packed fields
     void set_hot(uint32_t s);
     std::vector<uint32_t> pres_off_;  // CSR over presences: [slot] -> first presence
@@ -792,6 +802,8 @@ public:
     // NKM_DENSE=0: single-search pools take the generic walk too (A/B, tests)
     bool dense_mode_ = true;
     bool pipe_mode_ = true;  // NKM_PIPE=0: the pool walks' merge runs after all walks, not beside them
+    bool gpipe_mode_ = true; // NKM_GPIPE=0: identity pools gather their copies before the walks, not beside them
+    int32_t max_pres_ = 1;   // most presences of any ticket inserted (an entry bound of the pipelined merge)
     // NKM_FAST=0: every row takes the exact loop body, also when no two live
     // tickets share a session (the fast walk, replay_core.h) (A/B, tests)
     bool fast_mode_ = true;
@@ -810,6 +822,12 @@ public:
     std::vector<int32_t> out_offs_;
     std::vector<int64_t> out_created_;
     std::atomic<bool> out_in_use_{false};
+    // The pass has claimed the output arena (out_in_use_ set) to fill its
+    // result early: the pipelined merge writes the result entries of its
+    // groups beside the pool walks, and groups [0, filled_groups_) of the pass
+    // are filled (reset by anything that reorders them).
+    bool arena_claimed_ = false;
+    size_t filled_groups_ = 0;
     DevArray<uint32_t> d_pm_;      // pair matrices (RevPrecision combos)
     PinnedArray<uint32_t> h_pm_;
     // processCustom's device enumeration (enum_kernel): rows, hits, work items,

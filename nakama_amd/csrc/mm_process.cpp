@@ -18,6 +18,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <stdexcept>
 #include <thread>
 #include <cstdlib>
 #include <cstring>
@@ -865,23 +866,34 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& br
     const unsigned nchunk = nb >= par_min(65536) ? wp.size() : 1;
     std::vector<uint32_t> cnt((size_t)nchunk * ng, 0);
     std::vector<uint8_t> cbad(nchunk, 0);
+    // per (chunk, pool): a row that is not known to carry its own search's
+    // terms (self_match_) — the pool is then not known to hold all its rows
+    std::vector<uint8_t> cforeign((size_t)nchunk * ng, 0);
     wp.run(nchunk, [&](size_t c) {
         std::vector<uint32_t> k(ng, 0);
         for (size_t bi = nb * c / nchunk; bi < nb * (c + 1) / nchunk; bi++) {
             const uint32_t r = brow[bi];
-            const uint32_t p = search_pool[brow_group[bi]];
+            const uint32_t gi = brow_group[bi];
+            const uint32_t p = search_pool[gi];
+            k[p]++;
+            // the row carries every term of its own search: the pool's keys among them
+            if (self_match_[r] && indexed_[r] && sig_[r] == bg[gi].sig) continue;
+            cforeign[c * ng + p] = 1;
             const auto& pk = pool_keys[p];
             for (size_t f = 0; f < keyf.size(); f++)
                 if (fkind_[keyf[f]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[f]][r] != pk[f]) {
                     cbad[c] = 1;
                     return;
                 }
-            k[p]++;
         }
         std::copy(k.begin(), k.end(), cnt.begin() + c * ng);
     });
     for (unsigned c = 0; c < nchunk; c++)
         if (cbad[c]) return false;
+    P.self_rows.assign(ng, 1);
+    for (unsigned c = 0; c < nchunk; c++)
+        for (size_t p = 0; p < ng; p++)
+            if (cforeign[c * ng + p]) P.self_rows[p] = 0;
     P.pool_off.assign(ng + 1, 0);
     for (size_t p = 0; p < ng; p++) {  // cnt becomes each (chunk, pool)'s first position
         uint32_t run = P.pool_off[p];
@@ -1010,24 +1022,90 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     // idle while the merge waits for the slowest walk.
     const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
     const bool pipe = few && pipe_mode_ && !dense_ids.empty() && dense_ids.size() == ng && nch > 1;
-    // each pool's entry bound (every ticket of its list and rows joins at
-    // most one group): the walk reserves it so readers never see a move
-    std::vector<uint64_t> esum(pipe ? ntask_g * ng : 0, 0);
+    // Pipelined gather: when every pool's rows are its list in list order
+    // (identity pools — C3 / C4: every member of a pool of fresh tickets
+    // searches, and batch order is scan order) no slot -> position map is
+    // built, and the gathers run in the walks' job: tasks after the walks
+    // gather piece t of every pool and publish each pool's gathered prefix;
+    // a walk reads a position once it is covered (DenseRun::need).  Needs a
+    // worker beyond the walks (tasks are claimed in index order).
     const auto tg0 = clk::now();
-    wp.run(ntask_g, [&](size_t t) {
+    bool gpipe = false;
+    if (pipe && gpipe_mode_ && wp.size() > ntask) {
+        bool all = true;
+        for (uint32_t gi : dense_ids) all = all && dense_pools_[gi].nrows == dense_pools_[gi].n;
+        // Slots in time order (monotone_): scan order = batch order, so the
+        // rows ARE the list when they are as many and each lies in it — a
+        // row carrying its term-only search's terms matches that search
+        // (its own counts meet its count ranges; the party exclusion is the
+        // walk's) and is alive.  Otherwise compare position by position.
+        bool known = all && monotone_;
+        for (uint32_t gi : dense_ids) {
+            if (!known) break;
+            const Sig& sg = sigs_[bg[sidx[soff[gi]]].sig];
+            known = P.self_rows[gi] && sg.qkind == QK_BOOL && sg.must_terms.size() == sg.n_clauses;
+        }
+        if (known) {
+            gpipe = true;
+        } else if (all) {
+            std::vector<uint8_t> ok(ntask_g, 1);
+            wp.run(ntask_g, [&](size_t t) {
+                for (uint32_t gi : dense_ids) {
+                    const DensePool& D = dense_pools_[gi];
+                    uint32_t lo, hi;
+                    piece(D, t, lo, hi);
+                    if (!D.rows_are_list(lo, hi)) { ok[t] = 0; return; }
+                }
+            });
+            gpipe = std::all_of(ok.begin(), ok.end(), [](uint8_t x) { return x != 0; });
+        }
+    }
+    std::unique_ptr<std::atomic<uint32_t>[]> gfront(gpipe ? new std::atomic<uint32_t>[ng] : nullptr);
+    std::unique_ptr<std::atomic<uint8_t>[]> gdone(gpipe ? new std::atomic<uint8_t>[ng * ntask_g] : nullptr);
+    std::atomic<bool> id_broken{false};  // an identity pool whose row was not at its position (a bug: fail loudly)
+    if (gpipe) {
+        for (size_t gi = 0; gi < ng; gi++) gfront[gi].store(0);
+        for (size_t k = 0; k < ng * ntask_g; k++) gdone[k].store(0);
+        for (uint32_t gi : dense_ids) {
+            DensePool& D = dense_pools_[gi];
+            D.identity = true;
+            D.pieces = (uint32_t)ntask_g;
+            D.front = &gfront[gi];
+            D.broken = &id_broken;
+        }
+    }
+    // piece t of every pool, then each pool's published prefix advanced over
+    // the pieces done (whichever worker completes the next piece moves it on)
+    auto gather_piece = [&](size_t t) {
         for (uint32_t gi : dense_ids) {
             DensePool& D = dense_pools_[gi];
             uint32_t lo, hi;
             piece(D, t, lo, hi);
             D.gather(rv, lo, hi, pos_of_.data());
-            if (!pipe) continue;
-            uint64_t e = 0;
-            for (uint32_t k = lo; k < hi; k++) e += (uint64_t)D.rec[k].count;
-            const uint32_t r0 = (uint32_t)((uint64_t)D.nrows * t / ntask_g), r1 = (uint32_t)((uint64_t)D.nrows * (t + 1) / ntask_g);
-            for (uint32_t j = r0; j < r1; j++) e += (uint64_t)rv.hot[brow[D.bis[j]]].count;
-            esum[t * ng + gi] = e;
+            gdone[gi * ntask_g + t].store(1);
+            uint32_t f = gfront[gi].load();
+            while (f < ntask_g && gdone[gi * ntask_g + f].load())
+                if (gfront[gi].compare_exchange_weak(f, f + 1)) f++;
         }
-    });
+    };
+    // each pool's entry bound (every ticket of its list and rows joins at
+    // most one group): the walk reserves it so readers never see a move
+    std::vector<uint64_t> esum(pipe && !gpipe ? ntask_g * ng : 0, 0);
+    if (!gpipe)
+        wp.run(ntask_g, [&](size_t t) {
+            for (uint32_t gi : dense_ids) {
+                DensePool& D = dense_pools_[gi];
+                uint32_t lo, hi;
+                piece(D, t, lo, hi);
+                D.gather(rv, lo, hi, pos_of_.data());
+                if (!pipe) continue;
+                uint64_t e = 0;
+                for (uint32_t k = lo; k < hi; k++) e += (uint64_t)D.rec[k].count;
+                const uint32_t r0 = (uint32_t)((uint64_t)D.nrows * t / ntask_g), r1 = (uint32_t)((uint64_t)D.nrows * (t + 1) / ntask_g);
+                for (uint32_t j = r0; j < r1; j++) e += (uint64_t)rv.hot[brow[D.bis[j]]].count;
+                esum[t * ng + gi] = e;
+            }
+        });
     struct alignas(128) Prog {
         std::atomic<uint64_t> st{0};  // (records published << 32) | rows done
         const PoolRec* recs = nullptr;
@@ -1036,8 +1114,10 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     std::unique_ptr<Prog[]> prog(pipe ? new Prog[ng] : nullptr);
     std::vector<uint64_t> ebound(pipe ? ng : 0, 0);
     uint64_t ebound_all = 0;
-    for (size_t t = 0; pipe && t < ntask_g; t++)
+    for (size_t t = 0; pipe && !gpipe && t < ntask_g; t++)
         for (size_t gi = 0; gi < ng; gi++) ebound[gi] += esum[t * ng + gi];
+    if (gpipe)  // identity pools: the rows are list members, whose entries are at most max_pres_ each
+        for (uint32_t gi : dense_ids) ebound[gi] = (uint64_t)dense_pools_[gi].n * (uint64_t)std::max(1, max_pres_);
     for (uint64_t e : ebound) ebound_all += e;
     const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
     if (pipe) {  // bounds now (no zero-fill: default-initialising vectors), the totals after the job
@@ -1045,6 +1125,16 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         grow_to(out_groups.ents, e0 + ebound_all);
         grow_to(expired, x0 + nb);
         grow_to(newly, n0 + ebound_all);
+    }
+    // the result entries too, when every earlier group of the pass is filled
+    // and the output arena is (or can be) this pass's
+    const bool fill = pipe && filled_groups_ == g0 && (arena_claimed_ || !out_in_use_.exchange(true));
+    if (fill) {
+        arena_claimed_ = true;
+        if (out_offs_.size() < g0 + 1 + nb) grow_to(out_offs_, g0 + 1 + nb);
+        if (out_ents_.size() < e0 + ebound_all) grow_to(out_ents_, e0 + ebound_all);
+        if (out_created_.size() < g0 + nb) grow_to(out_created_, g0 + nb);
+        out_offs_[0] = 0;
     }
     // one chunk of the pipelined merge (merge_pools' chunk body, offsets
     // from the pools' running counts instead of a global prefix)
@@ -1098,9 +1188,12 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                 out_groups.ents[ek + k] = e;
                 newly[n0 + (ek - e0) + k] = e.first;
                 sel[e.first] = 1;
+                if (fill) out_ents_[ek + k] = mm_entry_ref{tk_ptr_[e.first], e.second, 0};
             }
+            if (fill) out_created_[gk] = created_[T];  // the group's searching ticket (its last entry)
             ek += r.len;
             out_groups.off[++gk] = (uint32_t)ek;
+            if (fill) out_offs_[gk] = (int32_t)ek;
         }
     };
     std::vector<double> task_ms(ntask, 0.0);
@@ -1187,9 +1280,11 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     const auto tg1 = clk::now();
     stats.par_gather_ms += msd(tg0, tg1);
     if (pipe) {
-        wp.run(ntask + nch, [&](size_t t) {
+        const size_t ngt = gpipe ? ntask_g : 0;
+        wp.run(ntask + ngt + nch, [&](size_t t) {
             if (t < ntask) worker(t);
-            else merge_chunk(t - ntask);
+            else if (t < ntask + ngt) gather_piece(t - ntask);
+            else merge_chunk(t - ntask - ngt);
         });
         size_t G = 0, E = 0, X = 0;  // totals: the pools' sentinels
         for (size_t gi = 0; gi < ng; gi++) {
@@ -1202,12 +1297,14 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         out_groups.ents.resize(e0 + E);
         expired.resize(x0 + X);
         newly.resize(n0 + E);
+        if (fill) filled_groups_ = g0 + G;
     } else {
         wp.run(ntask, worker);
     }
     const auto tg2 = clk::now();
     stats.par_job_ms += msd(tg1, tg2);
-    wp.run(ntask_g, [&](size_t t) {
+    if (id_broken.load()) throw std::runtime_error("pool replay: a row was not at its list position");
+    if (!gpipe) wp.run(ntask_g, [&](size_t t) {
         for (uint32_t gi : dense_ids) {
             const DensePool& D = dense_pools_[gi];
             uint32_t lo, hi;
@@ -1413,6 +1510,7 @@ void Core::choose_source(const Sig& s, DGroup& g, SrcChoice* ch) {
 int Core::process_default(GroupList& out_groups,
                           std::vector<uint32_t>& expired, PassStats& stats) {
     const uint32_t N = (uint32_t)nslots();
+    filled_groups_ = 0;
     std::vector<uint8_t>& sel = sel_;
     sel.assign(N, 0);
     std::vector<uint8_t>& dec = dec_;  // rows decided ahead of `pos` by a partial parallel replay
@@ -1780,6 +1878,7 @@ int Core::process_default(GroupList& out_groups,
         }
     }
     if (out_of_order) {
+        filled_groups_ = 0;  // the early-filled result entries are in the old order
         // back into the pinned row order: a group's searching ticket (its last
         // entry) is the row that formed it
         const size_t ng = out_groups.size();
@@ -2249,6 +2348,81 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
                      expired.size(), f_ms(f0, f1), f_ms(f1, f2), f_ms(f2 > f0 ? f2 : f0, fclk::now()));
 }
 
+// finish_pass(expired, groups, true) + fill_matched(groups, out, false) for
+// the common large processDefault pass — no group lost a ticket, no session or
+// party holds two tickets, the output arena is free — in two parallel sweeps:
+// the completeness re-check (matchmaker.go:326-343) over every group, then
+// per chunk of groups the result entries and the retirement of their tickets
+// (groups are disjoint, so the sweeps see the state the serial loop would).
+// Returns false, having changed nothing but the expired tickets' active flags
+// (finish_pass sets them again), when a condition fails.
+bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& groups, mm_matched* out) {
+    const size_t ng = groups.size(), ne = groups.ents.size();
+    if (!par_mode_ || ng < par_min(16384) || !sess_slots_.more.empty() || !party_slots_.more.empty()) return false;
+    if (!arena_claimed_ && out_in_use_.exchange(true)) return false;  // a second outstanding result: fill_matched copies
+    arena_claimed_ = true;
+    const bool filled = filled_groups_ == ng;  // the pipelined merge wrote the result entries
+    WorkPool& wp = workers();
+    const size_t nch = (size_t)wp.size() * 2;
+    std::vector<uint8_t> bad(nch, 0);
+    const size_t nx = expired.size();
+    wp.run(nch, [&](size_t c) {
+        for (size_t i = nx * c / nch; i < nx * (c + 1) / nch; i++) is_active_[expired[i]] = 0;
+        for (size_t g = ng * c / nch; g < ng * (c + 1) / nch && !bad[c]; g++)
+            for (const auto* e = groups.begin(g); e != groups.end(g); ++e)
+                if (e->first == kNoSlot || !live_[e->first]) { bad[c] = 1; break; }
+    });
+    for (uint8_t b : bad)
+        if (b) return false;  // fill_matched, on the claimed arena, after finish_pass's re-check
+    if (out_offs_.size() < ng + 1) grow_to(out_offs_, ng + 1);
+    if (out_ents_.size() < std::max<size_t>(ne, 1)) grow_to(out_ents_, std::max<size_t>(ne, 1));
+    if (out_created_.size() < std::max<size_t>(ng, 1)) grow_to(out_created_, std::max<size_t>(ng, 1));
+    int32_t* offs = out_offs_.data();
+    mm_entry_ref* ents = out_ents_.data();
+    int64_t* gc = out_created_.data();
+    std::vector<uint32_t> killed(nch, 0);
+    std::vector<std::vector<std::string>> gone(track_removed_ ? nch : 0);
+    wp.run(nch, [&](size_t c) {
+        const size_t g0 = ng * c / nch, g1 = ng * (c + 1) / nch;
+        uint32_t k = 0;
+        if (!filled) {
+            for (size_t g = g0; g < g1; g++) {
+                offs[g] = (int32_t)groups.off[g];
+                gc[g] = groups.len(g) ? created_[groups.end(g)[-1].first] : 0;
+            }
+            if (c + 1 == nch) offs[ng] = (int32_t)groups.off[ng];
+        }
+        for (size_t i = groups.off[g0]; i < groups.off[g1]; i++) {
+            const uint32_t s = groups.ents[i].first;
+            if (!filled) {
+                ents[i].ticket = tk_ptr_[s];
+                ents[i].presence_index = groups.ents[i].second;
+                ents[i].reserved = 0;
+            }
+            if (!live_[s]) continue;  // a ticket's presence entries repeat its slot
+            if (track_removed_) gone[c].emplace_back(tk(s));
+            live_[s] = 0;  // retired: sessionTickets / partyTickets read live_ (SlotSets)
+            is_active_[s] = 0;
+            k++;
+        }
+        killed[c] = k;
+    });
+    for (uint32_t k : killed) n_live_ -= k;
+    for (auto& v : gone) removed_ids_.insert(removed_ids_.end(), v.begin(), v.end());
+    filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, list_tmp_,
+                 [&](uint32_t s) { return live_[s] && is_active_[s]; });
+    active_list_.swap(list_tmp_);
+    out->group_created = gc;
+    out->n_groups = (int32_t)ng;
+    out->n_entries = (int32_t)ne;
+    out->group_offsets = offs;
+    out->entries = ents;
+    out->is_candidates = 0;
+    out->reserved2 = 1;  // the handle's arena (out_in_use_ until mm_free_matched)
+    arena_claimed_ = false;
+    return true;
+}
+
 void Core::finish_pass_serial(GroupList& groups, bool selected) {
     std::vector<uint32_t> order(groups.size());
     for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
@@ -2285,7 +2459,8 @@ void Core::fill_matched(const GroupList& groups, mm_matched* out,
     // store's ticket-string arena, which does not move while the result is
     // outstanding (compaction waits for mm_free_matched).  A second
     // outstanding result gets private copies.
-    const bool arena = !out_in_use_.exchange(true);
+    const bool arena = arena_claimed_ || !out_in_use_.exchange(true);
+    arena_claimed_ = false;
     int32_t* offs;
     mm_entry_ref* ents;
     char* buf = nullptr;
@@ -2378,6 +2553,10 @@ int Core::process(mm_matched* out) {
     std::unique_lock<std::mutex> pl(process_mu_);
     std::unique_lock<std::mutex> lk(mu_);
     if (custom_open_) return MM_ERR_STATE;
+    if (arena_claimed_) {  // an earlier pass that claimed the arena failed before handing it out
+        arena_claimed_ = false;
+        out_in_use_.store(false);
+    }
     bool any_active = false;
     for (uint32_t s : active_list_)
         if (live_[s] && is_active_[s]) { any_active = true; break; }
@@ -2440,10 +2619,11 @@ int Core::process(mm_matched* out) {
         lk.lock();  // matchmaker.go:320
         out->n_expired = (int32_t)expired.size();
         apply_pending();
-        finish_pass(expired, groups, true);
+        const bool fused = finish_fill_fast(expired, groups, out);
+        if (!fused) finish_pass(expired, groups, true);
         pass_running_ = false;
         const auto t3 = std::chrono::steady_clock::now();
-        fill_matched(groups, out, false);
+        if (!fused) fill_matched(groups, out, false);
         const auto t4 = std::chrono::steady_clock::now();
         if (std::getenv("NKM_PROFILE")) {
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };

@@ -102,6 +102,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     NKM_HIP(hipEventCreateWithFlags(&apply_ev_, hipEventDisableTiming));
     if (const char* e = std::getenv("NKM_DENSE")) dense_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_PIPE")) pipe_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_GPIPE")) gpipe_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FAST")) fast_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FULLVAR")) full_var_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_SLOTLISTS")) {
@@ -563,6 +564,7 @@ int Core::add_locked(const mm_ticket& t, uint32_t sg, bool from_insert) {
     maxc_.push_back(t.max_count);
     cm_.push_back(t.count_multiple);
     count_.push_back(t.n_presences);
+    max_pres_ = std::max(max_pres_, t.n_presences);
     intervals_.push_back(from_insert ? t.intervals : 0);
     const std::string_view pid = S(t.party_id);
     const uint32_t party = pid.empty() ? kNoParty : party_dict_.intern(pid);
@@ -609,6 +611,8 @@ int Core::add_locked(const mm_ticket& t, uint32_t sg, bool from_insert) {
     // tickets then share their pool's search (sig: the caller's sig_of with
     // kNoParty).
     sig_.push_back(sg);
+    self_match_.push_back(self_match_of(s));
+    if (s > 0) monotone_ = monotone_ && created_[s] > created_[s - 1] && ckey_[s] > ckey_[s - 1];
     squery_.push_back(DQuery{sigs_[sg].clause_off, sigs_[sg].n_clauses, sigs_[sg].qkind, 0});
     slot_of_.put(th, s, [&](uint32_t v) { return tk(v) == tkv; });
     n_live_++;
@@ -626,6 +630,13 @@ int Core::add_locked(const mm_ticket& t, uint32_t sg, bool from_insert) {
     order_.push_back(s);
     index_dirty_ = true;
     return MM_OK;
+}
+
+uint8_t Core::self_match_of(uint32_t s) const {
+    for (auto& mt : sigs_[sig_[s]].must_terms)
+        if (fkind_[mt.first].size() <= s || fkind_[mt.first][s] != KIND_KEYWORD || (uint32_t)fval_[mt.first][s] != mt.second)
+            return 0;
+    return 1;
 }
 
 // sig_of through the (query text, MinCount, MaxCount) cache.  The cache is
@@ -1161,6 +1172,7 @@ void Core::compact() {
     cold_.compact(live_);
     keep(tk_ptr_); keep(tk_len_); keep(tnode_); keep(created_); keep(ckey_); keep(minc_); keep(maxc_); keep(cm_);
     keep(count_); keep(intervals_); keep(party_); keep(is_active_); keep(sig_); keep(squery_); keep(indexed_);
+    keep(self_match_);
     for (size_t f = 0; f < fval_.size(); f++) {
         if (fval_[f].size() == n) { keep(fval_[f]); keep(fkind_[f]); }
     }
@@ -1226,6 +1238,8 @@ void Core::compact() {
     order_ = std::move(nord);
     pending_dead_.clear();
     apply_defer_.clear();  // old slot numbers; the re-upload below carries the flags
+    monotone_ = true;      // the live slots alone
+    for (uint32_t s = 1; s < m && monotone_; s++) monotone_ = created_[s] > created_[s - 1] && ckey_[s] > ckey_[s - 1];
     index_dirty_ = true;
     dev_slots_ = 0;
     for (auto& d : dev_field_slots_) d = 0;

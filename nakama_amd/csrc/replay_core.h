@@ -531,6 +531,15 @@ struct DensePool {
     const uint32_t* brow = nullptr;  // batch row -> slot
     std::vector<DenseRec> rec;
     std::vector<uint32_t> slot;
+    // identity: the pool's rows are its list, in list order (row j's ticket is
+    // position j — every pool member searches, batch order = scan order, as in
+    // a pool of fresh tickets): no slot -> position map is needed
+    bool identity = false;
+    // pipelined gather (identity pools): pieces [0, *front) of `pieces` are
+    // gathered; null: the whole list is gathered before the walk
+    const std::atomic<uint32_t>* front = nullptr;
+    uint32_t pieces = 1;
+    std::atomic<bool>* broken = nullptr;  // set when an identity row is not at its position
 
     void reset(const BGroup& g, const uint32_t* rows, uint32_t n_rows, const uint32_t* batch_slots) {
         sp = g.sp;
@@ -539,27 +548,49 @@ struct DensePool {
         bis = rows;
         nrows = n_rows;
         brow = batch_slots;
+        identity = false;
+        front = nullptr;
+        pieces = 1;
+        broken = nullptr;
         if (rec.size() < n) rec.resize(n);
         if (slot.size() < n) slot.resize(n);
     }
-    // positions [lo, hi): records, slots, and pos_of[slot] = position
+    uint32_t piece_lo(uint32_t t) const { return t >= pieces ? n : (uint32_t)((uint64_t)n * t / pieces); }
+    // the gathered bound once position i (< n) is gathered (spins meanwhile)
+    uint32_t wait_pos(uint32_t i) const {
+        for (;;) {
+            const uint32_t f = front->load(std::memory_order_acquire);
+            const uint32_t a = piece_lo(f);
+            if (i < a) return a;
+            __builtin_ia32_pause();
+        }
+    }
+    // does row j's ticket sit at list position j for every row? (positions [lo, hi))
+    bool rows_are_list(uint32_t lo, uint32_t hi) const {
+        for (uint32_t k = lo; k < hi; k++)
+            if (sp[(size_t)k * ss] != brow[bis[k]]) return false;
+        return true;
+    }
+    // positions [lo, hi): records, slots, and (unless identity) pos_of[slot] = position
     void gather(const ReplayView& v, uint32_t lo, uint32_t hi, uint32_t* pos_of) {
+        const bool map = !identity;
         for (uint32_t k = lo; k < hi; k++) {
             const uint32_t s = sp[(size_t)k * ss];
             if (k + 16 < hi) {
                 const uint32_t p = sp[(size_t)(k + 16) * ss];
                 __builtin_prefetch(&v.hot[p]);
                 __builtin_prefetch(&v.intervals[p]);
-                __builtin_prefetch(&pos_of[p], 1);
+                if (map) __builtin_prefetch(&pos_of[p], 1);
             }
             const HotRec& h = v.hot[s];
             rec[k] = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party, h.sess0, h.pres_off,
                               (uint32_t)v.intervals[s], h.smask};
             slot[k] = s;
-            pos_of[s] = k;
+            if (map) pos_of[s] = k;
         }
     }
     void clear_pos(uint32_t lo, uint32_t hi, uint32_t* pos_of) const {
+        if (identity) return;
         for (uint32_t k = lo; k < hi; k++) pos_of[slot[k]] = kNoSlot;
     }
 };
@@ -580,6 +611,21 @@ struct DenseRun {
     std::vector<std::pair<uint32_t, int>> grp;
     FastCombos fcb;
     bool fast = true;  // fast_step() for the rows it covers (NKM_FAST=0: step() only)
+    uint32_t avail = 0;  // positions known gathered (pipelined gather, DensePool::front)
+
+    // position i (< P.n) gathered before its copies are read
+    void need(const DensePool& P, uint32_t i) {
+        if (i >= avail) avail = P.wait_pos(i);
+    }
+    // the row's own position: j for an identity pool, else the gather's map
+    uint32_t pos_of_row(const DensePool& P, const uint32_t* pos_of, uint32_t j, uint32_t T) {
+        if (P.identity) {
+            need(P, j);
+            if (P.slot[j] != T && P.broken) P.broken->store(true);
+            return j;
+        }
+        return pos_of[T];
+    }
 
     void reset(uint32_t n) {
         sel.assign(n, 0);
@@ -597,7 +643,7 @@ struct DenseRun {
         const uint32_t n = P.n;
         const uint32_t bi = P.bis[j];
         const uint32_t T = P.brow[bi];
-        const uint32_t kT = pos_of[T];
+        const uint32_t kT = pos_of_row(P, pos_of, j, T);
         if (kT != kNoSlot && sel[kT]) return false;
         DenseRec rt;
         const uint32_t* tpres = v.pres_sess;
@@ -629,6 +675,7 @@ struct DenseRun {
         for (uint32_t i = head; i < n; i++) {
             hits_seen++;
             if (i == kT || sel[i]) continue;
+            need(P, i);
             const DenseRec& hh = P.rec[i];
             if (tparty != kNoParty && hh.party == tparty) continue;                      // :80-85
             if (tmax < hh.maxc && (int)hh.intervals + proc[i] <= max_intervals) continue;  // :150-153
@@ -681,8 +728,11 @@ struct DenseRun {
             bool form = l == tmax;
             if (!form && last && l >= tmin && l <= tmax) {
                 bool more = false;  // an unselected, non-self, non-party hit after i (:130, :233)
-                for (uint32_t q = i + 1; q < n && !more; q++)
-                    more = q != kT && !sel[q] && !(tparty != kNoParty && P.rec[q].party == tparty);
+                for (uint32_t q = i + 1; q < n && !more; q++) {
+                    if (q == kT || sel[q]) continue;
+                    need(P, q);
+                    more = !(tparty != kNoParty && P.rec[q].party == tparty);
+                }
                 form = !more;
             }
             if (!form) continue;
@@ -749,7 +799,7 @@ struct DenseRun {
         const uint32_t n = P.n;
         const uint32_t bi = P.bis[j];
         const uint32_t T = P.brow[bi];
-        const uint32_t kT = pos_of[T];
+        const uint32_t kT = pos_of_row(P, pos_of, j, T);
         if (kT != kNoSlot && sel[kT]) return 0;
         int32_t tcount, tmin, tmax, tcm;
         uint32_t tparty, tivl;
@@ -768,6 +818,7 @@ struct DenseRun {
         for (uint32_t i = head; i < n; i++) {
             hits_seen++;
             if (i == kT || sel[i]) continue;
+            need(P, i);
             const DenseRec& hh = P.rec[i];
             if (tparty != kNoParty && hh.party == tparty) continue;                      // :80-85
             if (tmax < hh.maxc && (int)hh.intervals + proc[i] <= max_intervals) continue;  // :150-153
@@ -788,8 +839,11 @@ struct DenseRun {
             bool form = l == tmax;  // :233
             if (!form && last && l >= tmin && l <= tmax) {
                 bool more = false;
-                for (uint32_t q = i + 1; q < n && !more; q++)
-                    more = q != kT && !sel[q] && !(tparty != kNoParty && P.rec[q].party == tparty);
+                for (uint32_t q = i + 1; q < n && !more; q++) {
+                    if (q == kT || sel[q]) continue;
+                    need(P, q);
+                    more = !(tparty != kNoParty && P.rec[q].party == tparty);
+                }
                 form = !more;
             }
             if (!form) continue;
@@ -825,6 +879,7 @@ struct DenseRun {
 
     void walk(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of, uint32_t j0,
               uint32_t j1) {
+        avail = P.front ? 0 : P.n;
         const bool f = fast && v.sessions_exclusive;
         for (uint32_t j = j0; j < j1; j++)
             if (!f || fast_step(P, v, max_intervals, pos_of, j) == 2) step(P, v, max_intervals, pos_of, j);
@@ -837,6 +892,7 @@ struct DenseRun {
     void walk_published(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of,
                         std::atomic<uint64_t>* progress) {
         constexpr uint32_t kPublish = 512;
+        avail = P.front ? 0 : P.n;
         const bool f = fast && v.sessions_exclusive;
         for (uint32_t j = 0; j < P.nrows; j++) {
             if (!f || fast_step(P, v, max_intervals, pos_of, j) == 2) step(P, v, max_intervals, pos_of, j);

@@ -85,8 +85,9 @@ def test_full_size_pass_equals_oracle(name):
     _check(name)
 
 
-@pytest.mark.parametrize("env", [{"NKM_PIPE": "0"}, {"NKM_FAST": "0"}, {"NKM_DENSE": "0"}, {"NKM_KERNEL": "scan"}],
-                         ids=["nopipe", "exact-walk", "generic-walk", "scan-kernel"])
+@pytest.mark.parametrize("env", [{"NKM_PIPE": "0"}, {"NKM_GPIPE": "0"}, {"NKM_FAST": "0"}, {"NKM_DENSE": "0"},
+                                 {"NKM_KERNEL": "scan"}, {"NKM_THREADS": "4"}],
+                         ids=["nopipe", "gather-first", "exact-walk", "generic-walk", "scan-kernel", "4-threads"])
 def test_full_size_c3_host_paths(env, monkeypatch):
     """C3 at 1M through the other host replay paths and the chunked scan."""
     for k, v in env.items():
