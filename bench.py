@@ -50,12 +50,19 @@ WORKLOADS = {
     4: "C4: solo 1v1, 4M tickets over 64 mode x region pools (in total)",
     5: "C5: RevPrecision, buckets of 8, Min=2 Max=4, 1M in total",
     7: "C7: regexp / wildcard / fuzzy clauses (blocked lists, alternations, fuzzy map names)",
+    11: "C5 with buckets of 64 (63 filtered hits per row: processCustom's combineIndexes hands over no candidate, "
+        "matchmaker_process.go:588), RevPrecision, Min=2 Max=4, 1M in total",
 }
 # the query fields a pool is keyed on (the cluster front's routing)
 POOL_FIELDS = {1: ("properties.mode", "properties.region"), 3: ("properties.mode", "properties.region"),
-               4: ("properties.mode", "properties.region"), 5: ("properties.bucket",)}
+               4: ("properties.mode", "properties.region"), 5: ("properties.bucket",), 11: ("properties.bucket",)}
 DEFAULT_TICKETS = {4: 4_000_000}  # C4 is quoted on 4M in total; the others on 1M (per GPU for C3)
-STRONG = (4, 5)                   # configs whose ticket count is the whole job's
+STRONG = (4, 5, 11)               # configs whose ticket count is the whole job's
+REV = (5, 11)                     # RevPrecision configs
+# full oracle passes measured offline (tools/make_full_golden.py: every pool's
+# whole pass, pools concurrently), the calibration of the live extrapolations
+FULL_CPU = {3: os.path.join(ROOT, "profiles", "r03_cpu_full_c3.json"),
+            4: os.path.join(ROOT, "profiles", "r03_cpu_full_c4.json")}
 
 
 def parse():
@@ -140,54 +147,44 @@ def host_info():
     return model, os.cpu_count(), usable
 
 
-def cpu_baseline(args, n_pools, searches, matched):
-    """The reference Go/bluge path cannot run here (no Go toolchain; SURVEY
-    §8(c)), so the baseline is the oracle restatement (oracle/mm_oracle.cpp:
-    the reference's per-row search + full sort + greedy walk), timed on this
-    host as BASELINE.md prescribes for C3: a prefix of the 1M-ticket pass (the
-    first --cpu-rows rows active, every row a full search of the 1M index),
-    extrapolated to the whole pass with the sum of c * P * log2 P over its
-    searches, P = the searching ticket's remaining pool (pools shrink linearly
-    as the pass consumes them; the search and group counts are the measured
-    pass's, identical to the reference's).  All-cores figure: pools are
-    independent, so per-pool passes run in parallel, ideally balanced over
-    min(pools, cores).  Both figures are EXTRAPOLATED, labelled so."""
-    from nakama_amd import capi, synth
-    lib = capi.load_library(os.path.join(ROOT, "oracle", "liboracle_mm.so"))
-    ts = synth.TicketSet(args.config, args.tickets, first=0)
-    for k in range(args.cpu_rows, ts.n):
-        ts.tickets[k].intervals = 2
-    mm = capi.Matchmaker(lib, max_intervals=2, rev_precision=args.config == 5, rev_threshold=0)
-    try:
-        ts.insert_into(mm)
-        t0 = time.perf_counter()
-        r = mm.process_raw()
-        dt = time.perf_counter() - t0
-        pre_matched = sum(len({t for t, _ in g}) for g in r.groups)
-    finally:
-        mm.close()
-        ts.close()
-    p0 = args.tickets / n_pools
-    c = (dt / args.cpu_rows) / (p0 * math.log2(p0))
-    per_pool_s, per_pool_m = searches / n_pools, matched / n_pools
-    steps = max(1, int(round(per_pool_s)))
-    total = 0.0
-    for k in range(steps):  # one pool's searches, pool shrinking linearly
-        p = max(2.0, p0 - per_pool_m * k / steps)
-        total += c * p * math.log2(p)
-    total *= per_pool_s / steps * n_pools
-    model, ncpu, usable = host_info()
-    par = min(n_pools, usable)
-    return {"value": matched / total, "unit": "tickets/s", "cores": 1, "kind": "port",
-            "sample": (f"EXTRAPOLATED: oracle prefix of the {args.tickets}-ticket config-{args.config} pass "
-                       f"({args.cpu_rows} searches over the full index, {dt:.2f} s, {pre_matched} tickets matched) "
-                       f"scaled by sum(c*P*log2 P) over the pass's {searches} searches in {n_pools} shrinking "
-                       f"pools -> {total:.0f} s for {matched} matched tickets on one core"),
-            "all_cores": {"value": matched / (total / par), "cores": par,
-                          "note": f"per-pool passes in parallel, ideal balance over min({n_pools} pools, "
-                                  f"{usable} usable cores)"},
-            "host": {"cpu_model": model, "nproc": ncpu, "usable_cores": usable},
-            "prefix_s": dt, "extrapolated_pass_s": total}
+def cpu_baseline(args, searches, matched):
+    """The oracle restatement of the reference's pass on this host's cores
+    (the reference Go/bluge path cannot run: no Go toolchain),
+    bounded to ~10-30 s of CPU: tools/cpu_baseline.py in a child process
+    (this process has initialised the GPU; the child never touches it).
+    `value`: per-pool passes on one core — the cost class of bluge's
+    posting-driven search, each search visiting its own pool — timed as
+    concurrent prefixes of every pool and extrapolated (EXTRAPOLATED);
+    `all_cores`: the same pools on all cores concurrently; `full_index`: one
+    core scanning the whole index per search, the oracle's own algorithm
+    class (a lower bound on the reference); `measured_full_pass`: whole
+    per-pool oracle passes measured offline (not extrapolated) on the named
+    CPU, for calibration."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "cpu_baseline.py"), "--config", str(args.config),
+           "--tickets", str(args.tickets), "--searches", str(searches), "--matched", str(matched)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"value": None, "unit": "tickets/s", "cores": 1, "kind": "port",
+                "sample": "cpu_baseline.py failed: " + r.stderr[-300:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    fi = d["full_index"]
+    if "per_pool" in d:
+        pp = d["per_pool"]
+        out = {"value": pp["value_one_core"], "unit": "tickets/s", "cores": 1, "kind": "port",
+               "sample": pp["sample"] + f"; one-core time {pp['sum_pool_pass_s']:.0f} s",
+               "all_cores": {"value": pp["value_all_cores"], "cores": pp["cores"],
+                             "note": f"the slowest pool's extrapolated pass, {pp['parallel_pass_s']:.0f} s; timed "
+                                     f"concurrently ({pp['timed_wall_s']:.1f} s of wall)"}}
+    else:
+        out = {"value": fi["value"], "unit": "tickets/s", "cores": 1, "kind": "port", "sample": fi["sample"]}
+    out["full_index"] = {"value": fi["value"], "cores": 1, "sample": fi["sample"]}
+    out["algorithm"] = d["algorithm"]
+    out["host"] = d["host"]
+    full = FULL_CPU.get(args.config)
+    if full and os.path.exists(full) and args.tickets == json.load(open(full)).get("tickets"):
+        out["measured_full_pass"] = json.load(open(full))
+    return out
 
 
 def make_set(args, world, rank, step):
@@ -212,7 +209,7 @@ def main():
 
     # SURVEY 8(d) harness pins: MaxIntervals=2, RevThreshold=0 (no wall-clock cutoff)
     from nakama_amd import synth
-    mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config == 5, rev_threshold=0,
+    mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config in REV, rev_threshold=0,
                                     override=(lambda groups: groups) if args.override else None)
     cm = None
     if world > 1:
@@ -221,7 +218,7 @@ def main():
                                        comm_device=torch.device("cuda", local) if backend == "nccl" else None,
                                        override_commit=synth.override_commit if args.override else None)
     times, matched_all, presences_all, ins_times, searched = [], [], [], [], []
-    eval_ms = eval_bytes = launches = 0
+    eval_ms = eval_bytes = launches = pair_evals = cands = 0
     batches, kernels, unroutable = [], set(), 0
     breakdown = {"local_call_ms": [], "summary_ms": [], "merge_ms": []}  # rank 0's cluster-pass phases
     for step in range(args.warmup + args.steps):
@@ -236,6 +233,8 @@ def main():
         t0 = time.perf_counter()
         if cm is None:
             out = mm.process_call()  # the C-ABI call: one whole Process() pass
+            n_cands = out.n_groups if out.is_candidates else 0
+            cand_pe = out.pair_evals
             if args.override and out.is_candidates:  # processCustom: override + commit, in the timed step
                 out = synth.override_commit(mm, out)
         else:
@@ -245,7 +244,8 @@ def main():
         if cm is None:
             n_groups, matched, pres, r = mm.process_summary(out)  # untimed: counts the groups, frees them
             st = {"eval_ms": r.eval_ms, "eval_bytes": r.eval_bytes, "eval_launches": r.eval_launches,
-                  "n_batches": r.n_batches, "eval_kernel": r.eval_kernel}
+                  "n_batches": r.n_batches, "eval_kernel": r.eval_kernel,
+                  "pair_evals": cand_pe if args.override else r.pair_evals, "candidates": n_cands}
         else:
             n_groups, matched, pres = cp.n_groups, cp.matched_tickets, cp.matched_presences
             st = cp.local_stats
@@ -264,6 +264,8 @@ def main():
             eval_ms += st["eval_ms"]
             eval_bytes += st["eval_bytes"]
             launches += st["eval_launches"]
+            pair_evals += st.get("pair_evals", 0)
+            cands += st.get("candidates", 0)
             batches.append(st["n_batches"])
             kernels.add(KERNELS.get(st["eval_kernel"], str(st["eval_kernel"])))
         # drain what is left so the next step starts from a fresh set
@@ -302,6 +304,9 @@ def main():
         "ms_per_step": 1e3 * total_t / args.steps,
         "p50_ms": 1e3 * statistics.median(times),
         "presences_per_s": sum(presences_all) / total_t,
+        # (row, candidate) predicate evaluations the pass's searches issued
+        # (BASELINE.md GPU-side reporting), per second of the timed steps
+        "pair_evals_per_s": pair_evals / total_t,
         # the host-to-HBM hand-over: the Insert() call that precedes each pass
         # (not part of value: inputs are resident when the timed region starts)
         "insert_ms": 1e3 * statistics.median(ins_times),
@@ -314,10 +319,11 @@ def main():
         "config": {"workload": WORKLOADS.get(args.config, str(args.config)) +
                                (" + MatchmakerOverride (processCustom candidates, native first-disjoint override, "
                                 "mm_process_commit)" if args.override else
-                                " (processDefault: no override registered)" if args.config == 5 else ""),
+                                " (processDefault: no override registered)" if args.config in REV else ""),
                    ("tickets_total" if strong else "tickets_per_gpu"): args.tickets,
                    "max_intervals": 2, "parallelism": par, "unroutable": unroutable,
                    "matched_per_step": sum(matched_all) / args.steps, "batches_per_pass_rank0": batches,
+                   "candidates_per_pass": (cands / args.steps) if args.override else None,
                    "cluster_phases_ms_rank0": ({k: statistics.median(v) for k, v in breakdown.items()}
                                                if cm is not None else None)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -325,9 +331,8 @@ def main():
                      "kernel": "+".join(sorted(kernels)), "launches": launches, "avg_launch_ms": avg_launch_ms,
                      "bytes_per_launch": eval_bytes / max(1, launches), "rank": 0},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 3:
-        cb = cpu_baseline(args, 8, int(statistics.median(searched)), int(statistics.median(matched_all)))
-        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "all_cores", "host")}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in (3, 4, 5) and not args.override:
+        out["cpu_baseline"] = cpu_baseline(args, int(statistics.median(searched)), int(statistics.median(matched_all)))
     else:
         out["cpu_baseline"] = None
     mm.close()

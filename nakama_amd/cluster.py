@@ -265,8 +265,17 @@ class ClusterMatchmaker:
         import time
         t0 = time.perf_counter()
         out = self.local.process_call()
+        err = None
         if out.is_candidates:  # processCustom: this rank's override hand-off
-            out = self._override(out)
+            out, err = self._override(out)
+        if self.local.override is not None or self.override_commit is not None:
+            # an override that raised on any rank fails the pass on every rank
+            # (every rank takes part, with or without candidates of its own)
+            flag = self._t(np.array([1 if err is not None else 0], dtype=np.int32))
+            self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX)
+            if int(self._host(flag)[0]):
+                self.local.lib.mm_free_matched(self.local.h, C.byref(out))
+                raise err if err is not None else RuntimeError("MatchmakerOverride failed on another rank")
         t1 = time.perf_counter()
         try:
             ng = out.n_groups
@@ -296,9 +305,20 @@ class ClusterMatchmaker:
             ties = router_lib().mm_merge_positions(allk.ctypes.data, counts.ctypes.data, self.world, self.rank,
                                                    pos.ctypes.data)
             cp.positions = pos[:ng]
+            # mm_merge_positions needs every rank's keys ascending: processDefault's
+            # groups are, an override's choice need not be (it may reorder):
+            # then the groups take a stable global order by (key, rank, index)
+            bounds = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+            ascending = all(np.all(np.diff(allk[bounds[r]:bounds[r + 1]]) >= 0) for r in range(self.world))
+            if not ascending:
+                order = np.lexsort((np.arange(len(allk)), np.repeat(np.arange(self.world), counts), allk))
+                glob = np.empty(len(allk), dtype=np.int64)
+                glob[order] = np.arange(len(allk))
+                cp.positions = glob[bounds[self.rank]:bounds[self.rank + 1]]
+                ties = 0
             flag = self._t(np.array([ties], dtype=np.int32))
             self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX)
-            if int(self._host(flag)[0]):  # rare: the searching tickets' ids order the tied groups
+            if int(self._host(flag)[0]) and ascending:  # rare: the searching tickets' ids order the tied groups
                 offs = out.group_offsets
                 tie_ids = [out.entries[offs[g + 1] - 1].ticket.decode() for g in range(ng)]
                 self._order_ties(cp, allk, counts, tie_ids)
@@ -312,14 +332,29 @@ class ClusterMatchmaker:
         return cp
 
     def _override(self, out):
-        if self.override_commit is not None:
-            return self.override_commit(self.local, out)
+        """This rank's override hand-off -> (committed result, error).  An
+        override that raises must not leave the pass open (later passes would
+        fail with MM_ERR_STATE while the other ranks wait in the next
+        collective): the candidates are committed as an empty choice, and
+        Process tells every rank of the failure in one all-reduce."""
+        err = None
         try:
-            cands = capi.Matchmaker._groups(out)
-        finally:
-            self.local.lib.mm_free_matched(self.local.h, C.byref(out))
-        chosen = self.local.override(cands) if self.local.override is not None else []
-        return self.local.commit_call(chosen)
+            if self.override_commit is not None:
+                res = self.override_commit(self.local, out)
+            else:
+                try:
+                    cands = capi.Matchmaker._groups(out)
+                finally:
+                    self.local.lib.mm_free_matched(self.local.h, C.byref(out))
+                chosen = self.local.override(cands) if self.local.override is not None else []
+                res = self.local.commit_call(chosen)
+        except Exception as e:  # close the pass with an empty choice
+            err = e
+            res = capi.mm_matched()
+            rc = self.local.lib.mm_process_commit(self.local.h, None, None, 0, C.byref(res))
+            if rc != capi.MM_OK:
+                res = capi.mm_matched()
+        return res, err
 
     def _order_ties(self, cp: ClusterPass, allk: np.ndarray, counts: np.ndarray, tie_ids):
         """Equal CreatedAt on two ranks: those groups are ordered by their
@@ -366,10 +401,111 @@ class ClusterMatchmaker:
             return None
         return sorted((t for ts in gathered for t in ts), key=lambda t: t.ticket)
 
-    def Remove(self, tickets: Sequence[str]):
-        """Remove (matchmaker.go:972-1024): ids may live on any rank; every
-        rank removes the ones it holds (the others are no-ops there)."""
-        self.local.Remove(list(tickets))
+    # Mutators.  Every rank calls each of them (a collective), passing its own
+    # request or None; the requests of all ranks are gathered and applied on
+    # every rank in rank order — the rank holding a ticket removes it, the
+    # others find nothing — so a caller may name a ticket that lives on any rank.
+    def _gather(self, req):
+        gathered = [None] * self.world
+        self.dist.all_gather_object(gathered, req)
+        return gathered
+
+    def _targeted(self, fn, req) -> Optional[Exception]:
+        """fn(local, *args) for every rank's request on every rank; a request
+        succeeds when the rank holding its ticket succeeds.  Returns this
+        rank's error (None: success or no request)."""
+        reqs = self._gather(req)
+        ok = np.zeros(self.world, dtype=np.int32)
+        for r, q in enumerate(reqs):
+            if q is None:
+                continue
+            try:
+                fn(self.local, *q)
+                ok[r] = 1
+            except capi.ErrMatchmakerTicketNotFound:
+                pass
+        t = self._t(ok)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        if req is not None and not int(self._host(t)[self.rank]):
+            return capi.ErrMatchmakerTicketNotFound(req[-1])
+        return None
+
+    def Remove(self, tickets: Optional[Sequence[str]]):
+        """Remove (matchmaker.go:972-1024) of ids that may live on any rank."""
+        ids = [t for ts in self._gather(list(tickets or [])) for t in ts]
+        if ids:
+            self.local.Remove(ids)
+
+    def RemoveSession(self, session_id: Optional[str], ticket: Optional[str] = None):
+        """RemoveSession (matchmaker.go:725-767); ErrMatchmakerTicketNotFound
+        unless the rank holding the ticket removed it."""
+        err = self._targeted(lambda m, sid, tk: m.RemoveSession(sid, tk),
+                             None if session_id is None else (session_id, ticket))
+        if err is not None:
+            raise err
+
+    def RemoveParty(self, party_id: Optional[str], ticket: Optional[str] = None):
+        """RemoveParty (matchmaker.go:830-870)."""
+        err = self._targeted(lambda m, pid, tk: m.RemoveParty(pid, tk), None if party_id is None else (party_id, ticket))
+        if err is not None:
+            raise err
+
+    def RemoveSessionAll(self, session_id: Optional[str]):
+        """RemoveSessionAll (matchmaker.go:769-828): one session's tickets on every rank."""
+        for sid in self._gather(session_id):
+            if sid is not None:
+                self.local.RemoveSessionAll(sid)
+
+    def RemovePartyAll(self, party_id: Optional[str]):
+        """RemovePartyAll (matchmaker.go:872-917)."""
+        for pid in self._gather(party_id):
+            if pid is not None:
+                self.local.RemovePartyAll(pid)
+
+    def RemoveAll(self, node: Optional[str]):
+        """RemoveAll (matchmaker.go:919-970)."""
+        for nd in self._gather(node):
+            if nd is not None:
+                self.local.RemoveAll(nd)
+
+    def Add(self, ticket: Optional[capi.Ticket]) -> Optional[Exception]:
+        """Add (matchmaker.go:443-565) of this rank's ticket (or None), routed
+        to its pool's rank (a new pool goes to the least-loaded rank).
+        Returns the caller's error (None: added).  MaxTickets is checked by
+        the owning rank's handle against the tickets it holds: a session
+        whose tickets sit in pools of different ranks is limited per rank.
+        The exact node-wide check is the in-process front's (mm_create_multi,
+        include/nakama_cluster.h), the handle a Go server drives."""
+        reqs = self._gather(ticket)
+        mine = capi._TicketPack([ticket] if ticket is not None else [])
+        self._place_new_pools(route_keys(mine.arr, 1 if ticket is not None else 0, self.pool_fields))
+        pack = capi._TicketPack([t for t in reqs if t is not None])
+        keys = route_keys(pack.arr, sum(t is not None for t in reqs), self.pool_fields)
+        own = self.owners(keys)
+        err = None
+        k = 0
+        for r, t in enumerate(reqs):
+            if t is None:
+                continue
+            e = None
+            if own[k] < 0:
+                e = capi.ErrMatchmakerUnsupportedQuery("query does not pin every pool field to the ticket's own value")
+            elif own[k] == self.rank:
+                try:
+                    self.local.Add(t.presences, t.session_id, t.party_id, t.query, t.min_count, t.max_count,
+                                   t.count_multiple, t.string_properties, t.numeric_properties, ticket=t.ticket,
+                                   created_at=t.created_at)
+                except capi.MatchmakerError as x:
+                    e = x
+            codes = [None] * self.world
+            self.dist.all_gather_object(codes, None if e is None else (type(e).__name__, str(e)) if own[k] == self.rank or own[k] < 0 else None)
+            src = own[k] if own[k] >= 0 else r
+            got = codes[src]
+            if r == self.rank and got is not None:
+                cls = getattr(capi, got[0], capi.MatchmakerError)
+                err = cls(got[1])
+            k += 1
+        return err
 
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64))

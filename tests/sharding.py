@@ -1,4 +1,6 @@
-"""Pool sharding for one-process-per-GPU runs.
+"""Pool sharding helpers of the gloo multi-rank tests (tests/test_distributed.py):
+the static form of what the product's fronts do online (nakama_amd/cluster.py
+places pools over ranks, mm_create_multi over devices).
 
 A pool is the set of tickets whose queries all require the same keyword term
 on the pool-key fields (e.g. mode x region).  A ticket can only ever be

@@ -301,3 +301,192 @@ def test_cluster_gpu_pass_equals_single_oracle_pass(config, n, groups, passes):
     for (merged, state, active, ng, matched), (g, st, act) in zip(out, want):
         assert merged == g
         assert state == st and active == act
+
+
+# ---- mutators as collectives ----
+
+def _script(ts_all, k):
+    """The scripted mutations: (issuing rank, op, args) over tickets of the
+    whole set — each names a ticket that may live on either rank."""
+    t = [ts_all.tickets[i] for i in range(ts_all.n)]
+    tid = lambda i: t[i].ticket.decode()
+    solo = [i for i in range(ts_all.n) if t[i].n_presences == 1]
+    party = [i for i in range(ts_all.n) if t[i].n_presences > 1]
+    s = [(0, "Remove", ([tid(i) for i in range(1, ts_all.n, 37)],)),
+         (1, "RemoveSession", (t[solo[3]].presences[0].session_id.decode(), tid(solo[3]))),
+         (0, "RemoveSession", (t[solo[7]].presences[0].session_id.decode(), tid(solo[7]))),
+         (1, "RemoveSession", ("no-such-session", tid(solo[9]))),
+         (0, "RemoveSessionAll", (t[solo[11]].presences[0].session_id.decode(),)),
+         (1, "RemovePartyAll", (t[party[2]].party_id.decode(),)),
+         (0, "RemoveParty", (t[party[5]].party_id.decode(), tid(party[5]))),
+         (1, "RemoveAll", ("node-nobody",))]
+    return s
+
+
+def mutator_worker(rank, world, port, n, q):
+    import harness
+    from nakama_amd import capi, cluster, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mm = capi.Matchmaker(harness.oracle_lib(), max_intervals=3)
+        cm = cluster.ClusterMatchmaker(mm, dist, POOL_FIELDS[3])
+        ts = _make(3, n, world, rank, 2)
+        cm.Insert(ts.ptr(), ts.n)
+        full = synth.TicketSet(3, n, pool_groups=2)
+        results = []
+        for who, op, args in _script(full, rank):
+            mine = args if who == rank else None
+            try:
+                if op == "Remove":
+                    cm.Remove(mine[0] if mine else None)
+                else:
+                    getattr(cm, op)(*(mine if mine else (None,) * len(args)))
+                results.append((op, None))
+            except capi.MatchmakerError as e:
+                results.append((op, type(e).__name__))
+        # an Add routed from rank 1 into a pool rank 0 may own, and one refused
+        add = capi.Ticket(ticket="added-1", presences=[capi.Presence("ua", "sa", "ua", "n")], session_id="sa",
+                          query="+properties.mode:ranked +properties.region:eu-g0", min_count=10, max_count=10,
+                          count_multiple=5, string_properties={"mode": "ranked", "region": "eu-g0"},
+                          created_at=synth.T0 + 1024 * (n + 5))
+        bad_add = capi.Ticket(ticket="added-2", presences=[capi.Presence("ub", "sb", "ub", "n")], session_id="sb",
+                              query="*", string_properties={"mode": "ranked", "region": "eu-g0"},
+                              created_at=synth.T0 + 1024 * (n + 6))
+        e1 = cm.Add(add if rank == 1 else None)
+        e2 = cm.Add(bad_add if rank == 0 else None)
+        results.append(("Add", None if e1 is None else type(e1).__name__))
+        results.append(("AddBad", None if e2 is None else type(e2).__name__))
+        passes = []
+        for _ in range(2):
+            cp = cm.Process(keep_groups=True)
+            passes.append((cm.gather_groups(cp), cm.Extract()))
+        gathered = [None] * world
+        dist.all_gather_object(gathered, results)
+        if rank == 0:
+            q.put((gathered, [(g, [(x.ticket, x.intervals) for x in st]) for g, st in passes]))
+        full.close()
+        ts.close()
+        mm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cluster_mutators_as_collectives():
+    """Remove / RemoveSession / RemoveSessionAll / RemoveParty / RemovePartyAll
+    / RemoveAll issued on one rank for tickets living on either rank, and a
+    routed Add, equal the same calls on one matchmaker (statuses included);
+    an unroutable Add is refused on the caller."""
+    import harness
+    from nakama_amd import capi, synth
+    n = 900
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=mutator_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    gathered, passes = _wait(q, procs)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = synth.TicketSet(3, n, pool_groups=2)
+    mm = capi.Matchmaker(harness.oracle_lib(), max_intervals=3)
+    try:
+        full.insert_into(mm)
+        want = []
+        for who, op, args in _script(full, 0):
+            try:
+                getattr(mm, op)(*args)
+                want.append((who, op, None))
+            except capi.MatchmakerError as e:
+                want.append((who, op, type(e).__name__))
+        mm.Add([capi.Presence("ua", "sa", "ua", "n")], "sa", "", "+properties.mode:ranked +properties.region:eu-g0",
+               10, 10, 5, {"mode": "ranked", "region": "eu-g0"}, {}, ticket="added-1",
+               created_at=synth.T0 + 1024 * (n + 5))
+        got = [(who, op, gathered[who][k][1]) for k, (who, op, _) in enumerate(want)]
+        assert got == want
+        assert gathered[1][-2] == ("Add", None)
+        assert gathered[0][-1] == ("AddBad", "ErrMatchmakerUnsupportedQuery")
+        for g, st in passes:
+            assert g == mm.Process()
+            assert st == [(x.ticket, x.intervals) for x in mm.Extract()]
+    finally:
+        mm.close()
+        full.close()
+
+
+def failing_override_worker(rank, world, port, q):
+    import harness
+    from nakama_amd import capi, cluster
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = {"n": 0}
+
+        def override(c):
+            calls["n"] += 1
+            if rank == 1 and calls["n"] == 1:
+                raise ValueError("user override failed")
+            return first_disjoint(c)
+        mm = capi.Matchmaker(harness.oracle_lib(), max_intervals=3, rev_precision=True, rev_threshold=0,
+                             override=override)
+        cm = cluster.ClusterMatchmaker(mm, dist, POOL_FIELDS[5])
+        ts = _make(5, 400, world, rank, 0)
+        cm.Insert(ts.ptr(), ts.n)
+        raised = False
+        try:
+            cm.Process()
+        except Exception:
+            raised = True
+        cp = cm.Process(keep_groups=True)  # the passes were closed: the front works on
+        merged = cm.gather_groups(cp)
+        if rank == 0:
+            q.put((raised, len(merged)))
+        else:
+            q.put((raised, None))
+        ts.close()
+        mm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cluster_override_failure_closes_every_pass():
+    """An override that raises on one rank: every rank raises (no rank is
+    left waiting in a collective), every rank's pass is closed with an empty
+    choice, and the next Process runs normally."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=failing_override_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [_wait(q, procs), _wait(q, procs)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert all(r[0] for r in res)
+    assert any(r[1] for r in res if r[1] is not None)
+
+
+def reversed_first_disjoint(groups):
+    """An override that returns its choice in reverse order (the groups'
+    searching-ticket keys then descend on every rank)."""
+    return list(reversed(first_disjoint(groups)))
+
+
+def test_cluster_merge_with_reordering_override():
+    """mm_merge_positions needs ascending keys per rank; a reordering
+    override breaks that, and the front falls back to a stable global order
+    by (key, rank, index): every group lands exactly once (a permutation, no
+    holes), the same groups one matchmaker forms with the same override."""
+    cfg = dict(max_intervals=2, rev_precision=True, rev_threshold=0, override=reversed_first_disjoint)
+    out, bad, loads = run_cluster(5, 640, 0, 1, cfg)
+    assert bad == [] and min(loads) > 0
+    want = single_pass(5, 640, 0, 1, cfg)
+    merged = out[0][0]
+    assert None not in merged and len(merged) == out[0][3]
+    assert sorted(map(tuple, map(lambda g: tuple(map(tuple, g)), merged))) == \
+        sorted(map(tuple, map(lambda g: tuple(map(tuple, g)), want[0][0])))

@@ -30,7 +30,8 @@ def _free_port():
 
 def _worker(rank, world, port, config, n, q):
     import harness
-    from nakama_amd import capi, sharding, synth
+    import sharding
+    from nakama_amd import capi, synth
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -58,7 +59,8 @@ def _worker(rank, world, port, config, n, q):
 @pytest.mark.parametrize("config,n", [(3, 900), (4, 1200)])
 def test_pool_sharded_pass_equals_global_pass(config, n):
     import harness
-    from nakama_amd import capi, sharding, synth
+    import sharding
+    from nakama_amd import capi, synth
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -91,7 +93,7 @@ def test_pool_sharded_pass_equals_global_pass(config, n):
 
 
 def test_assign_pools_balanced_and_deterministic():
-    from nakama_amd import sharding
+    import sharding
     sizes = [125, 124, 130, 126, 119, 127, 125, 124]
     a = sharding.assign_pools(sizes, 4)
     assert sorted(p for b in a for p in b) == list(range(8))
@@ -131,7 +133,8 @@ def test_shard_instances_equal_one_global_pass(config, n):
     all N instances together: the instances share no pool, so no group can
     span GPUs and no collective is needed in the data path."""
     import harness
-    from nakama_amd import capi, sharding, synth
+    import sharding
+    from nakama_amd import capi, synth
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

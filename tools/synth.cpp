@@ -211,10 +211,12 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             t.min_count = t.max_count = 2;
             break;
         }
-        case 5: {
+        case 5:
+        case 11: {  // 11: C5 with buckets of 64 -> 63 filtered hits per row, where
+                    // processCustom hands over no candidate (matchmaker_process.go:588)
             const int s = (int)std::lround(r.normal(1500.0, 300.0));
             char b[32];
-            std::snprintf(b, sizeof b, "b%lld", (long long)(i / 8));
+            std::snprintf(b, sizeof b, "b%lld", (long long)(i / (config == 11 ? 64 : 8)));
             S->sp.push_back({"bucket", S->keep(b)});
             S->np.push_back({"skill", (double)s});
             char q[160];
