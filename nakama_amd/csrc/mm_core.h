@@ -63,6 +63,16 @@ int scan_chunk_len();
 hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs, const DClause* d_mcl, uint32_t* d_scratch,
                         DGroupResult* d_cres, bool gen, hipStream_t stream, hipEvent_t ev0 = nullptr,
                         hipEvent_t ev1 = nullptr);
+// hashed multi-signature scan (ms.hmask != 0): d_blob = DMSig[n_sigs], u64
+// output word offsets[n_sigs], then at mscan_hash_table_off the cuckoo table
+// (DMHashEntry[hmask + 1]); d_work sized by mscan_hash_work_words
+hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_blob, uint32_t* d_work,
+                             DGroupResult* d_cres, uint32_t* d_out32, hipStream_t stream, hipEvent_t ev0 = nullptr,
+                             hipEvent_t ev1 = nullptr);
+uint64_t mscan_hash_work_words(const DMScan& ms);
+size_t mscan_hash_table_off(uint32_t n_sigs);
+size_t mscan_hash_blob_bytes(uint32_t n_sigs, uint32_t cap);
+int mscan_hash_chunk_len(bool contig);
 int mscan_chunk_len(uint32_t n_sigs);
 int mscan_max_sigs();
 int mscan_max_fields();
@@ -377,6 +387,7 @@ struct PassStats {
     // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel
     // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel
     double k_ms[4] = {0, 0, 0, 0};      // HIP-event time of the launches
+    bool mhash = false;                 // a batch's mscan ran hashed (mscan_hash_kernel)
     int64_t k_bytes[4] = {0, 0, 0, 0};  // algorithmic bytes
     int k_launches[4] = {0, 0, 0, 0};
     int64_t pair_evals = 0;
@@ -715,6 +726,8 @@ public:
     bool order_sorted_ = true;
     bool index_dirty_ = true;
     uint32_t order_head_ = 0;
+    bool order_identity_ = false;  // order_[p] == p for every p (build_index): the hashed mscan's contiguous mode
+    bool mcontig_mode_ = true;     // NKM_MCONTIG=0: never the contiguous mode
     std::unordered_map<uint64_t, PostingRange> postings_map_;
     std::vector<uint32_t> postings_;
     std::vector<uint32_t> pending_dead_;  // slots to clear on the device at next sync
@@ -813,6 +826,9 @@ public:
     // "scan" (scan_kernel at any size), "mscan" (mscan_kernel whenever eligible)
     enum KernelMode { KM_AUTO = 0, KM_SEARCH = 1, KM_SCAN = 2, KM_MSCAN = 3 };
     int kernel_mode_ = KM_AUTO;
+    // NKM_MHASH: 0 (default) the hashed mscan past 16 signatures, 1 whenever
+    // the signatures allow it, 2 never
+    int mhash_mode_ = 0;
     std::vector<uint32_t> custom_expired_;
 
     std::vector<std::string> debug_strings_;

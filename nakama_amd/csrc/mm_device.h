@@ -101,9 +101,38 @@ struct DMScan {
     uint32_t n_fields;
     uint32_t n_clauses;         // of all the signatures
     uint16_t field[4];
-    uint32_t chunk;             // candidates per chunk (workgroup): 4 or 8 per lane
+    uint32_t chunk;             // candidates per chunk (workgroup): 2, 4 or 8 per lane
+    uint32_t hmask;             // hashed lookup (mscan_hash_kernel): table entries - 1; 0: mscan_kernel
+    uint32_t contig;            // hashed: order[p] == p over the range, chunks are slot ranges aligned
+                                // to `chunk` from src_off rounded down
+    uint32_t hseed[2];          // hashed: the two cuckoo hash seeds
     uint32_t pad;
 };
+
+// Hashed signature lookup of mscan_hash_kernel: term-only pool signatures that
+// all require the same keyword fields, with pairwise distinct required values,
+// so a candidate matches at most one — found by its values (dictionary ids,
+// 32 bits) in a two-choice cuckoo table: every signature sits at one of its
+// two hashed positions, so a candidate reads exactly two entries, independent
+// of each other and of the signature count.  The host builds the table.
+constexpr uint32_t kMHashSigs = 256;  // signatures of one hashed scan
+constexpr uint32_t kMHashCap = 1024;  // table entries (a power of two >= 2 x signatures)
+constexpr uint32_t kMHashEmpty = 0xFFFFu;
+struct DMHashEntry {                  // 32 B
+    uint32_t key[4];                  // required dictionary id per scanned field (0 past n_fields)
+    uint32_t q;                       // signature, kMHashEmpty: free
+    int32_t tmin, tmax;               // its count-range musts
+    uint32_t pad;
+};
+static_assert(sizeof(DMHashEntry) == 32, "DMHashEntry is 32 bytes");
+NKM_HD inline uint32_t msig_mix(uint32_t h, uint32_t k) {  // 32-bit multiplies only
+    h = (h ^ k) * 0x9E3779B1u;
+    return h ^ (h >> 15);
+}
+NKM_HD inline uint32_t msig_fin(uint32_t h) {
+    h *= 0x85EBCA77u;
+    return h ^ (h >> 13);
+}
 
 // One signature of a multi-signature scan.  term_only: every clause is a
 // MUST keyword TERM, so the match is "field f == req[f] for every f in

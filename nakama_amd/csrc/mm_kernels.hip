@@ -666,6 +666,433 @@ __global__ __launch_bounds__(kBlock) void mscan_kernel(DStore st, DMScan ms, con
     }
 }
 
+// ---- hashed multi-signature scan ----------------------------------------------------
+// mscan_kernel holds one match bit per (signature, candidate) and a ballot per
+// signature: its cost grows with the signature count, and past 16 signatures
+// (C4: 64 mode x region pools on one GPU) the batch fell back to scan_kernel
+// over region posting lists shared by 8 modes (7.5x the column bytes).  When
+// the signatures are term-only pool signatures requiring the same fields with
+// distinct values, a candidate matches at most one: its required values find
+// that signature through the LDS hash table, so the per-candidate work is one
+// probe whatever the signature count.  The scan order is then stably
+// partitioned by signature in three launches:
+//   mscan_hash_kernel   per chunk: lookup, rank within (signature, chunk), the
+//                       chunk's hits signature-major into scratch, counts row;
+//   mscan_base_kernel   per signature: exclusive prefix over the chunks;
+//   mscan_place_kernel  per chunk: its hits to their signature's list.
+// Counts/bases are row-major [chunk][signature + 1] (column n_sigs: live
+// candidates, for the accounting).  Every list is in scan order — the hit
+// order of a constant-score search — exactly as mscan_kernel + stitch emit it.
+// kMJ consecutive candidates of one lane, from a column at slot `gs`
+// (aligned to kMJ elements): 16-B loads where they fit, one smaller load else.
+template <int N, typename T>
+__device__ __forceinline__ void load_run(T (&dst)[N], const T* p) {
+    constexpr int B = N * (int)sizeof(T);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    typedef const __attribute__((address_space(1))) u32x4 g16;
+    typedef const __attribute__((address_space(1))) u32x2 g8;
+    typedef const __attribute__((address_space(1))) uint32_t g4;
+    typedef const __attribute__((address_space(1))) uint16_t g2;
+    if constexpr (B >= 16) {
+#pragma unroll
+        for (int k = 0; k < B / 16; k++) {
+            const u32x4 v = ((g16*)p)[k];
+            __builtin_memcpy(reinterpret_cast<char*>(dst) + 16 * k, &v, 16);
+        }
+    } else if constexpr (B == 8) {
+        const u32x2 v = *(g8*)p;
+        __builtin_memcpy(dst, &v, 8);
+    } else if constexpr (B == 4) {
+        const uint32_t v = *(g4*)p;
+        __builtin_memcpy(dst, &v, 4);
+    } else {
+        static_assert(B == 2, "run of 2-64 bytes");
+        const uint16_t v = *(g2*)p;
+        __builtin_memcpy(dst, &v, 2);
+    }
+}
+
+// CONTIG (ms.contig): the scan order is the slot order (tickets added in
+// created-at order: order[p] == p), so a chunk is a slot range aligned to the
+// chunk length and every lane loads its kMJ consecutive candidates' columns
+// with 4-16-B vector loads (one instruction per column per lane instead of
+// kMJ gathers, and no slot ids read); the signatures found are handed through
+// LDS to the strided layout (candidate j * 256 + tid) the ranking uses.
+// LDS is sized at launch (mscan_hash_lds): the table, the (signature, j,
+// wave) counts, the chunk's signature offsets, its staged hits, and CONTIG's
+// hand-over — 12 KB for C4's 64 signatures, so occupancy stays high.
+template <int kMJ, bool CONTIG>
+struct MHashLds {
+    uint32_t cap, nq;
+    __host__ __device__ constexpr uint32_t table_off() const { return 0; }
+    __host__ __device__ constexpr uint32_t cnt_off() const { return cap * 32u; }
+    __host__ __device__ constexpr uint32_t loff_off() const { return cnt_off() + ((nq * kMJ * kWaves * 2u + 15u) & ~15u); }
+    __host__ __device__ constexpr uint32_t stage_off() const { return loff_off() + ((nq * 4u + 15u) & ~15u); }
+    __host__ __device__ constexpr uint32_t qs_off() const { return stage_off() + kMJ * kBlock * 4u; }
+    __host__ __device__ constexpr uint32_t bytes() const { return qs_off() + (CONTIG ? kMJ * kBlock * 2u : 0u); }
+};
+
+template <int NF, int kMJ, bool CONTIG>
+__global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms, const DMHashEntry* __restrict__ htab,
+                                                            uint32_t* __restrict__ scratch,
+                                                            uint32_t* __restrict__ counts) {
+    static_assert(NF >= 1 && NF <= 4, "1-4 required fields");
+    static_assert(!CONTIG || kMJ == 4 || kMJ == 8, "runs of 4 or 8 candidates");
+    constexpr int kMChunk = kMJ * kBlock;
+    constexpr uint32_t kNone = kMHashEmpty;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint32_t wsum[kWaves], wlive[kWaves];
+    const uint32_t nq = ms.n_sigs, hmask = ms.hmask;
+    const MHashLds<kMJ, CONTIG> L{hmask + 1, nq};
+    DMHashEntry* tab = reinterpret_cast<DMHashEntry*>(lds + L.table_off());
+    uint16_t* cnt = reinterpret_cast<uint16_t*>(lds + L.cnt_off());  // [q][j][wave]: count, then its rank base
+    uint32_t* loff = reinterpret_cast<uint32_t*>(lds + L.loff_off());
+    uint32_t* stage = reinterpret_cast<uint32_t*>(lds + L.stage_off());  // the chunk's hits, signature-major
+    uint16_t* qs = reinterpret_cast<uint16_t*>(lds + L.qs_off());
+    const uint32_t c = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef NKM_MH_DEBUG  // tools/mhash_bench.hip: phases switched off one by one (ms.pad bits)
+    const uint32_t dbg = ms.pad;
+#else
+    constexpr uint32_t dbg = 0;
+#endif
+    typedef const __attribute__((address_space(1))) uint8_t gu8;
+    typedef const __attribute__((address_space(1))) int64_t gi64;
+    gu8* fkp[NF];
+    gi64* fvp[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+        fkp[f] = (gu8*)st.fkind[ms.field[f]];
+        fvp[f] = (gi64*)st.fval[ms.field[f]];
+    }
+    // CONTIG: the chunk's slots [cs0, cs0 + kMChunk), the scan's [vlo, vhi)
+    const uint32_t cs0 = (ms.src_off & ~(uint32_t)(kMChunk - 1)) + c * (uint32_t)kMChunk;
+    const uint32_t vlo = ms.src_off, vhi = ms.src_off + ms.src_len;
+    uint32_t s[kMJ], sl[kMJ];
+    if constexpr (!CONTIG) {
+        // unconditional loads, tail lanes clamped (as in mscan_kernel)
+        const uint32_t base = c * (uint32_t)kMChunk;
+        const uint32_t len = ms.src_len - base < (uint32_t)kMChunk ? ms.src_len - base : (uint32_t)kMChunk;
+        const uint32_t* __restrict__ src = st.order + ms.src_off + base;
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) {
+            const uint32_t i = (uint32_t)(j * kBlock + tid);
+            sl[j] = src[i < len ? i : len - 1];
+            s[j] = i < len ? sl[j] : kNoSlot;
+        }
+    }
+    // the table and zeroed counts into LDS while the column loads are in flight
+    if (!(dbg & 4)) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* __restrict__ g4 = reinterpret_cast<const u32x4*>(htab);
+        u32x4* t4 = reinterpret_cast<u32x4*>(tab);
+        for (uint32_t t = (uint32_t)tid; t < 2 * (hmask + 1); t += kBlock) t4[t] = g4[t];
+        uint32_t* c4 = reinterpret_cast<uint32_t*>(cnt);
+        for (uint32_t t = (uint32_t)tid; t < (nq * kMJ * kWaves + 1) / 2; t += kBlock) c4[t] = 0u;
+    }
+    uint8_t al[kMJ];
+    int32_t mn[kMJ], mx[kMJ];
+    uint8_t kk[NF][kMJ];
+    int64_t vv[NF][kMJ];
+    bool a[kMJ];
+    if constexpr (CONTIG) {
+        const uint32_t gs = cs0 + (uint32_t)tid * kMJ;  // the lane's run: candidates (wave, lane, j)
+        if (gs >= vlo && gs + kMJ <= vhi) {
+            load_run(al, st.alive + gs);
+            load_run(mn, st.minc + gs);
+            load_run(mx, st.maxc + gs);
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                load_run(kk[f], (const uint8_t*)(fkp[f] + gs));
+                load_run(vv[f], (const int64_t*)(fvp[f] + gs));
+            }
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) a[j] = al[j] != 0;
+        } else {  // the scan's first / last chunk: per candidate, in range only
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) {
+                const uint32_t x = gs + j;
+                a[j] = x >= vlo && x < vhi;
+                al[j] = 0;
+                mn[j] = mx[j] = 0;
+#pragma unroll
+                for (int f = 0; f < NF; f++) {
+                    kk[f][j] = (uint8_t)KIND_ABSENT;
+                    vv[f][j] = 0;
+                }
+                if (!a[j]) continue;
+                al[j] = st.alive[x];
+                mn[j] = st.minc[x];
+                mx[j] = st.maxc[x];
+#pragma unroll
+                for (int f = 0; f < NF; f++) {
+                    kk[f][j] = fkp[f][x];
+                    vv[f][j] = fvp[f][x];
+                }
+                a[j] = al[j] != 0;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) {
+            al[j] = st.alive[sl[j]];
+            mn[j] = st.minc[sl[j]];
+            mx[j] = st.maxc[sl[j]];
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                kk[f][j] = fkp[f][sl[j]];
+                vv[f][j] = fvp[f][sl[j]];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) a[j] = s[j] != kNoSlot && al[j] != 0;
+    }
+    uint32_t live = 0;
+#pragma unroll
+    for (int j = 0; j < kMJ; j++) {
+        live += a[j];
+#pragma unroll
+        for (int f = 0; f < NF; f++) a[j] = a[j] && kk[f][j] == KIND_KEYWORD;  // every field is required
+    }
+    for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o);
+    if (lane == 0) wlive[wave] = live;
+    __syncthreads();  // table and zeroed counts are in LDS
+    // each candidate's signature (at most one): its two cuckoo entries, read
+    // together; then the signature's count-range musts.  A keyword value is a
+    // dictionary id (< 2^32), so the 32-bit keys compare exactly.
+    uint32_t q[kMJ];
+#pragma unroll
+    for (int j = 0; j < kMJ; j++) {
+        uint32_t h1 = ms.hseed[0], h2 = ms.hseed[1];
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            h1 = msig_mix(h1, (uint32_t)vv[f][j]);
+            h2 = msig_mix(h2, (uint32_t)vv[f][j]);
+        }
+        const DMHashEntry& e1 = tab[msig_fin(h1) & hmask];
+        const DMHashEntry& e2 = tab[msig_fin(h2) & hmask];
+        bool m1 = e1.q != kNone, m2 = e2.q != kNone;
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            m1 = m1 && e1.key[f] == (uint32_t)vv[f][j];
+            m2 = m2 && e2.key[f] == (uint32_t)vv[f][j];
+        }
+        const uint32_t qq = m1 ? e1.q : e2.q;
+        const int32_t tmin = m1 ? e1.tmin : e2.tmin, tmax = m1 ? e1.tmax : e2.tmax;
+        q[j] = a[j] && (m1 || m2) && mn[j] >= tmin && mx[j] <= tmax ? qq : kNone;
+        if (dbg & 1) q[j] = a[j] ? (uint32_t)(vv[0][j] ^ vv[NF - 1][j]) & (nq - 1) : kNone;  // no table probe
+    }
+    if constexpr (CONTIG) {
+        // runs (wave, lane, j) -> the strided layout j * 256 + tid, through LDS
+        uint16_t pk[kMJ];
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) pk[j] = (uint16_t)q[j];
+        __builtin_memcpy(&qs[tid * kMJ], pk, sizeof pk);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) {
+            const uint32_t i = (uint32_t)(j * kBlock + tid);
+            q[j] = qs[i];
+            s[j] = cs0 + i;
+        }
+    }
+    if (dbg & 2) {  // no ranking, prefix or scatter: a checksum of the signatures found
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) x += q[j];
+        counts[(uint64_t)c * kBlock + tid] = x;
+        return;
+    }
+    // rank within (signature, j, wave): the lanes holding the same signature
+    // are found with one ballot per signature-index bit
+    const uint32_t nbits = nq > 1 ? 32u - (uint32_t)__clz(nq - 1) : 0u;
+    uint32_t rk[kMJ];
+#pragma unroll
+    for (int j = 0; j < kMJ; j++) {
+        const bool m = q[j] != kNone;
+        uint64_t peer = __ballot((int)m);
+        for (uint32_t b = 0; b < nbits; b++) {
+            const bool bit = (q[j] >> b) & 1u;
+            const uint64_t bb = __ballot((int)(m && bit));
+            peer &= bit ? bb : ~bb;
+        }
+        rk[j] = lanes_below(peer);
+        if (m && rk[j] == 0) cnt[(q[j] * kMJ + j) * kWaves + wave] = (uint16_t)__popcll(peer);
+    }
+    __syncthreads();
+    // per signature: rank bases in candidate order (j, wave); the chunk's
+    // signature-major offsets by a block scan of the totals
+    uint32_t tot = 0;
+    if ((uint32_t)tid < nq) {
+        uint16_t* cq = cnt + (uint32_t)tid * kMJ * kWaves;
+        uint32_t run = 0;
+#pragma unroll
+        for (int k = 0; k < kMJ * kWaves; k++) {
+            const uint32_t v = cq[k];
+            cq[k] = (uint16_t)run;
+            run += v;
+        }
+        tot = run;
+    }
+    uint32_t incl = tot;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t ex = incl - tot, total = 0;
+    for (int w = 0; w < kWaves; w++) {
+        if (w < wave) ex += wsum[w];
+        total += wsum[w];
+    }
+    if ((uint32_t)tid < nq) {
+        loff[tid] = ex;
+        counts[(uint64_t)tid * ms.n_chunks + c] = tot;  // column-major: mscan_base_kernel reads columns
+    }
+    if (tid == 0) {
+        uint32_t lv = 0;
+        for (int w = 0; w < kWaves; w++) lv += wlive[w];
+        counts[(uint64_t)nq * ms.n_chunks + c] = lv;
+    }
+    __syncthreads();
+    // ranked into LDS, then out in 16-B stores: with many signatures a
+    // wave's hits fall in as many signature segments, and direct 4-B stores
+    // would cost one partial-line write each
+#pragma unroll
+    for (int j = 0; j < kMJ; j++)
+        if (q[j] != kNone) stage[loff[q[j]] + cnt[(q[j] * kMJ + j) * kWaves + wave] + rk[j]] = s[j];
+    __syncthreads();
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4* __restrict__ cs4 = reinterpret_cast<u32x4*>(scratch + (uint64_t)c * kMChunk);
+    const u32x4* st4 = reinterpret_cast<const u32x4*>(stage);
+    for (uint32_t v = (uint32_t)tid; 4 * v < total; v += kBlock) cs4[v] = st4[v];
+}
+
+// Per column of the counts (a signature, or n_sigs: live candidates), stored
+// column-major [column][chunk]: the exclusive prefix over the chunks into
+// bases[column][chunk] (entry n_chunks: the total) and the signature's result
+// record.  Each thread loads its run of up to 16 counts in one round trip.
+__global__ __launch_bounds__(kBlock) void mscan_base_kernel(DMScan ms, const uint32_t* __restrict__ counts,
+                                                            uint32_t* __restrict__ bases,
+                                                            DGroupResult* __restrict__ res) {
+    __shared__ uint32_t wsum[kWaves];
+    const uint32_t q = blockIdx.x, n = ms.n_chunks;
+    const uint32_t* __restrict__ col = counts + (uint64_t)q * n;
+    uint32_t* __restrict__ bcol = bases + (uint64_t)q * (n + 1);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t per = (n + kBlock - 1) / kBlock;
+    const uint32_t lo = min(n, per * (uint32_t)tid), hi = min(n, per * (uint32_t)(tid + 1));
+    constexpr int kUnroll = 16;  // C4 4M: 4,096 chunks -> 16 per thread
+    const bool unrolled = per <= (uint32_t)kUnroll;
+    uint32_t v[kUnroll];
+    uint32_t sum = 0;
+    if (unrolled) {
+#pragma unroll
+        for (int k = 0; k < kUnroll; k++) v[k] = lo + k < hi ? col[lo + k] : 0u;
+#pragma unroll
+        for (int k = 0; k < kUnroll; k++) sum += v[k];
+    } else {
+        for (uint32_t i = lo; i < hi; i++) sum += col[i];
+    }
+    uint32_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum, total = 0;
+    for (int w = 0; w < kWaves; w++) {
+        if (w < wave) run += wsum[w];
+        total += wsum[w];
+    }
+    if (unrolled) {
+#pragma unroll
+        for (int k = 0; k < kUnroll; k++) {
+            if (lo + k < hi) bcol[lo + k] = run;
+            run += v[k];
+        }
+    } else {
+        for (uint32_t i = lo; i < hi; i++) {
+            const uint32_t x = col[i];
+            bcol[i] = run;
+            run += x;
+        }
+    }
+    if (tid != 0) return;
+    bcol[n] = total;
+    if (q == ms.n_sigs) {  // the chunk's columns are accounted to signature 0 (as mscan_kernel does)
+        res[0].live = total;
+        return;
+    }
+    res[q].count = total;
+    res[q].complete = 1u;
+    res[q].matched = total;
+    res[q].scanned = q == 0 ? ms.src_len : 0u;
+    res[q].pad = 0u;
+    if (q != 0) res[q].live = 0u;
+}
+
+// Per chunk: its hits (signature-major in scratch) to out32[dst[q] + base + r].
+// Every thread loads its up-to-8 hits (e = k * 256 + tid) in one round trip,
+// finds each one's signature by a binary search of the chunk's signature
+// offsets in LDS, and stores it (a signature's run stays contiguous).
+__global__ __launch_bounds__(kBlock) void mscan_place_kernel(DMScan ms, const uint32_t* __restrict__ bases,
+                                                             const uint32_t* __restrict__ scratch,
+                                                             const uint64_t* __restrict__ dst,
+                                                             uint32_t* __restrict__ out32) {
+    __shared__ uint32_t loff[kMHashSigs];
+    __shared__ uint64_t lpos[kMHashSigs];
+    __shared__ uint32_t wsum[kWaves];
+    const uint32_t c = blockIdx.x, nq = ms.n_sigs, n1 = ms.n_chunks + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t n = 0, b = 0;
+    if ((uint32_t)tid < nq) {
+        const uint32_t* __restrict__ bq = bases + (uint64_t)tid * n1 + c;
+        b = bq[0];
+        n = bq[1] - b;
+    }
+    // the chunk's hits, loaded before their count is known (clamped to the chunk)
+    constexpr int kMaxPer = 8;
+    const uint32_t per = ms.chunk / kBlock;
+    const uint32_t* __restrict__ cs = scratch + (uint64_t)c * ms.chunk;
+    uint32_t v[kMaxPer];
+#pragma unroll
+    for (int k = 0; k < kMaxPer; k++) v[k] = (uint32_t)k < per ? cs[k * kBlock + tid] : 0u;
+    uint32_t incl = n;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t ex = incl - n, total = 0;
+    for (int w = 0; w < kWaves; w++) {
+        if (w < wave) ex += wsum[w];
+        total += wsum[w];
+    }
+    if ((uint32_t)tid < nq) {
+        loff[tid] = ex;
+        lpos[tid] = dst[tid] + b;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kMaxPer; k++) {
+        const uint32_t e = (uint32_t)(k * kBlock + tid);
+        if ((uint32_t)k >= per || e >= total) continue;
+        // the last signature whose offset is <= e (empty ones share it and lose)
+        uint32_t lo = 0, hi = nq;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (loff[mid] <= e) lo = mid;
+            else hi = mid;
+        }
+        out32[lpos[lo] + (e - loff[lo])] = v[k];
+    }
+}
+
 // Places every chunk's compacted hits at its search's output, at the chunk's
 // rank from cell_scan_kernel; entries past the search's capacity are dropped
 // (the host marks it incomplete).
@@ -1089,6 +1516,73 @@ hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs,
 #undef NKM_MSCAN
 #undef NKM_MSCAN_J
     return hipGetLastError();
+}
+
+// The hashed scan's three launches (see mscan_hash_kernel).  d_blob: the
+// DMSig array, then n_sigs u64 output word offsets, then the hmask + 1 cuckoo
+// entries (DMHashEntry, 32-B aligned); d_work (16-B aligned): chunks x chunk
+// scratch words, then (n_sigs + 1) x chunks counts, then (n_sigs + 1) x
+// (chunks + 1) bases (column-major).
+size_t mscan_hash_table_off(uint32_t n_sigs) {
+    return ((size_t)n_sigs * (sizeof(DMSig) + sizeof(uint64_t)) + 31) & ~(size_t)31;
+}
+size_t mscan_hash_blob_bytes(uint32_t n_sigs, uint32_t cap) {
+    return mscan_hash_table_off(n_sigs) + (size_t)cap * sizeof(DMHashEntry);
+}
+hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_blob, uint32_t* d_work,
+                             DGroupResult* d_cres, uint32_t* d_out32, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
+    if (ms.n_chunks == 0 || ms.n_sigs == 0) return hipSuccess;
+    const uint32_t mj = ms.chunk / kBlock;
+    const uint64_t covered = ms.contig ? (uint64_t)(ms.src_off & ~(ms.chunk - 1)) + (uint64_t)ms.n_chunks * ms.chunk
+                                       : (uint64_t)ms.n_chunks * ms.chunk;
+    if (ms.n_sigs > kMHashSigs || ms.hmask + 1 > kMHashCap || ((ms.hmask + 1) & ms.hmask) || ms.hmask + 1 < 2 * ms.n_sigs ||
+        ms.n_fields < 1 || ms.n_fields > 4 || ms.chunk % kBlock || (ms.chunk & (ms.chunk - 1)) ||
+        (ms.contig ? mj != 4 && mj != 8 : mj != 2 && mj != 4) ||
+        covered < (ms.contig ? (uint64_t)ms.src_off + ms.src_len : (uint64_t)ms.src_len))
+        return hipErrorInvalidValue;
+    const uint64_t* dst = reinterpret_cast<const uint64_t*>(static_cast<const DMSig*>(d_blob) + ms.n_sigs);
+    const DMHashEntry* htab =
+        reinterpret_cast<const DMHashEntry*>(static_cast<const char*>(d_blob) + mscan_hash_table_off(ms.n_sigs));
+    const uint64_t w1 = ms.n_sigs + 1;
+    uint32_t* scratch = d_work;  // first: 16-B aligned for the chunks' vector stores
+    uint32_t* counts = scratch + (uint64_t)ms.n_chunks * ms.chunk;
+    uint32_t* bases = counts + (uint64_t)ms.n_chunks * w1;
+    const dim3 grid(ms.n_chunks), block(kBlock);
+#define NKM_MHASH_K(NF, J, C)                                                                                        \
+    hipExtLaunchKernelGGL(mscan_hash_kernel<NF, J, C>, grid, block, (MHashLds<J, C>{ms.hmask + 1, ms.n_sigs}.bytes()), \
+                          stream, ev0, ev1, 0, st, ms, htab, scratch, counts)
+#define NKM_MHASH(NF)                                        \
+    do {                                                     \
+        if (ms.contig && mj == 8) NKM_MHASH_K(NF, 8, true);  \
+        else if (ms.contig) NKM_MHASH_K(NF, 4, true);        \
+        else if (mj == 4) NKM_MHASH_K(NF, 4, false);         \
+        else NKM_MHASH_K(NF, 2, false);                      \
+    } while (0)
+    switch (ms.n_fields) {
+        case 1: NKM_MHASH(1); break;
+        case 2: NKM_MHASH(2); break;
+        case 3: NKM_MHASH(3); break;
+        default: NKM_MHASH(4); break;
+    }
+#undef NKM_MHASH
+#undef NKM_MHASH_K
+#ifdef NKM_MH_DEBUG
+    if (ms.pad & 2) return hipGetLastError();  // no counts to place
+#endif
+    hipLaunchKernelGGL(mscan_base_kernel, dim3(ms.n_sigs + 1), block, 0, stream, ms, counts, bases, d_cres);
+    hipLaunchKernelGGL(mscan_place_kernel, grid, block, 0, stream, ms, bases, scratch, dst, d_out32);
+    return hipGetLastError();
+}
+uint64_t mscan_hash_work_words(const DMScan& ms) {
+    const uint64_t w1 = ms.n_sigs + 1;
+    return (uint64_t)ms.n_chunks * w1 + (uint64_t)(ms.n_chunks + 1) * w1 + (uint64_t)ms.n_chunks * ms.chunk;
+}
+// candidates per lane: gathered 2 or 4 (NKM_MHASH_J, default 4); contiguous
+// 4 or 8 (NKM_MCONTIG_J, default 4)
+int mscan_hash_chunk_len(bool contig) {
+    const char* e = std::getenv(contig ? "NKM_MCONTIG_J" : "NKM_MHASH_J");
+    const int j = e ? std::atoi(e) : 0;
+    return (contig ? (j == 8 ? 8 : 4) : (j == 2 ? 2 : 4)) * kBlock;
 }
 
 // Candidates per lane: NKM_MSCAN_J (2, 4 or 8; 8 needs <= 8 signatures), default 2

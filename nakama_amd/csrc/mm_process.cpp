@@ -239,8 +239,8 @@ struct Replay : ReplayCore {
         }
         size_t nclauses = 0;
         for (uint32_t i : m_list) nclauses += c.sigs_[bg[i].sig].n_clauses;
-        if (m_list.empty() || m_list.size() > (size_t)mscan_max_sigs() || fields.size() > (size_t)mscan_max_fields() ||
-            nclauses > (size_t)mscan_max_clauses() || (!any_size && 2 * covered < order_len)) {
+        if (m_list.empty() || m_list.size() > (size_t)kMHashSigs || fields.size() > (size_t)mscan_max_fields() ||
+            (!any_size && 2 * covered < order_len)) {
             m_list.clear();
             return false;
         }
@@ -248,22 +248,108 @@ struct Replay : ReplayCore {
         ms.src_off = c.order_head_;
         ms.src_len = (uint32_t)order_len;
         ms.n_sigs = (uint32_t)m_list.size();
-        const uint32_t mchunk = (uint32_t)mscan_chunk_len(ms.n_sigs);
-        ms.chunk = mchunk;
-        ms.n_chunks = (ms.src_len + mchunk - 1) / mchunk;
         ms.n_fields = (uint32_t)fields.size();
         ms.n_clauses = (uint32_t)nclauses;
         for (size_t f = 0; f < fields.size(); f++) ms.field[f] = fields[f];
+        msig.clear();
         for (uint32_t i : m_list) {
             const Sig& sg = c.sigs_[bg[i].sig];
+            const uint32_t off = (uint32_t)mcl.size();
             for (uint32_t k = 0; k < sg.n_clauses; k++) {
                 DClause cl = c.clauses_[sg.clause_off + k];
                 cl.field = cl.op == OP_FALSE ? 0
                                              : (uint16_t)(std::find(fields.begin(), fields.end(), cl.field) - fields.begin());
                 mcl.push_back(cl);
             }
+            msig.push_back(make_msig(bg[i].d, off));
+        }
+        // past mscan_kernel's 16 signatures, or on request (NKM_MHASH=1):
+        // the hashed lookup, when every signature is term-only on the same
+        // fields with distinct values
+        const bool hashable = plan_mscan_hash(ms);
+        if (ms.n_sigs > (uint32_t)mscan_max_sigs() || nclauses > (size_t)mscan_max_clauses() || c.mhash_mode_ == 1) {
+            if (!hashable) {
+                m_list.clear();
+                mcl.clear();
+                msig.clear();
+                return false;
+            }
+        } else {
+            ms.hmask = 0;
+            htab.clear();
+        }
+        ms.contig = ms.hmask && c.order_identity_ && c.mcontig_mode_ ? 1u : 0u;
+        ms.chunk = (uint32_t)(ms.hmask ? mscan_hash_chunk_len(ms.contig != 0) : mscan_chunk_len(ms.n_sigs));
+        if (ms.contig) {  // chunks: slot ranges aligned to the chunk length
+            const uint64_t g0 = ms.src_off & ~(uint64_t)(ms.chunk - 1);
+            ms.n_chunks = (uint32_t)(((uint64_t)ms.src_off + ms.src_len - g0 + ms.chunk - 1) / ms.chunk);
+        } else {
+            ms.n_chunks = (ms.src_len + ms.chunk - 1) / ms.chunk;
         }
         return true;
+    }
+
+    // The hashed lookup's cuckoo table (ms.hmask, ms.hseed, htab) when the
+    // signatures allow it: term-only, the same required fields, keyword ids
+    // (32 bits), pairwise distinct values.  Seeds are tried in a fixed order
+    // (deterministic tables), the capacity doubles if none places every key.
+    std::vector<DMHashEntry> htab;
+    bool plan_mscan_hash(DMScan& ms) {
+        ms.hmask = 0;
+        htab.clear();
+        if (c.mhash_mode_ == 2 || ms.n_fields == 0) return false;
+        const uint8_t all = (uint8_t)((1u << ms.n_fields) - 1);
+        for (const DMSig& m : msig) {
+            if (!m.term_only || m.req_mask != all) return false;
+            for (uint32_t f = 0; f < ms.n_fields; f++)
+                if (m.req[f] < 0 || m.req[f] > (int64_t)UINT32_MAX) return false;
+        }
+        auto hash = [&](uint32_t seed, const DMSig& m) {
+            uint32_t h = seed;
+            for (uint32_t f = 0; f < ms.n_fields; f++) h = msig_mix(h, (uint32_t)m.req[f]);
+            return msig_fin(h);
+        };
+        for (uint32_t cap = 4; cap <= kMHashCap; cap <<= 1) {
+            if (cap < 2 * ms.n_sigs) continue;
+            for (uint32_t attempt = 0; attempt < 32; attempt++) {
+                const uint32_t s0 = 0x2545F491u * (2 * attempt + 1), s1 = 0x9E3779B9u * (2 * attempt + 2);
+                std::vector<uint32_t> slot(cap, kMHashEmpty);
+                bool ok = true;
+                for (uint32_t q = 0; q < ms.n_sigs && ok; q++) {
+                    uint32_t cur = q, pos = hash(s0, msig[q]) & (cap - 1);
+                    for (uint32_t kick = 0;; kick++) {
+                        if (slot[pos] == kMHashEmpty) { slot[pos] = cur; break; }
+                        if (kick == 4 * cap) { ok = false; break; }
+                        std::swap(cur, slot[pos]);  // evict; the evicted key goes to its other position
+                        const uint32_t p0 = hash(s0, msig[cur]) & (cap - 1), p1 = hash(s1, msig[cur]) & (cap - 1);
+                        pos = pos == p0 ? p1 : p0;
+                    }
+                }
+                if (!ok) continue;
+                // distinct values: two signatures with equal keys would share both positions
+                for (uint32_t q = 0; q < ms.n_sigs; q++)
+                    for (uint32_t r = q + 1; r < ms.n_sigs; r++) {
+                        bool eq = true;
+                        for (uint32_t f = 0; f < ms.n_fields; f++) eq = eq && msig[q].req[f] == msig[r].req[f];
+                        if (eq) return false;
+                    }
+                htab.assign(cap, DMHashEntry{});
+                for (uint32_t p = 0; p < cap; p++) {
+                    DMHashEntry& e = htab[p];
+                    e.q = slot[p];
+                    if (slot[p] == kMHashEmpty) continue;
+                    const DMSig& m = msig[slot[p]];
+                    for (uint32_t f = 0; f < ms.n_fields; f++) e.key[f] = (uint32_t)m.req[f];
+                    e.tmin = m.tmin;
+                    e.tmax = m.tmax;
+                }
+                ms.hmask = cap - 1;
+                ms.hseed[0] = s0;
+                ms.hseed[1] = s1;
+                return true;
+            }
+        }
+        return false;
     }
 
     // overlap: host work run while the batch's kernels and copies are in
@@ -408,29 +494,38 @@ struct Replay : ReplayCore {
         const uint64_t scan_end = off;
         const bool slots_only = c.slot_lists_mode_ && full_var.empty() && !c.row_shard() &&
                                 (!rev || c.slot_lists_rev_) && scan_end > 0;
-        // mscan: signatures (DMSig, clause_off indexing mcl), result cells after the chunks
+        // mscan: signatures (DMSig, clause_off indexing mcl), result cells
+        // after the chunks — one per (signature, chunk) for stitch_kernel, or
+        // one per signature from the hashed scan's own placement
         const uint32_t mchunk = ms.chunk;
         const uint64_t mscratch = scratch;
-        uint32_t mcl_off = 0;
-        msig.clear();
+        const bool hashed = use_m && ms.hmask != 0;
+        const size_t n_stitch = cg_list.size();  // searches stitch_kernel places
+        std::vector<uint64_t> mdst;
         for (uint32_t q = 0; q < m_list.size(); q++) {
             const uint32_t i = m_list[q];
             const DGroup& d = bg[i].d;
-            msig.push_back(make_msig(d, mcl_off));
-            mcl_off += d.n_clauses;
             cg_list.push_back(i);
+            cg_off.push_back(off);
+            if (hashed) {
+                cg_first.push_back((uint32_t)nchunks + q);
+                cg_end.push_back((uint32_t)nchunks + q + 1);
+                mdst.push_back(4 * off);
+                off += d.k;
+                continue;
+            }
             const uint32_t first = (uint32_t)nchunks + q * ms.n_chunks;
             cg_first.push_back(first);
             cg_end.push_back(first + ms.n_chunks);
-            cg_off.push_back(off);
             // u32 cells and output: `so` in slot words from the scratch base
             for (uint32_t ch = 0; ch < ms.n_chunks; ch++)
                 lmap.push_back(DChunkMap{first, ch * mchunk, d.k, 1u, off,
                                          4 * mscratch + ((uint64_t)q * ms.n_chunks + ch) * mchunk});
             off += d.k;
         }
-        const uint32_t ncells = use_m ? ms.n_sigs * ms.n_chunks : 0;
-        if (use_m) scratch += ((uint64_t)ncells * mchunk + 3) / 4;  // 4-B slots in 16-B DHit units
+        const uint32_t ncells = !use_m ? 0 : hashed ? ms.n_sigs : ms.n_sigs * ms.n_chunks;
+        if (hashed) scratch += (mscan_hash_work_words(ms) + 3) / 4;
+        else if (use_m) scratch += ((uint64_t)ncells * mchunk + 3) / 4;  // 4-B slots in 16-B DHit units
         const int ng = (int)lg.size();
         const uint32_t nres = (uint32_t)(nwhole + nchunks) + ncells, nmap = (uint32_t)lmap.size();
         c.h_groups_.reserve(ng);
@@ -447,18 +542,26 @@ struct Replay : ReplayCore {
         c.d_res_.reserve(std::max<uint32_t>(nres, 1), false);
         c.d_out_.reserve(std::max<uint64_t>(off, 1), false);
         if (rev) c.d_rev_.reserve(std::max<uint64_t>(off, 1), false);
+        if (nmap || hashed) c.d_scan_.reserve(std::max<uint64_t>(scratch, 1), false);
         if (nmap) {
-            c.d_scan_.reserve(scratch, false);
             c.h_map_.reserve(nmap);
             std::memcpy(c.h_map_.p, lmap.data(), nmap * sizeof(DChunkMap));
             c.d_map_.reserve(nmap, false);
             NKM_HIP(hipMemcpyAsync(c.d_map_.p, c.h_map_.p, nmap * sizeof(DChunkMap), hipMemcpyHostToDevice, stream));
         }
         if (use_m) {
-            c.h_msig_.reserve(msig.size());
-            std::memcpy(c.h_msig_.p, msig.data(), msig.size() * sizeof(DMSig));
-            c.d_msig_.reserve(msig.size(), false);
-            NKM_HIP(hipMemcpyAsync(c.d_msig_.p, c.h_msig_.p, msig.size() * sizeof(DMSig), hipMemcpyHostToDevice, stream));
+            // the signatures; hashed: then the output word offsets and the table
+            const size_t blob = hashed ? mscan_hash_blob_bytes(ms.n_sigs, ms.hmask + 1) : msig.size() * sizeof(DMSig);
+            const size_t nblob = (blob + sizeof(DMSig) - 1) / sizeof(DMSig);
+            c.h_msig_.reserve(nblob);
+            char* hb = reinterpret_cast<char*>(c.h_msig_.p);
+            std::memcpy(hb, msig.data(), msig.size() * sizeof(DMSig));
+            if (hashed) {
+                std::memcpy(hb + msig.size() * sizeof(DMSig), mdst.data(), mdst.size() * sizeof(uint64_t));
+                std::memcpy(hb + mscan_hash_table_off(ms.n_sigs), htab.data(), htab.size() * sizeof(DMHashEntry));
+            }
+            c.d_msig_.reserve(nblob, false);
+            NKM_HIP(hipMemcpyAsync(c.d_msig_.p, c.h_msig_.p, blob, hipMemcpyHostToDevice, stream));
             c.h_mcl_.reserve(std::max<size_t>(mcl.size(), 1));
             std::memcpy(c.h_mcl_.p, mcl.data(), mcl.size() * sizeof(DClause));
             c.d_mcl_.reserve(std::max<size_t>(mcl.size(), 1), false);
@@ -536,7 +639,12 @@ struct Replay : ReplayCore {
         }
         NKM_HIP(launch_scan(st, c.d_groups_.p + nwhole, nchunks, c.d_scan_.p, c.d_res_.p + nwhole, stream, c.ev_[2],
                             c.ev_[3]));
-        if (use_m)
+        stats.mhash |= hashed;
+        if (hashed)
+            NKM_HIP(launch_mscan_hash(st, ms, c.d_msig_.p, reinterpret_cast<uint32_t*>(c.d_scan_.p + mscratch),
+                                      c.d_res_.p + nwhole + nchunks, reinterpret_cast<uint32_t*>(c.d_out_.p), stream,
+                                      c.ev_[4], c.ev_[5]));
+        else if (use_m)
             NKM_HIP(launch_mscan(st, ms, c.d_msig_.p, c.d_mcl_.p, reinterpret_cast<uint32_t*>(c.d_scan_.p + mscratch),
                                  c.d_res_.p + nwhole + nchunks,
                                  std::any_of(msig.begin(), msig.end(), [](const DMSig& m) { return !m.term_only; }),
@@ -546,7 +654,7 @@ struct Replay : ReplayCore {
         // one, and its stop event then reads the stitch's end
         NKM_HIP(hipEventRecord(c.ev_[6], stream));
         if (nmap) {
-            const size_t ns = cg_list.size();
+            const size_t ns = hashed ? n_stitch : cg_list.size();
             c.h_cranges_.reserve(2 * ns);
             for (size_t k = 0; k < ns; k++) {
                 c.h_cranges_.p[2 * k] = cg_first[k];
@@ -2644,7 +2752,7 @@ int Core::process(mm_matched* out) {
         }
     }
     const int dk = stats.dominant();  // bench.py's roofline kernel
-    out->eval_kernel = dk;
+    out->eval_kernel = dk == 2 && stats.mhash ? 4 : dk;
     out->eval_ms = stats.k_ms[dk];
     out->pair_evals = stats.pair_evals;
     out->eval_bytes = stats.k_bytes[dk];

@@ -105,6 +105,8 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_GPIPE")) gpipe_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FAST")) fast_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FULLVAR")) full_var_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_MHASH")) mhash_mode_ = std::atoi(e);
+    if (const char* e = std::getenv("NKM_MCONTIG")) mcontig_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_SLOTLISTS")) {
         slot_lists_mode_ = std::strcmp(e, "0") != 0;
         slot_lists_rev_ = std::strcmp(e, "2") == 0;
@@ -1266,6 +1268,8 @@ void Core::build_index() {
         std::stable_sort(order_.begin(), order_.end(), [&](uint32_t a, uint32_t b) { return ckey_[a] < ckey_[b]; });
         order_sorted_ = true;
     }
+    order_identity_ = true;
+    for (uint32_t p = 0; p < n && order_identity_; p++) order_identity_ = order_[p] == p;
     // posting lists for fields used as required-term sources
     postings_map_.clear();
     postings_.clear();

@@ -98,14 +98,23 @@ def run_passes(config, n, passes, cfg, extra=None):
 # NKM_KERNEL routes a batch's constant-score searches to one query-eval
 # kernel at any size (auto picks by size/coverage, which the small oracle
 # workloads here never reach): every kernel is checked against the oracle.
-KERNELS = ["search", "scan", "mscan"]
+# "mhash": mscan with the hashed signature lookup (mscan_hash_kernel) whenever
+# the signatures allow it (by default only past mscan_kernel's 16 signatures,
+# e.g. C4's 64 pools); "mscan16": never hashed (C4 then falls back to scan).
+KERNELS = ["search", "scan", "mscan", "mhash"]
+
+
+def set_kernel(monkeypatch, kernel):
+    monkeypatch.setenv("NKM_KERNEL", "mscan" if kernel in ("mhash", "mscan16") else kernel)
+    if kernel in ("mhash", "mscan16"):
+        monkeypatch.setenv("NKM_MHASH", "1" if kernel == "mhash" else "2")
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("n", [1200, 10_000])
 def test_c1_pool_query(kernel, n, monkeypatch):
     """C1 at its stated 10k (BASELINE configs[0]) on every query-eval kernel."""
-    monkeypatch.setenv("NKM_KERNEL", kernel)
+    set_kernel(monkeypatch, kernel)
     run_passes(1, n, 2, dict(max_intervals=2))
 
 
@@ -156,8 +165,34 @@ def test_c2_partial_parallel_replay(partial, monkeypatch):
 @pytest.mark.parametrize("config", [3, 4])
 def test_c3_c4_at_6k(config, kernel, monkeypatch):
     """C3 (parties, 5v5) and C4 (64 pools) at 6,000 tickets on every kernel."""
-    monkeypatch.setenv("NKM_KERNEL", kernel)
+    set_kernel(monkeypatch, kernel)
     run_passes(config, 6000, 2, dict(max_intervals=2))
+
+
+@pytest.mark.parametrize("kernel", ["mscan", "mhash"])
+@pytest.mark.parametrize("config,n,cfg", [(4, 20_000, dict(max_intervals=2)), (3, 20_000, dict(max_intervals=2)),
+                                          (1, 10_000, dict(max_intervals=2))])
+def test_hashed_mscan(config, n, cfg, kernel, monkeypatch):
+    """The hashed mscan (one table probe per candidate, signature-major
+    placement over chunks): C4's 64 pool signatures take it by default, C3's 8
+    and C1's when forced; every list must equal the oracle's and the batch
+    must have run on mscan (eval_kernel 2, hashed 4), not the scan fallback."""
+    set_kernel(monkeypatch, kernel)
+    rs = run_passes(config, n, 2, cfg)
+    assert rs[0].eval_kernel == (4 if kernel == "mhash" or config == 4 else 2)
+
+
+@pytest.mark.parametrize("contig,j", [("0", "2"), ("0", "4"), ("1", "4"), ("1", "8")])
+def test_hashed_mscan_chunk_lengths(contig, j, monkeypatch):
+    """Every chunk shape of the hashed scan: gathered through the scan order
+    (2 or 4 candidates per lane) and over contiguous slot runs (4 or 8 per
+    lane, 16-B column loads), with ragged first and last chunks (the second
+    pass starts past a matched prefix)."""
+    set_kernel(monkeypatch, "mhash")
+    monkeypatch.setenv("NKM_MCONTIG", contig)
+    monkeypatch.setenv("NKM_MHASH_J" if contig == "0" else "NKM_MCONTIG_J", j)
+    run_passes(4, 9_999, 2, dict(max_intervals=2))
+    run_passes(3, 7_777, 2, dict(max_intervals=2))
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -166,7 +201,7 @@ def test_datetime_props_and_date_ranges(kernel, monkeypatch):
     (indexed as raw-UnixNano numeric terms, match_common.go:161-170,221-236)
     mixed with strings none parses (keywords), queried with RFC3339 date-range
     clauses (query_string_parser.go:234-250; ConstantScorer(1))."""
-    monkeypatch.setenv("NKM_KERNEL", kernel)
+    set_kernel(monkeypatch, kernel)
     run_passes(8, 3000, 3, dict(max_intervals=3))
 
 
@@ -193,7 +228,7 @@ def test_wide_queries(kernel, monkeypatch):
     """Config 10: queries over 1-6 distinct keyword / numeric fields with every
     occur: the kernels' preloaded-column evaluation (search/rsmall <= 4 fields,
     scan <= 2) and its per-clause fallback beyond, on every kernel."""
-    monkeypatch.setenv("NKM_KERNEL", kernel)
+    set_kernel(monkeypatch, kernel)
     run_passes(10, 3000, 3, dict(max_intervals=3))
 
 
@@ -230,7 +265,7 @@ def test_rev_threshold_fired(config, n, mi):
 
 
 HOST_KERNEL = [("0", "1", "search"), ("force", "1", "scan"), ("force", "1", "mscan"), ("force", "0", "mscan"),
-               ("0", "1", "mscan")]
+               ("0", "1", "mscan"), ("force", "1", "mhash"), ("force", "1", "mscan16")]
 
 
 @pytest.mark.parametrize("par,dense,kernel", HOST_KERNEL)
@@ -240,7 +275,7 @@ def test_c3_parties_5v5(par, dense, kernel, monkeypatch):
     pool walk; NKM_KERNEL: the query-eval kernel."""
     monkeypatch.setenv("NKM_PARALLEL", par)
     monkeypatch.setenv("NKM_DENSE", dense)
-    monkeypatch.setenv("NKM_KERNEL", kernel)
+    set_kernel(monkeypatch, kernel)
     run_passes(3, 1500, 2, dict(max_intervals=2))
 
 
@@ -259,7 +294,7 @@ def test_pipelined_merge(config, n, passes, pipe, monkeypatch):
 def test_c4_many_pools(par, dense, kernel, monkeypatch):
     monkeypatch.setenv("NKM_PARALLEL", par)
     monkeypatch.setenv("NKM_DENSE", dense)
-    monkeypatch.setenv("NKM_KERNEL", kernel)
+    set_kernel(monkeypatch, kernel)
     run_passes(4, 1500, 1, dict(max_intervals=2))
 
 
@@ -334,7 +369,7 @@ def test_c5_override_candidates(config, n, devenum, monkeypatch):
 def test_mixed_parties_ranges_minmax(par, dense, kernel, monkeypatch):
     monkeypatch.setenv("NKM_PARALLEL", par)
     monkeypatch.setenv("NKM_DENSE", dense)
-    monkeypatch.setenv("NKM_KERNEL", kernel)
+    set_kernel(monkeypatch, kernel)
     run_passes(6, 1000, 3, dict(max_intervals=3))
 
 
@@ -486,7 +521,7 @@ def test_large_pool_properties(n):
 def _product_passes(config, n, passes, par, monkeypatch, dense="1", kernel="auto", fast="1"):
     monkeypatch.setenv("NKM_PARALLEL", par)
     monkeypatch.setenv("NKM_DENSE", dense)
-    monkeypatch.setenv("NKM_KERNEL", kernel)
+    set_kernel(monkeypatch, kernel)
     monkeypatch.setenv("NKM_FAST", fast)
     ts = synth.TicketSet(config, n)
     mm = capi.Matchmaker(product_lib(), max_intervals=2)
@@ -538,7 +573,7 @@ def test_multi_term_passes(kernel, page, fullvar, monkeypatch):
     """Config 7: blocked-list regexps, alternations, wildcards, fuzzy (variable
     scores), a pattern that fails every search; every query-eval kernel;
     truncated lists paged by any row (NKM_PAGE=1) or by batch restarts."""
-    monkeypatch.setenv("NKM_KERNEL", kernel)
+    set_kernel(monkeypatch, kernel)
     monkeypatch.setenv("NKM_PAGE", page)
     monkeypatch.setenv("NKM_FULLVAR", fullvar)
     rs = run_passes(7, 1200, 3, dict(max_intervals=3))
