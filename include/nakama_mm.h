@@ -63,7 +63,8 @@ typedef struct mm_config {
     int32_t interval_sec;    /* interval_sec (informational: the caller drives Process) */
     int32_t max_intervals;   /* max_intervals, default 2 */
     int32_t rev_precision;   /* rev_precision (bool) */
-    int32_t rev_threshold;   /* rev_threshold; the wall-clock cutoff is pinned off */
+    int32_t rev_threshold;   /* rev_threshold: reverse checks stop interval_sec * rev_threshold s into a pass
+                                (matchmaker_process.go:31-46); bench.py pins it to 0 */
     int32_t override_enabled;/* a MatchmakerOverride is registered -> processCustom path (matchmaker.go:314) */
     int32_t device;          /* HIP device ordinal for this handle (one process per GPU) */
     const char* node;        /* this node's name (config.GetName(), matchmaker.go:225) */
@@ -123,7 +124,7 @@ typedef struct mm_matched {
     int64_t eval_bytes;             /* algorithmic bytes of the search launches (DESIGN.md roofline) */
     int32_t eval_launches;          /* search kernel launches in the pass */
     int32_t n_batches;              /* replay batches */
-    int32_t eval_kernel;            /* query-eval kernel with the most bytes: 0 search, 1 scan, 2 mscan, 3 rsmall, 4 hashed mscan */
+    int32_t eval_kernel;            /* query-eval kernel with the most bytes: 0 search, 1 scan, 2 mscan, 3 rsmall, 4 hashed mscan, 5 rpack */
     int32_t full_lists;             /* variable-score searches run as full lists (host-sorted), 0 for the oracle */
     const int64_t* group_created;   /* n_groups: CreatedAt of each group's last entry (its searching ticket) — the
                                        key a pool-sharded cluster merges rank results by (ABI 3) */

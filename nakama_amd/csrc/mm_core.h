@@ -12,6 +12,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -37,6 +38,8 @@ namespace nkm {
 hipError_t launch_search(const DStore& st, const DGroup* d_groups, int n_groups, DHit* d_out, uint8_t* d_rev,
                          DGroupResult* d_res, hipStream_t stream, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
                          int kinds = 3);
+hipError_t launch_rpack(const DStore& st, const DSmallRow* d_rows, uint32_t n_rows, uint8_t* d_obuf, const PackLayout& L,
+                        hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_rsmall(const DStore& st, const DGroup* d_groups, const uint32_t* d_rows, uint32_t n_rows, DHit* d_out,
                          uint8_t* d_rev, uint32_t* d_pm, DGroupResult* d_res, hipStream_t stream, hipEvent_t ev0,
                          hipEvent_t ev1);
@@ -161,6 +164,11 @@ public:
         for (auto& t : th_) t.join();
     }
     unsigned size() const { return (unsigned)th_.size() + 1; }
+    // A pass issues a few dozen short jobs back to back: after a job a worker
+    // spins on the generation word (spin_window) before it sleeps on the condition
+    // variable, and the caller spins on the done count before it sleeps, so a
+    // job inside a pass starts and ends without futex wake-ups (tens of
+    // microseconds each across 15 threads).
     void run(size_t n, const std::function<void(size_t)>& fn) {
         if (n == 0) return;
         if (n == 1 || th_.empty()) {
@@ -173,16 +181,32 @@ public:
         {
             std::lock_guard<std::mutex> lk(m_);
             job_ = job;
-            gen_++;
+            gen_.fetch_add(1, std::memory_order_release);
         }
-        cv_.notify_all();
+        if (sleepers_.load(std::memory_order_acquire) > 0) cv_.notify_all();
         work(*job);
-        std::unique_lock<std::mutex> lk(m_);
-        done_cv_.wait(lk, [&] { return job->done.load() == n; });
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t k = 0; job->done.load(std::memory_order_acquire) != n; k++) {
+            if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > spin_window()) {
+                std::unique_lock<std::mutex> lk(m_);
+                done_cv_.wait(lk, [&] { return job->done.load() == n; });
+                break;
+            }
+            relax();
+        }
+        std::lock_guard<std::mutex> lk(m_);
         job_.reset();
     }
 
 private:
+    // spin window (NKM_SPIN_US, default 30): long enough to bridge the host
+    // code between a pass's back-to-back jobs, short enough that idle workers
+    // do not steal cycles (SMT siblings) from a long job's busy ones
+    static std::chrono::microseconds spin_window() {
+        static const std::chrono::microseconds w{std::getenv("NKM_SPIN_US") ? std::atol(std::getenv("NKM_SPIN_US")) : 30};
+        return w;
+    }
+    static inline void relax() { __builtin_ia32_pause(); }
     struct Job {
         Job(const std::function<void(size_t)>* f, size_t count) : fn(f), n(count) {}
         const std::function<void(size_t)>* fn;
@@ -205,12 +229,22 @@ private:
     void loop() {
         uint64_t seen = 0;
         for (;;) {
+            // spin for the next job of the same pass, then sleep
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint32_t k = 0; gen_.load(std::memory_order_acquire) == seen; k++) {
+                if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > spin_window()) break;
+                relax();
+            }
             std::shared_ptr<Job> j;
             {
                 std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                if (!quit_ && gen_.load() == seen) {
+                    sleepers_.fetch_add(1);
+                    cv_.wait(lk, [&] { return quit_ || gen_.load() != seen; });
+                    sleepers_.fetch_sub(1);
+                }
                 if (quit_) return;
-                seen = gen_;
+                seen = gen_.load();
                 j = job_;
             }
             if (j) work(*j);
@@ -220,7 +254,8 @@ private:
     std::mutex m_;
     std::condition_variable cv_, done_cv_;
     std::shared_ptr<Job> job_;
-    uint64_t gen_ = 0;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> sleepers_{0};
     bool quit_ = false;
 };
 
@@ -388,6 +423,7 @@ struct PassStats {
     // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel
     double k_ms[4] = {0, 0, 0, 0};      // HIP-event time of the launches
     bool mhash = false;                 // a batch's mscan ran hashed (mscan_hash_kernel)
+    bool rpack = false;                 // kernel 3's launches were packed batches (rpack_kernel)
     int64_t k_bytes[4] = {0, 0, 0, 0};  // algorithmic bytes
     int k_launches[4] = {0, 0, 0, 0};
     int64_t pair_evals = 0;
@@ -579,7 +615,7 @@ private:
     // the pass (processDefault), so members of a dropped group leave it
     void finish_pass_serial(GroupList& groups, bool selected);
     void fill_matched(const GroupList& groups, mm_matched* out, bool cands);
-    bool finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& groups, mm_matched* out);
+    bool finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& groups, mm_matched* out, bool mutated);
     void choose_source(const Sig& s, DGroup& g, SrcChoice* ch = nullptr);
     void source_of(const Sig& s, DGroup& g, SrcChoice* ch = nullptr) const;
     struct ParPlan {  // a batch's pools (plan_parallel), bucketed while its searches run
@@ -589,6 +625,7 @@ private:
         std::vector<uint32_t> pool_off;     // CSR: pool p's batch rows are pool_rows[pool_off[p], pool_off[p+1])
         std::vector<uint32_t> pool_rows;    // ascending per pool
         std::vector<uint8_t> self_rows;     // per pool: every row carries its own search's terms
+        std::vector<uint32_t> pool_key1;    // one key field: each pool's term
     };
     struct RowRec {  // a batch row's outcome in a parallel replay (indexed by batch row)
         uint32_t ent, len, task;  // its group's entries: task_ents_[task][ent, ent + len)
@@ -597,14 +634,41 @@ private:
     std::vector<RowRec> row_recs_;
     std::vector<std::vector<std::pair<uint32_t, int>>> task_ents_;
     std::vector<uint32_t> pool_remap_;  // dictionary id -> pool (one-field pool keys)
+    std::unique_ptr<std::atomic<uint32_t>[]> pool_first_;  // dictionary id -> first search with it
+    size_t pool_first_cap_ = 0;
+    UVec<uint32_t> pool_cnt_;            // plan_pools: [chunk][pool] row counts, then positions
+    UVec<uint8_t> pool_foreign_;         // plan_pools: [chunk][pool] a row not known to self-match
     ParPlan par_plan_;
     bool plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                        const UVec<uint32_t>& brow_group, ParPlan& P, PassStats& stats);
+    template <class SigOf, class GroupOf>
+    bool plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, const UVec<uint32_t>& brow, ParPlan& P,
+                    PassStats& stats);
     bool replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                          const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                          GroupList& out_groups,
                          std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats,
-                         bool rev, uint32_t* min_stop);
+                         bool rev, uint32_t* min_stop, const std::function<BGroup&(uint32_t)>* view = nullptr);
+    // ---- packed RevPrecision batches (rpack_kernel) ----
+    // A RevPrecision batch whose every row searches a source of <= 64
+    // entries: rows go to the device as 12-B DSmallRows, the lists come back
+    // fixed-stride in one buffer (pack_layout), and the replay reads each row
+    // through a thread-local BGroup view — no per-row search descriptors.
+    struct PackBatch {
+        size_t n = 0;        // rows in the batch
+        size_t end = 0;      // pass rows consumed (rows[pos, end))
+        int S = 8;           // list stride: the longest source, rounded up to 8 / 16 / 32 / 64
+        uint64_t scanned = 0;
+        double live_w = 0;   // sum over rows of src_len x the row's per-live-candidate bytes
+    };
+    bool pack_mode_ = true;  // NKM_RPACK=0: RevPrecision batches search per row (rsmall / search_kernel)
+    UVec<DSmallRow> pk_tmp_;
+    PinnedArray<DSmallRow> h_srows_;
+    DevArray<DSmallRow> d_srows_;
+    DevArray<uint8_t> d_pack_;
+    PinnedArray<uint8_t> h_pack_;
+    bool assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t cap, UVec<uint32_t>& brow, PackBatch& pb);
+    PackLayout run_packed(const PackBatch& pb, PassStats& stats, const std::function<void()>& overlap);
     std::vector<uint8_t> dec_;  // per pass: rows a parallel replay decided ahead of the pass's row pointer
     void apply_selected_to_device(const uint32_t* slots, size_t n);
     // A batch's selections reach the device alive mask before the next

@@ -152,12 +152,51 @@ struct DMSig {
 };
 static_assert(sizeof(DMSig) == 64, "DMSig is 64 bytes");
 
+// One row of a packed RevPrecision batch (rpack_kernel): every search of the
+// batch is one searching ticket over a short source, so the descriptor is the
+// ticket's slot (its query, Min/MaxCount and the reverse-check document are
+// store columns) and its source range.
+constexpr uint32_t kSrcOrder = 0x80000000u;  // src_len flag: the source is order[], else postings[]
+struct DSmallRow {
+    uint32_t slot;
+    uint32_t src_off;
+    uint32_t src_len;  // <= 64 entries, | kSrcOrder
+};
+static_assert(sizeof(DSmallRow) == 12, "DSmallRow is 12 bytes");
+
+// rpack_kernel's output for n rows of stride S (8, 16, 32 or 64 entries), one
+// buffer with 256-B aligned sections: per row S slot ids (u32), min(S, 32)
+// pair-matrix words of S bits (u8 / u16 / u32), S reverse-check bits in
+// entry order (u8 / u16 / u32 / u64) and the entry count (u8); then per
+// workgroup its live candidates and its entries (2 x u32: the roofline's bytes).
+constexpr int kPackRowsPerBlock(int S) { return 4 * (64 / S); }
+struct PackLayout {
+    uint64_t slot, pm, rev, cnt, live, total;
+    uint32_t blocks;
+    int S, pm_w, rev_w;
+};
+NKM_HD inline PackLayout pack_layout(uint64_t n, int S) {
+    auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    PackLayout L{};
+    L.S = S;
+    L.pm_w = S <= 8 ? 1 : S <= 16 ? 2 : 4;
+    L.rev_w = S / 8;
+    L.blocks = (uint32_t)((n + kPackRowsPerBlock(S) - 1) / kPackRowsPerBlock(S));
+    L.slot = 0;
+    L.pm = al(L.slot + n * S * 4);
+    L.rev = al(L.pm + n * (S < 32 ? S : 32) * L.pm_w);
+    L.cnt = al(L.rev + n * L.rev_w);
+    L.live = al(L.cnt + n);
+    L.total = al(L.live + (uint64_t)L.blocks * 8);
+    return L;
+}
+
 // Placement of one scan chunk (scan_kernel / mscan_kernel -> stitch_kernel).
 struct DChunkMap {
     uint32_t first;    // result index of the search's first chunk
     uint32_t start;    // chunk's first source position within the search
     uint32_t cap;      // the search's output capacity (k)
-    uint32_t u32;      // 1: the cell and the output hold 4-B slot ids (mscan), `so` / dst in slot words
+    uint32_t u32;      // 1: the cell and the output hold 4-B slot ids (mscan), `so` / dst_off in slot words
     uint64_t dst_off;  // the search's first output entry
     uint64_t so;       // the chunk's compacted hits in the scratch buffer
 };

@@ -1156,12 +1156,12 @@ __global__ __launch_bounds__(kBlock) void stitch_kernel(const DChunkMap* __restr
     const uint32_t prefix = offs[c];
     const uint32_t n = cres[c].count;
     const uint64_t so = mp.so;
-    if (mp.u32) {  // an mscan cell: 4-B slot ids, offsets in slot words
+    if (mp.u32) {  // an mscan cell: 4-B slot ids, `so` and dst_off in slot words
         const uint32_t* __restrict__ s32 = reinterpret_cast<const uint32_t*>(scratch);
         uint32_t* __restrict__ o32 = reinterpret_cast<uint32_t*>(out);
         const uint32_t lim = mp.cap > prefix ? mp.cap - prefix : 0u;
         const uint32_t m = n < lim ? n : lim;
-        for (uint32_t e = tid; e < m; e += 64) o32[4 * mp.dst_off + prefix + e] = s32[so + e];
+        for (uint32_t e = tid; e < m; e += 64) o32[mp.dst_off + prefix + e] = s32[so + e];
         return;
     }
     for (uint32_t e = tid; e < n; e += 64) {
@@ -1385,6 +1385,124 @@ __global__ __launch_bounds__(kBlock) void rsmall_kernel(DStore st, const DGroup*
     }
     const uint32_t nlive = (uint32_t)__popcll(__ballot(live));
     if (lane == 0) res[gi] = DGroupResult{cnt, 1u, g.src_len, cnt, nlive, 0u};
+}
+
+// ---- packed RevPrecision rows (rpack_kernel) -------------------------------------
+// A RevPrecision batch whose every search is one row over a source of at most
+// S entries (C5: buckets of 8 -> S = 8) packs 64 / S rows into each wave
+// (rsmall_kernel's one row per wave left 56 of 64 lanes idle on C5): lane j
+// of a row's S-lane segment evaluates source entry j — the predicate with the
+// row's own query and count range, its score key, and the reverse check
+// Q_H(T).  The segment's ballot bits rank the matches by (score key desc,
+// source position asc), search_kernel's top-K order, in S wave-uniform shuffle
+// steps; a second S steps give every entry its pair-matrix row (bit b: entry
+// b's document matches this entry's query) and the row its reverse bits in
+// entry order.  Outputs are fixed-stride per row (pack_layout: no offsets, no
+// per-row result record, no 80-B descriptor — the row is its 12-B DSmallRow).
+template <int S> struct PackT;
+template <> struct PackT<8> { using pm = uint8_t; using rv = uint8_t; };
+template <> struct PackT<16> { using pm = uint16_t; using rv = uint16_t; };
+template <> struct PackT<32> { using pm = uint32_t; using rv = uint32_t; };
+template <> struct PackT<64> { using pm = uint32_t; using rv = uint64_t; };
+
+template <int S>
+__global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRow* __restrict__ rows, uint32_t n_rows,
+                                                       uint8_t* __restrict__ obuf, PackLayout L) {
+    using PmT = typename PackT<S>::pm;
+    using RvT = typename PackT<S>::rv;
+    constexpr int R = 64 / S;           // rows per wave
+    constexpr int P = S < 32 ? S : 32;  // pair-matrix entries per row
+    __shared__ uint32_t wlive[kWaves], wmatch[kWaves];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int seg = lane / S, j = lane % S, base = seg * S;
+    const uint32_t r = (blockIdx.x * kWaves + wave) * R + seg;
+    const bool have = r < n_rows;
+    DSmallRow d{0u, 0u, 0u};
+    if (have) d = rows[r];
+    const uint32_t len = d.src_len & ~kSrcOrder;
+    bool m = false, live = false, rv = false;
+    uint32_t s = kNoSlot;
+    int64_t key = 0;
+    if (have && (uint32_t)j < len) {
+        s = ((d.src_len & kSrcOrder) ? st.order : st.postings)[d.src_off + j];
+        live = st.alive[s] != 0;
+        if (live) {
+            m = st.minc[s] >= st.minc[d.slot] && st.maxc[s] <= st.maxc[d.slot];
+            if (m) {
+                const DQuery q = st.squery[d.slot];
+                double sp = 0.0;
+                m = eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, s, &sp);
+                key = dsortable((sp + 1.0) + 1.0);
+            }
+            if (m) {
+                const DQuery h = st.squery[s];
+                double dd;
+                rv = eval_parsed(st, h.kind, st.clauses + h.clause_off, h.n_clauses, d.slot, &dd);
+            }
+        }
+    }
+    const uint64_t ball = __ballot(m);
+    const uint64_t mine = S == 64 ? ball : (ball >> base) & ((1ull << (S & 63)) - 1);
+    uint32_t rank = 0;
+#pragma unroll
+    for (int i = 0; i < S; i++) {
+        const int64_t ki = __shfl(key, base + i);
+        rank += (uint32_t)(((mine >> i) & 1) && (ki > key || (ki == key && i < j)));
+    }
+    PmT pmask = 0;
+    RvT rbits = 0;
+    const DQuery q = m ? st.squery[s] : DQuery{0u, 0, 0, 0};
+    for (int i = 0; i < S; i++) {
+        const uint32_t si = (uint32_t)__shfl((int)s, base + i);
+        const uint32_t ri = (uint32_t)__shfl((int)rank, base + i);
+        const int rvi = __shfl((int)rv, base + i);
+        if (!((mine >> i) & 1)) continue;  // segment-uniform: the shuffles above ran on every lane
+        if (rvi) rbits |= (RvT)((RvT)1 << ri);
+        if (m && rank < (uint32_t)P && ri < (uint32_t)P) {
+            double dd;
+            if (eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, si, &dd)) pmask |= (PmT)((PmT)1 << ri);
+        }
+    }
+    uint32_t* __restrict__ o_slot = reinterpret_cast<uint32_t*>(obuf + L.slot);
+    PmT* __restrict__ o_pm = reinterpret_cast<PmT*>(obuf + L.pm);
+    RvT* __restrict__ o_rev = reinterpret_cast<RvT*>(obuf + L.rev);
+    if (m) o_slot[(uint64_t)r * S + rank] = s;
+    if (m && rank < (uint32_t)P) o_pm[(uint64_t)r * P + rank] = pmask;
+    if (have && j == 0) {
+        o_rev[r] = rbits;
+        obuf[L.cnt + r] = (uint8_t)__popcll(mine);
+    }
+    const uint32_t wl = (uint32_t)__popcll(__ballot(live)), wm = (uint32_t)__popcll(ball);
+    if (lane == 0) {
+        wlive[wave] = wl;
+        wmatch[wave] = wm;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0, u = 0;
+        for (int w = 0; w < kWaves; w++) {
+            t += wlive[w];
+            u += wmatch[w];
+        }
+        uint32_t* o = reinterpret_cast<uint32_t*>(obuf + L.live) + 2 * (uint64_t)blockIdx.x;
+        o[0] = t;
+        o[1] = u;
+    }
+}
+
+hipError_t launch_rpack(const DStore& st, const DSmallRow* d_rows, uint32_t n_rows, uint8_t* d_obuf, const PackLayout& L,
+                        hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
+    if (n_rows == 0) return hipSuccess;
+    if (L.blocks != (n_rows + kPackRowsPerBlock(L.S) - 1) / kPackRowsPerBlock(L.S)) return hipErrorInvalidValue;
+    const dim3 grid(L.blocks), block(kBlock);
+    switch (L.S) {
+        case 8: hipExtLaunchKernelGGL(rpack_kernel<8>, grid, block, 0, stream, ev0, ev1, 0, st, d_rows, n_rows, d_obuf, L); break;
+        case 16: hipExtLaunchKernelGGL(rpack_kernel<16>, grid, block, 0, stream, ev0, ev1, 0, st, d_rows, n_rows, d_obuf, L); break;
+        case 32: hipExtLaunchKernelGGL(rpack_kernel<32>, grid, block, 0, stream, ev0, ev1, 0, st, d_rows, n_rows, d_obuf, L); break;
+        case 64: hipExtLaunchKernelGGL(rpack_kernel<64>, grid, block, 0, stream, ev0, ev1, 0, st, d_rows, n_rows, d_obuf, L); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_rsmall(const DStore& st, const DGroup* d_groups, const uint32_t* d_rows, uint32_t n_rows, DHit* d_out,

@@ -501,28 +501,37 @@ struct Replay : ReplayCore {
         const uint64_t mscratch = scratch;
         const bool hashed = use_m && ms.hmask != 0;
         const size_t n_stitch = cg_list.size();  // searches stitch_kernel places
+        // The mscan lists are 4-B slot ids packed back to back from slot word
+        // 4 * off (cg_off holds each list's first slot word): one contiguous
+        // region the first D2H round can copy whole (below).
         std::vector<uint64_t> mdst;
+        const uint64_t mw0 = 4 * off;
+        uint64_t mw = mw0;
         for (uint32_t q = 0; q < m_list.size(); q++) {
             const uint32_t i = m_list[q];
             const DGroup& d = bg[i].d;
             cg_list.push_back(i);
-            cg_off.push_back(off);
+            cg_off.push_back(mw);
             if (hashed) {
                 cg_first.push_back((uint32_t)nchunks + q);
                 cg_end.push_back((uint32_t)nchunks + q + 1);
-                mdst.push_back(4 * off);
-                off += d.k;
+                mdst.push_back(mw);
+                mw += d.k;
                 continue;
             }
             const uint32_t first = (uint32_t)nchunks + q * ms.n_chunks;
             cg_first.push_back(first);
             cg_end.push_back(first + ms.n_chunks);
-            // u32 cells and output: `so` in slot words from the scratch base
+            // u32 cells and output: `so` and dst_off in slot words
             for (uint32_t ch = 0; ch < ms.n_chunks; ch++)
-                lmap.push_back(DChunkMap{first, ch * mchunk, d.k, 1u, off,
+                lmap.push_back(DChunkMap{first, ch * mchunk, d.k, 1u, mw,
                                          4 * mscratch + ((uint64_t)q * ms.n_chunks + ch) * mchunk});
-            off += d.k;
+            mw += d.k;
         }
+        off += (mw - mw0 + 3) / 4;
+        // copied in the first round when the capacity is at most 2 slot ids
+        // per scanned candidate (C3 / C4: every candidate in at most one list)
+        const bool m_precopy = use_m && !c.row_shard() && mw - mw0 <= 2 * (uint64_t)ms.src_len;
         const uint32_t ncells = !use_m ? 0 : hashed ? ms.n_sigs : ms.n_sigs * ms.n_chunks;
         if (hashed) scratch += (mscan_hash_work_words(ms) + 3) / 4;
         else if (use_m) scratch += ((uint64_t)ncells * mchunk + 3) / 4;  // 4-B slots in 16-B DHit units
@@ -722,6 +731,10 @@ struct Replay : ReplayCore {
             } else if (whole_off) {
                 NKM_HIP(hipMemcpyAsync(c.h_out_.p, c.d_out_.p, whole_off * sizeof(DHit), hipMemcpyDeviceToHost, stream));
             }
+            if (m_precopy && mw > mw0)
+                NKM_HIP(hipMemcpyAsync(reinterpret_cast<uint32_t*>(c.h_out_.p) + mw0,
+                                       reinterpret_cast<const uint32_t*>(c.d_out_.p) + mw0, (mw - mw0) * sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, stream));
             if (rev) NKM_HIP(hipMemcpyAsync(c.h_rev_.p, c.d_rev_.p, off, hipMemcpyDeviceToHost, stream));
             if (need_pm && whole_off)
                 NKM_HIP(hipMemcpyAsync(c.h_pm_.p, c.d_pm_.p, whole_off * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -812,7 +825,8 @@ struct Replay : ReplayCore {
         const auto r4 = rclk::now();
         stats.rb_post_ms += rms(r3, r4);
         // chunked / mscan searches: exact hit counts are known now; copy just
-        // those (an mscan list: 4-B slot ids, in the first quarter of its region)
+        // those (an mscan list: 4-B slot ids, copied in the first round when
+        // m_precopy)
         const size_t n_scan_cg = cg_list.size() - (use_m ? m_list.size() : 0);
         for (size_t k = 0; k < cg_list.size(); k++) {
             BGroup& g = bg[cg_list[k]];
@@ -824,18 +838,23 @@ struct Replay : ReplayCore {
             if (slots && !complete)  // mscan lists are sized to their whole source (plan above)
                 throw DeviceError{hipErrorUnknown, "mscan list cut", __LINE__};
             const bool packed = !slots && slots_only;  // a chunked list: slot ids + its last DHit
-            if (n && packed) {
+            uint32_t* const h32 = reinterpret_cast<uint32_t*>(c.h_out_.p);
+            if (slots) {  // an mscan list: cg_off is its first slot word
+                if (n && !m_precopy)
+                    NKM_HIP(hipMemcpyAsync(h32 + cg_off[k], reinterpret_cast<const uint32_t*>(c.d_out_.p) + cg_off[k],
+                                           n * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+            } else if (n && packed) {
                 NKM_HIP(hipMemcpyAsync(c.h_slots_.p + cg_off[k], c.d_slots_.p + cg_off[k], n * sizeof(uint32_t),
                                        hipMemcpyDeviceToHost, stream));
                 NKM_HIP(hipMemcpyAsync(c.h_last_.p + nwhole + k, c.d_out_.p + cg_off[k] + n - 1, sizeof(DHit),
                                        hipMemcpyDeviceToHost, stream));
             } else if (n) {
-                NKM_HIP(hipMemcpyAsync(c.h_out_.p + cg_off[k], c.d_out_.p + cg_off[k], n * (slots ? 4 : sizeof(DHit)),
+                NKM_HIP(hipMemcpyAsync(c.h_out_.p + cg_off[k], c.d_out_.p + cg_off[k], n * sizeof(DHit),
                                        hipMemcpyDeviceToHost, stream));
             }
             g.head = 0;
             g.last_i = packed ? (uint32_t)(nwhole + k) : UINT32_MAX;
-            if (slots) g.set_slots(reinterpret_cast<const uint32_t*>(c.h_out_.p + cg_off[k]));
+            if (slots) g.set_slots(h32 + cg_off[k]);
             else if (packed) g.set_slots(c.h_slots_.p + cg_off[k]);
             else g.set_hits(c.h_out_.p + cg_off[k]);
             g.rev = nullptr;
@@ -844,7 +863,7 @@ struct Replay : ReplayCore {
             g.n = (uint32_t)n;
             g.complete = complete;
         }
-        if (!cg_list.empty()) NKM_HIP(hipStreamSynchronize(stream));
+        if (n_scan_cg || (use_m && !m_precopy)) NKM_HIP(hipStreamSynchronize(stream));
         stats.rb_lists_ms += rms(r4, rclk::now());
     }
 
@@ -877,8 +896,18 @@ struct Replay : ReplayCore {
 // on the device.  Returns false when the batch does not partition into pools.
 bool Core::plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                          const UVec<uint32_t>& brow_group, ParPlan& P, PassStats& stats) {
+    return plan_pools(
+        bg.size(), [&](size_t i) { return bg[i].sig; }, [&](size_t bi) { return brow_group[bi]; }, brow, P, stats);
+}
+
+// plan_parallel over `nsearch` searches: sig_of(i) is search i's signature,
+// group_of(bi) batch row bi's search (a packed RevPrecision batch: the row
+// itself).  Every step is a parallel sweep over the searches or the rows; the
+// pools are numbered in first-appearance order (C5: 125k pools per 1M rows).
+template <class SigOf, class GroupOf>
+bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, const UVec<uint32_t>& brow, ParPlan& P,
+                      PassStats& stats) {
     P.ok = false;
-    const size_t nsearch = bg.size();
     if (nsearch < 2) return false;
     using clk = std::chrono::steady_clock;
     auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -886,23 +915,29 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& br
     WorkPool& wp = workers();
     const bool par = nsearch >= par_min(65536) && par_mode_;
     const unsigned nsch = par ? wp.size() * 2 : 1;
+    auto sweep = [&](size_t n, unsigned nch, auto&& fn) {  // fn(chunk, lo, hi) over [0, n) in nch chunks
+        if (nch > 1)
+            wp.run(nch, [&](size_t c) { fn(c, n * c / nch, n * (c + 1) / nch); });
+        else
+            fn(0, 0, n);
+    };
     // pool key fields: fields every search requires a keyword term on (the
     // candidates are the first search's; each chunk of searches checks them)
     std::vector<uint16_t> cand;
-    for (auto& mt : sigs_[bg[0].sig].must_terms)
+    for (auto& mt : sigs_[sig_of(0)].must_terms)
         if (std::find(cand.begin(), cand.end(), mt.first) == cand.end()) cand.push_back(mt.first);
     std::vector<std::vector<uint8_t>> has(nsch, std::vector<uint8_t>(cand.size(), 1));
-    auto verify = [&](size_t ch) {
-        for (size_t i = nsearch * ch / nsch; i < nsearch * (ch + 1) / nsch; i++)
+    sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; i++) {
+            const auto& mts = sigs_[sig_of(i)].must_terms;
             for (size_t k = 0; k < cand.size(); k++) {
                 if (!has[ch][k]) continue;
                 bool h = false;
-                for (auto& m2 : sigs_[bg[i].sig].must_terms) h |= m2.first == cand[k];
+                for (auto& m2 : mts) h |= m2.first == cand[k];
                 if (!h) has[ch][k] = 0;
             }
-    };
-    if (nsch > 1) wp.run(nsch, verify);
-    else verify(0);
+        }
+    });
     std::vector<uint16_t> keyf;
     for (size_t k = 0; k < cand.size(); k++) {
         bool all = true;
@@ -915,110 +950,166 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& br
     // pool key of each search; a search requiring two different terms on one
     // field matches nothing (the batch then takes the serial replay).  One key
     // field (C5's buckets: ~10^5 pools): keys extracted on the workers and
-    // pools numbered through a dictionary-id table; more fields (mode x
-    // region: few pools): an ordered map.
+    // pools numbered in parallel through dictionary-id tables; more fields
+    // (mode x region: few pools): an ordered map.
     std::vector<uint32_t>& search_pool = P.search_pool;
-    search_pool.assign(nsearch, 0);
-    std::vector<std::vector<uint32_t>> pool_keys;
-    auto key_of = [&](size_t i, std::vector<uint32_t>& key) {
-        key.assign(keyf.size(), UINT32_MAX);
+    grow_to(search_pool, nsearch);
+    std::vector<uint32_t>& pool_key1 = P.pool_key1;  // one key field: pool -> its term
+    std::vector<std::vector<uint32_t>> pool_keys;    // several: pool -> its terms
+    auto key_of = [&](size_t i, uint32_t* key) {
+        for (size_t k = 0; k < keyf.size(); k++) key[k] = UINT32_MAX;
         for (size_t k = 0; k < keyf.size(); k++)
-            for (auto& mt : sigs_[bg[i].sig].must_terms)
+            for (auto& mt : sigs_[sig_of(i)].must_terms)
                 if (mt.first == keyf[k]) {
                     if (key[k] != UINT32_MAX && key[k] != mt.second) return false;
                     key[k] = mt.second;
                 }
         return true;
     };
-    std::vector<uint32_t> key;
+    size_t ng = 0;
     if (keyf.size() == 1) {
         std::vector<uint32_t>& k1 = search_pool;  // the key term first, renumbered in place below
         std::vector<uint8_t> bad(nsch, 0);
-        auto extract = [&](size_t ch) {
-            std::vector<uint32_t> kk;
-            for (size_t i = nsearch * ch / nsch; i < nsearch * (ch + 1) / nsch; i++) {
-                if (!key_of(i, kk)) { bad[ch] = 1; return; }
+        const size_t nd = dict_.size();
+        // first[t]: the lowest search index with term t (atomic min over the
+        // chunks); the heads (first[t] == i) are numbered in index order
+        if (pool_first_cap_ < nd) {
+            pool_first_.reset(new std::atomic<uint32_t>[nd + nd / 4]);
+            pool_first_cap_ = nd + nd / 4;
+        }
+        std::atomic<uint32_t>* first = pool_first_.get();
+        std::vector<uint32_t>& tpool = pool_remap_;  // term -> pool (written by its head only)
+        grow_to(tpool, nd);
+        sweep(nd, nsch, [&](size_t, size_t lo, size_t hi) {
+            for (size_t t = lo; t < hi; t++) first[t].store(UINT32_MAX, std::memory_order_relaxed);
+        });
+        std::vector<size_t> heads(nsch + 1, 0);
+        sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
+            uint32_t kk[4];
+            for (size_t i = lo; i < hi; i++) {
+                if (!key_of(i, kk) || kk[0] == UINT32_MAX || kk[0] >= nd) { bad[ch] = 1; return; }
                 k1[i] = kk[0];
+                uint32_t cur = first[kk[0]].load(std::memory_order_relaxed);
+                while ((uint32_t)i < cur && !first[kk[0]].compare_exchange_weak(cur, (uint32_t)i, std::memory_order_relaxed)) {
+                }
             }
-        };
-        if (nsch > 1) wp.run(nsch, extract);
-        else extract(0);
+        });
         for (uint8_t b : bad)
             if (b) return false;
-        std::vector<uint32_t>& remap = pool_remap_;
-        remap.assign(dict_.size(), UINT32_MAX);
-        for (size_t i = 0; i < nsearch; i++) {
-            uint32_t& p = remap[k1[i]];
-            if (p == UINT32_MAX) {
-                p = (uint32_t)pool_keys.size();
-                pool_keys.push_back({k1[i]});
-            }
-            k1[i] = p;
-        }
+        sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
+            size_t h = 0;
+            for (size_t i = lo; i < hi; i++) h += first[k1[i]].load(std::memory_order_relaxed) == (uint32_t)i;
+            heads[ch + 1] = h;
+        });
+        for (unsigned ch = 0; ch < nsch; ch++) heads[ch + 1] += heads[ch];
+        ng = heads[nsch];
+        grow_to(pool_key1, ng);
+        sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
+            size_t p = heads[ch];
+            for (size_t i = lo; i < hi; i++)
+                if (first[k1[i]].load(std::memory_order_relaxed) == (uint32_t)i) {
+                    tpool[k1[i]] = (uint32_t)p;
+                    pool_key1[p++] = k1[i];
+                }
+        });
+        sweep(nsearch, nsch, [&](size_t, size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; i++) k1[i] = tpool[k1[i]];
+        });
     } else {
         std::map<std::vector<uint32_t>, uint32_t> pool_of;
+        std::vector<uint32_t> key(keyf.size());
         for (size_t i = 0; i < nsearch; i++) {
-            if (!key_of(i, key)) return false;
+            if (!key_of(i, key.data())) return false;
             auto it = pool_of.emplace(key, (uint32_t)pool_of.size());
             if (it.second) pool_keys.push_back(key);
             search_pool[i] = it.first->second;
         }
+        ng = pool_keys.size();
     }
-    const size_t ng = pool_keys.size();
     if (ng < 2) return false;
     P.ng = ng;
+    auto pool_key = [&](size_t p, size_t f) { return keyf.size() == 1 ? pool_key1[p] : pool_keys[p][f]; };
     // every searching ticket must itself belong to its search's pool; the
     // rows are bucketed per pool in batch order (CSR: per-chunk counts, then
     // every chunk scatters at its offsets; counters stay thread-private)
     const size_t nb = brow.size();
     const unsigned nchunk = nb >= par_min(65536) ? wp.size() : 1;
-    std::vector<uint32_t> cnt((size_t)nchunk * ng, 0);
+    UVec<uint32_t>& cnt = pool_cnt_;  // [chunk][pool]: each chunk writes its row in full
+    grow_to(cnt, (size_t)nchunk * ng);
     std::vector<uint8_t> cbad(nchunk, 0);
     // per (chunk, pool): a row that is not known to carry its own search's
     // terms (self_match_) — the pool is then not known to hold all its rows
-    std::vector<uint8_t> cforeign((size_t)nchunk * ng, 0);
-    wp.run(nchunk, [&](size_t c) {
-        std::vector<uint32_t> k(ng, 0);
-        for (size_t bi = nb * c / nchunk; bi < nb * (c + 1) / nchunk; bi++) {
+    UVec<uint8_t>& cforeign = pool_foreign_;
+    grow_to(cforeign, (size_t)nchunk * ng);
+    const auto tp1 = clk::now();
+    sweep(nb, nchunk, [&](size_t c, size_t lo, size_t hi) {
+        // thread-private counters (few pools: the chunks' rows of cnt share
+        // cache lines), copied out at the end
+        static thread_local std::vector<uint32_t> k;
+        static thread_local std::vector<uint8_t> fo;
+        k.assign(ng, 0);
+        fo.assign(ng, 0);
+        for (size_t bi = lo; bi < hi; bi++) {
             const uint32_t r = brow[bi];
-            const uint32_t gi = brow_group[bi];
+            const uint32_t gi = group_of(bi);
             const uint32_t p = search_pool[gi];
             k[p]++;
             // the row carries every term of its own search: the pool's keys among them
-            if (self_match_[r] && indexed_[r] && sig_[r] == bg[gi].sig) continue;
-            cforeign[c * ng + p] = 1;
-            const auto& pk = pool_keys[p];
+            if (self_match_[r] && indexed_[r] && sig_[r] == sig_of(gi)) continue;
+            fo[p] = 1;
             for (size_t f = 0; f < keyf.size(); f++)
-                if (fkind_[keyf[f]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[f]][r] != pk[f]) {
+                if (fkind_[keyf[f]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[f]][r] != pool_key(p, f)) {
                     cbad[c] = 1;
                     return;
                 }
         }
-        std::copy(k.begin(), k.end(), cnt.begin() + c * ng);
+        std::memcpy(cnt.data() + c * ng, k.data(), ng * sizeof(uint32_t));
+        std::memcpy(cforeign.data() + c * ng, fo.data(), ng);
     });
+    const auto tp2 = clk::now();
     for (unsigned c = 0; c < nchunk; c++)
         if (cbad[c]) return false;
-    P.self_rows.assign(ng, 1);
-    for (unsigned c = 0; c < nchunk; c++)
-        for (size_t p = 0; p < ng; p++)
-            if (cforeign[c * ng + p]) P.self_rows[p] = 0;
-    P.pool_off.assign(ng + 1, 0);
-    for (size_t p = 0; p < ng; p++) {  // cnt becomes each (chunk, pool)'s first position
-        uint32_t run = P.pool_off[p];
-        for (unsigned c = 0; c < nchunk; c++) {
-            const uint32_t v = cnt[c * ng + p];
-            cnt[c * ng + p] = run;
-            run += v;
+    // per pool: rows and self flag (ranges of pools on the workers), the
+    // pool offsets (one scan), then each (chunk, pool)'s first position
+    grow_to(P.self_rows, ng);
+    grow_to(P.pool_off, ng + 1);
+    const unsigned npch = ng >= 65536 && nchunk > 1 ? nchunk : 1;
+    sweep(ng, npch, [&](size_t, size_t lo, size_t hi) {
+        for (size_t p = lo; p < hi; p++) {
+            uint32_t t = 0;
+            uint8_t f = 0;
+            for (unsigned c = 0; c < nchunk; c++) {
+                t += cnt[c * ng + p];
+                f |= cforeign[c * ng + p];
+            }
+            P.pool_off[p + 1] = t;
+            P.self_rows[p] = f ? 0 : 1;
         }
-        P.pool_off[p + 1] = run;
-    }
-    P.pool_rows.resize(nb);
-    wp.run(nchunk, [&](size_t c) {
-        std::vector<uint32_t> at(cnt.begin() + c * ng, cnt.begin() + (c + 1) * ng);
-        for (size_t bi = nb * c / nchunk; bi < nb * (c + 1) / nchunk; bi++)
-            P.pool_rows[at[search_pool[brow_group[bi]]]++] = (uint32_t)bi;
     });
-    stats.par_bucket_ms += msd(tp0, clk::now());
+    P.pool_off[0] = 0;
+    for (size_t p = 0; p < ng; p++) P.pool_off[p + 1] += P.pool_off[p];
+    sweep(ng, npch, [&](size_t, size_t lo, size_t hi) {
+        for (size_t p = lo; p < hi; p++) {
+            uint32_t run = P.pool_off[p];
+            for (unsigned c = 0; c < nchunk; c++) {
+                const uint32_t v = cnt[c * ng + p];
+                cnt[c * ng + p] = run;
+                run += v;
+            }
+        }
+    });
+    grow_to(P.pool_rows, nb);
+    const auto tp3 = clk::now();
+    sweep(nb, nchunk, [&](size_t c, size_t lo, size_t hi) {
+        static thread_local std::vector<uint32_t> at;
+        at.assign(cnt.begin() + c * ng, cnt.begin() + (c + 1) * ng);
+        for (size_t bi = lo; bi < hi; bi++) P.pool_rows[at[search_pool[group_of(bi)]]++] = (uint32_t)bi;
+    });
+    const auto tp4 = clk::now();
+    stats.par_bucket_ms += msd(tp0, tp4);
+    if (batch_profile_)
+        std::fprintf(stderr, "[nkm]   plan_pools: %zu pools | keys %.2f count %.2f offsets %.2f scatter %.2f ms\n", ng,
+                     msd(tp0, tp1), msd(tp1, tp2), msd(tp2, tp3), msd(tp3, tp4));
     P.ok = true;
     return true;
 }
@@ -1034,15 +1125,18 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                            const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                            GroupList& out_groups,
                            std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
-                           uint32_t* min_stop) {
+                           uint32_t* min_stop, const std::function<BGroup&(uint32_t)>* view) {
     *min_stop = UINT32_MAX;
     if (!P.ok) return false;
     // Truncated lists are allowed: a pool whose row runs past the end of its
     // list stops there (the row's search re-runs in the next batch), the other
     // pools carry on; every row a pool processed is decided (pools never share
     // a ticket), and the pass puts the groups back in row order at its end.
+    // view: a packed batch (rpack_kernel) — row bi's search is view(bi), a
+    // thread-local BGroup over the row's packed list (complete by construction)
     bool all_complete = true;
-    for (const BGroup& g : bg) all_complete = all_complete && g.complete;
+    if (!view)
+        for (const BGroup& g : bg) all_complete = all_complete && g.complete;
     if (!all_complete && !partial_mode_) return false;
     using clk = std::chrono::steady_clock;
     auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1052,11 +1146,13 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     WorkPool& wp = workers();
     const DStore st = dstore();
     const int maxI = cfg_.max_intervals;
-    // each pool's searches (CSR) and each search's index among them
-    std::vector<uint32_t> soff(ng + 1, 0), sidx(nsearch);
-    for (size_t i = 0; i < nsearch; i++) soff[search_pool[i] + 1]++;
-    for (size_t p = 0; p < ng; p++) soff[p + 1] += soff[p];
-    {
+    // each pool's searches (CSR) and each search's index among them: only
+    // the dense walk reads them (one search per pool, no RevPrecision)
+    const bool want_dense = dense_mode_ && !rev && !view;
+    std::vector<uint32_t> soff(want_dense ? ng + 1 : 0, 0), sidx(want_dense ? nsearch : 0);
+    if (want_dense) {
+        for (size_t i = 0; i < nsearch; i++) soff[search_pool[i] + 1]++;
+        for (size_t p = 0; p < ng; p++) soff[p + 1] += soff[p];
         std::vector<uint32_t> at(soff.begin(), soff.end() - 1);
         for (size_t i = 0; i < nsearch; i++) {
             const uint32_t p = search_pool[i];
@@ -1064,10 +1160,13 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         }
     }
     auto prows = [&](size_t p) { return P.pool_off[p + 1] - P.pool_off[p]; };
-    // tasks: pools by size (largest first), the small ones bundled
+    // tasks: pools by size (largest first), the small ones bundled; many
+    // pools (C5's 10^5 buckets) are bundled in pool order unsorted — every
+    // task holds many, so the largest-first order buys no balance
     std::vector<uint32_t> order_g(ng);
     for (size_t i = 0; i < ng; i++) order_g[i] = (uint32_t)i;
-    std::sort(order_g.begin(), order_g.end(), [&](uint32_t a, uint32_t b) { return prows(a) > prows(b); });
+    if (ng <= 4096)
+        std::sort(order_g.begin(), order_g.end(), [&](uint32_t a, uint32_t b) { return prows(a) > prows(b); });
     const size_t per_task = std::max<size_t>(1, nb / ((size_t)wp.size() * 8));
     std::vector<uint32_t> task_off{0};
     for (size_t k = 0, acc = 0; k < ng; k++) {
@@ -1108,8 +1207,8 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     std::vector<uint8_t> dense(ng, 0);
     std::vector<uint32_t> dense_ids;
     uint64_t dense_total = 0;
-    for (size_t gi = 0; gi < ng; gi++) {
-        if (soff[gi + 1] - soff[gi] != 1 || !dense_mode_ || rev) continue;  // the dense walk has no reverse checks
+    for (size_t gi = 0; gi < ng && want_dense; gi++) {
+        if (soff[gi + 1] - soff[gi] != 1) continue;  // the dense walk has no reverse checks
         if (!bg[sidx[soff[gi]]].complete) continue;                        // nor pages
         dense[gi] = 1;
         DensePool& D = dense_pools_[gi];
@@ -1376,9 +1475,13 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             } else {
                 rows_of.assign(P.pool_rows.begin() + P.pool_off[gi], P.pool_rows.begin() + P.pool_off[gi + 1]);
                 rp.hits_seen = 0;
-                pool_stop[gi] = replay_pool(rp, rows_of, brow.data(),
-                                            [&](uint32_t bi) -> BGroup& { return bg[brow_group[bi]]; },
-                                            tl_sel, tl_proc.data(), minc_.data(), maxc_.data(), po);
+                if (view)
+                    pool_stop[gi] = replay_pool(rp, rows_of, brow.data(), *view, tl_sel, tl_proc.data(), minc_.data(),
+                                                maxc_.data(), po);
+                else
+                    pool_stop[gi] = replay_pool(rp, rows_of, brow.data(),
+                                                [&](uint32_t bi) -> BGroup& { return bg[brow_group[bi]]; },
+                                                tl_sel, tl_proc.data(), minc_.data(), maxc_.data(), po);
                 task_hits[t] += rp.hits_seen;
             }
             if (!few) to_rows(o, (uint32_t)t, ents);
@@ -1615,6 +1718,157 @@ void Core::choose_source(const Sig& s, DGroup& g, SrcChoice* ch) {
     }
 }
 
+// Row bi of a packed batch as the replay's search view (its fixed-stride
+// list, reverse bits and pair words in the pinned output buffer).
+static inline void fill_packed(BGroup& g, const uint8_t* base, const PackLayout& L, uint32_t bi, uint32_t T,
+                               uint32_t sig) {
+    const uint32_t n = base[L.cnt + bi];
+    const uint32_t P = L.S < 32 ? (uint32_t)L.S : 32u;
+    g.sig = sig;
+    g.row_slot = T;
+    g.d.rev_slot = T;
+    g.nrows = 1;
+    g.set_slots(reinterpret_cast<const uint32_t*>(base + L.slot) + (size_t)bi * L.S);
+    g.last_i = UINT32_MAX;
+    g.rev = nullptr;
+    g.rev_packed = true;
+    const uint8_t* rv = base + L.rev;
+    g.rev_bits = L.rev_w == 1 ? rv[bi]
+               : L.rev_w == 2 ? reinterpret_cast<const uint16_t*>(rv)[bi]
+               : L.rev_w == 4 ? reinterpret_cast<const uint32_t*>(rv)[bi]
+                              : reinterpret_cast<const uint64_t*>(rv)[bi];
+    g.pm = base + L.pm + (size_t)bi * P * L.pm_w;
+    g.pm_w = (uint8_t)L.pm_w;
+    g.pm_n = std::min(n, P);
+    g.n = n;
+    g.complete = true;
+    g.head = 0;
+}
+
+// Packed RevPrecision batch assembly: the pass rows [pos, end) not yet
+// selected or decided, each its ticket's slot and source (source_of's choice:
+// the posting list of its most selective required term), straight into the
+// pinned upload buffer.  False (nothing changed) when some row's source holds
+// more than 64 entries: the per-search path then takes the batch.
+bool Core::assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t cap, UVec<uint32_t>& brow,
+                           PackBatch& pb) {
+    const size_t nr = std::min({rows.size() - pos, kMaxBatchRows, cap});
+    WorkPool& wp = workers();
+    const bool par = par_mode_ && nr >= par_min(65536);
+    const size_t nch = par ? (size_t)wp.size() * 4 : 1;
+    grow_to(pk_tmp_, nr);
+    std::vector<size_t> at(nch + 1, 0);
+    std::vector<uint32_t> maxlen(nch, 0);
+    std::vector<uint8_t> bad(nch, 0);
+    std::vector<uint64_t> scanned(nch, 0);
+    std::vector<double> live_w(nch, 0.0);
+    auto pass1 = [&](size_t c) {
+        size_t k = 0;
+        uint32_t mx = 0;
+        uint64_t sc = 0;
+        double lw = 0.0;
+        for (size_t i = nr * c / nch; i < nr * (c + 1) / nch; i++) {
+            const uint32_t r = rows[pos + i];
+            DSmallRow& o = pk_tmp_[i];
+            if (sel_[r] | dec_[r]) {
+                o.slot = kNoSlot;
+                continue;
+            }
+            const Sig& sg = sigs_[sig_[r]];
+            DGroup d;
+            source_of(sg, d);
+            if (d.src_len > 64) {
+                bad[c] = 1;
+                return;
+            }
+            o = DSmallRow{r, d.src_off, d.src_len | (d.src_kind == 0 ? kSrcOrder : 0u)};
+            k++;
+            mx = std::max(mx, d.src_len);
+            sc += d.src_len;
+            // per live candidate (search_bytes' rev form): Min/MaxCount, the
+            // query's field columns, the hit's query descriptor and clauses
+            lw += (double)d.src_len * (double)(8 + 9 * sg.n_fields + 8 + 32 * sg.n_clauses);
+        }
+        at[c + 1] = k;
+        maxlen[c] = mx;
+        scanned[c] = sc;
+        live_w[c] = lw;
+    };
+    if (nch > 1) wp.run(nch, pass1);
+    else pass1(0);
+    for (uint8_t b : bad)
+        if (b) return false;
+    for (size_t c = 0; c < nch; c++) at[c + 1] += at[c];
+    const size_t n = at[nch];
+    h_srows_.reserve(std::max<size_t>(n, 1));
+    grow_to(brow, n);
+    auto pass2 = [&](size_t c) {
+        size_t o = at[c];
+        for (size_t i = nr * c / nch; i < nr * (c + 1) / nch; i++) {
+            const DSmallRow& d = pk_tmp_[i];
+            if (d.slot == kNoSlot) continue;
+            h_srows_.p[o] = d;
+            brow[o] = d.slot;
+            o++;
+        }
+    };
+    if (nch > 1) wp.run(nch, pass2);
+    else pass2(0);
+    pb = PackBatch{};
+    pb.n = n;
+    pb.end = pos + nr;
+    uint32_t mx = 0;
+    for (size_t c = 0; c < nch; c++) {
+        mx = std::max(mx, maxlen[c]);
+        pb.scanned += scanned[c];
+        pb.live_w += live_w[c];
+    }
+    while ((uint32_t)pb.S < mx) pb.S *= 2;
+    return true;
+}
+
+// One packed batch on the device: rows up, rpack_kernel, the whole output
+// down in one copy (the host `overlap` work runs meanwhile).
+PackLayout Core::run_packed(const PackBatch& pb, PassStats& stats, const std::function<void()>& overlap) {
+    flush_apply();  // the previous batch's selections, before this batch's searches
+    const PackLayout L = pack_layout(pb.n, pb.S);
+    const DStore st = dstore();
+    d_srows_.reserve(std::max<size_t>(pb.n, 1), false);
+    d_pack_.reserve(L.total, false);
+    h_pack_.reserve(L.total);
+    if (pb.n) {
+        NKM_HIP(hipMemcpyAsync(d_srows_.p, h_srows_.p, pb.n * sizeof(DSmallRow), hipMemcpyHostToDevice, stream_));
+        NKM_HIP(launch_rpack(st, d_srows_.p, (uint32_t)pb.n, d_pack_.p, L, stream_, ev_[7], ev_[8]));
+        NKM_HIP(hipMemcpyAsync(h_pack_.p, d_pack_.p, L.total, hipMemcpyDeviceToHost, stream_));
+    }
+    if (overlap) overlap();
+    NKM_HIP(hipStreamSynchronize(stream_));
+    stats.batches++;
+    if (!pb.n) return L;
+    float ms = 0.f;
+    NKM_HIP(hipEventElapsedTime(&ms, ev_[7], ev_[8]));
+    stats.k_ms[3] += ms;
+    stats.k_launches[3]++;
+    stats.rpack = true;
+    uint64_t live = 0, ents = 0;
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(h_pack_.p + L.live);
+    for (uint32_t b = 0; b < L.blocks; b++) {
+        live += lw[2 * b];
+        ents += lw[2 * b + 1];
+    }
+    // algorithmic bytes: per row its descriptor and its query / count range;
+    // per scanned candidate slot id + alive; per live candidate the columns
+    // (average of the rows' per-live bytes, weighted by source length); per
+    // entry its slot id; per row its pair words, reverse bits and count
+    const double per_live = pb.scanned ? pb.live_w / (double)pb.scanned : 0.0;
+    const int P = pb.S < 32 ? pb.S : 32;
+    stats.k_bytes[3] += (int64_t)pb.n * (int64_t)(sizeof(DSmallRow) + 16) + (int64_t)pb.scanned * 5 +
+                        (int64_t)((double)live * per_live) + (int64_t)ents * 4 +
+                        (int64_t)pb.n * (int64_t)(P * L.pm_w + L.rev_w + 1);
+    stats.pair_evals += (int64_t)pb.scanned;
+    return L;
+}
+
 int Core::process_default(GroupList& out_groups,
                           std::vector<uint32_t>& expired, PassStats& stats) {
     const uint32_t N = (uint32_t)nslots();
@@ -1665,6 +1919,72 @@ int Core::process_default(GroupList& out_groups,
         // the RevThreshold timer fired: the remaining rows search as without
         // RevPrecision (row-sharded: decided at batch starts, OR-ed over the ranks)
         if (rev && (row_shard() ? shard_any(timer.check()) : timer.check())) rev = rp.rev = false;
+        // ---- packed RevPrecision batch (rpack_kernel) ----
+        if (rev && pack_mode_ && kernel_mode_ == KM_AUTO && retry_slot == kNoSlot && !row_shard()) {
+            using pclk = std::chrono::steady_clock;
+            auto pms = [](pclk::time_point a, pclk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            const auto ta0 = pclk::now();
+            PackBatch pb;
+            if (assemble_packed(rows, pos, win, brow, pb)) {
+                const auto tb0 = pclk::now();
+                stats.assemble_ms += pms(ta0, tb0);
+                ParPlan& plan = par_plan_;
+                plan.ok = false;
+                const bool timer_live = timer.armed && !timer.fired;
+                const PackLayout L = run_packed(pb, stats, [&] {  // pools bucketed while the rows search
+                    if (par_mode_ && !timer_live)
+                        plan_pools(
+                            pb.n, [&](size_t i) { return sig_[brow[i]]; }, [](size_t bi) { return (uint32_t)bi; }, brow,
+                            plan, stats);
+                });
+                const auto tb1 = pclk::now();
+                stats.search_ms += pms(tb0, tb1);
+                const uint8_t* base = h_pack_.p;
+                const std::function<BGroup&(uint32_t)> view = [&, base, L](uint32_t bi) -> BGroup& {
+                    static thread_local BGroup g;
+                    const uint32_t T = brow[bi];
+                    fill_packed(g, base, L, bi, T, sig_[T]);
+                    return g;
+                };
+                newly.clear();
+                uint32_t stop_bi = UINT32_MAX;
+                if (par_mode_ && replay_parallel(plan, bg, brow, brow_group, sel, out_groups, expired, newly, stats, rev,
+                                                 &stop_bi, &view)) {
+                    stats.parallel_batches++;
+                    if (stop_bi != UINT32_MAX) throw std::runtime_error("packed batch: a complete list ran out");
+                } else {
+                    for (size_t bi = 0; bi < pb.n; bi++) {
+                        const uint32_t T = brow[bi];
+                        if (sel[T]) continue;
+                        BGroup& g = view((uint32_t)bi);
+                        if (rp.rev && timer.check()) rp.rev = false;  // later rows skip the reverse checks
+                        const auto status = rp.decide(T, g, false, grp);
+                        if (status == Replay::EXHAUSTED) throw std::runtime_error("packed batch: a complete list ran out");
+                        intervals_[T]++;
+                        if (intervals_[T] >= maxI || minc_[T] == maxc_[T]) expired.push_back(T);
+                        if (status == Replay::MATCHED) {
+                            for (auto& e : grp) {
+                                if (!sel[e.first]) {
+                                    sel[e.first] = 1;
+                                    newly.push_back(e.first);
+                                }
+                            }
+                            out_groups.push(grp);
+                        }
+                    }
+                }
+                const auto tb2 = pclk::now();
+                stats.replay_ms += pms(tb1, tb2);
+                defer_apply(newly);
+                if (batch_profile_)
+                    std::fprintf(stderr, "[nkm]   batch %d (packed, S %d%s): rows %zu | assemble %.2f search %.2f replay %.2f ms\n",
+                                 stats.batches, pb.S, plan.ok ? ", parallel" : "", pb.n, pms(ta0, tb0), pms(tb0, tb1),
+                                 pms(tb1, tb2));
+                pos = pb.end;
+                if (win != SIZE_MAX) win = win > SIZE_MAX / 2 ? SIZE_MAX : 2 * win;
+                continue;
+            }
+        }
         // ---- assemble the batch ----
         const auto ta0 = std::chrono::steady_clock::now();
         for (auto& g : bg)
@@ -2107,7 +2427,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                 // a ticket an earlier processCustom pass retired is still in
                 // the search index, but not in indexesCopy: "missing index" (:432-437)
                 if (!live_[H]) continue;
-                if (row_rev && !g.rev[j]) continue;
+                if (row_rev && !g.rev_at(j)) continue;
                 if (maxc_[T] < maxc_[H] && intervals_[H] <= maxI) continue;
                 if (rp.share_session(T, H)) continue;
                 hits.push_back(H);
@@ -2129,7 +2449,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                 pm.assign(L, 0);
                 for (size_t a = 0; a < L; a++)
                     for (size_t b = 0; b < L; b++)
-                        if ((g.pm[hpos[a]] >> hpos[b]) & 1u) pm[a] |= 1ull << b;
+                        if ((g.pm_at(hpos[a]) >> hpos[b]) & 1u) pm[a] |= 1ull << b;
             } else if (row_rev) {
                 std::vector<uint32_t>& pr = sc.pr;
                 pr.clear();
@@ -2464,7 +2784,7 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
 // (groups are disjoint, so the sweeps see the state the serial loop would).
 // Returns false, having changed nothing but the expired tickets' active flags
 // (finish_pass sets them again), when a condition fails.
-bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& groups, mm_matched* out) {
+bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& groups, mm_matched* out, bool mutated) {
     const size_t ng = groups.size(), ne = groups.ents.size();
     if (!par_mode_ || ng < par_min(16384) || !sess_slots_.more.empty() || !party_slots_.more.empty()) return false;
     if (!arena_claimed_ && out_in_use_.exchange(true)) return false;  // a second outstanding result: fill_matched copies
@@ -2474,14 +2794,19 @@ bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& gro
     const size_t nch = (size_t)wp.size() * 2;
     std::vector<uint8_t> bad(nch, 0);
     const size_t nx = expired.size();
-    wp.run(nch, [&](size_t c) {
-        for (size_t i = nx * c / nch; i < nx * (c + 1) / nch; i++) is_active_[expired[i]] = 0;
-        for (size_t g = ng * c / nch; g < ng * (c + 1) / nch && !bad[c]; g++)
-            for (const auto* e = groups.begin(g); e != groups.end(g); ++e)
-                if (e->first == kNoSlot || !live_[e->first]) { bad[c] = 1; break; }
-    });
-    for (uint8_t b : bad)
-        if (b) return false;  // fill_matched, on the claimed arena, after finish_pass's re-check
+    // Without a mutation queued during the pass no member left the index
+    // (groups are formed from live tickets only): every group is complete
+    // and the re-check is skipped; the retire sweep clears the expired flags.
+    if (mutated) {
+        wp.run(nch, [&](size_t c) {
+            for (size_t i = nx * c / nch; i < nx * (c + 1) / nch; i++) is_active_[expired[i]] = 0;
+            for (size_t g = ng * c / nch; g < ng * (c + 1) / nch && !bad[c]; g++)
+                for (const auto* e = groups.begin(g); e != groups.end(g); ++e)
+                    if (e->first == kNoSlot || !live_[e->first]) { bad[c] = 1; break; }
+        });
+        for (uint8_t b : bad)
+            if (b) return false;  // fill_matched, on the claimed arena, after finish_pass's re-check
+    }
     if (out_offs_.size() < ng + 1) grow_to(out_offs_, ng + 1);
     if (out_ents_.size() < std::max<size_t>(ne, 1)) grow_to(out_ents_, std::max<size_t>(ne, 1));
     if (out_created_.size() < std::max<size_t>(ng, 1)) grow_to(out_created_, std::max<size_t>(ng, 1));
@@ -2493,6 +2818,8 @@ bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& gro
     wp.run(nch, [&](size_t c) {
         const size_t g0 = ng * c / nch, g1 = ng * (c + 1) / nch;
         uint32_t k = 0;
+        if (!mutated)
+            for (size_t i = nx * c / nch; i < nx * (c + 1) / nch; i++) is_active_[expired[i]] = 0;
         if (!filled) {
             for (size_t g = g0; g < g1; g++) {
                 offs[g] = (int32_t)groups.off[g];
@@ -2726,8 +3053,9 @@ int Core::process(mm_matched* out) {
         const auto t2 = std::chrono::steady_clock::now();
         lk.lock();  // matchmaker.go:320
         out->n_expired = (int32_t)expired.size();
+        const bool mutated = !pending_.empty();
         apply_pending();
-        const bool fused = finish_fill_fast(expired, groups, out);
+        const bool fused = finish_fill_fast(expired, groups, out, mutated);
         if (!fused) finish_pass(expired, groups, true);
         pass_running_ = false;
         const auto t3 = std::chrono::steady_clock::now();
@@ -2752,7 +3080,7 @@ int Core::process(mm_matched* out) {
         }
     }
     const int dk = stats.dominant();  // bench.py's roofline kernel
-    out->eval_kernel = dk == 2 && stats.mhash ? 4 : dk;
+    out->eval_kernel = dk == 2 && stats.mhash ? 4 : dk == 3 && stats.rpack ? 5 : dk;
     out->eval_ms = stats.k_ms[dk];
     out->pair_evals = stats.pair_evals;
     out->eval_bytes = stats.k_bytes[dk];

@@ -77,6 +77,8 @@ template struct PinnedArray<DGroupResult>;
 template struct PinnedArray<uint32_t>;
 template struct DevArray<uint64_t>;
 template struct DevArray<DEnumRow>;
+template struct DevArray<DSmallRow>;
+template struct PinnedArray<DSmallRow>;
 template struct DevArray<DEnumHit>;
 template struct DevArray<DEnumItem>;
 template struct PinnedArray<uint64_t>;
@@ -117,6 +119,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_PROFILE")) batch_profile_ = std::strcmp(e, "2") == 0;
     if (const char* e = std::getenv("NKM_PARTIAL")) partial_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_DEVENUM")) dev_enum_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_RPACK")) pack_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_WIN_MIN")) win_min_ = (size_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("NKM_VARK_MIN")) vark_min_ = (uint32_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("NKM_KERNEL"))

@@ -95,9 +95,21 @@ struct BGroup {
         sp = s;
         ss = 1;
     }
+    // RevPrecision reverse-check flags: one byte per entry (`rev`), or, for a
+    // packed row (rpack_kernel: <= 64 entries), bits in entry order (rev_bits)
     const uint8_t* rev = nullptr;
-    const uint32_t* pm = nullptr;  // kPairP masks per entry (rev rows with combos)
+    uint64_t rev_bits = 0;
+    bool rev_packed = false;
+    bool rev_at(uint32_t i) const { return rev_packed ? ((rev_bits >> i) & 1u) != 0 : rev[i] != 0; }
+    // pair-matrix words per entry (rev rows with combos): pm_w bytes each
+    // (4: search / rsmall lists; 1 or 2: packed rows of 8 or 16 entries)
+    const void* pm = nullptr;
     uint32_t pm_n = 0;             // entries covered by pm
+    uint8_t pm_w = 4;
+    uint32_t pm_at(uint32_t a) const {
+        return pm_w == 4 ? static_cast<const uint32_t*>(pm)[a]
+                         : pm_w == 2 ? static_cast<const uint16_t*>(pm)[a] : static_cast<const uint8_t*>(pm)[a];
+    }
     bool has_src_term = false;     // source = posting list of (src_field, src_term)
     uint16_t src_field = 0;
     uint32_t src_term = 0;
@@ -119,8 +131,11 @@ struct BGroup {
         ss = 4;
         last_i = UINT32_MAX;
         rev = nullptr;
+        rev_bits = 0;
+        rev_packed = false;
         pm = nullptr;
         pm_n = 0;
+        pm_w = 4;
         has_src_term = false;
         src_field = 0;
         src_term = 0;
@@ -213,7 +228,7 @@ struct ReplayCore {
 
     // validateMatch(from's query, to) for two entries of the same list.
     bool pair_ok(const BGroup& g, uint32_t from_pos, uint32_t to_pos) {
-        if (g.pm && from_pos < g.pm_n && to_pos < g.pm_n) return (g.pm[from_pos] >> to_pos) & 1u;
+        if (g.pm && from_pos < g.pm_n && to_pos < g.pm_n) return (g.pm_at(from_pos) >> to_pos) & 1u;
         return pair_slow(g, from_pos, to_pos);
     }
 
@@ -343,7 +358,7 @@ struct ReplayCore {
             if (H == T || sel[H]) continue;
             const HotRec& hh = v.hot[H];
             if (tparty != kNoParty && hh.party == tparty) continue;                       // :80-85
-            if (rev && !g.rev[i]) continue;                                            // :139-148
+            if (rev && !g.rev_at(i)) continue;                                         // :139-148
             if (tmax < hh.maxc && v.intervals[H] + (proc ? proc[H] : 0) <= max_intervals) continue;  // :150-153
             if (!v.sessions_exclusive && (ht.smask & hh.smask) && share_session(ht, hh)) continue;  // :155-165
             bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)

@@ -15,7 +15,7 @@ from . import capi
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "tools", "libmm_synth.so")
 T0 = (1_700_000_000_000_000_000 // 1024) * 1024
-SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005, 6: 0x5EED0006, 8: 0x5EED0008, 9: 0x5EED0009, 11: 0x5EED0005, 12: 0x5EED0006}
+SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005, 6: 0x5EED0006, 8: 0x5EED0008, 9: 0x5EED0009, 11: 0x5EED0005, 12: 0x5EED0006, 13: 0x5EED0005, 14: 0x5EED0005}
 _lib = None
 
 

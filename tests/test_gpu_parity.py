@@ -317,6 +317,24 @@ def test_c5_rev_precision_default_path(par, monkeypatch):
     run_passes(5, 800, 2, dict(max_intervals=2, rev_precision=True))
 
 
+@pytest.mark.parametrize("config,n,passes,stride", [(5, 800, 2, 8), (13, 900, 3, 16), (14, 960, 2, 32),
+                                                     (11, 640, 2, 64), (6, 600, 3, None)])
+@pytest.mark.parametrize("rpack,par", [("1", "0"), ("1", "force"), ("0", "force")])
+def test_packed_rev_precision(config, n, passes, stride, rpack, par, monkeypatch):
+    """RevPrecision batches whose rows all search short sources run packed
+    (rpack_kernel: 64/S rows per wave, fixed-stride lists, narrow pair-matrix
+    words, reverse bits) — C5's buckets of 8 (S = 8), config 13's buckets of 12
+    with parties, Min < Max and CountMultiple (S = 16), config 14's buckets of
+    24 with a required range (S = 32), config 11's buckets of 64 (S = 64) —
+    with the serial and the pool-parallel replay, and per row (NKM_RPACK=0:
+    rsmall_kernel); config 6's long sources take the per-row path either way."""
+    monkeypatch.setenv("NKM_RPACK", rpack)
+    monkeypatch.setenv("NKM_PARALLEL", par)
+    out = run_passes(config, n, passes, dict(max_intervals=passes, rev_precision=True))
+    packed = stride is not None and rpack == "1"
+    assert (out[0].eval_kernel == 5) == packed, out[0].eval_kernel
+
+
 def first_disjoint(cands):
     """The deterministic override of SURVEY.md 8(d) C5: keep candidates, in
     order, that do not overlap an already kept one."""

@@ -226,6 +226,38 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             t.max_count = 4;
             break;
         }
+        case 13: {  // C5 variant, buckets of 12 (packed RevPrecision lists of stride 16):
+                    // parties of 1-3, Min < Max, CountMultiple 2 on a third of the tickets
+            const double u = r.uni();
+            party = u < 0.6 ? 1 : u < 0.9 ? 2 : 3;
+            const int s = (int)std::lround(r.normal(1500.0, 300.0));
+            char b[32];
+            std::snprintf(b, sizeof b, "c%lld", (long long)(i / 12));
+            S->sp.push_back({"bucket", S->keep(b)});
+            S->np.push_back({"skill", (double)s});
+            char q[200];
+            std::snprintf(q, sizeof q, "+properties.bucket:%s properties.skill:>=%d^2 properties.skill:<=%d^3", b, s - 150,
+                          s + 100);
+            query = q;
+            const int shape = (int)(r.next() % 3);
+            t.min_count = 2;
+            t.max_count = shape == 0 ? 6 : 4;
+            if (shape == 0) t.count_multiple = 2;
+            break;
+        }
+        case 14: {  // C5 variant, buckets of 24 (stride 32), a required skill range, 3-player groups
+            const int s = (int)std::lround(r.normal(1500.0, 300.0));
+            char b[32];
+            std::snprintf(b, sizeof b, "d%lld", (long long)(i / 24));
+            S->sp.push_back({"bucket", S->keep(b)});
+            S->np.push_back({"skill", (double)s});
+            char q[200];
+            std::snprintf(q, sizeof q, "+properties.bucket:%s +properties.skill:>=%d properties.skill:>=%d^2", b, s - 400,
+                          s - 100);
+            query = q;
+            t.min_count = t.max_count = 3;
+            break;
+        }
         case 7: {  // multi-term clauses: regexp / wildcard / fuzzy (blocked-list pattern of
                    // TestMatchmakerPropertyRegexSubmatch, server/matchmaker_test.go:162-286)
             static const char* kMaps[8] = {"map1", "map2", "map3", "map4", "map5", "map6", "some_map", "other_map"};
