@@ -56,6 +56,19 @@ void mm_free_unpacked(void* set);
  * groups (linear in the keys).  Returns 1 when one of them has the same key
  * as a group of another rank (the caller orders those by ticket id), else 0. */
 int32_t mm_merge_positions(const int64_t* keys, const int32_t* counts, int32_t world, int32_t rank, int64_t* pos_out);
+/* The same over an all-gathered [world][stride] key matrix (rank r's keys at
+ * keys + r * stride, padding ignored), with no ascending precondition: when
+ * some rank's keys do not ascend (an override's choice may reorder its
+ * groups) the positions are the stable order by (key, rank, index) and the
+ * return value is 2 — every rank sees the same matrix, so every rank takes
+ * the same branch. */
+/* Matched tickets of a result (its entries with presence index 0: a
+ * ticket's presence entries hold index 0 exactly once), counted on host
+ * threads — the cluster front's per-pass summary without a Python pass over
+ * the entries. */
+int64_t mm_count_tickets(const mm_matched* m);
+int32_t mm_merge_positions_strided(const int64_t* keys, int64_t stride, const int32_t* counts, int32_t world,
+                                   int32_t rank, int64_t* pos_out);
 
 /* ---- Row-sharded mode --------------------------------------------------
  * For queries that cross pools (or a pool larger than one GPU) the pool

@@ -168,6 +168,29 @@ EXPORTED_SYMBOLS = (
 )
 
 
+_counter = None
+
+
+def _count_tickets(out: "mm_matched") -> int:
+    """Matched tickets of a result: mm_count_tickets of the product library
+    (host threads; any library's mm_matched), numpy when it is not built."""
+    global _counter
+    if _counter is None:
+        so = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnakama_mm.so")
+        try:
+            lib = C.CDLL(so, mode=C.RTLD_LOCAL)
+            lib.mm_count_tickets.restype = C.c_int64
+            lib.mm_count_tickets.argtypes = [C.c_void_p]
+            _counter = lib.mm_count_tickets
+        except OSError:
+            _counter = False
+    if _counter:
+        return int(_counter(C.addressof(out)))
+    import numpy as np
+    raw = (C.c_char * (out.n_entries * C.sizeof(mm_entry_ref))).from_address(C.addressof(out.entries.contents))
+    return int(np.count_nonzero(np.frombuffer(raw, dtype=np.int32).reshape(-1, 4)[:, 2] == 0))
+
+
 def load_library(path: str) -> C.CDLL:
     if not os.path.exists(path):
         raise FileNotFoundError(path)
@@ -448,14 +471,8 @@ class Matchmaker:
     def summary_counts(out):
         """(n_groups, matched tickets, matched presences, ProcessResult without
         the groups) of a process_call result (not freed)."""
-        import numpy as np
         n = out.n_entries
-        if n:
-            raw = (C.c_char * (n * C.sizeof(mm_entry_ref))).from_address(C.addressof(out.entries.contents))
-            arr = np.frombuffer(raw, dtype=np.dtype([("p", "<u8"), ("pi", "<i4"), ("r", "<i4")]))
-            tickets = int(np.count_nonzero(arr["pi"] == 0))
-        else:
-            tickets = 0
+        tickets = _count_tickets(out) if n else 0
         res = ProcessResult([], bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms, out.pair_evals,
                             out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel, out.full_lists)
         return out.n_groups, tickets, n, res

@@ -69,12 +69,17 @@ def router_lib(path: str = PRODUCT_SO) -> C.CDLL:
         lib.mm_free_unpacked.argtypes = [C.c_void_p]
         lib.mm_merge_positions.restype = C.c_int32
         lib.mm_merge_positions.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
+        lib.mm_count_tickets.restype = C.c_int64
+        lib.mm_count_tickets.argtypes = [C.c_void_p]
+        lib.mm_merge_positions_strided.restype = C.c_int32
+        lib.mm_merge_positions_strided.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_int32,
+                                                   C.c_void_p]
         _router = lib
     return _router
 
 
 CLUSTER_SYMBOLS = ("mm_route_keys", "mm_pack_tickets", "mm_unpack_tickets", "mm_free_unpacked",
-                   "mm_merge_positions", "mm_shard_rows", "mm_rccl_unique_id", "mm_shard_rows_rccl",
+                   "mm_merge_positions", "mm_merge_positions_strided", "mm_count_tickets", "mm_shard_rows", "mm_rccl_unique_id", "mm_shard_rows_rccl",
                    "mm_create_multi", "mm_multi_info")
 
 
@@ -294,34 +299,28 @@ class ClusterMatchmaker:
             hdr = np.stack([self._host(h) for h in hdr])
             counts = hdr[:, 0].astype(np.int32)
             cp.n_groups, cp.matched_tickets, cp.matched_presences = (int(x) for x in hdr.sum(axis=0))
-            # one all-gather of the keys (padded to the largest rank's count)
+            # one all-gather of the keys into a [world][m] matrix (padded to
+            # the largest rank's count; one collective, one copy to the host)
             m = max(int(counts.max()), 1)
             pad = np.zeros(m, dtype=np.int64)
             pad[:ng] = keys
-            outs = [self._t(np.zeros(m, dtype=np.int64)) for _ in range(self.world)]
-            self.dist.all_gather(outs, self._t(pad))
-            allk = np.concatenate([self._host(o)[:c] for o, c in zip(outs, counts)])
+            mat = self._t(np.zeros(self.world * m, dtype=np.int64))
+            self.dist.all_gather_into_tensor(mat, self._t(pad))
+            allk = np.ascontiguousarray(self._host(mat))
             pos = np.zeros(max(ng, 1), dtype=np.int64)
-            ties = router_lib().mm_merge_positions(allk.ctypes.data, counts.ctypes.data, self.world, self.rank,
-                                                   pos.ctypes.data)
+            # the merge in C: every rank's keys ascend for processDefault; an
+            # override's choice may reorder them, and then (rc 2, the same on
+            # every rank) the groups take the stable order by (key, rank, index)
+            rc = router_lib().mm_merge_positions_strided(allk.ctypes.data, m, counts.ctypes.data, self.world,
+                                                         self.rank, pos.ctypes.data)
             cp.positions = pos[:ng]
-            # mm_merge_positions needs every rank's keys ascending: processDefault's
-            # groups are, an override's choice need not be (it may reorder):
-            # then the groups take a stable global order by (key, rank, index)
-            bounds = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
-            ascending = all(np.all(np.diff(allk[bounds[r]:bounds[r + 1]]) >= 0) for r in range(self.world))
-            if not ascending:
-                order = np.lexsort((np.arange(len(allk)), np.repeat(np.arange(self.world), counts), allk))
-                glob = np.empty(len(allk), dtype=np.int64)
-                glob[order] = np.arange(len(allk))
-                cp.positions = glob[bounds[self.rank]:bounds[self.rank + 1]]
-                ties = 0
-            flag = self._t(np.array([ties], dtype=np.int32))
+            flag = self._t(np.array([1 if rc == 1 else 0], dtype=np.int32))
             self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX)
-            if int(self._host(flag)[0]) and ascending:  # rare: the searching tickets' ids order the tied groups
+            if int(self._host(flag)[0]) and rc != 2:  # rare: the searching tickets' ids order the tied groups
                 offs = out.group_offsets
                 tie_ids = [out.entries[offs[g + 1] - 1].ticket.decode() for g in range(ng)]
-                self._order_ties(cp, allk, counts, tie_ids)
+                flat = np.concatenate([allk[r * m:r * m + int(counts[r])] for r in range(self.world)])
+                self._order_ties(cp, flat, counts, tie_ids)
         finally:
             self.local.lib.mm_free_matched(self.local.h, C.byref(out))
         t3 = time.perf_counter()

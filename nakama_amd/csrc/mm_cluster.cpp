@@ -257,22 +257,57 @@ void* mm_unpack_tickets(const uint8_t* buf, int64_t len, int32_t* n_out, const m
 
 void mm_free_unpacked(void* set) { delete static_cast<Unpacked*>(set); }
 
-int32_t mm_merge_positions(const int64_t* keys, const int32_t* counts, int32_t world, int32_t rank, int64_t* pos_out) {
-    // my group i lands after my i earlier groups and after every other rank's
-    // groups with a smaller key: per other rank, a binary search for the
-    // range's first key, then a linear two-pointer walk.  Every rank's keys
-    // ascend (its groups are in the reference's order).  Large merges (8
-    // ranks x 175k groups: ~2.5M steps on the step's critical path) split my
-    // groups into ranges walked on threads.
+// The merge behind mm_merge_positions{,_strided}: rank r's keys at base[r].
+// My group i lands after my i earlier groups and after every other rank's
+// groups with a smaller key: per other rank, a binary search for the range's
+// first key, then a linear two-pointer walk.  Large merges (8 ranks x 175k
+// groups: ~2.5M steps on the step's critical path) split my groups into
+// ranges walked on threads.  check: first test that every rank's keys ascend
+// (the same answer on every rank); if one does not — an override's choice
+// may reorder its groups — the positions are the stable order by (key, rank,
+// index) and the return value is 2.  Else 1 when one of my groups has the
+// same key as another rank's group, 0 otherwise.
+static int32_t nkm_merge(const int64_t* const* base, const int32_t* counts, int32_t world, int32_t rank,
+                         int64_t* pos_out, bool check) {
     std::vector<int64_t> off((size_t)world + 1, 0);
     for (int32_t r = 0; r < world; r++) off[r + 1] = off[r] + counts[r];
-    const int64_t* mine = keys + off[rank];
+    const int64_t* mine = base[rank];
     const int64_t n = counts[rank];
+    const int64_t steps = n * (int64_t)world + off[world];
+    const int nt = steps < (1 << 20) ? 1 : (int)std::min<int64_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+    auto parallel = [&](auto&& fn) {  // fn(t) for t in [0, nt)
+        if (nt == 1) return fn(0);
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; t++) th.emplace_back(fn, t);
+        fn(0);
+        for (auto& x : th) x.join();
+    };
+    if (check) {
+        std::vector<uint8_t> bad((size_t)nt, 0);
+        parallel([&](int t) {
+            for (int32_t r = 0; r < world && !bad[t]; r++) {
+                const int64_t m = counts[r], lo = std::max<int64_t>(1, m * t / nt), hi = m * (t + 1) / nt;
+                for (int64_t i = lo; i < hi; i++)
+                    if (base[r][i] < base[r][i - 1]) { bad[t] = 1; break; }
+            }
+        });
+        if (std::any_of(bad.begin(), bad.end(), [](uint8_t b) { return b != 0; })) {
+            std::vector<std::pair<int64_t, int64_t>> all((size_t)off[world]);  // (key, global input index)
+            for (int32_t r = 0; r < world; r++)
+                for (int64_t i = 0; i < counts[r]; i++) all[(size_t)(off[r] + i)] = {base[r][i], off[r] + i};
+            std::stable_sort(all.begin(), all.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+            for (int64_t p = 0; p < off[world]; p++) {
+                const int64_t g = all[(size_t)p].second;
+                if (g >= off[rank] && g < off[rank + 1]) pos_out[g - off[rank]] = p;
+            }
+            return 2;
+        }
+    }
     auto walk = [&](int64_t i0, int64_t i1, int32_t* ties) {
         for (int64_t i = i0; i < i1; i++) pos_out[i] = i;
         for (int32_t q = 0; q < world; q++) {
             if (q == rank || i0 >= i1) continue;
-            const int64_t* other = keys + off[q];
+            const int64_t* other = base[q];
             const int64_t m = counts[q];
             int64_t j = std::lower_bound(other, other + m, mine[i0]) - other;
             for (int64_t i = i0; i < i1; i++) {
@@ -282,20 +317,47 @@ int32_t mm_merge_positions(const int64_t* keys, const int32_t* counts, int32_t w
             }
         }
     };
-    const int64_t steps = n * (int64_t)world + off[world];
-    const int nt = steps < (1 << 20) ? 1 : (int)std::min<int64_t>(8, std::max(1u, std::thread::hardware_concurrency()));
     std::vector<int32_t> ties((size_t)nt, 0);
-    if (nt == 1) {
-        walk(0, n, &ties[0]);
-    } else {
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; t++) th.emplace_back(walk, n * t / nt, n * (t + 1) / nt, &ties[t]);
-        walk(0, n / nt, &ties[0]);
-        for (auto& x : th) x.join();
-    }
+    parallel([&](int t) { walk(n * t / nt, n * (t + 1) / nt, &ties[t]); });
     int32_t any = 0;
     for (int32_t t : ties) any |= t;
     return any;
+}
+
+int64_t mm_count_tickets(const mm_matched* m) {
+    if (!m || m->n_entries <= 0 || !m->entries) return 0;
+    const int64_t n = m->n_entries;
+    const int nt = n < (1 << 18) ? 1 : (int)std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()));
+    std::vector<int64_t> part((size_t)nt, 0);
+    auto count = [&](int t) {
+        int64_t c = 0;
+        for (int64_t i = n * t / nt; i < n * (t + 1) / nt; i++) c += m->entries[i].presence_index == 0;
+        part[t] = c;
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; t++) th.emplace_back(count, t);
+    count(0);
+    for (auto& x : th) x.join();
+    int64_t c = 0;
+    for (int64_t v : part) c += v;
+    return c;
+}
+
+int32_t mm_merge_positions(const int64_t* keys, const int32_t* counts, int32_t world, int32_t rank, int64_t* pos_out) {
+    // every rank's keys ascend (processDefault's groups are in the reference's order)
+    std::vector<const int64_t*> base((size_t)world);
+    for (int32_t r = 0, o = 0; r < world; r++) {
+        base[r] = keys + o;
+        o += counts[r];
+    }
+    return nkm_merge(base.data(), counts, world, rank, pos_out, false);
+}
+
+int32_t mm_merge_positions_strided(const int64_t* keys, int64_t stride, const int32_t* counts, int32_t world,
+                                   int32_t rank, int64_t* pos_out) {
+    std::vector<const int64_t*> base((size_t)world);
+    for (int32_t r = 0; r < world; r++) base[r] = keys + (int64_t)r * stride;
+    return nkm_merge(base.data(), counts, world, rank, pos_out, true);
 }
 
 }  // extern "C"

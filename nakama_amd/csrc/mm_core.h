@@ -137,6 +137,7 @@ struct Sig {
     int64_t ub_key = INT64_MAX;
     uint16_t n_fields = 0;  // distinct field columns the clauses read
     std::vector<std::pair<uint16_t, uint32_t>> must_terms;  // candidate posting lists
+    uint64_t must_fmask = 0;  // bit f: a MUST keyword term on field f (f >= 63: bit 63)
 };
 
 // Persistent host workers for the pass's data-parallel host phases (pool
@@ -199,13 +200,11 @@ public:
     }
 
 private:
-    // spin window (NKM_SPIN_US, default 30): long enough to bridge the host
-    // code between a pass's back-to-back jobs, short enough that idle workers
-    // do not steal cycles (SMT siblings) from a long job's busy ones
-    static std::chrono::microseconds spin_window() {
-        static const std::chrono::microseconds w{std::getenv("NKM_SPIN_US") ? std::atol(std::getenv("NKM_SPIN_US")) : 30};
-        return w;
-    }
+    // spin window: long enough to bridge the host code between a pass's
+    // back-to-back jobs, short enough that idle workers do not steal cycles
+    // (SMT siblings) from a long job's busy ones (30 us; 200 us measured
+    // slower on C3, profiles r03h)
+    static std::chrono::microseconds spin_window() { return std::chrono::microseconds{30}; }
     static inline void relax() { __builtin_ia32_pause(); }
     struct Job {
         Job(const std::function<void(size_t)>* f, size_t count) : fn(f), n(count) {}
@@ -641,9 +640,9 @@ private:
     ParPlan par_plan_;
     bool plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                        const UVec<uint32_t>& brow_group, ParPlan& P, PassStats& stats);
-    template <class SigOf, class GroupOf>
-    bool plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, const UVec<uint32_t>& brow, ParPlan& P,
-                    PassStats& stats);
+    template <class SigOf, class GroupOf, class RowOf>
+    bool plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_of, const UVec<uint32_t>& brow,
+                    ParPlan& P, PassStats& stats);
     bool replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                          const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                          GroupList& out_groups,
@@ -776,17 +775,15 @@ public:
     bool slot_lists_mode_ = true;  // NKM_SLOTLISTS=0: hit lists come back as 16-B DHits, not 4-B slot ids
     bool slot_lists_rev_ = false;  // NKM_SLOTLISTS=2: RevPrecision batches' lists as slot ids too
     bool page_mode_ = true;  // NKM_PAGE=0: only a batch's first row pages a truncated list
-    // Batch window after a variable-score list ran out (NKM_WIN=0: off): the
-    // next batch takes twice the rows the last one decided (at least
-    // win_min_), not every remaining row, since its lists go stale at about
-    // the same depth; a batch that runs to its end doubles the window.
-    bool win_mode_ = true;
-    bool full_src_mode_ = true;
+    // Batch window after a variable-score list ran out: the next batch takes
+    // twice the rows the last one decided (at least kWinMin), not every
+    // remaining row, since its lists go stale at about the same depth; a
+    // batch that runs to its end doubles the window.
+    static constexpr size_t kWinMin = 2048;
+    static constexpr uint32_t kVarKMin = 64;  // floor of a variable-score search's hit capacity
     bool batch_profile_ = false;  // NKM_PROFILE=2: one stderr line per serial batch
     bool partial_mode_ = true;    // NKM_PARTIAL=0: a batch with a truncated list replays serially
     bool dev_enum_mode_ = true;   // NKM_DEVENUM=0: processCustom enumerates its subsets on the host
-    size_t win_min_ = 2048;   // NKM_WIN_MIN
-    uint32_t vark_min_ = 64;  // NKM_VARK_MIN: floor of a variable-score search's hit capacity
     bool order_sorted_ = true;
     bool index_dirty_ = true;
     uint32_t order_head_ = 0;
@@ -890,8 +887,8 @@ public:
     // "scan" (scan_kernel at any size), "mscan" (mscan_kernel whenever eligible)
     enum KernelMode { KM_AUTO = 0, KM_SEARCH = 1, KM_SCAN = 2, KM_MSCAN = 3 };
     int kernel_mode_ = KM_AUTO;
-    // NKM_MHASH: 0 (default) the hashed mscan past 16 signatures, 1 whenever
-    // the signatures allow it, 2 never
+    // NKM_MHASH: 0 (default) the hashed mscan past 16 signatures or when the
+    // scan is contiguous, 1 whenever the signatures allow it, 2 never
     int mhash_mode_ = 0;
     std::vector<uint32_t> custom_expired_;
 

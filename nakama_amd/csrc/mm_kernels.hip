@@ -1703,13 +1703,10 @@ int mscan_hash_chunk_len(bool contig) {
     return (contig ? (j == 8 ? 8 : 4) : (j == 2 ? 2 : 4)) * kBlock;
 }
 
-// Candidates per lane: NKM_MSCAN_J (2, 4 or 8; 8 needs <= 8 signatures), default 2
-// (C3 1M: 21.7 us at 2, 24.6 at 4, 35.2 at 8 — more, shorter waves hide more latency).
-int mscan_chunk_len(uint32_t n_sigs) {
-    static const int env = std::getenv("NKM_MSCAN_J") ? std::atoi(std::getenv("NKM_MSCAN_J")) : 0;
-    const int j = env == 2 || env == 4 || (env == 8 && n_sigs <= 8) ? env : 2;
-    return j * kBlock;
-}
+// Candidates per lane: 2 (C3 1M measured 21.7 us at 2, 24.6 at 4, 35.2 at 8
+// candidates per lane — more, shorter waves hide more latency; the 4 / 8
+// instantiations stay for tools/mscan_bench).
+int mscan_chunk_len(uint32_t) { return 2 * kBlock; }
 int mscan_max_sigs() { return kMaxMSig; }
 int mscan_max_fields() { return kMaxMField; }
 int mscan_max_clauses() { return kMaxMClause; }

@@ -263,11 +263,15 @@ struct Replay : ReplayCore {
             }
             msig.push_back(make_msig(bg[i].d, off));
         }
-        // past mscan_kernel's 16 signatures, or on request (NKM_MHASH=1):
-        // the hashed lookup, when every signature is term-only on the same
-        // fields with distinct values
+        // The hashed lookup, when every signature is term-only on the same
+        // fields with distinct values: past mscan_kernel's 16 signatures, when
+        // the scan is contiguous (its vector loads: C3 1M 15.1-15.9 us against
+        // mscan_kernel's 16.1-18.9 us on the same box, profiles/r03km_*), or
+        // on request (NKM_MHASH=1; 2: never)
         const bool hashable = plan_mscan_hash(ms);
-        if (ms.n_sigs > (uint32_t)mscan_max_sigs() || nclauses > (size_t)mscan_max_clauses() || c.mhash_mode_ == 1) {
+        const bool contig_ok = c.order_identity_ && c.mcontig_mode_;
+        if (ms.n_sigs > (uint32_t)mscan_max_sigs() || nclauses > (size_t)mscan_max_clauses() || c.mhash_mode_ == 1 ||
+            (c.mhash_mode_ == 0 && hashable && contig_ok)) {
             if (!hashable) {
                 m_list.clear();
                 mcl.clear();
@@ -454,7 +458,7 @@ struct Replay : ReplayCore {
             // full (a quarter of kOutCap for all promotions) returns its whole
             // list: rows that walk far (a row that matches nothing walks all
             // of it) then never page it one synchronous launch at a time.
-            if (w.path == 0 && !d.var_score && !rev && !d.has_cursor && d.k < d.src_len && c.full_src_mode_ &&
+            if (w.path == 0 && !d.var_score && !rev && !d.has_cursor && d.k < d.src_len &&
                 budget + (d.src_len - d.k) <= kOutCap / 4) {
                 budget += d.src_len - d.k;
                 w.k = d.src_len;
@@ -897,16 +901,20 @@ struct Replay : ReplayCore {
 bool Core::plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                          const UVec<uint32_t>& brow_group, ParPlan& P, PassStats& stats) {
     return plan_pools(
-        bg.size(), [&](size_t i) { return bg[i].sig; }, [&](size_t bi) { return brow_group[bi]; }, brow, P, stats);
+        bg.size(), [&](size_t i) { return bg[i].sig; }, [&](size_t bi) { return brow_group[bi]; },
+        [&](size_t i) { return bg[i].row_slot; }, brow, P, stats);
 }
 
 // plan_parallel over `nsearch` searches: sig_of(i) is search i's signature,
 // group_of(bi) batch row bi's search (a packed RevPrecision batch: the row
-// itself).  Every step is a parallel sweep over the searches or the rows; the
-// pools are numbered in first-appearance order (C5: 125k pools per 1M rows).
-template <class SigOf, class GroupOf>
-bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, const UVec<uint32_t>& brow, ParPlan& P,
-                      PassStats& stats) {
+// itself), row_of(i) the slot of a one-row search (RevPrecision) or kNoSlot.
+// Every step is a parallel sweep over the searches or the rows; the pools are
+// numbered in first-appearance order (C5: 125k pools per 1M rows).  A one-row
+// search whose ticket carries its own search's terms (self_match_) takes its
+// pool key from its own column, not from the signature's term list.
+template <class SigOf, class GroupOf, class RowOf>
+bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_of, const UVec<uint32_t>& brow,
+                      ParPlan& P, PassStats& stats) {
     P.ok = false;
     if (nsearch < 2) return false;
     using clk = std::chrono::steady_clock;
@@ -927,7 +935,21 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, const UVec
     for (auto& mt : sigs_[sig_of(0)].must_terms)
         if (std::find(cand.begin(), cand.end(), mt.first) == cand.end()) cand.push_back(mt.first);
     std::vector<std::vector<uint8_t>> has(nsch, std::vector<uint8_t>(cand.size(), 1));
+    // fields below 63: the signatures' must-field masks (no term lists read)
+    uint64_t cmask = 0;
+    bool narrow = true;
+    for (uint16_t f : cand) {
+        if (f >= 63) narrow = false;
+        else cmask |= 1ull << f;
+    }
+    std::vector<uint64_t> hmask(nsch, ~0ull);
     sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
+        if (narrow) {
+            uint64_t m = cmask;
+            for (size_t i = lo; i < hi && m; i++) m &= sigs_[sig_of(i)].must_fmask;
+            hmask[ch] = m;
+            return;
+        }
         for (size_t i = lo; i < hi; i++) {
             const auto& mts = sigs_[sig_of(i)].must_terms;
             for (size_t k = 0; k < cand.size(); k++) {
@@ -938,6 +960,9 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, const UVec
             }
         }
     });
+    if (narrow)
+        for (unsigned ch = 0; ch < nsch; ch++)
+            for (size_t k = 0; k < cand.size(); k++) has[ch][k] = (hmask[ch] >> cand[k]) & 1;
     std::vector<uint16_t> keyf;
     for (size_t k = 0; k < cand.size(); k++) {
         bool all = true;
@@ -984,10 +1009,17 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, const UVec
             for (size_t t = lo; t < hi; t++) first[t].store(UINT32_MAX, std::memory_order_relaxed);
         });
         std::vector<size_t> heads(nsch + 1, 0);
+        const uint16_t f0 = keyf[0];
         sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
             uint32_t kk[4];
             for (size_t i = lo; i < hi; i++) {
-                if (!key_of(i, kk) || kk[0] == UINT32_MAX || kk[0] >= nd) { bad[ch] = 1; return; }
+                const uint32_t r = row_of(i);
+                if (r != kNoSlot && self_match_[r] && indexed_[r] && sig_[r] == sig_of(i) &&
+                    fkind_[f0][r] == KIND_KEYWORD)
+                    kk[0] = (uint32_t)fval_[f0][r];  // the row carries its search's term on f0
+                else if (!key_of(i, kk))
+                    kk[0] = UINT32_MAX;
+                if (kk[0] == UINT32_MAX || kk[0] >= nd) { bad[ch] = 1; return; }
                 k1[i] = kk[0];
                 uint32_t cur = first[kk[0]].load(std::memory_order_relaxed);
                 while ((uint32_t)i < cur && !first[kk[0]].compare_exchange_weak(cur, (uint32_t)i, std::memory_order_relaxed)) {
@@ -1907,10 +1939,10 @@ int Core::process_default(GroupList& out_groups,
     const uint32_t kvar = (uint32_t)var_k_capacity();
     size_t pos = 0;
     uint32_t retry_slot = kNoSlot;
-    size_t win = SIZE_MAX;  // rows per batch (win_mode_)
+    size_t win = SIZE_MAX;  // rows per batch (kWinMin)
     // floor of a variable-score search's capacity: doubles (up to the top-K
     // capacity) each time a batch ends on a list that ran out
-    uint32_t vfloor = vark_min_;
+    uint32_t vfloor = kVarKMin;
     while (order_head_ < order_.size() && !live_[order_[order_head_]]) order_head_++;
 
     while (true) {
@@ -1934,8 +1966,8 @@ int Core::process_default(GroupList& out_groups,
                 const PackLayout L = run_packed(pb, stats, [&] {  // pools bucketed while the rows search
                     if (par_mode_ && !timer_live)
                         plan_pools(
-                            pb.n, [&](size_t i) { return sig_[brow[i]]; }, [](size_t bi) { return (uint32_t)bi; }, brow,
-                            plan, stats);
+                            pb.n, [&](size_t i) { return sig_[brow[i]]; }, [](size_t bi) { return (uint32_t)bi; },
+                            [&](size_t i) { return brow[i]; }, brow, plan, stats);
                 });
                 const auto tb1 = pclk::now();
                 stats.search_ms += pms(tb0, tb1);
@@ -2169,9 +2201,10 @@ int Core::process_default(GroupList& out_groups,
             }
             return true;
         };
+        bool par_asm = false;
         if (assemble_parallel_rev()) {
             q = rows.size();
-        } else if (!assemble_parallel()) {
+        } else if (!(par_asm = assemble_parallel())) {
             uint64_t total_k = 0;
             for (; q < rows.size() && brow.size() < kMaxBatchRows && brow.size() < win; q++) {
                 const uint32_t r = rows[q];
@@ -2227,8 +2260,11 @@ int Core::process_default(GroupList& out_groups,
             defer_apply(newly);
             stats.apply_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
             if (batch_profile_)
-                std::fprintf(stderr, "[nkm]   batch %d (parallel): rows %zu searches %zu%s | search %.2f replay %.2f ms\n",
-                             stats.batches, brow.size(), bg.size(), stop_bi != UINT32_MAX ? " (a list ran out)" : "",
+                std::fprintf(stderr,
+                             "[nkm]   batch %d (parallel%s): rows %zu searches %zu%s | assemble %.2f search %.2f replay %.2f ms\n",
+                             stats.batches, par_asm ? ", parallel assembly" : "", brow.size(), bg.size(),
+                             stop_bi != UINT32_MAX ? " (a list ran out)" : "",
+                             std::chrono::duration<double, std::milli>(tb0 - ta0).count(),
                              std::chrono::duration<double, std::milli>(tb1 - tb0).count(),
                              std::chrono::duration<double, std::milli>(tr - tb1).count());
             if (stop_bi == UINT32_MAX) {
@@ -2249,7 +2285,7 @@ int Core::process_default(GroupList& out_groups,
                 for (size_t k = pos; k < rows.size(); k++)
                     if (!(sel[rows[k]] | dec[rows[k]])) rows[w++] = rows[k];
                 rows.resize(w);
-                if (win_mode_) win = std::max(win_min_, 2 * (size_t)stop_bi);
+                win = std::max(kWinMin, 2 * (size_t)stop_bi);
                 vfloor = std::min<uint32_t>(kvar, 2 * vfloor);
             }
             continue;
@@ -2297,7 +2333,7 @@ int Core::process_default(GroupList& out_groups,
         // advance past the rows this batch decided
         if (exhausted) {
             while (pos < rows.size() && rows[pos] != retry_slot) pos++;
-            if (win_mode_) win = std::max(win_min_, 2 * done);
+            win = std::max(kWinMin, 2 * done);
             vfloor = std::min<uint32_t>(kvar, 2 * vfloor);
         } else {
             pos = q;

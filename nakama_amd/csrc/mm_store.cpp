@@ -114,14 +114,10 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
         slot_lists_rev_ = std::strcmp(e, "2") == 0;
     }
     if (const char* e = std::getenv("NKM_PAGE")) page_mode_ = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("NKM_WIN")) win_mode_ = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("NKM_FULLSRC")) full_src_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_PROFILE")) batch_profile_ = std::strcmp(e, "2") == 0;
     if (const char* e = std::getenv("NKM_PARTIAL")) partial_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_DEVENUM")) dev_enum_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_RPACK")) pack_mode_ = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("NKM_WIN_MIN")) win_min_ = (size_t)std::max(1L, std::atol(e));
-    if (const char* e = std::getenv("NKM_VARK_MIN")) vark_min_ = (uint32_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("NKM_KERNEL"))
         kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN
                      : !std::strcmp(e, "mscan") ? KM_MSCAN : KM_AUTO;
@@ -441,7 +437,10 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
         if (d.occur == OCC_MUST) {
             has_must = true;
             ms += d.score;
-            if (d.op == OP_TERM) s.must_terms.push_back({d.field, d.term});
+            if (d.op == OP_TERM) {
+                s.must_terms.push_back({d.field, d.term});
+                s.must_fmask |= 1ull << (d.field < 63 ? d.field : 63);
+            }
         } else if (d.occur == OCC_SHOULD) {
             has_should = true;
             if (d.op != OP_FALSE) {

@@ -170,6 +170,11 @@ struct FastCombos {
     int32_t size[kFastComb];            // entries
     uint32_t nmem[kFastComb];
     uint32_t mem[kFastComb][kFastMem];  // members, in the order they joined
+    // RevPrecision (lists of <= 32 entries, all covered by the pair words):
+    // the members' list positions, and the AND of the live members' pair words
+    // (bit b: every live member's query matches entry b's document)
+    uint64_t pos[kFastComb];
+    uint64_t rcol[kFastComb];
 };
 
 struct ReplayCore {
@@ -237,18 +242,21 @@ struct ReplayCore {
     // processDefault's loop body for T: fast_row() when it applies (and does
     // not bail), else row().
     Status decide(uint32_t T, BGroup& g, bool can_fetch, std::vector<std::pair<uint32_t, int>>& group_out) {
-        if (fast && !rev && v.sessions_exclusive && g.complete) {
+        if (fast && v.sessions_exclusive && g.complete && (!rev || (g.pm && g.pm_n >= g.n && g.n <= kPairP))) {
             const Status s = fast_row(T, g, group_out);
             if (s != BAIL) return s;
         }
         return row(T, g, can_fetch, group_out);
     }
 
-    // row() when no two live tickets share a session, without RevPrecision,
-    // over a complete list: every session check is false, so a combo is its
-    // member slots and entry count.  Returns BAIL, having changed nothing but
-    // the list head, when the row reaches the CountMultiple trim
-    // (matchmaker_process.go:234-280) or outgrows the fixed combos.
+    // row() when no two live tickets share a session, over a complete list:
+    // every session check is false, so a combo is its member slots and entry
+    // count.  With RevPrecision the list's pair words cover every entry, and
+    // a combo also keeps its members' positions and the AND of its live
+    // members' pair words, so validateMatch both ways against every member
+    // (matchmaker_process.go:178-203) is two mask tests.  Returns BAIL, having
+    // changed nothing but the list head, when the row reaches the
+    // CountMultiple trim (:234-280) or outgrows the fixed combos.
     Status fast_row(uint32_t T, BGroup& g, std::vector<std::pair<uint32_t, int>>& group_out) {
         const HotRec& ht = v.hot[T];
         const bool last = v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc;
@@ -268,20 +276,33 @@ struct ReplayCore {
             if (H == T || sel[H]) continue;
             const HotRec& hh = v.hot[H];
             if (tparty != kNoParty && hh.party == tparty) continue;                                  // :80-85
+            if (rev && !g.rev_at(i)) continue;                                                       // :139-148
             if (tmax < hh.maxc && v.intervals[H] + (proc ? proc[H] : 0) <= max_intervals) continue;  // :150-153
             const int hc = hh.count;
             int f = 0;  // first fit (:167-226)
-            while (f < ncomb && fcb.size[f] + hc > room) f++;
+            if (rev) {
+                const uint64_t mine = g.pm_at(i), bit = 1ull << i;
+                while (f < ncomb && (fcb.size[f] + hc > room || (mine & fcb.pos[f]) != fcb.pos[f] || !(fcb.rcol[f] & bit)))
+                    f++;
+            } else {
+                while (f < ncomb && fcb.size[f] + hc > room) f++;
+            }
             if (f == ncomb) {
                 if (f == kFastComb) return BAIL;
                 fcb.size[f] = 0;
                 fcb.nmem[f] = 0;
+                fcb.pos[f] = 0;
+                fcb.rcol[f] = ~0ull;
                 ncomb++;
             } else if (fcb.nmem[f] == (uint32_t)kFastMem) {
                 return BAIL;
             }
             fcb.size[f] += hc;
             fcb.mem[f][fcb.nmem[f]++] = H;
+            if (rev) {
+                fcb.pos[f] |= 1ull << i;
+                if (v.live[H]) fcb.rcol[f] &= g.pm_at(i);
+            }
             const int l = fcb.size[f] + tcount;
             bool form = l == tmax;  // :233
             if (!form && last && l >= tmin && l <= tmax) {

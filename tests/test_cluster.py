@@ -288,6 +288,63 @@ def test_merge_positions_large(world, n, tie):
             assert (pos == rank_of[r * n:(r + 1) * n]).all()
 
 
+@pytest.mark.parametrize("n", [0, 5, 400_000])
+def test_count_tickets(n):
+    """mm_count_tickets: entries with presence index 0 (one per matched
+    ticket), counted on host threads past 2^18 entries."""
+    import ctypes as C
+    from nakama_amd import capi, cluster
+    rng = np.random.default_rng(n)
+    pidx = rng.integers(0, 4, size=max(n, 1)).astype(np.int32)
+    ents = (capi.mm_entry_ref * max(n, 1))()
+    for i in range(n) if n < 1000 else ():
+        ents[i].presence_index = int(pidx[i])
+    if n >= 1000:  # fill the presence indexes through a numpy view of the array
+        np.frombuffer(ents, dtype=np.int32).reshape(-1, 4)[:, 2] = pidx
+    m = capi.mm_matched()
+    m.n_entries = n
+    m.entries = C.cast(ents, C.POINTER(capi.mm_entry_ref))
+    want = int(np.count_nonzero(pidx[:n] == 0))
+    assert cluster.router_lib().mm_count_tickets(C.addressof(m)) == want
+    assert capi._count_tickets(m) == want
+
+
+@pytest.mark.parametrize("world,n,ascending", [(3, 7, True), (8, 150_000, True), (3, 9, False), (4, 300_000, False)])
+def test_merge_positions_strided(world, n, ascending):
+    """mm_merge_positions_strided over a padded [world][stride] matrix (the
+    cluster front's one-tensor all-gather): equal to the concatenated merge
+    when every rank's keys ascend; else (an override's reordered choice) rc 2
+    and the stable global order by (key, rank, index), on every rank."""
+    from nakama_amd import cluster
+    lib = cluster.router_lib()
+    rng = np.random.default_rng(n)
+    counts = np.array([n - (r % 3) for r in range(world)], dtype=np.int32)
+    stride = int(counts.max()) + 2
+    mat = np.full(world * stride, -7, dtype=np.int64)  # padding the merge must ignore
+    parts = []
+    for r in range(world):
+        k = rng.integers(0, 3 * n, size=int(counts[r]), dtype=np.int64)  # repeated keys: ties within and across ranks
+        k = np.sort(k) if ascending else k
+        parts.append(k)
+        mat[r * stride:r * stride + counts[r]] = k
+    flat = np.concatenate(parts)
+    rank_col = np.repeat(np.arange(world), counts)
+    order = np.lexsort((np.arange(len(flat)), rank_col, flat))
+    glob = np.empty(len(flat), dtype=np.int64)
+    glob[order] = np.arange(len(flat))
+    off = np.concatenate([[0], np.cumsum(counts)])
+    for r in range(world):
+        pos = np.zeros(int(counts[r]), dtype=np.int64)
+        rc = lib.mm_merge_positions_strided(mat.ctypes.data, stride, counts.ctypes.data, world, r, pos.ctypes.data)
+        if ascending:
+            ref = np.zeros(int(counts[r]), dtype=np.int64)
+            rc0 = lib.mm_merge_positions(flat.ctypes.data, counts.ctypes.data, world, r, ref.ctypes.data)
+            assert rc == rc0 and (pos == ref).all()
+        else:
+            assert rc == 2
+            assert (pos == glob[off[r]:off[r + 1]]).all()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("config,n,groups,passes", [(3, 3000, 2, 2), (4, 2400, 0, 1), (5, 1200, 0, 2)])
 def test_cluster_gpu_pass_equals_single_oracle_pass(config, n, groups, passes):

@@ -19,6 +19,7 @@
 //   the fast walks apply by default)
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -66,12 +67,114 @@ static uint64_t checksum(const PoolOut& o) {
     return sum;
 }
 
+// RB_MODE=c5: C5's packed RevPrecision batch — solo tickets in buckets of 8
+// consecutive slots, Min 2 / Max 4, each row's list = its bucket's members
+// with skill >= own - 100 ordered by (score desc, position), reverse bits and
+// 8-bit pair words as rpack_kernel writes them; every bucket replayed by
+// replay_pool through a per-row view (as Core::process_default's packed path).
+static int bench_c5(uint32_t N, int reps) {
+    constexpr int S = 8;
+    uint64_t rng = 0x5EED0005ull;
+    std::vector<HotRec> hot(N);
+    std::vector<uint32_t> party(N, kNoParty), pres_sess(N);
+    std::vector<int32_t> intervals(N, 0), count(N, 1), minc(N, 2), maxc(N, 4);
+    std::vector<uint8_t> live(N, 1);
+    std::vector<int64_t> created(N);
+    std::vector<int> skill(N);
+    for (uint32_t i = 0; i < N; i++) {
+        const double u1 = ((splitmix(rng) >> 11) + 1) * 0x1.0p-53, u2 = (splitmix(rng) >> 11) * 0x1.0p-53;
+        skill[i] = (int)std::lround(1500.0 + 300.0 * std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2));
+        pres_sess[i] = i;
+        HotRec& h = hot[i];
+        h = HotRec{kNoParty, i, i, 1, 2, 4, 1, 1u << (i & 31)};
+        created[i] = 1700000000000000000ll + 1024ll * i;
+    }
+    // packed lists (C5's query "+bucket:b skill:>=s-100^2": the bucket is
+    // required, the skill clause only scores): every member of the row's
+    // bucket is a hit, those with skill >= own - 100 first (higher score),
+    // then the rest, each part in bucket order; every reverse check and pair
+    // check holds (every query accepts its whole bucket)
+    std::vector<uint32_t> slots((size_t)N * S), brow(N);
+    std::vector<uint8_t> cnt(N), revb(N), pm((size_t)N * S);
+    for (uint32_t i = 0; i < N; i++) {
+        brow[i] = i;
+        const uint32_t b0 = i / S * S;
+        uint32_t n = 0;
+        for (int part = 0; part < 2; part++)
+            for (uint32_t j = b0; j < b0 + S && j < N; j++)
+                if ((skill[j] >= skill[i] - 100) == (part == 0)) slots[(size_t)i * S + n++] = j;
+        cnt[i] = (uint8_t)n;
+        revb[i] = (uint8_t)((1u << n) - 1);
+        for (uint32_t a = 0; a < n; a++) pm[(size_t)i * S + a] = (uint8_t)((1u << n) - 1);
+    }
+    ReplayView v{hot.data(), pres_sess.data(), party.data(), intervals.data(), live.data(), count.data(), created.data(),
+                 true};
+    std::vector<uint8_t> psel(N, 0), proc(N, 0);
+    double best = 1e30;
+    uint64_t sum = 0;
+    size_t groups = 0;
+    const bool prof = std::getenv("RB_PROF") != nullptr;
+    if (prof) {
+        struct sigaction sa {};
+        sa.sa_sigaction = on_prof;
+        sa.sa_flags = SA_SIGINFO | SA_RESTART;
+        sigaction(SIGPROF, &sa, nullptr);
+        itimerval it{{0, 200}, {0, 200}};
+        setitimer(ITIMER_PROF, &it, nullptr);
+    }
+    const bool fast = !std::getenv("RB_FAST") || std::atoi(std::getenv("RB_FAST")) != 0;
+    for (int r = 0; r < reps; r++) {
+        NoDevice rp(v, psel, true, 2);
+        rp.fast = fast;
+        BGroup g;
+        auto view = [&](uint32_t bi) -> BGroup& {
+            g.set_slots(slots.data() + (size_t)bi * S);
+            g.rev_packed = true;
+            g.rev_bits = revb[bi];
+            g.pm = pm.data() + (size_t)bi * S;
+            g.pm_w = 1;
+            g.n = cnt[bi];
+            g.pm_n = cnt[bi];
+            g.complete = true;
+            g.head = 0;
+            return g;
+        };
+        PoolOut o;
+        std::vector<uint32_t> bis;
+        groups = 0;
+        const double t0 = now_ms();
+        for (uint32_t b0 = 0; b0 < N; b0 += S) {
+            bis.clear();
+            for (uint32_t j = b0; j < b0 + S && j < N; j++) bis.push_back(j);
+            o.recs.clear();
+            o.ents.clear();
+            replay_pool(rp, bis, brow.data(), view, psel, proc.data(), minc.data(), maxc.data(), o);
+            if (r == 0) sum ^= checksum(o);  // rep 0 checks; the later reps time the replay alone
+            groups += o.recs.back().gcum;
+        }
+        if (r > 0 || reps == 1) best = std::min(best, now_ms() - t0);
+    }
+    if (prof) {
+        itimerval off{};
+        setitimer(ITIMER_PROF, &off, nullptr);
+        std::map<uint64_t, size_t> h;
+        for (size_t i = 0; i < g_ns; i++) h[g_samples[i]]++;
+        FILE* f = std::fopen("/tmp/rb_prof.txt", "w");
+        for (auto& kv : h) std::fprintf(f, "%zu 0x%llx\n", kv.second, (unsigned long long)kv.first);
+        std::fclose(f);
+    }
+    std::printf("[c5] %u rows in buckets of %d: %zu groups | replay %.3f ms single thread (%.1f ns/row) | checksum %016llx\n",
+                N, S, groups, best, best * 1e6 / N, (unsigned long long)sum);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const uint32_t N = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 1000000;
     const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
     const int nthreads = argc > 3 ? std::atoi(argv[3]) : 0;
     const int npools = std::getenv("RB_POOLS") ? std::atoi(std::getenv("RB_POOLS")) : 8;
     const std::string mode = std::getenv("RB_MODE") ? std::getenv("RB_MODE") : "c3";
+    if (mode == "c5") return bench_c5(N, reps);
     const int maxI = 2;
     uint64_t rng = 0x5EED0003ull;
     std::vector<HotRec> hot(N);
