@@ -79,7 +79,7 @@ def parse():
     ap.add_argument("--override", action="store_true",
                     help="register a MatchmakerOverride (processCustom path): the timed step is the candidate pass, "
                          "a native first-disjoint override and mm_process_commit (per rank under the cluster front)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02g_traffic.json"))
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03l_traffic.json"))
     a = ap.parse_args()
     if a.tickets is None:
         a.tickets = DEFAULT_TICKETS.get(a.config, 1_000_000)

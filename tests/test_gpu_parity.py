@@ -98,10 +98,12 @@ def run_passes(config, n, passes, cfg, extra=None):
 # NKM_KERNEL routes a batch's constant-score searches to one query-eval
 # kernel at any size (auto picks by size/coverage, which the small oracle
 # workloads here never reach): every kernel is checked against the oracle.
-# "mhash": mscan with the hashed signature lookup (mscan_hash_kernel) whenever
-# the signatures allow it (by default only past mscan_kernel's 16 signatures,
-# e.g. C4's 64 pools); "mscan16": never hashed (C4 then falls back to scan).
-KERNELS = ["search", "scan", "mscan", "mhash"]
+# "mscan": the multi-signature scan as chosen by default — hashed
+# (mscan_hash_kernel) past mscan_kernel's 16 signatures (C4's 64 pools) or
+# when the scan order is the slot order (fresh sets: the contiguous mode);
+# "mhash": hashed whenever the signatures allow it; "mscan16": never hashed
+# (mscan_kernel; C4 then falls back to scan).
+KERNELS = ["search", "scan", "mscan", "mscan16", "mhash"]
 
 
 def set_kernel(monkeypatch, kernel):
@@ -169,17 +171,20 @@ def test_c3_c4_at_6k(config, kernel, monkeypatch):
     run_passes(config, 6000, 2, dict(max_intervals=2))
 
 
-@pytest.mark.parametrize("kernel", ["mscan", "mhash"])
+@pytest.mark.parametrize("kernel", ["mscan", "mhash", "mscan16"])
 @pytest.mark.parametrize("config,n,cfg", [(4, 20_000, dict(max_intervals=2)), (3, 20_000, dict(max_intervals=2)),
                                           (1, 10_000, dict(max_intervals=2))])
 def test_hashed_mscan(config, n, cfg, kernel, monkeypatch):
     """The hashed mscan (one table probe per candidate, signature-major
-    placement over chunks): C4's 64 pool signatures take it by default, C3's 8
-    and C1's when forced; every list must equal the oracle's and the batch
-    must have run on mscan (eval_kernel 2, hashed 4), not the scan fallback."""
+    placement over chunks): taken by default here (C4's 64 pool signatures;
+    C3's 8 and C1's over a contiguous scan order) and when forced; never
+    with "mscan16" (mscan_kernel, or scan_kernel past 16 signatures).  Every
+    list must equal the oracle's and the batch must have run on the expected
+    kernel (eval_kernel 1 scan, 2 mscan, 4 hashed)."""
     set_kernel(monkeypatch, kernel)
     rs = run_passes(config, n, 2, cfg)
-    assert rs[0].eval_kernel == (4 if kernel == "mhash" or config == 4 else 2)
+    want = (1 if config == 4 else 2) if kernel == "mscan16" else 4
+    assert rs[0].eval_kernel == want
 
 
 @pytest.mark.parametrize("contig,j", [("0", "2"), ("0", "4"), ("1", "4"), ("1", "8")])
