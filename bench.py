@@ -132,6 +132,15 @@ def max_over_ranks(pg, local, x):
     return float(t.item())
 
 
+def sum_over_ranks(pg, local, x):
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=_red_device(pg, local))
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return float(t.item())
+
+
 def host_info():
     model = "unknown"
     try:
@@ -272,6 +281,7 @@ def main():
         # drain what is left so the next step starts from a fresh set
         mm.Remove([t.ticket for t in mm.Extract()]) if mm.ticket_count() else None
     total_t = sum(times)
+    pair_evals = sum_over_ranks(pg, local, pair_evals)  # whole job (each rank counted its own pass)
     value = sum(matched_all) / total_t
     achieved = (eval_bytes / 1e9) / (eval_ms / 1e3) if eval_ms > 0 else 0.0
     avg_launch_ms = eval_ms / max(1, launches)

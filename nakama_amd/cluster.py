@@ -325,6 +325,7 @@ class ClusterMatchmaker:
             self.local.lib.mm_free_matched(self.local.h, C.byref(out))
         t3 = time.perf_counter()
         cp.local_stats = {"pass_ms": stats.pass_ms, "eval_ms": stats.eval_ms, "eval_bytes": stats.eval_bytes,
+                          "pair_evals": stats.pair_evals,
                           "eval_launches": stats.eval_launches, "n_batches": stats.n_batches,
                           "eval_kernel": stats.eval_kernel, "local_call_ms": 1e3 * (t1 - t0),
                           "summary_ms": 1e3 * (t2 - t1), "merge_ms": 1e3 * (t3 - t2)}

@@ -668,6 +668,12 @@ private:
     PinnedArray<uint8_t> h_pack_;
     bool assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t cap, UVec<uint32_t>& brow, PackBatch& pb);
     PackLayout run_packed(const PackBatch& pb, PassStats& stats, const std::function<void()>& overlap);
+    bool plan_packed(size_t n, const UVec<uint32_t>& brow, ParPlan& P, PassStats& stats);
+    std::function<BGroup&(uint32_t)> packed_view(const PackLayout& L, const UVec<uint32_t>& brow);
+    // the replay over this store (mm_process.cpp's Replay: device pages and
+    // pair checks), for the pool workers of replay_parallel
+    ReplayView replay_view() const;
+    std::unique_ptr<ReplayCore> make_replay(std::vector<uint8_t>& sel, bool rev, int max_intervals, PassStats& stats);
     std::vector<uint8_t> dec_;  // per pass: rows a parallel replay decided ahead of the pass's row pointer
     void apply_selected_to_device(const uint32_t* slots, size_t n);
     // A batch's selections reach the device alive mask before the next

@@ -1,0 +1,310 @@
+// nakama_amd/csrc/mm_finish.cpp — the pass's post-pass (matchmaker.go:
+// 320-372): expiry, the completeness re-check with the reference's
+// swap-remove, retirement of matched tickets, and the result arena.
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <stdexcept>
+#include <thread>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include "gocompat.h"
+#include "mm_core.h"
+#include "mm_pass.h"
+
+namespace nkm {
+
+// Process() post-pass (matchmaker.go:320-372).
+// Post-pass bookkeeping (matchmaker.go:320-375).  `disjoint`: no ticket is in
+// two groups (the default pass's selection guarantees it; an override's
+// groups may overlap and then follow the reference's sequential order, where
+// a group meeting an already-retired ticket is dropped).
+void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, bool disjoint) {
+    using fclk = std::chrono::steady_clock;
+    const auto f0 = fclk::now();
+    auto f_ms = [](fclk::time_point a, fclk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fclk::time_point f1 = f0, f2 = f0;
+    for (uint32_t s : expired) is_active_[s] = 0;
+    const size_t ngr = groups.size();
+    if (!disjoint || !par_mode_ || ngr < par_min(16384)) {
+        finish_pass_serial(groups, disjoint);
+    } else {
+        WorkPool& wp = workers();
+        const size_t nchunk = wp.size();
+        // a group is incomplete when one of its tickets left the index
+        std::vector<uint8_t> incomplete(ngr, 0);
+        wp.run(nchunk, [&](size_t c) {
+            for (size_t g = ngr * c / nchunk; g < ngr * (c + 1) / nchunk; g++)
+                for (const auto* e = groups.begin(g); e != groups.end(g); ++e)
+                    if (e->first == kNoSlot || !live_[e->first]) { incomplete[g] = 1; break; }
+        });
+        // group order after the reference's swap-removes (:337-341)
+        std::vector<uint32_t> order(ngr);
+        for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
+        bool removed = false;
+        for (size_t i = 0; i < order.size(); i++) {
+            if (incomplete[order[i]]) {
+                // its members were deleted from the search index when the pass
+                // selected them (matchmaker_process.go:306-321) and stay out of
+                // it: they remain in m.indexes and may still search
+                for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
+                    if (e->first != kNoSlot && live_[e->first]) indexed_[e->first] = 0;
+                order[i] = order.back();
+                order.pop_back();
+                removed = true;
+                i--;
+            }
+        }
+        if (removed) {
+            GroupList kept;
+            for (uint32_t g : order) kept.push(groups.begin(g), groups.end(g));
+            groups = std::move(kept);
+        }
+        f1 = fclk::now();
+        // Retire the matched tickets.  When no session or party holds more
+        // than one ticket, a retired slot left in sessionTickets /
+        // partyTickets counts as absent (SlotSets reads live_), so retiring is
+        // clearing the flags, in parallel chunks of whole groups.
+        if (sess_slots_.more.empty() && party_slots_.more.empty()) {
+            const size_t ng2 = groups.size();
+            std::vector<uint32_t> killed(nchunk, 0);
+            std::vector<std::vector<std::string>> gone(track_removed_ ? nchunk : 0);
+            wp.run(nchunk, [&](size_t c) {
+                uint32_t k = 0;
+                const size_t e0 = groups.off[ng2 * c / nchunk], e1 = groups.off[ng2 * (c + 1) / nchunk];
+                for (size_t i = e0; i < e1; i++) {
+                    const uint32_t s = groups.ents[i].first;
+                    if (!live_[s]) continue;  // a ticket's presence entries repeat its slot
+                    if (track_removed_) gone[c].emplace_back(tk(s));
+                    live_[s] = 0;
+                    is_active_[s] = 0;
+                    k++;
+                }
+                killed[c] = k;
+            });
+            for (uint32_t k : killed) n_live_ -= k;
+            for (auto& v : gone) removed_ids_.insert(removed_ids_.end(), v.begin(), v.end());
+        } else {
+            for (auto& e : groups.ents) kill_slot(e.first, true);
+        }
+        f2 = fclk::now();
+    }
+    filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, list_tmp_,
+                 [&](uint32_t s) { return live_[s] && is_active_[s]; });
+    active_list_.swap(list_tmp_);
+    if (batch_profile_)
+        std::fprintf(stderr, "[nkm]   finish: expired %zu, checks/order %.2f, retire %.2f, active filter %.2f ms\n",
+                     expired.size(), f_ms(f0, f1), f_ms(f1, f2), f_ms(f2 > f0 ? f2 : f0, fclk::now()));
+}
+
+// finish_pass(expired, groups, true) + fill_matched(groups, out, false) for
+// the common large processDefault pass — no group lost a ticket, no session or
+// party holds two tickets, the output arena is free — in two parallel sweeps:
+// the completeness re-check (matchmaker.go:326-343) over every group, then
+// per chunk of groups the result entries and the retirement of their tickets
+// (groups are disjoint, so the sweeps see the state the serial loop would).
+// Returns false, having changed nothing but the expired tickets' active flags
+// (finish_pass sets them again), when a condition fails.
+bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& groups, mm_matched* out, bool mutated) {
+    const size_t ng = groups.size(), ne = groups.ents.size();
+    if (!par_mode_ || ng < par_min(16384) || !sess_slots_.more.empty() || !party_slots_.more.empty()) return false;
+    if (!arena_claimed_ && out_in_use_.exchange(true)) return false;  // a second outstanding result: fill_matched copies
+    arena_claimed_ = true;
+    const bool filled = filled_groups_ == ng;  // the pipelined merge wrote the result entries
+    WorkPool& wp = workers();
+    const size_t nch = (size_t)wp.size() * 2;
+    std::vector<uint8_t> bad(nch, 0);
+    const size_t nx = expired.size();
+    // Without a mutation queued during the pass no member left the index
+    // (groups are formed from live tickets only): every group is complete
+    // and the re-check is skipped; the retire sweep clears the expired flags.
+    if (mutated) {
+        wp.run(nch, [&](size_t c) {
+            for (size_t i = nx * c / nch; i < nx * (c + 1) / nch; i++) is_active_[expired[i]] = 0;
+            for (size_t g = ng * c / nch; g < ng * (c + 1) / nch && !bad[c]; g++)
+                for (const auto* e = groups.begin(g); e != groups.end(g); ++e)
+                    if (e->first == kNoSlot || !live_[e->first]) { bad[c] = 1; break; }
+        });
+        for (uint8_t b : bad)
+            if (b) return false;  // fill_matched, on the claimed arena, after finish_pass's re-check
+    }
+    if (out_offs_.size() < ng + 1) grow_to(out_offs_, ng + 1);
+    if (out_ents_.size() < std::max<size_t>(ne, 1)) grow_to(out_ents_, std::max<size_t>(ne, 1));
+    if (out_created_.size() < std::max<size_t>(ng, 1)) grow_to(out_created_, std::max<size_t>(ng, 1));
+    int32_t* offs = out_offs_.data();
+    mm_entry_ref* ents = out_ents_.data();
+    int64_t* gc = out_created_.data();
+    std::vector<uint32_t> killed(nch, 0);
+    std::vector<std::vector<std::string>> gone(track_removed_ ? nch : 0);
+    wp.run(nch, [&](size_t c) {
+        const size_t g0 = ng * c / nch, g1 = ng * (c + 1) / nch;
+        uint32_t k = 0;
+        if (!mutated)
+            for (size_t i = nx * c / nch; i < nx * (c + 1) / nch; i++) is_active_[expired[i]] = 0;
+        if (!filled) {
+            for (size_t g = g0; g < g1; g++) {
+                offs[g] = (int32_t)groups.off[g];
+                gc[g] = groups.len(g) ? created_[groups.end(g)[-1].first] : 0;
+            }
+            if (c + 1 == nch) offs[ng] = (int32_t)groups.off[ng];
+        }
+        for (size_t i = groups.off[g0]; i < groups.off[g1]; i++) {
+            const uint32_t s = groups.ents[i].first;
+            if (!filled) {
+                ents[i].ticket = tk_ptr_[s];
+                ents[i].presence_index = groups.ents[i].second;
+                ents[i].reserved = 0;
+            }
+            if (!live_[s]) continue;  // a ticket's presence entries repeat its slot
+            if (track_removed_) gone[c].emplace_back(tk(s));
+            live_[s] = 0;  // retired: sessionTickets / partyTickets read live_ (SlotSets)
+            is_active_[s] = 0;
+            k++;
+        }
+        killed[c] = k;
+    });
+    for (uint32_t k : killed) n_live_ -= k;
+    for (auto& v : gone) removed_ids_.insert(removed_ids_.end(), v.begin(), v.end());
+    filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, list_tmp_,
+                 [&](uint32_t s) { return live_[s] && is_active_[s]; });
+    active_list_.swap(list_tmp_);
+    out->group_created = gc;
+    out->n_groups = (int32_t)ng;
+    out->n_entries = (int32_t)ne;
+    out->group_offsets = offs;
+    out->entries = ents;
+    out->is_candidates = 0;
+    out->reserved2 = 1;  // the handle's arena (out_in_use_ until mm_free_matched)
+    arena_claimed_ = false;
+    return true;
+}
+
+void Core::finish_pass_serial(GroupList& groups, bool selected) {
+    std::vector<uint32_t> order(groups.size());
+    for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
+    bool removed = false;
+    for (size_t i = 0; i < order.size(); i++) {
+        bool incomplete = false;
+        for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
+            if (e->first == kNoSlot || !live_[e->first]) { incomplete = true; break; }
+        if (incomplete) {  // swap-remove (:337-341)
+            // processDefault deleted the members from the search index when it
+            // selected them (matchmaker_process.go:306-321): they stay out of it
+            if (selected)
+                for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e)
+                    if (e->first != kNoSlot && live_[e->first]) indexed_[e->first] = 0;
+            order[i] = order.back();
+            order.pop_back();
+            removed = true;
+            i--;
+            continue;
+        }
+        for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e) kill_slot(e->first, true);
+    }
+    if (removed) {
+        GroupList kept;
+        for (uint32_t g : order) kept.push(groups.begin(g), groups.end(g));
+        groups = std::move(kept);
+    }
+}
+
+void Core::fill_matched(const GroupList& groups, mm_matched* out,
+                        bool cands) {
+    const size_t n = groups.ents.size();
+    // The handle's arena (reused: its pages stay mapped) points entries at the
+    // store's ticket-string arena, which does not move while the result is
+    // outstanding (compaction waits for mm_free_matched).  A second
+    // outstanding result gets private copies.
+    const bool arena = arena_claimed_ || !out_in_use_.exchange(true);
+    arena_claimed_ = false;
+    int32_t* offs;
+    mm_entry_ref* ents;
+    char* buf = nullptr;
+    if (arena) {
+        if (out_offs_.size() < groups.size() + 1) grow_to(out_offs_, groups.size() + 1);
+        if (out_ents_.size() < std::max<size_t>(n, 1)) grow_to(out_ents_, std::max<size_t>(n, 1));
+        offs = out_offs_.data();
+        ents = out_ents_.data();
+    } else {
+        size_t bytes = 0;
+        for (auto& e : groups.ents) bytes += tk_len_[e.first] + 1;
+        offs = new int32_t[groups.size() + 1];
+        ents = new mm_entry_ref[n ? n : 1];
+        buf = new char[bytes ? bytes : 1];
+    }
+    int64_t* gc;  // per group: its last entry's CreatedAt (the cluster merge's key)
+    if (arena) {
+        if (out_created_.size() < std::max<size_t>(groups.size(), 1)) grow_to(out_created_, std::max<size_t>(groups.size(), 1));
+        gc = out_created_.data();
+    } else {
+        gc = new int64_t[groups.size() ? groups.size() : 1];
+    }
+    auto created_of = [&](size_t g) {
+        const uint32_t last = groups.len(g) ? groups.end(g)[-1].first : kNoSlot;
+        gc[g] = last == kNoSlot ? 0 : created_[last];
+    };
+    size_t b = 0;
+    if (arena && par_mode_ && n >= par_min(65536)) {  // chunks of the result in parallel
+        WorkPool& wp = workers();
+        const size_t nch = wp.size(), ng = groups.size() + 1;
+        wp.run(nch, [&](size_t c) {
+            for (size_t gi = ng * c / nch; gi < ng * (c + 1) / nch; gi++) {
+                offs[gi] = (int32_t)groups.off[gi];
+                if (gi < ng - 1) created_of(gi);
+            }
+            for (size_t k = n * c / nch; k < n * (c + 1) / nch; k++) {
+                const auto& e = groups.ents[k];
+                ents[k].ticket = tk_ptr_[e.first];
+                ents[k].presence_index = e.second;
+                ents[k].reserved = 0;
+            }
+        });
+    } else {
+        for (size_t gi = 0; gi <= groups.size(); gi++) offs[gi] = (int32_t)groups.off[gi];
+        for (size_t g = 0; g < groups.size(); g++) created_of(g);
+        uint32_t prev = kNoSlot;
+        const char* prev_p = nullptr;
+        for (size_t k = 0; k < n; k++) {
+            const auto& e = groups.ents[k];
+            if (e.first != prev) {
+                if (arena) {
+                    prev_p = tk_ptr_[e.first];
+                } else {
+                    std::memcpy(buf + b, tk_ptr_[e.first], tk_len_[e.first] + 1);
+                    prev_p = buf + b;
+                    b += tk_len_[e.first] + 1;
+                }
+                prev = e.first;
+            }
+            ents[k].ticket = prev_p;
+            ents[k].presence_index = e.second;
+            ents[k].reserved = 0;
+        }
+    }
+    out->group_created = gc;
+    out->n_groups = (int32_t)groups.size();
+    out->n_entries = (int32_t)n;
+    out->group_offsets = offs;
+    out->entries = ents;
+    out->is_candidates = cands ? 1 : 0;
+    out->reserved2 = arena ? 1 : (int64_t)(intptr_t)buf;  // 1: the handle's arena
+}
+
+void Core::free_matched(mm_matched* out) {
+    if (!out) return;
+    if (out->reserved2 == 1) {
+        out_in_use_.store(false);
+    } else if (out->reserved2 != 0 || out->group_offsets) {
+        delete[] out->group_offsets;
+        delete[] out->entries;
+        delete[] out->group_created;
+        delete[] reinterpret_cast<char*>((intptr_t)out->reserved2);
+    }
+    std::memset(out, 0, sizeof(*out));
+}
+
+
+}  // namespace nkm

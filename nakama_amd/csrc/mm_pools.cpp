@@ -1,0 +1,1006 @@
+// nakama_amd/csrc/mm_pools.cpp — the pool-parallel replay (plan_pools,
+// replay_parallel and the merges back into the pinned row order) and the
+// packed RevPrecision batches (assembly, rpack_kernel's launch, per-row
+// views).  Part of Core's pass (mm_process.cpp).
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <stdexcept>
+#include <thread>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include "gocompat.h"
+#include "mm_core.h"
+#include "mm_pass.h"
+
+namespace nkm {
+
+// Pool-parallel replay.  When every search of the batch draws its hits from a
+// posting list of the same field with a distinct term, every searching ticket
+// carries its own search's term, and every list is complete, then each
+// search's rows only ever select tickets of its own posting list: the greedy
+// pass decomposes exactly into independent per-pool passes (processDefault's
+// sequential order is preserved within each pool, and no ticket is shared
+// across pools).  The pools run on host threads; results are merged back into
+// the pinned row order.  Returns false (nothing done) when the conditions fail.
+// The part of the pool-parallel replay that needs no hit list — the pool
+// keys and the rows bucketed per pool — run while the batch's searches are
+// on the device.  Returns false when the batch does not partition into pools.
+bool Core::plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
+                         const UVec<uint32_t>& brow_group, ParPlan& P, PassStats& stats) {
+    return plan_pools(
+        bg.size(), [&](size_t i) { return bg[i].sig; }, [&](size_t bi) { return brow_group[bi]; },
+        [&](size_t i) { return bg[i].row_slot; }, brow, P, stats);
+}
+
+// plan_parallel over `nsearch` searches: sig_of(i) is search i's signature,
+// group_of(bi) batch row bi's search (a packed RevPrecision batch: the row
+// itself), row_of(i) the slot of a one-row search (RevPrecision) or kNoSlot.
+// Every step is a parallel sweep over the searches or the rows; the pools are
+// numbered in first-appearance order (C5: 125k pools per 1M rows).  A one-row
+// search whose ticket carries its own search's terms (self_match_) takes its
+// pool key from its own column, not from the signature's term list.
+template <class SigOf, class GroupOf, class RowOf>
+bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_of, const UVec<uint32_t>& brow,
+                      ParPlan& P, PassStats& stats) {
+    P.ok = false;
+    if (nsearch < 2) return false;
+    using clk = std::chrono::steady_clock;
+    auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto tp0 = clk::now();
+    WorkPool& wp = workers();
+    const bool par = nsearch >= par_min(65536) && par_mode_;
+    const unsigned nsch = par ? wp.size() * 2 : 1;
+    auto sweep = [&](size_t n, unsigned nch, auto&& fn) {  // fn(chunk, lo, hi) over [0, n) in nch chunks
+        if (nch > 1)
+            wp.run(nch, [&](size_t c) { fn(c, n * c / nch, n * (c + 1) / nch); });
+        else
+            fn(0, 0, n);
+    };
+    // pool key fields: fields every search requires a keyword term on (the
+    // candidates are the first search's; each chunk of searches checks them)
+    std::vector<uint16_t> cand;
+    for (auto& mt : sigs_[sig_of(0)].must_terms)
+        if (std::find(cand.begin(), cand.end(), mt.first) == cand.end()) cand.push_back(mt.first);
+    std::vector<std::vector<uint8_t>> has(nsch, std::vector<uint8_t>(cand.size(), 1));
+    // fields below 63: the signatures' must-field masks (no term lists read)
+    uint64_t cmask = 0;
+    bool narrow = true;
+    for (uint16_t f : cand) {
+        if (f >= 63) narrow = false;
+        else cmask |= 1ull << f;
+    }
+    std::vector<uint64_t> hmask(nsch, ~0ull);
+    sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
+        if (narrow) {
+            uint64_t m = cmask;
+            for (size_t i = lo; i < hi && m; i++) m &= sigs_[sig_of(i)].must_fmask;
+            hmask[ch] = m;
+            return;
+        }
+        for (size_t i = lo; i < hi; i++) {
+            const auto& mts = sigs_[sig_of(i)].must_terms;
+            for (size_t k = 0; k < cand.size(); k++) {
+                if (!has[ch][k]) continue;
+                bool h = false;
+                for (auto& m2 : mts) h |= m2.first == cand[k];
+                if (!h) has[ch][k] = 0;
+            }
+        }
+    });
+    if (narrow)
+        for (unsigned ch = 0; ch < nsch; ch++)
+            for (size_t k = 0; k < cand.size(); k++) has[ch][k] = (hmask[ch] >> cand[k]) & 1;
+    std::vector<uint16_t> keyf;
+    for (size_t k = 0; k < cand.size(); k++) {
+        bool all = true;
+        for (unsigned ch = 0; ch < nsch; ch++) all = all && has[ch][k];
+        if (all) keyf.push_back(cand[k]);
+    }
+    if (keyf.empty()) return false;
+    for (uint16_t f : keyf)
+        if (fkind_[f].size() != nslots()) return false;
+    // pool key of each search; a search requiring two different terms on one
+    // field matches nothing (the batch then takes the serial replay).  One key
+    // field (C5's buckets: ~10^5 pools): keys extracted on the workers and
+    // pools numbered in parallel through dictionary-id tables; more fields
+    // (mode x region: few pools): an ordered map.
+    std::vector<uint32_t>& search_pool = P.search_pool;
+    grow_to(search_pool, nsearch);
+    std::vector<uint32_t>& pool_key1 = P.pool_key1;  // one key field: pool -> its term
+    std::vector<std::vector<uint32_t>> pool_keys;    // several: pool -> its terms
+    auto key_of = [&](size_t i, uint32_t* key) {
+        for (size_t k = 0; k < keyf.size(); k++) key[k] = UINT32_MAX;
+        for (size_t k = 0; k < keyf.size(); k++)
+            for (auto& mt : sigs_[sig_of(i)].must_terms)
+                if (mt.first == keyf[k]) {
+                    if (key[k] != UINT32_MAX && key[k] != mt.second) return false;
+                    key[k] = mt.second;
+                }
+        return true;
+    };
+    size_t ng = 0;
+    if (keyf.size() == 1) {
+        std::vector<uint32_t>& k1 = search_pool;  // the key term first, renumbered in place below
+        std::vector<uint8_t> bad(nsch, 0);
+        const size_t nd = dict_.size();
+        // first[t]: the lowest search index with term t (atomic min over the
+        // chunks); the heads (first[t] == i) are numbered in index order
+        if (pool_first_cap_ < nd) {
+            pool_first_.reset(new std::atomic<uint32_t>[nd + nd / 4]);
+            pool_first_cap_ = nd + nd / 4;
+        }
+        std::atomic<uint32_t>* first = pool_first_.get();
+        std::vector<uint32_t>& tpool = pool_remap_;  // term -> pool (written by its head only)
+        grow_to(tpool, nd);
+        sweep(nd, nsch, [&](size_t, size_t lo, size_t hi) {
+            for (size_t t = lo; t < hi; t++) first[t].store(UINT32_MAX, std::memory_order_relaxed);
+        });
+        std::vector<size_t> heads(nsch + 1, 0);
+        const uint16_t f0 = keyf[0];
+        sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
+            uint32_t kk[4];
+            for (size_t i = lo; i < hi; i++) {
+                const uint32_t r = row_of(i);
+                if (r != kNoSlot && self_match_[r] && indexed_[r] && sig_[r] == sig_of(i) &&
+                    fkind_[f0][r] == KIND_KEYWORD)
+                    kk[0] = (uint32_t)fval_[f0][r];  // the row carries its search's term on f0
+                else if (!key_of(i, kk))
+                    kk[0] = UINT32_MAX;
+                if (kk[0] == UINT32_MAX || kk[0] >= nd) { bad[ch] = 1; return; }
+                k1[i] = kk[0];
+                uint32_t cur = first[kk[0]].load(std::memory_order_relaxed);
+                while ((uint32_t)i < cur && !first[kk[0]].compare_exchange_weak(cur, (uint32_t)i, std::memory_order_relaxed)) {
+                }
+            }
+        });
+        for (uint8_t b : bad)
+            if (b) return false;
+        sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
+            size_t h = 0;
+            for (size_t i = lo; i < hi; i++) h += first[k1[i]].load(std::memory_order_relaxed) == (uint32_t)i;
+            heads[ch + 1] = h;
+        });
+        for (unsigned ch = 0; ch < nsch; ch++) heads[ch + 1] += heads[ch];
+        ng = heads[nsch];
+        grow_to(pool_key1, ng);
+        sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
+            size_t p = heads[ch];
+            for (size_t i = lo; i < hi; i++)
+                if (first[k1[i]].load(std::memory_order_relaxed) == (uint32_t)i) {
+                    tpool[k1[i]] = (uint32_t)p;
+                    pool_key1[p++] = k1[i];
+                }
+        });
+        sweep(nsearch, nsch, [&](size_t, size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; i++) k1[i] = tpool[k1[i]];
+        });
+    } else {
+        std::map<std::vector<uint32_t>, uint32_t> pool_of;
+        std::vector<uint32_t> key(keyf.size());
+        for (size_t i = 0; i < nsearch; i++) {
+            if (!key_of(i, key.data())) return false;
+            auto it = pool_of.emplace(key, (uint32_t)pool_of.size());
+            if (it.second) pool_keys.push_back(key);
+            search_pool[i] = it.first->second;
+        }
+        ng = pool_keys.size();
+    }
+    if (ng < 2) return false;
+    P.ng = ng;
+    auto pool_key = [&](size_t p, size_t f) { return keyf.size() == 1 ? pool_key1[p] : pool_keys[p][f]; };
+    // every searching ticket must itself belong to its search's pool; the
+    // rows are bucketed per pool in batch order (CSR: per-chunk counts, then
+    // every chunk scatters at its offsets; counters stay thread-private)
+    const size_t nb = brow.size();
+    const unsigned nchunk = nb >= par_min(65536) ? wp.size() : 1;
+    UVec<uint32_t>& cnt = pool_cnt_;  // [chunk][pool]: each chunk writes its row in full
+    grow_to(cnt, (size_t)nchunk * ng);
+    std::vector<uint8_t> cbad(nchunk, 0);
+    // per (chunk, pool): a row that is not known to carry its own search's
+    // terms (self_match_) — the pool is then not known to hold all its rows
+    UVec<uint8_t>& cforeign = pool_foreign_;
+    grow_to(cforeign, (size_t)nchunk * ng);
+    const auto tp1 = clk::now();
+    sweep(nb, nchunk, [&](size_t c, size_t lo, size_t hi) {
+        // thread-private counters (few pools: the chunks' rows of cnt share
+        // cache lines), copied out at the end
+        static thread_local std::vector<uint32_t> k;
+        static thread_local std::vector<uint8_t> fo;
+        k.assign(ng, 0);
+        fo.assign(ng, 0);
+        for (size_t bi = lo; bi < hi; bi++) {
+            const uint32_t r = brow[bi];
+            const uint32_t gi = group_of(bi);
+            const uint32_t p = search_pool[gi];
+            k[p]++;
+            // the row carries every term of its own search: the pool's keys among them
+            if (self_match_[r] && indexed_[r] && sig_[r] == sig_of(gi)) continue;
+            fo[p] = 1;
+            for (size_t f = 0; f < keyf.size(); f++)
+                if (fkind_[keyf[f]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[f]][r] != pool_key(p, f)) {
+                    cbad[c] = 1;
+                    return;
+                }
+        }
+        std::memcpy(cnt.data() + c * ng, k.data(), ng * sizeof(uint32_t));
+        std::memcpy(cforeign.data() + c * ng, fo.data(), ng);
+    });
+    const auto tp2 = clk::now();
+    for (unsigned c = 0; c < nchunk; c++)
+        if (cbad[c]) return false;
+    // per pool: rows and self flag (ranges of pools on the workers), the
+    // pool offsets (one scan), then each (chunk, pool)'s first position
+    grow_to(P.self_rows, ng);
+    grow_to(P.pool_off, ng + 1);
+    const unsigned npch = ng >= 65536 && nchunk > 1 ? nchunk : 1;
+    sweep(ng, npch, [&](size_t, size_t lo, size_t hi) {
+        for (size_t p = lo; p < hi; p++) {
+            uint32_t t = 0;
+            uint8_t f = 0;
+            for (unsigned c = 0; c < nchunk; c++) {
+                t += cnt[c * ng + p];
+                f |= cforeign[c * ng + p];
+            }
+            P.pool_off[p + 1] = t;
+            P.self_rows[p] = f ? 0 : 1;
+        }
+    });
+    P.pool_off[0] = 0;
+    for (size_t p = 0; p < ng; p++) P.pool_off[p + 1] += P.pool_off[p];
+    sweep(ng, npch, [&](size_t, size_t lo, size_t hi) {
+        for (size_t p = lo; p < hi; p++) {
+            uint32_t run = P.pool_off[p];
+            for (unsigned c = 0; c < nchunk; c++) {
+                const uint32_t v = cnt[c * ng + p];
+                cnt[c * ng + p] = run;
+                run += v;
+            }
+        }
+    });
+    grow_to(P.pool_rows, nb);
+    const auto tp3 = clk::now();
+    sweep(nb, nchunk, [&](size_t c, size_t lo, size_t hi) {
+        static thread_local std::vector<uint32_t> at;
+        at.assign(cnt.begin() + c * ng, cnt.begin() + (c + 1) * ng);
+        for (size_t bi = lo; bi < hi; bi++) P.pool_rows[at[search_pool[group_of(bi)]]++] = (uint32_t)bi;
+    });
+    const auto tp4 = clk::now();
+    stats.par_bucket_ms += msd(tp0, tp4);
+    if (batch_profile_)
+        std::fprintf(stderr, "[nkm]   plan_pools: %zu pools | keys %.2f count %.2f offsets %.2f scatter %.2f ms\n", ng,
+                     msd(tp0, tp1), msd(tp1, tp2), msd(tp2, tp3), msd(tp3, tp4));
+    P.ok = true;
+    return true;
+}
+
+// Pool-parallel replay over the bucketed rows (plan_parallel); false when a
+// pool's list came back truncated (the serial replay then decides the batch).
+// Pools are walked on the host workers (largest first, small ones bundled
+// into tasks); every processed row leaves a record at its batch position, and
+// one pass over the batch in row order assembles the groups, the expired list
+// and the Intervals increments — processDefault's sequential order, because
+// no pool ever selects another pool's ticket.
+bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
+                           const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel,
+                           GroupList& out_groups,
+                           std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
+                           uint32_t* min_stop, const std::function<BGroup&(uint32_t)>* view) {
+    *min_stop = UINT32_MAX;
+    if (!P.ok) return false;
+    // Truncated lists are allowed: a pool whose row runs past the end of its
+    // list stops there (the row's search re-runs in the next batch), the other
+    // pools carry on; every row a pool processed is decided (pools never share
+    // a ticket), and the pass puts the groups back in row order at its end.
+    // view: a packed batch (rpack_kernel) — row bi's search is view(bi), a
+    // thread-local BGroup over the row's packed list (complete by construction)
+    bool all_complete = true;
+    if (!view)
+        for (const BGroup& g : bg) all_complete = all_complete && g.complete;
+    if (!all_complete && !partial_mode_) return false;
+    using clk = std::chrono::steady_clock;
+    auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto tp1 = clk::now();
+    const size_t nsearch = bg.size(), ng = P.ng, nb = brow.size();
+    const std::vector<uint32_t>& search_pool = P.search_pool;
+    WorkPool& wp = workers();
+    const int maxI = cfg_.max_intervals;
+    // each pool's searches (CSR) and each search's index among them: only
+    // the dense walk reads them (one search per pool, no RevPrecision)
+    const bool want_dense = dense_mode_ && !rev && !view;
+    std::vector<uint32_t> soff(want_dense ? ng + 1 : 0, 0), sidx(want_dense ? nsearch : 0);
+    if (want_dense) {
+        for (size_t i = 0; i < nsearch; i++) soff[search_pool[i] + 1]++;
+        for (size_t p = 0; p < ng; p++) soff[p + 1] += soff[p];
+        std::vector<uint32_t> at(soff.begin(), soff.end() - 1);
+        for (size_t i = 0; i < nsearch; i++) {
+            const uint32_t p = search_pool[i];
+            sidx[at[p]++] = (uint32_t)i;
+        }
+    }
+    auto prows = [&](size_t p) { return P.pool_off[p + 1] - P.pool_off[p]; };
+    // tasks: pools by size (largest first), the small ones bundled; many
+    // pools (C5's 10^5 buckets) are bundled in pool order unsorted — every
+    // task holds many, so the largest-first order buys no balance
+    std::vector<uint32_t> order_g(ng);
+    for (size_t i = 0; i < ng; i++) order_g[i] = (uint32_t)i;
+    if (ng <= 4096)
+        std::sort(order_g.begin(), order_g.end(), [&](uint32_t a, uint32_t b) { return prows(a) > prows(b); });
+    const size_t per_task = std::max<size_t>(1, nb / ((size_t)wp.size() * 8));
+    std::vector<uint32_t> task_off{0};
+    for (size_t k = 0, acc = 0; k < ng; k++) {
+        acc += prows(order_g[k]);
+        if (acc >= per_task || k + 1 == ng) {
+            task_off.push_back((uint32_t)(k + 1));
+            acc = 0;
+        }
+    }
+    const size_t ntask = task_off.size() - 1;
+    // Few pools (C3's 8, C4's 64): each pool keeps its records in its own
+    // array and the merge interleaves them (their rows interleave finely in
+    // batch order, so per-row stores from several walks would share cache
+    // lines).  Many pools (C5's buckets: each a short run of the batch):
+    // records go straight to their batch rows.
+    const bool few = ng <= 64;
+    if (task_ents_.size() < ntask) task_ents_.resize(ntask);
+    if (few && pool_outs_.size() < ng) pool_outs_.resize(ng);
+    if (!few && row_recs_.size() < nb) grow_to(row_recs_, nb);
+    RowRec* rr = few ? nullptr : row_recs_.data();
+    if (!few)
+        wp.run(wp.size(), [&](size_t c) {  // rows no pool processes (selected before they were reached) stay zero
+            std::memset((void*)(rr + nb * c / wp.size()), 0, (nb * (c + 1) / wp.size() - nb * c / wp.size()) * sizeof(RowRec));
+        });
+    // Pools with one search (no RevPrecision) walk dense per-position copies
+    // of their list (DensePool/DenseRun), gathered first in chunks across the
+    // workers; the others take the generic walk over the store.
+    if (dense_pools_.size() < ng) dense_pools_.resize(ng);
+    if (pos_of_.size() < nslots()) pos_of_.resize(nslots(), kNoSlot);
+    const ReplayView rv = replay_view();
+    // The gathers run in tasks that each take the same fraction of EVERY
+    // dense pool's list: the pools interleave in scan order, so task t's
+    // pieces all read one slot region and the store lines it touches (2
+    // HotRecs, 16 Intervals / pos_of words per line) are shared by the pools'
+    // pieces while they sit in the core's cache — per-pool tasks read each
+    // line once per pool (C4: 64 pools, every read a miss).
+    constexpr uint32_t kGatherTask = 16384;  // list positions per task, over all pools
+    std::vector<uint8_t> dense(ng, 0);
+    std::vector<uint32_t> dense_ids;
+    uint64_t dense_total = 0;
+    for (size_t gi = 0; gi < ng && want_dense; gi++) {
+        if (soff[gi + 1] - soff[gi] != 1) continue;  // the dense walk has no reverse checks
+        if (!bg[sidx[soff[gi]]].complete) continue;                        // nor pages
+        dense[gi] = 1;
+        DensePool& D = dense_pools_[gi];
+        D.reset(bg[sidx[soff[gi]]], P.pool_rows.data() + P.pool_off[gi], (uint32_t)prows(gi), brow.data());
+        dense_ids.push_back((uint32_t)gi);
+        dense_total += D.n;
+    }
+    const size_t ntask_g = (size_t)((dense_total + kGatherTask - 1) / kGatherTask);
+    auto piece = [&](const DensePool& D, size_t t, uint32_t& lo, uint32_t& hi) {
+        lo = (uint32_t)((uint64_t)D.n * t / ntask_g);
+        hi = (uint32_t)((uint64_t)D.n * (t + 1) / ntask_g);
+    };
+    // Pipelined merge: with few pools, all dense, the merge runs in the same
+    // job as the walks — tasks [0, ntask) walk, the next nch tasks merge one
+    // chunk of batch rows each as soon as every walk has passed the chunk's
+    // end (tasks are claimed in index order, so every walk is running before
+    // any merge waits).  C3's 8 walks would otherwise leave 8 of 16 workers
+    // idle while the merge waits for the slowest walk.
+    const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
+    const bool pipe = few && pipe_mode_ && !dense_ids.empty() && dense_ids.size() == ng && nch > 1;
+    // Pipelined gather: when every pool's rows are its list in list order
+    // (identity pools — C3 / C4: every member of a pool of fresh tickets
+    // searches, and batch order is scan order) no slot -> position map is
+    // built, and the gathers run in the walks' job: tasks after the walks
+    // gather piece t of every pool and publish each pool's gathered prefix;
+    // a walk reads a position once it is covered (DenseRun::need).  Needs a
+    // worker beyond the walks (tasks are claimed in index order).
+    const auto tg0 = clk::now();
+    bool gpipe = false;
+    if (pipe && gpipe_mode_ && wp.size() > ntask) {
+        bool all = true;
+        for (uint32_t gi : dense_ids) all = all && dense_pools_[gi].nrows == dense_pools_[gi].n;
+        // Slots in time order (monotone_): scan order = batch order, so the
+        // rows ARE the list when they are as many and each lies in it — a
+        // row carrying its term-only search's terms matches that search
+        // (its own counts meet its count ranges; the party exclusion is the
+        // walk's) and is alive.  Otherwise compare position by position.
+        bool known = all && monotone_;
+        for (uint32_t gi : dense_ids) {
+            if (!known) break;
+            const Sig& sg = sigs_[bg[sidx[soff[gi]]].sig];
+            known = P.self_rows[gi] && sg.qkind == QK_BOOL && sg.must_terms.size() == sg.n_clauses;
+        }
+        if (known) {
+            gpipe = true;
+        } else if (all) {
+            std::vector<uint8_t> ok(ntask_g, 1);
+            wp.run(ntask_g, [&](size_t t) {
+                for (uint32_t gi : dense_ids) {
+                    const DensePool& D = dense_pools_[gi];
+                    uint32_t lo, hi;
+                    piece(D, t, lo, hi);
+                    if (!D.rows_are_list(lo, hi)) { ok[t] = 0; return; }
+                }
+            });
+            gpipe = std::all_of(ok.begin(), ok.end(), [](uint8_t x) { return x != 0; });
+        }
+    }
+    std::unique_ptr<std::atomic<uint32_t>[]> gfront(gpipe ? new std::atomic<uint32_t>[ng] : nullptr);
+    std::unique_ptr<std::atomic<uint8_t>[]> gdone(gpipe ? new std::atomic<uint8_t>[ng * ntask_g] : nullptr);
+    std::atomic<bool> id_broken{false};  // an identity pool whose row was not at its position (a bug: fail loudly)
+    if (gpipe) {
+        for (size_t gi = 0; gi < ng; gi++) gfront[gi].store(0);
+        for (size_t k = 0; k < ng * ntask_g; k++) gdone[k].store(0);
+        for (uint32_t gi : dense_ids) {
+            DensePool& D = dense_pools_[gi];
+            D.identity = true;
+            D.pieces = (uint32_t)ntask_g;
+            D.front = &gfront[gi];
+            D.broken = &id_broken;
+        }
+    }
+    // piece t of every pool, then each pool's published prefix advanced over
+    // the pieces done (whichever worker completes the next piece moves it on)
+    auto gather_piece = [&](size_t t) {
+        for (uint32_t gi : dense_ids) {
+            DensePool& D = dense_pools_[gi];
+            uint32_t lo, hi;
+            piece(D, t, lo, hi);
+            D.gather(rv, lo, hi, pos_of_.data());
+            gdone[gi * ntask_g + t].store(1);
+            uint32_t f = gfront[gi].load();
+            while (f < ntask_g && gdone[gi * ntask_g + f].load())
+                if (gfront[gi].compare_exchange_weak(f, f + 1)) f++;
+        }
+    };
+    // each pool's entry bound (every ticket of its list and rows joins at
+    // most one group): the walk reserves it so readers never see a move
+    std::vector<uint64_t> esum(pipe && !gpipe ? ntask_g * ng : 0, 0);
+    if (!gpipe)
+        wp.run(ntask_g, [&](size_t t) {
+            for (uint32_t gi : dense_ids) {
+                DensePool& D = dense_pools_[gi];
+                uint32_t lo, hi;
+                piece(D, t, lo, hi);
+                D.gather(rv, lo, hi, pos_of_.data());
+                if (!pipe) continue;
+                uint64_t e = 0;
+                for (uint32_t k = lo; k < hi; k++) e += (uint64_t)D.rec[k].count;
+                const uint32_t r0 = (uint32_t)((uint64_t)D.nrows * t / ntask_g), r1 = (uint32_t)((uint64_t)D.nrows * (t + 1) / ntask_g);
+                for (uint32_t j = r0; j < r1; j++) e += (uint64_t)rv.hot[brow[D.bis[j]]].count;
+                esum[t * ng + gi] = e;
+            }
+        });
+    struct alignas(128) Prog {
+        std::atomic<uint64_t> st{0};  // (records published << 32) | rows done
+        const PoolRec* recs = nullptr;
+        const std::pair<uint32_t, int>* ents = nullptr;
+    };
+    std::unique_ptr<Prog[]> prog(pipe ? new Prog[ng] : nullptr);
+    std::vector<uint64_t> ebound(pipe ? ng : 0, 0);
+    uint64_t ebound_all = 0;
+    for (size_t t = 0; pipe && !gpipe && t < ntask_g; t++)
+        for (size_t gi = 0; gi < ng; gi++) ebound[gi] += esum[t * ng + gi];
+    if (gpipe)  // identity pools: the rows are list members, whose entries are at most max_pres_ each
+        for (uint32_t gi : dense_ids) ebound[gi] = (uint64_t)dense_pools_[gi].n * (uint64_t)std::max(1, max_pres_);
+    for (uint64_t e : ebound) ebound_all += e;
+    const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
+    if (pipe) {  // bounds now (no zero-fill: default-initialising vectors), the totals after the job
+        grow_to(out_groups.off, g0 + 1 + nb);
+        grow_to(out_groups.ents, e0 + ebound_all);
+        grow_to(expired, x0 + nb);
+        grow_to(newly, n0 + ebound_all);
+    }
+    // the result entries too, when every earlier group of the pass is filled
+    // and the output arena is (or can be) this pass's
+    const bool fill = pipe && filled_groups_ == g0 && (arena_claimed_ || !out_in_use_.exchange(true));
+    if (fill) {
+        arena_claimed_ = true;
+        if (out_offs_.size() < g0 + 1 + nb) grow_to(out_offs_, g0 + 1 + nb);
+        if (out_ents_.size() < e0 + ebound_all) grow_to(out_ents_, e0 + ebound_all);
+        if (out_created_.size() < g0 + nb) grow_to(out_created_, g0 + nb);
+        out_offs_[0] = 0;
+    }
+    // one chunk of the pipelined merge (merge_pools' chunk body, offsets
+    // from the pools' running counts instead of a global prefix)
+    auto merge_chunk = [&](size_t c) {
+        const uint32_t lo = (uint32_t)(nb * c / nch), hi = (uint32_t)(nb * (c + 1) / nch);
+        size_t gk = g0, ek = e0, xk = x0;
+        static thread_local std::vector<uint64_t> span;  // per pool: records [a, b) of the chunk
+        span.assign(ng, 0);
+        for (size_t gi = 0; gi < ng; gi++) {
+            const DensePool& D = dense_pools_[gi];
+            const uint32_t need = (uint32_t)(std::lower_bound(D.bis, D.bis + D.nrows, hi) - D.bis);
+            if (!need) continue;
+            uint64_t v;
+            while (((v = prog[gi].st.load(std::memory_order_acquire)) & 0xffffffffu) < need) std::this_thread::yield();
+            const uint32_t nrec = (uint32_t)(v >> 32);
+            const PoolRec* R = prog[gi].recs;
+            auto by_bi = [](const PoolRec& x, uint32_t b) { return x.bi < b; };
+            const uint32_t a = (uint32_t)(std::lower_bound(R, R + nrec, lo, by_bi) - R);
+            const uint32_t b = (uint32_t)(std::lower_bound(R + a, R + nrec, hi, by_bi) - R);
+            if (a < nrec) {
+                gk += R[a].gcum;
+                ek += R[a].off;
+                xk += R[a].xcum;
+            } else if (nrec) {
+                const PoolRec& l = R[nrec - 1];
+                gk += l.gcum + l.matched;
+                ek += l.off + l.len;
+                xk += l.xcum + l.expired;
+            }
+            span[gi] = ((uint64_t)b << 32) | a;
+        }
+        static thread_local std::vector<uint64_t> at_row;  // (pool << 32 | record) + 1; 0: no record
+        at_row.assign(hi - lo, 0);
+        for (size_t gi = 0; gi < ng; gi++) {
+            const PoolRec* R = prog[gi].recs;
+            for (uint32_t k = (uint32_t)span[gi]; k < (uint32_t)(span[gi] >> 32); k++)
+                at_row[R[k].bi - lo] = (((uint64_t)gi << 32) | k) + 1;
+        }
+        for (uint32_t i = 0; i < hi - lo; i++) {
+            if (!at_row[i]) continue;
+            const uint64_t v = at_row[i] - 1;
+            const Prog& pr = prog[v >> 32];
+            const PoolRec& r = pr.recs[(uint32_t)v];
+            const uint32_t T = brow[r.bi];
+            intervals_[T]++;  // the row's pending Intervals increment
+            dec_[T] = 1;      // decided: a later batch of the pass skips it
+            if (r.expired) expired[xk++] = T;
+            if (!r.matched) continue;
+            for (uint32_t k = 0; k < r.len; k++) {
+                const auto& e = pr.ents[r.off + k];
+                out_groups.ents[ek + k] = e;
+                newly[n0 + (ek - e0) + k] = e.first;
+                sel[e.first] = 1;
+                if (fill) out_ents_[ek + k] = mm_entry_ref{tk_ptr_[e.first], e.second, 0};
+            }
+            if (fill) out_created_[gk] = created_[T];  // the group's searching ticket (its last entry)
+            ek += r.len;
+            out_groups.off[++gk] = (uint32_t)ek;
+            if (fill) out_offs_[gk] = (int32_t)ek;
+        }
+    };
+    std::vector<double> task_ms(ntask, 0.0);
+    std::vector<uint64_t> task_hits(ntask, 0);
+    std::vector<uint32_t> pool_stop(ng, UINT32_MAX);  // per pool: the batch row its list ran out at
+    auto to_rows = [&](const PoolOut& o, uint32_t task, std::vector<std::pair<uint32_t, int>>& ents) {
+        const uint32_t base = (uint32_t)ents.size();
+        ents.insert(ents.end(), o.ents.begin(), o.ents.end());
+        for (size_t k = 0; k + 1 < o.recs.size(); k++) {  // the last record is the sentinel
+            const PoolRec& r = o.recs[k];
+            rr[r.bi] = RowRec{base + r.off, r.len, task, r.matched, r.expired, 1, 0};
+        }
+    };
+    auto worker = [&](size_t t) {
+        const auto tw0 = clk::now();
+        auto& ents = task_ents_[t];
+        ents.clear();
+        static thread_local PoolOut o;
+        static thread_local DenseRun run;
+        // The worker thread's masks are all zero between pools.  Starting
+        // from zero is exact: this batch's rows and hit lists hold no ticket
+        // an earlier batch selected (assembly skips them; the device alive
+        // mask dropped them before this batch's searches).  Intervals stay
+        // unwritten during the walk (slots of all pools share its cache
+        // lines): a row's increment is pending in tl_proc until the merge.
+        static thread_local std::vector<uint8_t> tl_sel, tl_proc;
+        if (tl_sel.size() < sel.size()) tl_sel.resize(sel.size(), 0);
+        if (tl_proc.size() < sel.size()) tl_proc.resize(sel.size(), 0);
+        PassStats ls;
+        const std::unique_ptr<ReplayCore> rpp = make_replay(tl_sel, rev, maxI, ls);
+        ReplayCore& rp = *rpp;
+        std::vector<uint32_t> rows_of;
+        for (uint32_t k = task_off[t]; k < task_off[t + 1]; k++) {
+            const uint32_t gi = order_g[k];
+            PoolOut& po = few ? pool_outs_[gi] : o;
+            po.recs.clear();
+            po.ents.clear();
+            if (dense[gi] && pipe) {
+                const DensePool& D = dense_pools_[gi];
+                run.reset(D.n);
+                run.fast = fast_mode_;
+                run.recs.reserve((size_t)D.nrows + 1);
+                run.ents.reserve(ebound[gi]);
+                prog[gi].recs = run.recs.data();
+                prog[gi].ents = run.ents.data();
+                run.walk_published(D, rv, maxI, pos_of_.data(), &prog[gi].st);
+                if (run.ents.data() != prog[gi].ents || run.recs.data() != prog[gi].recs)
+                    std::abort();  // the bound above was wrong: readers hold the old buffers
+                task_hits[t] += run.hits_seen;
+                // the sentinel (its capacity was reserved), then the buffers to
+                // the pool's PoolOut (a header swap: the readers' pointers stay)
+                run.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)run.ents.size(), 0, run.g_run, run.x_run});
+                po.recs.swap(run.recs);
+                po.ents.swap(run.ents);
+                continue;
+            }
+            if (dense[gi]) {
+                run.reset(dense_pools_[gi].n);
+                run.fast = fast_mode_;
+                run.walk(dense_pools_[gi], rv, maxI, pos_of_.data(), 0, dense_pools_[gi].nrows);
+                task_hits[t] += run.hits_seen;
+                if (few) {
+                    run.finish(po);
+                    continue;
+                }
+                // the walk's records straight to the rows (entries offsets are run.ents')
+                const uint32_t base = (uint32_t)ents.size();
+                if (ents.empty()) ents.swap(run.ents);
+                else ents.insert(ents.end(), run.ents.begin(), run.ents.end());
+                for (const PoolRec& r : run.recs)
+                    rr[r.bi] = RowRec{base + r.off, r.len, (uint32_t)t, r.matched, r.expired, 1, 0};
+                continue;
+            } else {
+                rows_of.assign(P.pool_rows.begin() + P.pool_off[gi], P.pool_rows.begin() + P.pool_off[gi + 1]);
+                rp.hits_seen = 0;
+                if (view)
+                    pool_stop[gi] = replay_pool(rp, rows_of, brow.data(), *view, tl_sel, tl_proc.data(), minc_.data(),
+                                                maxc_.data(), po);
+                else
+                    pool_stop[gi] = replay_pool(rp, rows_of, brow.data(),
+                                                [&](uint32_t bi) -> BGroup& { return bg[brow_group[bi]]; },
+                                                tl_sel, tl_proc.data(), minc_.data(), maxc_.data(), po);
+                task_hits[t] += rp.hits_seen;
+            }
+            if (!few) to_rows(o, (uint32_t)t, ents);
+        }
+        task_ms[t] = msd(tw0, clk::now());
+    };
+    const auto tg1 = clk::now();
+    stats.par_gather_ms += msd(tg0, tg1);
+    if (pipe) {
+        const size_t ngt = gpipe ? ntask_g : 0;
+        wp.run(ntask + ngt + nch, [&](size_t t) {
+            if (t < ntask) worker(t);
+            else if (t < ntask + ngt) gather_piece(t - ntask);
+            else merge_chunk(t - ntask - ngt);
+        });
+        size_t G = 0, E = 0, X = 0;  // totals: the pools' sentinels
+        for (size_t gi = 0; gi < ng; gi++) {
+            const PoolRec& sr = pool_outs_[gi].recs.back();
+            G += sr.gcum;
+            E += sr.off;
+            X += sr.xcum;
+        }
+        out_groups.off.resize(g0 + 1 + G);
+        out_groups.ents.resize(e0 + E);
+        expired.resize(x0 + X);
+        newly.resize(n0 + E);
+        if (fill) filled_groups_ = g0 + G;
+    } else {
+        wp.run(ntask, worker);
+    }
+    const auto tg2 = clk::now();
+    stats.par_job_ms += msd(tg1, tg2);
+    if (id_broken.load()) throw std::runtime_error("pool replay: a row was not at its list position");
+    if (!gpipe) wp.run(ntask_g, [&](size_t t) {
+        for (uint32_t gi : dense_ids) {
+            const DensePool& D = dense_pools_[gi];
+            uint32_t lo, hi;
+            piece(D, t, lo, hi);
+            D.clear_pos(lo, hi, pos_of_.data());
+        }
+    });
+    const auto tp2 = clk::now();
+    stats.par_clear_ms += msd(tg2, tp2);
+    for (uint32_t v : pool_stop) *min_stop = std::min(*min_stop, v);
+    if (pipe) {
+    } else if (few) {
+        merge_pools(ng, nch, brow, sel, out_groups, expired, newly);
+    } else {
+        merge_rows(nb, nch, brow, sel, out_groups, expired, newly);
+    }
+    const auto tp3 = clk::now();
+    stats.par_work_ms += msd(tp1, tp2);
+    stats.par_merge_ms += msd(tp2, tp3);
+    for (size_t k = 0; k < ntask; k++) {
+        stats.par_task_max_ms = std::max(stats.par_task_max_ms, task_ms[k]);
+        stats.par_hits += task_hits[k];
+    }
+    stats.par_rows += nb;
+    return true;
+}
+
+// Merge of per-row records (many pools) back into the pinned row order.
+void Core::merge_rows(size_t nb, size_t nch, const UVec<uint32_t>& brow, std::vector<uint8_t>& sel,
+                      GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly) {
+    WorkPool& wp = workers();
+    const RowRec* rr = row_recs_.data();
+    struct Cnt { size_t g = 0, e = 0, x = 0; };
+    // Back into the pinned row order: per chunk of the batch, its groups /
+    // entries / expired counts, then every chunk fills its share at its
+    // offsets and applies its rows' pending Intervals increments.
+    std::vector<Cnt> at(nch + 1);
+    wp.run(nch, [&](size_t c) {
+        Cnt k;
+        for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++) {
+            const RowRec& r = rr[bi];
+            if (!r.processed) continue;
+            k.x += r.expired;
+            if (r.matched) k.g++, k.e += r.len;
+        }
+        at[c + 1] = k;
+    });
+    for (size_t c = 0; c < nch; c++) at[c + 1] = {at[c].g + at[c + 1].g, at[c].e + at[c + 1].e, at[c].x + at[c + 1].x};
+    const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
+    grow_to(out_groups.off, g0 + 1 + at[nch].g);
+    grow_to(out_groups.ents, e0 + at[nch].e);
+    grow_to(expired, x0 + at[nch].x);
+    grow_to(newly, n0 + at[nch].e);
+    wp.run(nch, [&](size_t c) {
+        size_t gk = g0 + at[c].g, ek = e0 + at[c].e, xk = x0 + at[c].x;
+        for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++) {
+            const RowRec& r = rr[bi];
+            if (!r.processed) continue;
+            const uint32_t T = brow[bi];
+            intervals_[T]++;  // the row's pending Intervals increment
+            dec_[T] = 1;      // decided: a later batch of the pass skips it
+            if (r.expired) expired[xk++] = T;
+            if (!r.matched) continue;
+            const auto* src = task_ents_[r.task].data() + r.ent;
+            for (uint32_t k = 0; k < r.len; k++) {
+                out_groups.ents[ek + k] = src[k];
+                newly[n0 + (ek - e0) + k] = src[k].first;
+                sel[src[k].first] = 1;
+            }
+            ek += r.len;
+            out_groups.off[++gk] = (uint32_t)ek;
+        }
+    });
+}
+
+// Merge of few pools' record arrays back into the pinned row order.  The
+// batch's row range is cut into chunks; each pool's records (ascending in
+// batch row, with running group / entry / expiry counts) are located in every
+// chunk by binary search, so each chunk knows its output offsets up front and
+// merges its share of the pools' records independently (through a
+// chunk-local row map).  Applies the rows' pending Intervals increments on
+// the way.
+void Core::merge_pools(size_t ng, size_t nch, const UVec<uint32_t>& brow, std::vector<uint8_t>& sel,
+                       GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly) {
+    using Rec = PoolRec;
+    auto& outs = pool_outs_;
+    WorkPool& wp = workers();
+    const size_t nb = brow.size();
+    std::vector<uint32_t> cut((nch + 1) * ng);  // [c][pool]: first record with bi >= chunk start
+    for (size_t c = 0; c <= nch; c++) {
+        const uint32_t lo = (uint32_t)(nb * c / nch);
+        for (size_t gi = 0; gi < ng; gi++) {
+            const auto& r = outs[gi].recs;  // sentinel at the end (bi = UINT32_MAX)
+            cut[c * ng + gi] = c == nch ? (uint32_t)(r.size() - 1)
+                                        : (uint32_t)(std::lower_bound(r.begin(), r.end(), lo,
+                                                                      [](const Rec& x, uint32_t v) { return x.bi < v; }) -
+                                                     r.begin());
+        }
+    }
+    struct Cnt { size_t g = 0, e = 0, x = 0; };
+    std::vector<Cnt> at(nch + 1);
+    for (size_t c = 0; c < nch; c++) {
+        Cnt k;
+        for (size_t gi = 0; gi < ng; gi++) {
+            const Rec& a0 = outs[gi].recs[cut[c * ng + gi]];
+            const Rec& a1 = outs[gi].recs[cut[(c + 1) * ng + gi]];
+            k.g += a1.gcum - a0.gcum;
+            k.e += a1.off - a0.off;
+            k.x += a1.xcum - a0.xcum;
+        }
+        at[c + 1] = {at[c].g + k.g, at[c].e + k.e, at[c].x + k.x};
+    }
+    const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
+    grow_to(out_groups.off, g0 + 1 + at[nch].g);
+    grow_to(out_groups.ents, e0 + at[nch].e);
+    grow_to(expired, x0 + at[nch].x);
+    grow_to(newly, n0 + at[nch].e);
+    wp.run(nch, [&](size_t c) {
+        // the chunk's records placed by batch row (a chunk-local map written by
+        // this worker alone), then swept in row order: linear in the chunk for
+        // any number of pools
+        const uint32_t lo = (uint32_t)(nb * c / nch), hi = (uint32_t)(nb * (c + 1) / nch);
+        static thread_local std::vector<uint64_t> at_row;  // (pool << 32 | record) + 1; 0: no record
+        at_row.assign(hi - lo, 0);
+        for (size_t gi = 0; gi < ng; gi++) {
+            const auto& recs = outs[gi].recs;
+            for (uint32_t k = cut[c * ng + gi]; k < cut[(c + 1) * ng + gi]; k++)
+                at_row[recs[k].bi - lo] = (((uint64_t)gi << 32) | k) + 1;
+        }
+        size_t gk = g0 + at[c].g, ek = e0 + at[c].e, xk = x0 + at[c].x;
+        for (uint32_t i = 0; i < hi - lo; i++) {
+            if (!at_row[i]) continue;
+            const uint64_t v = at_row[i] - 1;
+            const PoolOut& o = outs[v >> 32];
+            const Rec& r = o.recs[(uint32_t)v];
+            const uint32_t T = brow[r.bi];
+            intervals_[T]++;  // the row's pending Intervals increment
+            dec_[T] = 1;      // decided: a later batch of the pass skips it
+            if (r.expired) expired[xk++] = T;
+            if (!r.matched) continue;
+            for (uint32_t k = 0; k < r.len; k++) {
+                const auto& e = o.ents[r.off + k];
+                out_groups.ents[ek + k] = e;
+                newly[n0 + (ek - e0) + k] = e.first;
+                sel[e.first] = 1;
+            }
+            ek += r.len;
+            out_groups.off[++gk] = (uint32_t)ek;
+        }
+    });
+}
+
+// Row bi of a packed batch as the replay's search view (its fixed-stride
+// list, reverse bits and pair words in the pinned output buffer).
+static inline void fill_packed(BGroup& g, const uint8_t* base, const PackLayout& L, uint32_t bi, uint32_t T,
+                               uint32_t sig) {
+    const uint32_t n = base[L.cnt + bi];
+    const uint32_t P = L.S < 32 ? (uint32_t)L.S : 32u;
+    g.sig = sig;
+    g.row_slot = T;
+    g.d.rev_slot = T;
+    g.nrows = 1;
+    g.set_slots(reinterpret_cast<const uint32_t*>(base + L.slot) + (size_t)bi * L.S);
+    g.last_i = UINT32_MAX;
+    g.rev = nullptr;
+    g.rev_packed = true;
+    const uint8_t* rv = base + L.rev;
+    g.rev_bits = L.rev_w == 1 ? rv[bi]
+               : L.rev_w == 2 ? reinterpret_cast<const uint16_t*>(rv)[bi]
+               : L.rev_w == 4 ? reinterpret_cast<const uint32_t*>(rv)[bi]
+                              : reinterpret_cast<const uint64_t*>(rv)[bi];
+    g.pm = base + L.pm + (size_t)bi * P * L.pm_w;
+    g.pm_w = (uint8_t)L.pm_w;
+    g.pm_n = std::min(n, P);
+    g.n = n;
+    g.complete = true;
+    g.head = 0;
+}
+
+// Packed RevPrecision batch assembly: the pass rows [pos, end) not yet
+// selected or decided, each its ticket's slot and source (source_of's choice:
+// the posting list of its most selective required term), straight into the
+// pinned upload buffer.  False (nothing changed) when some row's source holds
+// more than 64 entries: the per-search path then takes the batch.
+bool Core::assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t cap, UVec<uint32_t>& brow,
+                           PackBatch& pb) {
+    const size_t nr = std::min({rows.size() - pos, kMaxBatchRows, cap});
+    WorkPool& wp = workers();
+    const bool par = par_mode_ && nr >= par_min(65536);
+    const size_t nch = par ? (size_t)wp.size() * 4 : 1;
+    grow_to(pk_tmp_, nr);
+    std::vector<size_t> at(nch + 1, 0);
+    std::vector<uint32_t> maxlen(nch, 0);
+    std::vector<uint8_t> bad(nch, 0);
+    std::vector<uint64_t> scanned(nch, 0);
+    std::vector<double> live_w(nch, 0.0);
+    auto pass1 = [&](size_t c) {
+        size_t k = 0;
+        uint32_t mx = 0;
+        uint64_t sc = 0;
+        double lw = 0.0;
+        for (size_t i = nr * c / nch; i < nr * (c + 1) / nch; i++) {
+            const uint32_t r = rows[pos + i];
+            DSmallRow& o = pk_tmp_[i];
+            if (sel_[r] | dec_[r]) {
+                o.slot = kNoSlot;
+                continue;
+            }
+            const Sig& sg = sigs_[sig_[r]];
+            DGroup d;
+            source_of(sg, d);
+            if (d.src_len > 64) {
+                bad[c] = 1;
+                return;
+            }
+            o = DSmallRow{r, d.src_off, d.src_len | (d.src_kind == 0 ? kSrcOrder : 0u)};
+            k++;
+            mx = std::max(mx, d.src_len);
+            sc += d.src_len;
+            // per live candidate (search_bytes' rev form): Min/MaxCount, the
+            // query's field columns, the hit's query descriptor and clauses
+            lw += (double)d.src_len * (double)(8 + 9 * sg.n_fields + 8 + 32 * sg.n_clauses);
+        }
+        at[c + 1] = k;
+        maxlen[c] = mx;
+        scanned[c] = sc;
+        live_w[c] = lw;
+    };
+    if (nch > 1) wp.run(nch, pass1);
+    else pass1(0);
+    for (uint8_t b : bad)
+        if (b) return false;
+    for (size_t c = 0; c < nch; c++) at[c + 1] += at[c];
+    const size_t n = at[nch];
+    h_srows_.reserve(std::max<size_t>(n, 1));
+    grow_to(brow, n);
+    auto pass2 = [&](size_t c) {
+        size_t o = at[c];
+        for (size_t i = nr * c / nch; i < nr * (c + 1) / nch; i++) {
+            const DSmallRow& d = pk_tmp_[i];
+            if (d.slot == kNoSlot) continue;
+            h_srows_.p[o] = d;
+            brow[o] = d.slot;
+            o++;
+        }
+    };
+    if (nch > 1) wp.run(nch, pass2);
+    else pass2(0);
+    pb = PackBatch{};
+    pb.n = n;
+    pb.end = pos + nr;
+    uint32_t mx = 0;
+    for (size_t c = 0; c < nch; c++) {
+        mx = std::max(mx, maxlen[c]);
+        pb.scanned += scanned[c];
+        pb.live_w += live_w[c];
+    }
+    while ((uint32_t)pb.S < mx) pb.S *= 2;
+    return true;
+}
+
+// One packed batch on the device: rows up, rpack_kernel, the whole output
+// down in one copy (the host `overlap` work runs meanwhile).
+PackLayout Core::run_packed(const PackBatch& pb, PassStats& stats, const std::function<void()>& overlap) {
+    flush_apply();  // the previous batch's selections, before this batch's searches
+    const PackLayout L = pack_layout(pb.n, pb.S);
+    const DStore st = dstore();
+    d_srows_.reserve(std::max<size_t>(pb.n, 1), false);
+    d_pack_.reserve(L.total, false);
+    h_pack_.reserve(L.total);
+    if (pb.n) {
+        NKM_HIP(hipMemcpyAsync(d_srows_.p, h_srows_.p, pb.n * sizeof(DSmallRow), hipMemcpyHostToDevice, stream_));
+        NKM_HIP(launch_rpack(st, d_srows_.p, (uint32_t)pb.n, d_pack_.p, L, stream_, ev_[7], ev_[8]));
+        NKM_HIP(hipMemcpyAsync(h_pack_.p, d_pack_.p, L.total, hipMemcpyDeviceToHost, stream_));
+    }
+    if (overlap) overlap();
+    NKM_HIP(hipStreamSynchronize(stream_));
+    stats.batches++;
+    if (!pb.n) return L;
+    float ms = 0.f;
+    NKM_HIP(hipEventElapsedTime(&ms, ev_[7], ev_[8]));
+    stats.k_ms[3] += ms;
+    stats.k_launches[3]++;
+    stats.rpack = true;
+    uint64_t live = 0, ents = 0;
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(h_pack_.p + L.live);
+    for (uint32_t b = 0; b < L.blocks; b++) {
+        live += lw[2 * b];
+        ents += lw[2 * b + 1];
+    }
+    // algorithmic bytes: per row its descriptor and its query / count range;
+    // per scanned candidate slot id + alive; per live candidate the columns
+    // (average of the rows' per-live bytes, weighted by source length); per
+    // entry its slot id; per row its pair words, reverse bits and count
+    const double per_live = pb.scanned ? pb.live_w / (double)pb.scanned : 0.0;
+    const int P = pb.S < 32 ? pb.S : 32;
+    stats.k_bytes[3] += (int64_t)pb.n * (int64_t)(sizeof(DSmallRow) + 16) + (int64_t)pb.scanned * 5 +
+                        (int64_t)((double)live * per_live) + (int64_t)ents * 4 +
+                        (int64_t)pb.n * (int64_t)(P * L.pm_w + L.rev_w + 1);
+    stats.pair_evals += (int64_t)pb.scanned;
+    return L;
+}
+
+// plan_pools over a packed batch: search i is batch row i (its ticket's
+// signature), and every search is one row.
+bool Core::plan_packed(size_t n, const UVec<uint32_t>& brow, ParPlan& P, PassStats& stats) {
+    return plan_pools(
+        n, [&](size_t i) { return sig_[brow[i]]; }, [](size_t bi) { return (uint32_t)bi; },
+        [&](size_t i) { return brow[i]; }, brow, P, stats);
+}
+
+// The replay's search view of a packed batch's row bi (a thread-local
+// BGroup refilled per row from the output buffer).
+std::function<BGroup&(uint32_t)> Core::packed_view(const PackLayout& L, const UVec<uint32_t>& brow) {
+    const uint8_t* base = h_pack_.p;
+    return [this, base, L, &brow](uint32_t bi) -> BGroup& {
+        static thread_local BGroup g;
+        const uint32_t T = brow[bi];
+        fill_packed(g, base, L, bi, T, sig_[T]);
+        return g;
+    };
+}
+
+
+}  // namespace nkm
