@@ -770,6 +770,7 @@ public:
     // ---- signatures / clauses ----
     std::unordered_map<std::string, uint32_t> sig_index_;
     std::vector<Sig> sigs_;
+    std::vector<uint64_t> sig_fmask_;  // per signature: its must_fmask (plan_pools reads 8 B, not the Sig)
     std::vector<DClause> clauses_;
     std::vector<DQuery> squery_;      // per slot
     std::vector<uint8_t> field_used_; // per field: referenced by some clause

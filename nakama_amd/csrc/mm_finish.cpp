@@ -114,6 +114,7 @@ bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& gro
     if (!arena_claimed_ && out_in_use_.exchange(true)) return false;  // a second outstanding result: fill_matched copies
     arena_claimed_ = true;
     const bool filled = filled_groups_ == ng;  // the pipelined merge wrote the result entries
+    const auto f0 = std::chrono::steady_clock::now();
     WorkPool& wp = workers();
     const size_t nch = (size_t)wp.size() * 2;
     std::vector<uint8_t> bad(nch, 0);
@@ -139,6 +140,11 @@ bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& gro
     int64_t* gc = out_created_.data();
     std::vector<uint32_t> killed(nch, 0);
     std::vector<std::vector<std::string>> gone(track_removed_ ? nch : 0);
+    // Without a mutation, the matched tickets are exactly the pass's selection
+    // (sel_): retired by one sequential sweep over the slots instead of
+    // scattered writes per result entry
+    const size_t N = nslots();
+    const bool by_slot = !mutated && !track_removed_ && sel_.size() == N;
     wp.run(nch, [&](size_t c) {
         const size_t g0 = ng * c / nch, g1 = ng * (c + 1) / nch;
         uint32_t k = 0;
@@ -150,27 +156,44 @@ bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& gro
                 gc[g] = groups.len(g) ? created_[groups.end(g)[-1].first] : 0;
             }
             if (c + 1 == nch) offs[ng] = (int32_t)groups.off[ng];
-        }
-        for (size_t i = groups.off[g0]; i < groups.off[g1]; i++) {
-            const uint32_t s = groups.ents[i].first;
-            if (!filled) {
+            for (size_t i = groups.off[g0]; i < groups.off[g1]; i++) {
+                const uint32_t s = groups.ents[i].first;
                 ents[i].ticket = tk_ptr_[s];
                 ents[i].presence_index = groups.ents[i].second;
                 ents[i].reserved = 0;
             }
-            if (!live_[s]) continue;  // a ticket's presence entries repeat its slot
-            if (track_removed_) gone[c].emplace_back(tk(s));
-            live_[s] = 0;  // retired: sessionTickets / partyTickets read live_ (SlotSets)
-            is_active_[s] = 0;
-            k++;
+        }
+        if (by_slot) {
+            for (size_t s = N * c / nch; s < N * (c + 1) / nch; s++)
+                if (sel_[s] & live_[s]) {
+                    live_[s] = 0;  // retired: sessionTickets / partyTickets read live_ (SlotSets)
+                    is_active_[s] = 0;
+                    k++;
+                }
+        } else {
+            for (size_t i = groups.off[g0]; i < groups.off[g1]; i++) {
+                const uint32_t s = groups.ents[i].first;
+                if (!live_[s]) continue;  // a ticket's presence entries repeat its slot
+                if (track_removed_) gone[c].emplace_back(tk(s));
+                live_[s] = 0;
+                is_active_[s] = 0;
+                k++;
+            }
         }
         killed[c] = k;
     });
+    const auto f1 = std::chrono::steady_clock::now();
     for (uint32_t k : killed) n_live_ -= k;
     for (auto& v : gone) removed_ids_.insert(removed_ids_.end(), v.begin(), v.end());
     filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, list_tmp_,
                  [&](uint32_t s) { return live_[s] && is_active_[s]; });
     active_list_.swap(list_tmp_);
+    if (const char* p = std::getenv("NKM_PROFILE"); p && std::atoi(p) >= 2) {
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "[nkm]   finish: retire %.3f ms (%s, %s) | filter %.3f ms (%zu active)\n", ms(f0, f1),
+                     by_slot ? "by slot" : "by entry", filled ? "filled" : "fill", ms(f1, std::chrono::steady_clock::now()),
+                     active_list_.size());
+    }
     out->group_created = gc;
     out->n_groups = (int32_t)ng;
     out->n_entries = (int32_t)ne;

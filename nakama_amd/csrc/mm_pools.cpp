@@ -77,7 +77,7 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
     sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
         if (narrow) {
             uint64_t m = cmask;
-            for (size_t i = lo; i < hi && m; i++) m &= sigs_[sig_of(i)].must_fmask;
+            for (size_t i = lo; i < hi && m; i++) m &= sig_fmask_[sig_of(i)];
             hmask[ch] = m;
             return;
         }
@@ -192,11 +192,81 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
     if (ng < 2) return false;
     P.ng = ng;
     auto pool_key = [&](size_t p, size_t f) { return keyf.size() == 1 ? pool_key1[p] : pool_keys[p][f]; };
-    // every searching ticket must itself belong to its search's pool; the
-    // rows are bucketed per pool in batch order (CSR: per-chunk counts, then
-    // every chunk scatters at its offsets; counters stay thread-private)
+    // every searching ticket must itself belong to its search's pool: a row
+    // not known to carry its own search's terms (self_match_) must hold the
+    // pool's key values, and its pool is then not known to hold all its rows
     const size_t nb = brow.size();
     const unsigned nchunk = nb >= par_min(65536) ? wp.size() : 1;
+    auto row_check = [&](size_t bi, uint32_t p) -> int {  // 0 self, 1 foreign, 2 not in its pool
+        const uint32_t r = brow[bi];
+        const uint32_t gi = group_of(bi);
+        if (self_match_[r] && indexed_[r] && sig_[r] == sig_of(gi)) return 0;
+        for (size_t f = 0; f < keyf.size(); f++)
+            if (fkind_[keyf[f]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[f]][r] != pool_key(p, f)) return 2;
+        return 1;
+    };
+    // Contiguous pools (C5: a bucket's tickets arrive together): when the row
+    // pool ids never decrease and step by at most one (pools are numbered in
+    // first appearance), every pool's rows are one run of the batch and the
+    // batch is its own CSR — no counting sort.
+    {
+        const auto tq0 = clk::now();
+        std::vector<uint8_t> ok(nchunk, 1), bad(nchunk, 0);
+        std::vector<uint32_t> pfirst(nchunk, 0), plast(nchunk, 0);
+        grow_to(P.self_rows, ng);
+        sweep(ng, ng >= 65536 ? nchunk : 1, [&](size_t, size_t lo, size_t hi) {
+            std::memset(P.self_rows.data() + lo, 1, hi - lo);
+        });
+        sweep(nb, nchunk, [&](size_t c, size_t lo, size_t hi) {
+            if (lo >= hi) return;
+            uint32_t prev = search_pool[group_of(lo)];
+            pfirst[c] = prev;
+            for (size_t bi = lo; bi < hi; bi++) {
+                const uint32_t p = search_pool[group_of(bi)];
+                if (p != prev && p != prev + 1) { ok[c] = 0; return; }
+                prev = p;
+                const int k = row_check(bi, p);
+                if (k == 2) { bad[c] = 1; return; }
+                if (k == 1) P.self_rows[p] = 0;  // benign: every writer stores 0
+            }
+            plast[c] = prev;
+        });
+        bool mono = nb > 0;
+        for (unsigned c = 0; c < nchunk && mono; c++) {
+            if (bad[c]) return false;
+            mono = ok[c] != 0;
+        }
+        bool seen = false;
+        uint32_t last = 0;
+        for (unsigned c = 0; c < nchunk && mono; c++) {
+            if (nb * c / nchunk >= nb * (c + 1) / nchunk) continue;  // an empty chunk
+            if (seen) mono = pfirst[c] == last || pfirst[c] == last + 1;
+            seen = true;
+            last = plast[c];
+        }
+        mono = mono && search_pool[group_of(0)] == 0 && search_pool[group_of(nb - 1)] + 1 == ng;
+        if (mono) {
+            grow_to(P.pool_off, ng + 1);
+            grow_to(P.pool_rows, nb);
+            sweep(nb, nchunk, [&](size_t, size_t lo, size_t hi) {
+                for (size_t bi = lo; bi < hi; bi++) {
+                    P.pool_rows[bi] = (uint32_t)bi;
+                    const uint32_t p = search_pool[group_of(bi)];
+                    if (bi == 0 || search_pool[group_of(bi - 1)] != p) P.pool_off[p] = (uint32_t)bi;
+                }
+            });
+            P.pool_off[ng] = (uint32_t)nb;
+            stats.par_bucket_ms += msd(tp0, clk::now());
+            if (batch_profile_)
+                std::fprintf(stderr, "[nkm]   plan_pools: %zu pools (contiguous runs) | keys %.2f runs %.2f ms\n", ng,
+                             msd(tp0, tq0), msd(tq0, clk::now()));
+            P.ok = true;
+            return true;
+        }
+    }
+    // otherwise the rows are bucketed per pool in batch order (CSR: per-chunk
+    // counts, then every chunk scatters at its offsets; counters stay
+    // thread-private)
     UVec<uint32_t>& cnt = pool_cnt_;  // [chunk][pool]: each chunk writes its row in full
     grow_to(cnt, (size_t)nchunk * ng);
     std::vector<uint8_t> cbad(nchunk, 0);
@@ -213,18 +283,14 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
         k.assign(ng, 0);
         fo.assign(ng, 0);
         for (size_t bi = lo; bi < hi; bi++) {
-            const uint32_t r = brow[bi];
-            const uint32_t gi = group_of(bi);
-            const uint32_t p = search_pool[gi];
+            const uint32_t p = search_pool[group_of(bi)];
             k[p]++;
-            // the row carries every term of its own search: the pool's keys among them
-            if (self_match_[r] && indexed_[r] && sig_[r] == sig_of(gi)) continue;
-            fo[p] = 1;
-            for (size_t f = 0; f < keyf.size(); f++)
-                if (fkind_[keyf[f]][r] != KIND_KEYWORD || (uint32_t)fval_[keyf[f]][r] != pool_key(p, f)) {
-                    cbad[c] = 1;
-                    return;
-                }
+            const int rc = row_check(bi, p);
+            if (rc == 2) {
+                cbad[c] = 1;
+                return;
+            }
+            if (rc == 1) fo[p] = 1;
         }
         std::memcpy(cnt.data() + c * ng, k.data(), ng * sizeof(uint32_t));
         std::memcpy(cforeign.data() + c * ng, fo.data(), ng);
@@ -595,6 +661,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         const std::unique_ptr<ReplayCore> rpp = make_replay(tl_sel, rev, maxI, ls);
         ReplayCore& rp = *rpp;
         std::vector<uint32_t> rows_of;
+        uint64_t hits = 0;  // task_hits[t] at the end: neighbouring tasks' counters share a line
         for (uint32_t k = task_off[t]; k < task_off[t + 1]; k++) {
             const uint32_t gi = order_g[k];
             PoolOut& po = few ? pool_outs_[gi] : o;
@@ -611,7 +678,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                 run.walk_published(D, rv, maxI, pos_of_.data(), &prog[gi].st);
                 if (run.ents.data() != prog[gi].ents || run.recs.data() != prog[gi].recs)
                     std::abort();  // the bound above was wrong: readers hold the old buffers
-                task_hits[t] += run.hits_seen;
+                hits += run.hits_seen;
                 // the sentinel (its capacity was reserved), then the buffers to
                 // the pool's PoolOut (a header swap: the readers' pointers stay)
                 run.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)run.ents.size(), 0, run.g_run, run.x_run});
@@ -623,7 +690,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                 run.reset(dense_pools_[gi].n);
                 run.fast = fast_mode_;
                 run.walk(dense_pools_[gi], rv, maxI, pos_of_.data(), 0, dense_pools_[gi].nrows);
-                task_hits[t] += run.hits_seen;
+                hits += run.hits_seen;
                 if (few) {
                     run.finish(po);
                     continue;
@@ -638,17 +705,18 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             } else {
                 rows_of.assign(P.pool_rows.begin() + P.pool_off[gi], P.pool_rows.begin() + P.pool_off[gi + 1]);
                 rp.hits_seen = 0;
-                if (view)
-                    pool_stop[gi] = replay_pool(rp, rows_of, brow.data(), *view, tl_sel, tl_proc.data(), minc_.data(),
-                                                maxc_.data(), po);
-                else
-                    pool_stop[gi] = replay_pool(rp, rows_of, brow.data(),
-                                                [&](uint32_t bi) -> BGroup& { return bg[brow_group[bi]]; },
-                                                tl_sel, tl_proc.data(), minc_.data(), maxc_.data(), po);
-                task_hits[t] += rp.hits_seen;
+                const uint32_t stop =
+                    view ? replay_pool(rp, rows_of, brow.data(), *view, tl_sel, tl_proc.data(), minc_.data(), maxc_.data(),
+                                       po)
+                         : replay_pool(rp, rows_of, brow.data(),
+                                       [&](uint32_t bi) -> BGroup& { return bg[brow_group[bi]]; }, tl_sel,
+                                       tl_proc.data(), minc_.data(), maxc_.data(), po);
+                if (stop != UINT32_MAX) pool_stop[gi] = stop;
+                hits += rp.hits_seen;
             }
             if (!few) to_rows(o, (uint32_t)t, ents);
         }
+        task_hits[t] = hits;
         task_ms[t] = msd(tw0, clk::now());
     };
     const auto tg1 = clk::now();

@@ -477,6 +477,7 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
     }
     for (auto& d : dc) clauses_.push_back(d);
     uint32_t id = (uint32_t)sigs_.size();
+    sig_fmask_.push_back(s.must_fmask);
     sigs_.push_back(std::move(s));
     sig_index_.emplace(std::move(key), id);
     // fields referenced for the first time get a dense host column now
@@ -1224,6 +1225,8 @@ void Core::compact() {
                                  ns[g].n_clauses),
                          g);
         sigs_.swap(ns);
+        sig_fmask_.resize(sigs_.size());
+        for (size_t g = 0; g < sigs_.size(); g++) sig_fmask_[g] = sigs_[g].must_fmask;
         clauses_.swap(nc);
         sig_index_.swap(nidx);
         dev_clauses_ = 0;
