@@ -547,10 +547,13 @@ uint32_t replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uin
 // (tools/replay_bench.cpp checks it; tests/test_gpu_parity.py checks the
 // parallel paths against the serial one).
 //
-// (A pool's walk is not cut into speculative segments: tried, with an exact
-// state-difference repair, but on C3 pools the speculative and true runs stay
-// one group boundary apart indefinitely — the greedy packing locks onto its
-// phase — so the repair degenerated to the serial walk.)
+// (A pool's walk is not cut into speculative segments.  A walk is "empty"
+// at row j — nothing before j unselected, nothing after it selected — only
+// where the position prefix holds a multiple of the gcd of the allowed group
+// sizes (10 on C3), so a segment must start at such a row to ever meet the
+// exact walk; cut there, every C3 segment joined within a few rows, but the
+// segment walks compete with the gathers for the process's 16 CPUs and the
+// pass got slower: DESIGN.md §9, profiles/r03t_spec_ab.txt.)
 
 struct DenseRec {
     int32_t count, minc, maxc, cm;
