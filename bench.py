@@ -57,7 +57,8 @@ WORKLOADS = {
 # the query fields a pool is keyed on (the cluster front's routing)
 POOL_FIELDS = {1: ("properties.mode", "properties.region"), 3: ("properties.mode", "properties.region"),
                4: ("properties.mode", "properties.region"), 5: ("properties.bucket",), 11: ("properties.bucket",)}
-DEFAULT_TICKETS = {4: 4_000_000}  # C4 is quoted on 4M in total; the others on 1M (per GPU for C3)
+# BASELINE.json configs: C1 10k, C2 100k, C4 4M in total; the others 1M (per GPU for C3)
+DEFAULT_TICKETS = {1: 10_000, 2: 100_000, 4: 4_000_000}
 STRONG = (4, 5, 11)               # configs whose ticket count is the whole job's
 REV = (5, 11)                     # RevPrecision configs
 # full oracle passes measured offline (tools/make_full_golden.py: every pool's
@@ -79,7 +80,7 @@ def parse():
     ap.add_argument("--override", action="store_true",
                     help="register a MatchmakerOverride (processCustom path): the timed step is the candidate pass, "
                          "a native first-disjoint override and mm_process_commit (per rank under the cluster front)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03l_traffic.json"))
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03z_traffic.json"))
     a = ap.parse_args()
     if a.tickets is None:
         a.tickets = DEFAULT_TICKETS.get(a.config, 1_000_000)
