@@ -883,7 +883,7 @@ public:
     // NKM_DENSE=0: single-search pools take the generic walk too (A/B, tests)
     bool dense_mode_ = true;
     bool pipe_mode_ = true;  // NKM_PIPE=0: the pool walks' merge runs after all walks, not beside them
-    bool gpipe_mode_ = true; // NKM_GPIPE=0: identity pools gather their copies before the walks, not beside them
+    bool gpipe_mode_ = true; // NKM_GPIPE=0: no identity-pool shortcut (slot -> position map, copies gathered before the walks)
     int32_t max_pres_ = 1;   // most presences of any ticket inserted (an entry bound of the pipelined merge)
     // NKM_FAST=0: every row takes the exact loop body, also when no two live
     // tickets share a session (the fast walk, replay_core.h) (A/B, tests)

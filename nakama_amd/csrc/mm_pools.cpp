@@ -457,16 +457,19 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     // idle while the merge waits for the slowest walk.
     const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
     const bool pipe = few && pipe_mode_ && !dense_ids.empty() && dense_ids.size() == ng && nch > 1;
-    // Pipelined gather: when every pool's rows are its list in list order
-    // (identity pools — C3 / C4: every member of a pool of fresh tickets
-    // searches, and batch order is scan order) no slot -> position map is
-    // built, and the gathers run in the walks' job: tasks after the walks
-    // gather piece t of every pool and publish each pool's gathered prefix;
-    // a walk reads a position once it is covered (DenseRun::need).  Needs a
-    // worker beyond the walks (tasks are claimed in index order).
+    // Identity pools: when every pool's rows are its list in list order
+    // (C3 / C4: every member of a pool of fresh tickets searches, and batch
+    // order is scan order) row j's ticket is list position j — no slot ->
+    // position map is built or read (a walk's map lookup is a cache miss per
+    // row when the pools interleave in the store: C4's 64).  Pipelined
+    // gather on top, when a worker is left beyond the walks: the gathers run
+    // in the walks' job, tasks after the walks gather piece t of every pool
+    // and publish each pool's gathered prefix, and a walk reads a position
+    // once it is covered (DenseRun::need); otherwise the copies are gathered
+    // before the walks.
     const auto tg0 = clk::now();
-    bool gpipe = false;
-    if (pipe && gpipe_mode_ && wp.size() > ntask) {
+    bool ident = false;
+    if (few && gpipe_mode_ && !dense_ids.empty() && dense_ids.size() == ng) {
         bool all = true;
         for (uint32_t gi : dense_ids) all = all && dense_pools_[gi].nrows == dense_pools_[gi].n;
         // Slots in time order (monotone_): scan order = batch order, so the
@@ -481,7 +484,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             known = P.self_rows[gi] && sg.qkind == QK_BOOL && sg.must_terms.size() == sg.n_clauses;
         }
         if (known) {
-            gpipe = true;
+            ident = true;
         } else if (all) {
             std::vector<uint8_t> ok(ntask_g, 1);
             wp.run(ntask_g, [&](size_t t) {
@@ -492,21 +495,25 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                     if (!D.rows_are_list(lo, hi)) { ok[t] = 0; return; }
                 }
             });
-            gpipe = std::all_of(ok.begin(), ok.end(), [](uint8_t x) { return x != 0; });
+            ident = std::all_of(ok.begin(), ok.end(), [](uint8_t x) { return x != 0; });
         }
     }
+    const bool gpipe = ident && pipe && wp.size() > ntask;
+    std::atomic<bool> id_broken{false};  // an identity pool whose row was not at its position (a bug: fail loudly)
+    if (ident)
+        for (uint32_t gi : dense_ids) {
+            dense_pools_[gi].identity = true;
+            dense_pools_[gi].broken = &id_broken;
+        }
     std::unique_ptr<std::atomic<uint32_t>[]> gfront(gpipe ? new std::atomic<uint32_t>[ng] : nullptr);
     std::unique_ptr<std::atomic<uint8_t>[]> gdone(gpipe ? new std::atomic<uint8_t>[ng * ntask_g] : nullptr);
-    std::atomic<bool> id_broken{false};  // an identity pool whose row was not at its position (a bug: fail loudly)
     if (gpipe) {
         for (size_t gi = 0; gi < ng; gi++) gfront[gi].store(0);
         for (size_t k = 0; k < ng * ntask_g; k++) gdone[k].store(0);
         for (uint32_t gi : dense_ids) {
             DensePool& D = dense_pools_[gi];
-            D.identity = true;
             D.pieces = (uint32_t)ntask_g;
             D.front = &gfront[gi];
-            D.broken = &id_broken;
         }
     }
     // piece t of every pool, then each pool's published prefix advanced over
@@ -631,7 +638,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             if (fill) out_offs_[gk] = (int32_t)ek;
         }
     };
-    std::vector<double> task_ms(ntask, 0.0);
+    std::vector<double> task_ms(ntask, 0.0), walk_prep_ms(ntask, 0.0), walk_ms(ntask, 0.0);  // NKM_PROFILE=2 split
     std::vector<uint64_t> task_hits(ntask, 0);
     std::vector<uint32_t> pool_stop(ng, UINT32_MAX);  // per pool: the batch row its list ran out at
     auto to_rows = [&](const PoolOut& o, uint32_t task, std::vector<std::pair<uint32_t, int>>& ents) {
@@ -669,13 +676,17 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             po.ents.clear();
             if (dense[gi] && pipe) {
                 const DensePool& D = dense_pools_[gi];
+                const auto tr0 = clk::now();
                 run.reset(D.n);
                 run.fast = fast_mode_;
                 run.recs.reserve((size_t)D.nrows + 1);
                 run.ents.reserve(ebound[gi]);
                 prog[gi].recs = run.recs.data();
                 prog[gi].ents = run.ents.data();
+                const auto tr1 = clk::now();
                 run.walk_published(D, rv, maxI, pos_of_.data(), &prog[gi].st);
+                walk_prep_ms[t] += msd(tr0, tr1);
+                walk_ms[t] += msd(tr1, clk::now());
                 if (run.ents.data() != prog[gi].ents || run.recs.data() != prog[gi].recs)
                     std::abort();  // the bound above was wrong: readers hold the old buffers
                 hits += run.hits_seen;
@@ -769,6 +780,17 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     for (size_t k = 0; k < ntask; k++) {
         stats.par_task_max_ms = std::max(stats.par_task_max_ms, task_ms[k]);
         stats.par_hits += task_hits[k];
+    }
+    if (batch_profile_ && pipe) {
+        double sp = 0, sw = 0, st = 0, mw = 0;
+        for (size_t k = 0; k < ntask; k++) {
+            sp += walk_prep_ms[k];
+            sw += walk_ms[k];
+            st += task_ms[k];
+            mw = std::max(mw, walk_ms[k]);
+        }
+        std::fprintf(stderr, "[nkm]   pool walks: %zu tasks, %zu pools on %u workers | sum: tasks %.2f, walks %.2f (max %.2f), "
+                     "reset+reserve %.2f ms | gather %s\n", ntask, ng, wp.size(), st, sw, mw, sp, gpipe ? "beside" : "before");
     }
     stats.par_rows += nb;
     return true;
