@@ -62,13 +62,13 @@ int32_t mm_merge_positions(const int64_t* keys, const int32_t* counts, int32_t w
  * groups) the positions are the stable order by (key, rank, index) and the
  * return value is 2 — every rank sees the same matrix, so every rank takes
  * the same branch. */
+int32_t mm_merge_positions_strided(const int64_t* keys, int64_t stride, const int32_t* counts, int32_t world,
+                                   int32_t rank, int64_t* pos_out);
 /* Matched tickets of a result (its entries with presence index 0: a
  * ticket's presence entries hold index 0 exactly once), counted on host
  * threads — the cluster front's per-pass summary without a Python pass over
  * the entries. */
 int64_t mm_count_tickets(const mm_matched* m);
-int32_t mm_merge_positions_strided(const int64_t* keys, int64_t stride, const int32_t* counts, int32_t world,
-                                   int32_t rank, int64_t* pos_out);
 
 /* ---- Row-sharded mode --------------------------------------------------
  * For queries that cross pools (or a pool larger than one GPU) the pool
@@ -78,7 +78,11 @@ int32_t mm_merge_positions_strided(const int64_t* keys, int64_t stride, const in
  * rank r evaluates block r only, and the blocks' results — per-search result
  * records, hit lists (16 B per hit), RevPrecision flags and pair matrices —
  * are exchanged in place, after which every rank replays the same lists into
- * the same groups (processDefault's single ordered replay, replicated).  The
+ * the same groups (processDefault's single ordered replay, replicated).  A
+ * batch's pool signatures on the hashed multi-signature scan (C4's 64 mode x
+ * region pools) are split by candidate instead: rank r scans one block of the
+ * scan order's chunks for every signature, the blocks' per-chunk hits and
+ * counts are exchanged the same way, and every rank places every list.  The
  * RevThreshold timer is read at batch boundaries and OR-ed over the ranks, so
  * the replicas never diverge.  Only mm_process's batch searches are split;
  * a row's extra pages (a truncated list) are searched by every rank alike. */
@@ -126,6 +130,8 @@ int mm_shard_rows_rccl(void* h, int32_t world, int32_t rank, const uint8_t* uid,
  *   row-sharded mode above): over RCCL between distinct devices
  *   (transport MM_MULTI_RCCL, ncclCommInitRank per sub-handle thread), or
  *   through host memory (MM_MULTI_HOST: sub-handles may share a device).
+ *   A mutator called during a pass waits for the pass to end (the replicas
+ *   must see it at the same point); Process itself never waits for one.
  *
  * api: the entry points of the library the sub-handles come from; NULL =
  * this library (HIP sub-handles, cfg->device replaced by devices[i]).  The

@@ -415,20 +415,37 @@ class ClusterMatchmaker:
         succeeds when the rank holding its ticket succeeds.  Returns this
         rank's error (None: success or no request)."""
         reqs = self._gather(req)
-        ok = np.zeros(self.world, dtype=np.int32)
+        # per request r: st[r] = 1 when the rank holding it removed it,
+        # st[world + r] = 1 when some rank failed on it otherwise.  Every rank
+        # takes part in the all_reduce whatever happened locally (an
+        # exception here would leave the others hanging in the collective); a
+        # local failure is re-raised after it.
+        st = np.zeros(2 * self.world, dtype=np.int32)
+        local_exc = None
         for r, q in enumerate(reqs):
             if q is None:
                 continue
             try:
                 fn(self.local, *q)
-                ok[r] = 1
+                st[r] = 1
             except capi.ErrMatchmakerTicketNotFound:
                 pass
-        t = self._t(ok)
+            except Exception as e:  # noqa: BLE001 - re-raised below, after the collective
+                st[self.world + r] = 1
+                if local_exc is None:
+                    local_exc = e
+        t = self._t(st)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        if req is not None and not int(self._host(t)[self.rank]):
-            return capi.ErrMatchmakerTicketNotFound(req[-1])
-        return None
+        if local_exc is not None:
+            raise local_exc
+        if req is None:
+            return None
+        h = self._host(t)
+        if int(h[self.rank]):
+            return None
+        if int(h[self.world + self.rank]):
+            return capi.MatchmakerError(f"request {req!r} failed on another rank")
+        return capi.ErrMatchmakerTicketNotFound(req[-1])
 
     def Remove(self, tickets: Optional[Sequence[str]]):
         """Remove (matchmaker.go:972-1024) of ids that may live on any rank."""
@@ -483,6 +500,7 @@ class ClusterMatchmaker:
         keys = route_keys(pack.arr, sum(t is not None for t in reqs), self.pool_fields)
         own = self.owners(keys)
         err = None
+        local_exc = None  # a failure that is not a matchmaker status: re-raised after every collective
         k = 0
         for r, t in enumerate(reqs):
             if t is None:
@@ -497,6 +515,10 @@ class ClusterMatchmaker:
                                    created_at=t.created_at)
                 except capi.MatchmakerError as x:
                     e = x
+                except Exception as x:  # noqa: BLE001 - the requester gets a MatchmakerError, this rank re-raises
+                    e = capi.MatchmakerError(f"{type(x).__name__}: {x}")
+                    if local_exc is None:
+                        local_exc = x
             codes = [None] * self.world
             self.dist.all_gather_object(codes, None if e is None else (type(e).__name__, str(e)) if own[k] == self.rank or own[k] < 0 else None)
             src = own[k] if own[k] >= 0 else r
@@ -505,6 +527,8 @@ class ClusterMatchmaker:
                 cls = getattr(capi, got[0], capi.MatchmakerError)
                 err = cls(got[1])
             k += 1
+        if local_exc is not None:
+            raise local_exc
         return err
 
 

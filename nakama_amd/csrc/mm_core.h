@@ -69,9 +69,15 @@ hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs,
 // hashed multi-signature scan (ms.hmask != 0): d_blob = DMSig[n_sigs], u64
 // output word offsets[n_sigs], then at mscan_hash_table_off the cuckoo table
 // (DMHashEntry[hmask + 1]); d_work sized by mscan_hash_work_words
+// phases: kMHashEval runs mscan_hash_kernel over chunks [c_lo, c_hi) (a
+// row-sharded rank's block), kMHashPlace mscan_base + mscan_place over every
+// chunk (after the blocks' scratch and counts were all-gathered)
 hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_blob, uint32_t* d_work,
                              DGroupResult* d_cres, uint32_t* d_out32, hipStream_t stream, hipEvent_t ev0 = nullptr,
-                             hipEvent_t ev1 = nullptr);
+                             hipEvent_t ev1 = nullptr, int phases = kMHashEval | kMHashPlace, uint32_t c_lo = 0,
+                             uint32_t c_hi = UINT32_MAX);
+// word offset of the counts in d_work (the chunks' scratch comes first: chunk c at c * ms.chunk)
+uint64_t mscan_hash_counts_word(const DMScan& ms);
 uint64_t mscan_hash_work_words(const DMScan& ms);
 size_t mscan_hash_table_off(uint32_t n_sigs);
 size_t mscan_hash_blob_bytes(uint32_t n_sigs, uint32_t cap);
@@ -418,7 +424,6 @@ struct RevTimer {
 
 struct PassStats {
     int full_lists = 0;  // variable-score searches run as full lists (host-sorted)
-    // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel
     // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel
     double k_ms[4] = {0, 0, 0, 0};      // HIP-event time of the launches
     bool mhash = false;                 // a batch's mscan ran hashed (mscan_hash_kernel)
@@ -840,6 +845,7 @@ public:
     PinnedArray<DClause> h_mcl_;
     DevArray<DMSig> d_msig_;         // mscan_kernel's signatures
     PinnedArray<DMSig> h_msig_;
+    PinnedArray<uint32_t> h_mx_;     // row-sharded hashed scan: scratch + counts through the host exchange
     DevArray<uint8_t> d_rev_;
     DevArray<uint32_t> d_small_;     // rsmall_kernel's rows (indexes of the batch's whole searches)
     PinnedArray<uint32_t> h_small_;

@@ -16,6 +16,7 @@ namespace nkm {
 
 constexpr uint32_t kNoParty = 0xFFFFFFFFu;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+constexpr uint32_t kMaxShardBlocks = 8;  // ranks of a row-sharded hashed scan (one node's GPUs)
 
 // Column value kinds (one byte per (field, slot)).
 enum : uint8_t { KIND_ABSENT = 0, KIND_KEYWORD = 1, KIND_NUMERIC = 2 };
@@ -107,7 +108,22 @@ struct DMScan {
                                 // to `chunk` from src_off rounded down
     uint32_t hseed[2];          // hashed: the two cuckoo hash seeds
     uint32_t pad;
+    // hashed, row-sharded: rank r evaluates chunks [cb[r], cb[r + 1]) and its
+    // (n_sigs + 1) count columns are one contiguous block (mhash_cidx), so the
+    // ranks' scratch and counts are all-gathered as one segment each.
+    // n_blk <= 1: one block, the plain column-major layout.
+    uint32_t n_blk;
+    uint32_t cb[kMaxShardBlocks + 1];
 };
+
+// Index of the (column q, chunk c) count of a hashed scan (see DMScan::cb).
+NKM_HD inline uint64_t mhash_cidx(const DMScan& ms, uint32_t q, uint32_t c) {
+    if (ms.n_blk <= 1) return (uint64_t)q * ms.n_chunks + c;
+    uint32_t r = 0;
+    while (r + 1 < ms.n_blk && c >= ms.cb[r + 1]) r++;
+    const uint32_t b0 = ms.cb[r], len = ms.cb[r + 1] - b0;
+    return (uint64_t)(ms.n_sigs + 1) * b0 + (uint64_t)q * len + (c - b0);
+}
 
 // Hashed signature lookup of mscan_hash_kernel: term-only pool signatures that
 // all require the same keyword fields, with pairwise distinct required values,
@@ -118,6 +134,7 @@ struct DMScan {
 constexpr uint32_t kMHashSigs = 256;  // signatures of one hashed scan
 constexpr uint32_t kMHashCap = 1024;  // table entries (a power of two >= 2 x signatures)
 constexpr uint32_t kMHashEmpty = 0xFFFFu;
+constexpr int kMHashEval = 1, kMHashPlace = 2;  // launch_mscan_hash phases
 struct DMHashEntry {                  // 32 B
     uint32_t key[4];                  // required dictionary id per scanned field (0 past n_fields)
     uint32_t q;                       // signature, kMHashEmpty: free

@@ -736,7 +736,7 @@ struct MHashLds {
 template <int NF, int kMJ, bool CONTIG>
 __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms, const DMHashEntry* __restrict__ htab,
                                                             uint32_t* __restrict__ scratch,
-                                                            uint32_t* __restrict__ counts) {
+                                                            uint32_t* __restrict__ counts, uint32_t c0) {
     static_assert(NF >= 1 && NF <= 4, "1-4 required fields");
     static_assert(!CONTIG || kMJ == 4 || kMJ == 8, "runs of 4 or 8 candidates");
     constexpr int kMChunk = kMJ * kBlock;
@@ -750,7 +750,7 @@ __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms
     uint32_t* loff = reinterpret_cast<uint32_t*>(lds + L.loff_off());
     uint32_t* stage = reinterpret_cast<uint32_t*>(lds + L.stage_off());  // the chunk's hits, signature-major
     uint16_t* qs = reinterpret_cast<uint16_t*>(lds + L.qs_off());
-    const uint32_t c = blockIdx.x;
+    const uint32_t c = blockIdx.x + c0;  // c0: a row-sharded rank's first chunk
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #ifdef NKM_MH_DEBUG  // tools/mhash_bench.hip: phases switched off one by one (ms.pad bits)
     const uint32_t dbg = ms.pad;
@@ -949,12 +949,12 @@ __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms
     }
     if ((uint32_t)tid < nq) {
         loff[tid] = ex;
-        counts[(uint64_t)tid * ms.n_chunks + c] = tot;  // column-major: mscan_base_kernel reads columns
+        counts[mhash_cidx(ms, (uint32_t)tid, c)] = tot;  // column-major: mscan_base_kernel reads columns
     }
     if (tid == 0) {
         uint32_t lv = 0;
         for (int w = 0; w < kWaves; w++) lv += wlive[w];
-        counts[(uint64_t)nq * ms.n_chunks + c] = lv;
+        counts[mhash_cidx(ms, nq, c)] = lv;
     }
     __syncthreads();
     // ranked into LDS, then out in 16-B stores: with many signatures a
@@ -979,7 +979,9 @@ __global__ __launch_bounds__(kBlock) void mscan_base_kernel(DMScan ms, const uin
                                                             DGroupResult* __restrict__ res) {
     __shared__ uint32_t wsum[kWaves];
     const uint32_t q = blockIdx.x, n = ms.n_chunks;
+    // one block (the common case): the column is contiguous
     const uint32_t* __restrict__ col = counts + (uint64_t)q * n;
+    const bool blocked = ms.n_blk > 1;
     uint32_t* __restrict__ bcol = bases + (uint64_t)q * (n + 1);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t per = (n + kBlock - 1) / kBlock;
@@ -990,11 +992,12 @@ __global__ __launch_bounds__(kBlock) void mscan_base_kernel(DMScan ms, const uin
     uint32_t sum = 0;
     if (unrolled) {
 #pragma unroll
-        for (int k = 0; k < kUnroll; k++) v[k] = lo + k < hi ? col[lo + k] : 0u;
+        for (int k = 0; k < kUnroll; k++)
+            v[k] = lo + k < hi ? (blocked ? counts[mhash_cidx(ms, q, lo + k)] : col[lo + k]) : 0u;
 #pragma unroll
         for (int k = 0; k < kUnroll; k++) sum += v[k];
     } else {
-        for (uint32_t i = lo; i < hi; i++) sum += col[i];
+        for (uint32_t i = lo; i < hi; i++) sum += blocked ? counts[mhash_cidx(ms, q, i)] : col[i];
     }
     uint32_t incl = sum;
     for (int o = 1; o < 64; o <<= 1) {
@@ -1016,7 +1019,7 @@ __global__ __launch_bounds__(kBlock) void mscan_base_kernel(DMScan ms, const uin
         }
     } else {
         for (uint32_t i = lo; i < hi; i++) {
-            const uint32_t x = col[i];
+            const uint32_t x = blocked ? counts[mhash_cidx(ms, q, i)] : col[i];
             bcol[i] = run;
             run += x;
         }
@@ -1647,9 +1650,18 @@ size_t mscan_hash_table_off(uint32_t n_sigs) {
 size_t mscan_hash_blob_bytes(uint32_t n_sigs, uint32_t cap) {
     return mscan_hash_table_off(n_sigs) + (size_t)cap * sizeof(DMHashEntry);
 }
+uint64_t mscan_hash_counts_word(const DMScan& ms) { return (uint64_t)ms.n_chunks * ms.chunk; }
 hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_blob, uint32_t* d_work,
-                             DGroupResult* d_cres, uint32_t* d_out32, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
+                             DGroupResult* d_cres, uint32_t* d_out32, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1,
+                             int phases, uint32_t c_lo, uint32_t c_hi) {
     if (ms.n_chunks == 0 || ms.n_sigs == 0) return hipSuccess;
+    c_hi = c_hi < ms.n_chunks ? c_hi : ms.n_chunks;
+    if (c_lo > c_hi || ms.n_blk > kMaxShardBlocks) return hipErrorInvalidValue;
+    if (ms.n_blk > 1) {  // the blocks tile [0, n_chunks) in order
+        if (ms.cb[0] != 0 || ms.cb[ms.n_blk] != ms.n_chunks) return hipErrorInvalidValue;
+        for (uint32_t r = 0; r < ms.n_blk; r++)
+            if (ms.cb[r] > ms.cb[r + 1]) return hipErrorInvalidValue;
+    }
     const uint32_t mj = ms.chunk / kBlock;
     const uint64_t covered = ms.contig ? (uint64_t)(ms.src_off & ~(ms.chunk - 1)) + (uint64_t)ms.n_chunks * ms.chunk
                                        : (uint64_t)ms.n_chunks * ms.chunk;
@@ -1665,10 +1677,10 @@ hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_b
     uint32_t* scratch = d_work;  // first: 16-B aligned for the chunks' vector stores
     uint32_t* counts = scratch + (uint64_t)ms.n_chunks * ms.chunk;
     uint32_t* bases = counts + (uint64_t)ms.n_chunks * w1;
-    const dim3 grid(ms.n_chunks), block(kBlock);
-#define NKM_MHASH_K(NF, J, C)                                                                                        \
-    hipExtLaunchKernelGGL(mscan_hash_kernel<NF, J, C>, grid, block, (MHashLds<J, C>{ms.hmask + 1, ms.n_sigs}.bytes()), \
-                          stream, ev0, ev1, 0, st, ms, htab, scratch, counts)
+    const dim3 grid(ms.n_chunks), egrid(c_hi - c_lo), block(kBlock);
+#define NKM_MHASH_K(NF, J, C)                                                                                         \
+    hipExtLaunchKernelGGL(mscan_hash_kernel<NF, J, C>, egrid, block, (MHashLds<J, C>{ms.hmask + 1, ms.n_sigs}.bytes()), \
+                          stream, ev0, ev1, 0, st, ms, htab, scratch, counts, c_lo)
 #define NKM_MHASH(NF)                                        \
     do {                                                     \
         if (ms.contig && mj == 8) NKM_MHASH_K(NF, 8, true);  \
@@ -1676,17 +1688,20 @@ hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_b
         else if (mj == 4) NKM_MHASH_K(NF, 4, false);         \
         else NKM_MHASH_K(NF, 2, false);                      \
     } while (0)
-    switch (ms.n_fields) {
-        case 1: NKM_MHASH(1); break;
-        case 2: NKM_MHASH(2); break;
-        case 3: NKM_MHASH(3); break;
-        default: NKM_MHASH(4); break;
+    if ((phases & kMHashEval) && c_hi > c_lo) {
+        switch (ms.n_fields) {
+            case 1: NKM_MHASH(1); break;
+            case 2: NKM_MHASH(2); break;
+            case 3: NKM_MHASH(3); break;
+            default: NKM_MHASH(4); break;
+        }
     }
 #undef NKM_MHASH
 #undef NKM_MHASH_K
 #ifdef NKM_MH_DEBUG
     if (ms.pad & 2) return hipGetLastError();  // no counts to place
 #endif
+    if (!(phases & kMHashPlace)) return hipGetLastError();
     hipLaunchKernelGGL(mscan_base_kernel, dim3(ms.n_sigs + 1), block, 0, stream, ms, counts, bases, d_cres);
     hipLaunchKernelGGL(mscan_place_kernel, grid, block, 0, stream, ms, bases, scratch, dst, d_out32);
     return hipGetLastError();

@@ -230,6 +230,25 @@ private:
     void each_serial(F&& f) {
         for (int i = 0; i < (int)subs_.size(); i++) f(i);
     }
+    // Rows: one mutator on every replica, one after the other (mu_ held, so
+    // never during a pass: process() holds mu_ for the whole pass in rows
+    // mode).  The replicas hold the same tickets, so they must answer alike;
+    // a different answer means they diverged, which is reported.
+    template <class F>
+    int rows_apply(F&& f) {
+        int rc0 = MM_OK;
+        for (int i = 0; i < (int)subs_.size(); i++) {
+            const int rc = f(subs_[(size_t)i]);
+            if (i == 0) {
+                rc0 = sub_status(0, rc);
+            } else if (rc != rc0) {
+                last_error_ = "replica " + std::to_string(i) + " answered " + std::to_string(rc) + ", replica 0 " +
+                              std::to_string(rc0) + " (replicas diverged)";
+                return MM_ERR_INDEX;
+            }
+        }
+        return rc0;
+    }
     int sub_status(int i, int rc) {  // a sub-handle's failure becomes this handle's
         if (rc != MM_OK) {
             const char* e = api_.last_error(subs_[(size_t)i]);
@@ -467,14 +486,7 @@ void MultiCore::sync_removed(bool all_subs) {
 int MultiCore::add(const mm_ticket& t) {
     if (stopped_) return MM_ERR_NOT_AVAILABLE;
     std::lock_guard<std::mutex> lk(mu_);
-    if (rows()) {
-        int rc0 = MM_OK;
-        each_serial([&](int i) {
-            const int rc = api_.add(subs_[(size_t)i], &t);
-            if (i == 0) rc0 = sub_status(0, rc);
-        });
-        return rc0;
-    }
+    if (rows()) return rows_apply([&](void* sh) { return api_.add(sh, &t); });
     const QC& q = compiled(t.query);
     if (q.status != CQ_OK) return status_of(q.status);
     {
@@ -575,12 +587,9 @@ int MultiCore::insert(const mm_ticket* ts, int32_t n) {
 int MultiCore::remove_session(const std::string& sid, const std::string& ticket) {
     std::lock_guard<std::mutex> lk(mu_);
     if (rows()) {
-        int rc0 = MM_OK;
-        each_serial([&](int i) {
-            const int rc = api_.remove_session(subs_[(size_t)i], sid.c_str(), ticket.c_str());
-            if (i == 0) rc0 = rc;
-        });
-        return rc0;
+        const int rc = rows_apply([&](void* sh) { return api_.remove_session(sh, sid.c_str(), ticket.c_str()); });
+        sync_removed(false);
+        return rc;
     }
     auto it = tk_.find(ticket);
     if (it == tk_.end()) return MM_ERR_TICKET_NOT_FOUND;
@@ -593,12 +602,9 @@ int MultiCore::remove_session(const std::string& sid, const std::string& ticket)
 int MultiCore::remove_party(const std::string& pid, const std::string& ticket) {
     std::lock_guard<std::mutex> lk(mu_);
     if (rows()) {
-        int rc0 = MM_OK;
-        each_serial([&](int i) {
-            const int rc = api_.remove_party(subs_[(size_t)i], pid.c_str(), ticket.c_str());
-            if (i == 0) rc0 = rc;
-        });
-        return rc0;
+        const int rc = rows_apply([&](void* sh) { return api_.remove_party(sh, pid.c_str(), ticket.c_str()); });
+        sync_removed(false);
+        return rc;
     }
     auto it = tk_.find(ticket);
     if (it == tk_.end()) return MM_ERR_TICKET_NOT_FOUND;
@@ -667,13 +673,9 @@ int MultiCore::remove_all(const std::string& node) {
 int MultiCore::remove(const char* const* tickets, int32_t n) {
     std::lock_guard<std::mutex> lk(mu_);
     if (rows()) {
-        int rc0 = MM_OK;
-        each_serial([&](int i) {
-            const int rc = api_.remove(subs_[(size_t)i], tickets, n);
-            if (i == 0) rc0 = sub_status(0, rc);
-        });
+        const int rc = rows_apply([&](void* sh) { return api_.remove(sh, tickets, n); });
         sync_removed(false);
-        return rc0;
+        return rc;
     }
     std::vector<std::vector<const char*>> part(subs_.size());
     std::vector<std::string> ids;
@@ -729,12 +731,19 @@ int MultiCore::process(mm_matched* out) {
     const int ns = (int)subs_.size();
     std::vector<mm_matched> outs((size_t)ns);
     std::vector<int> rc((size_t)ns, MM_OK);
+    // Rows: the replicas take their pass snapshots at their own moments, so a
+    // mutation must not land between them — mu_ is held across the whole
+    // pass and a concurrent mutator waits for its end (the reference allows
+    // a mutation anywhere in the pass, matchmaker.go:290-343; this serialises
+    // it after the pass).  Pools: each sub-handle queues its own mutations.
+    std::unique_lock<std::mutex> lk(mu_, std::defer_lock);
+    if (rows()) lk.lock();
     if (ex_) ex_->reset();
     each([&](int i) {
         rc[(size_t)i] = api_.process(subs_[(size_t)i], &outs[(size_t)i]);
         if (rc[(size_t)i] != MM_OK && ex_) ex_->abort();  // the other replicas stop waiting for this one
     });
-    std::lock_guard<std::mutex> lk(mu_);
+    if (!rows()) lk.lock();
     int bad = -1;
     for (int i = 0; i < ns; i++)
         if (rc[(size_t)i] != MM_OK && (bad < 0 || rc[(size_t)bad] == MM_ERR_DEVICE)) bad = i;

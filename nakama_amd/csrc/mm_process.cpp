@@ -188,7 +188,8 @@ struct Replay : ReplayCore {
         m_list.clear();
         mcl.clear();
         const int km = c.kernel_mode_;
-        if (rev || km == Core::KM_SEARCH || km == Core::KM_SCAN || c.order_head_ >= c.order_.size() || c.row_shard())
+        if (rev || km == Core::KM_SEARCH || km == Core::KM_SCAN || c.order_head_ >= c.order_.size() ||
+            c.shard_world_ > (int)kMaxShardBlocks)
             return false;
         const bool any_size = km == Core::KM_MSCAN;
         const uint64_t order_len = c.order_.size() - c.order_head_;
@@ -238,10 +239,13 @@ struct Replay : ReplayCore {
         // the scan is contiguous (its vector loads: C3 1M 15.1-15.9 us against
         // mscan_kernel's 16.1-18.9 us on the same box, profiles/r03km_*), or
         // on request (NKM_MHASH=1; 2: never)
+        // Row-sharded: the hashed scan only — each rank scans one block of
+        // the chunks, and the blocks' per-chunk outputs are all-gathered
+        // before every rank places the lists (run_batch).
         const bool hashable = plan_mscan_hash(ms);
         const bool contig_ok = c.order_identity_ && c.mcontig_mode_;
         if (ms.n_sigs > (uint32_t)mscan_max_sigs() || nclauses > (size_t)mscan_max_clauses() || c.mhash_mode_ == 1 ||
-            (c.mhash_mode_ == 0 && hashable && contig_ok)) {
+            (c.mhash_mode_ == 0 && hashable && contig_ok) || c.row_shard()) {
             if (!hashable) {
                 m_list.clear();
                 mcl.clear();
@@ -259,6 +263,11 @@ struct Replay : ReplayCore {
             ms.n_chunks = (uint32_t)(((uint64_t)ms.src_off + ms.src_len - g0 + ms.chunk - 1) / ms.chunk);
         } else {
             ms.n_chunks = (ms.src_len + ms.chunk - 1) / ms.chunk;
+        }
+        if (c.row_shard()) {  // rank r scans chunks [cb[r], cb[r + 1])
+            const uint32_t W = (uint32_t)c.shard_world_;
+            ms.n_blk = W;
+            for (uint32_t r = 0; r <= W; r++) ms.cb[r] = (uint32_t)((uint64_t)ms.n_chunks * r / W);
         }
         return true;
     }
@@ -324,6 +333,47 @@ struct Replay : ReplayCore {
             }
         }
         return false;
+    }
+
+    // The hashed scan of a row-sharded batch: this rank's block of chunks,
+    // the blocks' chunk outputs (scratch) and count columns all-gathered in
+    // place — over RCCL between the devices, or through the host exchange —
+    // then every rank places every list (mscan_base + mscan_place), so the
+    // lists and result cells are identical on every rank.  Gathered: 4 B per
+    // scanned candidate + 4 B per (signature + 1, chunk).
+    void mscan_hash_sharded(const DMScan& ms, uint32_t* work, DGroupResult* cres) {
+        const int W = c.shard_world_, r = c.shard_rank_;
+        NKM_HIP(launch_mscan_hash(st, ms, c.d_msig_.p, work, cres, reinterpret_cast<uint32_t*>(c.d_out_.p), stream,
+                                  c.ev_[4], c.ev_[5], kMHashEval, ms.cb[r], ms.cb[r + 1]));
+        const uint64_t cw = mscan_hash_counts_word(ms), w1 = ms.n_sigs + 1;
+        std::vector<int64_t> o_sc(W + 1), o_cn(W + 1);
+        for (int q = 0; q <= W; q++) {
+            o_sc[q] = (int64_t)((uint64_t)ms.cb[q] * ms.chunk * 4);
+            o_cn[q] = (int64_t)((cw + w1 * ms.cb[q]) * 4);
+        }
+        if (c.nccl_comm_) {
+            c.shard_gather_device(work, o_sc);
+            c.shard_gather_device(work, o_cn);
+        } else {
+            const uint64_t words = cw + w1 * ms.n_chunks;
+            c.h_mx_.reserve(words);
+            char* h = reinterpret_cast<char*>(c.h_mx_.p);
+            char* d = reinterpret_cast<char*>(work);
+            for (const auto* o : {&o_sc, &o_cn})
+                if ((*o)[r + 1] > (*o)[r])
+                    NKM_HIP(hipMemcpyAsync(h + (*o)[r], d + (*o)[r], (size_t)((*o)[r + 1] - (*o)[r]),
+                                           hipMemcpyDeviceToHost, stream));
+            NKM_HIP(hipStreamSynchronize(stream));
+            c.shard_gather_host(h, o_sc);
+            c.shard_gather_host(h, o_cn);
+            for (const auto* o : {&o_sc, &o_cn})
+                for (int q = 0; q < W; q++)
+                    if (q != r && (*o)[q + 1] > (*o)[q])
+                        NKM_HIP(hipMemcpyAsync(d + (*o)[q], h + (*o)[q], (size_t)((*o)[q + 1] - (*o)[q]),
+                                               hipMemcpyHostToDevice, stream));
+        }
+        NKM_HIP(launch_mscan_hash(st, ms, c.d_msig_.p, work, cres, reinterpret_cast<uint32_t*>(c.d_out_.p), stream,
+                                  nullptr, nullptr, kMHashPlace));
     }
 
     // overlap: host work run while the batch's kernels and copies are in
@@ -623,7 +673,9 @@ struct Replay : ReplayCore {
         NKM_HIP(launch_scan(st, c.d_groups_.p + nwhole, nchunks, c.d_scan_.p, c.d_res_.p + nwhole, stream, c.ev_[2],
                             c.ev_[3]));
         stats.mhash |= hashed;
-        if (hashed)
+        if (hashed && c.row_shard())
+            mscan_hash_sharded(ms, reinterpret_cast<uint32_t*>(c.d_scan_.p + mscratch), c.d_res_.p + nwhole + nchunks);
+        else if (hashed)
             NKM_HIP(launch_mscan_hash(st, ms, c.d_msig_.p, reinterpret_cast<uint32_t*>(c.d_scan_.p + mscratch),
                                       c.d_res_.p + nwhole + nchunks, reinterpret_cast<uint32_t*>(c.d_out_.p), stream,
                                       c.ev_[4], c.ev_[5]));
@@ -693,6 +745,9 @@ struct Replay : ReplayCore {
             };
             d2h(c.h_res_.p, c.d_res_.p, o_res);
             d2h(c.h_out_.p, c.d_out_.p, o_out);
+            if (use_m)  // the hashed scan's result cells: every rank placed every list
+                NKM_HIP(hipMemcpyAsync(c.h_res_.p + nwhole + nchunks, c.d_res_.p + nwhole + nchunks,
+                                       (size_t)ncells * sizeof(DGroupResult), hipMemcpyDeviceToHost, stream));
             if (rev) d2h(c.h_rev_.p, c.d_rev_.p, o_rev);
             if (need_pm) d2h(c.h_pm_.p, c.d_pm_.p, o_pm);
         } else {
@@ -760,13 +815,28 @@ struct Replay : ReplayCore {
         }
         if (use_m) {
             // columns read once per candidate for all signatures; hits written per signature
+            // bytes each candidate's signature lookup loads: the alive flag,
+            // Min/MaxCount and per field a kind and a value (the contiguous
+            // hashed scan reads no slot id: 1 + 8 + 9 NF B; otherwise + 4);
+            // then 4 B per hit.  pair_evals: (row, candidate) decisions — one
+            // per scanned candidate and signature for mscan_kernel, one per
+            // scanned candidate for the hashed lookup (a candidate is tested
+            // against the one signature its values select).
+            const int64_t per_scan = ms.contig ? 1 : 5;
             const int64_t per_live = 8 + 9 * (int64_t)ms.n_fields;
             const DGroupResult* mr = c.h_res_.p + nwhole + nchunks;
+            // row-sharded: this rank scanned its block of the chunks
+            const double share = hashed && ms.n_blk > 1
+                                     ? (double)(ms.cb[c.shard_rank_ + 1] - ms.cb[c.shard_rank_]) / (double)ms.n_chunks
+                                     : 1.0;
+            int64_t kb = 0, pe = 0;
             for (uint32_t t = 0; t < ncells; t++) {
-                stats.k_bytes[2] += (int64_t)mr[t].scanned * 5 + (int64_t)mr[t].live * per_live + (int64_t)mr[t].count * 4;
-                stats.pair_evals += (int64_t)mr[t].scanned * ms.n_sigs;
+                kb += (int64_t)mr[t].scanned * per_scan + (int64_t)mr[t].live * per_live + (int64_t)mr[t].count * 4;
+                pe += (int64_t)mr[t].scanned * (hashed ? 1 : ms.n_sigs);
             }
-            stats.k_bytes[2] += (int64_t)(ms.n_sigs * sizeof(DMSig) + mcl.size() * sizeof(DClause));
+            stats.k_bytes[2] += (int64_t)((double)kb * share) +
+                                (int64_t)(ms.n_sigs * sizeof(DMSig) + mcl.size() * sizeof(DClause));
+            stats.pair_evals += (int64_t)((double)pe * share);
         }
         for (uint32_t i : full_var) {
             DHit* h = c.h_out_.p + lg[i].out_off;
@@ -1768,6 +1838,30 @@ int Core::process(mm_matched* out) {
     auto hook = [&] {
         if (pass_hook_) pass_hook_(pass_hook_ctx_);
     };
+    // A pass that fails (a device error) closes without a result: the handle
+    // lock is taken back, the queued mutations are applied, mutators stop
+    // queueing, the pass's selections are forgotten (no ticket left the
+    // index) and the device alive mask is re-uploaded whole at the next
+    // pass; only the decided rows' Intervals increments stay.  Then the
+    // error goes to the caller (mm_capi maps it).
+    struct Unwind {
+        Core& c;
+        std::unique_lock<std::mutex>& lk;
+        bool armed = true;
+        ~Unwind() {
+            if (!armed) return;
+            if (!lk.owns_lock()) lk.lock();
+            try {
+                c.apply_pending();
+            } catch (...) {
+            }
+            c.pass_running_ = false;
+            c.custom_open_ = false;
+            c.sel_.assign(c.sel_.size(), 0);
+            c.apply_defer_.clear();
+            c.dev_slots_ = 0;  // sync_device: every slot's alive flag again
+        }
+    } unwind{*this, lk};
     if (cfg_.override_enabled) {
         const auto t1 = std::chrono::steady_clock::now();
         process_custom(groups, expired, stats);
@@ -1829,6 +1923,7 @@ int Core::process(mm_matched* out) {
                          stats.par_gather_ms, stats.par_job_ms, stats.par_clear_ms);
         }
     }
+    unwind.armed = false;
     const int dk = stats.dominant();  // bench.py's roofline kernel
     out->eval_kernel = dk == 2 && stats.mhash ? 4 : dk == 3 && stats.rpack ? 5 : dk;
     out->eval_ms = stats.k_ms[dk];

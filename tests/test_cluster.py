@@ -547,3 +547,56 @@ def test_cluster_merge_with_reordering_override():
     assert None not in merged and len(merged) == out[0][3]
     assert sorted(map(tuple, map(lambda g: tuple(map(tuple, g)), merged))) == \
         sorted(map(tuple, map(lambda g: tuple(map(tuple, g)), want[0][0])))
+
+
+def failing_mutator_worker(rank, world, port, q):
+    import harness
+    from nakama_amd import capi, cluster
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mm = capi.Matchmaker(harness.oracle_lib(), max_intervals=3)
+        cm = cluster.ClusterMatchmaker(mm, dist, POOL_FIELDS[3])
+        ts = _make(3, 400, world, rank, 2)
+        cm.Insert(ts.ptr(), ts.n)
+        k0 = next(k for k in range(ts.n) if ts.tickets[k].session_id)  # a solo ticket (its own session)
+        tk = ts.ticket_id(k0) if rank == 0 else None
+        sid = ts.tickets[k0].session_id.decode() if rank == 0 else None
+        out = []
+
+        def broken(m, s, t):  # fails on rank 1 only, with an error that is not ErrMatchmakerTicketNotFound
+            if rank == 1:
+                raise capi.ErrMatchmakerNotAvailable("rank 1 stopped")
+            return m.RemoveSession(s, t)
+        try:
+            err = cm._targeted(broken, None if sid is None else (sid, tk))
+            out.append(None if err is None else type(err).__name__)
+        except capi.MatchmakerError as e:
+            out.append("raised " + type(e).__name__)
+        out.append(cm.ticket_count())  # the next collective still lines up on every rank
+        q.put((rank, out))
+        ts.close()
+        mm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cluster_targeted_error_keeps_collectives_aligned():
+    """A mutator that fails with an unexpected error on one rank: that rank
+    re-raises after the all_reduce (no rank is left in a collective), the
+    requester's own rank still succeeds (it held the ticket), and the next
+    collective runs on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=failing_mutator_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict([_wait(q, procs), _wait(q, procs)])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert res[1][0] == "raised ErrMatchmakerNotAvailable"
+    assert res[0][0] is None
+    assert res[0][1] == res[1][1] > 0

@@ -268,3 +268,83 @@ def test_gpu_multi_rows_host_exchange(config, n, kw):
         mm.close()
         one.close()
         ts.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,n", [(4, 12_000), (3, 9_000)])
+def test_gpu_multi_rows_hashed_scan(config, n, monkeypatch):
+    """MM_MULTI_ROWS on C4's shape (64 mode x region pools) and C3's: the
+    pool signatures run on the hashed scan split by candidate chunks between
+    the two sub-handles (the blocks' chunk outputs exchanged through host
+    memory, every sub-handle placing every list), equal to one oracle pass;
+    eval_kernel 4 = mscan_hash_kernel."""
+    monkeypatch.setenv("NKM_KERNEL", "mscan")
+    kw = dict(max_intervals=2)
+    ts = synth.TicketSet(config, n)
+    one = capi.Matchmaker(harness.oracle_lib(), **kw)
+    mm = multi(2, config, None, mode=capi.MM_MULTI_ROWS, transport=capi.MM_MULTI_HOST, **kw)
+    try:
+        ts.insert_into(one)
+        ts.insert_into(mm)
+        for p in range(2):
+            r = mm.process_raw()
+            assert r.groups == one.Process(), f"pass {p}"
+            assert state(mm) == state(one)
+            if p == 0:
+                assert r.eval_kernel == 4
+    finally:
+        mm.close()
+        one.close()
+        ts.close()
+
+
+@pytest.mark.gpu
+def test_gpu_multi_rows_mutations_during_pass_wait_for_it():
+    """MM_MULTI_ROWS: a mutator called while a pass runs waits for the pass
+    to end and then reaches every replica, so the replicas never diverge (a
+    mutation seen by one replica's pass and not another's would split their
+    searches).  Equal to the oracle running the same mutations after its pass."""
+    import threading
+
+    from test_concurrency import _mutations, _state
+
+    def run(mm, concurrent):
+        base = synth.TicketSet(6, 400)
+        extra = synth.TicketSet(6, 300, first=400)
+        try:
+            base.insert_into(mm)
+            mm.drain_removed()
+            statuses, err = [], []
+
+            def mutate():
+                try:
+                    _mutations(mm, base, extra, statuses)
+                except Exception as e:  # surfaced below
+                    err.append(e)
+            th = threading.Thread(target=mutate)
+            if concurrent:
+                mm.set_pass_hook(th.start)  # the mutations start inside sub-handle 0's pass
+                groups = mm.Process()
+                th.join(120)
+                mm.set_pass_hook(None)
+            else:
+                groups = mm.Process()
+                th.start()
+                th.join(120)
+            assert not th.is_alive() and not err, err
+            out = [groups, statuses, _state(mm), sorted(mm.drain_removed()), mm.Process(), _state(mm),
+                   sorted(mm.drain_removed())]
+            if concurrent:
+                assert mm.lib.mm_multi_info(mm.h, 1) == mm.ticket_count()  # the replicas agree
+            return out
+        finally:
+            mm.close()
+            base.close()
+            extra.close()
+
+    got = run(multi(2, 6, None, mode=capi.MM_MULTI_ROWS, transport=capi.MM_MULTI_HOST, max_tickets=3, max_intervals=3),
+              True)
+    want = run(capi.Matchmaker(harness.oracle_lib(), max_tickets=3, max_intervals=3), False)
+    names = ["groups", "statuses", "state", "removed", "next groups", "next state", "next removed"]
+    for name, a, b in zip(names, got, want):
+        assert a == b, name

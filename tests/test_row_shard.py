@@ -24,7 +24,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from test_cluster import _free_port, _wait  # noqa: E402
 
 
-def row_worker(rank, world, port, config, n, passes, cfg, transport, use_product, q, backend="gloo"):
+def row_worker(rank, world, port, config, n, passes, cfg, transport, use_product, q, backend="gloo", env=None):
+    os.environ.update(env or {})
     import harness
     from nakama_amd import capi, cluster, synth
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -49,7 +50,7 @@ def row_worker(rank, world, port, config, n, passes, cfg, transport, use_product
         out = []
         for _ in range(passes):
             r = rm.Process()
-            out.append((r.groups, [(t.ticket, t.intervals) for t in rm.Extract()], mm.active_count(), r.n_batches))
+            out.append((r.groups, [(t.ticket, t.intervals) for t in rm.Extract()], mm.active_count(), r.eval_kernel))
         allout = [None] * world
         dist.all_gather_object(allout, (out, rm.gather_bytes))
         if rank == 0:
@@ -60,12 +61,12 @@ def row_worker(rank, world, port, config, n, passes, cfg, transport, use_product
         dist.destroy_process_group()
 
 
-def run_rows(config, n, passes, cfg, transport, use_product, world=2, backend="gloo"):
+def run_rows(config, n, passes, cfg, transport, use_product, world=2, backend="gloo", env=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=row_worker,
-                         args=(r, world, port, config, n, passes, cfg, transport, use_product, q, backend))
+                         args=(r, world, port, config, n, passes, cfg, transport, use_product, q, backend, env))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -110,6 +111,23 @@ def test_row_sharded_host_transport(config, n, passes, mi, rev):
     for out, nbytes in allout:
         assert [(g, s, a) for g, s, a, _ in out] == want
         assert nbytes > 0  # the blocks really were exchanged
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,n", [(4, 12_000), (3, 9_000)])
+def test_row_sharded_hashed_scan_host_transport(config, n):
+    """C4's shape (64 mode x region pools, its BASELINE mode: row-sharded)
+    and C3's: every batch's pool signatures run as one hashed scan split by
+    candidate chunks — each rank scans its block, the chunk outputs and
+    counts are all-gathered, every rank places every list — equal to one
+    oracle pass, with eval_kernel 4 (mscan_hash_kernel) on every rank."""
+    cfg = dict(max_intervals=2)
+    allout = run_rows(config, n, 2, cfg, "host", True, env={"NKM_KERNEL": "mscan"})
+    want = oracle_passes(config, n, 2, cfg)
+    for out, nbytes in allout:
+        assert [(g, s, a) for g, s, a, _ in out] == want
+        assert out[0][3] == 4
+        assert nbytes > 0
 
 
 @pytest.mark.gpu

@@ -162,7 +162,7 @@ static int run_shape(uint32_t n, int nmode, int nregion, uint4* evict, size_t ev
                         CK(hipStreamSynchronize(s));
                         std::this_thread::sleep_for(std::chrono::milliseconds(5));
                     }
-                    CK(launch_mscan_hash(st, ms, d_blob, d_work, d_res, d_out, s, e0, e1));
+                    CK(launch_mscan_hash(st, ms, d_blob, d_work, d_res, d_out, s, e0, e1, kMHashEval | kMHashPlace, 0, UINT32_MAX));
                     CK(hipEventRecord(e2, s));
                     CK(hipEventSynchronize(e2));
                     float a, b;
