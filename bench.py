@@ -80,10 +80,23 @@ def parse():
     ap.add_argument("--override", action="store_true",
                     help="register a MatchmakerOverride (processCustom path): the timed step is the candidate pass, "
                          "a native first-disjoint override and mm_process_commit (per rank under the cluster front)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03z_traffic.json"))
+    ap.add_argument("--multi-handle", type=int, default=0, metavar="N",
+                    help="one process drives ONE C-ABI handle over N devices (mm_create_multi, the handle a Go "
+                         "server constructs, main.go:160): N x the per-GPU set (C3) or the whole set (C4/C5); "
+                         "devices cycle over the visible GPUs (a one-GPU box: N sub-handles on device 0)")
+    ap.add_argument("--multi-mode", choices=["pools", "rows"], default="pools",
+                    help="with --multi-handle: MM_MULTI_POOLS (pools placed whole) or MM_MULTI_ROWS (row-sharded)")
+    ap.add_argument("--front", choices=["cluster", "multi"], default=os.environ.get("NKM_BENCH_FRONT", "cluster"),
+                    help="under torchrun (WORLD_SIZE > 1): 'cluster' = one process per GPU through cluster.py; "
+                         "'multi' = rank 0 drives one multi-device handle over all WORLD_SIZE GPUs through the C ABI "
+                         "(the other ranks only take part in the barriers)")
+    ap.add_argument("--traffic", default=None,
+                    help="PMC traffic file (tools/pmc_traffic.py); default profiles/r04_c<config>_traffic.json")
     a = ap.parse_args()
     if a.tickets is None:
         a.tickets = DEFAULT_TICKETS.get(a.config, 1_000_000)
+    if a.traffic is None:
+        a.traffic = os.path.join(ROOT, "profiles", f"r04_c{a.config}_traffic.json")
     return a
 
 
@@ -215,6 +228,8 @@ def main():
     world, rank, local, pg, backend = dist_setup(args)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if args.multi_handle or (world > 1 and args.front == "multi"):
+        return main_multi(args, world, rank, local, pg)
     import nakama_amd
     import torch
 
@@ -288,11 +303,14 @@ def main():
     avg_launch_ms = eval_ms / max(1, launches)
     # HBM bytes per launch from the PMC passes of the committed rocprofv3 run
     # (tools/pmc_traffic.py) — not measured in this process, labelled so
+    # Only a file measured on this line's kernel, config and ticket count
+    # (the PMC run's own workload) is attached; otherwise traffic is null.
     traffic, traffic_src = None, None
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
-            if tr.get("kernel") in kernels:
+            if (tr.get("kernel") in kernels and len(kernels) == 1 and tr.get("config") == args.config and
+                    tr.get("tickets") == args.tickets):
                 traffic, traffic_src = tr.get("bytes_per_launch"), os.path.relpath(args.traffic, ROOT)
         except Exception:
             traffic = None
@@ -349,6 +367,118 @@ def main():
         out["cpu_baseline"] = None
     mm.close()
     if rank == 0:
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.barrier()
+        pg.destroy_process_group()
+
+
+def main_multi(args, world, rank, local, pg):
+    """ONE matchmaker handle over N devices in this process, through the C ABI
+    (mm_create_multi, include/nakama_cluster.h) — what a Go server
+    constructs (main.go:160) with the INTEGRATION.md shim.  Under torchrun
+    (--front multi) rank 0 drives all WORLD_SIZE GPUs and the other ranks
+    only join the barriers; alone (--multi-handle N) the process drives N
+    sub-handles over the visible GPUs.  Same step as main(): insert a fresh set
+    (untimed: routed by pool inside the library), one timed Process()."""
+    import torch
+
+    import nakama_amd
+    from nakama_amd import capi, synth
+    n_sub = args.multi_handle or world
+    visible = max(1, torch.cuda.device_count())
+    devs = [i % visible for i in range(n_sub)]
+    strong = args.config in STRONG
+    total = args.tickets if strong else args.tickets * n_sub
+    mm = None
+    if rank == 0:
+        if world > 1:
+            os.environ["LOCAL_WORLD_SIZE"] = "1"  # the other ranks sit idle: the sub-handles share all host cores
+        mode = capi.MM_MULTI_ROWS if args.multi_mode == "rows" else capi.MM_MULTI_POOLS
+        mm = nakama_amd.LocalMatchmaker(max_intervals=2, rev_precision=args.config in REV, rev_threshold=0,
+                                        override=(lambda groups: groups) if args.override else None,
+                                        multi=dict(devices=devs, mode=mode, pool_fields=list(POOL_FIELDS[args.config])))
+    times, matched_all, presences_all, ins_times = [], [], [], []
+    eval_ms = eval_bytes = launches = pair_evals = cands = 0
+    batches, kernels = [], set()
+    for step in range(args.warmup + args.steps):
+        ins_dt = dt = 0.0
+        if rank == 0:
+            groups = n_sub if (args.config in (1, 2, 3) and n_sub > 1) else None
+            ts = synth.TicketSet(args.config, total, first=step * total, pool_groups=groups)
+            t_ins = time.perf_counter()
+            ts.insert_into(mm)  # untimed: routed to the sub-handles by pool (or replicated: rows)
+            ins_dt = time.perf_counter() - t_ins
+        barrier_sync(pg, local)
+        t0 = time.perf_counter()
+        if rank == 0:
+            out = mm.process_call()
+            n_cands = out.n_groups if out.is_candidates else 0
+            cand_pe = out.pair_evals
+            if args.override and out.is_candidates:
+                out = synth.override_commit(mm, out)
+            for d in sorted(set(devs)):
+                torch.cuda.synchronize(d)
+        barrier_sync(pg, local)
+        dt = time.perf_counter() - t0
+        if rank == 0:
+            n_groups, matched, pres, r = mm.process_summary(out)
+            ts.close()
+            if step >= args.warmup:
+                times.append(dt)
+                ins_times.append(ins_dt)
+                matched_all.append(matched)
+                presences_all.append(pres)
+                eval_ms += r.eval_ms
+                eval_bytes += r.eval_bytes
+                launches += r.eval_launches
+                pair_evals += cand_pe if args.override else r.pair_evals
+                cands += n_cands
+                batches.append(r.n_batches)
+                kernels.add(KERNELS.get(r.eval_kernel, str(r.eval_kernel)))
+            mm.Remove([t.ticket for t in mm.Extract()]) if mm.ticket_count() else None
+    if rank == 0:
+        total_t = sum(times)
+        achieved = (eval_bytes / 1e9) / (eval_ms / 1e3) if eval_ms > 0 else 0.0
+        n_dev = len(set(devs))
+        out = {
+            "metric": "tickets matched/sec + Process() interval p50 latency at 1M active tickets",
+            "value": sum(matched_all) / total_t,
+            "unit": "tickets/s",
+            "n_gpus": n_dev,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * total_t / args.steps,
+            "p50_ms": 1e3 * statistics.median(times),
+            "presences_per_s": sum(presences_all) / total_t,
+            "pair_evals_per_s": pair_evals / total_t,
+            "insert_ms": 1e3 * statistics.median(ins_times),
+            "with_insert_tickets_per_s": sum(matched_all) / (total_t + sum(ins_times)),
+            "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
+            "vs_baseline": None,
+            "dtype": "int64/f64",
+            "data": "synthetic",
+            "config": {"workload": WORKLOADS.get(args.config, str(args.config)) +
+                                   (" + MatchmakerOverride" if args.override else ""),
+                       ("tickets_total" if strong else "tickets_per_gpu"): args.tickets,
+                       "max_intervals": 2,
+                       "parallelism": (f"one C-ABI handle over {n_sub} sub-handles (mm_create_multi, "
+                                       f"{'MM_MULTI_ROWS' if args.multi_mode == 'rows' else 'MM_MULTI_POOLS'}) on "
+                                       f"devices {devs}" + (" (one GPU: the sub-handles share it)" if n_dev < n_sub
+                                                            else "")),
+                       "matched_per_step": sum(matched_all) / args.steps, "batches_per_pass": batches,
+                       "candidates_per_pass": (cands / args.steps) if args.override else None},
+            # the sub-handles' launches run concurrently: eval time is the slowest device's
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "traffic_source": None,
+                         "kernel": "+".join(sorted(kernels)), "launches": launches,
+                         "avg_launch_ms": eval_ms / max(1, launches), "bytes_per_launch": eval_bytes / max(1, launches),
+                         "note": "eval bytes of the sub-handles on the dominant kernel / the slowest sub-handle's "
+                                 "event time"},
+            "cpu_baseline": None,
+        }
+        mm.close()
         print(json.dumps(out), flush=True)
     if pg is not None:
         pg.barrier()

@@ -163,6 +163,9 @@ typedef struct mm_sub_api {
     void (*free_str_list)(void*, mm_str_list*);
     int32_t (*debug_hits)(void*, const char*, const char**, double*, int32_t);
     void (*debug_set_pass_hook)(void*, void (*)(void*), void*);
+    int32_t (*session_ticket_count)(void*, const char*);
+    int32_t (*party_ticket_count)(void*, const char*);
+    int32_t (*find_tickets)(void*, const char* const*, int32_t, uint8_t*);
 } mm_sub_api;
 
 #define MM_MULTI_POOLS 0

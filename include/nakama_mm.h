@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MM_ABI_VERSION 3
+#define MM_ABI_VERSION 4
 
 /* Status codes. */
 #define MM_OK 0
@@ -173,10 +173,12 @@ int  mm_process_commit(void* h, const int32_t* group_offsets, const mm_entry_ref
                        int32_t n_groups, mm_matched* out);
 void mm_free_matched(void* h, mm_matched* out);
 
-/* Tickets that left the matchmaker (Remove*, a re-inserted ticket id, or
- * matched and retired by a pass) since the previous call; the first call
- * starts the recording.  The Go shim drops its delivery entries with them
- * (ABI 3). */
+/* Tickets that left the matchmaker by a removal (Remove*, or a re-inserted
+ * ticket id replacing its old record) since the previous call; the first call
+ * starts the recording.  Tickets matched by a pass are not repeated here: they
+ * are the pass's result (mm_matched), delivered and dropped from there.  The
+ * Go shim drops its delivery entries with them (ABI 4: before, matched
+ * tickets were logged too, a million strings per 1M-ticket pass). */
 int  mm_drain_removed(void* h, mm_str_list* out);
 void mm_free_str_list(void* h, mm_str_list* out);
 
@@ -187,6 +189,17 @@ void mm_free_str_list(void* h, mm_str_list* out);
 void mm_debug_set_pass_hook(void* h, void (*fn)(void*), void* ctx);
 int32_t mm_ticket_count(void* h);
 int32_t mm_active_count(void* h);
+/* sessionTickets / partyTickets sizes (matchmaker.go:201-204): the tickets
+ * one session (a presence's session id) or one party holds, counting the
+ * mutations queued during a running pass (the state Add checks MaxTickets
+ * against, matchmaker.go:505-520).  The multi-device handle sums them over
+ * its sub-handles for a session whose tickets sit in different pools (ABI 4). */
+int32_t mm_session_ticket_count(void* h, const char* session_id);
+int32_t mm_party_ticket_count(void* h, const char* party_id);
+/* found[i] = 1 when tickets[i] is in m.indexes (queued mutations included);
+ * returns how many were found.  The multi-device handle finds a ticket's
+ * sub-handle with it instead of keeping a per-ticket map (ABI 4). */
+int32_t mm_find_tickets(void* h, const char* const* tickets, int32_t n, uint8_t* found);
 /* Hit list of one active ticket as processDefault's search would return it
  * right now (sorted, self removed): up to cap ticket strings written as
  * pointers valid until the next call on h; returns the total hit count. */

@@ -136,7 +136,9 @@ SUB_API = (("create", "mm_create"), ("destroy", "mm_destroy"), ("pause", "mm_pau
            ("process", "mm_process"), ("process_commit", "mm_process_commit"), ("free_matched", "mm_free_matched"),
            ("ticket_count", "mm_ticket_count"), ("active_count", "mm_active_count"),
            ("drain_removed", "mm_drain_removed"), ("free_str_list", "mm_free_str_list"),
-           ("debug_hits", "mm_debug_hits"), ("debug_set_pass_hook", "mm_debug_set_pass_hook"))
+           ("debug_hits", "mm_debug_hits"), ("debug_set_pass_hook", "mm_debug_set_pass_hook"),
+           ("session_ticket_count", "mm_session_ticket_count"), ("party_ticket_count", "mm_party_ticket_count"),
+           ("find_tickets", "mm_find_tickets"))
 
 
 class mm_sub_api(C.Structure):
@@ -164,7 +166,8 @@ EXPORTED_SYMBOLS = (
     "mm_remove_session_all", "mm_remove_party", "mm_remove_party_all", "mm_remove_all", "mm_remove",
     "mm_process", "mm_process_commit", "mm_free_matched", "mm_ticket_count", "mm_active_count",
     "mm_debug_hits", "mm_debug_compile", "mm_debug_term_match", "mm_debug_group_indexes",
-    "mm_drain_removed", "mm_free_str_list", "mm_debug_set_pass_hook",
+    "mm_drain_removed", "mm_free_str_list", "mm_debug_set_pass_hook", "mm_session_ticket_count",
+    "mm_party_ticket_count", "mm_find_tickets",
 )
 
 
@@ -226,6 +229,9 @@ def load_library(path: str) -> C.CDLL:
         "mm_drain_removed": (C.c_int, [vp, C.POINTER(mm_str_list)]),
         "mm_free_str_list": (None, [vp, C.POINTER(mm_str_list)]),
         "mm_debug_set_pass_hook": (None, [vp, PASS_HOOK, vp]),
+        "mm_session_ticket_count": (C.c_int32, [vp, C.c_char_p]),
+        "mm_party_ticket_count": (C.c_int32, [vp, C.c_char_p]),
+        "mm_find_tickets": (C.c_int32, [vp, C.POINTER(C.c_char_p), C.c_int32, C.POINTER(C.c_uint8)]),
         "mm_debug_term_match": (C.c_int, [C.c_int32, C.c_char_p, C.c_int32, C.c_char_p, C.POINTER(C.c_double)]),
         "mm_debug_group_indexes": (C.c_int32, [C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_int32, C.c_int32,
                                                C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int64),
@@ -563,6 +569,20 @@ class Matchmaker:
         self.lib.mm_debug_set_pass_hook(self.h, self._hook if fn is not None else PASS_HOOK(), None)
 
     # introspection
+    def session_ticket_count(self, session_id: str) -> int:
+        return int(self.lib.mm_session_ticket_count(self.h, _b(session_id)))
+
+    def party_ticket_count(self, party_id: str) -> int:
+        return int(self.lib.mm_party_ticket_count(self.h, _b(party_id)))
+
+    def find_tickets(self, tickets: Sequence[str]) -> List[bool]:
+        ids = (C.c_char_p * max(1, len(tickets)))(*[_b(t) for t in tickets])
+        found = (C.c_uint8 * max(1, len(tickets)))()
+        n = self.lib.mm_find_tickets(self.h, ids, len(tickets), found)
+        if n < 0:
+            self._check(n)
+        return [bool(found[i]) for i in range(len(tickets))]
+
     def ticket_count(self) -> int:
         return self.lib.mm_ticket_count(self.h)
 

@@ -129,6 +129,22 @@ int32_t mm_active_count(void* h) {
     (void)guarded(h, [&](Handle& c) { n = c.active_count(); return MM_OK; });
     return n;
 }
+int32_t mm_session_ticket_count(void* h, const char* session_id) {
+    int32_t n = -1;
+    const int rc = guarded(h, [&](Handle& c) { n = c.session_ticket_count(S(session_id)); return MM_OK; });
+    return rc == MM_OK ? n : rc;
+}
+int32_t mm_party_ticket_count(void* h, const char* party_id) {
+    int32_t n = -1;
+    const int rc = guarded(h, [&](Handle& c) { n = c.party_ticket_count(S(party_id)); return MM_OK; });
+    return rc == MM_OK ? n : rc;
+}
+int32_t mm_find_tickets(void* h, const char* const* tickets, int32_t n, uint8_t* found) {
+    if (n < 0 || (n > 0 && (!tickets || !found))) return MM_ERR_ARG;
+    int32_t k = 0;
+    const int rc = guarded(h, [&](Handle& c) { k = c.find_tickets(tickets, n, found); return MM_OK; });
+    return rc == MM_OK ? k : rc;
+}
 int mm_drain_removed(void* h, mm_str_list* out) {
     if (!out) return MM_ERR_ARG;
     return guarded(h, [&](Handle& c) { return c.drain_removed(out); });

@@ -494,6 +494,9 @@ public:
     int32_t ticket_count() override;
     int32_t active_count() override;
     int32_t debug_hits(const std::string& ticket, const char** tk, double* sc, int32_t cap) override;
+    int32_t session_ticket_count(const std::string& sid) override;
+    int32_t party_ticket_count(const std::string& pid) override;
+    int32_t find_tickets(const char* const* ids, int32_t n, uint8_t* found) override;
 
     void pause() override { active_flag_ = false; }
     void resume() override { active_flag_ = true; }
@@ -597,7 +600,9 @@ private:
     uint32_t termset_of(const HostClause& c);  // interned regexp/wildcard/fuzzy matcher
     void refresh_termsets();                   // extends accepted sets over new dictionary terms, uploads
     void set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val);
-    void kill_slot(uint32_t slot, bool device_cleared = false, bool replaced = false);  // ticket leaves the index and the maps
+    // the ticket leaves the index and the maps; quiet: not reported by
+    // mm_drain_removed (a replaced id lives on, a matched ticket is in the pass result)
+    void kill_slot(uint32_t slot, bool device_cleared = false, bool quiet = false);
     void maybe_compact();
     void compact();
     bool live(uint32_t slot) const { return live_[slot] != 0; }

@@ -71,14 +71,12 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
         if (sess_slots_.more.empty() && party_slots_.more.empty()) {
             const size_t ng2 = groups.size();
             std::vector<uint32_t> killed(nchunk, 0);
-            std::vector<std::vector<std::string>> gone(track_removed_ ? nchunk : 0);
             wp.run(nchunk, [&](size_t c) {
                 uint32_t k = 0;
                 const size_t e0 = groups.off[ng2 * c / nchunk], e1 = groups.off[ng2 * (c + 1) / nchunk];
                 for (size_t i = e0; i < e1; i++) {
                     const uint32_t s = groups.ents[i].first;
                     if (!live_[s]) continue;  // a ticket's presence entries repeat its slot
-                    if (track_removed_) gone[c].emplace_back(tk(s));
                     live_[s] = 0;
                     is_active_[s] = 0;
                     k++;
@@ -86,9 +84,8 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
                 killed[c] = k;
             });
             for (uint32_t k : killed) n_live_ -= k;
-            for (auto& v : gone) removed_ids_.insert(removed_ids_.end(), v.begin(), v.end());
         } else {
-            for (auto& e : groups.ents) kill_slot(e.first, true);
+            for (auto& e : groups.ents) kill_slot(e.first, true, true);  // matched: in the result, not the drain
         }
         f2 = fclk::now();
     }
@@ -139,12 +136,11 @@ bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& gro
     mm_entry_ref* ents = out_ents_.data();
     int64_t* gc = out_created_.data();
     std::vector<uint32_t> killed(nch, 0);
-    std::vector<std::vector<std::string>> gone(track_removed_ ? nch : 0);
     // Without a mutation, the matched tickets are exactly the pass's selection
     // (sel_): retired by one sequential sweep over the slots instead of
     // scattered writes per result entry
     const size_t N = nslots();
-    const bool by_slot = !mutated && !track_removed_ && sel_.size() == N;
+    const bool by_slot = !mutated && sel_.size() == N;
     wp.run(nch, [&](size_t c) {
         const size_t g0 = ng * c / nch, g1 = ng * (c + 1) / nch;
         uint32_t k = 0;
@@ -174,7 +170,6 @@ bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& gro
             for (size_t i = groups.off[g0]; i < groups.off[g1]; i++) {
                 const uint32_t s = groups.ents[i].first;
                 if (!live_[s]) continue;  // a ticket's presence entries repeat its slot
-                if (track_removed_) gone[c].emplace_back(tk(s));
                 live_[s] = 0;
                 is_active_[s] = 0;
                 k++;
@@ -184,7 +179,6 @@ bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& gro
     });
     const auto f1 = std::chrono::steady_clock::now();
     for (uint32_t k : killed) n_live_ -= k;
-    for (auto& v : gone) removed_ids_.insert(removed_ids_.end(), v.begin(), v.end());
     filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, list_tmp_,
                  [&](uint32_t s) { return live_[s] && is_active_[s]; });
     active_list_.swap(list_tmp_);
@@ -225,7 +219,7 @@ void Core::finish_pass_serial(GroupList& groups, bool selected) {
             i--;
             continue;
         }
-        for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e) kill_slot(e->first, true);
+        for (const auto* e = groups.begin(order[i]); e != groups.end(order[i]); ++e) kill_slot(e->first, true, true);
     }
     if (removed) {
         GroupList kept;

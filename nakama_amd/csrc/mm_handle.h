@@ -33,6 +33,9 @@ struct Handle {
     virtual int32_t ticket_count() = 0;
     virtual int32_t active_count() = 0;
     virtual int32_t debug_hits(const std::string& ticket, const char** tk, double* sc, int32_t cap) = 0;
+    virtual int32_t session_ticket_count(const std::string& sid) = 0;
+    virtual int32_t party_ticket_count(const std::string& pid) = 0;
+    virtual int32_t find_tickets(const char* const* ids, int32_t n, uint8_t* found) = 0;
     virtual void pause() = 0;
     virtual void resume() = 0;
     virtual void stop() = 0;

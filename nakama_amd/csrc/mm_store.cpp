@@ -512,9 +512,9 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
     return id;
 }
 
-void Core::kill_slot(uint32_t s, bool device_cleared, bool replaced) {
+void Core::kill_slot(uint32_t s, bool device_cleared, bool quiet) {
     if (!live_[s]) return;
-    if (track_removed_ && !replaced) removed_ids_.emplace_back(tk(s));  // a replaced id lives on
+    if (track_removed_ && !quiet) removed_ids_.emplace_back(tk(s));
     live_[s] = 0;
     is_active_[s] = 0;
     n_live_--;
@@ -1096,6 +1096,45 @@ int Core::remove_locked(const std::vector<std::string>& ids) {
         if (s >= 0) kill_slot((uint32_t)s);
     }
     return MM_OK;
+}
+
+int32_t Core::session_ticket_count(const std::string& sid) {
+    std::lock_guard<std::mutex> lk(mu_);
+    return eff_sess_count(sid);
+}
+int32_t Core::party_ticket_count(const std::string& pid) {
+    std::lock_guard<std::mutex> lk(mu_);
+    return pid.empty() ? 0 : eff_party_count(pid);
+}
+
+// Membership in m.indexes, queued mutations included; large lists on the
+// workers (read-only lookups) when no pass owns them.
+int32_t Core::find_tickets(const char* const* ids, int32_t n, uint8_t* found) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto one = [&](int32_t i) -> uint8_t {
+        const std::string_view id = ids[i] ? std::string_view(ids[i]) : std::string_view();
+        if (pass_running_ && !pend_tk_.empty()) {
+            auto it = pend_tk_.find(std::string(id));
+            if (it != pend_tk_.end()) return it->second.alive ? 1 : 0;
+        }
+        return slot_of_ticket(id) >= 0 ? 1 : 0;
+    };
+    if (n >= 65536 && par_mode_ && !pass_running_) {
+        WorkPool& wp = workers();
+        const size_t nch = (size_t)wp.size() * 4;
+        std::vector<int32_t> cnt(nch, 0);
+        wp.run(nch, [&](size_t c) {
+            int32_t k = 0;
+            for (int32_t i = (int32_t)((size_t)n * c / nch); i < (int32_t)((size_t)n * (c + 1) / nch); i++) k += found[i] = one(i);
+            cnt[c] = k;
+        });
+        int32_t k = 0;
+        for (int32_t x : cnt) k += x;
+        return k;
+    }
+    int32_t k = 0;
+    for (int32_t i = 0; i < n; i++) k += found[i] = one(i);
+    return k;
 }
 
 int32_t Core::ticket_count() {

@@ -968,8 +968,7 @@ static void finish_pass(Matchmaker& m, const vector<string>& expired, vector<vec
             continue;
         }
         for (auto& e : matched[i]) {
-            const string t = e.idx->ticket;
-            if (m.indexes.count(t)) m.note_removed(t);
+            const string t = e.idx->ticket;  // matched: reported by the pass result, not the drain (ABI 4)
             m.indexes.erase(t);
             m.active_indexes.erase(t);
             m.rev_cache.erase(t);
@@ -1405,6 +1404,30 @@ void mm_free_matched(void* h, mm_matched* out) {
 }
 
 int32_t mm_ticket_count(void* h) { auto& m = *static_cast<Matchmaker*>(h); std::lock_guard<std::mutex> lk(m.mu); return (int32_t)m.indexes.size(); }
+// m.sessionTickets / m.partyTickets sizes (matchmaker.go:201-204, read by Add :505-520)
+int32_t mm_session_ticket_count(void* h, const char* sid) {
+    auto& m = *static_cast<Matchmaker*>(h);
+    std::lock_guard<std::mutex> lk(m.mu);
+    auto it = m.session_tickets.find(sid ? sid : "");
+    return it == m.session_tickets.end() ? 0 : (int32_t)it->second.size();
+}
+int32_t mm_party_ticket_count(void* h, const char* pid) {
+    auto& m = *static_cast<Matchmaker*>(h);
+    std::lock_guard<std::mutex> lk(m.mu);
+    auto it = m.party_tickets.find(pid ? pid : "");
+    return it == m.party_tickets.end() ? 0 : (int32_t)it->second.size();
+}
+// membership in m.indexes
+int32_t mm_find_tickets(void* h, const char* const* ids, int32_t n, uint8_t* found) {
+    auto& m = *static_cast<Matchmaker*>(h);
+    std::lock_guard<std::mutex> lk(m.mu);
+    int32_t k = 0;
+    for (int32_t i = 0; i < n; i++) {
+        found[i] = m.indexes.count(ids[i] ? ids[i] : "") ? 1 : 0;
+        k += found[i];
+    }
+    return k;
+}
 int32_t mm_active_count(void* h) { auto& m = *static_cast<Matchmaker*>(h); std::lock_guard<std::mutex> lk(m.mu); return (int32_t)m.active_indexes.size(); }
 
 int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, double* scores_out, int32_t cap) {

@@ -123,7 +123,8 @@ def test_oracle_mutations_during_pass():
     remaining = {t for t, _ in state}
     gone = {t for g in groups for t, _ in g}
     assert not (gone & remaining)
-    assert gone <= set(removed)
+    # matched tickets are reported by the pass result, removals by the drain (ABI 4)
+    assert not (gone & set(removed))
 
 
 @pytest.mark.gpu

@@ -51,7 +51,7 @@ def test_header_symbols_exported(product):
         assert hasattr(harness.oracle_lib(), s), f"oracle does not export {s}"
     assert set(syms) == set(capi.EXPORTED_SYMBOLS)
     assert product.mm_backend_name() == b"hip-gfx950"
-    assert product.mm_abi_version() == 3
+    assert product.mm_abi_version() == 4
 
 
 def test_library_is_gfx950(product):

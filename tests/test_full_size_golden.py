@@ -28,18 +28,20 @@ NAMES = ["c2", "c3", "c4", "c5", "c5o"]
 
 def _golden(name):
     path = os.path.join(harness.GOLDEN, f"full_{name}.json")
+    # every BASELINE config's fixture is required: a missing one fails (a skip
+    # would let a green run hide an unpinned config)
     if not os.path.exists(path):
-        pytest.skip(f"{path} not generated (tools/make_full_golden.py {name})")
+        pytest.fail(f"{path} missing: generate it with tools/make_full_golden.py {name}")
     with open(path) as f:
         return json.load(f)
 
 
-def _product_pass(g):
+def _product_pass(g, multi=None):
     import nakama_amd
     lib = nakama_amd.load_library()
     kw = dict(g["matchmaker"])
     ts = synth.TicketSet(g["config"], g["tickets"])
-    mm = capi.Matchmaker(lib, override=(lambda c: c) if g["override"] else None, **kw)
+    mm = capi.Matchmaker(lib, override=(lambda c: c) if g["override"] else None, multi=multi, **kw)
     got = {}
     try:
         ts.insert_into(mm)
@@ -70,9 +72,9 @@ def _product_pass(g):
         ts.close()
 
 
-def _check(name):
+def _check(name, multi=None):
     g = _golden(name)
-    got = _product_pass(g)
+    got = _product_pass(g, multi)
     keys = ["groups", "entries", "matched_tickets", "remaining", "active", "groups_sha256", "state_sha256"]
     if g["override"]:
         keys += ["candidates", "candidate_entries", "candidates_sha256"]
@@ -93,3 +95,24 @@ def test_full_size_c3_host_paths(env, monkeypatch):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     _check("c3")
+
+
+POOL_FIELDS = {2: ["properties.region"], 3: ["properties.mode", "properties.region"],
+               4: ["properties.mode", "properties.region"], 5: ["properties.bucket"]}
+
+
+@pytest.mark.parametrize("name,mode", [("c4", "rows"), ("c4", "pools"), ("c3", "pools"), ("c5o", "pools")])
+def test_full_size_multi_handle(name, mode):
+    """The full-size passes through one multi-device handle (mm_create_multi,
+    two sub-handles on device 0): C4 in its BASELINE mode — row-sharded, the
+    hashed scan split by candidate chunks between the sub-handles and
+    exchanged through host memory, every sub-handle replaying — and with its
+    pools placed whole; C3 and C5 + override pool-sharded.  Same digests as
+    one oracle pass; C4 rows must run on mscan_hash_kernel (eval_kernel 4)."""
+    g = _golden(name)
+    m = dict(devices=[0, 0], pool_fields=POOL_FIELDS[g["config"]],
+             mode=capi.MM_MULTI_ROWS if mode == "rows" else capi.MM_MULTI_POOLS,
+             transport=capi.MM_MULTI_HOST)
+    got = _check(name, m)
+    if mode == "rows":
+        assert got["eval_kernel"] == 4

@@ -79,6 +79,33 @@ def test_multi_pools_default_pass_equals_one_handle(config, n, subs):
     assert _compare(config, n, 3, harness.oracle_lib(), n_subs=subs, max_intervals=3) == subs
 
 
+@pytest.mark.parametrize("config,n,subs", [(3, 3000, 3), (4, 3000, 4), (12, 900, 3)])
+def test_multi_pools_parallel_merge(config, n, subs, monkeypatch):
+    """The key-range parallel merge of the sub-handles' lists (forced at any
+    size): the same groups, in the same order, as one handle."""
+    monkeypatch.setenv("NKM_MERGE_MIN", "1")
+    assert _compare(config, n, 2, harness.oracle_lib(), n_subs=subs, max_intervals=3) == subs
+
+
+def test_multi_pools_parallel_merge_ties():
+    """Groups of different sub-handles whose searching tickets share a
+    CreatedAt are ordered by ticket id (the pinned active order); the
+    parallel merge keeps every tie inside one key range."""
+    def run(m):
+        for k in range(240):
+            mode = f"m{k % 3}"
+            for j in range(2):
+                _add(m, f"t{k:03d}-{j}", [f"s{k}-{j}"], query=f"+properties.mode:{mode}", props={"mode": mode},
+                     created=k // 6)
+        return m.Process()
+    import os
+    os.environ["NKM_MERGE_MIN"] = "1"
+    try:
+        _both(run)
+    finally:
+        del os.environ["NKM_MERGE_MIN"]
+
+
 def test_multi_pools_rev_precision():
     _compare(5, 1200, 2, harness.oracle_lib(), n_subs=3, max_intervals=2, rev_precision=True, rev_threshold=0)
 
@@ -198,6 +225,25 @@ def test_multi_drain_removed():
             return a, b, sorted({t for g in groups for t, _ in g})
         finally:
             ts.close()
+    _both(run)
+
+
+def test_multi_lookups_across_sub_handles():
+    """mm_session_ticket_count / mm_party_ticket_count / mm_find_tickets of the
+    multi handle (ABI 4) answer for every sub-handle: a session's and a
+    party's tickets in three pools, found wherever they live."""
+    def run(m):
+        modes = ["m0", "m1", "m2"]
+        for k in range(3):
+            _add(m, f"t{k}", ["s1"], query=f"+properties.mode:{modes[k]}", props={"mode": modes[k]}, created=k)
+            _add(m, f"p{k}", ["ps1", "ps2"], party="party1", query=f"+properties.mode:{modes[k]}",
+                 props={"mode": modes[k]}, created=10 + k)
+        out = [m.session_ticket_count("s1"), m.session_ticket_count("ps2"), m.party_ticket_count("party1"),
+               m.session_ticket_count("nobody"), m.party_ticket_count(""),
+               m.find_tickets(["t0", "t2", "p1", "zz", "t1"])]
+        m.RemoveSession("s1", "t2")
+        out += [m.session_ticket_count("s1"), m.find_tickets(["t2", "t0"])]
+        return out
     _both(run)
 
 
