@@ -330,35 +330,18 @@ struct PostingRange {
     uint32_t off = 0, len = 0, head = 0;  // head: first entry possibly alive
 };
 
+// Identity of a signature (the sig_idx_ hash): query kind, the searching
+// ticket's filters and the compiled clauses.
+uint64_t sig_clause_hash(const DClause* dc, size_t n);
+uint64_t sig_hash(uint64_t clause_hash, uint8_t kind, int32_t mn, int32_t mx, uint32_t party);
+
 // Builtin document fields (MapMatchmakerIndex, matchmaker.go:1026-1040).
 enum BuiltinField : uint16_t { F_TICKET = 0, F_MIN = 1, F_MAX = 2, F_PARTY = 3, F_CREATED = 4, F_NBUILTIN = 5 };
 
 
 // Matched (or candidate) groups of a pass as a flat CSR of (slot, presence
 // index) entries: group g = ents[off[g], off[g+1]).
-// std::allocator whose value-less construct() default-initialises, so
-// resize() of trivially constructible elements leaves them unwritten: the
-// pass's output arrays are filled in full by the parallel merges, and
-// std::vector's value-initialisation was a serial zero-fill of the whole
-// output ahead of them (C3: 21 MB per pass).
-template <class T>
-struct DefaultInitAlloc : std::allocator<T> {
-    template <class U>
-    struct rebind {
-        using other = DefaultInitAlloc<U>;
-    };
-    DefaultInitAlloc() = default;
-    template <class U>
-    DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
-    template <class U>
-    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
-        ::new ((void*)p) U;
-    }
-    template <class U, class... A>
-    void construct(U* p, A&&... a) {
-        ::new ((void*)p) U(std::forward<A>(a)...);
-    }
-};
+// (DefaultInitAlloc: strstore.h)
 template <class T>
 using UVec = std::vector<T, DefaultInitAlloc<T>>;
 
@@ -597,6 +580,14 @@ private:
     uint16_t prop_field(std::string_view key);
     uint16_t field_of(const std::string& name);
     uint32_t sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party);
+    static void sig_describe(Sig& s, const std::vector<DClause>& dc, const CompiledQuery& cq, int32_t mn, int32_t mx,
+                             uint32_t party);
+    uint32_t sig_commit(Sig&& s, const DClause* dc, size_t n, uint64_t hash, bool materialize);
+    bool sig_eq(uint32_t id, uint8_t kind, int32_t mn, int32_t mx, uint32_t party, const DClause* dc, size_t n) const;
+    void materialize_fields();
+    // Insert of a large batch on the host workers (mm_insert.cpp); false:
+    // the batch takes the per-ticket path (nothing was changed)
+    bool insert_bulk(const mm_ticket* ts, int32_t n, double* phase_ms);
     uint32_t termset_of(const HostClause& c);  // interned regexp/wildcard/fuzzy matcher
     void refresh_termsets();                   // extends accepted sets over new dictionary terms, uploads
     void set_field(uint16_t f, uint32_t slot, uint8_t kind, int64_t val);
@@ -670,6 +661,7 @@ private:
         uint64_t scanned = 0;
         double live_w = 0;   // sum over rows of src_len x the row's per-live-candidate bytes
     };
+    int bulk_mode_ = 1;      // NKM_BULK: 0 = Insert per ticket, 1 = batches of >= 4096 on the workers, 2 = any batch
     bool pack_mode_ = true;  // NKM_RPACK=0: RevPrecision batches search per row (rsmall / search_kernel)
     UVec<DSmallRow> pk_tmp_;
     PinnedArray<DSmallRow> h_srows_;
@@ -778,7 +770,7 @@ public:
     uint32_t n_live_ = 0;
 
     // ---- signatures / clauses ----
-    std::unordered_map<std::string, uint32_t> sig_index_;
+    HashIndex sig_idx_;  // signature identity (sig_hash) -> id, compared by sig_eq
     std::vector<Sig> sigs_;
     std::vector<uint64_t> sig_fmask_;  // per signature: its must_fmask (plan_pools reads 8 B, not the Sig)
     std::vector<DClause> clauses_;

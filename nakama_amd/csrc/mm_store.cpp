@@ -118,6 +118,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_PARTIAL")) partial_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_DEVENUM")) dev_enum_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_RPACK")) pack_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_BULK")) bulk_mode_ = std::strcmp(e, "0") == 0 ? 0 : std::strcmp(e, "force") == 0 ? 2 : 1;
     if (const char* e = std::getenv("NKM_KERNEL"))
         kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN
                      : !std::strcmp(e, "mscan") ? KM_MSCAN : KM_AUTO;
@@ -383,48 +384,28 @@ void Core::refresh_termsets() {
 }
 
 // Identity of a signature: query kind, the searching ticket's filters and the
-// compiled clauses (field / term ids, bounds, boosts).
-static std::string sig_key(uint8_t kind, int32_t mn, int32_t mx, uint32_t party, const DClause* dc, size_t n) {
-    std::string key;
-    key.reserve(16 + n * sizeof(DClause));
-    key.push_back((char)kind);
-    key.append((const char*)&mn, 4);
-    key.append((const char*)&mx, 4);
-    key.append((const char*)&party, 4);
-    if (n) key.append((const char*)dc, n * sizeof(DClause));
-    return key;
+// compiled clauses (field / term ids, bounds, boosts) — hashed here, compared
+// against the stored signature (sig_eq): the index keeps no key strings.
+uint64_t sig_clause_hash(const DClause* dc, size_t n) { return str_hash((const char*)dc, n * sizeof(DClause)); }
+uint64_t sig_hash(uint64_t clause_hash, uint8_t kind, int32_t mn, int32_t mx, uint32_t party) {
+    uint64_t h = clause_hash ^ ((uint64_t)kind << 56);
+    h = (h ^ (uint32_t)mn) * 0x9E3779B97F4A7C15ull;
+    h = (h ^ (uint32_t)mx) * 0xBF58476D1CE4E5B9ull;
+    h = (h ^ party) * 0x94D049BB133111EBull;
+    return h ^ (h >> 31);
+}
+bool Core::sig_eq(uint32_t id, uint8_t kind, int32_t mn, int32_t mx, uint32_t party, const DClause* dc, size_t n) const {
+    const Sig& g = sigs_[id];
+    return g.qkind == kind && g.tmin == mn && g.tmax == mx && g.tparty == party && g.n_clauses == n &&
+           (n == 0 || std::memcmp(clauses_.data() + g.clause_off, dc, n * sizeof(DClause)) == 0);
 }
 
-// Assigns (or reuses) the compiled signature of a ticket's search.
-uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party) {
-    std::vector<DClause> dc;
-    dc.reserve(cq.clauses.size());
-    for (auto& c : cq.clauses) {
-        DClause d{};
-        d.op = c.op;
-        d.occur = c.occur;
-        d.lo = c.lo;
-        d.hi = c.hi;
-        d.score = c.score;
-        d.field = 0;
-        d.term = 0;
-        if (c.op != OP_FALSE) {
-            d.field = field_of(c.field);
-            if (c.op == OP_TERM || c.op == OP_NUMLIT) d.term = dict_.intern(c.term);
-            else if (c.op == OP_TERMSET) d.term = termset_of(c);
-        }
-        dc.push_back(d);
-    }
-    // a fuzzy clause scores per accepted term: variable-score search, no score bound
-    bool fuzzy = false;
-    for (auto& c : cq.clauses)
-        if (c.op == OP_TERMSET && c.mt_kind == TermMatcher::K_FUZZY && c.occur != OCC_MUSTNOT) fuzzy = true;
-    std::string key = sig_key(cq.kind, mn, mx, party, dc.data(), dc.size());
-    auto it = sig_index_.find(key);
-    if (it != sig_index_.end()) return it->second;
-
-    Sig s;
-    s.clause_off = (uint32_t)clauses_.size();
+// A signature's descriptor from its compiled clauses (no store state is
+// touched: the bulk Insert runs it on the workers): score bound, variable
+// score, MUST terms, fields.  clause_off is set when it is committed.
+void Core::sig_describe(Sig& s, const std::vector<DClause>& dc, const CompiledQuery& cq, int32_t mn, int32_t mx,
+                        uint32_t party) {
+    s = Sig{};
     s.n_clauses = (uint16_t)dc.size();
     s.qkind = cq.kind;
     s.tmin = mn;
@@ -449,13 +430,11 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
                 else best_neg = std::max(best_neg, d.score);
             }
         }
-        if (d.op != OP_FALSE) {
-            field_used_[d.field] = 1;
-        }
     }
-    for (auto& mt : s.must_terms) {
-        if (!field_posting_[mt.first]) { field_posting_[mt.first] = 1; index_dirty_ = true; }
-    }
+    // a fuzzy clause scores per accepted term: variable-score search, no score bound
+    bool fuzzy = false;
+    for (auto& c : cq.clauses)
+        if (c.op == OP_TERMSET && c.mt_kind == TermMatcher::K_FUZZY && c.occur != OCC_MUSTNOT) fuzzy = true;
     s.var_score = cq.kind == QK_BOOL && !(n_should_live == 0 || (!has_must && n_should_live == 1));
     double S;
     if (cq.kind != QK_BOOL) S = 1.0;
@@ -469,18 +448,35 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
         s.var_score = true;
         s.ub_key = INT64_MAX;
     }
-    {
-        std::vector<uint16_t> fs;
-        for (auto& d : dc)
-            if (d.op != OP_FALSE && std::find(fs.begin(), fs.end(), d.field) == fs.end()) fs.push_back(d.field);
-        s.n_fields = (uint16_t)fs.size();
+    std::vector<uint16_t> fs;
+    for (auto& d : dc)
+        if (d.op != OP_FALSE && std::find(fs.begin(), fs.end(), d.field) == fs.end()) fs.push_back(d.field);
+    s.n_fields = (uint16_t)fs.size();
+}
+
+// Adds a described signature: its clauses, the fields it references (and
+// posting lists of its MUST terms), the index entry.  materialize: build the
+// dense host column of a field referenced for the first time now (the bulk
+// Insert does it once for the batch: materialize_fields).
+uint32_t Core::sig_commit(Sig&& s, const DClause* dc, size_t n, uint64_t hash, bool materialize) {
+    s.clause_off = (uint32_t)clauses_.size();
+    for (size_t k = 0; k < n; k++) {
+        if (dc[k].op != OP_FALSE) field_used_[dc[k].field] = 1;
+        clauses_.push_back(dc[k]);
     }
-    for (auto& d : dc) clauses_.push_back(d);
-    uint32_t id = (uint32_t)sigs_.size();
+    for (auto& mt : s.must_terms)
+        if (!field_posting_[mt.first]) { field_posting_[mt.first] = 1; index_dirty_ = true; }
+    const uint32_t id = (uint32_t)sigs_.size();
     sig_fmask_.push_back(s.must_fmask);
     sigs_.push_back(std::move(s));
-    sig_index_.emplace(std::move(key), id);
-    // fields referenced for the first time get a dense host column now
+    sig_idx_.put_new(hash, id);
+    if (materialize) materialize_fields();
+    return id;
+}
+
+// Fields referenced for the first time get a dense host column over the
+// existing slots.
+void Core::materialize_fields() {
     const size_t n = nslots();
     for (size_t f = 0; f < field_used_.size(); f++) {
         if (field_used_[f] && fval_[f].size() != n) {
@@ -509,7 +505,34 @@ uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t 
             dev_field_slots_[f] = 0;
         }
     }
-    return id;
+}
+
+// Assigns (or reuses) the compiled signature of a ticket's search.
+uint32_t Core::sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party) {
+    std::vector<DClause> dc;
+    dc.reserve(cq.clauses.size());
+    for (auto& c : cq.clauses) {
+        DClause d{};
+        d.op = c.op;
+        d.occur = c.occur;
+        d.lo = c.lo;
+        d.hi = c.hi;
+        d.score = c.score;
+        d.field = 0;
+        d.term = 0;
+        if (c.op != OP_FALSE) {
+            d.field = field_of(c.field);
+            if (c.op == OP_TERM || c.op == OP_NUMLIT) d.term = dict_.intern(c.term);
+            else if (c.op == OP_TERMSET) d.term = termset_of(c);
+        }
+        dc.push_back(d);
+    }
+    const uint64_t h = sig_hash(sig_clause_hash(dc.data(), dc.size()), cq.kind, mn, mx, party);
+    const int64_t f = sig_idx_.find(h, [&](uint32_t id) { return sig_eq(id, cq.kind, mn, mx, party, dc.data(), dc.size()); });
+    if (f >= 0) return (uint32_t)f;
+    Sig s;
+    sig_describe(s, dc, cq, mn, mx, party);
+    return sig_commit(std::move(s), dc.data(), dc.size(), h, true);
 }
 
 void Core::kill_slot(uint32_t s, bool device_cleared, bool quiet) {
@@ -884,16 +907,24 @@ int Core::insert(const mm_ticket* ts, int32_t n) {
     const auto t1 = clk::now();
     maybe_compact();
     const auto t2 = clk::now();
-    for (int i = 0; i < n; i++) {
-        const int64_t sg = sig_cached(ts[i]);
-        if (sg >= 0) add_locked(ts[i], (uint32_t)sg, true);
-    }
+    // a large batch on the host workers (mm_insert.cpp); NKM_BULK=0: always
+    // per ticket, =force: at any size (tests)
+    double ph[5] = {0, 0, 0, 0, 0};
+    const bool bulk = bulk_mode_ != 0 && par_mode_ && (bulk_mode_ == 2 || n >= 4096) && insert_bulk(ts, n, ph);
+    if (!bulk)
+        for (int i = 0; i < n; i++) {
+            const int64_t sg = sig_cached(ts[i]);
+            if (sg >= 0) add_locked(ts[i], (uint32_t)sg, true);
+        }
     const auto t3 = clk::now();
     if (n >= 1024) sync_device();  // index the batch now (bluge indexes synchronously too)
     if (std::getenv("NKM_PROFILE") && n >= 1024) {
         auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "[nkm] insert %d: compact %.1f ms | add (incl. compiles) %.1f ms | sync/index/upload %.1f ms\n", n,
-                     ms(t1, t2), ms(t2, t3), ms(t3, clk::now()));
+        std::fprintf(stderr,
+                     "[nkm] insert %d: compact %.1f ms | %s %.1f ms (ids %.1f, sigs %.1f, strings %.1f, columns %.1f, "
+                     "indexes %.1f) | sync/index/upload %.1f ms\n",
+                     n, ms(t1, t2), bulk ? "bulk add" : "add (incl. compiles)", ms(t2, t3), ph[0], ph[1], ph[2], ph[3],
+                     ph[4], ms(t3, clk::now()));
     }
     return MM_OK;
 }
@@ -1257,17 +1288,18 @@ void Core::compact() {
             g = smap[g];
             squery_[s].clause_off = ns[g].clause_off;
         }
-        std::unordered_map<std::string, uint32_t> nidx;
-        nidx.reserve(ns.size());
-        for (uint32_t g = 0; g < ns.size(); g++)
-            nidx.emplace(sig_key(ns[g].qkind, ns[g].tmin, ns[g].tmax, ns[g].tparty, nc.data() + ns[g].clause_off,
-                                 ns[g].n_clauses),
-                         g);
         sigs_.swap(ns);
         sig_fmask_.resize(sigs_.size());
         for (size_t g = 0; g < sigs_.size(); g++) sig_fmask_[g] = sigs_[g].must_fmask;
         clauses_.swap(nc);
-        sig_index_.swap(nidx);
+        sig_idx_.clear();
+        sig_idx_.reserve(sigs_.size());
+        for (uint32_t g = 0; g < sigs_.size(); g++) {
+            const Sig& x = sigs_[g];
+            sig_idx_.put_new(sig_hash(sig_clause_hash(clauses_.data() + x.clause_off, x.n_clauses), x.qkind, x.tmin,
+                                      x.tmax, x.tparty),
+                             g);
+        }
         dev_clauses_ = 0;
         qtext_.clear();  // the (query, counts) -> signature cache holds old ids
         qstatus_.clear();

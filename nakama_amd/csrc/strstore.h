@@ -13,13 +13,41 @@
 // and dropping a million dead tickets frees a handful of blocks.
 #pragma once
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <string>
 #include <string_view>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 namespace nkm {
+
+// std::allocator whose value-less construct() default-initialises, so
+// resize() of trivially constructible elements leaves them unwritten: the
+// pass's output arrays are filled in full by the parallel merges, and
+// std::vector's value-initialisation was a serial zero-fill of the whole
+// output ahead of them (C3: 21 MB per pass); the bulk Insert's cold records
+// likewise (C3 1M: ~400 MB).
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInitAlloc<U>;
+    };
+    DefaultInitAlloc() = default;
+    template <class U>
+    DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
 
 // 64-bit hash of a byte string (8 bytes per step, multiply-xorshift mixing).
 inline uint64_t str_hash(const char* p, size_t n) {
@@ -59,6 +87,14 @@ struct StrArena {
         p[s.size()] = 0;
         used += need;
         return p;
+    }
+    // A block of exactly `bytes` the caller fills (a bulk append: the
+    // Insert workers copy their strings into it in parallel); the next put()
+    // starts a new block.
+    char* block(size_t bytes) {
+        blocks.emplace_back(new char[std::max<size_t>(bytes, 1)]);
+        used = cap = std::max<size_t>(bytes, 1);
+        return blocks.back().get();
     }
     void clear() {
         blocks.clear();
@@ -107,6 +143,21 @@ struct HashIndex {
     // Inserts a key the caller knows is absent.
     void put_new(uint64_t h, uint32_t v) {
         put(h, v, [](uint32_t) { return false; });
+    }
+    // put_new from several threads at once: keys absent and pairwise
+    // distinct, capacity reserved beforehand (no rehash); each thread claims
+    // an empty word with a compare-exchange.  The caller adds the count to n
+    // after the threads are done.
+    void put_new_concurrent(uint64_t h, uint32_t v) {
+        const size_t mask = tab.size() - 1;
+        const uint32_t tag = (uint32_t)(h >> 32);
+        const uint64_t word = ((uint64_t)tag << 32) | (uint64_t)(v + 1);
+        for (size_t i = tag & mask;; i = (i + 1) & mask) {
+            uint64_t expect = 0;
+            if (__atomic_load_n(&tab[i], __ATOMIC_RELAXED) == 0 &&
+                __atomic_compare_exchange_n(&tab[i], &expect, word, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED))
+                return;
+        }
     }
     void reserve(size_t count) {
         size_t c = 16;
@@ -218,12 +269,12 @@ struct ColdView {
 };
 
 struct ColdStore {
-    std::vector<char> bytes;
+    std::vector<char, DefaultInitAlloc<char>> bytes;  // resized then written (bulk Insert): no zero-fill
     std::vector<uint64_t> off;  // per slot
     size_t size() const { return off.size(); }
 
     struct Writer {
-        std::vector<char>& b;
+        std::vector<char, DefaultInitAlloc<char>>& b;
         void u32(uint32_t v) {
             const size_t at = b.size();
             b.resize(at + 4);
@@ -266,7 +317,7 @@ struct ColdStore {
     }
     // Keeps the records of the slots where keep[s] (in slot order).
     void compact(const std::vector<uint8_t>& keep) {
-        std::vector<char> nb;
+        std::vector<char, DefaultInitAlloc<char>> nb;
         std::vector<uint64_t> no;
         size_t total = 0;
         for (uint32_t s = 0; s < off.size(); s++)

@@ -210,6 +210,61 @@ def test_datetime_props_and_date_ranges(kernel, monkeypatch):
     run_passes(8, 3000, 3, dict(max_intervals=3))
 
 
+@pytest.mark.parametrize("config,n,cfg", [(1, 3000, dict(max_intervals=2)), (2, 2500, dict(max_intervals=2)),
+                                          (3, 3000, dict(max_intervals=2)), (4, 3000, dict(max_intervals=2)),
+                                          (5, 2000, dict(max_intervals=2, rev_precision=True, rev_threshold=0)),
+                                          (6, 1500, dict(max_intervals=3)), (7, 1500, dict(max_intervals=2)),
+                                          (8, 2000, dict(max_intervals=3)), (10, 1500, dict(max_intervals=2)),
+                                          (13, 1500, dict(max_intervals=2, rev_precision=True, rev_threshold=0))])
+def test_bulk_insert(config, n, cfg, monkeypatch):
+    """Insert on the host workers (mm_insert.cpp), forced at small sizes:
+    parties, datetime-typed string properties, numeric and keyword fields,
+    regexp / wildcard / fuzzy clauses (their signatures made serially), wide
+    queries over builtin fields — passes and state equal to the oracle, and
+    the same hit lists as the per-ticket Insert."""
+    monkeypatch.setenv("NKM_BULK", "force")
+    run_passes(config, n, 2, cfg)
+    ts = synth.TicketSet(config, 400)
+    monkeypatch.setenv("NKM_BULK", "0")
+    ref = capi.Matchmaker(product_lib(), **cfg)
+    monkeypatch.setenv("NKM_BULK", "force")
+    blk = capi.Matchmaker(product_lib(), **cfg)
+    try:
+        ts.insert_into(ref)
+        ts.insert_into(blk)
+        assert state(blk) == state(ref)
+        for k in range(0, 400, 17):
+            t = ts.ticket_id(k)
+            assert blk.debug_hits(t) == ref.debug_hits(t)
+    finally:
+        ref.close()
+        blk.close()
+        ts.close()
+
+
+def test_bulk_insert_falls_back_on_known_ids(monkeypatch):
+    """A batch that re-inserts a known id (live, or a dead record a later
+    Insert must overwrite) or names one id twice takes the per-ticket path."""
+    monkeypatch.setenv("NKM_BULK", "force")
+    gpu, orc = pair(dict(max_intervals=3))
+    a, b = synth.TicketSet(6, 500), synth.TicketSet(6, 500, first=250)  # b overlaps a by 250 ids
+    try:
+        for mm in (gpu, orc):
+            a.insert_into(mm)
+            b.insert_into(mm)
+        assert state(gpu) == state(orc)
+        assert gpu.Process() == orc.Process()
+        for mm in (gpu, orc):
+            a.insert_into(mm)  # matched ids come back
+        assert state(gpu) == state(orc)
+        assert gpu.Process() == orc.Process()
+    finally:
+        gpu.close()
+        orc.close()
+        a.close()
+        b.close()
+
+
 def test_datetime_hit_lists():
     ts = synth.TicketSet(8, 600)
     gpu, orc = pair(dict(max_intervals=2))
