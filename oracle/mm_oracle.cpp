@@ -28,6 +28,7 @@
 #include "go_regexp.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <map>
@@ -69,9 +70,24 @@ struct Query {
     // RegexpQuery / WildcardQuery (term = pattern) and FuzzyQuery (term, fuzziness)
     std::shared_ptr<oracle_re::Regexp> re;
     int fuzziness = 0;
+    uint32_t fid = 0;  // field_id(field), set when the query is parsed (bind_fields)
 };
 
 static double boost_value(const Query& q) { return q.has_boost ? q.boost : 1.0; }
+
+// Field names interned to small ids (process-wide: handles share it), so a
+// document's fields are a short vector searched by id — the per-document
+// evaluation of every search reads no string map.
+static uint32_t field_id(const string& name) {
+    static std::mutex mu;
+    static std::unordered_map<string, uint32_t> ids;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = ids.find(name);
+    if (it != ids.end()) return it->second;
+    const uint32_t id = (uint32_t)ids.size();
+    ids.emplace(name, id);
+    return id;
+}
 
 // Field values of one indexed document (MapMatchmakerIndex, matchmaker.go:1026-1040).
 struct FieldVal {
@@ -79,7 +95,20 @@ struct FieldVal {
     string kw;
     int64_t num = 0;
 };
-using Doc = std::unordered_map<string, FieldVal>;
+struct Doc {
+    vector<std::pair<uint32_t, FieldVal>> f;  // by field id, each field once
+    const FieldVal* find(uint32_t fid) const {
+        for (auto& kv : f)
+            if (kv.first == fid) return &kv.second;
+        return nullptr;
+    }
+    void set(const string& name, FieldVal v) {
+        const uint32_t id = field_id(name);
+        for (auto& kv : f)
+            if (kv.first == id) { kv.second = std::move(v); return; }
+        f.push_back({id, std::move(v)});
+    }
+};
 
 struct EvalRes { bool match; double score; };
 
@@ -93,19 +122,19 @@ static EvalRes eval(const Query& q, const Doc& d) {
     case Q_UNSUPPORTED:
         return {false, 0.0};
     case Q_TERM: {    // TermSearcher + ConstantScorer(boost) (search_term.go, match_common.go:259)
-        auto it = d.find(q.field);
-        if (it != d.end() && it->second.kind == 1 && it->second.kw == q.term) return {true, boost_value(q)};
+        const FieldVal* it = d.find(q.fid);
+        if (it && it->kind == 1 && it->kw == q.term) return {true, boost_value(q)};
         return {false, 0.0};
     }
     case Q_REGEXP: {  // multi-term disjunction of TermSearchers(boost), one term per keyword doc
-        auto it = d.find(q.field);
-        if (it != d.end() && it->second.kind == 1 && q.re->matches(it->second.kw)) return {true, boost_value(q)};
+        const FieldVal* it = d.find(q.fid);
+        if (it && it->kind == 1 && q.re->matches(it->kw)) return {true, boost_value(q)};
         return {false, 0.0};
     }
     case Q_FUZZY: {   // FuzzySearcher: TermSearcher(boost * boostFromDistance) (search_fuzzy.go:99-126)
-        auto it = d.find(q.field);
-        if (it == d.end() || it->second.kind != 1) return {false, 0.0};
-        const string& t = it->second.kw;
+        const FieldVal* it = d.find(q.fid);
+        if (!it || it->kind != 1) return {false, 0.0};
+        const string& t = it->kw;
         int dist = oracle_re::osa(q.term, t);
         if (dist > q.fuzziness) return {false, 0.0};
         double tb = 1.0;
@@ -116,8 +145,8 @@ static EvalRes eval(const Query& q, const Doc& d) {
         return {true, boost_value(q) * tb};
     }
     case Q_RANGE: {   // NumericRangeSearcher: disjoint prefix-coded terms, one hit per doc
-        auto it = d.find(q.field);
-        if (it != d.end() && it->second.kind == 2 && it->second.num >= q.lo && it->second.num <= q.hi)
+        const FieldVal* it = d.find(q.fid);
+        if (it && it->kind == 2 && it->num >= q.lo && it->num <= q.hi)
             return {true, q.const_score};
         return {false, 0.0};
     }
@@ -511,6 +540,12 @@ struct Parser {
     }
 };
 
+static void bind_fields(Query& q) {
+    q.fid = field_id(q.field);
+    for (auto* v : {&q.must, &q.should, &q.mustnot})
+        for (auto& c : *v) bind_fields(*c);
+}
+
 // ParseQueryString (server/match_common.go:244-251 + query_string_parser.go:92-103).
 // Returns 0 ok, MM_ERR_QUERY_INVALID, MM_ERR_UNSUPPORTED.
 static int parse_query(const string& query, QP* out) {
@@ -534,6 +569,7 @@ static int parse_query(const string& query, QP* out) {
             q = std::make_shared<Query>();
             q->kind = Q_MATCHNONE;
         }
+        bind_fields(*q);
         *out = q;
         return 0;
     } catch (const Unsupported&) {
@@ -562,6 +598,7 @@ struct Index {  // MatchmakerIndex (matchmaker.go:88-108)
     QP parsed;
     vector<Presence> entries;
     Doc doc;
+    uint64_t selected_in = 0;  // processDefault's `selected` set: the pass (process_default's serial) that selected it
 };
 using IP = std::shared_ptr<Index>;
 
@@ -615,11 +652,11 @@ static void bluge_update(Matchmaker& m, const IP& idx) {  // Writer.Update / Bat
 // match_common.go:78-212).  Numeric props win on key clash (matchmaker.go:460-466).
 static void build_doc(Index& ix) {
     Doc d;
-    d["ticket"] = FieldVal{1, ix.ticket, 0};
-    d["min_count"] = FieldVal{2, "", f2i((double)ix.min_count)};
-    d["max_count"] = FieldVal{2, "", f2i((double)ix.max_count)};
-    d["party_id"] = FieldVal{1, ix.party_id, 0};
-    d["created_at"] = FieldVal{2, "", f2i((double)ix.created_at)};
+    d.set("ticket", FieldVal{1, ix.ticket, 0});
+    d.set("min_count", FieldVal{2, "", f2i((double)ix.min_count)});
+    d.set("max_count", FieldVal{2, "", f2i((double)ix.max_count)});
+    d.set("party_id", FieldVal{1, ix.party_id, 0});
+    d.set("created_at", FieldVal{2, "", f2i((double)ix.created_at)});
     std::map<string, FieldVal> props;
     for (auto& kv : ix.sprops) {
         int64_t ns;
@@ -627,7 +664,7 @@ static void build_doc(Index& ix) {
         else props[kv.first] = FieldVal{1, kv.second, 0};
     }
     for (auto& kv : ix.nprops) props[kv.first] = FieldVal{2, "", f2i(kv.second)};
-    for (auto& kv : props) d["properties." + kv.first] = kv.second;
+    for (auto& kv : props) d.set("properties." + kv.first, kv.second);
     ix.doc = std::move(d);
 }
 
@@ -660,6 +697,48 @@ static vector<Hit> search_hits(Matchmaker& m, const Index& T) {
         return a.docnum < b.docnum;
     });
     return hits;
+}
+
+// The same hits for processDefault's walk, which reads them in order and
+// usually stops after a few: the hits that are not the searching ticket and
+// not selected earlier in the pass (matchmaker_process.go:112-126) are kept
+// as a heap under the same total order (score desc, created_at asc, doc
+// order) and popped one at a time — the sequence std::sort would give, at
+// O(n + k log n) for k hits read instead of O(n log n) (a 62,500-ticket C4
+// pool pass: 31k searches over 62.5k documents each).
+struct LazyHit { Index* idx; int64_t skey; int64_t ckey; uint64_t docnum; };
+static bool lazy_before(const LazyHit& a, const LazyHit& b) {
+    if (a.skey != b.skey) return a.skey > b.skey;
+    if (a.ckey != b.ckey) return a.ckey < b.ckey;
+    return a.docnum < b.docnum;
+}
+struct LazyHits {
+    vector<LazyHit> h;
+    size_t n = 0, taken = 0;
+    static bool heap_less(const LazyHit& a, const LazyHit& b) { return lazy_before(b, a); }
+    void build() {
+        n = h.size();
+        std::make_heap(h.begin(), h.end(), heap_less);
+    }
+    size_t size() const { return n; }
+    // the next hit in sorted order (call at most size() times)
+    const LazyHit& next() {
+        std::pop_heap(h.begin(), h.begin() + (n - taken), heap_less);
+        taken++;
+        return h[n - taken];
+    }
+};
+static void search_hits_walk(Matchmaker& m, const Index& T, uint64_t pass, LazyHits& out) {
+    out.h.clear();
+    out.taken = 0;
+    for (auto& bd : m.bluge) {
+        if (!bd.alive) continue;
+        Index* H = bd.idx.get();
+        if (H == &T || H->selected_in == pass) continue;  // self: the same MatchmakerIndex
+        double s;
+        if (eval_search(T, *H, &s)) out.h.push_back({H, f2i(s), f2i((double)H->created_at), bd.docnum});
+    }
+    out.build();
 }
 
 // validateMatch (matchmaker.go:1042-1068): to's document must match from's parsed query.
@@ -730,34 +809,32 @@ static vector<IP> active_order(Matchmaker& m) {  // pin: (CreatedAt, Ticket)
 static void process_default(Matchmaker& m, const vector<IP>& order,
                             const std::unordered_map<string, IP>& indexes_copy,
                             vector<vector<Entry>>& matched, vector<string>& expired, int64_t* pair_evals) {
-    std::unordered_set<string> selected;
+    // `selected` (a set of ticket ids): Index::selected_in == this pass
+    static std::atomic<uint64_t> pass_serial{0};
+    const uint64_t pass = ++pass_serial;
+    auto selected = [&](const Index* ix) { return ix->selected_in == pass; };
     const int max_intervals = m.cfg.max_intervals;
     // RevThreshold timer (matchmaker.go:244-248, matchmaker_process.go:31-46)
     RevThresholdTimer timer(m);
     bool threshold = false;
+    LazyHits h2;
     for (const IP& ai : order) {
         if (!threshold && timer.fired()) threshold = true;
         const bool rev = m.cfg.rev_precision != 0 && !threshold;  // :139, :178
         const string& ticket = ai->ticket;
-        if (selected.count(ticket)) continue;
+        if (selected(ai.get())) continue;
         ai->intervals++;
         bool last_interval = ai->intervals >= max_intervals || ai->min_count == ai->max_count;
         if (last_interval) expired.push_back(ticket);
         if (!m.active) continue;
 
-        vector<Hit> hits = search_hits(m, *ai);
+        // the hits, minus self and the already-selected (matchmaker_process.go:112-126)
+        search_hits_walk(m, *ai, pass, h2);
         *pair_evals += (int64_t)m.bluge_pos.size();
-        // drop self and already-selected (matchmaker_process.go:112-126)
-        vector<Hit> h2;
-        for (auto& h : hits) {
-            if (h.idx->ticket == ticket) continue;
-            if (selected.count(h.idx->ticket)) continue;
-            h2.push_back(h);
-        }
         vector<vector<Entry>> combos;
         int last_hit_counter = (int)h2.size() - 1;
         for (int hit_counter = 0; hit_counter < (int)h2.size(); hit_counter++) {
-            const string& hid = h2[hit_counter].idx->ticket;
+            const string& hid = h2.next().idx->ticket;
             auto hi_it = indexes_copy.find(hid);
             if (hi_it == indexes_copy.end()) continue;  // missing index
             const IP& hit = hi_it->second;
@@ -843,8 +920,8 @@ static void process_default(Matchmaker& m, const vector<IP>& order,
                 for (int k = 0; k < (int)ai->entries.size(); k++) current.push_back({ai, k});
                 combos.erase(combos.begin() + found_idx);
                 for (auto& e : current) {
-                    if (selected.count(e.idx->ticket)) continue;
-                    selected.insert(e.idx->ticket);
+                    if (selected(e.idx.get())) continue;
+                    e.idx->selected_in = pass;
                     bluge_delete(m, e.idx->ticket);   // synchronous batch delete (:306-321)
                 }
                 matched.push_back(std::move(current));
