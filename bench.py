@@ -61,10 +61,6 @@ POOL_FIELDS = {1: ("properties.mode", "properties.region"), 3: ("properties.mode
 DEFAULT_TICKETS = {1: 10_000, 2: 100_000, 4: 4_000_000}
 STRONG = (4, 5, 11)               # configs whose ticket count is the whole job's
 REV = (5, 11)                     # RevPrecision configs
-# full oracle passes measured offline (tools/make_full_golden.py: every pool's
-# whole pass, pools concurrently), the calibration of the live extrapolations
-FULL_CPU = {3: os.path.join(ROOT, "profiles", "r03_cpu_full_c3.json"),
-            4: os.path.join(ROOT, "profiles", "r03_cpu_full_c4.json")}
 
 
 def parse():
@@ -176,14 +172,12 @@ def cpu_baseline(args, searches, matched):
     (the reference Go/bluge path cannot run: no Go toolchain),
     bounded to ~10-30 s of CPU: tools/cpu_baseline.py in a child process
     (this process has initialised the GPU; the child never touches it).
-    `value`: per-pool passes on one core — the cost class of bluge's
-    posting-driven search, each search visiting its own pool — timed as
-    concurrent prefixes of every pool and extrapolated (EXTRAPOLATED);
-    `all_cores`: the same pools on all cores concurrently; `full_index`: one
-    core scanning the whole index per search, the oracle's own algorithm
-    class (a lower bound on the reference); `measured_full_pass`: whole
-    per-pool oracle passes measured offline (not extrapolated) on the named
-    CPU, for calibration."""
+    C3/C4: every pool's per-search cost (a * documents visited + b * hits)
+    measured from two short prefixes of its own pass, all pools concurrently,
+    extrapolated to the pool's pass; C5: whole 1000-ticket chunk passes timed
+    and scaled by the chunk count.  `measured_full_pass`: whole per-pool
+    passes of the same oracle timed offline (tools/make_full_golden.py), and
+    `calibration`: the model against them (profiles/r04_cpu_calib_*.json)."""
     import subprocess
     cmd = [sys.executable, os.path.join(ROOT, "tools", "cpu_baseline.py"), "--config", str(args.config),
            "--tickets", str(args.tickets), "--searches", str(searches), "--matched", str(matched)]
@@ -192,22 +186,15 @@ def cpu_baseline(args, searches, matched):
         return {"value": None, "unit": "tickets/s", "cores": 1, "kind": "port",
                 "sample": "cpu_baseline.py failed: " + r.stderr[-300:]}
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    fi = d["full_index"]
-    if "per_pool" in d:
-        pp = d["per_pool"]
-        out = {"value": pp["value_one_core"], "unit": "tickets/s", "cores": 1, "kind": "port",
-               "sample": pp["sample"] + f"; one-core time {pp['sum_pool_pass_s']:.0f} s",
-               "all_cores": {"value": pp["value_all_cores"], "cores": pp["cores"],
-                             "note": f"the slowest pool's extrapolated pass, {pp['parallel_pass_s']:.0f} s; timed "
-                                     f"concurrently ({pp['timed_wall_s']:.1f} s of wall)"}}
-    else:
-        out = {"value": fi["value"], "unit": "tickets/s", "cores": 1, "kind": "port", "sample": fi["sample"]}
-    out["full_index"] = {"value": fi["value"], "cores": 1, "sample": fi["sample"]}
-    out["algorithm"] = d["algorithm"]
-    out["host"] = d["host"]
-    full = FULL_CPU.get(args.config)
-    if full and os.path.exists(full) and args.tickets == json.load(open(full)).get("tickets"):
+    out = {"value": d["value"], "unit": "tickets/s", "cores": d["cores"], "kind": "port", "sample": d["sample"],
+           "all_cores": d.get("all_cores"), "algorithm": d["algorithm"], "host": d["host"]}
+    name = f"c{args.config}"
+    full = os.path.join(ROOT, "profiles", f"r04_cpu_full_{name}.json")
+    if os.path.exists(full) and args.tickets == json.load(open(full)).get("tickets"):
         out["measured_full_pass"] = json.load(open(full))
+    calib = os.path.join(ROOT, "profiles", f"r04_cpu_calib_{name}.json")
+    if os.path.exists(calib) and args.tickets == json.load(open(calib)).get("tickets"):
+        out["calibration"] = json.load(open(calib))["model_over_measured"]
     return out
 
 

@@ -144,6 +144,9 @@ struct Sig {
     uint16_t n_fields = 0;  // distinct field columns the clauses read
     std::vector<std::pair<uint16_t, uint32_t>> must_terms;  // candidate posting lists
     uint64_t must_fmask = 0;  // bit f: a MUST keyword term on field f (f >= 63: bit 63)
+    // every clause score is a multiple of 2^-20 below 2^20 in magnitude: any
+    // sum of them is exact in double, whatever the order (top-tier lists)
+    bool exact_scores = false;
 };
 
 // Persistent host workers for the pass's data-parallel host phases (pool
@@ -407,6 +410,7 @@ struct RevTimer {
 
 struct PassStats {
     int full_lists = 0;  // variable-score searches run as full lists (host-sorted)
+    int tier_lists = 0;  // variable-score searches run as top-tier lists (search_kernel path 2)
     // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel
     double k_ms[4] = {0, 0, 0, 0};      // HIP-event time of the launches
     bool mhash = false;                 // a batch's mscan ran hashed (mscan_hash_kernel)
@@ -661,6 +665,7 @@ private:
         uint64_t scanned = 0;
         double live_w = 0;   // sum over rows of src_len x the row's per-live-candidate bytes
     };
+    bool tier_mode_ = true;  // NKM_TIER=0: variable-score searches never return top-tier lists
     int bulk_mode_ = 1;      // NKM_BULK: 0 = Insert per ticket, 1 = batches of >= 4096 on the workers, 2 = any batch
     bool pack_mode_ = true;  // NKM_RPACK=0: RevPrecision batches search per row (rsmall / search_kernel)
     UVec<DSmallRow> pk_tmp_;

@@ -73,7 +73,10 @@ struct DGroup {
     uint32_t src_off;
     uint32_t src_len;
     uint32_t k;            // max entries to emit
-    uint32_t path;         // 0: search_kernel; 1: rsmall_kernel (a short source, one wave per row)
+    uint32_t path;         // 0: search_kernel; 1: rsmall_kernel (a short source, one wave per row);
+                           // 2: a variable-score search as a top-tier list: search_kernel<0>
+                           //    compacts its hits scoring ub_key in source order, then
+                           //    search_kernel<kVarK> appends the top-K of the rest if room is left
     uint64_t out_off;      // first output entry
     int64_t ub_key;        // sortable key of an upper bound of any score (early exit)
     int64_t cur_key;       // pagination cursor: emit only entries after (cur_key, cur_idx)

@@ -145,8 +145,13 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     __shared__ uint32_t tslot[kBlock];
     __shared__ uint8_t trev[kBlock];
 
-    const DGroup g = groups[blockIdx.x];
-    if ((g.var_score != 0) != (VK > 0) || g.path != 0) return;  // another instantiation's / kernel's search
+    DGroup g = groups[blockIdx.x];
+    // path 2: a top-tier list.  The constant-score instantiation (launched
+    // first) compacts the hits scoring exactly ub_key in source order; the
+    // variable-score one then appends, when that tier ended before the
+    // capacity, the top-K of the hits scoring below it (see below).
+    const bool tier = g.path == 2;
+    if (tier ? false : ((g.var_score != 0) != (VK > 0) || g.path != 0)) return;  // another instantiation's / kernel's search
     const uint32_t* src = g.src_kind == 0 ? st.order : st.postings;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     if (tid == 0) s_live = 0;
     __syncthreads();
 
-    if (!g.var_score) {
+    if (VK == 0) {
         // ---- ordered compaction -------------------------------------------------
         uint32_t count = 0;
         uint32_t base = 0;
@@ -164,6 +169,13 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
         for (; base < g.src_len; base += kBlock) {
             Cand c = eval_candidate(st, g, src, base + tid);
             my_live += c.live;
+            // A variable-score search's list is sorted by (score desc, source
+            // position asc): its hits scoring the top score ub_key come first,
+            // in source order, so compacting only those gives an exact prefix
+            // of the sorted list of any length (the LDS top-K stops at kVarK).
+            // The host takes this path only when every clause score sums
+            // exactly in any order (ub_key is then the top tier's exact key).
+            if (tier) c.m = c.m && c.key == g.ub_key;
             const uint64_t mask = __ballot(c.m);
             if (lane == 0) wave_cnt[wave] = (uint32_t)__popcll(mask);
             __syncthreads();
@@ -187,14 +199,29 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
         atomicAdd(&s_live, my_live);
         __syncthreads();
         if (tid == 0) {
-            res[blockIdx.x] = DGroupResult{count < K ? count : K, stopped ? 0u : 1u,
+            // a top-tier list is never complete: lower-scoring hits may follow
+            res[blockIdx.x] = DGroupResult{count < K ? count : K, stopped || tier ? 0u : 1u,
                                            base < g.src_len ? base : g.src_len, count, s_live, 0u};
         }
         return;
     }
 
     // ---- variable-score top-K ------------------------------------------------------
-    const uint32_t KK = K < (uint32_t)VK ? K : (uint32_t)VK;
+    // A top-tier list's tail: the hits scoring below ub_key (a cursor at
+    // (ub_key, past every position)), at most the capacity left, written
+    // after the tier; nothing when the tier filled the list (it is cut there).
+    DGroupResult r0{0, 0, 0, 0, 0, 0};
+    uint32_t K_avail = K;
+    if (tier) {
+        r0 = res[blockIdx.x];
+        if (r0.count >= K) return;
+        K_avail = K - r0.count;
+        g.has_cursor = 1;
+        g.cur_key = g.ub_key;
+        g.cur_idx = 0xFFFFFFFFu;
+        g.out_off += r0.count;
+    }
+    const uint32_t KK = K_avail < (uint32_t)VK ? K_avail : (uint32_t)VK;
     uint32_t n = 0, total = 0;
     int cur = 0;
     bool early = false;
@@ -264,7 +291,9 @@ __global__ __launch_bounds__(kBlock) void search_kernel(DStore st, const DGroup*
     __syncthreads();
     if (tid == 0) {
         const bool complete = !early && total <= KK;
-        res[blockIdx.x] = DGroupResult{n, complete ? 1u : 0u, base < g.src_len ? base : g.src_len, total, s_live, 0u};
+        const uint32_t scanned = base < g.src_len ? base : g.src_len;
+        res[blockIdx.x] = DGroupResult{r0.count + n, complete ? 1u : 0u, scanned > r0.scanned ? scanned : r0.scanned,
+                                       r0.matched + total, r0.live + s_live, 0u};
     }
 }
 
@@ -1426,7 +1455,34 @@ __global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRo
     bool m = false, live = false, rv = false;
     uint32_t s = kNoSlot;
     int64_t key = 0;
-    if (have && (uint32_t)j < len) {
+    // A square wave (S = 8: C5's buckets): its 8 rows search one common
+    // source of 8 entries that ARE the rows, in order.  Every check of the
+    // wave — forward Q_row(doc), reverse Q_entry(doc_row), pair matrix
+    // Q_entry(doc_other) — is then an entry of the 8 x 8 matrix
+    // E[a][b] = Q_{member a}(doc of member b), and lane (a, b) computes exactly
+    // E[a][b] as its forward evaluation: one ballot hands the matrix to every
+    // lane, instead of up to 1 + 1 + 8 evaluations (and their dependent
+    // clause and column gathers) per lane.
+    bool square = false;
+    if constexpr (S == 8) {
+        const uint32_t off0 = __shfl(d.src_off, 0), len0 = __shfl(d.src_len, 0);
+        uint32_t s_sq = kNoSlot;
+        if (have && (uint32_t)j < len) s_sq = ((d.src_len & kSrcOrder) ? st.order : st.postings)[d.src_off + j];
+        const uint32_t row_j = __shfl(d.slot, j * S);  // the slot of the row whose segment is j
+        square = __ballot(have && d.src_off == off0 && d.src_len == len0 && len == (uint32_t)S && s_sq == row_j) == ~0ull;
+    }
+    uint64_t Ebits = 0;
+    if (square) {
+        s = ((d.src_len & kSrcOrder) ? st.order : st.postings)[d.src_off + j];
+        live = st.alive[s] != 0;
+        const DQuery q = st.squery[d.slot];
+        double sp = 0.0;
+        const bool e = eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, s, &sp);
+        Ebits = __ballot(e);  // bit a * 8 + b: member a's query matches member b's document
+        m = live && e && st.minc[s] >= st.minc[d.slot] && st.maxc[s] <= st.maxc[d.slot];
+        if (m) key = dsortable((sp + 1.0) + 1.0);
+        rv = m && ((Ebits >> (j * S + seg)) & 1);
+    } else if (have && (uint32_t)j < len) {
         s = ((d.src_len & kSrcOrder) ? st.order : st.postings)[d.src_off + j];
         live = st.alive[s] != 0;
         if (live) {
@@ -1454,16 +1510,27 @@ __global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRo
     }
     PmT pmask = 0;
     RvT rbits = 0;
-    const DQuery q = m ? st.squery[s] : DQuery{0u, 0, 0, 0};
-    for (int i = 0; i < S; i++) {
-        const uint32_t si = (uint32_t)__shfl((int)s, base + i);
-        const uint32_t ri = (uint32_t)__shfl((int)rank, base + i);
-        const int rvi = __shfl((int)rv, base + i);
-        if (!((mine >> i) & 1)) continue;  // segment-uniform: the shuffles above ran on every lane
-        if (rvi) rbits |= (RvT)((RvT)1 << ri);
-        if (m && rank < (uint32_t)P && ri < (uint32_t)P) {
-            double dd;
-            if (eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, si, &dd)) pmask |= (PmT)((PmT)1 << ri);
+    if (square) {
+        for (int i = 0; i < S; i++) {
+            const uint32_t ri = (uint32_t)__shfl((int)rank, base + i);
+            const int rvi = __shfl((int)rv, base + i);
+            if (!((mine >> i) & 1)) continue;
+            if (rvi) rbits |= (RvT)((RvT)1 << ri);
+            // entry j's query against entry i's document: E[j][i]
+            if (m && rank < (uint32_t)P && ri < (uint32_t)P && ((Ebits >> (j * S + i)) & 1)) pmask |= (PmT)((PmT)1 << ri);
+        }
+    } else {
+        const DQuery q = m ? st.squery[s] : DQuery{0u, 0, 0, 0};
+        for (int i = 0; i < S; i++) {
+            const uint32_t si = (uint32_t)__shfl((int)s, base + i);
+            const uint32_t ri = (uint32_t)__shfl((int)rank, base + i);
+            const int rvi = __shfl((int)rv, base + i);
+            if (!((mine >> i) & 1)) continue;  // segment-uniform: the shuffles above ran on every lane
+            if (rvi) rbits |= (RvT)((RvT)1 << ri);
+            if (m && rank < (uint32_t)P && ri < (uint32_t)P) {
+                double dd;
+                if (eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, si, &dd)) pmask |= (PmT)((PmT)1 << ri);
+            }
         }
     }
     uint32_t* __restrict__ o_slot = reinterpret_cast<uint32_t*>(obuf + L.slot);

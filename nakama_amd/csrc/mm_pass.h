@@ -41,6 +41,7 @@ inline void filter_slots(WorkPool* wp, const std::vector<uint32_t>& in, std::vec
 }
 constexpr uint64_t kOutCap = 1ull << 24;  // max hit entries per batch (16M x 16 B)
 constexpr uint32_t kFullVarMax = 16384;   // max source of a full-list variable-score search
+constexpr uint64_t kTierMax = 16384;      // max entries of a top-tier list (search_kernel path 2)
 
 
 }  // namespace nkm

@@ -411,6 +411,26 @@ struct Replay : ReplayCore {
         // A large RevPrecision batch (every search whole: no chunks, full
         // lists or promotions) builds its descriptors on the workers.
         const bool par_lg = rev && c.par_mode_ && m_list.empty() && bg.size() >= c.par_min(65536);
+        // Top-tier lists (search_kernel path 2) for the variable-score
+        // searches whose scores sum exactly: an exact list prefix of any
+        // length, so the rows of a large batch reach their partners without
+        // running off a 512-entry top-K list and restarting the batch (C2:
+        // 11 batches).  The searches share what the batch budget leaves (half
+        // of kOutCap), up to kTierMax entries each; the row a list stopped is
+        // re-searched with every tier (retry).
+        const auto tier_ok = [&](const BGroup& g) {
+            return c.tier_mode_ && !rev && g.d.var_score && !g.d.has_cursor && !g.retry && g.d.ub_key != INT64_MAX &&
+                   c.sigs_[g.sig].exact_scores && g.d.src_len > 0;
+        };
+        uint64_t tier_share = 0;
+        if (!par_lg && c.tier_mode_ && !rev) {
+            uint64_t n_tier = 0, other = 0;
+            for (const BGroup& g : bg) {
+                if (tier_ok(g)) n_tier++;
+                else other += g.d.k;
+            }
+            if (n_tier && other < kOutCap / 2) tier_share = std::min<uint64_t>(kTierMax, (kOutCap * 7 / 8 - other) / n_tier);
+        }
         if (par_lg) {
             WorkPool& wp = c.workers();
             const size_t nb = bg.size(), nch = (size_t)wp.size() * 4;
@@ -482,6 +502,12 @@ struct Replay : ReplayCore {
                 budget + (d.src_len - d.k) <= kOutCap / 4) {
                 budget += d.src_len - d.k;
                 w.k = d.src_len;
+            }
+            if (w.path == 0 && w.var_score && tier_share > d.k && tier_ok(bg[i])) {
+                w.path = 2;  // var_score stays set: both search_kernel instantiations take part
+                w.k = (uint32_t)std::min<uint64_t>(tier_share, d.src_len);
+                budget += w.k - std::min<uint64_t>(w.k, d.k);
+                stats.tier_lists++;
             }
             w.out_off = off;
             off += w.k;
@@ -635,7 +661,7 @@ struct Replay : ReplayCore {
                 int k = 0;
                 size_t m = 0;
                 for (size_t i = b0 + nblk * ch / nch; i < b0 + nblk * (ch + 1) / nch; i++) {
-                    k |= lg[i].var_score ? 2 : 1;
+                    k |= lg[i].path == 2 ? 3 : lg[i].var_score ? 2 : 1;
                     m += lg[i].path == 1;
                 }
                 ck[ch] = k;
@@ -652,7 +678,7 @@ struct Replay : ReplayCore {
                     if (lg[i].path == 1) small[o++] = (uint32_t)i;
             });
         } else {
-            for (int i = b0; i < b1; i++) kinds |= lg[i].var_score ? 2 : 1;
+            for (int i = b0; i < b1; i++) kinds |= lg[i].path == 2 ? 3 : lg[i].var_score ? 2 : 1;
             for (int i = b0; i < b1; i++)
                 if (lg[i].path == 1) small.push_back((uint32_t)i);
         }
@@ -1135,16 +1161,39 @@ int Core::process_default(GroupList& out_groups,
         // Parallel assembly (same batch as the serial loop below): chunks of
         // the rows count their signatures, groups are numbered in first-
         // appearance order, and each search's capacity is the serial loop's
-        // final value.  Taken only when the batch is all remaining rows, i.e.
-        // when even an upper bound of the serial loop's running capacity
-        // total stays within kOutCap (so it would not have cut the batch).
+        // final value.  The batch is the remaining rows up to the window
+        // (the first `win` undecided rows: a per-chunk count finds the cut);
+        // taken only when even an upper bound of the serial loop's running
+        // capacity total stays within kOutCap (so it would not have cut the
+        // batch earlier).
+        size_t q_par = rows.size();  // the batch's end in rows (the serial loop's q)
         auto assemble_parallel = [&]() -> bool {
-            const size_t nr = rows.size() - pos, nsig = sigs_.size();
-            if (rev || retry_slot != kNoSlot || !par_mode_ || nr < par_min(65536) || nr > kMaxBatchRows || nsig > 4096 ||
-                nr > win)
-                return false;
+            size_t nr = rows.size() - pos;
+            const size_t nsig = sigs_.size();
+            if (rev || !par_mode_ || nr < par_min(65536) || nsig > 65536) return false;
+            // the row a list stopped is the batch's first undecided row (the
+            // rows before it were decided): its search returns every tier
+            if (retry_slot != kNoSlot && (sel[rows[pos]] | dec[rows[pos]] || rows[pos] != retry_slot)) return false;
             WorkPool& wp = workers();
             const unsigned nch = wp.size();
+            q_par = rows.size();
+            if (nr > win || nr > kMaxBatchRows) {  // the window's cut: the row after its win-th undecided row
+                const size_t cap = std::min<size_t>(win, kMaxBatchRows);
+                std::vector<size_t> und(nch, 0);
+                wp.run(nch, [&](size_t c) {
+                    size_t k = 0;
+                    for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) k += !(sel[rows[i]] | dec[rows[i]]);
+                    und[c] = k;
+                });
+                size_t seen = 0;
+                for (unsigned c = 0; c < nch && q_par == rows.size(); c++) {
+                    if (seen + und[c] < cap) { seen += und[c]; continue; }
+                    for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++)
+                        if (!(sel[rows[i]] | dec[rows[i]]) && ++seen == cap) { q_par = i + 1; break; }
+                }
+                nr = q_par - pos;
+                if (nr < par_min(65536)) return false;
+            }
             struct Chunk {
                 std::vector<uint32_t> first, cnt;
                 std::vector<int32_t> lastm, maxm;
@@ -1185,7 +1234,11 @@ int Core::process_default(GroupList& out_groups,
                     }
                 g.nrows = (uint32_t)nrows;
                 g.d.k = cap_k(g, nrows, lastm);
-                bound += cap_k(g, nrows, maxm);
+                if (retry_slot != kNoSlot && g.sig == sig_[retry_slot]) {  // the serial loop's retry capacity
+                    g.retry = true;
+                    if (nrows == 1) g.d.k = g.d.var_score ? kvar : std::max<uint32_t>(g.d.src_len, 1);
+                }
+                bound += std::max<uint64_t>(cap_k(g, nrows, maxm), g.d.k);
             }
             if (bound > kOutCap) {  // the serial loop may cut this batch: let it
                 for (auto& g : bg) sig_group[g.sig] = -1;
@@ -1278,6 +1331,7 @@ int Core::process_default(GroupList& out_groups,
         if (assemble_parallel_rev()) {
             q = rows.size();
         } else if (!(par_asm = assemble_parallel())) {
+            q_par = rows.size();
             uint64_t total_k = 0;
             for (; q < rows.size() && brow.size() < kMaxBatchRows && brow.size() < win; q++) {
                 const uint32_t r = rows[q];
@@ -1291,7 +1345,10 @@ int Core::process_default(GroupList& out_groups,
                 BGroup& g = bg[gi];
                 g.nrows++;
                 uint32_t k = cap_k(g, g.nrows, maxc_[r]);
-                if (r == retry_slot) k = g.d.var_score ? kvar : std::max<uint32_t>(g.d.src_len, 1);
+                if (r == retry_slot) {
+                    k = g.d.var_score ? kvar : std::max<uint32_t>(g.d.src_len, 1);
+                    g.retry = true;
+                }
                 total_k += (uint64_t)k - g.d.k;
                 g.d.k = k;
                 brow.push_back(r);
@@ -1299,7 +1356,7 @@ int Core::process_default(GroupList& out_groups,
                 if (total_k > kOutCap && brow.size() > 1) { q++; break; }
             }
         } else {
-            q = rows.size();
+            q = q_par;
         }
         // ---- device search ----
         bool need_pm = false;
@@ -1909,13 +1966,13 @@ int Core::process(mm_matched* out) {
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
             std::fprintf(stderr,
                          "[nkm] sync %.2f ms | pass %.2f ms (assemble %.2f, search %.2f ms [kernel %.2f ms], replay %.2f "
-                         "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches) | finish %.2f ms | "
+                         "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches, %d tier lists) | finish %.2f ms | "
                          "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu | par bucket %.2f work %.2f "
                          "merge %.2f ms (task max %.2f ms, rows %llu, hits %llu) | batch: prep %.2f overlap %.2f wait %.2f "
                          "post %.2f lists %.2f | replay: gather %.2f job %.2f clear %.2f\n",
                          ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms(), stats.replay_ms,
                          stats.apply_ms, stats.batches,
-                         stats.parallel_batches, stats.refetches, stats.launches(), ms(t2, t3), ms(t3, t4),
+                         stats.parallel_batches, stats.refetches, stats.launches(), stats.tier_lists, ms(t2, t3), ms(t3, t4),
                          groups.size(), nslots(), n_live_, active_list_.size(), sigs_.size(),
                          dict_.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms,
                          stats.par_task_max_ms, (unsigned long long)stats.par_rows, (unsigned long long)stats.par_hits,

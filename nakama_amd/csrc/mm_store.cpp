@@ -118,6 +118,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_PARTIAL")) partial_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_DEVENUM")) dev_enum_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_RPACK")) pack_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_TIER")) tier_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_BULK")) bulk_mode_ = std::strcmp(e, "0") == 0 ? 0 : std::strcmp(e, "force") == 0 ? 2 : 1;
     if (const char* e = std::getenv("NKM_KERNEL"))
         kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN
@@ -452,6 +453,11 @@ void Core::sig_describe(Sig& s, const std::vector<DClause>& dc, const CompiledQu
     for (auto& d : dc)
         if (d.op != OP_FALSE && std::find(fs.begin(), fs.end(), d.field) == fs.end()) fs.push_back(d.field);
     s.n_fields = (uint16_t)fs.size();
+    s.exact_scores = dc.size() <= 64;
+    for (auto& d : dc) {
+        const double x = std::ldexp(d.score, 20);
+        s.exact_scores = s.exact_scores && std::isfinite(d.score) && std::fabs(d.score) <= 1048576.0 && x == std::nearbyint(x);
+    }
 }
 
 // Adds a described signature: its clauses, the fields it references (and

@@ -72,6 +72,7 @@ struct BGroup {
     uint16_t n_fields = 0;        // field columns the signature reads (roofline bytes)
     uint32_t nrows = 0;
     uint32_t row_slot = kNoSlot;  // RevPrecision: the single searching row
+    bool retry = false;           // holds the row a truncated list stopped: its search returns every tier
     DGroup d{};
     // The hit list: `hits` (16-B DHit, slot + source position + score key) or,
     // for mscan lists (never cut, so no cursor needs their keys), 4-B slot
@@ -125,6 +126,7 @@ struct BGroup {
         n_fields = 0;
         nrows = 0;
         row_slot = kNoSlot;
+        retry = false;
         d = DGroup{};
         hits = nullptr;
         sp = nullptr;

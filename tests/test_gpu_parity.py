@@ -129,7 +129,9 @@ def test_c2_region_lists_past_topk(fullvar, monkeypatch):
     """C2's shape at 10k: region posting lists of ~2,500 (past the 512-entry
     LDS top-K), ~1,000 skill-window signatures, so search_kernel<512>'s
     truncation, early exit at the score bound and batch restarts all run;
-    NKM_FULLVAR=1 also sends re-searched rows through full lists."""
+    NKM_FULLVAR=1 also sends re-searched rows through full lists.  (Top-tier
+    lists off: they would keep most rows from running off their lists.)"""
+    monkeypatch.setenv("NKM_TIER", "0")
     monkeypatch.setenv("NKM_FULLVAR", fullvar)
     rs = run_passes(2, 10_000, 2, dict(max_intervals=2))
     assert sum(r.n_batches for r in rs) > 2  # truncated lists restarted batches
@@ -150,6 +152,23 @@ def test_hit_list_transfer_modes(config, n, cfg, mode, monkeypatch):
     run_passes(config, n, 2, cfg)
 
 
+@pytest.mark.parametrize("config,n,cfg", [(2, 10_000, dict(max_intervals=2)), (2, 30_000, dict(max_intervals=2)),
+                                          (9, 5000, dict(max_intervals=2)), (10, 3000, dict(max_intervals=2)),
+                                          (6, 2000, dict(max_intervals=3)), (8, 2000, dict(max_intervals=3))])
+@pytest.mark.parametrize("tier", ["1", "0"])
+def test_top_tier_lists(config, n, cfg, tier, monkeypatch):
+    """Variable-score searches as top-tier lists (search_kernel path 2: the
+    hits scoring the query's top score, in source order — an exact prefix of
+    the sorted hit list of any length) when every clause score sums exactly:
+    C2's skill windows (boosts ^2), config 9 (no region must), wide queries
+    and mixed workloads (non-dyadic boosts keep the LDS top-K).  Groups and
+    state equal to the oracle; C2 at 30k needs no more than 3 batches."""
+    monkeypatch.setenv("NKM_TIER", tier)
+    rs = run_passes(config, n, 2, cfg)
+    if config == 2 and n == 30_000 and tier == "1":
+        assert rs[0].n_batches <= 3, rs[0].n_batches
+
+
 @pytest.mark.parametrize("partial", ["1", "0"])
 def test_c2_partial_parallel_replay(partial, monkeypatch):
     """Truncated variable-score lists under the pool-parallel replay (forced
@@ -158,6 +177,7 @@ def test_c2_partial_parallel_replay(partial, monkeypatch):
     order; NKM_PARTIAL=0 replays such batches serially."""
     monkeypatch.setenv("NKM_PARALLEL", "force")
     monkeypatch.setenv("NKM_FULLVAR", "0")
+    monkeypatch.setenv("NKM_TIER", "0")
     monkeypatch.setenv("NKM_PARTIAL", partial)
     rs = run_passes(2, 10_000, 2, dict(max_intervals=2))
     assert sum(r.n_batches for r in rs) > 2  # truncated lists restarted batches
