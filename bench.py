@@ -43,7 +43,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 KERNELS = {0: "search_kernel", 1: "scan_kernel", 2: "mscan_kernel", 3: "rsmall_kernel", 4: "mscan_hash_kernel",
-           5: "rpack_kernel"}  # mm_matched.eval_kernel
+           5: "rpack_kernel", 6: "rsrc_merge_kernel", 7: "rsrc_tile_kernel"}  # mm_matched.eval_kernel
 WORKLOADS = {
     1: "C1: 10k solo 1v1, '+properties.mode:ranked +properties.region:eu'",
     2: "C2: skill-window range queries with ^boost, 1v1",

@@ -30,6 +30,7 @@
 #include "mm_handle.h"
 #include "qcompile.h"
 #include "termmatch.h"
+#include "range_walk.h"
 #include "replay_core.h"
 #include "strstore.h"
 
@@ -86,6 +87,13 @@ int mscan_chunk_len(uint32_t n_sigs);
 int mscan_max_sigs();
 int mscan_max_fields();
 int mscan_max_clauses();
+// range batches (range_walk.h): the pools' candidates sorted by (value, source
+// position), then the bound queries; see mm_kernels.hip
+hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max_pad, const DRangeTile* d_tiles,
+                       uint32_t n_tiles, const uint32_t* d_blk_pool, uint32_t n_elems, int64_t* d_key[2],
+                       uint32_t* d_pos[2], const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds, int* which,
+                       hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1, const hipEvent_t* ev_merge,
+                       int max_merge, int* n_merge);
 
 struct DeviceError {
     hipError_t err;
@@ -147,6 +155,11 @@ struct Sig {
     // every clause score is a multiple of 2^-20 below 2^20 in magnitude: any
     // sum of them is exact in double, whatever the order (top-tier lists)
     bool exact_scores = false;
+    // a range-source search (range_walk.h): one MUST keyword term (must_terms[0],
+    // its pool) and numeric range clauses on this one other field, at least one
+    // MUST; kNoRange otherwise
+    static constexpr uint16_t kNoRange = 0xFFFF;
+    uint16_t rs_field = kNoRange;
 };
 
 // Persistent host workers for the pass's data-parallel host phases (pool
@@ -411,18 +424,28 @@ struct RevTimer {
 struct PassStats {
     int full_lists = 0;  // variable-score searches run as full lists (host-sorted)
     int tier_lists = 0;  // variable-score searches run as top-tier lists (search_kernel path 2)
-    // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel
-    double k_ms[4] = {0, 0, 0, 0};      // HIP-event time of the launches
+    // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel,
+    // 4 rsrc_merge_kernel, 5 rsrc_tile_kernel (range batches)
+    static constexpr int kKernels = 6;
+    double k_ms[kKernels] = {};         // HIP-event time of the launches
     bool mhash = false;                 // a batch's mscan ran hashed (mscan_hash_kernel)
     bool rpack = false;                 // kernel 3's launches were packed batches (rpack_kernel)
-    int64_t k_bytes[4] = {0, 0, 0, 0};  // algorithmic bytes
-    int k_launches[4] = {0, 0, 0, 0};
+    int64_t k_bytes[kKernels] = {};     // algorithmic bytes
+    int k_launches[kKernels] = {};
     int64_t pair_evals = 0;
-    double eval_ms() const { return k_ms[0] + k_ms[1] + k_ms[2] + k_ms[3]; }
-    int launches() const { return k_launches[0] + k_launches[1] + k_launches[2] + k_launches[3]; }
+    double eval_ms() const {
+        double t = 0;
+        for (int k = 0; k < kKernels; k++) t += k_ms[k];
+        return t;
+    }
+    int launches() const {
+        int t = 0;
+        for (int k = 0; k < kKernels; k++) t += k_launches[k];
+        return t;
+    }
     int dominant() const {  // the kernel with the most algorithmic bytes
         int d = 0;
-        for (int k = 1; k < 4; k++)
+        for (int k = 1; k < kKernels; k++)
             if (k_bytes[k] > k_bytes[d]) d = k;
         return d;
     }
@@ -666,6 +689,34 @@ private:
         double live_w = 0;   // sum over rows of src_len x the row's per-live-candidate bytes
     };
     bool tier_mode_ = true;  // NKM_TIER=0: variable-score searches never return top-tier lists
+    // ---- range batches (mm_range.cpp, range_walk.h) ----
+    // A batch whose every row is a range-source search (Sig::rs_field) of a
+    // pool on one keyword field: the pools' candidates sorted by value on the
+    // device (rsrc_* kernels), every remaining row decided in one batch by
+    // the min-tree walk.  false: the rows do not qualify (nothing changed).
+    bool range_mode_ = true;  // NKM_RANGE=0: such batches take the hit-list path
+    bool range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList& out_groups,
+                     std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats);
+    struct RangePoolHost {  // one pool of a range batch (kept across passes: capacity reused)
+        uint32_t term = 0;
+        uint16_t field = 0;
+        DRangePool d{};
+        std::vector<uint32_t> slot, rank, leaf_of;
+        RangeSrc src;
+    };
+    std::vector<RangePoolHost> rs_pools_;
+    std::unique_ptr<std::atomic<uint8_t>[]> rs_mark_;  // per signature: claimed by a batch row (all zero between batches)
+    size_t rs_mark_cap_ = 0;
+    std::vector<uint32_t> rs_sig_loc_;  // signature -> its index in the batch (valid for the batch's signatures)
+    std::vector<uint32_t> rs_leaf_;     // slot -> its leaf in its pool during a range batch, else kNoSlot
+    std::vector<RRange> rs_tiers_;      // the batch's signatures' tier lists
+    DevArray<uint8_t> d_rblob_;         // pools, tiles, block -> pool, bound queries
+    PinnedArray<uint8_t> h_rblob_;
+    DevArray<int64_t> d_rkey_[2];
+    DevArray<uint32_t> d_rpos_[2], d_rbound_;
+    PinnedArray<uint32_t> h_rpos_, h_rbound_;
+    static constexpr int kRsrcMaxMerge = 20;
+    hipEvent_t rs_ev_[2 + 2 * kRsrcMaxMerge] = {};  // the tile launch, then each merge launch
     int bulk_mode_ = 1;      // NKM_BULK: 0 = Insert per ticket, 1 = batches of >= 4096 on the workers, 2 = any batch
     bool pack_mode_ = true;  // NKM_RPACK=0: RevPrecision batches search per row (rsmall / search_kernel)
     UVec<DSmallRow> pk_tmp_;

@@ -211,6 +211,35 @@ NKM_HD inline PackLayout pack_layout(uint64_t n, int S) {
     return L;
 }
 
+// ---- range sources (rsrc_* kernels; range_walk.h) ----------------------------
+// A pool of a range batch: the posting range of its term (postings[src_off,
+// + src_len), source order) and the numeric field its searches' ranges read.
+// Its candidates are sorted by (value, source position) into the elements
+// [out_off, out_off + pad_len) of the key / position buffers (pad_len: src_len
+// rounded up to 256); a candidate that is not alive or holds no number in
+// `field`, and the padding, sort after every valid one (key INT64_MAX,
+// position | kRsrcInvalid), so the valid candidates are a prefix.
+constexpr uint32_t kRsrcTile = 2048;           // elements sorted in LDS by one workgroup
+constexpr uint32_t kRsrcInvalid = 0x80000000u;
+struct DRangePool {
+    uint32_t src_off, src_len;
+    uint32_t out_off, pad_len;
+    uint32_t field;
+    uint32_t pad;
+};
+static_assert(sizeof(DRangePool) == 24, "DRangePool is 24 bytes");
+// One tile of rsrc_tile_kernel: elements [start, start + len) of a pool.
+struct DRangeTile {
+    uint32_t pool, start, len, pad;
+};
+// A bound query of rsrc_bounds_kernel: the first sorted element of `pool`
+// whose key is >= key (upper = 0) or > key (upper = 1).
+struct DRangeBound {
+    int64_t key;
+    uint32_t pool, upper;
+};
+static_assert(sizeof(DRangeBound) == 16, "DRangeBound is 16 bytes");
+
 // Placement of one scan chunk (scan_kernel / mscan_kernel -> stitch_kernel).
 struct DChunkMap {
     uint32_t first;    // result index of the search's first chunk

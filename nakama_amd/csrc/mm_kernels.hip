@@ -1793,6 +1793,160 @@ int mscan_max_sigs() { return kMaxMSig; }
 int mscan_max_fields() { return kMaxMField; }
 int mscan_max_clauses() { return kMaxMClause; }
 
+// ---- range sources (range_walk.h) -----------------------------------------
+// A range batch's pools sorted by (value, source position): rsrc_tile_kernel
+// sorts tiles of kRsrcTile elements in LDS, rsrc_merge_kernel merges runs of R
+// into runs of 2R (R = kRsrcTile, 2 kRsrcTile, ...), rsrc_bounds_kernel finds
+// the clauses' bounds in the sorted keys.  Elements are (key, position) pairs,
+// distinct within a pool (positions are), so a merge places an element at its
+// index in its run plus its rank in the partner run — a binary search, no
+// ties to break.
+
+__device__ __forceinline__ bool rsrc_less(int64_t ka, uint32_t va, int64_t kb, uint32_t vb) {
+    return ka < kb || (ka == kb && va < vb);
+}
+
+// One tile per workgroup: 8 elements per lane loaded coalesced (the posting
+// entry, then alive / kind / value of that slot), then merged in LDS from
+// runs of 1 up to the tile.
+__global__ __launch_bounds__(kBlock) void rsrc_tile_kernel(DStore st, const DRangePool* __restrict__ pools,
+                                                           const DRangeTile* __restrict__ tiles, int64_t* __restrict__ okey,
+                                                           uint32_t* __restrict__ opos) {
+    constexpr int E = kRsrcTile / kBlock;
+    __shared__ int64_t sk[2][kRsrcTile];
+    __shared__ uint32_t sv[2][kRsrcTile];
+    const DRangeTile t = tiles[blockIdx.x];
+    const DRangePool P = pools[t.pool];
+    const int64_t* __restrict__ fv = st.fval[P.field];
+    const uint8_t* __restrict__ fk = st.fkind[P.field];
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+        const uint32_t e = threadIdx.x + j * kBlock;
+        const uint32_t i = t.start + e;  // position in the pool's source
+        int64_t k = INT64_MAX;
+        uint32_t v = kRsrcInvalid | i;
+        if (e < t.len && i < P.src_len) {
+            const uint32_t s = st.postings[P.src_off + i];
+            if (st.alive[s] && fk[s] == KIND_NUMERIC) {
+                k = fv[s];
+                v = i;
+            }
+        }
+        sk[0][e] = k;
+        sv[0][e] = v;
+    }
+    __syncthreads();
+    int b = 0;
+    for (uint32_t r = 1; r < t.len; r <<= 1, b ^= 1) {
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+            const uint32_t e = threadIdx.x + j * kBlock;
+            if (e >= t.len) continue;
+            const int64_t k = sk[b][e];
+            const uint32_t v = sv[b][e];
+            const uint32_t run = e / r, ps = (run ^ 1u) * r;
+            uint32_t o = e;
+            if (ps < t.len) {
+                uint32_t lo = ps, hi = min(ps + r, t.len);
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (rsrc_less(sk[b][mid], sv[b][mid], k, v)) lo = mid + 1;
+                    else hi = mid;
+                }
+                o = (run & ~1u) * r + (e - run * r) + (lo - ps);
+            }
+            sk[b ^ 1][o] = k;
+            sv[b ^ 1][o] = v;
+        }
+        __syncthreads();
+    }
+    const uint64_t base = (uint64_t)P.out_off + t.start;
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+        const uint32_t e = threadIdx.x + j * kBlock;
+        if (e < t.len) {
+            okey[base + e] = sk[b][e];
+            opos[base + e] = sv[b][e];
+        }
+    }
+}
+
+// Runs of R -> runs of 2R over every pool at once (one thread per element;
+// blk_pool: the pool of each 256-element block, pools being 256-aligned).
+__global__ __launch_bounds__(kBlock) void rsrc_merge_kernel(const DRangePool* __restrict__ pools,
+                                                            const uint32_t* __restrict__ blk_pool,
+                                                            const int64_t* __restrict__ ik, const uint32_t* __restrict__ ip,
+                                                            int64_t* __restrict__ ok, uint32_t* __restrict__ op, uint32_t R) {
+    const DRangePool P = pools[blk_pool[blockIdx.x]];
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t e = g - P.out_off;
+    const int64_t k = ik[g];
+    const uint32_t v = ip[g];
+    const uint32_t run = e / R, ps = (run ^ 1u) * R;
+    uint32_t o = e;
+    if (ps < P.pad_len) {
+        const int64_t* __restrict__ bk = ik + P.out_off;
+        const uint32_t* __restrict__ bp = ip + P.out_off;
+        uint32_t lo = ps, hi = min(ps + R, P.pad_len);
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (rsrc_less(bk[mid], bp[mid], k, v)) lo = mid + 1;
+            else hi = mid;
+        }
+        o = (run & ~1u) * R + (e - run * R) + (lo - ps);
+    }
+    ok[(uint64_t)P.out_off + o] = k;
+    op[(uint64_t)P.out_off + o] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void rsrc_bounds_kernel(const DRangePool* __restrict__ pools,
+                                                             const int64_t* __restrict__ key,
+                                                             const DRangeBound* __restrict__ q, uint32_t nq,
+                                                             uint32_t* __restrict__ out) {
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= nq) return;
+    const DRangeBound b = q[t];
+    const DRangePool P = pools[b.pool];
+    const int64_t* __restrict__ k = key + P.out_off;
+    uint32_t lo = 0, hi = P.pad_len;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (b.upper ? k[mid] <= b.key : k[mid] < b.key) lo = mid + 1;
+        else hi = mid;
+    }
+    out[t] = lo;
+}
+
+// The whole sort + bounds.  Buffers: keys / positions 2 x n_elems each (ping-
+// pong); the sorted ones end in *which (0 or 1).  Event pairs: ev_tile around
+// the tile launch, ev_merge[2m], ev_merge[2m + 1] around merge launch m (at
+// most max_merge of them).  Returns the number of merge launches in *n_merge.
+hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max_pad, const DRangeTile* d_tiles,
+                       uint32_t n_tiles, const uint32_t* d_blk_pool, uint32_t n_elems, int64_t* d_key[2],
+                       uint32_t* d_pos[2], const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds, int* which,
+                       hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1, const hipEvent_t* ev_merge,
+                       int max_merge, int* n_merge) {
+    *which = 0;
+    *n_merge = 0;
+    if (n_elems == 0 || n_tiles == 0) return hipSuccess;
+    if (n_elems % kBlock) return hipErrorInvalidValue;
+    hipExtLaunchKernelGGL(rsrc_tile_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, ev_tile0, ev_tile1, 0, st, d_pools,
+                          d_tiles, d_key[0], d_pos[0]);
+    int b = 0, m = 0;
+    for (uint32_t R = kRsrcTile; R < max_pad; R <<= 1, b ^= 1, m++) {
+        if (m >= max_merge) return hipErrorInvalidValue;
+        hipExtLaunchKernelGGL(rsrc_merge_kernel, dim3(n_elems / kBlock), dim3(kBlock), 0, stream, ev_merge[2 * m],
+                              ev_merge[2 * m + 1], 0, d_pools, d_blk_pool, d_key[b], d_pos[b], d_key[b ^ 1], d_pos[b ^ 1],
+                              R);
+    }
+    if (nq)
+        hipLaunchKernelGGL(rsrc_bounds_kernel, dim3((nq + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, d_pools,
+                           d_key[b], d_q, nq, d_bounds);
+    *which = b;
+    *n_merge = m;
+    return hipGetLastError();
+}
+
 int var_k_capacity() { return kVarK; }
 int scan_chunk_len() { return kScanChunk; }
 

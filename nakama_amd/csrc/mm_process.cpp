@@ -1059,6 +1059,14 @@ int Core::process_default(GroupList& out_groups,
         // the RevThreshold timer fired: the remaining rows search as without
         // RevPrecision (row-sharded: decided at batch starts, OR-ed over the ranks)
         if (rev && (row_shard() ? shard_any(timer.check()) : timer.check())) rev = rp.rev = false;
+        // ---- range batch (mm_range.cpp): every remaining row decided at once ----
+        if (!rev && range_mode_ && kernel_mode_ == KM_AUTO && retry_slot == kNoSlot && !row_shard() && par_mode_) {
+            newly.clear();
+            if (range_batch(rows, pos, out_groups, expired, newly, stats)) {
+                defer_apply(newly);
+                continue;
+            }
+        }
         // ---- packed RevPrecision batch (rpack_kernel) ----
         if (rev && pack_mode_ && kernel_mode_ == KM_AUTO && retry_slot == kNoSlot && !row_shard()) {
             using pclk = std::chrono::steady_clock;
@@ -1982,7 +1990,7 @@ int Core::process(mm_matched* out) {
     }
     unwind.armed = false;
     const int dk = stats.dominant();  // bench.py's roofline kernel
-    out->eval_kernel = dk == 2 && stats.mhash ? 4 : dk == 3 && stats.rpack ? 5 : dk;
+    out->eval_kernel = dk == 2 && stats.mhash ? 4 : dk == 3 && stats.rpack ? 5 : dk == 4 ? 6 : dk == 5 ? 7 : dk;
     out->eval_ms = stats.k_ms[dk];
     out->pair_evals = stats.pair_evals;
     out->eval_bytes = stats.k_bytes[dk];

@@ -119,6 +119,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_DEVENUM")) dev_enum_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_RPACK")) pack_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_TIER")) tier_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_RANGE")) range_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_BULK")) bulk_mode_ = std::strcmp(e, "0") == 0 ? 0 : std::strcmp(e, "force") == 0 ? 2 : 1;
     if (const char* e = std::getenv("NKM_KERNEL"))
         kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN
@@ -247,6 +248,8 @@ Core::~Core() {
     for (auto* p : d_fval_) delete p;
     for (auto* p : d_fkind_) delete p;
     for (auto& e : ev_)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : rs_ev_)
         if (e) (void)hipEventDestroy(e);
     if (apply_ev_) (void)hipEventDestroy(apply_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -457,6 +460,27 @@ void Core::sig_describe(Sig& s, const std::vector<DClause>& dc, const CompiledQu
     for (auto& d : dc) {
         const double x = std::ldexp(d.score, 20);
         s.exact_scores = s.exact_scores && std::isfinite(d.score) && std::fabs(d.score) <= 1048576.0 && x == std::nearbyint(x);
+    }
+    // range source: exactly one MUST keyword term, every other clause a numeric
+    // range on one other field, at least one of them MUST (so every hit holds
+    // a number there), at most 32 ranges (range_walk.h: build_tiers)
+    if (cq.kind == QK_BOOL && !fuzzy && dc.size() <= 33) {
+        int n_term = 0, n_must_range = 0, n_range = 0, rf = -1;
+        bool ok = true;
+        for (auto& d : dc) {
+            if (d.op == OP_TERM && d.occur == OCC_MUST) {
+                n_term++;
+            } else if (d.op == OP_RANGE) {
+                if (rf < 0) rf = d.field;
+                ok = ok && d.field == rf;
+                n_range++;
+                n_must_range += d.occur == OCC_MUST;
+            } else {
+                ok = false;
+            }
+        }
+        if (ok && n_term == 1 && n_must_range >= 1 && n_range <= 32 && rf != (int)s.must_terms[0].first)
+            s.rs_field = (uint16_t)rf;
     }
 }
 

@@ -1,0 +1,399 @@
+// nakama_amd/csrc/range_walk.h — processDefault's greedy walk over a
+// numeric-range source (the C2 skill-window searches).
+//
+// A range-source search (Sig::rs_field) is "+term:<pool> and numeric range
+// clauses on one field f" (MUST / SHOULD / MUST_NOT, with boosts): every
+// candidate of its pool that holds a number in f scores by which clauses
+// contain that number, so the hit list in the reference's order (score desc,
+// created_at asc, doc order; matchmaker_process.go:86-90 over
+// bluge/search/searcher/search_numeric_range.go:26-83) is: tier by tier (one
+// score each, highest first), the tier's candidates in source order.  With the
+// pool's candidates sorted by f on the device (rsrc_* kernels), a tier is a
+// few leaf intervals of that order.  The walk keeps, per pool, a min tree over
+// the leaves holding each candidate's source position (its hit rank), or
+// kInf once it is selected: a row's next hit is the smallest rank over the
+// current tier's intervals — O(log n) per hit, whatever the depth at which the
+// reference's walk finds it (a list-based replay skips every earlier-selected
+// hit, so late rows walked thousands of entries and lists ran out).  Hits the
+// row has read are masked (kInf) until the row ends, so the row sees exactly
+// the reference's sequence; the loop body is ReplayCore::row's.
+//
+// Pure host code over plain arrays (no store, no HIP): timed and checked on
+// its own by tools/range_bench.cpp.
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "gocompat.h"
+#include "mm_device.h"
+#include "qcompile.h"
+#include "replay_core.h"
+
+namespace nkm {
+
+// Min over leaf intervals with point updates: fan-out 16 levels (a query
+// touches at most two partial blocks per level; 25k leaves are 4 levels).
+struct MinTree16 {
+    static constexpr uint32_t kInf = 0xFFFFFFFFu;
+    std::vector<std::vector<uint32_t>> lv;  // lv[0]: leaves; lv[k][i] = min of lv[k-1][16i, 16i + 16)
+    void build(const uint32_t* v, uint32_t n) {
+        size_t L = 1;
+        for (uint32_t m = n; m > 16; m = (m + 15) / 16) L++;
+        lv.resize(L);
+        uint32_t m = n;
+        lv[0].resize(((size_t)m + 15) & ~(size_t)15);
+        std::memcpy(lv[0].data(), v, (size_t)n * 4);
+        std::fill(lv[0].begin() + n, lv[0].end(), kInf);
+        for (size_t k = 1; k < L; k++) {
+            const uint32_t pm = m;
+            m = (m + 15) / 16;
+            lv[k].resize(((size_t)m + 15) & ~(size_t)15);
+            std::fill(lv[k].begin(), lv[k].end(), kInf);
+            const uint32_t* c = lv[k - 1].data();
+            for (uint32_t i = 0; i < m; i++) {
+                uint32_t x = kInf;
+                for (uint32_t j = 16 * i; j < 16 * i + 16 && j < ((pm + 15) & ~15u); j++) x = std::min(x, c[j]);
+                lv[k][i] = x;
+            }
+        }
+    }
+    static uint32_t min16(const uint32_t* p) {
+        uint32_t x = p[0];
+        for (int j = 1; j < 16; j++) x = std::min(x, p[j]);
+        return x;
+    }
+    // min over leaves [a, b)
+    uint32_t range_min(uint32_t a, uint32_t b) const {
+        uint32_t m = kInf;
+        for (size_t k = 0; a < b; k++) {
+            const uint32_t* v = lv[k].data();
+            if ((a >> 4) == ((b - 1) >> 4) || k + 1 == lv.size()) {
+                for (uint32_t i = a; i < b; i++) m = std::min(m, v[i]);
+                break;
+            }
+            if (a & 15) {
+                const uint32_t e = (a | 15) + 1;
+                for (uint32_t i = a; i < e; i++) m = std::min(m, v[i]);
+                a = e;
+            }
+            if (b & 15) {
+                const uint32_t s = b & ~15u;
+                for (uint32_t i = s; i < b; i++) m = std::min(m, v[i]);
+                b = s;
+            }
+            a >>= 4;
+            b >>= 4;
+        }
+        return m;
+    }
+    void set(uint32_t i, uint32_t x) {
+        lv[0][i] = x;
+        for (size_t k = 1; k < lv.size(); k++) {
+            const uint32_t blk = i >> 4;
+            const uint32_t nm = min16(lv[k - 1].data() + ((size_t)blk << 4));
+            if (lv[k][blk] == nm) return;  // the parents are unchanged
+            lv[k][blk] = nm;
+            i = blk;
+        }
+    }
+};
+
+// One leaf interval of a tier; `tend` is the index (in the signature's range
+// list) one past the tier's last interval.
+struct RRange {
+    uint32_t a, b, tend;
+};
+
+// The tiers of a range-source signature over its pool's sorted leaves
+// [0, n_valid): clause c (in clause order, range clauses only) contains the
+// leaves [lo[c], hi[c]).  Each elementary interval between the clauses'
+// boundaries is scored exactly as search_kernel's eval_parsed sums it for
+// every candidate inside (same clause order, same double additions), so the
+// tier keys equal the device's score keys bit for bit.  Appends the tiers,
+// highest key first, each a list of disjoint intervals in leaf order.
+inline void build_tiers(const DClause* cl, int n, const uint32_t* lo, const uint32_t* hi, uint32_t n_valid,
+                        std::vector<RRange>& out) {
+    uint32_t xs[2 + 2 * 64];
+    int nx = 0;
+    xs[nx++] = 0;
+    xs[nx++] = n_valid;
+    int nr = 0;
+    for (int i = 0; i < n; i++)
+        if (cl[i].op == OP_RANGE) {
+            xs[nx++] = std::min(lo[nr], n_valid);
+            xs[nx++] = std::min(hi[nr], n_valid);
+            nr++;
+        }
+    std::sort(xs, xs + nx);
+    nx = (int)(std::unique(xs, xs + nx) - xs);
+    struct E { int64_t key; uint32_t a, b; };
+    E es[2 + 2 * 64];
+    int ne = 0;
+    for (int k = 0; k + 1 < nx; k++) {
+        const uint32_t a = xs[k], b = xs[k + 1];
+        double ms = 0.0, ss = 0.0;
+        bool has_must = false, any_should = false, fail = false;
+        int r = 0;
+        for (int i = 0; i < n; i++) {
+            bool h = true;  // the pool's MUST term: every candidate holds it
+            if (cl[i].op == OP_RANGE) {
+                h = std::min(lo[r], n_valid) <= a && b <= std::min(hi[r], n_valid);
+                r++;
+            }
+            if (cl[i].occur == OCC_MUST) {
+                has_must = true;
+                if (h) ms += cl[i].score;
+                else fail = true;
+            } else if (cl[i].occur == OCC_SHOULD) {
+                if (h) { ss += cl[i].score; any_should = true; }
+            } else if (h) {
+                fail = true;
+            }
+        }
+        if (fail || !has_must) continue;
+        const double sp = any_should ? ms + ss : ms;
+        es[ne++] = E{sortable_i64((sp + 1.0) + 1.0), a, b};
+    }
+    std::stable_sort(es, es + ne, [](const E& x, const E& y) { return x.key > y.key; });
+    for (int k = 0; k < ne;) {
+        int j = k;
+        while (j < ne && es[j].key == es[k].key) j++;
+        // [k, j): one tier, intervals ascending (stable sort), adjacent ones merged
+        const size_t t0 = out.size();
+        for (int q = k; q < j; q++) {
+            if (out.size() > t0 && out.back().b == es[q].a) out.back().b = es[q].b;
+            else out.push_back(RRange{es[q].a, es[q].b, 0});
+        }
+        for (size_t q = t0; q < out.size(); q++) out[q].tend = (uint32_t)out.size();
+        k = j;
+    }
+}
+
+// One pool's candidates in value order (the device sort's valid prefix).
+struct RangeSrc {
+    uint32_t n = 0;               // leaves
+    const uint32_t* slot = nullptr;  // per leaf: ticket slot
+    const uint32_t* rank = nullptr;  // per leaf: source position (hit rank)
+    const uint32_t* leaf_of = nullptr;  // per rank: its leaf
+    MinTree16 tree;
+};
+
+// The walk of one pool's rows (RangeRun::walk); records as replay_pool's.
+struct RangeRun {
+    ReplayView v;
+    int max_intervals;
+    uint8_t* psel;  // per slot: selected in this batch (starts and ends all zero)
+    uint8_t* proc;  // per slot: processed earlier in this batch (pending Intervals)
+    uint32_t* leaf_of_slot;  // per slot: its leaf in this pool, or kNoSlot (rows' own leaves)
+    std::vector<std::vector<CE>> combos;
+    std::vector<uint32_t> cmask, open, masked;
+    std::vector<std::pair<uint32_t, int>> grp;
+    uint64_t hits_seen = 0;
+
+    // iterator over one row's hits: tier by tier, smallest rank first;
+    // every hit read is masked until the row ends
+    RangeSrc* S = nullptr;
+    const RRange* rg = nullptr;
+    uint32_t cur = 0, end = 0;
+    void mask(uint32_t leaf) {
+        S->tree.set(leaf, MinTree16::kInf);
+        masked.push_back(leaf);
+    }
+    bool next(uint32_t& leaf) {
+        while (cur < end) {
+            const uint32_t te = rg[cur].tend;
+            uint32_t m = MinTree16::kInf;
+            for (uint32_t k = cur; k < te; k++) m = std::min(m, S->tree.range_min(rg[k].a, rg[k].b));
+            if (m != MinTree16::kInf) {
+                leaf = S->leaf_of[m];
+                return true;
+            }
+            cur = te;
+        }
+        return false;
+    }
+
+    bool share_session(const HotRec& a, const HotRec& b) const {
+        if (a.count == 1 && b.count == 1) return a.sess0 == b.sess0;
+        for (uint32_t p = a.pres_off; p < a.pres_off + (uint32_t)a.count; p++)
+            for (uint32_t q = b.pres_off; q < b.pres_off + (uint32_t)b.count; q++)
+                if (v.pres_sess[p] == v.pres_sess[q]) return true;
+        return false;
+    }
+    bool has_session(const HotRec& h, uint32_t sess) const {
+        if (h.count == 1) return h.sess0 == sess;
+        for (uint32_t q = h.pres_off; q < h.pres_off + (uint32_t)h.count; q++)
+            if (v.pres_sess[q] == sess) return true;
+        return false;
+    }
+
+    // processDefault's loop body (ReplayCore::row) for row T, whose search's
+    // tiers are rg[r0, r1).  Candidates the device search would not return —
+    // the searching ticket's party (:80-85) and the count-range musts
+    // (MinCount >= T's Min, MaxCount <= T's Max) — are not hits: they are
+    // skipped without counting.  Returns MATCHED / NOMATCH; group_out = grp.
+    ReplayCore::Status row(uint32_t T, const RRange* r, uint32_t r0, uint32_t r1) {
+        const HotRec& ht = v.hot[T];
+        const bool last = v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc;
+        const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
+        const uint32_t tparty = ht.party;
+        auto is_hit = [&](const HotRec& hh) {
+            return !(tparty != kNoParty && hh.party == tparty) && hh.minc >= tmin && hh.maxc <= tmax;
+        };
+        rg = r;
+        cur = r0;
+        end = r1;
+        masked.clear();
+        if (leaf_of_slot[T] != kNoSlot) mask(leaf_of_slot[T]);  // self (:112-126)
+        size_t ncomb = 0;
+        open.clear();
+        uint32_t leaf;
+        while (next(leaf)) {
+            const uint32_t H = S->slot[leaf];
+            mask(leaf);
+            const HotRec& hh = v.hot[H];
+            if (!is_hit(hh)) continue;
+            hits_seen++;
+            if (tmax < hh.maxc && v.intervals[H] + proc[H] <= max_intervals) continue;          // :150-153
+            if (!v.sessions_exclusive && (ht.smask & hh.smask) && share_session(ht, hh)) continue;  // :155-165
+            bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
+            int found = -1;
+            const int hcount = hh.count;
+            const uint32_t hp = hh.pres_off;
+            size_t w = 0, q = 0;  // first fit over the open combos, dropping full ones on the way
+            for (; q < open.size(); q++) {
+                const uint32_t ci = open[q];
+                auto& combo = combos[ci];
+                if ((int)combo.size() + tcount >= tmax) continue;  // full for good
+                open[w++] = ci;
+                if ((int)combo.size() + hcount + tcount <= tmax) {
+                    if (!v.sessions_exclusive && (cmask[ci] & hh.smask) != 0)
+                        for (const CE& e : combo)
+                            if (has_session(hh, e.sess)) { sconf = true; break; }
+                    if (sconf) continue;
+                    for (int k = 0; k < hcount; k++)
+                        combo.push_back(CE{H, (uint32_t)k, leaf, hcount == 1 ? hh.sess0 : v.pres_sess[hp + k]});
+                    cmask[ci] |= hh.smask;
+                    found = (int)ci;
+                    q++;
+                    break;
+                }
+            }
+            for (; q < open.size(); q++) open[w++] = open[q];
+            open.resize(w);
+            if (found < 0) {
+                if (ncomb == combos.size()) {
+                    combos.emplace_back();
+                    cmask.push_back(0);
+                }
+                std::vector<CE>& nc = combos[ncomb];
+                nc.clear();
+                for (int k = 0; k < hcount; k++) nc.push_back(CE{H, (uint32_t)k, leaf, hcount == 1 ? hh.sess0 : v.pres_sess[hp + k]});
+                cmask[ncomb] = hh.smask;
+                found = (int)ncomb++;
+                if (hcount + tcount < tmax) open.push_back((uint32_t)found);
+            }
+            std::vector<CE>& fc = combos[found];
+            int l = (int)fc.size() + tcount;
+            bool form = l == tmax;
+            if (!form && last && l >= tmin && l <= tmax) {
+                // another hit after this one? (:130, :233) — peek, skipping non-hits
+                bool more = false;
+                uint32_t pl;
+                while (!more && next(pl)) {
+                    if (is_hit(v.hot[S->slot[pl]])) more = true;
+                    else mask(pl);
+                }
+                form = !more;
+            }
+            if (!form) continue;
+            const int rem = l % tcm;
+            if (rem != 0) {                                                              // :234-280
+                std::vector<uint32_t> elig;
+                for (const CE& e : fc) {
+                    if (!v.live[e.slot] || v.count[e.slot] > rem) continue;
+                    if (std::find(elig.begin(), elig.end(), e.slot) == elig.end()) elig.push_back(e.slot);
+                }
+                std::vector<IG> groups;
+                group_indexes(elig, 0, rem, v.count, v.created, groups);
+                if (groups.empty()) continue;
+                std::stable_sort(groups.begin(), groups.end(), [](const IG& a, const IG& b) { return a.avg < b.avg; });
+                for (uint32_t gs : groups[0].idx) {
+                    for (int k = 0; k < (int)fc.size(); k++) {
+                        if (fc[k].slot == gs) {
+                            fc[k] = fc.back();
+                            fc.pop_back();
+                            k--;
+                        }
+                    }
+                }
+                l = (int)fc.size() + tcount;
+                if (l < tmax && std::find(open.begin(), open.end(), (uint32_t)found) == open.end())
+                    open.insert(std::lower_bound(open.begin(), open.end(), (uint32_t)found), (uint32_t)found);
+                if (l % tcm != 0) continue;
+            }
+            bool failed = false;                                                         // :287-296
+            for (const CE& e : fc) {
+                const uint32_t s = e.slot;
+                const HotRec& hs = v.hot[s];
+                if (!v.live[s]) continue;
+                if (hs.minc > l || hs.maxc < l || l % hs.cm != 0) { failed = true; break; }
+            }
+            if (failed) continue;
+            grp.clear();
+            for (const CE& e : fc) grp.push_back({e.slot, (int)e.pi});
+            for (int k = 0; k < tcount; k++) grp.push_back({T, k});
+            return ReplayCore::MATCHED;
+        }
+        return ReplayCore::NOMATCH;
+    }
+
+    // The hits the row masked go back into the tree, except the selected.
+    void unmask() {
+        for (uint32_t leaf : masked)
+            if (!psel[S->slot[leaf]]) S->tree.set(leaf, S->rank[leaf]);
+        masked.clear();
+    }
+
+    // Walks a pool's rows (batch rows `bis`, ascending; slot brow[bi]);
+    // sig_range(bi, base, r0, r1) gives the row's tier list base[r0, r1).
+    // Appends records + a sentinel to `o`; psel / proc / the tree's masks are
+    // restored on return except for the selections (the tree keeps them).
+    template <class SigRange>
+    void walk(RangeSrc& src, const uint32_t* bis, uint32_t nrows, const uint32_t* brow, SigRange sig_range, PoolOut& o) {
+        S = &src;
+        uint32_t gcum = 0, xcum = 0;
+        for (uint32_t j = 0; j < nrows; j++) {
+            const uint32_t bi = bis[j];
+            const uint32_t T = brow[bi];
+            if (psel[T]) continue;
+            const RRange* base;
+            uint32_t r0, r1;
+            sig_range(bi, base, r0, r1);
+            const auto status = row(T, base, r0, r1);
+            const HotRec& ht = v.hot[T];
+            PoolRec rec{bi, 0, (uint8_t)(v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc),
+                        (uint32_t)o.ents.size(), 0, gcum, xcum};
+            xcum += rec.expired;
+            if (status == ReplayCore::MATCHED) {
+                rec.matched = 1;
+                rec.len = (uint32_t)grp.size();
+                gcum++;
+                for (auto& e : grp) {
+                    psel[e.first] = 1;
+                    o.ents.push_back(e);
+                }
+            }
+            unmask();
+            proc[T] = 1;
+            o.recs.push_back(rec);
+        }
+        for (auto& e : o.ents) psel[e.first] = 0;
+        for (size_t k = 0; k < o.recs.size(); k++) proc[brow[o.recs[k].bi]] = 0;
+        o.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)o.ents.size(), 0, gcum, xcum});  // sentinel
+    }
+};
+
+}  // namespace nkm

@@ -130,7 +130,9 @@ def test_c2_region_lists_past_topk(fullvar, monkeypatch):
     LDS top-K), ~1,000 skill-window signatures, so search_kernel<512>'s
     truncation, early exit at the score bound and batch restarts all run;
     NKM_FULLVAR=1 also sends re-searched rows through full lists.  (Top-tier
-    lists off: they would keep most rows from running off their lists.)"""
+    lists and range batches off: they would keep rows from running off their
+    lists.)"""
+    monkeypatch.setenv("NKM_RANGE", "0")
     monkeypatch.setenv("NKM_TIER", "0")
     monkeypatch.setenv("NKM_FULLVAR", fullvar)
     rs = run_passes(2, 10_000, 2, dict(max_intervals=2))
@@ -162,11 +164,32 @@ def test_top_tier_lists(config, n, cfg, tier, monkeypatch):
     the sorted hit list of any length) when every clause score sums exactly:
     C2's skill windows (boosts ^2), config 9 (no region must), wide queries
     and mixed workloads (non-dyadic boosts keep the LDS top-K).  Groups and
-    state equal to the oracle; C2 at 30k needs no more than 3 batches."""
+    state equal to the oracle; C2 at 30k needs no more than 3 batches.  (Range
+    batches off: they take C2's rows otherwise.)"""
+    monkeypatch.setenv("NKM_RANGE", "0")
     monkeypatch.setenv("NKM_TIER", tier)
     rs = run_passes(config, n, 2, cfg)
     if config == 2 and n == 30_000 and tier == "1":
         assert rs[0].n_batches <= 3, rs[0].n_batches
+
+
+@pytest.mark.parametrize("par", ["1", "force"])
+@pytest.mark.parametrize("config,n,passes,cfg", [(2, 1500, 2, dict(max_intervals=2)), (2, 10_000, 2, dict(max_intervals=2)),
+                                                 (2, 30_000, 2, dict(max_intervals=2)), (15, 3000, 3, dict(max_intervals=3)),
+                                                 (15, 12_000, 2, dict(max_intervals=2)), (16, 3000, 3, dict(max_intervals=3))])
+def test_range_batches(config, n, passes, cfg, par, monkeypatch):
+    """Range batches (mm_range.cpp, range_walk.h): every row a pool term plus
+    numeric ranges on one field — C2's skill windows; config 15 adds parties,
+    Min < Max, CountMultiple, Intervals, MUST_NOT and ^0.5 ranges and tickets
+    whose skill is a keyword; 16 puts every ticket in one pool.  The pools'
+    candidates are sorted on the device (rsrc_tile / rsrc_merge / rsrc_bounds)
+    and the min-tree walk decides every row of the pass in ONE batch: groups
+    and post-pass state equal to the oracle's, on the serial and the parallel
+    host sweeps (NKM_PARALLEL=force)."""
+    monkeypatch.setenv("NKM_PARALLEL", par)
+    rs = run_passes(config, n, passes, cfg)
+    assert rs[0].n_batches == 1, rs[0].n_batches
+    assert rs[0].eval_kernel in (6, 7), rs[0].eval_kernel
 
 
 @pytest.mark.parametrize("partial", ["1", "0"])
@@ -174,7 +197,8 @@ def test_c2_partial_parallel_replay(partial, monkeypatch):
     """Truncated variable-score lists under the pool-parallel replay (forced
     at 10k): a pool whose row runs past its list stops there and re-searches,
     the other pools carry on, and the pass restores the reference's group
-    order; NKM_PARTIAL=0 replays such batches serially."""
+    order; NKM_PARTIAL=0 replays such batches serially.  (Range batches off.)"""
+    monkeypatch.setenv("NKM_RANGE", "0")
     monkeypatch.setenv("NKM_PARALLEL", "force")
     monkeypatch.setenv("NKM_FULLVAR", "0")
     monkeypatch.setenv("NKM_TIER", "0")

@@ -245,6 +245,37 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             if (shape == 0) t.count_multiple = 2;
             break;
         }
+        case 15:
+        case 16: {  // C2 variant for the range batches (mm_range.cpp): parties of 1-3,
+                    // Min<Max and CountMultiple shapes, MUST_NOT and fractional-boost
+                    // ranges, tickets whose skill is a keyword (never a range hit);
+                    // 16: every ticket in one region (a single pool)
+            const double u = r.uni();
+            party = u < 0.7 ? 1 : u < 0.9 ? 2 : 3;
+            const char* region = shard_regions_i[config == 16 ? 0 : (r.next() & 3)];
+            const int s = (int)std::lround(r.normal(1500.0, 300.0));
+            S->sp.push_back({"region", region});
+            if (r.uni() < 0.95) S->np.push_back({"skill", (double)s});
+            else S->sp.push_back({"skill", "unrated"});
+            char q[320];
+            if (r.next() % 3 == 0)
+                std::snprintf(q, sizeof q,
+                              "+properties.region:%s +properties.skill:>=%d +properties.skill:<=%d "
+                              "properties.skill:>=%d^2 properties.skill:<=%d^2 -properties.skill:>%d "
+                              "properties.skill:<%d^0.5",
+                              region, s - 250, s + 250, s - 60, s + 60, s + 200, s - 100);
+            else
+                std::snprintf(q, sizeof q,
+                              "+properties.region:%s +properties.skill:>=%d +properties.skill:<=%d "
+                              "properties.skill:>=%d^2 properties.skill:<=%d^2",
+                              region, s - 200, s + 200, s - 50, s + 50);
+            query = q;
+            const int shape = (int)(r.next() % 3);
+            if (shape == 0) { t.min_count = 2; t.max_count = 2; }
+            else if (shape == 1) { t.min_count = 2; t.max_count = 4; }
+            else { t.min_count = 4; t.max_count = 6; t.count_multiple = 2; }
+            break;
+        }
         case 14: {  // C5 variant, buckets of 24 (stride 32), a required skill range, 3-player groups
             const int s = (int)std::lround(r.normal(1500.0, 300.0));
             char b[32];
