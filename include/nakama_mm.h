@@ -52,7 +52,9 @@ extern "C" {
 #define MM_ERR_NOT_AVAILABLE     (-5) /* runtime.ErrMatchmakerNotAvailable (matchmaker.go:446) */
 #define MM_ERR_TOO_MANY_TICKETS  (-6) /* runtime.ErrMatchmakerTooManyTickets (matchmaker.go:512,518) */
 #define MM_ERR_TICKET_NOT_FOUND  (-7) /* runtime.ErrMatchmakerTicketNotFound (matchmaker.go:732,836) */
-#define MM_ERR_UNSUPPORTED       (-8) /* query feature not yet lowered (regexp/wildcard/fuzzy); shim maps to QueryInvalid */
+#define MM_ERR_UNSUPPORTED       (-8) /* a ticket the call cannot take: mm_create_multi MM_MULTI_POOLS, a query that does not
+                                         pin every pool field to the ticket's own value; (reserved for a query feature not
+                                         lowered: none remain).  The shim maps it to QueryInvalid */
 #define MM_ERR_DEVICE            (-9) /* HIP runtime failure / no usable gfx950 device */
 #define MM_ERR_ARG               (-10)/* malformed call (null handle, bad sizes) */
 #define MM_ERR_STATE             (-11)/* e.g. mm_process_commit without an open custom pass */
@@ -66,7 +68,8 @@ typedef struct mm_config {
     int32_t rev_threshold;   /* rev_threshold: reverse checks stop interval_sec * rev_threshold s into a pass
                                 (matchmaker_process.go:31-46); bench.py pins it to 0 */
     int32_t override_enabled;/* a MatchmakerOverride is registered -> processCustom path (matchmaker.go:314) */
-    int32_t device;          /* HIP device ordinal for this handle (one process per GPU) */
+    int32_t device;          /* HIP device ordinal of this handle (mm_create_multi, include/nakama_cluster.h,
+                                drives several devices from one handle) */
     const char* node;        /* this node's name (config.GetName(), matchmaker.go:225) */
 } mm_config;
 

@@ -160,6 +160,7 @@ struct Sig {
     // MUST; kNoRange otherwise
     static constexpr uint16_t kNoRange = 0xFFFF;
     uint16_t rs_field = kNoRange;
+    uint8_t rs_nrange = 0;  // its range clauses
 };
 
 // Persistent host workers for the pass's data-parallel host phases (pool
@@ -668,6 +669,11 @@ private:
     ParPlan par_plan_;
     bool plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                        const UVec<uint32_t>& brow_group, ParPlan& P, PassStats& stats);
+    // plan_parallel when the batch assembly already bucketed the rows per
+    // search (P.pool_off / P.pool_rows) and every row carries its own terms:
+    // each search its own pool when their pool keys are pairwise distinct
+    bool plan_fused(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow, const UVec<uint32_t>& brow_group,
+                    ParPlan& P, PassStats& stats);
     template <class SigOf, class GroupOf, class RowOf>
     bool plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_of, const UVec<uint32_t>& brow,
                     ParPlan& P, PassStats& stats);

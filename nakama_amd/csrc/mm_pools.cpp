@@ -36,6 +36,63 @@ bool Core::plan_parallel(const std::vector<BGroup>& bg, const UVec<uint32_t>& br
         [&](size_t i) { return bg[i].row_slot; }, brow, P, stats);
 }
 
+// plan_fused: the rows are bucketed per search already (assemble_parallel,
+// which also checked that every row carries its own search's terms); the
+// searches are the pools when their keys — their MUST terms on the fields
+// every search requires a term on — are pairwise distinct.  Only the
+// searches are read here (C3: 8), not the rows.  Otherwise plan_parallel.
+bool Core::plan_fused(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow, const UVec<uint32_t>& brow_group,
+                      ParPlan& P, PassStats& stats) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const size_t G = bg.size();
+    P.ok = false;
+    std::vector<uint16_t> keyf;
+    for (auto& mt : sigs_[bg[0].sig].must_terms)
+        if (std::find(keyf.begin(), keyf.end(), mt.first) == keyf.end()) keyf.push_back(mt.first);
+    for (size_t i = 1; i < G && !keyf.empty(); i++) {
+        const auto& mts = sigs_[bg[i].sig].must_terms;
+        keyf.erase(std::remove_if(keyf.begin(), keyf.end(),
+                                  [&](uint16_t f) {
+                                      return std::none_of(mts.begin(), mts.end(), [&](const std::pair<uint16_t, uint32_t>& m) {
+                                          return m.first == f;
+                                      });
+                                  }),
+                   keyf.end());
+    }
+    bool ok = !keyf.empty();
+    for (uint16_t f : keyf) ok = ok && fkind_[f].size() == nslots();
+    std::vector<std::vector<uint32_t>> key(G, std::vector<uint32_t>(keyf.size(), UINT32_MAX));
+    for (size_t i = 0; i < G && ok; i++)
+        for (auto& mt : sigs_[bg[i].sig].must_terms)
+            for (size_t k = 0; k < keyf.size(); k++)
+                if (mt.first == keyf[k]) {
+                    if (key[i][k] != UINT32_MAX && key[i][k] != mt.second) ok = false;  // two terms on one field
+                    key[i][k] = mt.second;
+                }
+    if (ok) {
+        std::vector<uint32_t> ord(G);
+        for (uint32_t i = 0; i < G; i++) ord[i] = i;
+        std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+        for (size_t i = 1; i < G && ok; i++) ok = key[ord[i]] != key[ord[i - 1]];
+    }
+    if (!ok) return plan_parallel(bg, brow, brow_group, P, stats);
+    P.ng = G;
+    grow_to(P.search_pool, G);
+    for (uint32_t i = 0; i < G; i++) P.search_pool[i] = i;
+    P.self_rows.assign(G, 1);
+    if (keyf.size() == 1) {
+        grow_to(P.pool_key1, G);
+        for (size_t i = 0; i < G; i++) P.pool_key1[i] = key[i][0];
+    } else {
+        P.pool_key1.clear();
+    }
+    P.ok = true;
+    stats.par_bucket_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    if (batch_profile_) std::fprintf(stderr, "[nkm]   plan_fused: %zu pools (the assembly's buckets)\n", G);
+    return true;
+}
+
 // plan_parallel over `nsearch` searches: sig_of(i) is search i's signature,
 // group_of(bi) batch row bi's search (a packed RevPrecision batch: the row
 // itself), row_of(i) the slot of a one-row search (RevPrecision) or kNoSlot.
@@ -179,6 +236,7 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
             for (size_t i = lo; i < hi; i++) k1[i] = tpool[k1[i]];
         });
     } else {
+        pool_key1.clear();
         std::map<std::vector<uint32_t>, uint32_t> pool_of;
         std::vector<uint32_t> key(keyf.size());
         for (size_t i = 0; i < nsearch; i++) {

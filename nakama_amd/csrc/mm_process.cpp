@@ -1175,6 +1175,7 @@ int Core::process_default(GroupList& out_groups,
         // capacity total stays within kOutCap (so it would not have cut the
         // batch earlier).
         size_t q_par = rows.size();  // the batch's end in rows (the serial loop's q)
+        bool fused_plan = false;     // assemble_parallel bucketed the rows per search (plan_fused)
         auto assemble_parallel = [&]() -> bool {
             size_t nr = rows.size() - pos;
             const size_t nsig = sigs_.size();
@@ -1206,6 +1207,7 @@ int Core::process_default(GroupList& out_groups,
                 std::vector<uint32_t> first, cnt;
                 std::vector<int32_t> lastm, maxm;
                 size_t n = 0;
+                bool self = true;  // every row carries its own search's terms (self_match_) and is indexed
             };
             std::vector<Chunk> ch(nch);
             wp.run(nch, [&](size_t c) {
@@ -1213,6 +1215,7 @@ int Core::process_default(GroupList& out_groups,
                 k.cnt.assign(nsig, 0);
                 k.lastm.assign(nsig, 0);
                 k.maxm.assign(nsig, 0);
+                bool self = true;
                 for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
                     const uint32_t r = rows[i];
                     if (sel[r] | dec[r]) continue;
@@ -1221,8 +1224,10 @@ int Core::process_default(GroupList& out_groups,
                     const int32_t m = std::max(2, maxc_[r]);
                     k.lastm[sg] = m;
                     k.maxm[sg] = std::max(k.maxm[sg], m);
+                    self = self && self_match_[r] && indexed_[r];
                     k.n++;
                 }
+                k.self = self;
             });
             uint64_t bound = 0;
             for (unsigned c = 0; c < nch; c++)
@@ -1257,13 +1262,45 @@ int Core::process_default(GroupList& out_groups,
             for (unsigned c = 0; c < nch; c++) at[c + 1] = at[c] + ch[c].n;
             grow_to(brow, at[nch]);
             grow_to(brow_group, at[nch]);
+            // The rows bucketed per search in the same sweep (plan_fused: the
+            // pool-parallel replay's plan when every search is its own pool):
+            // pool_rows holds each search's batch rows, ascending.
+            const size_t G = bg.size();
+            fused_plan = G >= 2 && G <= 4096 && par_mode_ &&
+                         std::all_of(ch.begin(), ch.end(), [](const Chunk& k) { return k.self; });
+            std::vector<uint32_t> gat;  // [chunk][search]: the chunk's next position in pool_rows
+            if (fused_plan) {
+                ParPlan& P = par_plan_;
+                grow_to(P.pool_off, G + 1);
+                P.pool_off[0] = 0;
+                for (size_t g = 0; g < G; g++) P.pool_off[g + 1] = P.pool_off[g] + bg[g].nrows;
+                gat.resize(nch * G);
+                for (size_t g = 0; g < G; g++) {
+                    uint32_t run = P.pool_off[g];
+                    for (unsigned c = 0; c < nch; c++) {
+                        gat[c * G + g] = run;
+                        run += ch[c].cnt[bg[g].sig];
+                    }
+                }
+                grow_to(P.pool_rows, at[nch]);
+            }
             wp.run(nch, [&](size_t c) {
                 size_t o = at[c];
+                // the chunk's positions, thread-private (the chunks' rows of gat share cache lines)
+                static thread_local std::vector<uint32_t> gl;
+                uint32_t* ga = nullptr;
+                if (fused_plan) {
+                    gl.assign(gat.begin() + c * G, gat.begin() + (c + 1) * G);
+                    ga = gl.data();
+                }
+                uint32_t* prow = par_plan_.pool_rows.data();
                 for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
                     const uint32_t r = rows[i];
                     if (sel[r] | dec[r]) continue;
+                    const uint32_t gi = (uint32_t)sig_group[sig_[r]];
                     brow[o] = r;
-                    brow_group[o] = (uint32_t)sig_group[sig_[r]];
+                    brow_group[o] = gi;
+                    if (ga) prow[ga[gi]++] = (uint32_t)o;
                     o++;
                 }
             });
@@ -1381,7 +1418,9 @@ int Core::process_default(GroupList& out_groups,
         // a RevThreshold timer that may still fire is read per row: serial replay
         const bool timer_live = rev && timer.armed && !timer.fired;
         rp.run_batch(bg, need_pm, [&] {  // pools bucketed while the searches run
-            if (par_mode_ && !timer_live) plan_parallel(bg, brow, brow_group, plan, stats);
+            if (par_mode_ && !timer_live)
+                (par_asm && fused_plan) ? plan_fused(bg, brow, brow_group, plan, stats)
+                                        : plan_parallel(bg, brow, brow_group, plan, stats);
         });
         auto tb1 = std::chrono::steady_clock::now();
         stats.search_ms += std::chrono::duration<double, std::milli>(tb1 - tb0).count();

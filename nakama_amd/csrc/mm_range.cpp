@@ -138,9 +138,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
         rs_sig_loc_[sg] = (uint32_t)k;
         const Sig& s = sigs_[sg];
         ls_pool[k] = ng == 1 ? 0u : pool_remap_[s.must_terms[0].second];
-        uint32_t nrange = 0;
-        for (uint32_t c = 0; c < s.n_clauses; c++) nrange += clauses_[s.clause_off + c].op == OP_RANGE;
-        ls_q[k + 1] = ls_q[k] + 2 * nrange;
+        ls_q[k + 1] = ls_q[k] + 2 * (uint32_t)s.rs_nrange;
     }
     const uint32_t nq = ls_q[ns];
     // ---- device: pools (posting ranges), tiles, block -> pool, bound queries ----

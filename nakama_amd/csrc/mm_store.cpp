@@ -479,8 +479,10 @@ void Core::sig_describe(Sig& s, const std::vector<DClause>& dc, const CompiledQu
                 ok = false;
             }
         }
-        if (ok && n_term == 1 && n_must_range >= 1 && n_range <= 32 && rf != (int)s.must_terms[0].first)
+        if (ok && n_term == 1 && n_must_range >= 1 && n_range <= 32 && rf != (int)s.must_terms[0].first) {
             s.rs_field = (uint16_t)rf;
+            s.rs_nrange = (uint8_t)n_range;
+        }
     }
 }
 

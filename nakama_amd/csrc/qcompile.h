@@ -48,9 +48,10 @@ enum CompileStatus { CQ_OK = 0, CQ_INVALID = -1, CQ_UNSUPPORTED = -8 };
 // vellum's compiler) rejects, or a fuzziness outside [0, 2], is accepted at Add
 // (RegexpQuery.Validate returns nil, query.go:1271-1273) but fails every search:
 // such a query compiles to QK_MATCHNONE, the outcome of processDefault's
-// `continue` on a search error (matchmaker_process.go:97-101).  Regexp constructs
-// not lowered here (Unicode classes, flag groups, POSIX classes) return
-// CQ_UNSUPPORTED.
+// `continue` on a search error (matchmaker_process.go:97-101).  CQ_UNSUPPORTED is
+// reserved for a construct Go accepts that is not lowered here: none remains
+// (Unicode category and script classes, flag groups incl. (?U), POSIX classes
+// are all lowered, termmatch.h).
 int compile_query(const std::string& q, CompiledQuery* out);
 
 }  // namespace nkm

@@ -33,6 +33,8 @@
 
 namespace nkm {
 
+#define NKM_INLINE inline __attribute__((always_inline))
+
 // Min over leaf intervals with point updates: fan-out 16 levels (a query
 // touches at most two partial blocks per level; 25k leaves are 4 levels).
 struct MinTree16 {
@@ -59,36 +61,47 @@ struct MinTree16 {
             }
         }
     }
-    static uint32_t min16(const uint32_t* p) {
-        uint32_t x = p[0];
-        for (int j = 1; j < 16; j++) x = std::min(x, p[j]);
+    // fixed 16-wide loops: vector mins (4 x 128 bits, or 2 x 256 bits in the
+    // walk's AVX2 instantiation, RangeRun::walk)
+    static NKM_INLINE uint32_t min16(const uint32_t* p) {
+        uint32_t x = kInf;
+        for (int j = 0; j < 16; j++) x = p[j] < x ? p[j] : x;
+        return x;
+    }
+    // min of blk[lo, hi) for a 16-aligned block
+    static NKM_INLINE uint32_t min16_in(const uint32_t* blk, uint32_t lo, uint32_t hi) {
+        uint32_t x = kInf;
+        for (uint32_t j = 0; j < 16; j++) {
+            const uint32_t y = (j >= lo && j < hi) ? blk[j] : kInf;
+            x = y < x ? y : x;
+        }
         return x;
     }
     // min over leaves [a, b)
-    uint32_t range_min(uint32_t a, uint32_t b) const {
+    NKM_INLINE uint32_t range_min(uint32_t a, uint32_t b) const {
         uint32_t m = kInf;
         for (size_t k = 0; a < b; k++) {
             const uint32_t* v = lv[k].data();
-            if ((a >> 4) == ((b - 1) >> 4) || k + 1 == lv.size()) {
-                for (uint32_t i = a; i < b; i++) m = std::min(m, v[i]);
-                break;
+            if ((a >> 4) == ((b - 1) >> 4)) {
+                const uint32_t x = min16_in(v + (a & ~15u), a & 15, ((b - 1) & 15) + 1);
+                return x < m ? x : m;
             }
             if (a & 15) {
-                const uint32_t e = (a | 15) + 1;
-                for (uint32_t i = a; i < e; i++) m = std::min(m, v[i]);
-                a = e;
+                const uint32_t x = min16_in(v + (a & ~15u), a & 15, 16);
+                m = x < m ? x : m;
+                a = (a | 15) + 1;
             }
             if (b & 15) {
-                const uint32_t s = b & ~15u;
-                for (uint32_t i = s; i < b; i++) m = std::min(m, v[i]);
-                b = s;
+                const uint32_t x = min16_in(v + (b & ~15u), 0, b & 15);
+                m = x < m ? x : m;
+                b &= ~15u;
             }
             a >>= 4;
             b >>= 4;
         }
         return m;
     }
-    void set(uint32_t i, uint32_t x) {
+    NKM_INLINE void set(uint32_t i, uint32_t x) {
         lv[0][i] = x;
         for (size_t k = 1; k < lv.size(); k++) {
             const uint32_t blk = i >> 4;
@@ -197,11 +210,11 @@ struct RangeRun {
     RangeSrc* S = nullptr;
     const RRange* rg = nullptr;
     uint32_t cur = 0, end = 0;
-    void mask(uint32_t leaf) {
+    NKM_INLINE void mask(uint32_t leaf) {
         S->tree.set(leaf, MinTree16::kInf);
         masked.push_back(leaf);
     }
-    bool next(uint32_t& leaf) {
+    NKM_INLINE bool next(uint32_t& leaf) {
         while (cur < end) {
             const uint32_t te = rg[cur].tend;
             uint32_t m = MinTree16::kInf;
@@ -234,7 +247,7 @@ struct RangeRun {
     // the searching ticket's party (:80-85) and the count-range musts
     // (MinCount >= T's Min, MaxCount <= T's Max) — are not hits: they are
     // skipped without counting.  Returns MATCHED / NOMATCH; group_out = grp.
-    ReplayCore::Status row(uint32_t T, const RRange* r, uint32_t r0, uint32_t r1) {
+    NKM_INLINE ReplayCore::Status row(uint32_t T, const RRange* r, uint32_t r0, uint32_t r1) {
         const HotRec& ht = v.hot[T];
         const bool last = v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc;
         const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
@@ -351,7 +364,7 @@ struct RangeRun {
     }
 
     // The hits the row masked go back into the tree, except the selected.
-    void unmask() {
+    NKM_INLINE void unmask() {
         for (uint32_t leaf : masked)
             if (!psel[S->slot[leaf]]) S->tree.set(leaf, S->rank[leaf]);
         masked.clear();
@@ -363,11 +376,29 @@ struct RangeRun {
     // restored on return except for the selections (the tree keeps them).
     template <class SigRange>
     void walk(RangeSrc& src, const uint32_t* bis, uint32_t nrows, const uint32_t* brow, SigRange sig_range, PoolOut& o) {
+        if (__builtin_cpu_supports("avx2")) walk_avx2(src, bis, nrows, brow, sig_range, o);
+        else walk_impl(src, bis, nrows, brow, sig_range, o);
+    }
+    template <class SigRange>
+    __attribute__((target("avx2"))) void walk_avx2(RangeSrc& src, const uint32_t* bis, uint32_t nrows,
+                                                   const uint32_t* brow, SigRange sig_range, PoolOut& o) {
+        walk_impl(src, bis, nrows, brow, sig_range, o);
+    }
+    template <class SigRange>
+    NKM_INLINE void walk_impl(RangeSrc& src, const uint32_t* bis, uint32_t nrows, const uint32_t* brow,
+                              SigRange sig_range, PoolOut& o) {
         S = &src;
         uint32_t gcum = 0, xcum = 0;
         for (uint32_t j = 0; j < nrows; j++) {
             const uint32_t bi = bis[j];
             const uint32_t T = brow[bi];
+            if (j + 2 < nrows) {  // the next rows' records (their hits are unknown until searched)
+                const uint32_t T2 = brow[bis[j + 2]];
+                __builtin_prefetch(&v.hot[T2]);
+                __builtin_prefetch(&psel[T2]);
+                __builtin_prefetch(&leaf_of_slot[T2]);
+                __builtin_prefetch(&v.intervals[T2]);
+            }
             if (psel[T]) continue;
             const RRange* base;
             uint32_t r0, r1;

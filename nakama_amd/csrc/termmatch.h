@@ -24,7 +24,7 @@ namespace nkm {
 enum MtStatus {
     MT_OK = 0,
     MT_SEARCH_ERROR = 1,  // bluge accepts the query but every search with it fails (processDefault `continue`)
-    MT_UNSUPPORTED = 2,   // valid in Go, not lowered here (Unicode script classes \p{Greek}, the (?U) flag)
+    MT_UNSUPPORTED = 2,   // reserved: valid in Go, not lowered here (none remain: script classes and (?U) are lowered)
 };
 
 class GoRegexp {
