@@ -172,12 +172,13 @@ def cpu_baseline(args, searches, matched):
     (the reference Go/bluge path cannot run: no Go toolchain),
     bounded to ~10-30 s of CPU: tools/cpu_baseline.py in a child process
     (this process has initialised the GPU; the child never touches it).
-    C3/C4: every pool's per-search cost (a * documents visited + b * hits)
-    measured from two short prefixes of its own pass, all pools concurrently,
-    extrapolated to the pool's pass; C5: whole 1000-ticket chunk passes timed
-    and scaled by the chunk count.  `measured_full_pass`: whole per-pool
-    passes of the same oracle timed offline (tools/make_full_golden.py), and
-    `calibration`: the model against them (profiles/r04_cpu_calib_*.json)."""
+    C2/C3/C4: every pool's per-search time sampled at five points along its
+    own pass (the earlier-matched tickets removed, the next rows searching),
+    all pools concurrently, its pass = searches x the samples' trapezoid
+    mean; C5: every 1000-ticket chunk pass timed whole.  `measured_full_pass`:
+    whole per-pool passes of the same oracle timed offline
+    (tools/make_full_golden.py), and `calibration`: the model against them
+    (profiles/r04_cpu_calib_*.json)."""
     import subprocess
     cmd = [sys.executable, os.path.join(ROOT, "tools", "cpu_baseline.py"), "--config", str(args.config),
            "--tickets", str(args.tickets), "--searches", str(searches), "--matched", str(matched)]
@@ -348,7 +349,7 @@ def main():
                      "kernel": "+".join(sorted(kernels)), "launches": launches, "avg_launch_ms": avg_launch_ms,
                      "bytes_per_launch": eval_bytes / max(1, launches), "rank": 0},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in (3, 4, 5) and not args.override:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in (2, 3, 4, 5) and not args.override:
         out["cpu_baseline"] = cpu_baseline(args, int(statistics.median(searched)), int(statistics.median(matched_all)))
     else:
         out["cpu_baseline"] = None

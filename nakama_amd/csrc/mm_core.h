@@ -692,6 +692,7 @@ private:
         size_t end = 0;      // pass rows consumed (rows[pos, end))
         int S = 8;           // list stride: the longest source, rounded up to 8 / 16 / 32 / 64
         uint64_t scanned = 0;
+        uint64_t unique = 0; // distinct candidates per wave, summed (the loads a wave issues, once each)
         double live_w = 0;   // sum over rows of src_len x the row's per-live-candidate bytes
     };
     bool tier_mode_ = true;  // NKM_TIER=0: variable-score searches never return top-tier lists

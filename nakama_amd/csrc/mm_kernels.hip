@@ -1806,44 +1806,39 @@ __device__ __forceinline__ bool rsrc_less(int64_t ka, uint32_t va, int64_t kb, u
     return ka < kb || (ka == kb && va < vb);
 }
 
-// One tile per workgroup: 8 elements per lane loaded coalesced (the posting
-// entry, then alive / kind / value of that slot), then merged in LDS from
-// runs of 1 up to the tile.
-__global__ __launch_bounds__(kBlock) void rsrc_tile_kernel(DStore st, const DRangePool* __restrict__ pools,
-                                                           const DRangeTile* __restrict__ tiles, int64_t* __restrict__ okey,
-                                                           uint32_t* __restrict__ opos) {
-    constexpr int E = kRsrcTile / kBlock;
+// One tile per workgroup of kRsrcTile lanes, one element each (loaded
+// coalesced: the posting entry, then alive / kind / value of that slot), then
+// merged in LDS from runs of 1 up to the tile: each lane's binary search in
+// the partner run is log2(run) dependent LDS reads, one element per lane.
+constexpr int kRsrcBlock = (int)kRsrcTile;
+__global__ __launch_bounds__(kRsrcBlock) void rsrc_tile_kernel(DStore st, const DRangePool* __restrict__ pools,
+                                                               const DRangeTile* __restrict__ tiles,
+                                                               int64_t* __restrict__ okey, uint32_t* __restrict__ opos) {
     __shared__ int64_t sk[2][kRsrcTile];
     __shared__ uint32_t sv[2][kRsrcTile];
     const DRangeTile t = tiles[blockIdx.x];
     const DRangePool P = pools[t.pool];
     const int64_t* __restrict__ fv = st.fval[P.field];
     const uint8_t* __restrict__ fk = st.fkind[P.field];
-#pragma unroll
-    for (int j = 0; j < E; j++) {
-        const uint32_t e = threadIdx.x + j * kBlock;
-        const uint32_t i = t.start + e;  // position in the pool's source
-        int64_t k = INT64_MAX;
-        uint32_t v = kRsrcInvalid | i;
-        if (e < t.len && i < P.src_len) {
-            const uint32_t s = st.postings[P.src_off + i];
-            if (st.alive[s] && fk[s] == KIND_NUMERIC) {
-                k = fv[s];
-                v = i;
-            }
+    const uint32_t e = threadIdx.x;
+    const uint32_t i = t.start + e;  // position in the pool's source
+    int64_t k = INT64_MAX;
+    uint32_t v = kRsrcInvalid | i;
+    if (e < t.len && i < P.src_len) {
+        const uint32_t s = st.postings[P.src_off + i];
+        if (st.alive[s] && fk[s] == KIND_NUMERIC) {
+            k = fv[s];
+            v = i;
         }
-        sk[0][e] = k;
-        sv[0][e] = v;
     }
+    sk[0][e] = k;
+    sv[0][e] = v;
     __syncthreads();
     int b = 0;
     for (uint32_t r = 1; r < t.len; r <<= 1, b ^= 1) {
-#pragma unroll
-        for (int j = 0; j < E; j++) {
-            const uint32_t e = threadIdx.x + j * kBlock;
-            if (e >= t.len) continue;
-            const int64_t k = sk[b][e];
-            const uint32_t v = sv[b][e];
+        if (e < t.len) {
+            k = sk[b][e];  // the element now at this position
+            v = sv[b][e];
             const uint32_t run = e / r, ps = (run ^ 1u) * r;
             uint32_t o = e;
             if (ps < t.len) {
@@ -1860,14 +1855,10 @@ __global__ __launch_bounds__(kBlock) void rsrc_tile_kernel(DStore st, const DRan
         }
         __syncthreads();
     }
-    const uint64_t base = (uint64_t)P.out_off + t.start;
-#pragma unroll
-    for (int j = 0; j < E; j++) {
-        const uint32_t e = threadIdx.x + j * kBlock;
-        if (e < t.len) {
-            okey[base + e] = sk[b][e];
-            opos[base + e] = sv[b][e];
-        }
+    if (e < t.len) {
+        const uint64_t base = (uint64_t)P.out_off + t.start;
+        okey[base + e] = sk[b][e];
+        opos[base + e] = sv[b][e];
     }
 }
 
@@ -1930,8 +1921,8 @@ hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max
     *n_merge = 0;
     if (n_elems == 0 || n_tiles == 0) return hipSuccess;
     if (n_elems % kBlock) return hipErrorInvalidValue;
-    hipExtLaunchKernelGGL(rsrc_tile_kernel, dim3(n_tiles), dim3(kBlock), 0, stream, ev_tile0, ev_tile1, 0, st, d_pools,
-                          d_tiles, d_key[0], d_pos[0]);
+    hipExtLaunchKernelGGL(rsrc_tile_kernel, dim3(n_tiles), dim3(kRsrcBlock), 0, stream, ev_tile0, ev_tile1, 0, st,
+                          d_pools, d_tiles, d_key[0], d_pos[0]);
     int b = 0, m = 0;
     for (uint32_t R = kRsrcTile; R < max_pad; R <<= 1, b ^= 1, m++) {
         if (m >= max_merge) return hipErrorInvalidValue;

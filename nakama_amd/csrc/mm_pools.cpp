@@ -1076,6 +1076,38 @@ bool Core::assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t
         pb.live_w += live_w[c];
     }
     while ((uint32_t)pb.S < mx) pb.S *= 2;
+    // distinct candidates per wave (its 64 / S rows' source ranges merged):
+    // what the wave's loads bring in, each once (the roofline's bytes; C5's
+    // square waves: the 8 rows ARE their shared source, 8 candidates)
+    const uint32_t rpw = 64u / (uint32_t)pb.S;
+    const size_t nw = (n + rpw - 1) / rpw;
+    const size_t wch = par && nw >= 4096 ? (size_t)wp.size() * 4 : 1;
+    std::vector<uint64_t> uniq(wch, 0);
+    auto pass3 = [&](size_t c) {
+        uint64_t u = 0;
+        std::pair<uint64_t, uint64_t> rg[64];
+        for (size_t w = nw * c / wch; w < nw * (c + 1) / wch; w++) {
+            const size_t r0 = w * rpw, r1 = std::min(n, r0 + rpw);
+            int k = 0;
+            for (size_t r = r0; r < r1; r++) {
+                const DSmallRow& d = h_srows_.p[r];
+                const uint64_t base = (d.src_len & kSrcOrder) ? (1ull << 40) : 0;  // order[] vs postings[]
+                const uint64_t a = base + d.src_off;
+                rg[k++] = {a, a + (d.src_len & ~kSrcOrder)};
+            }
+            std::sort(rg, rg + k);
+            uint64_t hi = 0;
+            for (int q = 0; q < k; q++) {
+                const uint64_t lo = std::max(rg[q].first, hi);
+                if (rg[q].second > lo) u += rg[q].second - lo;
+                hi = std::max(hi, rg[q].second);
+            }
+        }
+        uniq[c] = u;
+    };
+    if (wch > 1) wp.run(wch, pass3);
+    else pass3(0);
+    for (uint64_t u : uniq) pb.unique += u;
     return true;
 }
 
@@ -1109,13 +1141,18 @@ PackLayout Core::run_packed(const PackBatch& pb, PassStats& stats, const std::fu
         ents += lw[2 * b + 1];
     }
     // algorithmic bytes: per row its descriptor and its query / count range;
-    // per scanned candidate slot id + alive; per live candidate the columns
-    // (average of the rows' per-live bytes, weighted by source length); per
-    // entry its slot id; per row its pair words, reverse bits and count
+    // per distinct candidate of a wave (pb.unique: the wave's loads bring each
+    // in once, the S x S evaluations re-read them from L1 / LDS) its slot id,
+    // alive flag and columns, query descriptor and clauses (the rows' average
+    // per-candidate bytes, weighted by source length); per entry its slot id;
+    // per row its pair words, reverse bits and count.  (Rounds 1-3 charged
+    // every (row, candidate) pair's loads: C5 894 MB per launch vs 170 MB of
+    // PMC traffic, profiles/r04q_c5_traffic.json.)
+    (void)live;
     const double per_live = pb.scanned ? pb.live_w / (double)pb.scanned : 0.0;
     const int P = pb.S < 32 ? pb.S : 32;
-    stats.k_bytes[3] += (int64_t)pb.n * (int64_t)(sizeof(DSmallRow) + 16) + (int64_t)pb.scanned * 5 +
-                        (int64_t)((double)live * per_live) + (int64_t)ents * 4 +
+    stats.k_bytes[3] += (int64_t)pb.n * (int64_t)(sizeof(DSmallRow) + 16) +
+                        (int64_t)((double)pb.unique * (5.0 + per_live)) + (int64_t)ents * 4 +
                         (int64_t)pb.n * (int64_t)(P * L.pm_w + L.rev_w + 1);
     stats.pair_evals += (int64_t)pb.scanned;
     return L;

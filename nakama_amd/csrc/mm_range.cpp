@@ -255,6 +255,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     RowRec* rr = few ? nullptr : row_recs_.data();
     if (!few) std::memset((void*)rr, 0, nb * sizeof(RowRec));
     std::vector<uint64_t> task_hits(ntask, 0);
+    std::vector<double> pool_build_ms(ng, 0.0), pool_walk_ms(ng, 0.0);  // NKM_PROFILE=2
     // each pool's valid candidates: a prefix of its sorted elements
     std::vector<uint32_t> valid(ng, 0);
     for (size_t p = 0; p < ng; p++) {
@@ -303,6 +304,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
         run.psel = tl_sel.data();
         run.proc = tl_proc.data();
         run.leaf_of_slot = rs_leaf_.data();
+        run.fast = fast_mode_;
         run.hits_seen = 0;
         static thread_local PoolOut o;
         auto& ents = task_ents_[t];
@@ -311,6 +313,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             const uint32_t p = order_p[k];
             RangePoolHost& H = rs_pools_[p];
             const DRangePool& d = H.d;
+            const auto tb0 = clk::now();
             const uint32_t* pv = h_rpos_.p + d.out_off;
             const uint32_t nv = valid[p];
             grow_to(H.slot, nv);
@@ -318,6 +321,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             grow_to(H.leaf_of, d.src_len);
             for (uint32_t j = 0; j < nv; j++) {
                 const uint32_t rk = pv[j];
+                if (rk >= d.src_len) throw DeviceError{hipErrorUnknown, "range source: a sorted position out of range", __LINE__};
                 const uint32_t s = postings_[d.src_off + rk];
                 H.rank[j] = rk;
                 H.slot[j] = s;
@@ -329,6 +333,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             H.src.rank = H.rank.data();
             H.src.leaf_of = H.leaf_of.data();
             H.src.tree.build(H.rank.data(), nv);
+            const auto tb1 = clk::now();
             PoolOut& po = few ? pool_outs_[p] : o;
             po.recs.clear();
             po.ents.clear();
@@ -340,6 +345,8 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
                          r1 = ls_t1[ls];
                      },
                      po);
+            pool_walk_ms[p] = msd(tb1, clk::now());
+            pool_build_ms[p] = msd(tb0, tb1);
             for (uint32_t j = 0; j < nv; j++) rs_leaf_[H.slot[j]] = kNoSlot;
             if (!few) {
                 const uint32_t base = (uint32_t)ents.size();
@@ -375,12 +382,16 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     stats.par_gather_ms += msd(t2, t2b);
     stats.par_work_ms += msd(t2, t3);
     stats.par_merge_ms += msd(t3, t4);
-    if (batch_profile_)
+    if (batch_profile_) {
+        const size_t pm = (size_t)(std::max_element(pool_walk_ms.begin(), pool_walk_ms.end()) - pool_walk_ms.begin());
         std::fprintf(stderr,
                      "[nkm]   batch %d (range): rows %zu pools %zu signatures %zu candidates %llu (valid %llu), %d merges "
-                     "| plan %.2f device %.2f tiers %.2f walks %.2f merge %.2f ms\n",
+                     "| plan %.2f device %.2f tiers %.2f walks %.2f merge %.2f ms | slowest pool: %u rows, build %.2f "
+                     "walk %.2f ms\n",
                      stats.batches, nb, ng, ns, (unsigned long long)src_total, (unsigned long long)nvalid, n_merge,
-                     msd(t0, t1), msd(t1, t2), msd(t2, t2b), msd(t2b, t3), msd(t3, t4));
+                     msd(t0, t1), msd(t1, t2), msd(t2, t2b), msd(t2b, t3), msd(t3, t4), (unsigned)prows(pm),
+                     pool_build_ms[pm], pool_walk_ms[pm]);
+    }
     return true;
 }
 

@@ -204,6 +204,8 @@ struct RangeRun {
     std::vector<uint32_t> cmask, open, masked;
     std::vector<std::pair<uint32_t, int>> grp;
     uint64_t hits_seen = 0;
+    bool fast = true;  // fast_row() for the rows it covers (NKM_FAST=0: row() only)
+    FastCombos fcb;
 
     // iterator over one row's hits: tier by tier, smallest rank first;
     // every hit read is masked until the row ends
@@ -247,6 +249,79 @@ struct RangeRun {
     // the searching ticket's party (:80-85) and the count-range musts
     // (MinCount >= T's Min, MaxCount <= T's Max) — are not hits: they are
     // skipped without counting.  Returns MATCHED / NOMATCH; group_out = grp.
+    // row() when no two live tickets share a session (ReplayCore::fast_row
+    // without the reverse checks): a combo is its member slots and entry
+    // count.  BAIL when the row reaches the CountMultiple trim or outgrows the
+    // fixed combos: nothing is selected yet, the caller restores the masks and
+    // takes row().
+    NKM_INLINE ReplayCore::Status fast_row(uint32_t T, const RRange* r, uint32_t r0, uint32_t r1) {
+        const HotRec& ht = v.hot[T];
+        const bool last = v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc;
+        const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
+        const int room = tmax - tcount;
+        const uint32_t tparty = ht.party;
+        auto is_hit = [&](const HotRec& hh) {
+            return !(tparty != kNoParty && hh.party == tparty) && hh.minc >= tmin && hh.maxc <= tmax;
+        };
+        rg = r;
+        cur = r0;
+        end = r1;
+        masked.clear();
+        if (leaf_of_slot[T] != kNoSlot) mask(leaf_of_slot[T]);
+        int ncomb = 0;
+        uint32_t leaf;
+        while (next(leaf)) {
+            const uint32_t H = S->slot[leaf];
+            mask(leaf);
+            const HotRec& hh = v.hot[H];
+            if (!is_hit(hh)) continue;
+            hits_seen++;
+            if (tmax < hh.maxc && v.intervals[H] + proc[H] <= max_intervals) continue;  // :150-153
+            const int hc = hh.count;
+            int f = 0;  // first fit (:167-226)
+            while (f < ncomb && fcb.size[f] + hc > room) f++;
+            if (f == ncomb) {
+                if (f == kFastComb) return ReplayCore::BAIL;
+                fcb.size[f] = 0;
+                fcb.nmem[f] = 0;
+                ncomb++;
+            } else if (fcb.nmem[f] == (uint32_t)kFastMem) {
+                return ReplayCore::BAIL;
+            }
+            fcb.size[f] += hc;
+            fcb.mem[f][fcb.nmem[f]++] = H;
+            const int l = fcb.size[f] + tcount;
+            bool form = l == tmax;  // :233
+            if (!form && last && l >= tmin && l <= tmax) {
+                bool more = false;
+                uint32_t pl;
+                while (!more && next(pl)) {
+                    if (is_hit(v.hot[S->slot[pl]])) more = true;
+                    else mask(pl);
+                }
+                form = !more;
+            }
+            if (!form) continue;
+            if (l % tcm != 0) return ReplayCore::BAIL;
+            bool failed = false;  // :287-296
+            for (uint32_t k = 0; k < fcb.nmem[f] && !failed; k++) {
+                const uint32_t m = fcb.mem[f][k];
+                if (!v.live[m]) continue;
+                const HotRec& hs = v.hot[m];
+                failed = hs.minc > l || hs.maxc < l || l % hs.cm != 0;
+            }
+            if (failed) continue;
+            grp.clear();
+            for (uint32_t k = 0; k < fcb.nmem[f]; k++) {
+                const uint32_t m = fcb.mem[f][k];
+                for (int e = 0; e < v.hot[m].count; e++) grp.push_back({m, e});
+            }
+            for (int e = 0; e < tcount; e++) grp.push_back({T, e});
+            return ReplayCore::MATCHED;
+        }
+        return ReplayCore::NOMATCH;
+    }
+
     NKM_INLINE ReplayCore::Status row(uint32_t T, const RRange* r, uint32_t r0, uint32_t r1) {
         const HotRec& ht = v.hot[T];
         const bool last = v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc;
@@ -403,7 +478,11 @@ struct RangeRun {
             const RRange* base;
             uint32_t r0, r1;
             sig_range(bi, base, r0, r1);
-            const auto status = row(T, base, r0, r1);
+            auto status = fast && v.sessions_exclusive ? fast_row(T, base, r0, r1) : ReplayCore::BAIL;
+            if (status == ReplayCore::BAIL) {
+                unmask();  // nothing selected yet: every mask goes back
+                status = row(T, base, r0, r1);
+            }
             const HotRec& ht = v.hot[T];
             PoolRec rec{bi, 0, (uint8_t)(v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc),
                         (uint32_t)o.ents.size(), 0, gcum, xcum};

@@ -5,7 +5,7 @@ ways — replay_pool (replay_core.h) over every row's full hit list in the
 reference's order (score desc, created_at asc; matchmaker_process.go:86-130),
 and RangeRun over a min tree of the value-sorted candidates with build_tiers'
 tier lists — and exits 1 unless the records and group entries are identical.
-Solo 1v1 rows, and mixed rows (parties, shared sessions, Min < Max,
+Solo 1v1 rows, and mixed rows (parties, shared or exclusive sessions, Min < Max,
 CountMultiple, Intervals, MUST_NOT and fractional-boost ranges, candidates
 without a number in the field).
 """
@@ -25,7 +25,11 @@ def range_bench(tmp_path_factory):
 
 
 @pytest.mark.parametrize("n,mode,seed", [(3000, "solo", 1), (3000, "mixed", 1), (3000, "mixed", 2), (1200, "mixed", 7),
-                                         (64, "mixed", 3), (1, "solo", 4)])
-def test_range_walk_equals_list_replay(range_bench, n, mode, seed):
-    out = subprocess.run([range_bench, str(n), mode, str(seed)], capture_output=True, text=True, timeout=120)
+                                         (64, "mixed", 3), (1, "solo", 4), (3000, "mixedx", 1), (2000, "mixedx", 5)])
+@pytest.mark.parametrize("body", ["fast", "exact"])
+def test_range_walk_equals_list_replay(range_bench, n, mode, seed, body):
+    """mixedx: exclusive sessions, so the fast body runs (bailing to the exact
+    one at the CountMultiple trim); "exact" forces the exact body."""
+    out = subprocess.run([range_bench, str(n), mode, str(seed), "ref", body], capture_output=True, text=True,
+                         timeout=120)
     assert out.returncode == 0 and "MATCH" in out.stdout, out.stdout + out.stderr

@@ -45,7 +45,10 @@ from concurrent.futures import ProcessPoolExecutor
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-N_POOLS = {3: 8, 4: 64}
+N_POOLS = {2: 4, 3: 8, 4: 64}
+# searching rows per sample: enough searches for a stable per-search time
+# (C3: ~10 rows per group; C2 / C4: 2)
+POOL_ROWS = {2: 200, 3: 400, 4: 100}
 C5_CHUNK = 1000
 
 
@@ -206,7 +209,7 @@ def main():
     ap.add_argument("--tickets", type=int)
     ap.add_argument("--searches", type=float, help="searches of the measured GPU pass (whole set)")
     ap.add_argument("--matched", type=float, help="tickets the measured GPU pass matched")
-    ap.add_argument("--pool-rows", type=int, default=100)
+    ap.add_argument("--pool-rows", type=int, default=0, help="searching rows per sample (default POOL_ROWS)")
     ap.add_argument("--chunks", type=int, default=1000, help="C5: chunk passes timed (all 1000: the whole pass)")
     ap.add_argument("--workers", type=int, default=0, help="concurrent pool processes (default: the usable cores, <= 16)")
     a = ap.parse_args()
@@ -215,7 +218,8 @@ def main():
     if a.record:
         return record(a.record)
     if a.calibrate:
-        return calibrate(a.calibrate, a.pool_rows, workers)
+        cfg = json.load(open(os.path.join(ROOT, "tests", "golden", f"full_{a.calibrate}.json")))["config"]
+        return calibrate(a.calibrate, a.pool_rows or POOL_ROWS[cfg], workers)
     out = {"host": {"cpu_model": model, "nproc": ncpu, "usable_cores": usable}, "algorithm": (
         "oracle restatement (port): per search a visit of every document of its index + a heap of the hits in "
         "the reference's sort order; searches visit their own pool's index (the cost class of bluge's posting-"
@@ -223,13 +227,14 @@ def main():
     if a.config in N_POOLS:
         npools = N_POOLS[a.config]
         w = max(1, min(npools, workers))
-        t, h, per, wall = per_pool(a.config, a.tickets, a.pool_rows, a.searches, a.matched, w)
+        rows = a.pool_rows or POOL_ROWS[a.config]
+        t, h, per, wall = per_pool(a.config, a.tickets, rows, a.searches, a.matched, w)
         rounds = math.ceil(npools / w)
         par = max(per) * rounds if rounds > 1 else max(per)
         out["value"] = a.matched / sum(per)
         out["cores"] = 1
         out["sample"] = (f"EXTRAPOLATED per pool: per-search times SAMPLED at {SAMPLES} points of each pool's own "
-                         f"pass ({a.pool_rows} searching rows each, the earlier-matched tickets removed), TIMED "
+                         f"pass ({rows} searching rows each, the earlier-matched tickets removed), TIMED "
                          f"concurrently on {w} cores, pass = searches x their trapezoid mean "
                          f"(profiles/r04_cpu_calib_c*.json checks it against measured whole passes): {npools} pools "
                          f"of ~{h[0][0]} tickets, one-core time = sum of the pools' passes {sum(per):.0f} s")

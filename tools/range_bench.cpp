@@ -9,7 +9,7 @@
 // number in the field).  The hit lists apply the device search's filters (the
 // searching ticket's party, MinCount >= Min, MaxCount <= Max).
 //
-//   tools/range_bench [tickets] [mode: solo|mixed] [seed] [noref: time the walk only]
+//   tools/range_bench [tickets] [mode: solo|mixed|mixedx] [seed] [noref|ref] [exact: no fast body]
 // prints the records' checksum for both and the walk time; exit status 1 when
 // they differ.
 #include <algorithm>
@@ -46,7 +46,10 @@ static double now_ms() {
 
 int main(int argc, char** argv) {
     const uint32_t N = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 5000;
-    const bool mixed = argc > 2 && std::string(argv[2]) == "mixed";
+    // mixed: shared sessions too (the exact row body); mixedx: exclusive
+    // sessions (the fast body, bailing to the exact one at the CountMultiple trim)
+    const bool mixed = argc > 2 && (std::string(argv[2]) == "mixed" || std::string(argv[2]) == "mixedx");
+    const bool share = argc > 2 && std::string(argv[2]) == "mixed";
     uint64_t seed = argc > 3 ? std::strtoull(argv[3], nullptr, 10) : 1;
     const int maxI = 3;
     // ---- tickets ----
@@ -83,7 +86,7 @@ int main(int argc, char** argv) {
         h.smask = 0;
         for (int p = 0; p < c; p++) {
             uint32_t s = i * 4 + (uint32_t)p;
-            if (mixed && i > 0 && uni(seed) < 0.03) {  // an earlier ticket's session
+            if (share && i > 0 && uni(seed) < 0.03) {  // an earlier ticket's session
                 const uint32_t j = (uint32_t)(splitmix(seed) % i);
                 s = pres_sess[hot[j].pres_off];
                 shared = true;
@@ -200,6 +203,7 @@ int main(int argc, char** argv) {
     run.psel = psel.data();
     run.proc = proc2.data();
     run.leaf_of_slot = leaf_of_slot.data();
+    run.fast = !(argc > 5 && std::string(argv[5]) == "exact");
     PoolOut out;
     run.walk(src, bis.data(), N, brow.data(),
              [&](uint32_t bi, const RRange*& base, uint32_t& a, uint32_t& b) {
@@ -226,6 +230,6 @@ int main(int argc, char** argv) {
                 "(tiers %.2f ms, walk %.2f ms = %.0f ns/row, %llu hits) | %s\n",
                 N, mixed ? "mixed" : "solo", shared ? ", shared sessions" : "", groups, (unsigned long long)a, r1 - r0,
                 (unsigned long long)b, w1 - w0, w2 - w1, (w2 - w1) * 1e6 / N, (unsigned long long)run.hits_seen,
-                a == b ? "MATCH" : "DIFFER");
+                no_ref ? "timing only" : a == b ? "MATCH" : "DIFFER");
     return a == b || no_ref ? 0 : 1;
 }
