@@ -168,17 +168,20 @@ struct Sig {
 // workers and the caller, and returns when all n tasks are done.
 class WorkPool {
 public:
-    // cpus: optional placement for the workers (worker i -> cpus[i % size]).
-    explicit WorkPool(unsigned n_threads, const std::vector<int>& cpus = {}) {
+    // cpus: optional placement for the workers (worker i -> cpus[i % size]);
+    // else `area`: every worker may run on any of those CPUs (none: anywhere).
+    explicit WorkPool(unsigned n_threads, const std::vector<int>& cpus = {}, const std::vector<int>& area = {}) {
         for (unsigned i = 0; i + 1 < n_threads; i++) {
             const int cpu = cpus.empty() ? -1 : cpus[i % cpus.size()];
-            th_.emplace_back([this, cpu] {
+            th_.emplace_back([this, cpu, area] {
                 if (cpu >= 0) pin(cpu);
+                else if (!area.empty()) pin_set(area);
                 loop();
             });
         }
     }
     static void pin(int cpu);
+    static void pin_set(const std::vector<int>& cpus);
     ~WorkPool() {
         {
             std::lock_guard<std::mutex> lk(m_);

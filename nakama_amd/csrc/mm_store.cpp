@@ -142,6 +142,14 @@ void WorkPool::pin(int cpu) {
     (void)pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
 }
 
+void WorkPool::pin_set(const std::vector<int>& cpus) {
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    for (int c : cpus)
+        if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &cs);
+    (void)pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
+}
+
 namespace {
 std::vector<int> parse_cpulist(const std::string& path) {  // "0-3,8,10-11"
     std::vector<int> out;
@@ -168,12 +176,37 @@ std::vector<int> parse_cpulist(const std::string& path) {  // "0-3,8,10-11"
 }
 }  // namespace
 
-// Worker placement: the host phases walk store columns that the inserting
-// thread first-touched, so workers go next to the calling thread — first the
-// physical cores sharing its L3, then the rest of its NUMA node (one hardware
-// thread per core before any SMT sibling).  Opt-in (NKM_PIN=1): on a host
-// shared with other jobs a pinned worker cannot move off a busy core, and the
-// OS placement measured better there.
+// The CPUs of the calling thread's NUMA node (that the process may use), or
+// none when the host has one node.  Default worker placement: every worker may
+// run anywhere on that node, so the OS still moves it off a busy core, but it
+// never leaves the socket whose memory the store was first-touched on (MI355X
+// boxes: 2 x EPYC 9575F, 2 NUMA nodes; unrestricted workers drifting to the
+// other socket made every walk's store access remote: C2 p50 5.44 -> 3.31 ms,
+// C3 5.42 -> 4.73 ms with node-local workers, profiles/r04n_pin.txt).
+static std::vector<int> node_cpus() {
+    std::vector<int> out;
+    const int cpu = sched_getcpu();
+    cpu_set_t allowed;
+    if (cpu < 0 || sched_getaffinity(0, sizeof allowed, &allowed) != 0) return out;
+    int nodes = 0;
+    std::vector<int> mine;
+    for (int nd = 0; nd < 64; nd++) {
+        std::vector<int> l = parse_cpulist("/sys/devices/system/node/node" + std::to_string(nd) + "/cpulist");
+        if (l.empty()) continue;
+        nodes++;
+        if (std::find(l.begin(), l.end(), cpu) != l.end()) mine = l;
+    }
+    if (nodes < 2) return out;
+    for (int c : mine)
+        if (c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) out.push_back(c);
+    return out;
+}
+
+// Worker placement NKM_PIN=1: each worker pinned to one CPU next to the
+// calling thread — first the physical cores sharing its L3, then the rest of
+// its NUMA node (one hardware thread per core before any SMT sibling).  On a
+// host shared with other jobs a pinned worker cannot move off a busy core
+// (the default node-wide placement can).
 static std::vector<int> worker_cpus(unsigned want) {
     std::vector<int> out;
     const char* e = std::getenv("NKM_PIN");
@@ -236,7 +269,10 @@ WorkPool& Core::workers() {
         n /= std::max(1u, host_share_);  // sub-handles of one multi handle (mm_multi.cpp) split them too
         n = std::max(1u, std::min(16u, n));
         if (const char* e = std::getenv("NKM_THREADS")) n = std::max(1, std::atoi(e));
-        workers_.reset(new WorkPool(n, worker_cpus(n - 1)));
+        // NKM_PIN: unset = node-local workers (node_cpus), 1 = one CPU each, 0 = no placement
+        const char* pe = std::getenv("NKM_PIN");
+        const bool node_wide = !pe || (std::strcmp(pe, "0") && std::strcmp(pe, "1"));
+        workers_.reset(new WorkPool(n, worker_cpus(n - 1), node_wide ? node_cpus() : std::vector<int>{}));
     }
     return *workers_;
 }
