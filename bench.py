@@ -73,6 +73,8 @@ def parse():
                     help="tickets per GPU per step (C3), or in total (C4, C5); default 1M (C4: 4M)")
     ap.add_argument("--cpu-rows", type=int, default=24, help="active rows in the CPU-baseline prefix sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="do not bind the process to one NUMA node (default: local rank r of L on node r * nodes / L)")
     ap.add_argument("--override", action="store_true",
                     help="register a MatchmakerOverride (processCustom path): the timed step is the candidate pass, "
                          "a native first-disjoint override and mm_process_commit (per rank under the cluster front)")
@@ -211,8 +213,44 @@ def make_set(args, world, rank, step):
     return synth.TicketSet(args.config, n, first=lo, pool_groups=groups)
 
 
+def numa_bind(local_rank, local_world):
+    """Binds this process to one NUMA node (numactl --cpunodebind): local
+    rank r of L to node r * nodes // L (an 8-GPU node's GPUs 0-3 / 4-7 hang off
+    its two sockets), a single rank to the node it runs on.  The library's
+    host workers stay on the calling thread's node (mm_store.cpp node_cpus);
+    this keeps the caller there too.  Returns the node or None."""
+    try:
+        allowed = os.sched_getaffinity(0)
+        nodes = []
+        for nd in range(64):
+            path = f"/sys/devices/system/node/node{nd}/cpulist"
+            if not os.path.exists(path):
+                continue
+            cpus = set()
+            for part in open(path).read().strip().split(","):
+                if part:
+                    a, _, b = part.partition("-")
+                    cpus.update(range(int(a), int(b or a) + 1))
+            nodes.append((nd, cpus & allowed))
+        nodes = [(nd, c) for nd, c in nodes if c]
+        if len(nodes) < 2:
+            return None
+        if local_world > 1:
+            nd, cpus = nodes[local_rank * len(nodes) // local_world]
+        else:
+            import ctypes
+            here = ctypes.CDLL(None).sched_getcpu()
+            nd, cpus = next(((n, c) for n, c in nodes if here in c), nodes[0])
+        os.sched_setaffinity(0, cpus)
+        return nd
+    except OSError:
+        return None
+
+
 def main():
     args = parse()
+    if not args.no_numa_bind:
+        numa_bind(int(os.environ.get("LOCAL_RANK", "0")), int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
     world, rank, local, pg, backend = dist_setup(args)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
@@ -232,7 +270,7 @@ def main():
                                        comm_device=torch.device("cuda", local) if backend == "nccl" else None,
                                        override_commit=synth.override_commit if args.override else None)
     times, matched_all, presences_all, ins_times, searched = [], [], [], [], []
-    eval_ms = eval_bytes = launches = pair_evals = cands = 0
+    eval_ms = eval_bytes = launches = pair_evals = pairs_decided = cands = 0
     batches, kernels, unroutable = [], set(), 0
     breakdown = {"local_call_ms": [], "summary_ms": [], "merge_ms": []}  # rank 0's cluster-pass phases
     for step in range(args.warmup + args.steps):
@@ -259,7 +297,8 @@ def main():
             n_groups, matched, pres, r = mm.process_summary(out)  # untimed: counts the groups, frees them
             st = {"eval_ms": r.eval_ms, "eval_bytes": r.eval_bytes, "eval_launches": r.eval_launches,
                   "n_batches": r.n_batches, "eval_kernel": r.eval_kernel,
-                  "pair_evals": cand_pe if args.override else r.pair_evals, "candidates": n_cands}
+                  "pair_evals": cand_pe if args.override else r.pair_evals, "pairs_decided": r.pairs_decided,
+                  "candidates": n_cands}
         else:
             n_groups, matched, pres = cp.n_groups, cp.matched_tickets, cp.matched_presences
             st = cp.local_stats
@@ -279,6 +318,7 @@ def main():
             eval_bytes += st["eval_bytes"]
             launches += st["eval_launches"]
             pair_evals += st.get("pair_evals", 0)
+            pairs_decided += st.get("pairs_decided", 0)
             cands += st.get("candidates", 0)
             batches.append(st["n_batches"])
             kernels.add(KERNELS.get(st["eval_kernel"], str(st["eval_kernel"])))
@@ -286,6 +326,7 @@ def main():
         mm.Remove([t.ticket for t in mm.Extract()]) if mm.ticket_count() else None
     total_t = sum(times)
     pair_evals = sum_over_ranks(pg, local, pair_evals)  # whole job (each rank counted its own pass)
+    pairs_decided = sum_over_ranks(pg, local, pairs_decided)
     value = sum(matched_all) / total_t
     achieved = (eval_bytes / 1e9) / (eval_ms / 1e3) if eval_ms > 0 else 0.0
     avg_launch_ms = eval_ms / max(1, launches)
@@ -322,9 +363,15 @@ def main():
         "ms_per_step": 1e3 * total_t / args.steps,
         "p50_ms": 1e3 * statistics.median(times),
         "presences_per_s": sum(presences_all) / total_t,
-        # (row, candidate) predicate evaluations the pass's searches issued
-        # (BASELINE.md GPU-side reporting), per second of the timed steps
+        # (row, candidate) predicate evaluations the device issued: one per
+        # candidate scanned by a search (a shared search decides all its rows
+        # at once; the hashed scan tests each candidate against the one
+        # signature its values select), per second of the timed steps
         "pair_evals_per_s": pair_evals / total_t,
+        # (row, candidate) pairs decided: over the rows that searched, the
+        # candidates of their search's source — what the reference's per-row
+        # bluge search evaluates (BASELINE.md GPU-side reporting), summed over ranks
+        "pairs_decided_per_s": pairs_decided / total_t,
         # the host-to-HBM hand-over: the Insert() call that precedes each pass
         # (not part of value: inputs are resident when the timed region starts)
         "insert_ms": 1e3 * statistics.median(ins_times),
@@ -387,7 +434,7 @@ def main_multi(args, world, rank, local, pg):
                                         override=(lambda groups: groups) if args.override else None,
                                         multi=dict(devices=devs, mode=mode, pool_fields=list(POOL_FIELDS[args.config])))
     times, matched_all, presences_all, ins_times = [], [], [], []
-    eval_ms = eval_bytes = launches = pair_evals = cands = 0
+    eval_ms = eval_bytes = launches = pair_evals = pairs_decided = cands = 0
     batches, kernels = [], set()
     for step in range(args.warmup + args.steps):
         ins_dt = dt = 0.0
@@ -421,6 +468,7 @@ def main_multi(args, world, rank, local, pg):
                 eval_bytes += r.eval_bytes
                 launches += r.eval_launches
                 pair_evals += cand_pe if args.override else r.pair_evals
+                pairs_decided += r.pairs_decided
                 cands += n_cands
                 batches.append(r.n_batches)
                 kernels.add(KERNELS.get(r.eval_kernel, str(r.eval_kernel)))
@@ -440,6 +488,7 @@ def main_multi(args, world, rank, local, pg):
             "p50_ms": 1e3 * statistics.median(times),
             "presences_per_s": sum(presences_all) / total_t,
             "pair_evals_per_s": pair_evals / total_t,
+            "pairs_decided_per_s": pairs_decided / total_t,
             "insert_ms": 1e3 * statistics.median(ins_times),
             "with_insert_tickets_per_s": sum(matched_all) / (total_t + sum(ins_times)),
             "higher_is_better": True,

@@ -131,6 +131,9 @@ typedef struct mm_matched {
     int32_t full_lists;             /* variable-score searches run as full lists (host-sorted), 0 for the oracle */
     const int64_t* group_created;   /* n_groups: CreatedAt of each group's last entry (its searching ticket) — the
                                        key a pool-sharded cluster merges rank results by (ABI 3) */
+    int64_t pairs_decided;          /* (row, candidate) pairs the pass decided: over the rows that searched, the
+                                       candidates their search's source holds — what the reference's per-row
+                                       bluge search evaluates (ABI 4) */
 } mm_matched;
 
 typedef struct mm_extract_list {

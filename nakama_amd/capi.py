@@ -113,7 +113,7 @@ class mm_matched(C.Structure):
                 ("pass_ms", C.c_double), ("eval_ms", C.c_double), ("pair_evals", C.c_int64),
                 ("reserved2", C.c_int64), ("eval_bytes", C.c_int64), ("eval_launches", C.c_int32),
                 ("n_batches", C.c_int32), ("eval_kernel", C.c_int32), ("full_lists", C.c_int32),
-                ("group_created", C.POINTER(C.c_int64))]
+                ("group_created", C.POINTER(C.c_int64)), ("pairs_decided", C.c_int64)]
 
 
 class mm_extract_list(C.Structure):
@@ -287,6 +287,7 @@ class ProcessResult:
     n_batches: int = 0
     eval_kernel: int = 0  # 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel, 4 mscan_hash_kernel, 5 rpack_kernel, 6 rsrc_merge_kernel, 7 rsrc_tile_kernel
     full_lists: int = 0   # variable-score searches run as host-sorted full lists
+    pairs_decided: int = 0  # (row, candidate) pairs decided: rows that searched x their search's source
 
 
 class _TicketPack:
@@ -460,7 +461,7 @@ class Matchmaker:
         try:
             res = ProcessResult(self._groups(out), bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms,
                                 out.pair_evals, out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel,
-                                out.full_lists)
+                                out.full_lists, out.pairs_decided)
         finally:
             self.lib.mm_free_matched(self.h, C.byref(out))
         return res
@@ -480,7 +481,8 @@ class Matchmaker:
         n = out.n_entries
         tickets = _count_tickets(out) if n else 0
         res = ProcessResult([], bool(out.is_candidates), out.n_expired, out.pass_ms, out.eval_ms, out.pair_evals,
-                            out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel, out.full_lists)
+                            out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel, out.full_lists,
+                            out.pairs_decided)
         return out.n_groups, tickets, n, res
 
     def process_summary(self, out):

@@ -289,7 +289,7 @@ class ClusterMatchmaker:
             if keep_groups:
                 res = capi.ProcessResult(capi.Matchmaker._groups(out), bool(out.is_candidates), out.n_expired,
                                          out.pass_ms, out.eval_ms, out.pair_evals, out.eval_bytes, out.eval_launches,
-                                         out.n_batches, out.eval_kernel, out.full_lists)
+                                         out.n_batches, out.eval_kernel, out.full_lists, out.pairs_decided)
             _, tickets, pres, stats = self.local.summary_counts(out)
             t2 = time.perf_counter()
             cp = ClusterPass(local=res)
@@ -325,7 +325,7 @@ class ClusterMatchmaker:
             self.local.lib.mm_free_matched(self.local.h, C.byref(out))
         t3 = time.perf_counter()
         cp.local_stats = {"pass_ms": stats.pass_ms, "eval_ms": stats.eval_ms, "eval_bytes": stats.eval_bytes,
-                          "pair_evals": stats.pair_evals,
+                          "pair_evals": stats.pair_evals, "pairs_decided": stats.pairs_decided,
                           "eval_launches": stats.eval_launches, "n_batches": stats.n_batches,
                           "eval_kernel": stats.eval_kernel, "local_call_ms": 1e3 * (t1 - t0),
                           "summary_ms": 1e3 * (t2 - t1), "merge_ms": 1e3 * (t3 - t2)}

@@ -437,6 +437,7 @@ struct PassStats {
     int64_t k_bytes[kKernels] = {};     // algorithmic bytes
     int k_launches[kKernels] = {};
     int64_t pair_evals = 0;
+    int64_t pairs_decided = 0;  // rows that searched x their search's source (mm_matched.pairs_decided)
     double eval_ms() const {
         double t = 0;
         for (int k = 0; k < kKernels; k++) t += k_ms[k];

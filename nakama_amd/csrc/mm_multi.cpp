@@ -654,6 +654,7 @@ void MultiCore::fill_stats(const std::vector<mm_matched>& outs, mm_matched* out)
     for (size_t i = 0; i < outs.size(); i++) {
         out->n_expired += outs[i].n_expired;
         out->pair_evals += outs[i].pair_evals;
+        out->pairs_decided += outs[i].pairs_decided;
         out->eval_launches += outs[i].eval_launches;
         out->full_lists += outs[i].full_lists;
         out->n_batches = std::max(out->n_batches, outs[i].n_batches);

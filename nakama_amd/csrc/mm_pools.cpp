@@ -1155,6 +1155,7 @@ PackLayout Core::run_packed(const PackBatch& pb, PassStats& stats, const std::fu
                         (int64_t)((double)pb.unique * (5.0 + per_live)) + (int64_t)ents * 4 +
                         (int64_t)pb.n * (int64_t)(P * L.pm_w + L.rev_w + 1);
     stats.pair_evals += (int64_t)pb.scanned;
+    stats.pairs_decided += (int64_t)pb.scanned;  // every row one search over its own source
     return L;
 }
 

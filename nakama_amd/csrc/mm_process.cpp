@@ -818,6 +818,8 @@ struct Replay : ReplayCore {
             stats.k_launches[kk]++;
         }
         stats.batches++;
+        if (!c.row_shard() || c.shard_rank_ == 0)  // the replicated replay decides every row on every rank
+            for (const BGroup& g : bg) stats.pairs_decided += (int64_t)g.nrows * (int64_t)g.d.src_len;
         {
             // per-search accounting (on the workers for large batches)
             const size_t ns = (size_t)(nwhole + nchunks);
@@ -2032,6 +2034,7 @@ int Core::process(mm_matched* out) {
     out->eval_kernel = dk == 2 && stats.mhash ? 4 : dk == 3 && stats.rpack ? 5 : dk == 4 ? 6 : dk == 5 ? 7 : dk;
     out->eval_ms = stats.k_ms[dk];
     out->pair_evals = stats.pair_evals;
+    out->pairs_decided = stats.pairs_decided;
     out->eval_bytes = stats.k_bytes[dk];
     out->eval_launches = stats.k_launches[dk];
     out->n_batches = stats.batches;

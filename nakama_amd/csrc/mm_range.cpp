@@ -374,6 +374,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     stats.k_bytes[5] += (int64_t)(src_total * 5 + nvalid * 9 + n_elems * 12);
     stats.k_bytes[4] += (int64_t)(n_merge * n_elems * 24);
     stats.pair_evals += (int64_t)src_total;
+    for (size_t p = 0; p < ng; p++) stats.pairs_decided += (int64_t)prows(p) * (int64_t)rs_pools_[p].d.src_len;
     for (uint64_t h : task_hits) stats.par_hits += h;
     stats.par_rows += nb;
     stats.assemble_ms += msd(t0, t1);

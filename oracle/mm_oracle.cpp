@@ -1436,6 +1436,7 @@ int mm_process(void* h, mm_matched* out) {
         fill_matched(m, matched, out, false);
     }
     out->pair_evals = pe;
+    out->pairs_decided = pe;  // every row that searched visited every document
     out->pass_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MM_OK;
 }
