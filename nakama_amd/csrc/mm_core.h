@@ -713,6 +713,8 @@ private:
         uint16_t field = 0;
         DRangePool d{};
         std::vector<uint32_t> slot, rank, leaf_of;
+        std::vector<HotRec> lhot;
+        std::vector<int32_t> livl;
         RangeSrc src;
     };
     std::vector<RangePoolHost> rs_pools_;

@@ -716,7 +716,6 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         PassStats ls;
         const std::unique_ptr<ReplayCore> rpp = make_replay(tl_sel, rev, maxI, ls);
         ReplayCore& rp = *rpp;
-        std::vector<uint32_t> rows_of;
         uint64_t hits = 0;  // task_hits[t] at the end: neighbouring tasks' counters share a line
         for (uint32_t k = task_off[t]; k < task_off[t + 1]; k++) {
             const uint32_t gi = order_g[k];
@@ -763,12 +762,13 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                     rr[r.bi] = RowRec{base + r.off, r.len, (uint32_t)t, r.matched, r.expired, 1, 0};
                 continue;
             } else {
-                rows_of.assign(P.pool_rows.begin() + P.pool_off[gi], P.pool_rows.begin() + P.pool_off[gi + 1]);
+                const uint32_t* prow = P.pool_rows.data() + P.pool_off[gi];
+                const size_t npr = P.pool_off[gi + 1] - P.pool_off[gi];
                 rp.hits_seen = 0;
                 const uint32_t stop =
-                    view ? replay_pool(rp, rows_of, brow.data(), *view, tl_sel, tl_proc.data(), minc_.data(), maxc_.data(),
-                                       po)
-                         : replay_pool(rp, rows_of, brow.data(),
+                    view ? replay_pool(rp, prow, npr, brow.data(), *view, tl_sel, tl_proc.data(), minc_.data(),
+                                       maxc_.data(), po)
+                         : replay_pool(rp, prow, npr, brow.data(),
                                        [&](uint32_t bi) -> BGroup& { return bg[brow_group[bi]]; }, tl_sel,
                                        tl_proc.data(), minc_.data(), maxc_.data(), po);
                 if (stop != UINT32_MAX) pool_stop[gi] = stop;

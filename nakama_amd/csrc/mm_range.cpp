@@ -11,6 +11,7 @@
 // exactly as in the pool-parallel replay (plan_pools): rows of one pool only
 // select tickets of that pool.
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -72,6 +73,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     });
     // ---- pools: plan_pools with every row its own search (several pools), or
     // one pool when every row requires the same term ----
+    const auto tp_rows = clk::now();
     ParPlan& P = par_plan_;
     if (!plan_packed(nb, brow, P, stats)) {
         const uint32_t t0term = sigs_[sig_[brow[0]]].must_terms[0].second;
@@ -112,6 +114,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     for (uint8_t b : bad)
         if (b) return false;
     // From here on the batch is taken: nothing below declines.
+    const auto tp_pools = clk::now();
     // ---- the batch's signatures (each claimed once, by an atomic flag) ----
     const size_t nsig = sigs_.size();
     if (rs_mark_cap_ < nsig) {
@@ -133,14 +136,19 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     // per batch signature: its pool and its first bound query
     const size_t ns = lsig.size();
     std::vector<uint32_t> ls_pool(ns), ls_q(ns + 1, 0);
-    for (size_t k = 0; k < ns; k++) {
-        const uint32_t sg = lsig[k];
-        rs_sig_loc_[sg] = (uint32_t)k;
-        const Sig& s = sigs_[sg];
-        ls_pool[k] = ng == 1 ? 0u : pool_remap_[s.must_terms[0].second];
-        ls_q[k + 1] = ls_q[k] + 2 * (uint32_t)s.rs_nrange;
-    }
+    const size_t sch = ns >= 4096 ? nch : 1;
+    sweep(sch, [&](size_t c) {
+        for (size_t k = ns * c / sch; k < ns * (c + 1) / sch; k++) {
+            const uint32_t sg = lsig[k];
+            rs_sig_loc_[sg] = (uint32_t)k;
+            const Sig& s = sigs_[sg];
+            ls_pool[k] = ng == 1 ? 0u : pool_remap_[s.must_terms[0].second];
+            ls_q[k + 1] = 2 * (uint32_t)s.rs_nrange;
+        }
+    });
+    for (size_t k = 0; k < ns; k++) ls_q[k + 1] += ls_q[k];
     const uint32_t nq = ls_q[ns];
+    const auto tp_sigs = clk::now();
     // ---- device: pools (posting ranges), tiles, block -> pool, bound queries ----
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     uint64_t n_elems = 0, src_total = 0;
@@ -314,11 +322,15 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             RangePoolHost& H = rs_pools_[p];
             const DRangePool& d = H.d;
             const auto tb0 = clk::now();
+            // the pool's leaves (filled by its walker: the walk then finds
+            // them in this core's cache)
             const uint32_t* pv = h_rpos_.p + d.out_off;
             const uint32_t nv = valid[p];
             grow_to(H.slot, nv);
             grow_to(H.rank, nv);
             grow_to(H.leaf_of, d.src_len);
+            grow_to(H.lhot, nv);
+            grow_to(H.livl, nv);
             for (uint32_t j = 0; j < nv; j++) {
                 const uint32_t rk = pv[j];
                 if (rk >= d.src_len) throw DeviceError{hipErrorUnknown, "range source: a sorted position out of range", __LINE__};
@@ -327,11 +339,15 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
                 H.slot[j] = s;
                 H.leaf_of[rk] = j;
                 rs_leaf_[s] = j;
+                H.lhot[j] = hot_[s];
+                H.livl[j] = intervals_[s];
             }
             H.src.n = nv;
             H.src.slot = H.slot.data();
             H.src.rank = H.rank.data();
             H.src.leaf_of = H.leaf_of.data();
+            H.src.lhot = H.lhot.data();
+            H.src.livl = H.livl.data();
             H.src.tree.build(H.rank.data(), nv);
             const auto tb1 = clk::now();
             PoolOut& po = few ? pool_outs_[p] : o;
@@ -387,10 +403,11 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
         const size_t pm = (size_t)(std::max_element(pool_walk_ms.begin(), pool_walk_ms.end()) - pool_walk_ms.begin());
         std::fprintf(stderr,
                      "[nkm]   batch %d (range): rows %zu pools %zu signatures %zu candidates %llu (valid %llu), %d merges "
-                     "| plan %.2f device %.2f tiers %.2f walks %.2f merge %.2f ms | slowest pool: %u rows, build %.2f "
-                     "walk %.2f ms\n",
+                     "| plan %.2f (rows %.2f pools %.2f signatures %.2f upload %.2f) device %.2f tiers %.2f walks %.2f "
+                     "merge %.2f ms | slowest pool: %u rows, build %.2f walk %.2f ms\n",
                      stats.batches, nb, ng, ns, (unsigned long long)src_total, (unsigned long long)nvalid, n_merge,
-                     msd(t0, t1), msd(t1, t2), msd(t2, t2b), msd(t2b, t3), msd(t3, t4), (unsigned)prows(pm),
+                     msd(t0, t1), msd(t0, tp_rows), msd(tp_rows, tp_pools), msd(tp_pools, tp_sigs), msd(tp_sigs, t1),
+                     msd(t1, t2), msd(t2, t2b), msd(t2b, t3), msd(t3, t4), (unsigned)prows(pm),
                      pool_build_ms[pm], pool_walk_ms[pm]);
     }
     return true;

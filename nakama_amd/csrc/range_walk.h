@@ -185,11 +185,15 @@ inline void build_tiers(const DClause* cl, int n, const uint32_t* lo, const uint
 }
 
 // One pool's candidates in value order (the device sort's valid prefix).
+// The fields the walk reads of a hit are copied per leaf (a pool's hits are
+// value-neighbours: its leaves are its working set, not the whole store).
 struct RangeSrc {
     uint32_t n = 0;               // leaves
     const uint32_t* slot = nullptr;  // per leaf: ticket slot
     const uint32_t* rank = nullptr;  // per leaf: source position (hit rank)
     const uint32_t* leaf_of = nullptr;  // per rank: its leaf
+    const HotRec* lhot = nullptr;    // per leaf: the ticket's HotRec
+    const int32_t* livl = nullptr;   // per leaf: the ticket's Intervals
     MinTree16 tree;
 };
 
@@ -254,7 +258,7 @@ struct RangeRun {
     // count.  BAIL when the row reaches the CountMultiple trim or outgrows the
     // fixed combos: nothing is selected yet, the caller restores the masks and
     // takes row().
-    NKM_INLINE ReplayCore::Status fast_row(uint32_t T, const RRange* r, uint32_t r0, uint32_t r1) {
+    NKM_INLINE ReplayCore::Status fast_row(uint32_t T, uint32_t self_leaf, const RRange* r, uint32_t r0, uint32_t r1) {
         const HotRec& ht = v.hot[T];
         const bool last = v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc;
         const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
@@ -267,16 +271,16 @@ struct RangeRun {
         cur = r0;
         end = r1;
         masked.clear();
-        if (leaf_of_slot[T] != kNoSlot) mask(leaf_of_slot[T]);
+        if (self_leaf != kNoSlot) mask(self_leaf);
         int ncomb = 0;
         uint32_t leaf;
         while (next(leaf)) {
             const uint32_t H = S->slot[leaf];
             mask(leaf);
-            const HotRec& hh = v.hot[H];
+            const HotRec& hh = S->lhot[leaf];
             if (!is_hit(hh)) continue;
             hits_seen++;
-            if (tmax < hh.maxc && v.intervals[H] + proc[H] <= max_intervals) continue;  // :150-153
+            if (tmax < hh.maxc && S->livl[leaf] + proc[H] <= max_intervals) continue;  // :150-153
             const int hc = hh.count;
             int f = 0;  // first fit (:167-226)
             while (f < ncomb && fcb.size[f] + hc > room) f++;
@@ -296,7 +300,7 @@ struct RangeRun {
                 bool more = false;
                 uint32_t pl;
                 while (!more && next(pl)) {
-                    if (is_hit(v.hot[S->slot[pl]])) more = true;
+                    if (is_hit(S->lhot[pl])) more = true;
                     else mask(pl);
                 }
                 form = !more;
@@ -322,7 +326,7 @@ struct RangeRun {
         return ReplayCore::NOMATCH;
     }
 
-    NKM_INLINE ReplayCore::Status row(uint32_t T, const RRange* r, uint32_t r0, uint32_t r1) {
+    NKM_INLINE ReplayCore::Status row(uint32_t T, uint32_t self_leaf, const RRange* r, uint32_t r0, uint32_t r1) {
         const HotRec& ht = v.hot[T];
         const bool last = v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc;
         const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
@@ -334,17 +338,17 @@ struct RangeRun {
         cur = r0;
         end = r1;
         masked.clear();
-        if (leaf_of_slot[T] != kNoSlot) mask(leaf_of_slot[T]);  // self (:112-126)
+        if (self_leaf != kNoSlot) mask(self_leaf);  // self (:112-126)
         size_t ncomb = 0;
         open.clear();
         uint32_t leaf;
         while (next(leaf)) {
             const uint32_t H = S->slot[leaf];
             mask(leaf);
-            const HotRec& hh = v.hot[H];
+            const HotRec& hh = S->lhot[leaf];
             if (!is_hit(hh)) continue;
             hits_seen++;
-            if (tmax < hh.maxc && v.intervals[H] + proc[H] <= max_intervals) continue;          // :150-153
+            if (tmax < hh.maxc && S->livl[leaf] + proc[H] <= max_intervals) continue;          // :150-153
             if (!v.sessions_exclusive && (ht.smask & hh.smask) && share_session(ht, hh)) continue;  // :155-165
             bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
             int found = -1;
@@ -391,7 +395,7 @@ struct RangeRun {
                 bool more = false;
                 uint32_t pl;
                 while (!more && next(pl)) {
-                    if (is_hit(v.hot[S->slot[pl]])) more = true;
+                    if (is_hit(S->lhot[pl])) more = true;
                     else mask(pl);
                 }
                 form = !more;
@@ -446,7 +450,9 @@ struct RangeRun {
     }
 
     // Walks a pool's rows (batch rows `bis`, ascending; slot brow[bi]);
-    // sig_range(bi, base, r0, r1) gives the row's tier list base[r0, r1).
+    // sig_range(bi, base, r0, r1) gives the row's tier list base[r0, r1)
+    // (one `base` for every row).  The rows' tier ranges and own leaves are
+    // looked up first, in one pass whose independent misses overlap.
     // Appends records + a sentinel to `o`; psel / proc / the tree's masks are
     // restored on return except for the selections (the tree keeps them).
     template <class SigRange>
@@ -464,6 +470,14 @@ struct RangeRun {
                               SigRange sig_range, PoolOut& o) {
         S = &src;
         uint32_t gcum = 0, xcum = 0;
+        static thread_local std::vector<uint32_t> pre;  // per row: r0, r1, own leaf
+        pre.resize((size_t)3 * nrows);
+        const RRange* base = nullptr;
+        for (uint32_t j = 0; j < nrows; j++) {
+            const uint32_t bi = bis[j];
+            sig_range(bi, base, pre[3 * (size_t)j], pre[3 * (size_t)j + 1]);
+            pre[3 * (size_t)j + 2] = leaf_of_slot[brow[bi]];
+        }
         for (uint32_t j = 0; j < nrows; j++) {
             const uint32_t bi = bis[j];
             const uint32_t T = brow[bi];
@@ -471,17 +485,14 @@ struct RangeRun {
                 const uint32_t T2 = brow[bis[j + 2]];
                 __builtin_prefetch(&v.hot[T2]);
                 __builtin_prefetch(&psel[T2]);
-                __builtin_prefetch(&leaf_of_slot[T2]);
                 __builtin_prefetch(&v.intervals[T2]);
             }
             if (psel[T]) continue;
-            const RRange* base;
-            uint32_t r0, r1;
-            sig_range(bi, base, r0, r1);
-            auto status = fast && v.sessions_exclusive ? fast_row(T, base, r0, r1) : ReplayCore::BAIL;
+            const uint32_t r0 = pre[3 * (size_t)j], r1 = pre[3 * (size_t)j + 1], self = pre[3 * (size_t)j + 2];
+            auto status = fast && v.sessions_exclusive ? fast_row(T, self, base, r0, r1) : ReplayCore::BAIL;
             if (status == ReplayCore::BAIL) {
                 unmask();  // nothing selected yet: every mask goes back
-                status = row(T, base, r0, r1);
+                status = row(T, self, base, r0, r1);
             }
             const HotRec& ht = v.hot[T];
             PoolRec rec{bi, 0, (uint8_t)(v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc),

@@ -506,12 +506,13 @@ struct alignas(128) PoolOut {
 // list runs out (EXHAUSTED: its search must re-run after the batch) stops the
 // pool there: returns its batch row, else UINT32_MAX.
 template <class GroupOf>
-uint32_t replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uint32_t* brow, GroupOf group_of,
+uint32_t replay_pool(ReplayCore& rp, const uint32_t* bis, size_t nbis, const uint32_t* brow, GroupOf group_of,
                      std::vector<uint8_t>& psel, uint8_t* proc, const int32_t* minc, const int32_t* maxc, PoolOut& o) {
-    std::vector<std::pair<uint32_t, int>> grp;
+    static thread_local std::vector<std::pair<uint32_t, int>> grp;  // (C5: 10^5 pools of 8 rows per pass)
     uint32_t gcum = 0, xcum = 0, stop = UINT32_MAX;
     rp.proc = proc;
-    for (uint32_t bi : bis) {
+    for (size_t j = 0; j < nbis; j++) {
+        const uint32_t bi = bis[j];
         const uint32_t T = brow[bi];
         if (psel[T]) continue;
         auto status = rp.decide(T, group_of(bi), false, grp);
@@ -538,6 +539,11 @@ uint32_t replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uin
     for (const PoolRec& r : o.recs) proc[brow[r.bi]] = 0;
     o.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)o.ents.size(), 0, gcum, xcum});  // sentinel
     return stop;
+}
+template <class GroupOf>
+uint32_t replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uint32_t* brow, GroupOf group_of,
+                     std::vector<uint8_t>& psel, uint8_t* proc, const int32_t* minc, const int32_t* maxc, PoolOut& o) {
+    return replay_pool(rp, bis.data(), bis.size(), brow, group_of, psel, proc, minc, maxc, o);
 }
 
 // ---- dense pool replay (a pool with one complete search, no RevPrecision) ----

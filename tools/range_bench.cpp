@@ -178,6 +178,14 @@ int main(int argc, char** argv) {
     src.slot = lslot.data();
     src.rank = lrank.data();
     src.leaf_of = leaf_of.data();
+    std::vector<HotRec> lhot(nv);
+    std::vector<int32_t> livl(nv);
+    for (uint32_t k = 0; k < nv; k++) {
+        lhot[k] = hot[lslot[k]];
+        livl[k] = intervals[lslot[k]];
+    }
+    src.lhot = lhot.data();
+    src.livl = livl.data();
     src.tree.build(lrank.data(), nv);
     std::vector<RRange> tiers;
     std::vector<uint32_t> t0(N), t1(N);
