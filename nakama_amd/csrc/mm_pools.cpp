@@ -548,6 +548,14 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         }
     }
     const bool gpipe = ident && pipe && wp.size() > ntask;
+    // Identity pools with more walks than workers (C4: 64 pools on 16): no
+    // worker is left to gather beside the walks.  NKM_TGATHER=1: each walk
+    // gathers its own pool first (its copies then in its core's cache)
+    // instead of a separate gather phase before all walks — measured even
+    // with the default on C4 (same box, 2 x 2 runs: p50 30.2 / 31.3 vs
+    // 31.3 / 29.3 ms, profiles/r04ab_tgather.txt), so off by default.
+    static const bool tgather_mode = std::getenv("NKM_TGATHER") && !std::strcmp(std::getenv("NKM_TGATHER"), "1");
+    const bool tgather = tgather_mode && ident && pipe && !gpipe;
     std::atomic<bool> id_broken{false};  // an identity pool whose row was not at its position (a bug: fail loudly)
     if (ident)
         for (uint32_t gi : dense_ids) {
@@ -581,8 +589,8 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     };
     // each pool's entry bound (every ticket of its list and rows joins at
     // most one group): the walk reserves it so readers never see a move
-    std::vector<uint64_t> esum(pipe && !gpipe ? ntask_g * ng : 0, 0);
-    if (!gpipe)
+    std::vector<uint64_t> esum(pipe && !gpipe && !tgather ? ntask_g * ng : 0, 0);
+    if (!gpipe && !tgather)
         wp.run(ntask_g, [&](size_t t) {
             for (uint32_t gi : dense_ids) {
                 DensePool& D = dense_pools_[gi];
@@ -605,9 +613,9 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     std::unique_ptr<Prog[]> prog(pipe ? new Prog[ng] : nullptr);
     std::vector<uint64_t> ebound(pipe ? ng : 0, 0);
     uint64_t ebound_all = 0;
-    for (size_t t = 0; pipe && !gpipe && t < ntask_g; t++)
+    for (size_t t = 0; pipe && !gpipe && !tgather && t < ntask_g; t++)
         for (size_t gi = 0; gi < ng; gi++) ebound[gi] += esum[t * ng + gi];
-    if (gpipe)  // identity pools: the rows are list members, whose entries are at most max_pres_ each
+    if (gpipe || tgather)  // identity pools: the rows are list members, whose entries are at most max_pres_ each
         for (uint32_t gi : dense_ids) ebound[gi] = (uint64_t)dense_pools_[gi].n * (uint64_t)std::max(1, max_pres_);
     for (uint64_t e : ebound) ebound_all += e;
     const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
@@ -725,6 +733,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             if (dense[gi] && pipe) {
                 const DensePool& D = dense_pools_[gi];
                 const auto tr0 = clk::now();
+                if (tgather) dense_pools_[gi].gather(rv, 0, D.n, pos_of_.data());  // identity: no slot map written
                 run.reset(D.n);
                 run.fast = fast_mode_;
                 run.recs.reserve((size_t)D.nrows + 1);
@@ -839,7 +848,8 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             mw = std::max(mw, walk_ms[k]);
         }
         std::fprintf(stderr, "[nkm]   pool walks: %zu tasks, %zu pools on %u workers | sum: tasks %.2f, walks %.2f (max %.2f), "
-                     "reset+reserve %.2f ms | gather %s\n", ntask, ng, wp.size(), st, sw, mw, sp, gpipe ? "beside" : "before");
+                     "gather+reset+reserve %.2f ms | gather %s\n", ntask, ng, wp.size(), st, sw, mw, sp,
+                     gpipe ? "beside" : tgather ? "in each walk's task" : "before");
     }
     stats.par_rows += nb;
     return true;
