@@ -55,7 +55,8 @@ WORKLOADS = {
         "matchmaker_process.go:588), RevPrecision, Min=2 Max=4, 1M in total",
 }
 # the query fields a pool is keyed on (the cluster front's routing)
-POOL_FIELDS = {1: ("properties.mode", "properties.region"), 3: ("properties.mode", "properties.region"),
+POOL_FIELDS = {1: ("properties.mode", "properties.region"), 2: ("properties.region",),
+               3: ("properties.mode", "properties.region"),
                4: ("properties.mode", "properties.region"), 5: ("properties.bucket",), 11: ("properties.bucket",)}
 # BASELINE.json configs: C1 10k, C2 100k, C4 4M in total; the others 1M (per GPU for C3)
 DEFAULT_TICKETS = {1: 10_000, 2: 100_000, 4: 4_000_000}
