@@ -19,7 +19,8 @@ import pytest
 import harness
 from nakama_amd import capi, synth
 
-POOL_FIELDS = {1: ["properties.mode", "properties.region"], 3: ["properties.mode", "properties.region"],
+POOL_FIELDS = {1: ["properties.mode", "properties.region"], 2: ["properties.region"], 15: ["properties.region"],
+               3: ["properties.mode", "properties.region"],
                4: ["properties.mode", "properties.region"], 5: ["properties.bucket"], 12: ["properties.mode"]}
 
 
@@ -277,9 +278,11 @@ def test_multi_rows_mode_needs_own_library():
 @pytest.mark.gpu
 @pytest.mark.parametrize("config,n,kw", [(3, 6000, dict(max_intervals=2)), (4, 6000, dict(max_intervals=2)),
                                          (12, 1000, dict(max_intervals=3)),
-                                         (5, 2000, dict(max_intervals=2, rev_precision=True, rev_threshold=0))])
+                                         (5, 2000, dict(max_intervals=2, rev_precision=True, rev_threshold=0)),
+                                         (2, 6000, dict(max_intervals=2)), (15, 3000, dict(max_intervals=3))])
 def test_gpu_multi_pools_equal_one_oracle(config, n, kw):
-    """Two HIP sub-handles on device 0, pools placed whole, vs one oracle pass."""
+    """Two HIP sub-handles on device 0, pools placed whole, vs one oracle pass
+    (configs 2 and 15: each sub-handle's pass a range batch)."""
     _compare(config, n, 2, None, n_subs=2, **kw)
 
 
