@@ -467,6 +467,7 @@ struct PassStats {
     // overlapped host work, the wait for the device, result accounting and
     // wiring, the hit-list copies; replay_parallel's gathers and the walk job
     double rb_prep_ms = 0, rb_overlap_ms = 0, rb_wait_ms = 0, rb_post_ms = 0, rb_lists_ms = 0;
+    int mscan_lists = 0, lists_proven = 0;  // mscan lists placed / proven equal to their rows (not downloaded)
     double par_gather_ms = 0, par_job_ms = 0, par_clear_ms = 0;
     uint64_t par_rows = 0, par_hits = 0;
 };
@@ -686,6 +687,23 @@ private:
                          GroupList& out_groups,
                          std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats,
                          bool rev, uint32_t* min_stop, const std::function<BGroup&(uint32_t)>* view = nullptr);
+    // ---- proven mscan lists ----
+    // A hashed-scan list (term-only pool signature) always holds every batch
+    // row of its search: the row is alive on the device (live, indexed, not
+    // selected), carries its signature's key terms (self_match_) and its own
+    // counts meet the signature's count musts.  So when the list's count
+    // equals the search's batch rows, the list IS those rows; and with slots
+    // in time order (monotone_: scan order = slot order = pinned order) it
+    // holds them in batch order.  Such a list is not downloaded
+    // (BGroup::rows_list).  NKM_LISTPROOF=0: every list is downloaded;
+    // 2: downloaded and compared with the proof's claim (throws on a miss).
+    int list_proof_mode_ = 1;
+    bool row_lists_pending_ = false;  // the last batch flagged some BGroup::rows_list
+    // writes every rows_list search's host list from its batch rows (a reader
+    // other than the dense identity walk) and clears the flags
+    void fill_row_lists(std::vector<BGroup>& bg, const UVec<uint32_t>& brow, const UVec<uint32_t>& brow_group);
+    // NKM_LISTPROOF=2: the downloaded lists against the proof's claim
+    void check_row_lists(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow, const UVec<uint32_t>& brow_group);
     // ---- packed RevPrecision batches (rpack_kernel) ----
     // A RevPrecision batch whose every row searches a source of <= 64
     // entries: rows go to the device as 12-B DSmallRows, the lists come back

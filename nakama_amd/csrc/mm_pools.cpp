@@ -408,6 +408,39 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
 // one pass over the batch in row order assembles the groups, the expired list
 // and the Intervals increments — processDefault's sequential order, because
 // no pool ever selects another pool's ticket.
+void Core::fill_row_lists(std::vector<BGroup>& bg, const UVec<uint32_t>& brow, const UVec<uint32_t>& brow_group) {
+    if (!row_lists_pending_) return;
+    row_lists_pending_ = false;
+    std::vector<uint32_t> at(bg.size(), 0);
+    for (size_t bi = 0; bi < brow.size(); bi++) {
+        const uint32_t gi = brow_group[bi];
+        BGroup& g = bg[gi];
+        if (!g.rows_list) continue;
+        if (at[gi] >= g.n || g.ss != 1) throw std::logic_error("fill_row_lists: a proven list is shorter than its rows");
+        const_cast<uint32_t*>(g.sp)[at[gi]++] = brow[bi];
+    }
+    for (size_t gi = 0; gi < bg.size(); gi++) {
+        if (bg[gi].rows_list && at[gi] != bg[gi].n) throw std::logic_error("fill_row_lists: a proven list is longer than its rows");
+        bg[gi].rows_list = false;
+    }
+}
+
+void Core::check_row_lists(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow, const UVec<uint32_t>& brow_group) {
+    if (!row_lists_pending_) return;
+    std::vector<uint32_t> at(bg.size(), 0);
+    for (size_t bi = 0; bi < brow.size(); bi++) {
+        const uint32_t gi = brow_group[bi];
+        const BGroup& g = bg[gi];
+        if (!g.rows_list) continue;
+        if (at[gi] >= g.n || g.slot(at[gi]) != brow[bi])
+            throw std::logic_error("NKM_LISTPROOF=2: a proven mscan list differs from its search's rows");
+        at[gi]++;
+    }
+    for (size_t gi = 0; gi < bg.size(); gi++)
+        if (bg[gi].rows_list && at[gi] != bg[gi].n)
+            throw std::logic_error("NKM_LISTPROOF=2: a proven mscan list is longer than its search's rows");
+}
+
 bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                            const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                            GroupList& out_groups,
@@ -547,6 +580,9 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             ident = std::all_of(ok.begin(), ok.end(), [](uint8_t x) { return x != 0; });
         }
     }
+    // proven lists (BGroup::rows_list) not downloaded: only the identity walk
+    // goes without them
+    if (!ident && !view) fill_row_lists(bg, brow, brow_group);
     const bool gpipe = ident && pipe && wp.size() > ntask;
     // Identity pools with more walks than workers (C4: 64 pools on 16): no
     // worker is left to gather beside the walks.  NKM_TGATHER=1: each walk

@@ -377,8 +377,12 @@ struct Replay : ReplayCore {
     }
 
     // overlap: host work run while the batch's kernels and copies are in
-    // flight (the pool bucketing of the rows, which needs no hit list)
-    void run_batch(std::vector<BGroup>& bg, bool need_pm, const std::function<void()>& overlap = nullptr) {
+    // flight (the pool bucketing of the rows, which needs no hit list).
+    // rows_self: every batch row carries its own search's terms and is
+    // indexed (assemble_parallel's fused plan) — a hashed-scan list may then
+    // be proven equal to its search's rows (Core::list_proof_mode_).
+    void run_batch(std::vector<BGroup>& bg, bool need_pm, const std::function<void()>& overlap = nullptr,
+                   bool rows_self = false) {
         using rclk = std::chrono::steady_clock;
         auto rms = [](rclk::time_point a, rclk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         const auto r0 = rclk::now();
@@ -581,7 +585,12 @@ struct Replay : ReplayCore {
         off += (mw - mw0 + 3) / 4;
         // copied in the first round when the capacity is at most 2 slot ids
         // per scanned candidate (C3 / C4: every candidate in at most one list)
-        const bool m_precopy = use_m && !c.row_shard() && mw - mw0 <= 2 * (uint64_t)ms.src_len;
+        // unless proven (Core::list_proof_mode_): a list whose count is its
+        // search's batch rows is those rows, not downloaded (mode 2: it is,
+        // and the claim checked against it)
+        const bool proof = hashed && rows_self && c.list_proof_mode_ != 0 && c.monotone_ && !c.row_shard() && !rev;
+        const bool skip_lists = proof && c.list_proof_mode_ == 1;
+        const bool m_precopy = use_m && !c.row_shard() && mw - mw0 <= 2 * (uint64_t)ms.src_len && !skip_lists;
         const uint32_t ncells = !use_m ? 0 : hashed ? ms.n_sigs : ms.n_sigs * ms.n_chunks;
         if (hashed) scratch += (mscan_hash_work_words(ms) + 3) / 4;
         else if (use_m) scratch += ((uint64_t)ncells * mchunk + 3) / 4;  // 4-B slots in 16-B DHit units
@@ -875,6 +884,7 @@ struct Replay : ReplayCore {
                 BGroup& g = bg[lg_group[i]];
                 const DGroupResult& r = c.h_res_.p[i];
                 g.head = 0;
+                g.rows_list = false;
                 if (slots_only) {
                     g.set_slots(c.h_slots_.p + lg[i].out_off);
                     g.last_i = (uint32_t)i;
@@ -900,6 +910,8 @@ struct Replay : ReplayCore {
         // those (an mscan list: 4-B slot ids, copied in the first round when
         // m_precopy)
         const size_t n_scan_cg = cg_list.size() - (use_m ? m_list.size() : 0);
+        bool m_copied = false;
+        c.row_lists_pending_ = false;
         for (size_t k = 0; k < cg_list.size(); k++) {
             BGroup& g = bg[cg_list[k]];
             const bool slots = k >= n_scan_cg;
@@ -911,10 +923,18 @@ struct Replay : ReplayCore {
                 throw DeviceError{hipErrorUnknown, "mscan list cut", __LINE__};
             const bool packed = !slots && slots_only;  // a chunked list: slot ids + its last DHit
             uint32_t* const h32 = reinterpret_cast<uint32_t*>(c.h_out_.p);
+            g.rows_list = false;
             if (slots) {  // an mscan list: cg_off is its first slot word
-                if (n && !m_precopy)
+                const bool proven = proof && n == g.nrows;
+                if (n && !m_precopy && !(proven && skip_lists)) {
                     NKM_HIP(hipMemcpyAsync(h32 + cg_off[k], reinterpret_cast<const uint32_t*>(c.d_out_.p) + cg_off[k],
                                            n * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+                    m_copied = true;
+                }
+                g.rows_list = proven;
+                c.row_lists_pending_ = c.row_lists_pending_ || proven;
+                stats.mscan_lists++;
+                stats.lists_proven += proven;
             } else if (n && packed) {
                 NKM_HIP(hipMemcpyAsync(c.h_slots_.p + cg_off[k], c.d_slots_.p + cg_off[k], n * sizeof(uint32_t),
                                        hipMemcpyDeviceToHost, stream));
@@ -935,7 +955,7 @@ struct Replay : ReplayCore {
             g.n = (uint32_t)n;
             g.complete = complete;
         }
-        if (n_scan_cg || (use_m && !m_precopy)) NKM_HIP(hipStreamSynchronize(stream));
+        if (n_scan_cg || m_copied) NKM_HIP(hipStreamSynchronize(stream));
         stats.rb_lists_ms += rms(r4, rclk::now());
     }
 
@@ -1419,11 +1439,15 @@ int Core::process_default(GroupList& out_groups,
         plan.ok = false;
         // a RevThreshold timer that may still fire is read per row: serial replay
         const bool timer_live = rev && timer.armed && !timer.fired;
-        rp.run_batch(bg, need_pm, [&] {  // pools bucketed while the searches run
-            if (par_mode_ && !timer_live)
-                (par_asm && fused_plan) ? plan_fused(bg, brow, brow_group, plan, stats)
-                                        : plan_parallel(bg, brow, brow_group, plan, stats);
-        });
+        rp.run_batch(
+            bg, need_pm,
+            [&] {  // pools bucketed while the searches run
+                if (par_mode_ && !timer_live)
+                    (par_asm && fused_plan) ? plan_fused(bg, brow, brow_group, plan, stats)
+                                            : plan_parallel(bg, brow, brow_group, plan, stats);
+            },
+            par_asm && fused_plan);
+        if (list_proof_mode_ == 2) check_row_lists(bg, brow, brow_group);
         auto tb1 = std::chrono::steady_clock::now();
         stats.search_ms += std::chrono::duration<double, std::milli>(tb1 - tb0).count();
         // ---- replay ----
@@ -1433,6 +1457,7 @@ int Core::process_default(GroupList& out_groups,
         uint32_t stop_bi = UINT32_MAX;
         if (par_mode_ && replay_parallel(plan, bg, brow, brow_group, sel, out_groups, expired, newly, stats, rev,
                                          &stop_bi)) {
+            row_lists_pending_ = false;  // consumed by the walk (or filled by replay_parallel)
             stats.parallel_batches++;
             const auto tr = std::chrono::steady_clock::now();
             stats.replay_ms += std::chrono::duration<double, std::milli>(tr - tb1).count();
@@ -1469,6 +1494,7 @@ int Core::process_default(GroupList& out_groups,
             }
             continue;
         }
+        fill_row_lists(bg, brow, brow_group);  // the serial replay reads every list
         for (size_t bi = 0; bi < brow.size(); bi++) {
             const uint32_t T = brow[bi];
             if (sel[T]) { done = bi + 1; continue; }
@@ -2018,15 +2044,15 @@ int Core::process(mm_matched* out) {
                          "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches, %d tier lists) | finish %.2f ms | "
                          "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu | par bucket %.2f work %.2f "
                          "merge %.2f ms (task max %.2f ms, rows %llu, hits %llu) | batch: prep %.2f overlap %.2f wait %.2f "
-                         "post %.2f lists %.2f | replay: gather %.2f job %.2f clear %.2f\n",
+                         "post %.2f lists %.2f (%d of %d proven) | replay: gather %.2f job %.2f clear %.2f\n",
                          ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms(), stats.replay_ms,
                          stats.apply_ms, stats.batches,
                          stats.parallel_batches, stats.refetches, stats.launches(), stats.tier_lists, ms(t2, t3), ms(t3, t4),
                          groups.size(), nslots(), n_live_, active_list_.size(), sigs_.size(),
                          dict_.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms,
                          stats.par_task_max_ms, (unsigned long long)stats.par_rows, (unsigned long long)stats.par_hits,
-                         stats.rb_prep_ms, stats.rb_overlap_ms, stats.rb_wait_ms, stats.rb_post_ms, stats.rb_lists_ms,
-                         stats.par_gather_ms, stats.par_job_ms, stats.par_clear_ms);
+                         stats.rb_prep_ms, stats.rb_overlap_ms, stats.rb_wait_ms, stats.rb_post_ms, stats.rb_lists_ms, stats.lists_proven,
+                         stats.mscan_lists, stats.par_gather_ms, stats.par_job_ms, stats.par_clear_ms);
         }
     }
     unwind.armed = false;

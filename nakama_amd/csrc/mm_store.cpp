@@ -120,6 +120,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_RPACK")) pack_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_TIER")) tier_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_RANGE")) range_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_LISTPROOF")) list_proof_mode_ = std::atoi(e);
     if (const char* e = std::getenv("NKM_BULK")) bulk_mode_ = std::strcmp(e, "0") == 0 ? 0 : std::strcmp(e, "force") == 0 ? 2 : 1;
     if (const char* e = std::getenv("NKM_KERNEL"))
         kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN

@@ -116,6 +116,11 @@ struct BGroup {
     uint32_t src_term = 0;
     uint32_t n = 0;
     bool complete = true;
+    // an mscan list proven equal to the search's own batch rows (Core::
+    // list_proven): its host buffer (sp) is not filled — the dense walk takes
+    // row j's slot as position j; any other reader fills it first
+    // (Core::fill_row_lists)
+    bool rows_list = false;
     uint32_t head = 0;
     std::vector<DHit> ext;
     std::vector<uint8_t> ext_rev;
@@ -143,6 +148,7 @@ struct BGroup {
         src_term = 0;
         n = 0;
         complete = true;
+        rows_list = false;
         head = 0;
         ext.clear();
         ext_rev.clear();
@@ -578,6 +584,7 @@ struct DensePool {
     const uint32_t* brow = nullptr;  // batch row -> slot
     std::vector<DenseRec> rec;
     std::vector<uint32_t> slot;
+    bool rows_list = false;  // BGroup::rows_list: position k's slot is brow[bis[k]], sp unfilled
     // identity: the pool's rows are its list, in list order (row j's ticket is
     // position j — every pool member searches, batch order = scan order, as in
     // a pool of fresh tickets): no slot -> position map is needed
@@ -592,6 +599,7 @@ struct DensePool {
         sp = g.sp;
         ss = g.ss;
         n = g.n;
+        rows_list = g.rows_list;
         bis = rows;
         nrows = n_rows;
         brow = batch_slots;
@@ -614,6 +622,7 @@ struct DensePool {
     }
     // does row j's ticket sit at list position j for every row? (positions [lo, hi))
     bool rows_are_list(uint32_t lo, uint32_t hi) const {
+        if (rows_list) return true;
         for (uint32_t k = lo; k < hi; k++)
             if (sp[(size_t)k * ss] != brow[bis[k]]) return false;
         return true;
@@ -622,9 +631,9 @@ struct DensePool {
     void gather(const ReplayView& v, uint32_t lo, uint32_t hi, uint32_t* pos_of) {
         const bool map = !identity;
         for (uint32_t k = lo; k < hi; k++) {
-            const uint32_t s = sp[(size_t)k * ss];
+            const uint32_t s = rows_list ? brow[bis[k]] : sp[(size_t)k * ss];
             if (k + 16 < hi) {
-                const uint32_t p = sp[(size_t)(k + 16) * ss];
+                const uint32_t p = rows_list ? brow[bis[k + 16]] : sp[(size_t)(k + 16) * ss];
                 __builtin_prefetch(&v.hot[p]);
                 __builtin_prefetch(&v.intervals[p]);
                 if (map) __builtin_prefetch(&pos_of[p], 1);

@@ -8,6 +8,7 @@ states) — all through the C ABI of include/nakama_mm.h.
 """
 import math
 import os
+import re
 
 import pytest
 
@@ -242,6 +243,30 @@ def test_hashed_mscan_chunk_lengths(contig, j, monkeypatch):
     monkeypatch.setenv("NKM_MHASH_J" if contig == "0" else "NKM_MCONTIG_J", j)
     run_passes(4, 9_999, 2, dict(max_intervals=2))
     run_passes(3, 7_777, 2, dict(max_intervals=2))
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+@pytest.mark.parametrize("config,n,contig", [(3, 20_000, "1"), (4, 20_000, "1"), (3, 7_777, "0"),
+                                             (4, 9_999, "0")])
+def test_proven_mscan_lists(config, n, contig, mode, monkeypatch, capfd):
+    """Hashed-scan lists proven equal to their search's batch rows are not
+    downloaded (Core::list_proof_mode_): NKM_LISTPROOF=1 (default) skips
+    them, 0 downloads every list, 2 downloads them and throws if a proven
+    list differs from its rows — over contiguous slot runs and through the
+    scan order (NKM_MCONTIG=0).  Groups and state equal to the oracle's
+    either way; the profile line reports the proven lists."""
+    set_kernel(monkeypatch, "mhash")
+    monkeypatch.setenv("NKM_MCONTIG", contig)
+    monkeypatch.setenv("NKM_LISTPROOF", mode)
+    monkeypatch.setenv("NKM_PARALLEL", "force")
+    monkeypatch.setenv("NKM_PROFILE", "1")
+    rs = run_passes(config, n, 2, dict(max_intervals=2))
+    assert rs[0].eval_kernel == 4
+    err = capfd.readouterr().err
+    got = [tuple(map(int, m)) for m in re.findall(r"\((\d+) of (\d+) proven\)", err)]
+    assert got, err[-2000:]
+    proven = sum(p for p, _ in got)
+    assert (proven == 0) if mode == "0" else (proven > 0), got
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
