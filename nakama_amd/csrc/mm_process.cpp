@@ -835,13 +835,14 @@ struct Replay : ReplayCore {
             const size_t nch = ns >= 65536 && c.par_mode_ ? c.workers().size() : 1;
             std::vector<std::array<int64_t, 5>> acc(nch, std::array<int64_t, 5>{0, 0, 0, 0, 0});
             auto count = [&](size_t ch) {
-                auto& a = acc[ch];
+                std::array<int64_t, 5> a{0, 0, 0, 0, 0};  // thread-private: the chunks' sums share cache lines
                 for (size_t t = ns * ch / nch; t < ns * (ch + 1) / nch; t++) {
                     if ((int)t < b0 || ((int)t >= b1 && (int)t < nwhole)) continue;  // another rank's block
                     a[4] += c.h_res_.p[t].scanned;
                     const int kk = (int)t >= nwhole ? 1 : lg[t].path == 1 ? 3 : 0;
                     a[kk] += search_bytes(bg[lg_group[t]].n_fields, lg[t], c.h_res_.p[t]);
                 }
+                acc[ch] = a;
             };
             if (nch > 1) c.workers().run(nch, count);
             else count(0);
@@ -1033,6 +1034,7 @@ void Core::choose_source(const Sig& s, DGroup& g, SrcChoice* ch) {
 
 int Core::process_default(GroupList& out_groups,
                           std::vector<uint32_t>& expired, PassStats& stats) {
+    const auto tp0 = std::chrono::steady_clock::now();
     const uint32_t N = (uint32_t)nslots();
     filled_groups_ = 0;
     std::vector<uint8_t>& sel = sel_;
@@ -1048,6 +1050,7 @@ int Core::process_default(GroupList& out_groups,
     std::vector<uint32_t>& rows = rows_;
     filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, rows,
                  [&](uint32_t s) { return live_[s] && is_active_[s]; });
+    stats.prologue_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
 
     if (!active_flag_) {  // paused: intervals still advance (matchmaker_process.go:53-63)
         for (uint32_t r : rows) {
@@ -1232,25 +1235,41 @@ int Core::process_default(GroupList& out_groups,
                 bool self = true;  // every row carries its own search's terms (self_match_) and is indexed
             };
             std::vector<Chunk> ch(nch);
+            const auto ts0 = std::chrono::steady_clock::now();
+            std::vector<double> cbeg(nch), cend(nch);
             wp.run(nch, [&](size_t c) {
-                Chunk& k = ch[c];
-                k.cnt.assign(nsig, 0);
-                k.lastm.assign(nsig, 0);
-                k.maxm.assign(nsig, 0);
+                cbeg[c] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
+                // thread-private until the end (adjacent Chunks share cache
+                // lines: a per-row k.n++ made this sweep 3-4x slower)
+                std::vector<uint32_t> first, cnt(nsig, 0);
+                std::vector<int32_t> lastm(nsig, 0), maxm(nsig, 0);
+                size_t n = 0;
                 bool self = true;
                 for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
                     const uint32_t r = rows[i];
                     if (sel[r] | dec[r]) continue;
                     const uint32_t sg = sig_[r];
-                    if (!k.cnt[sg]++) k.first.push_back(sg);
+                    if (!cnt[sg]++) first.push_back(sg);
                     const int32_t m = std::max(2, maxc_[r]);
-                    k.lastm[sg] = m;
-                    k.maxm[sg] = std::max(k.maxm[sg], m);
+                    lastm[sg] = m;
+                    maxm[sg] = std::max(maxm[sg], m);
                     self = self && self_match_[r] && indexed_[r];
-                    k.n++;
+                    n++;
                 }
+                Chunk& k = ch[c];
+                k.first = std::move(first);
+                k.cnt = std::move(cnt);
+                k.lastm = std::move(lastm);
+                k.maxm = std::move(maxm);
+                k.n = n;
                 k.self = self;
+                cend[c] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
             });
+            for (unsigned c = 0; c < nch; c++) {
+                stats.asm_start_max_ms = std::max(stats.asm_start_max_ms, cbeg[c]);
+                stats.asm_chunk_max_ms = std::max(stats.asm_chunk_max_ms, cend[c] - cbeg[c]);
+            }
+            stats.asm_count_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
             uint64_t bound = 0;
             for (unsigned c = 0; c < nch; c++)
                 for (uint32_t sg : ch[c].first)
@@ -1306,6 +1325,7 @@ int Core::process_default(GroupList& out_groups,
                 }
                 grow_to(P.pool_rows, at[nch]);
             }
+            const auto ts1 = std::chrono::steady_clock::now();
             wp.run(nch, [&](size_t c) {
                 size_t o = at[c];
                 // the chunk's positions, thread-private (the chunks' rows of gat share cache lines)
@@ -1326,6 +1346,7 @@ int Core::process_default(GroupList& out_groups,
                     o++;
                 }
             });
+            stats.asm_scatter_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts1).count();
             return true;
         };
         // RevPrecision: one search per row; large batches build them on the
@@ -1353,6 +1374,7 @@ int Core::process_default(GroupList& out_groups,
             grow_to(brow_group, n);
             wp.run(nch, [&](size_t c) {
                 size_t o = at[c];
+                uint64_t kc = 0;  // thread-private (ck's words share cache lines)
                 for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
                     const uint32_t r = rows[i];
                     if (sel[r] | dec[r]) continue;
@@ -1378,11 +1400,12 @@ int Core::process_default(GroupList& out_groups,
                     g.row_slot = r;
                     g.nrows = 1;
                     g.d.k = cap_k(g, 1, maxc_[r]);
-                    ck[c] += g.d.k;
+                    kc += g.d.k;
                     brow[o] = r;
                     brow_group[o] = (uint32_t)o;
                     o++;
                 }
+                ck[c] = kc;
             });
             uint64_t tot = 0;
             for (unsigned c = 0; c < nch; c++) tot += ck[c];
@@ -2044,7 +2067,7 @@ int Core::process(mm_matched* out) {
                          "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches, %d tier lists) | finish %.2f ms | "
                          "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu | par bucket %.2f work %.2f "
                          "merge %.2f ms (task max %.2f ms, rows %llu, hits %llu) | batch: prep %.2f overlap %.2f wait %.2f "
-                         "post %.2f lists %.2f (%d of %d proven) | replay: gather %.2f job %.2f clear %.2f\n",
+                         "post %.2f lists %.2f (%d of %d proven) | replay: gather %.2f job %.2f clear %.2f | prologue %.2f asm: count %.2f (last start %.2f, chunk max %.2f) scatter %.2f\n",
                          ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms(), stats.replay_ms,
                          stats.apply_ms, stats.batches,
                          stats.parallel_batches, stats.refetches, stats.launches(), stats.tier_lists, ms(t2, t3), ms(t3, t4),
@@ -2052,7 +2075,8 @@ int Core::process(mm_matched* out) {
                          dict_.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms,
                          stats.par_task_max_ms, (unsigned long long)stats.par_rows, (unsigned long long)stats.par_hits,
                          stats.rb_prep_ms, stats.rb_overlap_ms, stats.rb_wait_ms, stats.rb_post_ms, stats.rb_lists_ms, stats.lists_proven,
-                         stats.mscan_lists, stats.par_gather_ms, stats.par_job_ms, stats.par_clear_ms);
+                         stats.mscan_lists, stats.par_gather_ms, stats.par_job_ms, stats.par_clear_ms, stats.prologue_ms, stats.asm_count_ms,
+                         stats.asm_start_max_ms, stats.asm_chunk_max_ms, stats.asm_scatter_ms);
         }
     }
     unwind.armed = false;

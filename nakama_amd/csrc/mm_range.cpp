@@ -124,11 +124,13 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     }
     std::vector<std::vector<uint32_t>> claimed(nch);
     sweep(nch, [&](size_t c) {
+        std::vector<uint32_t> mine;  // thread-private (the chunks' vector headers share cache lines)
         for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++) {
             const uint32_t sg = sig_[brow[bi]];
             if (!rs_mark_[sg].load(std::memory_order_relaxed) && !rs_mark_[sg].exchange(1, std::memory_order_relaxed))
-                claimed[c].push_back(sg);
+                mine.push_back(sg);
         }
+        claimed[c] = std::move(mine);
     });
     std::vector<uint32_t> lsig;
     for (auto& v : claimed) lsig.insert(lsig.end(), v.begin(), v.end());

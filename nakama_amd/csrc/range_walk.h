@@ -306,13 +306,13 @@ struct RangeRun {
                 form = !more;
             }
             if (!form) continue;
-            if (l % tcm != 0) return ReplayCore::BAIL;
+            if (!multiple_of(l, tcm)) return ReplayCore::BAIL;
             bool failed = false;  // :287-296
             for (uint32_t k = 0; k < fcb.nmem[f] && !failed; k++) {
                 const uint32_t m = fcb.mem[f][k];
                 if (!v.live[m]) continue;
                 const HotRec& hs = v.hot[m];
-                failed = hs.minc > l || hs.maxc < l || l % hs.cm != 0;
+                failed = hs.minc > l || hs.maxc < l || !multiple_of(l, hs.cm);
             }
             if (failed) continue;
             grp.clear();
@@ -424,14 +424,14 @@ struct RangeRun {
                 l = (int)fc.size() + tcount;
                 if (l < tmax && std::find(open.begin(), open.end(), (uint32_t)found) == open.end())
                     open.insert(std::lower_bound(open.begin(), open.end(), (uint32_t)found), (uint32_t)found);
-                if (l % tcm != 0) continue;
+                if (!multiple_of(l, tcm)) continue;
             }
             bool failed = false;                                                         // :287-296
             for (const CE& e : fc) {
                 const uint32_t s = e.slot;
                 const HotRec& hs = v.hot[s];
                 if (!v.live[s]) continue;
-                if (hs.minc > l || hs.maxc < l || l % hs.cm != 0) { failed = true; break; }
+                if (hs.minc > l || hs.maxc < l || !multiple_of(l, hs.cm)) { failed = true; break; }
             }
             if (failed) continue;
             grp.clear();

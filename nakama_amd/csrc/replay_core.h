@@ -26,6 +26,21 @@ struct HotRec {
 };
 static_assert(sizeof(HotRec) == 32, "HotRec is half a cache line");
 
+// l % cm == 0 by a table of the multiples below 64 when l < 64 and cm <= 64
+// (the group-forming checks run it once per row and once per member: an
+// integer division each otherwise)
+struct MultipleTable {
+    uint64_t m[65] = {};
+    constexpr MultipleTable() {
+        for (int c = 1; c <= 64; c++)
+            for (int l = 0; l < 64; l += c) m[c] |= 1ull << l;
+    }
+};
+inline constexpr MultipleTable kMultiples{};
+inline bool multiple_of(int l, int cm) {
+    return (unsigned)l < 64u && (unsigned)(cm - 1) < 64u ? ((kMultiples.m[cm] >> l) & 1u) != 0 : l % cm == 0;
+}
+
 struct CE {  // combo entry: (ticket slot, presence index, list position of its hit, session)
     uint32_t slot;
     uint32_t pi;
@@ -322,13 +337,13 @@ struct ReplayCore {
                 form = !more;
             }
             if (!form) continue;
-            if (l % tcm != 0) return BAIL;
+            if (!multiple_of(l, tcm)) return BAIL;
             bool failed = false;  // :287-296
             for (uint32_t k = 0; k < fcb.nmem[f] && !failed; k++) {
                 const uint32_t s = fcb.mem[f][k];
                 if (!v.live[s]) continue;
                 const HotRec& hs = v.hot[s];
-                failed = hs.minc > l || hs.maxc < l || l % hs.cm != 0;
+                failed = hs.minc > l || hs.maxc < l || !multiple_of(l, hs.cm);
             }
             if (failed) continue;
             group_out.clear();
@@ -466,7 +481,7 @@ struct ReplayCore {
                 // a combo created full may have room again: back into the scan, in index order
                 if (l < tmax && std::find(open.begin(), open.end(), (uint32_t)found) == open.end())
                     open.insert(std::lower_bound(open.begin(), open.end(), (uint32_t)found), (uint32_t)found);
-                if (l % tcm != 0) continue;
+                if (!multiple_of(l, tcm)) continue;
             }
             bool failed = false;                                                           // :287-296
             int32_t last_cm = 0;  // l % cm for the previous entry's cm (entries mostly share one)
@@ -476,7 +491,7 @@ struct ReplayCore {
                 const HotRec& hs = v.hot[s];
                 if (!v.live[s]) continue;
                 if (hs.minc > l || hs.maxc < l) { failed = true; break; }
-                if (hs.cm != last_cm) { last_cm = hs.cm; last_ok = l % hs.cm == 0; }
+                if (hs.cm != last_cm) { last_cm = hs.cm; last_ok = multiple_of(l, hs.cm); }
                 if (!last_ok) { failed = true; break; }
             }
             if (failed) continue;
@@ -572,6 +587,7 @@ uint32_t replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uin
 struct DenseRec {
     int32_t count, minc, maxc, cm;
     uint32_t party, sess0, pres_off, intervals, smask;
+    uint32_t live;  // the ticket's live_ flag (constant during a pass: mutators queue), read with its record
 };
 
 // One pool's per-position copies (filled by gather, in parallel chunks).
@@ -636,11 +652,12 @@ struct DensePool {
                 const uint32_t p = rows_list ? brow[bis[k + 16]] : sp[(size_t)(k + 16) * ss];
                 __builtin_prefetch(&v.hot[p]);
                 __builtin_prefetch(&v.intervals[p]);
+                __builtin_prefetch(&v.live[p]);
                 if (map) __builtin_prefetch(&pos_of[p], 1);
             }
             const HotRec& h = v.hot[s];
             rec[k] = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party, h.sess0, h.pres_off,
-                              (uint32_t)v.intervals[s], h.smask};
+                              (uint32_t)v.intervals[s], h.smask, (uint32_t)v.live[s]};
             slot[k] = s;
             if (map) pos_of[s] = k;
         }
@@ -707,7 +724,8 @@ struct DenseRun {
             rt = P.rec[kT];
         } else {
             const HotRec& h = v.hot[T];
-            rt = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party, h.sess0, h.pres_off, (uint32_t)v.intervals[T], h.smask};
+            rt = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party, h.sess0, h.pres_off, (uint32_t)v.intervals[T], h.smask,
+                          (uint32_t)v.live[T]};
         }
         const bool last = (int)rt.intervals + 1 >= max_intervals || rt.minc == rt.maxc;
         const int tcount = rt.count, tmax = rt.maxc, tmin = rt.minc, tcm = rt.cm;
@@ -815,16 +833,16 @@ struct DenseRun {
                 l = (int)fc.size() + tcount;
                 if (l < tmax && std::find(open.begin(), open.end(), (uint32_t)found) == open.end())
                     open.insert(std::lower_bound(open.begin(), open.end(), (uint32_t)found), (uint32_t)found);
-                if (l % tcm != 0) continue;
+                if (!multiple_of(l, tcm)) continue;
             }
             bool failed = false;                                                         // :287-296
             int32_t last_cm = 0;
             bool last_ok = true;
             for (const CE& e : fc) {
-                if (!v.live[e.slot]) continue;
                 const DenseRec& hs = P.rec[e.lpos];
+                if (!hs.live) continue;
                 if (hs.minc > l || hs.maxc < l) { failed = true; break; }
-                if (hs.cm != last_cm) { last_cm = hs.cm; last_ok = l % hs.cm == 0; }
+                if (hs.cm != last_cm) { last_cm = hs.cm; last_ok = multiple_of(l, hs.cm); }
                 if (!last_ok) { failed = true; break; }
             }
             if (failed) continue;
@@ -903,13 +921,12 @@ struct DenseRun {
                 form = !more;
             }
             if (!form) continue;
-            if (l % tcm != 0) return 2;  // the CountMultiple trim: step()
+            if (!multiple_of(l, tcm)) return 2;  // the CountMultiple trim: step()
             bool failed = false;         // :287-296
             for (uint32_t k = 0; k < fcb.nmem[f] && !failed; k++) {
-                const uint32_t m = fcb.mem[f][k];
-                if (!v.live[P.slot[m]]) continue;
-                const DenseRec& hs = P.rec[m];
-                failed = hs.minc > l || hs.maxc < l || l % hs.cm != 0;
+                const DenseRec& hs = P.rec[fcb.mem[f][k]];
+                if (!hs.live) continue;
+                failed = hs.minc > l || hs.maxc < l || !multiple_of(l, hs.cm);
             }
             if (failed) continue;
             fi = f;
