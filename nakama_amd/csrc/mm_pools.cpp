@@ -564,9 +564,10 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         bool all = true;
         for (uint32_t gi : dense_ids) all = all && dense_pools_[gi].nrows == dense_pools_[gi].n;
         // Compared position by position (a parallel pass over the rows,
-        // ~0.1 ms at C3's 1M): identity is decided before any walk or merge
+        // ~0.1 ms at C3's 1M; nothing to compare for a proven list,
+        // BGroup::rows_list): identity is decided before any walk or merge
         // changes the pass state, so a wrong guess can never be caught
-        // half-way (the walk's own check below stays as a guard).
+        // half-way — the walks then read row j's slot from position j.
         if (all) {
             std::vector<uint8_t> ok(ntask_g, 1);
             wp.run(ntask_g, [&](size_t t) {
@@ -592,12 +593,8 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     // 31.3 / 29.3 ms, profiles/r04ab_tgather.txt), so off by default.
     static const bool tgather_mode = std::getenv("NKM_TGATHER") && !std::strcmp(std::getenv("NKM_TGATHER"), "1");
     const bool tgather = tgather_mode && ident && pipe && !gpipe;
-    std::atomic<bool> id_broken{false};  // an identity pool whose row was not at its position (a bug: fail loudly)
     if (ident)
-        for (uint32_t gi : dense_ids) {
-            dense_pools_[gi].identity = true;
-            dense_pools_[gi].broken = &id_broken;
-        }
+        for (uint32_t gi : dense_ids) dense_pools_[gi].identity = true;
     std::unique_ptr<std::atomic<uint32_t>[]> gfront(gpipe ? new std::atomic<uint32_t>[ng] : nullptr);
     std::unique_ptr<std::atomic<uint8_t>[]> gdone(gpipe ? new std::atomic<uint8_t>[ng * ntask_g] : nullptr);
     if (gpipe) {
@@ -850,7 +847,6 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     }
     const auto tg2 = clk::now();
     stats.par_job_ms += msd(tg1, tg2);
-    if (id_broken.load()) throw std::runtime_error("pool replay: a row was not at its list position");
     if (!gpipe) wp.run(ntask_g, [&](size_t t) {
         for (uint32_t gi : dense_ids) {
             const DensePool& D = dense_pools_[gi];

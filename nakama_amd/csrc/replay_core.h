@@ -609,7 +609,6 @@ struct DensePool {
     // gathered; null: the whole list is gathered before the walk
     const std::atomic<uint32_t>* front = nullptr;
     uint32_t pieces = 1;
-    std::atomic<bool>* broken = nullptr;  // set when an identity row is not at its position
 
     void reset(const BGroup& g, const uint32_t* rows, uint32_t n_rows, const uint32_t* batch_slots) {
         sp = g.sp;
@@ -622,7 +621,6 @@ struct DensePool {
         identity = false;
         front = nullptr;
         pieces = 1;
-        broken = nullptr;
         if (rec.size() < n) rec.resize(n);
         if (slot.size() < n) slot.resize(n);
     }
@@ -690,14 +688,20 @@ struct DenseRun {
     void need(const DensePool& P, uint32_t i) {
         if (i >= avail) avail = P.wait_pos(i);
     }
-    // the row's own position: j for an identity pool, else the gather's map
-    uint32_t pos_of_row(const DensePool& P, const uint32_t* pos_of, uint32_t j, uint32_t T) {
+    // row j's ticket T and its position kT.  An identity pool's row j is
+    // position j (checked position by position, or proven, before any walk:
+    // replay_parallel): T is the gathered copy's slot, read in sequence
+    // instead of through the batch rows (a cache miss per row when the pools
+    // interleave: C4's 64).  Else the gather's slot -> position map.
+    void row_at(const DensePool& P, const uint32_t* pos_of, uint32_t j, uint32_t& T, uint32_t& kT) {
         if (P.identity) {
             need(P, j);
-            if (P.slot[j] != T && P.broken) P.broken->store(true);
-            return j;
+            T = P.slot[j];
+            kT = j;
+        } else {
+            T = P.brow[P.bis[j]];
+            kT = pos_of[T];
         }
-        return pos_of[T];
     }
 
     void reset(uint32_t n) {
@@ -715,8 +719,8 @@ struct DenseRun {
     bool step(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of, uint32_t j) {
         const uint32_t n = P.n;
         const uint32_t bi = P.bis[j];
-        const uint32_t T = P.brow[bi];
-        const uint32_t kT = pos_of_row(P, pos_of, j, T);
+        uint32_t T, kT;
+        row_at(P, pos_of, j, T, kT);
         if (kT != kNoSlot && sel[kT]) return false;
         DenseRec rt;
         const uint32_t* tpres = v.pres_sess;
@@ -872,8 +876,8 @@ struct DenseRun {
     int fast_step(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of, uint32_t j) {
         const uint32_t n = P.n;
         const uint32_t bi = P.bis[j];
-        const uint32_t T = P.brow[bi];
-        const uint32_t kT = pos_of_row(P, pos_of, j, T);
+        uint32_t T, kT;
+        row_at(P, pos_of, j, T, kT);
         if (kT != kNoSlot && sel[kT]) return 0;
         int32_t tcount, tmin, tmax, tcm;
         uint32_t tparty, tivl;

@@ -227,22 +227,25 @@ int main(int argc, char** argv) {
         // pool 0: the generic and dense walks, each exact (row()/step()) and
         // fast (exclusive sessions): all four must give the same output
         std::vector<uint8_t> psel(N, 0), proc(N, 0);
-        PoolOut out[4];
-        const char* name[4] = {"generic", "generic-fast", "dense", "dense-fast"};
-        double best[4] = {1e30, 1e30, 1e30, 1e30};
+        PoolOut out[5];
+        const char* name[5] = {"generic", "generic-fast", "dense", "dense-fast", "identity-walk-only"};
+        double best[5] = {1e30, 1e30, 1e30, 1e30, 1e30};
         DensePool P;
         DenseRun run;
         BGroup g;
         g.set_hits(ph[0].data());
         g.n = (uint32_t)ph[0].size();
         const bool prof = std::getenv("RB_PROF") != nullptr;
+        const bool prof_walk = prof && std::atoi(std::getenv("RB_PROF")) == 2;  // the identity walk only
         if (prof) {
             struct sigaction sa {};
             sa.sa_sigaction = on_prof;
             sa.sa_flags = SA_SIGINFO | SA_RESTART;
             sigaction(SIGPROF, &sa, nullptr);
-            itimerval it{{0, 200}, {0, 200}};
-            setitimer(ITIMER_PROF, &it, nullptr);
+            if (!prof_walk) {
+                itimerval it{{0, 200}, {0, 200}};
+                setitimer(ITIMER_PROF, &it, nullptr);
+            }
         }
         for (int r = 0; r < reps; r++) {
             for (int k = 0; k < 2; k++) {
@@ -267,6 +270,25 @@ int main(int argc, char** argv) {
                 P.clear_pos(0, P.n, pos_of.data());
                 best[k] = std::min(best[k], now_ms() - t0);
             }
+            {  // the product's identity pools: the walk alone (gathered untimed)
+                P.reset(g, pbis[0].data(), (uint32_t)pbis[0].size(), brow.data());
+                P.identity = true;
+                P.gather(v, 0, P.n, pos_of.data());
+                run.fast = true;
+                run.reset(P.n);
+                if (prof_walk) {
+                    itimerval it{{0, 100}, {0, 100}};
+                    setitimer(ITIMER_PROF, &it, nullptr);
+                }
+                const double t0 = now_ms();
+                run.walk(P, v, maxI, pos_of.data(), 0, P.nrows);
+                best[4] = std::min(best[4], now_ms() - t0);
+                if (prof_walk) {
+                    itimerval off{};
+                    setitimer(ITIMER_PROF, &off, nullptr);
+                }
+                run.finish(out[4]);
+            }
         }
         if (prof) {
             itimerval off{};
@@ -279,10 +301,10 @@ int main(int argc, char** argv) {
         }
         bool same = true;
         const uint64_t c0 = checksum(out[0]);
-        for (int k = 1; k < 4; k++) same &= checksum(out[k]) == c0;
+        for (int k = 1; k < 5; k++) same &= checksum(out[k]) == c0;
         std::printf("[%s] pool of %u tickets: %zu rows, %u groups |", mode.c_str(), g.n, out[0].recs.size() - 1,
                     out[0].recs.back().gcum);
-        for (int k = 0; k < 4; k++) std::printf(" %s %.3f ms", name[k], best[k]);
+        for (int k = 0; k < 5; k++) std::printf(" %s %.3f ms", name[k], best[k]);
         std::printf(" | checksum %016llx %s\n", (unsigned long long)c0, same ? "MATCH" : "MISMATCH");
         return same ? 0 : 1;
     }
