@@ -131,17 +131,35 @@ void bulk_intern(WorkPool& wp, Dict& d, size_t n, const std::string_view* s, con
     const std::vector<uint32_t> miss = select(wp, n, [&](size_t k) { return !(skip && skip[k]) && ids[k] == UINT32_MAX; });
     const size_t m = miss.size();
     if (!m) return;
+    const size_t nchm = std::max<size_t>(1, std::min<size_t>((size_t)wp.size() * 4, (m + 4095) / 4096));
     std::vector<uint64_t> mh(m);
-    for (size_t i = 0; i < m; i++) mh[i] = h[miss[i]];
+    wp.run(nchm, [&](size_t c) {
+        for (size_t i = m * c / nchm; i < m * (c + 1) / nchm; i++) mh[i] = h[miss[i]];
+    });
     std::vector<uint32_t> rep;
     dedup(wp, m, mh.data(), [&](uint32_t a, uint32_t b) { return s[miss[a]] == s[miss[b]]; }, rep);
     const std::vector<uint32_t> first = select(wp, m, [&](size_t i) { return rep[i] == i; });
     const uint32_t base = (uint32_t)d.size();
     std::vector<uint32_t> nid(m, 0);  // at each first: its new id
     std::vector<uint64_t> boff(first.size() + 1, 0);
-    for (size_t j = 0; j < first.size(); j++) {
-        nid[first[j]] = base + (uint32_t)j;
-        boff[j + 1] = boff[j] + s[miss[first[j]]].size() + 1;
+    {
+        // new ids and arena offsets (a prefix sum of the sizes) in chunks
+        const size_t nfirst = first.size();
+        const size_t ncf = std::max<size_t>(1, std::min<size_t>((size_t)wp.size() * 4, (nfirst + 4095) / 4096));
+        std::vector<uint64_t> part(ncf + 1, 0);
+        wp.run(ncf, [&](size_t c) {
+            uint64_t b = 0;
+            for (size_t j = nfirst * c / ncf; j < nfirst * (c + 1) / ncf; j++) {
+                nid[first[j]] = base + (uint32_t)j;
+                b += s[miss[first[j]]].size() + 1;
+                boff[j + 1] = b;  // chunk-local, rebased below
+            }
+            part[c + 1] = b;
+        });
+        for (size_t c = 0; c < ncf; c++) part[c + 1] += part[c];
+        wp.run(ncf, [&](size_t c) {
+            for (size_t j = nfirst * c / ncf; j < nfirst * (c + 1) / ncf; j++) boff[j + 1] += part[c];
+        });
     }
     char* blk = d.arena.block(boff[first.size()]);
     d.ptr.resize(base + first.size());
@@ -160,7 +178,6 @@ void bulk_intern(WorkPool& wp, Dict& d, size_t n, const std::string_view* s, con
         }
     });
     d.idx.n += nf;
-    const size_t nchm = std::max<size_t>(1, std::min<size_t>((size_t)wp.size() * 4, (m + 4095) / 4096));
     wp.run(nchm, [&](size_t c) {
         for (size_t i = m * c / nchm; i < m * (c + 1) / nchm; i++) ids[miss[i]] = nid[rep[i]];
     });
@@ -228,7 +245,9 @@ bool Core::insert_bulk(const mm_ticket* ts, int32_t n_in, double* ph) {
         for (size_t k = lo; k < hi; k++) qh[k] = str_hash(SV(ts[k].query));
     });
     std::vector<uint32_t> qrep;
-    dedup(wp, n, qh.data(), [&](uint32_t a, uint32_t b) { return SV(ts[a].query) == SV(ts[b].query); }, qrep);
+    dedup(wp, n, qh.data(), [&](uint32_t a, uint32_t b) {  // a shared query string compares by pointer
+        return ts[a].query == ts[b].query || SV(ts[a].query) == SV(ts[b].query);
+    }, qrep);
     const std::vector<uint32_t> qfirst = select(wp, n, [&](size_t k) { return qrep[k] == k; });
     const size_t nq = qfirst.size();
     std::vector<uint32_t> qpos(n, 0);  // at each first: its distinct-query index

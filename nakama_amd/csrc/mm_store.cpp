@@ -1270,16 +1270,30 @@ void Core::maybe_compact() {
 
 // Drops dead slots and renumbers the store (preserves relative slot order, so
 // the scan order stays sorted and insertion-order tie-breaks are unchanged).
-// The work is proportional to the slot count for the fixed-size columns and
-// to the live tickets for strings and dictionaries (a store whose tickets all
-// matched drops its arenas as a few blocks).
+// The work is proportional to the slot count for the fixed-size columns —
+// one column per host worker — and to the live tickets for strings and
+// dictionaries (a store whose tickets all matched drops its arenas as a few
+// blocks, and its columns are simply emptied).
 void Core::compact() {
+    using cclk = std::chrono::steady_clock;
+    const auto c0 = cclk::now();
+    double cph[6] = {0, 0, 0, 0, 0, 0};
+    auto lap = [&, t = c0](int k) mutable {
+        const auto now = cclk::now();
+        cph[k] = std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+    };
     const size_t n = nslots();
     std::vector<uint32_t> remap(n, kNoSlot);
     uint32_t m = 0;
     for (uint32_t s = 0; s < n; s++)
         if (live_[s]) remap[s] = m++;
+    const bool none = m == 0;  // every ticket left (a drained store)
     auto keep = [&](auto& vec) {
+        if (none) {
+            vec.clear();
+            return;
+        }
         size_t w = 0;
         for (uint32_t s = 0; s < n; s++)
             if (live_[s]) vec[w++] = std::move(vec[s]);
@@ -1290,36 +1304,49 @@ void Core::compact() {
     std::vector<uint32_t> npoff{0};
     std::vector<uint32_t> npsess;
     Dict nsess;
-    for (uint32_t s = 0; s < n; s++) {
+    for (uint32_t s = 0; s < n && !none; s++) {
         if (!live_[s]) continue;
         for (uint32_t p = pres_off_[s]; p < pres_off_[s + 1]; p++)
             npsess.push_back(nsess.intern(sess_dict_.str(pres_sess_[p])));
         npoff.push_back((uint32_t)npsess.size());
     }
+    lap(0);
     pres_off_ = std::move(npoff);
     pres_sess_ = std::move(npsess);
     sess_dict_ = std::move(nsess);
     // party dictionary: live parties only
     {
         Dict np;
-        for (uint32_t s = 0; s < n; s++)
+        for (uint32_t s = 0; s < n && !none; s++)
             if (live_[s] && party_[s] != kNoParty) party_[s] = np.intern(party_dict_.str(party_[s]));
         party_dict_ = std::move(np);
     }
     // ticket-id arena: live ids only
     {
         StrArena na;
-        for (uint32_t s = 0; s < n; s++)
+        for (uint32_t s = 0; s < n && !none; s++)
             if (live_[s]) tk_ptr_[s] = na.put(tk(s));
         tk_arena_ = std::move(na);
     }
-    cold_.compact(live_);
-    keep(tk_ptr_); keep(tk_len_); keep(tnode_); keep(created_); keep(ckey_); keep(minc_); keep(maxc_); keep(cm_);
-    keep(count_); keep(intervals_); keep(party_); keep(is_active_); keep(sig_); keep(squery_); keep(indexed_);
-    keep(self_match_);
-    for (size_t f = 0; f < fval_.size(); f++) {
-        if (fval_[f].size() == n) { keep(fval_[f]); keep(fkind_[f]); }
+    lap(1);
+    if (none) cold_.clear();
+    else cold_.compact(live_);
+    {
+        // the columns, one job each on the workers
+        std::vector<std::function<void()>> jobs = {
+            [&] { keep(tk_ptr_); },   [&] { keep(tk_len_); }, [&] { keep(tnode_); },    [&] { keep(created_); },
+            [&] { keep(ckey_); },     [&] { keep(minc_); },   [&] { keep(maxc_); },     [&] { keep(cm_); },
+            [&] { keep(count_); },    [&] { keep(intervals_); }, [&] { keep(party_); }, [&] { keep(is_active_); },
+            [&] { keep(sig_); },      [&] { keep(squery_); }, [&] { keep(indexed_); }, [&] { keep(self_match_); }};
+        for (size_t f = 0; f < fval_.size(); f++)
+            if (fval_[f].size() == n) {
+                jobs.push_back([&, f] { keep(fval_[f]); });
+                jobs.push_back([&, f] { keep(fkind_[f]); });
+            }
+        if (none || !par_mode_) for (auto& j : jobs) j();
+        else workers().run(jobs.size(), [&](size_t k) { jobs[k](); });
     }
+    lap(2);
     live_.assign(m, 1);
     hot_.resize(m);
     for (uint32_t s = 0; s < m; s++) set_hot(s);
@@ -1338,6 +1365,7 @@ void Core::compact() {
         }
         if (party_[s] != kNoParty) party_slots_.add(party_[s], s);
     }
+    lap(3);
     // signatures and clauses: the live tickets' only (a workload of unique
     // queries would grow them without bound); renumbered in slot order
     {
@@ -1375,13 +1403,14 @@ void Core::compact() {
         qsig_.clear();
         qsig_idx_.clear();
     }
+    lap(4);
     std::vector<uint32_t> nact;
     for (uint32_t s : active_list_)
         if (remap[s] != kNoSlot && is_active_[remap[s]]) nact.push_back(remap[s]);
     active_list_ = std::move(nact);
     std::vector<uint32_t> nord;
-    for (uint32_t s : order_)
-        if (remap[s] != kNoSlot) nord.push_back(remap[s]);
+    for (size_t k = 0; k < order_.size() && !none; k++)
+        if (remap[order_[k]] != kNoSlot) nord.push_back(remap[order_[k]]);
     order_ = std::move(nord);
     pending_dead_.clear();
     apply_defer_.clear();  // old slot numbers; the re-upload below carries the flags
@@ -1391,6 +1420,12 @@ void Core::compact() {
     dev_slots_ = 0;
     for (auto& d : dev_field_slots_) d = 0;
     n_live_ = m;
+    lap(5);
+    if (std::getenv("NKM_PROFILE"))
+        std::fprintf(stderr,
+                     "[nkm] compact %zu -> %u slots: remap+sessions %.2f, parties+ids %.2f, cold+columns %.2f, "
+                     "hot+maps %.2f, signatures %.2f, lists %.2f ms\n",
+                     n, m, cph[0], cph[1], cph[2], cph[3], cph[4], cph[5]);
 }
 
 // ---------------------------------------------------------------------------

@@ -315,6 +315,12 @@ struct ColdStore {
     size_t record_bytes(uint32_t s) const {
         return (s + 1 < off.size() ? off[s + 1] : bytes.size()) - off[s];
     }
+    // Drops every record, keeping the buffers' capacity (a drained store:
+    // the next Insert writes into pages already mapped)
+    void clear() {
+        bytes.clear();
+        off.clear();
+    }
     // Keeps the records of the slots where keep[s] (in slot order).
     void compact(const std::vector<uint8_t>& keep) {
         std::vector<char, DefaultInitAlloc<char>> nb;

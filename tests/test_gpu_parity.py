@@ -577,6 +577,37 @@ def test_interleaved_mutations():
             s.close()
 
 
+def test_drained_store_compacts_and_refills():
+    """Every ticket removed, then an Insert: the compaction takes the drained
+    store's shortcut (columns emptied, the cold records' buffer kept) and the
+    refilled store passes like the oracle's — twice, so the second drain
+    reuses the first refill's buffers."""
+    gpu, orc = pair(dict(max_intervals=2))
+    big = synth.TicketSet(3, 70_000)
+    try:
+        for rnd in range(2):
+            small = synth.TicketSet(6, 500, first=100_000 * (rnd + 1))
+            big.insert_into(gpu)
+            big.insert_into(orc)
+            ids = [t.ticket for t in gpu.Extract()]
+            gpu.Remove(ids)
+            orc.Remove(ids)
+            assert gpu.ticket_count() == orc.ticket_count() == 0
+            small.insert_into(gpu)  # compacts: 70,000+ slots, none live
+            small.insert_into(orc)
+            assert state(gpu) == state(orc)
+            assert gpu.Process() == orc.Process()
+            assert state(gpu) == state(orc)
+            rest = [t.ticket for t in gpu.Extract()]
+            gpu.Remove(rest)
+            orc.Remove(rest)
+            small.close()
+    finally:
+        gpu.close()
+        orc.close()
+        big.close()
+
+
 def test_store_compaction_extract_and_replace():
     """Store maintenance at a size that compacts (>= 65,536 slots, over half
     dead): bulk Insert, mass Remove, the compaction on the next Insert, ids
