@@ -469,9 +469,8 @@ struct PassStats {
     double rb_prep_ms = 0, rb_overlap_ms = 0, rb_wait_ms = 0, rb_post_ms = 0, rb_lists_ms = 0;
     int mscan_lists = 0, lists_proven = 0;  // mscan lists placed / proven equal to their rows (not downloaded)
     double par_gather_ms = 0, par_job_ms = 0, par_clear_ms = 0;
-    double asm_count_ms = 0, asm_scatter_ms = 0;
+    double asm_count_ms = 0, asm_scatter_ms = 0;  // assemble_parallel's two sweeps over the rows
     double prologue_ms = 0;  // process_default before its first batch (sel / dec, the active rows)
-    double asm_start_max_ms = 0, asm_chunk_max_ms = 0;  // the count sweep's latest chunk start / longest chunk  // assemble_parallel's two sweeps over the rows
     uint64_t par_rows = 0, par_hits = 0;
 };
 

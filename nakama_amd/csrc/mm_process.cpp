@@ -1236,9 +1236,7 @@ int Core::process_default(GroupList& out_groups,
             };
             std::vector<Chunk> ch(nch);
             const auto ts0 = std::chrono::steady_clock::now();
-            std::vector<double> cbeg(nch), cend(nch);
             wp.run(nch, [&](size_t c) {
-                cbeg[c] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
                 // thread-private until the end (adjacent Chunks share cache
                 // lines: a per-row k.n++ made this sweep 3-4x slower)
                 std::vector<uint32_t> first, cnt(nsig, 0);
@@ -1263,12 +1261,7 @@ int Core::process_default(GroupList& out_groups,
                 k.maxm = std::move(maxm);
                 k.n = n;
                 k.self = self;
-                cend[c] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
             });
-            for (unsigned c = 0; c < nch; c++) {
-                stats.asm_start_max_ms = std::max(stats.asm_start_max_ms, cbeg[c]);
-                stats.asm_chunk_max_ms = std::max(stats.asm_chunk_max_ms, cend[c] - cbeg[c]);
-            }
             stats.asm_count_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
             uint64_t bound = 0;
             for (unsigned c = 0; c < nch; c++)
@@ -2067,7 +2060,7 @@ int Core::process(mm_matched* out) {
                          "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches, %d tier lists) | finish %.2f ms | "
                          "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu | par bucket %.2f work %.2f "
                          "merge %.2f ms (task max %.2f ms, rows %llu, hits %llu) | batch: prep %.2f overlap %.2f wait %.2f "
-                         "post %.2f lists %.2f (%d of %d proven) | replay: gather %.2f job %.2f clear %.2f | prologue %.2f asm: count %.2f (last start %.2f, chunk max %.2f) scatter %.2f\n",
+                         "post %.2f lists %.2f (%d of %d proven) | replay: gather %.2f job %.2f clear %.2f | prologue %.2f asm: count %.2f scatter %.2f\n",
                          ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms(), stats.replay_ms,
                          stats.apply_ms, stats.batches,
                          stats.parallel_batches, stats.refetches, stats.launches(), stats.tier_lists, ms(t2, t3), ms(t3, t4),
@@ -2076,7 +2069,7 @@ int Core::process(mm_matched* out) {
                          stats.par_task_max_ms, (unsigned long long)stats.par_rows, (unsigned long long)stats.par_hits,
                          stats.rb_prep_ms, stats.rb_overlap_ms, stats.rb_wait_ms, stats.rb_post_ms, stats.rb_lists_ms, stats.lists_proven,
                          stats.mscan_lists, stats.par_gather_ms, stats.par_job_ms, stats.par_clear_ms, stats.prologue_ms, stats.asm_count_ms,
-                         stats.asm_start_max_ms, stats.asm_chunk_max_ms, stats.asm_scatter_ms);
+                         stats.asm_scatter_ms);
         }
     }
     unwind.armed = false;
