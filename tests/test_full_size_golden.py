@@ -88,13 +88,24 @@ def test_full_size_pass_equals_oracle(name):
 
 
 @pytest.mark.parametrize("env", [{"NKM_PIPE": "0"}, {"NKM_GPIPE": "0"}, {"NKM_FAST": "0"}, {"NKM_DENSE": "0"},
-                                 {"NKM_KERNEL": "scan"}, {"NKM_THREADS": "4"}],
-                         ids=["nopipe", "gather-first", "exact-walk", "generic-walk", "scan-kernel", "4-threads"])
+                                 {"NKM_KERNEL": "scan"}, {"NKM_THREADS": "4"}, {"NKM_LISTPROOF": "0"},
+                                 {"NKM_LISTPROOF": "2"}],
+                         ids=["nopipe", "gather-first", "exact-walk", "generic-walk", "scan-kernel", "4-threads",
+                              "lists-downloaded", "lists-proof-checked"])
 def test_full_size_c3_host_paths(env, monkeypatch):
-    """C3 at 1M through the other host replay paths and the chunked scan."""
+    """C3 at 1M through the other host replay paths and the chunked scan;
+    the hashed scan's lists downloaded although proven (NKM_LISTPROOF=0), and
+    downloaded and compared with the proof's claim (2: throws on a miss)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     _check("c3")
+
+
+def test_full_size_c4_lists_proof_checked(monkeypatch):
+    """C4's 64 proven lists at 4M, each downloaded and compared with its
+    search's batch rows (NKM_LISTPROOF=2)."""
+    monkeypatch.setenv("NKM_LISTPROOF", "2")
+    _check("c4")
 
 
 POOL_FIELDS = {2: ["properties.region"], 3: ["properties.mode", "properties.region"],
