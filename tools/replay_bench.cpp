@@ -14,7 +14,9 @@
 //                  dense walk (checksums must match; exit status 1 if not)
 //     threads > 0: every pool, dense: gathers in chunks, then one walk per
 //                  pool, on `threads` threads
-//   RB_POOLS=n (default 8), RB_PROF=1 (SIGPROF sampler -> /tmp/rb_prof.txt),
+//   RB_POOLS=n (default 8), RB_PROF=1 (SIGPROF sampler -> /tmp/rb_prof.txt; 2:
+//   the identity walk only), RB_SHUFFLE=1 (c5: the buckets' tickets at random
+//   slots, as a store filled in arrival order holds them),
 //   RB_FAST=0 (threads > 0: exact walk only; sessions here are exclusive, so
 //   the fast walks apply by default)
 #include <atomic>
@@ -106,6 +108,21 @@ static int bench_c5(uint32_t N, int reps) {
         cnt[i] = (uint8_t)n;
         revb[i] = (uint8_t)((1u << n) - 1);
         for (uint32_t a = 0; a < n; a++) pm[(size_t)i * S + a] = (uint8_t)((1u << n) - 1);
+    }
+    if (std::getenv("RB_SHUFFLE")) {
+        // the buckets' tickets at random slots (as a store filled in arrival
+        // order holds them); rows stay in bucket order
+        std::vector<uint32_t> pi(N);
+        for (uint32_t i = 0; i < N; i++) pi[i] = i;
+        for (uint32_t i = N - 1; i > 0; i--) std::swap(pi[i], pi[splitmix(rng) % (i + 1)]);
+        auto perm = [&](auto& a) {
+            auto b = a;
+            for (uint32_t i = 0; i < N; i++) b[pi[i]] = a[i];
+            a.swap(b);
+        };
+        perm(hot); perm(party); perm(intervals); perm(count); perm(minc); perm(maxc); perm(live); perm(created);
+        for (uint32_t i = 0; i < N; i++) brow[i] = pi[i];
+        for (auto& x : slots) x = pi[x];
     }
     ReplayView v{hot.data(), pres_sess.data(), party.data(), intervals.data(), live.data(), count.data(), created.data(),
                  true};
