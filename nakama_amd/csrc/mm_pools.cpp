@@ -408,6 +408,9 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
 // one pass over the batch in row order assembles the groups, the expired list
 // and the Intervals increments — processDefault's sequential order, because
 // no pool ever selects another pool's ticket.
+// A proven list's sp points at its reserved words in the library's pinned
+// host list buffer (Core::h_out_, run_batch's cg_off), which the download
+// would have filled: the batch rows are written there instead.
 void Core::fill_row_lists(std::vector<BGroup>& bg, const UVec<uint32_t>& brow, const UVec<uint32_t>& brow_group) {
     if (!row_lists_pending_) return;
     row_lists_pending_ = false;
