@@ -179,12 +179,16 @@ int  mm_process_commit(void* h, const int32_t* group_offsets, const mm_entry_ref
                        int32_t n_groups, mm_matched* out);
 void mm_free_matched(void* h, mm_matched* out);
 
-/* Tickets that left the matchmaker by a removal (Remove*, or a re-inserted
- * ticket id replacing its old record) since the previous call; the first call
- * starts the recording.  Tickets matched by a pass are not repeated here: they
- * are the pass's result (mm_matched), delivered and dropped from there.  The
- * Go shim drops its delivery entries with them (ABI 4: before, matched
- * tickets were logged too, a million strings per 1M-ticket pass). */
+/* Tickets that left the matchmaker by an explicit removal (Remove*) since the
+ * previous call; the first call starts the recording.  A re-inserted ticket id
+ * that replaces its old record is not reported (the id stays in the
+ * matchmaker).  Tickets matched by a pass are not repeated here: they are the
+ * pass's result (mm_matched), delivered and dropped from there.  The Go shim
+ * drops its delivery entries with them (ABI 4: before, matched tickets were
+ * logged too, a million strings per 1M-ticket pass).  The multi-device handle
+ * (mm_create_multi) reports only ids no sub-handle holds at the drain: an id
+ * removed and then added again before the drain is live and not reported
+ * there, while a single handle reports its removal. */
 int  mm_drain_removed(void* h, mm_str_list* out);
 void mm_free_str_list(void* h, mm_str_list* out);
 
@@ -210,10 +214,6 @@ int32_t mm_find_tickets(void* h, const char* const* tickets, int32_t n, uint8_t*
  * right now (sorted, self removed): up to cap ticket strings written as
  * pointers valid until the next call on h; returns the total hit count. */
 int32_t mm_debug_hits(void* h, const char* ticket, const char** tickets_out, double* scores_out, int32_t cap);
-/* groupIndexes (matchmaker.go:132-167) over n synthetic indexes (count,
- * created_at); writes up to cap groups as member positions (into the input
- * arrays, in the reference's append order) and avgCreatedAt; returns the
- * number of groups.  group_members must hold 8*cap entries. */
 /* Query-string compile status only (no device work): MM_OK,
  * MM_ERR_QUERY_INVALID or MM_ERR_UNSUPPORTED. */
 int mm_debug_compile(const char* query);
@@ -225,6 +225,10 @@ int mm_debug_compile(const char* query);
  * every search with the pattern fails (Go/vellum parse error, fuzziness outside
  * [0, 2]), -2 for a construct not lowered (MM_ERR_UNSUPPORTED at Add). */
 int mm_debug_term_match(int32_t kind, const char* pattern, int32_t fuzziness, const char* term, double* boost);
+/* groupIndexes (matchmaker.go:132-167) over n synthetic indexes (count,
+ * created_at); writes up to cap groups as member positions (into the input
+ * arrays, in the reference's append order) and avgCreatedAt; returns the
+ * number of groups.  group_members must hold 8*cap entries. */
 int32_t mm_debug_group_indexes(const int32_t* counts, const int64_t* created_at, int32_t n, int32_t required,
                                int32_t* group_offsets, int32_t* group_members, int64_t* avg_created_at, int32_t cap);
 

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <exception>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -163,6 +164,26 @@ struct Sig {
     uint8_t rs_nrange = 0;  // its range clauses
 };
 
+// Moved on by every failed pass of any handle (Core::reset_pass_scratch).
+inline std::atomic<uint64_t> g_scratch_epoch{0};
+
+// A worker thread's per-slot flags for the parallel walks (selected this
+// batch, Intervals increment pending): zero between tasks; re-zeroed whole
+// when the handle's scratch epoch moved on (a pass threw midway).
+struct TlFlags {
+    std::vector<uint8_t> sel, proc;
+    uint64_t epoch = 0;
+    void ready(size_t n, uint64_t cur_epoch) {
+        if (epoch != cur_epoch) {
+            sel.assign(sel.size(), 0);
+            proc.assign(proc.size(), 0);
+            epoch = cur_epoch;
+        }
+        if (sel.size() < n) sel.resize(n, 0);
+        if (proc.size() < n) proc.resize(n, 0);
+    }
+};
+
 // Persistent host workers for the pass's data-parallel host phases (pool
 // replay, post-pass bookkeeping): run(n, fn) calls fn(0..n-1) over the
 // workers and the caller, and returns when all n tasks are done.
@@ -221,8 +242,13 @@ public:
             }
             relax();
         }
-        std::lock_guard<std::mutex> lk(m_);
-        job_.reset();
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_.reset();
+        }
+        // a task's exception, rethrown on the caller once every task is done
+        // (no worker is still inside fn, whose captures may be on this stack)
+        if (job->failed.load(std::memory_order_acquire)) std::rethrow_exception(job->err);
     }
 
 private:
@@ -237,13 +263,22 @@ private:
         const std::function<void(size_t)>* fn;
         const size_t n;
         std::atomic<size_t> next{0}, done{0};
+        std::atomic<bool> failed{false};
+        std::mutex err_mu;
+        std::exception_ptr err;  // the first task exception (under err_mu)
     };
     void work(Job& j) {
         size_t mine = 0;
         for (;;) {
             const size_t i = j.next.fetch_add(1);
             if (i >= j.n) break;
-            (*j.fn)(i);
+            try {
+                (*j.fn)(i);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(j.err_mu);
+                if (!j.err) j.err = std::current_exception();
+                j.failed.store(true, std::memory_order_release);
+            }
             mine++;
         }
         if (mine && j.done.fetch_add(mine) + mine == j.n) {
@@ -742,6 +777,13 @@ private:
     size_t rs_mark_cap_ = 0;
     std::vector<uint32_t> rs_sig_loc_;  // signature -> its index in the batch (valid for the batch's signatures)
     std::vector<uint32_t> rs_leaf_;     // slot -> its leaf in its pool during a range batch, else kNoSlot
+    // Per-slot scratch that the parallel walks keep all zero (kNoSlot) between
+    // tasks — rs_mark_, rs_leaf_, pos_of_ and every worker's thread-local
+    // selection / pending-Intervals flags (TlFlags).  A pass that throws
+    // midway may leave entries set: reset_pass_scratch() clears the shared
+    // arrays and moves g_scratch_epoch on, and each worker re-zeroes its
+    // thread-local flags before it uses them again.
+    void reset_pass_scratch();
     std::vector<RRange> rs_tiers_;      // the batch's signatures' tier lists
     DevArray<uint8_t> d_rblob_;         // pools, tiles, block -> pool, bound queries
     PinnedArray<uint8_t> h_rblob_;

@@ -588,14 +588,9 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     // goes without them
     if (!ident && !view) fill_row_lists(bg, brow, brow_group);
     const bool gpipe = ident && pipe && wp.size() > ntask;
-    // Identity pools with more walks than workers (C4: 64 pools on 16): no
-    // worker is left to gather beside the walks.  NKM_TGATHER=1: each walk
-    // gathers its own pool first (its copies then in its core's cache)
-    // instead of a separate gather phase before all walks — measured even
-    // with the default on C4 (same box, 2 x 2 runs: p50 30.2 / 31.3 vs
-    // 31.3 / 29.3 ms, profiles/r04ab_tgather.txt), so off by default.
-    static const bool tgather_mode = std::getenv("NKM_TGATHER") && !std::strcmp(std::getenv("NKM_TGATHER"), "1");
-    const bool tgather = tgather_mode && ident && pipe && !gpipe;
+    // (Identity pools with more walks than workers, C4's 64 on 16, gather
+    // in a separate phase before the walks: gathering each pool inside its
+    // walk's task measured even, profiles/r04ab_tgather.txt, and was removed.)
     if (ident)
         for (uint32_t gi : dense_ids) dense_pools_[gi].identity = true;
     std::unique_ptr<std::atomic<uint32_t>[]> gfront(gpipe ? new std::atomic<uint32_t>[ng] : nullptr);
@@ -625,8 +620,8 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     };
     // each pool's entry bound (every ticket of its list and rows joins at
     // most one group): the walk reserves it so readers never see a move
-    std::vector<uint64_t> esum(pipe && !gpipe && !tgather ? ntask_g * ng : 0, 0);
-    if (!gpipe && !tgather)
+    std::vector<uint64_t> esum(pipe && !gpipe ? ntask_g * ng : 0, 0);
+    if (!gpipe)
         wp.run(ntask_g, [&](size_t t) {
             for (uint32_t gi : dense_ids) {
                 DensePool& D = dense_pools_[gi];
@@ -649,9 +644,9 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     std::unique_ptr<Prog[]> prog(pipe ? new Prog[ng] : nullptr);
     std::vector<uint64_t> ebound(pipe ? ng : 0, 0);
     uint64_t ebound_all = 0;
-    for (size_t t = 0; pipe && !gpipe && !tgather && t < ntask_g; t++)
+    for (size_t t = 0; pipe && !gpipe && t < ntask_g; t++)
         for (size_t gi = 0; gi < ng; gi++) ebound[gi] += esum[t * ng + gi];
-    if (gpipe || tgather)  // identity pools: the rows are list members, whose entries are at most max_pres_ each
+    if (gpipe)  // identity pools: the rows are list members, whose entries are at most max_pres_ each
         for (uint32_t gi : dense_ids) ebound[gi] = (uint64_t)dense_pools_[gi].n * (uint64_t)std::max(1, max_pres_);
     for (uint64_t e : ebound) ebound_all += e;
     const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
@@ -732,7 +727,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         }
     };
     std::vector<double> task_ms(ntask, 0.0), walk_prep_ms(ntask, 0.0), walk_ms(ntask, 0.0);  // NKM_PROFILE=2 split
-    std::vector<uint64_t> task_hits(ntask, 0);
+    std::vector<uint64_t> task_hits(ntask, 0), task_pairs(ntask, 0);
     std::vector<uint32_t> pool_stop(ng, UINT32_MAX);  // per pool: the batch row its list ran out at
     auto to_rows = [&](const PoolOut& o, uint32_t task, std::vector<std::pair<uint32_t, int>>& ents) {
         const uint32_t base = (uint32_t)ents.size();
@@ -754,13 +749,14 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         // mask dropped them before this batch's searches).  Intervals stay
         // unwritten during the walk (slots of all pools share its cache
         // lines): a row's increment is pending in tl_proc until the merge.
-        static thread_local std::vector<uint8_t> tl_sel, tl_proc;
-        if (tl_sel.size() < sel.size()) tl_sel.resize(sel.size(), 0);
-        if (tl_proc.size() < sel.size()) tl_proc.resize(sel.size(), 0);
+        static thread_local TlFlags tl;
+        tl.ready(sel.size(), g_scratch_epoch.load(std::memory_order_relaxed));
+        std::vector<uint8_t>& tl_sel = tl.sel;
+        std::vector<uint8_t>& tl_proc = tl.proc;
         PassStats ls;
         const std::unique_ptr<ReplayCore> rpp = make_replay(tl_sel, rev, maxI, ls);
         ReplayCore& rp = *rpp;
-        uint64_t hits = 0;  // task_hits[t] at the end: neighbouring tasks' counters share a line
+        uint64_t hits = 0, pairs = 0;  // task_hits / task_pairs[t] at the end: neighbouring tasks' counters share a line
         for (uint32_t k = task_off[t]; k < task_off[t + 1]; k++) {
             const uint32_t gi = order_g[k];
             PoolOut& po = few ? pool_outs_[gi] : o;
@@ -769,7 +765,6 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             if (dense[gi] && pipe) {
                 const DensePool& D = dense_pools_[gi];
                 const auto tr0 = clk::now();
-                if (tgather) dense_pools_[gi].gather(rv, 0, D.n, pos_of_.data());  // identity: no slot map written
                 run.reset(D.n);
                 run.fast = fast_mode_;
                 run.recs.reserve((size_t)D.nrows + 1);
@@ -783,6 +778,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                 if (run.ents.data() != prog[gi].ents || run.recs.data() != prog[gi].recs)
                     std::abort();  // the bound above was wrong: readers hold the old buffers
                 hits += run.hits_seen;
+                pairs += (uint64_t)run.recs.size() * D.src_len;
                 // the sentinel (its capacity was reserved), then the buffers to
                 // the pool's PoolOut (a header swap: the readers' pointers stay)
                 run.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)run.ents.size(), 0, run.g_run, run.x_run});
@@ -795,6 +791,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                 run.fast = fast_mode_;
                 run.walk(dense_pools_[gi], rv, maxI, pos_of_.data(), 0, dense_pools_[gi].nrows);
                 hits += run.hits_seen;
+                pairs += (uint64_t)run.recs.size() * dense_pools_[gi].src_len;
                 if (few) {
                     run.finish(po);
                     continue;
@@ -810,6 +807,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                 const uint32_t* prow = P.pool_rows.data() + P.pool_off[gi];
                 const size_t npr = P.pool_off[gi + 1] - P.pool_off[gi];
                 rp.hits_seen = 0;
+                rp.pairs = 0;
                 const uint32_t stop =
                     view ? replay_pool(rp, prow, npr, brow.data(), *view, tl_sel, tl_proc.data(), minc_.data(),
                                        maxc_.data(), po)
@@ -818,10 +816,12 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                                        tl_proc.data(), minc_.data(), maxc_.data(), po);
                 if (stop != UINT32_MAX) pool_stop[gi] = stop;
                 hits += rp.hits_seen;
+                pairs += rp.pairs;
             }
             if (!few) to_rows(o, (uint32_t)t, ents);
         }
         task_hits[t] = hits;
+        task_pairs[t] = pairs;
         task_ms[t] = msd(tw0, clk::now());
     };
     const auto tg1 = clk::now();
@@ -873,6 +873,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     for (size_t k = 0; k < ntask; k++) {
         stats.par_task_max_ms = std::max(stats.par_task_max_ms, task_ms[k]);
         stats.par_hits += task_hits[k];
+        if (!row_shard() || shard_rank_ == 0) stats.pairs_decided += (int64_t)task_pairs[k];
     }
     if (batch_profile_ && pipe) {
         double sp = 0, sw = 0, st = 0, mw = 0;
@@ -884,7 +885,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         }
         std::fprintf(stderr, "[nkm]   pool walks: %zu tasks, %zu pools on %u workers | sum: tasks %.2f, walks %.2f (max %.2f), "
                      "gather+reset+reserve %.2f ms | gather %s\n", ntask, ng, wp.size(), st, sw, mw, sp,
-                     gpipe ? "beside" : tgather ? "in each walk's task" : "before");
+                     gpipe ? "beside" : "before");
     }
     stats.par_rows += nb;
     return true;
@@ -1200,7 +1201,6 @@ PackLayout Core::run_packed(const PackBatch& pb, PassStats& stats, const std::fu
                         (int64_t)((double)pb.unique * (5.0 + per_live)) + (int64_t)ents * 4 +
                         (int64_t)pb.n * (int64_t)(P * L.pm_w + L.rev_w + 1);
     stats.pair_evals += (int64_t)pb.scanned;
-    stats.pairs_decided += (int64_t)pb.scanned;  // every row one search over its own source
     return L;
 }
 
@@ -1220,6 +1220,7 @@ std::function<BGroup&(uint32_t)> Core::packed_view(const PackLayout& L, const UV
         static thread_local BGroup g;
         const uint32_t T = brow[bi];
         fill_packed(g, base, L, bi, T, sig_[T]);
+        g.d.src_len = h_srows_.p[bi].src_len & ~kSrcOrder;  // the row's source (pairs decided)
         return g;
     };
 }

@@ -38,6 +38,9 @@ struct Replay : ReplayCore {
     PassStats& stats;
     DStore st;
     hipStream_t stream;
+    // processCustom: every batch row searches (pairs decided counted per batch);
+    // processDefault counts the rows that searched as they are decided
+    bool all_rows_search = false;
 
     static ReplayView view(const Core& core) {
         return ReplayView{core.hot_.data(), core.pres_sess_.data(), core.party_.data(), core.intervals_.data(),
@@ -827,7 +830,7 @@ struct Replay : ReplayCore {
             stats.k_launches[kk]++;
         }
         stats.batches++;
-        if (!c.row_shard() || c.shard_rank_ == 0)  // the replicated replay decides every row on every rank
+        if (all_rows_search && (!c.row_shard() || c.shard_rank_ == 0))  // processCustom: every row searches
             for (const BGroup& g : bg) stats.pairs_decided += (int64_t)g.nrows * (int64_t)g.d.src_len;
         {
             // per-search accounting (on the workers for large batches)
@@ -1562,6 +1565,9 @@ int Core::process_default(GroupList& out_groups,
             if (win != SIZE_MAX) win = win > SIZE_MAX / 2 ? SIZE_MAX : 2 * win;
         }
     }
+    // rows that searched x their sources (the parallel replays add theirs);
+    // row-sharded: the replicated replay decides every row on every rank
+    if (!row_shard() || shard_rank_ == 0) stats.pairs_decided += (int64_t)rp.pairs;
     if (out_of_order) {
         filled_groups_ = 0;  // the early-filled result entries are in the old order
         // back into the pinned row order: a group's searching ticket (its last
@@ -1599,6 +1605,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
     const DStore st = dstore();
     std::vector<uint8_t> sel(nslots(), 0);  // processCustom never selects
     Replay rp(*this, sel, rev, maxI, stats, st, stream_);
+    rp.all_rows_search = true;
     while (order_head_ < order_.size() && !live_[order_[order_head_]]) order_head_++;
     const uint32_t kvar = (uint32_t)var_k_capacity();
     // every row is independent: one search per row, in chunks
@@ -2005,6 +2012,7 @@ int Core::process(mm_matched* out) {
             }
             c.pass_running_ = false;
             c.custom_open_ = false;
+            c.reset_pass_scratch();  // a walk may have thrown with its flags set
             c.sel_.assign(c.sel_.size(), 0);
             c.apply_defer_.clear();
             c.dev_slots_ = 0;  // sync_device: every slot's alive flag again

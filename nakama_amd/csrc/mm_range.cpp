@@ -24,6 +24,13 @@
 
 namespace nkm {
 
+void Core::reset_pass_scratch() {
+    for (size_t k = 0; k < rs_mark_cap_; k++) rs_mark_[k].store(0, std::memory_order_relaxed);
+    std::fill(rs_leaf_.begin(), rs_leaf_.end(), kNoSlot);
+    std::fill(pos_of_.begin(), pos_of_.end(), kNoSlot);
+    g_scratch_epoch.fetch_add(1, std::memory_order_relaxed);
+}
+
 bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList& out_groups,
                        std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats) {
     using clk = std::chrono::steady_clock;
@@ -264,7 +271,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     if (task_ents_.size() < ntask) task_ents_.resize(ntask);
     RowRec* rr = few ? nullptr : row_recs_.data();
     if (!few) std::memset((void*)rr, 0, nb * sizeof(RowRec));
-    std::vector<uint64_t> task_hits(ntask, 0);
+    std::vector<uint64_t> task_hits(ntask, 0), task_pairs(ntask, 0);
     std::vector<double> pool_build_ms(ng, 0.0), pool_walk_ms(ng, 0.0);  // NKM_PROFILE=2
     // each pool's valid candidates: a prefix of its sorted elements
     std::vector<uint32_t> valid(ng, 0);
@@ -305,9 +312,10 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     });
     const auto t2b = clk::now();
     auto worker = [&](size_t t) {
-        static thread_local std::vector<uint8_t> tl_sel, tl_proc;
-        if (tl_sel.size() < sel.size()) tl_sel.resize(sel.size(), 0);
-        if (tl_proc.size() < sel.size()) tl_proc.resize(sel.size(), 0);
+        static thread_local TlFlags tl;
+        tl.ready(sel.size(), g_scratch_epoch.load(std::memory_order_relaxed));
+        std::vector<uint8_t>& tl_sel = tl.sel;
+        std::vector<uint8_t>& tl_proc = tl.proc;
         static thread_local RangeRun run{};
         run.v = rv;
         run.max_intervals = maxI;
@@ -319,6 +327,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
         static thread_local PoolOut o;
         auto& ents = task_ents_[t];
         ents.clear();
+        uint64_t pairs = 0;
         for (uint32_t k = task_off[t]; k < task_off[t + 1]; k++) {
             const uint32_t p = order_p[k];
             RangePoolHost& H = rs_pools_[p];
@@ -364,6 +373,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
                      },
                      po);
             pool_walk_ms[p] = msd(tb1, clk::now());
+            pairs += (uint64_t)(po.recs.size() - 1) * d.src_len;  // rows that searched (the last record is the sentinel)
             pool_build_ms[p] = msd(tb0, tb1);
             for (uint32_t j = 0; j < nv; j++) rs_leaf_[H.slot[j]] = kNoSlot;
             if (!few) {
@@ -376,6 +386,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             }
         }
         task_hits[t] = run.hits_seen;
+        task_pairs[t] = pairs;
     };
     wp.run(ntask, worker);
     const auto t3 = clk::now();
@@ -392,7 +403,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     stats.k_bytes[5] += (int64_t)(src_total * 5 + nvalid * 9 + n_elems * 12);
     stats.k_bytes[4] += (int64_t)(n_merge * n_elems * 24);
     stats.pair_evals += (int64_t)src_total;
-    for (size_t p = 0; p < ng; p++) stats.pairs_decided += (int64_t)prows(p) * (int64_t)rs_pools_[p].d.src_len;
+    for (uint64_t q : task_pairs) stats.pairs_decided += (int64_t)q;
     for (uint64_t h : task_hits) stats.par_hits += h;
     stats.par_rows += nb;
     stats.assemble_ms += msd(t0, t1);

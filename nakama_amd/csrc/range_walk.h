@@ -422,8 +422,7 @@ struct RangeRun {
                     }
                 }
                 l = (int)fc.size() + tcount;
-                if (l < tmax && std::find(open.begin(), open.end(), (uint32_t)found) == open.end())
-                    open.insert(std::lower_bound(open.begin(), open.end(), (uint32_t)found), (uint32_t)found);
+                close_trimmed(open, (uint32_t)found);
                 if (!multiple_of(l, tcm)) continue;
             }
             bool failed = false;                                                         // :287-296

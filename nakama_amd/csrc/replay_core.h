@@ -70,6 +70,19 @@ inline void group_indexes(const std::vector<uint32_t>& in, size_t from, int requ
     group_indexes(in, from + 1, required, cnt, created, out);
 }
 
+// After the CountMultiple trim the combo is out of the first-fit scan for the
+// rest of the row, whatever follows.  Go trims `foundCombo`, a slice header
+// over the backing array of entryCombos[foundComboIdx]
+// (matchmaker_process.go:213-214, 262-271): the stored slice keeps its
+// pre-trim length (tail slots nil'd), so a trimmed combo that is then rejected
+// (:276-279, :294-296) still counts as full at :170 — it formed at
+// l == MaxCount — and never takes another hit.  (A trim in the last-interval
+// branch happens at the row's last hit, after which nothing is scanned.)
+inline void close_trimmed(std::vector<uint32_t>& open, uint32_t combo) {
+    auto it = std::find(open.begin(), open.end(), combo);
+    if (it != open.end()) open.erase(it);
+}
+
 // The smallest mask >= x with at most c bits set (c >= 1).  Every value
 // skipped lies in (x, x + lowbit(x)) for an x with more than c bits, i.e. it
 // holds x's bits plus lower ones: combineIndexes (matchmaker_process.go:
@@ -217,6 +230,9 @@ struct ReplayCore {
     // MaxCount) scans nothing instead of every earlier hit's combo.
     std::vector<uint32_t> open;
     uint64_t hits_seen = 0;  // profiling: hit-list entries the rows walked
+    // (row, candidate) pairs decided: the source lengths of the rows that
+    // searched (PassStats::pairs_decided)
+    uint64_t pairs = 0;
     // pool-parallel replay: rows this worker processed earlier in the batch,
     // whose Intervals increments are applied after the batch (1 = one pending)
     const uint8_t* proc = nullptr;
@@ -265,11 +281,12 @@ struct ReplayCore {
     // processDefault's loop body for T: fast_row() when it applies (and does
     // not bail), else row().
     Status decide(uint32_t T, BGroup& g, bool can_fetch, std::vector<std::pair<uint32_t, int>>& group_out) {
-        if (fast && v.sessions_exclusive && g.complete && (!rev || (g.pm && g.pm_n >= g.n && g.n <= kPairP))) {
-            const Status s = fast_row(T, g, group_out);
-            if (s != BAIL) return s;
-        }
-        return row(T, g, can_fetch, group_out);
+        Status s = BAIL;
+        if (fast && v.sessions_exclusive && g.complete && (!rev || (g.pm && g.pm_n >= g.n && g.n <= kPairP)))
+            s = fast_row(T, g, group_out);
+        if (s == BAIL) s = row(T, g, can_fetch, group_out);
+        if (s != EXHAUSTED) pairs += g.d.src_len;  // the row searched: its source's candidates decided
+        return s;
     }
 
     // row() when no two live tickets share a session, over a complete list:
@@ -478,9 +495,7 @@ struct ReplayCore {
                     }
                 }
                 l = (int)fc.size() + tcount;
-                // a combo created full may have room again: back into the scan, in index order
-                if (l < tmax && std::find(open.begin(), open.end(), (uint32_t)found) == open.end())
-                    open.insert(std::lower_bound(open.begin(), open.end(), (uint32_t)found), (uint32_t)found);
+                close_trimmed(open, (uint32_t)found);
                 if (!multiple_of(l, tcm)) continue;
             }
             bool failed = false;                                                           // :287-296
@@ -595,6 +610,7 @@ struct DensePool {
     const uint32_t* sp = nullptr;  // the list's slots (BGroup::slot)
     uint32_t ss = 4;
     uint32_t n = 0;
+    uint32_t src_len = 0;  // the pool's search source (pairs decided per row that searches)
     const uint32_t* bis = nullptr;  // the pool's batch rows, ascending
     uint32_t nrows = 0;
     const uint32_t* brow = nullptr;  // batch row -> slot
@@ -614,6 +630,7 @@ struct DensePool {
         sp = g.sp;
         ss = g.ss;
         n = g.n;
+        src_len = g.d.src_len;
         rows_list = g.rows_list;
         bis = rows;
         nrows = n_rows;
@@ -835,8 +852,7 @@ struct DenseRun {
                     }
                 }
                 l = (int)fc.size() + tcount;
-                if (l < tmax && std::find(open.begin(), open.end(), (uint32_t)found) == open.end())
-                    open.insert(std::lower_bound(open.begin(), open.end(), (uint32_t)found), (uint32_t)found);
+                close_trimmed(open, (uint32_t)found);
                 if (!multiple_of(l, tcm)) continue;
             }
             bool failed = false;                                                         // :287-296

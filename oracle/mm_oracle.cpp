@@ -31,6 +31,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -853,6 +854,14 @@ static void process_default(Matchmaker& m, const vector<IP>& order,
                 if ((int)combo.size() + (int)hit->entries.size() + ai->count <= ai->max_count) {
                     bool mutual_conflict = false;
                     for (auto& e : combo) {
+                        // A nil'd slot of a trimmed combo (below) would be a nil
+                        // dereference in Go here; unreachable: such a combo formed
+                        // at l == MaxCount and has no room at :170 (or it was
+                        // trimmed at the row's last hit).
+                        if (!e.idx) {
+                            std::fprintf(stderr, "oracle: nil MatchmakerEntry in a combo with room (matchmaker_process.go:174)\n");
+                            std::abort();
+                        }
                         if (hit->session_set.count(e.idx->entries[e.pi].session_id)) { session_conflict = true; break; }
                         if (rev) {
                             if (!validate_match(m, *hit, e.idx->ticket)) { mutual_conflict = true; break; }
@@ -874,8 +883,13 @@ static void process_default(Matchmaker& m, const vector<IP>& order,
                 combos.push_back(std::move(nc));
                 found_idx = (int)combos.size() - 1;
             }
-            vector<Entry>& found = combos[found_idx];
-            int l = (int)found.size() + ai->count;
+            // foundCombo (:213, :224) is a slice header over the backing array of
+            // entryCombos[foundComboIdx]: `stored` is that array, `flen` the
+            // header's length.  The trim below shortens the header only; the
+            // stored slice keeps its length with nil'd tail slots (:265-267).
+            vector<Entry>& stored = combos[found_idx];
+            int flen = (int)stored.size();
+            int l = flen + ai->count;
             if (l == ai->max_count ||
                 (last_interval && l >= ai->min_count && l <= ai->max_count && hit_counter >= last_hit_counter)) {
                 int rem = l % ai->count_multiple;
@@ -883,8 +897,8 @@ static void process_default(Matchmaker& m, const vector<IP>& order,
                     // eligibleIndexesUniq, pinned to first-appearance order
                     vector<IP> eligible;
                     std::unordered_set<const Index*> seen;
-                    for (auto& e : found) {
-                        auto fi = indexes_copy.find(e.idx->ticket);
+                    for (int i = 0; i < flen; i++) {
+                        auto fi = indexes_copy.find(stored[i].idx->ticket);
                         if (fi != indexes_copy.end() && fi->second->count <= rem && !seen.count(fi->second.get())) {
                             seen.insert(fi->second.get());
                             eligible.push_back(fi->second);
@@ -895,20 +909,21 @@ static void process_default(Matchmaker& m, const vector<IP>& order,
                     std::stable_sort(groups.begin(), groups.end(),
                                      [](const IGroup& a, const IGroup& b) { return a.avg < b.avg; });
                     for (auto& eg : groups[0].indexes) {
-                        for (int i = 0; i < (int)found.size(); i++) {
-                            if (eg->ticket == found[i].idx->ticket) {
-                                found[i] = found.back();   // swap-remove (:262-271)
-                                found.pop_back();
+                        for (int i = 0; i < flen; i++) {
+                            if (eg->ticket == stored[i].idx->ticket) {
+                                stored[i] = stored[flen - 1];       // swap-remove in the shared array (:265)
+                                stored[flen - 1] = Entry{nullptr, 0};  // :266
+                                flen--;                               // :267 (the header only)
                                 i--;
                             }
                         }
                     }
-                    l = (int)found.size() + ai->count;
+                    l = flen + ai->count;
                     if (l % ai->count_multiple != 0) continue;
                 }
                 bool cond_failed = false;
-                for (auto& e : found) {
-                    auto fi = indexes_copy.find(e.idx->ticket);
+                for (int i = 0; i < flen; i++) {
+                    auto fi = indexes_copy.find(stored[i].idx->ticket);
                     if (fi != indexes_copy.end() &&
                         (fi->second->min_count > l || fi->second->max_count < l || l % fi->second->count_multiple != 0)) {
                         cond_failed = true;
@@ -916,7 +931,7 @@ static void process_default(Matchmaker& m, const vector<IP>& order,
                     }
                 }
                 if (cond_failed) continue;
-                vector<Entry> current = found;
+                vector<Entry> current(stored.begin(), stored.begin() + flen);
                 for (int k = 0; k < (int)ai->entries.size(); k++) current.push_back({ai, k});
                 combos.erase(combos.begin() + found_idx);
                 for (auto& e : current) {

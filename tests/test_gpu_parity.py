@@ -334,6 +334,41 @@ def test_bulk_insert_falls_back_on_known_ids(monkeypatch):
         b.close()
 
 
+@pytest.mark.parametrize("idq", ["party", "ticket"])
+def test_bulk_insert_first_id_field_query(idq, monkeypatch):
+    """A bulk Insert whose batch holds the first query reading the `party_id`
+    or `ticket` field (MapMatchmakerIndex indexes both, match_common.go): the
+    batch falls back to the per-ticket path, which fills those columns for its
+    own tickets, so searches see every ticket's id terms."""
+    monkeypatch.setenv("NKM_BULK", "force")
+    n, t0 = 5000, 1_700_000_000_000_000_000
+    ts = []
+    for i in range(n):
+        mode = "m%d" % (i % 3)
+        party = "p%d" % (i // 2) if i % 5 == 0 else ""
+        q = "+properties.mode:" + mode
+        if i % 7 == 0:
+            q += (" -party_id:p%d" % ((i // 2 + 1) % (n // 2))) if idq == "party" else \
+                 (" -ticket:t%05d properties.mode:%s^2" % ((i + 3) % n, mode))
+        ts.append(capi.Ticket(ticket="t%05d" % i, presences=[capi.Presence("u%d" % i, "s%d" % i, "u%d" % i, "n")],
+                              session_id="" if party else "s%d" % i, party_id=party, query=q, min_count=2,
+                              max_count=3, string_properties={"mode": mode}, created_at=t0 + 1024 * i,
+                              node="node1"))  # Extract lists this node's tickets (matchmaker.go:684-720)
+    gpu, orc = pair(dict(max_intervals=3))
+    try:
+        gpu.Insert(ts)
+        orc.Insert(ts)
+        assert state(gpu) == state(orc)
+        for k in range(0, n, 97):
+            assert gpu.debug_hits(ts[k].ticket) == orc.debug_hits(ts[k].ticket)
+        for _ in range(2):
+            assert gpu.Process() == orc.Process()
+            assert state(gpu) == state(orc)
+    finally:
+        gpu.close()
+        orc.close()
+
+
 def test_datetime_hit_lists():
     ts = synth.TicketSet(8, 600)
     gpu, orc = pair(dict(max_intervals=2))
@@ -425,6 +460,25 @@ def test_c4_many_pools(par, dense, kernel, monkeypatch):
     monkeypatch.setenv("NKM_DENSE", dense)
     set_kernel(monkeypatch, kernel)
     run_passes(4, 1500, 1, dict(max_intervals=2))
+
+
+@pytest.mark.parametrize("par,dense,fast", [("0", "1", "1"), ("force", "1", "1"), ("force", "0", "1"),
+                                            ("force", "1", "0"), ("0", "1", "0")])
+@pytest.mark.parametrize("config,n", [(17, 3000), (17, 12_000), (18, 3000)])
+def test_count_multiple_trim_keeps_combo_full(config, n, par, dense, fast, monkeypatch):
+    """MaxCount % CountMultiple != 0 (Add accepts it): combos formed at
+    l == MaxCount are trimmed and often rejected; Go's stored combo keeps its
+    pre-trim length (a slice header is trimmed, matchmaker_process.go:262-271)
+    and never takes another hit.  Serial / pool-parallel, dense / generic and
+    fast / exact walks (config 17) and the range walk (18) against the oracle;
+    the known-answer scenarios CountMultipleTrimRejectedStaysFull-* pin the
+    oracle."""
+    monkeypatch.setenv("NKM_PARALLEL", par)
+    monkeypatch.setenv("NKM_DENSE", dense)
+    monkeypatch.setenv("NKM_FAST", fast)
+    rs = run_passes(config, n, 3, dict(max_intervals=3))
+    if config == 18:
+        assert rs[0].eval_kernel in (6, 7), rs[0].eval_kernel
 
 
 @pytest.mark.parametrize("config,n,passes,mi", [(3, 1500, 2, 2), (6, 1000, 3, 3), (4, 1500, 1, 2)])

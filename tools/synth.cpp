@@ -276,6 +276,38 @@ void* synth_make_impl(int config, uint64_t seed, int64_t first, int64_t n_all, i
             else { t.min_count = 4; t.max_count = 6; t.count_multiple = 2; }
             break;
         }
+        case 17:
+        case 18: {  // MaxCount % CountMultiple != 0 (Add / Insert accept it; the
+                    // pipeline does not): combos formed at l == MaxCount = 5 are
+                    // trimmed for CountMultiple 2 / 3 and often rejected by a
+                    // member's own CountMultiple (matchmaker_process.go:234-296).
+                    // 17: C3's 8 mode x region pools, one search per pool (the
+                    // dense walk); 18: config 15's range searches (the range walk)
+            const double u = r.uni();
+            party = u < 0.6 ? 1 : u < 0.85 ? 2 : 3;
+            t.count_multiple = (int)(r.next() % 3) + 1;
+            t.min_count = 3;
+            t.max_count = 5;
+            if (config == 17) {
+                const char* mode = kModes[r.next() & 1];
+                const char* region = shard_regions_i[r.next() & 3];
+                S->sp.push_back({"mode", mode});
+                S->sp.push_back({"region", region});
+                query = std::string("+properties.mode:") + mode + " +properties.region:" + region;
+            } else {
+                const char* region = shard_regions_i[r.next() & 3];
+                const int s = (int)std::lround(r.normal(1500.0, 300.0));
+                S->sp.push_back({"region", region});
+                S->np.push_back({"skill", (double)s});
+                char q[256];
+                std::snprintf(q, sizeof q,
+                              "+properties.region:%s +properties.skill:>=%d +properties.skill:<=%d "
+                              "properties.skill:>=%d^2 properties.skill:<=%d^2",
+                              region, s - 300, s + 300, s - 80, s + 80);
+                query = q;
+            }
+            break;
+        }
         case 14: {  // C5 variant, buckets of 24 (stride 32), a required skill range, 3-player groups
             const int s = (int)std::lround(r.normal(1500.0, 300.0));
             char b[32];
