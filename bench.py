@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=24, help="active rows in the CPU-baseline prefix sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-numa-bind", action="store_true",
-                    help="do not bind the process to one NUMA node (default: local rank r of L on node r * nodes / L)")
+                    help="do not bind the process to its GPU's NUMA node (one process per GPU)")
     ap.add_argument("--override", action="store_true",
                     help="register a MatchmakerOverride (processCustom path): the timed step is the candidate pass, "
                          "a native first-disjoint override and mm_process_commit (per rank under the cluster front)")
@@ -185,6 +185,8 @@ def cpu_baseline(args, searches, matched):
     import subprocess
     cmd = [sys.executable, os.path.join(ROOT, "tools", "cpu_baseline.py"), "--config", str(args.config),
            "--tickets", str(args.tickets), "--searches", str(searches), "--matched", str(matched)]
+    if args.override:  # C5 + override: a bounded prefix of the chunk passes, extrapolated
+        cmd += ["--override", "--chunks", "100"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
         return {"value": None, "unit": "tickets/s", "cores": 1, "kind": "port",
@@ -192,7 +194,7 @@ def cpu_baseline(args, searches, matched):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     out = {"value": d["value"], "unit": "tickets/s", "cores": d["cores"], "kind": "port", "sample": d["sample"],
            "all_cores": d.get("all_cores"), "algorithm": d["algorithm"], "host": d["host"]}
-    name = f"c{args.config}"
+    name = f"c{args.config}" + ("o" if args.override else "")
     full = os.path.join(ROOT, "profiles", f"r04_cpu_full_{name}.json")
     if os.path.exists(full) and args.tickets == json.load(open(full)).get("tickets"):
         out["measured_full_pass"] = json.load(open(full))
@@ -200,6 +202,14 @@ def cpu_baseline(args, searches, matched):
     if os.path.exists(calib) and args.tickets == json.load(open(calib)).get("tickets"):
         out["calibration"] = json.load(open(calib))["model_over_measured"]
     return out
+
+
+def candidate_stats(out):
+    """The pass statistics of an mm_process result (before an override's
+    commit replaces it)."""
+    return {"eval_ms": out.eval_ms, "eval_bytes": out.eval_bytes, "eval_launches": out.eval_launches,
+            "n_batches": out.n_batches, "eval_kernel": out.eval_kernel, "pair_evals": out.pair_evals,
+            "pairs_decided": out.pairs_decided}
 
 
 def make_set(args, world, rank, step):
@@ -214,12 +224,14 @@ def make_set(args, world, rank, step):
     return synth.TicketSet(args.config, n, first=lo, pool_groups=groups)
 
 
-def numa_bind(local_rank, local_world):
-    """Binds this process to one NUMA node (numactl --cpunodebind): local
-    rank r of L to node r * nodes // L (an 8-GPU node's GPUs 0-3 / 4-7 hang off
-    its two sockets), a single rank to the node it runs on.  The library's
-    host workers stay on the calling thread's node (mm_store.cpp node_cpus);
-    this keeps the caller there too.  Returns the node or None."""
+def numa_bind(device):
+    """Binds this process to the NUMA node its GPU hangs off (the device's PCI
+    numa_node, read by the library: mm_device_numa_node), like numactl
+    --cpunodebind; when that is unknown, to the node the process runs on.  The
+    library's host workers sit on the device's node too (mm_store.cpp
+    node_cpus); this keeps the caller with them.  Called after the HIP runtime
+    is up (dist_setup), before the library's first handle.  Returns the node or
+    None (a one-node host)."""
     try:
         allowed = os.sched_getaffinity(0)
         nodes = []
@@ -236,27 +248,30 @@ def numa_bind(local_rank, local_world):
         nodes = [(nd, c) for nd, c in nodes if c]
         if len(nodes) < 2:
             return None
-        if local_world > 1:
-            nd, cpus = nodes[local_rank * len(nodes) // local_world]
-        else:
+        import nakama_amd
+        want = int(nakama_amd.load_library().mm_device_numa_node(device))
+        pick = next(((n, c) for n, c in nodes if n == want), None)
+        if pick is None:
             import ctypes
             here = ctypes.CDLL(None).sched_getcpu()
-            nd, cpus = next(((n, c) for n, c in nodes if here in c), nodes[0])
-        os.sched_setaffinity(0, cpus)
-        return nd
+            pick = next(((n, c) for n, c in nodes if here in c), nodes[0])
+        os.sched_setaffinity(0, pick[1])
+        return pick[0]
     except OSError:
         return None
 
 
 def main():
     args = parse()
-    if not args.no_numa_bind:
-        numa_bind(int(os.environ.get("LOCAL_RANK", "0")), int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
     world, rank, local, pg, backend = dist_setup(args)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # one handle over several devices: its sub-handles place themselves on
+    # their devices' nodes (mm_multi.cpp), the process stays unbound
     if args.multi_handle or (world > 1 and args.front == "multi"):
         return main_multi(args, world, rank, local, pg)
+    if not args.no_numa_bind:
+        numa_bind(local)
     import nakama_amd
     import torch
 
@@ -287,7 +302,7 @@ def main():
         if cm is None:
             out = mm.process_call()  # the C-ABI call: one whole Process() pass
             n_cands = out.n_groups if out.is_candidates else 0
-            cand_pe = out.pair_evals
+            cand = candidate_stats(out)  # the candidate pass ran the searches (a few scalar reads)
             if args.override and out.is_candidates:  # processCustom: override + commit, in the timed step
                 out = synth.override_commit(mm, out)
         else:
@@ -296,10 +311,12 @@ def main():
         dt = time.perf_counter() - t0
         if cm is None:
             n_groups, matched, pres, r = mm.process_summary(out)  # untimed: counts the groups, frees them
-            st = {"eval_ms": r.eval_ms, "eval_bytes": r.eval_bytes, "eval_launches": r.eval_launches,
-                  "n_batches": r.n_batches, "eval_kernel": r.eval_kernel,
-                  "pair_evals": cand_pe if args.override else r.pair_evals, "pairs_decided": r.pairs_decided,
-                  "candidates": n_cands}
+            # the override's commit runs no search: the pass statistics are the candidate pass's
+            st = dict(cand) if args.override else {
+                "eval_ms": r.eval_ms, "eval_bytes": r.eval_bytes, "eval_launches": r.eval_launches,
+                "n_batches": r.n_batches, "eval_kernel": r.eval_kernel, "pair_evals": r.pair_evals,
+                "pairs_decided": r.pairs_decided}
+            st["candidates"] = n_cands
         else:
             n_groups, matched, pres = cp.n_groups, cp.matched_tickets, cp.matched_presences
             st = cp.local_stats
@@ -397,7 +414,7 @@ def main():
                      "kernel": "+".join(sorted(kernels)), "launches": launches, "avg_launch_ms": avg_launch_ms,
                      "bytes_per_launch": eval_bytes / max(1, launches), "rank": 0},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in (2, 3, 4, 5) and not args.override:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in (2, 3, 4, 5):
         out["cpu_baseline"] = cpu_baseline(args, int(statistics.median(searched)), int(statistics.median(matched_all)))
     else:
         out["cpu_baseline"] = None
@@ -450,7 +467,7 @@ def main_multi(args, world, rank, local, pg):
         if rank == 0:
             out = mm.process_call()
             n_cands = out.n_groups if out.is_candidates else 0
-            cand_pe = out.pair_evals
+            cand = candidate_stats(out)
             if args.override and out.is_candidates:
                 out = synth.override_commit(mm, out)
             for d in sorted(set(devs)):
@@ -465,14 +482,15 @@ def main_multi(args, world, rank, local, pg):
                 ins_times.append(ins_dt)
                 matched_all.append(matched)
                 presences_all.append(pres)
-                eval_ms += r.eval_ms
-                eval_bytes += r.eval_bytes
-                launches += r.eval_launches
-                pair_evals += cand_pe if args.override else r.pair_evals
-                pairs_decided += r.pairs_decided
+                st = cand if args.override else candidate_stats(r)
+                eval_ms += st["eval_ms"]
+                eval_bytes += st["eval_bytes"]
+                launches += st["eval_launches"]
+                pair_evals += st["pair_evals"]
+                pairs_decided += st["pairs_decided"]
                 cands += n_cands
-                batches.append(r.n_batches)
-                kernels.add(KERNELS.get(r.eval_kernel, str(r.eval_kernel)))
+                batches.append(st["n_batches"])
+                kernels.add(KERNELS.get(st["eval_kernel"], str(st["eval_kernel"])))
             mm.Remove([t.ticket for t in mm.Extract()]) if mm.ticket_count() else None
     if rank == 0:
         total_t = sum(times)

@@ -189,6 +189,12 @@ void* mm_create_multi(const mm_config* cfg, const mm_multi_config* mc);
  * with sub >= 0, that sub-handle's ticket count. */
 int32_t mm_multi_info(void* h, int32_t sub);
 
+/* The NUMA node a device hangs off (its PCI device's numa_node), -1 when
+ * unknown.  A handle places its host workers on its device's node (and a
+ * multi handle each sub-handle's); a one-process-per-GPU launcher binds each
+ * rank there (bench.py). */
+int32_t mm_device_numa_node(int32_t device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -240,6 +240,7 @@ def load_library(path: str) -> C.CDLL:
     if hasattr(lib, "mm_create_multi"):  # the product: one handle over several devices (nakama_cluster.h)
         sig["mm_create_multi"] = (vp, [C.POINTER(mm_config), C.POINTER(mm_multi_config)])
         sig["mm_multi_info"] = (C.c_int32, [vp, C.c_int32])
+        sig["mm_device_numa_node"] = (C.c_int32, [C.c_int32])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -502,6 +502,7 @@ struct PassStats {
     // overlapped host work, the wait for the device, result accounting and
     // wiring, the hit-list copies; replay_parallel's gathers and the walk job
     double rb_prep_ms = 0, rb_overlap_ms = 0, rb_wait_ms = 0, rb_post_ms = 0, rb_lists_ms = 0;
+    int mhash_respec = 0;  // counts-only hashed scans re-run in full (a list not proven)
     int mscan_lists = 0, lists_proven = 0;  // mscan lists placed / proven equal to their rows (not downloaded)
     double par_gather_ms = 0, par_job_ms = 0, par_clear_ms = 0;
     double asm_count_ms = 0, asm_scatter_ms = 0;  // assemble_parallel's two sweeps over the rows
@@ -735,6 +736,18 @@ private:
     // (BGroup::rows_list).  NKM_LISTPROOF=0: every list is downloaded;
     // 2: downloaded and compared with the proof's claim (throws on a miss).
     int list_proof_mode_ = 1;
+    // Counts-only speculation (mode 1, contiguous hashed scans): the scan
+    // writes only the per-(signature, chunk) counts — no ranking into scratch,
+    // no placement — since a proven list is never read.  A search whose count
+    // then differs from its rows needs its list: the full scan runs again for
+    // that batch and the speculation pauses for kSpecPause passes.
+    // NKM_MHCOUNT=0: always the full scan.
+    bool mhash_count_mode_ = true;
+    uint32_t mhash_spec_pause_ = 0;
+    static constexpr uint32_t kSpecPause = 16;
+    // the contiguous hashed scan as the resident pipelined loop
+    // (mscan_hash_loop_kernel); NKM_MHLOOP=0: one chunk per workgroup
+    bool mhash_loop_mode_ = true;
     bool row_lists_pending_ = false;  // the last batch flagged some BGroup::rows_list
     // writes every rows_list search's host list from its batch rows (a reader
     // other than the dense identity walk) and clears the flags
@@ -830,7 +843,8 @@ private:
     hipEvent_t apply_ev_ = nullptr;  // after the last asynchronous alive-flag update (h_slots_tmp_ reuse)
     bool apply_pending_ = false;
     std::unique_ptr<WorkPool> workers_;  // created on the first large pass
-    unsigned host_share_ = 1;            // Cores sharing the host cores (multi handle)
+    unsigned host_share_ = 1;            // Cores sharing the host cores (multi handle: those on this NUMA node)
+    int numa_node_ = -1;                 // the device's NUMA node (device_numa_node), -1 unknown
     WorkPool& workers();
     size_t par_min(size_t auto_min) const { return par_mode_ == 2 ? 0 : auto_min; }
     bool big_list(const std::vector<uint32_t>& v) const { return par_mode_ != 0 && v.size() >= par_min(65536); }

@@ -137,7 +137,11 @@ NKM_HD inline uint64_t mhash_cidx(const DMScan& ms, uint32_t q, uint32_t c) {
 constexpr uint32_t kMHashSigs = 256;  // signatures of one hashed scan
 constexpr uint32_t kMHashCap = 1024;  // table entries (a power of two >= 2 x signatures)
 constexpr uint32_t kMHashEmpty = 0xFFFFu;
-constexpr int kMHashEval = 1, kMHashPlace = 2;  // launch_mscan_hash phases
+// launch_mscan_hash phases: kMHashEval the per-chunk scan, kMHashPlace the
+// bases + placement; kMHashLoop the scan as a resident pipelined loop
+// (contiguous chunks); kMHashCount the loop writing counts only (no lists:
+// placement reduced to the bases)
+constexpr int kMHashEval = 1, kMHashPlace = 2, kMHashLoop = 4, kMHashCount = 8;
 struct DMHashEntry {                  // 32 B
     uint32_t key[4];                  // required dictionary id per scanned field (0 past n_fields)
     uint32_t q;                       // signature, kMHashEmpty: free

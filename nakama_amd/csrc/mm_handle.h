@@ -59,4 +59,10 @@ struct CompiledQuery;
 uint64_t route_key(const mm_ticket& t, const std::vector<std::string>& fields);
 uint64_t route_key(const mm_ticket& t, const std::vector<std::string>& fields, const CompiledQuery& cq);
 
+// The NUMA node of a GPU (sysfs numa_node of its PCI device), -1 unknown;
+// the usable CPUs of node `prefer` (else of the calling thread's node; none on
+// a one-node host).  mm_store.cpp.
+int device_numa_node(int device);
+std::vector<int> node_cpus(int prefer);
+
 }  // namespace nkm

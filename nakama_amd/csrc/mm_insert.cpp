@@ -394,8 +394,12 @@ bool Core::insert_bulk(const mm_ticket* ts, int32_t n_in, double* ph) {
     // field (sig_commit switched it on): those columns are filled per ticket
     // (add_locked), so the batch takes the per-ticket path.  Nothing of the
     // store is written yet — the signatures and interned terms made above are
-    // what that path looks up.
-    if (field_used_.size() > F_PARTY && (field_used_[F_TICKET] || field_used_[F_PARTY])) return false;
+    // what that path looks up; the fields they switched on get their columns
+    // over the existing slots first (sig_commit deferred that to step 3).
+    if (field_used_.size() > F_PARTY && (field_used_[F_TICKET] || field_used_[F_PARTY])) {
+        materialize_fields();
+        return false;
+    }
     std::vector<uint32_t> tpos(m, 0);
     for (size_t j = 0; j < nt; j++) tpos[tfirst[j]] = (uint32_t)j;
     ph[1] = ms_since(t0);

@@ -999,6 +999,217 @@ __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms
     for (uint32_t v = (uint32_t)tid; 4 * v < total; v += kBlock) cs4[v] = st4[v];
 }
 
+// ---- the contiguous hashed scan as a resident, pipelined loop ----------------
+// mscan_hash_kernel<CONTIG> loads a chunk, then works on it: a workgroup's
+// loads are in flight only at its start, so with one chunk per workgroup the
+// HBM pipe drains at every round boundary of the grid (C4's 4,096 chunks on
+// 256 CUs: two rounds) and every workgroup copies the cuckoo table into LDS
+// again.  Here the grid is what stays resident (the CUs x the occupancy) and
+// each workgroup walks the chunks c, c + grid, ...: the table is loaded once,
+// and the next chunk's columns are requested before the current chunk is
+// hashed, ranked and stored, so they arrive while it works.  COUNT: only the
+// per-(signature, chunk) counts are written (no ranking into scratch): the
+// proven-list pass (Core::list_proof_mode_), whose lists are never placed.
+// Same LDS layout (MHashLds<kMJ, true>), same outputs as mscan_hash_kernel.
+template <int NF, int kMJ>
+struct MHashCols {
+    uint8_t al[kMJ];
+    int32_t mn[kMJ], mx[kMJ];
+    uint8_t kk[NF][kMJ];
+    int64_t vv[NF][kMJ];
+};
+
+// chunk c's columns of this lane's run (candidates cs0 + tid * kMJ + j); a run
+// outside the scan's [vlo, vhi) is loaded per candidate (in range only)
+template <int NF, int kMJ>
+__device__ __forceinline__ void mhash_load(MHashCols<NF, kMJ>& R, const DStore& st,
+                                           const __attribute__((address_space(1))) uint8_t* const (&fkp)[NF],
+                                           const __attribute__((address_space(1))) int64_t* const (&fvp)[NF],
+                                           uint32_t gs, uint32_t vlo, uint32_t vhi) {
+    if (gs >= vlo && gs + kMJ <= vhi) {
+        load_run(R.al, st.alive + gs);
+        load_run(R.mn, st.minc + gs);
+        load_run(R.mx, st.maxc + gs);
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            load_run(R.kk[f], (const uint8_t*)(fkp[f] + gs));
+            load_run(R.vv[f], (const int64_t*)(fvp[f] + gs));
+        }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < kMJ; j++) {
+        const uint32_t x = gs + j;
+        const bool in = x >= vlo && x < vhi;
+        R.al[j] = in ? st.alive[x] : (uint8_t)0;
+        R.mn[j] = in ? st.minc[x] : 0;
+        R.mx[j] = in ? st.maxc[x] : 0;
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            R.kk[f][j] = in ? fkp[f][x] : (uint8_t)KIND_ABSENT;
+            R.vv[f][j] = in ? fvp[f][x] : 0;
+        }
+    }
+}
+
+template <int NF, int kMJ, bool COUNT>
+__global__ __launch_bounds__(kBlock) void mscan_hash_loop_kernel(DStore st, DMScan ms, const DMHashEntry* __restrict__ htab,
+                                                                 uint32_t* __restrict__ scratch,
+                                                                 uint32_t* __restrict__ counts, uint32_t c_lo,
+                                                                 uint32_t c_hi) {
+    static_assert(NF >= 1 && NF <= 4, "1-4 required fields");
+    static_assert(kMJ == 4 || kMJ == 8, "runs of 4 or 8 candidates");
+    constexpr int kMChunk = kMJ * kBlock;
+    constexpr uint32_t kNone = kMHashEmpty;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint32_t wsum[kWaves], wlive[kWaves];
+    const uint32_t nq = ms.n_sigs, hmask = ms.hmask;
+    const MHashLds<kMJ, true> L{hmask + 1, nq};
+    DMHashEntry* tab = reinterpret_cast<DMHashEntry*>(lds + L.table_off());
+    uint16_t* cnt = reinterpret_cast<uint16_t*>(lds + L.cnt_off());
+    uint32_t* loff = reinterpret_cast<uint32_t*>(lds + L.loff_off());
+    uint32_t* stage = reinterpret_cast<uint32_t*>(lds + L.stage_off());
+    uint16_t* qs = reinterpret_cast<uint16_t*>(lds + L.qs_off());
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    typedef const __attribute__((address_space(1))) uint8_t gu8;
+    typedef const __attribute__((address_space(1))) int64_t gi64;
+    gu8* fkp[NF];
+    gi64* fvp[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+        fkp[f] = (gu8*)st.fkind[ms.field[f]];
+        fvp[f] = (gi64*)st.fval[ms.field[f]];
+    }
+    const uint32_t base0 = ms.src_off & ~(uint32_t)(kMChunk - 1);
+    const uint32_t vlo = ms.src_off, vhi = ms.src_off + ms.src_len;
+    const uint32_t stride = gridDim.x;
+    uint32_t c = c_lo + blockIdx.x;
+    MHashCols<NF, kMJ> cur, nxt;
+    if (c < c_hi) mhash_load(cur, st, fkp, fvp, base0 + c * (uint32_t)kMChunk + (uint32_t)tid * kMJ, vlo, vhi);
+    {  // the table, once per workgroup, while the first chunk's loads are in flight
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* __restrict__ g4 = reinterpret_cast<const u32x4*>(htab);
+        u32x4* t4 = reinterpret_cast<u32x4*>(tab);
+        for (uint32_t t = (uint32_t)tid; t < 2 * (hmask + 1); t += kBlock) t4[t] = g4[t];
+    }
+    const uint32_t nbits = nq > 1 ? 32u - (uint32_t)__clz(nq - 1) : 0u;
+    for (; c < c_hi; c += stride) {
+        const uint32_t cn = c + stride;
+        if (cn < c_hi) mhash_load(nxt, st, fkp, fvp, base0 + cn * (uint32_t)kMChunk + (uint32_t)tid * kMJ, vlo, vhi);
+        const uint32_t cs0 = base0 + c * (uint32_t)kMChunk;
+        __syncthreads();  // the previous chunk is out of stage / cnt / qs (and the table is in)
+        {
+            uint32_t* c4 = reinterpret_cast<uint32_t*>(cnt);
+            for (uint32_t t = (uint32_t)tid; t < (nq * kMJ * kWaves + 1) / 2; t += kBlock) c4[t] = 0u;
+        }
+        bool a[kMJ];
+        uint32_t live = 0;
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) {
+            a[j] = cur.al[j] != 0;
+            live += a[j];
+#pragma unroll
+            for (int f = 0; f < NF; f++) a[j] = a[j] && cur.kk[f][j] == KIND_KEYWORD;  // every field is required
+        }
+        for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o);
+        if (lane == 0) wlive[wave] = live;
+        uint32_t q[kMJ];
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) {
+            uint32_t h1 = ms.hseed[0], h2 = ms.hseed[1];
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                h1 = msig_mix(h1, (uint32_t)cur.vv[f][j]);
+                h2 = msig_mix(h2, (uint32_t)cur.vv[f][j]);
+            }
+            const DMHashEntry& e1 = tab[msig_fin(h1) & hmask];
+            const DMHashEntry& e2 = tab[msig_fin(h2) & hmask];
+            bool m1 = e1.q != kNone, m2 = e2.q != kNone;
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                m1 = m1 && e1.key[f] == (uint32_t)cur.vv[f][j];
+                m2 = m2 && e2.key[f] == (uint32_t)cur.vv[f][j];
+            }
+            const uint32_t qq = m1 ? e1.q : e2.q;
+            const int32_t tmin = m1 ? e1.tmin : e2.tmin, tmax = m1 ? e1.tmax : e2.tmax;
+            q[j] = a[j] && (m1 || m2) && cur.mn[j] >= tmin && cur.mx[j] <= tmax ? qq : kNone;
+        }
+        // runs (wave, lane, j) -> the strided layout j * 256 + tid (candidate order), through LDS
+        {
+            uint16_t pk[kMJ];
+#pragma unroll
+            for (int j = 0; j < kMJ; j++) pk[j] = (uint16_t)q[j];
+            __builtin_memcpy(&qs[tid * kMJ], pk, sizeof pk);
+        }
+        __syncthreads();  // qs written, cnt zeroed, wlive in
+        uint32_t s[kMJ];
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) {
+            const uint32_t i = (uint32_t)(j * kBlock + tid);
+            q[j] = qs[i];
+            s[j] = cs0 + i;
+        }
+        // rank within (signature, j, wave): one ballot per signature-index bit
+        uint32_t rk[kMJ];
+#pragma unroll
+        for (int j = 0; j < kMJ; j++) {
+            const bool m = q[j] != kNone;
+            uint64_t peer = __ballot((int)m);
+            for (uint32_t b = 0; b < nbits; b++) {
+                const bool bit = (q[j] >> b) & 1u;
+                const uint64_t bb = __ballot((int)(m && bit));
+                peer &= bit ? bb : ~bb;
+            }
+            rk[j] = lanes_below(peer);
+            if (m && rk[j] == 0) cnt[(q[j] * kMJ + j) * kWaves + wave] = (uint16_t)__popcll(peer);
+        }
+        __syncthreads();
+        uint32_t tot = 0;
+        if ((uint32_t)tid < nq) {
+            uint16_t* cq = cnt + (uint32_t)tid * kMJ * kWaves;
+            uint32_t run = 0;
+#pragma unroll
+            for (int k = 0; k < kMJ * kWaves; k++) {
+                const uint32_t v = cq[k];
+                cq[k] = (uint16_t)run;
+                run += v;
+            }
+            tot = run;
+        }
+        if ((uint32_t)tid < nq) counts[mhash_cidx(ms, (uint32_t)tid, c)] = tot;
+        if (tid == 0) {
+            uint32_t lv = 0;
+            for (int w = 0; w < kWaves; w++) lv += wlive[w];
+            counts[mhash_cidx(ms, nq, c)] = lv;
+        }
+        if constexpr (!COUNT) {
+            uint32_t incl = tot;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(incl, o);
+                if (lane >= o) incl += u;
+            }
+            if (lane == 63) wsum[wave] = incl;
+            __syncthreads();
+            uint32_t ex = incl - tot, total = 0;
+            for (int w = 0; w < kWaves; w++) {
+                if (w < wave) ex += wsum[w];
+                total += wsum[w];
+            }
+            if ((uint32_t)tid < nq) loff[tid] = ex;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kMJ; j++)
+                if (q[j] != kNone) stage[loff[q[j]] + cnt[(q[j] * kMJ + j) * kWaves + wave] + rk[j]] = s[j];
+            __syncthreads();
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4* __restrict__ cs4 = reinterpret_cast<u32x4*>(scratch + (uint64_t)c * kMChunk);
+            const u32x4* st4 = reinterpret_cast<const u32x4*>(stage);
+            for (uint32_t v = (uint32_t)tid; 4 * v < total; v += kBlock) cs4[v] = st4[v];
+        }
+        cur = nxt;
+    }
+}
+
 // Per column of the counts (a signature, or n_sigs: live candidates), stored
 // column-major [column][chunk]: the exclusive prefix over the chunks into
 // bases[column][chunk] (entry n_chunks: the total) and the signature's result
@@ -1711,6 +1922,29 @@ hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs,
 // entries (DMHashEntry, 32-B aligned); d_work (16-B aligned): chunks x chunk
 // scratch words, then (n_sigs + 1) x chunks counts, then (n_sigs + 1) x
 // (chunks + 1) bases (column-major).
+// The resident grid of mscan_hash_loop_kernel: the device's CUs x the
+// workgroups one CU holds at this LDS size (cached per kernel and size), at
+// most the chunks.
+static uint32_t mhash_loop_grid(const void* fn, size_t lds, uint32_t chunks) {
+    struct Key { const void* fn; size_t lds; int dev; uint32_t n; };
+    static thread_local Key memo[8] = {};
+    static thread_local int next = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    uint32_t n = 0;
+    for (const Key& k : memo)
+        if (k.fn == fn && k.lds == lds && k.dev == dev && k.n) n = k.n;
+    if (!n) {
+        int cus = 0, per = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kBlock, lds);
+        n = (uint32_t)(cus > 0 ? cus : 256) * (uint32_t)(per > 0 ? per : 1);
+        memo[next] = Key{fn, lds, dev, n};
+        next = (next + 1) & 7;
+    }
+    return n < chunks ? n : chunks;
+}
+
 size_t mscan_hash_table_off(uint32_t n_sigs) {
     return ((size_t)n_sigs * (sizeof(DMSig) + sizeof(uint64_t)) + 31) & ~(size_t)31;
 }
@@ -1755,14 +1989,42 @@ hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_b
         else if (mj == 4) NKM_MHASH_K(NF, 4, false);         \
         else NKM_MHASH_K(NF, 2, false);                      \
     } while (0)
+    // the resident loop (mscan_hash_loop_kernel): contiguous chunks only
+    const bool loop = ms.contig && (phases & (kMHashLoop | kMHashCount));
+    const bool count_only = loop && (phases & kMHashCount);
+#define NKM_MHLOOP_K(NF, J, CNT)                                                                                    \
+    do {                                                                                                            \
+        const size_t lb = MHashLds<J, true>{ms.hmask + 1, ms.n_sigs}.bytes();                                        \
+        const uint32_t grid_n = mhash_loop_grid((const void*)mscan_hash_loop_kernel<NF, J, CNT>, lb, c_hi - c_lo);    \
+        hipExtLaunchKernelGGL(mscan_hash_loop_kernel<NF, J, CNT>, dim3(grid_n), block, lb, stream, ev0, ev1, 0, st, ms, \
+                              htab, scratch, counts, c_lo, c_hi);                                                   \
+    } while (0)
+#define NKM_MHLOOP(NF)                                          \
+    do {                                                        \
+        if (mj == 8 && count_only) NKM_MHLOOP_K(NF, 8, true);   \
+        else if (mj == 8) NKM_MHLOOP_K(NF, 8, false);           \
+        else if (count_only) NKM_MHLOOP_K(NF, 4, true);         \
+        else NKM_MHLOOP_K(NF, 4, false);                        \
+    } while (0)
     if ((phases & kMHashEval) && c_hi > c_lo) {
-        switch (ms.n_fields) {
-            case 1: NKM_MHASH(1); break;
-            case 2: NKM_MHASH(2); break;
-            case 3: NKM_MHASH(3); break;
-            default: NKM_MHASH(4); break;
+        if (loop) {
+            switch (ms.n_fields) {
+                case 1: NKM_MHLOOP(1); break;
+                case 2: NKM_MHLOOP(2); break;
+                case 3: NKM_MHLOOP(3); break;
+                default: NKM_MHLOOP(4); break;
+            }
+        } else {
+            switch (ms.n_fields) {
+                case 1: NKM_MHASH(1); break;
+                case 2: NKM_MHASH(2); break;
+                case 3: NKM_MHASH(3); break;
+                default: NKM_MHASH(4); break;
+            }
         }
     }
+#undef NKM_MHLOOP
+#undef NKM_MHLOOP_K
 #undef NKM_MHASH
 #undef NKM_MHASH_K
 #ifdef NKM_MH_DEBUG
@@ -1770,7 +2032,8 @@ hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_b
 #endif
     if (!(phases & kMHashPlace)) return hipGetLastError();
     hipLaunchKernelGGL(mscan_base_kernel, dim3(ms.n_sigs + 1), block, 0, stream, ms, counts, bases, d_cres);
-    hipLaunchKernelGGL(mscan_place_kernel, grid, block, 0, stream, ms, bases, scratch, dst, d_out32);
+    if (!count_only)  // counts only: the lists are never placed (proven, Core::list_proof_mode_)
+        hipLaunchKernelGGL(mscan_place_kernel, grid, block, 0, stream, ms, bases, scratch, dst, d_out32);
     return hipGetLastError();
 }
 uint64_t mscan_hash_work_words(const DMScan& ms) {

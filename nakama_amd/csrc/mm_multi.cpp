@@ -31,6 +31,9 @@
 // replays the same lists into the same groups; sub-handle 0 answers.
 #include <hip/hip_runtime.h>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -221,15 +224,30 @@ private:
     void each(F&& f) {
         const int n = (int)subs_.size();
         if (n == 1) { f(0); return; }
+        // every sub-handle on a thread of its own, confined to its device's
+        // node (the caller's thread keeps its placement)
         std::vector<std::thread> th;
-        for (int i = 1; i < n; i++)
+        for (int i = 0; i < n; i++)
             th.emplace_back([&, i] {
-                if (own_) (void)hipSetDevice(devs_[(size_t)i]);
+                if (own_) {
+                    (void)hipSetDevice(devs_[(size_t)i]);
+                    place_thread(i);
+                }
                 f(i);
             });
-        if (own_) (void)hipSetDevice(devs_[0]);
-        f(0);
         for (auto& t : th) t.join();
+    }
+    // Confines the calling (per-sub-handle) thread to the CPUs of sub-handle
+    // i's device node, so what it first-touches (Insert's columns and records)
+    // lands in that node's memory; nothing on a one-node host.
+    void place_thread(int i) {
+        const std::vector<int> cpus = node_cpus(device_numa_node(devs_[(size_t)i]));
+        if (cpus.empty()) return;
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        for (int c : cpus)
+            if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &cs);
+        (void)pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
     }
     template <class F>
     void each_serial(F&& f) {
@@ -333,10 +351,17 @@ MultiCore::MultiCore(const mm_config& cfg, const mm_multi_config& mc) {
     const int n = mc.n_devices;
     devs_.assign(mc.devices, mc.devices + n);
     load_.assign((size_t)n, 0);
+    // each sub-handle's host share: the sub-handles on its device's NUMA node
+    // (every one when the nodes are unknown) split that node's cores
+    std::vector<int> nodes((size_t)n, -1);
+    if (own_)
+        for (int i = 0; i < n; i++) nodes[(size_t)i] = device_numa_node(devs_[(size_t)i]);
     for (int i = 0; i < n; i++) {
         mm_config c = cfg;
         c.device = devs_[(size_t)i];
-        g_create_share = (unsigned)n;
+        unsigned share = 0;
+        for (int k = 0; k < n; k++) share += nodes[(size_t)i] < 0 || nodes[(size_t)k] == nodes[(size_t)i];
+        g_create_share = nodes[(size_t)i] < 0 ? (unsigned)n : share;
         void* s = api_.create(&c);
         g_create_share = 1;
         if (!s) {
@@ -1134,6 +1159,14 @@ void* mm_create_multi(const mm_config* cfg, const mm_multi_config* mc) {
         nkm::set_create_error("mm_create_multi: internal error");
     }
     return nullptr;
+}
+
+int32_t mm_device_numa_node(int32_t device) {
+    try {
+        return nkm::device_numa_node(device);
+    } catch (...) {
+        return -1;
+    }
 }
 
 int32_t mm_multi_info(void* h, int32_t sub) {

@@ -593,6 +593,11 @@ struct Replay : ReplayCore {
         // and the claim checked against it)
         const bool proof = hashed && rows_self && c.list_proof_mode_ != 0 && c.monotone_ && !c.row_shard() && !rev;
         const bool skip_lists = proof && c.list_proof_mode_ == 1;
+        // counts only (Core::mhash_count_mode_): every list is expected proven
+        const bool count_only = skip_lists && ms.contig && c.mhash_count_mode_ && c.mhash_spec_pause_ == 0;
+        if (c.mhash_spec_pause_) c.mhash_spec_pause_--;
+        const int mh_phases = kMHashEval | kMHashPlace | (count_only ? kMHashCount : 0) |
+                              (c.mhash_loop_mode_ ? kMHashLoop : 0);
         const bool m_precopy = use_m && !c.row_shard() && mw - mw0 <= 2 * (uint64_t)ms.src_len && !skip_lists;
         const uint32_t ncells = !use_m ? 0 : hashed ? ms.n_sigs : ms.n_sigs * ms.n_chunks;
         if (hashed) scratch += (mscan_hash_work_words(ms) + 3) / 4;
@@ -716,7 +721,7 @@ struct Replay : ReplayCore {
         else if (hashed)
             NKM_HIP(launch_mscan_hash(st, ms, c.d_msig_.p, reinterpret_cast<uint32_t*>(c.d_scan_.p + mscratch),
                                       c.d_res_.p + nwhole + nchunks, reinterpret_cast<uint32_t*>(c.d_out_.p), stream,
-                                      c.ev_[4], c.ev_[5]));
+                                      c.ev_[4], c.ev_[5], mh_phases));
         else if (use_m)
             NKM_HIP(launch_mscan(st, ms, c.d_msig_.p, c.d_mcl_.p, reinterpret_cast<uint32_t*>(c.d_scan_.p + mscratch),
                                  c.d_res_.p + nwhole + nchunks,
@@ -871,8 +876,9 @@ struct Replay : ReplayCore {
                                      ? (double)(ms.cb[c.shard_rank_ + 1] - ms.cb[c.shard_rank_]) / (double)ms.n_chunks
                                      : 1.0;
             int64_t kb = 0, pe = 0;
+            const int64_t per_hit = count_only ? 0 : 4;  // counts only: no list written
             for (uint32_t t = 0; t < ncells; t++) {
-                kb += (int64_t)mr[t].scanned * per_scan + (int64_t)mr[t].live * per_live + (int64_t)mr[t].count * 4;
+                kb += (int64_t)mr[t].scanned * per_scan + (int64_t)mr[t].live * per_live + (int64_t)mr[t].count * per_hit;
                 pe += (int64_t)mr[t].scanned * (hashed ? 1 : ms.n_sigs);
             }
             stats.k_bytes[2] += (int64_t)((double)kb * share) +
@@ -916,6 +922,23 @@ struct Replay : ReplayCore {
         const size_t n_scan_cg = cg_list.size() - (use_m ? m_list.size() : 0);
         bool m_copied = false;
         c.row_lists_pending_ = false;
+        if (count_only) {
+            // a list the counts do not prove was never written: the full scan
+            // for this batch, and the speculation pauses
+            bool all_proven = true;
+            for (size_t k = n_scan_cg; k < cg_list.size() && all_proven; k++) {
+                uint64_t n = 0;
+                for (uint32_t t = cg_first[k]; t < cg_end[k]; t++) n += c.h_res_.p[nwhole + t].count;
+                all_proven = n == bg[cg_list[k]].nrows;
+            }
+            if (!all_proven) {
+                NKM_HIP(launch_mscan_hash(st, ms, c.d_msig_.p, reinterpret_cast<uint32_t*>(c.d_scan_.p + mscratch),
+                                          c.d_res_.p + nwhole + nchunks, reinterpret_cast<uint32_t*>(c.d_out_.p), stream,
+                                          nullptr, nullptr, mh_phases & ~kMHashCount));
+                stats.mhash_respec++;
+                c.mhash_spec_pause_ = Core::kSpecPause;
+            }
+        }
         for (size_t k = 0; k < cg_list.size(); k++) {
             BGroup& g = bg[cg_list[k]];
             const bool slots = k >= n_scan_cg;
@@ -1637,6 +1660,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                 g.d.k = g.d.var_score ? std::min<uint32_t>(kvar, std::max<uint32_t>(g.d.src_len, 1))
                                        : std::min<uint32_t>(std::max<uint32_t>(g.d.src_len, 1), 128);
                 g.row_slot = r;
+                g.nrows = 1;  // one row per search (processCustom)
             }
         };
         const bool par = par_mode_ && bg.size() >= par_min(4096);
@@ -2068,7 +2092,7 @@ int Core::process(mm_matched* out) {
                          "ms, apply %.2f ms, %d batches (%d parallel), %d refetches, %d launches, %d tier lists) | finish %.2f ms | "
                          "fill %.2f ms | groups %zu | slots %zu live %u active %zu sigs %zu dict %zu | par bucket %.2f work %.2f "
                          "merge %.2f ms (task max %.2f ms, rows %llu, hits %llu) | batch: prep %.2f overlap %.2f wait %.2f "
-                         "post %.2f lists %.2f (%d of %d proven) | replay: gather %.2f job %.2f clear %.2f | prologue %.2f asm: count %.2f scatter %.2f\n",
+                         "post %.2f lists %.2f (%d of %d proven, %d re-run) | replay: gather %.2f job %.2f clear %.2f | prologue %.2f asm: count %.2f scatter %.2f\n",
                          ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms(), stats.replay_ms,
                          stats.apply_ms, stats.batches,
                          stats.parallel_batches, stats.refetches, stats.launches(), stats.tier_lists, ms(t2, t3), ms(t3, t4),
@@ -2076,7 +2100,7 @@ int Core::process(mm_matched* out) {
                          dict_.size(), stats.par_bucket_ms, stats.par_work_ms, stats.par_merge_ms,
                          stats.par_task_max_ms, (unsigned long long)stats.par_rows, (unsigned long long)stats.par_hits,
                          stats.rb_prep_ms, stats.rb_overlap_ms, stats.rb_wait_ms, stats.rb_post_ms, stats.rb_lists_ms, stats.lists_proven,
-                         stats.mscan_lists, stats.par_gather_ms, stats.par_job_ms, stats.par_clear_ms, stats.prologue_ms, stats.asm_count_ms,
+                         stats.mscan_lists, stats.mhash_respec, stats.par_gather_ms, stats.par_job_ms, stats.par_clear_ms, stats.prologue_ms, stats.asm_count_ms,
                          stats.asm_scatter_ms);
         }
     }

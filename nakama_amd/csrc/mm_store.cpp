@@ -4,6 +4,7 @@
 // Reference: server/matchmaker.go:443-1040 (mutators, MapMatchmakerIndex),
 // server/match_common.go:78-212 (document field mapping).
 #include <algorithm>
+#include <cctype>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -93,6 +94,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     cfg_.node = nullptr;
     device_ = cfg.device;
     host_share_ = g_create_share;
+    numa_node_ = device_numa_node(device_);
     sess_slots_.live = &live_;
     party_slots_.live = &live_;
     int ndev = 0;
@@ -121,6 +123,8 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_TIER")) tier_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_RANGE")) range_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_LISTPROOF")) list_proof_mode_ = std::atoi(e);
+    if (const char* e = std::getenv("NKM_MHCOUNT")) mhash_count_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_MHLOOP")) mhash_loop_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_BULK")) bulk_mode_ = std::strcmp(e, "0") == 0 ? 0 : std::strcmp(e, "force") == 0 ? 2 : 1;
     if (const char* e = std::getenv("NKM_KERNEL"))
         kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN
@@ -177,27 +181,48 @@ std::vector<int> parse_cpulist(const std::string& path) {  // "0-3,8,10-11"
 }
 }  // namespace
 
-// The CPUs of the calling thread's NUMA node (that the process may use), or
-// none when the host has one node.  Default worker placement: every worker may
-// run anywhere on that node, so the OS still moves it off a busy core, but it
-// never leaves the socket whose memory the store was first-touched on (MI355X
-// boxes: 2 x EPYC 9575F, 2 NUMA nodes; unrestricted workers drifting to the
-// other socket made every walk's store access remote: C2 p50 5.44 -> 3.31 ms,
-// C3 5.42 -> 4.73 ms with node-local workers, profiles/r04n_pin.txt).
-static std::vector<int> node_cpus() {
+// The NUMA node a GPU hangs off (its PCI device's numa_node in sysfs), or -1
+// (unknown, or a one-node host).
+int device_numa_node(int device) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof bus - 1, device) != hipSuccess || !bus[0]) return -1;
+    std::string id(bus);
+    for (char& ch : id) ch = (char)std::tolower((unsigned char)ch);
+    FILE* f = std::fopen(("/sys/bus/pci/devices/" + id + "/numa_node").c_str(), "r");
+    if (!f) return -1;
+    int nd = -1;
+    if (std::fscanf(f, "%d", &nd) != 1) nd = -1;
+    std::fclose(f);
+    return nd;
+}
+
+// The CPUs (that the process may use) of NUMA node `prefer` — the handle's
+// GPU's node — or, when that is unknown or holds none of them, of the calling
+// thread's node; none when the host has one node.  Default worker placement:
+// every worker may run anywhere on that node, so the OS still moves it off a
+// busy core, but it never leaves the socket whose memory the store was
+// first-touched on (MI355X boxes: 2 x EPYC 9575F, 2 NUMA nodes; unrestricted
+// workers drifting to the other socket made every walk's store access remote:
+// C2 p50 5.44 -> 3.31 ms, C3 5.42 -> 4.73 ms with node-local workers,
+// profiles/r04n_pin.txt).
+std::vector<int> node_cpus(int prefer) {
     std::vector<int> out;
     const int cpu = sched_getcpu();
     cpu_set_t allowed;
     if (cpu < 0 || sched_getaffinity(0, sizeof allowed, &allowed) != 0) return out;
     int nodes = 0;
-    std::vector<int> mine;
+    std::vector<int> mine, pref;
     for (int nd = 0; nd < 64; nd++) {
         std::vector<int> l = parse_cpulist("/sys/devices/system/node/node" + std::to_string(nd) + "/cpulist");
         if (l.empty()) continue;
         nodes++;
         if (std::find(l.begin(), l.end(), cpu) != l.end()) mine = l;
+        if (nd == prefer) pref = l;
     }
     if (nodes < 2) return out;
+    for (int c : pref)
+        if (c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) out.push_back(c);
+    if (!out.empty()) return out;
     for (int c : mine)
         if (c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) out.push_back(c);
     return out;
@@ -273,7 +298,12 @@ WorkPool& Core::workers() {
         // NKM_PIN: unset = node-local workers (node_cpus), 1 = one CPU each, 0 = no placement
         const char* pe = std::getenv("NKM_PIN");
         const bool node_wide = !pe || (std::strcmp(pe, "0") && std::strcmp(pe, "1"));
-        workers_.reset(new WorkPool(n, worker_cpus(n - 1), node_wide ? node_cpus() : std::vector<int>{}));
+        std::vector<int> area = node_wide ? node_cpus(numa_node_) : std::vector<int>{};
+        // the node's share: its CPUs over the handles placed on it (a multi
+        // handle's sub-handles on that node, or the local ranks)
+        if (!area.empty() && !std::getenv("NKM_THREADS") && !std::getenv("LOCAL_WORLD_SIZE"))
+            n = std::max(1u, std::min(16u, (unsigned)area.size() / std::max(1u, host_share_)));
+        workers_.reset(new WorkPool(n, worker_cpus(n - 1), area));
     }
     return *workers_;
 }

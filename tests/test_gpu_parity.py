@@ -232,32 +232,40 @@ def test_hashed_mscan(config, n, cfg, kernel, monkeypatch):
     assert rs[0].eval_kernel == want
 
 
-@pytest.mark.parametrize("contig,j", [("0", "2"), ("0", "4"), ("1", "4"), ("1", "8")])
-def test_hashed_mscan_chunk_lengths(contig, j, monkeypatch):
+@pytest.mark.parametrize("contig,j,loop", [("0", "2", "0"), ("0", "4", "0"), ("1", "4", "0"), ("1", "8", "0"),
+                                           ("1", "4", "1"), ("1", "8", "1")])
+def test_hashed_mscan_chunk_lengths(contig, j, loop, monkeypatch):
     """Every chunk shape of the hashed scan: gathered through the scan order
     (2 or 4 candidates per lane) and over contiguous slot runs (4 or 8 per
-    lane, 16-B column loads), with ragged first and last chunks (the second
-    pass starts past a matched prefix)."""
+    lane, 16-B column loads), one chunk per workgroup or the resident
+    pipelined loop (NKM_MHLOOP), with ragged first and last chunks (the
+    second pass starts past a matched prefix).  Lists downloaded
+    (NKM_LISTPROOF=0), so every list is placed and read."""
     set_kernel(monkeypatch, "mhash")
     monkeypatch.setenv("NKM_MCONTIG", contig)
     monkeypatch.setenv("NKM_MHASH_J" if contig == "0" else "NKM_MCONTIG_J", j)
+    monkeypatch.setenv("NKM_MHLOOP", loop)
+    monkeypatch.setenv("NKM_LISTPROOF", "0")
     run_passes(4, 9_999, 2, dict(max_intervals=2))
     run_passes(3, 7_777, 2, dict(max_intervals=2))
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2"])
+@pytest.mark.parametrize("mode,count", [("0", "1"), ("1", "1"), ("1", "0"), ("2", "1")])
 @pytest.mark.parametrize("config,n,contig", [(3, 20_000, "1"), (4, 20_000, "1"), (3, 7_777, "0"),
                                              (4, 9_999, "0")])
-def test_proven_mscan_lists(config, n, contig, mode, monkeypatch, capfd):
+def test_proven_mscan_lists(config, n, contig, mode, count, monkeypatch, capfd):
     """Hashed-scan lists proven equal to their search's batch rows are not
     downloaded (Core::list_proof_mode_): NKM_LISTPROOF=1 (default) skips
-    them, 0 downloads every list, 2 downloads them and throws if a proven
-    list differs from its rows — over contiguous slot runs and through the
-    scan order (NKM_MCONTIG=0).  Groups and state equal to the oracle's
-    either way; the profile line reports the proven lists."""
+    them — with the contiguous scan writing counts only (NKM_MHCOUNT=1,
+    default) or the lists as well (0) — 0 downloads every list, 2 downloads
+    them and throws if a proven list differs from its rows — over contiguous
+    slot runs and through the scan order (NKM_MCONTIG=0).  Groups and state
+    equal to the oracle's either way; the profile line reports the proven
+    lists."""
     set_kernel(monkeypatch, "mhash")
     monkeypatch.setenv("NKM_MCONTIG", contig)
     monkeypatch.setenv("NKM_LISTPROOF", mode)
+    monkeypatch.setenv("NKM_MHCOUNT", count)
     monkeypatch.setenv("NKM_PARALLEL", "force")
     monkeypatch.setenv("NKM_PROFILE", "1")
     rs = run_passes(config, n, 2, dict(max_intervals=2))
@@ -267,6 +275,39 @@ def test_proven_mscan_lists(config, n, contig, mode, monkeypatch, capfd):
     assert got, err[-2000:]
     proven = sum(p for p, _ in got)
     assert (proven == 0) if mode == "0" else (proven > 0), got
+
+
+@pytest.mark.parametrize("config,n", [(3, 9_000), (4, 9_999)])
+def test_counts_only_scan_falls_back(config, n, monkeypatch, capfd):
+    """Counts-only hashed scans (Core::mhash_count_mode_) expect every list
+    proven; with every third ticket inserted inactive (Intervals at
+    MaxIntervals: in the index, never a row) the pool lists hold more than
+    their rows, the batch re-runs the full scan and downloads them, and the
+    speculation pauses.  Groups and state equal to the oracle's."""
+    set_kernel(monkeypatch, "mhash")
+    monkeypatch.setenv("NKM_MCONTIG", "1")
+    monkeypatch.setenv("NKM_PARALLEL", "force")
+    monkeypatch.setenv("NKM_PROFILE", "1")
+    cfg = dict(max_intervals=2)
+    gpu, orc = pair(cfg)
+    ts = synth.TicketSet(config, n)
+    try:
+        for k in range(0, ts.n, 3):
+            ts.tickets[k].intervals = 2
+        ts.insert_into(gpu)
+        ts.insert_into(orc)
+        for _ in range(2):
+            r = gpu.process_raw()
+            assert r.groups == orc.Process()
+            assert state(gpu) == state(orc)
+            assert r.eval_kernel == 4
+    finally:
+        gpu.close()
+        orc.close()
+        ts.close()
+    err = capfd.readouterr().err
+    rerun = [int(m) for m in re.findall(r"proven, (\d+) re-run\)", err)]
+    assert rerun and rerun[0] >= 1, err[-2000:]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -477,7 +518,7 @@ def test_count_multiple_trim_keeps_combo_full(config, n, par, dense, fast, monke
     monkeypatch.setenv("NKM_DENSE", dense)
     monkeypatch.setenv("NKM_FAST", fast)
     rs = run_passes(config, n, 3, dict(max_intervals=3))
-    if config == 18:
+    if config == 18 and par != "0":  # range batches run on the parallel host paths
         assert rs[0].eval_kernel in (6, 7), rs[0].eval_kernel
 
 

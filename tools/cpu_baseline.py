@@ -137,21 +137,33 @@ def per_pool(config, tickets, rows, searches, matched, workers):
     return t, h, per, wall
 
 
-def c5_chunks(config, tickets, chunks):
-    """Whole passes of `chunks` 1000-ticket chunks spread over the set."""
+def c5_chunks(config, tickets, chunks, override=False):
+    """Whole passes of `chunks` 1000-ticket chunks spread over the set.
+    override: the pass is processCustom's candidate pass, the bench's native
+    first-disjoint override (tools/synth.cpp) and mm_process_commit — the
+    same step bench.py --override times on the GPU."""
     from nakama_amd import capi, synth
     nch = tickets // C5_CHUNK
     picks = sorted({(nch * i) // chunks for i in range(chunks)})
     total, matched = 0.0, 0
     for c in picks:
         ts = synth.TicketSet(config, C5_CHUNK, first=c * C5_CHUNK)
-        mm = capi.Matchmaker(_oracle(), max_intervals=2, rev_precision=True, rev_threshold=0)
+        mm = capi.Matchmaker(_oracle(), max_intervals=2, rev_precision=True, rev_threshold=0,
+                             override=(lambda g: g) if override else None)
         try:
             ts.insert_into(mm)
-            t0 = time.perf_counter()
-            r = mm.process_raw()
-            total += time.perf_counter() - t0
-            matched += sum(len({t for t, _ in g}) for g in r.groups)
+            if override:
+                t0 = time.perf_counter()
+                out = mm.process_call()
+                if out.is_candidates:
+                    out = synth.override_commit(mm, out)
+                total += time.perf_counter() - t0
+                matched += mm.process_summary(out)[1]
+            else:
+                t0 = time.perf_counter()
+                r = mm.process_raw()
+                total += time.perf_counter() - t0
+                matched += sum(len({t for t, _ in g}) for g in r.groups)
         finally:
             mm.close()
             ts.close()
@@ -211,6 +223,7 @@ def main():
     ap.add_argument("--matched", type=float, help="tickets the measured GPU pass matched")
     ap.add_argument("--pool-rows", type=int, default=0, help="searching rows per sample (default POOL_ROWS)")
     ap.add_argument("--chunks", type=int, default=1000, help="C5: chunk passes timed (all 1000: the whole pass)")
+    ap.add_argument("--override", action="store_true", help="C5: with the MatchmakerOverride hand-off (bench --override)")
     ap.add_argument("--workers", type=int, default=0, help="concurrent pool processes (default: the usable cores, <= 16)")
     a = ap.parse_args()
     model, ncpu, usable = host_info()
@@ -242,7 +255,10 @@ def main():
                             "note": f"the slowest pool's pass x {rounds} round(s) = {par:.0f} s"}
         out["model"] = {"per_search_ms_pool0": [round(x * 1e3, 3) for x in t[0]], "timed_wall_s": round(wall, 1)}
     else:
-        t, m, k, nch = c5_chunks(a.config, a.tickets, a.chunks)
+        t, m, k, nch = c5_chunks(a.config, a.tickets, a.chunks, a.override)
+        if a.override:
+            out["algorithm"] += ("; + MatchmakerOverride: processCustom's candidates (combineIndexes), the native "
+                                 "first-disjoint override and mm_process_commit, as bench.py --override")
         total = t * nch / k
         out["value"] = a.matched / total
         out["cores"] = 1

@@ -129,11 +129,16 @@ static int run_shape(uint32_t n, int nmode, int nregion, uint4* evict, size_t ev
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     CK(hipEventCreate(&e2));
-    const double bytes = (double)n * (5 + 8 + 18) + (double)n * 4;
-    struct Shape { int contig, j; };
-    const Shape shapes[] = {{0, 2}, {0, 4}, {1, 4}, {1, 8}};
+    // algorithmic bytes: per candidate its slot id (gathered only), alive flag,
+    // counts and two (kind, value) columns; per hit its 4-B slot id
+    auto bytes_of = [&](bool contig) { return (double)n * (contig ? 1 + 8 + 18 : 5 + 8 + 18) + (double)n * 4; };
+    // loop: 0 one chunk per workgroup (mscan_hash_kernel), 1 the resident
+    // pipelined loop (mscan_hash_loop_kernel), 2 the loop writing counts only
+    struct Shape { int contig, j, loop; };
+    const Shape shapes[] = {{0, 2, 0}, {0, 4, 0}, {1, 4, 0}, {1, 8, 0}, {1, 4, 1}, {1, 8, 1}, {1, 4, 2}, {1, 8, 2}};
     for (const Shape& sh : shapes) {
         for (uint32_t dbg : {0u, 1u, 2u, 3u}) {
+            if (sh.loop && dbg) continue;  // the phase switches are mscan_hash_kernel's
             DMScan ms{};
             ms.src_off = 0;
             ms.src_len = n;
@@ -162,7 +167,8 @@ static int run_shape(uint32_t n, int nmode, int nregion, uint4* evict, size_t ev
                         CK(hipStreamSynchronize(s));
                         std::this_thread::sleep_for(std::chrono::milliseconds(5));
                     }
-                    CK(launch_mscan_hash(st, ms, d_blob, d_work, d_res, d_out, s, e0, e1, kMHashEval | kMHashPlace, 0, UINT32_MAX));
+                    const int ph = kMHashEval | kMHashPlace | (sh.loop == 1 ? kMHashLoop : sh.loop == 2 ? kMHashCount : 0);
+                    CK(launch_mscan_hash(st, ms, d_blob, d_work, d_res, d_out, s, e0, e1, ph, 0, UINT32_MAX));
                     CK(hipEventRecord(e2, s));
                     CK(hipEventSynchronize(e2));
                     float a, b;
@@ -173,18 +179,19 @@ static int run_shape(uint32_t n, int nmode, int nregion, uint4* evict, size_t ev
                 std::sort(t.begin(), t.end());
                 std::sort(tall.begin(), tall.end());
                 const double us = 1e3 * t[t.size() / 2];
-                std::printf("n %u sigs %3u %s J%d dbg %u %-4s hash kernel %7.2f us (frac %.3f)  all three %7.2f us\n", n, nq,
-                            sh.contig ? "contig" : "gather", sh.j, dbg, cold == 2 ? "cldW" : cold ? "cldR" : "warm", us, bytes / us / 1e3 / 8000.0,
-                            1e3 * tall[tall.size() / 2]);
+                std::printf("n %u sigs %3u %s J%d %s dbg %u %-4s hash kernel %7.2f us (frac %.3f)  all %7.2f us\n", n, nq,
+                            sh.contig ? "contig" : "gather", sh.j, sh.loop == 2 ? "loopcnt" : sh.loop ? "loop   " : "chunk  ",
+                            dbg, cold == 2 ? "cldW" : cold ? "cldR" : "warm", us,
+                            (sh.loop == 2 ? bytes_of(sh.contig) - (double)n * 4 : bytes_of(sh.contig)) / us / 1e3 / 8000.0, 1e3 * tall[tall.size() / 2]);
             }
-            if (dbg == 0) {  // every list equals the host partition in scan order
+            if (dbg == 0) {  // every list equals the host partition in scan order (counts only: the counts)
                 std::vector<uint32_t> got(off);
                 CK(hipMemcpy(got.data(), d_out, off * 4, hipMemcpyDeviceToHost));
                 std::vector<DGroupResult> res(nq);
                 CK(hipMemcpy(res.data(), d_res, nq * sizeof(DGroupResult), hipMemcpyDeviceToHost));
                 std::vector<uint64_t> at(dst);
                 bool ok = true;
-                for (uint32_t i = 0; i < n && ok; i++) {
+                for (uint32_t i = 0; i < n && ok && sh.loop != 2; i++) {
                     if (!alive[i]) continue;
                     const uint32_t q = (uint32_t)((mode[i] - 100) * nregion + (region[i] - 200));
                     ok = got[at[q]++] == i;
