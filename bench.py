@@ -289,6 +289,7 @@ def main():
     eval_ms = eval_bytes = launches = pair_evals = pairs_decided = cands = 0
     batches, kernels, unroutable = [], set(), 0
     breakdown = {"local_call_ms": [], "summary_ms": [], "merge_ms": []}  # rank 0's cluster-pass phases
+    ov_times, step_phases = {}, {}  # --override: the step's candidate pass / override / commit
     for step in range(args.warmup + args.steps):
         ts = make_set(args, world, rank, step)
         t_ins = time.perf_counter()
@@ -301,14 +302,19 @@ def main():
         t0 = time.perf_counter()
         if cm is None:
             out = mm.process_call()  # the C-ABI call: one whole Process() pass
+            t_pass = time.perf_counter()
             n_cands = out.n_groups if out.is_candidates else 0
             cand = candidate_stats(out)  # the candidate pass ran the searches (a few scalar reads)
             if args.override and out.is_candidates:  # processCustom: override + commit, in the timed step
-                out = synth.override_commit(mm, out)
+                out = synth.override_commit(mm, out, ov_times)
         else:
             cp = cm.Process()        # every rank's pass + the merge into the reference's group order
         barrier_sync(pg, local)
         dt = time.perf_counter() - t0
+        if cm is None and args.override and step >= args.warmup:
+            for k, v in (("candidate_pass_ms", 1e3 * (t_pass - t0)), ("override_ms", ov_times.get("override_ms", 0.0)),
+                         ("commit_ms", ov_times.get("commit_ms", 0.0))):
+                step_phases.setdefault(k, []).append(v)
         if cm is None:
             n_groups, matched, pres, r = mm.process_summary(out)  # untimed: counts the groups, frees them
             # the override's commit runs no search: the pass statistics are the candidate pass's
@@ -408,7 +414,11 @@ def main():
                    "matched_per_step": sum(matched_all) / args.steps, "batches_per_pass_rank0": batches,
                    "candidates_per_pass": (cands / args.steps) if args.override else None,
                    "cluster_phases_ms_rank0": ({k: statistics.median(v) for k, v in breakdown.items()}
-                                               if cm is not None else None)},
+                                               if cm is not None else None),
+                   # --override: medians of the step's parts (the override is the bench's native
+                   # first-disjoint stand-in for the user's MatchmakerOverride, runtime.go:212)
+                   "override_step_ms": ({k: statistics.median(v) for k, v in step_phases.items()}
+                                        if step_phases else None)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "+".join(sorted(kernels)), "launches": launches, "avg_launch_ms": avg_launch_ms,

@@ -80,7 +80,7 @@ def router_lib(path: str = PRODUCT_SO) -> C.CDLL:
 
 CLUSTER_SYMBOLS = ("mm_route_keys", "mm_pack_tickets", "mm_unpack_tickets", "mm_free_unpacked",
                    "mm_merge_positions", "mm_merge_positions_strided", "mm_count_tickets", "mm_shard_rows", "mm_rccl_unique_id", "mm_shard_rows_rccl",
-                   "mm_create_multi", "mm_multi_info")
+                   "mm_create_multi", "mm_multi_info", "mm_device_numa_node")
 
 
 def route_keys(tickets, n: int, pool_fields: Sequence[str]) -> np.ndarray:
@@ -293,34 +293,11 @@ class ClusterMatchmaker:
             _, tickets, pres, stats = self.local.summary_counts(out)
             t2 = time.perf_counter()
             cp = ClusterPass(local=res)
-            # one all-gather of (groups, matched tickets, presences): sizes + totals
-            hdr = [self._t(np.zeros(3, dtype=np.int64)) for _ in range(self.world)]
-            self.dist.all_gather(hdr, self._t(np.array([ng, tickets, pres], dtype=np.int64)))
-            hdr = np.stack([self._host(h) for h in hdr])
-            counts = hdr[:, 0].astype(np.int32)
-            cp.n_groups, cp.matched_tickets, cp.matched_presences = (int(x) for x in hdr.sum(axis=0))
-            # one all-gather of the keys into a [world][m] matrix (padded to
-            # the largest rank's count; one collective, one copy to the host)
-            m = max(int(counts.max()), 1)
-            pad = np.zeros(m, dtype=np.int64)
-            pad[:ng] = keys
-            mat = self._t(np.zeros(self.world * m, dtype=np.int64))
-            self.dist.all_gather_into_tensor(mat, self._t(pad))
-            allk = np.ascontiguousarray(self._host(mat))
-            pos = np.zeros(max(ng, 1), dtype=np.int64)
-            # the merge in C: every rank's keys ascend for processDefault; an
-            # override's choice may reorder them, and then (rc 2, the same on
-            # every rank) the groups take the stable order by (key, rank, index)
-            rc = router_lib().mm_merge_positions_strided(allk.ctypes.data, m, counts.ctypes.data, self.world,
-                                                         self.rank, pos.ctypes.data)
-            cp.positions = pos[:ng]
-            flag = self._t(np.array([1 if rc == 1 else 0], dtype=np.int32))
-            self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX)
-            if int(self._host(flag)[0]) and rc != 2:  # rare: the searching tickets' ids order the tied groups
+
+            def tie_ids():
                 offs = out.group_offsets
-                tie_ids = [out.entries[offs[g + 1] - 1].ticket.decode() for g in range(ng)]
-                flat = np.concatenate([allk[r * m:r * m + int(counts[r])] for r in range(self.world)])
-                self._order_ties(cp, flat, counts, tie_ids)
+                return [out.entries[offs[g + 1] - 1].ticket.decode() for g in range(ng)]
+            self.merge_keys(cp, keys, tickets, pres, tie_ids)
         finally:
             self.local.lib.mm_free_matched(self.local.h, C.byref(out))
         t3 = time.perf_counter()
@@ -330,6 +307,41 @@ class ClusterMatchmaker:
                           "eval_kernel": stats.eval_kernel, "local_call_ms": 1e3 * (t1 - t0),
                           "summary_ms": 1e3 * (t2 - t1), "merge_ms": 1e3 * (t3 - t2)}
         return cp
+
+    def merge_keys(self, cp: ClusterPass, keys: np.ndarray, tickets: int, pres: int, tie_ids=None):
+        """The merge of a cluster pass: this rank's groups' keys (the searching
+        ticket's CreatedAt, in this rank's group order) -> cp's totals and
+        cp.positions, the global position of each of this rank's groups in the
+        reference's order.  Two all-gathers and one all-reduce per pass.
+        tie_ids(): this rank's searching ticket ids, asked for only when two
+        ranks' keys tie (the ids then order the tied groups)."""
+        ng = len(keys)
+        # one all-gather of (groups, matched tickets, presences): sizes + totals
+        hdr = [self._t(np.zeros(3, dtype=np.int64)) for _ in range(self.world)]
+        self.dist.all_gather(hdr, self._t(np.array([ng, tickets, pres], dtype=np.int64)))
+        hdr = np.stack([self._host(h) for h in hdr])
+        counts = hdr[:, 0].astype(np.int32)
+        cp.n_groups, cp.matched_tickets, cp.matched_presences = (int(x) for x in hdr.sum(axis=0))
+        # one all-gather of the keys into a [world][m] matrix (padded to
+        # the largest rank's count; one collective, one copy to the host)
+        m = max(int(counts.max()), 1)
+        pad = np.zeros(m, dtype=np.int64)
+        pad[:ng] = keys
+        mat = self._t(np.zeros(self.world * m, dtype=np.int64))
+        self.dist.all_gather_into_tensor(mat, self._t(pad))
+        allk = np.ascontiguousarray(self._host(mat))
+        pos = np.zeros(max(ng, 1), dtype=np.int64)
+        # the merge in C: every rank's keys ascend for processDefault; an
+        # override's choice may reorder them, and then (rc 2, the same on
+        # every rank) the groups take the stable order by (key, rank, index)
+        rc = router_lib().mm_merge_positions_strided(allk.ctypes.data, m, counts.ctypes.data, self.world,
+                                                     self.rank, pos.ctypes.data)
+        cp.positions = pos[:ng]
+        flag = self._t(np.array([1 if rc == 1 else 0], dtype=np.int32))
+        self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX)
+        if int(self._host(flag)[0]) and rc != 2:  # rare: the searching tickets' ids order the tied groups
+            flat = np.concatenate([allk[r * m:r * m + int(counts[r])] for r in range(self.world)])
+            self._order_ties(cp, flat, counts, tie_ids() if tie_ids is not None else [""] * ng)
 
     def _override(self, out):
         """This rank's override hand-off -> (committed result, error).  An

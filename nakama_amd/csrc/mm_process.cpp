@@ -1629,6 +1629,9 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
     std::vector<uint8_t> sel(nslots(), 0);  // processCustom never selects
     Replay rp(*this, sel, rev, maxI, stats, st, stream_);
     rp.all_rows_search = true;
+    // packed batches (assemble_packed) skip selected / decided rows: none here
+    sel_.assign(nslots(), 0);
+    dec_.assign(nslots(), 0);
     while (order_head_ < order_.size() && !live_[order_[order_head_]]) order_head_++;
     const uint32_t kvar = (uint32_t)var_k_capacity();
     // every row is independent: one search per row, in chunks
@@ -1636,7 +1639,29 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
         const size_t end = std::min(rows.size(), base + kMaxBatchRows / 4);
         if (rev && (row_shard() ? shard_any(timer.check()) : timer.check())) rev = rp.rev = false;
         std::vector<BGroup>& bg = bg_;  // kept across passes (refilled in place: no allocation per row)
-        bg.resize(end - base);
+        const size_t nchunk = end - base;
+        // RevPrecision rows whose sources hold <= 64 entries (C5's buckets)
+        // search as one packed batch (rpack_kernel, as processDefault's
+        // packed batches): a row's hits, reverse bits and pair words come
+        // back in its fixed-stride section, read through packed_view.
+        bool packed = false;
+        std::function<BGroup&(uint32_t)> view;
+        const auto tc0 = std::chrono::steady_clock::now();
+        if (rev && pack_mode_ && kernel_mode_ == KM_AUTO && !row_shard()) {
+            PackBatch pb;
+            if (assemble_packed(rows, base, nchunk, brow_, pb) && pb.n == nchunk) {
+                const auto tp1 = std::chrono::steady_clock::now();
+                stats.assemble_ms += std::chrono::duration<double, std::milli>(tp1 - tc0).count();
+                const PackLayout L = run_packed(pb, stats, nullptr);
+                view = packed_view(L, brow_);
+                stats.pairs_decided += (int64_t)pb.scanned;  // every row one search over its own source
+                stats.search_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp1).count();
+                packed = true;
+            }
+        }
+        // row i's search: its packed section, or the per-row search below
+        auto G = [&](size_t i) -> BGroup& { return packed ? view((uint32_t)i) : bg[i]; };
+        if (!packed) bg.resize(nchunk);
         // the rows' searches (built on the workers for large chunks: the
         // sources from the non-mutating posting lookup)
         auto build = [&](size_t lo, size_t hi) {
@@ -1663,20 +1688,21 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                 g.nrows = 1;  // one row per search (processCustom)
             }
         };
-        const bool par = par_mode_ && bg.size() >= par_min(4096);
-        const auto tc0 = std::chrono::steady_clock::now();
-        if (par) {
-            WorkPool& wp = workers();
-            const size_t nch = (size_t)wp.size() * 4;
-            wp.run(nch, [&](size_t c) { build(bg.size() * c / nch, bg.size() * (c + 1) / nch); });
-        } else {
-            build(0, bg.size());
+        const bool par = par_mode_ && nchunk >= par_min(4096);
+        if (!packed) {
+            if (par) {
+                WorkPool& wp = workers();
+                const size_t nch = (size_t)wp.size() * 4;
+                wp.run(nch, [&](size_t c) { build(bg.size() * c / nch, bg.size() * (c + 1) / nch); });
+            } else {
+                build(0, bg.size());
+            }
+            const auto tc1 = std::chrono::steady_clock::now();
+            rp.run_batch(bg, rev);
+            stats.assemble_ms += std::chrono::duration<double, std::milli>(tc1 - tc0).count();
+            stats.search_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc1).count();
         }
-        const auto tc1 = std::chrono::steady_clock::now();
-        rp.run_batch(bg, rev);
         const auto tc2 = std::chrono::steady_clock::now();
-        stats.assemble_ms += std::chrono::duration<double, std::milli>(tc1 - tc0).count();
-        stats.search_ms += std::chrono::duration<double, std::milli>(tc2 - tc1).count();
         // Every row is independent (processCustom selects nothing): chunks of
         // rows run on the workers into their own candidate lists, appended in
         // row order — unless a RevThreshold timer that may still fire is read
@@ -1692,7 +1718,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
         // The row's filtered hits (:425-468) and, with RevPrecision, their
         // pairwise validateMatch masks; false: the row yields no candidates.
         auto filter_row = [&](size_t i, Scratch& sc, bool row_rev, int& cmin, int& cmax) -> bool {
-            BGroup& g = bg[i];
+            BGroup& g = G(i);
             const uint32_t T = g.row_slot;
             // all hits (paging through the list), filtered as :425-468
             std::vector<uint32_t>& hits = sc.hits;
@@ -1764,7 +1790,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
         auto do_row = [&](size_t i, GroupList& out, Scratch& sc, bool row_rev) {
             int cmin, cmax;
             if (!filter_row(i, sc, row_rev, cmin, cmax)) return;
-            const uint32_t T = bg[i].row_slot;
+            const uint32_t T = G(i).row_slot;
             const std::vector<uint32_t>& hits = sc.hits;
             const std::vector<uint64_t>& pm = sc.pm;
             const size_t L = hits.size();
@@ -1847,10 +1873,10 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
             auto gather = [&](size_t c) {
                 Scratch sc;
                 EnumChunk& E = ec[c];
-                for (size_t i = bg.size() * c / nch; i < bg.size() * (c + 1) / nch; i++) {
+                for (size_t i = nchunk * c / nch; i < nchunk * (c + 1) / nch; i++) {
                     int cmin, cmax;
                     if (!filter_row(i, sc, rev, cmin, cmax)) continue;
-                    const uint32_t T = bg[i].row_slot;
+                    const uint32_t T = G(i).row_slot;
                     const int L = (int)sc.hits.size();
                     const uint64_t V = masks_le(L, std::min(cmax, L));  // ranks 1 .. V-1 (rank 0: the empty mask)
                     if ((V - 1) / kEnumSpan >= (1ull << 26)) {
@@ -1959,7 +1985,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
             std::vector<GroupList> outs(nch);
             wp.run(nch, [&](size_t c) {
                 Scratch sc;
-                for (size_t i = bg.size() * c / nch; i < bg.size() * (c + 1) / nch; i++) do_row(i, outs[c], sc, rev);
+                for (size_t i = nchunk * c / nch; i < nchunk * (c + 1) / nch; i++) do_row(i, outs[c], sc, rev);
             });
             size_t ng = 0, ne = 0;
             for (auto& o : outs) ng += o.size(), ne += o.ents.size();
@@ -1971,7 +1997,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
             }
         } else {
             Scratch sc;
-            for (size_t i = 0; i < bg.size(); i++) {
+            for (size_t i = 0; i < nchunk; i++) {
                 if (rev && !row_shard() && timer.check()) rev = rp.rev = false;  // :353-358
                 do_row(i, cands, sc, rev);
             }

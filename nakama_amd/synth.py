@@ -158,12 +158,15 @@ class TicketSet:
             pass
 
 
-def override_commit(mm: "capi.Matchmaker", out) -> "capi.mm_matched":
+def override_commit(mm: "capi.Matchmaker", out, times=None) -> "capi.mm_matched":
     """The bench's override step on a candidate result `out` (freed here): the
     native first-disjoint override (tools/synth.cpp) picks groups, and
     mm_process_commit hands them back.  Returns the commit's result (free it
-    with the library's mm_free_matched)."""
+    with the library's mm_free_matched).  times: a dict that receives the
+    override's and the commit's milliseconds."""
+    import time
     import numpy as np
+    t0 = time.perf_counter()
     n = out.n_groups
     ne = out.n_entries
     # output room for every candidate, left uninitialised (numpy.empty: only
@@ -174,9 +177,13 @@ def override_commit(mm: "capi.Matchmaker", out) -> "capi.mm_matched":
     offs = offs_buf.ctypes.data_as(C.POINTER(C.c_int32))
     ents = ents_buf.ctypes.data_as(C.POINTER(capi.mm_entry_ref))
     kept = lib().synth_override_first_disjoint(out.group_offsets, out.entries, n, offs, ents)
+    t1 = time.perf_counter()
     res = capi.mm_matched()
     try:  # the kept entries point into the candidate result: it goes back after the commit
         mm._check(mm.lib.mm_process_commit(mm.h, offs, ents, kept, C.byref(res)))
     finally:
         mm.lib.mm_free_matched(mm.h, C.byref(out))
+    if times is not None:
+        times["override_ms"] = 1e3 * (t1 - t0)
+        times["commit_ms"] = 1e3 * (time.perf_counter() - t1)
     return res

@@ -162,3 +162,63 @@ def test_shard_instances_equal_one_global_pass(config, n):
             ts.close()
     assert merged == ref
     assert sum(g[2] for g in gathered) == sum(len({t for t, _ in g}) for g in ref) > 0
+
+
+def _merge_worker(rank, world, port, n_groups, reps, q):
+    """ClusterMatchmaker.merge_keys over gloo on synthetic keys: rank r's
+    groups at CreatedAt keys interleaved with every other rank's (C3's
+    pools: every rank's groups spread over the whole time range)."""
+    import time
+
+    import numpy as np
+
+    from nakama_amd import cluster
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(1000 + rank)
+        # distinct keys across ranks (key % world == rank), ascending per rank
+        keys = np.sort(rng.choice(np.arange(4 * n_groups, dtype=np.int64), n_groups, replace=False)) * world + rank
+        cm = cluster.ClusterMatchmaker(None, dist, ("properties.mode", "properties.region"))
+        times = []
+        for _ in range(reps):
+            cp = cluster.ClusterPass()
+            dist.barrier()
+            t0 = time.perf_counter()
+            cm.merge_keys(cp, keys, 10 * n_groups, 17 * n_groups)
+            times.append(1e3 * (time.perf_counter() - t0))
+        got = [None] * world
+        dist.all_gather_object(got, (keys, cp.positions, cp.n_groups, times))
+        if rank == 0:
+            q.put(got)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_groups", [(8, 175_000), (2, 20_000)])
+def test_cluster_merge_at_c3_volume(world, n_groups):
+    """The pool-sharded merge (two all-gathers, mm_merge_positions_strided,
+    one all-reduce) at world 8 with C3's group volume per rank (175k groups
+    of a 1M-ticket pass): every group's global position is its key's rank in
+    the merged key list.  Prints the merge time (rank 0's median, gloo on the
+    host: DESIGN.md §7 records it)."""
+    import numpy as np
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_merge_worker, args=(r, world, port, n_groups, 5, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    allk = np.concatenate([g[0] for g in got])
+    allp = np.concatenate([g[1] for g in got])
+    assert got[0][2] == world * n_groups
+    assert np.array_equal(np.sort(allp), np.arange(world * n_groups))
+    assert np.array_equal(allk[np.argsort(allp)], np.sort(allk))
+    med = sorted(got[0][3])[len(got[0][3]) // 2]
+    print(f"\ncluster merge world {world} x {n_groups} groups: rank-0 median {med:.2f} ms "
+          f"(all ranks: {[round(sorted(g[3])[2], 2) for g in got]})")

@@ -508,18 +508,15 @@ void synth_free(void* h) { delete static_cast<Synth*>(h); }
 // Tickets are told apart by their ids' text.  Writes the kept groups'
 // offsets (n_kept + 1) and entries into the caller's arrays (sized like the
 // candidates'); returns the number of kept groups.
+//
+// Each distinct entry pointer is mapped once to a ticket number (its text
+// hashed into a table of ids), then "taken" is a flag per ticket number: a
+// library whose entries share one pointer per ticket (the product) hashes
+// each id's text once, and the candidates of one row — a handful of tickets
+// over and over — hit a small direct-mapped pointer cache; a library whose
+// entries are copies (the oracle) hashes every entry's text, as before.
 int32_t synth_override_first_disjoint(const int32_t* offs, const mm_entry_ref* ents, int32_t n_groups,
                                       int32_t* out_offs, mm_entry_ref* out_ents) {
-    // The taken ticket ids: an open-addressing set of their texts (every
-    // library's entries compare by text; the product's share one pointer per
-    // ticket, the oracle's are copies), grown at half load.
-    struct Key {
-        const char* p;
-        uint32_t n;
-        uint32_t tag;
-    };
-    std::vector<Key> tab(1u << 16, Key{nullptr, 0, 0});
-    size_t used = 0;
     auto hash = [](const char* p, size_t n) {
         uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
         size_t i = 0;
@@ -536,61 +533,86 @@ int32_t synth_override_first_disjoint(const int32_t* offs, const mm_entry_ref* e
         }
         return h ^ (h >> 29);
     };
-    auto find = [&](const char* p, size_t n, uint64_t h) -> Key* {  // the key's slot, or the empty one it goes in
-        const size_t mask = tab.size() - 1;
-        for (size_t i = h & mask;; i = (i + 1) & mask) {
-            Key& k = tab[i];
-            if (!k.p || (k.tag == (uint32_t)(h >> 32) && k.n == n && (k.p == p || !std::memcmp(k.p, p, n)))) return &k;
+    // ticket numbers by text
+    struct TKey {
+        const char* p;
+        uint32_t n, tag, id;
+    };
+    std::vector<TKey> ttab(1u << 16, TKey{nullptr, 0, 0, 0});
+    uint32_t n_ids = 0;
+    auto text_id = [&](const char* p) -> uint32_t {
+        const size_t n = std::strlen(p);
+        const uint64_t h = hash(p, n);
+        for (;;) {
+            const size_t mask = ttab.size() - 1;
+            for (size_t i = h & mask;; i = (i + 1) & mask) {
+                TKey& k = ttab[i];
+                if (!k.p) {
+                    if (2 * (n_ids + 1) > ttab.size()) break;  // grow first
+                    k = TKey{p, (uint32_t)n, (uint32_t)(h >> 32), n_ids};
+                    return n_ids++;
+                }
+                if (k.tag == (uint32_t)(h >> 32) && k.n == n && (k.p == p || !std::memcmp(k.p, p, n))) return k.id;
+            }
+            std::vector<TKey> old(ttab.size() * 2, TKey{nullptr, 0, 0, 0});
+            old.swap(ttab);
+            const size_t m2 = ttab.size() - 1;
+            for (const TKey& o : old) {
+                if (!o.p) continue;
+                size_t i = hash(o.p, o.n) & m2;
+                while (ttab[i].p) i = (i + 1) & m2;
+                ttab[i] = o;
+            }
         }
     };
-    auto insert = [&](const char* p, size_t n, uint64_t h) {
-        Key* k = find(p, n, h);
-        if (k->p) return;
-        *k = Key{p, (uint32_t)n, (uint32_t)(h >> 32)};
-        if (2 * ++used > tab.size()) {
-            std::vector<Key> old(tab.size() * 2, Key{nullptr, 0, 0});
-            old.swap(tab);
-            for (const Key& o : old)
-                if (o.p) *find(o.p, o.n, hash(o.p, o.n)) = o;
-        }
+    // ticket numbers by pointer, behind a direct-mapped cache
+    struct PKey {
+        const char* p;
+        uint32_t id;
     };
-    // The pointers of taken entries, checked first: a library whose entries
-    // share one pointer per ticket answers most lookups without hashing text.
-    std::vector<const char*> ptab(1u << 16, nullptr);
+    std::vector<PKey> ptab(1u << 16, PKey{nullptr, 0});
     size_t pused = 0;
-    auto pslot = [&](const char* p) -> const char** {
-        const size_t mask = ptab.size() - 1;
-        uint64_t h = (uint64_t)(uintptr_t)p * 0x9E3779B97F4A7C15ull;
-        for (size_t i = (h >> 20) & mask;; i = (i + 1) & mask)
-            if (!ptab[i] || ptab[i] == p) return &ptab[i];
-    };
-    auto pinsert = [&](const char* p) {
-        const char** q = pslot(p);
-        if (*q) return;
-        *q = p;
+    auto pmix = [](const char* p) { return ((uint64_t)(uintptr_t)p * 0x9E3779B97F4A7C15ull) >> 20; };
+    auto ptr_id = [&](const char* p) -> uint32_t {
+        size_t mask = ptab.size() - 1;
+        size_t i = pmix(p) & mask;
+        for (; ptab[i].p; i = (i + 1) & mask)
+            if (ptab[i].p == p) return ptab[i].id;
+        const uint32_t id = text_id(p);
+        ptab[i] = PKey{p, id};
         if (2 * ++pused > ptab.size()) {
-            std::vector<const char*> old(ptab.size() * 2, nullptr);
+            std::vector<PKey> old(ptab.size() * 2, PKey{nullptr, 0});
             old.swap(ptab);
-            for (const char* o : old)
-                if (o) *pslot(o) = o;
+            mask = ptab.size() - 1;
+            for (const PKey& o : old) {
+                if (!o.p) continue;
+                size_t k = pmix(o.p) & mask;
+                while (ptab[k].p) k = (k + 1) & mask;
+                ptab[k] = o;
+            }
         }
+        return id;
     };
-    auto taken = [&](const char* t) {
-        if (*pslot(t)) return true;
-        const size_t n = std::strlen(t);
-        return find(t, n, hash(t, n))->p != nullptr;
+    PKey cache[256];
+    for (PKey& c : cache) c = PKey{nullptr, 0};
+    auto id_of = [&](const char* p) -> uint32_t {
+        PKey& c = cache[((uintptr_t)p >> 4) & 255];
+        if (c.p == p) return c.id;
+        c = PKey{p, ptr_id(p)};
+        return c.id;
     };
+    std::vector<uint8_t> taken;
+    auto is_taken = [&](uint32_t id) { return id < taken.size() && taken[id]; };
     int32_t kept = 0, e = 0;
     out_offs[0] = 0;
     for (int32_t g = 0; g < n_groups; g++) {
         bool free = true;
-        for (int32_t k = offs[g]; k < offs[g + 1] && free; k++) free = !taken(ents[k].ticket);
+        for (int32_t k = offs[g]; k < offs[g + 1] && free; k++) free = !is_taken(id_of(ents[k].ticket));
         if (!free) continue;
         for (int32_t k = offs[g]; k < offs[g + 1]; k++) {
-            const char* t = ents[k].ticket;
-            const size_t n = std::strlen(t);
-            insert(t, n, hash(t, n));
-            pinsert(t);
+            const uint32_t id = id_of(ents[k].ticket);
+            if (id >= taken.size()) taken.resize(std::max<size_t>(2 * taken.size(), id + 1), 0);
+            taken[id] = 1;
             out_ents[e++] = ents[k];
         }
         out_offs[++kept] = e;
