@@ -82,7 +82,7 @@ hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_b
 uint64_t mscan_hash_counts_word(const DMScan& ms);
 uint64_t mscan_hash_work_words(const DMScan& ms);
 size_t mscan_hash_table_off(uint32_t n_sigs);
-size_t mscan_hash_blob_bytes(uint32_t n_sigs, uint32_t cap);
+size_t mscan_hash_blob_bytes(uint32_t n_sigs, uint32_t cap, uint32_t dsize);
 int mscan_hash_chunk_len(bool contig);
 int mscan_chunk_len(uint32_t n_sigs);
 int mscan_max_sigs();
@@ -745,9 +745,9 @@ private:
     bool mhash_count_mode_ = true;
     uint32_t mhash_spec_pause_ = 0;
     static constexpr uint32_t kSpecPause = 16;
-    // the contiguous hashed scan as the resident pipelined loop
-    // (mscan_hash_loop_kernel); NKM_MHLOOP=0: one chunk per workgroup
-    bool mhash_loop_mode_ = true;
+    // the hashed scan's direct key-grid lookup when the signatures' values
+    // span small ranges (DMScan::dsize); NKM_MHGRID=0: the cuckoo table always
+    bool mhash_grid_mode_ = true;
     bool row_lists_pending_ = false;  // the last batch flagged some BGroup::rows_list
     // writes every rows_list search's host list from its batch rows (a reader
     // other than the dense identity walk) and clears the flags
@@ -909,6 +909,10 @@ public:
     std::vector<std::vector<uint8_t>> fkind_;
     HashIndex slot_of_;               // ticket id -> latest slot (may be dead: checked with live_)
     std::vector<uint32_t> active_list_;                  // pinned (CreatedAt, Ticket) order, may hold inactive
+    // every entry of active_list_ is live and active (set by the filters that
+    // end a pass and a compaction, kept by appends, cleared by kill_slot):
+    // the next pass's rows are then the list itself, copied, not filtered
+    bool active_exact_ = false;
     bool active_sorted_ = true;
     SlotSets sess_slots_;             // session dict id -> slots (sessionTickets)
     SlotSets party_slots_;            // party dict id -> slots (partyTickets)

@@ -111,6 +111,10 @@ struct DMScan {
                                 // to `chunk` from src_off rounded down
     uint32_t hseed[2];          // hashed: the two cuckoo hash seeds
     uint32_t pad;
+    // hashed, direct lookup (dsize > 0): the key grid over the signatures'
+    // values, cell = sum_f (value_f - dlo[f]) * prod_{g > f} drng[g]
+    uint32_t dsize;
+    uint32_t dlo[4], drng[4];
     // hashed, row-sharded: rank r evaluates chunks [cb[r], cb[r + 1]) and its
     // (n_sigs + 1) count columns are one contiguous block (mhash_cidx), so the
     // ranks' scratch and counts are all-gathered as one segment each.
@@ -138,10 +142,10 @@ constexpr uint32_t kMHashSigs = 256;  // signatures of one hashed scan
 constexpr uint32_t kMHashCap = 1024;  // table entries (a power of two >= 2 x signatures)
 constexpr uint32_t kMHashEmpty = 0xFFFFu;
 // launch_mscan_hash phases: kMHashEval the per-chunk scan, kMHashPlace the
-// bases + placement; kMHashLoop the scan as a resident pipelined loop
-// (contiguous chunks); kMHashCount the loop writing counts only (no lists:
-// placement reduced to the bases)
-constexpr int kMHashEval = 1, kMHashPlace = 2, kMHashLoop = 4, kMHashCount = 8;
+// bases + placement; kMHashCount (contiguous chunks) the scan writing counts
+// only (no lists: placement reduced to the bases)
+constexpr int kMHashEval = 1, kMHashPlace = 2, kMHashCount = 8;
+constexpr uint32_t kMHashGrid = 4096;  // key-grid cells (u16 each) of the direct lookup
 struct DMHashEntry {                  // 32 B
     uint32_t key[4];                  // required dictionary id per scanned field (0 past n_fields)
     uint32_t q;                       // signature, kMHashEmpty: free

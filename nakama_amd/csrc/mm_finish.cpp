@@ -92,6 +92,7 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
     filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, list_tmp_,
                  [&](uint32_t s) { return live_[s] && is_active_[s]; });
     active_list_.swap(list_tmp_);
+    active_exact_ = true;
     if (batch_profile_)
         std::fprintf(stderr, "[nkm]   finish: expired %zu, checks/order %.2f, retire %.2f, active filter %.2f ms\n",
                      expired.size(), f_ms(f0, f1), f_ms(f1, f2), f_ms(f2 > f0 ? f2 : f0, fclk::now()));
@@ -182,6 +183,7 @@ bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& gro
     filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, list_tmp_,
                  [&](uint32_t s) { return live_[s] && is_active_[s]; });
     active_list_.swap(list_tmp_);
+    active_exact_ = true;
     if (const char* p = std::getenv("NKM_PROFILE"); p && std::atoi(p) >= 2) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "[nkm]   finish: retire %.3f ms (%s, %s) | filter %.3f ms (%zu active)\n", ms(f0, f1),

@@ -748,21 +748,40 @@ __device__ __forceinline__ void load_run(T (&dst)[N], const T* p) {
 // with 4-16-B vector loads (one instruction per column per lane instead of
 // kMJ gathers, and no slot ids read); the signatures found are handed through
 // LDS to the strided layout (candidate j * 256 + tid) the ranking uses.
-// LDS is sized at launch (mscan_hash_lds): the table, the (signature, j,
-// wave) counts, the chunk's signature offsets, its staged hits, and CONTIG's
-// hand-over — 12 KB for C4's 64 signatures, so occupancy stays high.
+// LDS is sized at launch: the lookup (cuckoo table or key grid, tab_bytes),
+// the (j, wave, signature) counts, the chunk's signature offsets, its staged
+// hits, and CONTIG's hand-over — 12 KB for C4's 64 signatures, so occupancy
+// stays high.
 template <int kMJ, bool CONTIG>
 struct MHashLds {
-    uint32_t cap, nq;
+    uint32_t tab_bytes, nq;
     __host__ __device__ constexpr uint32_t table_off() const { return 0; }
-    __host__ __device__ constexpr uint32_t cnt_off() const { return cap * 32u; }
+    __host__ __device__ constexpr uint32_t cnt_off() const { return (tab_bytes + 15u) & ~15u; }
     __host__ __device__ constexpr uint32_t loff_off() const { return cnt_off() + ((nq * kMJ * kWaves * 2u + 15u) & ~15u); }
     __host__ __device__ constexpr uint32_t stage_off() const { return loff_off() + ((nq * 4u + 15u) & ~15u); }
     __host__ __device__ constexpr uint32_t qs_off() const { return stage_off() + kMJ * kBlock * 4u; }
     __host__ __device__ constexpr uint32_t bytes() const { return qs_off() + (CONTIG ? kMJ * kBlock * 2u : 0u); }
 };
+// the lookup's LDS bytes: the key grid (u16 per cell) + the signatures' count
+// ranges, or the cuckoo table
+__host__ __device__ inline uint32_t mhash_tab_bytes(const DMScan& ms) {
+    return ms.dsize ? ((ms.dsize * 2u + 15u) & ~15u) + ((ms.n_sigs * 8u + 15u) & ~15u) : (ms.hmask + 1) * 32u;
+}
 
-template <int NF, int kMJ, bool CONTIG>
+// COUNT: only the per-(signature, chunk) counts are written, no ranking into
+// scratch — the proven-list pass (Core::mhash_count_mode_), whose lists are
+// never placed.
+//
+// The lookup.  A candidate's required keyword values select at most one
+// signature.  When the signatures' values span small ranges per field (every
+// pool value a dictionary id: C3 / C4's modes and regions), the key grid
+// (ms.dsize cells of u16, indexed by the values' offsets from the ranges'
+// lows) gives it with one 2-B LDS read — exact, no key compare.  Otherwise
+// two-choice cuckoo hashing: two 32-B entries, whose random 16-B LDS reads
+// are bank-conflicted (rocprofv3 on C4's 64-signature table:
+// SQ_LDS_BANK_CONFLICT ~7 cycles per LDS instruction, the kernel LDS-bound
+// at ~36 us warm or cold, profiles/r05c_*).
+template <int NF, int kMJ, bool CONTIG, bool COUNT>
 __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms, const DMHashEntry* __restrict__ htab,
                                                             uint32_t* __restrict__ scratch,
                                                             uint32_t* __restrict__ counts, uint32_t c0) {
@@ -773,9 +792,12 @@ __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t wsum[kWaves], wlive[kWaves];
     const uint32_t nq = ms.n_sigs, hmask = ms.hmask;
-    const MHashLds<kMJ, CONTIG> L{hmask + 1, nq};
+    const bool grid = ms.dsize != 0;
+    const MHashLds<kMJ, CONTIG> L{mhash_tab_bytes(ms), nq};
     DMHashEntry* tab = reinterpret_cast<DMHashEntry*>(lds + L.table_off());
-    uint16_t* cnt = reinterpret_cast<uint16_t*>(lds + L.cnt_off());  // [q][j][wave]: count, then its rank base
+    uint16_t* dgrid = reinterpret_cast<uint16_t*>(lds + L.table_off());
+    int32_t* dlim = reinterpret_cast<int32_t*>(lds + L.table_off() + ((ms.dsize * 2u + 15u) & ~15u));
+    uint16_t* cnt = reinterpret_cast<uint16_t*>(lds + L.cnt_off());  // [j][wave][q]: count, then its rank base
     uint32_t* loff = reinterpret_cast<uint32_t*>(lds + L.loff_off());
     uint32_t* stage = reinterpret_cast<uint32_t*>(lds + L.stage_off());  // the chunk's hits, signature-major
     uint16_t* qs = reinterpret_cast<uint16_t*>(lds + L.qs_off());
@@ -811,12 +833,13 @@ __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms
             s[j] = i < len ? sl[j] : kNoSlot;
         }
     }
-    // the table and zeroed counts into LDS while the column loads are in flight
+    // the lookup and zeroed counts into LDS while the column loads are in flight
     if (!(dbg & 4)) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4* __restrict__ g4 = reinterpret_cast<const u32x4*>(htab);
+        const u32x4* __restrict__ g4 = reinterpret_cast<const u32x4*>(htab);  // the grid follows the cuckoo table
         u32x4* t4 = reinterpret_cast<u32x4*>(tab);
-        for (uint32_t t = (uint32_t)tid; t < 2 * (hmask + 1); t += kBlock) t4[t] = g4[t];
+        const uint32_t g0 = grid ? 2 * (hmask + 1) : 0u, nv = L.tab_bytes / 16u;
+        for (uint32_t t = (uint32_t)tid; t < nv; t += kBlock) t4[t] = g4[g0 + t];
         uint32_t* c4 = reinterpret_cast<uint32_t*>(cnt);
         for (uint32_t t = (uint32_t)tid; t < (nq * kMJ * kWaves + 1) / 2; t += kBlock) c4[t] = 0u;
     }
@@ -826,22 +849,46 @@ __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms
     int64_t vv[NF][kMJ];
     bool a[kMJ];
     if constexpr (CONTIG) {
-        const uint32_t gs = cs0 + (uint32_t)tid * kMJ;  // the lane's run: candidates (wave, lane, j)
-        if (gs >= vlo && gs + kMJ <= vhi) {
-            load_run(al, st.alive + gs);
-            load_run(mn, st.minc + gs);
-            load_run(mx, st.maxc + gs);
+        // wave w takes the chunk's candidates [w * 64 kMJ, (w + 1) * 64 kMJ) in
+        // pairs: lane l's candidates j = 2p, 2p + 1 are wb + 128 p + 2 l + {0, 1},
+        // so each column load instruction of the wave reads one contiguous
+        // span (an int64 pair per lane: 1 KB; an int32 pair: 512 B) — the
+        // fully coalesced shape, where a lane-contiguous run of kMJ values
+        // spread every instruction over kMJ / 2 times the cache lines
+        const uint32_t wb = cs0 + (uint32_t)wave * 64u * kMJ;
+        if (wb >= vlo && wb + 64u * kMJ <= vhi) {
 #pragma unroll
-            for (int f = 0; f < NF; f++) {
-                load_run(kk[f], (const uint8_t*)(fkp[f] + gs));
-                load_run(vv[f], (const int64_t*)(fvp[f] + gs));
+            for (int p = 0; p < kMJ / 2; p++) {
+                const uint32_t x = wb + 128u * p + 2u * (uint32_t)lane;
+                uint8_t a2[2], k2[NF][2];
+                int32_t n2[2], m2[2];
+                int64_t v2[NF][2];
+                load_run(a2, st.alive + x);
+                load_run(n2, st.minc + x);
+                load_run(m2, st.maxc + x);
+#pragma unroll
+                for (int f = 0; f < NF; f++) {
+                    load_run(k2[f], (const uint8_t*)(fkp[f] + x));
+                    load_run(v2[f], (const int64_t*)(fvp[f] + x));
+                }
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    al[2 * p + e] = a2[e];
+                    mn[2 * p + e] = n2[e];
+                    mx[2 * p + e] = m2[e];
+#pragma unroll
+                    for (int f = 0; f < NF; f++) {
+                        kk[f][2 * p + e] = k2[f][e];
+                        vv[f][2 * p + e] = v2[f][e];
+                    }
+                }
             }
 #pragma unroll
             for (int j = 0; j < kMJ; j++) a[j] = al[j] != 0;
         } else {  // the scan's first / last chunk: per candidate, in range only
 #pragma unroll
             for (int j = 0; j < kMJ; j++) {
-                const uint32_t x = gs + j;
+                const uint32_t x = wb + 128u * (uint32_t)(j / 2) + 2u * (uint32_t)lane + (uint32_t)(j & 1);
                 a[j] = x >= vlo && x < vhi;
                 al[j] = 0;
                 mn[j] = mx[j] = 0;
@@ -886,38 +933,76 @@ __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms
     }
     for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o);
     if (lane == 0) wlive[wave] = live;
-    __syncthreads();  // table and zeroed counts are in LDS
-    // each candidate's signature (at most one): its two cuckoo entries, read
-    // together; then the signature's count-range musts.  A keyword value is a
-    // dictionary id (< 2^32), so the 32-bit keys compare exactly.
+    __syncthreads();  // lookup and zeroed counts are in LDS
+    // each candidate's signature (at most one), then the signature's
+    // count-range musts.  A keyword value is a dictionary id (< 2^32), so the
+    // 32-bit keys compare exactly.
     uint32_t q[kMJ];
+    if (grid) {
 #pragma unroll
-    for (int j = 0; j < kMJ; j++) {
-        uint32_t h1 = ms.hseed[0], h2 = ms.hseed[1];
+        for (int j = 0; j < kMJ; j++) {
+            uint32_t idx = 0;
+            bool in = a[j];
 #pragma unroll
-        for (int f = 0; f < NF; f++) {
-            h1 = msig_mix(h1, (uint32_t)vv[f][j]);
-            h2 = msig_mix(h2, (uint32_t)vv[f][j]);
+            for (int f = 0; f < NF; f++) {
+                const uint32_t d = (uint32_t)vv[f][j] - ms.dlo[f];
+                in = in && d < ms.drng[f];
+                idx = idx * ms.drng[f] + d;
+            }
+            const uint32_t qq = in ? (uint32_t)dgrid[idx] : 0xFFFFu;
+            const bool hit = qq != 0xFFFFu;
+            const int32_t tmin = hit ? dlim[2 * qq] : 0, tmax = hit ? dlim[2 * qq + 1] : 0;
+            q[j] = hit && mn[j] >= tmin && mx[j] <= tmax ? qq : kNone;
         }
-        const DMHashEntry& e1 = tab[msig_fin(h1) & hmask];
-        const DMHashEntry& e2 = tab[msig_fin(h2) & hmask];
-        bool m1 = e1.q != kNone, m2 = e2.q != kNone;
+    } else {
 #pragma unroll
-        for (int f = 0; f < NF; f++) {
-            m1 = m1 && e1.key[f] == (uint32_t)vv[f][j];
-            m2 = m2 && e2.key[f] == (uint32_t)vv[f][j];
+        for (int j = 0; j < kMJ; j++) {
+            uint32_t h1 = ms.hseed[0], h2 = ms.hseed[1];
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                h1 = msig_mix(h1, (uint32_t)vv[f][j]);
+                h2 = msig_mix(h2, (uint32_t)vv[f][j]);
+            }
+            const DMHashEntry& e1 = tab[msig_fin(h1) & hmask];
+            const DMHashEntry& e2 = tab[msig_fin(h2) & hmask];
+            bool m1 = e1.q != kNone, m2 = e2.q != kNone;
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                m1 = m1 && e1.key[f] == (uint32_t)vv[f][j];
+                m2 = m2 && e2.key[f] == (uint32_t)vv[f][j];
+            }
+            const uint32_t qq = m1 ? e1.q : e2.q;
+            const int32_t tmin = m1 ? e1.tmin : e2.tmin, tmax = m1 ? e1.tmax : e2.tmax;
+            q[j] = a[j] && (m1 || m2) && mn[j] >= tmin && mx[j] <= tmax ? qq : kNone;
         }
-        const uint32_t qq = m1 ? e1.q : e2.q;
-        const int32_t tmin = m1 ? e1.tmin : e2.tmin, tmax = m1 ? e1.tmax : e2.tmax;
-        q[j] = a[j] && (m1 || m2) && mn[j] >= tmin && mx[j] <= tmax ? qq : kNone;
-        if (dbg & 1) q[j] = a[j] ? (uint32_t)(vv[0][j] ^ vv[NF - 1][j]) & (nq - 1) : kNone;  // no table probe
+    }
+#pragma unroll
+    for (int j = 0; j < kMJ; j++)
+        if (dbg & 1) q[j] = a[j] ? (uint32_t)(vv[0][j] ^ vv[NF - 1][j]) & (nq - 1) : kNone;  // no lookup
+    if constexpr (COUNT) {
+        // counts only: the order of the hits does not matter, so no exchange
+        // and no ranking — one LDS increment per hit (the zeroed counts'
+        // first nq words)
+        uint32_t* cq = reinterpret_cast<uint32_t*>(cnt);
+#pragma unroll
+        for (int j = 0; j < kMJ; j++)
+            if (q[j] != kNone) atomicAdd(&cq[q[j]], 1u);
+        __syncthreads();
+        if ((uint32_t)tid < nq) counts[mhash_cidx(ms, (uint32_t)tid, c)] = cq[tid];
+        if (tid == 0) {
+            uint32_t lv = 0;
+            for (int w = 0; w < kWaves; w++) lv += wlive[w];
+            counts[mhash_cidx(ms, nq, c)] = lv;
+        }
+        return;
     }
     if constexpr (CONTIG) {
-        // runs (wave, lane, j) -> the strided layout j * 256 + tid, through LDS
-        uint16_t pk[kMJ];
+        // (wave, pair, lane, e) -> the strided layout j * 256 + tid (candidate
+        // order), through LDS
 #pragma unroll
-        for (int j = 0; j < kMJ; j++) pk[j] = (uint16_t)q[j];
-        __builtin_memcpy(&qs[tid * kMJ], pk, sizeof pk);
+        for (int j = 0; j < kMJ; j++)
+            qs[(uint32_t)wave * 64u * kMJ + 128u * (uint32_t)(j / 2) + 2u * (uint32_t)lane + (uint32_t)(j & 1)] =
+                (uint16_t)q[j];
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < kMJ; j++) {
@@ -947,22 +1032,29 @@ __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms
             peer &= bit ? bb : ~bb;
         }
         rk[j] = lanes_below(peer);
-        if (m && rk[j] == 0) cnt[(q[j] * kMJ + j) * kWaves + wave] = (uint16_t)__popcll(peer);
+        if (m && rk[j] == 0) cnt[(j * kWaves + wave) * nq + q[j]] = (uint16_t)__popcll(peer);
     }
     __syncthreads();
-    // per signature: rank bases in candidate order (j, wave); the chunk's
-    // signature-major offsets by a block scan of the totals
+    // per signature: rank bases in candidate order (j, wave) — thread q reads
+    // column q of the [j][wave][q] counts (consecutive threads, consecutive
+    // halfwords); the chunk's signature-major offsets by a block scan of the totals
     uint32_t tot = 0;
     if ((uint32_t)tid < nq) {
-        uint16_t* cq = cnt + (uint32_t)tid * kMJ * kWaves;
         uint32_t run = 0;
 #pragma unroll
         for (int k = 0; k < kMJ * kWaves; k++) {
-            const uint32_t v = cq[k];
-            cq[k] = (uint16_t)run;
+            uint16_t* cq = cnt + (uint32_t)k * nq + (uint32_t)tid;
+            const uint32_t v = *cq;
+            *cq = (uint16_t)run;
             run += v;
         }
         tot = run;
+        counts[mhash_cidx(ms, (uint32_t)tid, c)] = tot;  // column-major: mscan_base_kernel reads columns
+    }
+    if (tid == 0) {
+        uint32_t lv = 0;
+        for (int w = 0; w < kWaves; w++) lv += wlive[w];
+        counts[mhash_cidx(ms, nq, c)] = lv;
     }
     uint32_t incl = tot;
     for (int o = 1; o < 64; o <<= 1) {
@@ -976,238 +1068,19 @@ __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms
         if (w < wave) ex += wsum[w];
         total += wsum[w];
     }
-    if ((uint32_t)tid < nq) {
-        loff[tid] = ex;
-        counts[mhash_cidx(ms, (uint32_t)tid, c)] = tot;  // column-major: mscan_base_kernel reads columns
-    }
-    if (tid == 0) {
-        uint32_t lv = 0;
-        for (int w = 0; w < kWaves; w++) lv += wlive[w];
-        counts[mhash_cidx(ms, nq, c)] = lv;
-    }
+    if ((uint32_t)tid < nq) loff[tid] = ex;
     __syncthreads();
     // ranked into LDS, then out in 16-B stores: with many signatures a
     // wave's hits fall in as many signature segments, and direct 4-B stores
     // would cost one partial-line write each
 #pragma unroll
     for (int j = 0; j < kMJ; j++)
-        if (q[j] != kNone) stage[loff[q[j]] + cnt[(q[j] * kMJ + j) * kWaves + wave] + rk[j]] = s[j];
+        if (q[j] != kNone) stage[loff[q[j]] + cnt[(j * kWaves + wave) * nq + q[j]] + rk[j]] = s[j];
     __syncthreads();
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x4* __restrict__ cs4 = reinterpret_cast<u32x4*>(scratch + (uint64_t)c * kMChunk);
     const u32x4* st4 = reinterpret_cast<const u32x4*>(stage);
     for (uint32_t v = (uint32_t)tid; 4 * v < total; v += kBlock) cs4[v] = st4[v];
-}
-
-// ---- the contiguous hashed scan as a resident, pipelined loop ----------------
-// mscan_hash_kernel<CONTIG> loads a chunk, then works on it: a workgroup's
-// loads are in flight only at its start, so with one chunk per workgroup the
-// HBM pipe drains at every round boundary of the grid (C4's 4,096 chunks on
-// 256 CUs: two rounds) and every workgroup copies the cuckoo table into LDS
-// again.  Here the grid is what stays resident (the CUs x the occupancy) and
-// each workgroup walks the chunks c, c + grid, ...: the table is loaded once,
-// and the next chunk's columns are requested before the current chunk is
-// hashed, ranked and stored, so they arrive while it works.  COUNT: only the
-// per-(signature, chunk) counts are written (no ranking into scratch): the
-// proven-list pass (Core::list_proof_mode_), whose lists are never placed.
-// Same LDS layout (MHashLds<kMJ, true>), same outputs as mscan_hash_kernel.
-template <int NF, int kMJ>
-struct MHashCols {
-    uint8_t al[kMJ];
-    int32_t mn[kMJ], mx[kMJ];
-    uint8_t kk[NF][kMJ];
-    int64_t vv[NF][kMJ];
-};
-
-// chunk c's columns of this lane's run (candidates cs0 + tid * kMJ + j); a run
-// outside the scan's [vlo, vhi) is loaded per candidate (in range only)
-template <int NF, int kMJ>
-__device__ __forceinline__ void mhash_load(MHashCols<NF, kMJ>& R, const DStore& st,
-                                           const __attribute__((address_space(1))) uint8_t* const (&fkp)[NF],
-                                           const __attribute__((address_space(1))) int64_t* const (&fvp)[NF],
-                                           uint32_t gs, uint32_t vlo, uint32_t vhi) {
-    if (gs >= vlo && gs + kMJ <= vhi) {
-        load_run(R.al, st.alive + gs);
-        load_run(R.mn, st.minc + gs);
-        load_run(R.mx, st.maxc + gs);
-#pragma unroll
-        for (int f = 0; f < NF; f++) {
-            load_run(R.kk[f], (const uint8_t*)(fkp[f] + gs));
-            load_run(R.vv[f], (const int64_t*)(fvp[f] + gs));
-        }
-        return;
-    }
-#pragma unroll
-    for (int j = 0; j < kMJ; j++) {
-        const uint32_t x = gs + j;
-        const bool in = x >= vlo && x < vhi;
-        R.al[j] = in ? st.alive[x] : (uint8_t)0;
-        R.mn[j] = in ? st.minc[x] : 0;
-        R.mx[j] = in ? st.maxc[x] : 0;
-#pragma unroll
-        for (int f = 0; f < NF; f++) {
-            R.kk[f][j] = in ? fkp[f][x] : (uint8_t)KIND_ABSENT;
-            R.vv[f][j] = in ? fvp[f][x] : 0;
-        }
-    }
-}
-
-template <int NF, int kMJ, bool COUNT>
-__global__ __launch_bounds__(kBlock) void mscan_hash_loop_kernel(DStore st, DMScan ms, const DMHashEntry* __restrict__ htab,
-                                                                 uint32_t* __restrict__ scratch,
-                                                                 uint32_t* __restrict__ counts, uint32_t c_lo,
-                                                                 uint32_t c_hi) {
-    static_assert(NF >= 1 && NF <= 4, "1-4 required fields");
-    static_assert(kMJ == 4 || kMJ == 8, "runs of 4 or 8 candidates");
-    constexpr int kMChunk = kMJ * kBlock;
-    constexpr uint32_t kNone = kMHashEmpty;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ uint32_t wsum[kWaves], wlive[kWaves];
-    const uint32_t nq = ms.n_sigs, hmask = ms.hmask;
-    const MHashLds<kMJ, true> L{hmask + 1, nq};
-    DMHashEntry* tab = reinterpret_cast<DMHashEntry*>(lds + L.table_off());
-    uint16_t* cnt = reinterpret_cast<uint16_t*>(lds + L.cnt_off());
-    uint32_t* loff = reinterpret_cast<uint32_t*>(lds + L.loff_off());
-    uint32_t* stage = reinterpret_cast<uint32_t*>(lds + L.stage_off());
-    uint16_t* qs = reinterpret_cast<uint16_t*>(lds + L.qs_off());
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    typedef const __attribute__((address_space(1))) uint8_t gu8;
-    typedef const __attribute__((address_space(1))) int64_t gi64;
-    gu8* fkp[NF];
-    gi64* fvp[NF];
-#pragma unroll
-    for (int f = 0; f < NF; f++) {
-        fkp[f] = (gu8*)st.fkind[ms.field[f]];
-        fvp[f] = (gi64*)st.fval[ms.field[f]];
-    }
-    const uint32_t base0 = ms.src_off & ~(uint32_t)(kMChunk - 1);
-    const uint32_t vlo = ms.src_off, vhi = ms.src_off + ms.src_len;
-    const uint32_t stride = gridDim.x;
-    uint32_t c = c_lo + blockIdx.x;
-    MHashCols<NF, kMJ> cur, nxt;
-    if (c < c_hi) mhash_load(cur, st, fkp, fvp, base0 + c * (uint32_t)kMChunk + (uint32_t)tid * kMJ, vlo, vhi);
-    {  // the table, once per workgroup, while the first chunk's loads are in flight
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4* __restrict__ g4 = reinterpret_cast<const u32x4*>(htab);
-        u32x4* t4 = reinterpret_cast<u32x4*>(tab);
-        for (uint32_t t = (uint32_t)tid; t < 2 * (hmask + 1); t += kBlock) t4[t] = g4[t];
-    }
-    const uint32_t nbits = nq > 1 ? 32u - (uint32_t)__clz(nq - 1) : 0u;
-    for (; c < c_hi; c += stride) {
-        const uint32_t cn = c + stride;
-        if (cn < c_hi) mhash_load(nxt, st, fkp, fvp, base0 + cn * (uint32_t)kMChunk + (uint32_t)tid * kMJ, vlo, vhi);
-        const uint32_t cs0 = base0 + c * (uint32_t)kMChunk;
-        __syncthreads();  // the previous chunk is out of stage / cnt / qs (and the table is in)
-        {
-            uint32_t* c4 = reinterpret_cast<uint32_t*>(cnt);
-            for (uint32_t t = (uint32_t)tid; t < (nq * kMJ * kWaves + 1) / 2; t += kBlock) c4[t] = 0u;
-        }
-        bool a[kMJ];
-        uint32_t live = 0;
-#pragma unroll
-        for (int j = 0; j < kMJ; j++) {
-            a[j] = cur.al[j] != 0;
-            live += a[j];
-#pragma unroll
-            for (int f = 0; f < NF; f++) a[j] = a[j] && cur.kk[f][j] == KIND_KEYWORD;  // every field is required
-        }
-        for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o);
-        if (lane == 0) wlive[wave] = live;
-        uint32_t q[kMJ];
-#pragma unroll
-        for (int j = 0; j < kMJ; j++) {
-            uint32_t h1 = ms.hseed[0], h2 = ms.hseed[1];
-#pragma unroll
-            for (int f = 0; f < NF; f++) {
-                h1 = msig_mix(h1, (uint32_t)cur.vv[f][j]);
-                h2 = msig_mix(h2, (uint32_t)cur.vv[f][j]);
-            }
-            const DMHashEntry& e1 = tab[msig_fin(h1) & hmask];
-            const DMHashEntry& e2 = tab[msig_fin(h2) & hmask];
-            bool m1 = e1.q != kNone, m2 = e2.q != kNone;
-#pragma unroll
-            for (int f = 0; f < NF; f++) {
-                m1 = m1 && e1.key[f] == (uint32_t)cur.vv[f][j];
-                m2 = m2 && e2.key[f] == (uint32_t)cur.vv[f][j];
-            }
-            const uint32_t qq = m1 ? e1.q : e2.q;
-            const int32_t tmin = m1 ? e1.tmin : e2.tmin, tmax = m1 ? e1.tmax : e2.tmax;
-            q[j] = a[j] && (m1 || m2) && cur.mn[j] >= tmin && cur.mx[j] <= tmax ? qq : kNone;
-        }
-        // runs (wave, lane, j) -> the strided layout j * 256 + tid (candidate order), through LDS
-        {
-            uint16_t pk[kMJ];
-#pragma unroll
-            for (int j = 0; j < kMJ; j++) pk[j] = (uint16_t)q[j];
-            __builtin_memcpy(&qs[tid * kMJ], pk, sizeof pk);
-        }
-        __syncthreads();  // qs written, cnt zeroed, wlive in
-        uint32_t s[kMJ];
-#pragma unroll
-        for (int j = 0; j < kMJ; j++) {
-            const uint32_t i = (uint32_t)(j * kBlock + tid);
-            q[j] = qs[i];
-            s[j] = cs0 + i;
-        }
-        // rank within (signature, j, wave): one ballot per signature-index bit
-        uint32_t rk[kMJ];
-#pragma unroll
-        for (int j = 0; j < kMJ; j++) {
-            const bool m = q[j] != kNone;
-            uint64_t peer = __ballot((int)m);
-            for (uint32_t b = 0; b < nbits; b++) {
-                const bool bit = (q[j] >> b) & 1u;
-                const uint64_t bb = __ballot((int)(m && bit));
-                peer &= bit ? bb : ~bb;
-            }
-            rk[j] = lanes_below(peer);
-            if (m && rk[j] == 0) cnt[(q[j] * kMJ + j) * kWaves + wave] = (uint16_t)__popcll(peer);
-        }
-        __syncthreads();
-        uint32_t tot = 0;
-        if ((uint32_t)tid < nq) {
-            uint16_t* cq = cnt + (uint32_t)tid * kMJ * kWaves;
-            uint32_t run = 0;
-#pragma unroll
-            for (int k = 0; k < kMJ * kWaves; k++) {
-                const uint32_t v = cq[k];
-                cq[k] = (uint16_t)run;
-                run += v;
-            }
-            tot = run;
-        }
-        if ((uint32_t)tid < nq) counts[mhash_cidx(ms, (uint32_t)tid, c)] = tot;
-        if (tid == 0) {
-            uint32_t lv = 0;
-            for (int w = 0; w < kWaves; w++) lv += wlive[w];
-            counts[mhash_cidx(ms, nq, c)] = lv;
-        }
-        if constexpr (!COUNT) {
-            uint32_t incl = tot;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t u = __shfl_up(incl, o);
-                if (lane >= o) incl += u;
-            }
-            if (lane == 63) wsum[wave] = incl;
-            __syncthreads();
-            uint32_t ex = incl - tot, total = 0;
-            for (int w = 0; w < kWaves; w++) {
-                if (w < wave) ex += wsum[w];
-                total += wsum[w];
-            }
-            if ((uint32_t)tid < nq) loff[tid] = ex;
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < kMJ; j++)
-                if (q[j] != kNone) stage[loff[q[j]] + cnt[(q[j] * kMJ + j) * kWaves + wave] + rk[j]] = s[j];
-            __syncthreads();
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            u32x4* __restrict__ cs4 = reinterpret_cast<u32x4*>(scratch + (uint64_t)c * kMChunk);
-            const u32x4* st4 = reinterpret_cast<const u32x4*>(stage);
-            for (uint32_t v = (uint32_t)tid; 4 * v < total; v += kBlock) cs4[v] = st4[v];
-        }
-        cur = nxt;
-    }
 }
 
 // Per column of the counts (a signature, or n_sigs: live candidates), stored
@@ -1919,37 +1792,18 @@ hipError_t launch_mscan(const DStore& st, const DMScan& ms, const DMSig* d_sigs,
 
 // The hashed scan's three launches (see mscan_hash_kernel).  d_blob: the
 // DMSig array, then n_sigs u64 output word offsets, then the hmask + 1 cuckoo
-// entries (DMHashEntry, 32-B aligned); d_work (16-B aligned): chunks x chunk
-// scratch words, then (n_sigs + 1) x chunks counts, then (n_sigs + 1) x
-// (chunks + 1) bases (column-major).
-// The resident grid of mscan_hash_loop_kernel: the device's CUs x the
-// workgroups one CU holds at this LDS size (cached per kernel and size), at
-// most the chunks.
-static uint32_t mhash_loop_grid(const void* fn, size_t lds, uint32_t chunks) {
-    struct Key { const void* fn; size_t lds; int dev; uint32_t n; };
-    static thread_local Key memo[8] = {};
-    static thread_local int next = 0;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    uint32_t n = 0;
-    for (const Key& k : memo)
-        if (k.fn == fn && k.lds == lds && k.dev == dev && k.n) n = k.n;
-    if (!n) {
-        int cus = 0, per = 0;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kBlock, lds);
-        n = (uint32_t)(cus > 0 ? cus : 256) * (uint32_t)(per > 0 ? per : 1);
-        memo[next] = Key{fn, lds, dev, n};
-        next = (next + 1) & 7;
-    }
-    return n < chunks ? n : chunks;
-}
-
+// entries (DMHashEntry, 32-B aligned), then (ms.dsize > 0) the key grid —
+// dsize u16 cells (q, 0xFFFF none), padded to 16 B — and the signatures'
+// count ranges (tmin, tmax int32 pairs); d_work (16-B aligned): chunks x
+// chunk scratch words, then (n_sigs + 1) x chunks counts, then (n_sigs + 1) x
+// (chunks + 1) bases (column-major).  phases kMHashCount (contiguous chunks):
+// the scan writes counts only and the placement is the bases alone.
 size_t mscan_hash_table_off(uint32_t n_sigs) {
     return ((size_t)n_sigs * (sizeof(DMSig) + sizeof(uint64_t)) + 31) & ~(size_t)31;
 }
-size_t mscan_hash_blob_bytes(uint32_t n_sigs, uint32_t cap) {
-    return mscan_hash_table_off(n_sigs) + (size_t)cap * sizeof(DMHashEntry);
+size_t mscan_hash_blob_bytes(uint32_t n_sigs, uint32_t cap, uint32_t dsize) {
+    return mscan_hash_table_off(n_sigs) + (size_t)cap * sizeof(DMHashEntry) +
+           (dsize ? (((size_t)dsize * 2 + 15) & ~(size_t)15) + (((size_t)n_sigs * 8 + 15) & ~(size_t)15) : 0);
 }
 uint64_t mscan_hash_counts_word(const DMScan& ms) { return (uint64_t)ms.n_chunks * ms.chunk; }
 hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_blob, uint32_t* d_work,
@@ -1966,10 +1820,13 @@ hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_b
     const uint32_t mj = ms.chunk / kBlock;
     const uint64_t covered = ms.contig ? (uint64_t)(ms.src_off & ~(ms.chunk - 1)) + (uint64_t)ms.n_chunks * ms.chunk
                                        : (uint64_t)ms.n_chunks * ms.chunk;
+    uint64_t cells = 1;
+    for (uint32_t f = 0; f < ms.n_fields && f < 4; f++) cells *= ms.dsize ? (uint64_t)ms.drng[f] : 1u;
     if (ms.n_sigs > kMHashSigs || ms.hmask + 1 > kMHashCap || ((ms.hmask + 1) & ms.hmask) || ms.hmask + 1 < 2 * ms.n_sigs ||
         ms.n_fields < 1 || ms.n_fields > 4 || ms.chunk % kBlock || (ms.chunk & (ms.chunk - 1)) ||
         (ms.contig ? mj != 4 && mj != 8 : mj != 2 && mj != 4) ||
-        covered < (ms.contig ? (uint64_t)ms.src_off + ms.src_len : (uint64_t)ms.src_len))
+        covered < (ms.contig ? (uint64_t)ms.src_off + ms.src_len : (uint64_t)ms.src_len) ||
+        ms.dsize > kMHashGrid || (ms.dsize && cells != ms.dsize))
         return hipErrorInvalidValue;
     const uint64_t* dst = reinterpret_cast<const uint64_t*>(static_cast<const DMSig*>(d_blob) + ms.n_sigs);
     const DMHashEntry* htab =
@@ -1979,52 +1836,28 @@ hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_b
     uint32_t* counts = scratch + (uint64_t)ms.n_chunks * ms.chunk;
     uint32_t* bases = counts + (uint64_t)ms.n_chunks * w1;
     const dim3 grid(ms.n_chunks), egrid(c_hi - c_lo), block(kBlock);
-#define NKM_MHASH_K(NF, J, C)                                                                                         \
-    hipExtLaunchKernelGGL(mscan_hash_kernel<NF, J, C>, egrid, block, (MHashLds<J, C>{ms.hmask + 1, ms.n_sigs}.bytes()), \
+    const bool count_only = ms.contig && (phases & kMHashCount);
+    const uint32_t tb = mhash_tab_bytes(ms);
+#define NKM_MHASH_K(NF, J, C, CNT)                                                                                  \
+    hipExtLaunchKernelGGL(mscan_hash_kernel<NF, J, C, CNT>, egrid, block, (MHashLds<J, C>{tb, ms.n_sigs}.bytes()), \
                           stream, ev0, ev1, 0, st, ms, htab, scratch, counts, c_lo)
-#define NKM_MHASH(NF)                                        \
-    do {                                                     \
-        if (ms.contig && mj == 8) NKM_MHASH_K(NF, 8, true);  \
-        else if (ms.contig) NKM_MHASH_K(NF, 4, true);        \
-        else if (mj == 4) NKM_MHASH_K(NF, 4, false);         \
-        else NKM_MHASH_K(NF, 2, false);                      \
-    } while (0)
-    // the resident loop (mscan_hash_loop_kernel): contiguous chunks only
-    const bool loop = ms.contig && (phases & (kMHashLoop | kMHashCount));
-    const bool count_only = loop && (phases & kMHashCount);
-#define NKM_MHLOOP_K(NF, J, CNT)                                                                                    \
-    do {                                                                                                            \
-        const size_t lb = MHashLds<J, true>{ms.hmask + 1, ms.n_sigs}.bytes();                                        \
-        const uint32_t grid_n = mhash_loop_grid((const void*)mscan_hash_loop_kernel<NF, J, CNT>, lb, c_hi - c_lo);    \
-        hipExtLaunchKernelGGL(mscan_hash_loop_kernel<NF, J, CNT>, dim3(grid_n), block, lb, stream, ev0, ev1, 0, st, ms, \
-                              htab, scratch, counts, c_lo, c_hi);                                                   \
-    } while (0)
-#define NKM_MHLOOP(NF)                                          \
-    do {                                                        \
-        if (mj == 8 && count_only) NKM_MHLOOP_K(NF, 8, true);   \
-        else if (mj == 8) NKM_MHLOOP_K(NF, 8, false);           \
-        else if (count_only) NKM_MHLOOP_K(NF, 4, true);         \
-        else NKM_MHLOOP_K(NF, 4, false);                        \
+#define NKM_MHASH(NF)                                                         \
+    do {                                                                      \
+        if (ms.contig && mj == 8 && count_only) NKM_MHASH_K(NF, 8, true, true); \
+        else if (ms.contig && mj == 8) NKM_MHASH_K(NF, 8, true, false);       \
+        else if (ms.contig && count_only) NKM_MHASH_K(NF, 4, true, true);     \
+        else if (ms.contig) NKM_MHASH_K(NF, 4, true, false);                  \
+        else if (mj == 4) NKM_MHASH_K(NF, 4, false, false);                   \
+        else NKM_MHASH_K(NF, 2, false, false);                                \
     } while (0)
     if ((phases & kMHashEval) && c_hi > c_lo) {
-        if (loop) {
-            switch (ms.n_fields) {
-                case 1: NKM_MHLOOP(1); break;
-                case 2: NKM_MHLOOP(2); break;
-                case 3: NKM_MHLOOP(3); break;
-                default: NKM_MHLOOP(4); break;
-            }
-        } else {
-            switch (ms.n_fields) {
-                case 1: NKM_MHASH(1); break;
-                case 2: NKM_MHASH(2); break;
-                case 3: NKM_MHASH(3); break;
-                default: NKM_MHASH(4); break;
-            }
+        switch (ms.n_fields) {
+            case 1: NKM_MHASH(1); break;
+            case 2: NKM_MHASH(2); break;
+            case 3: NKM_MHASH(3); break;
+            default: NKM_MHASH(4); break;
         }
     }
-#undef NKM_MHLOOP
-#undef NKM_MHLOOP_K
 #undef NKM_MHASH
 #undef NKM_MHASH_K
 #ifdef NKM_MH_DEBUG

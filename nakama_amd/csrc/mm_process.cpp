@@ -257,7 +257,9 @@ struct Replay : ReplayCore {
             }
         } else {
             ms.hmask = 0;
+            ms.dsize = 0;
             htab.clear();
+            dgrid.clear();
         }
         ms.contig = ms.hmask && c.order_identity_ && c.mcontig_mode_ ? 1u : 0u;
         ms.chunk = (uint32_t)(ms.hmask ? mscan_hash_chunk_len(ms.contig != 0) : mscan_chunk_len(ms.n_sigs));
@@ -282,7 +284,9 @@ struct Replay : ReplayCore {
     std::vector<DMHashEntry> htab;
     bool plan_mscan_hash(DMScan& ms) {
         ms.hmask = 0;
+        ms.dsize = 0;
         htab.clear();
+        dgrid.clear();
         if (c.mhash_mode_ == 2 || ms.n_fields == 0) return false;
         const uint8_t all = (uint8_t)((1u << ms.n_fields) - 1);
         for (const DMSig& m : msig) {
@@ -332,10 +336,49 @@ struct Replay : ReplayCore {
                 ms.hmask = cap - 1;
                 ms.hseed[0] = s0;
                 ms.hseed[1] = s1;
+                plan_key_grid(ms);
                 return true;
             }
         }
         return false;
+    }
+
+    // The direct lookup (DMScan::dsize) beside the cuckoo table: when the
+    // signatures' values span at most kMHashGrid cells over all fields (pool
+    // values are dictionary ids, interned close together), a grid cell per
+    // value combination holds its signature (u16, 0xFFFF none), followed by
+    // the signatures' count ranges; the kernel reads one 2-B cell per
+    // candidate instead of two 32-B cuckoo entries.
+    std::vector<uint8_t> dgrid;
+    void plan_key_grid(DMScan& ms) {
+        ms.dsize = 0;
+        dgrid.clear();
+        if (!c.mhash_grid_mode_) return;
+        uint64_t cells = 1;
+        for (uint32_t f = 0; f < ms.n_fields; f++) {
+            int64_t lo = INT64_MAX, hi = INT64_MIN;
+            for (const DMSig& m : msig) {
+                lo = std::min(lo, m.req[f]);
+                hi = std::max(hi, m.req[f]);
+            }
+            ms.dlo[f] = (uint32_t)lo;
+            ms.drng[f] = (uint32_t)(hi - lo + 1);
+            cells *= (uint64_t)(hi - lo + 1);
+            if (cells > kMHashGrid) return;
+        }
+        const size_t gbytes = ((size_t)cells * 2 + 15) & ~(size_t)15;
+        dgrid.assign(gbytes + (((size_t)ms.n_sigs * 8 + 15) & ~(size_t)15), 0);
+        uint16_t* g = reinterpret_cast<uint16_t*>(dgrid.data());
+        for (uint64_t k = 0; k < cells; k++) g[k] = 0xFFFFu;
+        int32_t* lim = reinterpret_cast<int32_t*>(dgrid.data() + gbytes);
+        for (uint32_t q = 0; q < ms.n_sigs; q++) {
+            uint64_t idx = 0;
+            for (uint32_t f = 0; f < ms.n_fields; f++) idx = idx * ms.drng[f] + (uint64_t)(msig[q].req[f] - ms.dlo[f]);
+            g[idx] = (uint16_t)q;
+            lim[2 * q] = msig[q].tmin;
+            lim[2 * q + 1] = msig[q].tmax;
+        }
+        ms.dsize = (uint32_t)cells;
     }
 
     // The hashed scan of a row-sharded batch: this rank's block of chunks,
@@ -596,8 +639,7 @@ struct Replay : ReplayCore {
         // counts only (Core::mhash_count_mode_): every list is expected proven
         const bool count_only = skip_lists && ms.contig && c.mhash_count_mode_ && c.mhash_spec_pause_ == 0;
         if (c.mhash_spec_pause_) c.mhash_spec_pause_--;
-        const int mh_phases = kMHashEval | kMHashPlace | (count_only ? kMHashCount : 0) |
-                              (c.mhash_loop_mode_ ? kMHashLoop : 0);
+        const int mh_phases = kMHashEval | kMHashPlace | (count_only ? kMHashCount : 0);
         const bool m_precopy = use_m && !c.row_shard() && mw - mw0 <= 2 * (uint64_t)ms.src_len && !skip_lists;
         const uint32_t ncells = !use_m ? 0 : hashed ? ms.n_sigs : ms.n_sigs * ms.n_chunks;
         if (hashed) scratch += (mscan_hash_work_words(ms) + 3) / 4;
@@ -627,7 +669,7 @@ struct Replay : ReplayCore {
         }
         if (use_m) {
             // the signatures; hashed: then the output word offsets and the table
-            const size_t blob = hashed ? mscan_hash_blob_bytes(ms.n_sigs, ms.hmask + 1) : msig.size() * sizeof(DMSig);
+            const size_t blob = hashed ? mscan_hash_blob_bytes(ms.n_sigs, ms.hmask + 1, ms.dsize) : msig.size() * sizeof(DMSig);
             const size_t nblob = (blob + sizeof(DMSig) - 1) / sizeof(DMSig);
             c.h_msig_.reserve(nblob);
             char* hb = reinterpret_cast<char*>(c.h_msig_.p);
@@ -635,6 +677,9 @@ struct Replay : ReplayCore {
             if (hashed) {
                 std::memcpy(hb + msig.size() * sizeof(DMSig), mdst.data(), mdst.size() * sizeof(uint64_t));
                 std::memcpy(hb + mscan_hash_table_off(ms.n_sigs), htab.data(), htab.size() * sizeof(DMHashEntry));
+                if (ms.dsize)
+                    std::memcpy(hb + mscan_hash_table_off(ms.n_sigs) + htab.size() * sizeof(DMHashEntry), dgrid.data(),
+                                dgrid.size());
             }
             c.d_msig_.reserve(nblob, false);
             NKM_HIP(hipMemcpyAsync(c.d_msig_.p, c.h_msig_.p, blob, hipMemcpyHostToDevice, stream));
@@ -1074,8 +1119,18 @@ int Core::process_default(GroupList& out_groups,
                    (double)cfg_.interval_sec * (double)cfg_.rev_threshold);
     const int maxI = cfg_.max_intervals;
     std::vector<uint32_t>& rows = rows_;
-    filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, rows,
-                 [&](uint32_t s) { return live_[s] && is_active_[s]; });
+    if (active_exact_ && big_list(active_list_)) {  // every entry is a row: one parallel copy
+        rows.resize(active_list_.size());
+        WorkPool& wp = workers();
+        const size_t n = active_list_.size(), nch = wp.size();
+        wp.run(nch, [&](size_t c) {
+            const size_t lo = n * c / nch, hi = n * (c + 1) / nch;
+            std::memcpy(rows.data() + lo, active_list_.data() + lo, (hi - lo) * sizeof(uint32_t));
+        });
+    } else {
+        filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, rows,
+                     [&](uint32_t s) { return live_[s] && is_active_[s]; });
+    }
     stats.prologue_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
 
     if (!active_flag_) {  // paused: intervals still advance (matchmaker_process.go:53-63)
@@ -1906,8 +1961,12 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                         E.items.push_back(DEnumItem{r0, r, (uint32_t)std::min<uint64_t>(kEnumSpan, V - r0)});
                 }
             };
+            using eclk = std::chrono::steady_clock;
+            auto ems = [](eclk::time_point a, eclk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            const auto te0 = eclk::now();
             if (nch > 1) wp.run(nch, gather);
             else gather(0);
+            const auto te1 = eclk::now();
             for (uint8_t x : huge)
                 if (x) throw std::length_error("processCustom: a row's subsets exceed the enumeration limit");
             std::vector<size_t> rb(nch + 1, 0), hb(nch + 1, 0), ib(nch + 1, 0);
@@ -1951,6 +2010,7 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                                     nullptr, stream_));
                 NKM_HIP(hipMemcpyAsync(h_ecnt_.p, d_ecnt_.p, 2 * nitem * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
                 NKM_HIP(hipStreamSynchronize(stream_));
+                const auto te2 = eclk::now();
                 h_ebase_.reserve(2 * nitem);  // exclusive scan: every item's first group and entry
                 uint64_t G = 0, E = 0;
                 for (size_t k = 0; k < nitem; k++) {
@@ -1978,6 +2038,12 @@ int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
                                            hipMemcpyDeviceToHost, stream_));
                     NKM_HIP(hipStreamSynchronize(stream_));
                 }
+                if (batch_profile_)
+                    std::fprintf(stderr,
+                                 "[nkm]   custom enum: rows %zu hits %zu items %zu | gather %.2f, pack+count %.2f, "
+                                 "scan+write+copy %.2f ms | %llu candidates, %llu entries\n",
+                                 nrow, nhit, nitem, ems(te0, te1), ems(te1, te2), ems(te2, eclk::now()),
+                                 (unsigned long long)G, (unsigned long long)E);
             }
         } else if (par && !timer_live) {
             WorkPool& wp = workers();

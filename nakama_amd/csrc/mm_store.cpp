@@ -124,7 +124,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_RANGE")) range_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_LISTPROOF")) list_proof_mode_ = std::atoi(e);
     if (const char* e = std::getenv("NKM_MHCOUNT")) mhash_count_mode_ = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("NKM_MHLOOP")) mhash_loop_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_MHGRID")) mhash_grid_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_BULK")) bulk_mode_ = std::strcmp(e, "0") == 0 ? 0 : std::strcmp(e, "force") == 0 ? 2 : 1;
     if (const char* e = std::getenv("NKM_KERNEL"))
         kernel_mode_ = !std::strcmp(e, "search") ? KM_SEARCH : !std::strcmp(e, "scan") ? KM_SCAN
@@ -639,6 +639,7 @@ void Core::kill_slot(uint32_t s, bool device_cleared, bool quiet) {
     if (track_removed_ && !quiet) removed_ids_.emplace_back(tk(s));
     live_[s] = 0;
     is_active_[s] = 0;
+    active_exact_ = false;
     n_live_--;
     if (!device_cleared) pending_dead_.push_back(s);
     uint32_t p0 = pres_off_[s], p1 = pres_off_[s + 1];
@@ -1438,6 +1439,7 @@ void Core::compact() {
     for (uint32_t s : active_list_)
         if (remap[s] != kNoSlot && is_active_[remap[s]]) nact.push_back(remap[s]);
     active_list_ = std::move(nact);
+    active_exact_ = true;  // remapped slots are live
     std::vector<uint32_t> nord;
     for (size_t k = 0; k < order_.size() && !none; k++)
         if (remap[order_[k]] != kNoSlot) nord.push_back(remap[order_[k]]);

@@ -6,7 +6,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-T=${1:-r05c}
+T=${1:-r05d}
 timeout -k 10 120 tools/mhash_bench > gpurun_out/${T}_mhash_bench.txt 2>&1 || { echo MHB_FAIL; tail -20 gpurun_out/${T}_mhash_bench.txt; exit 1; }
 grep -E "cldW|lists" gpurun_out/${T}_mhash_bench.txt
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_mhb_trace -o run -- tools/mhash_bench > gpurun_out/${T}_mhb_trace.log 2>&1 || { echo TRACE_FAIL; exit 1; }

@@ -113,10 +113,22 @@ static int run_shape(uint32_t n, int nmode, int nregion, uint4* evict, size_t ev
         htab[p].tmin = sigs[slot[p]].tmin;
         htab[p].tmax = sigs[slot[p]].tmax;
     }
-    std::vector<char> blob(mscan_hash_blob_bytes(nq, cap));
+    // the key grid (mm_process.cpp plan_key_grid): modes x regions cells
+    const uint32_t cells = (uint32_t)(nmode * nregion);
+    const size_t gbytes = ((size_t)cells * 2 + 15) & ~(size_t)15;
+    std::vector<char> grid(gbytes + (((size_t)nq * 8 + 15) & ~(size_t)15), 0);
+    for (uint32_t k = 0; k < cells; k++) reinterpret_cast<uint16_t*>(grid.data())[k] = 0xFFFFu;
+    for (uint32_t q = 0; q < nq; q++) {
+        const uint32_t idx = (uint32_t)(sigs[q].req[0] - 100) * nregion + (uint32_t)(sigs[q].req[1] - 200);
+        reinterpret_cast<uint16_t*>(grid.data())[idx] = (uint16_t)q;
+        reinterpret_cast<int32_t*>(grid.data() + gbytes)[2 * q] = sigs[q].tmin;
+        reinterpret_cast<int32_t*>(grid.data() + gbytes)[2 * q + 1] = sigs[q].tmax;
+    }
+    std::vector<char> blob(mscan_hash_blob_bytes(nq, cap, cells));
     std::memcpy(blob.data(), sigs.data(), nq * sizeof(DMSig));
     std::memcpy(blob.data() + nq * sizeof(DMSig), dst.data(), nq * 8);
     std::memcpy(blob.data() + mscan_hash_table_off(nq), htab.data(), cap * sizeof(DMHashEntry));
+    std::memcpy(blob.data() + mscan_hash_table_off(nq) + cap * sizeof(DMHashEntry), grid.data(), grid.size());
     std::printf("cuckoo table: %u entries for %u signatures\n", cap, nq);
     const void* d_blob = up(blob.data(), blob.size());
     uint32_t* d_out;
@@ -132,13 +144,13 @@ static int run_shape(uint32_t n, int nmode, int nregion, uint4* evict, size_t ev
     // algorithmic bytes: per candidate its slot id (gathered only), alive flag,
     // counts and two (kind, value) columns; per hit its 4-B slot id
     auto bytes_of = [&](bool contig) { return (double)n * (contig ? 1 + 8 + 18 : 5 + 8 + 18) + (double)n * 4; };
-    // loop: 0 one chunk per workgroup (mscan_hash_kernel), 1 the resident
-    // pipelined loop (mscan_hash_loop_kernel), 2 the loop writing counts only
-    struct Shape { int contig, j, loop; };
-    const Shape shapes[] = {{0, 2, 0}, {0, 4, 0}, {1, 4, 0}, {1, 8, 0}, {1, 4, 1}, {1, 8, 1}, {1, 4, 2}, {1, 8, 2}};
+    // grid: the key-grid lookup (else the cuckoo table); loop 2: counts only
+    struct Shape { int contig, j, grid, loop; };
+    const Shape shapes[] = {{0, 4, 0, 0}, {0, 4, 1, 0}, {1, 4, 0, 0}, {1, 4, 1, 0}, {1, 8, 0, 0}, {1, 8, 1, 0},
+                            {1, 4, 1, 2}, {1, 8, 1, 2}, {1, 4, 0, 2}};
     for (const Shape& sh : shapes) {
-        for (uint32_t dbg : {0u, 1u, 2u, 3u}) {
-            if (sh.loop && dbg) continue;  // the phase switches are mscan_hash_kernel's
+        for (uint32_t dbg : {0u, 1u, 2u}) {
+            if (sh.loop && dbg) continue;
             DMScan ms{};
             ms.src_off = 0;
             ms.src_len = n;
@@ -149,6 +161,13 @@ static int run_shape(uint32_t n, int nmode, int nregion, uint4* evict, size_t ev
             ms.hmask = cap - 1;
             ms.hseed[0] = s0;
             ms.hseed[1] = s1;
+            if (sh.grid) {
+                ms.dsize = cells;
+                ms.dlo[0] = 100;
+                ms.dlo[1] = 200;
+                ms.drng[0] = (uint32_t)nmode;
+                ms.drng[1] = (uint32_t)nregion;
+            }
             ms.contig = (uint32_t)sh.contig;
             ms.chunk = (uint32_t)(sh.j * 256);
             ms.n_chunks = (n + ms.chunk - 1) / ms.chunk;
@@ -167,7 +186,7 @@ static int run_shape(uint32_t n, int nmode, int nregion, uint4* evict, size_t ev
                         CK(hipStreamSynchronize(s));
                         std::this_thread::sleep_for(std::chrono::milliseconds(5));
                     }
-                    const int ph = kMHashEval | kMHashPlace | (sh.loop == 1 ? kMHashLoop : sh.loop == 2 ? kMHashCount : 0);
+                    const int ph = kMHashEval | kMHashPlace | (sh.loop == 2 ? kMHashCount : 0);
                     CK(launch_mscan_hash(st, ms, d_blob, d_work, d_res, d_out, s, e0, e1, ph, 0, UINT32_MAX));
                     CK(hipEventRecord(e2, s));
                     CK(hipEventSynchronize(e2));
@@ -179,8 +198,8 @@ static int run_shape(uint32_t n, int nmode, int nregion, uint4* evict, size_t ev
                 std::sort(t.begin(), t.end());
                 std::sort(tall.begin(), tall.end());
                 const double us = 1e3 * t[t.size() / 2];
-                std::printf("n %u sigs %3u %s J%d %s dbg %u %-4s hash kernel %7.2f us (frac %.3f)  all %7.2f us\n", n, nq,
-                            sh.contig ? "contig" : "gather", sh.j, sh.loop == 2 ? "loopcnt" : sh.loop ? "loop   " : "chunk  ",
+                std::printf("n %u sigs %3u %s J%d %s %s dbg %u %-4s hash kernel %7.2f us (frac %.3f)  all %7.2f us\n", n, nq,
+                            sh.contig ? "contig" : "gather", sh.j, sh.grid ? "grid  " : "cuckoo", sh.loop == 2 ? "count" : "lists",
                             dbg, cold == 2 ? "cldW" : cold ? "cldR" : "warm", us,
                             (sh.loop == 2 ? bytes_of(sh.contig) - (double)n * 4 : bytes_of(sh.contig)) / us / 1e3 / 8000.0, 1e3 * tall[tall.size() / 2]);
             }
