@@ -94,8 +94,11 @@ def parse():
     a = ap.parse_args()
     if a.tickets is None:
         a.tickets = DEFAULT_TICKETS.get(a.config, 1_000_000)
-    if a.traffic is None:
-        a.traffic = os.path.join(ROOT, "profiles", f"r04_c{a.config}_traffic.json")
+    if a.traffic is None:  # the newest committed PMC pass of this config (bench.py matches kernel + tickets)
+        for r in ("r05", "r04"):
+            a.traffic = os.path.join(ROOT, "profiles", f"{r}_c{a.config}_traffic.json")
+            if os.path.exists(a.traffic):
+                break
     return a
 
 
