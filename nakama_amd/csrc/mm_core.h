@@ -697,7 +697,22 @@ private:
         std::vector<uint32_t> pool_rows;    // ascending per pool
         std::vector<uint8_t> self_rows;     // per pool: every row carries its own search's terms
         std::vector<uint32_t> pool_key1;    // one key field: each pool's term
+        bool runs = false;                  // every pool is one run of the batch, pools in row order
     };
+    // replay_runs: one task's output (its rows' groups in row order)
+    struct alignas(128) RunOut {
+        std::vector<uint32_t> gend;  // per group: the end of its entries in `ents`
+        std::vector<uint32_t> gT;    // per group: its searching ticket
+        std::vector<std::pair<uint32_t, int>> ents;
+        std::vector<uint32_t> expired;
+        uint64_t hits = 0, pairs = 0;
+        double ms = 0.0;
+    };
+    std::vector<RunOut> run_outs_;
+    bool replay_runs(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
+                     const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel, GroupList& out_groups,
+                     std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
+                     uint32_t* min_stop, const std::function<BGroup&(uint32_t)>* view);
     struct RowRec {  // a batch row's outcome in a parallel replay (indexed by batch row)
         uint32_t ent, len, task;  // its group's entries: task_ents_[task][ent, ent + len)
         uint8_t matched, expired, processed, pad;
@@ -1036,6 +1051,7 @@ public:
     bool dense_mode_ = true;
     bool pipe_mode_ = true;  // NKM_PIPE=0: the pool walks' merge runs after all walks, not beside them
     bool gpipe_mode_ = true; // NKM_GPIPE=0: no identity-pool shortcut (slot -> position map, copies gathered before the walks)
+    bool runs_mode_ = true;  // NKM_RUNS=0: pools in contiguous runs take the per-row records + merge_rows
     int32_t max_pres_ = 1;   // most presences of any ticket inserted (an entry bound of the pipelined merge)
     // NKM_FAST=0: every row takes the exact loop body, also when no two live
     // tickets share a session (the fast walk, replay_core.h) (A/B, tests)

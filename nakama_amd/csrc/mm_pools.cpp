@@ -47,6 +47,7 @@ bool Core::plan_fused(const std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
     const auto t0 = clk::now();
     const size_t G = bg.size();
     P.ok = false;
+    P.runs = false;
     std::vector<uint16_t> keyf;
     for (auto& mt : sigs_[bg[0].sig].must_terms)
         if (std::find(keyf.begin(), keyf.end(), mt.first) == keyf.end()) keyf.push_back(mt.first);
@@ -104,6 +105,7 @@ template <class SigOf, class GroupOf, class RowOf>
 bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_of, const UVec<uint32_t>& brow,
                       ParPlan& P, PassStats& stats) {
     P.ok = false;
+    P.runs = false;
     if (nsearch < 2) return false;
     using clk = std::chrono::steady_clock;
     auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -319,6 +321,7 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
                 std::fprintf(stderr, "[nkm]   plan_pools: %zu pools (contiguous runs) | keys %.2f runs %.2f ms\n", ng,
                              msd(tp0, tq0), msd(tq0, clk::now()));
             P.ok = true;
+            P.runs = true;
             return true;
         }
     }
@@ -461,6 +464,8 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     if (!view)
         for (const BGroup& g : bg) all_complete = all_complete && g.complete;
     if (!all_complete && !partial_mode_) return false;
+    if (P.runs && runs_mode_ && P.ng > 64 && !(dense_mode_ && !rev && !view))
+        return replay_runs(P, bg, brow, brow_group, sel, out_groups, expired, newly, stats, rev, min_stop, view);
     using clk = std::chrono::steady_clock;
     auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     const auto tp1 = clk::now();
@@ -886,6 +891,149 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         std::fprintf(stderr, "[nkm]   pool walks: %zu tasks, %zu pools on %u workers | sum: tasks %.2f, walks %.2f (max %.2f), "
                      "gather+reset+reserve %.2f ms | gather %s\n", ntask, ng, wp.size(), st, sw, mw, sp,
                      gpipe ? "beside" : "before");
+    }
+    stats.par_rows += nb;
+    return true;
+}
+
+// Pools in contiguous runs of the batch (ParPlan::runs — C5's buckets: a
+// bucket's tickets arrive together), none dense: a task takes consecutive
+// pools, i.e. one range of batch rows, so the tasks' outputs in task order
+// are the row order and no per-row record or merge_rows pass is needed.
+// Pools share no ticket (replay_parallel's premise), so every ticket a task
+// reads or writes — its rows, their hits — is its own: the workers update
+// the pass state directly (Intervals, decided, selected) instead of through
+// thread-local masks and a merge, and each row's Intervals increment is
+// visible to the pool's later rows exactly as the sequential pass sees it.
+// The outputs are then placed at their offsets in one parallel copy (plus
+// the result arena's entries when this pass owns it, as the pipelined merge).
+bool Core::replay_runs(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
+                       const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel, GroupList& out_groups,
+                       std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
+                       uint32_t* min_stop, const std::function<BGroup&(uint32_t)>* view) {
+    using clk = std::chrono::steady_clock;
+    auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto tp1 = clk::now();
+    WorkPool& wp = workers();
+    const size_t ng = P.ng, nb = brow.size();
+    const int maxI = cfg_.max_intervals;
+    if (!view) fill_row_lists(bg, brow, brow_group);
+    const size_t per_task = std::max<size_t>(1, nb / ((size_t)wp.size() * 8));
+    std::vector<uint32_t> task_off{0};  // pools [task_off[t], task_off[t+1])
+    for (size_t p = 0, acc = 0; p < ng; p++) {
+        acc += P.pool_off[p + 1] - P.pool_off[p];
+        if (acc >= per_task || p + 1 == ng) {
+            task_off.push_back((uint32_t)(p + 1));
+            acc = 0;
+        }
+    }
+    const size_t ntask = task_off.size() - 1;
+    if (run_outs_.size() < ntask) run_outs_.resize(ntask);
+    std::vector<uint32_t> task_stop(ntask, UINT32_MAX);
+    int32_t* iv = intervals_.data();
+    uint8_t* dec = dec_.data();
+    auto worker = [&](size_t t) {
+        const auto tw0 = clk::now();
+        RunOut& o = run_outs_[t];
+        o.gend.clear();
+        o.gT.clear();
+        o.ents.clear();
+        o.expired.clear();
+        PassStats ls;
+        const std::unique_ptr<ReplayCore> rpp = make_replay(sel, rev, maxI, ls);
+        ReplayCore& rp = *rpp;
+        rp.proc = nullptr;  // increments are written as the rows go
+        static thread_local std::vector<std::pair<uint32_t, int>> grp;
+        for (uint32_t p = task_off[t]; p < task_off[t + 1]; p++) {
+            for (uint32_t bi = P.pool_off[p]; bi < P.pool_off[p + 1]; bi++) {
+                const uint32_t T = brow[bi];
+                if (sel[T]) continue;
+                BGroup& g = view ? (*view)(bi) : bg[brow_group[bi]];
+                const auto status = rp.decide(T, g, false, grp);
+                if (status == ReplayCore::EXHAUSTED) {  // the pool stops here; its search re-runs next batch
+                    task_stop[t] = std::min(task_stop[t], bi);
+                    break;
+                }
+                if (iv[T] + 1 >= maxI || minc_[T] == maxc_[T]) o.expired.push_back(T);
+                iv[T]++;
+                dec[T] = 1;
+                if (status != ReplayCore::MATCHED) continue;
+                for (const auto& e : grp) {
+                    sel[e.first] = 1;
+                    o.ents.push_back(e);
+                }
+                o.gend.push_back((uint32_t)o.ents.size());
+                o.gT.push_back(T);
+            }
+        }
+        o.hits = rp.hits_seen;
+        o.pairs = rp.pairs;
+        o.ms = msd(tw0, clk::now());
+    };
+    wp.run(ntask, worker);
+    const auto tp2 = clk::now();
+    // offsets: the tasks in order
+    struct Cnt { size_t g = 0, e = 0, x = 0; };
+    std::vector<Cnt> at(ntask + 1);
+    for (size_t t = 0; t < ntask; t++) {
+        const RunOut& o = run_outs_[t];
+        at[t + 1] = {at[t].g + o.gend.size(), at[t].e + o.ents.size(), at[t].x + o.expired.size()};
+    }
+    const size_t g0 = out_groups.size(), e0 = out_groups.ents.size(), x0 = expired.size(), n0 = newly.size();
+    const size_t G = at[ntask].g, E = at[ntask].e, X = at[ntask].x;
+    grow_to(out_groups.off, g0 + 1 + G);
+    grow_to(out_groups.ents, e0 + E);
+    grow_to(expired, x0 + X);
+    grow_to(newly, n0 + E);
+    const bool fill = filled_groups_ == g0 && (arena_claimed_ || !out_in_use_.exchange(true));
+    if (fill) {
+        arena_claimed_ = true;
+        if (out_offs_.size() < g0 + 1 + G) grow_to(out_offs_, g0 + 1 + G);
+        if (out_ents_.size() < e0 + E) grow_to(out_ents_, e0 + E);
+        if (out_created_.size() < g0 + G) grow_to(out_created_, g0 + G);
+        out_offs_[0] = 0;
+    }
+    wp.run(ntask, [&](size_t t) {
+        const RunOut& o = run_outs_[t];
+        const size_t gk = g0 + at[t].g, ek = e0 + at[t].e;
+        for (size_t k = 0; k < o.gend.size(); k++) {
+            out_groups.off[gk + 1 + k] = (uint32_t)(ek + o.gend[k]);
+            if (fill) {
+                out_offs_[gk + 1 + k] = (int32_t)(ek + o.gend[k]);
+                out_created_[gk + k] = created_[o.gT[k]];
+            }
+        }
+        for (size_t k = 0; k < o.ents.size(); k++) {
+            const auto& e = o.ents[k];
+            out_groups.ents[ek + k] = e;
+            newly[n0 + (ek - e0) + k] = e.first;
+            if (fill) out_ents_[ek + k] = mm_entry_ref{tk_ptr_[e.first], e.second, 0};
+        }
+        std::copy(o.expired.begin(), o.expired.end(), expired.begin() + (ptrdiff_t)(x0 + at[t].x));
+    });
+    out_groups.off.resize(g0 + 1 + G);
+    out_groups.ents.resize(e0 + E);
+    expired.resize(x0 + X);
+    newly.resize(n0 + E);
+    if (fill) filled_groups_ = g0 + G;
+    const auto tp3 = clk::now();
+    *min_stop = UINT32_MAX;
+    for (uint32_t s : task_stop) *min_stop = std::min(*min_stop, s);
+    stats.par_job_ms += msd(tp1, tp2);
+    stats.par_work_ms += msd(tp1, tp2);
+    stats.par_merge_ms += msd(tp2, tp3);
+    for (size_t t = 0; t < ntask; t++) {
+        const RunOut& o = run_outs_[t];
+        stats.par_task_max_ms = std::max(stats.par_task_max_ms, o.ms);
+        stats.par_hits += o.hits;
+        if (!row_shard() || shard_rank_ == 0) stats.pairs_decided += (int64_t)o.pairs;
+    }
+    if (batch_profile_) {
+        double sum = 0;
+        for (size_t t = 0; t < ntask; t++) sum += run_outs_[t].ms;
+        std::fprintf(stderr, "[nkm]   pool runs: %zu tasks, %zu pools on %u workers | tasks sum %.2f ms (mean %.3f) | "
+                     "job %.2f copy %.2f ms\n", ntask, ng, wp.size(), sum, sum / (double)ntask, msd(tp1, tp2),
+                     msd(tp2, tp3));
     }
     stats.par_rows += nb;
     return true;

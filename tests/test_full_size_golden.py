@@ -108,6 +108,16 @@ def test_full_size_c4_lists_proof_checked(monkeypatch):
     _check("c4")
 
 
+@pytest.mark.parametrize("env", [{"NKM_RUNS": "0"}, {"NKM_RPACK": "0"}], ids=["row-records", "per-row-lists"])
+def test_full_size_c5_host_paths(env, monkeypatch):
+    """C5 at 1M with per-row records + merge_rows instead of the run-ordered
+    task outputs (NKM_RUNS=0), and with rsmall_kernel's per-row lists instead
+    of packed rows (NKM_RPACK=0)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    _check("c5")
+
+
 POOL_FIELDS = {2: ["properties.region"], 3: ["properties.mode", "properties.region"],
                4: ["properties.mode", "properties.region"], 5: ["properties.bucket"]}
 

@@ -560,6 +560,25 @@ def test_packed_rev_precision(config, n, passes, stride, rpack, par, monkeypatch
     assert (out[0].eval_kernel == 5) == packed, out[0].eval_kernel
 
 
+@pytest.mark.parametrize("config,n,passes,rpack", [(5, 800, 2, "1"), (5, 800, 2, "0"), (13, 1800, 3, "1"),
+                                                   (14, 3000, 2, "1"), (11, 6400, 2, "1")])
+@pytest.mark.parametrize("runs", ["1", "0"])
+def test_pool_runs_replay(config, n, passes, rpack, runs, monkeypatch, capfd):
+    """Pools that are contiguous runs of the batch (buckets whose tickets
+    arrive together, > 64 pools): NKM_RUNS=1 replays each task's row range
+    straight into the pass state and copies the tasks' outputs in order
+    (replay_runs); 0 keeps per-row records and merge_rows.  Packed and
+    per-row (NKM_RPACK=0) RevPrecision lists, against the oracle."""
+    monkeypatch.setenv("NKM_PARALLEL", "force")
+    monkeypatch.setenv("NKM_RPACK", rpack)
+    monkeypatch.setenv("NKM_RUNS", runs)
+    monkeypatch.setenv("NKM_PROFILE", "2")
+    # RevThreshold 0: no timer (an armed one keeps RevPrecision batches serial)
+    out = run_passes(config, n, passes, dict(max_intervals=passes, rev_precision=True, rev_threshold=0))
+    assert len(out[0].groups) > 0
+    assert ("pool runs:" in capfd.readouterr().err) == (runs == "1")
+
+
 def first_disjoint(cands):
     """The deterministic override of SURVEY.md 8(d) C5: keep candidates, in
     order, that do not overlap an already kept one."""
