@@ -246,6 +246,17 @@ public:
             std::lock_guard<std::mutex> lk(m_);
             job_.reset();
         }
+        // Workers that went to sleep during a long, uneven job (C3's walks
+        // leave most of them idle for milliseconds) are woken now to spin for
+        // the next job: a pass's next job then starts without a futex wake-up
+        // per worker on its critical path (NKM_PREWAKE=0: off).
+        if (prewake_ && sleepers_.load(std::memory_order_acquire) > 0) {
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                wake_.fetch_add(1, std::memory_order_release);
+            }
+            cv_.notify_all();
+        }
         // a task's exception, rethrown on the caller once every task is done
         // (no worker is still inside fn, whose captures may be on this stack)
         if (job->failed.load(std::memory_order_acquire)) std::rethrow_exception(job->err);
@@ -299,11 +310,13 @@ private:
             {
                 std::unique_lock<std::mutex> lk(m_);
                 if (!quit_ && gen_.load() == seen) {
+                    const uint64_t w = wake_.load();
                     sleepers_.fetch_add(1);
-                    cv_.wait(lk, [&] { return quit_ || gen_.load() != seen; });
+                    cv_.wait(lk, [&] { return quit_ || gen_.load() != seen || wake_.load() != w; });
                     sleepers_.fetch_sub(1);
                 }
                 if (quit_) return;
+                if (gen_.load() == seen) continue;  // woken ahead of a job: spin for it
                 seen = gen_.load();
                 j = job_;
             }
@@ -316,6 +329,8 @@ private:
     std::shared_ptr<Job> job_;
     std::atomic<uint64_t> gen_{0};
     std::atomic<int> sleepers_{0};
+    std::atomic<uint64_t> wake_{0};
+    const bool prewake_ = !(std::getenv("NKM_PREWAKE") && std::getenv("NKM_PREWAKE")[0] == '0');
     bool quit_ = false;
 };
 
@@ -1051,6 +1066,7 @@ public:
     bool dense_mode_ = true;
     bool pipe_mode_ = true;  // NKM_PIPE=0: the pool walks' merge runs after all walks, not beside them
     bool gpipe_mode_ = true; // NKM_GPIPE=0: no identity-pool shortcut (slot -> position map, copies gathered before the walks)
+    int merge_mult_ = 8;     // NKM_MCH: pipelined merge chunks per worker (the last one is the tail after the slowest walk)
     bool runs_mode_ = true;  // NKM_RUNS=0: pools in contiguous runs take the per-row records + merge_rows
     int32_t max_pres_ = 1;   // most presences of any ticket inserted (an entry bound of the pipelined merge)
     // NKM_FAST=0: every row takes the exact loop body, also when no two live

@@ -554,8 +554,11 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     // end (tasks are claimed in index order, so every walk is running before
     // any merge waits).  C3's 8 walks would otherwise leave 8 of 16 workers
     // idle while the merge waits for the slowest walk.
-    const size_t nch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
-    const bool pipe = few && pipe_mode_ && !dense_ids.empty() && dense_ids.size() == ng && nch > 1;
+    const size_t nch0 = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
+    const bool pipe = few && pipe_mode_ && !dense_ids.empty() && dense_ids.size() == ng && nch0 > 1;
+    // the pipelined merge's chunks: the last one waits for the slowest walk,
+    // so its size is the merge's tail (NKM_MCH: chunks per worker)
+    const size_t nch = pipe ? (size_t)wp.size() * (size_t)merge_mult_ : nch0;
     // Identity pools: when every pool's rows are its list in list order
     // (C3 / C4: every member of a pool of fresh tickets searches, and batch
     // order is scan order) row j's ticket is list position j — no slot ->
@@ -732,6 +735,8 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         }
     };
     std::vector<double> task_ms(ntask, 0.0), walk_prep_ms(ntask, 0.0), walk_ms(ntask, 0.0);  // NKM_PROFILE=2 split
+    std::vector<double> walk_end_ms(ntask, 0.0);  // since the job's start
+    clk::time_point tjob0 = clk::now();
     std::vector<uint64_t> task_hits(ntask, 0), task_pairs(ntask, 0);
     std::vector<uint32_t> pool_stop(ng, UINT32_MAX);  // per pool: the batch row its list ran out at
     auto to_rows = [&](const PoolOut& o, uint32_t task, std::vector<std::pair<uint32_t, int>>& ents) {
@@ -778,8 +783,10 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                 prog[gi].ents = run.ents.data();
                 const auto tr1 = clk::now();
                 run.walk_published(D, rv, maxI, pos_of_.data(), &prog[gi].st);
+                const auto tr2 = clk::now();
                 walk_prep_ms[t] += msd(tr0, tr1);
-                walk_ms[t] += msd(tr1, clk::now());
+                walk_ms[t] += msd(tr1, tr2);
+                walk_end_ms[t] = msd(tjob0, tr2);
                 if (run.ents.data() != prog[gi].ents || run.recs.data() != prog[gi].recs)
                     std::abort();  // the bound above was wrong: readers hold the old buffers
                 hits += run.hits_seen;
@@ -830,6 +837,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         task_ms[t] = msd(tw0, clk::now());
     };
     const auto tg1 = clk::now();
+    tjob0 = tg1;
     stats.par_gather_ms += msd(tg0, tg1);
     if (pipe) {
         const size_t ngt = gpipe ? ntask_g : 0;
@@ -881,16 +889,17 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         if (!row_shard() || shard_rank_ == 0) stats.pairs_decided += (int64_t)task_pairs[k];
     }
     if (batch_profile_ && pipe) {
-        double sp = 0, sw = 0, st = 0, mw = 0;
+        double sp = 0, sw = 0, st = 0, mw = 0, we = 0;
         for (size_t k = 0; k < ntask; k++) {
             sp += walk_prep_ms[k];
             sw += walk_ms[k];
             st += task_ms[k];
             mw = std::max(mw, walk_ms[k]);
+            we = std::max(we, walk_end_ms[k]);
         }
         std::fprintf(stderr, "[nkm]   pool walks: %zu tasks, %zu pools on %u workers | sum: tasks %.2f, walks %.2f (max %.2f), "
-                     "gather+reset+reserve %.2f ms | gather %s\n", ntask, ng, wp.size(), st, sw, mw, sp,
-                     gpipe ? "beside" : "before");
+                     "gather+reset+reserve %.2f ms | gather %s | last walk ends %.2f, job %.2f ms (%zu merge chunks)\n",
+                     ntask, ng, wp.size(), st, sw, mw, sp, gpipe ? "beside" : "before", we, msd(tg1, tg2), nch);
     }
     stats.par_rows += nb;
     return true;
