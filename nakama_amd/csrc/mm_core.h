@@ -692,16 +692,16 @@ private:
     DStore dstore() const;
 
     // ---- pass ----
-    int process_default(GroupList& groups, std::vector<uint32_t>& expired,
+    int process_default(GroupList& groups, UVec<uint32_t>& expired,
                         PassStats& st);
-    int process_custom(GroupList& cands, std::vector<uint32_t>& expired,
+    int process_custom(GroupList& cands, UVec<uint32_t>& expired,
                        PassStats& st);
-    void finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, bool disjoint);
+    void finish_pass(const UVec<uint32_t>& expired, GroupList& groups, bool disjoint);
     // selected: the groups' tickets were deleted from the search index during
     // the pass (processDefault), so members of a dropped group leave it
     void finish_pass_serial(GroupList& groups, bool selected);
     void fill_matched(const GroupList& groups, mm_matched* out, bool cands);
-    bool finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& groups, mm_matched* out, bool mutated);
+    bool finish_fill_fast(const UVec<uint32_t>& expired, GroupList& groups, mm_matched* out, bool mutated);
     void choose_source(const Sig& s, DGroup& g, SrcChoice* ch = nullptr);
     void source_of(const Sig& s, DGroup& g, SrcChoice* ch = nullptr) const;
     struct ParPlan {  // a batch's pools (plan_parallel), bucketed while its searches run
@@ -719,14 +719,14 @@ private:
         std::vector<uint32_t> gend;  // per group: the end of its entries in `ents`
         std::vector<uint32_t> gT;    // per group: its searching ticket
         std::vector<std::pair<uint32_t, int>> ents;
-        std::vector<uint32_t> expired;
+        UVec<uint32_t> expired;
         uint64_t hits = 0, pairs = 0;
         double ms = 0.0;
     };
     std::vector<RunOut> run_outs_;
     bool replay_runs(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                      const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel, GroupList& out_groups,
-                     std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
+                     UVec<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
                      uint32_t* min_stop, const std::function<BGroup&(uint32_t)>* view);
     struct RowRec {  // a batch row's outcome in a parallel replay (indexed by batch row)
         uint32_t ent, len, task;  // its group's entries: task_ents_[task][ent, ent + len)
@@ -753,7 +753,7 @@ private:
     bool replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                          const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                          GroupList& out_groups,
-                         std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats,
+                         UVec<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats,
                          bool rev, uint32_t* min_stop, const std::function<BGroup&(uint32_t)>* view = nullptr);
     // ---- proven mscan lists ----
     // A hashed-scan list (term-only pool signature) always holds every batch
@@ -805,7 +805,7 @@ private:
     // the min-tree walk.  false: the rows do not qualify (nothing changed).
     bool range_mode_ = true;  // NKM_RANGE=0: such batches take the hit-list path
     bool range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList& out_groups,
-                     std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats);
+                     UVec<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats);
     struct RangePoolHost {  // one pool of a range batch (kept across passes: capacity reused)
         uint32_t term = 0;
         uint16_t field = 0;
@@ -892,16 +892,16 @@ public:
     UVec<uint32_t> brow_, brow_group_;  // the batch's rows and their searches (filled in full)
     UVec<uint32_t> newly_;  // slots selected by the batch (filled in full by the merges)
     GroupList pass_groups_;
-    std::vector<uint32_t> expired_;
+    UVec<uint32_t> expired_;
     std::vector<BGroup> bg_;              // a pass's batch searches (kept: capacity reused)
     std::vector<DGroup> lg_;              // their device descriptors (Replay::lg)
     std::vector<uint32_t> lg_group_;
     std::vector<DensePool> dense_pools_;  // dense replay per pool (kept: capacity reused)
     std::vector<PoolOut> pool_outs_;      // few-pool replays: each pool's records
     void merge_pools(size_t ng, size_t nch, const UVec<uint32_t>& brow, std::vector<uint8_t>& sel,
-                     GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly);
+                     GroupList& out_groups, UVec<uint32_t>& expired, UVec<uint32_t>& newly);
     void merge_rows(size_t nb, size_t nch, const UVec<uint32_t>& brow, std::vector<uint8_t>& sel,
-                    GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly);
+                    GroupList& out_groups, UVec<uint32_t>& expired, UVec<uint32_t>& newly);
     std::vector<uint32_t> pos_of_;        // slot -> list position during a dense replay, else kNoSlot
     Dict field_dict_;                 // field names -> field id
     std::vector<const char*> tk_ptr_;  // per slot: NUL-terminated ticket id in tk_arena_
@@ -1066,8 +1066,10 @@ public:
     bool dense_mode_ = true;
     bool pipe_mode_ = true;  // NKM_PIPE=0: the pool walks' merge runs after all walks, not beside them
     bool gpipe_mode_ = true; // NKM_GPIPE=0: no identity-pool shortcut (slot -> position map, copies gathered before the walks)
+    int mwait_us_ = 0;       // NKM_MWAIT: a pipelined merge chunk's sleep while the walks have not passed it (0: yield)
     int merge_mult_ = 8;     // NKM_MCH: pipelined merge chunks per worker (the last one is the tail after the slowest walk)
-    bool runs_mode_ = true;  // NKM_RUNS=0: pools in contiguous runs take the per-row records + merge_rows
+    bool runs_mode_ = true;
+    bool rleaf_mode_ = false;  // NKM_RLEAF=1: range pools' leaves gathered across the workers, not by each walker  // NKM_RUNS=0: pools in contiguous runs take the per-row records + merge_rows
     int32_t max_pres_ = 1;   // most presences of any ticket inserted (an entry bound of the pipelined merge)
     // NKM_FAST=0: every row takes the exact loop body, also when no two live
     // tickets share a session (the fast walk, replay_core.h) (A/B, tests)
@@ -1081,7 +1083,7 @@ public:
     // NKM_MHASH: 0 (default) the hashed mscan past 16 signatures or when the
     // scan is contiguous, 1 whenever the signatures allow it, 2 never
     int mhash_mode_ = 0;
-    std::vector<uint32_t> custom_expired_;
+    UVec<uint32_t> custom_expired_;
 
     std::vector<std::string> debug_strings_;
     // reusable output arena of mm_process (pages stay mapped across passes)

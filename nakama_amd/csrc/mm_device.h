@@ -193,13 +193,15 @@ struct DSmallRow {
 static_assert(sizeof(DSmallRow) == 12, "DSmallRow is 12 bytes");
 
 // rpack_kernel's output for n rows of stride S (8, 16, 32 or 64 entries), one
-// buffer with 256-B aligned sections: per row S slot ids (u32), min(S, 32)
+// buffer with 256-B aligned sections: per row its S entries' source positions
+// (u8: entry k is source entry pos[k], the host maps it to the slot through
+// its mirror of the posting / order list — a quarter of the D2H of slot ids), min(S, 32)
 // pair-matrix words of S bits (u8 / u16 / u32), S reverse-check bits in
 // entry order (u8 / u16 / u32 / u64) and the entry count (u8); then per
 // workgroup its live candidates and its entries (2 x u32: the roofline's bytes).
 constexpr int kPackRowsPerBlock(int S) { return 4 * (64 / S); }
 struct PackLayout {
-    uint64_t slot, pm, rev, cnt, live, total;
+    uint64_t pos, pm, rev, cnt, live, total;
     uint32_t blocks;
     int S, pm_w, rev_w;
 };
@@ -210,8 +212,8 @@ NKM_HD inline PackLayout pack_layout(uint64_t n, int S) {
     L.pm_w = S <= 8 ? 1 : S <= 16 ? 2 : 4;
     L.rev_w = S / 8;
     L.blocks = (uint32_t)((n + kPackRowsPerBlock(S) - 1) / kPackRowsPerBlock(S));
-    L.slot = 0;
-    L.pm = al(L.slot + n * S * 4);
+    L.pos = 0;
+    L.pm = al(L.pos + n * S);
     L.rev = al(L.pm + n * (S < 32 ? S : 32) * L.pm_w);
     L.cnt = al(L.rev + n * L.rev_w);
     L.live = al(L.cnt + n);

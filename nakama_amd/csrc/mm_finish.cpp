@@ -22,7 +22,7 @@ namespace nkm {
 // two groups (the default pass's selection guarantees it; an override's
 // groups may overlap and then follow the reference's sequential order, where
 // a group meeting an already-retired ticket is dropped).
-void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, bool disjoint) {
+void Core::finish_pass(const UVec<uint32_t>& expired, GroupList& groups, bool disjoint) {
     using fclk = std::chrono::steady_clock;
     const auto f0 = fclk::now();
     auto f_ms = [](fclk::time_point a, fclk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -106,7 +106,7 @@ void Core::finish_pass(const std::vector<uint32_t>& expired, GroupList& groups, 
 // (groups are disjoint, so the sweeps see the state the serial loop would).
 // Returns false, having changed nothing but the expired tickets' active flags
 // (finish_pass sets them again), when a condition fails.
-bool Core::finish_fill_fast(const std::vector<uint32_t>& expired, GroupList& groups, mm_matched* out, bool mutated) {
+bool Core::finish_fill_fast(const UVec<uint32_t>& expired, GroupList& groups, mm_matched* out, bool mutated) {
     const size_t ng = groups.size(), ne = groups.ents.size();
     if (!par_mode_ || ng < par_min(16384) || !sess_slots_.more.empty() || !party_slots_.more.empty()) return false;
     if (!arena_claimed_ && out_in_use_.exchange(true)) return false;  // a second outstanding result: fill_matched copies

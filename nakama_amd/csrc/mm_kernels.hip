@@ -1617,10 +1617,10 @@ __global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRo
             }
         }
     }
-    uint32_t* __restrict__ o_slot = reinterpret_cast<uint32_t*>(obuf + L.slot);
+    uint8_t* __restrict__ o_pos = obuf + L.pos;
     PmT* __restrict__ o_pm = reinterpret_cast<PmT*>(obuf + L.pm);
     RvT* __restrict__ o_rev = reinterpret_cast<RvT*>(obuf + L.rev);
-    if (m) o_slot[(uint64_t)r * S + rank] = s;
+    if (m) o_pos[(uint64_t)r * S + rank] = (uint8_t)j;  // the entry's source position
     if (m && rank < (uint32_t)P) o_pm[(uint64_t)r * P + rank] = pmask;
     if (have && j == 0) {
         o_rev[r] = rbits;

@@ -187,17 +187,21 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
         std::vector<uint8_t> bad(nsch, 0);
         const size_t nd = dict_.size();
         // first[t]: the lowest search index with term t (atomic min over the
-        // chunks); the heads (first[t] == i) are numbered in index order
+        // chunks); the heads (first[t] == i) are numbered in index order.
+        // Every entry is UINT32_MAX between calls: the heads reset their own
+        // on the way out, so a pass costs O(searches), not O(dictionary) (the
+        // dictionary only grows: C5's bench adds 125k bucket terms a step)
         if (pool_first_cap_ < nd) {
             pool_first_.reset(new std::atomic<uint32_t>[nd + nd / 4]);
             pool_first_cap_ = nd + nd / 4;
+            std::atomic<uint32_t>* f = pool_first_.get();
+            sweep(pool_first_cap_, nsch, [&](size_t, size_t lo, size_t hi) {
+                for (size_t t = lo; t < hi; t++) f[t].store(UINT32_MAX, std::memory_order_relaxed);
+            });
         }
         std::atomic<uint32_t>* first = pool_first_.get();
         std::vector<uint32_t>& tpool = pool_remap_;  // term -> pool (written by its head only)
         grow_to(tpool, nd);
-        sweep(nd, nsch, [&](size_t, size_t lo, size_t hi) {
-            for (size_t t = lo; t < hi; t++) first[t].store(UINT32_MAX, std::memory_order_relaxed);
-        });
         std::vector<size_t> heads(nsch + 1, 0);
         const uint16_t f0 = keyf[0];
         sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
@@ -216,8 +220,12 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
                 }
             }
         });
-        for (uint8_t b : bad)
-            if (b) return false;
+        if (std::any_of(bad.begin(), bad.end(), [](uint8_t b) { return b != 0; })) {
+            sweep(pool_first_cap_, nsch, [&](size_t, size_t lo, size_t hi) {  // back to all-empty
+                for (size_t t = lo; t < hi; t++) first[t].store(UINT32_MAX, std::memory_order_relaxed);
+            });
+            return false;
+        }
         sweep(nsearch, nsch, [&](size_t ch, size_t lo, size_t hi) {
             size_t h = 0;
             for (size_t i = lo; i < hi; i++) h += first[k1[i]].load(std::memory_order_relaxed) == (uint32_t)i;
@@ -235,7 +243,12 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
                 }
         });
         sweep(nsearch, nsch, [&](size_t, size_t lo, size_t hi) {
-            for (size_t i = lo; i < hi; i++) k1[i] = tpool[k1[i]];
+            for (size_t i = lo; i < hi; i++) {
+                const uint32_t t = k1[i];
+                k1[i] = tpool[t];
+                if (first[t].load(std::memory_order_relaxed) == (uint32_t)i)  // the head clears its term's entry
+                    first[t].store(UINT32_MAX, std::memory_order_relaxed);
+            }
         });
     } else {
         pool_key1.clear();
@@ -450,7 +463,7 @@ void Core::check_row_lists(const std::vector<BGroup>& bg, const UVec<uint32_t>& 
 bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                            const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel,
                            GroupList& out_groups,
-                           std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
+                           UVec<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
                            uint32_t* min_stop, const std::function<BGroup&(uint32_t)>* view) {
     *min_stop = UINT32_MAX;
     if (!P.ok) return false;
@@ -686,7 +699,13 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             const uint32_t need = (uint32_t)(std::lower_bound(D.bis, D.bis + D.nrows, hi) - D.bis);
             if (!need) continue;
             uint64_t v;
-            while (((v = prog[gi].st.load(std::memory_order_acquire)) & 0xffffffffu) < need) std::this_thread::yield();
+            // waiting for the walks: sched_yield (NKM_MWAIT=N: asleep N µs at a
+            // time — measured slower, walks sum 13.5-14 -> 15-16 ms on C3,
+            // profiles/r05/r05l_mwait_ab.txt)
+            while (((v = prog[gi].st.load(std::memory_order_acquire)) & 0xffffffffu) < need) {
+                if (mwait_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(mwait_us_));
+                else std::this_thread::yield();
+            }
             const uint32_t nrec = (uint32_t)(v >> 32);
             const PoolRec* R = prog[gi].recs;
             auto by_bi = [](const PoolRec& x, uint32_t b) { return x.bi < b; };
@@ -918,7 +937,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
 // the result arena's entries when this pass owns it, as the pipelined merge).
 bool Core::replay_runs(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uint32_t>& brow,
                        const UVec<uint32_t>& brow_group, std::vector<uint8_t>& sel, GroupList& out_groups,
-                       std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
+                       UVec<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats, bool rev,
                        uint32_t* min_stop, const std::function<BGroup&(uint32_t)>* view) {
     using clk = std::chrono::steady_clock;
     auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1050,7 +1069,7 @@ bool Core::replay_runs(const ParPlan& P, std::vector<BGroup>& bg, const UVec<uin
 
 // Merge of per-row records (many pools) back into the pinned row order.
 void Core::merge_rows(size_t nb, size_t nch, const UVec<uint32_t>& brow, std::vector<uint8_t>& sel,
-                      GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly) {
+                      GroupList& out_groups, UVec<uint32_t>& expired, UVec<uint32_t>& newly) {
     WorkPool& wp = workers();
     const RowRec* rr = row_recs_.data();
     struct Cnt { size_t g = 0, e = 0, x = 0; };
@@ -1104,7 +1123,7 @@ void Core::merge_rows(size_t nb, size_t nch, const UVec<uint32_t>& brow, std::ve
 // chunk-local row map).  Applies the rows' pending Intervals increments on
 // the way.
 void Core::merge_pools(size_t ng, size_t nch, const UVec<uint32_t>& brow, std::vector<uint8_t>& sel,
-                       GroupList& out_groups, std::vector<uint32_t>& expired, UVec<uint32_t>& newly) {
+                       GroupList& out_groups, UVec<uint32_t>& expired, UVec<uint32_t>& newly) {
     using Rec = PoolRec;
     auto& outs = pool_outs_;
     WorkPool& wp = workers();
@@ -1174,16 +1193,20 @@ void Core::merge_pools(size_t ng, size_t nch, const UVec<uint32_t>& brow, std::v
 }
 
 // Row bi of a packed batch as the replay's search view (its fixed-stride
-// list, reverse bits and pair words in the pinned output buffer).
+// list, reverse bits and pair words in the pinned output buffer).  The list
+// comes as source positions: `src` is the row's source (its posting or order
+// list on the host mirror), `slots` the thread's buffer its slot ids go to.
 static inline void fill_packed(BGroup& g, const uint8_t* base, const PackLayout& L, uint32_t bi, uint32_t T,
-                               uint32_t sig) {
+                               uint32_t sig, const uint32_t* src, uint32_t* slots) {
     const uint32_t n = base[L.cnt + bi];
     const uint32_t P = L.S < 32 ? (uint32_t)L.S : 32u;
+    const uint8_t* pos = base + L.pos + (size_t)bi * L.S;
+    for (uint32_t k = 0; k < n; k++) slots[k] = src[pos[k]];
     g.sig = sig;
     g.row_slot = T;
     g.d.rev_slot = T;
     g.nrows = 1;
-    g.set_slots(reinterpret_cast<const uint32_t*>(base + L.slot) + (size_t)bi * L.S);
+    g.set_slots(slots);
     g.last_i = UINT32_MAX;
     g.rev = nullptr;
     g.rev_packed = true;
@@ -1347,15 +1370,16 @@ PackLayout Core::run_packed(const PackBatch& pb, PassStats& stats, const std::fu
     // per distinct candidate of a wave (pb.unique: the wave's loads bring each
     // in once, the S x S evaluations re-read them from L1 / LDS) its slot id,
     // alive flag and columns, query descriptor and clauses (the rows' average
-    // per-candidate bytes, weighted by source length); per entry its slot id;
-    // per row its pair words, reverse bits and count.  (Rounds 1-3 charged
+    // per-candidate bytes, weighted by source length); per entry its source position (1 B);
+    // per row its pair words, reverse bits and count (4-B slot ids per entry
+    // until round 5).  (Rounds 1-3 charged
     // every (row, candidate) pair's loads: C5 894 MB per launch vs 170 MB of
     // PMC traffic, profiles/r04q_c5_traffic.json.)
     (void)live;
     const double per_live = pb.scanned ? pb.live_w / (double)pb.scanned : 0.0;
     const int P = pb.S < 32 ? pb.S : 32;
     stats.k_bytes[3] += (int64_t)pb.n * (int64_t)(sizeof(DSmallRow) + 16) +
-                        (int64_t)((double)pb.unique * (5.0 + per_live)) + (int64_t)ents * 4 +
+                        (int64_t)((double)pb.unique * (5.0 + per_live)) + (int64_t)ents +
                         (int64_t)pb.n * (int64_t)(P * L.pm_w + L.rev_w + 1);
     stats.pair_evals += (int64_t)pb.scanned;
     return L;
@@ -1375,9 +1399,12 @@ std::function<BGroup&(uint32_t)> Core::packed_view(const PackLayout& L, const UV
     const uint8_t* base = h_pack_.p;
     return [this, base, L, &brow](uint32_t bi) -> BGroup& {
         static thread_local BGroup g;
+        static thread_local uint32_t slots[64];
         const uint32_t T = brow[bi];
-        fill_packed(g, base, L, bi, T, sig_[T]);
-        g.d.src_len = h_srows_.p[bi].src_len & ~kSrcOrder;  // the row's source (pairs decided)
+        const DSmallRow& d = h_srows_.p[bi];
+        const uint32_t* src = ((d.src_len & kSrcOrder) ? order_.data() : postings_.data()) + d.src_off;
+        fill_packed(g, base, L, bi, T, sig_[T], src, slots);
+        g.d.src_len = d.src_len & ~kSrcOrder;  // the row's source (pairs decided)
         return g;
     };
 }

@@ -1104,7 +1104,7 @@ void Core::choose_source(const Sig& s, DGroup& g, SrcChoice* ch) {
 }
 
 int Core::process_default(GroupList& out_groups,
-                          std::vector<uint32_t>& expired, PassStats& stats) {
+                          UVec<uint32_t>& expired, PassStats& stats) {
     const auto tp0 = std::chrono::steady_clock::now();
     const uint32_t N = (uint32_t)nslots();
     filled_groups_ = 0;
@@ -1666,7 +1666,7 @@ int Core::process_default(GroupList& out_groups,
 }
 
 // processCustom (matchmaker_process.go:336-612), up to the override call.
-int Core::process_custom(GroupList& cands, std::vector<uint32_t>& expired,
+int Core::process_custom(GroupList& cands, UVec<uint32_t>& expired,
                          PassStats& stats) {
     const bool rev_cfg = cfg_.rev_precision != 0;
     const int maxI = cfg_.max_intervals;
@@ -2100,7 +2100,7 @@ int Core::process(mm_matched* out) {
         });
         active_sorted_ = true;
     }
-    std::vector<uint32_t>& expired = expired_;
+    UVec<uint32_t>& expired = expired_;
     expired.clear();
     PassStats stats;
     // the snapshot is taken: mutators queue until the pass ends (matchmaker.go:309)
@@ -2247,7 +2247,7 @@ int Core::process_commit(const int32_t* offs, const mm_entry_ref* ents, int32_t 
     // tickets leave it here (their zombie documents would be filtered as
     // "missing index" by later passes, matchmaker_process.go:432-437).
     const auto t1 = std::chrono::steady_clock::now();
-    std::vector<uint32_t> exp = custom_expired_;
+    UVec<uint32_t> exp = custom_expired_;
     finish_pass(exp, groups, false);
     custom_open_ = false;
     pass_running_ = false;

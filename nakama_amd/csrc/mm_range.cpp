@@ -26,13 +26,14 @@ namespace nkm {
 
 void Core::reset_pass_scratch() {
     for (size_t k = 0; k < rs_mark_cap_; k++) rs_mark_[k].store(0, std::memory_order_relaxed);
+    for (size_t k = 0; k < pool_first_cap_; k++) pool_first_[k].store(UINT32_MAX, std::memory_order_relaxed);
     std::fill(rs_leaf_.begin(), rs_leaf_.end(), kNoSlot);
     std::fill(pos_of_.begin(), pos_of_.end(), kNoSlot);
     g_scratch_epoch.fetch_add(1, std::memory_order_relaxed);
 }
 
 bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList& out_groups,
-                       std::vector<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats) {
+                       UVec<uint32_t>& expired, UVec<uint32_t>& newly, PassStats& stats) {
     using clk = std::chrono::steady_clock;
     auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     const auto t0 = clk::now();
@@ -293,7 +294,55 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     for (size_t k = 0; k < ns; k++) ls_t0[k] = ls_q[k] + (uint32_t)k;
     grow_to(rs_tiers_, (size_t)nq + ns);
     const size_t tch = ns >= 512 ? (size_t)wp.size() * 2 : 1;
-    sweep(tch, [&](size_t c) {
+    // every pool's leaves (slot, rank, HotRec and Intervals copies, the
+    // slot -> leaf maps), in pieces: by the pool's walker before its walk (the
+    // walk then finds them in this core's cache), or (NKM_RLEAF=1) across the
+    // workers in the tiers' job — measured slower on C2 (its walks then read
+    // other cores' lines: slowest walk 1.7 -> 2.0-2.7 ms, profiles/r05/r05j)
+    constexpr uint32_t kLeafPiece = 4096;
+    const bool leaves_in_job = rleaf_mode_;
+    std::vector<uint64_t> piece_at{0};  // pools' pieces, prefix
+    for (size_t p = 0; p < ng; p++) {
+        RangePoolHost& H = rs_pools_[p];
+        const uint32_t nv = valid[p];
+        grow_to(H.slot, nv);
+        grow_to(H.rank, nv);
+        grow_to(H.leaf_of, H.d.src_len);
+        grow_to(H.lhot, nv);
+        grow_to(H.livl, nv);
+        piece_at.push_back(piece_at.back() + (nv + kLeafPiece - 1) / kLeafPiece);
+    }
+    const size_t npiece = piece_at.back();
+    std::vector<uint8_t> leaf_bad(npiece, 0);
+    auto leaf_piece = [&](size_t t) {
+        const size_t p = (size_t)(std::upper_bound(piece_at.begin(), piece_at.end(), (uint64_t)t) - piece_at.begin()) - 1;
+        RangePoolHost& H = rs_pools_[p];
+        const DRangePool& d = H.d;
+        const uint32_t* pv = h_rpos_.p + d.out_off;
+        const uint32_t j0 = (uint32_t)(t - piece_at[p]) * kLeafPiece, j1 = std::min(valid[p], j0 + kLeafPiece);
+        for (uint32_t j = j0; j < j1; j++) {
+            const uint32_t rk = pv[j];
+            if (rk >= d.src_len) { leaf_bad[t] = 1; return; }
+            if (j + 8 < j1 && pv[j + 8] < d.src_len) {
+                const uint32_t s8 = postings_[d.src_off + pv[j + 8]];
+                __builtin_prefetch(&hot_[s8]);
+                __builtin_prefetch(&intervals_[s8]);
+            }
+            const uint32_t s = postings_[d.src_off + rk];
+            H.rank[j] = rk;
+            H.slot[j] = s;
+            H.leaf_of[rk] = j;
+            rs_leaf_[s] = j;
+            H.lhot[j] = hot_[s];
+            H.livl[j] = intervals_[s];
+        }
+    };
+    const size_t njob = tch + (leaves_in_job ? npiece : 0);
+    sweep(njob > 1 ? njob : 1, [&](size_t c) {
+        if (c >= tch) {
+            leaf_piece(c - tch);
+            return;
+        }
         static thread_local std::vector<RRange> tmp;
         for (size_t k = ns * c / tch; k < ns * (c + 1) / tch; k++) {
             const Sig& s = sigs_[lsig[k]];
@@ -333,26 +382,9 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             RangePoolHost& H = rs_pools_[p];
             const DRangePool& d = H.d;
             const auto tb0 = clk::now();
-            // the pool's leaves (filled by its walker: the walk then finds
-            // them in this core's cache)
-            const uint32_t* pv = h_rpos_.p + d.out_off;
             const uint32_t nv = valid[p];
-            grow_to(H.slot, nv);
-            grow_to(H.rank, nv);
-            grow_to(H.leaf_of, d.src_len);
-            grow_to(H.lhot, nv);
-            grow_to(H.livl, nv);
-            for (uint32_t j = 0; j < nv; j++) {
-                const uint32_t rk = pv[j];
-                if (rk >= d.src_len) throw DeviceError{hipErrorUnknown, "range source: a sorted position out of range", __LINE__};
-                const uint32_t s = postings_[d.src_off + rk];
-                H.rank[j] = rk;
-                H.slot[j] = s;
-                H.leaf_of[rk] = j;
-                rs_leaf_[s] = j;
-                H.lhot[j] = hot_[s];
-                H.livl[j] = intervals_[s];
-            }
+            if (!leaves_in_job)
+                for (uint64_t q = piece_at[p]; q < piece_at[p + 1]; q++) leaf_piece(q);
             H.src.n = nv;
             H.src.slot = H.slot.data();
             H.src.rank = H.rank.data();
@@ -389,6 +421,8 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
         task_pairs[t] = pairs;
     };
     wp.run(ntask, worker);
+    for (uint8_t b : leaf_bad)
+        if (b) throw DeviceError{hipErrorUnknown, "range source: a sorted position out of range", __LINE__};
     const auto t3 = clk::now();
     for (size_t k = 0; k < ns; k++) rs_mark_[lsig[k]].store(0, std::memory_order_relaxed);
     const size_t mch = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
