@@ -299,29 +299,45 @@ struct ReplayCore {
     // changed nothing but the list head, when the row reaches the
     // CountMultiple trim (:234-280) or outgrows the fixed combos.
     Status fast_row(uint32_t T, BGroup& g, std::vector<std::pair<uint32_t, int>>& group_out) {
-        const HotRec& ht = v.hot[T];
+        // members the loop reads are copied into locals (`sel` is a byte
+        // array: a char load may alias any member, see DenseRun::fast_step)
+        const HotRec* const hot = v.hot;
+        const HotRec& ht = hot[T];
         const bool last = v.intervals[T] + 1 >= max_intervals || ht.minc == ht.maxc;
         const int tcount = ht.count, tmax = ht.maxc, tmin = ht.minc, tcm = ht.cm;
         const int room = tmax - tcount;  // entries a combo may hold
         const uint32_t tparty = ht.party;
+        const uint8_t* const S = sel.data();
+        const uint8_t* const pr = proc;
+        const int32_t* const ivl = v.intervals;
+        const uint8_t* const lv = v.live;
+        const bool rv = rev;
+        const int maxI = max_intervals;
+        const uint32_t n = g.n;
+        uint32_t h0 = g.head;
+        while (h0 < n && S[g.slot(h0)]) h0++;
+        g.head = h0;
         int ncomb = 0;
-        while (g.head < g.n && sel[g.slot(g.head)]) g.head++;
-        for (uint32_t i = g.head; i < g.n; i++) {
-            if (i + kPrefetch < g.n) {
+        uint64_t seen = 0;
+        Status st = NOMATCH;
+        int ff = -1;
+        int lf = 0;
+        for (uint32_t i = h0; i < n; i++) {
+            if (i + kPrefetch < n) {
                 const uint32_t P = g.slot(i + kPrefetch);
-                __builtin_prefetch(&sel[P]);
-                __builtin_prefetch(&v.hot[P]);
+                __builtin_prefetch(&S[P]);
+                __builtin_prefetch(&hot[P]);
             }
             const uint32_t H = g.slot(i);
-            hits_seen++;
-            if (H == T || sel[H]) continue;
-            const HotRec& hh = v.hot[H];
-            if (tparty != kNoParty && hh.party == tparty) continue;                                  // :80-85
-            if (rev && !g.rev_at(i)) continue;                                                       // :139-148
-            if (tmax < hh.maxc && v.intervals[H] + (proc ? proc[H] : 0) <= max_intervals) continue;  // :150-153
+            seen++;
+            if (H == T || S[H]) continue;
+            const HotRec& hh = hot[H];
+            if (tparty != kNoParty && hh.party == tparty) continue;                          // :80-85
+            if (rv && !g.rev_at(i)) continue;                                               // :139-148
+            if (tmax < hh.maxc && ivl[H] + (pr ? pr[H] : 0) <= maxI) continue;              // :150-153
             const int hc = hh.count;
             int f = 0;  // first fit (:167-226)
-            if (rev) {
+            if (rv) {
                 const uint64_t mine = g.pm_at(i), bit = 1ull << i;
                 while (f < ncomb && (fcb.size[f] + hc > room || (mine & fcb.pos[f]) != fcb.pos[f] || !(fcb.rcol[f] & bit)))
                     f++;
@@ -329,50 +345,57 @@ struct ReplayCore {
                 while (f < ncomb && fcb.size[f] + hc > room) f++;
             }
             if (f == ncomb) {
-                if (f == kFastComb) return BAIL;
+                if (f == kFastComb) { st = BAIL; break; }
                 fcb.size[f] = 0;
                 fcb.nmem[f] = 0;
                 fcb.pos[f] = 0;
                 fcb.rcol[f] = ~0ull;
                 ncomb++;
             } else if (fcb.nmem[f] == (uint32_t)kFastMem) {
-                return BAIL;
+                st = BAIL;
+                break;
             }
             fcb.size[f] += hc;
             fcb.mem[f][fcb.nmem[f]++] = H;
-            if (rev) {
+            if (rv) {
                 fcb.pos[f] |= 1ull << i;
-                if (v.live[H]) fcb.rcol[f] &= g.pm_at(i);
+                if (lv[H]) fcb.rcol[f] &= g.pm_at(i);
             }
             const int l = fcb.size[f] + tcount;
             bool form = l == tmax;  // :233
             if (!form && last && l >= tmin && l <= tmax) {
                 bool more = false;
-                for (uint32_t q = i + 1; q < g.n && !more; q++) {
-                    const uint32_t s = g.slot(q);
-                    more = s != T && !sel[s] && !same_party(T, s);
+                for (uint32_t q = i + 1; q < n && !more; q++) {
+                    const uint32_t s2 = g.slot(q);
+                    more = s2 != T && !S[s2] && !same_party(T, s2);
                 }
                 form = !more;
             }
             if (!form) continue;
-            if (!multiple_of(l, tcm)) return BAIL;
+            if (!multiple_of(l, tcm)) { st = BAIL; break; }
             bool failed = false;  // :287-296
             for (uint32_t k = 0; k < fcb.nmem[f] && !failed; k++) {
-                const uint32_t s = fcb.mem[f][k];
-                if (!v.live[s]) continue;
-                const HotRec& hs = v.hot[s];
+                const uint32_t s2 = fcb.mem[f][k];
+                if (!lv[s2]) continue;
+                const HotRec& hs = hot[s2];
                 failed = hs.minc > l || hs.maxc < l || !multiple_of(l, hs.cm);
             }
             if (failed) continue;
-            group_out.clear();
-            for (uint32_t k = 0; k < fcb.nmem[f]; k++) {
-                const uint32_t s = fcb.mem[f][k];
-                for (int e = 0; e < v.hot[s].count; e++) group_out.push_back({s, e});
-            }
-            for (int e = 0; e < tcount; e++) group_out.push_back({T, e});
-            return MATCHED;
+            st = MATCHED;
+            ff = f;
+            lf = l;
+            break;
         }
-        return NOMATCH;
+        hits_seen += seen;
+        (void)lf;
+        if (st != MATCHED) return st;
+        group_out.clear();
+        for (uint32_t k = 0; k < fcb.nmem[ff]; k++) {
+            const uint32_t m = fcb.mem[ff][k];
+            for (int e = 0; e < hot[m].count; e++) group_out.push_back({m, e});
+        }
+        for (int e = 0; e < tcount; e++) group_out.push_back({T, e});
+        return MATCHED;
     }
 
     // Is there an unselected, non-self hit after position i?  (the
@@ -600,10 +623,26 @@ uint32_t replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uin
 // segment walks compete with the gathers for the process's 16 CPUs and the
 // pass got slower: DESIGN.md §9, profiles/r03t_spec_ab.txt.)
 
+// The per-position fields every walk reads (24 B: 2.7 records per cache line,
+// none straddling two when aligned in threes), and the exact walk's session
+// fields beside them (DenseCold).
+#ifdef NKM_WALK_STATS
+inline uint64_t g_walk_stats[8];
+#define NKM_WS(k) (g_walk_stats[k]++)
+#else
+#define NKM_WS(k) ((void)0)
+#endif
 struct DenseRec {
     int32_t count, minc, maxc, cm;
-    uint32_t party, sess0, pres_off, intervals, smask;
-    uint32_t live;  // the ticket's live_ flag (constant during a pass: mutators queue), read with its record
+    uint32_t party;
+    // Intervals (< 2^31) | the ticket's live_ flag << 31 (live_ is constant
+    // during a pass: mutators queue), read with the record
+    uint32_t ivl_live;
+    uint32_t intervals() const { return ivl_live & 0x7fffffffu; }
+    bool live() const { return (ivl_live >> 31) != 0; }
+};
+struct DenseCold {
+    uint32_t sess0, pres_off, smask;
 };
 
 // One pool's per-position copies (filled by gather, in parallel chunks).
@@ -616,6 +655,7 @@ struct DensePool {
     uint32_t nrows = 0;
     const uint32_t* brow = nullptr;  // batch row -> slot
     std::vector<DenseRec> rec;
+    std::vector<DenseCold> cold;
     std::vector<uint32_t> slot;
     bool rows_list = false;  // BGroup::rows_list: position k's slot is brow[bis[k]], sp unfilled
     // identity: the pool's rows are its list, in list order (row j's ticket is
@@ -640,6 +680,7 @@ struct DensePool {
         front = nullptr;
         pieces = 1;
         if (rec.size() < n) rec.resize(n);
+        if (cold.size() < n) cold.resize(n);
         if (slot.size() < n) slot.resize(n);
     }
     uint32_t piece_lo(uint32_t t) const { return t >= pieces ? n : (uint32_t)((uint64_t)n * t / pieces); }
@@ -672,8 +713,9 @@ struct DensePool {
                 if (map) __builtin_prefetch(&pos_of[p], 1);
             }
             const HotRec& h = v.hot[s];
-            rec[k] = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party, h.sess0, h.pres_off,
-                              (uint32_t)v.intervals[s], h.smask, (uint32_t)v.live[s]};
+            rec[k] = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party,
+                              (uint32_t)v.intervals[s] | (v.live[s] ? 0x80000000u : 0u)};
+            cold[k] = DenseCold{h.sess0, h.pres_off, h.smask};
             slot[k] = s;
             if (map) pos_of[s] = k;
         }
@@ -741,27 +783,30 @@ struct DenseRun {
         row_at(P, pos_of, j, T, kT);
         if (kT != kNoSlot && sel[kT]) return false;
         DenseRec rt;
+        DenseCold rc;
         const uint32_t* tpres = v.pres_sess;
         if (kT != kNoSlot) {
             rt = P.rec[kT];
+            rc = P.cold[kT];
         } else {
             const HotRec& h = v.hot[T];
-            rt = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party, h.sess0, h.pres_off, (uint32_t)v.intervals[T], h.smask,
-                          (uint32_t)v.live[T]};
+            rt = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party,
+                          (uint32_t)v.intervals[T] | (v.live[T] ? 0x80000000u : 0u)};
+            rc = DenseCold{h.sess0, h.pres_off, h.smask};
         }
-        const bool last = (int)rt.intervals + 1 >= max_intervals || rt.minc == rt.maxc;
+        const bool last = (int)rt.intervals() + 1 >= max_intervals || rt.minc == rt.maxc;
         const int tcount = rt.count, tmax = rt.maxc, tmin = rt.minc, tcm = rt.cm;
         const uint32_t tparty = rt.party;
         auto t_has = [&](uint32_t sess) {
-            if (tcount == 1) return rt.sess0 == sess;
+            if (tcount == 1) return rc.sess0 == sess;
             for (int q = 0; q < tcount; q++)
-                if (tpres[rt.pres_off + q] == sess) return true;
+                if (tpres[rc.pres_off + q] == sess) return true;
             return false;
         };
-        auto h_has = [&](const DenseRec& h, uint32_t sess) {
-            if (h.count == 1) return h.sess0 == sess;
+        auto h_has = [&](const DenseRec& h, const DenseCold& c, uint32_t sess) {
+            if (h.count == 1) return c.sess0 == sess;
             for (int q = 0; q < h.count; q++)
-                if (v.pres_sess[h.pres_off + q] == sess) return true;
+                if (v.pres_sess[c.pres_off + q] == sess) return true;
             return false;
         };
         size_t ncomb = 0;
@@ -773,13 +818,14 @@ struct DenseRun {
             if (i == kT || sel[i]) continue;
             need(P, i);
             const DenseRec& hh = P.rec[i];
+            const DenseCold& hc0 = P.cold[i];
             if (tparty != kNoParty && hh.party == tparty) continue;                      // :80-85
-            if (tmax < hh.maxc && (int)hh.intervals + proc[i] <= max_intervals) continue;  // :150-153
-            if (!v.sessions_exclusive && (rt.smask & hh.smask)) {                        // :155-165
+            if (tmax < hh.maxc && (int)hh.intervals() + proc[i] <= max_intervals) continue;  // :150-153
+            if (!v.sessions_exclusive && (rc.smask & hc0.smask)) {                       // :155-165
                 bool shared = false;
-                if (hh.count == 1) shared = t_has(hh.sess0);
+                if (hh.count == 1) shared = t_has(hc0.sess0);
                 else
-                    for (int q = 0; q < hh.count && !shared; q++) shared = t_has(v.pres_sess[hh.pres_off + q]);
+                    for (int q = 0; q < hh.count && !shared; q++) shared = t_has(v.pres_sess[hc0.pres_off + q]);
                 if (shared) continue;
             }
             bool sconf = false;  // sticky across combos of this hit (:156, :174-176, :206)
@@ -792,13 +838,13 @@ struct DenseRun {
                 if ((int)combo.size() + tcount >= tmax) continue;  // full for good
                 open[w++] = ci;
                 if ((int)combo.size() + hcount + tcount <= tmax) {
-                    if (!v.sessions_exclusive && (cmask[ci] & hh.smask))
+                    if (!v.sessions_exclusive && (cmask[ci] & hc0.smask))
                         for (const CE& e : combo)
-                            if (h_has(hh, e.sess)) { sconf = true; break; }
+                            if (h_has(hh, hc0, e.sess)) { sconf = true; break; }
                     if (sconf) continue;
                     for (int k = 0; k < hcount; k++)
-                        combo.push_back(CE{P.slot[i], (uint32_t)k, i, hcount == 1 ? hh.sess0 : v.pres_sess[hh.pres_off + k]});
-                    cmask[ci] |= hh.smask;
+                        combo.push_back(CE{P.slot[i], (uint32_t)k, i, hcount == 1 ? hc0.sess0 : v.pres_sess[hc0.pres_off + k]});
+                    cmask[ci] |= hc0.smask;
                     found = (int)ci;
                     r++;
                     break;
@@ -814,8 +860,8 @@ struct DenseRun {
                 std::vector<CE>& nc = combos[ncomb];
                 nc.clear();
                 for (int k = 0; k < hcount; k++)
-                    nc.push_back(CE{P.slot[i], (uint32_t)k, i, hcount == 1 ? hh.sess0 : v.pres_sess[hh.pres_off + k]});
-                cmask[ncomb] = hh.smask;
+                    nc.push_back(CE{P.slot[i], (uint32_t)k, i, hcount == 1 ? hc0.sess0 : v.pres_sess[hc0.pres_off + k]});
+                cmask[ncomb] = hc0.smask;
                 found = (int)ncomb++;
                 if (hcount + tcount < tmax) open.push_back((uint32_t)found);
             }
@@ -861,7 +907,7 @@ struct DenseRun {
             bool last_ok = true;
             for (const CE& e : fc) {
                 const DenseRec& hs = P.rec[e.lpos];
-                if (!hs.live) continue;
+                if (!hs.live()) continue;
                 if (hs.minc > l || hs.maxc < l) { failed = true; break; }
                 if (hs.cm != last_cm) { last_cm = hs.cm; last_ok = multiple_of(l, hs.cm); }
                 if (!last_ok) { failed = true; break; }
@@ -891,16 +937,23 @@ struct DenseRun {
     // or 2 when the row reaches the CountMultiple trim or outgrows the fixed
     // combos — nothing changed but the head; step() then decides the row.
     int fast_step(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of, uint32_t j) {
+        // Members used in the loops are read into locals first: `sel` is a
+        // byte array, and a char-typed load may alias any member, so member
+        // counters (hits_seen, head, avail) would otherwise be stored and
+        // reloaded around every one (the box's PMU: 1,043 instructions per
+        // processed C3 row, 5.8 branch misses; tools/replay_bench RB_PERF=1)
         const uint32_t n = P.n;
         const uint32_t bi = P.bis[j];
         uint32_t T, kT;
         row_at(P, pos_of, j, T, kT);
-        if (kT != kNoSlot && sel[kT]) return 0;
+        const uint8_t* const S = sel.data();
+        if (kT != kNoSlot && S[kT]) return 0;
+        const DenseRec* const R = P.rec.data();
         int32_t tcount, tmin, tmax, tcm;
         uint32_t tparty, tivl;
         if (kT != kNoSlot) {
-            const DenseRec& r = P.rec[kT];
-            tcount = r.count; tmin = r.minc; tmax = r.maxc; tcm = r.cm; tparty = r.party; tivl = r.intervals;
+            const DenseRec& r = R[kT];
+            tcount = r.count; tmin = r.minc; tmax = r.maxc; tcm = r.cm; tparty = r.party; tivl = r.intervals();
         } else {
             const HotRec& h = v.hot[T];
             tcount = h.count; tmin = h.minc; tmax = h.maxc; tcm = h.cm; tparty = h.party;
@@ -908,61 +961,85 @@ struct DenseRun {
         }
         const bool last = (int)tivl + 1 >= max_intervals || tmin == tmax;
         const int room = tmax - tcount;
+        const uint8_t* const pr = proc.data();
+        uint32_t av = avail;
+        auto ready = [&](uint32_t i) {
+            if (i >= av) av = P.wait_pos(i);
+        };
+        uint32_t h0 = head;
+        while (h0 < n && S[h0]) { h0++; NKM_WS(0); }
+        head = h0;
+        int32_t* const csize = fcb.size;
+        uint32_t* const cnmem = fcb.nmem;
         int ncomb = 0, fi = -1;
-        while (head < n && sel[head]) head++;
-        for (uint32_t i = head; i < n; i++) {
-            hits_seen++;
-            if (i == kT || sel[i]) continue;
-            need(P, i);
-            const DenseRec& hh = P.rec[i];
-            if (tparty != kNoParty && hh.party == tparty) continue;                      // :80-85
-            if (tmax < hh.maxc && (int)hh.intervals + proc[i] <= max_intervals) continue;  // :150-153
+        uint64_t seen = 0;
+        bool bail = false;
+        for (uint32_t i = h0; i < n; i++) {
+            seen++;
+            if (i == kT || S[i]) continue;
+            ready(i);
+            const DenseRec& hh = R[i];
+            if (tparty != kNoParty && hh.party == tparty) continue;                    // :80-85
+            if (tmax < hh.maxc && (int)hh.intervals() + pr[i] <= max_intervals) continue;  // :150-153
             const int hc = hh.count;
             int f = 0;  // first fit (:167-226)
-            while (f < ncomb && fcb.size[f] + hc > room) f++;
+            while (f < ncomb && csize[f] + hc > room) { f++; NKM_WS(1); }
+            NKM_WS(2);
             if (f == ncomb) {
-                if (f == kFastComb) return 2;
-                fcb.size[f] = 0;
-                fcb.nmem[f] = 0;
+                if (f == kFastComb) { bail = true; break; }
+                csize[f] = 0;
+                cnmem[f] = 0;
                 ncomb++;
-            } else if (fcb.nmem[f] == (uint32_t)kFastMem) {
-                return 2;
+            } else if (cnmem[f] == (uint32_t)kFastMem) {
+                bail = true;
+                break;
             }
-            fcb.size[f] += hc;
-            fcb.mem[f][fcb.nmem[f]++] = i;
-            const int l = fcb.size[f] + tcount;
+            const int sz = csize[f] + hc;
+            csize[f] = sz;
+            fcb.mem[f][cnmem[f]++] = i;
+            const int l = sz + tcount;
             bool form = l == tmax;  // :233
             if (!form && last && l >= tmin && l <= tmax) {
                 bool more = false;
                 for (uint32_t q = i + 1; q < n && !more; q++) {
-                    if (q == kT || sel[q]) continue;
-                    need(P, q);
-                    more = !(tparty != kNoParty && P.rec[q].party == tparty);
+                    if (q == kT || S[q]) continue;
+                    ready(q);
+                    more = !(tparty != kNoParty && R[q].party == tparty);
                 }
                 form = !more;
             }
             if (!form) continue;
-            if (!multiple_of(l, tcm)) return 2;  // the CountMultiple trim: step()
-            bool failed = false;         // :287-296
-            for (uint32_t k = 0; k < fcb.nmem[f] && !failed; k++) {
-                const DenseRec& hs = P.rec[fcb.mem[f][k]];
-                if (!hs.live) continue;
+            if (!multiple_of(l, tcm)) { bail = true; break; }  // the CountMultiple trim: step()
+            bool failed = false;                                 // :287-296
+            const uint32_t* mem = fcb.mem[f];
+            for (uint32_t k = 0, nm = cnmem[f]; k < nm && !failed; k++) {
+                NKM_WS(3);
+                const DenseRec& hs = R[mem[k]];
+                if (!hs.live()) continue;
                 failed = hs.minc > l || hs.maxc < l || !multiple_of(l, hs.cm);
             }
             if (failed) continue;
             fi = f;
             break;
         }
+        hits_seen += seen;
+        avail = av;
+        if (bail) return 2;
         const uint32_t off = (uint32_t)ents.size();
         if (fi >= 0) {
-            for (uint32_t k = 0; k < fcb.nmem[fi]; k++) {
-                const uint32_t m = fcb.mem[fi][k];
+            const uint32_t* mem = fcb.mem[fi];
+            const uint32_t nm = cnmem[fi];
+            // entries first, the selection bytes after (a byte store between
+            // push_backs would make the vector's end pointer reload each time)
+            for (uint32_t k = 0; k < nm; k++) {
+                const uint32_t m = mem[k];
                 const uint32_t s = P.slot[m];
-                for (int e = 0; e < P.rec[m].count; e++) ents.push_back({s, e});
-                sel[m] = 1;
+                for (int e = 0, c = R[m].count; e < c; e++) ents.push_back({s, e});
             }
             for (int e = 0; e < tcount; e++) ents.push_back({T, e});
-            if (kT != kNoSlot) sel[kT] = 1;
+            uint8_t* const W = sel.data();
+            for (uint32_t k = 0; k < nm; k++) W[mem[k]] = 1;
+            if (kT != kNoSlot) W[kT] = 1;
         }
         if (kT != kNoSlot) proc[kT] = 1;
         recs.push_back(PoolRec{bi, (uint8_t)(fi >= 0), (uint8_t)last, off, (uint32_t)ents.size() - off, g_run, x_run});
@@ -979,6 +1056,7 @@ struct DenseRun {
         if (!P.identity) return j;
         const uint8_t* s = sel.data();
         while (j < end && s[j]) {
+            NKM_WS(4);
             uint64_t w;
             while (j + 8 <= end && (std::memcpy(&w, s + j, 8), w == 0x0101010101010101ull)) j += 8;
             while (j < end && s[j]) j++;

@@ -32,6 +32,10 @@
 #include <sys/time.h>
 #include <thread>
 #include <ucontext.h>
+#include <linux/perf_event.h>
+#include <sys/ioctl.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "../nakama_amd/csrc/replay_core.h"
 
@@ -55,6 +59,45 @@ static uint64_t splitmix(uint64_t& s) {
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
+
+// RB_PERF=1: hardware counters (user space, this thread) around the identity
+// walk — cycles, instructions, branch misses, L1D read misses — where the host
+// exposes a PMU (the GPU boxes; not this build container)
+struct PerfGroup {
+    int fd[4] = {-1, -1, -1, -1};
+    uint64_t v[4] = {};
+    static int open1(uint32_t type, uint64_t config) {
+        perf_event_attr a;
+        std::memset(&a, 0, sizeof a);
+        a.type = type;
+        a.size = sizeof a;
+        a.config = config;
+        a.disabled = 1;
+        a.exclude_kernel = 1;
+        a.exclude_hv = 1;
+        return (int)syscall(__NR_perf_event_open, &a, 0, -1, -1, 0);
+    }
+    PerfGroup() {
+        fd[0] = open1(PERF_TYPE_HARDWARE, PERF_COUNT_HW_CPU_CYCLES);
+        fd[1] = open1(PERF_TYPE_HARDWARE, PERF_COUNT_HW_INSTRUCTIONS);
+        fd[2] = open1(PERF_TYPE_HARDWARE, PERF_COUNT_HW_BRANCH_MISSES);
+        fd[3] = open1(PERF_TYPE_HW_CACHE, PERF_COUNT_HW_CACHE_L1D | (PERF_COUNT_HW_CACHE_OP_READ << 8) |
+                                              (PERF_COUNT_HW_CACHE_RESULT_MISS << 16));
+    }
+    bool ok() const { return fd[0] >= 0; }
+    void start() {
+        for (int k = 0; k < 4; k++)
+            if (fd[k] >= 0) { ioctl(fd[k], PERF_EVENT_IOC_RESET, 0); ioctl(fd[k], PERF_EVENT_IOC_ENABLE, 0); }
+    }
+    void stop() {
+        for (int k = 0; k < 4; k++) {
+            if (fd[k] < 0) continue;
+            ioctl(fd[k], PERF_EVENT_IOC_DISABLE, 0);
+            uint64_t x = 0;
+            if (read(fd[k], &x, sizeof x) == (ssize_t)sizeof x) v[k] += x;
+        }
+    }
+};
 
 static double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -297,9 +340,37 @@ int main(int argc, char** argv) {
                     itimerval it{{0, 100}, {0, 100}};
                     setitimer(ITIMER_PROF, &it, nullptr);
                 }
+                static PerfGroup pg;
+                const bool perf = std::getenv("RB_PERF") != nullptr && pg.ok();
+                if (perf) pg.start();
                 const double t0 = now_ms();
+#ifdef NKM_WALK_STATS
+                std::memset(g_walk_stats, 0, sizeof g_walk_stats);
+#endif
                 run.walk(P, v, maxI, pos_of.data(), 0, P.nrows);
                 best[4] = std::min(best[4], now_ms() - t0);
+#ifdef NKM_WALK_STATS
+                if (r == 0) {
+                    const double rows = (double)run.recs.size();
+                    std::printf("[stats] per processed row: head steps %.2f, first-fit steps %.2f, hits placed %.2f, "
+                                "member checks %.2f, skip loops %.2f, hits seen %.2f, entries %.2f\n",
+                                g_walk_stats[0] / rows, g_walk_stats[1] / rows, g_walk_stats[2] / rows,
+                                g_walk_stats[3] / rows, g_walk_stats[4] / rows, run.hits_seen / rows,
+                                run.ents.size() / rows);
+                }
+#endif
+                if (perf) {
+                    pg.stop();
+                    if (r + 1 == reps) {
+                        const double steps = (double)run.recs.size();
+                        std::printf("[perf] identity walk, %d reps: per processed row %.0f cycles, %.0f instructions "
+                                    "(IPC %.2f), %.2f branch misses, %.2f L1D read misses; hits examined %.2f per row\n",
+                                    reps, pg.v[0] / steps / reps, pg.v[1] / steps / reps, (double)pg.v[1] / (double)pg.v[0],
+                                    pg.v[2] / steps / reps, pg.v[3] / steps / reps, run.hits_seen / steps);
+                    }
+                } else if (std::getenv("RB_PERF") && r == 0) {
+                    std::printf("[perf] no PMU here\n");
+                }
                 if (prof_walk) {
                     itimerval off{};
                     setitimer(ITIMER_PROF, &off, nullptr);
@@ -345,13 +416,22 @@ int main(int argc, char** argv) {
         for (auto& t : th) t.join();
     };
     constexpr uint32_t kChunk = 16384;
+    // RB_IDENT=1: identity pools (the product's C3 / C4 walks: row j is list
+    // position j); RB_SELFGATHER=1: each walk gathers its own pool first (in its
+    // timed task) instead of the chunked gather across the threads
+    const bool ident = std::getenv("RB_IDENT") && std::atoi(std::getenv("RB_IDENT")) != 0;
+    const bool selfg = std::getenv("RB_SELFGATHER") && std::atoi(std::getenv("RB_SELFGATHER")) != 0;
     for (int r = 0; r < reps; r++) {
         const double t0 = now_ms();
         std::vector<std::pair<int, uint32_t>> chunks;
+        bool all_ident = ident;
         for (int p = 0; p < npools; p++) {
             P[p].reset(gs[p], pbis[p].data(), (uint32_t)pbis[p].size(), brow.data());
-            for (uint32_t c = 0; c * kChunk < P[p].n; c++) chunks.push_back({p, c});
+            all_ident = all_ident && P[p].nrows == P[p].n && P[p].rows_are_list(0, P[p].n);
+            for (uint32_t c = 0; c * kChunk < P[p].n && !selfg; c++) chunks.push_back({p, c});
         }
+        for (int p = 0; p < npools; p++) P[p].identity = all_ident;
+        if (r == 0 && ident && !all_ident) std::printf("RB_IDENT: the pools' rows are not their lists\n");
         par(chunks.size(), [&](size_t t) {
             DensePool& q = P[chunks[t].first];
             const uint32_t lo = chunks[t].second * kChunk;
@@ -361,6 +441,7 @@ int main(int argc, char** argv) {
         std::vector<double> task(npools);
         par(npools, [&](size_t p) {
             const double a = now_ms();
+            if (selfg) P[p].gather(v, 0, P[p].n, pos_of.data());
             runs[p].reset(P[p].n);
             runs[p].fast = fast;
             runs[p].walk(P[p], v, maxI, pos_of.data(), 0, P[p].nrows);
