@@ -137,12 +137,14 @@ bool Core::finish_fill_fast(const UVec<uint32_t>& expired, GroupList& groups, mm
     mm_entry_ref* ents = out_ents_.data();
     int64_t* gc = out_created_.data();
     std::vector<uint32_t> killed(nch, 0);
+    std::vector<double> task_us(nch, 0.0), start_us(nch, 0.0);  // NKM_PROFILE=2: the job's own time vs its wall
     // Without a mutation, the matched tickets are exactly the pass's selection
     // (sel_): retired by one sequential sweep over the slots instead of
     // scattered writes per result entry
     const size_t N = nslots();
     const bool by_slot = !mutated && sel_.size() == N;
     wp.run(nch, [&](size_t c) {
+        const auto tc0 = std::chrono::steady_clock::now();
         const size_t g0 = ng * c / nch, g1 = ng * (c + 1) / nch;
         uint32_t k = 0;
         if (!mutated)
@@ -177,6 +179,9 @@ bool Core::finish_fill_fast(const UVec<uint32_t>& expired, GroupList& groups, mm
             }
         }
         killed[c] = k;
+        const auto tc1 = std::chrono::steady_clock::now();
+        start_us[c] = std::chrono::duration<double, std::micro>(tc0 - f0).count();
+        task_us[c] = std::chrono::duration<double, std::micro>(tc1 - tc0).count();
     });
     const auto f1 = std::chrono::steady_clock::now();
     for (uint32_t k : killed) n_live_ -= k;
@@ -186,9 +191,11 @@ bool Core::finish_fill_fast(const UVec<uint32_t>& expired, GroupList& groups, mm
     active_exact_ = true;
     if (const char* p = std::getenv("NKM_PROFILE"); p && std::atoi(p) >= 2) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "[nkm]   finish: retire %.3f ms (%s, %s) | filter %.3f ms (%zu active)\n", ms(f0, f1),
-                     by_slot ? "by slot" : "by entry", filled ? "filled" : "fill", ms(f1, std::chrono::steady_clock::now()),
-                     active_list_.size());
+        std::fprintf(stderr, "[nkm]   finish: retire %.3f ms (%s, %s; its tasks: max %.0f us, last start %.0f us) | "
+                     "filter %.3f ms (%zu active)\n", ms(f0, f1),
+                     by_slot ? "by slot" : "by entry", filled ? "filled" : "fill",
+                     *std::max_element(task_us.begin(), task_us.end()), *std::max_element(start_us.begin(), start_us.end()),
+                     ms(f1, std::chrono::steady_clock::now()), active_list_.size());
     }
     out->group_created = gc;
     out->n_groups = (int32_t)ng;

@@ -607,6 +607,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     }
     // proven lists (BGroup::rows_list) not downloaded: only the identity walk
     // goes without them
+    const auto tg_ident = clk::now();
     if (!ident && !view) fill_row_lists(bg, brow, brow_group);
     const bool gpipe = ident && pipe && wp.size() > ntask;
     // (Identity pools with more walks than workers, C4's 64 on 16, gather
@@ -641,6 +642,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     };
     // each pool's entry bound (every ticket of its list and rows joins at
     // most one group): the walk reserves it so readers never see a move
+    const auto tg_setup = clk::now();
     std::vector<uint64_t> esum(pipe && !gpipe ? ntask_g * ng : 0, 0);
     if (!gpipe)
         wp.run(ntask_g, [&](size_t t) {
@@ -657,6 +659,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                 esum[t * ng + gi] = e;
             }
         });
+    const auto tg_gather = clk::now();
     struct alignas(128) Prog {
         std::atomic<uint64_t> st{0};  // (records published << 32) | rows done
         const PoolRec* recs = nullptr;
@@ -917,8 +920,10 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             we = std::max(we, walk_end_ms[k]);
         }
         std::fprintf(stderr, "[nkm]   pool walks: %zu tasks, %zu pools on %u workers | sum: tasks %.2f, walks %.2f (max %.2f), "
-                     "gather+reset+reserve %.2f ms | gather %s | last walk ends %.2f, job %.2f ms (%zu merge chunks)\n",
-                     ntask, ng, wp.size(), st, sw, mw, sp, gpipe ? "beside" : "before", we, msd(tg1, tg2), nch);
+                     "gather+reset+reserve %.2f ms | gather %s | last walk ends %.2f, job %.2f ms (%zu merge chunks) | "
+                     "before the job: identity check %.2f, lists + setup %.2f, gather %.2f, bounds %.2f ms\n",
+                     ntask, ng, wp.size(), st, sw, mw, sp, gpipe ? "beside" : "before", we, msd(tg1, tg2), nch,
+                     msd(tg0, tg_ident), msd(tg_ident, tg_setup), msd(tg_setup, tg_gather), msd(tg_gather, tg1));
     }
     stats.par_rows += nb;
     return true;

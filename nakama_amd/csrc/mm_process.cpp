@@ -1109,9 +1109,19 @@ int Core::process_default(GroupList& out_groups,
     const uint32_t N = (uint32_t)nslots();
     filled_groups_ = 0;
     std::vector<uint8_t>& sel = sel_;
-    sel.assign(N, 0);
     std::vector<uint8_t>& dec = dec_;  // rows decided ahead of `pos` by a partial parallel replay
-    dec.assign(N, 0);
+    if (par_mode_ && N >= par_min(1u << 20) && sel.size() == N && dec.size() == N) {
+        WorkPool& wp = workers();  // 2 x 1 MB at C3: cleared on the workers
+        const size_t nch = wp.size();
+        wp.run(nch, [&](size_t c) {
+            const size_t lo = (size_t)N * c / nch, hi = (size_t)N * (c + 1) / nch;
+            std::memset(sel.data() + lo, 0, hi - lo);
+            std::memset(dec.data() + lo, 0, hi - lo);
+        });
+    } else {
+        sel.assign(N, 0);
+        dec.assign(N, 0);
+    }
     bool out_of_order = false;         // groups appended out of row order (sorted at the end)
     std::vector<uint32_t>& rowpos = list_tmp_;  // slot -> pinned position (set when out_of_order)
     bool rev = cfg_.rev_precision != 0;
@@ -1317,7 +1327,9 @@ int Core::process_default(GroupList& out_groups,
             };
             std::vector<Chunk> ch(nch);
             const auto ts0 = std::chrono::steady_clock::now();
+            std::vector<double> cnt_task_us(nch, 0.0), cnt_start_us(nch, 0.0);  // NKM_PROFILE=2
             wp.run(nch, [&](size_t c) {
+                const auto tc0 = std::chrono::steady_clock::now();
                 // thread-private until the end (adjacent Chunks share cache
                 // lines: a per-row k.n++ made this sweep 3-4x slower)
                 std::vector<uint32_t> first, cnt(nsig, 0);
@@ -1342,8 +1354,15 @@ int Core::process_default(GroupList& out_groups,
                 k.maxm = std::move(maxm);
                 k.n = n;
                 k.self = self;
+                const auto tc1 = std::chrono::steady_clock::now();
+                cnt_start_us[c] = std::chrono::duration<double, std::micro>(tc0 - ts0).count();
+                cnt_task_us[c] = std::chrono::duration<double, std::micro>(tc1 - tc0).count();
             });
             stats.asm_count_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
+            if (batch_profile_)
+                std::fprintf(stderr, "[nkm]   assemble count sweep: tasks max %.0f us, last start %.0f us\n",
+                             *std::max_element(cnt_task_us.begin(), cnt_task_us.end()),
+                             *std::max_element(cnt_start_us.begin(), cnt_start_us.end()));
             uint64_t bound = 0;
             for (unsigned c = 0; c < nch; c++)
                 for (uint32_t sg : ch[c].first)
