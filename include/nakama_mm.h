@@ -192,6 +192,33 @@ void mm_free_matched(void* h, mm_matched* out);
 int  mm_drain_removed(void* h, mm_str_list* out);
 void mm_free_str_list(void* h, mm_str_list* out);
 
+/* ---- pipelined delivery (matchmaker.go:374-440) ----
+ * The reference delivers a pass's matched groups — a token or the
+ * OnMatchedEntries hook per group, and the router fan-out — from Process
+ * itself, so the next interval waits for it.  Here delivery runs behind the
+ * pass: mm_process_deliver runs the pass (as mm_process) and hands its result
+ * to a library-owned delivery thread, which calls fn(ctx, matched, pass_seq)
+ * once per pass in pass order (pass_seq counts from 0 per mm_set_delivery)
+ * while the caller's next pass may already run, then frees the result.  Up to
+ * `depth` (>= 1) results wait for the callback; a further mm_process_deliver
+ * blocks until one is delivered (a buffered Go channel's back-pressure).
+ * `summary` receives the pass's counts and statistics with the group arrays
+ * NULL — except on the override path, where the processCustom candidates
+ * (is_candidates = 1) are returned in full exactly as by mm_process, and the
+ * chosen groups are queued by mm_process_commit_deliver instead.  fn runs on
+ * the delivery thread; it may call the handle's mutators and queries, not
+ * mm_process*, mm_set_delivery, mm_delivery_flush or mm_destroy.  Entry points
+ * of this section return MM_ERR_STATE when no delivery is set. */
+typedef void (*mm_deliver_fn)(void* ctx, const mm_matched* matched, int64_t pass_seq);
+/* fn NULL: deliver what is queued, then stop the thread.  Replaces an earlier
+ * setting after delivering its queue. */
+int  mm_set_delivery(void* h, mm_deliver_fn fn, void* ctx, int32_t depth);
+int  mm_process_deliver(void* h, mm_matched* summary);
+int  mm_process_commit_deliver(void* h, const int32_t* group_offsets, const mm_entry_ref* entries,
+                               int32_t n_groups, mm_matched* summary);
+/* Returns when every result queued so far has been delivered and freed. */
+int  mm_delivery_flush(void* h);
+
 /* ---- introspection used by tests and the bench ---- */
 /* Test hook: fn(ctx) is called once per pass, on the pass's thread, after the
  * device searches and the replay and before the post-pass finish, with the

@@ -125,6 +125,8 @@ class mm_str_list(C.Structure):
 
 
 PASS_HOOK = C.CFUNCTYPE(None, C.c_void_p)
+# mm_deliver_fn(ctx, matched, pass_seq) (include/nakama_mm.h, pipelined delivery)
+DELIVER_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int64)
 
 # mm_sub_api (include/nakama_cluster.h): the entry points a multi handle
 # drives its sub-handles through, in declaration order -> exported symbol
@@ -167,7 +169,8 @@ EXPORTED_SYMBOLS = (
     "mm_process", "mm_process_commit", "mm_free_matched", "mm_ticket_count", "mm_active_count",
     "mm_debug_hits", "mm_debug_compile", "mm_debug_term_match", "mm_debug_group_indexes",
     "mm_drain_removed", "mm_free_str_list", "mm_debug_set_pass_hook", "mm_session_ticket_count",
-    "mm_party_ticket_count", "mm_find_tickets",
+    "mm_party_ticket_count", "mm_find_tickets", "mm_set_delivery", "mm_process_deliver",
+    "mm_process_commit_deliver", "mm_delivery_flush",
 )
 
 
@@ -236,6 +239,11 @@ def load_library(path: str) -> C.CDLL:
         "mm_debug_group_indexes": (C.c_int32, [C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_int32, C.c_int32,
                                                C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int64),
                                                C.c_int32]),
+        "mm_set_delivery": (C.c_int, [vp, DELIVER_FN, vp, C.c_int32]),
+        "mm_process_deliver": (C.c_int, [vp, C.POINTER(mm_matched)]),
+        "mm_process_commit_deliver": (C.c_int, [vp, C.POINTER(C.c_int32), C.POINTER(mm_entry_ref), C.c_int32,
+                                                C.POINTER(mm_matched)]),
+        "mm_delivery_flush": (C.c_int, [vp]),
     }
     if hasattr(lib, "mm_create_multi"):  # the product: one handle over several devices (nakama_cluster.h)
         sig["mm_create_multi"] = (vp, [C.POINTER(mm_config), C.POINTER(mm_multi_config)])
@@ -552,6 +560,62 @@ class Matchmaker:
         if r.groups and self._matched_fn is not None:
             self._matched_fn(r.groups)
         return r.groups
+
+    # pipelined delivery (include/nakama_mm.h; matchmaker.go:374-440 behind the next pass)
+    def set_delivery(self, fn, depth: int = 4):
+        """fn(groups, pass_seq) is called on the library's delivery thread once
+        per pass, in pass order, with the pass's matched groups; None stops
+        the delivery after the queued results.  The ctypes trampoline is kept
+        on the handle (the library holds a raw pointer to it)."""
+        if fn is None:
+            self._check(self.lib.mm_set_delivery(self.h, C.cast(None, DELIVER_FN), None, 0))
+            self._deliver_cb = None
+            return
+        groups_of = self._groups
+
+        def tramp(_ctx, matched, seq):
+            fn(groups_of(C.cast(matched, C.POINTER(mm_matched)).contents), int(seq))
+
+        cb = DELIVER_FN(tramp)
+        self._check(self.lib.mm_set_delivery(self.h, cb, None, depth))
+        self._deliver_cb = cb
+
+    def process_deliver(self) -> ProcessResult:
+        """One pass through mm_process_deliver: the groups go to the delivery
+        callback; returns the counts (groups empty) — or, on the override
+        path, the candidates in full (is_candidates), to be chosen and passed
+        to commit_deliver."""
+        out = mm_matched()
+        self._check(self.lib.mm_process_deliver(self.h, C.byref(out)))
+        if out.is_candidates:
+            try:
+                return ProcessResult(self._groups(out), True, out.n_expired, out.pass_ms, out.eval_ms, out.pair_evals,
+                                     out.eval_bytes, out.eval_launches, out.n_batches, out.eval_kernel,
+                                     out.full_lists, out.pairs_decided)
+            finally:
+                self.lib.mm_free_matched(self.h, C.byref(out))
+        return ProcessResult([], False, out.n_expired, out.pass_ms, out.eval_ms, out.pair_evals, out.eval_bytes,
+                             out.eval_launches, out.n_batches, out.eval_kernel, out.full_lists, out.pairs_decided)
+
+    def commit_deliver(self, groups: Sequence[Sequence[Tuple[str, int]]]) -> int:
+        """mm_process_commit_deliver of the override's choice; returns the
+        committed group count (the groups go to the delivery callback)."""
+        offs = [0]
+        ents = []
+        for g in groups:
+            ents.extend(g)
+            offs.append(len(ents))
+        off_arr = (C.c_int32 * len(offs))(*offs)
+        keep = [_b(t) for t, _ in ents]
+        ent_arr = (mm_entry_ref * max(1, len(ents)))()
+        for i, (t, pi) in enumerate(ents):
+            ent_arr[i] = mm_entry_ref(keep[i], pi, 0)
+        out = mm_matched()
+        self._check(self.lib.mm_process_commit_deliver(self.h, off_arr, ent_arr, len(groups), C.byref(out)))
+        return out.n_groups
+
+    def delivery_flush(self):
+        self._check(self.lib.mm_delivery_flush(self.h))
 
     def drain_removed(self) -> List[str]:
         """Tickets that left the matchmaker since the previous call (the first

@@ -1,9 +1,15 @@
 // nakama_amd/csrc/mm_capi.cpp — extern "C" entry points of include/nakama_mm.h.
 // Every entry converts device failures into MM_ERR_DEVICE with a message in
 // mm_last_error; nothing here falls back to a CPU search.
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 
 #include "mm_core.h"
 
@@ -38,6 +44,82 @@ int guarded(void* h, F&& f) {
     }
 }
 std::string S(const char* p) { return p ? std::string(p) : std::string(); }
+
+// Pipelined delivery (nakama_mm.h): one thread per handle
+// that hands each queued pass result to the caller's callback, in pass order,
+// then frees it; the queue holds at most `depth` results (push blocks beyond:
+// back-pressure).  The handle itself is untouched — a queued result is an
+// ordinary outstanding mm_matched (a second one takes private copies).
+struct Delivery {
+    Handle* h;
+    mm_deliver_fn fn;
+    void* ctx;
+    size_t depth;
+    std::mutex mu;
+    std::condition_variable cv_item, cv_space, cv_idle;
+    std::deque<std::pair<mm_matched, int64_t>> q;
+    bool busy = false, quit = false;
+    int64_t seq = 0;
+    std::thread th;
+
+    Delivery(Handle* hh, mm_deliver_fn f, void* c, size_t d) : h(hh), fn(f), ctx(c), depth(d) {
+        th = std::thread([this] { loop(); });
+    }
+    ~Delivery() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+        }
+        cv_item.notify_all();
+        th.join();  // the loop delivers what is queued before it exits
+    }
+    void loop() {
+        for (;;) {
+            std::unique_lock<std::mutex> lk(mu);
+            cv_item.wait(lk, [&] { return quit || !q.empty(); });
+            if (q.empty()) return;  // quit, nothing left
+            std::pair<mm_matched, int64_t> it = q.front();
+            q.pop_front();
+            busy = true;
+            lk.unlock();
+            cv_space.notify_all();
+            fn(ctx, &it.first, it.second);
+            (void)guarded(h, [&](Handle& c) { c.free_matched(&it.first); return MM_OK; });
+            lk.lock();
+            busy = false;
+            lk.unlock();
+            cv_idle.notify_all();
+        }
+    }
+    void push(const mm_matched& m) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_space.wait(lk, [&] { return q.size() < depth; });
+        q.emplace_back(m, seq++);
+        lk.unlock();
+        cv_item.notify_one();
+    }
+    void flush() {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_idle.wait(lk, [&] { return q.empty() && !busy; });
+    }
+};
+std::mutex g_deliv_mu;
+std::map<void*, std::unique_ptr<Delivery>> g_deliv;
+
+Delivery* delivery_of(void* h) {
+    std::lock_guard<std::mutex> lk(g_deliv_mu);
+    auto it = g_deliv.find(h);
+    return it == g_deliv.end() ? nullptr : it->second.get();
+}
+// the pass's counts and statistics without its arrays (the result is queued)
+mm_matched summary_of(const mm_matched& m) {
+    mm_matched s = m;
+    s.group_offsets = nullptr;
+    s.entries = nullptr;
+    s.group_created = nullptr;
+    s.reserved2 = 0;
+    return s;
+}
 }  // namespace
 
 void nkm::set_create_error(const std::string& e) { g_create_error = e; }
@@ -64,6 +146,16 @@ void* mm_create(const mm_config* cfg) {
 }
 void mm_destroy(void* h) {
     try {
+        std::unique_ptr<Delivery> d;
+        {
+            std::lock_guard<std::mutex> lk(g_deliv_mu);
+            auto it = g_deliv.find(h);
+            if (it != g_deliv.end()) {
+                d = std::move(it->second);
+                g_deliv.erase(it);
+            }
+        }
+        d.reset();  // the queued results are delivered and freed first
         delete static_cast<Handle*>(h);
     } catch (...) {
     }
@@ -118,6 +210,63 @@ int mm_process_commit(void* h, const int32_t* group_offsets, const mm_entry_ref*
 }
 void mm_free_matched(void* h, mm_matched* out) {
     (void)guarded(h, [&](Handle& c) { c.free_matched(out); return MM_OK; });
+}
+int mm_set_delivery(void* h, mm_deliver_fn fn, void* ctx, int32_t depth) {
+    if (!h || (fn && depth < 1)) return MM_ERR_ARG;
+    try {
+        std::unique_ptr<Delivery> old;
+        {
+            std::lock_guard<std::mutex> lk(g_deliv_mu);
+            auto it = g_deliv.find(h);
+            if (it != g_deliv.end()) {
+                old = std::move(it->second);
+                g_deliv.erase(it);
+            }
+        }
+        old.reset();  // its queue delivered, its thread joined
+        if (fn) {
+            std::unique_ptr<Delivery> d(new Delivery(static_cast<Handle*>(h), fn, ctx, (size_t)depth));
+            std::lock_guard<std::mutex> lk(g_deliv_mu);
+            g_deliv[h] = std::move(d);
+        }
+        return MM_OK;
+    } catch (...) {
+        static_cast<Handle*>(h)->set_error("mm_set_delivery: could not start the delivery thread");
+        return MM_ERR_INDEX;
+    }
+}
+int mm_process_deliver(void* h, mm_matched* summary) {
+    if (!summary) return MM_ERR_ARG;
+    Delivery* d = delivery_of(h);
+    if (!d) return h ? MM_ERR_STATE : MM_ERR_ARG;
+    mm_matched m{};
+    const int rc = guarded(h, [&](Handle& c) { return c.process(&m); });
+    if (rc != MM_OK) return rc;
+    if (m.is_candidates) {  // processCustom: the override chooses first (mm_process_commit_deliver)
+        *summary = m;
+        return MM_OK;
+    }
+    *summary = summary_of(m);
+    d->push(m);
+    return MM_OK;
+}
+int mm_process_commit_deliver(void* h, const int32_t* group_offsets, const mm_entry_ref* entries, int32_t n_groups,
+                              mm_matched* summary) {
+    if (!summary || (n_groups > 0 && (!group_offsets || !entries))) return MM_ERR_ARG;
+    Delivery* d = delivery_of(h);
+    if (!d) return h ? MM_ERR_STATE : MM_ERR_ARG;
+    mm_matched m{};
+    const int rc = guarded(h, [&](Handle& c) { return c.process_commit(group_offsets, entries, n_groups, &m); });
+    if (rc != MM_OK) return rc;
+    *summary = summary_of(m);
+    d->push(m);
+    return MM_OK;
+}
+int mm_delivery_flush(void* h) {
+    Delivery* d = delivery_of(h);
+    if (!d) return h ? MM_ERR_STATE : MM_ERR_ARG;
+    d->flush();
+    return MM_OK;
 }
 int32_t mm_ticket_count(void* h) {
     int32_t n = -1;

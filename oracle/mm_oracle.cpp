@@ -612,6 +612,11 @@ struct Matchmaker {
     mm_config cfg;
     string node;
     bool active = true, stopped = false;
+    // mm_set_delivery: the checker delivers synchronously, in pass order (the
+    // contract's observable part; the product's delivery thread pipelines it)
+    mm_deliver_fn deliver_fn = nullptr;
+    void* deliver_ctx = nullptr;
+    int64_t deliver_seq = 0;
     string last_error;
     uint64_t next_docnum = 0;
     vector<BlugeDoc> bluge;                               // the in-memory index, insertion order
@@ -1494,6 +1499,56 @@ void mm_free_matched(void* h, mm_matched* out) {
     delete[] out->group_created;
     delete reinterpret_cast<vector<string>*>((intptr_t)out->reserved2);
     std::memset(out, 0, sizeof(*out));
+}
+
+// Delivery (nakama_mm.h "pipelined delivery"): the result goes to fn in pass
+// order, then is freed; the caller gets the counts (test infrastructure: no
+// thread, no queue — depth only validated).
+int mm_set_delivery(void* h, mm_deliver_fn fn, void* ctx, int32_t depth) {
+    if (!h || (fn && depth < 1)) return MM_ERR_ARG;
+    auto& m = *static_cast<Matchmaker*>(h);
+    m.deliver_fn = fn;
+    m.deliver_ctx = ctx;
+    m.deliver_seq = 0;
+    return MM_OK;
+}
+static void deliver_now(Matchmaker& m, void* h, mm_matched& r, mm_matched* summary) {
+    *summary = r;
+    summary->group_offsets = nullptr;
+    summary->entries = nullptr;
+    summary->group_created = nullptr;
+    summary->reserved2 = 0;
+    m.deliver_fn(m.deliver_ctx, &r, m.deliver_seq++);
+    mm_free_matched(h, &r);
+}
+int mm_process_deliver(void* h, mm_matched* summary) {
+    if (!h || !summary) return MM_ERR_ARG;
+    auto& m = *static_cast<Matchmaker*>(h);
+    if (!m.deliver_fn) return MM_ERR_STATE;
+    mm_matched r{};
+    const int rc = mm_process(h, &r);
+    if (rc != MM_OK) return rc;
+    if (r.is_candidates) {
+        *summary = r;
+        return MM_OK;
+    }
+    deliver_now(m, h, r, summary);
+    return MM_OK;
+}
+int mm_process_commit_deliver(void* h, const int32_t* group_offsets, const mm_entry_ref* entries, int32_t n_groups,
+                              mm_matched* summary) {
+    if (!h || !summary) return MM_ERR_ARG;
+    auto& m = *static_cast<Matchmaker*>(h);
+    if (!m.deliver_fn) return MM_ERR_STATE;
+    mm_matched r{};
+    const int rc = mm_process_commit(h, group_offsets, entries, n_groups, &r);
+    if (rc != MM_OK) return rc;
+    deliver_now(m, h, r, summary);
+    return MM_OK;
+}
+int mm_delivery_flush(void* h) {
+    if (!h) return MM_ERR_ARG;
+    return static_cast<Matchmaker*>(h)->deliver_fn ? MM_OK : MM_ERR_STATE;
 }
 
 int32_t mm_ticket_count(void* h) { auto& m = *static_cast<Matchmaker*>(h); std::lock_guard<std::mutex> lk(m.mu); return (int32_t)m.indexes.size(); }
