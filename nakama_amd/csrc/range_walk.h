@@ -40,6 +40,10 @@ namespace nkm {
 struct MinTree16 {
     static constexpr uint32_t kInf = 0xFFFFFFFFu;
     std::vector<std::vector<uint32_t>> lv;  // lv[0]: leaves; lv[k][i] = min of lv[k-1][16i, 16i + 16)
+    // the levels' arrays, cached after build (range_min / set read them per
+    // level: one load instead of the vector-of-vectors' two)
+    uint32_t* lp[8] = {};
+    uint32_t nlev = 0;
     void build(const uint32_t* v, uint32_t n) {
         size_t L = 1;
         for (uint32_t m = n; m > 16; m = (m + 15) / 16) L++;
@@ -60,6 +64,8 @@ struct MinTree16 {
                 lv[k][i] = x;
             }
         }
+        nlev = (uint32_t)L;
+        for (size_t k = 0; k < L; k++) lp[k] = lv[k].data();
     }
     // fixed 16-wide loops: vector mins (4 x 128 bits, or 2 x 256 bits in the
     // walk's AVX2 instantiation, RangeRun::walk)
@@ -81,7 +87,7 @@ struct MinTree16 {
     NKM_INLINE uint32_t range_min(uint32_t a, uint32_t b) const {
         uint32_t m = kInf;
         for (size_t k = 0; a < b; k++) {
-            const uint32_t* v = lv[k].data();
+            const uint32_t* v = lp[k];
             if ((a >> 4) == ((b - 1) >> 4)) {
                 const uint32_t x = min16_in(v + (a & ~15u), a & 15, ((b - 1) & 15) + 1);
                 return x < m ? x : m;
@@ -102,12 +108,12 @@ struct MinTree16 {
         return m;
     }
     NKM_INLINE void set(uint32_t i, uint32_t x) {
-        lv[0][i] = x;
-        for (size_t k = 1; k < lv.size(); k++) {
+        lp[0][i] = x;
+        for (uint32_t k = 1; k < nlev; k++) {
             const uint32_t blk = i >> 4;
-            const uint32_t nm = min16(lv[k - 1].data() + ((size_t)blk << 4));
-            if (lv[k][blk] == nm) return;  // the parents are unchanged
-            lv[k][blk] = nm;
+            const uint32_t nm = min16(lp[k - 1] + ((size_t)blk << 4));
+            if (lp[k][blk] == nm) return;  // the parents are unchanged
+            lp[k][blk] = nm;
             i = blk;
         }
     }
