@@ -786,7 +786,7 @@ __global__ __launch_bounds__(kBlock) void mscan_hash_kernel(DStore st, DMScan ms
                                                             uint32_t* __restrict__ scratch,
                                                             uint32_t* __restrict__ counts, uint32_t c0) {
     static_assert(NF >= 1 && NF <= 4, "1-4 required fields");
-    static_assert(!CONTIG || kMJ == 4 || kMJ == 8, "runs of 4 or 8 candidates");
+    static_assert(!CONTIG || kMJ == 2 || kMJ == 4 || kMJ == 8, "runs of 2, 4 or 8 candidates");
     constexpr int kMChunk = kMJ * kBlock;
     constexpr uint32_t kNone = kMHashEmpty;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -1824,7 +1824,7 @@ hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_b
     for (uint32_t f = 0; f < ms.n_fields && f < 4; f++) cells *= ms.dsize ? (uint64_t)ms.drng[f] : 1u;
     if (ms.n_sigs > kMHashSigs || ms.hmask + 1 > kMHashCap || ((ms.hmask + 1) & ms.hmask) || ms.hmask + 1 < 2 * ms.n_sigs ||
         ms.n_fields < 1 || ms.n_fields > 4 || ms.chunk % kBlock || (ms.chunk & (ms.chunk - 1)) ||
-        (ms.contig ? mj != 4 && mj != 8 : mj != 2 && mj != 4) ||
+        (ms.contig ? mj != 2 && mj != 4 && mj != 8 : mj != 2 && mj != 4) ||
         covered < (ms.contig ? (uint64_t)ms.src_off + ms.src_len : (uint64_t)ms.src_len) ||
         ms.dsize > kMHashGrid || (ms.dsize && cells != ms.dsize))
         return hipErrorInvalidValue;
@@ -1845,6 +1845,8 @@ hipError_t launch_mscan_hash(const DStore& st, const DMScan& ms, const void* d_b
     do {                                                                      \
         if (ms.contig && mj == 8 && count_only) NKM_MHASH_K(NF, 8, true, true); \
         else if (ms.contig && mj == 8) NKM_MHASH_K(NF, 8, true, false);       \
+        else if (ms.contig && mj == 2 && count_only) NKM_MHASH_K(NF, 2, true, true); \
+        else if (ms.contig && mj == 2) NKM_MHASH_K(NF, 2, true, false);       \
         else if (ms.contig && count_only) NKM_MHASH_K(NF, 4, true, true);     \
         else if (ms.contig) NKM_MHASH_K(NF, 4, true, false);                  \
         else if (mj == 4) NKM_MHASH_K(NF, 4, false, false);                   \
@@ -1874,11 +1876,11 @@ uint64_t mscan_hash_work_words(const DMScan& ms) {
     return (uint64_t)ms.n_chunks * w1 + (uint64_t)(ms.n_chunks + 1) * w1 + (uint64_t)ms.n_chunks * ms.chunk;
 }
 // candidates per lane: gathered 2 or 4 (NKM_MHASH_J, default 4); contiguous
-// 4 or 8 (NKM_MCONTIG_J, default 4)
+// 2, 4 or 8 (NKM_MCONTIG_J, default 4)
 int mscan_hash_chunk_len(bool contig) {
     const char* e = std::getenv(contig ? "NKM_MCONTIG_J" : "NKM_MHASH_J");
     const int j = e ? std::atoi(e) : 0;
-    return (contig ? (j == 8 ? 8 : 4) : (j == 2 ? 2 : 4)) * kBlock;
+    return (contig ? (j == 8 ? 8 : j == 2 ? 2 : 4) : (j == 2 ? 2 : 4)) * kBlock;
 }
 
 // Candidates per lane: 2 (C3 1M measured 21.7 us at 2, 24.6 at 4, 35.2 at 8

@@ -232,12 +232,12 @@ def test_hashed_mscan(config, n, cfg, kernel, monkeypatch):
     assert rs[0].eval_kernel == want
 
 
-@pytest.mark.parametrize("contig,j,grid", [("0", "2", "1"), ("0", "4", "1"), ("1", "4", "1"), ("1", "8", "1"),
-                                           ("0", "4", "0"), ("1", "4", "0"), ("1", "8", "0")])
+@pytest.mark.parametrize("contig,j,grid", [("0", "2", "1"), ("0", "4", "1"), ("1", "2", "1"), ("1", "4", "1"),
+                                           ("1", "8", "1"), ("0", "4", "0"), ("1", "4", "0"), ("1", "8", "0")])
 def test_hashed_mscan_chunk_lengths(contig, j, grid, monkeypatch):
     """Every chunk shape of the hashed scan: gathered through the scan order
-    (2 or 4 candidates per lane) and over contiguous slot runs (4 or 8 per
-    lane, 16-B column loads), with ragged first and last chunks (the second
+    (2 or 4 candidates per lane) and over contiguous slot runs (2, 4 or 8
+    per lane, vector column loads), with ragged first and last chunks (the second
     pass starts past a matched prefix), through the key grid or the cuckoo
     table (NKM_MHGRID).  Lists downloaded (NKM_LISTPROOF=0), so every list
     is placed and read."""
@@ -252,7 +252,7 @@ def test_hashed_mscan_chunk_lengths(contig, j, grid, monkeypatch):
 
 @pytest.mark.parametrize("mode,count", [("0", "1"), ("1", "1"), ("1", "0"), ("2", "1")])
 @pytest.mark.parametrize("config,n,contig", [(3, 20_000, "1"), (4, 20_000, "1"), (3, 7_777, "0"),
-                                             (4, 9_999, "0")])
+                                             (4, 9_999, "0"), (3, 20_000, "j2")])
 def test_proven_mscan_lists(config, n, contig, mode, count, monkeypatch, capfd):
     """Hashed-scan lists proven equal to their search's batch rows are not
     downloaded (Core::list_proof_mode_): NKM_LISTPROOF=1 (default) skips
@@ -263,6 +263,9 @@ def test_proven_mscan_lists(config, n, contig, mode, count, monkeypatch, capfd):
     equal to the oracle's either way; the profile line reports the proven
     lists."""
     set_kernel(monkeypatch, "mhash")
+    if contig == "j2":  # contiguous, 2 candidates per lane
+        contig = "1"
+        monkeypatch.setenv("NKM_MCONTIG_J", "2")
     monkeypatch.setenv("NKM_MCONTIG", contig)
     monkeypatch.setenv("NKM_LISTPROOF", mode)
     monkeypatch.setenv("NKM_MHCOUNT", count)

@@ -147,7 +147,7 @@ static int run_shape(uint32_t n, int nmode, int nregion, uint4* evict, size_t ev
     // grid: the key-grid lookup (else the cuckoo table); loop 2: counts only
     struct Shape { int contig, j, grid, loop; };
     const Shape shapes[] = {{0, 4, 0, 0}, {0, 4, 1, 0}, {1, 4, 0, 0}, {1, 4, 1, 0}, {1, 8, 0, 0}, {1, 8, 1, 0},
-                            {1, 4, 1, 2}, {1, 8, 1, 2}, {1, 4, 0, 2}};
+                            {1, 2, 1, 0}, {1, 4, 1, 2}, {1, 8, 1, 2}, {1, 2, 1, 2}, {1, 4, 0, 2}};
     for (const Shape& sh : shapes) {
         for (uint32_t dbg : {0u, 1u, 2u}) {
             if (sh.loop && dbg) continue;
