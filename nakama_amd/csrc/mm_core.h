@@ -53,7 +53,7 @@ hipError_t launch_pairs(const DStore& st, const uint32_t* d_pairs, uint32_t n, u
 // d_cnt); else the write pass (entries as word pairs, group ends + e0).
 hipError_t launch_enum(const DEnumRow* d_rows, const DEnumHit* d_hits, const DEnumItem* d_items, uint32_t n_items,
                        uint32_t* d_cnt, const uint64_t* d_base, uint32_t e0, uint32_t* d_ents, uint32_t* d_off,
-                       hipStream_t stream);
+                       hipStream_t stream, bool slots = false);
 int var_k_capacity();
 hipError_t launch_scan(const DStore& st, const DGroup* d_chunks, int n_chunks, DHit* d_scratch, DGroupResult* d_cres,
                        hipStream_t stream, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
@@ -1112,6 +1112,15 @@ public:
     PinnedArray<DEnumItem> h_eitems_;
     PinnedArray<uint32_t> h_ecnt_;
     PinnedArray<uint64_t> h_ebase_;
+    // the candidates straight into the result arena (fill_custom_direct):
+    // two pinned chunk buffers of entry word pairs, the group ends, events
+    bool custom_direct_mode_ = true;  // NKM_CDIRECT=0: candidate list + fill_matched
+    bool custom_filled_ = false;      // this pass's candidates are in the arena
+    size_t custom_filled_g_ = 0, custom_filled_e_ = 0;
+    PinnedArray<uint32_t> h_ech_[2];
+    PinnedArray<uint32_t> h_eoff_;
+    hipEvent_t ech_ev_[2] = {nullptr, nullptr};
+    void fill_custom_direct(size_t G, size_t E, bool slots);
 };
 
 }  // namespace nkm

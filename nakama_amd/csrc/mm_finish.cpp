@@ -319,6 +319,95 @@ void Core::fill_matched(const GroupList& groups, mm_matched* out,
     out->reserved2 = arena ? 1 : (int64_t)(intptr_t)buf;  // 1: the handle's arena
 }
 
+// processCustom's candidates (enum_kernel's write pass: entries as (slot,
+// presence) word pairs in d_eents_, group ends in d_eoff_) straight into the
+// result arena, which the caller claimed: the group ends first, then the
+// entries in chunks through two pinned buffers — chunk k + 1 copies while the
+// workers turn chunk k into result entries (ticket string, presence) and set
+// the CreatedAt of every group that ends in it.  Replaces one pageable copy
+// of the whole list (1.12 GB on C5's 35M candidates) plus fill_matched's pass
+// over it.  process() then hands the arena out (custom_filled_).
+void Core::fill_custom_direct(size_t G, size_t E, bool slots) {
+    // slots: the write pass gave slot ids alone (every presence index 0) and
+    // a byte of size per group (enum_kernel<false, true>); else (slot,
+    // presence) word pairs and group ends
+    WorkPool& wp = workers();
+    if (!ech_ev_[0])
+        for (auto& e : ech_ev_) NKM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (out_offs_.size() < G + 1) grow_to(out_offs_, G + 1);
+    if (out_ents_.size() < E) grow_to(out_ents_, E);
+    if (out_created_.size() < G) grow_to(out_created_, G);
+    int32_t* offs = out_offs_.data();
+    mm_entry_ref* ents = out_ents_.data();
+    int64_t* gc = out_created_.data();
+    const size_t off_bytes = slots ? G : G * sizeof(uint32_t);
+    h_eoff_.reserve((off_bytes + 3) / 4);
+    NKM_HIP(hipMemcpyAsync(h_eoff_.p, d_eoff_.p, off_bytes, hipMemcpyDeviceToHost, stream_));
+    const size_t W = slots ? 1 : 2;  // words per entry
+    const size_t kChunk = (size_t)1 << 23;  // entries per chunk (32 / 64 MB)
+    const size_t nck = (E + kChunk - 1) / kChunk;
+    for (auto& b : h_ech_) b.reserve(W * std::min(kChunk, E));
+    auto issue = [&](size_t k) {
+        const size_t lo = k * kChunk, n = std::min(kChunk, E - lo);
+        NKM_HIP(hipMemcpyAsync(h_ech_[k & 1].p, d_eents_.p + W * lo, n * W * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               stream_));
+        NKM_HIP(hipEventRecord(ech_ev_[k & 1], stream_));
+    };
+    issue(0);
+    if (nck > 1) issue(1);
+    NKM_HIP(hipStreamSynchronize(stream_));  // the group ends / sizes (and the first chunks) are down
+    const size_t nch = (size_t)wp.size() * 2;
+    if (slots) {  // sizes -> ends: chunk sums, then every chunk's running ends
+        const uint8_t* sz = reinterpret_cast<const uint8_t*>(h_eoff_.p);
+        std::vector<uint64_t> at(nch + 1, 0);
+        wp.run(nch, [&](size_t c) {
+            uint64_t t = 0;
+            for (size_t g = G * c / nch; g < G * (c + 1) / nch; g++) t += sz[g];
+            at[c + 1] = t;
+        });
+        for (size_t c = 0; c < nch; c++) at[c + 1] += at[c];
+        if (at[nch] != E) throw std::logic_error("processCustom: group sizes do not add up to the entries");
+        wp.run(nch, [&](size_t c) {
+            uint64_t t = at[c];
+            if (c == 0) offs[0] = 0;
+            for (size_t g = G * c / nch; g < G * (c + 1) / nch; g++) offs[g + 1] = (int32_t)(t += sz[g]);
+        });
+    } else {
+        wp.run(nch, [&](size_t c) {
+            const size_t g0 = G * c / nch, g1 = G * (c + 1) / nch;
+            if (c == 0) offs[0] = 0;
+            for (size_t g = g0; g < g1; g++) offs[g + 1] = (int32_t)h_eoff_.p[g];
+        });
+    }
+    for (size_t k = 0; k < nck; k++) {
+        NKM_HIP(hipEventSynchronize(ech_ev_[k & 1]));
+        const uint32_t* w = h_ech_[k & 1].p;
+        const size_t lo = k * kChunk, n = std::min(kChunk, E - lo);
+        wp.run(nch, [&](size_t c) {
+            const size_t a = lo + n * c / nch, b = lo + n * (c + 1) / nch;
+            // streaming stores: 2.24 GB of result entries on C5 + override
+            // never fit a cache, and a normal store reads each line first
+            typedef long long v2i __attribute__((vector_size(16)));
+            static_assert(sizeof(mm_entry_ref) == 16 && alignof(mm_entry_ref) <= 16, "16-B result entries");
+            v2i* dst = reinterpret_cast<v2i*>(ents);
+            for (size_t i = a; i < b; i++) {
+                const uint32_t slot = w[W * (i - lo)];
+                const long long pi = slots ? 0 : (long long)(uint32_t)w[W * (i - lo) + 1];  // presence_index, reserved = 0
+                const v2i v = {(long long)(intptr_t)tk_ptr_[slot], pi};
+                __builtin_nontemporal_store(v, dst + i);
+            }
+            std::atomic_thread_fence(std::memory_order_seq_cst);  // this worker's streaming stores drained
+            // groups whose last entry (the searching ticket) lies in [a, b): end in (a, b]
+            size_t g = (size_t)(std::upper_bound(offs + 1, offs + 1 + G, (int32_t)a) - (offs + 1));
+            for (; g < G && (size_t)offs[g + 1] <= b; g++) gc[g] = created_[w[W * ((size_t)offs[g + 1] - 1 - lo)]];
+        });
+        if (k + 2 < nck) issue(k + 2);  // into the buffer just converted
+    }
+    custom_filled_ = true;
+    custom_filled_g_ = G;
+    custom_filled_e_ = E;
+}
+
 void Core::free_matched(mm_matched* out) {
     if (!out) return;
     if (out->reserved2 == 1) {

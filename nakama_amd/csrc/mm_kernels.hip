@@ -1319,7 +1319,11 @@ __global__ __launch_bounds__(kBlock) void last_hits_kernel(const DGroup* __restr
 // Sessions are exclusive on this path (no two live tickets share one), so the
 // pairwise session test (:509-519) never rejects; the mutual validateMatch
 // test is a mask test: every member's pm covers the other members.
-template <bool COUNT>
+// SLOTS (every ticket holds one presence, so every presence index is 0):
+// entries as slot ids alone and each group's size as one byte (<= 63 entries)
+// in place of its end offset — half the entry bytes and a quarter of the
+// offsets' for the host copy.
+template <bool COUNT, bool SLOTS = false>
 __global__ __launch_bounds__(kBlock) void enum_kernel(const DEnumRow* __restrict__ rows,
                                                       const DEnumHit* __restrict__ hits,
                                                       const DEnumItem* __restrict__ items, uint32_t n_items,
@@ -1364,6 +1368,12 @@ __global__ __launch_bounds__(kBlock) void enum_kernel(const DEnumRow* __restrict
         if (COUNT) {
             ng++;
             ne += (uint32_t)hc;
+            continue;
+        }
+        if (SLOTS) {
+            for (uint64_t b = m; b; b &= b - 1, ek++) ents[ek] = h[__builtin_ctzll(b)].slot;
+            ents[ek++] = row.T;
+            reinterpret_cast<uint8_t*>(off)[gk++] = (uint8_t)hc;
             continue;
         }
         for (uint64_t b = m; b; b &= b - 1) {
@@ -1704,12 +1714,15 @@ hipError_t launch_clear_alive(uint8_t* d_alive, const uint32_t* d_slots, uint32_
 
 hipError_t launch_enum(const DEnumRow* d_rows, const DEnumHit* d_hits, const DEnumItem* d_items, uint32_t n_items,
                        uint32_t* d_cnt, const uint64_t* d_base, uint32_t e0, uint32_t* d_ents, uint32_t* d_off,
-                       hipStream_t stream) {
+                       hipStream_t stream, bool slots) {
     if (n_items == 0) return hipSuccess;
     const dim3 grid((n_items + kBlock - 1) / kBlock);
     if (d_base == nullptr)
         hipLaunchKernelGGL(enum_kernel<true>, grid, dim3(kBlock), 0, stream, d_rows, d_hits, d_items, n_items, d_cnt,
                            nullptr, 0u, nullptr, nullptr);
+    else if (slots)
+        hipLaunchKernelGGL((enum_kernel<false, true>), grid, dim3(kBlock), 0, stream, d_rows, d_hits, d_items, n_items,
+                           nullptr, d_base, e0, d_ents, d_off);
     else
         hipLaunchKernelGGL(enum_kernel<false>, grid, dim3(kBlock), 0, stream, d_rows, d_hits, d_items, n_items, nullptr,
                            d_base, e0, d_ents, d_off);

@@ -2032,15 +2032,62 @@ int Core::process_custom(GroupList& cands, UVec<uint32_t>& expired,
                 const auto te2 = eclk::now();
                 h_ebase_.reserve(2 * nitem);  // exclusive scan: every item's first group and entry
                 uint64_t G = 0, E = 0;
-                for (size_t k = 0; k < nitem; k++) {
-                    h_ebase_.p[2 * k] = G;
-                    h_ebase_.p[2 * k + 1] = E;
-                    G += h_ecnt_.p[2 * k];
-                    E += h_ecnt_.p[2 * k + 1];
+                const size_t sch = nch > 1 && nitem >= 65536 ? (size_t)wp.size() : 1;  // chunk sums, then bases
+                std::vector<uint64_t> cg(sch + 1, 0), ce(sch + 1, 0);
+                auto scan_sum = [&](size_t c) {
+                    uint64_t g = 0, e = 0;
+                    for (size_t k = nitem * c / sch; k < nitem * (c + 1) / sch; k++) {
+                        g += h_ecnt_.p[2 * k];
+                        e += h_ecnt_.p[2 * k + 1];
+                    }
+                    cg[c + 1] = g;
+                    ce[c + 1] = e;
+                };
+                auto scan_put = [&](size_t c) {
+                    uint64_t g = cg[c], e = ce[c];
+                    for (size_t k = nitem * c / sch; k < nitem * (c + 1) / sch; k++) {
+                        h_ebase_.p[2 * k] = g;
+                        h_ebase_.p[2 * k + 1] = e;
+                        g += h_ecnt_.p[2 * k];
+                        e += h_ecnt_.p[2 * k + 1];
+                    }
+                };
+                if (sch > 1) wp.run(sch, scan_sum);
+                else scan_sum(0);
+                for (size_t c = 0; c < sch; c++) {
+                    cg[c + 1] += cg[c];
+                    ce[c + 1] += ce[c];
                 }
+                if (sch > 1) wp.run(sch, scan_put);
+                else scan_put(0);
+                G = cg[sch];
+                E = ce[sch];
                 const size_t g0 = cands.size(), e0 = cands.ents.size();
                 if (e0 + E >= UINT32_MAX) throw std::length_error("processCustom: more than 2^32 candidate entries");
-                if (G) {
+                // The whole candidate list from the device straight into the
+                // result arena (custom_direct_): the entries come down in
+                // pinned chunks while the workers turn the previous chunk into
+                // result entries, instead of one pageable copy into the
+                // candidate list and a second pass (fill_matched) over it.
+                const bool direct = G && g0 == 0 && e0 == 0 && par && custom_direct_mode_ && !row_shard() &&
+                                    !out_in_use_.exchange(true);
+                if (direct) {
+                    struct Release {  // the arena goes back unless the result is handed out
+                        std::atomic<bool>& f;
+                        bool keep = false;
+                        ~Release() { if (!keep) f.store(false); }
+                    } rel{out_in_use_};
+                    d_ebase_.reserve(2 * nitem, false);
+                    d_eents_.reserve(2 * E, false);
+                    d_eoff_.reserve(G, false);
+                    NKM_HIP(hipMemcpyAsync(d_ebase_.p, h_ebase_.p, 2 * nitem * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                           stream_));
+                    const bool slots = max_pres_ <= 1;  // every presence index 0: slot ids + group sizes
+                    NKM_HIP(launch_enum(d_erows_.p, d_ehits_.p, d_eitems_.p, (uint32_t)nitem, nullptr, d_ebase_.p, 0u,
+                                        d_eents_.p, d_eoff_.p, stream_, slots));
+                    fill_custom_direct(G, E, slots);
+                    rel.keep = true;
+                } else if (G) {
                     static_assert(sizeof(GroupList::Entry) == 8, "(slot, presence index) word pairs");
                     d_ebase_.reserve(2 * nitem, false);
                     d_eents_.reserve(2 * E, false);
@@ -2147,6 +2194,7 @@ int Core::process(mm_matched* out) {
             }
             c.pass_running_ = false;
             c.custom_open_ = false;
+            c.custom_filled_ = false;
             c.reset_pass_scratch();  // a walk may have thrown with its flags set
             c.sel_.assign(c.sel_.size(), 0);
             c.apply_defer_.clear();
@@ -2160,7 +2208,7 @@ int Core::process(mm_matched* out) {
         const auto t2 = std::chrono::steady_clock::now();
         lk.lock();
         out->n_expired = (int32_t)expired.size();
-        if (groups.empty()) {
+        if (groups.empty() && !custom_filled_) {
             apply_pending();
             GroupList none;
             finish_pass(expired, none, true);
@@ -2171,15 +2219,26 @@ int Core::process(mm_matched* out) {
             // mm_process_commit hands back the override's choice
             custom_open_ = true;
             custom_expired_ = expired;
-            fill_matched(groups, out, true);
+            if (custom_filled_) {  // the candidates are in the arena already (fill_custom_direct)
+                out->group_created = out_created_.data();
+                out->n_groups = (int32_t)custom_filled_g_;
+                out->n_entries = (int32_t)custom_filled_e_;
+                out->group_offsets = out_offs_.data();
+                out->entries = out_ents_.data();
+                out->is_candidates = 1;
+                out->reserved2 = 1;  // the handle's arena
+                custom_filled_ = false;
+            } else {
+                fill_matched(groups, out, true);
+            }
         }
         if (std::getenv("NKM_PROFILE")) {
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
             std::fprintf(stderr,
                          "[nkm] custom: sync %.2f ms | pass %.2f ms (build %.2f, search %.2f ms [kernel %.2f ms], "
-                         "combos %.2f ms, %d refetches) | candidates %zu (%zu entries) | fill %.2f ms\n",
+                         "combos %.2f ms, %d refetches) | candidates %d (%d entries) | fill %.2f ms\n",
                          ms(t0, t1), ms(t1, t2), stats.assemble_ms, stats.search_ms, stats.eval_ms(), stats.replay_ms,
-                         stats.refetches, groups.size(), groups.ents.size(), ms(t2, std::chrono::steady_clock::now()));
+                         stats.refetches, out->n_groups, out->n_entries, ms(t2, std::chrono::steady_clock::now()));
         }
     } else {
         const auto t1 = std::chrono::steady_clock::now();

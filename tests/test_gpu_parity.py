@@ -582,6 +582,43 @@ def test_pool_runs_replay(config, n, passes, rpack, runs, monkeypatch, capfd):
     assert ("pool runs:" in capfd.readouterr().err) == (runs == "1")
 
 
+@pytest.mark.parametrize("direct", ["1", "0"])
+@pytest.mark.parametrize("config,n", [(5, 5000), (6, 100), (13, 900)])
+def test_custom_candidates_into_result_arena(config, n, direct, monkeypatch):
+    """processCustom's device candidates written straight into the result
+    arena in pinned chunks (NKM_CDIRECT=1, forced at any size by
+    NKM_PARALLEL=force) or through the candidate list and fill_matched (0):
+    the override sees the oracle's candidate list either way, and a second
+    pass's result while the first is still held takes private copies."""
+    monkeypatch.setenv("NKM_PARALLEL", "force")
+    monkeypatch.setenv("NKM_CDIRECT", direct)
+    monkeypatch.setenv("NKM_DEVENUM", "1")
+    seen = {}
+
+    def rec(tag):
+        def f(c):
+            seen[tag] = [list(x) for x in c]
+            return first_disjoint(c)
+        return f
+
+    ts = synth.TicketSet(config, n)
+    gpu = capi.Matchmaker(product_lib(), override=rec("g"), max_intervals=2, rev_precision=True)
+    orc = capi.Matchmaker(harness.oracle_lib(), override=rec("o"), max_intervals=2, rev_precision=True)
+    try:
+        ts.insert_into(gpu)
+        ts.insert_into(orc)
+        for _ in range(2):
+            seen.clear()
+            g, o = gpu.Process(), orc.Process()
+            assert seen.get("g") == seen.get("o"), "processCustom candidate lists differ"
+            assert g == o
+            assert state(gpu) == state(orc)
+    finally:
+        gpu.close()
+        orc.close()
+        ts.close()
+
+
 def first_disjoint(cands):
     """The deterministic override of SURVEY.md 8(d) C5: keep candidates, in
     order, that do not overlap an already kept one."""
