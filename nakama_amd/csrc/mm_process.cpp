@@ -2194,6 +2194,7 @@ int Core::process(mm_matched* out) {
             }
             c.pass_running_ = false;
             c.custom_open_ = false;
+            if (c.custom_filled_) c.out_in_use_.store(false);  // the candidates' arena was never handed out
             c.custom_filled_ = false;
             c.reset_pass_scratch();  // a walk may have thrown with its flags set
             c.sel_.assign(c.sel_.size(), 0);
