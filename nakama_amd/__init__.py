@@ -12,7 +12,8 @@ from .capi import (ErrMatchmakerDelete, ErrMatchmakerDuplicateSession, ErrMatchm
                    ErrMatchmakerNotAvailable, ErrMatchmakerQueryInvalid, ErrMatchmakerTicketNotFound,
                    ErrMatchmakerTooManyTickets, ErrMatchmakerUnsupportedQuery, MatchmakerError, Presence, Ticket)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnakama_mm.so")
+# NKM_LIBRARY: another build of the same library (A/B runs of tools/ scripts)
+LIB_PATH = os.environ.get("NKM_LIBRARY") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnakama_mm.so")
 _lib = None
 
 

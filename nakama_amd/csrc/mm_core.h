@@ -400,6 +400,72 @@ struct PostingRange {
     uint32_t off = 0, len = 0, head = 0;  // head: first entry possibly alive
 };
 
+// The posting-list directory, (field << 32 | term) -> PostingRange: one flat
+// open-addressed table (linear probing, power-of-two size, at most half
+// full): a lookup reads one slot instead of unordered_map's bucket + node.
+// Keys are scrambled in blocks of eight: eight consecutive dictionary ids of
+// a field sit in consecutive slots (C5's buckets, interned in arrival order
+// and looked up in row order, then read a few lines per 64 rows), the blocks
+// spread over the table so no field's ids form one long probe run.  A fully
+// scrambling hash measured +0.8 ms on C5's assembly
+// (profiles/r05/r05ae_c5_pruns.txt).  Keys never equal kEmpty (fields fit 16
+// bits).  Iteration visits the live slots in table order.
+struct PostingMap {
+    static constexpr uint64_t kEmpty = ~0ull;
+    struct Slot {
+        uint64_t first = kEmpty;
+        PostingRange second;
+    };
+    std::vector<Slot> slots;
+    size_t used = 0;
+
+    static size_t mix(uint64_t k) {
+        uint64_t b = k >> 3;
+        b ^= b >> 33;
+        b *= 0xff51afd7ed558ccdull;
+        b ^= b >> 33;
+        return (size_t)((b << 3) | (k & 7));
+    }
+    void clear() {
+        for (Slot& s : slots) s = Slot{};
+        used = 0;
+    }
+    PostingRange* find(uint64_t k) {
+        if (slots.empty()) return nullptr;
+        const size_t m = slots.size() - 1;
+        for (size_t i = mix(k) & m;; i = (i + 1) & m) {
+            if (slots[i].first == k) return &slots[i].second;
+            if (slots[i].first == kEmpty) return nullptr;
+        }
+    }
+    const PostingRange* find(uint64_t k) const { return const_cast<PostingMap*>(this)->find(k); }
+    PostingRange& operator[](uint64_t k) {
+        if ((used + 1) * 2 > slots.size()) grow();
+        const size_t m = slots.size() - 1;
+        size_t i = mix(k) & m;
+        while (slots[i].first != k && slots[i].first != kEmpty) i = (i + 1) & m;
+        if (slots[i].first == kEmpty) {
+            slots[i].first = k;
+            used++;
+        }
+        return slots[i].second;
+    }
+    template <class F> void for_each(F&& f) {
+        for (Slot& s : slots)
+            if (s.first != kEmpty) f(s.second);
+    }
+
+private:
+    void grow() {
+        std::vector<Slot> old;
+        old.swap(slots);
+        slots.assign(std::max<size_t>(64, old.size() * 2), Slot{});
+        used = 0;
+        for (Slot& s : old)
+            if (s.first != kEmpty) (*this)[s.first] = s.second;
+    }
+};
+
 // Identity of a signature (the sig_idx_ hash): query kind, the searching
 // ticket's filters and the compiled clauses.
 uint64_t sig_clause_hash(const DClause* dc, size_t n);
@@ -737,6 +803,7 @@ private:
     std::vector<uint32_t> pool_remap_;  // dictionary id -> pool (one-field pool keys)
     std::unique_ptr<std::atomic<uint32_t>[]> pool_first_;  // dictionary id -> first search with it
     size_t pool_first_cap_ = 0;
+    std::vector<uint32_t> run_terms_;  // plan_packed_runs: per row its pool term | foreign bit
     UVec<uint32_t> pool_cnt_;            // plan_pools: [chunk][pool] row counts, then positions
     UVec<uint8_t> pool_foreign_;         // plan_pools: [chunk][pool] a row not known to self-match
     ParPlan par_plan_;
@@ -845,6 +912,8 @@ private:
     bool assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t cap, UVec<uint32_t>& brow, PackBatch& pb);
     PackLayout run_packed(const PackBatch& pb, PassStats& stats, const std::function<void()>& overlap);
     bool plan_packed(size_t n, const UVec<uint32_t>& brow, ParPlan& P, PassStats& stats);
+    int plan_packed_runs(size_t n, const UVec<uint32_t>& brow, ParPlan& P, PassStats& stats);
+    std::atomic<uint32_t>* pool_first_table(size_t nd);
     std::function<BGroup&(uint32_t)> packed_view(const PackLayout& L, const UVec<uint32_t>& brow);
     // the replay over this store (mm_process.cpp's Replay: device pages and
     // pair checks), for the pool workers of replay_parallel
@@ -977,7 +1046,7 @@ public:
     uint32_t order_head_ = 0;
     bool order_identity_ = false;  // order_[p] == p for every p (build_index): the hashed mscan's contiguous mode
     bool mcontig_mode_ = true;     // NKM_MCONTIG=0: never the contiguous mode
-    std::unordered_map<uint64_t, PostingRange> postings_map_;
+    PostingMap postings_map_;
     std::vector<uint32_t> postings_;
     std::vector<uint32_t> pending_dead_;  // slots to clear on the device at next sync
 
@@ -1069,6 +1138,7 @@ public:
     int mwait_us_ = 0;       // NKM_MWAIT: a pipelined merge chunk's sleep while the walks have not passed it (0: yield)
     int merge_mult_ = 8;     // NKM_MCH: pipelined merge chunks per worker (the last one is the tail after the slowest walk)
     bool runs_mode_ = true;
+    bool pruns_mode_ = true;  // NKM_PRUNS=0: packed batches always plan through plan_pools
     bool rleaf_mode_ = false;  // NKM_RLEAF=1: range pools' leaves gathered across the workers, not by each walker  // NKM_RUNS=0: pools in contiguous runs take the per-row records + merge_rows
     int32_t max_pres_ = 1;   // most presences of any ticket inserted (an entry bound of the pipelined merge)
     // NKM_FAST=0: every row takes the exact loop body, also when no two live

@@ -191,15 +191,7 @@ bool Core::plan_pools(size_t nsearch, SigOf sig_of, GroupOf group_of, RowOf row_
         // Every entry is UINT32_MAX between calls: the heads reset their own
         // on the way out, so a pass costs O(searches), not O(dictionary) (the
         // dictionary only grows: C5's bench adds 125k bucket terms a step)
-        if (pool_first_cap_ < nd) {
-            pool_first_.reset(new std::atomic<uint32_t>[nd + nd / 4]);
-            pool_first_cap_ = nd + nd / 4;
-            std::atomic<uint32_t>* f = pool_first_.get();
-            sweep(pool_first_cap_, nsch, [&](size_t, size_t lo, size_t hi) {
-                for (size_t t = lo; t < hi; t++) f[t].store(UINT32_MAX, std::memory_order_relaxed);
-            });
-        }
-        std::atomic<uint32_t>* first = pool_first_.get();
+        std::atomic<uint32_t>* first = pool_first_table(nd);
         std::vector<uint32_t>& tpool = pool_remap_;  // term -> pool (written by its head only)
         grow_to(tpool, nd);
         std::vector<size_t> heads(nsch + 1, 0);
@@ -1390,9 +1382,174 @@ PackLayout Core::run_packed(const PackBatch& pb, PassStats& stats, const std::fu
     return L;
 }
 
+// The dictionary id -> first search table plan_pools numbers pools with: all
+// entries UINT32_MAX between calls (every user resets what it set).
+std::atomic<uint32_t>* Core::pool_first_table(size_t nd) {
+    if (pool_first_cap_ < nd) {
+        pool_first_.reset(new std::atomic<uint32_t>[nd + nd / 4]);
+        pool_first_cap_ = nd + nd / 4;
+        std::atomic<uint32_t>* f = pool_first_.get();
+        WorkPool& wp = workers();
+        const size_t nch = pool_first_cap_ >= 65536 ? wp.size() : 1;
+        auto clear = [&](size_t c) {
+            for (size_t t = pool_first_cap_ * c / nch; t < pool_first_cap_ * (c + 1) / nch; t++)
+                f[t].store(UINT32_MAX, std::memory_order_relaxed);
+        };
+        if (nch > 1) wp.run(nch, clear);
+        else clear(0);
+    }
+    return pool_first_.get();
+}
+
+// plan_pools' one-key-field contiguous case in three sweeps (C5: a bucket's
+// tickets arrive together, so every pool is one run of the packed batch):
+//   A  each row's pool term (its own column when it carries its search's
+//      terms, else its signature's required term), the row check, and an
+//      atomic min of first[term] at every run start;
+//   B  per chunk: run starts, and those that are their term's first (heads);
+//   C  when every run start is a head (no term comes back after its run),
+//      each chunk numbers the runs starting in it (pool = run index, the
+//      first-appearance order plan_pools uses) and fills the CSR, the pool
+//      terms and the self flags, and clears first[] for its heads.
+// 1: planned; 0: not this shape (nothing changed; plan_pools decides);
+// -1: plan_pools would fail too (a search without the key, two terms on it,
+// a row outside its pool).  first[] is all-empty again on every return.
+int Core::plan_packed_runs(size_t n, const UVec<uint32_t>& brow, ParPlan& P, PassStats& stats) {
+    using clk = std::chrono::steady_clock;
+    const auto tp0 = clk::now();
+    WorkPool& wp = workers();
+    if (n < 2 || !par_mode_ || n < par_min(65536) || n >= (1u << 31)) return 0;
+    const auto& mts0 = sigs_[sig_[brow[0]]].must_terms;
+    if (mts0.empty()) return 0;
+    const uint16_t f0 = mts0[0].first;
+    for (auto& mt : mts0)
+        if (mt.first != f0) return 0;  // several key candidates: plan_pools
+    if (f0 >= 63 || fkind_[f0].size() != nslots()) return 0;
+    const size_t nd = dict_.size();
+    if (nd >= (1u << 31)) return 0;
+    constexpr uint32_t kForeign = 1u << 31, kTerm = kForeign - 1;
+    std::atomic<uint32_t>* first = pool_first_table(nd);
+    std::vector<uint32_t>& k1 = run_terms_;  // per row: term | kForeign
+    grow_to(k1, n);
+    grow_to(P.search_pool, n);
+    const unsigned nch = wp.size() * 2;
+    std::vector<uint8_t> bad(nch, 0);
+    const uint64_t fbit = 1ull << f0;
+    // the row's pool term and foreign flag (UINT32_MAX: plan_pools fails)
+    auto term_of = [&](size_t i) -> uint32_t {
+        const uint32_t r = brow[i];
+        const uint32_t s = sig_[r];
+        if (!(sig_fmask_[s] & fbit)) return UINT32_MAX;
+        const bool self = self_match_[r] && indexed_[r];
+        const bool kw = fkind_[f0][r] == KIND_KEYWORD;
+        if (self && kw) return (uint32_t)fval_[f0][r];
+        uint32_t t = UINT32_MAX;
+        for (auto& mt : sigs_[s].must_terms)
+            if (mt.first == f0) {
+                if (t != UINT32_MAX && t != mt.second) return UINT32_MAX;
+                t = mt.second;
+            }
+        if (t >= nd) return UINT32_MAX;
+        if (self) return t;
+        if (!kw || (uint32_t)fval_[f0][r] != t) return UINT32_MAX;  // not in its search's pool
+        return t | kForeign;
+    };
+    auto reset_first = [&] {
+        wp.run(nch, [&](size_t c) {
+            for (size_t t = pool_first_cap_ * c / nch; t < pool_first_cap_ * (c + 1) / nch; t++)
+                first[t].store(UINT32_MAX, std::memory_order_relaxed);
+        });
+    };
+    wp.run(nch, [&](size_t c) {  // A
+        const size_t lo = n * c / nch, hi = n * (c + 1) / nch;
+        if (lo >= hi) return;
+        uint32_t prev = lo ? term_of(lo - 1) : UINT32_MAX;
+        if (prev != UINT32_MAX) prev &= kTerm;
+        for (size_t i = lo; i < hi; i++) {
+            const uint32_t k = term_of(i);
+            if (k == UINT32_MAX || (k & kTerm) >= nd) { bad[c] = 1; return; }
+            k1[i] = k;
+            const uint32_t t = k & kTerm;
+            if (t != prev) {
+                uint32_t cur = first[t].load(std::memory_order_relaxed);
+                while ((uint32_t)i < cur && !first[t].compare_exchange_weak(cur, (uint32_t)i, std::memory_order_relaxed)) {
+                }
+            }
+            prev = t;
+        }
+    });
+    if (std::any_of(bad.begin(), bad.end(), [](uint8_t b) { return b != 0; })) {
+        reset_first();
+        return -1;
+    }
+    std::vector<size_t> heads(nch + 1, 0), starts(nch + 1, 0);
+    auto run_start = [&](size_t i) { return i == 0 || ((k1[i] ^ k1[i - 1]) & kTerm) != 0; };
+    wp.run(nch, [&](size_t c) {  // B
+        size_t h = 0, st = 0;
+        for (size_t i = n * c / nch; i < n * (c + 1) / nch; i++)
+            if (run_start(i)) {
+                st++;
+                h += first[k1[i] & kTerm].load(std::memory_order_relaxed) == (uint32_t)i;
+            }
+        heads[c + 1] = h;
+        starts[c + 1] = st;
+    });
+    for (unsigned c = 0; c < nch; c++) {
+        heads[c + 1] += heads[c];
+        starts[c + 1] += starts[c];
+    }
+    const size_t ng = heads[nch];
+    if (ng != starts[nch]) {  // a term returns after its run: plan_pools' counting sort
+        wp.run(nch, [&](size_t c) {
+            for (size_t i = n * c / nch; i < n * (c + 1) / nch; i++)
+                if (run_start(i)) first[k1[i] & kTerm].store(UINT32_MAX, std::memory_order_relaxed);
+        });
+        return 0;
+    }
+    grow_to(P.pool_key1, ng);
+    grow_to(P.self_rows, ng);
+    grow_to(P.pool_off, ng + 1);
+    grow_to(P.pool_rows, n);
+    wp.run(nch, [&](size_t c) {  // C: the runs starting in [lo, hi), each to its end
+        size_t p = heads[c];
+        for (size_t i = n * c / nch; i < n * (c + 1) / nch; i++) {
+            if (!run_start(i)) continue;
+            const uint32_t t = k1[i] & kTerm;
+            first[t].store(UINT32_MAX, std::memory_order_relaxed);
+            P.pool_key1[p] = t;
+            P.pool_off[p] = (uint32_t)i;
+            uint32_t fo = 0;
+            size_t j = i;
+            for (; j < n && (k1[j] & kTerm) == t; j++) {
+                fo |= k1[j];
+                P.pool_rows[j] = (uint32_t)j;
+            }
+            P.self_rows[p] = (fo & kForeign) ? 0 : 1;
+            for (size_t q = i; q < j; q++) P.search_pool[q] = (uint32_t)p;
+            p++;
+        }
+    });
+    P.pool_off[ng] = (uint32_t)n;
+    stats.par_bucket_ms += std::chrono::duration<double, std::milli>(clk::now() - tp0).count();
+    if (batch_profile_)
+        std::fprintf(stderr, "[nkm]   plan_pools: %zu pools (contiguous runs, 3 sweeps) %.2f ms\n", ng,
+                     std::chrono::duration<double, std::milli>(clk::now() - tp0).count());
+    if (ng < 2) return -1;
+    P.ng = ng;
+    P.ok = true;
+    P.runs = true;
+    return 1;
+}
+
 // plan_pools over a packed batch: search i is batch row i (its ticket's
 // signature), and every search is one row.
 bool Core::plan_packed(size_t n, const UVec<uint32_t>& brow, ParPlan& P, PassStats& stats) {
+    P.ok = false;
+    P.runs = false;
+    if (runs_mode_ && pruns_mode_) {
+        const int k = plan_packed_runs(n, brow, P, stats);
+        if (k != 0) return k > 0;
+    }
     return plan_pools(
         n, [&](size_t i) { return sig_[brow[i]]; }, [](size_t bi) { return (uint32_t)bi; },
         [&](size_t i) { return brow[i]; }, brow, P, stats);

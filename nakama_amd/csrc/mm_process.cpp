@@ -1062,11 +1062,11 @@ void Core::source_of(const Sig& s, DGroup& g, SrcChoice* ch) const {
     bool have = false;
     if (ch) ch->has_term = false;
     for (auto& mt : s.must_terms) {
-        auto it = postings_map_.find(((uint64_t)mt.first << 32) | mt.second);
+        const PostingRange* it = postings_map_.find(((uint64_t)mt.first << 32) | mt.second);
         uint32_t off = 0, len = 0;
-        if (it != postings_map_.end()) {
-            off = it->second.off + it->second.head;
-            len = it->second.len - it->second.head;
+        if (it) {
+            off = it->off + it->head;
+            len = it->len - it->head;
         }
         if (!have || len < g.src_len) {
             if (ch) { ch->has_term = true; ch->field = mt.first; ch->term = mt.second; }
@@ -1085,10 +1085,10 @@ void Core::choose_source(const Sig& s, DGroup& g, SrcChoice* ch) {
     bool have = false;
     if (ch) ch->has_term = false;
     for (auto& mt : s.must_terms) {
-        auto it = postings_map_.find(((uint64_t)mt.first << 32) | mt.second);
+        PostingRange* it = postings_map_.find(((uint64_t)mt.first << 32) | mt.second);
         uint32_t off = 0, len = 0;
-        if (it != postings_map_.end()) {
-            PostingRange& r = it->second;
+        if (it) {
+            PostingRange& r = *it;
             while (r.head < r.len && !live_[postings_[r.off + r.head]]) r.head++;  // skip the dead prefix
             off = r.off + r.head;
             len = r.len - r.head;
@@ -1321,7 +1321,6 @@ int Core::process_default(GroupList& out_groups,
             }
             struct Chunk {
                 std::vector<uint32_t> first, cnt;
-                std::vector<int32_t> lastm, maxm;
                 size_t n = 0;
                 bool self = true;  // every row carries its own search's terms (self_match_) and is indexed
             };
@@ -1332,8 +1331,10 @@ int Core::process_default(GroupList& out_groups,
                 const auto tc0 = std::chrono::steady_clock::now();
                 // thread-private until the end (adjacent Chunks share cache
                 // lines: a per-row k.n++ made this sweep 3-4x slower)
+                // (a row's MaxCount is its signature's: signatures key on the
+                // searching ticket's Min / MaxCount, Core::sig_eq — so it is
+                // read per search below, not per row)
                 std::vector<uint32_t> first, cnt(nsig, 0);
-                std::vector<int32_t> lastm(nsig, 0), maxm(nsig, 0);
                 size_t n = 0;
                 bool self = true;
                 for (size_t i = pos + nr * c / nch; i < pos + nr * (c + 1) / nch; i++) {
@@ -1341,17 +1342,12 @@ int Core::process_default(GroupList& out_groups,
                     if (sel[r] | dec[r]) continue;
                     const uint32_t sg = sig_[r];
                     if (!cnt[sg]++) first.push_back(sg);
-                    const int32_t m = std::max(2, maxc_[r]);
-                    lastm[sg] = m;
-                    maxm[sg] = std::max(maxm[sg], m);
                     self = self && self_match_[r] && indexed_[r];
                     n++;
                 }
                 Chunk& k = ch[c];
                 k.first = std::move(first);
                 k.cnt = std::move(cnt);
-                k.lastm = std::move(lastm);
-                k.maxm = std::move(maxm);
                 k.n = n;
                 k.self = self;
                 const auto tc1 = std::chrono::steady_clock::now();
@@ -1372,13 +1368,8 @@ int Core::process_default(GroupList& out_groups,
                     }
             for (BGroup& g : bg) {
                 uint64_t nrows = 0;
-                int32_t lastm = 0, maxm = 0;
-                for (unsigned c = 0; c < nch; c++)
-                    if (ch[c].cnt[g.sig]) {
-                        nrows += ch[c].cnt[g.sig];
-                        lastm = ch[c].lastm[g.sig];
-                        maxm = std::max(maxm, ch[c].maxm[g.sig]);
-                    }
+                for (unsigned c = 0; c < nch; c++) nrows += ch[c].cnt[g.sig];
+                const int32_t lastm = std::max(2, sigs_[g.sig].tmax), maxm = lastm;
                 g.nrows = (uint32_t)nrows;
                 g.d.k = cap_k(g, nrows, lastm);
                 if (retry_slot != kNoSlot && g.sig == sig_[retry_slot]) {  // the serial loop's retry capacity

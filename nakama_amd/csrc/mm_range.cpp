@@ -167,9 +167,8 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
         RangePoolHost& H = rs_pools_[p];
         DRangePool& d = H.d;
         d = DRangePool{};
-        auto it = postings_map_.find(((uint64_t)kf << 32) | H.term);
-        if (it != postings_map_.end()) {
-            PostingRange& pr = it->second;
+        if (PostingRange* it = postings_map_.find(((uint64_t)kf << 32) | H.term)) {
+            PostingRange& pr = *it;
             while (pr.head < pr.len && !live_[postings_[pr.off + pr.head]]) pr.head++;  // the dead prefix
             d.src_off = pr.off + pr.head;
             d.src_len = pr.len - pr.head;

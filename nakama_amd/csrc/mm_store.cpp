@@ -108,6 +108,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_PIPE")) pipe_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_GPIPE")) gpipe_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_RUNS")) runs_mode_ = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("NKM_PRUNS")) pruns_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_RLEAF")) rleaf_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_CDIRECT")) custom_direct_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_MWAIT")) mwait_us_ = std::max(0, std::min(1000, std::atoi(e)));
@@ -1503,9 +1504,8 @@ void Core::build_index() {
             }
         }
         uint32_t off = 0;
-        for (auto& kv : postings_map_) { kv.second.off = off; off += kv.second.len; kv.second.head = 0; }
+        postings_map_.for_each([&](PostingRange& r) { r.off = off; off += r.len; r.head = r.off; });
         postings_.resize(off);
-        for (auto& kv : postings_map_) kv.second.head = kv.second.off;
         for (uint32_t s : order_) {
             if (!live_[s]) continue;
             for (uint16_t f : pf) {
@@ -1515,7 +1515,7 @@ void Core::build_index() {
                 postings_[r.head++] = s;
             }
         }
-        for (auto& kv : postings_map_) kv.second.head = 0;
+        postings_map_.for_each([](PostingRange& r) { r.head = 0; });
     }
     order_head_ = 0;
     d_order_.reserve(std::max<size_t>(n, 1), false);

@@ -624,8 +624,10 @@ uint32_t replay_pool(ReplayCore& rp, const std::vector<uint32_t>& bis, const uin
 // pass got slower: DESIGN.md §9, profiles/r03t_spec_ab.txt.)
 
 // The per-position fields every walk reads (24 B: 2.7 records per cache line,
-// none straddling two when aligned in threes), and the exact walk's session
-// fields beside them (DenseCold).
+// none straddling two when aligned in threes).  The exact walk's session
+// fields (HotRec's sess0 / pres_off / smask) are read from the store through
+// the position's slot: only step() needs them, and not gathering them saves
+// the gather 12 of its 40 written bytes per position.
 #ifdef NKM_WALK_STATS
 inline uint64_t g_walk_stats[8];
 #define NKM_WS(k) (g_walk_stats[k]++)
@@ -641,9 +643,6 @@ struct DenseRec {
     uint32_t intervals() const { return ivl_live & 0x7fffffffu; }
     bool live() const { return (ivl_live >> 31) != 0; }
 };
-struct DenseCold {
-    uint32_t sess0, pres_off, smask;
-};
 
 // One pool's per-position copies (filled by gather, in parallel chunks).
 struct DensePool {
@@ -655,7 +654,6 @@ struct DensePool {
     uint32_t nrows = 0;
     const uint32_t* brow = nullptr;  // batch row -> slot
     std::vector<DenseRec> rec;
-    std::vector<DenseCold> cold;
     std::vector<uint32_t> slot;
     bool rows_list = false;  // BGroup::rows_list: position k's slot is brow[bis[k]], sp unfilled
     // identity: the pool's rows are its list, in list order (row j's ticket is
@@ -680,7 +678,6 @@ struct DensePool {
         front = nullptr;
         pieces = 1;
         if (rec.size() < n) rec.resize(n);
-        if (cold.size() < n) cold.resize(n);
         if (slot.size() < n) slot.resize(n);
     }
     uint32_t piece_lo(uint32_t t) const { return t >= pieces ? n : (uint32_t)((uint64_t)n * t / pieces); }
@@ -715,7 +712,6 @@ struct DensePool {
             const HotRec& h = v.hot[s];
             rec[k] = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party,
                               (uint32_t)v.intervals[s] | (v.live[s] ? 0x80000000u : 0u)};
-            cold[k] = DenseCold{h.sess0, h.pres_off, h.smask};
             slot[k] = s;
             if (map) pos_of[s] = k;
         }
@@ -783,16 +779,13 @@ struct DenseRun {
         row_at(P, pos_of, j, T, kT);
         if (kT != kNoSlot && sel[kT]) return false;
         DenseRec rt;
-        DenseCold rc;
+        const HotRec& rc = v.hot[T];  // the session fields
         const uint32_t* tpres = v.pres_sess;
         if (kT != kNoSlot) {
             rt = P.rec[kT];
-            rc = P.cold[kT];
         } else {
-            const HotRec& h = v.hot[T];
-            rt = DenseRec{h.count, h.minc, h.maxc, h.cm, h.party,
+            rt = DenseRec{rc.count, rc.minc, rc.maxc, rc.cm, rc.party,
                           (uint32_t)v.intervals[T] | (v.live[T] ? 0x80000000u : 0u)};
-            rc = DenseCold{h.sess0, h.pres_off, h.smask};
         }
         const bool last = (int)rt.intervals() + 1 >= max_intervals || rt.minc == rt.maxc;
         const int tcount = rt.count, tmax = rt.maxc, tmin = rt.minc, tcm = rt.cm;
@@ -803,7 +796,7 @@ struct DenseRun {
                 if (tpres[rc.pres_off + q] == sess) return true;
             return false;
         };
-        auto h_has = [&](const DenseRec& h, const DenseCold& c, uint32_t sess) {
+        auto h_has = [&](const DenseRec& h, const HotRec& c, uint32_t sess) {
             if (h.count == 1) return c.sess0 == sess;
             for (int q = 0; q < h.count; q++)
                 if (v.pres_sess[c.pres_off + q] == sess) return true;
@@ -818,7 +811,7 @@ struct DenseRun {
             if (i == kT || sel[i]) continue;
             need(P, i);
             const DenseRec& hh = P.rec[i];
-            const DenseCold& hc0 = P.cold[i];
+            const HotRec& hc0 = v.hot[P.slot[i]];  // session fields only
             if (tparty != kNoParty && hh.party == tparty) continue;                      // :80-85
             if (tmax < hh.maxc && (int)hh.intervals() + proc[i] <= max_intervals) continue;  // :150-153
             if (!v.sessions_exclusive && (rc.smask & hc0.smask)) {                       // :155-165
