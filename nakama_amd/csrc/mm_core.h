@@ -803,6 +803,7 @@ private:
     std::vector<uint32_t> pool_remap_;  // dictionary id -> pool (one-field pool keys)
     std::unique_ptr<std::atomic<uint32_t>[]> pool_first_;  // dictionary id -> first search with it
     size_t pool_first_cap_ = 0;
+    UVec<uint32_t> pool_cuts_;  // pipelined merge: [pool][chunk] the walk's records before the chunk's end
     std::vector<uint32_t> run_terms_;  // plan_packed_runs: per row its pool term | foreign bit
     UVec<uint32_t> pool_cnt_;            // plan_pools: [chunk][pool] row counts, then positions
     UVec<uint8_t> pool_foreign_;         // plan_pools: [chunk][pool] a row not known to self-match
@@ -1138,7 +1139,8 @@ public:
     int mwait_us_ = 0;       // NKM_MWAIT: a pipelined merge chunk's sleep while the walks have not passed it (0: yield)
     int merge_mult_ = 8;     // NKM_MCH: pipelined merge chunks per worker (the last one is the tail after the slowest walk)
     bool runs_mode_ = true;
-    bool pruns_mode_ = true;  // NKM_PRUNS=0: packed batches always plan through plan_pools
+    bool pruns_mode_ = true;
+    bool merge_nt_mode_ = false;  // NKM_MNT=1: the pipelined merge writes its output streams non-temporally  // NKM_PRUNS=0: packed batches always plan through plan_pools
     bool rleaf_mode_ = false;  // NKM_RLEAF=1: range pools' leaves gathered across the workers, not by each walker  // NKM_RUNS=0: pools in contiguous runs take the per-row records + merge_rows
     int32_t max_pres_ = 1;   // most presences of any ticket inserted (an entry bound of the pipelined merge)
     // NKM_FAST=0: every row takes the exact loop body, also when no two live

@@ -653,11 +653,19 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         });
     const auto tg_gather = clk::now();
     struct alignas(128) Prog {
-        std::atomic<uint64_t> st{0};  // (records published << 32) | rows done
+        std::atomic<uint32_t> ncut{0};  // merge chunk boundaries the walk has passed
         const PoolRec* recs = nullptr;
         const std::pair<uint32_t, int>* ents = nullptr;
+        uint32_t* cut = nullptr;  // per boundary: the walk's records before it
     };
     std::unique_ptr<Prog[]> prog(pipe ? new Prog[ng] : nullptr);
+    // the merge chunks' ends (batch rows), and per pool its record counts there
+    std::vector<uint32_t> chunk_end(pipe ? nch : 0);
+    for (size_t c = 0; c < chunk_end.size(); c++) chunk_end[c] = (uint32_t)(nb * (c + 1) / nch);
+    if (pipe) {
+        grow_to(pool_cuts_, ng * nch);
+        for (size_t gi = 0; gi < ng; gi++) prog[gi].cut = pool_cuts_.data() + gi * nch;
+    }
     std::vector<uint64_t> ebound(pipe ? ng : 0, 0);
     uint64_t ebound_all = 0;
     for (size_t t = 0; pipe && !gpipe && t < ntask_g; t++)
@@ -684,40 +692,37 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     }
     // one chunk of the pipelined merge (merge_pools' chunk body, offsets
     // from the pools' running counts instead of a global prefix)
+    std::vector<double> mch_wait(pipe ? nch : 0, 0.0), mch_ms(pipe ? nch : 0, 0.0);  // NKM_PROFILE=2 split
+    typedef long long v2i __attribute__((vector_size(16)));
+    static_assert(sizeof(mm_entry_ref) == 16 && sizeof(std::pair<uint32_t, int>) == 8, "16-B result entries, 8-B pairs");
+    const bool mnt = merge_nt_mode_;
     auto merge_chunk = [&](size_t c) {
+        const auto tm0 = clk::now();
         const uint32_t lo = (uint32_t)(nb * c / nch), hi = (uint32_t)(nb * (c + 1) / nch);
         size_t gk = g0, ek = e0, xk = x0;
         static thread_local std::vector<uint64_t> span;  // per pool: records [a, b) of the chunk
         span.assign(ng, 0);
         for (size_t gi = 0; gi < ng; gi++) {
-            const DensePool& D = dense_pools_[gi];
-            const uint32_t need = (uint32_t)(std::lower_bound(D.bis, D.bis + D.nrows, hi) - D.bis);
-            if (!need) continue;
-            uint64_t v;
             // waiting for the walks: sched_yield (NKM_MWAIT=N: asleep N µs at a
             // time — measured slower, walks sum 13.5-14 -> 15-16 ms on C3,
             // profiles/r05/r05l_mwait_ab.txt)
-            while (((v = prog[gi].st.load(std::memory_order_acquire)) & 0xffffffffu) < need) {
+            while (prog[gi].ncut.load(std::memory_order_acquire) <= c) {
                 if (mwait_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(mwait_us_));
                 else std::this_thread::yield();
             }
-            const uint32_t nrec = (uint32_t)(v >> 32);
-            const PoolRec* R = prog[gi].recs;
-            auto by_bi = [](const PoolRec& x, uint32_t b) { return x.bi < b; };
-            const uint32_t a = (uint32_t)(std::lower_bound(R, R + nrec, lo, by_bi) - R);
-            const uint32_t b = (uint32_t)(std::lower_bound(R + a, R + nrec, hi, by_bi) - R);
-            if (a < nrec) {
-                gk += R[a].gcum;
-                ek += R[a].off;
-                xk += R[a].xcum;
-            } else if (nrec) {
-                const PoolRec& l = R[nrec - 1];
+            // the chunk's records [a, b) from the walk's cuts (no search: a
+            // binary search per pool per chunk was a miss chain each, 64
+            // pools x 128 chunks on C4); the running counts after record a - 1
+            const uint32_t a = c ? prog[gi].cut[c - 1] : 0u, b = prog[gi].cut[c];
+            if (a) {
+                const PoolRec& l = prog[gi].recs[a - 1];
                 gk += l.gcum + l.matched;
                 ek += l.off + l.len;
                 xk += l.xcum + l.expired;
             }
             span[gi] = ((uint64_t)b << 32) | a;
         }
+        const auto tm1 = clk::now();
         static thread_local std::vector<uint64_t> at_row;  // (pool << 32 | record) + 1; 0: no record
         at_row.assign(hi - lo, 0);
         for (size_t gi = 0; gi < ng; gi++) {
@@ -725,7 +730,20 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             for (uint32_t k = (uint32_t)span[gi]; k < (uint32_t)(span[gi] >> 32); k++)
                 at_row[R[k].bi - lo] = (((uint64_t)gi << 32) | k) + 1;
         }
-        for (uint32_t i = 0; i < hi - lo; i++) {
+        // rows interleave the pools' record and entry arrays (C4: 64 pools,
+        // 128 streams — past what the hardware prefetchers track): each row's
+        // record is prefetched 16 rows ahead, its entries 8 ahead
+        const uint32_t nrow = hi - lo;
+        for (uint32_t i = 0; i < nrow; i++) {
+            if (i + 16 < nrow && at_row[i + 16]) {
+                const uint64_t w = at_row[i + 16] - 1;
+                __builtin_prefetch(&prog[w >> 32].recs[(uint32_t)w]);
+            }
+            if (i + 8 < nrow && at_row[i + 8]) {
+                const uint64_t w = at_row[i + 8] - 1;
+                const Prog& p8 = prog[w >> 32];
+                __builtin_prefetch(&p8.ents[p8.recs[(uint32_t)w].off]);
+            }
             if (!at_row[i]) continue;
             const uint64_t v = at_row[i] - 1;
             const Prog& pr = prog[v >> 32];
@@ -735,6 +753,28 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             dec_[T] = 1;      // decided: a later batch of the pass skips it
             if (r.expired) expired[xk++] = T;
             if (!r.matched) continue;
+            if (mnt) {
+                // streaming stores into the output streams (C4: ~150 MB a
+                // pass, read again only after the pass): no line is read
+                // for ownership first
+                for (uint32_t k = 0; k < r.len; k++) {
+                    const auto& e = pr.ents[r.off + k];
+                    long long pe;
+                    std::memcpy(&pe, &e, 8);
+                    __builtin_nontemporal_store(pe, reinterpret_cast<long long*>(&out_groups.ents[ek + k]));
+                    __builtin_nontemporal_store(e.first, &newly[n0 + (ek - e0) + k]);
+                    sel[e.first] = 1;
+                    if (fill) {
+                        const v2i ev = {(long long)(intptr_t)tk_ptr_[e.first], (long long)(uint32_t)e.second};
+                        __builtin_nontemporal_store(ev, reinterpret_cast<v2i*>(out_ents_.data()) + ek + k);
+                    }
+                }
+                if (fill) __builtin_nontemporal_store((long long)created_[T], reinterpret_cast<long long*>(&out_created_[gk]));
+                ek += r.len;
+                __builtin_nontemporal_store((uint32_t)ek, &out_groups.off[++gk]);
+                if (fill) __builtin_nontemporal_store((int32_t)ek, &out_offs_[gk]);
+                continue;
+            }
             for (uint32_t k = 0; k < r.len; k++) {
                 const auto& e = pr.ents[r.off + k];
                 out_groups.ents[ek + k] = e;
@@ -747,6 +787,9 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             out_groups.off[++gk] = (uint32_t)ek;
             if (fill) out_offs_[gk] = (int32_t)ek;
         }
+        if (mnt) std::atomic_thread_fence(std::memory_order_seq_cst);  // this worker's streaming stores drained
+        mch_wait[c] = msd(tm0, tm1);
+        mch_ms[c] = msd(tm0, clk::now());
     };
     std::vector<double> task_ms(ntask, 0.0), walk_prep_ms(ntask, 0.0), walk_ms(ntask, 0.0);  // NKM_PROFILE=2 split
     std::vector<double> walk_end_ms(ntask, 0.0);  // since the job's start
@@ -796,7 +839,8 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                 prog[gi].recs = run.recs.data();
                 prog[gi].ents = run.ents.data();
                 const auto tr1 = clk::now();
-                run.walk_published(D, rv, maxI, pos_of_.data(), &prog[gi].st);
+                run.walk_cuts(D, rv, maxI, pos_of_.data(), chunk_end.data(), (uint32_t)nch, prog[gi].cut,
+                              &prog[gi].ncut);
                 const auto tr2 = clk::now();
                 walk_prep_ms[t] += msd(tr0, tr1);
                 walk_ms[t] += msd(tr1, tr2);
@@ -911,10 +955,16 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             mw = std::max(mw, walk_ms[k]);
             we = std::max(we, walk_end_ms[k]);
         }
+        double cw = 0, cm = 0;
+        for (size_t c = 0; c < nch; c++) {
+            cw += mch_wait[c];
+            cm += mch_ms[c];
+        }
         std::fprintf(stderr, "[nkm]   pool walks: %zu tasks, %zu pools on %u workers | sum: tasks %.2f, walks %.2f (max %.2f), "
-                     "gather+reset+reserve %.2f ms | gather %s | last walk ends %.2f, job %.2f ms (%zu merge chunks) | "
-                     "before the job: identity check %.2f, lists + setup %.2f, gather %.2f, bounds %.2f ms\n",
-                     ntask, ng, wp.size(), st, sw, mw, sp, gpipe ? "beside" : "before", we, msd(tg1, tg2), nch,
+                     "gather+reset+reserve %.2f ms | gather %s | last walk ends %.2f, job %.2f ms (%zu merge chunks: "
+                     "sum %.2f, of it waiting %.2f ms) | before the job: identity check %.2f, lists + setup %.2f, "
+                     "gather %.2f, bounds %.2f ms\n",
+                     ntask, ng, wp.size(), st, sw, mw, sp, gpipe ? "beside" : "before", we, msd(tg1, tg2), nch, cm, cw,
                      msd(tg0, tg_ident), msd(tg_ident, tg_setup), msd(tg_setup, tg_gather), msd(tg_gather, tg1));
     }
     stats.par_rows += nb;
@@ -1269,8 +1319,11 @@ bool Core::assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t
         scanned[c] = sc;
         live_w[c] = lw;
     };
+    using aclk = std::chrono::steady_clock;
+    const auto ta0 = aclk::now();
     if (nch > 1) wp.run(nch, pass1);
     else pass1(0);
+    const auto ta1 = aclk::now();
     for (uint8_t b : bad)
         if (b) return false;
     for (size_t c = 0; c < nch; c++) at[c + 1] += at[c];
@@ -1289,6 +1342,7 @@ bool Core::assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t
     };
     if (nch > 1) wp.run(nch, pass2);
     else pass2(0);
+    const auto ta2 = aclk::now();
     pb = PackBatch{};
     pb.n = n;
     pb.end = pos + nr;
@@ -1318,7 +1372,15 @@ bool Core::assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t
                 const uint64_t a = base + d.src_off;
                 rg[k++] = {a, a + (d.src_len & ~kSrcOrder)};
             }
-            std::sort(rg, rg + k);
+            // insertion sort: a wave's rows are mostly one bucket's, their
+            // ranges equal or ascending already (std::sort measured ~100 ns a
+            // wave, 125k waves per C5 pass)
+            for (int q = 1; q < k; q++) {
+                const std::pair<uint64_t, uint64_t> x = rg[q];
+                int p = q - 1;
+                while (p >= 0 && x < rg[p]) { rg[p + 1] = rg[p]; p--; }
+                rg[p + 1] = x;
+            }
             uint64_t hi = 0;
             for (int q = 0; q < k; q++) {
                 const uint64_t lo = std::max(rg[q].first, hi);
@@ -1331,6 +1393,11 @@ bool Core::assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t
     if (wch > 1) wp.run(wch, pass3);
     else pass3(0);
     for (uint64_t u : uniq) pb.unique += u;
+    if (batch_profile_) {
+        auto ms = [](aclk::time_point a, aclk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "[nkm]   assemble_packed: %zu rows | sources %.2f compact %.2f wave bytes %.2f ms\n", n,
+                     ms(ta0, ta1), ms(ta1, ta2), ms(ta2, aclk::now()));
+    }
     return true;
 }
 

@@ -1065,21 +1065,31 @@ struct DenseRun {
             if (!f || fast_step(P, v, max_intervals, pos_of, j) == 2) step(P, v, max_intervals, pos_of, j);
     }
 
-    // walk() over all rows that publishes its progress every kPublish rows
-    // for readers on other threads (the pipelined merge): one release store
-    // of (records pushed so far << 32 | rows done).  The caller reserved recs
-    // and ents so that neither reallocates under the readers.
-    void walk_published(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of,
-                        std::atomic<uint64_t>* progress) {
-        constexpr uint32_t kPublish = 512;
+    // walk() over all rows that records, for every merge chunk boundary
+    // bnd[c] (batch rows, ascending; c < nbnd), the number of records of the
+    // pool's rows before it — cut[c] — and publishes the count of boundaries
+    // passed (release) for the pipelined merge, which then reads its chunk's
+    // records [cut[c-1], cut[c]) with no search.  The caller reserved recs and
+    // ents so that neither reallocates under the readers.
+    void walk_cuts(const DensePool& P, const ReplayView& v, int max_intervals, const uint32_t* pos_of,
+                   const uint32_t* bnd, uint32_t nbnd, uint32_t* cut, std::atomic<uint32_t>* ncut) {
         avail = P.front ? 0 : P.n;
         const bool f = fast && v.sessions_exclusive;
-        for (uint32_t b = 0; b < P.nrows; b += kPublish) {  // rows [b, e), then publish
-            const uint32_t e = std::min(P.nrows, b + kPublish);
-            for (uint32_t j = skip_selected(P, b, e); j < e; j = skip_selected(P, j + 1, e))
-                if (!f || fast_step(P, v, max_intervals, pos_of, j) == 2) step(P, v, max_intervals, pos_of, j);
-            progress->store(((uint64_t)recs.size() << 32) | e, std::memory_order_release);
+        uint32_t nc = 0, next = nbnd ? bnd[0] : UINT32_MAX;
+        auto pass = [&](uint32_t j) {  // the rows before j are done
+            const uint32_t b = j < P.nrows ? P.bis[j] : UINT32_MAX;
+            if (b < next) return;
+            const uint32_t r = (uint32_t)recs.size();
+            do cut[nc++] = r;
+            while (nc < nbnd && b >= bnd[nc]);
+            next = nc < nbnd ? bnd[nc] : UINT32_MAX;
+            ncut->store(nc, std::memory_order_release);
+        };
+        for (uint32_t j = skip_selected(P, 0, P.nrows); j < P.nrows; j = skip_selected(P, j + 1, P.nrows)) {
+            pass(j);
+            if (!f || fast_step(P, v, max_intervals, pos_of, j) == 2) step(P, v, max_intervals, pos_of, j);
         }
+        if (nc < nbnd) pass(P.nrows);
     }
 
     // Hands the records to a PoolOut (running offsets/counts, sentinel).
