@@ -1138,10 +1138,9 @@ public:
     bool gpipe_mode_ = true; // NKM_GPIPE=0: no identity-pool shortcut (slot -> position map, copies gathered before the walks)
     int mwait_us_ = 0;       // NKM_MWAIT: a pipelined merge chunk's sleep while the walks have not passed it (0: yield)
     int merge_mult_ = 8;     // NKM_MCH: pipelined merge chunks per worker (the last one is the tail after the slowest walk)
-    bool runs_mode_ = true;
-    bool pruns_mode_ = true;
-    bool merge_nt_mode_ = false;  // NKM_MNT=1: the pipelined merge writes its output streams non-temporally  // NKM_PRUNS=0: packed batches always plan through plan_pools
-    bool rleaf_mode_ = false;  // NKM_RLEAF=1: range pools' leaves gathered across the workers, not by each walker  // NKM_RUNS=0: pools in contiguous runs take the per-row records + merge_rows
+    bool runs_mode_ = true;    // NKM_RUNS=0: pools in contiguous runs take the per-row records + merge_rows
+    bool pruns_mode_ = true;   // NKM_PRUNS=0: packed batches always plan through plan_pools
+    bool rleaf_mode_ = false;  // NKM_RLEAF=1: range pools' leaves gathered across the workers, not by each walker
     int32_t max_pres_ = 1;   // most presences of any ticket inserted (an entry bound of the pipelined merge)
     // NKM_FAST=0: every row takes the exact loop body, also when no two live
     // tickets share a session (the fast walk, replay_core.h) (A/B, tests)

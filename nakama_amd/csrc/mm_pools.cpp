@@ -693,9 +693,6 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     // one chunk of the pipelined merge (merge_pools' chunk body, offsets
     // from the pools' running counts instead of a global prefix)
     std::vector<double> mch_wait(pipe ? nch : 0, 0.0), mch_ms(pipe ? nch : 0, 0.0);  // NKM_PROFILE=2 split
-    typedef long long v2i __attribute__((vector_size(16)));
-    static_assert(sizeof(mm_entry_ref) == 16 && sizeof(std::pair<uint32_t, int>) == 8, "16-B result entries, 8-B pairs");
-    const bool mnt = merge_nt_mode_;
     auto merge_chunk = [&](size_t c) {
         const auto tm0 = clk::now();
         const uint32_t lo = (uint32_t)(nb * c / nch), hi = (uint32_t)(nb * (c + 1) / nch);
@@ -753,28 +750,6 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             dec_[T] = 1;      // decided: a later batch of the pass skips it
             if (r.expired) expired[xk++] = T;
             if (!r.matched) continue;
-            if (mnt) {
-                // streaming stores into the output streams (C4: ~150 MB a
-                // pass, read again only after the pass): no line is read
-                // for ownership first
-                for (uint32_t k = 0; k < r.len; k++) {
-                    const auto& e = pr.ents[r.off + k];
-                    long long pe;
-                    std::memcpy(&pe, &e, 8);
-                    __builtin_nontemporal_store(pe, reinterpret_cast<long long*>(&out_groups.ents[ek + k]));
-                    __builtin_nontemporal_store(e.first, &newly[n0 + (ek - e0) + k]);
-                    sel[e.first] = 1;
-                    if (fill) {
-                        const v2i ev = {(long long)(intptr_t)tk_ptr_[e.first], (long long)(uint32_t)e.second};
-                        __builtin_nontemporal_store(ev, reinterpret_cast<v2i*>(out_ents_.data()) + ek + k);
-                    }
-                }
-                if (fill) __builtin_nontemporal_store((long long)created_[T], reinterpret_cast<long long*>(&out_created_[gk]));
-                ek += r.len;
-                __builtin_nontemporal_store((uint32_t)ek, &out_groups.off[++gk]);
-                if (fill) __builtin_nontemporal_store((int32_t)ek, &out_offs_[gk]);
-                continue;
-            }
             for (uint32_t k = 0; k < r.len; k++) {
                 const auto& e = pr.ents[r.off + k];
                 out_groups.ents[ek + k] = e;
@@ -787,7 +762,6 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             out_groups.off[++gk] = (uint32_t)ek;
             if (fill) out_offs_[gk] = (int32_t)ek;
         }
-        if (mnt) std::atomic_thread_fence(std::memory_order_seq_cst);  // this worker's streaming stores drained
         mch_wait[c] = msd(tm0, tm1);
         mch_ms[c] = msd(tm0, clk::now());
     };
