@@ -1,4 +1,4 @@
-# Round 5 checkpoint (after the merge cuts / packed plan changes): the whole
+# Round 5 checkpoint (merge cuts, packed plan, head moving with skipped rows): the whole
 # GPU suite, smoke(), the default bench line (C3, with its cpu_baseline), the
 # rocprofv3 kernel-trace summary of C3, then the C4, C5 and C2 lines.  $1 = tag.
 set -o pipefail
@@ -19,4 +19,12 @@ for k in 4 5 2; do
   python3 -c "
 import json; d=json.loads(open('gpurun_out/${T}_c$k.json').read().strip().splitlines()[-1]); r=d['roofline']
 print('c$k', round(d['value']/1e6, 3), 'M/s p50', round(d['p50_ms'], 2), r.get('kernel'), round(r['avg_launch_ms']*1e3, 2), 'us frac', round(r['frac'], 3))"
+done
+# the identity walk on the box's host (PMU counters): the previous commit's
+# replay_core.h (tools/replay_bench_r05old) against this tree's, interleaved
+for k in a b c; do
+  for b in replay_bench_r05old replay_bench; do
+    RB_PERF=1 timeout -k 10 120 tools/$b 1000000 5 0 > gpurun_out/${T}_rb_$b$k.txt 2>&1 || { echo RB_FAIL; tail -5 gpurun_out/${T}_rb_$b$k.txt; exit 1; }
+    echo "$b $k: $(grep -oE 'identity-walk-only [0-9.]+ ms' gpurun_out/${T}_rb_$b$k.txt) $(grep -E '^\[perf\]' gpurun_out/${T}_rb_$b$k.txt | tail -1 | cut -c1-200)"
+  done
 done
