@@ -722,45 +722,70 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         const auto tm1 = clk::now();
         static thread_local std::vector<uint64_t> at_row;  // (pool << 32 | record) + 1; 0: no record
         at_row.assign(hi - lo, 0);
+        // the pools' arrays and every output's base pointer in locals: the
+        // loop's byte stores (decided, selected) may alias any memory, so
+        // pointers read through members or the Prog array would be reloaded
+        // after each one
+        static thread_local std::vector<const PoolRec*> precs;
+        static thread_local std::vector<const std::pair<uint32_t, int>*> pents;
+        precs.resize(ng);
+        pents.resize(ng);
+        uint64_t* const AR = at_row.data();
         for (size_t gi = 0; gi < ng; gi++) {
             const PoolRec* R = prog[gi].recs;
+            precs[gi] = R;
+            pents[gi] = prog[gi].ents;
             for (uint32_t k = (uint32_t)span[gi]; k < (uint32_t)(span[gi] >> 32); k++)
-                at_row[R[k].bi - lo] = (((uint64_t)gi << 32) | k) + 1;
+                AR[R[k].bi - lo] = (((uint64_t)gi << 32) | k) + 1;
         }
+        const PoolRec* const* const PR = precs.data();
+        const std::pair<uint32_t, int>* const* const PE = pents.data();
+        const uint32_t* const B = brow.data();
+        int32_t* const IV = intervals_.data();
+        uint8_t* const DEC = dec_.data();
+        uint8_t* const SEL = sel.data();
+        uint32_t* const XP = expired.data();
+        GroupList::Entry* const OGE = out_groups.ents.data();
+        uint32_t* const OGO = out_groups.off.data();
+        uint32_t* const NW = newly.data() + n0 - e0;  // entry k's slot at NW[k]
+        mm_entry_ref* const OE = fill ? out_ents_.data() : nullptr;
+        int64_t* const OC = fill ? out_created_.data() : nullptr;
+        int32_t* const OO = fill ? out_offs_.data() : nullptr;
+        const char* const* const TK = tk_ptr_.data();
+        const int64_t* const CR = created_.data();
         // rows interleave the pools' record and entry arrays (C4: 64 pools,
         // 128 streams — past what the hardware prefetchers track): each row's
         // record is prefetched 16 rows ahead, its entries 8 ahead
         const uint32_t nrow = hi - lo;
         for (uint32_t i = 0; i < nrow; i++) {
-            if (i + 16 < nrow && at_row[i + 16]) {
-                const uint64_t w = at_row[i + 16] - 1;
-                __builtin_prefetch(&prog[w >> 32].recs[(uint32_t)w]);
+            if (i + 16 < nrow && AR[i + 16]) {
+                const uint64_t w = AR[i + 16] - 1;
+                __builtin_prefetch(PR[w >> 32] + (uint32_t)w);
             }
-            if (i + 8 < nrow && at_row[i + 8]) {
-                const uint64_t w = at_row[i + 8] - 1;
-                const Prog& p8 = prog[w >> 32];
-                __builtin_prefetch(&p8.ents[p8.recs[(uint32_t)w].off]);
+            if (i + 8 < nrow && AR[i + 8]) {
+                const uint64_t w = AR[i + 8] - 1;
+                __builtin_prefetch(PE[w >> 32] + PR[w >> 32][(uint32_t)w].off);
             }
-            if (!at_row[i]) continue;
-            const uint64_t v = at_row[i] - 1;
-            const Prog& pr = prog[v >> 32];
-            const PoolRec& r = pr.recs[(uint32_t)v];
-            const uint32_t T = brow[r.bi];
-            intervals_[T]++;  // the row's pending Intervals increment
-            dec_[T] = 1;      // decided: a later batch of the pass skips it
-            if (r.expired) expired[xk++] = T;
+            if (!AR[i]) continue;
+            const uint64_t v = AR[i] - 1;
+            const PoolRec r = PR[v >> 32][(uint32_t)v];
+            const std::pair<uint32_t, int>* const ents = PE[v >> 32] + r.off;
+            const uint32_t T = B[r.bi];
+            IV[T]++;     // the row's pending Intervals increment
+            DEC[T] = 1;  // decided: a later batch of the pass skips it
+            if (r.expired) XP[xk++] = T;
             if (!r.matched) continue;
             for (uint32_t k = 0; k < r.len; k++) {
-                const auto& e = pr.ents[r.off + k];
-                out_groups.ents[ek + k] = e;
-                newly[n0 + (ek - e0) + k] = e.first;
-                sel[e.first] = 1;
-                if (fill) out_ents_[ek + k] = mm_entry_ref{tk_ptr_[e.first], e.second, 0};
+                const std::pair<uint32_t, int> e = ents[k];
+                OGE[ek + k] = GroupList::Entry(e.first, e.second);
+                NW[ek + k] = e.first;
+                SEL[e.first] = 1;
+                if (fill) OE[ek + k] = mm_entry_ref{TK[e.first], e.second, 0};
             }
-            if (fill) out_created_[gk] = created_[T];  // the group's searching ticket (its last entry)
+            if (fill) OC[gk] = CR[T];  // the group's searching ticket (its last entry)
             ek += r.len;
-            out_groups.off[++gk] = (uint32_t)ek;
-            if (fill) out_offs_[gk] = (int32_t)ek;
+            OGO[++gk] = (uint32_t)ek;
+            if (fill) OO[gk] = (int32_t)ek;
         }
         mch_wait[c] = msd(tm0, tm1);
         mch_ms[c] = msd(tm0, clk::now());
