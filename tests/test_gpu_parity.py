@@ -582,6 +582,44 @@ def test_pool_runs_replay(config, n, passes, rpack, runs, monkeypatch, capfd):
     assert ("pool runs:" in capfd.readouterr().err) == (runs == "1")
 
 
+@pytest.mark.parametrize("pruns", ["1", "0"])
+def test_packed_plan_bucket_in_two_runs(pruns, monkeypatch, capfd):
+    """Every C5 bucket arriving in two runs (a second set with the same bucket
+    names, created after the first): the packed batch's three-sweep plan
+    (plan_packed_runs) meets each term again after its run and hands the batch
+    to plan_pools' counting sort; NKM_PRUNS=0 goes there directly.  Groups and
+    post-pass state equal the oracle's; with contiguous buckets (config 5
+    alone) the three-sweep plan is the one taken."""
+    monkeypatch.setenv("NKM_PARALLEL", "force")
+    monkeypatch.setenv("NKM_PRUNS", pruns)
+    monkeypatch.setenv("NKM_PROFILE", "2")
+    kw = dict(max_intervals=2, rev_precision=True, rev_threshold=0)
+    n = 800
+    sets = [synth.TicketSet(5, n), synth.TicketSet(5, n, seed=0x5EED0105, t0=synth.T0 + 1024 * n)]
+    gpu = capi.Matchmaker(product_lib(), **kw)
+    orc = capi.Matchmaker(harness.oracle_lib(), **kw)
+    try:
+        for ts in sets:
+            ts.insert_into(gpu)
+            ts.insert_into(orc)
+        for p in range(2):
+            g, o = gpu.process_raw(), orc.process_raw()
+            assert g.groups == o.groups, f"pass {p}: {len(g.groups)} vs oracle {len(o.groups)} groups"
+            assert state(gpu) == state(orc)
+            assert p or g.groups
+    finally:
+        gpu.close()
+        orc.close()
+        for ts in sets:
+            ts.close()
+    err = capfd.readouterr().err
+    assert "3 sweeps" not in err  # never planned as runs: the buckets come back
+    assert ("pool runs:" in err) is False
+    out = run_passes(5, n, 1, kw)
+    assert len(out[0].groups) > 0
+    assert ("3 sweeps" in capfd.readouterr().err) == (pruns == "1")
+
+
 @pytest.mark.parametrize("direct", ["1", "0"])
 @pytest.mark.parametrize("config,n", [(5, 5000), (6, 100), (13, 900)])
 def test_custom_candidates_into_result_arena(config, n, direct, monkeypatch):
