@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <stdexcept>
 #include <thread>
+#include <unordered_set>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -1520,6 +1521,18 @@ int Core::plan_packed_runs(size_t n, const UVec<uint32_t>& brow, ParPlan& P, Pas
         if (!kw || (uint32_t)fval_[f0][r] != t) return UINT32_MAX;  // not in its search's pool
         return t | kForeign;
     };
+    {  // a prefix where a term comes back after its run (C2's interleaved
+       // region pools): not this shape, decided before any sweep
+        std::unordered_set<uint32_t> seen;
+        uint32_t prev = UINT32_MAX;
+        for (size_t i = 0; i < std::min<size_t>(n, 2048); i++) {
+            const uint32_t k = term_of(i);
+            if (k == UINT32_MAX) break;  // the sweeps report it
+            const uint32_t t = k & kTerm;
+            if (t != prev && !seen.insert(t).second) return 0;
+            prev = t;
+        }
+    }
     auto reset_first = [&] {
         wp.run(nch, [&](size_t c) {
             for (size_t t = pool_first_cap_ * c / nch; t < pool_first_cap_ * (c + 1) / nch; t++)
