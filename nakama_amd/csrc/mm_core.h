@@ -152,6 +152,9 @@ struct Sig {
     int64_t ub_key = INT64_MAX;
     uint16_t n_fields = 0;  // distinct field columns the clauses read
     std::vector<std::pair<uint16_t, uint32_t>> must_terms;  // candidate posting lists
+    // the only MUST term's posting key (field << 32 | term) when there is
+    // exactly one, else UINT64_MAX: source_of reads no term list then
+    uint64_t must_key1 = UINT64_MAX;
     uint64_t must_fmask = 0;  // bit f: a MUST keyword term on field f (f >= 63: bit 63)
     // every clause score is a multiple of 2^-20 below 2^20 in magnitude: any
     // sum of them is exact in double, whatever the order (top-tier lists)

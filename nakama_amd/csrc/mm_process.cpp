@@ -1056,6 +1056,18 @@ std::unique_ptr<ReplayCore> Core::make_replay(std::vector<uint8_t>& sel, bool re
 // choose_source without advancing the posting lists' dead-prefix heads (safe
 // on the host workers): the same list, possibly starting at dead entries.
 void Core::source_of(const Sig& s, DGroup& g, SrcChoice* ch) const {
+    if (s.must_key1 != UINT64_MAX) {  // one MUST term: its posting list (C5's bucket)
+        const PostingRange* it = postings_map_.find(s.must_key1);
+        g.src_kind = 1;
+        g.src_off = it ? it->off + it->head : 0;
+        g.src_len = it ? it->len - it->head : 0;
+        if (ch) {
+            ch->has_term = true;
+            ch->field = (uint16_t)(s.must_key1 >> 32);
+            ch->term = (uint32_t)s.must_key1;
+        }
+        return;
+    }
     g.src_kind = 0;
     g.src_off = order_head_;
     g.src_len = (uint32_t)order_.size() - order_head_;

@@ -508,6 +508,7 @@ void Core::sig_describe(Sig& s, const std::vector<DClause>& dc, const CompiledQu
             }
         }
     }
+    if (s.must_terms.size() == 1) s.must_key1 = ((uint64_t)s.must_terms[0].first << 32) | s.must_terms[0].second;
     // a fuzzy clause scores per accepted term: variable-score search, no score bound
     bool fuzzy = false;
     for (auto& c : cq.clauses)
