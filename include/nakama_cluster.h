@@ -64,6 +64,13 @@ int32_t mm_merge_positions(const int64_t* keys, const int32_t* counts, int32_t w
  * the same branch. */
 int32_t mm_merge_positions_strided(const int64_t* keys, int64_t stride, const int32_t* counts, int32_t world,
                                    int32_t rank, int64_t* pos_out);
+/* mm_merge_positions_strided when the caller already knows whether every
+ * rank's keys ascend (sorted != 0: each rank checked its own before the
+ * all-gather, and the flags came with the group counts), so no rank re-reads
+ * the whole matrix to find out; sorted == 0 is mm_merge_positions_strided.
+ * The positions are computed on the library's persistent host threads. */
+int32_t mm_merge_positions_ex(const int64_t* keys, int64_t stride, const int32_t* counts, int32_t world, int32_t rank,
+                              int32_t sorted, int64_t* pos_out);
 /* Matched tickets of a result (its entries with presence index 0: a
  * ticket's presence entries hold index 0 exactly once), counted on host
  * threads — the cluster front's per-pass summary without a Python pass over

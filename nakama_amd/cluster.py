@@ -74,12 +74,15 @@ def router_lib(path: str = PRODUCT_SO) -> C.CDLL:
         lib.mm_merge_positions_strided.restype = C.c_int32
         lib.mm_merge_positions_strided.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_int32,
                                                    C.c_void_p]
+        lib.mm_merge_positions_ex.restype = C.c_int32
+        lib.mm_merge_positions_ex.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+                                              C.c_void_p]
         _router = lib
     return _router
 
 
 CLUSTER_SYMBOLS = ("mm_route_keys", "mm_pack_tickets", "mm_unpack_tickets", "mm_free_unpacked",
-                   "mm_merge_positions", "mm_merge_positions_strided", "mm_count_tickets", "mm_shard_rows", "mm_rccl_unique_id", "mm_shard_rows_rccl",
+                   "mm_merge_positions", "mm_merge_positions_strided", "mm_merge_positions_ex", "mm_count_tickets", "mm_shard_rows", "mm_rccl_unique_id", "mm_shard_rows_rccl",
                    "mm_create_multi", "mm_multi_info", "mm_device_numa_node")
 
 
@@ -168,6 +171,7 @@ class ClusterMatchmaker:
         self.directory: Dict[int, int] = {}
         self.load = [0] * self.world
         self.owner_of: Dict[str, int] = {}  # rank 0, global override scope: ticket -> rank
+        self._bufs: Dict[str, tuple] = {}  # merge staging buffers (host, device), reused across passes
 
     # ---- collectives over tensors ----
     def _t(self, arr: np.ndarray):
@@ -301,47 +305,83 @@ class ClusterMatchmaker:
         finally:
             self.local.lib.mm_free_matched(self.local.h, C.byref(out))
         t3 = time.perf_counter()
-        cp.local_stats = {"pass_ms": stats.pass_ms, "eval_ms": stats.eval_ms, "eval_bytes": stats.eval_bytes,
+        cp.local_stats = {**cp.local_stats, "pass_ms": stats.pass_ms, "eval_ms": stats.eval_ms, "eval_bytes": stats.eval_bytes,
                           "pair_evals": stats.pair_evals, "pairs_decided": stats.pairs_decided,
                           "eval_launches": stats.eval_launches, "n_batches": stats.n_batches,
                           "eval_kernel": stats.eval_kernel, "local_call_ms": 1e3 * (t1 - t0),
                           "summary_ms": 1e3 * (t2 - t1), "merge_ms": 1e3 * (t3 - t2)}
         return cp
 
+    def _staging(self, name: str, n: int, dtype):
+        """A reusable host buffer of at least n elements (pinned when the
+        collectives run on the device: the keys' copies then run at full PCIe
+        rate and need no per-pass allocation) and its device twin."""
+        import torch
+        buf = self._bufs.get(name)
+        if buf is None or buf[0].numel() < n:
+            cap = max(n, 1024)
+            host = torch.empty(cap, dtype=dtype, pin_memory=self.comm_device is not None)
+            dev = torch.empty(cap, dtype=dtype, device=self.comm_device) if self.comm_device is not None else host
+            buf = self._bufs[name] = (host, dev)
+        return buf
+
     def merge_keys(self, cp: ClusterPass, keys: np.ndarray, tickets: int, pres: int, tie_ids=None):
         """The merge of a cluster pass: this rank's groups' keys (the searching
         ticket's CreatedAt, in this rank's group order) -> cp's totals and
         cp.positions, the global position of each of this rank's groups in the
-        reference's order.  Two all-gathers and one all-reduce per pass.
-        tie_ids(): this rank's searching ticket ids, asked for only when two
-        ranks' keys tie (the ids then order the tied groups)."""
+        reference's order.  Two all-gathers and one all-reduce per pass; the
+        positions are computed in C on the library's persistent host threads
+        (mm_merge_positions_ex).  tie_ids(): this rank's searching ticket ids,
+        asked for only when two ranks' keys tie (the ids then order the tied
+        groups).  cp.local_stats gets the merge's split: collectives + copies
+        (merge_comm_ms) and the C merge (merge_c_ms)."""
+        import time
+
+        import torch
+        t0 = time.perf_counter()
         ng = len(keys)
-        # one all-gather of (groups, matched tickets, presences): sizes + totals
-        hdr = [self._t(np.zeros(3, dtype=np.int64)) for _ in range(self.world)]
-        self.dist.all_gather(hdr, self._t(np.array([ng, tickets, pres], dtype=np.int64)))
+        # processDefault's groups ascend by key; an override's choice may not.
+        # Each rank checks its own, and the flag travels with the counts, so
+        # no rank re-reads the whole matrix to find out.
+        asc = 1 if ng < 2 or bool(np.all(keys[1:] >= keys[:-1])) else 0
+        # one all-gather of (groups, matched tickets, presences, ascending)
+        hdr = [self._t(np.zeros(4, dtype=np.int64)) for _ in range(self.world)]
+        self.dist.all_gather(hdr, self._t(np.array([ng, tickets, pres, asc], dtype=np.int64)))
         hdr = np.stack([self._host(h) for h in hdr])
-        counts = hdr[:, 0].astype(np.int32)
-        cp.n_groups, cp.matched_tickets, cp.matched_presences = (int(x) for x in hdr.sum(axis=0))
-        # one all-gather of the keys into a [world][m] matrix (padded to
-        # the largest rank's count; one collective, one copy to the host)
+        counts = np.ascontiguousarray(hdr[:, 0].astype(np.int32))
+        cp.n_groups, cp.matched_tickets, cp.matched_presences = (int(x) for x in hdr[:, :3].sum(axis=0))
+        sorted_all = int(hdr[:, 3].min()) == 1
+        # one all-gather of the keys into a [world][m] matrix (padded to the
+        # largest rank's count; one collective, one copy each way)
         m = max(int(counts.max()), 1)
-        pad = np.zeros(m, dtype=np.int64)
-        pad[:ng] = keys
-        mat = self._t(np.zeros(self.world * m, dtype=np.int64))
-        self.dist.all_gather_into_tensor(mat, self._t(pad))
-        allk = np.ascontiguousarray(self._host(mat))
+        host_in, dev_in = self._staging("keys_in", m, torch.int64)
+        host_out, dev_out = self._staging("keys_out", self.world * m, torch.int64)
+        hin = host_in.numpy()
+        hin[:ng] = keys
+        hin[ng:m] = 0
+        if self.comm_device is not None:
+            dev_in[:m].copy_(host_in[:m], non_blocking=True)
+            self.dist.all_gather_into_tensor(dev_out[:self.world * m], dev_in[:m])
+            host_out[:self.world * m].copy_(dev_out[:self.world * m], non_blocking=False)
+        else:
+            self.dist.all_gather_into_tensor(dev_out[:self.world * m], dev_in[:m])
+        allk = host_out.numpy()
+        t1 = time.perf_counter()
         pos = np.zeros(max(ng, 1), dtype=np.int64)
-        # the merge in C: every rank's keys ascend for processDefault; an
-        # override's choice may reorder them, and then (rc 2, the same on
-        # every rank) the groups take the stable order by (key, rank, index)
-        rc = router_lib().mm_merge_positions_strided(allk.ctypes.data, m, counts.ctypes.data, self.world,
-                                                     self.rank, pos.ctypes.data)
+        # the merge in C: when some rank's keys do not ascend (rc 2, the same
+        # on every rank) the groups take the stable order by (key, rank, index)
+        rc = router_lib().mm_merge_positions_ex(allk.ctypes.data, m, counts.ctypes.data, self.world, self.rank,
+                                                1 if sorted_all else 0, pos.ctypes.data)
         cp.positions = pos[:ng]
+        t2 = time.perf_counter()
         flag = self._t(np.array([1 if rc == 1 else 0], dtype=np.int32))
         self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX)
         if int(self._host(flag)[0]) and rc != 2:  # rare: the searching tickets' ids order the tied groups
             flat = np.concatenate([allk[r * m:r * m + int(counts[r])] for r in range(self.world)])
             self._order_ties(cp, flat, counts, tie_ids() if tie_ids is not None else [""] * ng)
+        t3 = time.perf_counter()
+        cp.local_stats["merge_comm_ms"] = 1e3 * ((t1 - t0) + (t3 - t2))
+        cp.local_stats["merge_c_ms"] = 1e3 * (t2 - t1)
 
     def _override(self, out):
         """This rank's override hand-off -> (committed result, error).  An

@@ -11,13 +11,17 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <immintrin.h>
 #include <deque>
+#include <mutex>
+#include <sched.h>
 #include <thread>
 #include <string>
 #include <vector>
 
 #include "../../include/nakama_cluster.h"
 #include "gocompat.h"
+#include "mm_core.h"
 #include "mm_handle.h"
 #include "qcompile.h"
 
@@ -259,36 +263,133 @@ void mm_free_unpacked(void* set) { delete static_cast<Unpacked*>(set); }
 
 // The merge behind mm_merge_positions{,_strided}: rank r's keys at base[r].
 // My group i lands after my i earlier groups and after every other rank's
-// groups with a smaller key: per other rank, a binary search for the range's
-// first key, then a linear two-pointer walk.  Large merges (8 ranks x 175k
-// groups: ~2.5M steps on the step's critical path) split my groups into
-// ranges walked on threads.  check: first test that every rank's keys ascend
-// (the same answer on every rank); if one does not — an override's choice
-// may reorder its groups — the positions are the stable order by (key, rank,
-// index) and the return value is 2.  Else 1 when one of my groups has the
-// same key as another rank's group, 0 otherwise.
+// groups with a smaller key, so pos[i] = i + sum over the other ranks q of
+// #{q's keys < mine[i]}.  One sweep over my keys advances a cursor into every
+// other rank's keys at once: per (i, q) one 4-key vector compare whose
+// popcount is the cursor's step (a step of 4 compares again), so the other
+// ranks' cursors are independent dependency chains and no branch depends on
+// how the ranks' keys interleave — the two-pointer walk this replaces
+// mispredicted about once per (i, q) on C3's interleaved CreatedAt keys (8
+// ranks x 175k groups: 3.5-4.7 ms on 8 threads -> see DESIGN.md §7).
+// check: first test that every rank's keys ascend (the same answer on every
+// rank); if one does not — an override's choice may reorder its groups — the
+// positions are the stable order by (key, rank, index) and the return value
+// is 2.  Else 1 when one of my groups has the same key as another rank's
+// group, 0 otherwise.
+namespace {
+
+// The host threads of the cluster entry points: one persistent pool per
+// process (created on first use, its workers asleep between calls), so a
+// pass's merge starts no thread.  Sized like a handle's workers — the
+// process's CPUs over the node's local ranks — and capped at 8: the merge of
+// 8 x 175k keys is ~0.5 M cursor steps per thread there.  Calls from several
+// threads take turns (WorkPool runs one job at a time).
+struct MergePool {
+    std::mutex mu;
+    std::unique_ptr<nkm::WorkPool> pool;
+    nkm::WorkPool& get() {
+        if (!pool) {
+            unsigned n = std::thread::hardware_concurrency();
+            cpu_set_t cs;
+            if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = (unsigned)CPU_COUNT(&cs);
+            if (const char* lw = std::getenv("LOCAL_WORLD_SIZE")) n /= (unsigned)std::max(1, std::atoi(lw));
+            pool.reset(new nkm::WorkPool(std::max(1u, std::min(8u, n))));
+        }
+        return *pool;
+    }
+};
+MergePool& merge_pool() {
+    static MergePool* p = new MergePool();  // never destroyed: no join at process exit
+    return *p;
+}
+
+// fn(t, nt) for t in [0, nt) on the merge pool: nt grows with the work
+// (one thread per 2^18 units), 1 runs inline.
+void run_split(int64_t units, const std::function<void(int, int)>& fn) {
+    const int64_t want = std::max<int64_t>(1, units >> 18);
+    if (want == 1) return fn(0, 1);
+    MergePool& mp = merge_pool();
+    std::lock_guard<std::mutex> lk(mp.mu);
+    nkm::WorkPool& wp = mp.get();
+    const int nt = (int)std::min<int64_t>(want, wp.size());
+    wp.run((size_t)nt, [&](size_t t) { fn((int)t, nt); });
+}
+
+bool ascending(const int64_t* k, int64_t n) {
+    int64_t bad = 0;
+    for (int64_t i = 1; i < n; i++) bad |= (int64_t)(k[i] < k[i - 1]);  // vectorises
+    return bad == 0;
+}
+
+// pos[i] for my keys [i0, i1): every other rank's cursor starts at its first
+// key >= mine[i0] and moves with a 4-key compare per (i, q) — the cursors are
+// independent dependency chains, so the loop is throughput-bound.
+__attribute__((target("avx2,popcnt"))) int32_t merge_walk_avx2(const int64_t* mine, int64_t i0, int64_t i1,
+                                                                const int64_t* const* other, const int64_t* m, int nq,
+                                                                int64_t* pos) {
+    if (i0 >= i1) return 0;
+    int64_t J[64];
+    for (int q = 0; q < nq; q++) J[q] = std::lower_bound(other[q], other[q] + m[q], mine[i0]) - other[q];
+    int eq = 0;
+    for (int64_t i = i0; i < i1; i++) {
+        const int64_t k = mine[i];
+        const __m256i kv = _mm256_set1_epi64x(k);
+        int64_t acc = i;
+        for (int q = 0; q < nq; q++) {
+            const int64_t* o = other[q];
+            int64_t j = J[q];
+            for (;;) {
+                if (__builtin_expect(j + 4 <= m[q], 1)) {
+                    const __m256i v = _mm256_loadu_si256((const __m256i*)(o + j));
+                    const int lt = _mm256_movemask_pd(_mm256_castsi256_pd(_mm256_cmpgt_epi64(kv, v)));
+                    eq |= _mm256_movemask_pd(_mm256_castsi256_pd(_mm256_cmpeq_epi64(kv, v)));
+                    const int c = __builtin_popcount((unsigned)lt);
+                    j += c;
+                    if (c < 4) break;
+                } else {
+                    while (j < m[q] && o[j] < k) j++;
+                    eq |= j < m[q] && o[j] == k;
+                    break;
+                }
+            }
+            J[q] = j;
+            acc += j;
+        }
+        pos[i] = acc;
+    }
+    return eq != 0;
+}
+
+int32_t merge_walk_scalar(const int64_t* mine, int64_t i0, int64_t i1, const int64_t* const* other,
+                          const int64_t* m, int nq, int64_t* pos) {
+    if (i0 >= i1) return 0;
+    int32_t ties = 0;
+    for (int64_t i = i0; i < i1; i++) pos[i] = i;
+    for (int q = 0; q < nq; q++) {
+        const int64_t* o = other[q];
+        int64_t j = std::lower_bound(o, o + m[q], mine[i0]) - o;
+        for (int64_t i = i0; i < i1; i++) {
+            while (j < m[q] && o[j] < mine[i]) j++;
+            ties |= j < m[q] && o[j] == mine[i];
+            pos[i] += j;
+        }
+    }
+    return ties;
+}
+
+}  // namespace
+
 static int32_t nkm_merge(const int64_t* const* base, const int32_t* counts, int32_t world, int32_t rank,
                          int64_t* pos_out, bool check) {
     std::vector<int64_t> off((size_t)world + 1, 0);
     for (int32_t r = 0; r < world; r++) off[r + 1] = off[r] + counts[r];
-    const int64_t* mine = base[rank];
-    const int64_t n = counts[rank];
-    const int64_t steps = n * (int64_t)world + off[world];
-    const int nt = steps < (1 << 20) ? 1 : (int)std::min<int64_t>(8, std::max(1u, std::thread::hardware_concurrency()));
-    auto parallel = [&](auto&& fn) {  // fn(t) for t in [0, nt)
-        if (nt == 1) return fn(0);
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; t++) th.emplace_back(fn, t);
-        fn(0);
-        for (auto& x : th) x.join();
-    };
     if (check) {
-        std::vector<uint8_t> bad((size_t)nt, 0);
-        parallel([&](int t) {
-            for (int32_t r = 0; r < world && !bad[t]; r++) {
-                const int64_t m = counts[r], lo = std::max<int64_t>(1, m * t / nt), hi = m * (t + 1) / nt;
-                for (int64_t i = lo; i < hi; i++)
-                    if (base[r][i] < base[r][i - 1]) { bad[t] = 1; break; }
+        // every rank's keys, in slices over the pool
+        std::vector<uint8_t> bad(64, 0);
+        run_split(off[world], [&](int t, int nt) {
+            for (int32_t r = 0; r < world; r++) {
+                const int64_t m = counts[r], lo = std::max<int64_t>(0, m * t / nt - 1), hi = m * (t + 1) / nt;
+                if (!ascending(base[r] + lo, hi - lo)) bad[t] = 1;
             }
         });
         if (std::any_of(bad.begin(), bad.end(), [](uint8_t b) { return b != 0; })) {
@@ -303,41 +404,36 @@ static int32_t nkm_merge(const int64_t* const* base, const int32_t* counts, int3
             return 2;
         }
     }
-    auto walk = [&](int64_t i0, int64_t i1, int32_t* ties) {
-        for (int64_t i = i0; i < i1; i++) pos_out[i] = i;
-        for (int32_t q = 0; q < world; q++) {
-            if (q == rank || i0 >= i1) continue;
-            const int64_t* other = base[q];
-            const int64_t m = counts[q];
-            int64_t j = std::lower_bound(other, other + m, mine[i0]) - other;
-            for (int64_t i = i0; i < i1; i++) {
-                while (j < m && other[j] < mine[i]) j++;
-                if (j < m && other[j] == mine[i]) *ties = 1;  // equal CreatedAt on two ranks
-                pos_out[i] += j;
-            }
+    std::vector<const int64_t*> other;
+    std::vector<int64_t> m;
+    for (int32_t q = 0; q < world; q++)
+        if (q != rank && counts[q] > 0) {
+            other.push_back(base[q]);
+            m.push_back(counts[q]);
         }
-    };
-    std::vector<int32_t> ties((size_t)nt, 0);
-    parallel([&](int t) { walk(n * t / nt, n * (t + 1) / nt, &ties[t]); });
+    const int64_t n = counts[rank];
+    static const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("popcnt");
+    std::vector<int32_t> ties(64, 0);
+    run_split(n * (int64_t)(other.size() + 1), [&](int t, int nt) {
+        const int64_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+        ties[t] = avx2 && other.size() <= 64
+                      ? merge_walk_avx2(base[rank], i0, i1, other.data(), m.data(), (int)other.size(), pos_out)
+                      : merge_walk_scalar(base[rank], i0, i1, other.data(), m.data(), (int)other.size(), pos_out);
+    });
     int32_t any = 0;
-    for (int32_t t : ties) any |= t;
+    for (int32_t x : ties) any |= x;
     return any;
 }
 
 int64_t mm_count_tickets(const mm_matched* m) {
     if (!m || m->n_entries <= 0 || !m->entries) return 0;
     const int64_t n = m->n_entries;
-    const int nt = n < (1 << 18) ? 1 : (int)std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()));
-    std::vector<int64_t> part((size_t)nt, 0);
-    auto count = [&](int t) {
+    std::vector<int64_t> part(64, 0);
+    run_split(n >> 1, [&](int t, int nt) {
         int64_t c = 0;
         for (int64_t i = n * t / nt; i < n * (t + 1) / nt; i++) c += m->entries[i].presence_index == 0;
         part[t] = c;
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; t++) th.emplace_back(count, t);
-    count(0);
-    for (auto& x : th) x.join();
+    });
     int64_t c = 0;
     for (int64_t v : part) c += v;
     return c;
@@ -355,9 +451,14 @@ int32_t mm_merge_positions(const int64_t* keys, const int32_t* counts, int32_t w
 
 int32_t mm_merge_positions_strided(const int64_t* keys, int64_t stride, const int32_t* counts, int32_t world,
                                    int32_t rank, int64_t* pos_out) {
+    return mm_merge_positions_ex(keys, stride, counts, world, rank, 0, pos_out);
+}
+
+int32_t mm_merge_positions_ex(const int64_t* keys, int64_t stride, const int32_t* counts, int32_t world, int32_t rank,
+                              int32_t sorted, int64_t* pos_out) {
     std::vector<const int64_t*> base((size_t)world);
     for (int32_t r = 0; r < world; r++) base[r] = keys + (int64_t)r * stride;
-    return nkm_merge(base.data(), counts, world, rank, pos_out, true);
+    return nkm_merge(base.data(), counts, world, rank, pos_out, sorted == 0);
 }
 
 }  // extern "C"

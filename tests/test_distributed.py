@@ -175,21 +175,24 @@ def _merge_worker(rank, world, port, n_groups, reps, q):
     from nakama_amd import cluster
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["LOCAL_WORLD_SIZE"] = str(world)  # as torchrun sets it: the ranks split the host's cores
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         rng = np.random.default_rng(1000 + rank)
         # distinct keys across ranks (key % world == rank), ascending per rank
         keys = np.sort(rng.choice(np.arange(4 * n_groups, dtype=np.int64), n_groups, replace=False)) * world + rank
         cm = cluster.ClusterMatchmaker(None, dist, ("properties.mode", "properties.region"))
-        times = []
+        times, comm, cmerge = [], [], []
         for _ in range(reps):
             cp = cluster.ClusterPass()
             dist.barrier()
             t0 = time.perf_counter()
             cm.merge_keys(cp, keys, 10 * n_groups, 17 * n_groups)
             times.append(1e3 * (time.perf_counter() - t0))
+            comm.append(cp.local_stats["merge_comm_ms"])
+            cmerge.append(cp.local_stats["merge_c_ms"])
         got = [None] * world
-        dist.all_gather_object(got, (keys, cp.positions, cp.n_groups, times))
+        dist.all_gather_object(got, (keys, cp.positions, cp.n_groups, times, comm, cmerge))
         if rank == 0:
             q.put(got)
     finally:
@@ -219,6 +222,8 @@ def test_cluster_merge_at_c3_volume(world, n_groups):
     assert got[0][2] == world * n_groups
     assert np.array_equal(np.sort(allp), np.arange(world * n_groups))
     assert np.array_equal(allk[np.argsort(allp)], np.sort(allk))
-    med = sorted(got[0][3])[len(got[0][3]) // 2]
-    print(f"\ncluster merge world {world} x {n_groups} groups: rank-0 median {med:.2f} ms "
-          f"(all ranks: {[round(sorted(g[3])[2], 2) for g in got]})")
+    def med(x):
+        return sorted(x)[len(x) // 2]
+    print(f"\ncluster merge world {world} x {n_groups} groups: rank-0 median {med(got[0][3]):.2f} ms "
+          f"(collectives {med(got[0][4]):.2f}, C merge {med(got[0][5]):.2f}; all ranks' C merge: "
+          f"{[round(med(g[5]), 2) for g in got]})")
