@@ -43,7 +43,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 KERNELS = {0: "search_kernel", 1: "scan_kernel", 2: "mscan_kernel", 3: "rsmall_kernel", 4: "mscan_hash_kernel",
-           5: "rpack_kernel", 6: "rsrc_merge_kernel", 7: "rsrc_tile_kernel"}  # mm_matched.eval_kernel
+           5: "rpack_kernel", 6: "rsrc_rank_kernel", 7: "rsrc_tile_kernel"}  # mm_matched.eval_kernel
 WORKLOADS = {
     1: "C1: 10k solo 1v1, '+properties.mode:ranked +properties.region:eu'",
     2: "C2: skill-window range queries with ^boost, 1v1",
@@ -396,9 +396,15 @@ def main():
         # signature its values select), per second of the timed steps
         "pair_evals_per_s": pair_evals / total_t,
         # (row, candidate) pairs decided: over the rows that searched, the
-        # candidates of their search's source — what the reference's per-row
-        # bluge search evaluates (BASELINE.md GPU-side reporting), summed over ranks
+        # candidates of their search's source — the posting list of the
+        # query's most selective required term, which bluge's conjunction
+        # searcher walks (C3: the row's region list, 2 modes x 125k = 250k,
+        # not its 125k pool) — what the reference's per-row bluge search
+        # evaluates (BASELINE.md GPU-side reporting), summed over ranks.
+        # Check: pairs_decided_per_s x ms_per_step / 1e3 = searches_per_pass x
+        # that source length.
         "pairs_decided_per_s": pairs_decided / total_t,
+        "searches_per_pass": statistics.median(searched) if searched else None,
         # the host-to-HBM hand-over: the Insert() call that precedes each pass
         # (not part of value: inputs are resident when the timed region starts)
         "insert_ms": 1e3 * statistics.median(ins_times),

@@ -127,13 +127,15 @@ typedef struct mm_matched {
     int64_t eval_bytes;             /* algorithmic bytes of the search launches (DESIGN.md roofline) */
     int32_t eval_launches;          /* search kernel launches in the pass */
     int32_t n_batches;              /* replay batches */
-    int32_t eval_kernel;            /* query-eval kernel with the most bytes: 0 search, 1 scan, 2 mscan, 3 rsmall, 4 hashed mscan, 5 rpack, 6 range merge, 7 range tile */
+    int32_t eval_kernel;            /* query-eval kernel with the most bytes: 0 search, 1 scan, 2 mscan, 3 rsmall, 4 hashed mscan, 5 rpack, 6 range rank (multiway merge), 7 range tile */
     int32_t full_lists;             /* variable-score searches run as full lists (host-sorted), 0 for the oracle */
     const int64_t* group_created;   /* n_groups: CreatedAt of each group's last entry (its searching ticket) — the
                                        key a pool-sharded cluster merges rank results by (ABI 3) */
     int64_t pairs_decided;          /* (row, candidate) pairs the pass decided: over the rows that searched, the
-                                       candidates their search's source holds — what the reference's per-row
-                                       bluge search evaluates (ABI 4) */
+                                       candidates their search's source holds (the posting list of the
+                                       query's most selective MUST term, which bluge's conjunction walks:
+                                       C3's region list of 250k, not the 125k mode x region pool) — what
+                                       the reference's per-row bluge search evaluates (ABI 4) */
 } mm_matched;
 
 typedef struct mm_extract_list {
@@ -207,8 +209,10 @@ void mm_free_str_list(void* h, mm_str_list* out);
  * (is_candidates = 1) are returned in full exactly as by mm_process, and the
  * chosen groups are queued by mm_process_commit_deliver instead.  fn runs on
  * the delivery thread; it may call the handle's mutators and queries, not
- * mm_process*, mm_set_delivery, mm_delivery_flush or mm_destroy.  Entry points
- * of this section return MM_ERR_STATE when no delivery is set. */
+ * mm_process*, mm_set_delivery, mm_delivery_flush or mm_destroy (from the
+ * callback mm_set_delivery and mm_delivery_flush return MM_ERR_STATE and
+ * mm_destroy does nothing: each would wait for the thread it runs on).  Entry
+ * points of this section return MM_ERR_STATE when no delivery is set. */
 typedef void (*mm_deliver_fn)(void* ctx, const mm_matched* matched, int64_t pass_seq);
 /* fn NULL: deliver what is queued, then stop the thread.  Replaces an earlier
  * setting after delivering its queue. */

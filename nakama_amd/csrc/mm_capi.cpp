@@ -104,12 +104,22 @@ struct Delivery {
     }
 };
 std::mutex g_deliv_mu;
-std::map<void*, std::unique_ptr<Delivery>> g_deliv;
+// shared: a caller of push / flush holds its own reference, so a concurrent
+// mm_set_delivery / mm_destroy cannot free the Delivery under it (the last
+// reference joins the thread)
+std::map<void*, std::shared_ptr<Delivery>> g_deliv;
 
-Delivery* delivery_of(void* h) {
+std::shared_ptr<Delivery> delivery_of(void* h) {
     std::lock_guard<std::mutex> lk(g_deliv_mu);
     auto it = g_deliv.find(h);
-    return it == g_deliv.end() ? nullptr : it->second.get();
+    return it == g_deliv.end() ? nullptr : it->second;
+}
+// The calling thread is h's delivery thread (inside the callback): the calls
+// that would join or wait for that thread are refused with MM_ERR_STATE.
+bool on_delivery_thread(void* h) {
+    std::lock_guard<std::mutex> lk(g_deliv_mu);
+    auto it = g_deliv.find(h);
+    return it != g_deliv.end() && it->second->th.get_id() == std::this_thread::get_id();
 }
 // the pass's counts and statistics without its arrays (the result is queued)
 mm_matched summary_of(const mm_matched& m) {
@@ -146,7 +156,8 @@ void* mm_create(const mm_config* cfg) {
 }
 void mm_destroy(void* h) {
     try {
-        std::unique_ptr<Delivery> d;
+        if (on_delivery_thread(h)) return;  // from the callback: refused (the header forbids it)
+        std::shared_ptr<Delivery> d;
         {
             std::lock_guard<std::mutex> lk(g_deliv_mu);
             auto it = g_deliv.find(h);
@@ -213,8 +224,9 @@ void mm_free_matched(void* h, mm_matched* out) {
 }
 int mm_set_delivery(void* h, mm_deliver_fn fn, void* ctx, int32_t depth) {
     if (!h || (fn && depth < 1)) return MM_ERR_ARG;
+    if (on_delivery_thread(h)) return MM_ERR_STATE;  // it would join its own thread
     try {
-        std::unique_ptr<Delivery> old;
+        std::shared_ptr<Delivery> old;
         {
             std::lock_guard<std::mutex> lk(g_deliv_mu);
             auto it = g_deliv.find(h);
@@ -225,7 +237,7 @@ int mm_set_delivery(void* h, mm_deliver_fn fn, void* ctx, int32_t depth) {
         }
         old.reset();  // its queue delivered, its thread joined
         if (fn) {
-            std::unique_ptr<Delivery> d(new Delivery(static_cast<Handle*>(h), fn, ctx, (size_t)depth));
+            std::shared_ptr<Delivery> d = std::make_shared<Delivery>(static_cast<Handle*>(h), fn, ctx, (size_t)depth);
             std::lock_guard<std::mutex> lk(g_deliv_mu);
             g_deliv[h] = std::move(d);
         }
@@ -237,7 +249,7 @@ int mm_set_delivery(void* h, mm_deliver_fn fn, void* ctx, int32_t depth) {
 }
 int mm_process_deliver(void* h, mm_matched* summary) {
     if (!summary) return MM_ERR_ARG;
-    Delivery* d = delivery_of(h);
+    const std::shared_ptr<Delivery> d = delivery_of(h);
     if (!d) return h ? MM_ERR_STATE : MM_ERR_ARG;
     mm_matched m{};
     const int rc = guarded(h, [&](Handle& c) { return c.process(&m); });
@@ -253,7 +265,7 @@ int mm_process_deliver(void* h, mm_matched* summary) {
 int mm_process_commit_deliver(void* h, const int32_t* group_offsets, const mm_entry_ref* entries, int32_t n_groups,
                               mm_matched* summary) {
     if (!summary || (n_groups > 0 && (!group_offsets || !entries))) return MM_ERR_ARG;
-    Delivery* d = delivery_of(h);
+    const std::shared_ptr<Delivery> d = delivery_of(h);
     if (!d) return h ? MM_ERR_STATE : MM_ERR_ARG;
     mm_matched m{};
     const int rc = guarded(h, [&](Handle& c) { return c.process_commit(group_offsets, entries, n_groups, &m); });
@@ -263,7 +275,8 @@ int mm_process_commit_deliver(void* h, const int32_t* group_offsets, const mm_en
     return MM_OK;
 }
 int mm_delivery_flush(void* h) {
-    Delivery* d = delivery_of(h);
+    if (on_delivery_thread(h)) return MM_ERR_STATE;  // it would wait for itself
+    const std::shared_ptr<Delivery> d = delivery_of(h);
     if (!d) return h ? MM_ERR_STATE : MM_ERR_ARG;
     d->flush();
     return MM_OK;

@@ -137,6 +137,109 @@ uint64_t route_key(const mm_ticket& t, const std::vector<std::string>& fields, c
 
 }  // namespace nkm
 
+namespace {
+
+// The host threads of the cluster entry points: one persistent pool per
+// process (created on first use, its workers asleep between calls), so a
+// pass's merge starts no thread.  Sized like a handle's workers — the
+// process's CPUs over the node's local ranks — and capped at 8: the merge of
+// 8 x 175k keys is ~0.5 M cursor steps per thread there.  Calls from several
+// threads take turns (WorkPool runs one job at a time).
+struct MergePool {
+    std::mutex mu;
+    std::unique_ptr<nkm::WorkPool> pool;
+    nkm::WorkPool& get() {
+        if (!pool) {
+            unsigned n = std::thread::hardware_concurrency();
+            cpu_set_t cs;
+            if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = (unsigned)CPU_COUNT(&cs);
+            if (const char* lw = std::getenv("LOCAL_WORLD_SIZE")) n /= (unsigned)std::max(1, std::atoi(lw));
+            pool.reset(new nkm::WorkPool(std::max(1u, std::min(8u, n))));
+        }
+        return *pool;
+    }
+};
+MergePool& merge_pool() {
+    static MergePool* p = new MergePool();  // never destroyed: no join at process exit
+    return *p;
+}
+
+// fn(t, nt) for t in [0, nt) on the merge pool: nt grows with the work
+// (one thread per 2^18 units), 1 runs inline.
+void run_split(int64_t units, const std::function<void(int, int)>& fn) {
+    const int64_t want = std::max<int64_t>(1, units >> 18);
+    if (want == 1) return fn(0, 1);
+    MergePool& mp = merge_pool();
+    std::lock_guard<std::mutex> lk(mp.mu);
+    nkm::WorkPool& wp = mp.get();
+    const int nt = (int)std::min<int64_t>(want, wp.size());
+    wp.run((size_t)nt, [&](size_t t) { fn((int)t, nt); });
+}
+
+bool ascending(const int64_t* k, int64_t n) {
+    int64_t bad = 0;
+    for (int64_t i = 1; i < n; i++) bad |= (int64_t)(k[i] < k[i - 1]);  // vectorises
+    return bad == 0;
+}
+
+// pos[i] for my keys [i0, i1): every other rank's cursor starts at its first
+// key >= mine[i0] and moves with a 4-key compare per (i, q) — the cursors are
+// independent dependency chains, so the loop is throughput-bound.
+__attribute__((target("avx2,popcnt"))) int32_t merge_walk_avx2(const int64_t* mine, int64_t i0, int64_t i1,
+                                                                const int64_t* const* other, const int64_t* m, int nq,
+                                                                int64_t* pos) {
+    if (i0 >= i1) return 0;
+    int64_t J[64];
+    for (int q = 0; q < nq; q++) J[q] = std::lower_bound(other[q], other[q] + m[q], mine[i0]) - other[q];
+    int eq = 0;
+    for (int64_t i = i0; i < i1; i++) {
+        const int64_t k = mine[i];
+        const __m256i kv = _mm256_set1_epi64x(k);
+        int64_t acc = i;
+        for (int q = 0; q < nq; q++) {
+            const int64_t* o = other[q];
+            int64_t j = J[q];
+            for (;;) {
+                if (__builtin_expect(j + 4 <= m[q], 1)) {
+                    const __m256i v = _mm256_loadu_si256((const __m256i*)(o + j));
+                    const int lt = _mm256_movemask_pd(_mm256_castsi256_pd(_mm256_cmpgt_epi64(kv, v)));
+                    eq |= _mm256_movemask_pd(_mm256_castsi256_pd(_mm256_cmpeq_epi64(kv, v)));
+                    const int c = __builtin_popcount((unsigned)lt);
+                    j += c;
+                    if (c < 4) break;
+                } else {
+                    while (j < m[q] && o[j] < k) j++;
+                    eq |= j < m[q] && o[j] == k;
+                    break;
+                }
+            }
+            J[q] = j;
+            acc += j;
+        }
+        pos[i] = acc;
+    }
+    return eq != 0;
+}
+
+int32_t merge_walk_scalar(const int64_t* mine, int64_t i0, int64_t i1, const int64_t* const* other,
+                          const int64_t* m, int nq, int64_t* pos) {
+    if (i0 >= i1) return 0;
+    int32_t ties = 0;
+    for (int64_t i = i0; i < i1; i++) pos[i] = i;
+    for (int q = 0; q < nq; q++) {
+        const int64_t* o = other[q];
+        int64_t j = std::lower_bound(o, o + m[q], mine[i0]) - o;
+        for (int64_t i = i0; i < i1; i++) {
+            while (j < m[q] && o[j] < mine[i]) j++;
+            ties |= j < m[q] && o[j] == mine[i];
+            pos[i] += j;
+        }
+    }
+    return ties;
+}
+
+}  // namespace
+
 extern "C" {
 
 int32_t mm_route_keys(const mm_ticket* ts, int32_t n, const char* const* pool_fields, int32_t n_fields,
@@ -276,109 +379,6 @@ void mm_free_unpacked(void* set) { delete static_cast<Unpacked*>(set); }
 // positions are the stable order by (key, rank, index) and the return value
 // is 2.  Else 1 when one of my groups has the same key as another rank's
 // group, 0 otherwise.
-namespace {
-
-// The host threads of the cluster entry points: one persistent pool per
-// process (created on first use, its workers asleep between calls), so a
-// pass's merge starts no thread.  Sized like a handle's workers — the
-// process's CPUs over the node's local ranks — and capped at 8: the merge of
-// 8 x 175k keys is ~0.5 M cursor steps per thread there.  Calls from several
-// threads take turns (WorkPool runs one job at a time).
-struct MergePool {
-    std::mutex mu;
-    std::unique_ptr<nkm::WorkPool> pool;
-    nkm::WorkPool& get() {
-        if (!pool) {
-            unsigned n = std::thread::hardware_concurrency();
-            cpu_set_t cs;
-            if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = (unsigned)CPU_COUNT(&cs);
-            if (const char* lw = std::getenv("LOCAL_WORLD_SIZE")) n /= (unsigned)std::max(1, std::atoi(lw));
-            pool.reset(new nkm::WorkPool(std::max(1u, std::min(8u, n))));
-        }
-        return *pool;
-    }
-};
-MergePool& merge_pool() {
-    static MergePool* p = new MergePool();  // never destroyed: no join at process exit
-    return *p;
-}
-
-// fn(t, nt) for t in [0, nt) on the merge pool: nt grows with the work
-// (one thread per 2^18 units), 1 runs inline.
-void run_split(int64_t units, const std::function<void(int, int)>& fn) {
-    const int64_t want = std::max<int64_t>(1, units >> 18);
-    if (want == 1) return fn(0, 1);
-    MergePool& mp = merge_pool();
-    std::lock_guard<std::mutex> lk(mp.mu);
-    nkm::WorkPool& wp = mp.get();
-    const int nt = (int)std::min<int64_t>(want, wp.size());
-    wp.run((size_t)nt, [&](size_t t) { fn((int)t, nt); });
-}
-
-bool ascending(const int64_t* k, int64_t n) {
-    int64_t bad = 0;
-    for (int64_t i = 1; i < n; i++) bad |= (int64_t)(k[i] < k[i - 1]);  // vectorises
-    return bad == 0;
-}
-
-// pos[i] for my keys [i0, i1): every other rank's cursor starts at its first
-// key >= mine[i0] and moves with a 4-key compare per (i, q) — the cursors are
-// independent dependency chains, so the loop is throughput-bound.
-__attribute__((target("avx2,popcnt"))) int32_t merge_walk_avx2(const int64_t* mine, int64_t i0, int64_t i1,
-                                                                const int64_t* const* other, const int64_t* m, int nq,
-                                                                int64_t* pos) {
-    if (i0 >= i1) return 0;
-    int64_t J[64];
-    for (int q = 0; q < nq; q++) J[q] = std::lower_bound(other[q], other[q] + m[q], mine[i0]) - other[q];
-    int eq = 0;
-    for (int64_t i = i0; i < i1; i++) {
-        const int64_t k = mine[i];
-        const __m256i kv = _mm256_set1_epi64x(k);
-        int64_t acc = i;
-        for (int q = 0; q < nq; q++) {
-            const int64_t* o = other[q];
-            int64_t j = J[q];
-            for (;;) {
-                if (__builtin_expect(j + 4 <= m[q], 1)) {
-                    const __m256i v = _mm256_loadu_si256((const __m256i*)(o + j));
-                    const int lt = _mm256_movemask_pd(_mm256_castsi256_pd(_mm256_cmpgt_epi64(kv, v)));
-                    eq |= _mm256_movemask_pd(_mm256_castsi256_pd(_mm256_cmpeq_epi64(kv, v)));
-                    const int c = __builtin_popcount((unsigned)lt);
-                    j += c;
-                    if (c < 4) break;
-                } else {
-                    while (j < m[q] && o[j] < k) j++;
-                    eq |= j < m[q] && o[j] == k;
-                    break;
-                }
-            }
-            J[q] = j;
-            acc += j;
-        }
-        pos[i] = acc;
-    }
-    return eq != 0;
-}
-
-int32_t merge_walk_scalar(const int64_t* mine, int64_t i0, int64_t i1, const int64_t* const* other,
-                          const int64_t* m, int nq, int64_t* pos) {
-    if (i0 >= i1) return 0;
-    int32_t ties = 0;
-    for (int64_t i = i0; i < i1; i++) pos[i] = i;
-    for (int q = 0; q < nq; q++) {
-        const int64_t* o = other[q];
-        int64_t j = std::lower_bound(o, o + m[q], mine[i0]) - o;
-        for (int64_t i = i0; i < i1; i++) {
-            while (j < m[q] && o[j] < mine[i]) j++;
-            ties |= j < m[q] && o[j] == mine[i];
-            pos[i] += j;
-        }
-    }
-    return ties;
-}
-
-}  // namespace
-
 static int32_t nkm_merge(const int64_t* const* base, const int32_t* counts, int32_t world, int32_t rank,
                          int64_t* pos_out, bool check) {
     std::vector<int64_t> off((size_t)world + 1, 0);

@@ -252,8 +252,8 @@ public:
         // Workers that went to sleep during a long, uneven job (C3's walks
         // leave most of them idle for milliseconds) are woken now to spin for
         // the next job: a pass's next job then starts without a futex wake-up
-        // per worker on its critical path (NKM_PREWAKE=0: off).
-        if (prewake_ && sleepers_.load(std::memory_order_acquire) > 0) {
+        // per worker on its critical path.
+        if (sleepers_.load(std::memory_order_acquire) > 0) {
             {
                 std::lock_guard<std::mutex> lk(m_);
                 wake_.fetch_add(1, std::memory_order_release);
@@ -333,7 +333,6 @@ private:
     std::atomic<uint64_t> gen_{0};
     std::atomic<int> sleepers_{0};
     std::atomic<uint64_t> wake_{0};
-    const bool prewake_ = !(std::getenv("NKM_PREWAKE") && std::getenv("NKM_PREWAKE")[0] == '0');
     bool quit_ = false;
 };
 
@@ -548,7 +547,7 @@ struct PassStats {
     int full_lists = 0;  // variable-score searches run as full lists (host-sorted)
     int tier_lists = 0;  // variable-score searches run as top-tier lists (search_kernel path 2)
     // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel,
-    // 4 rsrc_merge_kernel, 5 rsrc_tile_kernel (range batches)
+    // 4 rsrc_rank_kernel, 5 rsrc_tile_kernel (range batches)
     static constexpr int kKernels = 6;
     double k_ms[kKernels] = {};         // HIP-event time of the launches
     bool mhash = false;                 // a batch's mscan ran hashed (mscan_hash_kernel)
@@ -1139,11 +1138,9 @@ public:
     bool dense_mode_ = true;
     bool pipe_mode_ = true;  // NKM_PIPE=0: the pool walks' merge runs after all walks, not beside them
     bool gpipe_mode_ = true; // NKM_GPIPE=0: no identity-pool shortcut (slot -> position map, copies gathered before the walks)
-    int mwait_us_ = 0;       // NKM_MWAIT: a pipelined merge chunk's sleep while the walks have not passed it (0: yield)
-    int merge_mult_ = 8;     // NKM_MCH: pipelined merge chunks per worker (the last one is the tail after the slowest walk)
+    static constexpr int kMergeMult = 8;  // pipelined merge chunks per worker (the last one is the tail after the slowest walk)
     bool runs_mode_ = true;    // NKM_RUNS=0: pools in contiguous runs take the per-row records + merge_rows
     bool pruns_mode_ = true;   // NKM_PRUNS=0: packed batches always plan through plan_pools
-    bool rleaf_mode_ = false;  // NKM_RLEAF=1: range pools' leaves gathered across the workers, not by each walker
     int32_t max_pres_ = 1;   // most presences of any ticket inserted (an entry bound of the pipelined merge)
     // NKM_FAST=0: every row takes the exact loop body, also when no two live
     // tickets share a session (the fast walk, replay_core.h) (A/B, tests)

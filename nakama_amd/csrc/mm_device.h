@@ -229,7 +229,7 @@ NKM_HD inline PackLayout pack_layout(uint64_t n, int S) {
 // rounded up to 256); a candidate that is not alive or holds no number in
 // `field`, and the padding, sort after every valid one (key INT64_MAX,
 // position | kRsrcInvalid), so the valid candidates are a prefix.
-constexpr uint32_t kRsrcTile = 1024;           // elements sorted in LDS by one workgroup (one per lane)
+constexpr uint32_t kRsrcTile = 512;            // elements sorted in LDS by one workgroup (four per lane)
 constexpr uint32_t kRsrcInvalid = 0x80000000u;
 struct DRangePool {
     uint32_t src_off, src_len;

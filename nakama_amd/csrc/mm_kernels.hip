@@ -1888,13 +1888,10 @@ uint64_t mscan_hash_work_words(const DMScan& ms) {
     const uint64_t w1 = ms.n_sigs + 1;
     return (uint64_t)ms.n_chunks * w1 + (uint64_t)(ms.n_chunks + 1) * w1 + (uint64_t)ms.n_chunks * ms.chunk;
 }
-// candidates per lane: gathered 2 or 4 (NKM_MHASH_J, default 4); contiguous
-// 2, 4 or 8 (NKM_MCONTIG_J, default 4)
-int mscan_hash_chunk_len(bool contig) {
-    const char* e = std::getenv(contig ? "NKM_MCONTIG_J" : "NKM_MHASH_J");
-    const int j = e ? std::atoi(e) : 0;
-    return (contig ? (j == 8 ? 8 : j == 2 ? 2 : 4) : (j == 2 ? 2 : 4)) * kBlock;
-}
+// candidates per lane: 4, gathered or contiguous (C4: 4 and 8 per lane
+// measured the same, profiles/r05/r05ar_contig_j_kernel_ab.txt; the 2 / 8
+// instantiations stay for tools/mhash_bench)
+int mscan_hash_chunk_len(bool) { return 4 * kBlock; }
 
 // Candidates per lane: 2 (C3 1M measured 21.7 us at 2, 24.6 at 4, 35.2 at 8
 // candidates per lane — more, shorter waves hide more latency; the 4 / 8
@@ -1905,124 +1902,338 @@ int mscan_max_fields() { return kMaxMField; }
 int mscan_max_clauses() { return kMaxMClause; }
 
 // ---- range sources (range_walk.h) -----------------------------------------
-// A range batch's pools sorted by (value, source position): rsrc_tile_kernel
-// sorts tiles of kRsrcTile elements in LDS, rsrc_merge_kernel merges runs of R
-// into runs of 2R (R = kRsrcTile, 2 kRsrcTile, ...), rsrc_bounds_kernel finds
-// the clauses' bounds in the sorted keys.  Elements are (key, position) pairs,
-// distinct within a pool (positions are), so a merge places an element at its
-// index in its run plus its rank in the partner run — a binary search, no
-// ties to break.
+// A range batch's pools sorted by (value, source position).  rsrc_tile_kernel
+// sorts tiles of kRsrcTile elements in LDS (4 per lane; 512-element tiles keep
+// ~200 workgroups busy on C2's 100k candidates instead of one CU's LDS per
+// 4k), then each rsrc_rank_kernel launch merges groups of up to kRsrcGroup
+// runs of R into one run of 8R: an element's place is its index in its run
+// plus its rank in each other run of its group.  A workgroup holds 256
+// consecutive elements of one run; per partner run it reads every
+// stride-th element (the run's sample, one strided load round), ranks its
+// elements among the samples in LDS, loads the partner window its elements
+// fall in (coalesced, ~256 + 2 strides of elements) into LDS and finishes
+// each rank by a log2(stride)-step search there — no per-element binary
+// search through L2.  C2's 25k-candidate pools: tile + 2 rank launches.  The
+// last launch also answers the bound queries (the first sorted element of a
+// pool >= or > a clause bound = the sum of its ranks in the pool's runs) and
+// writes positions only: the host reads no key.  Ranks in a run to the left
+// count elements <= the element, to the right elements <, so equal elements
+// (the tile's padding) land on distinct places.
 
 __device__ __forceinline__ bool rsrc_less(int64_t ka, uint32_t va, int64_t kb, uint32_t vb) {
     return ka < kb || (ka == kb && va < vb);
 }
+__device__ __forceinline__ bool rsrc_leq(int64_t ka, uint32_t va, int64_t kb, uint32_t vb) {
+    return ka < kb || (ka == kb && va <= vb);
+}
 
-// One tile per workgroup of kRsrcTile lanes, one element each (loaded
-// coalesced: the posting entry, then alive / kind / value of that slot), then
-// merged in LDS from runs of 1 up to the tile: each lane's binary search in
-// the partner run is log2(run) dependent LDS reads, one element per lane.
-constexpr int kRsrcBlock = (int)kRsrcTile;
-__global__ __launch_bounds__(kRsrcBlock) void rsrc_tile_kernel(DStore st, const DRangePool* __restrict__ pools,
-                                                               const DRangeTile* __restrict__ tiles,
-                                                               int64_t* __restrict__ okey, uint32_t* __restrict__ opos) {
-    __shared__ int64_t sk[2][kRsrcTile];
-    __shared__ uint32_t sv[2][kRsrcTile];
+// One tile per workgroup of kRsrcTile / 4 lanes, 4 consecutive elements per
+// lane (the posting entries, then every element's alive / kind / value
+// gathers in one round), sorted in registers, then merged in LDS from runs of
+// 4 up to the tile: a lane's 4 binary searches in the partner run are
+// independent (log2(run) LDS reads each, in flight together).  Positions
+// past the tile's length hold (INT64_MAX, 0xFFFFFFFF): they sort last and
+// are not written.
+constexpr int kRsrcTileThreads = (int)(kRsrcTile / 4);
+__global__ __launch_bounds__(kRsrcTileThreads) void rsrc_tile_kernel(DStore st, const DRangePool* __restrict__ pools,
+                                                                     const DRangeTile* __restrict__ tiles,
+                                                                     int64_t* __restrict__ okey,
+                                                                     uint32_t* __restrict__ opos) {
+    __shared__ int64_t sk[kRsrcTile];
+    __shared__ uint32_t sv[kRsrcTile];
     const DRangeTile t = tiles[blockIdx.x];
     const DRangePool P = pools[t.pool];
     const int64_t* __restrict__ fv = st.fval[P.field];
     const uint8_t* __restrict__ fk = st.fkind[P.field];
-    const uint32_t e = threadIdx.x;
-    const uint32_t i = t.start + e;  // position in the pool's source
-    int64_t k = INT64_MAX;
-    uint32_t v = kRsrcInvalid | i;
-    if (e < t.len && i < P.src_len) {
-        const uint32_t s = st.postings[P.src_off + i];
-        if (st.alive[s] && fk[s] == KIND_NUMERIC) {
-            k = fv[s];
-            v = i;
+    const uint32_t e0 = threadIdx.x * 4;
+    int64_t k[4];
+    uint32_t v[4];
+    {
+        const uint32_t i0 = t.start + e0;
+        const uint32_t last = P.src_len - 1;  // a tile exists only for a pool with candidates
+        uint32_t sl[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) sl[j] = st.postings[P.src_off + min(i0 + j, last)];
+        uint8_t al[4], kd[4];
+        int64_t val[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            al[j] = st.alive[sl[j]];
+            kd[j] = fk[sl[j]];
+            val[j] = fv[sl[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t e = e0 + j, i = i0 + j;
+            const bool in_tile = e < t.len, in_src = i < P.src_len;
+            const bool ok = in_tile && in_src && al[j] && kd[j] == KIND_NUMERIC;
+            k[j] = ok ? val[j] : INT64_MAX;
+            v[j] = !in_tile ? 0xFFFFFFFFu : ok ? i : (kRsrcInvalid | i);
         }
     }
-    sk[0][e] = k;
-    sv[0][e] = v;
+    // sort the lane's 4 in registers (5 compare-exchanges)
+    auto cx = [&](int a, int b) {
+        if (rsrc_less(k[b], v[b], k[a], v[a])) {
+            const int64_t tk = k[a];
+            k[a] = k[b];
+            k[b] = tk;
+            const uint32_t tv = v[a];
+            v[a] = v[b];
+            v[b] = tv;
+        }
+    };
+    cx(0, 1);
+    cx(2, 3);
+    cx(0, 2);
+    cx(1, 3);
+    cx(1, 2);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        sk[e0 + j] = k[j];
+        sv[e0 + j] = v[j];
+    }
     __syncthreads();
-    int b = 0;
-    for (uint32_t r = 1; r < t.len; r <<= 1, b ^= 1) {
-        if (e < t.len) {
-            k = sk[b][e];  // the element now at this position
-            v = sv[b][e];
-            const uint32_t run = e / r, ps = (run ^ 1u) * r;
-            uint32_t o = e;
-            if (ps < t.len) {
-                uint32_t lo = ps, hi = min(ps + r, t.len);
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (rsrc_less(sk[b][mid], sv[b][mid], k, v)) lo = mid + 1;
-                    else hi = mid;
+    for (uint32_t r = 4; r < kRsrcTile; r <<= 1) {
+        const uint32_t run = e0 / r, ps = (run ^ 1u) * r;
+        const bool right = run & 1u;  // the partner run is to the left: count elements <=
+        uint32_t lo[4], len[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            k[j] = sk[e0 + j];
+            v[j] = sv[e0 + j];
+            lo[j] = ps;
+            len[j] = r;
+        }
+        for (uint32_t step = r; step > 0; step >>= 1) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (len[j] == 0) continue;
+                const uint32_t half = len[j] >> 1, mid = lo[j] + half;
+                const bool go = right ? rsrc_leq(sk[mid], sv[mid], k[j], v[j]) : rsrc_less(sk[mid], sv[mid], k[j], v[j]);
+                if (go) {
+                    lo[j] = mid + 1;
+                    len[j] -= half + 1;
+                } else {
+                    len[j] = half;
                 }
-                o = (run & ~1u) * r + (e - run * r) + (lo - ps);
             }
-            sk[b ^ 1][o] = k;
-            sv[b ^ 1][o] = v;
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) o[j] = (run & ~1u) * r + (e0 + j - run * r) + (lo[j] - ps);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            sk[o[j]] = k[j];
+            sv[o[j]] = v[j];
         }
         __syncthreads();
     }
-    if (e < t.len) {
-        const uint64_t base = (uint64_t)P.out_off + t.start;
-        okey[base + e] = sk[b][e];
-        opos[base + e] = sv[b][e];
-    }
+    const uint64_t base = (uint64_t)P.out_off + t.start;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (e0 + j < t.len) {
+            okey[base + e0 + j] = sk[e0 + j];
+            opos[base + e0 + j] = sv[e0 + j];
+        }
 }
 
-// Runs of R -> runs of 2R over every pool at once (one thread per element;
-// blk_pool: the pool of each 256-element block, pools being 256-aligned).
-__global__ __launch_bounds__(kBlock) void rsrc_merge_kernel(const DRangePool* __restrict__ pools,
-                                                            const uint32_t* __restrict__ blk_pool,
-                                                            const int64_t* __restrict__ ik, const uint32_t* __restrict__ ip,
-                                                            int64_t* __restrict__ ok, uint32_t* __restrict__ op, uint32_t R) {
-    const DRangePool P = pools[blk_pool[blockIdx.x]];
-    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t e = g - P.out_off;
-    const int64_t k = ik[g];
-    const uint32_t v = ip[g];
-    const uint32_t run = e / R, ps = (run ^ 1u) * R;
-    uint32_t o = e;
-    if (ps < P.pad_len) {
-        const int64_t* __restrict__ bk = ik + P.out_off;
-        const uint32_t* __restrict__ bp = ip + P.out_off;
-        uint32_t lo = ps, hi = min(ps + R, P.pad_len);
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (rsrc_less(bk[mid], bp[mid], k, v)) lo = mid + 1;
-            else hi = mid;
+// Groups of up to kRsrcGroup runs of R -> one run each, over every pool at
+// once: one workgroup per 256 elements (blk_pool: the pool of each
+// 256-element block; pools and runs are 256-aligned, so a block lies in one
+// run).  Blocks past n_eblk answer bound queries (the last launch: ok ==
+// nullptr, the pool's runs are one group).
+constexpr uint32_t kRsrcGroup = 8;
+constexpr uint32_t kRsrcSamples = 128;                           // per partner run at most
+constexpr uint32_t kRsrcWin = 3584;                              // window elements in LDS (42 KB)
+__device__ __forceinline__ uint32_t rsrc_stride(uint32_t R) { return max(32u, R / kRsrcSamples); }
+
+__global__ __launch_bounds__(kBlock) void rsrc_rank_kernel(const DRangePool* __restrict__ pools,
+                                                           const uint32_t* __restrict__ blk_pool, uint32_t n_eblk,
+                                                           const int64_t* __restrict__ ik, const uint32_t* __restrict__ ip,
+                                                           int64_t* __restrict__ ok, uint32_t* __restrict__ op, uint32_t R,
+                                                           const DRangeBound* __restrict__ q, uint32_t nq,
+                                                           uint32_t* __restrict__ bounds) {
+    if (blockIdx.x >= n_eblk) {
+        const uint32_t t = (blockIdx.x - n_eblk) * kBlock + threadIdx.x;
+        if (t >= nq) return;
+        const DRangeBound b = q[t];
+        const DRangePool P = pools[b.pool];
+        const int64_t* __restrict__ kk = ik + P.out_off;
+        uint32_t lo[kRsrcGroup], len[kRsrcGroup];
+#pragma unroll
+        for (uint32_t g = 0; g < kRsrcGroup; g++) {
+            lo[g] = g * R;
+            len[g] = g * R < P.pad_len ? min(R, P.pad_len - g * R) : 0u;
         }
-        o = (run & ~1u) * R + (e - run * R) + (lo - ps);
+        for (uint32_t step = R; step > 0; step >>= 1) {
+#pragma unroll
+            for (uint32_t g = 0; g < kRsrcGroup; g++) {
+                if (len[g] == 0) continue;
+                const uint32_t half = len[g] >> 1, mid = lo[g] + half;
+                if (b.upper ? kk[mid] <= b.key : kk[mid] < b.key) {
+                    lo[g] = mid + 1;
+                    len[g] -= half + 1;
+                } else {
+                    len[g] = half;
+                }
+            }
+        }
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t g = 0; g < kRsrcGroup; g++) c += g * R < P.pad_len ? lo[g] - g * R : 0u;
+        bounds[t] = c;
+        return;
     }
-    ok[(uint64_t)P.out_off + o] = k;
+    __shared__ int64_t samk[kRsrcGroup * kRsrcSamples];
+    __shared__ uint32_t samv[kRsrcGroup * kRsrcSamples];
+    __shared__ int64_t wk[kRsrcWin];
+    __shared__ uint32_t wv[kRsrcWin];
+    __shared__ uint32_t wlo[kRsrcGroup], whi[kRsrcGroup];
+    const DRangePool P = pools[blk_pool[blockIdx.x]];
+    const uint32_t gi = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t e = gi - P.out_off;
+    const int64_t k = ik[gi];
+    const uint32_t v = ip[gi];
+    const int64_t* __restrict__ bk = ik + P.out_off;
+    const uint32_t* __restrict__ bp = ip + P.out_off;
+    const uint32_t a = e / R, g0 = a - a % kRsrcGroup;
+    const uint32_t S = rsrc_stride(R);
+    // the group's runs: start and length (0: absent, or this block's own run)
+    uint32_t rs[kRsrcGroup], rl[kRsrcGroup];
+#pragma unroll
+    for (uint32_t g = 0; g < kRsrcGroup; g++) {
+        rs[g] = (g0 + g) * R;
+        rl[g] = (g0 + g != a && rs[g] < P.pad_len) ? min(R, P.pad_len - rs[g]) : 0u;
+    }
+    // the partners' samples (element j * S of each), one strided round
+    for (uint32_t x = threadIdx.x; x < kRsrcGroup * kRsrcSamples; x += kBlock) {
+        const uint32_t g = x / kRsrcSamples, j = x % kRsrcSamples;
+        uint32_t len = 0, st0 = 0;
+#pragma unroll
+        for (uint32_t h = 0; h < kRsrcGroup; h++)
+            if (h == g) {
+                len = rl[h];
+                st0 = rs[h];
+            }
+        if (j * S < len) {
+            samk[x] = bk[st0 + j * S];
+            samv[x] = bp[st0 + j * S];
+        }
+    }
+    __syncthreads();
+    // per partner: the window [r_lo, r_hi) of its run that holds this
+    // element's rank beyond r_lo (r_lo elements are certainly before it)
+    uint32_t r_lo[kRsrcGroup], r_hi[kRsrcGroup];
+#pragma unroll
+    for (uint32_t g = 0; g < kRsrcGroup; g++) {
+        r_lo[g] = r_hi[g] = 0;
+        if (rl[g] == 0) continue;
+        const bool left = g0 + g < a;  // count partner elements <= this one, else <
+        const uint32_t ns = (rl[g] + S - 1) / S;
+        uint32_t lo = 0, len = ns;
+        const int64_t* sk_ = samk + g * kRsrcSamples;
+        const uint32_t* sv_ = samv + g * kRsrcSamples;
+        while (len > 0) {
+            const uint32_t half = len >> 1, mid = lo + half;
+            if (left ? rsrc_leq(sk_[mid], sv_[mid], k, v) : rsrc_less(sk_[mid], sv_[mid], k, v)) {
+                lo = mid + 1;
+                len -= half + 1;
+            } else {
+                len = half;
+            }
+        }
+        if (lo > 0) {
+            r_lo[g] = (lo - 1) * S + 1;
+            r_hi[g] = min(lo * S, rl[g]);
+        }
+    }
+    // the block's window per partner: its first element's r_lo to its last
+    // element's r_hi (the block's elements ascend, so do their windows)
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (uint32_t g = 0; g < kRsrcGroup; g++) wlo[g] = r_lo[g];
+    if (threadIdx.x == kBlock - 1)
+#pragma unroll
+        for (uint32_t g = 0; g < kRsrcGroup; g++) whi[g] = r_hi[g];
+    __syncthreads();
+    uint32_t o = g0 * R + (e - a * R);
+    // rounds: as many partners' windows as fit in LDS; a window larger than
+    // the buffer is searched in global memory (log2(S) steps).  Every array
+    // is indexed by unrolled constants (registers, no scratch); the round
+    // plan is the same on every lane (wlo / whi are shared).
+    uint32_t base[kRsrcGroup], round_of[kRsrcGroup], wlen[kRsrcGroup];
+    uint32_t used = 0, nround = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < kRsrcGroup; g++) {
+        wlen[g] = whi[g] > wlo[g] ? whi[g] - wlo[g] : 0u;
+        if (wlen[g] > kRsrcWin) {
+            base[g] = UINT32_MAX;
+            round_of[g] = nround;
+            continue;
+        }
+        if (used + wlen[g] > kRsrcWin) {
+            nround++;
+            used = 0;
+        }
+        base[g] = used;
+        round_of[g] = nround;
+        used += wlen[g];
+    }
+    for (uint32_t rnd = 0; rnd <= nround; rnd++) {
+#pragma unroll
+        for (uint32_t g = 0; g < kRsrcGroup; g++) {
+            if (round_of[g] != rnd || base[g] == UINT32_MAX || wlen[g] == 0) continue;
+            const uint32_t src = rs[g] + wlo[g];
+            for (uint32_t x = threadIdx.x; x < wlen[g]; x += kBlock) {
+                wk[base[g] + x] = bk[src + x];
+                wv[base[g] + x] = bp[src + x];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t g = 0; g < kRsrcGroup; g++) {
+            if (round_of[g] != rnd || rl[g] == 0) continue;
+            const bool left = g0 + g < a;
+            uint32_t lo = r_lo[g], len = r_hi[g] - r_lo[g];
+            if (base[g] != UINT32_MAX) {
+                const int64_t* wk_ = wk + base[g] - wlo[g];
+                const uint32_t* wv_ = wv + base[g] - wlo[g];
+                while (len > 0) {
+                    const uint32_t half = len >> 1, mid = lo + half;
+                    if (left ? rsrc_leq(wk_[mid], wv_[mid], k, v) : rsrc_less(wk_[mid], wv_[mid], k, v)) {
+                        lo = mid + 1;
+                        len -= half + 1;
+                    } else {
+                        len = half;
+                    }
+                }
+            } else {
+                const int64_t* gk_ = bk + rs[g];
+                const uint32_t* gv_ = bp + rs[g];
+                while (len > 0) {
+                    const uint32_t half = len >> 1, mid = lo + half;
+                    if (left ? rsrc_leq(gk_[mid], gv_[mid], k, v) : rsrc_less(gk_[mid], gv_[mid], k, v)) {
+                        lo = mid + 1;
+                        len -= half + 1;
+                    } else {
+                        len = half;
+                    }
+                }
+            }
+            o += lo;
+        }
+        __syncthreads();
+    }
+    if (ok) ok[(uint64_t)P.out_off + o] = k;
     op[(uint64_t)P.out_off + o] = v;
 }
 
-__global__ __launch_bounds__(kBlock) void rsrc_bounds_kernel(const DRangePool* __restrict__ pools,
-                                                             const int64_t* __restrict__ key,
-                                                             const DRangeBound* __restrict__ q, uint32_t nq,
-                                                             uint32_t* __restrict__ out) {
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= nq) return;
-    const DRangeBound b = q[t];
-    const DRangePool P = pools[b.pool];
-    const int64_t* __restrict__ k = key + P.out_off;
-    uint32_t lo = 0, hi = P.pad_len;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (b.upper ? k[mid] <= b.key : k[mid] < b.key) lo = mid + 1;
-        else hi = mid;
-    }
-    out[t] = lo;
-}
-
 // The whole sort + bounds.  Buffers: keys / positions 2 x n_elems each (ping-
-// pong); the sorted ones end in *which (0 or 1).  Event pairs: ev_tile around
-// the tile launch, ev_merge[2m], ev_merge[2m + 1] around merge launch m (at
-// most max_merge of them).  Returns the number of merge launches in *n_merge.
+// pong); the sorted positions end in d_pos[*which].  Event pairs: ev_tile
+// around the tile launch, ev_merge[2m], ev_merge[2m + 1] around rank launch m
+// (at most max_merge of them).  Returns the number of rank launches in
+// *n_merge (at least one: it also answers the bound queries).
 hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max_pad, const DRangeTile* d_tiles,
                        uint32_t n_tiles, const uint32_t* d_blk_pool, uint32_t n_elems, int64_t* d_key[2],
                        uint32_t* d_pos[2], const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds, int* which,
@@ -2032,18 +2243,23 @@ hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max
     *n_merge = 0;
     if (n_elems == 0 || n_tiles == 0) return hipSuccess;
     if (n_elems % kBlock) return hipErrorInvalidValue;
-    hipExtLaunchKernelGGL(rsrc_tile_kernel, dim3(n_tiles), dim3(kRsrcBlock), 0, stream, ev_tile0, ev_tile1, 0, st,
+    hipExtLaunchKernelGGL(rsrc_tile_kernel, dim3(n_tiles), dim3(kRsrcTileThreads), 0, stream, ev_tile0, ev_tile1, 0, st,
                           d_pools, d_tiles, d_key[0], d_pos[0]);
     int b = 0, m = 0;
-    for (uint32_t R = kRsrcTile; R < max_pad; R <<= 1, b ^= 1, m++) {
+    const uint32_t n_eblk = n_elems / kBlock;
+    for (uint64_t R = kRsrcTile;; R *= kRsrcGroup, b ^= 1, m++) {
         if (m >= max_merge) return hipErrorInvalidValue;
-        hipExtLaunchKernelGGL(rsrc_merge_kernel, dim3(n_elems / kBlock), dim3(kBlock), 0, stream, ev_merge[2 * m],
-                              ev_merge[2 * m + 1], 0, d_pools, d_blk_pool, d_key[b], d_pos[b], d_key[b ^ 1], d_pos[b ^ 1],
-                              R);
+        const bool last = R * kRsrcGroup >= max_pad;
+        const uint32_t qblk = last ? (nq + kBlock - 1) / kBlock : 0;
+        hipExtLaunchKernelGGL(rsrc_rank_kernel, dim3(n_eblk + qblk), dim3(kBlock), 0, stream, ev_merge[2 * m],
+                              ev_merge[2 * m + 1], 0, d_pools, d_blk_pool, n_eblk, d_key[b], d_pos[b],
+                              last ? nullptr : d_key[b ^ 1], d_pos[b ^ 1], (uint32_t)R, d_q, last ? nq : 0u, d_bounds);
+        if (last) {
+            b ^= 1;
+            m++;
+            break;
+        }
     }
-    if (nq)
-        hipLaunchKernelGGL(rsrc_bounds_kernel, dim3((nq + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, d_pools,
-                           d_key[b], d_q, nq, d_bounds);
     *which = b;
     *n_merge = m;
     return hipGetLastError();

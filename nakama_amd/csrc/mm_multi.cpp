@@ -717,8 +717,10 @@ void MultiCore::merge_groups(const std::vector<mm_matched>& outs, MatchedHold* h
     for (auto& o : outs)
         for (int32_t g = 1; g < o.n_groups && asc; g++) asc = o.group_created[g - 1] <= o.group_created[g];
     unsigned W = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const char* mm_env = std::getenv("NKM_MERGE_MIN");  // the parallel merge's threshold (tests: 1)
-    const size_t kMergeMin = mm_env ? (size_t)std::max(1, std::atoi(mm_env)) : (size_t)65536;
+    // the parallel merge's threshold; NKM_PARALLEL=force (the host paths' "at
+    // any size" switch, tests) takes it at every size
+    const char* par_env = std::getenv("NKM_PARALLEL");
+    const size_t kMergeMin = par_env && !std::strcmp(par_env, "force") ? 1 : (size_t)65536;
     if (ng < kMergeMin || !asc) W = 1;  // small (or, defensively, unsorted) lists: one serial merge
     // splitters: every (ng / 64W)-th key of every list, sorted, at the W - 1 quantiles
     std::vector<int64_t> cut;  // W + 1 keys: [cut[p], cut[p + 1]) is range p

@@ -564,7 +564,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     const bool pipe = few && pipe_mode_ && !dense_ids.empty() && dense_ids.size() == ng && nch0 > 1;
     // the pipelined merge's chunks: the last one waits for the slowest walk,
     // so its size is the merge's tail (NKM_MCH: chunks per worker)
-    const size_t nch = pipe ? (size_t)wp.size() * (size_t)merge_mult_ : nch0;
+    const size_t nch = pipe ? (size_t)wp.size() * (size_t)kMergeMult : nch0;
     // Identity pools: when every pool's rows are its list in list order
     // (C3 / C4: every member of a pool of fresh tickets searches, and batch
     // order is scan order) row j's ticket is list position j — no slot ->
@@ -609,6 +609,10 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     if (ident)
         for (uint32_t gi : dense_ids) dense_pools_[gi].identity = true;
     std::unique_ptr<std::atomic<uint32_t>[]> gfront(gpipe ? new std::atomic<uint32_t>[ng] : nullptr);
+    // a task of the pipelined job threw: the tasks waiting on others (merge
+    // chunks on the walks' cuts, walks on the gather front) return instead of
+    // spinning, and WorkPool::run rethrows the error once every task is done
+    std::atomic<bool> job_failed{false};
     std::unique_ptr<std::atomic<uint8_t>[]> gdone(gpipe ? new std::atomic<uint8_t>[ng * ntask_g] : nullptr);
     if (gpipe) {
         for (size_t gi = 0; gi < ng; gi++) gfront[gi].store(0);
@@ -617,6 +621,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
             DensePool& D = dense_pools_[gi];
             D.pieces = (uint32_t)ntask_g;
             D.front = &gfront[gi];
+            D.abort = &job_failed;
         }
     }
     // piece t of every pool, then each pool's published prefix advanced over
@@ -701,12 +706,11 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
         static thread_local std::vector<uint64_t> span;  // per pool: records [a, b) of the chunk
         span.assign(ng, 0);
         for (size_t gi = 0; gi < ng; gi++) {
-            // waiting for the walks: sched_yield (NKM_MWAIT=N: asleep N µs at a
-            // time — measured slower, walks sum 13.5-14 -> 15-16 ms on C3,
-            // profiles/r05/r05l_mwait_ab.txt)
+            // waiting for the walks: sched_yield (sleeping instead measured
+            // slower, profiles/r05/r05l_mwait_ab.txt)
             while (prog[gi].ncut.load(std::memory_order_acquire) <= c) {
-                if (mwait_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(mwait_us_));
-                else std::this_thread::yield();
+                if (job_failed.load(std::memory_order_relaxed)) return;
+                std::this_thread::yield();
             }
             // the chunk's records [a, b) from the walk's cuts (no search: a
             // binary search per pool per chunk was a miss chain each, 64
@@ -900,9 +904,14 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     if (pipe) {
         const size_t ngt = gpipe ? ntask_g : 0;
         wp.run(ntask + ngt + nch, [&](size_t t) {
-            if (t < ntask) worker(t);
-            else if (t < ntask + ngt) gather_piece(t - ntask);
-            else merge_chunk(t - ntask - ngt);
+            try {
+                if (t < ntask) worker(t);
+                else if (t < ntask + ngt) gather_piece(t - ntask);
+                else merge_chunk(t - ntask - ngt);
+            } catch (...) {
+                job_failed.store(true);
+                throw;
+            }
         });
         size_t G = 0, E = 0, X = 0;  // totals: the pools' sentinels
         for (size_t gi = 0; gi < ng; gi++) {

@@ -2,8 +2,8 @@
 // remaining rows are all range-source searches (Sig::rs_field: a pool term and
 // numeric ranges on one field, e.g. C2's skill windows with ^boost) is decided
 // in ONE batch.  The device sorts every pool's candidates by their value and
-// finds each signature's range bounds in that order (rsrc_tile / rsrc_merge /
-// rsrc_bounds kernels); the host walks each pool's rows on its own worker
+// finds each signature's range bounds in that order (rsrc_tile /
+// rsrc_rank kernels); the host walks each pool's rows on its own worker
 // with a min tree over the sorted candidates, so a row's next hit costs
 // O(log n) instead of a walk over its hit list past every earlier selection
 // (matchmaker_process.go:86-130 over bluge's numeric range searcher,
@@ -294,12 +294,11 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     grow_to(rs_tiers_, (size_t)nq + ns);
     const size_t tch = ns >= 512 ? (size_t)wp.size() * 2 : 1;
     // every pool's leaves (slot, rank, HotRec and Intervals copies, the
-    // slot -> leaf maps), in pieces: by the pool's walker before its walk (the
-    // walk then finds them in this core's cache), or (NKM_RLEAF=1) across the
-    // workers in the tiers' job — measured slower on C2 (its walks then read
-    // other cores' lines: slowest walk 1.7 -> 2.0-2.7 ms, profiles/r05/r05j)
+    // slot -> leaf maps), in pieces, by the pool's walker before its walk (the
+    // walk then finds them in this core's cache; gathering them across the
+    // workers measured slower on C2 — its walks then read other cores' lines:
+    // slowest walk 1.7 -> 2.0-2.7 ms, profiles/r05/r05j)
     constexpr uint32_t kLeafPiece = 4096;
-    const bool leaves_in_job = rleaf_mode_;
     std::vector<uint64_t> piece_at{0};  // pools' pieces, prefix
     for (size_t p = 0; p < ng; p++) {
         RangePoolHost& H = rs_pools_[p];
@@ -336,12 +335,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             H.livl[j] = intervals_[s];
         }
     };
-    const size_t njob = tch + (leaves_in_job ? npiece : 0);
-    sweep(njob > 1 ? njob : 1, [&](size_t c) {
-        if (c >= tch) {
-            leaf_piece(c - tch);
-            return;
-        }
+    sweep(tch, [&](size_t c) {
         static thread_local std::vector<RRange> tmp;
         for (size_t k = ns * c / tch; k < ns * (c + 1) / tch; k++) {
             const Sig& s = sigs_[lsig[k]];
@@ -382,8 +376,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             const DRangePool& d = H.d;
             const auto tb0 = clk::now();
             const uint32_t nv = valid[p];
-            if (!leaves_in_job)
-                for (uint64_t q = piece_at[p]; q < piece_at[p + 1]; q++) leaf_piece(q);
+            for (uint64_t q = piece_at[p]; q < piece_at[p + 1]; q++) leaf_piece(q);
             H.src.n = nv;
             H.src.slot = H.slot.data();
             H.src.rank = H.rank.data();
@@ -430,11 +423,15 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     const auto t4 = clk::now();
     // algorithmic bytes: the tile kernel reads every source entry's slot id and
     // alive flag (5 B), the valid candidates' kind and value (9 B), and writes
-    // each element's key and position (12 B); a merge reads and writes them
+    // each element's key and position (12 B); a rank launch reads them and
+    // writes them (the last one: the position only, and the bound queries:
+    // 16 B read, 4 B written each; the runs' binary searches re-read lines
+    // already in L2 and are not counted)
     uint64_t nvalid = 0;
     for (uint32_t v : valid) nvalid += v;
     stats.k_bytes[5] += (int64_t)(src_total * 5 + nvalid * 9 + n_elems * 12);
-    stats.k_bytes[4] += (int64_t)(n_merge * n_elems * 24);
+    if (n_merge > 0) stats.k_bytes[4] += (int64_t)((uint64_t)n_merge * n_elems * 12 + (uint64_t)(n_merge - 1) * n_elems * 12 +
+                                                   n_elems * 4 + (uint64_t)nq * 20);
     stats.pair_evals += (int64_t)src_total;
     for (uint64_t q : task_pairs) stats.pairs_decided += (int64_t)q;
     for (uint64_t h : task_hits) stats.par_hits += h;

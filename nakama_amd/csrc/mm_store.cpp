@@ -109,10 +109,7 @@ Core::Core(const mm_config& cfg) : cfg_(cfg) {
     if (const char* e = std::getenv("NKM_GPIPE")) gpipe_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_RUNS")) runs_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_PRUNS")) pruns_mode_ = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("NKM_RLEAF")) rleaf_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_CDIRECT")) custom_direct_mode_ = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("NKM_MWAIT")) mwait_us_ = std::max(0, std::min(1000, std::atoi(e)));
-    if (const char* e = std::getenv("NKM_MCH")) merge_mult_ = std::max(1, std::min(64, std::atoi(e)));
     if (const char* e = std::getenv("NKM_FAST")) fast_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_FULLVAR")) full_var_mode_ = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("NKM_MHASH")) mhash_mode_ = std::atoi(e);

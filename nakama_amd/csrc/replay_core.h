@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <stdexcept>
 #include <cstring>
 #include <utility>
 #include <vector>
@@ -664,6 +665,9 @@ struct DensePool {
     // gathered; null: the whole list is gathered before the walk
     const std::atomic<uint32_t>* front = nullptr;
     uint32_t pieces = 1;
+    // set when another task of the pipelined job failed: a walk waiting for a
+    // gather piece that will never come throws instead of spinning
+    const std::atomic<bool>* abort = nullptr;
 
     void reset(const BGroup& g, const uint32_t* rows, uint32_t n_rows, const uint32_t* batch_slots) {
         sp = g.sp;
@@ -676,6 +680,7 @@ struct DensePool {
         brow = batch_slots;
         identity = false;
         front = nullptr;
+        abort = nullptr;
         pieces = 1;
         if (rec.size() < n) rec.resize(n);
         if (slot.size() < n) slot.resize(n);
@@ -687,6 +692,7 @@ struct DensePool {
             const uint32_t f = front->load(std::memory_order_acquire);
             const uint32_t a = piece_lo(f);
             if (i < a) return a;
+            if (abort && abort->load(std::memory_order_relaxed)) throw std::runtime_error("parallel replay: a task failed");
             __builtin_ia32_pause();
         }
     }

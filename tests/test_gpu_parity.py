@@ -183,7 +183,7 @@ def test_range_batches(config, n, passes, cfg, par, monkeypatch):
     numeric ranges on one field — C2's skill windows; config 15 adds parties,
     Min < Max, CountMultiple, Intervals, MUST_NOT and ^0.5 ranges and tickets
     whose skill is a keyword; 16 puts every ticket in one pool.  The pools'
-    candidates are sorted on the device (rsrc_tile / rsrc_merge / rsrc_bounds)
+    candidates are sorted on the device (rsrc_tile / rsrc_rank)
     and the min-tree walk decides every row of the pass in ONE batch: groups
     and post-pass state equal to the oracle's, on the serial and the parallel
     host sweeps (NKM_PARALLEL=force)."""
@@ -191,6 +191,32 @@ def test_range_batches(config, n, passes, cfg, par, monkeypatch):
     rs = run_passes(config, n, passes, cfg)
     assert rs[0].n_batches == 1, rs[0].n_batches
     assert rs[0].eval_kernel in (6, 7), rs[0].eval_kernel
+
+
+def test_range_batch_multilevel_sort(monkeypatch):
+    """One pool of 40,000 range-source tickets (config 16): past rsrc_rank_kernel's
+    one-launch reach (8 tiles x 4,096 = 32,768 candidates), so the pool's
+    sort takes two rank launches.  The range batch (NKM_RANGE default) must
+    form exactly the groups and post-pass state of the list-based replay
+    (NKM_RANGE=0), which the oracle pins at the smaller sizes above."""
+    def one(rng):
+        monkeypatch.setenv("NKM_RANGE", rng)
+        ts = synth.TicketSet(16, 40_000)
+        mm = capi.Matchmaker(product_lib(), max_intervals=2)
+        try:
+            ts.insert_into(mm)
+            r = mm.process_raw()
+            return r, state(mm)
+        finally:
+            mm.close()
+            ts.close()
+    got, got_state = one("1")
+    want, want_state = one("0")
+    assert got.n_batches == 1 and got.eval_kernel in (6, 7), (got.n_batches, got.eval_kernel)
+    assert got.eval_kernel == 6 and got.eval_launches == 2, (got.eval_kernel, got.eval_launches)  # rank launches
+    assert len(got.groups) > 1000
+    assert got.groups == want.groups
+    assert got_state == want_state
 
 
 @pytest.mark.parametrize("partial", ["1", "0"])
@@ -232,18 +258,15 @@ def test_hashed_mscan(config, n, cfg, kernel, monkeypatch):
     assert rs[0].eval_kernel == want
 
 
-@pytest.mark.parametrize("contig,j,grid", [("0", "2", "1"), ("0", "4", "1"), ("1", "2", "1"), ("1", "4", "1"),
-                                           ("1", "8", "1"), ("0", "4", "0"), ("1", "4", "0"), ("1", "8", "0")])
-def test_hashed_mscan_chunk_lengths(contig, j, grid, monkeypatch):
-    """Every chunk shape of the hashed scan: gathered through the scan order
-    (2 or 4 candidates per lane) and over contiguous slot runs (2, 4 or 8
-    per lane, vector column loads), with ragged first and last chunks (the second
-    pass starts past a matched prefix), through the key grid or the cuckoo
-    table (NKM_MHGRID).  Lists downloaded (NKM_LISTPROOF=0), so every list
-    is placed and read."""
+@pytest.mark.parametrize("contig,grid", [("0", "1"), ("1", "1"), ("0", "0"), ("1", "0")])
+def test_hashed_mscan_chunk_lengths(contig, grid, monkeypatch):
+    """Both chunk shapes of the hashed scan: gathered through the scan order
+    and over contiguous slot runs (vector column loads), with ragged first
+    and last chunks (the second pass starts past a matched prefix), through
+    the key grid or the cuckoo table (NKM_MHGRID).  Lists downloaded
+    (NKM_LISTPROOF=0), so every list is placed and read."""
     set_kernel(monkeypatch, "mhash")
     monkeypatch.setenv("NKM_MCONTIG", contig)
-    monkeypatch.setenv("NKM_MHASH_J" if contig == "0" else "NKM_MCONTIG_J", j)
     monkeypatch.setenv("NKM_MHGRID", grid)
     monkeypatch.setenv("NKM_LISTPROOF", "0")
     run_passes(4, 9_999, 2, dict(max_intervals=2))
@@ -252,7 +275,7 @@ def test_hashed_mscan_chunk_lengths(contig, j, grid, monkeypatch):
 
 @pytest.mark.parametrize("mode,count", [("0", "1"), ("1", "1"), ("1", "0"), ("2", "1")])
 @pytest.mark.parametrize("config,n,contig", [(3, 20_000, "1"), (4, 20_000, "1"), (3, 7_777, "0"),
-                                             (4, 9_999, "0"), (3, 20_000, "j2")])
+                                             (4, 9_999, "0")])
 def test_proven_mscan_lists(config, n, contig, mode, count, monkeypatch, capfd):
     """Hashed-scan lists proven equal to their search's batch rows are not
     downloaded (Core::list_proof_mode_): NKM_LISTPROOF=1 (default) skips
@@ -263,9 +286,6 @@ def test_proven_mscan_lists(config, n, contig, mode, count, monkeypatch, capfd):
     equal to the oracle's either way; the profile line reports the proven
     lists."""
     set_kernel(monkeypatch, "mhash")
-    if contig == "j2":  # contiguous, 2 candidates per lane
-        contig = "1"
-        monkeypatch.setenv("NKM_MCONTIG_J", "2")
     monkeypatch.setenv("NKM_MCONTIG", contig)
     monkeypatch.setenv("NKM_LISTPROOF", mode)
     monkeypatch.setenv("NKM_MHCOUNT", count)

@@ -84,7 +84,7 @@ def test_multi_pools_default_pass_equals_one_handle(config, n, subs):
 def test_multi_pools_parallel_merge(config, n, subs, monkeypatch):
     """The key-range parallel merge of the sub-handles' lists (forced at any
     size): the same groups, in the same order, as one handle."""
-    monkeypatch.setenv("NKM_MERGE_MIN", "1")
+    monkeypatch.setenv("NKM_PARALLEL", "force")
     assert _compare(config, n, 2, harness.oracle_lib(), n_subs=subs, max_intervals=3) == subs
 
 
@@ -100,11 +100,11 @@ def test_multi_pools_parallel_merge_ties():
                      created=k // 6)
         return m.Process()
     import os
-    os.environ["NKM_MERGE_MIN"] = "1"
+    os.environ["NKM_PARALLEL"] = "force"
     try:
         _both(run)
     finally:
-        del os.environ["NKM_MERGE_MIN"]
+        del os.environ["NKM_PARALLEL"]
 
 
 def test_multi_pools_rev_precision():
