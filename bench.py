@@ -76,6 +76,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-numa-bind", action="store_true",
                     help="do not bind the process to its GPU's NUMA node (one process per GPU)")
+    ap.add_argument("--deliver", action="store_true",
+                    help="pipelined delivery (mm_set_delivery + mm_process_deliver): the timed step is the pass and "
+                         "its hand-off to the library's delivery thread, whose callback is a native no-op router "
+                         "(tools/synth.cpp synth_deliver_noop: every entry read, tickets counted); the callback's "
+                         "time and the flush wait after the step are reported beside the line")
     ap.add_argument("--override", action="store_true",
                     help="register a MatchmakerOverride (processCustom path): the timed step is the candidate pass, "
                          "a native first-disjoint override and mm_process_commit (per rank under the cluster front)")
@@ -283,6 +288,20 @@ def main():
     mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config in REV, rev_threshold=0,
                                     override=(lambda groups: groups) if args.override else None)
     cm = None
+    deliv = None  # --deliver: the callback's counters (tools/synth.cpp SynthDelivered)
+    if args.deliver:
+        if world > 1 or args.override:
+            raise SystemExit("--deliver: one GPU, processDefault (the cluster front and the override path are "
+                             "measured without it)")
+        import ctypes
+        from nakama_amd import capi
+
+        class SynthDelivered(ctypes.Structure):
+            _fields_ = [(k, ctypes.c_int64) for k in ("passes", "groups", "tickets", "presences", "id_bytes", "ns")]
+        deliv = SynthDelivered()
+        deliv_fn = ctypes.cast(synth.lib().synth_deliver_noop, capi.DELIVER_FN)
+        mm._check(mm.lib.mm_set_delivery(mm.h, deliv_fn, ctypes.byref(deliv), 2))
+    deliver_ms, flush_ms = [], []
     if world > 1:
         from nakama_amd import cluster
         cm = cluster.ClusterMatchmaker(mm, pg, POOL_FIELDS[args.config],
@@ -303,7 +322,11 @@ def main():
         ins_dt = time.perf_counter() - t_ins
         barrier_sync(pg, local)
         t0 = time.perf_counter()
-        if cm is None:
+        if deliv is not None:
+            out = capi.mm_matched()  # the summary: counts + statistics, the groups queued for the delivery thread
+            mm._check(mm.lib.mm_process_deliver(mm.h, ctypes.byref(out)))
+            t_pass = time.perf_counter()
+        elif cm is None:
             out = mm.process_call()  # the C-ABI call: one whole Process() pass
             t_pass = time.perf_counter()
             n_cands = out.n_groups if out.is_candidates else 0
@@ -318,7 +341,19 @@ def main():
             for k, v in (("candidate_pass_ms", 1e3 * (t_pass - t0)), ("override_ms", ov_times.get("override_ms", 0.0)),
                          ("commit_ms", ov_times.get("commit_ms", 0.0))):
                 step_phases.setdefault(k, []).append(v)
-        if cm is None:
+        if deliv is not None:
+            # untimed: wait until the no-op router has the pass (it ran behind
+            # the step's end), then read what it delivered
+            t_f0 = time.perf_counter()
+            before_t, before_ns = deliv.tickets, deliv.ns
+            mm._check(mm.lib.mm_delivery_flush(mm.h))
+            if step >= args.warmup:
+                flush_ms.append(1e3 * (time.perf_counter() - t_f0))
+                deliver_ms.append((deliv.ns - before_ns) / 1e6)
+            n_groups, matched, pres = out.n_groups, deliv.tickets - before_t, out.n_entries
+            st = candidate_stats(out)
+            st["candidates"] = 0
+        elif cm is None:
             n_groups, matched, pres, r = mm.process_summary(out)  # untimed: counts the groups, frees them
             # the override's commit runs no search: the pass statistics are the candidate pass's
             st = dict(cand) if args.override else {
@@ -427,7 +462,14 @@ def main():
                    # --override: medians of the step's parts (the override is the bench's native
                    # first-disjoint stand-in for the user's MatchmakerOverride, runtime.go:212)
                    "override_step_ms": ({k: statistics.median(v) for k, v in step_phases.items()}
-                                        if step_phases else None)},
+                                        if step_phases else None),
+                   # --deliver: the timed step ends when mm_process_deliver returns (the pass done, its
+                   # result queued); the no-op router's callback runs on the delivery thread behind it
+                   "delivery": ({"mode": "pipelined (mm_process_deliver, depth 2)",
+                                 "callback_ms_p50": statistics.median(deliver_ms),
+                                 "flush_wait_ms_p50": statistics.median(flush_ms),
+                                 "tickets_delivered_per_step": sum(matched_all) / args.steps}
+                                if deliver_ms else None)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "+".join(sorted(kernels)), "launches": launches, "avg_launch_ms": avg_launch_ms,

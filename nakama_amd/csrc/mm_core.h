@@ -92,9 +92,9 @@ int mscan_max_clauses();
 // position), then the bound queries; see mm_kernels.hip
 hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max_pad, const DRangeTile* d_tiles,
                        uint32_t n_tiles, const uint32_t* d_blk_pool, uint32_t n_elems, int64_t* d_key[2],
-                       uint32_t* d_pos[2], const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds, int* which,
-                       hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1, const hipEvent_t* ev_merge,
-                       int max_merge, int* n_merge);
+                       uint32_t* d_pos[2], int64_t* d_samp, const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds,
+                       int* which, hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1,
+                       const hipEvent_t* ev_merge, int max_merge, int* n_merge);
 
 struct DeviceError {
     hipError_t err;
@@ -902,9 +902,10 @@ private:
     PinnedArray<uint8_t> h_rblob_;
     DevArray<int64_t> d_rkey_[2];
     DevArray<uint32_t> d_rpos_[2], d_rbound_;
+    DevArray<int64_t> d_rsamp_;  // every kRsrcBStride-th sorted key (the bound queries' samples)
     PinnedArray<uint32_t> h_rpos_, h_rbound_;
     static constexpr int kRsrcMaxMerge = 20;
-    hipEvent_t rs_ev_[2 + 2 * kRsrcMaxMerge] = {};  // the tile launch, then each merge launch
+    hipEvent_t rs_ev_[2 + 2 * kRsrcMaxMerge] = {};  // the tile launch, each rank launch, the bounds (last pair)
     int bulk_mode_ = 1;      // NKM_BULK: 0 = Insert per ticket, 1 = batches of >= 4096 on the workers, 2 = any batch
     bool pack_mode_ = true;  // NKM_RPACK=0: RevPrecision batches search per row (rsmall / search_kernel)
     UVec<DSmallRow> pk_tmp_;

@@ -58,6 +58,7 @@ struct DStore {
     const uint32_t* tset_desc;  // [2 * n_sets] (offset, length) of each OP_TERMSET matcher's set
     const uint32_t* tset_ids;   // accepted keyword dictionary ids, ascending per set
     const double* tset_sc;      // the clause's score contribution for each accepted id
+    uint32_t n_fields;          // entries of fval / fkind
 };
 
 // One search (a group of rows sharing a compiled signature, or one row).
@@ -231,6 +232,7 @@ NKM_HD inline PackLayout pack_layout(uint64_t n, int S) {
 // position | kRsrcInvalid), so the valid candidates are a prefix.
 constexpr uint32_t kRsrcTile = 512;            // elements sorted in LDS by one workgroup (four per lane)
 constexpr uint32_t kRsrcInvalid = 0x80000000u;
+constexpr uint32_t kRsrcBStride = 16;          // sorted keys per bound-query sample (divides 256)
 struct DRangePool {
     uint32_t src_off, src_len;
     uint32_t out_off, pad_len;

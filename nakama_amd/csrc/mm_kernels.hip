@@ -64,8 +64,9 @@ __device__ __forceinline__ bool eval_parsed(const DStore& st, uint8_t qkind, con
         bool h = false;
         double sc = c.score;
         if (c.op != OP_FALSE) {
-            const uint8_t kind = st.fkind[c.field][s];
-            const int64_t val = st.fval[c.field][s];
+            // global, not flat, loads (a column pointer read from memory is generic)
+            const uint8_t kind = ((const __attribute__((address_space(1))) uint8_t*)st.fkind[c.field])[s];
+            const int64_t val = ((const __attribute__((address_space(1))) int64_t*)st.fval[c.field])[s];
             if (c.op == OP_TERM) h = kind == KIND_KEYWORD && val == (int64_t)c.term;
             else if (c.op == OP_RANGE) h = kind == KIND_NUMERIC && val >= c.lo && val <= c.hi;
             else if (c.op == OP_TERMSET) h = kind == KIND_KEYWORD && termset_hit(st, c.term, val, &sc);
@@ -77,6 +78,80 @@ __device__ __forceinline__ bool eval_parsed(const DStore& st, uint8_t qkind, con
     }
     if (fail) return false;
     if (!has_must && !has_should) { *sp = 1.0; return true; }  // only mustNots: MatchAll(1)
+    if (!has_must) { *sp = ss; return any_should; }
+    *sp = any_should ? ms + ss : ms;
+    return true;
+}
+
+// eval_parsed with its loads in two batched rounds: a query of at most
+// kEvalBatch clauses has every clause loaded at once, then every clause's
+// column value and kind at slot s at once (the column pointers of the first
+// kFieldLds fields from the workgroup's LDS table, load_field_table), instead
+// of a clause -> pointer -> column chain per clause in turn.  The hit and
+// score logic, and the order of the double additions, are eval_parsed's, so
+// the score bits are identical.  Longer queries: eval_parsed.
+constexpr int kEvalBatch = 4;
+constexpr uint32_t kFieldLds = 64;
+struct FieldTable {
+    const int64_t* val[kFieldLds];
+    const uint8_t* kind[kFieldLds];
+};
+// threads [0, kFieldLds) copy the table; the caller syncs before use.  A
+// kernel uses eval_batched only when the table holds every field
+// (field_table_ok: a uniform test), eval_parsed otherwise.
+__device__ __forceinline__ void load_field_table(const DStore& st, FieldTable& ft) {
+    if (threadIdx.x < kFieldLds && threadIdx.x < st.n_fields) {
+        ft.val[threadIdx.x] = st.fval[threadIdx.x];
+        ft.kind[threadIdx.x] = st.fkind[threadIdx.x];
+    }
+}
+__device__ __forceinline__ bool field_table_ok(const DStore& st) { return st.n_fields <= kFieldLds; }
+__device__ __forceinline__ bool eval_batched(const DStore& st, const FieldTable& ft, uint8_t qkind,
+                                             const DClause* __restrict__ cl, int n, uint32_t s, double* sp) {
+    // every load first and unconditional — clause indexes clamped into the
+    // list (the table's first clause for an empty one), field ids into the
+    // table (OP_FALSE names no column) — so the clauses come in one round and
+    // their columns in the next; the uncommon query shapes are decided after
+    const int nn = n < 1 ? 1 : (n > kEvalBatch ? kEvalBatch : n);
+    const DClause* __restrict__ cb = n >= 1 ? cl : st.clauses;
+    DClause c[kEvalBatch];
+#pragma unroll
+    for (int i = 0; i < kEvalBatch; i++) c[i] = cb[i < nn ? i : nn - 1];
+    uint8_t kind[kEvalBatch];
+    int64_t val[kEvalBatch];
+    // global (not flat) loads: a flat load also counts against lgkmcnt, so
+    // every LDS wait would wait for it
+    typedef const __attribute__((address_space(1))) uint8_t gu8;
+    typedef const __attribute__((address_space(1))) int64_t gi64;
+#pragma unroll
+    for (int i = 0; i < kEvalBatch; i++) {
+        const uint32_t f = c[i].op == OP_FALSE ? 0u : min((uint32_t)c[i].field, st.n_fields - 1);
+        kind[i] = ((gu8*)ft.kind[f])[s];
+        val[i] = ((gi64*)ft.val[f])[s];
+    }
+    if (qkind == QK_MATCHALL) { *sp = 1.0; return true; }
+    if (qkind == QK_MATCHNONE) return false;
+    if (n > kEvalBatch) return eval_parsed(st, qkind, cl, n, s, sp);
+    if (n <= 0) { *sp = 1.0; return true; }  // eval_parsed: no must, no should -> MatchAll(1)
+    double ms = 0.0, ss = 0.0;
+    bool has_must = false, has_should = false, any_should = false, fail = false;
+#pragma unroll
+    for (int i = 0; i < kEvalBatch; i++) {
+        if (i >= n) break;
+        bool h = false;
+        double sc = c[i].score;
+        if (c[i].op != OP_FALSE) {
+            if (c[i].op == OP_TERM) h = kind[i] == KIND_KEYWORD && val[i] == (int64_t)c[i].term;
+            else if (c[i].op == OP_RANGE) h = kind[i] == KIND_NUMERIC && val[i] >= c[i].lo && val[i] <= c[i].hi;
+            else if (c[i].op == OP_TERMSET) h = kind[i] == KIND_KEYWORD && termset_hit(st, c[i].term, val[i], &sc);
+            else h = (kind[i] == KIND_KEYWORD && val[i] == (int64_t)c[i].term) || (kind[i] == KIND_NUMERIC && val[i] == c[i].lo);
+        }
+        if (c[i].occur == OCC_MUST) { has_must = true; if (h) ms += sc; else fail = true; }
+        else if (c[i].occur == OCC_SHOULD) { has_should = true; if (h) { ss += sc; any_should = true; } }
+        else if (h) fail = true;
+    }
+    if (fail) return false;
+    if (!has_must && !has_should) { *sp = 1.0; return true; }
     if (!has_must) { *sp = ss; return any_should; }
     *sp = any_should ? ms + ss : ms;
     return true;
@@ -1539,13 +1614,23 @@ __global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRo
     constexpr int R = 64 / S;           // rows per wave
     constexpr int P = S < 32 ? S : 32;  // pair-matrix entries per row
     __shared__ uint32_t wlive[kWaves], wmatch[kWaves];
+    __shared__ FieldTable ft;
+    load_field_table(st, ft);
+    const bool batched = field_table_ok(st);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int seg = lane / S, j = lane % S, base = seg * S;
     const uint32_t r = (blockIdx.x * kWaves + wave) * R + seg;
     const bool have = r < n_rows;
-    DSmallRow d{0u, 0u, 0u};
-    if (have) d = rows[r];
+    // Unconditional loads (a lane past the last row reads the last row's
+    // record, then is masked), in dependent rounds: the row record; then its
+    // source entry, its own query and count range together
+    const DSmallRow d = rows[have ? r : n_rows - 1];
     const uint32_t len = d.src_len & ~kSrcOrder;
+    const uint32_t* srcb = (d.src_len & kSrcOrder) ? st.order : st.postings;
+    const uint32_t s_src = len ? srcb[d.src_off + ((uint32_t)j < len ? (uint32_t)j : len - 1)] : kNoSlot;
+    const DQuery rq = st.squery[d.slot];
+    const int32_t rmin = st.minc[d.slot], rmax = st.maxc[d.slot];
+    __syncthreads();  // ft
     bool m = false, live = false, rv = false;
     uint32_t s = kNoSlot;
     int64_t key = 0;
@@ -1560,37 +1645,41 @@ __global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRo
     bool square = false;
     if constexpr (S == 8) {
         const uint32_t off0 = __shfl(d.src_off, 0), len0 = __shfl(d.src_len, 0);
-        uint32_t s_sq = kNoSlot;
-        if (have && (uint32_t)j < len) s_sq = ((d.src_len & kSrcOrder) ? st.order : st.postings)[d.src_off + j];
+        const uint32_t s_sq = have && (uint32_t)j < len ? s_src : kNoSlot;
         const uint32_t row_j = __shfl(d.slot, j * S);  // the slot of the row whose segment is j
         square = __ballot(have && d.src_off == off0 && d.src_len == len0 && len == (uint32_t)S && s_sq == row_j) == ~0ull;
     }
     uint64_t Ebits = 0;
-    if (square) {
-        s = ((d.src_len & kSrcOrder) ? st.order : st.postings)[d.src_off + j];
-        live = st.alive[s] != 0;
-        const DQuery q = st.squery[d.slot];
+    if (square) {  // wave-uniform: the entry's columns, then the row query's clauses and their columns
+        s = s_src;
+        const uint8_t al = st.alive[s];
+        const int32_t smin = st.minc[s], smax = st.maxc[s];
+        live = al != 0;
         double sp = 0.0;
-        const bool e = eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, s, &sp);
+        const bool e = batched ? eval_batched(st, ft, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp)
+                               : eval_parsed(st, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp);
         Ebits = __ballot(e);  // bit a * 8 + b: member a's query matches member b's document
-        m = live && e && st.minc[s] >= st.minc[d.slot] && st.maxc[s] <= st.maxc[d.slot];
+        m = live && e && smin >= rmin && smax <= rmax;
         if (m) key = dsortable((sp + 1.0) + 1.0);
         rv = m && ((Ebits >> (j * S + seg)) & 1);
     } else if (have && (uint32_t)j < len) {
-        s = ((d.src_len & kSrcOrder) ? st.order : st.postings)[d.src_off + j];
-        live = st.alive[s] != 0;
+        s = s_src;
+        const uint8_t al = st.alive[s];
+        const int32_t smin = st.minc[s], smax = st.maxc[s];
+        const DQuery h = st.squery[s];
+        live = al != 0;
         if (live) {
-            m = st.minc[s] >= st.minc[d.slot] && st.maxc[s] <= st.maxc[d.slot];
+            m = smin >= rmin && smax <= rmax;
             if (m) {
-                const DQuery q = st.squery[d.slot];
                 double sp = 0.0;
-                m = eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, s, &sp);
+                m = batched ? eval_batched(st, ft, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp)
+                            : eval_parsed(st, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp);
                 key = dsortable((sp + 1.0) + 1.0);
             }
             if (m) {
-                const DQuery h = st.squery[s];
                 double dd;
-                rv = eval_parsed(st, h.kind, st.clauses + h.clause_off, h.n_clauses, d.slot, &dd);
+                rv = batched ? eval_batched(st, ft, h.kind, st.clauses + h.clause_off, h.n_clauses, d.slot, &dd)
+                             : eval_parsed(st, h.kind, st.clauses + h.clause_off, h.n_clauses, d.slot, &dd);
             }
         }
     }
@@ -1623,7 +1712,9 @@ __global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRo
             if (rvi) rbits |= (RvT)((RvT)1 << ri);
             if (m && rank < (uint32_t)P && ri < (uint32_t)P) {
                 double dd;
-                if (eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, si, &dd)) pmask |= (PmT)((PmT)1 << ri);
+                const bool hit = batched ? eval_batched(st, ft, q.kind, st.clauses + q.clause_off, q.n_clauses, si, &dd)
+                                         : eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, si, &dd);
+                if (hit) pmask |= (PmT)((PmT)1 << ri);
             }
         }
     }
@@ -1904,36 +1995,57 @@ int mscan_max_clauses() { return kMaxMClause; }
 // ---- range sources (range_walk.h) -----------------------------------------
 // A range batch's pools sorted by (value, source position).  rsrc_tile_kernel
 // sorts tiles of kRsrcTile elements in LDS (4 per lane; 512-element tiles keep
-// ~200 workgroups busy on C2's 100k candidates instead of one CU's LDS per
-// 4k), then each rsrc_rank_kernel launch merges groups of up to kRsrcGroup
-// runs of R into one run of 8R: an element's place is its index in its run
-// plus its rank in each other run of its group.  A workgroup holds 256
-// consecutive elements of one run; per partner run it reads every
-// stride-th element (the run's sample, one strided load round), ranks its
-// elements among the samples in LDS, loads the partner window its elements
-// fall in (coalesced, ~256 + 2 strides of elements) into LDS and finishes
-// each rank by a log2(stride)-step search there — no per-element binary
-// search through L2.  C2's 25k-candidate pools: tile + 2 rank launches.  The
-// last launch also answers the bound queries (the first sorted element of a
-// pool >= or > a clause bound = the sum of its ranks in the pool's runs) and
-// writes positions only: the host reads no key.  Ranks in a run to the left
-// count elements <= the element, to the right elements <, so equal elements
-// (the tile's padding) land on distinct places.
+// ~200 workgroups busy on C2's 100k candidates), then each rsrc_rank_kernel
+// launch merges groups of up to kRsrcGroup runs of R into one run of 8R: an
+// element's place is its index in its run plus its rank in each other run of
+// its group.  A workgroup holds 256 consecutive elements of one run; per
+// partner run it reads every stride-th element (the run's sample, one strided
+// load round), ranks its elements among the samples in LDS, loads the partner
+// window its elements fall in (coalesced, ~256 + 2 strides of elements) into
+// LDS and finishes each rank by a log2(stride)-step search there — no
+// per-element binary search through L2.  C2's 25k-candidate pools: tile + 2
+// rank launches.  The last one also writes every kRsrcBStride-th sorted key
+// (a sample) and rsrc_bounds_kernel answers the bound queries (the first
+// sorted element of a pool >= or > a clause bound) from those samples in LDS
+// plus one window of kRsrcBStride keys.  Every search here is branchless with
+// a fixed step count and a lane's independent searches interleaved, so their
+// LDS reads issue together (a data-dependent loop per search serialised them:
+// 17 us of LDS waits per tile).  Ranks in a run to the left count elements <=
+// the element, to the right elements <, so equal elements (the tile's
+// padding) land on distinct places.
 
+// Comparisons with non-short-circuit operators: with || / && the compiler
+// sank the position's LDS read into a branch taken only on equal keys, and
+// every search step became read, wait, branch, read, wait.
 __device__ __forceinline__ bool rsrc_less(int64_t ka, uint32_t va, int64_t kb, uint32_t vb) {
-    return ka < kb || (ka == kb && va < vb);
+    return (ka < kb) | ((ka == kb) & (va < vb));
 }
 __device__ __forceinline__ bool rsrc_leq(int64_t ka, uint32_t va, int64_t kb, uint32_t vb) {
-    return ka < kb || (ka == kb && va <= vb);
+    return (ka < kb) | ((ka == kb) & (va <= vb));
 }
+// a is "before" x: to the left (a partner run left of x's) a <= x, else a < x
+__device__ __forceinline__ bool rsrc_before(bool left, int64_t ka, uint32_t va, int64_t kx, uint32_t vx) {
+    return (ka < kx) | ((ka == kx) & ((va < vx) | (left & (va == vx))));
+}
+__device__ __forceinline__ uint32_t rsrc_step(bool go, uint32_t step) { return step & (0u - (uint32_t)go); }
+
+#ifdef NKM_RS_PROF  // tools/rsrc_bench.hip: per-workgroup phase timestamps (wall clock)
+__device__ uint64_t g_rs_prof[3][8192][6];
+#define RS_MARK(k, i)                                                                            \
+    do {                                                                                         \
+        if (threadIdx.x == 0 && blockIdx.x < 8192) g_rs_prof[k][blockIdx.x][i] = wall_clock64(); \
+    } while (0)
+#else
+#define RS_MARK(k, i) \
+    do {              \
+    } while (0)
+#endif
 
 // One tile per workgroup of kRsrcTile / 4 lanes, 4 consecutive elements per
 // lane (the posting entries, then every element's alive / kind / value
 // gathers in one round), sorted in registers, then merged in LDS from runs of
-// 4 up to the tile: a lane's 4 binary searches in the partner run are
-// independent (log2(run) LDS reads each, in flight together).  Positions
-// past the tile's length hold (INT64_MAX, 0xFFFFFFFF): they sort last and
-// are not written.
+// 4 up to the tile.  The tile always holds kRsrcTile elements: positions past
+// its length hold (INT64_MAX, 0xFFFFFFFF), sort last and are not written.
 constexpr int kRsrcTileThreads = (int)(kRsrcTile / 4);
 __global__ __launch_bounds__(kRsrcTileThreads) void rsrc_tile_kernel(DStore st, const DRangePool* __restrict__ pools,
                                                                      const DRangeTile* __restrict__ tiles,
@@ -1941,6 +2053,7 @@ __global__ __launch_bounds__(kRsrcTileThreads) void rsrc_tile_kernel(DStore st, 
                                                                      uint32_t* __restrict__ opos) {
     __shared__ int64_t sk[kRsrcTile];
     __shared__ uint32_t sv[kRsrcTile];
+    RS_MARK(0, 0);
     const DRangeTile t = tiles[blockIdx.x];
     const DRangePool P = pools[t.pool];
     const int64_t* __restrict__ fv = st.fval[P.field];
@@ -1971,16 +2084,16 @@ __global__ __launch_bounds__(kRsrcTileThreads) void rsrc_tile_kernel(DStore st, 
             v[j] = !in_tile ? 0xFFFFFFFFu : ok ? i : (kRsrcInvalid | i);
         }
     }
+    RS_MARK(0, 1);
     // sort the lane's 4 in registers (5 compare-exchanges)
     auto cx = [&](int a, int b) {
-        if (rsrc_less(k[b], v[b], k[a], v[a])) {
-            const int64_t tk = k[a];
-            k[a] = k[b];
-            k[b] = tk;
-            const uint32_t tv = v[a];
-            v[a] = v[b];
-            v[b] = tv;
-        }
+        const bool sw = rsrc_less(k[b], v[b], k[a], v[a]);
+        const int64_t ka = k[a], kb = k[b];
+        const uint32_t va = v[a], vb = v[b];
+        k[a] = sw ? kb : ka;
+        k[b] = sw ? ka : kb;
+        v[a] = sw ? vb : va;
+        v[b] = sw ? va : vb;
     };
     cx(0, 1);
     cx(2, 3);
@@ -1995,40 +2108,37 @@ __global__ __launch_bounds__(kRsrcTileThreads) void rsrc_tile_kernel(DStore st, 
     __syncthreads();
     for (uint32_t r = 4; r < kRsrcTile; r <<= 1) {
         const uint32_t run = e0 / r, ps = (run ^ 1u) * r;
-        const bool right = run & 1u;  // the partner run is to the left: count elements <=
-        uint32_t lo[4], len[4];
+        const bool left = run & 1u;  // the partner run is to the left
+        uint32_t c[4] = {0u, 0u, 0u, 0u};
+        // the lane's 4 elements are consecutive in its run: held in registers
+        // since the last write (k, v), re-read after the barrier
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             k[j] = sk[e0 + j];
             v[j] = sv[e0 + j];
-            lo[j] = ps;
-            len[j] = r;
         }
-        for (uint32_t step = r; step > 0; step >>= 1) {
+        for (uint32_t step = r >> 1; step > 0; step >>= 1) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                if (len[j] == 0) continue;
-                const uint32_t half = len[j] >> 1, mid = lo[j] + half;
-                const bool go = right ? rsrc_leq(sk[mid], sv[mid], k[j], v[j]) : rsrc_less(sk[mid], sv[mid], k[j], v[j]);
-                if (go) {
-                    lo[j] = mid + 1;
-                    len[j] -= half + 1;
-                } else {
-                    len[j] = half;
-                }
+                const uint32_t idx = ps + c[j] + step - 1;
+                c[j] += rsrc_step(rsrc_before(left, sk[idx], sv[idx], k[j], v[j]), step);
             }
         }
-        uint32_t o[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) o[j] = (run & ~1u) * r + (e0 + j - run * r) + (lo[j] - ps);
+        for (int j = 0; j < 4; j++) {
+            const uint32_t idx = ps + c[j];
+            c[j] += (uint32_t)rsrc_before(left, sk[idx], sv[idx], k[j], v[j]);
+        }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            sk[o[j]] = k[j];
-            sv[o[j]] = v[j];
+            const uint32_t o = (run & ~1u) * r + (e0 + j - run * r) + c[j];
+            sk[o] = k[j];
+            sv[o] = v[j];
         }
         __syncthreads();
     }
+    RS_MARK(0, 2);
     const uint64_t base = (uint64_t)P.out_off + t.start;
 #pragma unroll
     for (int j = 0; j < 4; j++)
@@ -2036,60 +2146,29 @@ __global__ __launch_bounds__(kRsrcTileThreads) void rsrc_tile_kernel(DStore st, 
             okey[base + e0 + j] = sk[e0 + j];
             opos[base + e0 + j] = sv[e0 + j];
         }
+    RS_MARK(0, 3);
 }
 
 // Groups of up to kRsrcGroup runs of R -> one run each, over every pool at
 // once: one workgroup per 256 elements (blk_pool: the pool of each
 // 256-element block; pools and runs are 256-aligned, so a block lies in one
-// run).  Blocks past n_eblk answer bound queries (the last launch: ok ==
-// nullptr, the pool's runs are one group).
+// run).  The last launch (samp != nullptr) also writes the bounds' samples.
 constexpr uint32_t kRsrcGroup = 8;
-constexpr uint32_t kRsrcSamples = 128;                           // per partner run at most
-constexpr uint32_t kRsrcWin = 3584;                              // window elements in LDS (42 KB)
+constexpr uint32_t kRsrcSamples = 128;  // per partner run (LDS), sentinel-padded
+constexpr uint32_t kRsrcWin = 3584;     // window elements in LDS (42 KB)
 __device__ __forceinline__ uint32_t rsrc_stride(uint32_t R) { return max(32u, R / kRsrcSamples); }
 
 __global__ __launch_bounds__(kBlock) void rsrc_rank_kernel(const DRangePool* __restrict__ pools,
-                                                           const uint32_t* __restrict__ blk_pool, uint32_t n_eblk,
+                                                           const uint32_t* __restrict__ blk_pool,
                                                            const int64_t* __restrict__ ik, const uint32_t* __restrict__ ip,
                                                            int64_t* __restrict__ ok, uint32_t* __restrict__ op, uint32_t R,
-                                                           const DRangeBound* __restrict__ q, uint32_t nq,
-                                                           uint32_t* __restrict__ bounds) {
-    if (blockIdx.x >= n_eblk) {
-        const uint32_t t = (blockIdx.x - n_eblk) * kBlock + threadIdx.x;
-        if (t >= nq) return;
-        const DRangeBound b = q[t];
-        const DRangePool P = pools[b.pool];
-        const int64_t* __restrict__ kk = ik + P.out_off;
-        uint32_t lo[kRsrcGroup], len[kRsrcGroup];
-#pragma unroll
-        for (uint32_t g = 0; g < kRsrcGroup; g++) {
-            lo[g] = g * R;
-            len[g] = g * R < P.pad_len ? min(R, P.pad_len - g * R) : 0u;
-        }
-        for (uint32_t step = R; step > 0; step >>= 1) {
-#pragma unroll
-            for (uint32_t g = 0; g < kRsrcGroup; g++) {
-                if (len[g] == 0) continue;
-                const uint32_t half = len[g] >> 1, mid = lo[g] + half;
-                if (b.upper ? kk[mid] <= b.key : kk[mid] < b.key) {
-                    lo[g] = mid + 1;
-                    len[g] -= half + 1;
-                } else {
-                    len[g] = half;
-                }
-            }
-        }
-        uint32_t c = 0;
-#pragma unroll
-        for (uint32_t g = 0; g < kRsrcGroup; g++) c += g * R < P.pad_len ? lo[g] - g * R : 0u;
-        bounds[t] = c;
-        return;
-    }
+                                                           int64_t* __restrict__ samp) {
     __shared__ int64_t samk[kRsrcGroup * kRsrcSamples];
     __shared__ uint32_t samv[kRsrcGroup * kRsrcSamples];
     __shared__ int64_t wk[kRsrcWin];
     __shared__ uint32_t wv[kRsrcWin];
     __shared__ uint32_t wlo[kRsrcGroup], whi[kRsrcGroup];
+    RS_MARK(1, 0);
     const DRangePool P = pools[blk_pool[blockIdx.x]];
     const uint32_t gi = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t e = gi - P.out_off;
@@ -2106,7 +2185,8 @@ __global__ __launch_bounds__(kBlock) void rsrc_rank_kernel(const DRangePool* __r
         rs[g] = (g0 + g) * R;
         rl[g] = (g0 + g != a && rs[g] < P.pad_len) ? min(R, P.pad_len - rs[g]) : 0u;
     }
-    // the partners' samples (element j * S of each), one strided round
+    // the partners' samples (element j * S of each; sentinels past the end),
+    // one strided round
     for (uint32_t x = threadIdx.x; x < kRsrcGroup * kRsrcSamples; x += kBlock) {
         const uint32_t g = x / kRsrcSamples, j = x % kRsrcSamples;
         uint32_t len = 0, st0 = 0;
@@ -2116,37 +2196,32 @@ __global__ __launch_bounds__(kBlock) void rsrc_rank_kernel(const DRangePool* __r
                 len = rl[h];
                 st0 = rs[h];
             }
-        if (j * S < len) {
-            samk[x] = bk[st0 + j * S];
-            samv[x] = bp[st0 + j * S];
-        }
+        const bool in = j * S < len;
+        samk[x] = in ? bk[st0 + j * S] : INT64_MAX;
+        samv[x] = in ? bp[st0 + j * S] : 0xFFFFFFFFu;
     }
     __syncthreads();
-    // per partner: the window [r_lo, r_hi) of its run that holds this
-    // element's rank beyond r_lo (r_lo elements are certainly before it)
+    RS_MARK(1, 1);
+    // per partner: c = samples before this element (all partners' searches
+    // interleaved), then the window [r_lo, r_hi) of the partner's run that
+    // holds its rank beyond r_lo (r_lo elements are certainly before it)
+    uint32_t c[kRsrcGroup];
+#pragma unroll
+    for (uint32_t g = 0; g < kRsrcGroup; g++) c[g] = 0;
+    for (uint32_t step = kRsrcSamples >> 1; step > 0; step >>= 1) {
+#pragma unroll
+        for (uint32_t g = 0; g < kRsrcGroup; g++) {
+            const uint32_t idx = g * kRsrcSamples + c[g] + step - 1;
+            c[g] += rsrc_step(rsrc_before(g0 + g < a, samk[idx], samv[idx], k, v), step);
+        }
+    }
     uint32_t r_lo[kRsrcGroup], r_hi[kRsrcGroup];
 #pragma unroll
     for (uint32_t g = 0; g < kRsrcGroup; g++) {
-        r_lo[g] = r_hi[g] = 0;
-        if (rl[g] == 0) continue;
-        const bool left = g0 + g < a;  // count partner elements <= this one, else <
-        const uint32_t ns = (rl[g] + S - 1) / S;
-        uint32_t lo = 0, len = ns;
-        const int64_t* sk_ = samk + g * kRsrcSamples;
-        const uint32_t* sv_ = samv + g * kRsrcSamples;
-        while (len > 0) {
-            const uint32_t half = len >> 1, mid = lo + half;
-            if (left ? rsrc_leq(sk_[mid], sv_[mid], k, v) : rsrc_less(sk_[mid], sv_[mid], k, v)) {
-                lo = mid + 1;
-                len -= half + 1;
-            } else {
-                len = half;
-            }
-        }
-        if (lo > 0) {
-            r_lo[g] = (lo - 1) * S + 1;
-            r_hi[g] = min(lo * S, rl[g]);
-        }
+        const uint32_t idx = g * kRsrcSamples + c[g];
+        c[g] += (uint32_t)rsrc_before(g0 + g < a, samk[idx], samv[idx], k, v);  // c <= kRsrcSamples - 1 + 1
+        r_lo[g] = c[g] ? (c[g] - 1) * S + 1 : 0u;
+        r_hi[g] = c[g] ? min(c[g] * S, rl[g]) : 0u;
     }
     // the block's window per partner: its first element's r_lo to its last
     // element's r_hi (the block's elements ascend, so do their windows)
@@ -2157,19 +2232,22 @@ __global__ __launch_bounds__(kBlock) void rsrc_rank_kernel(const DRangePool* __r
 #pragma unroll
         for (uint32_t g = 0; g < kRsrcGroup; g++) whi[g] = r_hi[g];
     __syncthreads();
+    RS_MARK(1, 2);
     uint32_t o = g0 * R + (e - a * R);
     // rounds: as many partners' windows as fit in LDS; a window larger than
-    // the buffer is searched in global memory (log2(S) steps).  Every array
-    // is indexed by unrolled constants (registers, no scratch); the round
-    // plan is the same on every lane (wlo / whi are shared).
+    // the buffer is searched in global memory.  Every array is indexed by
+    // unrolled constants (registers, no scratch); the round plan is the same
+    // on every lane (wlo / whi are shared).
     uint32_t base[kRsrcGroup], round_of[kRsrcGroup], wlen[kRsrcGroup];
     uint32_t used = 0, nround = 0;
+    bool any_global = false;
 #pragma unroll
     for (uint32_t g = 0; g < kRsrcGroup; g++) {
         wlen[g] = whi[g] > wlo[g] ? whi[g] - wlo[g] : 0u;
         if (wlen[g] > kRsrcWin) {
             base[g] = UINT32_MAX;
-            round_of[g] = nround;
+            round_of[g] = UINT32_MAX;
+            any_global = true;
             continue;
         }
         if (used + wlen[g] > kRsrcWin) {
@@ -2183,7 +2261,7 @@ __global__ __launch_bounds__(kBlock) void rsrc_rank_kernel(const DRangePool* __r
     for (uint32_t rnd = 0; rnd <= nround; rnd++) {
 #pragma unroll
         for (uint32_t g = 0; g < kRsrcGroup; g++) {
-            if (round_of[g] != rnd || base[g] == UINT32_MAX || wlen[g] == 0) continue;
+            if (round_of[g] != rnd || wlen[g] == 0) continue;  // uniform
             const uint32_t src = rs[g] + wlo[g];
             for (uint32_t x = threadIdx.x; x < wlen[g]; x += kBlock) {
                 wk[base[g] + x] = bk[src + x];
@@ -2191,54 +2269,119 @@ __global__ __launch_bounds__(kBlock) void rsrc_rank_kernel(const DRangePool* __r
             }
         }
         __syncthreads();
+        // every partner of the round: a fixed log2(S) + 1 steps over [r_lo,
+        // r_lo + S), positions at or past r_hi never before the element
+        uint32_t cc[kRsrcGroup];
+#pragma unroll
+        for (uint32_t g = 0; g < kRsrcGroup; g++) cc[g] = 0;
+        for (uint32_t step = S >> 1; step > 0; step >>= 1) {
+#pragma unroll
+            for (uint32_t g = 0; g < kRsrcGroup; g++) {
+                const uint32_t idx = r_lo[g] + cc[g] + step - 1;
+                const uint32_t li = min(base[g] + (idx - wlo[g]), kRsrcWin - 1);
+                const bool go = round_of[g] == rnd && idx < r_hi[g] && rsrc_before(g0 + g < a, wk[li], wv[li], k, v);
+                cc[g] += rsrc_step(go, step);
+            }
+        }
 #pragma unroll
         for (uint32_t g = 0; g < kRsrcGroup; g++) {
-            if (round_of[g] != rnd || rl[g] == 0) continue;
+            const uint32_t idx = r_lo[g] + cc[g];
+            const uint32_t li = min(base[g] + (idx - wlo[g]), kRsrcWin - 1);
+            const bool go = round_of[g] == rnd && idx < r_hi[g] && rsrc_before(g0 + g < a, wk[li], wv[li], k, v);
+            cc[g] += (uint32_t)go;
+            if (round_of[g] == rnd) o += r_lo[g] + cc[g];
+        }
+        __syncthreads();
+    }
+    if (any_global)  // rare: a partner window past the LDS buffer, searched in L2
+#pragma unroll
+        for (uint32_t g = 0; g < kRsrcGroup; g++) {
+            if (base[g] != UINT32_MAX) continue;
             const bool left = g0 + g < a;
+            const int64_t* gk_ = bk + rs[g];
+            const uint32_t* gv_ = bp + rs[g];
             uint32_t lo = r_lo[g], len = r_hi[g] - r_lo[g];
-            if (base[g] != UINT32_MAX) {
-                const int64_t* wk_ = wk + base[g] - wlo[g];
-                const uint32_t* wv_ = wv + base[g] - wlo[g];
-                while (len > 0) {
-                    const uint32_t half = len >> 1, mid = lo + half;
-                    if (left ? rsrc_leq(wk_[mid], wv_[mid], k, v) : rsrc_less(wk_[mid], wv_[mid], k, v)) {
-                        lo = mid + 1;
-                        len -= half + 1;
-                    } else {
-                        len = half;
-                    }
-                }
-            } else {
-                const int64_t* gk_ = bk + rs[g];
-                const uint32_t* gv_ = bp + rs[g];
-                while (len > 0) {
-                    const uint32_t half = len >> 1, mid = lo + half;
-                    if (left ? rsrc_leq(gk_[mid], gv_[mid], k, v) : rsrc_less(gk_[mid], gv_[mid], k, v)) {
-                        lo = mid + 1;
-                        len -= half + 1;
-                    } else {
-                        len = half;
-                    }
+            while (len > 0) {
+                const uint32_t half = len >> 1, mid = lo + half;
+                if (rsrc_before(left, gk_[mid], gv_[mid], k, v)) {
+                    lo = mid + 1;
+                    len -= half + 1;
+                } else {
+                    len = half;
                 }
             }
             o += lo;
         }
-        __syncthreads();
-    }
-    if (ok) ok[(uint64_t)P.out_off + o] = k;
+    RS_MARK(1, 3);
+    ok[(uint64_t)P.out_off + o] = k;
     op[(uint64_t)P.out_off + o] = v;
+    if (samp && (o % kRsrcBStride) == 0) samp[((uint64_t)P.out_off + o) / kRsrcBStride] = k;
+    RS_MARK(1, 4);
+}
+
+// The bound queries over the sorted keys: every block stages the samples
+// (every kRsrcBStride-th sorted key, all pools: pools are 256-aligned, so each
+// pool's samples are a contiguous range) in LDS when they fit, ranks each
+// query among its pool's samples there, and finishes in one window of
+// kRsrcBStride keys (one vector-load round).  Samples that do not fit: the
+// same search over the sample array in L2.
+constexpr uint32_t kRsrcBSampCap = 8192;  // 64 KB of LDS
+__global__ __launch_bounds__(kBlock) void rsrc_bounds_kernel(const DRangePool* __restrict__ pools,
+                                                             const int64_t* __restrict__ key,
+                                                             const int64_t* __restrict__ samp, uint32_t n_samp,
+                                                             const DRangeBound* __restrict__ q, uint32_t nq,
+                                                             uint32_t* __restrict__ out) {
+    __shared__ int64_t ls[kRsrcBSampCap];
+    RS_MARK(2, 0);
+    const bool in_lds = n_samp <= kRsrcBSampCap;
+    if (in_lds)
+        for (uint32_t x = threadIdx.x; x < n_samp; x += kBlock) ls[x] = samp[x];
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    DRangeBound b{0, 0u, 0u};
+    if (t < nq) b = q[t];
+    const DRangePool P = pools[b.pool];
+    __syncthreads();
+    RS_MARK(2, 1);
+    if (t >= nq) return;
+    const int64_t* __restrict__ kk = key + P.out_off;
+    const uint32_t s0 = P.out_off / kRsrcBStride, ns = P.pad_len / kRsrcBStride;
+    auto before = [&](int64_t x) { return (x < b.key) | ((x == b.key) & (b.upper != 0)); };
+    // samples before the bound: a branchless search over ns (>= 1) samples
+    uint32_t lo = 0, n = ns;
+    while (n > 1) {
+        const uint32_t half = n >> 1;
+        const int64_t x = in_lds ? ls[s0 + lo + half - 1] : samp[s0 + lo + half - 1];
+        lo += rsrc_step(before(x), half);
+        n -= half;
+    }
+    lo += (uint32_t)before(in_lds ? ls[s0 + lo] : samp[s0 + lo]);
+    // lo samples before it: the bound is in ((lo - 1) * B, lo * B]; the
+    // window's kRsrcBStride - 1 keys after sample lo - 1, in one round
+    uint32_t c = 0;
+    if (lo > 0) {
+        const uint32_t w0 = (lo - 1) * kRsrcBStride + 1;
+        int64_t x[kRsrcBStride - 1];
+#pragma unroll
+        for (uint32_t i = 0; i < kRsrcBStride - 1; i++) x[i] = w0 + i < P.pad_len ? kk[w0 + i] : INT64_MAX;
+        c = w0;
+#pragma unroll
+        for (uint32_t i = 0; i < kRsrcBStride - 1; i++) c += (uint32_t)(w0 + i < P.pad_len && before(x[i]));
+    }
+    out[t] = c;
+    RS_MARK(2, 2);
 }
 
 // The whole sort + bounds.  Buffers: keys / positions 2 x n_elems each (ping-
-// pong); the sorted positions end in d_pos[*which].  Event pairs: ev_tile
-// around the tile launch, ev_merge[2m], ev_merge[2m + 1] around rank launch m
-// (at most max_merge of them).  Returns the number of rank launches in
-// *n_merge (at least one: it also answers the bound queries).
+// pong); the sorted positions end in d_pos[*which]; d_samp holds n_elems /
+// kRsrcBStride samples.  Event pairs: ev_tile around the tile launch,
+// ev_merge[2m], ev_merge[2m + 1] around rank launch m (at most max_merge of
+// them), the last pair around the bounds launch.  Returns the number of rank
+// launches in *n_merge (at least one).
 hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max_pad, const DRangeTile* d_tiles,
                        uint32_t n_tiles, const uint32_t* d_blk_pool, uint32_t n_elems, int64_t* d_key[2],
-                       uint32_t* d_pos[2], const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds, int* which,
-                       hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1, const hipEvent_t* ev_merge,
-                       int max_merge, int* n_merge) {
+                       uint32_t* d_pos[2], int64_t* d_samp, const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds,
+                       int* which, hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1,
+                       const hipEvent_t* ev_merge, int max_merge, int* n_merge) {
     *which = 0;
     *n_merge = 0;
     if (n_elems == 0 || n_tiles == 0) return hipSuccess;
@@ -2247,19 +2390,20 @@ hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max
                           d_pools, d_tiles, d_key[0], d_pos[0]);
     int b = 0, m = 0;
     const uint32_t n_eblk = n_elems / kBlock;
-    for (uint64_t R = kRsrcTile;; R *= kRsrcGroup, b ^= 1, m++) {
-        if (m >= max_merge) return hipErrorInvalidValue;
+    for (uint64_t R = kRsrcTile;; R *= kRsrcGroup) {
+        if (m + 1 >= max_merge) return hipErrorInvalidValue;  // the last pair is the bounds'
         const bool last = R * kRsrcGroup >= max_pad;
-        const uint32_t qblk = last ? (nq + kBlock - 1) / kBlock : 0;
-        hipExtLaunchKernelGGL(rsrc_rank_kernel, dim3(n_eblk + qblk), dim3(kBlock), 0, stream, ev_merge[2 * m],
-                              ev_merge[2 * m + 1], 0, d_pools, d_blk_pool, n_eblk, d_key[b], d_pos[b],
-                              last ? nullptr : d_key[b ^ 1], d_pos[b ^ 1], (uint32_t)R, d_q, last ? nq : 0u, d_bounds);
-        if (last) {
-            b ^= 1;
-            m++;
-            break;
-        }
+        hipExtLaunchKernelGGL(rsrc_rank_kernel, dim3(n_eblk), dim3(kBlock), 0, stream, ev_merge[2 * m],
+                              ev_merge[2 * m + 1], 0, d_pools, d_blk_pool, d_key[b], d_pos[b], d_key[b ^ 1],
+                              d_pos[b ^ 1], (uint32_t)R, last ? d_samp : nullptr);
+        b ^= 1;
+        m++;
+        if (last) break;
     }
+    if (nq)
+        hipExtLaunchKernelGGL(rsrc_bounds_kernel, dim3((nq + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+                              ev_merge[2 * (max_merge - 1)], ev_merge[2 * (max_merge - 1) + 1], 0, d_pools, d_key[b],
+                              d_samp, n_elems / kRsrcBStride, d_q, nq, d_bounds);
     *which = b;
     *n_merge = m;
     return hipGetLastError();

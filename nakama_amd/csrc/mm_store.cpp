@@ -1616,6 +1616,7 @@ DStore Core::dstore() const {
     st.tset_desc = d_tset_desc_.p;
     st.tset_ids = d_tset_ids_.p;
     st.tset_sc = d_tset_sc_.p;
+    st.n_fields = (uint32_t)std::max<size_t>(fval_.size(), 1);
     return st;
 }
 

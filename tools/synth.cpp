@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -683,6 +684,33 @@ struct Sha256 {
             for (int k = 0; k < 4; k++) out[4 * i + k] = (uint8_t)(h[i] >> (24 - 8 * k));
     }
 };
+
+// The bench's delivery callback (mm_deliver_fn, include/nakama_mm.h) standing
+// in for the reference's per-group delivery to a no-op router
+// (matchmaker.go:374-440: per group the users list and envelope are built
+// from every entry, then one SendToPresenceIDs per entry): it reads every
+// entry's ticket id and presence index, counts the delivered groups, tickets
+// (presence index 0) and presences, and its own time.  ctx: SynthDelivered.
+struct SynthDelivered {
+    int64_t passes, groups, tickets, presences, id_bytes, ns;
+};
+void synth_deliver_noop(void* ctx, const mm_matched* m, int64_t) {
+    const auto t0 = std::chrono::steady_clock::now();
+    SynthDelivered* d = static_cast<SynthDelivered*>(ctx);
+    int64_t tickets = 0, bytes = 0;
+    for (int32_t g = 0; g < m->n_groups; g++)
+        for (int32_t e = m->group_offsets[g]; e < m->group_offsets[g + 1]; e++) {
+            const mm_entry_ref& r = m->entries[e];
+            tickets += r.presence_index == 0;
+            bytes += r.ticket ? (int64_t)std::strlen(r.ticket) : 0;
+        }
+    d->passes++;
+    d->groups += m->n_groups;
+    d->tickets += tickets;
+    d->presences += m->n_entries;
+    d->id_bytes += bytes;
+    d->ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
 
 void* synth_sha_new() { return new Sha256(); }
 void synth_sha_bytes(void* s, const uint8_t* p, int64_t n) { static_cast<Sha256*>(s)->update(p, (size_t)n); }
