@@ -43,7 +43,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 KERNELS = {0: "search_kernel", 1: "scan_kernel", 2: "mscan_kernel", 3: "rsmall_kernel", 4: "mscan_hash_kernel",
-           5: "rpack_kernel", 6: "rsrc_rank_kernel", 7: "rsrc_tile_kernel"}  # mm_matched.eval_kernel
+           5: "rpack_kernel", 6: "rsrc_merge_kernel", 7: "rsrc_tile_kernel"}  # mm_matched.eval_kernel
 WORKLOADS = {
     1: "C1: 10k solo 1v1, '+properties.mode:ranked +properties.region:eu'",
     2: "C2: skill-window range queries with ^boost, 1v1",
@@ -310,7 +310,8 @@ def main():
     times, matched_all, presences_all, ins_times, searched = [], [], [], [], []
     eval_ms = eval_bytes = launches = pair_evals = pairs_decided = cands = 0
     batches, kernels, unroutable = [], set(), 0
-    breakdown = {"local_call_ms": [], "summary_ms": [], "merge_ms": []}  # rank 0's cluster-pass phases
+    breakdown = {"local_call_ms": [], "summary_ms": [], "merge_ms": [], "merge_wait_ms": [], "merge_comm_ms": [],
+                 "merge_c_ms": []}  # rank 0's cluster-pass phases
     ov_times, step_phases = {}, {}  # --override: the step's candidate pass / override / commit
     for step in range(args.warmup + args.steps):
         ts = make_set(args, world, rank, step)

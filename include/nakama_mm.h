@@ -127,7 +127,7 @@ typedef struct mm_matched {
     int64_t eval_bytes;             /* algorithmic bytes of the search launches (DESIGN.md roofline) */
     int32_t eval_launches;          /* search kernel launches in the pass */
     int32_t n_batches;              /* replay batches */
-    int32_t eval_kernel;            /* query-eval kernel with the most bytes: 0 search, 1 scan, 2 mscan, 3 rsmall, 4 hashed mscan, 5 rpack, 6 range rank (multiway merge), 7 range tile */
+    int32_t eval_kernel;            /* query-eval kernel with the most bytes: 0 search, 1 scan, 2 mscan, 3 rsmall, 4 hashed mscan, 5 rpack, 6 range merge, 7 range tile */
     int32_t full_lists;             /* variable-score searches run as full lists (host-sorted), 0 for the oracle */
     const int64_t* group_created;   /* n_groups: CreatedAt of each group's last entry (its searching ticket) — the
                                        key a pool-sharded cluster merges rank results by (ABI 3) */

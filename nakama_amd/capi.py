@@ -294,7 +294,7 @@ class ProcessResult:
     eval_bytes: int = 0
     eval_launches: int = 0
     n_batches: int = 0
-    eval_kernel: int = 0  # 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel, 4 mscan_hash_kernel, 5 rpack_kernel, 6 rsrc_rank_kernel, 7 rsrc_tile_kernel
+    eval_kernel: int = 0  # 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel, 4 mscan_hash_kernel, 5 rpack_kernel, 6 rsrc_merge_kernel, 7 rsrc_tile_kernel
     full_lists: int = 0   # variable-score searches run as host-sorted full lists
     pairs_decided: int = 0  # (row, candidate) pairs decided: rows that searched x their search's source
 

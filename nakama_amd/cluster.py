@@ -333,8 +333,10 @@ class ClusterMatchmaker:
         positions are computed in C on the library's persistent host threads
         (mm_merge_positions_ex).  tie_ids(): this rank's searching ticket ids,
         asked for only when two ranks' keys tie (the ids then order the tied
-        groups).  cp.local_stats gets the merge's split: collectives + copies
-        (merge_comm_ms) and the C merge (merge_c_ms)."""
+        groups).  cp.local_stats gets the merge's split: the counts'
+        all-gather, which waits for the slowest rank's pass (merge_wait_ms),
+        the other collectives + copies (merge_comm_ms) and the C merge
+        (merge_c_ms)."""
         import time
 
         import torch
@@ -348,6 +350,7 @@ class ClusterMatchmaker:
         hdr = [self._t(np.zeros(4, dtype=np.int64)) for _ in range(self.world)]
         self.dist.all_gather(hdr, self._t(np.array([ng, tickets, pres, asc], dtype=np.int64)))
         hdr = np.stack([self._host(h) for h in hdr])
+        t_hdr = time.perf_counter()  # the first collective after the pass: it also absorbs the ranks' skew
         counts = np.ascontiguousarray(hdr[:, 0].astype(np.int32))
         cp.n_groups, cp.matched_tickets, cp.matched_presences = (int(x) for x in hdr[:, :3].sum(axis=0))
         sorted_all = int(hdr[:, 3].min()) == 1
@@ -380,7 +383,8 @@ class ClusterMatchmaker:
             flat = np.concatenate([allk[r * m:r * m + int(counts[r])] for r in range(self.world)])
             self._order_ties(cp, flat, counts, tie_ids() if tie_ids is not None else [""] * ng)
         t3 = time.perf_counter()
-        cp.local_stats["merge_comm_ms"] = 1e3 * ((t1 - t0) + (t3 - t2))
+        cp.local_stats["merge_wait_ms"] = 1e3 * (t_hdr - t0)
+        cp.local_stats["merge_comm_ms"] = 1e3 * ((t1 - t_hdr) + (t3 - t2))
         cp.local_stats["merge_c_ms"] = 1e3 * (t2 - t1)
 
     def _override(self, out):

@@ -416,9 +416,9 @@ static int32_t nkm_merge(const int64_t* const* base, const int32_t* counts, int3
     std::vector<int32_t> ties(64, 0);
     run_split(n * (int64_t)(other.size() + 1), [&](int t, int nt) {
         const int64_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
-        ties[t] = avx2 && other.size() <= 64
-                      ? merge_walk_avx2(base[rank], i0, i1, other.data(), m.data(), (int)other.size(), pos_out)
-                      : merge_walk_scalar(base[rank], i0, i1, other.data(), m.data(), (int)other.size(), pos_out);
+        const int nq = (int)other.size();
+        ties[t] = avx2 && nq <= 64 ? merge_walk_avx2(base[rank], i0, i1, other.data(), m.data(), nq, pos_out)
+                                   : merge_walk_scalar(base[rank], i0, i1, other.data(), m.data(), nq, pos_out);
     });
     int32_t any = 0;
     for (int32_t x : ties) any |= x;

@@ -92,9 +92,9 @@ int mscan_max_clauses();
 // position), then the bound queries; see mm_kernels.hip
 hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max_pad, const DRangeTile* d_tiles,
                        uint32_t n_tiles, const uint32_t* d_blk_pool, uint32_t n_elems, int64_t* d_key[2],
-                       uint32_t* d_pos[2], int64_t* d_samp, const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds,
-                       int* which, hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1,
-                       const hipEvent_t* ev_merge, int max_merge, int* n_merge);
+                       uint32_t* d_pos[2], const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds, int* which,
+                       hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1, const hipEvent_t* ev_merge,
+                       int max_merge, int* n_merge);
 
 struct DeviceError {
     hipError_t err;
@@ -547,7 +547,7 @@ struct PassStats {
     int full_lists = 0;  // variable-score searches run as full lists (host-sorted)
     int tier_lists = 0;  // variable-score searches run as top-tier lists (search_kernel path 2)
     // per query-eval kernel: 0 search_kernel, 1 scan_kernel, 2 mscan_kernel, 3 rsmall_kernel,
-    // 4 rsrc_rank_kernel, 5 rsrc_tile_kernel (range batches)
+    // 4 rsrc_merge_kernel, 5 rsrc_tile_kernel (range batches)
     static constexpr int kKernels = 6;
     double k_ms[kKernels] = {};         // HIP-event time of the launches
     bool mhash = false;                 // a batch's mscan ran hashed (mscan_hash_kernel)
@@ -736,6 +736,9 @@ private:
     uint32_t sig_of(const CompiledQuery& cq, int32_t mn, int32_t mx, uint32_t party);
     static void sig_describe(Sig& s, const std::vector<DClause>& dc, const CompiledQuery& cq, int32_t mn, int32_t mx,
                              uint32_t party);
+    template <class Get>
+    void commit_new_sigs(WorkPool& wp, size_t nt, const std::vector<int64_t>& tfound, const std::vector<uint64_t>& thash,
+                         std::vector<Sig>& tsig, std::vector<uint32_t>& tsg, Get get);
     uint32_t sig_commit(Sig&& s, const DClause* dc, size_t n, uint64_t hash, bool materialize);
     bool sig_eq(uint32_t id, uint8_t kind, int32_t mn, int32_t mx, uint32_t party, const DClause* dc, size_t n) const;
     void materialize_fields();
@@ -902,10 +905,9 @@ private:
     PinnedArray<uint8_t> h_rblob_;
     DevArray<int64_t> d_rkey_[2];
     DevArray<uint32_t> d_rpos_[2], d_rbound_;
-    DevArray<int64_t> d_rsamp_;  // every kRsrcBStride-th sorted key (the bound queries' samples)
     PinnedArray<uint32_t> h_rpos_, h_rbound_;
     static constexpr int kRsrcMaxMerge = 20;
-    hipEvent_t rs_ev_[2 + 2 * kRsrcMaxMerge] = {};  // the tile launch, each rank launch, the bounds (last pair)
+    hipEvent_t rs_ev_[2 + 2 * kRsrcMaxMerge] = {};  // the tile launch, then each merge launch
     int bulk_mode_ = 1;      // NKM_BULK: 0 = Insert per ticket, 1 = batches of >= 4096 on the workers, 2 = any batch
     bool pack_mode_ = true;  // NKM_RPACK=0: RevPrecision batches search per row (rsmall / search_kernel)
     UVec<DSmallRow> pk_tmp_;

@@ -230,9 +230,8 @@ NKM_HD inline PackLayout pack_layout(uint64_t n, int S) {
 // rounded up to 256); a candidate that is not alive or holds no number in
 // `field`, and the padding, sort after every valid one (key INT64_MAX,
 // position | kRsrcInvalid), so the valid candidates are a prefix.
-constexpr uint32_t kRsrcTile = 512;            // elements sorted in LDS by one workgroup (four per lane)
+constexpr uint32_t kRsrcTile = 1024;           // elements sorted in LDS by one workgroup (one per lane)
 constexpr uint32_t kRsrcInvalid = 0x80000000u;
-constexpr uint32_t kRsrcBStride = 16;          // sorted keys per bound-query sample (divides 256)
 struct DRangePool {
     uint32_t src_off, src_len;
     uint32_t out_off, pad_len;

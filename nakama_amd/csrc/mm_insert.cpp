@@ -22,6 +22,7 @@
 // dictionary entries first seen in the batch (ids are compared for equality
 // only: a value's id never changes a search, a hit order or a group).
 #include <algorithm>
+#include <stdexcept>
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -204,6 +205,99 @@ inline char* put_str(char* p, std::string_view v) {
 
 }  // namespace
 
+// The new signatures of a bulk Insert, committed on the workers (the serial
+// sig_commit per triple was 160-350 ms of a C5 1M Insert: up to a million
+// new signatures, one push_back chain each): the new triples are
+// deduplicated among themselves (distinct query strings can compile to one
+// signature), numbered in first-appearance order — the ids the serial loop
+// assigns — and their clauses, descriptors, field flags and index entries
+// written in parallel.  tfound[j] >= 0: triple j's existing signature.
+template <class Get>
+void Core::commit_new_sigs(WorkPool& wp, size_t nt, const std::vector<int64_t>& tfound,
+                           const std::vector<uint64_t>& thash, std::vector<Sig>& tsig, std::vector<uint32_t>& tsg,
+                           Get get) {
+    std::vector<uint32_t> nw;  // the new triples, in order
+    for (size_t j = 0; j < nt; j++) {
+        if (tfound[j] >= 0) tsg[j] = (uint32_t)tfound[j];
+        else nw.push_back((uint32_t)j);
+    }
+    const size_t nn = nw.size();
+    if (nn == 0) return;
+    std::vector<uint64_t> nh(nn);
+    for (size_t k = 0; k < nn; k++) nh[k] = thash[nw[k]];
+    std::vector<uint32_t> rep;
+    dedup(wp, nn, nh.data(), [&](uint32_t a, uint32_t b) {
+        const DClause *da, *db;
+        size_t na, nb;
+        uint8_t ka, kb;
+        int32_t mna, mxa, mnb, mxb;
+        get(nw[a], da, na, ka, mna, mxa);
+        get(nw[b], db, nb, kb, mnb, mxb);
+        return ka == kb && mna == mnb && mxa == mxb && na == nb && (na == 0 || std::memcmp(da, db, na * sizeof(DClause)) == 0);
+    }, rep);
+    // ids and clause offsets of the distinct new signatures, in order
+    std::vector<uint32_t> nid(nn), coff(nn, 0);
+    const uint32_t id0 = (uint32_t)sigs_.size();
+    const uint64_t c0 = clauses_.size();
+    uint32_t nd = 0;
+    uint64_t ncl = 0;
+    for (size_t k = 0; k < nn; k++) {
+        if (rep[k] != k) continue;
+        const DClause* dc;
+        size_t ndc;
+        uint8_t kind;
+        int32_t mn, mx;
+        get(nw[k], dc, ndc, kind, mn, mx);
+        nid[k] = id0 + nd++;
+        coff[k] = (uint32_t)(c0 + ncl);
+        ncl += ndc;
+    }
+    if (c0 + ncl > UINT32_MAX) throw std::length_error("clause table past 2^32 entries");
+    sigs_.resize((size_t)id0 + nd);
+    sig_fmask_.resize((size_t)id0 + nd);
+    clauses_.resize(c0 + ncl);
+    sig_idx_.reserve(sig_idx_.n + nd);
+    const size_t nf = field_used_.size();
+    const size_t nch = std::max<size_t>(1, std::min<size_t>((size_t)wp.size() * 4, (nn + 4095) / 4096));
+    std::vector<std::vector<uint8_t>> used(nch), posting(nch);
+    wp.run(nch, [&](size_t c) {
+        std::vector<uint8_t>& u = used[c];
+        std::vector<uint8_t>& pst = posting[c];
+        u.assign(nf, 0);
+        pst.assign(nf, 0);
+        for (size_t k = nn * c / nch; k < nn * (c + 1) / nch; k++) {
+            const uint32_t j = nw[k];
+            if (rep[k] != k) continue;
+            const DClause* dc;
+            size_t ndc;
+            uint8_t kind;
+            int32_t mn, mx;
+            get(j, dc, ndc, kind, mn, mx);
+            Sig& g = tsig[j];
+            g.clause_off = coff[k];
+            for (size_t x = 0; x < ndc; x++) {
+                if (dc[x].op != OP_FALSE) u[dc[x].field] = 1;
+                clauses_[coff[k] + x] = dc[x];
+            }
+            for (auto& mt : g.must_terms) pst[mt.first] = 1;
+            const uint32_t id = nid[k];
+            sig_fmask_[id] = g.must_fmask;
+            sigs_[id] = std::move(g);
+            sig_idx_.put_new_concurrent(thash[j], id);
+        }
+    });
+    sig_idx_.n += nd;
+    for (size_t c = 0; c < nch; c++)
+        for (size_t f = 0; f < nf; f++) {
+            if (used[c][f]) field_used_[f] = 1;
+            if (posting[c][f] && !field_posting_[f]) {
+                field_posting_[f] = 1;
+                index_dirty_ = true;
+            }
+        }
+    for (size_t k = 0; k < nn; k++) tsg[nw[k]] = nid[rep[k]];
+}
+
 bool Core::insert_bulk(const mm_ticket* ts, int32_t n_in, double* ph) {
     const size_t n = (size_t)n_in;
     if (field_used_.size() > F_PARTY && (field_used_[F_TICKET] || field_used_[F_PARTY])) return false;  // id-valued fields
@@ -244,6 +338,12 @@ bool Core::insert_bulk(const mm_ticket* ts, int32_t n_in, double* ph) {
     par([&](size_t lo, size_t hi) {
         for (size_t k = lo; k < hi; k++) qh[k] = str_hash(SV(ts[k].query));
     });
+    auto tlap = t0;
+    auto lap = [&](int k) {  // ph[5..10]: the signature phase's parts (NKM_PROFILE)
+        const auto now = clk::now();
+        ph[k] += std::chrono::duration<double, std::milli>(now - tlap).count();
+        tlap = now;
+    };
     std::vector<uint32_t> qrep;
     dedup(wp, n, qh.data(), [&](uint32_t a, uint32_t b) {  // a shared query string compares by pointer
         return ts[a].query == ts[b].query || SV(ts[a].query) == SV(ts[b].query);
@@ -252,6 +352,7 @@ bool Core::insert_bulk(const mm_ticket* ts, int32_t n_in, double* ph) {
     const size_t nq = qfirst.size();
     std::vector<uint32_t> qpos(n, 0);  // at each first: its distinct-query index
     for (size_t j = 0; j < nq; j++) qpos[qfirst[j]] = (uint32_t)j;
+    lap(5);  // query hashes, dedup
     std::vector<CompiledQuery> cq(nq);
     std::vector<int> cst(nq);
     wp.run(std::max<size_t>(1, std::min<size_t>(nq, (size_t)wp.size() * 8)), [&](size_t c) {
@@ -259,6 +360,7 @@ bool Core::insert_bulk(const mm_ticket* ts, int32_t n_in, double* ph) {
         for (size_t j = nq * c / nc; j < nq * (c + 1) / nc; j++)
             cst[j] = compile_query(std::string(SV(ts[qfirst[j]].query)), &cq[j]);
     });
+    lap(6);  // compiles
     // tickets whose query does not compile are skipped (the reference logs and continues)
     std::vector<uint32_t> qof(n);
     par([&](size_t lo, size_t hi) {
@@ -281,6 +383,7 @@ bool Core::insert_bulk(const mm_ticket* ts, int32_t n_in, double* ph) {
     }, trep);
     const std::vector<uint32_t> tfirst = select(wp, m, [&](size_t i) { return trep[i] == i; });
     const size_t nt = tfirst.size();
+    lap(7);  // (query, Min, Max) triples
     // the distinct queries' field names and terms: names are few (serial
     // field_of for the new ones), terms are interned in bulk
     std::vector<uint8_t> used_q(nq, 0);
@@ -343,6 +446,7 @@ bool Core::insert_bulk(const mm_ticket* ts, int32_t n_in, double* ph) {
             qch[q] = sig_clause_hash(qdc.data() + cl_off[q], cq[q].clauses.size());
         }
     });
+    lap(8);  // fields, terms, clause words
     // every distinct triple: looked up on the workers (described when new),
     // committed in first-appearance order
     std::vector<uint64_t> thash(nt, 0);
@@ -372,24 +476,44 @@ bool Core::insert_bulk(const mm_ticket* ts, int32_t n_in, double* ph) {
             }
         }
     });
+    lap(9);  // lookups, descriptors
     std::vector<uint32_t> tsg(nt);
-    for (size_t j = 0; j < nt; j++) {
-        uint32_t q;
-        const mm_ticket* t;
-        triple(j, q, t);
-        if (serial_q[q]) {
-            tsg[j] = sig_of(cq[q], t->min_count, t->max_count, kNoParty);
-        } else if (tfound[j] >= 0) {
-            tsg[j] = (uint32_t)tfound[j];
-        } else {
-            const DClause* dc = qdc.data() + cl_off[q];
-            const size_t ndc = cq[q].clauses.size();
-            const int64_t f = sig_idx_.find(thash[j], [&](uint32_t id) {  // an earlier triple of this batch may have made it
-                return sig_eq(id, cq[q].kind, t->min_count, t->max_count, kNoParty, dc, ndc);
-            });
-            tsg[j] = f >= 0 ? (uint32_t)f : sig_commit(std::move(tsig[j]), dc, ndc, thash[j], false);
+    bool any_serial = false;
+    for (size_t j = 0; j < nt && !any_serial; j++) any_serial = serial_q[qof[keep[tfirst[j]]]] != 0;
+    if (any_serial) {
+        // a regexp / wildcard / fuzzy query (sig_of interns its matchers): one
+        // triple at a time, in first-appearance order
+        for (size_t j = 0; j < nt; j++) {
+            uint32_t q;
+            const mm_ticket* t;
+            triple(j, q, t);
+            if (serial_q[q]) {
+                tsg[j] = sig_of(cq[q], t->min_count, t->max_count, kNoParty);
+            } else if (tfound[j] >= 0) {
+                tsg[j] = (uint32_t)tfound[j];
+            } else {
+                const DClause* dc = qdc.data() + cl_off[q];
+                const size_t ndc = cq[q].clauses.size();
+                const int64_t f = sig_idx_.find(thash[j], [&](uint32_t id) {  // an earlier triple may have made it
+                    return sig_eq(id, cq[q].kind, t->min_count, t->max_count, kNoParty, dc, ndc);
+                });
+                tsg[j] = f >= 0 ? (uint32_t)f : sig_commit(std::move(tsig[j]), dc, ndc, thash[j], false);
+            }
         }
+    } else {
+        commit_new_sigs(wp, nt, tfound, thash, tsig, tsg, [&](size_t j, const DClause*& dc, size_t& ndc, uint8_t& kind,
+                                                              int32_t& mn, int32_t& mx) {
+            uint32_t q;
+            const mm_ticket* t;
+            triple(j, q, t);
+            dc = qdc.data() + cl_off[q];
+            ndc = cq[q].clauses.size();
+            kind = cq[q].kind;
+            mn = t->min_count;
+            mx = t->max_count;
+        });
     }
+    lap(10);  // commits
     // A query of this batch may be the first to read the ticket / party_id
     // field (sig_commit switched it on): those columns are filled per ticket
     // (add_locked), so the batch takes the per-ticket path.  Nothing of the

@@ -1993,417 +1993,149 @@ int mscan_max_fields() { return kMaxMField; }
 int mscan_max_clauses() { return kMaxMClause; }
 
 // ---- range sources (range_walk.h) -----------------------------------------
-// A range batch's pools sorted by (value, source position).  rsrc_tile_kernel
-// sorts tiles of kRsrcTile elements in LDS (4 per lane; 512-element tiles keep
-// ~200 workgroups busy on C2's 100k candidates), then each rsrc_rank_kernel
-// launch merges groups of up to kRsrcGroup runs of R into one run of 8R: an
-// element's place is its index in its run plus its rank in each other run of
-// its group.  A workgroup holds 256 consecutive elements of one run; per
-// partner run it reads every stride-th element (the run's sample, one strided
-// load round), ranks its elements among the samples in LDS, loads the partner
-// window its elements fall in (coalesced, ~256 + 2 strides of elements) into
-// LDS and finishes each rank by a log2(stride)-step search there — no
-// per-element binary search through L2.  C2's 25k-candidate pools: tile + 2
-// rank launches.  The last one also writes every kRsrcBStride-th sorted key
-// (a sample) and rsrc_bounds_kernel answers the bound queries (the first
-// sorted element of a pool >= or > a clause bound) from those samples in LDS
-// plus one window of kRsrcBStride keys.  Every search here is branchless with
-// a fixed step count and a lane's independent searches interleaved, so their
-// LDS reads issue together (a data-dependent loop per search serialised them:
-// 17 us of LDS waits per tile).  Ranks in a run to the left count elements <=
-// the element, to the right elements <, so equal elements (the tile's
-// padding) land on distinct places.
+// A range batch's pools sorted by (value, source position): rsrc_tile_kernel
+// sorts tiles of kRsrcTile elements in LDS, rsrc_merge_kernel merges runs of R
+// into runs of 2R (R = kRsrcTile, 2 kRsrcTile, ...), rsrc_bounds_kernel finds
+// the clauses' bounds in the sorted keys.  Elements are (key, position) pairs,
+// distinct within a pool (positions are), so a merge places an element at its
+// index in its run plus its rank in the partner run — a binary search, no
+// ties to break.
 
-// Comparisons with non-short-circuit operators: with || / && the compiler
-// sank the position's LDS read into a branch taken only on equal keys, and
-// every search step became read, wait, branch, read, wait.
+// Non-short-circuit: with || / && the compiler sinks the position's load into
+// a branch taken on equal keys, and a search step on C2's repeated skill values
+// becomes two dependent reads (load key, compare, load position) instead of one
+// round (tools/rsrc_bench).
 __device__ __forceinline__ bool rsrc_less(int64_t ka, uint32_t va, int64_t kb, uint32_t vb) {
     return (ka < kb) | ((ka == kb) & (va < vb));
 }
-__device__ __forceinline__ bool rsrc_leq(int64_t ka, uint32_t va, int64_t kb, uint32_t vb) {
-    return (ka < kb) | ((ka == kb) & (va <= vb));
-}
-// a is "before" x: to the left (a partner run left of x's) a <= x, else a < x
-__device__ __forceinline__ bool rsrc_before(bool left, int64_t ka, uint32_t va, int64_t kx, uint32_t vx) {
-    return (ka < kx) | ((ka == kx) & ((va < vx) | (left & (va == vx))));
-}
-__device__ __forceinline__ uint32_t rsrc_step(bool go, uint32_t step) { return step & (0u - (uint32_t)go); }
 
-#ifdef NKM_RS_PROF  // tools/rsrc_bench.hip: per-workgroup phase timestamps (wall clock)
-__device__ uint64_t g_rs_prof[3][8192][6];
-#define RS_MARK(k, i)                                                                            \
-    do {                                                                                         \
-        if (threadIdx.x == 0 && blockIdx.x < 8192) g_rs_prof[k][blockIdx.x][i] = wall_clock64(); \
-    } while (0)
-#else
-#define RS_MARK(k, i) \
-    do {              \
-    } while (0)
-#endif
-
-// One tile per workgroup of kRsrcTile / 4 lanes, 4 consecutive elements per
-// lane (the posting entries, then every element's alive / kind / value
-// gathers in one round), sorted in registers, then merged in LDS from runs of
-// 4 up to the tile.  The tile always holds kRsrcTile elements: positions past
-// its length hold (INT64_MAX, 0xFFFFFFFF), sort last and are not written.
-constexpr int kRsrcTileThreads = (int)(kRsrcTile / 4);
-__global__ __launch_bounds__(kRsrcTileThreads) void rsrc_tile_kernel(DStore st, const DRangePool* __restrict__ pools,
-                                                                     const DRangeTile* __restrict__ tiles,
-                                                                     int64_t* __restrict__ okey,
-                                                                     uint32_t* __restrict__ opos) {
-    __shared__ int64_t sk[kRsrcTile];
-    __shared__ uint32_t sv[kRsrcTile];
-    RS_MARK(0, 0);
+// One tile per workgroup of kRsrcTile lanes, one element each (loaded
+// coalesced: the posting entry, then alive / kind / value of that slot), then
+// merged in LDS from runs of 1 up to the tile: each lane's binary search in
+// the partner run is log2(run) dependent LDS reads, one element per lane.
+constexpr int kRsrcBlock = (int)kRsrcTile;
+__global__ __launch_bounds__(kRsrcBlock) void rsrc_tile_kernel(DStore st, const DRangePool* __restrict__ pools,
+                                                               const DRangeTile* __restrict__ tiles,
+                                                               int64_t* __restrict__ okey, uint32_t* __restrict__ opos) {
+    __shared__ int64_t sk[2][kRsrcTile];
+    __shared__ uint32_t sv[2][kRsrcTile];
     const DRangeTile t = tiles[blockIdx.x];
     const DRangePool P = pools[t.pool];
     const int64_t* __restrict__ fv = st.fval[P.field];
     const uint8_t* __restrict__ fk = st.fkind[P.field];
-    const uint32_t e0 = threadIdx.x * 4;
-    int64_t k[4];
-    uint32_t v[4];
-    {
-        const uint32_t i0 = t.start + e0;
-        const uint32_t last = P.src_len - 1;  // a tile exists only for a pool with candidates
-        uint32_t sl[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) sl[j] = st.postings[P.src_off + min(i0 + j, last)];
-        uint8_t al[4], kd[4];
-        int64_t val[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            al[j] = st.alive[sl[j]];
-            kd[j] = fk[sl[j]];
-            val[j] = fv[sl[j]];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t e = e0 + j, i = i0 + j;
-            const bool in_tile = e < t.len, in_src = i < P.src_len;
-            const bool ok = in_tile && in_src && al[j] && kd[j] == KIND_NUMERIC;
-            k[j] = ok ? val[j] : INT64_MAX;
-            v[j] = !in_tile ? 0xFFFFFFFFu : ok ? i : (kRsrcInvalid | i);
+    const uint32_t e = threadIdx.x;
+    const uint32_t i = t.start + e;  // position in the pool's source
+    int64_t k = INT64_MAX;
+    uint32_t v = kRsrcInvalid | i;
+    if (e < t.len && i < P.src_len) {
+        const uint32_t s = st.postings[P.src_off + i];
+        if (st.alive[s] && fk[s] == KIND_NUMERIC) {
+            k = fv[s];
+            v = i;
         }
     }
-    RS_MARK(0, 1);
-    // sort the lane's 4 in registers (5 compare-exchanges)
-    auto cx = [&](int a, int b) {
-        const bool sw = rsrc_less(k[b], v[b], k[a], v[a]);
-        const int64_t ka = k[a], kb = k[b];
-        const uint32_t va = v[a], vb = v[b];
-        k[a] = sw ? kb : ka;
-        k[b] = sw ? ka : kb;
-        v[a] = sw ? vb : va;
-        v[b] = sw ? va : vb;
-    };
-    cx(0, 1);
-    cx(2, 3);
-    cx(0, 2);
-    cx(1, 3);
-    cx(1, 2);
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        sk[e0 + j] = k[j];
-        sv[e0 + j] = v[j];
-    }
+    sk[0][e] = k;
+    sv[0][e] = v;
     __syncthreads();
-    for (uint32_t r = 4; r < kRsrcTile; r <<= 1) {
-        const uint32_t run = e0 / r, ps = (run ^ 1u) * r;
-        const bool left = run & 1u;  // the partner run is to the left
-        uint32_t c[4] = {0u, 0u, 0u, 0u};
-        // the lane's 4 elements are consecutive in its run: held in registers
-        // since the last write (k, v), re-read after the barrier
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            k[j] = sk[e0 + j];
-            v[j] = sv[e0 + j];
-        }
-        for (uint32_t step = r >> 1; step > 0; step >>= 1) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t idx = ps + c[j] + step - 1;
-                c[j] += rsrc_step(rsrc_before(left, sk[idx], sv[idx], k[j], v[j]), step);
+    int b = 0;
+    for (uint32_t r = 1; r < t.len; r <<= 1, b ^= 1) {
+        if (e < t.len) {
+            k = sk[b][e];  // the element now at this position
+            v = sv[b][e];
+            const uint32_t run = e / r, ps = (run ^ 1u) * r;
+            uint32_t o = e;
+            if (ps < t.len) {
+                uint32_t lo = ps, hi = min(ps + r, t.len);
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (rsrc_less(sk[b][mid], sv[b][mid], k, v)) lo = mid + 1;
+                    else hi = mid;
+                }
+                o = (run & ~1u) * r + (e - run * r) + (lo - ps);
             }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t idx = ps + c[j];
-            c[j] += (uint32_t)rsrc_before(left, sk[idx], sv[idx], k[j], v[j]);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t o = (run & ~1u) * r + (e0 + j - run * r) + c[j];
-            sk[o] = k[j];
-            sv[o] = v[j];
+            sk[b ^ 1][o] = k;
+            sv[b ^ 1][o] = v;
         }
         __syncthreads();
     }
-    RS_MARK(0, 2);
-    const uint64_t base = (uint64_t)P.out_off + t.start;
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-        if (e0 + j < t.len) {
-            okey[base + e0 + j] = sk[e0 + j];
-            opos[base + e0 + j] = sv[e0 + j];
-        }
-    RS_MARK(0, 3);
+    if (e < t.len) {
+        const uint64_t base = (uint64_t)P.out_off + t.start;
+        okey[base + e] = sk[b][e];
+        opos[base + e] = sv[b][e];
+    }
 }
 
-// Groups of up to kRsrcGroup runs of R -> one run each, over every pool at
-// once: one workgroup per 256 elements (blk_pool: the pool of each
-// 256-element block; pools and runs are 256-aligned, so a block lies in one
-// run).  The last launch (samp != nullptr) also writes the bounds' samples.
-constexpr uint32_t kRsrcGroup = 8;
-constexpr uint32_t kRsrcSamples = 128;  // per partner run (LDS), sentinel-padded
-constexpr uint32_t kRsrcWin = 3584;     // window elements in LDS (42 KB)
-__device__ __forceinline__ uint32_t rsrc_stride(uint32_t R) { return max(32u, R / kRsrcSamples); }
-
-__global__ __launch_bounds__(kBlock) void rsrc_rank_kernel(const DRangePool* __restrict__ pools,
-                                                           const uint32_t* __restrict__ blk_pool,
-                                                           const int64_t* __restrict__ ik, const uint32_t* __restrict__ ip,
-                                                           int64_t* __restrict__ ok, uint32_t* __restrict__ op, uint32_t R,
-                                                           int64_t* __restrict__ samp) {
-    __shared__ int64_t samk[kRsrcGroup * kRsrcSamples];
-    __shared__ uint32_t samv[kRsrcGroup * kRsrcSamples];
-    __shared__ int64_t wk[kRsrcWin];
-    __shared__ uint32_t wv[kRsrcWin];
-    __shared__ uint32_t wlo[kRsrcGroup], whi[kRsrcGroup];
-    RS_MARK(1, 0);
+// Runs of R -> runs of 2R over every pool at once (one thread per element;
+// blk_pool: the pool of each 256-element block, pools being 256-aligned).
+__global__ __launch_bounds__(kBlock) void rsrc_merge_kernel(const DRangePool* __restrict__ pools,
+                                                            const uint32_t* __restrict__ blk_pool,
+                                                            const int64_t* __restrict__ ik, const uint32_t* __restrict__ ip,
+                                                            int64_t* __restrict__ ok, uint32_t* __restrict__ op, uint32_t R) {
     const DRangePool P = pools[blk_pool[blockIdx.x]];
-    const uint32_t gi = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t e = gi - P.out_off;
-    const int64_t k = ik[gi];
-    const uint32_t v = ip[gi];
-    const int64_t* __restrict__ bk = ik + P.out_off;
-    const uint32_t* __restrict__ bp = ip + P.out_off;
-    const uint32_t a = e / R, g0 = a - a % kRsrcGroup;
-    const uint32_t S = rsrc_stride(R);
-    // the group's runs: start and length (0: absent, or this block's own run)
-    uint32_t rs[kRsrcGroup], rl[kRsrcGroup];
-#pragma unroll
-    for (uint32_t g = 0; g < kRsrcGroup; g++) {
-        rs[g] = (g0 + g) * R;
-        rl[g] = (g0 + g != a && rs[g] < P.pad_len) ? min(R, P.pad_len - rs[g]) : 0u;
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t e = g - P.out_off;
+    const int64_t k = ik[g];
+    const uint32_t v = ip[g];
+    const uint32_t run = e / R, ps = (run ^ 1u) * R;
+    uint32_t o = e;
+    if (ps < P.pad_len) {
+        const int64_t* __restrict__ bk = ik + P.out_off;
+        const uint32_t* __restrict__ bp = ip + P.out_off;
+        uint32_t lo = ps, hi = min(ps + R, P.pad_len);
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (rsrc_less(bk[mid], bp[mid], k, v)) lo = mid + 1;
+            else hi = mid;
+        }
+        o = (run & ~1u) * R + (e - run * R) + (lo - ps);
     }
-    // the partners' samples (element j * S of each; sentinels past the end),
-    // one strided round
-    for (uint32_t x = threadIdx.x; x < kRsrcGroup * kRsrcSamples; x += kBlock) {
-        const uint32_t g = x / kRsrcSamples, j = x % kRsrcSamples;
-        uint32_t len = 0, st0 = 0;
-#pragma unroll
-        for (uint32_t h = 0; h < kRsrcGroup; h++)
-            if (h == g) {
-                len = rl[h];
-                st0 = rs[h];
-            }
-        const bool in = j * S < len;
-        samk[x] = in ? bk[st0 + j * S] : INT64_MAX;
-        samv[x] = in ? bp[st0 + j * S] : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    RS_MARK(1, 1);
-    // per partner: c = samples before this element (all partners' searches
-    // interleaved), then the window [r_lo, r_hi) of the partner's run that
-    // holds its rank beyond r_lo (r_lo elements are certainly before it)
-    uint32_t c[kRsrcGroup];
-#pragma unroll
-    for (uint32_t g = 0; g < kRsrcGroup; g++) c[g] = 0;
-    for (uint32_t step = kRsrcSamples >> 1; step > 0; step >>= 1) {
-#pragma unroll
-        for (uint32_t g = 0; g < kRsrcGroup; g++) {
-            const uint32_t idx = g * kRsrcSamples + c[g] + step - 1;
-            c[g] += rsrc_step(rsrc_before(g0 + g < a, samk[idx], samv[idx], k, v), step);
-        }
-    }
-    uint32_t r_lo[kRsrcGroup], r_hi[kRsrcGroup];
-#pragma unroll
-    for (uint32_t g = 0; g < kRsrcGroup; g++) {
-        const uint32_t idx = g * kRsrcSamples + c[g];
-        c[g] += (uint32_t)rsrc_before(g0 + g < a, samk[idx], samv[idx], k, v);  // c <= kRsrcSamples - 1 + 1
-        r_lo[g] = c[g] ? (c[g] - 1) * S + 1 : 0u;
-        r_hi[g] = c[g] ? min(c[g] * S, rl[g]) : 0u;
-    }
-    // the block's window per partner: its first element's r_lo to its last
-    // element's r_hi (the block's elements ascend, so do their windows)
-    if (threadIdx.x == 0)
-#pragma unroll
-        for (uint32_t g = 0; g < kRsrcGroup; g++) wlo[g] = r_lo[g];
-    if (threadIdx.x == kBlock - 1)
-#pragma unroll
-        for (uint32_t g = 0; g < kRsrcGroup; g++) whi[g] = r_hi[g];
-    __syncthreads();
-    RS_MARK(1, 2);
-    uint32_t o = g0 * R + (e - a * R);
-    // rounds: as many partners' windows as fit in LDS; a window larger than
-    // the buffer is searched in global memory.  Every array is indexed by
-    // unrolled constants (registers, no scratch); the round plan is the same
-    // on every lane (wlo / whi are shared).
-    uint32_t base[kRsrcGroup], round_of[kRsrcGroup], wlen[kRsrcGroup];
-    uint32_t used = 0, nround = 0;
-    bool any_global = false;
-#pragma unroll
-    for (uint32_t g = 0; g < kRsrcGroup; g++) {
-        wlen[g] = whi[g] > wlo[g] ? whi[g] - wlo[g] : 0u;
-        if (wlen[g] > kRsrcWin) {
-            base[g] = UINT32_MAX;
-            round_of[g] = UINT32_MAX;
-            any_global = true;
-            continue;
-        }
-        if (used + wlen[g] > kRsrcWin) {
-            nround++;
-            used = 0;
-        }
-        base[g] = used;
-        round_of[g] = nround;
-        used += wlen[g];
-    }
-    for (uint32_t rnd = 0; rnd <= nround; rnd++) {
-#pragma unroll
-        for (uint32_t g = 0; g < kRsrcGroup; g++) {
-            if (round_of[g] != rnd || wlen[g] == 0) continue;  // uniform
-            const uint32_t src = rs[g] + wlo[g];
-            for (uint32_t x = threadIdx.x; x < wlen[g]; x += kBlock) {
-                wk[base[g] + x] = bk[src + x];
-                wv[base[g] + x] = bp[src + x];
-            }
-        }
-        __syncthreads();
-        // every partner of the round: a fixed log2(S) + 1 steps over [r_lo,
-        // r_lo + S), positions at or past r_hi never before the element
-        uint32_t cc[kRsrcGroup];
-#pragma unroll
-        for (uint32_t g = 0; g < kRsrcGroup; g++) cc[g] = 0;
-        for (uint32_t step = S >> 1; step > 0; step >>= 1) {
-#pragma unroll
-            for (uint32_t g = 0; g < kRsrcGroup; g++) {
-                const uint32_t idx = r_lo[g] + cc[g] + step - 1;
-                const uint32_t li = min(base[g] + (idx - wlo[g]), kRsrcWin - 1);
-                const bool go = round_of[g] == rnd && idx < r_hi[g] && rsrc_before(g0 + g < a, wk[li], wv[li], k, v);
-                cc[g] += rsrc_step(go, step);
-            }
-        }
-#pragma unroll
-        for (uint32_t g = 0; g < kRsrcGroup; g++) {
-            const uint32_t idx = r_lo[g] + cc[g];
-            const uint32_t li = min(base[g] + (idx - wlo[g]), kRsrcWin - 1);
-            const bool go = round_of[g] == rnd && idx < r_hi[g] && rsrc_before(g0 + g < a, wk[li], wv[li], k, v);
-            cc[g] += (uint32_t)go;
-            if (round_of[g] == rnd) o += r_lo[g] + cc[g];
-        }
-        __syncthreads();
-    }
-    if (any_global)  // rare: a partner window past the LDS buffer, searched in L2
-#pragma unroll
-        for (uint32_t g = 0; g < kRsrcGroup; g++) {
-            if (base[g] != UINT32_MAX) continue;
-            const bool left = g0 + g < a;
-            const int64_t* gk_ = bk + rs[g];
-            const uint32_t* gv_ = bp + rs[g];
-            uint32_t lo = r_lo[g], len = r_hi[g] - r_lo[g];
-            while (len > 0) {
-                const uint32_t half = len >> 1, mid = lo + half;
-                if (rsrc_before(left, gk_[mid], gv_[mid], k, v)) {
-                    lo = mid + 1;
-                    len -= half + 1;
-                } else {
-                    len = half;
-                }
-            }
-            o += lo;
-        }
-    RS_MARK(1, 3);
     ok[(uint64_t)P.out_off + o] = k;
     op[(uint64_t)P.out_off + o] = v;
-    if (samp && (o % kRsrcBStride) == 0) samp[((uint64_t)P.out_off + o) / kRsrcBStride] = k;
-    RS_MARK(1, 4);
 }
 
-// The bound queries over the sorted keys: every block stages the samples
-// (every kRsrcBStride-th sorted key, all pools: pools are 256-aligned, so each
-// pool's samples are a contiguous range) in LDS when they fit, ranks each
-// query among its pool's samples there, and finishes in one window of
-// kRsrcBStride keys (one vector-load round).  Samples that do not fit: the
-// same search over the sample array in L2.
-constexpr uint32_t kRsrcBSampCap = 8192;  // 64 KB of LDS
 __global__ __launch_bounds__(kBlock) void rsrc_bounds_kernel(const DRangePool* __restrict__ pools,
                                                              const int64_t* __restrict__ key,
-                                                             const int64_t* __restrict__ samp, uint32_t n_samp,
                                                              const DRangeBound* __restrict__ q, uint32_t nq,
                                                              uint32_t* __restrict__ out) {
-    __shared__ int64_t ls[kRsrcBSampCap];
-    RS_MARK(2, 0);
-    const bool in_lds = n_samp <= kRsrcBSampCap;
-    if (in_lds)
-        for (uint32_t x = threadIdx.x; x < n_samp; x += kBlock) ls[x] = samp[x];
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    DRangeBound b{0, 0u, 0u};
-    if (t < nq) b = q[t];
-    const DRangePool P = pools[b.pool];
-    __syncthreads();
-    RS_MARK(2, 1);
     if (t >= nq) return;
-    const int64_t* __restrict__ kk = key + P.out_off;
-    const uint32_t s0 = P.out_off / kRsrcBStride, ns = P.pad_len / kRsrcBStride;
-    auto before = [&](int64_t x) { return (x < b.key) | ((x == b.key) & (b.upper != 0)); };
-    // samples before the bound: a branchless search over ns (>= 1) samples
-    uint32_t lo = 0, n = ns;
-    while (n > 1) {
-        const uint32_t half = n >> 1;
-        const int64_t x = in_lds ? ls[s0 + lo + half - 1] : samp[s0 + lo + half - 1];
-        lo += rsrc_step(before(x), half);
-        n -= half;
+    const DRangeBound b = q[t];
+    const DRangePool P = pools[b.pool];
+    const int64_t* __restrict__ k = key + P.out_off;
+    uint32_t lo = 0, hi = P.pad_len;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (b.upper ? k[mid] <= b.key : k[mid] < b.key) lo = mid + 1;
+        else hi = mid;
     }
-    lo += (uint32_t)before(in_lds ? ls[s0 + lo] : samp[s0 + lo]);
-    // lo samples before it: the bound is in ((lo - 1) * B, lo * B]; the
-    // window's kRsrcBStride - 1 keys after sample lo - 1, in one round
-    uint32_t c = 0;
-    if (lo > 0) {
-        const uint32_t w0 = (lo - 1) * kRsrcBStride + 1;
-        int64_t x[kRsrcBStride - 1];
-#pragma unroll
-        for (uint32_t i = 0; i < kRsrcBStride - 1; i++) x[i] = w0 + i < P.pad_len ? kk[w0 + i] : INT64_MAX;
-        c = w0;
-#pragma unroll
-        for (uint32_t i = 0; i < kRsrcBStride - 1; i++) c += (uint32_t)(w0 + i < P.pad_len && before(x[i]));
-    }
-    out[t] = c;
-    RS_MARK(2, 2);
+    out[t] = lo;
 }
 
 // The whole sort + bounds.  Buffers: keys / positions 2 x n_elems each (ping-
-// pong); the sorted positions end in d_pos[*which]; d_samp holds n_elems /
-// kRsrcBStride samples.  Event pairs: ev_tile around the tile launch,
-// ev_merge[2m], ev_merge[2m + 1] around rank launch m (at most max_merge of
-// them), the last pair around the bounds launch.  Returns the number of rank
-// launches in *n_merge (at least one).
+// pong); the sorted ones end in *which (0 or 1).  Event pairs: ev_tile around
+// the tile launch, ev_merge[2m], ev_merge[2m + 1] around merge launch m (at
+// most max_merge of them).  Returns the number of merge launches in *n_merge.
 hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max_pad, const DRangeTile* d_tiles,
                        uint32_t n_tiles, const uint32_t* d_blk_pool, uint32_t n_elems, int64_t* d_key[2],
-                       uint32_t* d_pos[2], int64_t* d_samp, const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds,
-                       int* which, hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1,
-                       const hipEvent_t* ev_merge, int max_merge, int* n_merge) {
+                       uint32_t* d_pos[2], const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds, int* which,
+                       hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1, const hipEvent_t* ev_merge,
+                       int max_merge, int* n_merge) {
     *which = 0;
     *n_merge = 0;
     if (n_elems == 0 || n_tiles == 0) return hipSuccess;
     if (n_elems % kBlock) return hipErrorInvalidValue;
-    hipExtLaunchKernelGGL(rsrc_tile_kernel, dim3(n_tiles), dim3(kRsrcTileThreads), 0, stream, ev_tile0, ev_tile1, 0, st,
+    hipExtLaunchKernelGGL(rsrc_tile_kernel, dim3(n_tiles), dim3(kRsrcBlock), 0, stream, ev_tile0, ev_tile1, 0, st,
                           d_pools, d_tiles, d_key[0], d_pos[0]);
     int b = 0, m = 0;
-    const uint32_t n_eblk = n_elems / kBlock;
-    for (uint64_t R = kRsrcTile;; R *= kRsrcGroup) {
-        if (m + 1 >= max_merge) return hipErrorInvalidValue;  // the last pair is the bounds'
-        const bool last = R * kRsrcGroup >= max_pad;
-        hipExtLaunchKernelGGL(rsrc_rank_kernel, dim3(n_eblk), dim3(kBlock), 0, stream, ev_merge[2 * m],
-                              ev_merge[2 * m + 1], 0, d_pools, d_blk_pool, d_key[b], d_pos[b], d_key[b ^ 1],
-                              d_pos[b ^ 1], (uint32_t)R, last ? d_samp : nullptr);
-        b ^= 1;
-        m++;
-        if (last) break;
+    for (uint32_t R = kRsrcTile; R < max_pad; R <<= 1, b ^= 1, m++) {
+        if (m >= max_merge) return hipErrorInvalidValue;
+        hipExtLaunchKernelGGL(rsrc_merge_kernel, dim3(n_elems / kBlock), dim3(kBlock), 0, stream, ev_merge[2 * m],
+                              ev_merge[2 * m + 1], 0, d_pools, d_blk_pool, d_key[b], d_pos[b], d_key[b ^ 1], d_pos[b ^ 1],
+                              R);
     }
     if (nq)
-        hipExtLaunchKernelGGL(rsrc_bounds_kernel, dim3((nq + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
-                              ev_merge[2 * (max_merge - 1)], ev_merge[2 * (max_merge - 1) + 1], 0, d_pools, d_key[b],
-                              d_samp, n_elems / kRsrcBStride, d_q, nq, d_bounds);
+        hipLaunchKernelGGL(rsrc_bounds_kernel, dim3((nq + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, d_pools,
+                           d_key[b], d_q, nq, d_bounds);
     *which = b;
     *n_merge = m;
     return hipGetLastError();

@@ -2,8 +2,8 @@
 // remaining rows are all range-source searches (Sig::rs_field: a pool term and
 // numeric ranges on one field, e.g. C2's skill windows with ^boost) is decided
 // in ONE batch.  The device sorts every pool's candidates by their value and
-// finds each signature's range bounds in that order (rsrc_tile /
-// rsrc_rank kernels); the host walks each pool's rows on its own worker
+// finds each signature's range bounds in that order (rsrc_tile / rsrc_merge /
+// rsrc_bounds kernels); the host walks each pool's rows on its own worker
 // with a min tree over the sorted candidates, so a row's next hit costs
 // O(log n) instead of a walk over its hit list past every earlier selection
 // (matchmaker_process.go:86-130 over bluge's numeric range searcher,
@@ -214,7 +214,6 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     for (auto& a : d_rkey_) a.reserve(std::max<uint64_t>(n_elems, 1), false);
     for (auto& a : d_rpos_) a.reserve(std::max<uint64_t>(n_elems, 1), false);
     d_rbound_.reserve(std::max<uint32_t>(nq, 1), false);
-    d_rsamp_.reserve(std::max<uint64_t>(n_elems / kRsrcBStride, 1), false);
     h_rpos_.reserve(std::max<uint64_t>(n_elems, 1));
     h_rbound_.reserve(std::max<uint32_t>(nq, 1));
     if (!rs_ev_[0])
@@ -227,7 +226,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     const uint8_t* db = d_rblob_.p;
     NKM_HIP(launch_rsrc(dstore(), reinterpret_cast<const DRangePool*>(db), max_pad,
                         reinterpret_cast<const DRangeTile*>(db + o_tiles), n_tiles,
-                        reinterpret_cast<const uint32_t*>(db + o_blk), (uint32_t)n_elems, dk, dp, d_rsamp_.p,
+                        reinterpret_cast<const uint32_t*>(db + o_blk), (uint32_t)n_elems, dk, dp,
                         reinterpret_cast<const DRangeBound*>(db + o_q), nq, d_rbound_.p, &which, stream_, rs_ev_[0],
                         rs_ev_[1], rs_ev_ + 2, kRsrcMaxMerge, &n_merge));
     if (n_elems) NKM_HIP(hipMemcpyAsync(h_rpos_.p, d_rpos_[which].p, n_elems * 4, hipMemcpyDeviceToHost, stream_));
@@ -424,14 +423,11 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     const auto t4 = clk::now();
     // algorithmic bytes: the tile kernel reads every source entry's slot id and
     // alive flag (5 B), the valid candidates' kind and value (9 B), and writes
-    // each element's key and position (12 B); a rank launch reads and writes
-    // them (24 B; the last also a sample key per kRsrcBStride elements); the
-    // samples and windows its searches re-read are lines already in L2 and
-    // are not counted, nor are the bound queries' (16 B read, 4 B written each)
+    // each element's key and position (12 B); a merge reads and writes them
     uint64_t nvalid = 0;
     for (uint32_t v : valid) nvalid += v;
     stats.k_bytes[5] += (int64_t)(src_total * 5 + nvalid * 9 + n_elems * 12);
-    if (n_merge > 0) stats.k_bytes[4] += (int64_t)((uint64_t)n_merge * n_elems * 24 + n_elems / kRsrcBStride * 8);
+    stats.k_bytes[4] += (int64_t)(n_merge * n_elems * 24);
     stats.pair_evals += (int64_t)src_total;
     for (uint64_t q : task_pairs) stats.pairs_decided += (int64_t)q;
     for (uint64_t h : task_hits) stats.par_hits += h;

@@ -1013,7 +1013,7 @@ int Core::insert(const mm_ticket* ts, int32_t n) {
     const auto t2 = clk::now();
     // a large batch on the host workers (mm_insert.cpp); NKM_BULK=0: always
     // per ticket, =force: at any size (tests)
-    double ph[5] = {0, 0, 0, 0, 0};
+    double ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const bool bulk = bulk_mode_ != 0 && par_mode_ && (bulk_mode_ == 2 || n >= 4096) && insert_bulk(ts, n, ph);
     if (!bulk)
         for (int i = 0; i < n; i++) {
@@ -1025,10 +1025,11 @@ int Core::insert(const mm_ticket* ts, int32_t n) {
     if (std::getenv("NKM_PROFILE") && n >= 1024) {
         auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr,
-                     "[nkm] insert %d: compact %.1f ms | %s %.1f ms (ids %.1f, sigs %.1f, strings %.1f, columns %.1f, "
+                     "[nkm] insert %d: compact %.1f ms | %s %.1f ms (ids %.1f, sigs %.1f [queries %.1f compile %.1f "
+                     "triples %.1f clauses %.1f lookup %.1f commit %.1f], strings %.1f, columns %.1f, "
                      "indexes %.1f) | sync/index/upload %.1f ms\n",
-                     n, ms(t1, t2), bulk ? "bulk add" : "add (incl. compiles)", ms(t2, t3), ph[0], ph[1], ph[2], ph[3],
-                     ph[4], ms(t3, clk::now()));
+                     n, ms(t1, t2), bulk ? "bulk add" : "add (incl. compiles)", ms(t2, t3), ph[0], ph[1], ph[5], ph[6],
+                     ph[7], ph[8], ph[9], ph[10], ph[2], ph[3], ph[4], ms(t3, clk::now()));
     }
     return MM_OK;
 }

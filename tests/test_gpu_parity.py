@@ -183,7 +183,7 @@ def test_range_batches(config, n, passes, cfg, par, monkeypatch):
     numeric ranges on one field — C2's skill windows; config 15 adds parties,
     Min < Max, CountMultiple, Intervals, MUST_NOT and ^0.5 ranges and tickets
     whose skill is a keyword; 16 puts every ticket in one pool.  The pools'
-    candidates are sorted on the device (rsrc_tile / rsrc_rank)
+    candidates are sorted on the device (rsrc_tile / rsrc_merge / rsrc_bounds)
     and the min-tree walk decides every row of the pass in ONE batch: groups
     and post-pass state equal to the oracle's, on the serial and the parallel
     host sweeps (NKM_PARALLEL=force)."""
@@ -194,9 +194,9 @@ def test_range_batches(config, n, passes, cfg, par, monkeypatch):
 
 
 def test_range_batch_multilevel_sort(monkeypatch):
-    """One pool of 40,000 range-source tickets (config 16): past two
-    rsrc_rank_kernel launches' reach (512-element tiles, runs x 8 per launch:
-    32,768 candidates), so the pool's sort takes three rank launches.  The range batch (NKM_RANGE default) must
+    """One pool of 40,000 range-source tickets (config 16): 1,024-element
+    tiles merged up to runs of 65,536 (6 rsrc_merge launches, the last one
+    over a partner run shorter than its own).  The range batch (NKM_RANGE default) must
     form exactly the groups and post-pass state of the list-based replay
     (NKM_RANGE=0), which the oracle pins at the smaller sizes above."""
     def one(rng):
@@ -213,7 +213,7 @@ def test_range_batch_multilevel_sort(monkeypatch):
     got, got_state = one("1")
     want, want_state = one("0")
     assert got.n_batches == 1 and got.eval_kernel in (6, 7), (got.n_batches, got.eval_kernel)
-    assert got.eval_kernel == 6 and got.eval_launches == 3, (got.eval_kernel, got.eval_launches)  # rank launches
+    assert got.eval_kernel == 6 and got.eval_launches == 6, (got.eval_kernel, got.eval_launches)  # merge launches
     assert len(got.groups) > 1000
     assert got.groups == want.groups
     assert got_state == want_state

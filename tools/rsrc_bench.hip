@@ -1,11 +1,11 @@
 // tools/rsrc_bench.hip — the library's range-batch sort (rsrc_tile_kernel +
-// rsrc_rank_kernel launches, launch_rsrc) in isolation on C2's shape: 4 pools
+// rsrc_merge_kernel launches + rsrc_bounds_kernel, launch_rsrc) in isolation
+// on C2's shape: 4 pools
 // of 25,000 candidates whose numeric values repeat (integer skills ~ N(1500,
 // 300)), 54k bound queries.  Times every launch by its event pair (warm, back
 // to back, as in the pass: the store was just uploaded) and checks the sorted
 // positions and the bounds against a host sort.  argv[1]: pools (default 4),
 // argv[2]: candidates per pool (25000), argv[3]: bound queries (54000).
-#define NKM_RS_PROF 1
 #include "../nakama_amd/csrc/mm_kernels.hip"
 
 #include <algorithm>
@@ -82,11 +82,10 @@ int main(int argc, char** argv) {
     }
     uint32_t* d_bounds;
     CK(hipMalloc(&d_bounds, 4 * (size_t)nq));
-    int64_t* d_samp;
-    CK(hipMalloc(&d_samp, 8 * (size_t)(n_elems / kRsrcBStride + 1)));
+
     hipStream_t s;
     CK(hipStreamCreate(&s));
-    constexpr int kMax = 8;
+    constexpr int kMax = 20;
     hipEvent_t ev[2 + 2 * kMax];
     for (auto& evx : ev) CK(hipEventCreate(&evx));
     std::vector<double> t_tile, t_rank[kMax], t_all, t_bound;
@@ -96,7 +95,7 @@ int main(int argc, char** argv) {
         CK(hipEventCreate(&a));
         CK(hipEventCreate(&b));
         CK(hipEventRecord(a, s));
-        CK(launch_rsrc(st, d_pools, max_pad, d_tiles, (uint32_t)tiles.size(), d_blk, n_elems, dk, dp, d_samp, d_q, nq, d_bounds,
+        CK(launch_rsrc(st, d_pools, max_pad, d_tiles, (uint32_t)tiles.size(), d_blk, n_elems, dk, dp, d_q, nq, d_bounds,
                        &which, s, ev[0], ev[1], ev + 2, kMax, &nm));
         CK(hipEventRecord(b, s));
         CK(hipStreamSynchronize(s));
@@ -108,45 +107,15 @@ int main(int argc, char** argv) {
             CK(hipEventElapsedTime(&ms, ev[2 + 2 * m], ev[3 + 2 * m]));
             t_rank[m].push_back(ms * 1e3);
         }
-        CK(hipEventElapsedTime(&ms, ev[2 + 2 * (kMax - 1)], ev[3 + 2 * (kMax - 1)]));
-        t_bound.push_back(ms * 1e3);
         CK(hipEventElapsedTime(&ms, a, b));
         t_all.push_back(ms * 1e3);
     }
     auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
-    std::printf("rsrc: %u pools x %u, %u elements, %zu tiles, %d rank launches, %u bounds\n", np, per, n_elems,
+    std::printf("rsrc: %u pools x %u, %u elements, %zu tiles, %d merge launches, %u bounds\n", np, per, n_elems,
                 tiles.size(), nm, nq);
     std::printf("  tile %.2f us", med(t_tile));
-    for (int m = 0; m < nm; m++) std::printf(" | rank%d %.2f us", m, med(t_rank[m]));
-    std::printf(" | bounds %.2f us | all (events around the launches) %.2f us\n", med(t_bound), med(t_all));
-    // phase profile of the last repetition (wall clock, 100 MHz): per kernel the
-    // median workgroup's phases and the spread of workgroup starts / ends
-    {
-        static uint64_t prof[3][8192][6];
-        CK(hipMemcpyFromSymbol(prof, HIP_SYMBOL(g_rs_prof), sizeof prof));
-        int khz = 0;
-        CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
-        const double us = 1e3 / (double)khz;
-        const uint32_t nwg[3] = {(uint32_t)tiles.size(), n_elems / 256, (nq + 255) / 256};
-        const int nph[3] = {3, 4, 2};
-        const char* names[3] = {"tile", "rank(last)", "bounds"};
-        for (int k = 0; k < 3; k++) {
-            uint64_t s0 = UINT64_MAX, e1 = 0;
-            std::vector<double> ph[4];
-            for (uint32_t w = 0; w < nwg[k] && w < 8192; w++) {
-                s0 = std::min(s0, prof[k][w][0]);
-                e1 = std::max(e1, prof[k][w][nph[k]]);
-                for (int i = 0; i < nph[k]; i++) ph[i].push_back((double)(prof[k][w][i + 1] - prof[k][w][i]) * us);
-            }
-            std::vector<double> starts;
-            for (uint32_t w = 0; w < nwg[k] && w < 8192; w++) starts.push_back((double)(prof[k][w][0] - s0) * us);
-            std::printf("  %s (%u wg): first start -> last end %.2f us; start spread p50 %.2f max %.2f; phases p50:",
-                        names[k], nwg[k], (double)(e1 - s0) * us, med(starts),
-                        *std::max_element(starts.begin(), starts.end()));
-            for (int i = 0; i < nph[k]; i++) std::printf(" %.2f", med(ph[i]));
-            std::printf(" us\n");
-        }
-    }
+    for (int m = 0; m < nm; m++) std::printf(" | merge%d %.2f us", m, med(t_rank[m]));
+    std::printf(" | all (events around the launches, bounds included) %.2f us\n", med(t_all));
     // check
     std::vector<uint32_t> got(n_elems), gb(nq);
     CK(hipMemcpy(got.data(), dp[which], 4 * (size_t)n_elems, hipMemcpyDeviceToHost));
