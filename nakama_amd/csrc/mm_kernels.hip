@@ -106,37 +106,38 @@ __device__ __forceinline__ void load_field_table(const DStore& st, FieldTable& f
     }
 }
 __device__ __forceinline__ bool field_table_ok(const DStore& st) { return st.n_fields <= kFieldLds; }
+template <int NB = kEvalBatch>
 __device__ __forceinline__ bool eval_batched(const DStore& st, const FieldTable& ft, uint8_t qkind,
                                              const DClause* __restrict__ cl, int n, uint32_t s, double* sp) {
     // every load first and unconditional — clause indexes clamped into the
     // list (the table's first clause for an empty one), field ids into the
     // table (OP_FALSE names no column) — so the clauses come in one round and
     // their columns in the next; the uncommon query shapes are decided after
-    const int nn = n < 1 ? 1 : (n > kEvalBatch ? kEvalBatch : n);
+    const int nn = n < 1 ? 1 : (n > NB ? NB : n);
     const DClause* __restrict__ cb = n >= 1 ? cl : st.clauses;
-    DClause c[kEvalBatch];
+    DClause c[NB];
 #pragma unroll
-    for (int i = 0; i < kEvalBatch; i++) c[i] = cb[i < nn ? i : nn - 1];
-    uint8_t kind[kEvalBatch];
-    int64_t val[kEvalBatch];
+    for (int i = 0; i < NB; i++) c[i] = cb[i < nn ? i : nn - 1];
+    uint8_t kind[NB];
+    int64_t val[NB];
     // global (not flat) loads: a flat load also counts against lgkmcnt, so
     // every LDS wait would wait for it
     typedef const __attribute__((address_space(1))) uint8_t gu8;
     typedef const __attribute__((address_space(1))) int64_t gi64;
 #pragma unroll
-    for (int i = 0; i < kEvalBatch; i++) {
+    for (int i = 0; i < NB; i++) {
         const uint32_t f = c[i].op == OP_FALSE ? 0u : min((uint32_t)c[i].field, st.n_fields - 1);
         kind[i] = ((gu8*)ft.kind[f])[s];
         val[i] = ((gi64*)ft.val[f])[s];
     }
     if (qkind == QK_MATCHALL) { *sp = 1.0; return true; }
     if (qkind == QK_MATCHNONE) return false;
-    if (n > kEvalBatch) return eval_parsed(st, qkind, cl, n, s, sp);
+    if (n > NB) return eval_parsed(st, qkind, cl, n, s, sp);
     if (n <= 0) { *sp = 1.0; return true; }  // eval_parsed: no must, no should -> MatchAll(1)
     double ms = 0.0, ss = 0.0;
     bool has_must = false, has_should = false, any_should = false, fail = false;
 #pragma unroll
-    for (int i = 0; i < kEvalBatch; i++) {
+    for (int i = 0; i < NB; i++) {
         if (i >= n) break;
         bool h = false;
         double sc = c[i].score;
@@ -1607,7 +1608,7 @@ template <> struct PackT<32> { using pm = uint32_t; using rv = uint32_t; };
 template <> struct PackT<64> { using pm = uint32_t; using rv = uint64_t; };
 
 template <int S>
-__global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRow* __restrict__ rows, uint32_t n_rows,
+__global__ __launch_bounds__(kBlock, 8) void rpack_kernel(DStore st, const DSmallRow* __restrict__ rows, uint32_t n_rows,
                                                        uint8_t* __restrict__ obuf, PackLayout L) {
     using PmT = typename PackT<S>::pm;
     using RvT = typename PackT<S>::rv;
@@ -1656,8 +1657,12 @@ __global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRo
         const int32_t smin = st.minc[s], smax = st.maxc[s];
         live = al != 0;
         double sp = 0.0;
-        const bool e = batched ? eval_batched(st, ft, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp)
-                               : eval_parsed(st, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp);
+        // every row of the wave with at most 2 clauses (C5's bucket term and
+        // skill range): the 2-clause batch (half the registers: 8 waves per
+        // SIMD instead of 5)
+        const bool two = __ballot(rq.n_clauses > 2) == 0;
+        const bool e = batched && two ? eval_batched<2>(st, ft, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp)
+                                      : eval_parsed(st, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp);
         Ebits = __ballot(e);  // bit a * 8 + b: member a's query matches member b's document
         m = live && e && smin >= rmin && smax <= rmax;
         if (m) key = dsortable((sp + 1.0) + 1.0);
@@ -1672,14 +1677,12 @@ __global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRo
             m = smin >= rmin && smax <= rmax;
             if (m) {
                 double sp = 0.0;
-                m = batched ? eval_batched(st, ft, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp)
-                            : eval_parsed(st, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp);
+                m = eval_parsed(st, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp);
                 key = dsortable((sp + 1.0) + 1.0);
             }
             if (m) {
                 double dd;
-                rv = batched ? eval_batched(st, ft, h.kind, st.clauses + h.clause_off, h.n_clauses, d.slot, &dd)
-                             : eval_parsed(st, h.kind, st.clauses + h.clause_off, h.n_clauses, d.slot, &dd);
+                rv = eval_parsed(st, h.kind, st.clauses + h.clause_off, h.n_clauses, d.slot, &dd);
             }
         }
     }
@@ -1712,9 +1715,7 @@ __global__ __launch_bounds__(kBlock) void rpack_kernel(DStore st, const DSmallRo
             if (rvi) rbits |= (RvT)((RvT)1 << ri);
             if (m && rank < (uint32_t)P && ri < (uint32_t)P) {
                 double dd;
-                const bool hit = batched ? eval_batched(st, ft, q.kind, st.clauses + q.clause_off, q.n_clauses, si, &dd)
-                                         : eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, si, &dd);
-                if (hit) pmask |= (PmT)((PmT)1 << ri);
+                if (eval_parsed(st, q.kind, st.clauses + q.clause_off, q.n_clauses, si, &dd)) pmask |= (PmT)((PmT)1 << ri);
             }
         }
     }
