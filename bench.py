@@ -76,11 +76,14 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-numa-bind", action="store_true",
                     help="do not bind the process to its GPU's NUMA node (one process per GPU)")
-    ap.add_argument("--deliver", action="store_true",
-                    help="pipelined delivery (mm_set_delivery + mm_process_deliver): the timed step is the pass and "
-                         "its hand-off to the library's delivery thread, whose callback is a native no-op router "
-                         "(tools/synth.cpp synth_deliver_noop: every entry read, tickets counted); the callback's "
-                         "time and the flush wait after the step are reported beside the line")
+    ap.add_argument("--no-deliver", dest="deliver", action="store_false",
+                    help="time mm_process alone and free its result untimed, instead of the default pipelined "
+                         "delivery (BASELINE.md: the pass includes delivery to a no-op router): mm_set_delivery + "
+                         "mm_process_deliver, the timed step ending when the pass's result is handed to the "
+                         "library's delivery thread, whose callback is a native no-op router (tools/synth.cpp "
+                         "synth_deliver_noop: every entry read, tickets counted) running behind the step; its time and "
+                         "the flush wait after the step are reported beside the line (single GPU, processDefault; "
+                         "the cluster front and the override path time mm_process)")
     ap.add_argument("--override", action="store_true",
                     help="register a MatchmakerOverride (processCustom path): the timed step is the candidate pass, "
                          "a native first-disjoint override and mm_process_commit (per rank under the cluster front)")
@@ -288,11 +291,8 @@ def main():
     mm = nakama_amd.LocalMatchmaker(max_intervals=2, device=local, rev_precision=args.config in REV, rev_threshold=0,
                                     override=(lambda groups: groups) if args.override else None)
     cm = None
-    deliv = None  # --deliver: the callback's counters (tools/synth.cpp SynthDelivered)
-    if args.deliver:
-        if world > 1 or args.override:
-            raise SystemExit("--deliver: one GPU, processDefault (the cluster front and the override path are "
-                             "measured without it)")
+    deliv = None  # pipelined delivery: the callback's counters (tools/synth.cpp SynthDelivered)
+    if args.deliver and world == 1 and not args.override:
         import ctypes
         from nakama_amd import capi
 
@@ -464,7 +464,7 @@ def main():
                    # first-disjoint stand-in for the user's MatchmakerOverride, runtime.go:212)
                    "override_step_ms": ({k: statistics.median(v) for k, v in step_phases.items()}
                                         if step_phases else None),
-                   # --deliver: the timed step ends when mm_process_deliver returns (the pass done, its
+                   # the default (--no-deliver off): the timed step ends when mm_process_deliver returns (the pass done, its
                    # result queued); the no-op router's callback runs on the delivery thread behind it
                    "delivery": ({"mode": "pipelined (mm_process_deliver, depth 2)",
                                  "callback_ms_p50": statistics.median(deliver_ms),

@@ -1607,6 +1607,26 @@ template <> struct PackT<16> { using pm = uint16_t; using rv = uint16_t; };
 template <> struct PackT<32> { using pm = uint32_t; using rv = uint32_t; };
 template <> struct PackT<64> { using pm = uint32_t; using rv = uint64_t; };
 
+// Lane `base + i` of this lane's 8-lane segment (i a constant after
+// unrolling): ds_swizzle in bitmask mode — lane = (lane & 0x18) | i within
+// each 32-lane half — with no address operand (__shfl is a ds_bpermute).
+__device__ __forceinline__ int seg8_bcast(int v, int i) {
+    switch (i & 7) {
+        case 0: return __builtin_amdgcn_ds_swizzle(v, 0x18 | (0 << 5));
+        case 1: return __builtin_amdgcn_ds_swizzle(v, 0x18 | (1 << 5));
+        case 2: return __builtin_amdgcn_ds_swizzle(v, 0x18 | (2 << 5));
+        case 3: return __builtin_amdgcn_ds_swizzle(v, 0x18 | (3 << 5));
+        case 4: return __builtin_amdgcn_ds_swizzle(v, 0x18 | (4 << 5));
+        case 5: return __builtin_amdgcn_ds_swizzle(v, 0x18 | (5 << 5));
+        case 6: return __builtin_amdgcn_ds_swizzle(v, 0x18 | (6 << 5));
+        default: return __builtin_amdgcn_ds_swizzle(v, 0x18 | (7 << 5));
+    }
+}
+__device__ __forceinline__ int64_t seg8_bcast64(int64_t v, int i) {
+    const int lo = seg8_bcast((int)(uint32_t)v, i), hi = seg8_bcast((int)(uint32_t)((uint64_t)v >> 32), i);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 template <int S>
 __global__ __launch_bounds__(kBlock, 8) void rpack_kernel(DStore st, const DSmallRow* __restrict__ rows, uint32_t n_rows,
                                                        uint8_t* __restrict__ obuf, PackLayout L) {
@@ -1691,17 +1711,19 @@ __global__ __launch_bounds__(kBlock, 8) void rpack_kernel(DStore st, const DSmal
     uint32_t rank = 0;
 #pragma unroll
     for (int i = 0; i < S; i++) {
-        const int64_t ki = __shfl(key, base + i);
+        const int64_t ki = S == 8 ? seg8_bcast64(key, i) : __shfl(key, base + i);
         rank += (uint32_t)(((mine >> i) & 1) && (ki > key || (ki == key && i < j)));
     }
     PmT pmask = 0;
     RvT rbits = 0;
     if (square) {
+#pragma unroll
         for (int i = 0; i < S; i++) {
-            const uint32_t ri = (uint32_t)__shfl((int)rank, base + i);
-            const int rvi = __shfl((int)rv, base + i);
+            const uint32_t ri = (uint32_t)(S == 8 ? seg8_bcast((int)rank, i) : __shfl((int)rank, base + i));
             if (!((mine >> i) & 1)) continue;
-            if (rvi) rbits |= (RvT)((RvT)1 << ri);
+            // entry i's reverse bit: rv of lane i = its match (mine bit i) and
+            // E[i][seg] — from the ballot, no exchange
+            if ((Ebits >> (i * S + seg)) & 1) rbits |= (RvT)((RvT)1 << ri);
             // entry j's query against entry i's document: E[j][i]
             if (m && rank < (uint32_t)P && ri < (uint32_t)P && ((Ebits >> (j * S + i)) & 1)) pmask |= (PmT)((PmT)1 << ri);
         }
