@@ -26,6 +26,15 @@ inline bool go_parse_float(const std::string& s, double* out) {
     if (n == 0) return false;
     bool neg = false;
     if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; i = 1; }
+    if (n - i >= 1 && n - i <= 15) {  // a plain decimal integer below 2^53: exact, strtod's value
+        uint64_t v = 0;
+        size_t k = i;
+        for (; k < n && s[k] >= '0' && s[k] <= '9'; k++) v = v * 10 + (uint64_t)(s[k] - '0');
+        if (k == n) {
+            *out = neg ? -(double)v : (double)v;
+            return true;
+        }
+    }
     auto lower_eq = [&](size_t from, const char* w) {
         size_t wl = std::strlen(w);
         if (n - from != wl) return false;

@@ -358,7 +358,7 @@ bool Core::insert_bulk(const mm_ticket* ts, int32_t n_in, double* ph) {
     wp.run(std::max<size_t>(1, std::min<size_t>(nq, (size_t)wp.size() * 8)), [&](size_t c) {
         const size_t nc = std::max<size_t>(1, std::min<size_t>(nq, (size_t)wp.size() * 8));
         for (size_t j = nq * c / nc; j < nq * (c + 1) / nc; j++)
-            cst[j] = compile_query(std::string(SV(ts[qfirst[j]].query)), &cq[j]);
+            cst[j] = compile_query(SV(ts[qfirst[j]].query), &cq[j]);
     });
     lap(6);  // compiles
     // tickets whose query does not compile are skipped (the reference logs and continues)

@@ -551,7 +551,7 @@ int MultiCore::insert(const mm_ticket* ts, int32_t n) {
                 if (it == local.end()) {
                     if (local.size() >= (1u << 12)) local.clear();
                     QC c;
-                    c.status = compile_query(std::string(q), &c.cq);
+                    c.status = compile_query(q, &c.cq);
                     it = local.emplace(q, std::move(c)).first;
                 }
                 if (it->second.status != CQ_OK) { skip[(size_t)k] = 1; continue; }

@@ -786,7 +786,7 @@ int64_t Core::sig_cached(const mm_ticket& t) {
     CompiledQuery cq;
     bool compiled = false;
     if (qi < 0) {
-        const int rc = compile_query(std::string(q), &cq);
+        const int rc = compile_query(q, &cq);
         compiled = true;
         qi = qtext_.intern(q);
         qstatus_.push_back(rc);
@@ -799,7 +799,7 @@ int64_t Core::sig_cached(const mm_ticket& t) {
     auto eq = [&](uint32_t i) { return qsig_[i].q == qi && qsig_[i].mn == t.min_count && qsig_[i].mx == t.max_count; };
     const int64_t e = qsig_idx_.find(h, eq);
     if (e >= 0) return qsig_[e].sig;
-    if (!compiled) compile_query(std::string(q), &cq);
+    if (!compiled) compile_query(q, &cq);
     const uint32_t sg = sig_of(cq, t.min_count, t.max_count, kNoParty);  // may materialise new columns
     qsig_idx_.put_new(h, (uint32_t)qsig_.size());
     qsig_.push_back(QSig{(uint32_t)qi, t.min_count, t.max_count, sg});

@@ -11,6 +11,7 @@
 #include "termmatch.h"
 
 #include <cmath>
+#include <string_view>
 
 #include "gocompat.h"
 
@@ -22,9 +23,9 @@ struct Tk { TokKind k; std::string s; };
 
 // One UTF-8 rune as Go's bufio.Reader.ReadRune sees it; invalid input yields
 // U+FFFD consuming one byte.
-struct Rune { uint32_t cp; std::string bytes; };
+struct Rune { uint32_t cp; std::string_view bytes; };  // bytes: a view into the input (or U+FFFD's encoding)
 
-bool next_rune(const std::string& in, size_t& at, Rune& r) {
+bool next_rune(std::string_view in, size_t& at, Rune& r) {
     if (at >= in.size()) return false;
     const unsigned char* p = reinterpret_cast<const unsigned char*>(in.data()) + at;
     size_t left = in.size() - at;
@@ -40,12 +41,12 @@ bool next_rune(const std::string& in, size_t& at, Rune& r) {
     }
     if (!ok) {
         r.cp = 0xFFFD;
-        r.bytes = "\xEF\xBF\xBD";
+        r.bytes = std::string_view("\xEF\xBF\xBD", 3);
         at += 1;
         return true;
     }
     r.cp = cp;
-    r.bytes.assign(in, at, len);
+    r.bytes = std::string_view(in.data() + at, len);
     at += len;
     return true;
 }
@@ -61,20 +62,20 @@ bool go_is_space(uint32_t c) {  // unicode.IsSpace
 }
 bool is_ascii_digit(uint32_t c) { return c >= '0' && c <= '9'; }
 
-std::string lex_unescape(const std::string& ch) {  // query_string_lex.go:27-34
-    static const std::string reserved = "+-=&|><!(){}[]^\"~*?:\\/ ";
-    if (ch.find_first_of(reserved) != std::string::npos) return ch;
-    return "\\" + ch;
+std::string lex_unescape(std::string_view ch) {  // query_string_lex.go:27-34
+    static constexpr std::string_view reserved = "+-=&|><!(){}[]^\"~*?:\\/ ";
+    if (ch.find_first_of(reserved) != std::string_view::npos) return std::string(ch);
+    return "\\" + std::string(ch);
 }
 
 class Lexer {
 public:
-    explicit Lexer(const std::string& in) : in_(in) {}
+    explicit Lexer(std::string_view in) : in_(in) {}
     bool run(std::vector<Tk>& out);  // false on lexer error (unterminated phrase)
 
 private:
     enum Mode { M_START, M_PHRASE, M_NUM, M_STR, M_BOOST, M_TILDE, M_OP };
-    const std::string& in_;
+    std::string_view in_;
 };
 
 bool Lexer::run(std::vector<Tk>& out) {
@@ -82,10 +83,10 @@ bool Lexer::run(std::vector<Tk>& out) {
     Mode mode = M_START;
     std::string buf;
     bool esc = false, dot = false, eof = false, take = true;
-    Rune r{0, ""};
+    Rune r{0, {}};
     for (;;) {
         if (take) {
-            if (!next_rune(in_, at, r)) { eof = true; r.cp = 0; r.bytes.clear(); }
+            if (!next_rune(in_, at, r)) { eof = true; r.cp = 0; r.bytes = {}; }
         }
         take = true;
         const bool ender = !esc && (r.cp == ' ' || r.cp == ':' || r.cp == '^' || r.cp == '~');
@@ -95,7 +96,7 @@ bool Lexer::run(std::vector<Tk>& out) {
             if (esc) { esc = false; buf += lex_unescape(r.bytes); mode = M_STR; }
             else if (r.cp == '"') mode = M_PHRASE;
             else if (r.cp == '+' || r.cp == '-' || r.cp == ':' || r.cp == '>' || r.cp == '<' || r.cp == '=') {
-                buf = r.bytes;
+                buf.assign(r.bytes);
                 mode = M_OP;
             } else if (r.cp == '^') mode = M_BOOST;
             else if (r.cp == '~') mode = M_TILDE;
@@ -117,7 +118,7 @@ bool Lexer::run(std::vector<Tk>& out) {
         case M_PHRASE:
             if (eof) return false;  // "unterminated quote"
             if (!esc && r.cp == '"') {
-                out.push_back({TK_PHRASE, buf});
+                out.push_back({TK_PHRASE, std::move(buf)});
                 buf.clear(); esc = false; dot = false;
                 mode = M_START;
             } else if (!esc && r.cp == '\\') esc = true;
@@ -127,7 +128,7 @@ bool Lexer::run(std::vector<Tk>& out) {
         case M_BOOST:
         case M_TILDE:
             if (eof || (!esc && r.cp == ' ')) {
-                out.push_back({mode == M_BOOST ? TK_BOOST : TK_TILDE, buf.empty() ? std::string("1") : buf});
+                out.push_back({mode == M_BOOST ? TK_BOOST : TK_TILDE, buf.empty() ? std::string("1") : std::move(buf)});
                 buf.clear(); esc = false; dot = false;
                 mode = M_START;
                 if (eof) return true;
@@ -138,7 +139,7 @@ bool Lexer::run(std::vector<Tk>& out) {
         case M_NUM:
         case M_STR:
             if (eof || ender) {
-                out.push_back({mode == M_NUM ? TK_NUM : TK_STR, buf});
+                out.push_back({mode == M_NUM ? TK_NUM : TK_STR, std::move(buf)});
                 buf.clear(); esc = false; dot = false;
                 mode = M_START;
                 if (eof) return true;
@@ -303,17 +304,17 @@ Compiler::Base Compiler::range(const std::string& field, bool greater, bool or_e
 }
 
 Compiler::Base Compiler::base() {
-    if (at() == TK_NUM) { std::string s = t_[i_++].s; return number_token("", s); }
+    if (at() == TK_NUM) { const std::string& s = t_[i_++].s; return number_token("", s); }
     if (at() == TK_PHRASE) { i_++; Base b; b.kind = Base::B_PHRASE; b.c.op = OP_FALSE; return b; }
     if (at() != TK_STR) bad();
-    std::string first = t_[i_++].s;
-    if (at() == TK_TILDE) { std::string fz = t_[i_++].s; return fuzzy_token("", first, fz); }
+    const std::string& first = t_[i_++].s;  // tokens are not modified while compiling: references stay valid
+    if (at() == TK_TILDE) { const std::string& fz = t_[i_++].s; return fuzzy_token("", first, fz); }
     if (at() != TK_COLON) return string_token("", first);
     i_++;
     switch (at()) {
     case TK_STR: {
-        std::string v = t_[i_++].s;
-        if (at() == TK_TILDE) { std::string fz = t_[i_++].s; return fuzzy_token(first, v, fz); }
+        const std::string& v = t_[i_++].s;
+        if (at() == TK_TILDE) { const std::string& fz = t_[i_++].s; return fuzzy_token(first, v, fz); }
         return string_token(first, v);
     }
     case TK_NUM:
@@ -338,6 +339,7 @@ Compiler::Base Compiler::base() {
 void Compiler::run() {
     out_->kind = QK_BOOL;
     if (at() == TK_END) bad();
+    out_->clauses.reserve(4);
     while (at() != TK_END) {
         Occur occ = OCC_SHOULD;
         if (at() == TK_PLUS) { occ = OCC_MUST; i_++; }
@@ -369,17 +371,18 @@ void Compiler::run() {
         case Base::B_FUZZY: b.c.score = boosted ? boost : 1.0; break;
         }
         b.c.occur = occ;
-        out_->clauses.push_back(b.c);
+        out_->clauses.push_back(std::move(b.c));
     }
 }
 
 }  // namespace
 
-int compile_query(const std::string& q, CompiledQuery* out) {
+int compile_query(std::string_view q, CompiledQuery* out) {
     out->clauses.clear();
     if (q == "*") { out->kind = QK_MATCHALL; return CQ_OK; }   // match_common.go:246-248
     if (q.empty()) { out->kind = QK_MATCHNONE; return CQ_OK; } // query_string_parser.go:93-95
     std::vector<Tk> toks;
+    toks.reserve(16);
     Lexer lx(q);
     if (!lx.run(toks)) return CQ_INVALID;
     try {

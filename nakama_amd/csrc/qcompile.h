@@ -10,6 +10,7 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <string_view>
 #include <vector>
 
 namespace nkm {
@@ -52,6 +53,6 @@ enum CompileStatus { CQ_OK = 0, CQ_INVALID = -1, CQ_UNSUPPORTED = -8 };
 // reserved for a construct Go accepts that is not lowered here: none remains
 // (Unicode category and script classes, flag groups incl. (?U), POSIX classes
 // are all lowered, termmatch.h).
-int compile_query(const std::string& q, CompiledQuery* out);
+int compile_query(std::string_view q, CompiledQuery* out);
 
 }  // namespace nkm
