@@ -98,12 +98,12 @@ def parse():
                          "'multi' = rank 0 drives one multi-device handle over all WORLD_SIZE GPUs through the C ABI "
                          "(the other ranks only take part in the barriers)")
     ap.add_argument("--traffic", default=None,
-                    help="PMC traffic file (tools/pmc_traffic.py); default profiles/r04_c<config>_traffic.json")
+                    help="PMC traffic file (tools/pmc_traffic.py); default the newest profiles/r0N_c<config>_traffic.json")
     a = ap.parse_args()
     if a.tickets is None:
         a.tickets = DEFAULT_TICKETS.get(a.config, 1_000_000)
     if a.traffic is None:  # the newest committed PMC pass of this config (bench.py matches kernel + tickets)
-        for r in ("r05", "r04"):
+        for r in ("r06", "r05", "r04"):
             a.traffic = os.path.join(ROOT, "profiles", f"{r}_c{a.config}_traffic.json")
             if os.path.exists(a.traffic):
                 break
