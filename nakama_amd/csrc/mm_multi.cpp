@@ -41,6 +41,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -48,6 +50,7 @@
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
+#include <utility>
 #include <vector>
 
 #include "mm_handle.h"
@@ -214,6 +217,7 @@ private:
     bool own_ = false;  // sub-handles are this library's (HIP) handles
     std::vector<void*> subs_;
     std::vector<int> devs_;
+    std::vector<std::vector<int>> sub_cpus_;  // per sub-handle: its device node's CPUs (read once)
     int mode_ = MM_MULTI_POOLS;
     bool rows() const { return mode_ == MM_MULTI_ROWS; }
     std::unique_ptr<Exchange> ex_;
@@ -224,8 +228,78 @@ private:
     void each(F&& f) {
         const int n = (int)subs_.size();
         if (n == 1) { f(0); return; }
-        // every sub-handle on a thread of its own, confined to its device's
-        // node (the caller's thread keeps its placement)
+        // every sub-handle on its persistent thread, confined once to its
+        // device's node (the caller's thread keeps its placement), its
+        // thread_local scratch kept between calls; a call made while another
+        // holds those threads (a mutator beside a pass, or from inside f)
+        // runs on fresh threads instead of waiting
+        std::unique_lock<std::mutex> rl(st_run_mu_, std::try_to_lock);
+        if (!rl.owns_lock()) { each_spawn(f); return; }
+        if (st_.th.empty())
+            for (int i = 0; i < n; i++) st_.th.emplace_back([this, i] { sub_thread(i); });
+        const std::function<void(int)> job = [&](int i) { f(i); };
+        std::unique_lock<std::mutex> lk(st_.mu);
+        st_.job = &job;
+        st_.pending = n;
+        st_.err = nullptr;
+        st_.gen++;
+        st_.cv.notify_all();
+        st_.done.wait(lk, [&] { return st_.pending == 0; });
+        st_.job = nullptr;
+        if (st_.err) std::rethrow_exception(std::exchange(st_.err, nullptr));
+    }
+    struct SubThreads {
+        std::mutex mu;
+        std::condition_variable cv, done;
+        std::vector<std::thread> th;
+        const std::function<void(int)>* job = nullptr;
+        uint64_t gen = 0;
+        int pending = 0;
+        bool stop = false;
+        std::exception_ptr err;
+        void halt() {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                stop = true;
+            }
+            cv.notify_all();
+            for (auto& t : th) t.join();
+            th.clear();
+        }
+        ~SubThreads() { halt(); }  // also when the constructor throws after a row-shard setup used them
+    };
+    SubThreads st_;
+    std::mutex st_run_mu_;  // one each() at a time on st_'s threads
+    void sub_thread(int i) {
+        if (own_) {
+            (void)hipSetDevice(devs_[(size_t)i]);
+            place_thread(i);
+        }
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* job;
+            {
+                std::unique_lock<std::mutex> lk(st_.mu);
+                st_.cv.wait(lk, [&] { return st_.stop || st_.gen != seen; });
+                if (st_.stop) return;
+                seen = st_.gen;
+                job = st_.job;
+            }
+            std::exception_ptr e;
+            try {
+                (*job)(i);
+            } catch (...) {
+                e = std::current_exception();
+            }
+            std::lock_guard<std::mutex> lk(st_.mu);
+            if (e && !st_.err) st_.err = e;
+            if (--st_.pending == 0) st_.done.notify_all();
+        }
+    }
+    void stop_threads() { st_.halt(); }
+    template <class F>
+    void each_spawn(F&& f) {
+        const int n = (int)subs_.size();
         std::vector<std::thread> th;
         for (int i = 0; i < n; i++)
             th.emplace_back([&, i] {
@@ -241,7 +315,7 @@ private:
     // i's device node, so what it first-touches (Insert's columns and records)
     // lands in that node's memory; nothing on a one-node host.
     void place_thread(int i) {
-        const std::vector<int> cpus = node_cpus(device_numa_node(devs_[(size_t)i]));
+        const std::vector<int>& cpus = sub_cpus_[(size_t)i];
         if (cpus.empty()) return;
         cpu_set_t cs;
         CPU_ZERO(&cs);
@@ -354,8 +428,12 @@ MultiCore::MultiCore(const mm_config& cfg, const mm_multi_config& mc) {
     // each sub-handle's host share: the sub-handles on its device's NUMA node
     // (every one when the nodes are unknown) split that node's cores
     std::vector<int> nodes((size_t)n, -1);
+    sub_cpus_.assign((size_t)n, {});
     if (own_)
-        for (int i = 0; i < n; i++) nodes[(size_t)i] = device_numa_node(devs_[(size_t)i]);
+        for (int i = 0; i < n; i++) {
+            nodes[(size_t)i] = device_numa_node(devs_[(size_t)i]);
+            sub_cpus_[(size_t)i] = node_cpus(nodes[(size_t)i]);
+        }
     for (int i = 0; i < n; i++) {
         mm_config c = cfg;
         c.device = devs_[(size_t)i];
@@ -409,6 +487,7 @@ MultiCore::MultiCore(const mm_config& cfg, const mm_multi_config& mc) {
 }
 
 MultiCore::~MultiCore() {
+    stop_threads();
     for (auto& kv : extracts_)
         for (size_t i = 0; i < kv.second->subs.size(); i++) api_.free_extract(subs_[i], &kv.second->subs[i]);
     if (ex_) ex_->abort();

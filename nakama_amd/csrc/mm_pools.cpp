@@ -563,7 +563,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     const size_t nch0 = nb >= par_min(65536) ? (size_t)wp.size() * 2 : 1;
     const bool pipe = few && pipe_mode_ && !dense_ids.empty() && dense_ids.size() == ng && nch0 > 1;
     // the pipelined merge's chunks: the last one waits for the slowest walk,
-    // so its size is the merge's tail (NKM_MCH: chunks per worker)
+    // so its size is the merge's tail
     const size_t nch = pipe ? (size_t)wp.size() * (size_t)kMergeMult : nch0;
     // Identity pools: when every pool's rows are its list in list order
     // (C3 / C4: every member of a pool of fresh tickets searches, and batch

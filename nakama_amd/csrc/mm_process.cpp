@@ -2066,7 +2066,9 @@ int Core::process_custom(GroupList& cands, UVec<uint32_t>& expired,
                 G = cg[sch];
                 E = ce[sch];
                 const size_t g0 = cands.size(), e0 = cands.ents.size();
-                if (e0 + E >= UINT32_MAX) throw std::length_error("processCustom: more than 2^32 candidate entries");
+                // mm_matched holds int32 entry counts and group offsets
+                if (e0 + E > (size_t)INT32_MAX || g0 + G > (size_t)INT32_MAX)
+                    throw std::length_error("processCustom: more than 2^31 - 1 candidate entries");
                 // The whole candidate list from the device straight into the
                 // result arena (custom_direct_): the entries come down in
                 // pinned chunks while the workers turn the previous chunk into

@@ -376,7 +376,22 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             const DRangePool& d = H.d;
             const auto tb0 = clk::now();
             const uint32_t nv = valid[p];
-            for (uint64_t q = piece_at[p]; q < piece_at[p + 1]; q++) leaf_piece(q);
+            bool bad = false;
+            for (uint64_t q = piece_at[p]; q < piece_at[p + 1]; q++) {
+                leaf_piece(q);
+                bad |= leaf_bad[q] != 0;
+            }
+            if (bad) {
+                // a device position out of range: this pool is not walked (its
+                // copies are partly unfilled); the leaf map entries its pieces
+                // did set are cleared, and the error is raised after the job
+                const uint32_t* pv = h_rpos_.p + d.out_off;
+                for (uint64_t q = piece_at[p]; q < piece_at[p + 1]; q++) {
+                    const uint32_t j0 = (uint32_t)(q - piece_at[p]) * kLeafPiece, j1 = std::min(nv, j0 + kLeafPiece);
+                    for (uint32_t j = j0; j < j1 && pv[j] < d.src_len; j++) rs_leaf_[postings_[d.src_off + pv[j]]] = kNoSlot;
+                }
+                continue;
+            }
             H.src.n = nv;
             H.src.slot = H.slot.data();
             H.src.rank = H.rank.data();

@@ -231,59 +231,6 @@ std::vector<int> node_cpus(int prefer) {
     return out;
 }
 
-// Worker placement NKM_PIN=1: each worker pinned to one CPU next to the
-// calling thread — first the physical cores sharing its L3, then the rest of
-// its NUMA node (one hardware thread per core before any SMT sibling).  On a
-// host shared with other jobs a pinned worker cannot move off a busy core
-// (the default node-wide placement can).
-static std::vector<int> worker_cpus(unsigned want) {
-    std::vector<int> out;
-    const char* e = std::getenv("NKM_PIN");
-    if (!e || std::strcmp(e, "1")) return out;
-    const int cpu = sched_getcpu();
-    if (cpu < 0) return out;
-    cpu_set_t allowed;
-    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return out;
-    const std::string base = "/sys/devices/system/cpu/cpu";
-    std::vector<int> l3 = parse_cpulist(base + std::to_string(cpu) + "/cache/index3/shared_cpu_list");
-    std::vector<int> node;
-    for (int nd = 0; nd < 64; nd++) {
-        std::vector<int> l = parse_cpulist("/sys/devices/system/node/node" + std::to_string(nd) + "/cpulist");
-        if (std::find(l.begin(), l.end(), cpu) != l.end()) { node = l; break; }
-    }
-    std::vector<int> cand;
-    auto add = [&](const std::vector<int>& l) {
-        for (int c : l)
-            if (c != cpu && CPU_ISSET(c, &allowed) && std::find(cand.begin(), cand.end(), c) == cand.end()) cand.push_back(c);
-    };
-    add(l3);
-    add(node);
-    // one hardware thread per physical core first
-    std::vector<int> first, second;
-    std::vector<std::string> seen;
-    {
-        std::vector<int> sib0 = parse_cpulist(base + std::to_string(cpu) + "/topology/thread_siblings_list");
-        std::string k;
-        for (int c : sib0) k += std::to_string(c) + ",";
-        seen.push_back(k);
-    }
-    for (int c : cand) {
-        std::vector<int> sib = parse_cpulist(base + std::to_string(c) + "/topology/thread_siblings_list");
-        std::string k;
-        for (int x : sib) k += std::to_string(x) + ",";
-        if (std::find(seen.begin(), seen.end(), k) == seen.end()) {
-            seen.push_back(k);
-            first.push_back(c);
-        } else {
-            second.push_back(c);
-        }
-    }
-    out = first;
-    out.insert(out.end(), second.begin(), second.end());
-    if (out.size() > want) out.resize(want);
-    return out;
-}
-
 // Host worker count: NKM_THREADS, else the visible cores capped at 16 (the
 // per-GPU host share on an 8-GPU node).  Same-box A/B runs on MI355X boxes
 // (profiles/r01_ab_threads.txt) put 8 and 16 workers within the boxes'
@@ -298,15 +245,14 @@ WorkPool& Core::workers() {
         n /= std::max(1u, host_share_);  // sub-handles of one multi handle (mm_multi.cpp) split them too
         n = std::max(1u, std::min(16u, n));
         if (const char* e = std::getenv("NKM_THREADS")) n = std::max(1, std::atoi(e));
-        // NKM_PIN: unset = node-local workers (node_cpus), 1 = one CPU each, 0 = no placement
-        const char* pe = std::getenv("NKM_PIN");
-        const bool node_wide = !pe || (std::strcmp(pe, "0") && std::strcmp(pe, "1"));
-        std::vector<int> area = node_wide ? node_cpus(numa_node_) : std::vector<int>{};
+        // node-local workers (node_cpus; per-CPU pinning measured no better
+        // and cannot move off a core another job keeps busy, profiles/r04n_pin.txt)
+        std::vector<int> area = node_cpus(numa_node_);
         // the node's share: its CPUs over the handles placed on it (a multi
         // handle's sub-handles on that node, or the local ranks)
         if (!area.empty() && !std::getenv("NKM_THREADS") && !std::getenv("LOCAL_WORLD_SIZE"))
             n = std::max(1u, std::min(16u, (unsigned)area.size() / std::max(1u, host_share_)));
-        workers_.reset(new WorkPool(n, worker_cpus(n - 1), area));
+        workers_.reset(new WorkPool(n, {}, area));
     }
     return *workers_;
 }
