@@ -2,6 +2,8 @@
 // replay_parallel and the merges back into the pinned row order) and the
 // packed RevPrecision batches (assembly, rpack_kernel's launch, per-row
 // views).  Part of Core's pass (mm_process.cpp).
+#include <sched.h>
+
 #include <algorithm>
 #include <array>
 #include <atomic>
@@ -797,6 +799,7 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
     };
     std::vector<double> task_ms(ntask, 0.0), walk_prep_ms(ntask, 0.0), walk_ms(ntask, 0.0);  // NKM_PROFILE=2 split
     std::vector<double> walk_end_ms(ntask, 0.0);  // since the job's start
+    std::vector<int> walk_cpu(2 * ntask, -1);       // NKM_PROFILE=2: the CPU a walk started / ended on
     clk::time_point tjob0 = clk::now();
     std::vector<uint64_t> task_hits(ntask, 0), task_pairs(ntask, 0);
     std::vector<uint32_t> pool_stop(ng, UINT32_MAX);  // per pool: the batch row its list ran out at
@@ -843,12 +846,14 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                 prog[gi].recs = run.recs.data();
                 prog[gi].ents = run.ents.data();
                 const auto tr1 = clk::now();
+                if (batch_profile_) walk_cpu[2 * t] = sched_getcpu();
                 run.walk_cuts(D, rv, maxI, pos_of_.data(), chunk_end.data(), (uint32_t)nch, prog[gi].cut,
                               &prog[gi].ncut);
                 const auto tr2 = clk::now();
                 walk_prep_ms[t] += msd(tr0, tr1);
                 walk_ms[t] += msd(tr1, tr2);
                 walk_end_ms[t] = msd(tjob0, tr2);
+                if (batch_profile_) walk_cpu[2 * t + 1] = sched_getcpu();
                 if (run.ents.data() != prog[gi].ents || run.recs.data() != prog[gi].recs)
                     std::abort();  // the bound above was wrong: readers hold the old buffers
                 hits += run.hits_seen;
@@ -975,6 +980,17 @@ bool Core::replay_parallel(const ParPlan& P, std::vector<BGroup>& bg, const UVec
                      "gather %.2f, bounds %.2f ms\n",
                      ntask, ng, wp.size(), st, sw, mw, sp, gpipe ? "beside" : "before", we, msd(tg1, tg2), nch, cm, cw,
                      msd(tg0, tg_ident), msd(tg_ident, tg_setup), msd(tg_setup, tg_gather), msd(tg_gather, tg1));
+        if (ntask <= 16) {  // each walk: pool, ms, rows, ends at (ms into the job), CPU at start/end
+            std::string w;
+            char buf[96];
+            for (size_t k = 0; k < ntask; k++) {
+                const uint32_t gi = order_g[task_off[k]];
+                std::snprintf(buf, sizeof buf, " [p%u %.2f ms %u rows end %.2f cpu %d/%d]", gi, walk_ms[k],
+                              dense_pools_[gi].nrows, walk_end_ms[k], walk_cpu[2 * k], walk_cpu[2 * k + 1]);
+                w += buf;
+            }
+            std::fprintf(stderr, "[nkm]   walks:%s\n", w.c_str());
+        }
     }
     stats.par_rows += nb;
     return true;
