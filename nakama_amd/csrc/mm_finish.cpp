@@ -163,12 +163,17 @@ bool Core::finish_fill_fast(const UVec<uint32_t>& expired, GroupList& groups, mm
             }
         }
         if (by_slot) {
-            for (size_t s = N * c / nch; s < N * (c + 1) / nch; s++)
-                if (sel_[s] & live_[s]) {
-                    live_[s] = 0;  // retired: sessionTickets / partyTickets read live_ (SlotSets)
-                    is_active_[s] = 0;
-                    k++;
-                }
+            // the arrays in locals: a byte store may alias a member vector's
+            // pointer, which would then be reloaded after every store
+            const uint8_t* const S = sel_.data();
+            uint8_t* const L = live_.data();
+            uint8_t* const A = is_active_.data();
+            for (size_t s = N * c / nch; s < N * (c + 1) / nch; s++) {
+                const uint8_t m = S[s] & L[s];  // retired: sessionTickets / partyTickets read live_ (SlotSets)
+                L[s] &= (uint8_t)(m ^ 1);
+                A[s] &= (uint8_t)(m ^ 1);
+                k += m;
+            }
         } else {
             for (size_t i = groups.off[g0]; i < groups.off[g1]; i++) {
                 const uint32_t s = groups.ents[i].first;

@@ -1366,7 +1366,8 @@ int Core::process_default(GroupList& out_groups,
                 cnt_start_us[c] = std::chrono::duration<double, std::micro>(tc0 - ts0).count();
                 cnt_task_us[c] = std::chrono::duration<double, std::micro>(tc1 - tc0).count();
             });
-            stats.asm_count_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
+            const auto tce = std::chrono::steady_clock::now();
+            stats.asm_count_ms += std::chrono::duration<double, std::milli>(tce - ts0).count();
             if (batch_profile_)
                 std::fprintf(stderr, "[nkm]   assemble count sweep: tasks max %.0f us, last start %.0f us\n",
                              *std::max_element(cnt_task_us.begin(), cnt_task_us.end()),
@@ -1422,7 +1423,9 @@ int Core::process_default(GroupList& out_groups,
                 grow_to(P.pool_rows, at[nch]);
             }
             const auto ts1 = std::chrono::steady_clock::now();
+            std::vector<double> sc_task_us(nch, 0.0), sc_start_us(nch, 0.0);  // NKM_PROFILE=2
             wp.run(nch, [&](size_t c) {
+                const auto tc0 = std::chrono::steady_clock::now();
                 size_t o = at[c];
                 // the chunk's positions, thread-private (the chunks' rows of gat share cache lines)
                 static thread_local std::vector<uint32_t> gl;
@@ -1441,8 +1444,15 @@ int Core::process_default(GroupList& out_groups,
                     if (ga) prow[ga[gi]++] = (uint32_t)o;
                     o++;
                 }
+                sc_start_us[c] = std::chrono::duration<double, std::micro>(tc0 - ts1).count();
+                sc_task_us[c] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc0).count();
             });
             stats.asm_scatter_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts1).count();
+            if (batch_profile_)
+                std::fprintf(stderr, "[nkm]   assemble scatter: tasks max %.0f us, last start %.0f us; serial between sweeps %.0f us\n",
+                             *std::max_element(sc_task_us.begin(), sc_task_us.end()),
+                             *std::max_element(sc_start_us.begin(), sc_start_us.end()),
+                             std::chrono::duration<double, std::micro>(ts1 - tce).count());
             return true;
         };
         // RevPrecision: one search per row; large batches build them on the
