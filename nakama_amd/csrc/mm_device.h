@@ -205,6 +205,14 @@ struct PackLayout {
     uint64_t pos, pm, rev, cnt, live, total;
     uint32_t blocks;
     int S, pm_w, rev_w;
+    // the store's query fields when at most 2 (Core::run_packed; npf = 0
+    // otherwise): the square wave loads entry j's values of these columns in
+    // the round that loads the row's query, so the clauses that name them need
+    // no column round after their own
+    uint32_t npf;
+    uint16_t pf[2];
+    const int64_t* pf_val[2];
+    const uint8_t* pf_kind[2];
 };
 NKM_HD inline PackLayout pack_layout(uint64_t n, int S) {
     auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };

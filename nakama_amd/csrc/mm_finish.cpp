@@ -168,12 +168,15 @@ bool Core::finish_fill_fast(const UVec<uint32_t>& expired, GroupList& groups, mm
             const uint8_t* const S = sel_.data();
             uint8_t* const L = live_.data();
             uint8_t* const A = is_active_.data();
-            for (size_t s = N * c / nch; s < N * (c + 1) / nch; s++) {
-                const uint8_t m = S[s] & L[s];  // retired: sessionTickets / partyTickets read live_ (SlotSets)
-                L[s] &= (uint8_t)(m ^ 1);
-                A[s] &= (uint8_t)(m ^ 1);
-                k += m;
-            }
+            // (conditional stores: another task clears is_active_ of this
+            // range's expired slots meanwhile, which a read-modify-write of
+            // every byte here could undo)
+            for (size_t s = N * c / nch; s < N * (c + 1) / nch; s++)
+                if (S[s] & L[s]) {
+                    L[s] = 0;  // retired: sessionTickets / partyTickets read live_ (SlotSets)
+                    A[s] = 0;
+                    k++;
+                }
         } else {
             for (size_t i = groups.off[g0]; i < groups.off[g1]; i++) {
                 const uint32_t s = groups.ents[i].first;

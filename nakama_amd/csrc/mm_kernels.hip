@@ -158,6 +158,66 @@ __device__ __forceinline__ bool eval_batched(const DStore& st, const FieldTable&
     return true;
 }
 
+// eval_batched<NB> on document s whose values of up to two fields (pf: the
+// launch's prefetch fields, npf of them) are already in registers (pk / pv):
+// a clause naming one of them reads the register, any other clause loads
+// its column as eval_batched does.  Same hit and score logic, same order of
+// the double additions.
+template <int NB>
+__device__ __forceinline__ bool eval_batched_pf(const DStore& st, const FieldTable& ft, uint8_t qkind,
+                                                const DClause* __restrict__ cl, int n, uint32_t s, double* sp,
+                                                uint32_t npf, const uint16_t* pf, const uint8_t* pk, const int64_t* pv) {
+    const int nn = n < 1 ? 1 : (n > NB ? NB : n);
+    const DClause* __restrict__ cb = n >= 1 ? cl : st.clauses;
+    DClause c[NB];
+#pragma unroll
+    for (int i = 0; i < NB; i++) c[i] = cb[i < nn ? i : nn - 1];
+    uint8_t kind[NB];
+    int64_t val[NB];
+    typedef const __attribute__((address_space(1))) uint8_t gu8;
+    typedef const __attribute__((address_space(1))) int64_t gi64;
+#pragma unroll
+    for (int i = 0; i < NB; i++) {
+        const uint32_t f = c[i].op == OP_FALSE ? 0u : min((uint32_t)c[i].field, st.n_fields - 1);
+        if (npf > 0 && f == pf[0]) {
+            kind[i] = pk[0];
+            val[i] = pv[0];
+        } else if (npf > 1 && f == pf[1]) {
+            kind[i] = pk[1];
+            val[i] = pv[1];
+        } else {
+            kind[i] = ((gu8*)ft.kind[f])[s];
+            val[i] = ((gi64*)ft.val[f])[s];
+        }
+    }
+    if (qkind == QK_MATCHALL) { *sp = 1.0; return true; }
+    if (qkind == QK_MATCHNONE) return false;
+    if (n > NB) return eval_parsed(st, qkind, cl, n, s, sp);
+    if (n <= 0) { *sp = 1.0; return true; }
+    double ms = 0.0, ss = 0.0;
+    bool has_must = false, has_should = false, any_should = false, fail = false;
+#pragma unroll
+    for (int i = 0; i < NB; i++) {
+        if (i >= n) break;
+        bool h = false;
+        double sc = c[i].score;
+        if (c[i].op != OP_FALSE) {
+            if (c[i].op == OP_TERM) h = kind[i] == KIND_KEYWORD && val[i] == (int64_t)c[i].term;
+            else if (c[i].op == OP_RANGE) h = kind[i] == KIND_NUMERIC && val[i] >= c[i].lo && val[i] <= c[i].hi;
+            else if (c[i].op == OP_TERMSET) h = kind[i] == KIND_KEYWORD && termset_hit(st, c[i].term, val[i], &sc);
+            else h = (kind[i] == KIND_KEYWORD && val[i] == (int64_t)c[i].term) || (kind[i] == KIND_NUMERIC && val[i] == c[i].lo);
+        }
+        if (c[i].occur == OCC_MUST) { has_must = true; if (h) ms += sc; else fail = true; }
+        else if (c[i].occur == OCC_SHOULD) { has_should = true; if (h) { ss += sc; any_should = true; } }
+        else if (h) fail = true;
+    }
+    if (fail) return false;
+    if (!has_must && !has_should) { *sp = 1.0; return true; }
+    if (!has_must) { *sp = ss; return any_should; }
+    *sp = any_should ? ms + ss : ms;
+    return true;
+}
+
 struct Cand {
     uint32_t slot;
     uint32_t idx;
@@ -1636,7 +1696,6 @@ __global__ __launch_bounds__(kBlock, 8) void rpack_kernel(DStore st, const DSmal
     constexpr int P = S < 32 ? S : 32;  // pair-matrix entries per row
     __shared__ uint32_t wlive[kWaves], wmatch[kWaves];
     __shared__ FieldTable ft;
-    load_field_table(st, ft);
     const bool batched = field_table_ok(st);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int seg = lane / S, j = lane % S, base = seg * S;
@@ -1651,6 +1710,32 @@ __global__ __launch_bounds__(kBlock, 8) void rpack_kernel(DStore st, const DSmal
     const uint32_t s_src = len ? srcb[d.src_off + ((uint32_t)j < len ? (uint32_t)j : len - 1)] : kNoSlot;
     const DQuery rq = st.squery[d.slot];
     const int32_t rmin = st.minc[d.slot], rmax = st.maxc[d.slot];
+    // A square wave's entry j is row j's ticket: its alive flag, counts and
+    // prefetch-field values load now, from the row records, in the round of
+    // the row's query and source (checked against the source below)
+    uint32_t row_j = 0;
+    uint8_t al_j = 0, pk[2] = {0, 0};
+    int32_t smin_j = 0, smax_j = 0;
+    int64_t pv[2] = {0, 0};
+    if constexpr (S == 8) {
+        typedef const __attribute__((address_space(1))) uint8_t gu8;
+        typedef const __attribute__((address_space(1))) int64_t gi64;
+        row_j = (uint32_t)__shfl((int)d.slot, j * S);  // the slot of the row whose segment is j
+        al_j = st.alive[row_j];
+        smin_j = st.minc[row_j];
+        smax_j = st.maxc[row_j];
+        if (L.npf > 0) {
+            pk[0] = ((gu8*)L.pf_kind[0])[row_j];
+            pv[0] = ((gi64*)L.pf_val[0])[row_j];
+        }
+        if (L.npf > 1) {
+            pk[1] = ((gu8*)L.pf_kind[1])[row_j];
+            pv[1] = ((gi64*)L.pf_val[1])[row_j];
+        }
+    }
+    // the column table in this round too (its copy into LDS waits for its
+    // loads: issued first, it cost the kernel a round of its own)
+    load_field_table(st, ft);
     __syncthreads();  // ft
     bool m = false, live = false, rv = false;
     uint32_t s = kNoSlot;
@@ -1667,21 +1752,21 @@ __global__ __launch_bounds__(kBlock, 8) void rpack_kernel(DStore st, const DSmal
     if constexpr (S == 8) {
         const uint32_t off0 = __shfl(d.src_off, 0), len0 = __shfl(d.src_len, 0);
         const uint32_t s_sq = have && (uint32_t)j < len ? s_src : kNoSlot;
-        const uint32_t row_j = __shfl(d.slot, j * S);  // the slot of the row whose segment is j
         square = __ballot(have && d.src_off == off0 && d.src_len == len0 && len == (uint32_t)S && s_sq == row_j) == ~0ull;
     }
     uint64_t Ebits = 0;
-    if (square) {  // wave-uniform: the entry's columns, then the row query's clauses and their columns
+    if (square) {  // wave-uniform: entry j is row j (its loads above), then the row query's clauses
         s = s_src;
-        const uint8_t al = st.alive[s];
-        const int32_t smin = st.minc[s], smax = st.maxc[s];
+        const uint8_t al = al_j;
+        const int32_t smin = smin_j, smax = smax_j;
         live = al != 0;
         double sp = 0.0;
         // every row of the wave with at most 2 clauses (C5's bucket term and
         // skill range): the 2-clause batch (half the registers: 8 waves per
-        // SIMD instead of 5)
+        // SIMD instead of 5), its columns from the prefetched values
         const bool two = __ballot(rq.n_clauses > 2) == 0;
-        const bool e = batched && two ? eval_batched<2>(st, ft, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp)
+        const bool e = batched && two ? eval_batched_pf<2>(st, ft, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s,
+                                                           &sp, L.npf, L.pf, pk, pv)
                                       : eval_parsed(st, rq.kind, st.clauses + rq.clause_off, rq.n_clauses, s, &sp);
         Ebits = __ballot(e);  // bit a * 8 + b: member a's query matches member b's document
         m = live && e && smin >= rmin && smax <= rmax;

@@ -1430,8 +1430,21 @@ bool Core::assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t
 // down in one copy (the host `overlap` work runs meanwhile).
 PackLayout Core::run_packed(const PackBatch& pb, PassStats& stats, const std::function<void()>& overlap) {
     flush_apply();  // the previous batch's selections, before this batch's searches
-    const PackLayout L = pack_layout(pb.n, pb.S);
+    PackLayout L = pack_layout(pb.n, pb.S);
     const DStore st = dstore();
+    {  // the columns the square wave prefetches: every field a clause names, when at most 2
+        uint32_t k = 0;
+        bool ok = true;
+        for (size_t f = 0; f < field_used_.size() && ok; f++) {
+            if (!field_used_[f]) continue;
+            if (k == 2 || f >= d_fval_.size() || !d_fval_[f] || !d_fkind_[f]) { ok = false; break; }
+            L.pf[k] = (uint16_t)f;
+            L.pf_val[k] = d_fval_[f]->p;
+            L.pf_kind[k] = d_fkind_[f]->p;
+            k++;
+        }
+        L.npf = ok ? k : 0;
+    }
     d_srows_.reserve(std::max<size_t>(pb.n, 1), false);
     d_pack_.reserve(L.total, false);
     h_pack_.reserve(L.total);
