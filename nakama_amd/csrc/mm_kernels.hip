@@ -196,20 +196,47 @@ __device__ __forceinline__ bool eval_batched_pf(const DStore& st, const FieldTab
     if (n <= 0) { *sp = 1.0; return true; }
     double ms = 0.0, ss = 0.0;
     bool has_must = false, has_should = false, any_should = false, fail = false;
+    bool tset = false;
 #pragma unroll
-    for (int i = 0; i < NB; i++) {
-        if (i >= n) break;
-        bool h = false;
-        double sc = c[i].score;
-        if (c[i].op != OP_FALSE) {
-            if (c[i].op == OP_TERM) h = kind[i] == KIND_KEYWORD && val[i] == (int64_t)c[i].term;
-            else if (c[i].op == OP_RANGE) h = kind[i] == KIND_NUMERIC && val[i] >= c[i].lo && val[i] <= c[i].hi;
-            else if (c[i].op == OP_TERMSET) h = kind[i] == KIND_KEYWORD && termset_hit(st, c[i].term, val[i], &sc);
-            else h = (kind[i] == KIND_KEYWORD && val[i] == (int64_t)c[i].term) || (kind[i] == KIND_NUMERIC && val[i] == c[i].lo);
+    for (int i = 0; i < NB; i++) tset |= (i < n) & (c[i].op == OP_TERMSET);
+    if (__ballot(tset) == 0) {
+        // no regexp / wildcard / fuzzy clause in the wave: every clause's hit
+        // and contribution by selects, no branch per clause (a skipped
+        // addition is an addition of +0.0: the sums' bits are the loop's)
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            const bool act = i < n;
+            const bool kw = kind[i] == KIND_KEYWORD, nu = kind[i] == KIND_NUMERIC;
+            const bool eqt = val[i] == (int64_t)c[i].term;
+            const uint8_t op = c[i].op;
+            const bool h = act & (((op == OP_TERM) & kw & eqt) |
+                                  ((op == OP_RANGE) & nu & (val[i] >= c[i].lo) & (val[i] <= c[i].hi)) |
+                                  ((op == OP_NUMLIT) & ((kw & eqt) | (nu & (val[i] == c[i].lo)))));
+            const bool must = act & (c[i].occur == OCC_MUST), should = act & (c[i].occur == OCC_SHOULD);
+            const bool mnot = act & (c[i].occur == OCC_MUSTNOT);
+            has_must |= must;
+            has_should |= should;
+            ms += (must & h) ? c[i].score : 0.0;
+            ss += (should & h) ? c[i].score : 0.0;
+            any_should |= should & h;
+            fail |= (must & !h) | (mnot & h);
         }
-        if (c[i].occur == OCC_MUST) { has_must = true; if (h) ms += sc; else fail = true; }
-        else if (c[i].occur == OCC_SHOULD) { has_should = true; if (h) { ss += sc; any_should = true; } }
-        else if (h) fail = true;
+    } else {
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            if (i >= n) break;
+            bool h = false;
+            double sc = c[i].score;
+            if (c[i].op != OP_FALSE) {
+                if (c[i].op == OP_TERM) h = kind[i] == KIND_KEYWORD && val[i] == (int64_t)c[i].term;
+                else if (c[i].op == OP_RANGE) h = kind[i] == KIND_NUMERIC && val[i] >= c[i].lo && val[i] <= c[i].hi;
+                else if (c[i].op == OP_TERMSET) h = kind[i] == KIND_KEYWORD && termset_hit(st, c[i].term, val[i], &sc);
+                else h = (kind[i] == KIND_KEYWORD && val[i] == (int64_t)c[i].term) || (kind[i] == KIND_NUMERIC && val[i] == c[i].lo);
+            }
+            if (c[i].occur == OCC_MUST) { has_must = true; if (h) ms += sc; else fail = true; }
+            else if (c[i].occur == OCC_SHOULD) { has_should = true; if (h) { ss += sc; any_should = true; } }
+            else if (h) fail = true;
+        }
     }
     if (fail) return false;
     if (!has_must && !has_should) { *sp = 1.0; return true; }
@@ -1686,6 +1713,36 @@ __device__ __forceinline__ int64_t seg8_bcast64(int64_t v, int i) {
     const int lo = seg8_bcast((int)(uint32_t)v, i), hi = seg8_bcast((int)(uint32_t)((uint64_t)v >> 32), i);
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
+// OR of a 64-bit value over the lane's 8-lane segment (ds_swizzle xor 1, 2, 4)
+__device__ __forceinline__ uint64_t seg8_or64(uint64_t v) {
+    auto x = [](uint64_t w, int which) -> uint64_t {
+        const int lo = (int)(uint32_t)w, hi = (int)(uint32_t)(w >> 32);
+        int l2, h2;
+        if (which == 1) { l2 = __builtin_amdgcn_ds_swizzle(lo, 0x1F | (1 << 10)); h2 = __builtin_amdgcn_ds_swizzle(hi, 0x1F | (1 << 10)); }
+        else if (which == 2) { l2 = __builtin_amdgcn_ds_swizzle(lo, 0x1F | (2 << 10)); h2 = __builtin_amdgcn_ds_swizzle(hi, 0x1F | (2 << 10)); }
+        else { l2 = __builtin_amdgcn_ds_swizzle(lo, 0x1F | (4 << 10)); h2 = __builtin_amdgcn_ds_swizzle(hi, 0x1F | (4 << 10)); }
+        return ((uint64_t)(uint32_t)h2 << 32) | (uint32_t)l2;
+    };
+    v |= x(v, 1);
+    v |= x(v, 2);
+    v |= x(v, 4);
+    return v;
+}
+// bit i of b (8 bits) -> byte i of the result, 0x00 or 0xFF
+__device__ __forceinline__ uint64_t byte_mask8(uint32_t b) {
+    uint64_t x = b & 0xFFu;
+    x = (x | (x << 28)) & 0x0000000F0000000Full;
+    x = (x | (x << 14)) & 0x0003000300030003ull;
+    x = (x | (x << 7)) & 0x0101010101010101ull;
+    return x * 0xFFull;
+}
+// OR of the 8 bytes of x
+__device__ __forceinline__ uint32_t or_bytes(uint64_t x) {
+    x |= x >> 32;
+    x |= x >> 16;
+    x |= x >> 8;
+    return (uint32_t)(x & 0xFFu);
+}
 
 template <int S>
 __global__ __launch_bounds__(kBlock, 8) void rpack_kernel(DStore st, const DSmallRow* __restrict__ rows, uint32_t n_rows,
@@ -1794,17 +1851,39 @@ __global__ __launch_bounds__(kBlock, 8) void rpack_kernel(DStore st, const DSmal
     const uint64_t ball = __ballot(m);
     const uint64_t mine = S == 64 ? ball : (ball >> base) & ((1ull << (S & 63)) - 1);
     uint32_t rank = 0;
+    // the keys' low words all zero (C5's scores are small sums of boosts):
+    // the int64 order is the high words' signed order, one 32-bit exchange
+    // per entry instead of two (wave-uniform)
+    const bool k32 = S == 8 && __ballot(m && (uint32_t)key != 0u) == 0;
+    if (k32) {
+        const int32_t kh = (int32_t)((uint64_t)key >> 32);
 #pragma unroll
-    for (int i = 0; i < S; i++) {
-        const int64_t ki = S == 8 ? seg8_bcast64(key, i) : __shfl(key, base + i);
-        rank += (uint32_t)(((mine >> i) & 1) && (ki > key || (ki == key && i < j)));
+        for (int i = 0; i < S; i++) {
+            const int32_t ki = seg8_bcast(kh, i);
+            rank += (uint32_t)((mine >> i) & 1) & (uint32_t)((ki > kh) | ((ki == kh) & (i < j)));
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < S; i++) {
+            const int64_t ki = S == 8 ? seg8_bcast64(key, i) : __shfl(key, base + i);
+            rank += (uint32_t)(((mine >> i) & 1) && (ki > key || (ki == key && i < j)));
+        }
     }
     PmT pmask = 0;
     RvT rbits = 0;
-    if (square) {
+    if (S == 8 && square) {
+        // byte i of `ranked`: entry i's rank as a bit (0 when it did not
+        // match), from one OR over the segment; then, with E's bytes as
+        // masks, the reverse bits (entry i's reverse check E[i][seg]) and this
+        // entry's pair-matrix row (its query against entry i's document,
+        // E[j][i]) are ORs of the selected bytes — no per-entry loop
+        const uint64_t ranked = seg8_or64((uint64_t)(m ? (1u << rank) : 0u) << (8 * j));
+        rbits = (RvT)or_bytes(ranked & (((Ebits >> seg) & 0x0101010101010101ull) * 0xFFull));
+        if (m) pmask = (PmT)or_bytes(ranked & byte_mask8((uint32_t)(Ebits >> (8 * j))));
+    } else if (square) {
 #pragma unroll
         for (int i = 0; i < S; i++) {
-            const uint32_t ri = (uint32_t)(S == 8 ? seg8_bcast((int)rank, i) : __shfl((int)rank, base + i));
+            const uint32_t ri = (uint32_t)__shfl((int)rank, base + i);
             if (!((mine >> i) & 1)) continue;
             // entry i's reverse bit: rv of lane i = its match (mine bit i) and
             // E[i][seg] — from the ballot, no exchange
