@@ -425,6 +425,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1e3 * total_t / args.steps,
         "p50_ms": 1e3 * statistics.median(times),
+        "step_ms": [round(1e3 * t, 3) for t in times],  # every timed step (max over ranks), in order
         "presences_per_s": sum(presences_all) / total_t,
         # (row, candidate) predicate evaluations the device issued: one per
         # candidate scanned by a search (a shared search decides all its rows
@@ -567,6 +568,7 @@ def main_multi(args, world, rank, local, pg):
             "warmup": args.warmup,
             "ms_per_step": 1e3 * total_t / args.steps,
             "p50_ms": 1e3 * statistics.median(times),
+        "step_ms": [round(1e3 * t, 3) for t in times],  # every timed step (max over ranks), in order
             "presences_per_s": sum(presences_all) / total_t,
             "pair_evals_per_s": pair_evals / total_t,
             "pairs_decided_per_s": pairs_decided / total_t,

@@ -1854,8 +1854,18 @@ __global__ __launch_bounds__(kBlock, 8) void rpack_kernel(DStore st, const DSmal
     // the keys' low words all zero (C5's scores are small sums of boosts):
     // the int64 order is the high words' signed order, one 32-bit exchange
     // per entry instead of two (wave-uniform)
-    const bool k32 = S == 8 && __ballot(m && (uint32_t)key != 0u) == 0;
-    if (k32) {
+    // and, beyond that, the high words non-negative with their 3 low bits
+    // zero: key and entry index fold into one 32-bit word whose unsigned
+    // order is the ranking order (larger key first, then smaller index;
+    // unmatched lanes 0), so the rank is a count of larger words
+    const uint32_t khw = (uint32_t)((uint64_t)key >> 32);
+    const bool k32c = S == 8 && __ballot(m && (((uint32_t)key != 0u) | ((khw & 0x80000007u) != 0u))) == 0;
+    const bool k32 = S == 8 && !k32c && __ballot(m && (uint32_t)key != 0u) == 0;
+    if (k32c) {
+        const uint32_t cw = m ? ((khw | 0x80000000u) | (uint32_t)(7 - j)) : 0u;
+#pragma unroll
+        for (int i = 0; i < S; i++) rank += (uint32_t)((uint32_t)seg8_bcast((int)cw, i) > cw);
+    } else if (k32) {
         const int32_t kh = (int32_t)((uint64_t)key >> 32);
 #pragma unroll
         for (int i = 0; i < S; i++) {
