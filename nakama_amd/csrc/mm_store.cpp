@@ -231,26 +231,6 @@ std::vector<int> node_cpus(int prefer) {
     return out;
 }
 
-// One hardware thread per physical core of `cpus` (the lowest of each core's
-// SMT siblings that `cpus` holds).  Two walks on the SMT siblings of one core
-// run ~1.4x slower each: on the MI355X boxes (2 x EPYC 9575F, siblings c and
-// c + 128) C3's walks that shared a core took 2.2-2.8 ms against 1.6 ms for
-// walks alone on their cores; one worker per core: same-box C3 p50 3.55 /
-// 3.55 / 3.91 vs 3.81 / 4.00 / 3.95 ms with siblings allowed, interleaved
-// (profiles/r06/r06m_c3_walks.txt, r06n_smt_ab.txt).
-std::vector<int> one_per_core(const std::vector<int>& cpus) {
-    std::vector<int> out;
-    for (int c : cpus) {
-        const std::vector<int> sib =
-            parse_cpulist("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/topology/thread_siblings_list");
-        bool first = true;
-        for (int x : sib)
-            if (x < c && std::find(cpus.begin(), cpus.end(), x) != cpus.end()) first = false;
-        if (first) out.push_back(c);
-    }
-    return out;
-}
-
 // Host worker count: NKM_THREADS, else the visible cores capped at 16 (the
 // per-GPU host share on an 8-GPU node).  Same-box A/B runs on MI355X boxes
 // (profiles/r01_ab_threads.txt) put 8 and 16 workers within the boxes'
@@ -273,16 +253,6 @@ WorkPool& Core::workers() {
         // handle's sub-handles on that node, or the local ranks)
         if (!area.empty() && !std::getenv("NKM_THREADS") && !std::getenv("LOCAL_WORLD_SIZE"))
             n = std::max(1u, std::min(16u, (unsigned)area.size() / std::max(1u, host_share_)));
-        // each worker on a core of its own when the node (or, on a one-node
-        // host, the process's CPUs) has a physical core per worker
-        {
-            std::vector<int> base = area;
-            if (base.empty())
-                for (int c = 0; c < CPU_SETSIZE; c++)
-                    if (CPU_ISSET(c, &cs)) base.push_back(c);
-            std::vector<int> cores = one_per_core(base);
-            if (cores.size() >= n && cores.size() < base.size()) area.swap(cores);
-        }
         workers_.reset(new WorkPool(n, {}, area));
     }
     return *workers_;
