@@ -775,6 +775,7 @@ private:
     bool finish_fill_fast(const UVec<uint32_t>& expired, GroupList& groups, mm_matched* out, bool mutated);
     void choose_source(const Sig& s, DGroup& g, SrcChoice* ch = nullptr);
     void source_of(const Sig& s, DGroup& g, SrcChoice* ch = nullptr) const;
+    void source_of_key1(uint64_t key1, DGroup& g) const;
     struct ParPlan {  // a batch's pools (plan_parallel), bucketed while its searches run
         bool ok = false;
         size_t ng = 0;
@@ -1027,6 +1028,16 @@ public:
     HashIndex sig_idx_;  // signature identity (sig_hash) -> id, compared by sig_eq
     std::vector<Sig> sigs_;
     std::vector<uint64_t> sig_fmask_;  // per signature: its must_fmask (plan_pools reads 8 B, not the Sig)
+    // per signature, what a packed batch's assembly reads of it (16 B, not the
+    // 88-B Sig over two lines): the single MUST term's posting key and the
+    // roofline's field / clause counts
+    struct SigLite {
+        uint64_t key1;
+        uint16_t n_fields, n_clauses;
+        uint32_t pad;
+    };
+    static SigLite lite_of(const Sig& s) { return SigLite{s.must_key1, s.n_fields, s.n_clauses, 0}; }
+    std::vector<SigLite> sig_lite_;
     std::vector<DClause> clauses_;
     std::vector<DQuery> squery_;      // per slot
     std::vector<uint8_t> field_used_; // per field: referenced by some clause

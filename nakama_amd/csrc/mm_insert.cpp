@@ -255,6 +255,7 @@ void Core::commit_new_sigs(WorkPool& wp, size_t nt, const std::vector<int64_t>& 
     if (c0 + ncl > UINT32_MAX) throw std::length_error("clause table past 2^32 entries");
     sigs_.resize((size_t)id0 + nd);
     sig_fmask_.resize((size_t)id0 + nd);
+    sig_lite_.resize((size_t)id0 + nd);
     clauses_.resize(c0 + ncl);
     sig_idx_.reserve(sig_idx_.n + nd);
     const size_t nf = field_used_.size();
@@ -282,6 +283,7 @@ void Core::commit_new_sigs(WorkPool& wp, size_t nt, const std::vector<int64_t>& 
             for (auto& mt : g.must_terms) pst[mt.first] = 1;
             const uint32_t id = nid[k];
             sig_fmask_[id] = g.must_fmask;
+            sig_lite_[id] = lite_of(g);
             sigs_[id] = std::move(g);
             sig_idx_.put_new_concurrent(thash[j], id);
         }

@@ -1324,9 +1324,14 @@ bool Core::assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t
                 o.slot = kNoSlot;
                 continue;
             }
-            const Sig& sg = sigs_[sig_[r]];
+            // the signature's 16-B summary (ids follow first appearance, so
+            // the rows read it nearly in sequence), the Sig itself only for
+            // a search with several MUST terms
+            const uint32_t sgi = sig_[r];
+            const SigLite& sl = sig_lite_[sgi];
             DGroup d;
-            source_of(sg, d);
+            if (sl.key1 != UINT64_MAX) source_of_key1(sl.key1, d);
+            else source_of(sigs_[sgi], d);
             if (d.src_len > 64) {
                 bad[c] = 1;
                 return;
@@ -1337,7 +1342,7 @@ bool Core::assemble_packed(const std::vector<uint32_t>& rows, size_t pos, size_t
             sc += d.src_len;
             // per live candidate (search_bytes' rev form): Min/MaxCount, the
             // query's field columns, the hit's query descriptor and clauses
-            lw += (double)d.src_len * (double)(8 + 9 * sg.n_fields + 8 + 32 * sg.n_clauses);
+            lw += (double)d.src_len * (double)(8 + 9 * sl.n_fields + 8 + 32 * sl.n_clauses);
         }
         at[c + 1] = k;
         maxlen[c] = mx;

@@ -1055,12 +1055,18 @@ std::unique_ptr<ReplayCore> Core::make_replay(std::vector<uint8_t>& sel, bool re
 
 // choose_source without advancing the posting lists' dead-prefix heads (safe
 // on the host workers): the same list, possibly starting at dead entries.
+// source_of for a signature with one MUST term (its posting key: field << 32
+// | term): that term's posting list (C5's bucket)
+void Core::source_of_key1(uint64_t key1, DGroup& g) const {
+    const PostingRange* it = postings_map_.find(key1);
+    g.src_kind = 1;
+    g.src_off = it ? it->off + it->head : 0;
+    g.src_len = it ? it->len - it->head : 0;
+}
+
 void Core::source_of(const Sig& s, DGroup& g, SrcChoice* ch) const {
-    if (s.must_key1 != UINT64_MAX) {  // one MUST term: its posting list (C5's bucket)
-        const PostingRange* it = postings_map_.find(s.must_key1);
-        g.src_kind = 1;
-        g.src_off = it ? it->off + it->head : 0;
-        g.src_len = it ? it->len - it->head : 0;
+    if (s.must_key1 != UINT64_MAX) {  // one MUST term: its posting list
+        source_of_key1(s.must_key1, g);
         if (ch) {
             ch->has_term = true;
             ch->field = (uint16_t)(s.must_key1 >> 32);

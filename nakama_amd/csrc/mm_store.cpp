@@ -518,6 +518,7 @@ uint32_t Core::sig_commit(Sig&& s, const DClause* dc, size_t n, uint64_t hash, b
         if (!field_posting_[mt.first]) { field_posting_[mt.first] = 1; index_dirty_ = true; }
     const uint32_t id = (uint32_t)sigs_.size();
     sig_fmask_.push_back(s.must_fmask);
+    sig_lite_.push_back(lite_of(s));
     sigs_.push_back(std::move(s));
     sig_idx_.put_new(hash, id);
     if (materialize) materialize_fields();
@@ -1371,6 +1372,8 @@ void Core::compact() {
         sigs_.swap(ns);
         sig_fmask_.resize(sigs_.size());
         for (size_t g = 0; g < sigs_.size(); g++) sig_fmask_[g] = sigs_[g].must_fmask;
+        sig_lite_.resize(sigs_.size());
+        for (size_t g = 0; g < sigs_.size(); g++) sig_lite_[g] = lite_of(sigs_[g]);
         clauses_.swap(nc);
         sig_idx_.clear();
         sig_idx_.reserve(sigs_.size());
