@@ -965,6 +965,20 @@ public:
     // per-pass scratch, kept across passes (no page faults on the hot path)
     std::vector<uint8_t> sel_;
     std::vector<uint32_t> rows_, list_tmp_;
+    // The first batch's signature counts, taken by the pass prologue while it
+    // copies the rows (nothing is selected or decided yet): per chunk of the
+    // workers' split, the signatures in first-appearance order, their counts,
+    // the rows and whether every row carries its own search's terms.
+    // assemble_parallel uses them instead of its count sweep when its batch
+    // is those rows in that split (valid: for this pass's rows).
+    struct PreCount {
+        bool valid = false;
+        size_t n_rows = 0;
+        std::vector<std::vector<uint32_t>> first, cnt;
+        std::vector<size_t> n;
+        std::vector<uint8_t> self;
+    };
+    PreCount precount_;
     UVec<uint32_t> brow_, brow_group_;  // the batch's rows and their searches (filled in full)
     UVec<uint32_t> newly_;  // slots selected by the batch (filled in full by the merges)
     GroupList pass_groups_;

@@ -1147,14 +1147,50 @@ int Core::process_default(GroupList& out_groups,
                    (double)cfg_.interval_sec * (double)cfg_.rev_threshold);
     const int maxI = cfg_.max_intervals;
     std::vector<uint32_t>& rows = rows_;
+    precount_.valid = false;
     if (active_exact_ && big_list(active_list_)) {  // every entry is a row: one parallel copy
         rows.resize(active_list_.size());
         WorkPool& wp = workers();
-        const size_t n = active_list_.size(), nch = wp.size();
+        const size_t n = active_list_.size(), nch = wp.size(), nsig = sigs_.size();
+        // with few signatures (assemble_parallel's own limit), the copy also
+        // counts them per chunk: the first batch's count sweep (C3: 1M rows)
+        const bool pre = par_mode_ && !cfg_.rev_precision && nsig <= 65536;
+        PreCount& pc = precount_;
+        if (pre) {
+            pc.first.resize(nch);
+            pc.cnt.resize(nch);
+            pc.n.assign(nch, 0);
+            pc.self.assign(nch, 1);
+        }
         wp.run(nch, [&](size_t c) {
             const size_t lo = n * c / nch, hi = n * (c + 1) / nch;
-            std::memcpy(rows.data() + lo, active_list_.data() + lo, (hi - lo) * sizeof(uint32_t));
+            if (!pre) {
+                std::memcpy(rows.data() + lo, active_list_.data() + lo, (hi - lo) * sizeof(uint32_t));
+                return;
+            }
+            std::vector<uint32_t> first, cnt(nsig, 0);  // thread-private until the end (shared lines)
+            const uint32_t* const A = active_list_.data();
+            uint32_t* const W = rows.data();
+            const uint32_t* const SG = sig_.data();
+            const uint8_t* const SM = self_match_.data();
+            const uint8_t* const IX = indexed_.data();
+            uint8_t self = 1;
+            for (size_t i = lo; i < hi; i++) {
+                const uint32_t r = A[i];
+                W[i] = r;
+                const uint32_t sg = SG[r];
+                if (!cnt[sg]++) first.push_back(sg);
+                self &= (uint8_t)(SM[r] & IX[r]);
+            }
+            pc.first[c] = std::move(first);
+            pc.cnt[c] = std::move(cnt);
+            pc.n[c] = hi - lo;
+            pc.self[c] = self;
         });
+        if (pre) {
+            pc.valid = true;
+            pc.n_rows = n;
+        }
     } else {
         filter_slots(big_list(active_list_) ? &workers() : nullptr, active_list_, rows,
                      [&](uint32_t s) { return live_[s] && is_active_[s]; });
@@ -1345,6 +1381,20 @@ int Core::process_default(GroupList& out_groups,
             std::vector<Chunk> ch(nch);
             const auto ts0 = std::chrono::steady_clock::now();
             std::vector<double> cnt_task_us(nch, 0.0), cnt_start_us(nch, 0.0);  // NKM_PROFILE=2
+            // the prologue counted these rows in this split already (the
+            // pass's first batch, nothing selected or decided: every row counts)
+            PreCount& pc = precount_;
+            const bool pre = pc.valid && pos == 0 && nr == rows.size() && pc.n_rows == nr && pc.n.size() == nch &&
+                             retry_slot == kNoSlot;
+            pc.valid = false;
+            if (pre) {
+                for (unsigned c = 0; c < nch; c++) {
+                    ch[c].first = std::move(pc.first[c]);
+                    ch[c].cnt = std::move(pc.cnt[c]);
+                    ch[c].n = pc.n[c];
+                    ch[c].self = pc.self[c] != 0;
+                }
+            } else
             wp.run(nch, [&](size_t c) {
                 const auto tc0 = std::chrono::steady_clock::now();
                 // thread-private until the end (adjacent Chunks share cache
