@@ -75,7 +75,14 @@ def _fuzz_corpus(n=3000, seed=7):
 
 def test_compile_status_matches_oracle(product):
     orc = harness.oracle_lib()
+    # numbers the parser's integer fast path takes (<= 15 digits after a
+    # sign) and the forms next to it that go through the general parse
+    nums = ["0", "00", "007", "-0", "+0", "-7", "+7", "123456789012345", "1234567890123456", "99999999999999999999",
+            "1_000", "0x10", "0x1p3", "1e3", "1.", ".5", "-", "+", "--1", "1-", "12a", "٣"]
     cases = [q for q, _ in harness.load_known_answer()["query_cases"]] + _fuzz_corpus()
+    for x in nums:
+        cases += [x, "properties.skill:" + x, "properties.skill:>=" + x, "properties.skill:<" + x + "^2",
+                  "+properties.a:" + x + " properties.b:>" + x]
     bad = []
     for q in cases:
         b = q.encode("utf-8", "surrogateescape")
