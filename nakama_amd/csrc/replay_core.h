@@ -747,7 +747,7 @@ struct DenseRun {
     uint32_t avail = 0;  // positions known gathered (pipelined gather, DensePool::front)
 
     // position i (< P.n) gathered before its copies are read
-    void need(const DensePool& P, uint32_t i) {
+    __attribute__((always_inline)) void need(const DensePool& P, uint32_t i) {
         if (i >= avail) avail = P.wait_pos(i);
     }
     // row j's ticket T and its position kT.  An identity pool's row j is
@@ -755,7 +755,7 @@ struct DenseRun {
     // replay_parallel): T is the gathered copy's slot, read in sequence
     // instead of through the batch rows (a cache miss per row when the pools
     // interleave: C4's 64).  Else the gather's slot -> position map.
-    void row_at(const DensePool& P, const uint32_t* pos_of, uint32_t j, uint32_t& T, uint32_t& kT) {
+    __attribute__((always_inline)) void row_at(const DensePool& P, const uint32_t* pos_of, uint32_t j, uint32_t& T, uint32_t& kT) {
         if (P.identity) {
             need(P, j);
             T = P.slot[j];
@@ -966,6 +966,21 @@ struct DenseRun {
             if (i >= av) av = P.wait_pos(i);
         };
         uint32_t h0 = head;
+        // the selected run after the head (the last group's members, ~6 on
+        // C3) skipped 8 bytes a time: the first unselected byte of a word is
+        // its lowest zero (selection bytes are 0 / 1), so the scan ends
+        // without a data-dependent branch per byte
+        while (h0 + 8 <= n) {
+            uint64_t w;
+            std::memcpy(&w, S + h0, 8);
+            const uint64_t z = ~w & 0x0101010101010101ull;  // bit 8k: byte k is 0
+            NKM_WS(0);
+            if (z) {
+                h0 += (uint32_t)(__builtin_ctzll(z) >> 3);
+                break;
+            }
+            h0 += 8;
+        }
         while (h0 < n && S[h0]) { h0++; NKM_WS(0); }
         head = h0;
         int32_t* const csize = fcb.size;
