@@ -35,13 +35,31 @@ namespace nkm {
 
 #define NKM_INLINE inline __attribute__((always_inline))
 
+// Lane masks of a 16-entry block: kLaneBelow.m[l] has lanes j < l all ones,
+// kLaneFrom.m[h] lanes j >= h (OR-ed into a block, they read as kInf).
+struct alignas(64) LaneMasks {
+    uint32_t m[17][16];
+};
+constexpr LaneMasks make_lane_masks(bool below) {
+    LaneMasks t{};
+    for (int i = 0; i <= 16; i++)
+        for (int j = 0; j < 16; j++) t.m[i][j] = (below ? j < i : j >= i) ? 0xFFFFFFFFu : 0u;
+    return t;
+}
+inline constexpr LaneMasks kLaneBelow = make_lane_masks(true), kLaneFrom = make_lane_masks(false);
+
 // Min over leaf intervals with point updates: fan-out 16 levels (a query
 // touches at most two partial blocks per level; 25k leaves are 4 levels).
+// (gcc's -Wpsabi note on the 64-B vector returns: they are always inlined)
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Wpsabi"
 struct MinTree16 {
     static constexpr uint32_t kInf = 0xFFFFFFFFu;
-    std::vector<std::vector<uint32_t>> lv;  // lv[0]: leaves; lv[k][i] = min of lv[k-1][16i, 16i + 16)
-    // the levels' arrays, cached after build (range_min / set read them per
-    // level: one load instead of the vector-of-vectors' two)
+    // level k's storage (16 spare entries: lp[k] is its first 64-B boundary,
+    // so a 16-entry block is exactly one cache line, not two)
+    std::vector<std::vector<uint32_t>> lv;
+    // lp[0]: leaves; lp[k][i] = min of lp[k-1][16i, 16i + 16) (range_min / set
+    // read them per level: one load instead of the vector-of-vectors' two)
     uint32_t* lp[8] = {};
     uint32_t nlev = 0;
     void build(const uint32_t* v, uint32_t n) {
@@ -49,64 +67,74 @@ struct MinTree16 {
         for (uint32_t m = n; m > 16; m = (m + 15) / 16) L++;
         lv.resize(L);
         uint32_t m = n;
-        lv[0].resize(((size_t)m + 15) & ~(size_t)15);
-        std::memcpy(lv[0].data(), v, (size_t)n * 4);
-        std::fill(lv[0].begin() + n, lv[0].end(), kInf);
+        for (size_t k = 0; k < L; k++, m = (m + 15) / 16) {
+            const size_t len = ((size_t)m + 15) & ~(size_t)15;
+            lv[k].resize(len + 16);
+            lp[k] = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(lv[k].data()) + 63) & ~(uintptr_t)63);
+            std::fill(lp[k], lp[k] + len, kInf);
+        }
+        std::memcpy(lp[0], v, (size_t)n * 4);
+        m = n;
         for (size_t k = 1; k < L; k++) {
-            const uint32_t pm = m;
             m = (m + 15) / 16;
-            lv[k].resize(((size_t)m + 15) & ~(size_t)15);
-            std::fill(lv[k].begin(), lv[k].end(), kInf);
-            const uint32_t* c = lv[k - 1].data();
-            for (uint32_t i = 0; i < m; i++) {
-                uint32_t x = kInf;
-                for (uint32_t j = 16 * i; j < 16 * i + 16 && j < ((pm + 15) & ~15u); j++) x = std::min(x, c[j]);
-                lv[k][i] = x;
-            }
+            const uint32_t* c = lp[k - 1];
+            for (uint32_t i = 0; i < m; i++) lp[k][i] = min16(c + 16 * (size_t)i);  // padding is kInf
         }
         nlev = (uint32_t)L;
-        for (size_t k = 0; k < L; k++) lp[k] = lv[k].data();
     }
-    // fixed 16-wide loops: vector mins (4 x 128 bits, or 2 x 256 bits in the
-    // walk's AVX2 instantiation, RangeRun::walk)
-    static NKM_INLINE uint32_t min16(const uint32_t* p) {
-        uint32_t x = kInf;
-        for (int j = 0; j < 16; j++) x = p[j] < x ? p[j] : x;
-        return x;
-    }
-    // min of blk[lo, hi) for a 16-aligned block
-    static NKM_INLINE uint32_t min16_in(const uint32_t* blk, uint32_t lo, uint32_t hi) {
-        uint32_t x = kInf;
-        for (uint32_t j = 0; j < 16; j++) {
-            const uint32_t y = (j >= lo && j < hi) ? blk[j] : kInf;
-            x = y < x ? y : x;
-        }
-        return x;
-    }
+    // 16-lane vector mins (4 x 128 bits, or 2 x 256 bits in the walk's AVX2
+    // instantiation, RangeRun::walk)
+    static NKM_INLINE uint32_t min16(const uint32_t* p) { return reduce(load16(p)); }
     // min over leaves [a, b)
     NKM_INLINE uint32_t range_min(uint32_t a, uint32_t b) const {
-        uint32_t m = kInf;
+        V16 acc = V16{} - 1u;
+        range_min_acc(a, b, acc);
+        return reduce(acc);
+    }
+    // Lane-wise min over leaves [a, b) into acc, without a horizontal reduce
+    // per block: per level, the blocks holding a and b - 1 with the lanes
+    // outside [a, b) OR-ed to all ones (= kInf, so they never win); the
+    // blocks strictly between are the next level's elements.
+    // (GNU vector extensions: clang and gcc; unsigned lane compares -> pminud)
+    using V16 = uint32_t __attribute__((vector_size(64)));
+    using V8 = uint32_t __attribute__((vector_size(32)));
+    using V4 = uint32_t __attribute__((vector_size(16)));
+    static NKM_INLINE V16 load16(const uint32_t* p) {
+        V16 x;
+        std::memcpy(&x, p, 64);
+        return x;
+    }
+    static NKM_INLINE uint32_t reduce(const V16& x) {
+        V8 h0, h1;
+        std::memcpy(&h0, &x, 32);
+        std::memcpy(&h1, reinterpret_cast<const char*>(&x) + 32, 32);
+        h0 = h1 < h0 ? h1 : h0;
+        V4 q0, q1;
+        std::memcpy(&q0, &h0, 16);
+        std::memcpy(&q1, reinterpret_cast<const char*>(&h0) + 16, 16);
+        q0 = q1 < q0 ? q1 : q0;
+        const uint32_t a = q0[0] < q0[1] ? q0[0] : q0[1], b = q0[2] < q0[3] ? q0[2] : q0[3];
+        return a < b ? a : b;
+    }
+    NKM_INLINE void range_min_acc(uint32_t a, uint32_t b, V16& acc) const {
         for (size_t k = 0; a < b; k++) {
             const uint32_t* v = lp[k];
-            if ((a >> 4) == ((b - 1) >> 4)) {
-                const uint32_t x = min16_in(v + (a & ~15u), a & 15, ((b - 1) & 15) + 1);
-                return x < m ? x : m;
+            const uint32_t ab = a >> 4, bb = (b - 1) >> 4;
+            if (ab == bb) {
+                const V16 x = load16(v + 16 * (size_t)ab) | load16(kBelow[a & 15]) | load16(kFrom[((b - 1) & 15) + 1]);
+                acc = x < acc ? x : acc;
+                return;
             }
-            if (a & 15) {
-                const uint32_t x = min16_in(v + (a & ~15u), a & 15, 16);
-                m = x < m ? x : m;
-                a = (a | 15) + 1;
-            }
-            if (b & 15) {
-                const uint32_t x = min16_in(v + (b & ~15u), 0, b & 15);
-                m = x < m ? x : m;
-                b &= ~15u;
-            }
-            a >>= 4;
-            b >>= 4;
+            const V16 x = load16(v + 16 * (size_t)ab) | load16(kBelow[a & 15]);
+            const V16 y = load16(v + 16 * (size_t)bb) | load16(kFrom[((b - 1) & 15) + 1]);
+            const V16 m = x < y ? x : y;
+            acc = m < acc ? m : acc;
+            a = ab + 1;
+            b = bb;
         }
-        return m;
     }
+    static constexpr const uint32_t (*kBelow)[16] = kLaneBelow.m;
+    static constexpr const uint32_t (*kFrom)[16] = kLaneFrom.m;
     NKM_INLINE void set(uint32_t i, uint32_t x) {
         lp[0][i] = x;
         for (uint32_t k = 1; k < nlev; k++) {
@@ -229,8 +257,9 @@ struct RangeRun {
     NKM_INLINE bool next(uint32_t& leaf) {
         while (cur < end) {
             const uint32_t te = rg[cur].tend;
-            uint32_t m = MinTree16::kInf;
-            for (uint32_t k = cur; k < te; k++) m = std::min(m, S->tree.range_min(rg[k].a, rg[k].b));
+            MinTree16::V16 acc = MinTree16::V16{} - 1u;
+            for (uint32_t k = cur; k < te; k++) S->tree.range_min_acc(rg[k].a, rg[k].b, acc);
+            const uint32_t m = MinTree16::reduce(acc);
             if (m != MinTree16::kInf) {
                 leaf = S->leaf_of[m];
                 return true;
@@ -521,5 +550,6 @@ struct RangeRun {
         o.recs.push_back(PoolRec{UINT32_MAX, 0, 0, (uint32_t)o.ents.size(), 0, gcum, xcum});  // sentinel
     }
 };
+#pragma GCC diagnostic pop
 
 }  // namespace nkm

@@ -23,6 +23,7 @@
 
 #include "../nakama_amd/csrc/range_walk.h"
 #include "../nakama_amd/csrc/replay_core.h"
+#include "perf_group.h"
 
 using namespace nkm;
 
@@ -221,6 +222,38 @@ int main(int argc, char** argv) {
              },
              out);
     const double w2 = now_ms();
+    // RB_PERF=1: the walk again (fresh tree), RB_REPS times, under the PMU
+    if (std::getenv("RB_PERF")) {
+        const int reps = std::getenv("RB_REPS") ? std::atoi(std::getenv("RB_REPS")) : 5;
+        PerfGroup pg;
+        double best = 1e30;
+        uint64_t rows = 0, hits = 0;
+        for (int r = 0; r < reps; r++) {
+            src.tree.build(lrank.data(), nv);
+            PoolOut o2;
+            run.hits_seen = 0;
+            const double a0 = now_ms();
+            pg.start();
+            run.walk(src, bis.data(), N, brow.data(),
+                     [&](uint32_t bi, const RRange*& base, uint32_t& a, uint32_t& b) {
+                         base = tiers.data();
+                         a = t0[brow[bi]];
+                         b = t1[brow[bi]];
+                     },
+                     o2);
+            pg.stop();
+            best = std::min(best, now_ms() - a0);
+            rows += o2.recs.size() - 1;  // processed rows (the last record is the sentinel)
+            hits += run.hits_seen;
+        }
+        if (pg.ok() && rows)
+            std::printf("[perf] range walk, %d reps: per processed row %.0f cycles, %.0f instructions (IPC %.2f), %.2f "
+                        "branch misses, %.2f L1D read misses; hits examined %.2f; best walk %.3f ms\n",
+                        reps, (double)pg.v[0] / rows, (double)pg.v[1] / rows, (double)pg.v[1] / pg.v[0],
+                        (double)pg.v[2] / rows, (double)pg.v[3] / rows, (double)hits / rows, best);
+        else
+            std::printf("[perf] no PMU here; best walk %.3f ms over %d reps\n", best, reps);
+    }
     // ---- compare ----
     auto digest = [](const PoolOut& o) {
         uint64_t h = 1469598103934665603ull;
