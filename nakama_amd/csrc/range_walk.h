@@ -244,6 +244,7 @@ struct RangeRun {
     uint64_t hits_seen = 0;
     bool fast = true;  // fast_row() for the rows it covers (NKM_FAST=0: row() only)
     FastCombos fcb;
+    uint32_t mleaf[kFastComb][kFastMem];  // fast_row: the members' leaves (fcb.mem's slots)
 
     // iterator over one row's hits: tier by tier, smallest rank first;
     // every hit read is masked until the row ends
@@ -328,6 +329,7 @@ struct RangeRun {
                 return ReplayCore::BAIL;
             }
             fcb.size[f] += hc;
+            mleaf[f][fcb.nmem[f]] = leaf;
             fcb.mem[f][fcb.nmem[f]++] = H;
             const int l = fcb.size[f] + tcount;
             bool form = l == tmax;  // :233
@@ -342,18 +344,17 @@ struct RangeRun {
             }
             if (!form) continue;
             if (!multiple_of(l, tcm)) return ReplayCore::BAIL;
-            bool failed = false;  // :287-296
+            bool failed = false;  // :287-296 (the members' HotRecs: this pool's leaf copies)
             for (uint32_t k = 0; k < fcb.nmem[f] && !failed; k++) {
-                const uint32_t m = fcb.mem[f][k];
-                if (!v.live[m]) continue;
-                const HotRec& hs = v.hot[m];
+                if (!v.live[fcb.mem[f][k]]) continue;
+                const HotRec& hs = S->lhot[mleaf[f][k]];
                 failed = hs.minc > l || hs.maxc < l || !multiple_of(l, hs.cm);
             }
             if (failed) continue;
             grp.clear();
             for (uint32_t k = 0; k < fcb.nmem[f]; k++) {
                 const uint32_t m = fcb.mem[f][k];
-                for (int e = 0; e < v.hot[m].count; e++) grp.push_back({m, e});
+                for (int e = 0, c = S->lhot[mleaf[f][k]].count; e < c; e++) grp.push_back({m, e});
             }
             for (int e = 0; e < tcount; e++) grp.push_back({T, e});
             return ReplayCore::MATCHED;
@@ -515,8 +516,9 @@ struct RangeRun {
         for (uint32_t j = 0; j < nrows; j++) {
             const uint32_t bi = bis[j];
             const uint32_t T = brow[bi];
-            if (j + 2 < nrows) {  // the next rows' records (their hits are unknown until searched)
-                const uint32_t T2 = brow[bis[j + 2]];
+            if (j + 6 < nrows) {  // the next rows' records (their hits are unknown until searched;
+                                  // about half the rows are skipped as selected, so 6 rows are ~3 walked)
+                const uint32_t T2 = brow[bis[j + 6]];
                 __builtin_prefetch(&v.hot[T2]);
                 __builtin_prefetch(&psel[T2]);
                 __builtin_prefetch(&v.intervals[T2]);
