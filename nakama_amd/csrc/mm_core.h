@@ -95,6 +95,8 @@ hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max
                        uint32_t* d_pos[2], const DRangeBound* d_q, uint32_t nq, uint32_t* d_bounds, int* which,
                        hipStream_t stream, hipEvent_t ev_tile0, hipEvent_t ev_tile1, const hipEvent_t* ev_merge,
                        int max_merge, int* n_merge);
+hipError_t launch_rsrc_bounds(const DRangePool* d_pools, const int64_t* d_key, const DRangeBound* d_q, uint32_t nq,
+                              uint32_t* d_bounds, hipStream_t stream);
 
 struct DeviceError {
     hipError_t err;
@@ -902,8 +904,10 @@ private:
     // thread-local flags before it uses them again.
     void reset_pass_scratch();
     std::vector<RRange> rs_tiers_;      // the batch's signatures' tier lists
-    DevArray<uint8_t> d_rblob_;         // pools, tiles, block -> pool, bound queries
+    DevArray<uint8_t> d_rblob_;         // pools, tiles, block -> pool
     PinnedArray<uint8_t> h_rblob_;
+    DevArray<uint8_t> d_rq_;            // the bound queries (DRangeBound), uploaded after the sort is issued
+    PinnedArray<uint8_t> h_rq_;
     DevArray<int64_t> d_rkey_[2];
     DevArray<uint32_t> d_rpos_[2], d_rbound_;
     PinnedArray<uint32_t> h_rpos_, h_rbound_;

@@ -2338,6 +2338,17 @@ hipError_t launch_rsrc(const DStore& st, const DRangePool* d_pools, uint32_t max
     return hipGetLastError();
 }
 
+// The bound queries alone, over keys a launch_rsrc (nq = 0) already sorted on
+// this stream (mm_range.cpp issues the sort before the batch's signatures
+// are known and the queries once they are).
+hipError_t launch_rsrc_bounds(const DRangePool* d_pools, const int64_t* d_key, const DRangeBound* d_q, uint32_t nq,
+                              uint32_t* d_bounds, hipStream_t stream) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(rsrc_bounds_kernel, dim3((nq + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, d_pools, d_key, d_q,
+                       nq, d_bounds);
+    return hipGetLastError();
+}
+
 int var_k_capacity() { return kVarK; }
 int scan_chunk_len() { return kScanChunk; }
 

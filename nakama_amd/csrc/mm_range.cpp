@@ -123,6 +123,62 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
         if (b) return false;
     // From here on the batch is taken: nothing below declines.
     const auto tp_pools = clk::now();
+    // ---- device, first: pools (posting ranges), tiles, block -> pool, and
+    // the sort, which runs while the host claims the batch's signatures
+    // below; the bound queries follow once those are known ----
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    uint64_t n_elems = 0, src_total = 0;
+    uint32_t max_pad = 0, n_tiles = 0;
+    for (size_t p = 0; p < ng; p++) {
+        RangePoolHost& H = rs_pools_[p];
+        DRangePool& d = H.d;
+        d = DRangePool{};
+        if (PostingRange* it = postings_map_.find(((uint64_t)kf << 32) | H.term)) {
+            PostingRange& pr = *it;
+            while (pr.head < pr.len && !live_[postings_[pr.off + pr.head]]) pr.head++;  // the dead prefix
+            d.src_off = pr.off + pr.head;
+            d.src_len = pr.len - pr.head;
+        }
+        d.out_off = (uint32_t)n_elems;
+        d.pad_len = (uint32_t)al(d.src_len);
+        d.field = H.field;
+        n_elems += d.pad_len;
+        src_total += d.src_len;
+        max_pad = std::max(max_pad, d.pad_len);
+        n_tiles += (d.pad_len + kRsrcTile - 1) / kRsrcTile;
+    }
+    if (n_elems >= (1ull << 31)) throw std::runtime_error("range batch: more than 2^31 candidates");
+    const size_t o_tiles = al(ng * sizeof(DRangePool)), o_blk = o_tiles + al((size_t)n_tiles * sizeof(DRangeTile)),
+                 blob = o_blk + al((size_t)(n_elems / 256) * 4);
+    h_rblob_.reserve(blob);
+    d_rblob_.reserve(blob, false);
+    DRangePool* hp = reinterpret_cast<DRangePool*>(h_rblob_.p);
+    DRangeTile* ht = reinterpret_cast<DRangeTile*>(h_rblob_.p + o_tiles);
+    uint32_t* hb = reinterpret_cast<uint32_t*>(h_rblob_.p + o_blk);
+    for (size_t p = 0, t = 0; p < ng; p++) {
+        const DRangePool& d = rs_pools_[p].d;
+        hp[p] = d;
+        for (uint32_t s0 = 0; s0 < d.pad_len; s0 += kRsrcTile)
+            ht[t++] = DRangeTile{(uint32_t)p, s0, std::min(kRsrcTile, d.pad_len - s0), 0};
+        for (uint32_t b = 0; b < d.pad_len / 256; b++) hb[d.out_off / 256 + b] = (uint32_t)p;
+    }
+    flush_apply();  // earlier batches' selections, before the candidates are read
+    for (auto& a : d_rkey_) a.reserve(std::max<uint64_t>(n_elems, 1), false);
+    for (auto& a : d_rpos_) a.reserve(std::max<uint64_t>(n_elems, 1), false);
+    h_rpos_.reserve(std::max<uint64_t>(n_elems, 1));
+    if (!rs_ev_[0])
+        for (auto& e : rs_ev_) NKM_HIP(hipEventCreate(&e));
+    NKM_HIP(hipMemcpyAsync(d_rblob_.p, h_rblob_.p, blob, hipMemcpyHostToDevice, stream_));
+    int which = 0, n_merge = 0;
+    int64_t* dk[2] = {d_rkey_[0].p, d_rkey_[1].p};
+    uint32_t* dp[2] = {d_rpos_[0].p, d_rpos_[1].p};
+    const uint8_t* db = d_rblob_.p;
+    const DRangePool* d_pools = reinterpret_cast<const DRangePool*>(db);
+    NKM_HIP(launch_rsrc(dstore(), d_pools, max_pad, reinterpret_cast<const DRangeTile*>(db + o_tiles), n_tiles,
+                        reinterpret_cast<const uint32_t*>(db + o_blk), (uint32_t)n_elems, dk, dp, nullptr, 0, nullptr,
+                        &which, stream_, rs_ev_[0], rs_ev_[1], rs_ev_ + 2, kRsrcMaxMerge, &n_merge));
+    if (n_elems) NKM_HIP(hipMemcpyAsync(h_rpos_.p, d_rpos_[which].p, n_elems * 4, hipMemcpyDeviceToHost, stream_));
+    const auto tp_sort = clk::now();
     // ---- the batch's signatures (each claimed once, by an atomic flag) ----
     const size_t nsig = sigs_.size();
     if (rs_mark_cap_ < nsig) {
@@ -159,44 +215,13 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     for (size_t k = 0; k < ns; k++) ls_q[k + 1] += ls_q[k];
     const uint32_t nq = ls_q[ns];
     const auto tp_sigs = clk::now();
-    // ---- device: pools (posting ranges), tiles, block -> pool, bound queries ----
-    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    uint64_t n_elems = 0, src_total = 0;
-    uint32_t max_pad = 0, n_tiles = 0;
-    for (size_t p = 0; p < ng; p++) {
-        RangePoolHost& H = rs_pools_[p];
-        DRangePool& d = H.d;
-        d = DRangePool{};
-        if (PostingRange* it = postings_map_.find(((uint64_t)kf << 32) | H.term)) {
-            PostingRange& pr = *it;
-            while (pr.head < pr.len && !live_[postings_[pr.off + pr.head]]) pr.head++;  // the dead prefix
-            d.src_off = pr.off + pr.head;
-            d.src_len = pr.len - pr.head;
-        }
-        d.out_off = (uint32_t)n_elems;
-        d.pad_len = (uint32_t)al(d.src_len);
-        d.field = H.field;
-        n_elems += d.pad_len;
-        src_total += d.src_len;
-        max_pad = std::max(max_pad, d.pad_len);
-        n_tiles += (d.pad_len + kRsrcTile - 1) / kRsrcTile;
-    }
-    if (n_elems >= (1ull << 31)) throw std::runtime_error("range batch: more than 2^31 candidates");
-    const size_t o_tiles = al(ng * sizeof(DRangePool)), o_blk = o_tiles + al((size_t)n_tiles * sizeof(DRangeTile)),
-                 o_q = o_blk + al((size_t)(n_elems / 256) * 4), blob = o_q + (size_t)nq * sizeof(DRangeBound);
-    h_rblob_.reserve(blob);
-    d_rblob_.reserve(blob, false);
-    DRangePool* hp = reinterpret_cast<DRangePool*>(h_rblob_.p);
-    DRangeTile* ht = reinterpret_cast<DRangeTile*>(h_rblob_.p + o_tiles);
-    uint32_t* hb = reinterpret_cast<uint32_t*>(h_rblob_.p + o_blk);
-    DRangeBound* hq = reinterpret_cast<DRangeBound*>(h_rblob_.p + o_q);
-    for (size_t p = 0, t = 0; p < ng; p++) {
-        const DRangePool& d = rs_pools_[p].d;
-        hp[p] = d;
-        for (uint32_t s0 = 0; s0 < d.pad_len; s0 += kRsrcTile)
-            ht[t++] = DRangeTile{(uint32_t)p, s0, std::min(kRsrcTile, d.pad_len - s0), 0};
-        for (uint32_t b = 0; b < d.pad_len / 256; b++) hb[d.out_off / 256 + b] = (uint32_t)p;
-    }
+    // ---- device, then: the bound queries over the sorted keys ----
+    const size_t qbytes = std::max<size_t>((size_t)nq * sizeof(DRangeBound), sizeof(DRangeBound));
+    h_rq_.reserve(qbytes);
+    d_rq_.reserve(qbytes, false);
+    d_rbound_.reserve(std::max<uint32_t>(nq, 1), false);
+    h_rbound_.reserve(std::max<uint32_t>(nq, 1));
+    DRangeBound* hq = reinterpret_cast<DRangeBound*>(h_rq_.p);
     const size_t qch = ns >= 4096 ? nch : 1;
     sweep(qch, [&](size_t c) {
         for (size_t k = ns * c / qch; k < ns * (c + 1) / qch; k++) {
@@ -210,27 +235,15 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             }
         }
     });
-    flush_apply();  // earlier batches' selections, before the candidates are read
-    for (auto& a : d_rkey_) a.reserve(std::max<uint64_t>(n_elems, 1), false);
-    for (auto& a : d_rpos_) a.reserve(std::max<uint64_t>(n_elems, 1), false);
-    d_rbound_.reserve(std::max<uint32_t>(nq, 1), false);
-    h_rpos_.reserve(std::max<uint64_t>(n_elems, 1));
-    h_rbound_.reserve(std::max<uint32_t>(nq, 1));
-    if (!rs_ev_[0])
-        for (auto& e : rs_ev_) NKM_HIP(hipEventCreate(&e));
     const auto t1 = clk::now();
-    NKM_HIP(hipMemcpyAsync(d_rblob_.p, h_rblob_.p, blob, hipMemcpyHostToDevice, stream_));
-    int which = 0, n_merge = 0;
-    int64_t* dk[2] = {d_rkey_[0].p, d_rkey_[1].p};
-    uint32_t* dp[2] = {d_rpos_[0].p, d_rpos_[1].p};
-    const uint8_t* db = d_rblob_.p;
-    NKM_HIP(launch_rsrc(dstore(), reinterpret_cast<const DRangePool*>(db), max_pad,
-                        reinterpret_cast<const DRangeTile*>(db + o_tiles), n_tiles,
-                        reinterpret_cast<const uint32_t*>(db + o_blk), (uint32_t)n_elems, dk, dp,
-                        reinterpret_cast<const DRangeBound*>(db + o_q), nq, d_rbound_.p, &which, stream_, rs_ev_[0],
-                        rs_ev_[1], rs_ev_ + 2, kRsrcMaxMerge, &n_merge));
-    if (n_elems) NKM_HIP(hipMemcpyAsync(h_rpos_.p, d_rpos_[which].p, n_elems * 4, hipMemcpyDeviceToHost, stream_));
-    if (nq) NKM_HIP(hipMemcpyAsync(h_rbound_.p, d_rbound_.p, (size_t)nq * 4, hipMemcpyDeviceToHost, stream_));
+    if (nq && n_elems && n_tiles) {
+        NKM_HIP(hipMemcpyAsync(d_rq_.p, h_rq_.p, (size_t)nq * sizeof(DRangeBound), hipMemcpyHostToDevice, stream_));
+        NKM_HIP(launch_rsrc_bounds(d_pools, dk[which], reinterpret_cast<const DRangeBound*>(d_rq_.p), nq, d_rbound_.p,
+                                   stream_));
+        NKM_HIP(hipMemcpyAsync(h_rbound_.p, d_rbound_.p, (size_t)nq * 4, hipMemcpyDeviceToHost, stream_));
+    } else if (nq) {
+        std::memset(h_rbound_.p, 0, (size_t)nq * 4);  // no candidates: every bound is 0 (build_tiers clamps to 0 anyway)
+    }
     NKM_HIP(hipStreamSynchronize(stream_));
     const auto t2 = clk::now();
     stats.batches++;
@@ -457,10 +470,11 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
         const size_t pm = (size_t)(std::max_element(pool_walk_ms.begin(), pool_walk_ms.end()) - pool_walk_ms.begin());
         std::fprintf(stderr,
                      "[nkm]   batch %d (range): rows %zu pools %zu signatures %zu candidates %llu (valid %llu), %d merges "
-                     "| plan %.2f (rows %.2f pools %.2f signatures %.2f upload %.2f) device %.2f tiers %.2f walks %.2f "
-                     "merge %.2f ms | slowest pool: %u rows, build %.2f walk %.2f ms\n",
+                     "| plan %.2f (rows %.2f pools %.2f sort issue %.2f signatures %.2f queries %.2f) device %.2f "
+                     "tiers %.2f walks %.2f merge %.2f ms | slowest pool: %u rows, build %.2f walk %.2f ms\n",
                      stats.batches, nb, ng, ns, (unsigned long long)src_total, (unsigned long long)nvalid, n_merge,
-                     msd(t0, t1), msd(t0, tp_rows), msd(tp_rows, tp_pools), msd(tp_pools, tp_sigs), msd(tp_sigs, t1),
+                     msd(t0, t1), msd(t0, tp_rows), msd(tp_rows, tp_pools), msd(tp_pools, tp_sort),
+                     msd(tp_sort, tp_sigs), msd(tp_sigs, t1),
                      msd(t1, t2), msd(t2, t2b), msd(t2b, t3), msd(t3, t4), (unsigned)prows(pm),
                      pool_build_ms[pm], pool_walk_ms[pm]);
     }
