@@ -348,7 +348,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             H.livl[j] = intervals_[s];
         }
     };
-    sweep(tch, [&](size_t c) {
+    auto tier_chunk = [&](size_t c) {
         static thread_local std::vector<RRange> tmp;
         for (size_t k = ns * c / tch; k < ns * (c + 1) / tch; k++) {
             const Sig& s = sigs_[lsig[k]];
@@ -364,7 +364,16 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             for (size_t q = 0; q < tmp.size(); q++) o[q] = RRange{tmp[q].a, tmp[q].b, tmp[q].tend + ls_t0[k]};
             ls_t1[k] = ls_t0[k] + (uint32_t)tmp.size();
         }
-    });
+    };
+    // The tiers and the pools' leaf builds are independent: with a thread to
+    // spare beyond the walk tasks, one job runs both — the walk tasks first
+    // (claimed in index order, so the tier chunks are claimed by the other
+    // threads and always finish), each building its pools' leaves while the
+    // tiers are built and waiting for all of them before its first walk.
+    const bool tier_overlap = tch > 1 && ntask < wp.size();
+    std::atomic<size_t> tiers_done{0};
+    std::atomic<bool> tiers_failed{false};
+    if (!tier_overlap) sweep(tch, tier_chunk);
     const auto t2b = clk::now();
     auto worker = [&](size_t t) {
         static thread_local TlFlags tl;
@@ -413,6 +422,11 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
             H.src.livl = H.livl.data();
             H.src.tree.build(H.rank.data(), nv);
             const auto tb1 = clk::now();
+            if (tier_overlap) {
+                while (tiers_done.load(std::memory_order_acquire) < tch) __builtin_ia32_pause();
+                if (tiers_failed.load(std::memory_order_acquire)) return;  // the tier chunk's exception ends the pass
+            }
+            const auto tw = clk::now();
             PoolOut& po = few ? pool_outs_[p] : o;
             po.recs.clear();
             po.ents.clear();
@@ -424,7 +438,7 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
                          r1 = ls_t1[ls];
                      },
                      po);
-            pool_walk_ms[p] = msd(tb1, clk::now());
+            pool_walk_ms[p] = msd(tw, clk::now());
             pairs += (uint64_t)(po.recs.size() - 1) * d.src_len;  // rows that searched (the last record is the sentinel)
             pool_build_ms[p] = msd(tb0, tb1);
             for (uint32_t j = 0; j < nv; j++) rs_leaf_[H.slot[j]] = kNoSlot;
@@ -440,7 +454,27 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
         task_hits[t] = run.hits_seen;
         task_pairs[t] = pairs;
     };
-    wp.run(ntask, worker);
+    if (tier_overlap) {
+        wp.run(ntask + tch, [&](size_t i) {
+            if (i < ntask) {
+                worker(i);
+                return;
+            }
+            // counted done even when it throws (the walks wait on the count)
+            struct Count {
+                std::atomic<size_t>& n;
+                ~Count() { n.fetch_add(1, std::memory_order_release); }
+            } count{tiers_done};
+            try {
+                tier_chunk(i - ntask);
+            } catch (...) {
+                tiers_failed.store(true, std::memory_order_release);
+                throw;
+            }
+        });
+    } else {
+        wp.run(ntask, worker);
+    }
     for (uint8_t b : leaf_bad)
         if (b) throw DeviceError{hipErrorUnknown, "range source: a sorted position out of range", __LINE__};
     const auto t3 = clk::now();
