@@ -114,14 +114,9 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
         H.term = P.pool_key1[p];
         H.field = sigs_[sig_[brow[P.pool_rows[P.pool_off[p]]]]].rs_field;
     }
-    std::fill(bad.begin(), bad.end(), 0);
-    sweep(nch, [&](size_t c) {
-        for (size_t bi = nb * c / nch; bi < nb * (c + 1) / nch; bi++)
-            if (sigs_[sig_[brow[bi]]].rs_field != rs_pools_[P.search_pool[bi]].field) { bad[c] = 1; return; }
-    });
-    for (uint8_t b : bad)
-        if (b) return false;
-    // From here on the batch is taken: nothing below declines.
+    // From here on the batch is taken: nothing below declines but the
+    // per-signature field check after the claims (every row's range field
+    // must be its pool's; a row's pool is its signature's MUST term's).
     const auto tp_pools = clk::now();
     // ---- device, first: pools (posting ranges), tiles, block -> pool, and
     // the sort, which runs while the host claims the batch's signatures
@@ -203,15 +198,26 @@ bool Core::range_batch(const std::vector<uint32_t>& rows, size_t pos, GroupList&
     const size_t ns = lsig.size();
     std::vector<uint32_t> ls_pool(ns), ls_q(ns + 1, 0);
     const size_t sch = ns >= 4096 ? nch : 1;
+    std::vector<uint8_t> field_bad(sch, 0);
     sweep(sch, [&](size_t c) {
+        bool fb = false;
         for (size_t k = ns * c / sch; k < ns * (c + 1) / sch; k++) {
             const uint32_t sg = lsig[k];
             rs_sig_loc_[sg] = (uint32_t)k;
             const Sig& s = sigs_[sg];
             ls_pool[k] = ng == 1 ? 0u : pool_remap_[s.must_terms[0].second];
             ls_q[k + 1] = 2 * (uint32_t)s.rs_nrange;
+            fb |= s.rs_field != rs_pools_[ls_pool[k]].field;
         }
+        field_bad[c] = fb;
     });
+    if (std::any_of(field_bad.begin(), field_bad.end(), [](uint8_t b) { return b != 0; })) {
+        // declined: the claims are released; the sort issued above wrote only
+        // the range buffers, and is waited for here
+        for (size_t k = 0; k < ns; k++) rs_mark_[lsig[k]].store(0, std::memory_order_relaxed);
+        NKM_HIP(hipStreamSynchronize(stream_));
+        return false;
+    }
     for (size_t k = 0; k < ns; k++) ls_q[k + 1] += ls_q[k];
     const uint32_t nq = ls_q[ns];
     const auto tp_sigs = clk::now();

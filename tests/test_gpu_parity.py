@@ -219,6 +219,48 @@ def test_range_batch_multilevel_sort(monkeypatch):
     assert got_state == want_state
 
 
+@pytest.mark.parametrize("mix", ["per_pool", "within_pool"])
+def test_range_batch_fields(mix, monkeypatch):
+    """Skill-window searches on two numeric fields.  per_pool: each pool (its
+    `mode` term) ranges on one field of its own, and the range batch takes the
+    pass, one sort per pool.  within_pool: a pool's searches range on both
+    fields, so the batch is declined after its sort was issued (mm_range.cpp's
+    per-signature field check, which releases the claimed signatures) and the
+    other paths decide the pass.  Groups and post-pass state equal to the
+    oracle's on both."""
+    import random
+    monkeypatch.setenv("NKM_PARALLEL", "force")
+    rng = random.Random(11)
+    n, t0 = 4000, 1_700_000_000_000_000_000
+    ts = []
+    for i in range(n):
+        mode = "m%d" % (i % 2)
+        skill, level = rng.randint(0, 3000), rng.randint(0, 100)
+        use_level = (i % 2 == 1) if mix == "per_pool" else (i % 3 == 0)
+        f, v, w, b = ("level", level, 10, 3) if use_level else ("skill", skill, 200, 50)
+        q = ("+properties.mode:%s +properties.%s:>=%d +properties.%s:<=%d properties.%s:>=%d^2 properties.%s:<=%d^2"
+             % (mode, f, max(0, v - w), f, v + w, f, max(0, v - b), f, v + b))
+        ts.append(capi.Ticket(ticket="t%05d" % i, presences=[capi.Presence("u%d" % i, "s%d" % i, "u%d" % i, "n")],
+                              session_id="s%d" % i, party_id="", query=q, min_count=2, max_count=2,
+                              string_properties={"mode": mode}, numeric_properties={"skill": float(skill), "level": float(level)},
+                              created_at=t0 + 1024 * i, node="node1"))
+    gpu, orc = pair(dict(max_intervals=2))
+    try:
+        gpu.Insert(ts)
+        orc.Insert(ts)
+        for p in range(2):
+            r = gpu.process_raw()
+            assert r.groups == orc.Process(), (mix, p)
+            assert state(gpu) == state(orc)
+            if mix == "per_pool" and p == 0:
+                assert r.n_batches == 1 and r.eval_kernel in (6, 7), (r.n_batches, r.eval_kernel)
+            if mix == "within_pool" and p == 0:
+                assert r.eval_kernel not in (6, 7), r.eval_kernel
+    finally:
+        gpu.close()
+        orc.close()
+
+
 @pytest.mark.parametrize("partial", ["1", "0"])
 def test_c2_partial_parallel_replay(partial, monkeypatch):
     """Truncated variable-score lists under the pool-parallel replay (forced
